@@ -1,0 +1,44 @@
+// Library identity, thread-local error reporting and device queries.
+#include <stdarg.h>
+
+#include "hbk_common.h"
+
+namespace hbk {
+
+static thread_local char g_last_error[1024] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_last_error, sizeof(g_last_error), fmt, ap);
+  va_end(ap);
+}
+
+int hip_error(hipError_t e, const char* where) {
+  set_error("hbk: HIP error %d (%s) at %s", static_cast<int>(e), hipGetErrorString(e), where);
+  return HBK_ERR_HIP;
+}
+
+}  // namespace hbk
+
+extern "C" {
+
+const char* hbk_version(void) { return "hbk 0.1.0 gfx950"; }
+
+const char* hbk_last_error(void) { return hbk::g_last_error; }
+
+int hbk_device_count(int* count) {
+  if (!count) return hbk::arg_error("count is NULL");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e == hipErrorNoDevice) {
+    (void)hipGetLastError();
+    *count = 0;
+    return HBK_OK;
+  }
+  if (e != hipSuccess) return hbk::hip_error(e, "hipGetDeviceCount");
+  *count = n;
+  return HBK_OK;
+}
+
+}  // extern "C"

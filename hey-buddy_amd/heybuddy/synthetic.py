@@ -1,0 +1,87 @@
+"""Synthetic inputs that stand in for TTS speech, the MIT IR survey and the
+background-noise datasets (none are available offline). SURVEY.md §8d.
+
+Generated with torch on the target device (input preparation, outside any
+timed region), seeded per (config, rank) so every rank's shard is fixed.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+SAMPLE_RATE = 16000
+CLIP_SAMPLES = 24000  # 1.5 s synthetic clips; the featurizer reads [0, 23040)
+
+
+def seed_for(config: int, rank: int = 0) -> int:
+    return 20251015 + 1000 * config + rank
+
+
+def synthetic_clips(n: int, length: int = CLIP_SAMPLES, seed: int = 0,
+                    device: torch.device | str = "cpu", chunk: int = 4096,
+                    out: torch.Tensor | None = None) -> torch.Tensor:
+    """[n, length] f32 clips in [-1, 1]: 0.25 * sum of 6 sinusoids (80-4000 Hz)
+    under a Hann burst of 0.3-1.0 s at a random offset, + 0.01 N(0, 1)."""
+    device = torch.device(device)
+    g = torch.Generator(device=device).manual_seed(seed)
+    if out is None:
+        out = torch.empty((n, length), dtype=torch.float32, device=device)
+    t = torch.arange(length, device=device, dtype=torch.float32) / SAMPLE_RATE
+    dur_total = length / SAMPLE_RATE
+    for s in range(0, n, chunk):
+        b = min(chunk, n - s)
+        f = torch.rand((b, 6, 1), generator=g, device=device) * (4000.0 - 80.0) + 80.0
+        ph = torch.rand((b, 6, 1), generator=g, device=device) * (2 * math.pi)
+        dur = torch.rand((b, 1), generator=g, device=device) * 0.7 + 0.3
+        off = torch.rand((b, 1), generator=g, device=device) * (dur_total - dur)
+        u = ((t[None, :] - off) / dur).clamp(0.0, 1.0)
+        env = 0.5 - 0.5 * torch.cos(2 * math.pi * u)
+        tones = torch.sin(2 * math.pi * f * t[None, None, :] + ph).sum(dim=1)
+        x = 0.25 * tones * env + 0.01 * torch.randn((b, length), generator=g, device=device)
+        out[s:s + b] = x.clamp_(-1.0, 1.0)
+    return out
+
+
+def edge_clips(length: int = CLIP_SAMPLES, device: torch.device | str = "cpu") -> torch.Tensor:
+    """All-zeros, DC 0.5, full-scale 440 Hz square, unit impulse."""
+    t = torch.arange(length, dtype=torch.float64) / SAMPLE_RATE
+    z = torch.zeros(length, dtype=torch.float64)
+    dc = torch.full((length,), 0.5, dtype=torch.float64)
+    sq = torch.sign(torch.sin(2 * math.pi * 440.0 * t))
+    imp = torch.zeros(length, dtype=torch.float64)
+    imp[length // 3] = 1.0
+    return torch.stack([z, dc, sq, imp]).to(torch.float32).to(device)
+
+
+def impulse_responses(n: int = 32, seed: int = 0, min_len: int = 4000, max_len: int = 16000,
+                      device: torch.device | str = "cpu") -> list[torch.Tensor]:
+    """Exponentially decaying noise IRs (RT60 0.2-1.0 s) with a direct-path
+    spike at index U[0, 200]."""
+    g = torch.Generator().manual_seed(seed)
+    irs = []
+    for _ in range(n):
+        L = int(torch.randint(min_len, max_len + 1, (1,), generator=g))
+        rt60 = float(torch.rand((1,), generator=g)) * 0.8 + 0.2
+        tt = torch.arange(L, dtype=torch.float32) / SAMPLE_RATE
+        ir = torch.randn((L,), generator=g) * torch.exp(-6.91 * tt / rt60) * 0.3
+        d = int(torch.randint(0, 201, (1,), generator=g))
+        ir[d] = 1.0
+        irs.append(ir.to(device))
+    return irs
+
+
+def noise_bank(n: int = 64, seed: int = 0, device: torch.device | str = "cpu") -> list[torch.Tensor]:
+    """3-10 s colored noise (1/f^beta, beta ~ U[-1, 2]), RMS-normalised to 0.1."""
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for _ in range(n):
+        L = int(torch.randint(3 * SAMPLE_RATE, 10 * SAMPLE_RATE + 1, (1,), generator=g))
+        beta = float(torch.rand((1,), generator=g)) * 3.0 - 1.0
+        spec = torch.fft.rfft(torch.randn((L,), generator=g, dtype=torch.float64))
+        freqs = torch.fft.rfftfreq(L, d=1.0 / SAMPLE_RATE, dtype=torch.float64)
+        freqs[0] = freqs[1]
+        x = torch.fft.irfft(spec / freqs.pow(beta / 2.0), n=L)
+        x = x / x.pow(2).mean().sqrt() * 0.1
+        out.append(x.to(torch.float32).to(device))
+    return out
