@@ -36,17 +36,22 @@ int hip_error(hipError_t e, const char* where);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
-// ---------------------------------------------------------------- device ----
-struct cf {  // complex float, kept in two VGPRs
-  float x, y;
-};
+// Grid size for a persistent (grid-stride) kernel on the current device.
+int64_t persistent_blocks(int blocks_per_cu);
 
-__device__ __forceinline__ cf cadd(cf a, cf b) { return {a.x + b.x, a.y + b.y}; }
-__device__ __forceinline__ cf csub(cf a, cf b) { return {a.x - b.x, a.y - b.y}; }
+// ---------------------------------------------------------------- device ----
+// Complex float as a 2-lane vector so adds / multiplies lower to the packed
+// v_pk_{add,mul,fma}_f32 (two f32 per lane per instruction on gfx950).
+typedef float cf __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ cf cadd(cf a, cf b) { return a + b; }
+__device__ __forceinline__ cf csub(cf a, cf b) { return a - b; }
+// (a.x b.x - a.y b.y, a.x b.y + a.y b.x) = a.x * b + a.y * (-b.y, b.x)
 __device__ __forceinline__ cf cmul(cf a, cf b) {
-  return {fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x)};
+  const cf bs = {-b.y, b.x};
+  return __builtin_elementwise_fma(cf{a.y, a.y}, bs, cf{a.x, a.x} * b);
 }
 // multiply by -i
-__device__ __forceinline__ cf cmul_mi(cf a) { return {a.y, -a.x}; }
+__device__ __forceinline__ cf cmul_mi(cf a) { return cf{a.y, -a.x}; }
 
 }  // namespace hbk

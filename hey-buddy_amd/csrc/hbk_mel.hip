@@ -16,6 +16,7 @@
 //   products (each filter's non-zero bins are contiguous), 10 log10, /10 + 2.
 // The 4 frames of a wave only exchange data through the wave's own LDS slice,
 // so no workgroup barrier is needed after the table load.
+#include <algorithm>
 #include <cmath>
 #include <vector>
 
@@ -33,6 +34,7 @@ constexpr int kRow = 17;                  // transpose row: 16 complex + 1 pad (
 constexpr int kFrameC = 16 * kRow + 1;    // 273 complex = 2184 B per frame (== 8 mod 16 B)
 constexpr int kMaxTaps = 16;              // widest mel filter supported
 constexpr int kMaxMels = 32;
+constexpr int kBlocksPerCU = 8;           // persistent grid: CUs x this
 
 struct MelArgs {
   const float* pcm;
@@ -104,105 +106,117 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+__device__ __forceinline__ void load_frame(const float* __restrict__ src, cf (&x)[16]) {
+#pragma unroll
+  for (int n1 = 0; n1 < 16; ++n1) x[n1] = *reinterpret_cast<const cf*>(src + 32 * n1);
+}
+
+// Persistent blocks: tables are staged into LDS once, then the block walks
+// groups of 16 consecutive frames (flattened over clips) with a grid stride,
+// prefetching the next group's samples while transforming the current one.
 __global__ void __launch_bounds__(kThreads) mel_frames_kernel(MelArgs a) {
-  __shared__ float s_win[kNfft];
-  __shared__ float2 s_tw256[256];
-  __shared__ float2 s_tw512[257];
+  __shared__ cf s_win[kNfft / 2];
+  __shared__ cf s_tw256[256];
+  __shared__ cf s_tw512[257];
   __shared__ int s_lo[kMaxMels];
   __shared__ float s_w[kMaxMels * kMaxTaps];
   __shared__ cf s_frame[kFramesPerBlock * kFrameC];
 
   const int tid = threadIdx.x;
-  for (int i = tid; i < kNfft; i += kThreads) s_win[i] = a.window[i];
-  for (int i = tid; i < 256; i += kThreads) s_tw256[i] = a.tw256[i];
-  for (int i = tid; i < 257; i += kThreads) s_tw512[i] = a.tw512[i];
+  for (int i = tid; i < kNfft / 2; i += kThreads) s_win[i] = cf{a.window[2 * i], a.window[2 * i + 1]};
+  for (int i = tid; i < 256; i += kThreads) s_tw256[i] = cf{a.tw256[i].x, a.tw256[i].y};
+  for (int i = tid; i < 257; i += kThreads) s_tw512[i] = cf{a.tw512[i].x, a.tw512[i].y};
   for (int i = tid; i < a.n_mels; i += kThreads) s_lo[i] = a.mel_lo[i];
   for (int i = tid; i < a.n_mels * a.taps; i += kThreads) s_w[i] = a.mel_w[i];
   __syncthreads();
 
   const int wave = tid >> 6;
   const int lane = tid & 63;
-  const int fl = lane >> 4;  // frame slot within the wave
-  const int j = lane & 15;   // lane within the frame
-  const int64_t total = a.n_clips * a.n_frames;
-  const int64_t g = static_cast<int64_t>(blockIdx.x) * kFramesPerBlock + wave * kFramesPerWave + fl;
-  const bool valid = g < total;
-  const int64_t clip = valid ? g / a.n_frames : 0;
-  const int64_t f = valid ? g - clip * a.n_frames : 0;
-  const float* src = a.pcm + clip * a.clip_stride + f * a.hop;
-  cf* buf = s_frame + (wave * kFramesPerWave + fl) * kFrameC;
-
-  // 1) windowed load: lane j holds z[16 n1 + j] = (x[32 n1 + 2 j], x[32 n1 + 2 j + 1]) * w
-  cf v[16];
-#pragma unroll
-  for (int n1 = 0; n1 < 16; ++n1) {
-    float2 s = make_float2(0.f, 0.f);
-    if (valid) s = *reinterpret_cast<const float2*>(src + 32 * n1 + 2 * j);
-    const float2 w = *reinterpret_cast<const float2*>(&s_win[32 * n1 + 2 * j]);
-    v[n1] = {s.x * w.x, s.y * w.y};
-  }
-  // 2) FFT16 over n1, twiddle W256^(j k1), transpose
-  fft16(v);
-#pragma unroll
-  for (int k1 = 1; k1 < 16; ++k1) {
-    const float2 t = s_tw256[j * k1];
-    v[k1] = cmul(v[k1], cf{t.x, t.y});
-  }
-#pragma unroll
-  for (int k1 = 0; k1 < 16; ++k1) buf[k1 * kRow + j] = v[k1];
-  wave_sync();
-#pragma unroll
-  for (int n2 = 0; n2 < 16; ++n2) v[n2] = buf[j * kRow + n2];
-  // 3) FFT16 over n2: v[k2] = Z[j + 16 k2]
-  fft16(v);
-  wave_sync();
-#pragma unroll
-  for (int k2 = 0; k2 < 16; ++k2) buf[j + 16 * k2] = v[k2];
-  wave_sync();
-  // 4) real-FFT split and power for the bins the filters read
-  float p[16];
-#pragma unroll
-  for (int k2 = 0; k2 < 16; ++k2) {
-    p[k2] = 0.f;
-    if (k2 < a.nk2) {
-      const int k = j + 16 * k2;
-      const cf z = v[k2];
-      const cf zc = buf[(256 - k) & 255];
-      const cf fe = {0.5f * (z.x + zc.x), 0.5f * (z.y - zc.y)};
-      const cf fo = {0.5f * (z.y + zc.y), -0.5f * (z.x - zc.x)};
-      const float2 t = s_tw512[k];
-      const cf x = cadd(fe, cmul(cf{t.x, t.y}, fo));
-      p[k2] = fmaf(x.x, x.x, x.y * x.y);
-    }
-  }
-  float p256 = 0.f;
-  if (a.need256) {
-    const cf z0 = buf[0];
-    const float x = z0.x - z0.y;
-    p256 = x * x;
-  }
-  wave_sync();
+  const int slot = wave * kFramesPerWave + (lane >> 4);  // frame slot within the group
+  const int j = lane & 15;                               // lane within the frame
+  const uint32_t total = static_cast<uint32_t>(a.n_clips * a.n_frames);
+  const uint32_t nf = static_cast<uint32_t>(a.n_frames);
+  const uint32_t groups = (total + kFramesPerBlock - 1) / kFramesPerBlock;
+  cf* buf = s_frame + slot * kFrameC;
   float* pbuf = reinterpret_cast<float*>(buf);
+
+  auto frame_src = [&](uint32_t grp) {
+    uint32_t g = min(grp, groups - 1) * kFramesPerBlock + slot;
+    g = g < total ? g : total - 1;  // clamp: tail slots recompute a valid frame, store nothing
+    const uint32_t clip = g / nf;
+    const uint32_t f = g - clip * nf;
+    return a.pcm + static_cast<int64_t>(clip) * a.clip_stride + static_cast<int64_t>(f) * a.hop + 2 * j;
+  };
+
+  uint32_t grp = blockIdx.x;
+  cf x[16];
+  if (grp < groups) load_frame(frame_src(grp), x);
+  for (; grp < groups; grp += gridDim.x) {
+    // 1) window: lane j holds z[16 n1 + j] = (x[32 n1 + 2 j], x[32 n1 + 2 j + 1]) * w
+    cf v[16];
 #pragma unroll
-  for (int k2 = 0; k2 < 16; ++k2)
-    if (k2 < a.nk2) pbuf[j + 16 * k2] = p[k2];
-  if (a.need256 && j == 0) pbuf[256] = p256;
-  wave_sync();
-  // 5) mel filters: lane j owns mels 2j, 2j+1
-  float y[2];
+    for (int n1 = 0; n1 < 16; ++n1) v[n1] = x[n1] * s_win[16 * n1 + j];
+    load_frame(frame_src(grp + gridDim.x), x);  // prefetch (clamped past the end)
+    // 2) FFT16 over n1, twiddle W256^(j k1), transpose through LDS
+    fft16(v);
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int m = 2 * j + q;
-    float acc = 0.f;
-    if (m < a.n_mels) {
-      const int lo = s_lo[m];
-      const float* w = &s_w[m * a.taps];
-      for (int t = 0; t < a.taps; ++t) acc = fmaf(w[t], pbuf[lo + t], acc);
+    for (int k1 = 1; k1 < 16; ++k1) v[k1] = cmul(v[k1], s_tw256[j * k1]);
+#pragma unroll
+    for (int k1 = 0; k1 < 16; ++k1) buf[k1 * kRow + j] = v[k1];
+    wave_sync();
+#pragma unroll
+    for (int n2 = 0; n2 < 16; ++n2) v[n2] = buf[j * kRow + n2];
+    // 3) FFT16 over n2: v[k2] = Z[j + 16 k2]
+    fft16(v);
+    wave_sync();
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) buf[j + 16 * k2] = v[k2];
+    wave_sync();
+    // 4) real-FFT split X[k] = Fe + W512^k Fo and |X[k]|^2 for the bins the filters read
+    float p[16];
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) {
+      p[k2] = 0.f;
+      if (k2 < a.nk2) {
+        const int k = j + 16 * k2;
+        const cf z = v[k2];
+        const cf zc = buf[(256 - k) & 255];
+        const cf fe = 0.5f * cf{z.x + zc.x, z.y - zc.y};
+        const cf fo = 0.5f * cf{z.y + zc.y, zc.x - z.x};
+        const cf xk = fe + cmul(s_tw512[k], fo);
+        p[k2] = fmaf(xk.x, xk.x, xk.y * xk.y);
+      }
     }
-    y[q] = 10.f * log10f(fmaxf(acc, a.log_floor)) / a.out_div + a.out_add;
+    float p256 = 0.f;
+    if (a.need256) {
+      const cf z0 = buf[0];
+      p256 = (z0.x - z0.y) * (z0.x - z0.y);
+    }
+    wave_sync();
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2)
+      if (k2 < a.nk2) pbuf[j + 16 * k2] = p[k2];
+    if (a.need256 && j == 0) pbuf[256] = p256;
+    wave_sync();
+    // 5) mel filters: lane j owns mels 2j, 2j+1
+    float y[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int m = 2 * j + q;
+      float acc = 0.f;
+      if (m < a.n_mels) {
+        const int lo = s_lo[m];
+        const float* w = &s_w[m * a.taps];
+#pragma unroll 4
+        for (int t = 0; t < a.taps; ++t) acc = fmaf(w[t], pbuf[lo + t], acc);
+      }
+      y[q] = 10.f * log10f(fmaxf(acc, a.log_floor)) / a.out_div + a.out_add;
+    }
+    const uint32_t g = grp * kFramesPerBlock + slot;
+    if (g < total && 2 * j < a.n_mels)
+      *reinterpret_cast<float2*>(a.out + static_cast<int64_t>(g) * a.n_mels + 2 * j) = make_float2(y[0], y[1]);
+    wave_sync();  // the next group's transpose overwrites pbuf
   }
-  if (valid && 2 * j < a.n_mels)
-    *reinterpret_cast<float2*>(a.out + g * a.n_mels + 2 * j) = make_float2(y[0], y[1]);
 }
 
 }  // namespace
@@ -348,8 +362,9 @@ int hbk_mel_frames(const hbk_mel_plan* plan, const float* pcm, int64_t n_clips, 
   a.out_div = plan->out_div;
   a.out_add = plan->out_add;
   const int64_t total = n_clips * n_frames;
-  const int64_t blocks = (total + kFramesPerBlock - 1) / kFramesPerBlock;
-  if (blocks > 0x7fffffff) return arg_error("too many frames for one launch");
+  if (total >= (int64_t(1) << 31)) return arg_error("more than 2^31 frames in one call");
+  const int64_t groups = (total + kFramesPerBlock - 1) / kFramesPerBlock;
+  const int64_t blocks = std::min<int64_t>(groups, persistent_blocks(kBlocksPerCU));
   hipLaunchKernelGGL(mel_frames_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kThreads), 0,
                      as_stream(stream), a);
   HBK_LAUNCH_CHECK("mel_frames_kernel");

@@ -19,6 +19,20 @@ int hip_error(hipError_t e, const char* where) {
   return HBK_ERR_HIP;
 }
 
+int64_t persistent_blocks(int blocks_per_cu) {
+  static thread_local int cached_dev = -1;
+  static thread_local int cached_cus = 256;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return int64_t(256) * blocks_per_cu;
+  if (dev != cached_dev) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+      cached_cus = cus;
+    cached_dev = dev;
+  }
+  return int64_t(cached_cus) * blocks_per_cu;
+}
+
 }  // namespace hbk
 
 extern "C" {

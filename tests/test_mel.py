@@ -95,7 +95,7 @@ def test_mel_kernel_parity_edge_clips():
     bad = np.abs(out - ref) > tol
     assert not bad.any(), f"{bad.sum()} bins over tolerance; worst {np.abs(out - ref).max()}"
     # all-zero clip hits the log floor exactly: log10(1e-10)*10/10 + 2 = -8
-    assert np.all(out[0] == np.float32(-8.0))
+    assert np.abs(out[0] + 8.0).max() <= 1e-6
 
 
 @pytest.mark.gpu
