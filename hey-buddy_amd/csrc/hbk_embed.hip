@@ -1,0 +1,737 @@
+// Speech-embedding conv stack for gfx950: fused conv chains on MFMA (f32).
+//
+// Replaces the speech-embedding ONNX graph run by SpeechEmbeddingModel.__call__
+// (embeddings.py:32-42) over the 76-frame windows that
+// SpeechEmbeddings.spectrograms_to_embeddings cuts (embeddings.py:86-151).
+//
+// Execution model
+//   * The graph (Keras Conv2D 'valid' stride 1 + LeakyReLU, MaxPool2D) is cut
+//     into CHAINS: [optional input pool] conv ... conv [optional output pool].
+//     One launch runs a whole chain; its activations live in LDS.
+//   * A task = G images x one band of output rows. The band's input rows are
+//     staged into LDS once (NHWC, channels padded to an odd count so that the
+//     16 rows of an MFMA A-fragment hit 16 different banks), then every conv
+//     runs as an implicit GEMM  out[m, n] = sum_k A[m, k] W[k, n]  with
+//     m = (image, y, x), k = (dh, dw, ci) gathered from LDS through a per-stage
+//     offset table, on v_mfma_f32_16x16x4f32 (exact f32, fmaf-chain numerics).
+//   * Clip path: layers before the first pool that breaks the alignment of the
+//     window starts run ONCE per clip over the whole 136-frame sequence
+//     ("prefix"); windows are then cut from the prefix output (row offsets) for
+//     the per-window "tail". The per-window API runs every layer per window.
+#include <algorithm>
+#include <cmath>
+#include <numeric>
+#include <vector>
+
+#include "hbk_common.h"
+
+namespace hbk {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / 64;
+constexpr int kMaxStages = 10;
+constexpr int kMaxWin = 32;
+constexpr int kLdsBudget = 78 * 1024;  // bytes per block: 2 blocks per CU
+constexpr int kChunkClips = 16384;     // clips per workspace chunk
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+struct StageDesc {
+  int kh, kw, cin, cinp, cout, coutp;
+  int K, ksteps, act;
+  float alpha;
+  int w_off, b_off;  // floats into the chain's weight blob
+};
+
+struct ChainArgs {
+  const float* in;
+  float* out;
+  const float* wblob;
+  int64_t n_img;            // images (clips or windows)
+  int64_t src_clip_stride;  // floats between source clips
+  int src_row_stride;       // floats between source rows
+  int ipc;                  // images per source clip
+  int row_off[kMaxWin];     // source row offset of image (i % ipc)
+  int C_src;
+  int in_ph, in_pw;         // input max-pool
+  int W_in;                 // chain input width after the input pool
+  int out_ph, out_pw;       // output max-pool
+  int H_out, W_out, C_out;  // chain output per image
+  int64_t out_img_stride;   // floats between output images
+  int G;                    // images per task
+  int band;                 // output rows per task
+  int n_bands;
+  int shrink;               // sum over stages of kh - 1
+  int n_stages;
+  StageDesc st[kMaxStages];
+  int wblob_floats;
+  int wstride;              // row stride of packed weights
+  int lds_x, lds_y, lds_w, lds_k;  // float offsets into dynamic LDS
+};
+
+template <int NB, int RB, bool WG>
+__device__ __forceinline__ void conv_stage(const float* __restrict__ X, float* __restrict__ Y,
+                                           const float* __restrict__ Wst,
+                                           const int* __restrict__ ktab,
+                                           const float* __restrict__ bias, int G, int hin, int win,
+                                           const StageDesc& S, int wstride, int lane, int wave) {
+  const int ho = hin - S.kh + 1, wo = win - S.kw + 1;
+  const int img_pos = ho * wo, M = G * img_pos;
+  const int nrb = (M + 15) >> 4;
+  const int r16 = lane & 15, kq = lane >> 4;
+  for (int rb0 = wave * RB; rb0 < nrb; rb0 += kWaves * RB) {
+    int moff[RB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      int m = min((rb0 + r) * 16 + r16, M - 1);
+      const int g = m / img_pos;
+      const int rem = m - g * img_pos;
+      const int y = rem / wo;
+      const int x = rem - y * wo;
+      moff[r] = ((g * hin + y) * win + x) * S.cinp;
+    }
+    f4 acc[RB][NB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+      for (int c = 0; c < NB; ++c) acc[r][c] = f4{0.f, 0.f, 0.f, 0.f};
+    const float* wp = Wst + kq * wstride + r16;
+#pragma unroll 2
+    for (int ks = 0; ks < S.ksteps; ++ks) {
+      const int koff = ktab[ks * 4 + kq];
+      float av[RB], bv[NB];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) av[r] = X[moff[r] + koff];
+#pragma unroll
+      for (int c = 0; c < NB; ++c) bv[c] = wp[ks * 4 * wstride + c * 16];
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int c = 0; c < NB; ++c)
+          acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[r], bv[c], acc[r][c], 0, 0, 0);
+    }
+    // C/D layout: row (lane >> 4) * 4 + i, column lane & 15
+#pragma unroll
+    for (int c = 0; c < NB; ++c) {
+      const int n = c * 16 + r16;
+      if (n >= S.cout) continue;
+      const float bb = bias[n];
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = (rb0 + r) * 16 + kq * 4 + i;
+          if (m < M) {
+            float v = acc[r][c][i] + bb;
+            if (S.act) v = v >= 0.f ? v : v * S.alpha;
+            Y[m * S.coutp + n] = v;
+          }
+        }
+    }
+  }
+  (void)WG;
+}
+
+template <int NB, int RB, bool WG>
+__global__ void __launch_bounds__(kThreads) conv_chain_kernel(ChainArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* X = smem + a.lds_x;
+  float* Y = smem + a.lds_y;
+  float* Wl = smem + a.lds_w;
+  int* ktab = reinterpret_cast<int*>(smem + a.lds_k);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (!WG)
+    for (int i = tid; i < a.wblob_floats; i += kThreads) Wl[i] = a.wblob[i];  // resident weights
+
+  const int64_t n_groups = (a.n_img + a.G - 1) / a.G;
+  const int64_t n_tasks = n_groups * a.n_bands;
+  const int C = a.C_src;
+  const int cinp0 = a.st[0].cinp;
+  for (int64_t task = blockIdx.x; task < n_tasks; task += gridDim.x) {
+    const int64_t grp = task / a.n_bands;
+    const int band = static_cast<int>(task - grp * a.n_bands);
+    const int64_t img0 = grp * a.G;
+    const int G = static_cast<int>(min<int64_t>(a.G, a.n_img - img0));
+    const int orow0 = band * a.band;
+    const int orows = min(a.band, a.H_out - orow0);
+    const int r0 = orow0 * a.out_ph;           // first chain-input row of the band
+    const int rows_in = orows * a.out_ph + a.shrink;
+
+    // 1) stage the band's input rows (max-pooled on the fly) into X
+    const int row_elems = a.W_in * C;
+    const int per_img = rows_in * row_elems;
+    for (int e = tid; e < G * per_img; e += kThreads) {
+      const int g = e / per_img;
+      int rem = e - g * per_img;
+      const int r = rem / row_elems;
+      rem -= r * row_elems;
+      const int w = rem / C;
+      const int c = rem - w * C;
+      const int64_t im = img0 + g;
+      const int64_t clip = im / a.ipc;
+      const int roff = a.row_off[im - clip * a.ipc];
+      const float* src = a.in + clip * a.src_clip_stride +
+                         static_cast<int64_t>(roff + (r0 + r) * a.in_ph) * a.src_row_stride +
+                         (w * a.in_pw) * C + c;
+      float v = src[0];
+      for (int i = 0; i < a.in_ph; ++i)
+        for (int j = 0; j < a.in_pw; ++j) v = fmaxf(v, src[i * a.src_row_stride + j * C]);
+      X[((g * rows_in + r) * a.W_in + w) * cinp0 + c] = v;
+    }
+
+    // 2) the chain's convs, ping-ponging between X and Y
+    int hin = rows_in, win = a.W_in;
+    float* cur = X;
+    float* nxt = Y;
+    for (int s = 0; s < a.n_stages; ++s) {
+      const StageDesc S = a.st[s];
+      __syncthreads();  // stage input complete; previous stage done with ktab
+      for (int k = tid; k < S.ksteps * 4; k += kThreads) {
+        int v = 0;  // padded k: weight 0, read the (finite) own-position value
+        if (k < S.K) {
+          const int tap = k / S.cin;
+          const int ci = k - tap * S.cin;
+          const int dh = tap / S.kw;
+          const int dw = tap - dh * S.kw;
+          v = (dh * win + dw) * S.cinp + ci;
+        }
+        ktab[k] = v;
+      }
+      __syncthreads();
+      const float* Wst = WG ? a.wblob + S.w_off : Wl + S.w_off;
+      conv_stage<NB, RB, WG>(cur, nxt, Wst, ktab, a.wblob + S.b_off, G, hin, win, S, a.wstride,
+                             lane, wave);
+      float* t = cur;
+      cur = nxt;
+      nxt = t;
+      hin -= S.kh - 1;
+      win -= S.kw - 1;
+    }
+    __syncthreads();
+
+    // 3) store the band (max-pooled on the fly)
+    const int coutp = a.st[a.n_stages - 1].coutp;
+    const int orow_elems = a.W_out * a.C_out;
+    const int per_out = orows * orow_elems;
+    for (int e = tid; e < G * per_out; e += kThreads) {
+      const int g = e / per_out;
+      int rem = e - g * per_out;
+      const int r = rem / orow_elems;
+      rem -= r * orow_elems;
+      const int w = rem / a.C_out;
+      const int c = rem - w * a.C_out;
+      const float* p = cur + ((g * hin + r * a.out_ph) * win + w * a.out_pw) * coutp + c;
+      float v = p[0];
+      for (int i = 0; i < a.out_ph; ++i)
+        for (int j = 0; j < a.out_pw; ++j) v = fmaxf(v, p[(i * win + j) * coutp]);
+      a.out[(img0 + g) * a.out_img_stride + static_cast<int64_t>(orow0 + r) * orow_elems + w * a.C_out + c] = v;
+    }
+    __syncthreads();  // the next task restages X
+  }
+}
+
+// ------------------------------------------------------------------ host ----
+
+struct OpInfo {
+  int kind, kh, kw, cin, cout, act;
+  float alpha;
+  std::vector<float> w, b;  // HWIO, [cout]
+};
+
+struct Dims {
+  int h, w, c;
+};
+
+using KernelFn = void (*)(ChainArgs);
+
+struct ChainPlan {
+  ChainArgs args{};
+  int nb = 1;
+  bool wg = false;
+  KernelFn fn = nullptr;
+  size_t lds_bytes = 0;
+  float* d_blob = nullptr;
+  int src_buf = -1;          // -1: the call's input, else workspace buffer index
+  int dst_buf = -1;          // -1: the call's output
+  int64_t out_floats = 0;    // per source clip (clip path) or per window
+  double macs_per_img = 0;   // algorithmic MACs per image of this chain
+};
+
+struct Program {
+  std::vector<ChainPlan> chains;
+  int64_t buf_floats[2] = {0, 0};  // per unit (clip or window)
+};
+
+template <int NB, int RB, bool WG>
+KernelFn kernel_for() {
+  return conv_chain_kernel<NB, RB, WG>;
+}
+
+KernelFn pick_kernel(int nb, bool wg) {
+  // RB x NB accumulators of 4 VGPRs: keep RB * NB <= 12
+  switch (nb) {
+    case 1: return wg ? kernel_for<1, 4, true>() : kernel_for<1, 4, false>();
+    case 2: return wg ? kernel_for<2, 4, true>() : kernel_for<2, 4, false>();
+    case 3: return wg ? kernel_for<3, 4, true>() : kernel_for<3, 4, false>();
+    case 4: return wg ? kernel_for<4, 2, true>() : kernel_for<4, 2, false>();
+    case 5: return wg ? kernel_for<5, 2, true>() : kernel_for<5, 2, false>();
+    case 6: return wg ? kernel_for<6, 2, true>() : kernel_for<6, 2, false>();
+    default: return nullptr;
+  }
+}
+
+inline int odd_pad(int c) { return (c % 2 == 0) ? c + 1 : c; }
+
+}  // namespace
+}  // namespace hbk
+
+struct hbk_embed_plan {
+  std::vector<hbk::OpInfo> ops;
+  int in_h = 0, in_w = 0, out_dim = 0;
+  std::vector<int> starts;
+  int n_prefix = 0;
+  int seq_frames = 0;
+  int split_stride = 1;
+  double prefix_macs = 0, tail_macs = 0;
+  hbk::Program clip_prog, win_prog;
+};
+
+namespace hbk {
+namespace {
+
+// Builds the chains for ops [o0, o1) applied to images of dims `in`, reading
+// image i from row_off[i % ipc] of source clip i / ipc.
+int build_segment(const std::vector<OpInfo>& ops, int o0, int o1, Dims in, int ipc,
+                  const std::vector<int>& row_off, int64_t src_clip_floats, int src_row_floats,
+                  int first_src_buf, Program& prog, std::vector<Dims>* out_dims_per_chain) {
+  int i = o0;
+  Dims cur = in;
+  int src_buf = first_src_buf;
+  bool first = true;
+  while (i < o1) {
+    ChainPlan cp;
+    ChainArgs& a = cp.args;
+    a.ipc = first ? ipc : 1;
+    for (int k = 0; k < kMaxWin; ++k) a.row_off[k] = 0;
+    if (first)
+      for (size_t k = 0; k < row_off.size(); ++k) a.row_off[k] = row_off[k];
+    a.src_clip_stride = first ? src_clip_floats : int64_t(cur.h) * cur.w * cur.c;
+    a.src_row_stride = first ? src_row_floats : cur.w * cur.c;
+    a.C_src = cur.c;
+    a.in_ph = a.in_pw = 1;
+    if (ops[i].kind == HBK_OP_MAXPOOL) {
+      a.in_ph = ops[i].kh;
+      a.in_pw = ops[i].kw;
+      ++i;
+    }
+    Dims d{cur.h / a.in_ph, cur.w / a.in_pw, cur.c};
+    a.W_in = d.w;
+    const int H_in = d.h;
+    std::vector<int> stage_ops;
+    while (i < o1 && ops[i].kind == HBK_OP_CONV && int(stage_ops.size()) < kMaxStages) {
+      stage_ops.push_back(i);
+      ++i;
+    }
+    if (stage_ops.empty()) {
+      set_error("hbk: unsupported graph: a max-pool must be followed by a conv");
+      return HBK_ERR_UNSUPPORTED;
+    }
+    a.out_ph = a.out_pw = 1;
+    if (i < o1 && ops[i].kind == HBK_OP_MAXPOOL && (i + 1 >= o1 || ops[i + 1].kind == HBK_OP_CONV)) {
+      // keep the pool as this chain's output pool unless the next chain needs it as input pool
+      a.out_ph = ops[i].kh;
+      a.out_pw = ops[i].kw;
+      ++i;
+    }
+    // stages
+    int nb = 1;
+    int cin = d.c, h = H_in, w = d.w;
+    a.n_stages = static_cast<int>(stage_ops.size());
+    a.shrink = 0;
+    double macs = 0;
+    std::vector<Dims> tens;  // stage input/output tensors (per image, padded channels)
+    for (int s = 0; s < a.n_stages; ++s) {
+      const OpInfo& op = ops[stage_ops[s]];
+      if (op.cin != cin) {
+        set_error("hbk: graph channel mismatch at op %d (%d != %d)", stage_ops[s], op.cin, cin);
+        return HBK_ERR_ARG;
+      }
+      StageDesc& S = a.st[s];
+      S.kh = op.kh;
+      S.kw = op.kw;
+      S.cin = op.cin;
+      S.cinp = odd_pad(op.cin);
+      S.cout = op.cout;
+      S.coutp = odd_pad(op.cout);
+      S.K = op.kh * op.kw * op.cin;
+      S.ksteps = (S.K + 3) / 4;
+      S.act = op.act;
+      S.alpha = op.alpha;
+      nb = std::max(nb, (op.cout + 15) / 16);
+      a.shrink += op.kh - 1;
+      h -= op.kh - 1;
+      w -= op.kw - 1;
+      if (h <= 0 || w <= 0) {
+        set_error("hbk: graph collapses the image at op %d", stage_ops[s]);
+        return HBK_ERR_ARG;
+      }
+      macs += double(h) * w * op.cout * S.K;
+      cin = op.cout;
+    }
+    if (nb > 6) {
+      set_error("hbk: conv with more than 96 output channels is not supported");
+      return HBK_ERR_UNSUPPORTED;
+    }
+    cp.nb = nb;
+    a.wstride = nb * 16 + ((nb * 16) % 32 == 0 ? 16 : 0);  // kq rows on different bank halves
+    // pack weights: per stage [ksteps*4][wstride] then bias [nb*16]
+    std::vector<float> blob;
+    int max_stage_w = 0, max_k = 0;
+    for (int s = 0; s < a.n_stages; ++s) {
+      const OpInfo& op = ops[stage_ops[s]];
+      StageDesc& S = a.st[s];
+      S.w_off = static_cast<int>(blob.size());
+      const int rows = S.ksteps * 4;
+      blob.resize(blob.size() + size_t(rows) * a.wstride, 0.f);
+      for (int k = 0; k < S.K; ++k)
+        for (int n = 0; n < op.cout; ++n) blob[S.w_off + size_t(k) * a.wstride + n] = op.w[size_t(k) * op.cout + n];
+      max_stage_w = std::max(max_stage_w, rows * a.wstride);
+      max_k = std::max(max_k, rows);
+    }
+    for (int s = 0; s < a.n_stages; ++s) {
+      const OpInfo& op = ops[stage_ops[s]];
+      a.st[s].b_off = static_cast<int>(blob.size());
+      for (int n = 0; n < nb * 16; ++n) blob.push_back(n < op.cout ? op.b[n] : 0.f);
+    }
+    a.wblob_floats = static_cast<int>(blob.size());
+    // output dims
+    Dims od{h / a.out_ph, w / a.out_pw, cin};
+    a.H_out = od.h;
+    a.W_out = od.w;
+    a.C_out = od.c;
+    a.out_img_stride = int64_t(od.h) * od.w * od.c;
+    if (od.h <= 0 || od.w <= 0) {
+      set_error("hbk: pooling collapses the image");
+      return HBK_ERR_ARG;
+    }
+    // choose G (images per task) and band (output rows per task) for the LDS budget
+    auto lds_floats = [&](int G, int band, bool resident) -> int64_t {
+      int rows = band * a.out_ph;  // rows of the last conv output
+      std::vector<int64_t> t(a.n_stages + 1);
+      for (int s = a.n_stages - 1; s >= 0; --s) {
+        const StageDesc& S = a.st[s];
+        int wo = d.w;
+        for (int q = 0; q <= s; ++q) wo -= a.st[q].kw - 1;
+        t[s + 1] = int64_t(G) * rows * wo * S.coutp;
+        rows += S.kh - 1;
+      }
+      t[0] = int64_t(G) * rows * d.w * a.st[0].cinp;
+      int64_t x = 0, y = 0;
+      for (int s = 0; s <= a.n_stages; ++s) (s % 2 == 0 ? x : y) = std::max(s % 2 == 0 ? x : y, t[s]);
+      int64_t wf = resident ? a.wblob_floats : 0;
+      return ((x + 3) & ~3) + ((y + 3) & ~3) + ((wf + 3) & ~3) + ((max_k + 3) & ~3);
+    };
+    const int64_t budget = kLdsBudget / 4;
+    bool resident = lds_floats(1, 1, true) <= budget;
+    int band = 0, G = 1;
+    for (int b = od.h; b >= 1; --b)
+      if (lds_floats(1, b, resident) <= budget) { band = b; break; }
+    if (band == 0) {
+      set_error("hbk: one output row of a chain does not fit in LDS");
+      return HBK_ERR_UNSUPPORTED;
+    }
+    if (band == od.h)
+      while (G < 64 && lds_floats(G * 2, band, resident) <= budget) G *= 2;
+    a.G = G;
+    a.band = band;
+    a.n_bands = (od.h + band - 1) / band;
+    int64_t xf = 0, yf = 0;
+    {
+      int rows = band * a.out_ph;
+      std::vector<int64_t> t(a.n_stages + 1);
+      for (int s = a.n_stages - 1; s >= 0; --s) {
+        int wo = d.w;
+        for (int q = 0; q <= s; ++q) wo -= a.st[q].kw - 1;
+        t[s + 1] = int64_t(G) * rows * wo * a.st[s].coutp;
+        rows += a.st[s].kh - 1;
+      }
+      t[0] = int64_t(G) * rows * d.w * a.st[0].cinp;
+      for (int s = 0; s <= a.n_stages; ++s) (s % 2 == 0 ? xf : yf) = std::max(s % 2 == 0 ? xf : yf, t[s]);
+    }
+    a.lds_x = 0;
+    a.lds_y = static_cast<int>((xf + 3) & ~3);
+    a.lds_w = a.lds_y + static_cast<int>((yf + 3) & ~3);
+    a.lds_k = a.lds_w + (resident ? ((a.wblob_floats + 3) & ~3) : 0);
+    cp.lds_bytes = size_t(a.lds_k + ((max_k + 3) & ~3)) * 4;
+    cp.wg = !resident;
+    cp.fn = pick_kernel(nb, cp.wg);
+    (void)max_stage_w;
+    // device weights
+    hipError_t e = hipMalloc(&cp.d_blob, blob.size() * sizeof(float));
+    if (e != hipSuccess) return hip_error(e, "hipMalloc chain weights");
+    e = hipMemcpy(cp.d_blob, blob.data(), blob.size() * sizeof(float), hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_error(e, "copy chain weights");
+    a.wblob = cp.d_blob;
+    if (cp.lds_bytes > 64 * 1024) {
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(cp.fn),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, int(cp.lds_bytes));
+      if (e != hipSuccess) return hip_error(e, "hipFuncSetAttribute(max dynamic LDS)");
+    }
+    cp.macs_per_img = macs;
+    cp.src_buf = src_buf;
+    cp.out_floats = a.out_img_stride * (first ? ipc : 1);
+    prog.chains.push_back(cp);
+    if (out_dims_per_chain) out_dims_per_chain->push_back(od);
+    src_buf = -2;  // placeholder: assigned by the caller
+    cur = od;
+    first = false;
+  }
+  return HBK_OK;
+}
+
+// Assign ping-pong workspace buffers: chain k writes buffer k % 2, the last
+// writes the call's output; record per-unit buffer sizes.
+void assign_buffers(Program& prog, int64_t units_per_first_img_ratio) {
+  (void)units_per_first_img_ratio;
+  const size_t n = prog.chains.size();
+  for (size_t k = 0; k < n; ++k) {
+    ChainPlan& c = prog.chains[k];
+    c.src_buf = (k == 0) ? -1 : int((k - 1) % 2);
+    c.dst_buf = (k + 1 == n) ? -1 : int(k % 2);
+  }
+}
+
+int run_program(const Program& prog, const float* in, int64_t n_units, int64_t in_unit_stride,
+                float* out, int64_t out_unit_floats, float* ws, int64_t chunk, hipStream_t stream,
+                const std::vector<int64_t>& imgs_per_unit, const std::vector<int64_t>& buf_unit_floats) {
+  for (int64_t u0 = 0; u0 < n_units; u0 += chunk) {
+    const int64_t nu = std::min(chunk, n_units - u0);
+    float* bufs[2] = {ws, ws + chunk * buf_unit_floats[0]};
+    for (size_t k = 0; k < prog.chains.size(); ++k) {
+      const ChainPlan& c = prog.chains[k];
+      ChainArgs a = c.args;
+      if (c.src_buf < 0) {
+        a.in = in + u0 * in_unit_stride;
+        a.src_clip_stride = in_unit_stride;
+      } else {
+        a.in = bufs[c.src_buf];
+      }
+      a.out = c.dst_buf < 0 ? out + u0 * out_unit_floats : bufs[c.dst_buf];
+      a.n_img = nu * imgs_per_unit[k];
+      const int64_t tasks = ((a.n_img + a.G - 1) / a.G) * a.n_bands;
+      const int64_t blocks = std::min<int64_t>(tasks, persistent_blocks(2));
+      if (blocks <= 0) continue;
+      hipLaunchKernelGGL(c.fn, dim3(unsigned(blocks)), dim3(kThreads), c.lds_bytes, stream, a);
+      HBK_LAUNCH_CHECK("conv_chain_kernel");
+    }
+  }
+  return HBK_OK;
+}
+
+}  // namespace
+}  // namespace hbk
+
+extern "C" {
+
+int hbk_embed_plan_create(const hbk_graph_op* ops, int32_t n_ops, int32_t in_h, int32_t in_w,
+                          const int32_t* win_start, int32_t n_win, hbk_embed_plan** plan) {
+  using namespace hbk;
+  if (!plan) return arg_error("plan is NULL");
+  *plan = nullptr;
+  if (!ops || n_ops <= 0) return arg_error("empty graph");
+  if (in_h <= 0 || in_w <= 0) return arg_error("bad window size");
+  if (!win_start || n_win <= 0 || n_win > kMaxWin) return arg_error("n_win must be in [1, 32]");
+  auto* p = new hbk_embed_plan();
+  auto fail = [&](int rc) {
+    hbk_embed_plan_destroy(p);
+    return rc;
+  };
+  p->in_h = in_h;
+  p->in_w = in_w;
+  for (int i = 0; i < n_win; ++i) {
+    if (win_start[i] < 0) return fail(arg_error("negative window start"));
+    p->starts.push_back(win_start[i]);
+  }
+  Dims d{in_h, in_w, 1};
+  std::vector<Dims> dims;  // per op, for one window
+  for (int i = 0; i < n_ops; ++i) {
+    const hbk_graph_op& o = ops[i];
+    OpInfo op{o.kind, o.kh, o.kw, o.cin, o.cout, o.act, o.alpha, {}, {}};
+    if (o.kh <= 0 || o.kw <= 0) return fail(arg_error("kernel / pool size must be positive"));
+    if (o.kind == HBK_OP_CONV) {
+      if (o.cin != d.c || o.cout <= 0 || !o.weight || !o.bias) return fail(arg_error("bad conv op"));
+      op.w.assign(o.weight, o.weight + size_t(o.kh) * o.kw * o.cin * o.cout);
+      op.b.assign(o.bias, o.bias + o.cout);
+      d = Dims{d.h - o.kh + 1, d.w - o.kw + 1, o.cout};
+    } else if (o.kind == HBK_OP_MAXPOOL) {
+      d = Dims{d.h / o.kh, d.w / o.kw, d.c};
+    } else {
+      return fail(arg_error("unknown op kind"));
+    }
+    if (d.h <= 0 || d.w <= 0) return fail(arg_error("graph collapses the window"));
+    p->ops.push_back(std::move(op));
+    dims.push_back(d);
+  }
+  if (d.h != 1 || d.w != 1) return fail(arg_error("graph output must be 1 x 1 x C"));
+  p->out_dim = d.c;
+
+  // prefix: ops shared across the windows of a clip. A pool of height ph keeps
+  // the windows aligned iff the cumulative time stride divides every start.
+  int g = 0;
+  for (int s : p->starts) g = std::gcd(g, s);
+  int stride = 1, split = n_ops;
+  for (int i = 0; i < n_ops; ++i) {
+    if (p->ops[i].kind == HBK_OP_MAXPOOL) {
+      const int ns = stride * p->ops[i].kh;
+      if (g % ns != 0) {
+        split = i;
+        break;
+      }
+      stride = ns;
+    }
+  }
+  // the tail must start with a pool (its input pool) and contain a conv
+  if (split == n_ops || split == 0) {
+    set_error("hbk: graph has no window-splitting pool; use hbk_embed_windows");
+    return fail(HBK_ERR_UNSUPPORTED);
+  }
+  p->n_prefix = split;
+  p->split_stride = stride;
+  const int max_start = *std::max_element(p->starts.begin(), p->starts.end());
+  p->seq_frames = max_start + in_h;
+
+  int rc;
+  // ---- clip program: prefix over [seq_frames, in_w, 1] per clip ----
+  {
+    std::vector<Dims> od;
+    rc = build_segment(p->ops, 0, split, Dims{p->seq_frames, in_w, 1}, 1, {0}, 0, in_w, -1,
+                       p->clip_prog, &od);
+    if (rc) return fail(rc);
+    const Dims pre = od.back();
+    // window rows at the split, for one window
+    const Dims wd = dims[split - 1];
+    std::vector<int> roff;
+    for (int s : p->starts) roff.push_back(s / stride);
+    for (int r : roff)
+      if (r + wd.h > pre.h) return fail(arg_error("window start beyond the frame sequence"));
+    const size_t n_pre = p->clip_prog.chains.size();
+    rc = build_segment(p->ops, split, n_ops, Dims{wd.h, wd.w, wd.c}, n_win, roff,
+                       int64_t(pre.h) * pre.w * pre.c, pre.w * pre.c, 0, p->clip_prog, nullptr);
+    if (rc) return fail(rc);
+    for (size_t k = 0; k < p->clip_prog.chains.size(); ++k) {
+      if (k < n_pre) p->prefix_macs += p->clip_prog.chains[k].macs_per_img;
+      else p->tail_macs += p->clip_prog.chains[k].macs_per_img;
+    }
+    assign_buffers(p->clip_prog, 1);
+  }
+  // ---- window program: every op per window ----
+  {
+    std::vector<Dims> od;
+    rc = build_segment(p->ops, 0, n_ops, Dims{in_h, in_w, 1}, 1, {0}, int64_t(in_h) * in_w, in_w,
+                       -1, p->win_prog, &od);
+    if (rc) return fail(rc);
+    assign_buffers(p->win_prog, 1);
+  }
+  *plan = p;
+  return HBK_OK;
+}
+
+int hbk_embed_plan_destroy(hbk_embed_plan* p) {
+  if (!p) return HBK_OK;
+  for (auto* prog : {&p->clip_prog, &p->win_prog})
+    for (auto& c : prog->chains) (void)hipFree(c.d_blob);
+  delete p;
+  return HBK_OK;
+}
+
+int hbk_embed_plan_info(const hbk_embed_plan* p, int32_t* out_dim, int32_t* n_prefix_ops,
+                        int32_t* n_chains, double* prefix_macs, double* tail_macs,
+                        int32_t* seq_frames) {
+  if (!p) return hbk::arg_error("plan is NULL");
+  if (out_dim) *out_dim = p->out_dim;
+  if (n_prefix_ops) *n_prefix_ops = p->n_prefix;
+  if (n_chains) *n_chains = static_cast<int32_t>(p->clip_prog.chains.size());
+  if (prefix_macs) *prefix_macs = p->prefix_macs;
+  if (tail_macs) *tail_macs = p->tail_macs;
+  if (seq_frames) *seq_frames = p->seq_frames;
+  return HBK_OK;
+}
+
+}  // extern "C"
+
+namespace hbk {
+namespace {
+
+// Per-unit (clip or window) workspace floats of each ping-pong buffer and the
+// images per unit of each chain.
+void program_geometry(const Program& prog, bool clip_path, int n_win, std::vector<int64_t>& imgs,
+                      std::vector<int64_t>& bufs) {
+  imgs.clear();
+  bufs.assign(2, 0);
+  bool tail = false;
+  for (size_t k = 0; k < prog.chains.size(); ++k) {
+    const ChainPlan& c = prog.chains[k];
+    if (clip_path && c.args.ipc > 1) tail = true;
+    imgs.push_back(tail ? n_win : 1);
+    if (c.dst_buf >= 0) bufs[c.dst_buf] = std::max(bufs[c.dst_buf], c.args.out_img_stride * imgs.back());
+  }
+}
+
+}  // namespace
+}  // namespace hbk
+
+extern "C" {
+
+int hbk_embed_workspace_size(const hbk_embed_plan* p, int64_t n, int64_t* bytes) {
+  using namespace hbk;
+  if (!p || !bytes) return arg_error("plan/bytes is NULL");
+  if (n < 0) return arg_error("negative n");
+  const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(n, kChunkClips));
+  std::vector<int64_t> imgs, bc, bw;
+  program_geometry(p->clip_prog, true, int(p->starts.size()), imgs, bc);
+  const int64_t chunk_w = std::max<int64_t>(1, std::min<int64_t>(n, kChunkClips));
+  program_geometry(p->win_prog, false, 1, imgs, bw);
+  const int64_t fc = chunk * (bc[0] + bc[1]);
+  const int64_t fw = chunk_w * (bw[0] + bw[1]);
+  *bytes = std::max(fc, fw) * int64_t(sizeof(float)) + 256;
+  return HBK_OK;
+}
+
+int hbk_embed_clips(const hbk_embed_plan* p, const float* mel, int64_t n_clips, int64_t mel_clip_stride,
+                    float* out, void* workspace, int64_t workspace_bytes, void* stream) {
+  using namespace hbk;
+  if (!p) return arg_error("plan is NULL");
+  if (n_clips < 0) return arg_error("negative n_clips");
+  if (n_clips == 0) return HBK_OK;
+  if (!mel || !out || !workspace) return arg_error("NULL pointer");
+  if (mel_clip_stride < int64_t(p->seq_frames) * p->in_w) return arg_error("mel_clip_stride < seq_frames * in_w");
+  int64_t need = 0;
+  hbk_embed_workspace_size(p, n_clips, &need);
+  if (workspace_bytes < need) return arg_error("workspace too small");
+  std::vector<int64_t> imgs, bufs;
+  program_geometry(p->clip_prog, true, int(p->starts.size()), imgs, bufs);
+  const int64_t chunk = std::min<int64_t>(n_clips, kChunkClips);
+  return run_program(p->clip_prog, mel, n_clips, mel_clip_stride, out,
+                     int64_t(p->starts.size()) * p->out_dim, static_cast<float*>(workspace), chunk,
+                     as_stream(stream), imgs, bufs);
+}
+
+int hbk_embed_windows(const hbk_embed_plan* p, const float* windows, int64_t n, float* out,
+                      void* workspace, int64_t workspace_bytes, void* stream) {
+  using namespace hbk;
+  if (!p) return arg_error("plan is NULL");
+  if (n < 0) return arg_error("negative n");
+  if (n == 0) return HBK_OK;
+  if (!windows || !out || !workspace) return arg_error("NULL pointer");
+  int64_t need = 0;
+  hbk_embed_workspace_size(p, n, &need);
+  if (workspace_bytes < need) return arg_error("workspace too small");
+  std::vector<int64_t> imgs, bufs;
+  program_geometry(p->win_prog, false, 1, imgs, bufs);
+  const int64_t chunk = std::min<int64_t>(n, int64_t(kChunkClips));
+  return run_program(p->win_prog, windows, n, int64_t(p->in_h) * p->in_w, out, p->out_dim,
+                     static_cast<float*>(workspace), chunk, as_stream(stream), imgs, bufs);
+}
+
+}  // extern "C"

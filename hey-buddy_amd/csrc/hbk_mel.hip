@@ -322,11 +322,11 @@ int hbk_mel_plan_create(const float* window, const float* fbank, int n_fft, int 
 
 int hbk_mel_plan_destroy(hbk_mel_plan* p) {
   if (!p) return HBK_OK;
-  hipFree(p->d_window);
-  hipFree(p->d_tw256);
-  hipFree(p->d_tw512);
-  hipFree(p->d_lo);
-  hipFree(p->d_w);
+  (void)hipFree(p->d_window);
+  (void)hipFree(p->d_tw256);
+  (void)hipFree(p->d_tw512);
+  (void)hipFree(p->d_lo);
+  (void)hipFree(p->d_w);
   delete p;
   return HBK_OK;
 }

@@ -51,7 +51,27 @@ _PROTOS = {
                                      _c_float, _c_float, ctypes.POINTER(_vp)]),
     "hbk_mel_plan_destroy": (_c_int, [_vp]),
     "hbk_mel_frames": (_c_int, [_vp, _vp, _c_int64, _c_int64, _c_int64, _vp, _vp]),
+    "hbk_embed_plan_create": (_c_int, [_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _vp,
+                                       ctypes.c_int32, ctypes.POINTER(_vp)]),
+    "hbk_embed_plan_destroy": (_c_int, [_vp]),
+    "hbk_embed_plan_info": (_c_int, [_vp, ctypes.POINTER(ctypes.c_int32),
+                                     ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
+                                     ctypes.POINTER(ctypes.c_double),
+                                     ctypes.POINTER(ctypes.c_double),
+                                     ctypes.POINTER(ctypes.c_int32)]),
+    "hbk_embed_workspace_size": (_c_int, [_vp, _c_int64, ctypes.POINTER(_c_int64)]),
+    "hbk_embed_clips": (_c_int, [_vp, _vp, _c_int64, _c_int64, _vp, _vp, _c_int64, _vp]),
+    "hbk_embed_windows": (_c_int, [_vp, _vp, _c_int64, _vp, _vp, _c_int64, _vp]),
 }
+
+
+class GraphOp(ctypes.Structure):
+    """hbk_graph_op (include/hbk.h)."""
+    _fields_ = [
+        ("kind", ctypes.c_int32), ("kh", ctypes.c_int32), ("kw", ctypes.c_int32),
+        ("cin", ctypes.c_int32), ("cout", ctypes.c_int32), ("act", ctypes.c_int32),
+        ("alpha", ctypes.c_float), ("weight", _vp), ("bias", _vp),
+    ]
 
 
 def exported_symbols() -> list[str]:

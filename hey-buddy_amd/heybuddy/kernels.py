@@ -108,3 +108,137 @@ def _aligned_copy(x: torch.Tensor) -> torch.Tensor:
     buf = torch.empty((x.shape[0], t + (t & 1)), dtype=x.dtype, device=x.device)
     buf[:, :t].copy_(x)
     return buf[:, :t]
+
+
+class EmbedPlan:
+    """Device plan of the speech-embedding graph (hbk_embed_plan_create).
+
+    ``graph`` is a heybuddy.embedding_graph.Graph; ``starts`` are the window
+    start frames of the clip path (the reference's 16 windows by default).
+    """
+
+    def __init__(self, graph, starts=None, device: torch.device | int | None = None) -> None:
+        from heybuddy.embedding_graph import WINDOW_STARTS, Conv
+        self.device = _native.require_device(device)
+        self.graph = graph
+        self.starts = tuple(WINDOW_STARTS if starts is None else starts)
+        ops = (_native.GraphOp * len(graph.ops))()
+        self._keep = []  # host arrays referenced by ops during create
+        for i, op in enumerate(graph.ops):
+            if isinstance(op, Conv):
+                w = np.ascontiguousarray(op.weight, dtype=np.float32)
+                b = np.ascontiguousarray(op.bias, dtype=np.float32)
+                self._keep += [w, b]
+                ops[i] = _native.GraphOp(0, op.kh, op.kw, op.cin, op.cout,
+                                         1 if op.act == "leaky_relu" else 0, float(op.alpha),
+                                         w.ctypes.data, b.ctypes.data)
+            else:
+                ops[i] = _native.GraphOp(1, op.ph, op.pw, 0, 0, 0, 0.0, None, None)
+        st = (ctypes.c_int32 * len(self.starts))(*self.starts)
+        h, w, _ = graph.in_shape
+        handle = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(lib().hbk_embed_plan_create(ops, len(graph.ops), h, w, st, len(self.starts),
+                                              ctypes.byref(handle)), "hbk_embed_plan_create")
+        self._handle = handle
+        self._keep = []
+        od, npre, nch, sf = (ctypes.c_int32() for _ in range(4))
+        pm, tm = ctypes.c_double(), ctypes.c_double()
+        check(lib().hbk_embed_plan_info(handle, ctypes.byref(od), ctypes.byref(npre),
+                                        ctypes.byref(nch), ctypes.byref(pm), ctypes.byref(tm),
+                                        ctypes.byref(sf)), "hbk_embed_plan_info")
+        self.out_dim = od.value
+        self.n_prefix_ops = npre.value
+        self.n_chains = nch.value
+        self.prefix_macs_per_clip = pm.value
+        self.tail_macs_per_window = tm.value
+        self.seq_frames = sf.value
+        self.in_h, self.in_w = h, w
+        self._ws: torch.Tensor | None = None
+        with _plans_lock:
+            self.id = next(_plan_ids)
+            _plans[self.id] = self
+
+    @property
+    def macs_per_clip(self) -> float:
+        """Algorithmic MACs of the clip path (shared prefix + per-window tail)."""
+        return self.prefix_macs_per_clip + len(self.starts) * self.tail_macs_per_window
+
+    def workspace(self, n: int) -> torch.Tensor:
+        need = ctypes.c_int64()
+        check(lib().hbk_embed_workspace_size(self._handle, int(n), ctypes.byref(need)),
+              "hbk_embed_workspace_size")
+        if self._ws is None or self._ws.numel() < need.value:
+            self._ws = torch.empty(need.value, dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    def clips(self, mel: torch.Tensor) -> torch.Tensor:
+        return embed_clips(mel, self)
+
+    def windows(self, windows: torch.Tensor) -> torch.Tensor:
+        return embed_windows(windows, self)
+
+    def __del__(self) -> None:
+        h = getattr(self, "_handle", None)
+        if h is not None and h.value:
+            try:
+                lib().hbk_embed_plan_destroy(h)
+            except Exception:
+                pass
+            self._handle = None
+
+
+@torch.library.custom_op("hbk::embed_clips", mutates_args=())
+def _embed_clips_op(mel: torch.Tensor, plan_id: int) -> torch.Tensor:
+    plan = _plans[plan_id]
+    n = mel.shape[0]
+    out = torch.empty((n, len(plan.starts), plan.out_dim), dtype=torch.float32, device=mel.device)
+    ws = plan.workspace(n)
+    check(lib().hbk_embed_clips(plan._handle, ptr(mel), n, mel.stride(0), ptr(out), ptr(ws),
+                                ws.numel(), stream_ptr(mel.device)), "hbk_embed_clips")
+    return out
+
+
+@_embed_clips_op.register_fake
+def _(mel, plan_id):
+    plan = _plans[plan_id]
+    return mel.new_empty((mel.shape[0], len(plan.starts), plan.out_dim))
+
+
+@torch.library.custom_op("hbk::embed_windows", mutates_args=())
+def _embed_windows_op(windows: torch.Tensor, plan_id: int) -> torch.Tensor:
+    plan = _plans[plan_id]
+    n = windows.shape[0]
+    out = torch.empty((n, plan.out_dim), dtype=torch.float32, device=windows.device)
+    ws = plan.workspace(n)
+    check(lib().hbk_embed_windows(plan._handle, ptr(windows), n, ptr(out), ptr(ws), ws.numel(),
+                                  stream_ptr(windows.device)), "hbk_embed_windows")
+    return out
+
+
+@_embed_windows_op.register_fake
+def _(windows, plan_id):
+    plan = _plans[plan_id]
+    return windows.new_empty((windows.shape[0], plan.out_dim))
+
+
+def embed_clips(mel: torch.Tensor, plan: EmbedPlan) -> torch.Tensor:
+    """Unique mel frames [B, F >= seq_frames, n_mels] -> embeddings
+    [B, n_windows, out_dim] in the reference's slot order."""
+    if mel.dim() != 3 or mel.dtype != torch.float32 or mel.device != plan.device:
+        raise ValueError(f"mel must be [B, F, {plan.in_w}] float32 on {plan.device}")
+    if mel.shape[2] != plan.in_w or mel.shape[1] < plan.seq_frames:
+        raise ValueError(f"mel {tuple(mel.shape)}: need >= {plan.seq_frames} frames of {plan.in_w}")
+    if mel.stride(2) != 1 or mel.stride(1) != plan.in_w:
+        mel = mel.contiguous()
+    return torch.ops.hbk.embed_clips(mel, plan.id)
+
+
+def embed_windows(windows: torch.Tensor, plan: EmbedPlan) -> torch.Tensor:
+    """Reference per-window API: [n, in_h, in_w] (or [n, in_h, in_w, 1]) -> [n, out_dim]."""
+    if windows.dim() == 4 and windows.shape[3] == 1:
+        windows = windows[..., 0]
+    if (windows.dim() != 3 or tuple(windows.shape[1:]) != (plan.in_h, plan.in_w)
+            or windows.dtype != torch.float32 or windows.device != plan.device):
+        raise ValueError(f"windows must be [n, {plan.in_h}, {plan.in_w}] float32 on {plan.device}")
+    return torch.ops.hbk.embed_windows(windows.contiguous(), plan.id)

@@ -1,0 +1,109 @@
+"""Speech embedding: graph / window-map checks (CPU) and HIP parity (GPU).
+
+The embedding graph is runtime data (heybuddy.embedding_graph); parity is
+against oracle.embed.run_graph, which evaluates every 76-frame window on its
+own exactly as SpeechEmbeddingModel.__call__ does (embeddings.py:32-42) — so
+the GPU clip path's shared-prefix deduplication is checked too.
+Tolerance: fp32 MFMA vs fp64 oracle, |diff| <= 1e-4 * (1 + |ref|).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import embed as oemb
+from oracle import mel as omel
+
+
+def test_se20_graph_signature():
+    from heybuddy.embedding_graph import Conv, se20_graph
+    g = se20_graph()
+    convs = [op for op in g.ops if isinstance(op, Conv)]
+    assert len(convs) == 20 and convs[-1].name == "conv2d_19" and convs[-1].act is None
+    assert g.shapes()[-1] == (1, 1, 96)
+    # reference KAT: SpeechEmbedding.test feeds [100, 32] zeros -> [4, 96]
+    # (speech-embedding.js:50-68): windows of 76 at stride 8 over 100 frames
+    assert (100 - 76) // 8 + 1 == 4
+
+
+def test_window_starts_match_reference_slots():
+    """slot 4w + q <- audio window w (1920 samples = 12 frames), embedding
+    window q at stride 8 (embeddings.py:190, :136-143)."""
+    from heybuddy.embedding_graph import WINDOW_STARTS
+    assert WINDOW_STARTS == (0, 8, 16, 24, 12, 20, 28, 36, 24, 32, 40, 48, 36, 44, 52, 60)
+    assert len(set(WINDOW_STARTS)) == 14 and max(WINDOW_STARTS) + 76 == 136
+
+
+def test_oracle_graph_shapes_and_squeeze():
+    from heybuddy.embedding_graph import se20_graph
+    g = se20_graph()
+    x = np.zeros((3, 76, 32, 1), dtype=np.float32)
+    out = oemb.speech_embedding_model(g, x)
+    assert out.shape == (3, 96)
+    one = oemb.speech_embedding_model(g, x[:1])
+    assert one.shape == (96,)  # the reference's .squeeze() drops n == 1
+
+
+def _mel_clips(n, seed=3):
+    from heybuddy.synthetic import synthetic_clips
+    clips = synthetic_clips(n, seed=seed)
+    mel, _, _ = omel.mel_frames(clips.numpy(), 141)
+    return mel
+
+
+def _oracle_clip_embeddings(graph, mel):
+    from heybuddy.embedding_graph import WINDOW_STARTS
+    wins = np.stack([mel[:, s:s + 76] for s in WINDOW_STARTS], axis=1)  # [B,16,76,32]
+    ref = oemb.run_graph(graph, wins.reshape(-1, 76, 32))
+    return ref.reshape(mel.shape[0], len(WINDOW_STARTS), -1)
+
+
+def _close(out, ref, tol=1e-4):
+    err = np.abs(out - ref)
+    bound = tol * (1.0 + np.abs(ref))
+    return (err <= bound).all(), err.max()
+
+
+@pytest.mark.gpu
+def test_embed_windows_parity():
+    from heybuddy.embedding_graph import se20_graph
+    from heybuddy.kernels import EmbedPlan
+    g = se20_graph()
+    plan = EmbedPlan(g)
+    rng = np.random.default_rng(5)
+    wins = (rng.standard_normal((37, 76, 32)) * 2 + 6).astype(np.float32)
+    out = plan.windows(torch.from_numpy(wins).cuda()).cpu().numpy()
+    ref = oemb.run_graph(g, wins)
+    ok, worst = _close(out, ref)
+    assert out.shape == (37, 96) and ok, f"max |diff| {worst}"
+
+
+@pytest.mark.gpu
+def test_embed_clips_parity_shared_prefix():
+    from heybuddy.embedding_graph import se20_graph
+    from heybuddy.kernels import EmbedPlan
+    g = se20_graph()
+    plan = EmbedPlan(g)
+    assert plan.seq_frames == 136 and plan.n_prefix_ops == 13
+    mel = _mel_clips(5)
+    out = plan.clips(torch.from_numpy(mel).cuda()).cpu().numpy()
+    ref = _oracle_clip_embeddings(g, mel)
+    ok, worst = _close(out, ref)
+    assert out.shape == (5, 16, 96) and ok, f"max |diff| {worst}"
+    # duplicated windows (start 24 and 36 appear twice) give identical rows
+    np.testing.assert_array_equal(out[:, 3], out[:, 8])
+    np.testing.assert_array_equal(out[:, 7], out[:, 12])
+
+
+@pytest.mark.gpu
+def test_embed_clips_ragged_batches():
+    """Clip counts that leave partial task groups, and one clip."""
+    from heybuddy.embedding_graph import se20_graph
+    from heybuddy.kernels import EmbedPlan
+    g = se20_graph()
+    plan = EmbedPlan(g)
+    mel = _mel_clips(3, seed=11)
+    ref = _oracle_clip_embeddings(g, mel)
+    for n in (1, 3):
+        out = plan.clips(torch.from_numpy(mel[:n]).cuda()).cpu().numpy()
+        ok, worst = _close(out, ref[:n])
+        assert ok, f"n={n}: max |diff| {worst}"
