@@ -1,0 +1,170 @@
+"""Generate tests/golden/*.npz by running the REFERENCE itself (container only).
+
+TEST INFRASTRUCTURE ONLY. Needs /root/reference (read-only); it copies
+src/python to a temp dir (the reference creates pretrained/ and precalculated/
+dirs at import, pretrained_util.py:5-6, precalculated.py:35-36), stubs the
+modules that are not installed (av, soundfile, wandb, piper_phonemize,
+torchaudio, torchmetrics — none is on the hot path), imports heybuddy and
+records its outputs on seeded inputs:
+
+  featurizer_index.npz   SpeechEmbeddings.__call__ (embeddings.py:153-234) with
+                         index-encoding fakes for the two ONNX models: pins the
+                         frame / audio-window / embedding-window maps, slot
+                         order and spectrogram truncation bit-exactly.
+  featurizer_oracle.npz  SpeechEmbeddings.__call__ with the oracle mel graph
+                         and the SE20 stand-in graph injected: pins the whole
+                         orchestration numerically (inputs included).
+  classifier.npz         WakeWordMLPModel forward / BCE / backward / Adam and
+                         WakeWordTrainer.train_epoch histories (seeded).
+
+Usage: python oracle/make_golden.py [--only featurizer|classifier]
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import shutil
+import sys
+import tempfile
+import types
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = "/root/reference/src/python"
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def import_reference():
+    """Import heybuddy from a temp copy of the reference with stub modules."""
+    import torch
+    tmp = tempfile.mkdtemp(prefix="hbref_")
+    shutil.copytree(REF, os.path.join(tmp, "src"))
+    sys.dont_write_bytecode = True
+    for m in ["av", "soundfile", "wandb", "piper_phonemize", "torchaudio"]:
+        sys.modules[m] = types.ModuleType(m)
+    sys.modules["piper_phonemize"].phonemize_espeak = None
+    tm = types.ModuleType("torchmetrics")
+
+    class _Recall:  # torchmetrics.Recall/Accuracy stand-in: only feeds logged metrics
+        def __init__(self, task=None, threshold=0.5):
+            self.t = threshold
+
+        def to(self, d):
+            return self
+
+        def __call__(self, p, y):
+            p = (p.flatten() >= self.t).float()
+            y = y.flatten().float()
+            return (p * y).sum() / torch.clamp(y.sum(), min=1)
+
+    tm.Recall = tm.Accuracy = _Recall
+    sys.modules["torchmetrics"] = tm
+    torch.cuda.synchronize = lambda *a, **k: None  # trainer.py:593-594 call these every step
+    torch.cuda.empty_cache = lambda *a, **k: None
+    cwd = os.getcwd()
+    os.chdir(tmp)
+    sys.path.insert(0, os.path.join(tmp, "src"))
+    import heybuddy.embeddings
+    import heybuddy.trainer
+    import heybuddy.wakeword
+    os.chdir(cwd)
+    return heybuddy
+
+
+def _fake_models():
+    """Index-encoding stand-ins for the two ONNX graphs.
+
+    The audio sample value at index k of clip c is (c * 1e5 + k) / 32767, so
+    after the reference's *32767 a frame's first sample rounds back to a global
+    sample index. The fake mel returns, for every frame, its global FRAME index
+    (= first sample / 160) in all 32 bins; the fake embedding returns, for
+    every window, its first frame value in all 96 dims (+ clip id * 1e3).
+    """
+    def mel(audio):
+        audio = np.asarray(audio, dtype=np.float64)
+        if audio.ndim == 1:
+            audio = audio[None]
+        b, t = audio.shape
+        nf = (t - 512) // 160 + 1
+        first = np.rint(audio[:, np.arange(nf) * 160]) % 100000
+        out = np.repeat((first / 160.0)[:, :, None], 32, axis=2)
+        clip = np.floor(np.rint(audio[:, :1]) / 100000)[:, :, None]
+        return (out + clip * 1000.0).astype(np.float32)
+
+    def emb(spectrograms):
+        s = np.asarray(spectrograms)[..., 0]        # [n, 76, 32]
+        return np.repeat(s[:, 0, :1], 96, axis=1)   # window's first frame code
+    return mel, emb
+
+
+def make_featurizer(hb):
+    import torch
+    from heybuddy.embedding_graph import se20_graph
+    from oracle import embed as oemb
+    from oracle import mel as omel
+    se = hb.embeddings.SpeechEmbeddings()
+    # --- index maps ---
+    mel, emb = _fake_models()
+    se.spectrogram = mel
+    se.embeddings = emb
+    t = 24000
+    k = np.arange(t, dtype=np.float64)
+    audio = np.stack([(c * 1e5 + k) / 32767.0 for c in range(2)])
+    res = {}
+    for name, length in (("t24000", 24000), ("t23040", 23040), ("t17280", 17280)):
+        # copy: the reference scales its input tensor IN PLACE (embeddings.py:182)
+        x = torch.from_numpy(audio[:, None, :length].copy())
+        e, s = se(x, return_spectrograms=True, remove_nan=False)
+        res[f"{name}_emb"] = e
+        res[f"{name}_spec"] = s
+    np.savez_compressed(os.path.join(GOLDEN, "featurizer_index.npz"), **res)
+    # --- numeric orchestration with oracle models injected ---
+    g = se20_graph(1234)
+    se.spectrogram = lambda a: omel.mel_spectrogram_model(a)
+    se.embeddings = lambda w: oemb.speech_embedding_model(g, w)
+    rng = np.random.default_rng(20251015)
+    tt = np.arange(24000) / 16000.0
+    clips = []
+    for _ in range(3):
+        f = rng.uniform(80, 4000, 6)
+        ph = rng.uniform(0, 2 * np.pi, 6)
+        x = 0.25 * np.sin(2 * np.pi * f[:, None] * tt[None] + ph[:, None]).sum(0)
+        x = x * np.hanning(24000) + 0.01 * rng.standard_normal(24000)
+        clips.append(np.clip(x, -1, 1).astype(np.float32))
+    clips = np.stack(clips)
+    int16 = (clips[:2, :23500] * 32767).astype(np.int16)
+    e_f32, s_f32 = se(list(clips), return_spectrograms=True)         # list of f32 arrays
+    e_i16 = se([int16[0], int16[1]], remove_nan=False)               # int16 path, cropped to min
+    e_2d = se(torch.from_numpy(clips[:2].copy()))                     # 2-D: ONE clip, 2 channels
+    np.savez_compressed(os.path.join(GOLDEN, "featurizer_oracle.npz"), clips=clips, int16=int16,
+                        emb_f32=e_f32, spec_f32=s_f32, emb_i16=e_i16, emb_2d=e_2d,
+                        graph_seed=np.array(1234))
+    print("featurizer fixtures written")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default=None)
+    args = ap.parse_args()
+    if not os.path.isdir(REF):
+        print("no /root/reference: nothing to do")
+        return
+    os.makedirs(GOLDEN, exist_ok=True)
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "hey-buddy_amd")]
+    hb = import_reference()
+    # our package is also called "heybuddy": the reference module objects are
+    # held in `hb`; drop them from sys.modules so oracle/ imports ours.
+    ref_mods = {k: v for k, v in sys.modules.items() if k == "heybuddy" or k.startswith("heybuddy.")}
+    for k in ref_mods:
+        del sys.modules[k]
+    sys.path = [p for p in sys.path if not p.endswith("/src")]
+    if args.only in (None, "featurizer"):
+        make_featurizer(hb)
+    if args.only in (None, "classifier"):
+        from oracle import golden_classifier
+        golden_classifier.make(hb, GOLDEN)
+
+
+if __name__ == "__main__":
+    main()
