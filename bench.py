@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--clips", type=int, default=100_000, help="clips per rank per step")
-    ap.add_argument("--cpu-sample", type=int, default=384, help="clips timed on the host CPU")
+    ap.add_argument("--cpu-sample", type=int, default=3000, help="clips timed on the host CPU (~10-30 s)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r01.json"),
                     help="per-kernel HBM bytes from a rocprofv3 --pmc pass (optional)")

@@ -51,6 +51,9 @@ __device__ __forceinline__ cf cmul(cf a, cf b) {
   const cf bs = {-b.y, b.x};
   return __builtin_elementwise_fma(cf{a.y, a.y}, bs, cf{a.x, a.x} * b);
 }
+// max that propagates NaN (torch / numpy max-pool semantics; fmaxf drops NaN)
+__device__ __forceinline__ float nan_max(float a, float b) { return (b > a || b != b) ? b : a; }
+
 // multiply by -i
 __device__ __forceinline__ cf cmul_mi(cf a) { return cf{a.y, -a.x}; }
 

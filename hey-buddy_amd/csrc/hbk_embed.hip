@@ -176,7 +176,7 @@ __global__ void __launch_bounds__(kThreads) conv_chain_kernel(ChainArgs a) {
                          (w * a.in_pw) * C + c;
       float v = src[0];
       for (int i = 0; i < a.in_ph; ++i)
-        for (int j = 0; j < a.in_pw; ++j) v = fmaxf(v, src[i * a.src_row_stride + j * C]);
+        for (int j = 0; j < a.in_pw; ++j) v = nan_max(v, src[i * a.src_row_stride + j * C]);
       X[((g * rows_in + r) * a.W_in + w) * cinp0 + c] = v;
     }
 
@@ -224,7 +224,7 @@ __global__ void __launch_bounds__(kThreads) conv_chain_kernel(ChainArgs a) {
       const float* p = cur + ((g * hin + r * a.out_ph) * win + w * a.out_pw) * coutp + c;
       float v = p[0];
       for (int i = 0; i < a.out_ph; ++i)
-        for (int j = 0; j < a.out_pw; ++j) v = fmaxf(v, p[(i * win + j) * coutp]);
+        for (int j = 0; j < a.out_pw; ++j) v = nan_max(v, p[(i * win + j) * coutp]);
       a.out[(img0 + g) * a.out_img_stride + static_cast<int64_t>(orow0 + r) * orow_elems + w * a.C_out + c] = v;
     }
     __syncthreads();  // the next task restages X
@@ -580,7 +580,9 @@ int hbk_embed_plan_create(const hbk_graph_op* ops, int32_t n_ops, int32_t in_h, 
   // the windows aligned iff the cumulative time stride divides every start.
   int g = 0;
   for (int s : p->starts) g = std::gcd(g, s);
-  int stride = 1, split = n_ops;
+  // If every pool keeps the alignment, split at the last pool (any earlier
+  // split is equally valid; the tail must start with a pool).
+  int stride = 1, split = n_ops, last_pool = -1, stride_before_last = 1;
   for (int i = 0; i < n_ops; ++i) {
     if (p->ops[i].kind == HBK_OP_MAXPOOL) {
       const int ns = stride * p->ops[i].kh;
@@ -588,8 +590,14 @@ int hbk_embed_plan_create(const hbk_graph_op* ops, int32_t n_ops, int32_t in_h, 
         split = i;
         break;
       }
+      last_pool = i;
+      stride_before_last = stride;
       stride = ns;
     }
+  }
+  if (split == n_ops && last_pool > 0) {
+    split = last_pool;
+    stride = stride_before_last;
   }
   // the tail must start with a pool (its input pool) and contain a conv
   if (split == n_ops || split == 0) {

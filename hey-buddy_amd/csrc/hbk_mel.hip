@@ -210,7 +210,9 @@ __global__ void __launch_bounds__(kThreads) mel_frames_kernel(MelArgs a) {
 #pragma unroll 4
         for (int t = 0; t < a.taps; ++t) acc = fmaf(w[t], pbuf[lo + t], acc);
       }
-      y[q] = 10.f * log10f(fmaxf(acc, a.log_floor)) / a.out_div + a.out_add;
+      // clamp(min=floor) that keeps NaN (torch.clamp / np.maximum semantics)
+      const float c = acc < a.log_floor ? a.log_floor : acc;
+      y[q] = 10.f * log10f(c) / a.out_div + a.out_add;
     }
     const uint32_t g = grp * kFramesPerBlock + slot;
     if (g < total && 2 * j < a.n_mels)
