@@ -242,3 +242,113 @@ def embed_windows(windows: torch.Tensor, plan: EmbedPlan) -> torch.Tensor:
             or windows.dtype != torch.float32 or windows.device != plan.device):
         raise ValueError(f"windows must be [n, {plan.in_h}, {plan.in_w}] float32 on {plan.device}")
     return torch.ops.hbk.embed_windows(windows.contiguous(), plan.id)
+
+
+class MlpPlan:
+    """The gated-MLP classifier on the HIP path (hbk_mlp_*): flat parameter
+    layout, forward, and the two halves of a train step."""
+
+    N_STATS = 8
+
+    def __init__(self, d_in: int = 1536, layer_dim: int = 96, hidden: int = 64, n_layers: int = 2) -> None:
+        handle = ctypes.c_void_p()
+        check(lib().hbk_mlp_plan_create(d_in, layer_dim, hidden, n_layers, ctypes.byref(handle)),
+              "hbk_mlp_plan_create")
+        self._handle = handle
+        self.d_in, self.layer_dim, self.hidden, self.n_layers = d_in, layer_dim, hidden, n_layers
+        n = ctypes.c_int64()
+        n_off = 2 + 4 * (n_layers + 2) + 2 * (n_layers + 1)
+        offs = (ctypes.c_int64 * n_off)()
+        check(lib().hbk_mlp_layout(handle, ctypes.byref(n), offs, n_off), "hbk_mlp_layout")
+        self.n_params = n.value
+        self.offsets = list(offs)
+        self._ws: Dict[torch.device, torch.Tensor] = {}
+
+    def views(self, flat: torch.Tensor) -> "Dict[str, torch.Tensor]":
+        """state_dict-named views (reference names and shapes) into ``flat``."""
+        from collections import OrderedDict
+        H, L, D = self.hidden, self.layer_dim, self.d_in
+        o = self.offsets
+        out = OrderedDict()
+
+        def v(off, *shape):
+            n = int(np.prod(shape))
+            return flat[off:off + n].view(*shape)
+
+        out["norm_in.weight"] = v(o[0], D)
+        out["norm_in.bias"] = v(o[1], D)
+        gm = o[2:2 + 4 * (self.n_layers + 2)]
+        ln = o[2 + 4 * (self.n_layers + 2):]
+
+        def gmlp(prefix, k, din, dout):
+            w_hg, b_hg, w_o, b_o = gm[4 * k:4 * k + 4]
+            out[f"{prefix}.hidden.weight"] = v(w_hg, H, din)
+            out[f"{prefix}.hidden.bias"] = v(b_hg, H)
+            out[f"{prefix}.output.weight"] = v(w_o, dout, H)
+            out[f"{prefix}.output.bias"] = v(b_o, dout)
+            out[f"{prefix}.gate.weight"] = v(w_hg + H * din, H, din)
+            out[f"{prefix}.gate.bias"] = v(b_hg + H, H)
+
+        gmlp("mlp_in", 0, D, L)
+        for l in range(self.n_layers):
+            out[f"layers.{l}.0.weight"] = v(ln[2 * l], L)
+            out[f"layers.{l}.0.bias"] = v(ln[2 * l + 1], L)
+            gmlp(f"layers.{l}.1", l + 1, L, L)
+        out["norm_out.weight"] = v(ln[2 * self.n_layers], L)
+        out["norm_out.bias"] = v(ln[2 * self.n_layers + 1], L)
+        gmlp("mlp_out", self.n_layers + 1, L, 1)
+        return out
+
+    def workspace(self, batch: int, device: torch.device) -> torch.Tensor:
+        need = ctypes.c_int64()
+        check(lib().hbk_mlp_workspace_size(self._handle, int(batch), ctypes.byref(need)),
+              "hbk_mlp_workspace_size")
+        ws = self._ws.get(device)
+        if ws is None or ws.numel() < need.value:
+            ws = torch.empty(need.value, dtype=torch.uint8, device=device)
+            self._ws[device] = ws
+        return ws
+
+    def _check(self, params: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+        if params.numel() != self.n_params or params.dtype != torch.float32 or not params.is_contiguous():
+            raise ValueError("params must be the contiguous flat f32 buffer")
+        x = x.reshape(x.shape[0], -1)
+        if x.shape[1] != self.d_in or x.dtype != torch.float32 or x.device != params.device:
+            raise ValueError(f"x must be [B, {self.d_in}] f32 on {params.device}")
+        return x.contiguous()
+
+    def forward(self, params: torch.Tensor, x: torch.Tensor, dropout_p: float = 0.0, seed: int = 0,
+                logits: bool = False):
+        x = self._check(params, x)
+        b = x.shape[0]
+        prob = torch.empty(b, dtype=torch.float32, device=x.device)
+        logit = torch.empty(b, dtype=torch.float32, device=x.device) if logits else None
+        ws = self.workspace(b, x.device)
+        check(lib().hbk_mlp_forward(self._handle, ptr(params), ptr(x), b, ptr(prob),
+                                    ptr(logit) if logit is not None else None, float(dropout_p),
+                                    int(seed) & (2 ** 64 - 1), ptr(ws), ws.numel(),
+                                    stream_ptr(x.device)), "hbk_mlp_forward")
+        return (prob, logit) if logits else prob
+
+    def train_fwd_bwd(self, params: torch.Tensor, x: torch.Tensor, y: torch.Tensor, bucket: torch.Tensor,
+                      neg_weight: float, threshold: float = 1e-4, activation_threshold: float = 0.5,
+                      dropout_p: float = 0.0, seed: int = 0, prob: torch.Tensor | None = None) -> None:
+        x = self._check(params, x)
+        b = x.shape[0]
+        y = y.to(device=x.device, dtype=torch.float32).contiguous()
+        if y.numel() != b or bucket.numel() != self.n_params + self.N_STATS:
+            raise ValueError("bad y / bucket size")
+        ws = self.workspace(b, x.device)
+        check(lib().hbk_mlp_train_fwd_bwd(self._handle, ptr(params), ptr(x), ptr(y), b, float(neg_weight),
+                                          float(threshold), float(activation_threshold), float(dropout_p),
+                                          int(seed) & (2 ** 64 - 1), ptr(bucket),
+                                          ptr(prob) if prob is not None else None, ptr(ws), ws.numel(),
+                                          stream_ptr(x.device)), "hbk_mlp_train_fwd_bwd")
+
+    def gate_adam(self, params, bucket, m, v, state, ctrl, history, lr, beta1=0.9, beta2=0.999,
+                  eps=1e-8) -> None:
+        cap = 0 if history is None else history.shape[0]
+        check(lib().hbk_mlp_gate_adam(self._handle, ptr(params), ptr(bucket), ptr(m), ptr(v), ptr(state),
+                                      ptr(ctrl), ptr(history) if history is not None else None, cap,
+                                      float(lr), float(beta1), float(beta2), float(eps),
+                                      stream_ptr(params.device)), "hbk_mlp_gate_adam")

@@ -1,0 +1,431 @@
+"""Drop-in for heybuddy.trainer (reference src/python/heybuddy/trainer.py).
+
+``WakeWordTrainer`` keeps the reference's constructor, ``get_learning_rate``,
+``loss``, ``num_false_positives``, ``train_epoch`` (same arguments, same
+11-tuple of histories) and the 3-stage ``__call__``, checkpoints
+(``{name}.pt`` + ``{name}_optimizer.pt``) and ``resume``. Each optimisation
+step is the fused HIP train step of libhbk.so:
+
+  hbk_mlp_train_fwd_bwd  forward (+ input dropout), high-loss filter, weighted
+                         BCE, backward -> gradient bucket + statistics
+  all_reduce(bucket)     RCCL, only when torch.distributed is initialised:
+                         every rank trains on a 1/world slice of each batch
+  hbk_mlp_gate_adam      the reference's < 128-sample accumulation gate on the
+                         global statistics, then Adam iff it fires
+
+No host synchronisation per step (the reference forces gc.collect(),
+empty_cache() and synchronize() every step, trainer.py:592-594); the loss /
+recall / false-positive histories are rebuilt from a device-side per-step
+record with the reference's bookkeeping rules (trainer.py:443-494).
+"""
+from __future__ import annotations
+
+import math
+import os
+import random
+from time import perf_counter
+from typing import Any, Dict, List, Optional, Tuple, Union
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from heybuddy.constants import *  # noqa: F401,F403
+from heybuddy.constants import (DEFAULT_ACTIVATION_THRESHOLD, DEFAULT_ARCHITECTURE,
+                                DEFAULT_BATCH_SIZE_ADJUST_RATIO, DEFAULT_CHECKPOINT_STEPS,
+                                DEFAULT_DYNAMIC_NEGATIVE_WEIGHT, DEFAULT_HEADS,
+                                DEFAULT_HIGH_LOSS_THRESHOLD, DEFAULT_HOLD_STEPS, DEFAULT_LAYER_DIM,
+                                DEFAULT_LAYERS, DEFAULT_LEARNING_RATE,
+                                DEFAULT_LEARNING_RATE_ADJUST_RATIO, DEFAULT_LOGGING_STEPS,
+                                DEFAULT_NEGATIVE_WEIGHT, DEFAULT_NEGATIVE_WEIGHT_ADJUST_RATIO,
+                                DEFAULT_STAGES, DEFAULT_STEP_ADJUST_RATIO, DEFAULT_STEPS,
+                                DEFAULT_TARGET_FALSE_POSITIVE_RATE, DEFAULT_VALIDATION_STEPS,
+                                DEFAULT_WARMUP_STEPS)
+from heybuddy.util import logger
+from heybuddy.wakeword import WakeWordMLPModel
+
+__all__ = ["Trainer", "WakeWordTrainer"]
+
+BETAS = (0.9, 0.999)
+EPS = 1e-8
+
+
+class Trainer(nn.Module):
+    """Base trainer: checkpoint dir, model, optimizer, LR schedule (trainer.py:27-204)."""
+
+    def __init__(self, checkpoint_dir: str = "./checkpoints", learning_rate: float = DEFAULT_LEARNING_RATE,
+                 device: Optional[Union[str, torch.device]] = None, **model_kwargs: Any) -> None:
+        super().__init__()
+        self.checkpoint_dir = os.path.abspath(checkpoint_dir)
+        os.makedirs(self.checkpoint_dir, exist_ok=True)
+        self.model = self.create_model(**model_kwargs)
+        if device is None and torch.cuda.is_available():
+            device = torch.device("cuda", torch.cuda.current_device())
+        if device is not None:
+            self.model.to(device)
+        self.learning_rate = learning_rate
+        self.optimizer = torch.optim.Adam(self.model.parameters(), lr=learning_rate)
+        self._init_state()
+
+    def create_model(self, **kwargs: Any) -> nn.Module:
+        raise NotImplementedError()
+
+    # device-resident optimiser state (the kernels' flat layout)
+    def _init_state(self) -> None:
+        flat = self.model.flat_parameters
+        dev = flat.device
+        self._m = torch.zeros_like(flat)
+        self._v = torch.zeros_like(flat)
+        self._state = torch.tensor([0.0, 1.0, 0.0, 0.0], dtype=torch.float32, device=dev)
+        self._ctrl = torch.zeros(4, dtype=torch.float32, device=dev)
+        self._bucket = torch.zeros(flat.numel() + self.model.plan.N_STATS, dtype=torch.float32, device=dev)
+
+    def _apply(self, fn, recurse=True):
+        super()._apply(fn, recurse)
+        if hasattr(self, "_m"):
+            self._m, self._v = fn(self._m), fn(self._v)
+            self._state, self._ctrl, self._bucket = fn(self._state), fn(self._ctrl), fn(self._bucket)
+        return self
+
+    @property
+    def device(self) -> torch.device:
+        return self.model.device
+
+    def get_learning_rate(self, step: int, warmup_steps: int = 0, hold_steps: int = 0, total_steps: int = 0,
+                          start_learning_rate: float = 0.0,
+                          target_learning_rate: float = DEFAULT_LEARNING_RATE) -> np.ndarray:
+        """Cosine decay with linear warmup and a hold (trainer.py:127-156)."""
+        learning_rate = 0.5 * target_learning_rate * (1 + np.cos(
+            np.pi * (step - warmup_steps - hold_steps) / float(total_steps - warmup_steps - hold_steps)))
+        warmup_learning_rate = target_learning_rate * (step / warmup_steps) if warmup_steps > 0 else 0.0
+        if hold_steps > 0:
+            learning_rate = np.where(step > warmup_steps + hold_steps, learning_rate, target_learning_rate)
+        return np.where(step < warmup_steps, warmup_learning_rate, learning_rate)
+
+    # -- checkpoints (trainer.py:186-198, resume :54-118) ----------------------
+    def _sync_torch_optimizer(self) -> None:
+        """Expose the kernels' Adam state through torch.optim.Adam's state_dict."""
+        t = int(self._state[2].item())
+        views_m = self.model.plan.views(self._m)
+        views_v = self.model.plan.views(self._v)
+        for name, p in self.model.named_parameters():
+            st = self.optimizer.state[p]
+            st["step"] = torch.tensor(float(t))
+            st["exp_avg"] = views_m[name]
+            st["exp_avg_sq"] = views_v[name]
+
+    def save_checkpoint(self, name: str, optimizer: bool = True) -> None:
+        torch.save(self.model.state_dict(), os.path.join(self.checkpoint_dir, f"{name}.pt"))
+        if optimizer:
+            self._sync_torch_optimizer()
+            torch.save(self.optimizer.state_dict(), os.path.join(self.checkpoint_dir, f"{name}_optimizer.pt"))
+
+    def resume(self, name: str) -> None:
+        files = os.listdir(self.checkpoint_dir)
+        models = sorted(((f, os.path.getmtime(os.path.join(self.checkpoint_dir, f))) for f in files
+                         if f.startswith(name) and f.endswith(".pt") and not f.endswith("_optimizer.pt")),
+                        key=lambda x: x[1], reverse=True)
+        opts = sorted(((f, os.path.getmtime(os.path.join(self.checkpoint_dir, f))) for f in files
+                       if f.startswith(name) and f.endswith("_optimizer.pt")), key=lambda x: x[1], reverse=True)
+        pair = next(((m, o) for m, mt in models for o, ot in opts if abs(mt - ot) < 2), None)
+        if pair is None:
+            raise FileNotFoundError(f"Checkpoint {name} not found.")
+        logger.info(f"Resuming training from {pair[0]} and {pair[1]}.")
+        self.model.load_state_dict(torch.load(os.path.join(self.checkpoint_dir, pair[0]), weights_only=True))
+        osd = torch.load(os.path.join(self.checkpoint_dir, pair[1]), weights_only=True)
+        names = [n for n, _ in self.model.named_parameters()]
+        vm, vv = self.model.plan.views(self._m), self.model.plan.views(self._v)
+        t = 0.0
+        for idx, st in osd.get("state", {}).items():
+            n = names[int(idx)]
+            vm[n].copy_(st["exp_avg"].to(vm[n].device))
+            vv[n].copy_(st["exp_avg_sq"].to(vv[n].device))
+            t = float(st["step"])
+        self._state.copy_(torch.tensor([0.0, 1.0, t, 0.0]))
+
+    def __call__(self, training: Any, **kwargs: Any) -> None:
+        raise NotImplementedError()
+
+
+def _recall(tp: float, n_pos: float) -> float:
+    return tp / n_pos if n_pos > 0 else 0.0
+
+
+class WakeWordTrainer(Trainer):
+    """Trainer for the wake-word classifier (trainer.py:206-1007)."""
+
+    def __init__(self, checkpoint_dir: str = "./checkpoints", learning_rate: float = DEFAULT_LEARNING_RATE,
+                 input_shape: Tuple[int, int] = (16, 96), num_layers: int = DEFAULT_LAYERS,
+                 layer_dim: int = DEFAULT_LAYER_DIM, num_heads: int = DEFAULT_HEADS,
+                 architecture: str = DEFAULT_ARCHITECTURE, device: Optional[Union[str, torch.device]] = None,
+                 **model_kwargs: Any) -> None:
+        super().__init__(checkpoint_dir=checkpoint_dir, learning_rate=learning_rate, device=device,
+                         input_shape=input_shape, num_layers=num_layers, layer_dim=layer_dim,
+                         num_heads=num_heads, architecture=architecture, **model_kwargs)
+        self.input_shape = input_shape
+        self.num_layers = num_layers
+        self.num_heads = num_heads
+        self.architecture = architecture
+        self.layer_dim = layer_dim
+
+    def create_model(self, input_shape=(16, 96), architecture: str = DEFAULT_ARCHITECTURE,
+                     layer_dim: int = DEFAULT_LAYER_DIM, num_layers: int = DEFAULT_LAYERS,
+                     num_heads: int = DEFAULT_HEADS, **kwargs: Any) -> nn.Module:
+        if architecture != "perceptron":
+            raise NotImplementedError("the MI355X path implements the default 'perceptron' architecture")
+        return WakeWordMLPModel(input_shape=input_shape, num_layers=num_layers, layer_dim=layer_dim, **kwargs)
+
+    def num_false_positives(self, x: torch.Tensor, y: torch.Tensor,
+                            activation_threshold: float = DEFAULT_ACTIVATION_THRESHOLD) -> torch.Tensor:
+        return (y - x <= -activation_threshold).sum()
+
+    def loss(self, x: torch.Tensor, y: torch.Tensor, weight: Optional[torch.Tensor] = None) -> torch.Tensor:
+        if weight is None:
+            return nn.functional.binary_cross_entropy(x, y)
+        return nn.functional.binary_cross_entropy(x, y, weight.to(x.device))
+
+    # -- data parallel ---------------------------------------------------------
+    @staticmethod
+    def _world() -> Tuple[int, int]:
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_rank(), dist.get_world_size()
+        return 0, 1
+
+    def _step(self, x: torch.Tensor, y: torch.Tensor, lr: float, neg_weight: float, threshold: float,
+              activation_threshold: float, history: Optional[torch.Tensor], seed: int) -> None:
+        rank, world = self._world()
+        if world > 1:  # class-stratified slice: batches are [positives | adversarial | negatives]
+            x, y = x[rank::world], y[rank::world]
+        dev = self.device
+        x = x.to(dev, non_blocking=True)
+        y = y.to(dev, non_blocking=True)
+        plan = self.model.plan
+        p = self.model.dropout.p if self.model.training else 0.0
+        plan.train_fwd_bwd(self.model.flat_parameters, x.reshape(x.shape[0], -1), y, self._bucket,
+                           neg_weight, threshold, activation_threshold, dropout_p=p,
+                           seed=seed * 1000003 + rank)
+        if world > 1:
+            dist.all_reduce(self._bucket)
+        plan.gate_adam(self.model.flat_parameters, self._bucket, self._m, self._v, self._state, self._ctrl,
+                       history, lr, BETAS[0], BETAS[1], EPS)
+
+    @torch.no_grad()
+    def _predict_all(self, data: Any) -> Tuple[torch.Tensor, torch.Tensor]:
+        preds, labels = [], []
+        for datum in data:
+            x, y = datum[0].to(self.device), datum[1].to(self.device)
+            preds.append(self.model(x)[:, 0])
+            labels.append(y)
+        return torch.cat(preds), torch.cat(labels)
+
+    def train_epoch(self, training: Any, validation: Optional[Any] = None, testing: Optional[Any] = None,
+                    num_steps: int = DEFAULT_STEPS, warmup_steps: int = DEFAULT_WARMUP_STEPS,
+                    hold_steps: int = DEFAULT_HOLD_STEPS,
+                    negative_weight_schedule: Union[float, List[float]] = DEFAULT_NEGATIVE_WEIGHT,
+                    negative_weight_adjust_ratio: Optional[float] = None,
+                    target_false_positive_rate: float = DEFAULT_TARGET_FALSE_POSITIVE_RATE,
+                    validation_steps: int = DEFAULT_VALIDATION_STEPS,
+                    checkpoint_steps: int = DEFAULT_CHECKPOINT_STEPS,
+                    logging_steps: int = DEFAULT_LOGGING_STEPS,
+                    learning_rate: float = DEFAULT_LEARNING_RATE,
+                    high_loss_threshold: float = DEFAULT_HIGH_LOSS_THRESHOLD,
+                    activation_threshold: float = DEFAULT_ACTIVATION_THRESHOLD,
+                    description: str = "Training", name: str = "heybuddy", last_loss: float = 0.0,
+                    last_recall: float = 0.0, last_false_positive_rate: float = 0.0,
+                    last_validation_false_positive_per_hour: float = 0.0,
+                    last_validation_recall: float = 0.0, last_testing_accuracy: float = 0.0,
+                    last_testing_recall: float = 0.0, last_testing_false_positive_rate: float = 0.0,
+                    use_wandb: bool = False) -> Tuple[Optional[torch.Tensor], ...]:
+        """One epoch (trainer.py:314-608). Returns the reference's 11 histories."""
+        if use_wandb:
+            logger.warning("wandb logging is outside the MI355X hot path; ignored")
+        self._state.copy_(torch.tensor([0.0, 1.0, float(self._state[2].item()), 0.0]))
+        history = torch.zeros((num_steps, 8), dtype=torch.float32, device=self.device)
+        lr_hist: List[float] = []
+        nw_hist: List[float] = []
+        batch_sizes: List[int] = []
+        v_fp: List[float] = []
+        v_rec: List[float] = []
+        t_acc: List[float] = []
+        t_rec: List[float] = []
+        t_fp: List[float] = []
+        seed0 = random.getrandbits(31)
+        for step, datum in enumerate(training):
+            if step >= num_steps:
+                break
+            x, y = datum[0], datum[1]
+            lr = float(self.get_learning_rate(step, warmup_steps=warmup_steps, hold_steps=hold_steps,
+                                              total_steps=num_steps, target_learning_rate=learning_rate))
+            lr_hist.append(lr)
+            for g in self.optimizer.param_groups:
+                g["lr"] = lr
+            if isinstance(negative_weight_schedule, (float, int)):
+                nw = float(negative_weight_schedule)
+            elif len(negative_weight_schedule) <= step:
+                nw = float(negative_weight_schedule[-1])
+            else:
+                nw = float(negative_weight_schedule[step])
+            nw_hist.append(nw)
+            batch_sizes.append(int(y.shape[0]))
+            self._step(x, y, lr, nw, high_loss_threshold, activation_threshold, history, seed0 + step)
+            if step > 0 and step % validation_steps == 0:
+                if validation is not None:
+                    preds, labels = self._predict_all(validation)
+                    n_neg = int((labels == 0).sum().item())
+                    hours = n_neg * 1.44 / 3600
+                    fph = float(self.num_false_positives(preds, labels, activation_threshold).item()) / hours
+                    v_fp.append(fph)
+                    pos = labels == 1
+                    v_rec.append(_recall(float((preds[pos] > activation_threshold).sum().item()),
+                                         float(pos.sum().item())))
+                    if negative_weight_adjust_ratio is not None:
+                        assert isinstance(negative_weight_schedule, float), \
+                            "Negative weight schedule must be a float when using dynamic negative weight adjustment."
+                        if fph > target_false_positive_rate:
+                            negative_weight_schedule = negative_weight_schedule * negative_weight_adjust_ratio
+                        else:
+                            negative_weight_schedule = max(1.0, negative_weight_schedule / negative_weight_adjust_ratio)
+                if testing is not None:
+                    preds, labels = self._predict_all(testing)
+                    n_neg = max(int((labels == 0).sum().item()), 1)
+                    t_fp.append(float(self.num_false_positives(preds, labels, activation_threshold).item()) / n_neg)
+                    pos = labels == 1
+                    t_rec.append(_recall(float((preds[pos] > activation_threshold).sum().item()),
+                                         float(pos.sum().item())))
+                    t_acc.append(float(((preds > activation_threshold).float() == labels.float()).float().mean().item()))
+            elif v_fp or t_acc:
+                if validation is not None:
+                    v_fp.append(v_fp[-1])
+                    v_rec.append(v_rec[-1])
+                if testing is not None:
+                    t_fp.append(t_fp[-1])
+                    t_rec.append(t_rec[-1])
+                    t_acc.append(t_acc[-1])
+            else:
+                if validation is not None:
+                    v_fp.append(last_validation_false_positive_per_hour)
+                    v_rec.append(last_validation_recall)
+                if testing is not None:
+                    t_fp.append(last_testing_false_positive_rate)
+                    t_rec.append(last_testing_recall)
+                    t_acc.append(last_testing_accuracy)
+            if step > 0 and step % checkpoint_steps == 0:
+                self.save_checkpoint(f"{name}_{step}")
+        n_steps = len(lr_hist)
+        h = history[:n_steps].cpu().numpy().astype(np.float64)
+        loss_h, rec_h, fp_h, hlr_h = self._rebuild_histories(h, batch_sizes, last_loss, last_recall,
+                                                             last_false_positive_rate)
+
+        def T(v):
+            return torch.tensor(v, dtype=torch.float64) if v else None
+
+        return (T(lr_hist), T(nw_hist), T(loss_h), T(hlr_h), T(rec_h), T(fp_h), T(v_fp), T(v_rec),
+                T(t_acc), T(t_rec), T(t_fp))
+
+    @staticmethod
+    def _rebuild_histories(h: np.ndarray, batch_sizes: List[int], last_loss: float, last_recall: float,
+                           last_fp: float):
+        """The reference's per-step bookkeeping (trainer.py:443-494) from the
+        device record [n_sel, acc_steps, fired, loss, n_neg, fp, n_pos, tp]."""
+        loss_h: List[float] = []
+        rec_h: List[float] = []
+        fp_h: List[float] = []
+        hlr_h: List[float] = []
+        acc = None  # accumulated (n_neg, fp, n_pos, tp) of the pending predictions
+        for k, row in enumerate(h):
+            n_sel, _, fired, loss, n_neg, fp, n_pos, tp = row
+            hlr_h.append(n_sel / batch_sizes[k])
+            cur = np.array([n_neg, fp, n_pos, tp])
+            if n_sel > 0:
+                if n_sel >= 128:
+                    acc = cur
+                if fired == 0:
+                    acc = cur if acc is None else acc + cur
+                    if loss_h:
+                        loss_h.append(loss_h[-1])
+                        rec_h.append(rec_h[-1])
+                        fp_h.append(fp_h[-1])
+                else:
+                    a = acc if acc is not None else np.zeros(4)
+                    loss_h.append(float(loss))
+                    rec_h.append(_recall(a[3], a[2]))
+                    fp_h.append(a[1] / max(a[0], 1.0))
+                    acc = None
+            elif loss_h:
+                loss_h.append(loss_h[-1])
+                rec_h.append(rec_h[-1])
+                fp_h.append(fp_h[-1])
+            else:
+                loss_h.append(last_loss)
+                rec_h.append(last_recall)
+                fp_h.append(last_fp)
+        return loss_h, rec_h, fp_h, hlr_h
+
+    def __call__(self, training: Any, validation: Optional[Any] = None, testing: Optional[Any] = None,
+                 num_steps: int = DEFAULT_STEPS, num_stages: int = DEFAULT_STAGES,
+                 max_negative_weight: float = DEFAULT_NEGATIVE_WEIGHT,
+                 logging_steps: int = DEFAULT_LOGGING_STEPS, validation_steps: int = DEFAULT_VALIDATION_STEPS,
+                 checkpoint_steps: int = DEFAULT_CHECKPOINT_STEPS,
+                 target_false_positive_rate: float = DEFAULT_TARGET_FALSE_POSITIVE_RATE,
+                 negative_weight_adjust_ratio: float = DEFAULT_NEGATIVE_WEIGHT_ADJUST_RATIO,
+                 dynamic_negative_weight: bool = DEFAULT_DYNAMIC_NEGATIVE_WEIGHT,
+                 batch_size_adjust_ratio: float = DEFAULT_BATCH_SIZE_ADJUST_RATIO,
+                 learning_rate_adjust_ratio: float = DEFAULT_LEARNING_RATE_ADJUST_RATIO,
+                 step_adjust_ratio: float = DEFAULT_STEP_ADJUST_RATIO,
+                 learning_rate: float = DEFAULT_LEARNING_RATE,
+                 high_loss_threshold: float = DEFAULT_HIGH_LOSS_THRESHOLD,
+                 activation_threshold: float = DEFAULT_ACTIVATION_THRESHOLD,
+                 wandb_entity: Optional[str] = None, name: str = "heybuddy", **kwargs: Any) -> Dict[str, Any]:
+        """3-stage training (trainer.py:764-1007): after each stage lr x 0.5,
+        steps x 2 (at least validation_steps), batch x 0.5, and the last
+        validated negative weight carries over."""
+        start = perf_counter()
+        hist: Dict[str, List[torch.Tensor]] = {k: [] for k in ("lr", "nw", "loss", "hlr", "recall", "fp")}
+        last = {"loss": 0.0, "recall": 0.0, "fp": 0.0, "vfp": 0.0, "vrec": 0.0, "tacc": 0.0, "trec": 0.0, "tfp": 0.0}
+        for hook in ("start",):
+            for d in (training, validation, testing):
+                if hasattr(d, hook):
+                    getattr(d, hook)()
+        for i in range(num_stages):
+            if dynamic_negative_weight:
+                weights: Union[float, List[float]] = max_negative_weight
+                ratio: Optional[float] = negative_weight_adjust_ratio
+            else:
+                weights = np.linspace(1, max_negative_weight, num_steps).tolist()
+                ratio = None
+            t0 = perf_counter()
+            lr, nw, loss, hlr, rec, fp, v_fp, v_rec, t_acc, t_rec, t_fp = self.train_epoch(
+                training, validation=validation, testing=testing, num_steps=num_steps,
+                negative_weight_schedule=weights, negative_weight_adjust_ratio=ratio,
+                target_false_positive_rate=target_false_positive_rate, learning_rate=learning_rate,
+                warmup_steps=num_steps // 5, hold_steps=num_steps // 3, logging_steps=logging_steps,
+                validation_steps=validation_steps, checkpoint_steps=checkpoint_steps,
+                description=f"Training Stage {i + 1}", high_loss_threshold=high_loss_threshold,
+                activation_threshold=activation_threshold, name=f"{name}_{i}", last_loss=last["loss"],
+                last_recall=last["recall"], last_false_positive_rate=last["fp"],
+                last_validation_false_positive_per_hour=last["vfp"], last_validation_recall=last["vrec"],
+                last_testing_accuracy=last["tacc"], last_testing_recall=last["trec"],
+                last_testing_false_positive_rate=last["tfp"])
+            logger.info(f"Training Stage {i + 1}: {len(lr)} steps in {perf_counter() - t0:.2f} s, "
+                        f"final loss {float(loss[-1]) if loss is not None else float('nan'):.5f}")
+            for k, v in zip(("lr", "nw", "loss", "hlr", "recall", "fp"), (lr, nw, loss, hlr, rec, fp)):
+                if v is not None:
+                    hist[k].append(v)
+            last.update(loss=float(loss[-1]), recall=float(rec[-1]), fp=float(fp[-1]))
+            if v_fp is not None:
+                last.update(vfp=float(v_fp[-1]), vrec=float(v_rec[-1]))
+            if t_acc is not None:
+                last.update(tacc=float(t_acc[-1]), trec=float(t_rec[-1]), tfp=float(t_fp[-1]))
+            learning_rate *= learning_rate_adjust_ratio
+            num_steps = max(validation_steps, int(num_steps * step_adjust_ratio))
+            if v_fp is not None and dynamic_negative_weight:
+                max_negative_weight = float(nw[-1])
+            if hasattr(training, "multiply_batch_size"):
+                training.multiply_batch_size(batch_size_adjust_ratio)
+        self.save_checkpoint(f"{name}_final")
+        for d in (training, validation, testing):
+            if hasattr(d, "stop"):
+                d.stop()
+        logger.info(f"Training complete in {perf_counter() - start:.2f} s")
+        return {k: torch.cat(v) for k, v in hist.items() if v}

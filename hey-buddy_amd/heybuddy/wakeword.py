@@ -1,0 +1,189 @@
+"""Drop-in for heybuddy.wakeword's default classifier (reference
+src/python/heybuddy/wakeword.py:171-348).
+
+``WakeWordMLPModel`` keeps the reference's constructor, state_dict names and
+shapes (checkpoints and the shipped src/js/models/*.onnx weights load with
+strict=True), ``from_file`` and ``predict``, but its parameters are views into
+ONE flat f32 buffer laid out for libhbk.so, and ``forward`` runs the fused HIP
+forward (hbk_mlp_forward). Training goes through the fused HIP train step
+(heybuddy.trainer), not autograd. Only the default architecture is on the MI355X
+path: gated MLP (DEFAULT_USE_GATING), no half layers, SiLU.
+"""
+from __future__ import annotations
+
+import random
+from collections import OrderedDict
+from typing import Any, List, Optional, Tuple, Union
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from heybuddy import _native
+from heybuddy.constants import (DEFAULT_LAYER_DIM, DEFAULT_LAYERS, DEFAULT_USE_GATING,
+                                DEFAULT_USE_HALF_LAYERS)
+from heybuddy.kernels import MlpPlan
+
+__all__ = ["WakeWordMLPModel", "get_normalized_dim"]
+
+
+def get_normalized_dim(dim: int, multiple_of: int = 8, down_ratio: float = 2 / 3) -> int:
+    """modeling_util.py:42-72: int(dim * 2/3) rounded up to a multiple of 8."""
+    v = int(dim * down_ratio)
+    return v if v % multiple_of == 0 else v + multiple_of - v % multiple_of
+
+
+class _Affine(nn.Module):
+    """Holds a weight and a bias (LayerNorm / Linear slots of the reference)."""
+
+    def __init__(self, w: torch.Tensor, b: torch.Tensor) -> None:
+        super().__init__()
+        self.weight = nn.Parameter(w)
+        self.bias = nn.Parameter(b)
+
+
+class _Gmlp(nn.Module):
+    def __init__(self, views, prefix: str) -> None:
+        super().__init__()
+        self.hidden = _Affine(views[f"{prefix}.hidden.weight"], views[f"{prefix}.hidden.bias"])
+        self.output = _Affine(views[f"{prefix}.output.weight"], views[f"{prefix}.output.bias"])
+        self.gate = _Affine(views[f"{prefix}.gate.weight"], views[f"{prefix}.gate.bias"])
+
+
+class WakeWordMLPModel(nn.Module):
+    """input > dropout > flatten > LN > gated MLP > [LN > gated MLP] x L > LN >
+    gated MLP > sigmoid (wakeword.py:334-348). Input [B, 16, 96] -> [B, 1]."""
+
+    def __init__(self, input_shape: Tuple[int, int] = (16, 96), layer_dim: int = DEFAULT_LAYER_DIM,
+                 num_layers: int = DEFAULT_LAYERS, use_gating: bool = DEFAULT_USE_GATING,
+                 use_half_layers: bool = DEFAULT_USE_HALF_LAYERS, dropout: float = 0.1,
+                 activation: Optional[str] = "silu") -> None:
+        super().__init__()
+        if not use_gating or use_half_layers or activation not in ("silu", "swish"):
+            raise NotImplementedError("the MI355X path implements the default architecture: gated MLP, "
+                                      "no half layers, SiLU")
+        self.input_shape = tuple(input_shape)
+        self.input_features = input_shape[0] * input_shape[1]
+        self.use_gating = use_gating
+        self.use_half_layers = use_half_layers
+        self.layer_dim = layer_dim
+        self.num_layers = num_layers
+        self.plan = MlpPlan(self.input_features, layer_dim, get_normalized_dim(layer_dim), num_layers)
+        self.dropout = nn.Dropout(dropout)
+        flat = torch.zeros(self.plan.n_params, dtype=torch.float32)
+        self._bind(flat, build=True)
+        self._reset_parameters()
+
+    # -- flat parameter buffer ------------------------------------------------
+    def _bind(self, flat: torch.Tensor, build: bool = False) -> None:
+        views = self.plan.views(flat)
+        if build:
+            self.norm_in = _Affine(views["norm_in.weight"], views["norm_in.bias"])
+            self.mlp_in = _Gmlp(views, "mlp_in")
+            self.layers = nn.ModuleList(
+                nn.ModuleList([_Affine(views[f"layers.{l}.0.weight"], views[f"layers.{l}.0.bias"]),
+                               _Gmlp(views, f"layers.{l}.1")]) for l in range(self.num_layers))
+            self.norm_out = _Affine(views["norm_out.weight"], views["norm_out.bias"])
+            self.mlp_out = _Gmlp(views, "mlp_out")
+        else:
+            params = dict(self.named_parameters())
+            for name, view in views.items():
+                params[name].data = view
+        self._flat = flat
+
+    @property
+    def flat_parameters(self) -> torch.Tensor:
+        """All parameters as one contiguous f32 tensor (the kernels' layout)."""
+        return self._flat
+
+    def _apply(self, fn, recurse=True):
+        flat = fn(self._flat)
+        if flat.data_ptr() != self._flat.data_ptr() or flat.device != self._flat.device:
+            self._bind(flat.contiguous())
+        for p in self.parameters():
+            if p.grad is not None:
+                p.grad = fn(p.grad)
+        return self
+
+    @torch.no_grad()
+    def _reset_parameters(self) -> None:
+        """nn.Linear / nn.LayerNorm default initialisation (fan-in uniform)."""
+        for name, p in self.named_parameters():
+            if ".hidden." in name or ".output." in name or ".gate." in name:
+                lin = name.rsplit(".", 1)[0]
+                fan_in = dict(self.named_parameters())[f"{lin}.weight"].shape[1]
+                bound = 1.0 / np.sqrt(fan_in)
+                p.uniform_(-bound, bound)
+            elif name.endswith("weight"):
+                p.fill_(1.0)
+            else:
+                p.zero_()
+
+    @property
+    def device(self) -> torch.device:
+        return self._flat.device
+
+    @property
+    def dtype(self) -> torch.dtype:
+        return self._flat.dtype
+
+    # -- inference ---------------------------------------------------------
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        """[B, 16, 96] -> [B, 1] probabilities on the HIP path. In training mode
+        the input dropout is applied, as in the reference (it never calls
+        .eval(), so its validation passes run with dropout too)."""
+        if self._flat.device.type != "cuda":
+            raise _native.HBKUnavailable("WakeWordMLPModel runs on a HIP device: call .to('cuda') first")
+        x = x.to(device=self._flat.device, dtype=torch.float32)
+        p = self.dropout.p if self.training else 0.0
+        prob = self.plan.forward(self._flat, x.reshape(x.shape[0], -1), dropout_p=p,
+                                 seed=random.getrandbits(63))
+        return prob.unsqueeze(1)
+
+    def logits(self, x: torch.Tensor) -> torch.Tensor:
+        """Pre-sigmoid outputs [B] (dropout off)."""
+        x = x.to(device=self._flat.device, dtype=torch.float32)
+        _, z = self.plan.forward(self._flat, x.reshape(x.shape[0], -1), logits=True)
+        return z
+
+    @classmethod
+    def from_file(cls, path: str, device: Optional[torch.device] = None) -> "WakeWordMLPModel":
+        """wakeword.py:249-276: infer layer_dim / num_layers from the state_dict."""
+        state_dict = torch.load(path, weights_only=True, map_location="cpu")
+        layer_dim = state_dict["norm_out.weight"].shape[0]
+        num_layers = 0
+        while f"layers.{num_layers}.0.weight" in state_dict:
+            num_layers += 1
+        model = cls(layer_dim=layer_dim, num_layers=num_layers)
+        model.load_state_dict(state_dict)
+        if device is not None:
+            model.to(device)
+        return model
+
+    # -- WakeWordInferenceMixin.predict (wakeword.py:129-169) ---------------
+    @property
+    def speech_embeddings(self):
+        from heybuddy.embeddings import get_speech_embeddings
+        if not hasattr(self, "_speech_embeddings"):
+            idx = self.device.index if self.device.type == "cuda" else None
+            self._speech_embeddings = get_speech_embeddings(device_id=idx)
+        return self._speech_embeddings
+
+    @torch.no_grad()
+    def predict(self, audio: Any, threshold: float = 0.5, embedding_spectrogram_batch_size: int = 32,
+                embedding_batch_size: int = 32, return_scores: bool = False,
+                min_frames: int = 23040) -> Union[Tuple[bool, ...], Tuple[float, ...]]:
+        from heybuddy.util import audio_to_bct_tensor
+        audio_tensor, _ = audio_to_bct_tensor(audio, sample_rate=16000)
+        n, c, t = audio_tensor.shape
+        if t < min_frames:
+            pad = min_frames - t
+            left = int(pad / 2)
+            audio_tensor = torch.cat([torch.zeros(n, c, left, dtype=audio_tensor.dtype), audio_tensor,
+                                      torch.zeros(n, c, pad - left, dtype=audio_tensor.dtype)], dim=-1)
+        emb = self.speech_embeddings(audio_tensor, embedding_batch_size=embedding_batch_size,
+                                     spectrogram_batch_size=embedding_spectrogram_batch_size)
+        pred = self(torch.tensor(emb, device=self.device, dtype=torch.float32)).cpu().numpy()
+        if return_scores:
+            return tuple(pred.flatten())
+        return tuple(pred > threshold)

@@ -126,6 +126,57 @@ int hbk_embed_clips(const hbk_embed_plan* plan, const float* mel, int64_t n_clip
 int hbk_embed_windows(const hbk_embed_plan* plan, const float* windows, int64_t n, float* out,
                       void* workspace, int64_t workspace_bytes, void* stream);
 
+/* ------------------------------------------------------------------------ *
+ * Wake-word classifier: gated MLP forward and the fused train step
+ *
+ * Replaces WakeWordMLPModel.forward (wakeword.py:334-348, gated MLP of
+ * modules/multi_layer_perceptron.py:76-124) and the optimisation path of
+ * WakeWordTrainer.train_epoch (trainer.py:380-494): high-loss filter
+ * (:407-424), weighted BCE (:301-312), backward, the < 128-sample
+ * accumulation gate (:443-465) and torch.optim.Adam (:45).
+ * Parameters live in ONE flat f32 buffer (layout: hbk_mlp_layout).
+ * ------------------------------------------------------------------------ */
+typedef struct hbk_mlp_plan hbk_mlp_plan;
+
+/* d_in = 16*96, layer_dim = 96, hidden = get_normalized_dim(96) = 64. */
+int hbk_mlp_plan_create(int32_t d_in, int32_t layer_dim, int32_t hidden, int32_t n_layers,
+                        hbk_mlp_plan** plan);
+int hbk_mlp_plan_destroy(hbk_mlp_plan* plan);
+/* n_params and the float offsets of: norm_in g,b; per GMLP (mlp_in,
+ * layers..., mlp_out) W_hg [2H,in] (hidden rows then gate rows), b_hg [2H],
+ * W_o [out,H], b_o [out]; per LN (layers..., norm_out) g, b. */
+int hbk_mlp_layout(const hbk_mlp_plan* plan, int64_t* n_params, int64_t* offsets, int32_t n_offsets);
+int hbk_mlp_workspace_size(const hbk_mlp_plan* plan, int64_t batch, int64_t* bytes);
+
+/* x [batch, d_in] f32 -> prob [batch] (and pre-sigmoid logit [batch] if non-NULL).
+ * dropout_p: input dropout (nn.Dropout before the first LayerNorm; the
+ * reference keeps it active in training AND validation since .eval() is never
+ * called), mask = f(seed, element index); 0 disables it. */
+int hbk_mlp_forward(const hbk_mlp_plan* plan, const float* params, const float* x, int64_t batch,
+                    float* prob, float* logit, float dropout_p, uint64_t seed, void* workspace,
+                    int64_t workspace_bytes, void* stream);
+
+/* Forward + filter + weighted BCE + backward. bucket [n_params + 8] is zeroed,
+ * then receives the UNNORMALISED gradient sum over the selected samples of
+ * w * dl/dz and the statistics [n_sel, sum w*l, n_neg_sel, fp_sel, n_pos_sel,
+ * tp_sel, batch, 0]; data-parallel ranks all-reduce (sum) the whole bucket.
+ * y: labels as f32 0/1. prob [batch] (optional) receives sigmoid outputs. */
+int hbk_mlp_train_fwd_bwd(const hbk_mlp_plan* plan, const float* params, const float* x,
+                          const float* y, int64_t batch, float neg_weight,
+                          float high_loss_threshold, float activation_threshold, float dropout_p,
+                          uint64_t seed, float* bucket, float* prob, void* workspace,
+                          int64_t workspace_bytes, void* stream);
+
+/* The accumulation gate on the (reduced) bucket statistics and, when it fires,
+ * Adam on params with grads * 1/(n_sel * accumulation_steps). state[4]:
+ * accumulated_samples, accumulation_steps (init 1), adam step, step index;
+ * ctrl[4] scratch; history (optional, [cap, 8]): per step n_sel,
+ * accumulation_steps used, fired, loss (BCE mean / accumulation_steps),
+ * n_neg_sel, fp_sel, n_pos_sel, tp_sel. */
+int hbk_mlp_gate_adam(const hbk_mlp_plan* plan, float* params, const float* bucket, float* m,
+                      float* v, float* state, float* ctrl, float* history, int32_t history_cap,
+                      float lr, float beta1, float beta2, float eps, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
