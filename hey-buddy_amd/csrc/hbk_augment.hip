@@ -1,0 +1,500 @@
+// Fused batch augmentation for gfx950: background-noise mix + IR reverb.
+//
+// Replaces add_background_noise_to_batch -> torchaudio.functional.add_noise
+// (augmented.py:234-276, :383-384) and speechbrain's reverberate(batch, ir)
+// (augmented.py:386-392) of AugmentedAudioGenerator.execute_augment_batch.
+//
+// One workgroup (512 threads) per clip, the whole clip resident in LDS:
+//   load x (and the clip's noise segment, in registers) -> E_x, E_n ->
+//   y = x + 10^((10 log10(E_x/E_n) - snr)/20) n -> a_in = mean|y|
+//   circular convolution with the batch's IR kernel of length T = 23040:
+//     z[n] = y[2n] + i y[2n+1], a 11520-point complex FFT done four-step as
+//     256 x 45 in LDS: 45 column FFT-256s (16 lanes each, FFT16 x FFT16 in
+//     VGPRs), twiddle W_M^(n2 k1), 256 row DFT-45s (one thread each, 5x3x3 in
+//     VGPRs) -> Z in (k1, k2) order; the real-FFT split, * H[k], and the
+//     inverse split on (k, M-k) pairs; the inverse transform with the steps
+//     reversed lands back in natural order.
+//   y <- a_in * y / (mean|y| + 1e-14), store.
+// The IR spectrum H (one per batch) comes from the same transform run on the
+// rotated kernel [ir[d:], 0..., ir[:d]] (hbk_reverb_spectrum).
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "hbk_common.h"
+
+namespace hbk {
+namespace {
+
+constexpr int kT = 23040;        // clip length (1.44 s @ 16 kHz, augmented.py:31)
+constexpr int kM = kT / 2;       // complex FFT length
+constexpr int kR = 256;          // rows of the four-step matrix (FFT-256 length)
+constexpr int kC = 45;           // columns (DFT-45 length)
+constexpr int kThreads = 512;    // 32 column FFTs (16 lanes each) per pass
+
+// ---- small DFTs in registers (constant twiddles) --------------------------
+template <bool INV>
+__device__ __forceinline__ cf tw_const(double frac) {  // exp(-+2 pi i frac)
+  const double a = (INV ? 2.0 : -2.0) * M_PI * frac;
+  return cf{static_cast<float>(cos(a)), static_cast<float>(sin(a))};
+}
+
+template <bool INV>
+__device__ __forceinline__ void dft3(cf& a, cf& b, cf& c) {
+  // X0 = a+b+c; X1 = a + w b + w^2 c; X2 = a + w^2 b + w c, w = exp(-+2pi i/3)
+  constexpr float h = 0.5f, s = 0.86602540378443865f;
+  const cf t = b + c;
+  const cf d = b - c;
+  const cf m = a - h * t;
+  // (-+) i s d
+  const cf r = INV ? cf{-s * d.y, s * d.x} : cf{s * d.y, -s * d.x};
+  a = a + t;
+  b = m + r;
+  c = m - r;
+}
+
+template <bool INV>
+__device__ __forceinline__ void dft5(cf (&x)[5]) {
+  cf y[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    cf acc = x[0];
+#pragma unroll
+    for (int n = 1; n < 5; ++n) acc = acc + cmul(x[n], tw_const<INV>(double((n * k) % 5) / 5.0));
+    y[k] = acc;
+  }
+#pragma unroll
+  for (int k = 0; k < 5; ++k) x[k] = y[k];
+}
+
+// DFT-9 as 3 x 3: n = 3u + v, k = c + 3d
+template <bool INV>
+__device__ __forceinline__ void dft9(cf (&x)[9]) {
+#pragma unroll
+  for (int v = 0; v < 3; ++v) dft3<INV>(x[v], x[3 + v], x[6 + v]);  // x[3c + v] = A[v][c]
+#pragma unroll
+  for (int c = 1; c < 3; ++c)
+#pragma unroll
+    for (int v = 1; v < 3; ++v) x[3 * c + v] = cmul(x[3 * c + v], tw_const<INV>(double(v * c) / 9.0));
+#pragma unroll
+  for (int c = 0; c < 3; ++c) dft3<INV>(x[3 * c + 0], x[3 * c + 1], x[3 * c + 2]);  // x[3c + d] = X[c + 3d]
+  cf t[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) t[k] = x[3 * (k % 3) + k / 3];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) x[k] = t[k];
+}
+
+// DFT-45 as 5 x 9: n = 5p + q, k = r + 9s; natural order in and out.
+template <bool INV>
+__device__ __forceinline__ void dft45(cf (&x)[45]) {
+  cf a[5][9];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    cf col[9];
+#pragma unroll
+    for (int p = 0; p < 9; ++p) col[p] = x[5 * p + q];
+    dft9<INV>(col);
+#pragma unroll
+    for (int r = 0; r < 9; ++r) a[q][r] = (q && r) ? cmul(col[r], tw_const<INV>(double(q * r) / 45.0)) : col[r];
+  }
+#pragma unroll
+  for (int r = 0; r < 9; ++r) {
+    cf v[5];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) v[q] = a[q][r];
+    dft5<INV>(v);
+#pragma unroll
+    for (int s = 0; s < 5; ++s) x[r + 9 * s] = v[s];
+  }
+}
+
+template <bool INV>
+__device__ __forceinline__ void fft4v(cf& a0, cf& a1, cf& a2, cf& a3) {
+  const cf t0 = a0 + a2, t1 = a0 - a2, t2 = a1 + a3;
+  const cf d = a1 - a3;
+  const cf t3 = INV ? cf{-d.y, d.x} : cf{d.y, -d.x};  // (+-i) d
+  a0 = t0 + t2;
+  a2 = t0 - t2;
+  a1 = t1 + t3;
+  a3 = t1 - t3;
+}
+
+template <bool INV>
+__device__ __forceinline__ void fft16v(cf (&v)[16]) {
+#pragma unroll
+  for (int m2 = 0; m2 < 4; ++m2) fft4v<INV>(v[m2], v[4 + m2], v[8 + m2], v[12 + m2]);
+#pragma unroll
+  for (int l1 = 1; l1 < 4; ++l1)
+#pragma unroll
+    for (int m2 = 1; m2 < 4; ++m2) v[4 * l1 + m2] = cmul(v[4 * l1 + m2], tw_const<INV>(double(m2 * l1) / 16.0));
+#pragma unroll
+  for (int l1 = 0; l1 < 4; ++l1) fft4v<INV>(v[4 * l1 + 0], v[4 * l1 + 1], v[4 * l1 + 2], v[4 * l1 + 3]);
+  cf t[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) t[k] = v[4 * (k & 3) + (k >> 2)];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] = t[k];
+}
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Column FFT-256 of column n2 (stride kC in z), 16 lanes (j = 0..15).
+// tw256: W_256^e table (or conjugate for INV).
+template <bool INV>
+__device__ __forceinline__ void column_fft256(cf* z, int n2, int j, const cf* tw256) {
+  cf v[16];
+#pragma unroll
+  for (int a = 0; a < 16; ++a) v[a] = z[(16 * a + j) * kC + n2];
+  fft16v<INV>(v);
+#pragma unroll
+  for (int k = 1; k < 16; ++k) {
+    const cf w = tw256[j * k];
+    v[k] = cmul(v[k], INV ? cf{w.x, -w.y} : w);
+  }
+  wave_sync();
+#pragma unroll
+  for (int k = 0; k < 16; ++k) z[(16 * k + j) * kC + n2] = v[k];
+  wave_sync();
+#pragma unroll
+  for (int b = 0; b < 16; ++b) v[b] = z[(16 * j + b) * kC + n2];
+  fft16v<INV>(v);
+  wave_sync();
+#pragma unroll
+  for (int k = 0; k < 16; ++k) z[(j + 16 * k) * kC + n2] = v[k];
+}
+
+// Row k1: (forward) twiddle W_M^(n2 k1) then DFT-45; (inverse) IDFT-45 then
+// conj twiddle. DFT-45 as 5 x 9 (n = 5p + q, k = r + 9s), reading the row
+// straight from LDS and writing results straight back, so that only the 5 x 9
+// intermediate is live in VGPRs.
+template <bool INV>
+__device__ __forceinline__ void row_dft45(cf* z, int k1, const cf* twm) {
+  cf* row = z + k1 * kC;
+  cf a[5][9];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    cf col[9];
+#pragma unroll
+    for (int p = 0; p < 9; ++p) {
+      const int n = 5 * p + q;
+      cf v = row[n];
+      if (!INV && n) v = cmul(v, twm[n * k1]);
+      col[p] = v;
+    }
+    dft9<INV>(col);
+#pragma unroll
+    for (int r = 0; r < 9; ++r) a[q][r] = (q && r) ? cmul(col[r], tw_const<INV>(double(q * r) / 45.0)) : col[r];
+  }
+#pragma unroll
+  for (int r = 0; r < 9; ++r) {
+    cf v[5];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) v[q] = a[q][r];
+    dft5<INV>(v);
+#pragma unroll
+    for (int s5 = 0; s5 < 5; ++s5) {
+      const int k = r + 9 * s5;
+      cf o = v[s5];
+      if (INV && k) {
+        const cf w = twm[k * k1];
+        o = cmul(o, cf{w.x, -w.y});
+      }
+      row[k] = o;
+    }
+  }
+}
+
+// Forward complex FFT of z (natural order) -> Z[k] at addr(k).
+__device__ __forceinline__ int zaddr(int k) { return (k & (kR - 1)) * kC + (k >> 8); }
+
+template <bool INV>
+__device__ __forceinline__ void columns(cf* z, const cf* tw256) {
+  for (int c = threadIdx.x >> 4; c < kC; c += kThreads / 16) column_fft256<INV>(z, c, threadIdx.x & 15, tw256);
+}
+
+template <bool INV>
+__device__ __forceinline__ void rows(cf* z, const cf* twm) {
+  for (int r = threadIdx.x; r < kR; r += kThreads) row_dft45<INV>(z, r, twm);
+}
+
+template <bool INV>
+__device__ __forceinline__ void transform(cf* z, const cf* tw256, const cf* twm) {
+  if (!INV) {
+    columns<false>(z, tw256);
+    __syncthreads();
+    rows<false>(z, twm);
+    __syncthreads();
+  } else {
+    rows<true>(z, twm);
+    __syncthreads();
+    columns<true>(z, tw256);
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ float block_sum(float v, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  float s = 0.f;
+  for (int w = 0; w < kThreads / 64; ++w) s += red[w];
+  return s;
+}
+
+struct AugArgs {
+  const float* x;
+  int64_t x_stride;
+  float* out;
+  int64_t out_stride;
+  int64_t n_clips;
+  const float* ring;        // background-noise ring (all noise clips back to back)
+  int64_t ring_len;
+  const int64_t* noise_off; // per clip: ring offset of its segment, < 0 = no noise
+  const float* snr_db;      // per clip
+  const float2* spectra;    // [n_spec][kM + 1]
+  const int* spec_idx;      // per clip: spectrum index, < 0 = no reverb
+  const float2* tw256;
+  const float2* twm;        // W_M^e, e < kM
+  const float2* twn;        // W_N^k, k <= kM
+};
+
+__global__ void __launch_bounds__(kThreads) augment_kernel(AugArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  cf* z = reinterpret_cast<cf*>(smem);                      // kM complex
+  float* red = smem + 2 * kM;                               // 16 floats
+  const cf* tw256 = reinterpret_cast<const cf*>(a.tw256);
+  const cf* twm = reinterpret_cast<const cf*>(a.twm);
+  const cf* twn = reinterpret_cast<const cf*>(a.twn);
+  float* zf = smem;
+  const int tid = threadIdx.x;
+  for (int64_t clip = blockIdx.x; clip < a.n_clips; clip += gridDim.x) {
+    const float* x = a.x + clip * a.x_stride;
+    // 1) load x into LDS, the noise segment into registers
+    float ex = 0.f;
+    for (int s = tid; s < kT; s += kThreads) {
+      const float v = x[s];
+      zf[s] = v;
+      ex += v * v;
+    }
+    const int64_t noff = a.noise_off[clip];
+    if (noff >= 0) {
+      // the noise segment is read twice (energy, then mix); the 2nd read hits L2
+      auto noise_at = [&](int s) {
+        int64_t r = noff + s;
+        if (r >= a.ring_len) r -= a.ring_len;
+        return a.ring[r];
+      };
+      float en = 0.f;
+      for (int s = tid; s < kT; s += kThreads) {
+        const float v = noise_at(s);
+        en += v * v;
+      }
+      const float Ex = block_sum(ex, red);
+      const float En = block_sum(en, red);
+      // torchaudio add_noise: snr0 = 10 (log10 Ex - log10 En); scale = 10^((snr0 - snr)/20)
+      const float snr0 = 10.f * (log10f(Ex) - log10f(En));
+      const float scale = powf(10.f, (snr0 - a.snr_db[clip]) / 20.f);
+      for (int s = tid; s < kT; s += kThreads) zf[s] = zf[s] + scale * noise_at(s);
+    }
+    __syncthreads();
+    const int sp = a.spec_idx[clip];
+    float* out = a.out + clip * a.out_stride;
+    if (sp < 0) {
+      for (int s = tid; s < kT; s += kThreads) out[s] = zf[s];
+      __syncthreads();
+      continue;
+    }
+    // 2) a_in = mean |y|
+    float aa = 0.f;
+    for (int s = tid; s < kT; s += kThreads) aa += fabsf(zf[s]);
+    const float a_in = block_sum(aa, red) / kT;
+    // 3) forward FFT (natural -> permuted)
+    transform<false>(z, tw256, twm);
+    // 4) split, multiply by H, inverse split, on (k, M-k) pairs
+    const cf* H = reinterpret_cast<const cf*>(a.spectra) + static_cast<int64_t>(sp) * (kM + 1);
+    for (int k = tid; k <= kM / 2; k += kThreads) {
+      const int kc = (kM - k) % kM;
+      const cf zk = z[zaddr(k)];
+      const cf zc = z[zaddr(kc)];
+      // X[k] = Fe + W_N^k Fo, X[M-k] = conj(Fe) + W_N^(M-k) conj(Fo)...: compute both directly
+      const cf fe = 0.5f * cf{zk.x + zc.x, zk.y - zc.y};
+      const cf fo = 0.5f * cf{zk.y + zc.y, zc.x - zk.x};
+      const cf wk = twn[k];
+      const cf Xk = fe + cmul(wk, fo);
+      // partner: Fe' = conj(fe), Fo' = conj(fo), W_N^(M-k) = -conj(W_N^k)
+      const cf fe2 = cf{fe.x, -fe.y};
+      const cf fo2 = cf{fo.x, -fo.y};
+      const cf wk2 = cf{-wk.x, wk.y};
+      const cf Xc = fe2 + cmul(wk2, fo2);  // X[M - k] (X[M] when k = 0)
+      const cf Yk = cmul(Xk, H[k]);
+      const cf Yc = cmul(Xc, H[kM - k]);
+      // inverse split: Z'[k] = (Y[k] + conj Y[M-k])/2 + i W_N^-k (Y[k] - conj Y[M-k])/2
+      const cf s1 = 0.5f * cf{Yk.x + Yc.x, Yk.y - Yc.y};
+      const cf d1 = 0.5f * cf{Yk.x - Yc.x, Yk.y + Yc.y};
+      const cf wd = cmul(cf{wk.x, -wk.y}, d1);
+      const cf zk2 = s1 + cf{-wd.y, wd.x};
+      // partner k' = M - k: Y[k'] = Yc, Y[M-k'] = Yk, W_N^-(M-k) = -W_N^k
+      const cf s2 = 0.5f * cf{Yc.x + Yk.x, Yc.y - Yk.y};
+      const cf d2 = 0.5f * cf{Yc.x - Yk.x, Yc.y + Yk.y};
+      const cf wd2 = cmul(cf{-wk.x, -wk.y}, d2);
+      const cf zc2 = s2 + cf{-wd2.y, wd2.x};
+      z[zaddr(k)] = zk2;
+      if (kc != k) z[zaddr(kc)] = zc2;
+    }
+    __syncthreads();
+    // 5) inverse FFT (permuted -> natural), 1/M
+    transform<true>(z, tw256, twm);
+    float ay = 0.f;
+    for (int s = tid; s < kT; s += kThreads) ay += fabsf(zf[s]);
+    const float a_out = block_sum(ay, red) / kT / kM;
+    const float g = a_in / (a_out + 1e-14f) / kM;
+    for (int s = tid; s < kT; s += kThreads) out[s] = zf[s] * g;
+    __syncthreads();
+  }
+}
+
+// Spectrum of one rotated IR kernel k [kT] -> H[k], k = 0..kM (natural order).
+__global__ void __launch_bounds__(kThreads) spectrum_kernel(const float* kern, int64_t kern_stride,
+                                                            float2* spectra, const float2* tw256_,
+                                                            const float2* twm_, const float2* twn_) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  cf* z = reinterpret_cast<cf*>(smem);
+  const cf* tw256 = reinterpret_cast<const cf*>(tw256_);
+  const cf* twm = reinterpret_cast<const cf*>(twm_);
+  const cf* twn = reinterpret_cast<const cf*>(twn_);
+  const float* k = kern + blockIdx.x * kern_stride;
+  for (int s = threadIdx.x; s < kT; s += kThreads) smem[s] = k[s];
+  __syncthreads();
+  transform<false>(z, tw256, twm);
+  float2* H = spectra + static_cast<int64_t>(blockIdx.x) * (kM + 1);
+  for (int q = threadIdx.x; q <= kM; q += kThreads) {
+    const int qq = q % kM, qc = (kM - q) % kM;
+    const cf zk = z[zaddr(qq)];
+    const cf zc = z[zaddr(qc)];
+    const cf fe = 0.5f * cf{zk.x + zc.x, zk.y - zc.y};
+    const cf fo = 0.5f * cf{zk.y + zc.y, zc.x - zk.x};
+    const cf X = fe + cmul(twn[q], fo);
+    H[q] = make_float2(X.x, X.y);
+  }
+}
+
+}  // namespace
+}  // namespace hbk
+
+struct hbk_reverb_plan {
+  float2* tw256 = nullptr;
+  float2* twm = nullptr;
+  float2* twn = nullptr;
+};
+
+extern "C" {
+
+int hbk_reverb_plan_create(int64_t T, hbk_reverb_plan** plan) {
+  using namespace hbk;
+  if (!plan) return arg_error("plan is NULL");
+  *plan = nullptr;
+  if (T != kT) {
+    set_error("hbk: reverb supports clips of %d samples (1.44 s @ 16 kHz), got %lld", kT, (long long)T);
+    return HBK_ERR_UNSUPPORTED;
+  }
+  std::vector<float2> t256(256), tm(kM), tn(kM + 1);
+  for (int i = 0; i < 256; ++i) {
+    const double a = -2.0 * M_PI * i / 256.0;
+    t256[i] = make_float2(float(cos(a)), float(sin(a)));
+  }
+  for (int i = 0; i < kM; ++i) {
+    const double a = -2.0 * M_PI * i / double(kM);
+    tm[i] = make_float2(float(cos(a)), float(sin(a)));
+  }
+  for (int i = 0; i <= kM; ++i) {
+    const double a = -2.0 * M_PI * i / double(kT);
+    tn[i] = make_float2(float(cos(a)), float(sin(a)));
+  }
+  auto* p = new hbk_reverb_plan();
+  hipError_t e;
+  if ((e = hipMalloc(&p->tw256, 256 * sizeof(float2))) != hipSuccess ||
+      (e = hipMalloc(&p->twm, kM * sizeof(float2))) != hipSuccess ||
+      (e = hipMalloc(&p->twn, (kM + 1) * sizeof(float2))) != hipSuccess ||
+      (e = hipMemcpy(p->tw256, t256.data(), 256 * sizeof(float2), hipMemcpyHostToDevice)) != hipSuccess ||
+      (e = hipMemcpy(p->twm, tm.data(), kM * sizeof(float2), hipMemcpyHostToDevice)) != hipSuccess ||
+      (e = hipMemcpy(p->twn, tn.data(), (kM + 1) * sizeof(float2), hipMemcpyHostToDevice)) != hipSuccess) {
+    hbk_reverb_plan_destroy(p);
+    return hip_error(e, "reverb plan tables");
+  }
+  const size_t lds = size_t(2 * kM + 32) * sizeof(float);
+  if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(augment_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, int(lds))) != hipSuccess ||
+      (e = hipFuncSetAttribute(reinterpret_cast<const void*>(spectrum_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, int(lds))) != hipSuccess) {
+    hbk_reverb_plan_destroy(p);
+    return hip_error(e, "hipFuncSetAttribute(augment LDS)");
+  }
+  *plan = p;
+  return HBK_OK;
+}
+
+int hbk_reverb_plan_destroy(hbk_reverb_plan* p) {
+  if (!p) return HBK_OK;
+  (void)hipFree(p->tw256);
+  (void)hipFree(p->twm);
+  (void)hipFree(p->twn);
+  delete p;
+  return HBK_OK;
+}
+
+int hbk_reverb_spectrum(const hbk_reverb_plan* p, const float* kernels, int64_t n_kernels, int64_t stride,
+                        float* spectra, void* stream) {
+  using namespace hbk;
+  if (!p) return arg_error("plan is NULL");
+  if (n_kernels < 0) return arg_error("negative n_kernels");
+  if (n_kernels == 0) return HBK_OK;
+  if (!kernels || !spectra) return arg_error("NULL pointer");
+  if (stride < kT) return arg_error("kernel stride < 23040");
+  const size_t lds = size_t(2 * kM + 32) * sizeof(float);
+  hipLaunchKernelGGL(spectrum_kernel, dim3(unsigned(n_kernels)), dim3(kThreads), lds, as_stream(stream), kernels,
+                     stride, reinterpret_cast<float2*>(spectra), p->tw256, p->twm, p->twn);
+  HBK_LAUNCH_CHECK("spectrum_kernel");
+  return HBK_OK;
+}
+
+int hbk_augment(const hbk_reverb_plan* p, const float* x, int64_t n_clips, int64_t x_stride,
+                const float* noise_ring, int64_t ring_len, const int64_t* noise_off, const float* snr_db,
+                const float* spectra, const int32_t* spec_idx, float* out, int64_t out_stride, void* stream) {
+  using namespace hbk;
+  if (!p) return arg_error("plan is NULL");
+  if (n_clips < 0) return arg_error("negative n_clips");
+  if (n_clips == 0) return HBK_OK;
+  if (!x || !out || !noise_off || !snr_db || !spec_idx) return arg_error("NULL pointer");
+  if (x_stride < kT || out_stride < kT) return arg_error("stride < 23040");
+  if (!noise_ring && ring_len > 0) return arg_error("noise ring is NULL");
+  AugArgs a;
+  a.x = x;
+  a.x_stride = x_stride;
+  a.out = out;
+  a.out_stride = out_stride;
+  a.n_clips = n_clips;
+  a.ring = noise_ring;
+  a.ring_len = ring_len;
+  a.noise_off = noise_off;
+  a.snr_db = snr_db;
+  a.spectra = reinterpret_cast<const float2*>(spectra);
+  a.spec_idx = spec_idx;
+  a.tw256 = p->tw256;
+  a.twm = p->twm;
+  a.twn = p->twn;
+  const size_t lds = size_t(2 * kM + 32) * sizeof(float);
+  const int64_t blocks = std::min<int64_t>(n_clips, persistent_blocks(1));
+  hipLaunchKernelGGL(augment_kernel, dim3(unsigned(blocks)), dim3(kThreads), lds, as_stream(stream), a);
+  HBK_LAUNCH_CHECK("augment_kernel");
+  return HBK_OK;
+}
+
+}  // extern "C"

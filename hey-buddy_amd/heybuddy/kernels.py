@@ -352,3 +352,72 @@ class MlpPlan:
                                       ptr(ctrl), ptr(history) if history is not None else None, cap,
                                       float(lr), float(beta1), float(beta2), float(eps),
                                       stream_ptr(params.device)), "hbk_mlp_gate_adam")
+
+
+class ReverbPlan:
+    """Batch augmentation on the HIP path (hbk_reverb_* / hbk_augment):
+    background-noise mix + IR reverb for clips of 23,040 samples."""
+
+    T = 23040
+
+    def __init__(self, device: torch.device | int | None = None) -> None:
+        self.device = _native.require_device(device)
+        handle = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(lib().hbk_reverb_plan_create(self.T, ctypes.byref(handle)), "hbk_reverb_plan_create")
+        self._handle = handle
+
+    @staticmethod
+    def rotated_kernel(ir: torch.Tensor, T: int = 23040) -> torch.Tensor:
+        """speechbrain convolve1d(use_fft=True, rotation_index=argmax|ir|):
+        [ir[d:], zeros(T - L), ir[:d]] with ir truncated to T first."""
+        ir = ir.reshape(-1).to(torch.float32)
+        d = int(torch.argmax(ir.abs()).item())
+        if ir.shape[0] > T:
+            ir = ir[:T]
+        z = torch.zeros(T - ir.shape[0], dtype=ir.dtype, device=ir.device)
+        return torch.cat([ir[d:], z, ir[:d]])
+
+    def spectra(self, kernels: torch.Tensor) -> torch.Tensor:
+        """[n, T] rotated kernels -> [n, T/2 + 1, 2] f32 (complex interleaved)."""
+        kernels = kernels.to(self.device, torch.float32).contiguous()
+        n = kernels.shape[0]
+        out = torch.empty((n, self.T // 2 + 1, 2), dtype=torch.float32, device=self.device)
+        check(lib().hbk_reverb_spectrum(self._handle, ptr(kernels), n, kernels.stride(0), ptr(out),
+                                        stream_ptr(self.device)), "hbk_reverb_spectrum")
+        return out
+
+    def augment(self, x: torch.Tensor, ring: torch.Tensor | None, noise_off: torch.Tensor,
+                snr_db: torch.Tensor, spectra: torch.Tensor | None, spec_idx: torch.Tensor,
+                out: torch.Tensor | None = None) -> torch.Tensor:
+        """x [n, >= T] -> out [n, T]; per clip noise (noise_off >= 0) then reverb (spec_idx >= 0)."""
+        n = x.shape[0]
+        if x.dim() != 2 or x.shape[1] < self.T or x.stride(1) != 1 or x.device != self.device:
+            raise ValueError(f"x must be [n, >= {self.T}] f32 rows on {self.device}")
+        if out is None:
+            out = torch.empty((n, self.T), dtype=torch.float32, device=self.device)
+        noise_off = noise_off.to(self.device, torch.int64).contiguous()
+        spec_idx = spec_idx.to(self.device, torch.int32).contiguous()
+        snr_db = snr_db.to(self.device, torch.float32).contiguous()
+        if noise_off.numel() != n or spec_idx.numel() != n or snr_db.numel() != n:
+            raise ValueError("per-clip arrays must have n entries")
+        if bool((noise_off >= 0).any()) and (ring is None or ring.numel() == 0):
+            raise ValueError("noise requested without a noise ring")
+        if spectra is not None and bool((spec_idx >= spectra.shape[0]).any()):
+            raise ValueError("spec_idx out of range")
+        ring_len = 0 if ring is None else ring.numel()
+        check(lib().hbk_augment(self._handle, ptr(x), n, x.stride(0),
+                                ptr(ring) if ring is not None else None, ring_len, ptr(noise_off),
+                                ptr(snr_db), ptr(spectra) if spectra is not None else None,
+                                ptr(spec_idx), ptr(out), out.stride(0), stream_ptr(self.device)),
+              "hbk_augment")
+        return out
+
+    def __del__(self) -> None:
+        h = getattr(self, "_handle", None)
+        if h is not None and h.value:
+            try:
+                lib().hbk_reverb_plan_destroy(h)
+            except Exception:
+                pass
+            self._handle = None

@@ -177,6 +177,37 @@ int hbk_mlp_gate_adam(const hbk_mlp_plan* plan, float* params, const float* buck
                       float* v, float* state, float* ctrl, float* history, int32_t history_cap,
                       float lr, float beta1, float beta2, float eps, void* stream);
 
+/* ------------------------------------------------------------------------ *
+ * Batch augmentation: background-noise mix + impulse-response reverb
+ *
+ * Replaces add_background_noise_to_batch -> torchaudio.functional.add_noise
+ * (dataset/augmented.py:234-276, applied :383-384) and speechbrain
+ * reverberate(batch, ir, rescale_amp="avg") (:386-392) of
+ * AugmentedAudioGenerator.execute_augment_batch, for clips of T = 23,040
+ * samples (1.44 s, augmented.py:31).
+ * ------------------------------------------------------------------------ */
+typedef struct hbk_reverb_plan hbk_reverb_plan;
+
+/* T must be 23040. */
+int hbk_reverb_plan_create(int64_t T, hbk_reverb_plan** plan);
+int hbk_reverb_plan_destroy(hbk_reverb_plan* plan);
+
+/* kernels [n_kernels, stride] f32: the ROTATED length-T kernels
+ * [ir[d:], zeros(T - L), ir[:d]] (d = argmax |ir|, ir truncated to T first),
+ * spectra [n_kernels, T/2 + 1] complex64 (interleaved f32) = rfft(kernel). */
+int hbk_reverb_spectrum(const hbk_reverb_plan* plan, const float* kernels, int64_t n_kernels,
+                        int64_t stride, float* spectra, void* stream);
+
+/* Per clip i of x [n_clips, x_stride] (first T samples used):
+ *   if noise_off[i] >= 0: y = x + 10^((10 log10(|x|^2/|n|^2) - snr_db[i]) / 20) n,
+ *      n = noise_ring[(noise_off[i] + t) mod ring_len], t < T;
+ *   if spec_idx[i] >= 0: y = mean|y| * c / (mean|c| + 1e-14), c = irfft(rfft(y) * spectra[spec_idx[i]]).
+ * out [n_clips, out_stride] (may equal x). All pointers are device pointers. */
+int hbk_augment(const hbk_reverb_plan* plan, const float* x, int64_t n_clips, int64_t x_stride,
+                const float* noise_ring, int64_t ring_len, const int64_t* noise_off,
+                const float* snr_db, const float* spectra, const int32_t* spec_idx, float* out,
+                int64_t out_stride, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,82 @@
+"""Augmentation oracle (TEST INFRASTRUCTURE ONLY, see oracle/__init__.py).
+
+Restates the two batch augmentations of AugmentedAudioGenerator.execute_augment_batch
+(reference src/python/heybuddy/dataset/augmented.py:383-392). Both live in
+third-party packages that are not installed here, so they are restated from
+their published algorithms at the versions environment.yml pins
+(PARITY UNPINNED at the third-party boundary; the reference holds no fixture):
+
+* torchaudio.functional.add_noise (torchaudio >= 2.3, environment.yml:28),
+  called by add_background_noise_to_batch (augmented.py:234-276):
+      E_x = ||x||^2, E_n = ||n||^2 (per clip)
+      snr_0 = 10 (log10 E_x - log10 E_n)
+      y = x + 10^((snr_0 - snr) / 20) * n
+  with the noise of clip b = samples [b T, (b+1) T) of the concatenation of
+  consecutive background clips (augmented.py:246-267).
+* speechbrain.processing.signal_processing.reverberate(x, ir, rescale_amp="avg")
+  (speechbrain >= 1.0, environment.yml:24), one IR per batch (augmented.py:389-392):
+      a_in = mean |x|  (per clip)
+      d = argmax |ir|; if L > T: ir = ir[:T]
+      k = [ir[d:], zeros(T - L), ir[:d]]
+      y = irfft(rfft(x) * rfft(k), n=T)          (circular, length T)
+      y = a_in * y / (mean |y| + 1e-14)
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def add_noise(x: np.ndarray, noise: np.ndarray, snr_db: np.ndarray, dtype=np.float64) -> np.ndarray:
+    x = np.asarray(x, dtype=dtype)
+    n = np.asarray(noise, dtype=dtype)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        ex = (x * x).sum(axis=-1)
+        en = (n * n).sum(axis=-1)
+        snr0 = 10.0 * (np.log10(ex) - np.log10(en))
+        scale = 10.0 ** ((snr0 - np.asarray(snr_db, dtype=dtype)) / 20.0)
+        return x + scale[..., None] * n
+
+
+def noise_segments(bank: list, start_clip: int, batch: int, T: int):
+    """augmented.py:246-267: concatenate background clips from ``start_clip``
+    (cycling) until >= batch*T samples, split into ``batch`` segments of T.
+    Returns (segments [batch, T], next clip index)."""
+    parts, total, i = [], 0, start_clip
+    while total < batch * T:
+        c = np.asarray(bank[i % len(bank)], dtype=np.float64)
+        parts.append(c)
+        total += c.shape[0]
+        i += 1
+    cat = np.concatenate(parts)[:batch * T]
+    return cat.reshape(batch, T), i
+
+
+def reverb_kernel(ir: np.ndarray, T: int) -> np.ndarray:
+    """The rotated length-T kernel of speechbrain's convolve1d(use_fft=True,
+    rotation_index=argmax|ir|)."""
+    ir = np.asarray(ir, dtype=np.float64)
+    d = int(np.argmax(np.abs(ir)))
+    if ir.shape[0] > T:
+        ir = ir[:T]
+    zeros = np.zeros(T - ir.shape[0])
+    return np.concatenate([ir[d:], zeros, ir[:d]])
+
+
+def reverberate(x: np.ndarray, ir: np.ndarray, dtype=np.float64) -> np.ndarray:
+    x = np.asarray(x, dtype=dtype)
+    T = x.shape[-1]
+    a_in = np.abs(x).mean(axis=-1, keepdims=True)
+    k = reverb_kernel(ir, T)
+    y = np.fft.irfft(np.fft.rfft(x, axis=-1) * np.fft.rfft(k), n=T, axis=-1)
+    return a_in * y / (np.abs(y).mean(axis=-1, keepdims=True) + 1e-14)
+
+
+def augment_batch(x, noise=None, snr_db=None, ir=None, dtype=np.float64):
+    """noise mix (if noise is given) then reverb (if ir is given), as
+    execute_augment_batch applies them (augmented.py:383-392)."""
+    y = np.asarray(x, dtype=dtype)
+    if noise is not None:
+        y = add_noise(y, noise, snr_db, dtype)
+    if ir is not None:
+        y = reverberate(y, ir, dtype)
+    return y

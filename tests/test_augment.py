@@ -1,0 +1,141 @@
+"""Background-noise mix + IR reverb: oracle properties (CPU), HIP parity (GPU).
+
+PARITY UNPINNED at the third-party boundary: torchaudio.add_noise and
+speechbrain.reverberate are not installed and the reference holds no fixture
+for them; oracle/augment.py restates their published algorithms. The CPU
+tests check that restatement against size-independent properties (linearity,
+circularity, the SNR definition, the rotation by argmax |ir|); the GPU tests
+check the HIP kernel against it. Tolerance: fp32 FFT of length 11,520 vs fp64,
+|diff| <= 2e-5 * max|ref| and RMS(diff) <= 2e-6 * RMS(ref).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import augment as oaug
+
+T = 23040
+
+
+def _clips(n, seed=0):
+    from heybuddy.synthetic import synthetic_clips
+    return synthetic_clips(n, length=T, seed=seed).numpy().astype(np.float64)
+
+
+def _bank(seed=1):
+    from heybuddy.synthetic import impulse_responses, noise_bank
+    return ([x.numpy() for x in noise_bank(6, seed=seed)],
+            [x.numpy() for x in impulse_responses(4, seed=seed)])
+
+
+def test_add_noise_hits_requested_snr():
+    x = _clips(3)
+    rng = np.random.default_rng(0)
+    n = rng.standard_normal((3, T)) * 0.1
+    snr = np.array([-10.0, 0.0, 15.0])
+    y = oaug.add_noise(x, n, snr)
+    scaled = y - x
+    got = 10 * np.log10((x ** 2).sum(1) / (scaled ** 2).sum(1))
+    np.testing.assert_allclose(got, snr, atol=1e-9)
+    # zero-energy noise -> NaN, zero-energy clip -> unchanged (torchaudio semantics)
+    z = oaug.add_noise(np.zeros((1, T)), n[:1], np.zeros(1))
+    assert np.all(z == 0)
+    assert np.isnan(oaug.add_noise(x[:1], np.zeros((1, T)), np.zeros(1))).all()
+
+
+def test_noise_segments_follow_the_dataset_order():
+    bank = [np.full(40000, float(i)) for i in range(3)]
+    seg, nxt = oaug.noise_segments(bank, 1, 4, T)
+    assert seg.shape == (4, T) and nxt == 1 + 3  # 3 clips of 40000 >= 4*23040
+    assert seg[0, 0] == 1 and seg[1, -1] == 2 and seg[3, -1] == 0
+
+
+def test_reverb_kernel_rotation_and_circularity():
+    ir = np.zeros(5000)
+    ir[37] = 2.0
+    ir[100] = 0.5
+    k = oaug.reverb_kernel(ir, T)
+    assert k.shape == (T,) and k[0] == 2.0 and k[63] == 0.5 and k[-37:].sum() == 0
+    # a pure delta at the direct path = identity (up to the mean-amplitude rescale)
+    x = _clips(2)
+    y = oaug.reverberate(x, np.eye(1, 300, 120)[0])
+    np.testing.assert_allclose(y, x, atol=1e-12)
+    # circular, not linear: a delayed tap wraps around the clip end
+    d = np.zeros(300)
+    d[0], d[200] = 1.0, 0.9
+    y = oaug.reverberate(x, d)
+    ref = x + 0.9 * np.roll(x, 200, axis=1)
+    ref *= np.abs(x).mean(1, keepdims=True) / np.abs(ref).mean(1, keepdims=True)
+    np.testing.assert_allclose(y, ref, atol=1e-9)
+
+
+def _close(out, ref):
+    err = np.abs(out - ref)
+    return (err.max() <= 2e-5 * np.abs(ref).max()
+            and np.sqrt((err ** 2).mean()) <= 2e-6 * np.sqrt((ref ** 2).mean())), err.max()
+
+
+@pytest.mark.gpu
+def test_reverb_spectrum_matches_rfft():
+    from heybuddy.kernels import ReverbPlan
+    plan = ReverbPlan()
+    _, irs = _bank()
+    ks = torch.stack([ReverbPlan.rotated_kernel(torch.from_numpy(ir), T) for ir in irs])
+    H = plan.spectra(ks.cuda()).cpu().numpy()
+    ref = np.fft.rfft(ks.numpy().astype(np.float64), axis=1)
+    got = H[..., 0] + 1j * H[..., 1]
+    assert np.abs(got - ref).max() <= 2e-5 * np.abs(ref).max()
+
+
+@pytest.mark.gpu
+def test_augment_noise_and_reverb_parity():
+    from heybuddy.kernels import ReverbPlan
+    plan = ReverbPlan()
+    x = _clips(6, seed=4)
+    noises, irs = _bank(seed=5)
+    ring = np.concatenate(noises)
+    starts = np.cumsum([0] + [len(n) for n in noises])[:-1]
+    # clips 0-2: noise + reverb (IR 0); 3: reverb only (IR 1); 4: noise only; 5: untouched
+    seg, _ = oaug.noise_segments(noises, 2, 3, T)
+    noise_off = np.array([starts[2], starts[2] + T, starts[2] + 2 * T, -1, starts[4], -1])
+    snr = np.array([-10.0, 3.0, 15.0, 0.0, 7.5, 0.0])
+    spec_idx = np.array([0, 0, 0, 1, -1, -1])
+    ks = torch.stack([ReverbPlan.rotated_kernel(torch.from_numpy(irs[i]), T) for i in range(2)]).cuda()
+    H = plan.spectra(ks)
+    out = plan.augment(torch.from_numpy(x).float().cuda(), torch.from_numpy(ring).float().cuda(),
+                       torch.from_numpy(noise_off), torch.from_numpy(snr), H,
+                       torch.from_numpy(spec_idx)).cpu().numpy()
+    xf = x.astype(np.float32).astype(np.float64)
+    ref = np.empty_like(xf)
+    ref[:3] = oaug.reverberate(oaug.add_noise(xf[:3], seg, snr[:3]), irs[0])
+    ref[3] = oaug.reverberate(xf[3:4], irs[1])[0]
+    n4 = np.asarray(noises[4], np.float64)[:T]
+    ref[4] = oaug.add_noise(xf[4:5], n4[None], snr[4:5])[0]
+    ref[5] = xf[5]
+    for i in range(6):
+        ok, worst = _close(out[i], ref[i])
+        assert ok, f"clip {i}: max |diff| {worst}"
+
+
+@pytest.mark.gpu
+def test_augment_ring_wraparound_and_long_ir():
+    """A noise segment that wraps the end of the ring, and an IR longer than
+    the clip (truncated to T before rotation, augmented.py -> convolve1d)."""
+    from heybuddy.kernels import ReverbPlan
+    plan = ReverbPlan()
+    x = _clips(2, seed=8)
+    rng = np.random.default_rng(3)
+    ring = rng.standard_normal(30000) * 0.05
+    long_ir = rng.standard_normal(30000) * np.exp(-np.arange(30000) / 3000.0)
+    long_ir[5] = 10.0
+    H = plan.spectra(ReverbPlan.rotated_kernel(torch.from_numpy(long_ir), T)[None].cuda())
+    off = np.array([20000, 29999])
+    out = plan.augment(torch.from_numpy(x).float().cuda(), torch.from_numpy(ring).float().cuda(),
+                       torch.from_numpy(off), torch.tensor([0.0, 5.0]), H,
+                       torch.tensor([0, 0])).cpu().numpy()
+    idx = (off[:, None] + np.arange(T)[None]) % ring.size
+    xf = x.astype(np.float32).astype(np.float64)
+    ref = oaug.reverberate(oaug.add_noise(xf, ring.astype(np.float32)[idx], np.array([0.0, 5.0])), long_ir)
+    for i in range(2):
+        ok, worst = _close(out[i], ref[i])
+        assert ok, f"clip {i}: max |diff| {worst}"
