@@ -42,6 +42,7 @@ from heybuddy.constants import (DEFAULT_ACTIVATION_THRESHOLD, DEFAULT_ARCHITECTU
                                 DEFAULT_STAGES, DEFAULT_STEP_ADJUST_RATIO, DEFAULT_STEPS,
                                 DEFAULT_TARGET_FALSE_POSITIVE_RATE, DEFAULT_VALIDATION_STEPS,
                                 DEFAULT_WARMUP_STEPS)
+from heybuddy import distributed
 from heybuddy.util import logger
 from heybuddy.wakeword import WakeWordMLPModel
 
@@ -188,15 +189,12 @@ class WakeWordTrainer(Trainer):
     # -- data parallel ---------------------------------------------------------
     @staticmethod
     def _world() -> Tuple[int, int]:
-        if dist.is_available() and dist.is_initialized():
-            return dist.get_rank(), dist.get_world_size()
-        return 0, 1
+        return distributed.world()
 
     def _step(self, x: torch.Tensor, y: torch.Tensor, lr: float, neg_weight: float, threshold: float,
               activation_threshold: float, history: Optional[torch.Tensor], seed: int) -> None:
         rank, world = self._world()
-        if world > 1:  # class-stratified slice: batches are [positives | adversarial | negatives]
-            x, y = x[rank::world], y[rank::world]
+        x, y = distributed.shard_batch(x, y, rank, world)
         dev = self.device
         x = x.to(dev, non_blocking=True)
         y = y.to(dev, non_blocking=True)
@@ -205,8 +203,7 @@ class WakeWordTrainer(Trainer):
         plan.train_fwd_bwd(self.model.flat_parameters, x.reshape(x.shape[0], -1), y, self._bucket,
                            neg_weight, threshold, activation_threshold, dropout_p=p,
                            seed=seed * 1000003 + rank)
-        if world > 1:
-            dist.all_reduce(self._bucket)
+        distributed.reduce_bucket(self._bucket)
         plan.gate_adam(self.model.flat_parameters, self._bucket, self._m, self._v, self._state, self._ctrl,
                        history, lr, BETAS[0], BETAS[1], EPS)
 

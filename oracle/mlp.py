@@ -257,3 +257,28 @@ def train_epoch(params, batches, num_steps, warmup_steps, hold_steps, learning_r
             hist["loss"].append(last_loss)
         hist["updated"].append(updated)
     return params, hist
+
+
+def flat_bucket(params, x, y, neg_weight=1.0, threshold=1e-4, act_thr=0.5):
+    """What hbk_mlp_train_fwd_bwd leaves in its bucket: the UNNORMALISED
+    gradient sum over the selected samples of w * dl/dz (state_dict order,
+    flattened) and the 8 statistics [n_sel, sum w*l, n_neg_sel, fp_sel,
+    n_pos_sel, tp_sel, batch, 0]."""
+    prob, z, cache = forward(params, x)
+    sel = select_high_loss(prob, y, threshold)
+    dz = np.zeros_like(prob)
+    stats = np.zeros(8)
+    stats[6] = prob.shape[0]
+    if sel.size:
+        ps, ys = prob[sel], y[sel].astype(np.float64)
+        w = np.where(ys == 1, 1.0, neg_weight)
+        dz[sel] = w * (ps - ys)
+        stats[0] = sel.size
+        stats[1] = float((w * bce_terms(ps, ys)).sum())
+        neg = ys == 0
+        stats[2] = neg.sum()
+        stats[3] = (neg & (ps >= act_thr)).sum()
+        stats[4] = (~neg).sum()
+        stats[5] = ((~neg) & (ps > act_thr)).sum()
+    grads = backward(params, cache, dz)
+    return np.concatenate([g.reshape(-1) for g in grads.values()]), stats

@@ -1,0 +1,85 @@
+"""Data-parallel design on CPU (gloo, world size 2).
+
+The trainer's exchange step is: each rank computes the UNNORMALISED gradient
+bucket of its class-stratified batch slice, one all-reduce sums the buckets,
+and the gate + normalisation use the global statistics. Here the oracle
+stands in for the HIP kernel on each rank (no GPU in this container); the
+test checks that the reduced, normalised gradient equals the single-process
+gradient of the whole batch, using the same sharding / reduce helpers the
+trainer calls (heybuddy.distributed).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, q):
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "hey-buddy_amd")]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from heybuddy import distributed as hd
+    from oracle import mlp as omlp
+    params = omlp.init_params(seed=3)
+    rng = np.random.default_rng(9)
+    B = 150
+    y = np.concatenate([np.ones(50, np.int64), np.zeros(100, np.int64)])
+    x = rng.standard_normal((B, 16, 96)).astype(np.float32)
+    xs, ys = hd.shard_batch(torch.from_numpy(x), torch.from_numpy(y), rank, world)
+    g, st = omlp.flat_bucket(params, xs.numpy(), ys.numpy(), neg_weight=2.0)
+    bucket = torch.from_numpy(np.concatenate([g, st]))
+    hd.reduce_bucket(bucket)
+    lo, hi = hd.clip_range(1003, rank, world)
+    q.put((rank, bucket.numpy(), (lo, hi), int(xs.shape[0]), int((ys == 1).sum())))
+    dist.destroy_process_group()
+
+
+def test_dp_bucket_allreduce_equals_full_batch():
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "hey-buddy_amd")]
+    from oracle import mlp as omlp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in procs], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    b0, b1 = res[0][1], res[1][1]
+    np.testing.assert_array_equal(b0, b1)  # every rank holds the same reduced bucket
+    # single process, whole batch
+    params = omlp.init_params(seed=3)
+    rng = np.random.default_rng(9)
+    y = np.concatenate([np.ones(50, np.int64), np.zeros(100, np.int64)])
+    x = rng.standard_normal((150, 16, 96)).astype(np.float32)
+    g, st = omlp.flat_bucket(params, x, y, neg_weight=2.0)
+    n = st[0]
+    np.testing.assert_allclose(b0[-8:], st, rtol=1e-12)
+    np.testing.assert_allclose(b0[:-8] / n, g / n, rtol=1e-9, atol=1e-14)
+    # normalised = the reference's dL/dtheta of BCE_mean over the selected set
+    prob, z, cache = omlp.forward(params, x)
+    loss, n_sel, dz = omlp.step_loss_and_dz(prob, y, 2.0)
+    ref = np.concatenate([v.reshape(-1) for v in omlp.backward(params, cache, dz).values()])
+    np.testing.assert_allclose(b0[:-8] / n, ref, rtol=1e-6, atol=1e-12)
+    # stratified shards and a complete clip partition
+    assert res[0][3] + res[1][3] == 150 and res[0][4] == res[1][4] == 25
+    assert res[0][2] == (0, 501) and res[1][2] == (501, 1003)

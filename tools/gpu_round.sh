@@ -1,5 +1,5 @@
 #!/bin/bash
-# One GPU session: tests, smoke, bench, rocprof kernel stats (+ optional PMC passes).
+# One GPU session: tests, smoke, bench (configs), rocprof kernel stats and PMC passes.
 # Every GPU step has its own time limit; the first failure ends the script.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
@@ -7,25 +7,31 @@ export TMPDIR=/tmp
 OUT=gpurun_out
 mkdir -p $OUT
 TAG=${TAG:-r01}
-step() { echo "=== $1"; }
-step tests
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > $OUT/tests_$TAG.log 2>&1 || { tail -40 $OUT/tests_$TAG.log; exit 1; }
-tail -3 $OUT/tests_$TAG.log
-step smoke
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$TAG.log 2>&1 || { tail -20 $OUT/smoke_$TAG.log; exit 1; }
-cat $OUT/smoke_$TAG.log | tail -2
-step bench
-timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err || { tail -20 $OUT/bench_$TAG.err; exit 1; }
-cat $OUT/bench_$TAG.json
+if [ -z "$SKIP_TESTS" ]; then
+  echo "=== tests"
+  timeout -k 10 900 python -m pytest tests -m gpu -x -q > $OUT/tests_$TAG.log 2>&1 || { tail -40 $OUT/tests_$TAG.log; exit 1; }
+  tail -2 $OUT/tests_$TAG.log
+  echo "=== smoke"
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$TAG.log 2>&1 || { tail -20 $OUT/smoke_$TAG.log; exit 1; }
+  tail -1 $OUT/smoke_$TAG.log
+fi
+for C in ${CONFIGS:-2}; do
+  echo "=== bench config $C"
+  timeout -k 10 600 python bench.py --config $C ${BENCH_ARGS:-} > $OUT/bench_${TAG}_c$C.json 2> $OUT/bench_${TAG}_c$C.err || { tail -20 $OUT/bench_${TAG}_c$C.err; exit 1; }
+  cat $OUT/bench_${TAG}_c$C.json
+done
 if [ -n "$PROF" ]; then
-  step rocprof
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof_$TAG -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu > $OUT/prof_$TAG.log 2>&1 || { tail -20 $OUT/prof_$TAG.log; exit 1; }
-  find $OUT/prof_$TAG -name "*stats*" | head
+  for C in ${PROF_CONFIGS:-2}; do
+    echo "=== rocprof config $C"
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof_${TAG}_c$C -o run -- python3 bench.py --config $C --steps 3 --warmup 1 --no-cpu > $OUT/prof_${TAG}_c$C.log 2>&1 || { tail -20 $OUT/prof_${TAG}_c$C.log; exit 1; }
+  done
 fi
 if [ -n "$PMC" ]; then
-  step pmc
-  timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -f csv -d $OUT/pmc_fetch_$TAG -o run -- python3 bench.py --steps 2 --warmup 0 --no-cpu > $OUT/pmc_fetch_$TAG.log 2>&1 || { tail -20 $OUT/pmc_fetch_$TAG.log; exit 1; }
-  timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -f csv -d $OUT/pmc_write_$TAG -o run -- python3 bench.py --steps 2 --warmup 0 --no-cpu > $OUT/pmc_write_$TAG.log 2>&1 || { tail -20 $OUT/pmc_write_$TAG.log; exit 1; }
-  find $OUT/pmc_*_$TAG -name "*.csv" | head
+  for C in ${PROF_CONFIGS:-2}; do
+    echo "=== pmc config $C"
+    timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/pmcf_${TAG}_c$C -o run -- python3 bench.py --config $C --steps 1 --warmup 0 --no-cpu --no-check > $OUT/pmcf_${TAG}_c$C.log 2>&1 || { tail -20 $OUT/pmcf_${TAG}_c$C.log; exit 1; }
+    timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -f csv -d $OUT/pmcw_${TAG}_c$C -o run -- python3 bench.py --config $C --steps 1 --warmup 0 --no-cpu --no-check > $OUT/pmcw_${TAG}_c$C.log 2>&1 || { tail -20 $OUT/pmcw_${TAG}_c$C.log; exit 1; }
+    python tools/pmc_summary.py $OUT/pmcf_${TAG}_c$C $OUT/pmcw_${TAG}_c$C $OUT/pmc_${TAG}_c$C.json
+  done
 fi
 echo "=== done"
