@@ -44,6 +44,9 @@ import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_MFMA_PEAK_TFLOPS = 157.3  # dense f32 MFMA = f32 vector peak
+F16_MFMA_PEAK_TFLOPS = 2516.6  # dense f16 MFMA: 1024 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz
+# split-f16 embedding GEMMs issue 3 f16 products per f32-accurate MAC
+SPLIT_PEAK_TFLOPS = round(F16_MFMA_PEAK_TFLOPS / 3, 1)
 MEL_READ_SAMPLES = 22912       # frame 140 ends at 140*160 + 512
 N_FRAMES = 141
 AUG_T = 23040
@@ -79,9 +82,10 @@ def load_traffic(path, kernel_substr):
     return None
 
 
-def roof(kernel, bound, work, ms, unit, traffic, **extra):
+def roof(kernel, bound, work, ms, unit, traffic, peak=None, **extra):
     ach = work / (ms * 1e-3) / (1e9 if unit == "GB/s" else 1e12)
-    peak = HBM_PEAK_GBS if unit == "GB/s" else FP32_MFMA_PEAK_TFLOPS
+    if peak is None:
+        peak = HBM_PEAK_GBS if unit == "GB/s" else FP32_MFMA_PEAK_TFLOPS
     d = {"kernel": kernel, "bound": bound, "achieved": round(ach, 3), "peak": peak, "unit": unit,
          "frac": round(ach / peak, 4), "traffic": traffic, "ms_per_step": round(ms, 3)}
     d.update(extra)
@@ -199,9 +203,14 @@ def setup_featurize(args, dev, rank, world, seed):
                         n * (MEL_READ_SAMPLES * 4 + N_FRAMES * 32 * 4), ms, "GB/s", load_traffic(pmc, "mel_frames"),
                         algorithmic_bytes_per_clip=MEL_READ_SAMPLES * 4 + N_FRAMES * 32 * 4)
         if name == "embed":
-            return roof("conv_chain_kernel (hbk_embed_clips: %d chained launches per %d-clip chunk)"
-                        % (eplan.n_chains, min(n, 16384)), "mfma", 2.0 * eplan.macs_per_clip * n, ms,
-                        "TFLOP/s", load_traffic(pmc, "conv_chain"),
+            split = eplan.precision == "split"
+            kname = "conv_chain_x3_kernel" if split else "conv_chain_kernel"
+            return roof("%s (hbk_embed_clips, %s: %d chained launches per %d-clip chunk)"
+                        % (kname, eplan.precision, eplan.n_chains, min(n, 16384)), "mfma",
+                        2.0 * eplan.macs_per_clip * n, ms, "TFLOP/s", load_traffic(pmc, "conv_chain"),
+                        peak=SPLIT_PEAK_TFLOPS if split else FP32_MFMA_PEAK_TFLOPS,
+                        peak_basis=("f16 dense MFMA peak / 3 (hi*hi + hi*lo + lo*hi per f32-accurate MAC)"
+                                    if split else "f32-input MFMA dense peak"),
                         algorithmic_flops_per_clip=2.0 * eplan.macs_per_clip)
         return roof("augment_kernel (hbk_augment: noise mix + 23040-pt circular FFT reverb, 1 launch)",
                     "hbm", n * AUG_T * 4 * 3, ms, "GB/s", load_traffic(pmc, "augment_kernel"),
@@ -287,16 +296,19 @@ def setup_train(args, dev, rank, world, seed):
         from oracle import mlp as omlp
         params = omlp.init_params(seed=0)
         rng = np.random.default_rng(0)
+        from threadpoolctl import threadpool_limits
         steps = sample or 20
+        threads = min(16, os.cpu_count() or 1)
         x = rng.standard_normal((B, 16, 96)).astype(np.float32)
         y = np.concatenate([np.ones(50), np.zeros(B - 50)]).astype(np.int64)
-        c0 = time.perf_counter()
-        for _ in range(steps):
-            prob, z, cache = omlp.forward(params, x, dtype=np.float32)
-            loss, n, dz = omlp.step_loss_and_dz(prob, y)
-            omlp.backward(params, cache, dz, dtype=np.float32)
-        el = time.perf_counter() - c0
-        return {"value": round(steps * B / el, 1), "unit": "embeddings/s", "cores": os.cpu_count() or 1,
+        with threadpool_limits(limits=threads):
+            c0 = time.perf_counter()
+            for _ in range(steps):
+                prob, z, cache = omlp.forward(params, x, dtype=np.float32)
+                loss, n, dz = omlp.step_loss_and_dz(prob, y)
+                omlp.backward(params, cache, dz, dtype=np.float32)
+            el = time.perf_counter() - c0
+        return {"value": round(steps * B / el, 1), "unit": "embeddings/s", "cores": threads,
                 "kind": "port", "sample": f"{steps} train steps of B={B} through oracle/mlp.py (numpy fp32, "
                                           f"BLAS threads), {el:.1f} s"}
 

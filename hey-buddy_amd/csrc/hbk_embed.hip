@@ -231,6 +231,393 @@ __global__ void __launch_bounds__(kThreads) conv_chain_kernel(ChainArgs a) {
   }
 }
 
+// ------------------------------------------------- split-f16 conv chain ----
+// Same task structure as conv_chain_kernel; the arithmetic is an fp16 pair per
+// value, x = hi + 2^-11 lo (lo = fp16((x - hi) * 2^11), hi rounded toward
+// zero), and each GEMM is
+//   acc_h = W_hi X_hi,  acc_x = W_hi X_lo + W_lo X_hi,  out = acc_h + 2^-11 acc_x
+// on v_mfma_f32_32x32x16_f16 (f32 accumulation), with the WEIGHTS as the A
+// operand (32 output channels) and 32 output POSITIONS as the B operand, so a
+// lane of the accumulator holds 4 consecutive channels of one position: the
+// epilogue packs them (v_cvt_pkrtz) and stores 8 B per plane.
+// Activations live in LDS as two fp16 planes [pos][cs] (cs = channels rounded
+// to 8, with cs / 8 odd so the 16-B fragment reads of 32 consecutive positions
+// are conflict-free); a K-group is 8 consecutive channels of one tap, the unit
+// of one lane's ds_read_b128. Weights are [n][wrow] fp16 planes (k contiguous
+// per output channel). A first stage whose cin is not a multiple of 8 (the
+// mel input, cin 1) is expanded im2col-style during staging and runs as a
+// 1x1 conv. Staging / store loops use a per-kernel 2-D thread mapping (row x
+// unit) so no integer division runs per element.
+constexpr int kXThreads = 256;
+constexpr int kXWaves = kXThreads / 64;
+constexpr float kLoScale = 2048.f;
+constexpr float kLoInv = 1.f / 2048.f;
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef __fp16 h2 __attribute__((ext_vector_type(2)));
+typedef float f16x __attribute__((ext_vector_type(16)));
+
+struct XStage {
+  int kh, kw, cin, cout;
+  int coutr;          // output channels written (cout rounded up to 8; the pad is exactly 0)
+  int cs_in, cs_out;  // fp16 elements per position of the input / output tensor
+  int ksteps;         // K steps of 16 (two 8-channel groups)
+  int nblk;           // 32-wide output-channel blocks
+  int act;
+  float alpha;
+  int w_off;          // fp16 offset of the hi plane [nblk * 32][wrow]
+  int w_lo;           // fp16 distance hi -> lo plane
+  int wrow;
+  int b_off;          // float offset into the bias blob
+  int kt_off;         // int offset of the stage's group-offset table
+};
+
+struct XArgs {
+  const float* in;
+  float* out;
+  const _Float16* wblob;   // global weights (WG mode reads them here)
+  const float* bblob;      // biases [per stage nblk * 32]
+  const int* ktab;         // group offsets, all stages
+  int64_t n_img;
+  int64_t src_clip_stride;
+  int src_row_stride;
+  int ipc;
+  int row_off[kMaxWin];
+  int C_src, cs0;          // source channels; fp16 stride of the staged tensor
+  int im2col;              // stage 0 input is the im2col expansion (K0 = kh kw cin)
+  int in_ph, in_pw, W_in;
+  int out_ph, out_pw, H_out, W_out, C_out;
+  int64_t out_img_stride;
+  int vec_out;             // C_out % 4 == 0 and 16-B aligned output: float4 stores
+  int G, band, n_bands, shrink, n_stages;
+  XStage st[kMaxStages];
+  int w_halfs;             // resident weights (0: WG mode)
+  int b_floats, kt_n;
+  int lds_x, lds_y, lds_w, lds_b, lds_k;  // byte offsets into dynamic LDS
+};
+
+// hi (round toward zero) and lo = (v - hi) * 2^11 for two values, packed
+__device__ __forceinline__ void split2(float a, float b, h2& hi, h2& lo) {
+  hi = __builtin_amdgcn_cvt_pkrtz(a, b);
+  lo = __builtin_amdgcn_cvt_pkrtz((a - static_cast<float>(hi.x)) * kLoScale,
+                                  (b - static_cast<float>(hi.y)) * kLoScale);
+}
+
+__device__ __forceinline__ uint32_t h2_bits(h2 v) { return __builtin_bit_cast(uint32_t, v); }
+
+// 2-D mapping of kXThreads threads onto rows of `units` work items: rpp rows
+// per pass; this thread takes unit t_u of row t_row (+ rpp per pass). When a
+// row has more units than threads, rpp = 1 and the unit loop strides by
+// kXThreads.
+struct RowMap {
+  int rpp, t_row, t_u, u_step;
+  __device__ __forceinline__ RowMap(int units, int tid) {
+    if (units <= kXThreads) {
+      rpp = kXThreads / units;
+      t_row = tid / units;
+      t_u = tid - t_row * units;
+      u_step = units;  // one unit per row per thread
+      if (t_row >= rpp) t_row = 1 << 30;  // idle thread
+    } else {
+      rpp = 1;
+      t_row = 0;
+      t_u = tid;
+      u_step = kXThreads;
+    }
+  }
+};
+
+template <int NB, int RB>
+__device__ __forceinline__ void xstage(const _Float16* __restrict__ Xh, const _Float16* __restrict__ Xl,
+                                       _Float16* __restrict__ Yh, _Float16* __restrict__ Yl,
+                                       const _Float16* __restrict__ Wh, const int* __restrict__ kt,
+                                       const float* __restrict__ bias, int M, int hA, int wA, int ho,
+                                       int wo, const XStage& S, int lane, int wave) {
+  const int img_pos = ho * wo;
+  const int nrb = (M + 31) >> 5;
+  const int r32 = lane & 31, khalf = lane >> 5;
+  const _Float16* wp = Wh + r32 * S.wrow + khalf * 8;
+  const int cstride = 32 * S.wrow;
+  for (int rb0 = wave * RB; rb0 < nrb; rb0 += kXWaves * RB) {
+    int xoff[RB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const int m = min((rb0 + r) * 32 + r32, M - 1);
+      const int g = m / img_pos;
+      const int rem = m - g * img_pos;
+      const int y = rem / wo;
+      const int x = rem - y * wo;
+      xoff[r] = ((g * hA + y) * wA + x) * S.cs_in;
+    }
+    f16x acc_h[RB][NB], acc_x[RB][NB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+      for (int c = 0; c < NB; ++c) {
+        acc_h[r][c] = f16x{};
+        acc_x[r][c] = f16x{};
+      }
+#pragma unroll 2
+    for (int ks = 0; ks < S.ksteps; ++ks) {
+      const int ko = kt[2 * ks + khalf];
+      h8 xh[RB], xl[RB];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        xh[r] = *reinterpret_cast<const h8*>(Xh + xoff[r] + ko);
+        xl[r] = *reinterpret_cast<const h8*>(Xl + xoff[r] + ko);
+      }
+#pragma unroll
+      for (int c = 0; c < NB; ++c) {
+        const h8 wh = *reinterpret_cast<const h8*>(wp + c * cstride + ks * 16);
+        const h8 wl = *reinterpret_cast<const h8*>(wp + S.w_lo + c * cstride + ks * 16);
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          acc_h[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xh[r], acc_h[r][c], 0, 0, 0);
+          acc_x[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xl[r], acc_x[r][c], 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+          acc_x[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, xh[r], acc_x[r][c], 0, 0, 0);
+      }
+    }
+    // D[n][m]: this lane holds position m = tile + (lane & 31) and channels
+    // n = 32 c + 8 q + 4 (lane >> 5) + j for register i = 4 q + j
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const int m = (rb0 + r) * 32 + r32;
+      if (m >= M) continue;
+      _Float16* yh = Yh + m * S.cs_out;
+      _Float16* yl = Yl + m * S.cs_out;
+#pragma unroll
+      for (int c = 0; c < NB; ++c)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int n0 = c * 32 + 8 * q + 4 * khalf;
+          if (n0 >= S.coutr) continue;
+          const float4 bb = *reinterpret_cast<const float4*>(bias + n0);
+          float v[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float t = acc_h[r][c][4 * q + j] + acc_x[r][c][4 * q + j] * kLoInv;
+            t += j == 0 ? bb.x : j == 1 ? bb.y : j == 2 ? bb.z : bb.w;
+            if (S.act) t = t >= 0.f ? t : t * S.alpha;
+            v[j] = t;
+          }
+          h2 h01, l01, h23, l23;
+          split2(v[0], v[1], h01, l01);
+          split2(v[2], v[3], h23, l23);
+          *reinterpret_cast<uint2*>(yh + n0) = uint2{h2_bits(h01), h2_bits(h23)};
+          *reinterpret_cast<uint2*>(yl + n0) = uint2{h2_bits(l01), h2_bits(l23)};
+        }
+    }
+  }
+}
+
+template <int NBMAX, bool WG>
+__global__ void __launch_bounds__(kXThreads) conv_chain_x3_kernel(XArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char xsmem[];
+  unsigned char* Xb = xsmem + a.lds_x;
+  unsigned char* Yb = xsmem + a.lds_y;
+  _Float16* Wl = reinterpret_cast<_Float16*>(xsmem + a.lds_w);
+  float* Bl = reinterpret_cast<float*>(xsmem + a.lds_b);
+  int* kt = reinterpret_cast<int*>(xsmem + a.lds_k);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (!WG)
+    for (int i = tid; i < a.w_halfs / 8; i += kXThreads)
+      reinterpret_cast<h8*>(Wl)[i] = reinterpret_cast<const h8*>(a.wblob)[i];
+  for (int i = tid; i < a.b_floats; i += kXThreads) Bl[i] = a.bblob[i];
+  for (int i = tid; i < a.kt_n; i += kXThreads) kt[i] = a.ktab[i];
+
+  const int64_t n_groups = (a.n_img + a.G - 1) / a.G;
+  const int64_t n_tasks = n_groups * a.n_bands;
+  const int C = a.C_src;
+  const XStage& S0 = a.st[0];
+  // per-kernel thread mappings
+  //  staging (no im2col): units of 8 channels, W_in * C / 8 per row
+  //  staging (im2col):    raw f32, W_in * C per row
+  //  im2col expansion:    positions, wo0 per row
+  //  store:               units of 4 channels (vec_out) or 1, W_out * C_out / (4|1) per row
+  const int st_units = a.im2col ? a.W_in * C : a.W_in * (C / 8);
+  const RowMap ms(st_units, tid);
+  const int st_w = a.im2col ? 0 : ms.t_u / (C / 8);
+  const int wo0 = a.W_in - S0.kw + 1;
+  const RowMap mi(wo0, tid);
+  const int cu = a.vec_out ? 4 : 1;
+  const RowMap mo(a.W_out * a.C_out / cu, tid);
+  const int o_w = mo.t_u / (a.C_out / cu), o_c = (mo.t_u - o_w * (a.C_out / cu)) * cu;
+
+  for (int64_t task = blockIdx.x; task < n_tasks; task += gridDim.x) {
+    const int64_t grp = task / a.n_bands;
+    const int band = static_cast<int>(task - grp * a.n_bands);
+    const int64_t img0 = grp * a.G;
+    const int G = static_cast<int>(min<int64_t>(a.G, a.n_img - img0));
+    const int orow0 = band * a.band;
+    const int orows = min(a.band, a.H_out - orow0);
+    const int r0 = orow0 * a.out_ph;
+    const int rows_in = orows * a.out_ph + a.shrink;
+    const int nrows = G * rows_in;
+
+    // 1) stage the band's input rows (max-pooled on the fly)
+    __syncthreads();  // previous task's readers of X / Y are done (kt, Wl, Bl on the first task)
+    for (int row = ms.t_row; row < nrows; row += ms.rpp) {
+      const int g = row / rows_in;
+      const int r = row - g * rows_in;
+      const int64_t im = img0 + g;
+      const int64_t clip = im / a.ipc;
+      const int roff = a.row_off[im - clip * a.ipc];
+      const float* srow = a.in + clip * a.src_clip_stride +
+                          static_cast<int64_t>(roff + (r0 + r) * a.in_ph) * a.src_row_stride;
+      for (int u = ms.t_u; u < st_units; u += ms.u_step) {
+        if (a.im2col) {  // raw f32 rows, u = w * C + c
+          const int w = u / C, c = u - w * C;
+          const float* src = srow + (w * a.in_pw) * C + c;
+          float v = src[0];
+          for (int i = 0; i < a.in_ph; ++i)
+            for (int j = 0; j < a.in_pw; ++j) v = nan_max(v, src[i * a.src_row_stride + j * C]);
+          reinterpret_cast<float*>(Yb)[row * st_units + u] = v;
+        } else {         // 8 channels of position w
+          const int w = (ms.u_step == st_units) ? st_w : u / (C / 8);
+          const int c8 = (u - w * (C / 8)) * 8;
+          const float* src = srow + (w * a.in_pw) * C + c8;
+          float4 lo4 = *reinterpret_cast<const float4*>(src);
+          float4 hi4 = *reinterpret_cast<const float4*>(src + 4);
+          for (int i = 0; i < a.in_ph; ++i)
+            for (int j = 0; j < a.in_pw; ++j) {
+              if (i == 0 && j == 0) continue;
+              const float* q = src + i * a.src_row_stride + j * C;
+              const float4 p0 = *reinterpret_cast<const float4*>(q);
+              const float4 p1 = *reinterpret_cast<const float4*>(q + 4);
+              lo4 = float4{nan_max(lo4.x, p0.x), nan_max(lo4.y, p0.y), nan_max(lo4.z, p0.z), nan_max(lo4.w, p0.w)};
+              hi4 = float4{nan_max(hi4.x, p1.x), nan_max(hi4.y, p1.y), nan_max(hi4.z, p1.z), nan_max(hi4.w, p1.w)};
+            }
+          h2 a0, b0, a1, b1, a2, b2, a3, b3;
+          split2(lo4.x, lo4.y, a0, b0);
+          split2(lo4.z, lo4.w, a1, b1);
+          split2(hi4.x, hi4.y, a2, b2);
+          split2(hi4.z, hi4.w, a3, b3);
+          _Float16* Sh = reinterpret_cast<_Float16*>(Xb);
+          const int idx = (row * a.W_in + w) * a.cs0 + c8;
+          *reinterpret_cast<uint4*>(Sh + idx) = uint4{h2_bits(a0), h2_bits(a1), h2_bits(a2), h2_bits(a3)};
+          *reinterpret_cast<uint4*>(Sh + nrows * a.W_in * a.cs0 + idx) =
+              uint4{h2_bits(b0), h2_bits(b1), h2_bits(b2), h2_bits(b3)};
+        }
+      }
+    }
+    int hin = rows_in, win = a.W_in;
+    if (a.im2col) {
+      // expand stage 0's taps: position (g, y, x) of its OUTPUT holds k = (dh kw + dw) C + ci
+      __syncthreads();
+      const int ho = hin - S0.kh + 1;
+      const int K0 = S0.kh * S0.kw * C, K8 = (K0 + 7) & ~7;
+      const float* R = reinterpret_cast<const float*>(Yb);
+      _Float16* Ih = reinterpret_cast<_Float16*>(Xb);
+      _Float16* Il = Ih + G * ho * wo0 * a.cs0;
+      for (int prow = mi.t_row; prow < G * ho; prow += mi.rpp)
+      for (int x = mi.t_u; x < wo0; x += mi.u_step) {
+        const int g = prow / ho, y = prow - g * ho;
+        const float* base = R + ((g * rows_in + y) * win + x) * C;
+        _Float16* dh_ = Ih + (prow * wo0 + x) * a.cs0;
+        _Float16* dl_ = Il + (prow * wo0 + x) * a.cs0;
+        int dh = 0, dw = 0, ci = 0;
+        for (int k = 0; k < K8; k += 2) {
+          float v[2];
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            v[t] = (k + t < K0) ? base[(dh * win + dw) * C + ci] : 0.f;
+            if (++ci == C) {
+              ci = 0;
+              if (++dw == S0.kw) {
+                dw = 0;
+                ++dh;
+              }
+            }
+          }
+          h2 hh, ll;
+          split2(v[0], v[1], hh, ll);
+          *reinterpret_cast<uint32_t*>(dh_ + k) = h2_bits(hh);
+          *reinterpret_cast<uint32_t*>(dl_ + k) = h2_bits(ll);
+        }
+      }
+    }
+
+    // 2) the chain's convs, ping-ponging between X and Y
+    unsigned char* cur = Xb;
+    unsigned char* nxt = Yb;
+    for (int s = 0; s < a.n_stages; ++s) {
+      const XStage S = a.st[s];
+      const int ho = hin - S.kh + 1, wo = win - S.kw + 1;
+      const bool i2c = a.im2col && s == 0;
+      const int hA = i2c ? ho : hin, wA = i2c ? wo : win;
+      const int M = G * ho * wo;
+      __syncthreads();  // stage input complete
+      const _Float16* Xh = reinterpret_cast<const _Float16*>(cur);
+      const _Float16* Xl = Xh + G * hA * wA * S.cs_in;
+      _Float16* Yh = reinterpret_cast<_Float16*>(nxt);
+      _Float16* Yl = Yh + M * S.cs_out;
+      const _Float16* Wst = WG ? a.wblob + S.w_off : Wl + S.w_off;
+      const int* kts = kt + S.kt_off;
+      const float* bs = Bl + S.b_off;
+      // RB x NB tiles of two 16-register accumulators: keep RB * NB <= 3 (2 waves / SIMD)
+      if (NBMAX >= 3 && S.nblk == 3)
+        xstage<3, 1>(Xh, Xl, Yh, Yl, Wst, kts, bs, M, hA, wA, ho, wo, S, lane, wave);
+      else if (NBMAX >= 2 && S.nblk == 2)
+        xstage<2, 1>(Xh, Xl, Yh, Yl, Wst, kts, bs, M, hA, wA, ho, wo, S, lane, wave);
+      else
+        xstage<1, 2>(Xh, Xl, Yh, Yl, Wst, kts, bs, M, hA, wA, ho, wo, S, lane, wave);
+      unsigned char* t = cur;
+      cur = nxt;
+      nxt = t;
+      hin = ho;
+      win = wo;
+    }
+    __syncthreads();
+
+    // 3) store the band (max-pooled on the fly), hi + 2^-11 lo back to f32
+    const int cso = a.st[a.n_stages - 1].cs_out;
+    const _Float16* Oh = reinterpret_cast<const _Float16*>(cur);
+    const _Float16* Ol = Oh + G * hin * win * cso;
+    const int units = a.W_out * a.C_out / cu;
+    for (int orow = mo.t_row; orow < G * orows; orow += mo.rpp) {
+      const int g = orow / orows, r = orow - g * orows;
+      float* drow = a.out + (img0 + g) * a.out_img_stride + static_cast<int64_t>(orow0 + r) * a.W_out * a.C_out;
+      for (int u = mo.t_u; u < units; u += mo.u_step) {
+        const int w = (mo.u_step == units) ? o_w : u / (a.C_out / cu);
+        const int c = (mo.u_step == units) ? o_c : (u - w * (a.C_out / cu)) * cu;
+        const int base = ((g * hin + r * a.out_ph) * win + w * a.out_pw) * cso + c;
+        if (a.vec_out) {
+          float4 v;
+          for (int i = 0; i < a.out_ph; ++i)
+            for (int j = 0; j < a.out_pw; ++j) {
+              const int q = base + (i * win + j) * cso;
+              const uint2 hb = *reinterpret_cast<const uint2*>(Oh + q);
+              const uint2 lb = *reinterpret_cast<const uint2*>(Ol + q);
+              const h2 h0 = __builtin_bit_cast(h2, hb.x), h1 = __builtin_bit_cast(h2, hb.y);
+              const h2 l0 = __builtin_bit_cast(h2, lb.x), l1 = __builtin_bit_cast(h2, lb.y);
+              const float4 t{static_cast<float>(h0.x) + static_cast<float>(l0.x) * kLoInv,
+                             static_cast<float>(h0.y) + static_cast<float>(l0.y) * kLoInv,
+                             static_cast<float>(h1.x) + static_cast<float>(l1.x) * kLoInv,
+                             static_cast<float>(h1.y) + static_cast<float>(l1.y) * kLoInv};
+              if (i == 0 && j == 0)
+                v = t;
+              else
+                v = float4{nan_max(v.x, t.x), nan_max(v.y, t.y), nan_max(v.z, t.z), nan_max(v.w, t.w)};
+            }
+          *reinterpret_cast<float4*>(drow + w * a.C_out + c) = v;
+        } else {
+          float v = 0.f;
+          for (int i = 0; i < a.out_ph; ++i)
+            for (int j = 0; j < a.out_pw; ++j) {
+              const int q = base + (i * win + j) * cso;
+              const float t = static_cast<float>(Oh[q]) + static_cast<float>(Ol[q]) * kLoInv;
+              v = (i == 0 && j == 0) ? t : nan_max(v, t);
+            }
+          drow[w * a.C_out + c] = v;
+        }
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ host ----
 
 struct OpInfo {
@@ -247,9 +634,12 @@ using KernelFn = void (*)(ChainArgs);
 
 struct ChainPlan {
   ChainArgs args{};
+  bool split = false;        // split-f16 kernel (XArgs x) instead of the exact one
+  XArgs x{};
   int nb = 1;
   bool wg = false;
   KernelFn fn = nullptr;
+  void (*xfn)(XArgs) = nullptr;
   size_t lds_bytes = 0;
   float* d_blob = nullptr;
   int src_buf = -1;          // -1: the call's input, else workspace buffer index
@@ -293,6 +683,7 @@ struct hbk_embed_plan {
   int n_prefix = 0;
   int seq_frames = 0;
   int split_stride = 1;
+  bool split_f16 = true;
   double prefix_macs = 0, tail_macs = 0;
   hbk::Program clip_prog, win_prog;
 };
@@ -300,11 +691,259 @@ struct hbk_embed_plan {
 namespace hbk {
 namespace {
 
+// fp16 elements per position for c channels: rounded up to 8, with an odd
+// number of 16-B groups (conflict-free ds_read_b128 over consecutive positions).
+inline int x_cs(int c) {
+  int cs = (c + 7) & ~7;
+  if ((cs / 8) % 2 == 0) cs += 8;
+  return cs;
+}
+
+using XKernelFn = void (*)(XArgs);
+
+template <int NBMAX, bool WG>
+XKernelFn xkernel_for() {
+  return conv_chain_x3_kernel<NBMAX, WG>;
+}
+
+XKernelFn pick_xkernel(int nb, bool wg) {
+  switch (nb) {
+    case 1: return wg ? xkernel_for<1, true>() : xkernel_for<1, false>();
+    case 2: return wg ? xkernel_for<2, true>() : xkernel_for<2, false>();
+    case 3: return wg ? xkernel_for<3, true>() : xkernel_for<3, false>();
+    default: return nullptr;
+  }
+}
+
+// Split-f16 layout of one chain whose source / pooling fields are already in
+// `a`: packs the fp16 weight planes, biases and group-offset tables, and picks
+// images-per-task and band for the LDS budget.
+int layout_split(const std::vector<OpInfo>& ops, const std::vector<int>& stage_ops, Dims d,
+                 const ChainArgs& a, ChainPlan& cp, Dims& od_out) {
+  XArgs& x = cp.x;
+  x.ipc = a.ipc;
+  for (int k = 0; k < kMaxWin; ++k) x.row_off[k] = a.row_off[k];
+  x.src_clip_stride = a.src_clip_stride;
+  x.src_row_stride = a.src_row_stride;
+  x.C_src = a.C_src;
+  x.in_ph = a.in_ph;
+  x.in_pw = a.in_pw;
+  x.W_in = a.W_in;
+  x.out_ph = a.out_ph;
+  x.out_pw = a.out_pw;
+  x.n_stages = static_cast<int>(stage_ops.size());
+  x.shrink = 0;
+  x.im2col = (d.c % 8) != 0;
+
+  std::vector<_Float16> wb;  // hi/lo planes per stage
+  std::vector<float> bb;
+  std::vector<int> kt;
+  int cin = d.c, h = d.h, w = d.w, nbmax = 1;
+  double macs = 0;
+  for (int s = 0; s < x.n_stages; ++s) {
+    const OpInfo& op = ops[stage_ops[s]];
+    if (op.cin != cin) {
+      set_error("hbk: graph channel mismatch at op %d (%d != %d)", stage_ops[s], op.cin, cin);
+      return HBK_ERR_ARG;
+    }
+    XStage& S = x.st[s];
+    S.kh = op.kh;
+    S.kw = op.kw;
+    S.cin = op.cin;
+    S.cout = op.cout;
+    S.coutr = (op.cout + 7) & ~7;
+    S.act = op.act;
+    S.alpha = op.alpha;
+    const bool i2c = x.im2col && s == 0;
+    const int K0 = op.kh * op.kw * op.cin;
+    const int cin8 = (op.cin + 7) & ~7;
+    const int groups = i2c ? (K0 + 7) / 8 : op.kh * op.kw * cin8 / 8;
+    S.cs_in = i2c ? x_cs(K0) : x_cs(op.cin);
+    S.cs_out = x_cs(op.cout);
+    S.ksteps = (groups + 1) / 2;
+    S.nblk = (op.cout + 31) / 32;
+    nbmax = std::max(nbmax, S.nblk);
+    S.wrow = S.ksteps * 16 + 8;
+    const int wo_in = w;  // this stage's input width (group offsets)
+    h -= op.kh - 1;
+    w -= op.kw - 1;
+    x.shrink += op.kh - 1;
+    if (h <= 0 || w <= 0) {
+      set_error("hbk: graph collapses the image at op %d", stage_ops[s]);
+      return HBK_ERR_ARG;
+    }
+    macs += double(h) * w * op.cout * K0;
+    // weights [n][k] (k = group * 8 + j), hi then lo plane
+    const int rows = S.nblk * 32;
+    S.w_off = static_cast<int>(wb.size());
+    S.w_lo = rows * S.wrow;
+    wb.resize(wb.size() + size_t(2) * rows * S.wrow, static_cast<_Float16>(0.f));
+    for (int n = 0; n < op.cout; ++n)
+      for (int k = 0; k < S.ksteps * 16; ++k) {
+        const int g = k / 8, j = k - g * 8;
+        int src = -1;  // index into HWIO weights (k' = tap * cin + ci)
+        if (i2c) {
+          if (k < K0) src = k;
+        } else if (g < groups) {
+          const int tap = g / (cin8 / 8), ci = (g - tap * (cin8 / 8)) * 8 + j;
+          if (ci < op.cin) src = tap * op.cin + ci;
+        }
+        if (src < 0) continue;
+        const float v = op.w[size_t(src) * op.cout + n];
+        const _Float16 hi = static_cast<_Float16>(v);
+        wb[S.w_off + size_t(n) * S.wrow + k] = hi;
+        wb[S.w_off + S.w_lo + size_t(n) * S.wrow + k] =
+            static_cast<_Float16>((v - static_cast<float>(hi)) * kLoScale);
+      }
+    S.b_off = static_cast<int>(bb.size());
+    for (int n = 0; n < rows; ++n) bb.push_back(n < op.cout ? op.b[n] : 0.f);
+    // group offsets (fp16 elements into the stage's input tensor); pad groups read offset 0
+    S.kt_off = static_cast<int>(kt.size());
+    for (int g = 0; g < 2 * S.ksteps; ++g) {
+      int v = 0;
+      if (g < groups) {
+        if (i2c) {
+          v = g * 8;
+        } else {
+          const int tap = g / (cin8 / 8), cg = g - tap * (cin8 / 8);
+          const int dh = tap / op.kw, dw = tap - dh * op.kw;
+          v = (dh * wo_in + dw) * S.cs_in + cg * 8;
+        }
+      }
+      kt.push_back(v);
+    }
+    cin = op.cout;
+  }
+  x.cs0 = x.st[0].cs_in;
+  cp.nb = nbmax;
+  const Dims od{h / x.out_ph, w / x.out_pw, cin};
+  if (od.h <= 0 || od.w <= 0) {
+    set_error("hbk: pooling collapses the image");
+    return HBK_ERR_ARG;
+  }
+  x.H_out = od.h;
+  x.W_out = od.w;
+  x.C_out = od.c;
+  x.out_img_stride = int64_t(od.h) * od.w * od.c;
+  x.kt_n = static_cast<int>(kt.size());
+  while (wb.size() % 8) wb.push_back(static_cast<_Float16>(0.f));
+
+  // LDS: tensor t (stage t input; t = n_stages: last output) alternates X / Y
+  auto region_bytes = [&](int G, int band, int64_t& xb, int64_t& yb) {
+    const int n = x.n_stages;
+    std::vector<int> rows(n + 1), wid(n + 1);
+    rows[n] = band * x.out_ph;
+    wid[0] = d.w;
+    for (int s = 0; s < n; ++s) wid[s + 1] = wid[s] - (x.st[s].kw - 1);
+    for (int s = n - 1; s >= 0; --s) rows[s] = rows[s + 1] + x.st[s].kh - 1;
+    xb = yb = 0;
+    for (int t = 0; t <= n; ++t) {
+      int64_t bytes;
+      if (t == 0 && x.im2col)  // stage 0 input = im2col tensor at its output geometry
+        bytes = int64_t(G) * rows[1] * wid[1] * x.st[0].cs_in * 4;
+      else
+        bytes = int64_t(G) * rows[t] * wid[t] * (t == 0 ? x.st[0].cs_in : x.st[t - 1].cs_out) * 4;
+      int64_t& r = (t % 2 == 0) ? xb : yb;
+      r = std::max(r, bytes);
+    }
+    if (x.im2col) yb = std::max(yb, int64_t(G) * rows[0] * wid[0] * d.c * 4);  // raw f32 rows
+    xb = (xb + 15) & ~int64_t(15);
+    yb = (yb + 15) & ~int64_t(15);
+  };
+  const int64_t w_bytes = int64_t(wb.size()) * 2, k_bytes = (int64_t(kt.size()) * 4 + 15) & ~int64_t(15);
+  const int64_t b_bytes = int64_t(bb.size()) * 4;  // multiple of 128
+  auto lds_total = [&](int G, int band, bool resident) {
+    int64_t xb, yb;
+    region_bytes(G, band, xb, yb);
+    return xb + yb + (resident ? w_bytes : 0) + b_bytes + k_bytes;
+  };
+  // MACs computed per output row of the whole image for a band of b rows
+  // (halo rows recomputed by every band): useful / computed = efficiency.
+  auto efficiency = [&](int b) {
+    const int n = x.n_stages, nb = (od.h + b - 1) / b;
+    double useful = 0, done = 0;
+    int rows_b = b * x.out_ph, rows_full = od.h * x.out_ph;
+    for (int s = n - 1; s >= 0; --s) {
+      const XStage& S = x.st[s];
+      int wo = d.w;
+      for (int q = 0; q <= s; ++q) wo -= x.st[q].kw - 1;
+      const double per_row = double(wo) * S.cout * S.kh * S.kw * S.cin;
+      useful += per_row * rows_full;
+      done += per_row * rows_b * nb;
+      rows_b += S.kh - 1;
+      rows_full += S.kh - 1;
+    }
+    return useful / done;
+  };
+  auto best_band = [&](bool res) {
+    for (int b = od.h; b >= 1; --b)
+      if (lds_total(1, b, res) <= kLdsBudget) return b;
+    return 0;
+  };
+  // resident weights unless they cost more than 5 % of the work in halo rows
+  const int band_r = lds_total(1, 1, true) <= kLdsBudget ? best_band(true) : 0;
+  const int band_g = best_band(false);
+  const bool resident = band_r > 0 && (band_g == 0 || efficiency(band_r) >= 0.95 * efficiency(band_g));
+  int band = resident ? band_r : band_g, G = 1;
+  if (band == 0) {
+    set_error("hbk: one output row of a chain does not fit in LDS");
+    return HBK_ERR_UNSUPPORTED;
+  }
+  if (band == od.h)
+    while (G < 64 && lds_total(G * 2, band, resident) <= kLdsBudget) G *= 2;
+  x.G = G;
+  x.band = band;
+  x.n_bands = (od.h + band - 1) / band;
+  int64_t xb, yb;
+  region_bytes(G, band, xb, yb);
+  x.lds_x = 0;
+  x.lds_y = static_cast<int>(xb);
+  x.lds_w = static_cast<int>(xb + yb);
+  x.lds_b = x.lds_w + static_cast<int>(resident ? w_bytes : 0);
+  x.lds_k = x.lds_b + static_cast<int>(b_bytes);
+  x.w_halfs = resident ? static_cast<int>(wb.size()) : 0;
+  x.b_floats = static_cast<int>(bb.size());
+  x.vec_out = od.c % 4 == 0;  // cleared at launch for an unaligned output
+  cp.lds_bytes = size_t(x.lds_k + k_bytes);
+  cp.wg = !resident;
+  cp.split = true;
+  cp.xfn = pick_xkernel(nbmax, cp.wg);
+  if (!cp.xfn) {
+    set_error("hbk: conv with more than 96 output channels is not supported");
+    return HBK_ERR_UNSUPPORTED;
+  }
+  // device blob: weights (fp16), biases (f32), group offsets (int)
+  const size_t wsz = wb.size() * 2, bsz = ((bb.size() * 4 + 15) & ~size_t(15)), ksz = kt.size() * 4;
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(&cp.d_blob), wsz + bsz + ksz);
+  if (e != hipSuccess) return hip_error(e, "hipMalloc chain weights");
+  unsigned char* base = reinterpret_cast<unsigned char*>(cp.d_blob);
+  e = hipMemcpy(base, wb.data(), wsz, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(base + wsz, bb.data(), bb.size() * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(base + wsz + bsz, kt.data(), ksz, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_error(e, "copy chain weights");
+  x.wblob = reinterpret_cast<const _Float16*>(base);
+  x.bblob = reinterpret_cast<const float*>(base + wsz);
+  x.ktab = reinterpret_cast<const int*>(base + wsz + bsz);
+  if (cp.lds_bytes > 64 * 1024) {
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(cp.xfn),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, int(cp.lds_bytes));
+    if (e != hipSuccess) return hip_error(e, "hipFuncSetAttribute(max dynamic LDS)");
+  }
+  cp.macs_per_img = macs;
+  od_out = od;
+  if (getenv("HBK_DEBUG_EMBED"))
+    fprintf(stderr, "hbk split chain: %d stages, in %dx%dx%d (pool %dx%d, im2col %d) -> %dx%dx%d (pool %dx%d); "
+            "G %d band %d/%d (eff %.3f), weights %s %lld B, LDS %zu B, nb %d\n",
+            x.n_stages, d.h, d.w, d.c, x.in_ph, x.in_pw, x.im2col, od.h, od.w, od.c, x.out_ph, x.out_pw, G,
+            band, od.h, efficiency(band), resident ? "LDS" : "global", (long long)w_bytes, cp.lds_bytes, nbmax);
+  return HBK_OK;
+}
+
 // Builds the chains for ops [o0, o1) applied to images of dims `in`, reading
 // image i from row_off[i % ipc] of source clip i / ipc.
 int build_segment(const std::vector<OpInfo>& ops, int o0, int o1, Dims in, int ipc,
                   const std::vector<int>& row_off, int64_t src_clip_floats, int src_row_floats,
-                  int first_src_buf, Program& prog, std::vector<Dims>* out_dims_per_chain) {
+                  int first_src_buf, bool split, Program& prog, std::vector<Dims>* out_dims_per_chain) {
   int i = o0;
   Dims cur = in;
   int src_buf = first_src_buf;
@@ -343,6 +982,19 @@ int build_segment(const std::vector<OpInfo>& ops, int o0, int o1, Dims in, int i
       a.out_ph = ops[i].kh;
       a.out_pw = ops[i].kw;
       ++i;
+    }
+    if (split) {
+      Dims od;
+      const int rc = layout_split(ops, stage_ops, d, a, cp, od);
+      if (rc) return rc;
+      cp.src_buf = src_buf;
+      cp.out_floats = cp.x.out_img_stride * (first ? ipc : 1);
+      prog.chains.push_back(cp);
+      if (out_dims_per_chain) out_dims_per_chain->push_back(od);
+      src_buf = -2;
+      cur = od;
+      first = false;
+      continue;
     }
     // stages
     int nb = 1;
@@ -510,6 +1162,24 @@ int run_program(const Program& prog, const float* in, int64_t n_units, int64_t i
     float* bufs[2] = {ws, ws + chunk * buf_unit_floats[0]};
     for (size_t k = 0; k < prog.chains.size(); ++k) {
       const ChainPlan& c = prog.chains[k];
+      if (c.split) {
+        XArgs x = c.x;
+        if (c.src_buf < 0) {
+          x.in = in + u0 * in_unit_stride;
+          x.src_clip_stride = in_unit_stride;
+        } else {
+          x.in = bufs[c.src_buf];
+        }
+        x.out = c.dst_buf < 0 ? out + u0 * out_unit_floats : bufs[c.dst_buf];
+        if ((reinterpret_cast<uintptr_t>(x.out) & 15) || (x.out_img_stride & 3)) x.vec_out = 0;
+        x.n_img = nu * imgs_per_unit[k];
+        const int64_t tasks = ((x.n_img + x.G - 1) / x.G) * x.n_bands;
+        const int64_t blocks = std::min<int64_t>(tasks, persistent_blocks(2));
+        if (blocks <= 0) continue;
+        hipLaunchKernelGGL(c.xfn, dim3(unsigned(blocks)), dim3(kXThreads), c.lds_bytes, stream, x);
+        HBK_LAUNCH_CHECK("conv_chain_x3_kernel");
+        continue;
+      }
       ChainArgs a = c.args;
       if (c.src_buf < 0) {
         a.in = in + u0 * in_unit_stride;
@@ -536,9 +1206,16 @@ extern "C" {
 
 int hbk_embed_plan_create(const hbk_graph_op* ops, int32_t n_ops, int32_t in_h, int32_t in_w,
                           const int32_t* win_start, int32_t n_win, hbk_embed_plan** plan) {
+  return hbk_embed_plan_create_ex(ops, n_ops, in_h, in_w, win_start, n_win, HBK_PREC_SPLIT_F16, plan);
+}
+
+int hbk_embed_plan_create_ex(const hbk_graph_op* ops, int32_t n_ops, int32_t in_h, int32_t in_w,
+                             const int32_t* win_start, int32_t n_win, int32_t precision,
+                             hbk_embed_plan** plan) {
   using namespace hbk;
   if (!plan) return arg_error("plan is NULL");
   *plan = nullptr;
+  if (precision != HBK_PREC_SPLIT_F16 && precision != HBK_PREC_EXACT_F32) return arg_error("unknown precision");
   if (!ops || n_ops <= 0) return arg_error("empty graph");
   if (in_h <= 0 || in_w <= 0) return arg_error("bad window size");
   if (!win_start || n_win <= 0 || n_win > kMaxWin) return arg_error("n_win must be in [1, 32]");
@@ -549,6 +1226,7 @@ int hbk_embed_plan_create(const hbk_graph_op* ops, int32_t n_ops, int32_t in_h, 
   };
   p->in_h = in_h;
   p->in_w = in_w;
+  p->split_f16 = precision == HBK_PREC_SPLIT_F16;
   for (int i = 0; i < n_win; ++i) {
     if (win_start[i] < 0) return fail(arg_error("negative window start"));
     p->starts.push_back(win_start[i]);
@@ -614,7 +1292,7 @@ int hbk_embed_plan_create(const hbk_graph_op* ops, int32_t n_ops, int32_t in_h, 
   {
     std::vector<Dims> od;
     rc = build_segment(p->ops, 0, split, Dims{p->seq_frames, in_w, 1}, 1, {0}, 0, in_w, -1,
-                       p->clip_prog, &od);
+                       p->split_f16, p->clip_prog, &od);
     if (rc) return fail(rc);
     const Dims pre = od.back();
     // window rows at the split, for one window
@@ -625,7 +1303,8 @@ int hbk_embed_plan_create(const hbk_graph_op* ops, int32_t n_ops, int32_t in_h, 
       if (r + wd.h > pre.h) return fail(arg_error("window start beyond the frame sequence"));
     const size_t n_pre = p->clip_prog.chains.size();
     rc = build_segment(p->ops, split, n_ops, Dims{wd.h, wd.w, wd.c}, n_win, roff,
-                       int64_t(pre.h) * pre.w * pre.c, pre.w * pre.c, 0, p->clip_prog, nullptr);
+                       int64_t(pre.h) * pre.w * pre.c, pre.w * pre.c, 0, p->split_f16, p->clip_prog,
+                       nullptr);
     if (rc) return fail(rc);
     for (size_t k = 0; k < p->clip_prog.chains.size(); ++k) {
       if (k < n_pre) p->prefix_macs += p->clip_prog.chains[k].macs_per_img;
@@ -637,7 +1316,7 @@ int hbk_embed_plan_create(const hbk_graph_op* ops, int32_t n_ops, int32_t in_h, 
   {
     std::vector<Dims> od;
     rc = build_segment(p->ops, 0, n_ops, Dims{in_h, in_w, 1}, 1, {0}, int64_t(in_h) * in_w, in_w,
-                       -1, p->win_prog, &od);
+                       -1, p->split_f16, p->win_prog, &od);
     if (rc) return fail(rc);
     assign_buffers(p->win_prog, 1);
   }
@@ -680,9 +1359,11 @@ void program_geometry(const Program& prog, bool clip_path, int n_win, std::vecto
   bool tail = false;
   for (size_t k = 0; k < prog.chains.size(); ++k) {
     const ChainPlan& c = prog.chains[k];
-    if (clip_path && c.args.ipc > 1) tail = true;
+    const int ipc = c.split ? c.x.ipc : c.args.ipc;
+    const int64_t ois = c.split ? c.x.out_img_stride : c.args.out_img_stride;
+    if (clip_path && ipc > 1) tail = true;
     imgs.push_back(tail ? n_win : 1);
-    if (c.dst_buf >= 0) bufs[c.dst_buf] = std::max(bufs[c.dst_buf], c.args.out_img_stride * imgs.back());
+    if (c.dst_buf >= 0) bufs[c.dst_buf] = std::max(bufs[c.dst_buf], ois * imgs.back());
   }
 }
 

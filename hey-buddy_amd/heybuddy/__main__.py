@@ -1,0 +1,197 @@
+"""``heybuddy train`` on the MI355X hot path (reference src/python/heybuddy/__main__.py:171-429).
+
+Same command and option names for the hot-path settings. The data sources the
+reference downloads or synthesizes with TTS (Piper positives and adversarial
+phrases, HF background-noise and impulse-response datasets, the hosted 72 GB
+negative embeddings) are unavailable offline, so this command builds them
+synthetically on the device (heybuddy.synthetic) and runs the reference's
+pipeline on them: augment (noise mix + reverb) -> featurize (mel + embedding)
+-> 3-stage classifier training with validation and testing. Under
+torch.distributed.run every rank featurizes its shard of the clips, the
+embedding pools are all-gathered, and training is data-parallel with one
+gradient all-reduce per step.
+"""
+from __future__ import annotations
+
+import os
+import re
+from typing import List, Optional
+
+import click
+import torch
+
+from heybuddy.constants import *  # noqa: F401,F403
+from heybuddy.constants import (DEFAULT_ACTIVATION_THRESHOLD, DEFAULT_ADVERSARIAL_BATCH_SIZE,
+                                DEFAULT_ADVERSARIAL_SAMPLES, DEFAULT_AUGMENT_BACKGROUND_NOISE_MAX_SNR_DB,
+                                DEFAULT_AUGMENT_BACKGROUND_NOISE_MIN_SNR_DB,
+                                DEFAULT_AUGMENT_BACKGROUND_NOISE_PROB, DEFAULT_AUGMENT_REVERB_PROB,
+                                DEFAULT_CHECKPOINT_STEPS, DEFAULT_HIGH_LOSS_THRESHOLD, DEFAULT_LAYER_DIM,
+                                DEFAULT_LAYERS, DEFAULT_LEARNING_RATE, DEFAULT_LOGGING_STEPS,
+                                DEFAULT_NEGATIVE_BATCH_SIZE, DEFAULT_NEGATIVE_WEIGHT,
+                                DEFAULT_POSITIVE_BATCH_SIZE, DEFAULT_POSITIVE_SAMPLES, DEFAULT_STAGES,
+                                DEFAULT_STEPS, DEFAULT_TARGET_FALSE_POSITIVE_RATE,
+                                DEFAULT_TESTING_ADVERSARIAL_SAMPLES, DEFAULT_TESTING_POSITIVE_SAMPLES,
+                                DEFAULT_USE_GATING, DEFAULT_USE_HALF_LAYERS, DEFAULT_VALIDATION_SAMPLES,
+                                DEFAULT_VALIDATION_STEPS)
+
+
+def safe_name(name: str) -> str:
+    """util/string_util.py:145-151: lower-case, non-alphanumerics -> '_'."""
+    return re.sub(r"[^a-z0-9]+", "_", name.lower()).strip("_")
+
+
+@click.group()
+def main() -> None:
+    """hey-buddy (MI355X hot path)."""
+
+
+def build_embeddings(n: int, seed: int, device: torch.device, augmenter=None, chunk: int = 65536,
+                     kind: str = "positive", phrase: str = "") -> torch.Tensor:
+    """Synthetic clips of one class -> [n, 16, 96] embeddings on the device,
+    featurized (and augmented, if given) in chunks, sharded over the ranks.
+    positive: phrase_clips(phrase); adversarial: random tone bursts;
+    negative: the same at 0.3x level."""
+    from heybuddy import distributed as hd
+    from heybuddy.embeddings import SpeechEmbeddings
+    from heybuddy.synthetic import phrase_clips, synthetic_clips
+    rank, world = hd.world()
+    lo, hi = hd.clip_range(n, rank, world)
+    se = SpeechEmbeddings(device_id=device.index)
+    parts = []
+    for s in range(lo, hi, chunk):
+        m = min(chunk, hi - s)
+        if kind == "positive":
+            clips = phrase_clips(phrase, m, seed=seed * 7919 + s, device=device)
+        else:
+            clips = synthetic_clips(m, seed=seed * 7919 + s, device=device)
+        if kind == "negative":  # noise-like negatives: random tones at low level, no burst
+            clips.mul_(0.3)
+        if augmenter is not None:
+            clips = augmenter(clips)
+        parts.append(se.featurize(clips))
+    local = torch.cat(parts) if parts else torch.empty((0, 16, 96), device=device)
+    if world == 1:
+        return local
+    sizes = [hd.clip_range(n, r, world) for r in range(world)]
+    buf = [torch.empty((b - a, 16, 96), device=device) for a, b in sizes]
+    torch.distributed.all_gather(buf, local.contiguous())
+    return torch.cat(buf)
+
+
+@main.command()
+@click.argument("phrase", type=str, nargs=1)
+@click.option("--additional-phrase", type=str, default=None, multiple=True)
+@click.option("--wandb-entity", type=str, default=None)
+@click.option("--perceptron", "architecture", flag_value="perceptron", default=True)
+@click.option("--transformer", "architecture", flag_value="transformer")
+@click.option("--use-half-layers/--no-use-half-layers", default=DEFAULT_USE_HALF_LAYERS)
+@click.option("--use-gating/--no-use-gating", default=DEFAULT_USE_GATING)
+@click.option("--layer-dim", type=int, default=DEFAULT_LAYER_DIM, show_default=True)
+@click.option("--num-layers", type=int, default=DEFAULT_LAYERS, show_default=True)
+@click.option("--steps", type=int, default=DEFAULT_STEPS, show_default=True)
+@click.option("--stages", type=int, default=DEFAULT_STAGES, show_default=True)
+@click.option("--threshold", type=float, default=DEFAULT_ACTIVATION_THRESHOLD, show_default=True)
+@click.option("--learning-rate", type=float, default=DEFAULT_LEARNING_RATE, show_default=True)
+@click.option("--high-loss-threshold", type=float, default=DEFAULT_HIGH_LOSS_THRESHOLD, show_default=True)
+@click.option("--target-false-positive-rate", type=float, default=DEFAULT_TARGET_FALSE_POSITIVE_RATE, show_default=True)
+@click.option("--dynamic-negative-weight/--no-dynamic-negative-weight", default=True)
+@click.option("--negative-weight", type=float, default=DEFAULT_NEGATIVE_WEIGHT, show_default=True)
+@click.option("--augmentation-background-noise-prob", type=float, default=DEFAULT_AUGMENT_BACKGROUND_NOISE_PROB, show_default=True)
+@click.option("--augmentation-background-noise-min-snr-db", type=float, default=DEFAULT_AUGMENT_BACKGROUND_NOISE_MIN_SNR_DB, show_default=True)
+@click.option("--augmentation-background-noise-max-snr-db", type=float, default=DEFAULT_AUGMENT_BACKGROUND_NOISE_MAX_SNR_DB, show_default=True)
+@click.option("--augmentation-reverb-prob", type=float, default=DEFAULT_AUGMENT_REVERB_PROB, show_default=True)
+@click.option("--logging-steps", type=int, default=DEFAULT_LOGGING_STEPS, show_default=True)
+@click.option("--validation-steps", type=int, default=DEFAULT_VALIDATION_STEPS, show_default=True)
+@click.option("--checkpoint-steps", type=int, default=DEFAULT_CHECKPOINT_STEPS, show_default=True)
+@click.option("--positive-samples", type=int, default=DEFAULT_POSITIVE_SAMPLES, show_default=True)
+@click.option("--adversarial-samples", type=int, default=DEFAULT_ADVERSARIAL_SAMPLES, show_default=True)
+@click.option("--negative-samples", type=int, default=200_000, show_default=True,
+              help="Synthetic negatives featurized in place of the hosted precalculated sets.")
+@click.option("--positive-batch-size", type=int, default=DEFAULT_POSITIVE_BATCH_SIZE, show_default=True)
+@click.option("--negative-batch-size", type=int, default=DEFAULT_NEGATIVE_BATCH_SIZE, show_default=True)
+@click.option("--adversarial-batch-size", type=int, default=DEFAULT_ADVERSARIAL_BATCH_SIZE, show_default=True)
+@click.option("--validation-samples", type=int, default=DEFAULT_VALIDATION_SAMPLES, show_default=True)
+@click.option("--testing-positive-samples", type=int, default=DEFAULT_TESTING_POSITIVE_SAMPLES, show_default=True)
+@click.option("--testing-adversarial-samples", type=int, default=DEFAULT_TESTING_ADVERSARIAL_SAMPLES, show_default=True)
+@click.option("--checkpoint-dir", type=str, default="./checkpoints", show_default=True)
+@click.option("--seed", type=int, default=0, show_default=True)
+@click.option("--resume/--no-resume", default=False)
+@click.option("--debug/--no-debug", default=False)
+def train(phrase: str, additional_phrase: List[str], wandb_entity: Optional[str], architecture: str,
+          use_half_layers: bool, use_gating: bool, layer_dim: int, num_layers: int, steps: int, stages: int,
+          threshold: float, learning_rate: float, high_loss_threshold: float,
+          target_false_positive_rate: float, dynamic_negative_weight: bool, negative_weight: float,
+          augmentation_background_noise_prob: float, augmentation_background_noise_min_snr_db: float,
+          augmentation_background_noise_max_snr_db: float, augmentation_reverb_prob: float,
+          logging_steps: int, validation_steps: int, checkpoint_steps: int, positive_samples: int,
+          adversarial_samples: int, negative_samples: int, positive_batch_size: int,
+          negative_batch_size: int, adversarial_batch_size: int, validation_samples: int,
+          testing_positive_samples: int, testing_adversarial_samples: int, checkpoint_dir: str, seed: int,
+          resume: bool, debug: bool) -> None:
+    """Trains a wake word detection model (synthetic data on the device)."""
+    import numpy as np
+    from heybuddy import distributed as hd
+    from heybuddy.dataset.augmented import BatchAugmenter
+    from heybuddy.dataset.training import DevicePool, TrainingDatasetIterator, WakeWordTrainingDatasetIterator
+    from heybuddy.synthetic import impulse_responses, noise_bank
+    from heybuddy.trainer import WakeWordTrainer
+    from heybuddy.util import logger
+
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) > 1 and not torch.distributed.is_initialized():
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", torch.cuda.current_device())
+    torch.manual_seed(seed)
+    np.random.seed(seed)
+    if additional_phrase:
+        logger.warning("additional phrases need TTS; the synthetic positives stand in for every phrase")
+    if wandb_entity:
+        logger.warning("wandb logging is outside the MI355X hot path; ignored")
+    aug = BatchAugmenter(noise_bank(64, seed=seed + 11, device=device),
+                         impulse_responses(32, seed=seed + 12, device=device), device=device,
+                         batch_size=128, background_noise_prob=augmentation_background_noise_prob,
+                         background_noise_min_snr_db=augmentation_background_noise_min_snr_db,
+                         background_noise_max_snr_db=augmentation_background_noise_max_snr_db,
+                         reverb_prob=augmentation_reverb_prob)
+    pos = build_embeddings(positive_samples, seed + 1, device, aug, kind="positive", phrase=phrase)
+    adv = build_embeddings(adversarial_samples, seed + 2, device, aug, kind="adversarial")
+    neg = build_embeddings(negative_samples, seed + 3, device, aug, kind="negative").half()
+    vpos = build_embeddings(validation_samples // 10 or 1, seed + 4, device, aug, kind="positive", phrase=phrase)
+    vneg = build_embeddings(validation_samples, seed + 5, device, aug, kind="negative")
+    tpos = build_embeddings(testing_positive_samples, seed + 6, device, aug, kind="positive", phrase=phrase)
+    tadv = build_embeddings(testing_adversarial_samples, seed + 7, device, aug, kind="adversarial")
+    g = torch.Generator(device=device).manual_seed(seed + 99)  # identical batches on every rank
+    half = int(negative_samples * 2 / 3)
+    training = WakeWordTrainingDatasetIterator.default(
+        pos, adv, neg[:half], neg[half:], positive_per_batch=positive_batch_size,
+        adversarial_per_batch=adversarial_batch_size, negative_per_batch=negative_batch_size, generator=g)
+
+    def fixed(xs, ys, bs=1000):
+        x = torch.cat(xs)
+        y = torch.cat(ys)
+        return [(x[i:i + bs], y[i:i + bs]) for i in range(0, x.shape[0], bs)]
+
+    validation = fixed([vpos, vneg], [torch.ones(vpos.shape[0], dtype=torch.int64, device=device),
+                                      torch.zeros(vneg.shape[0], dtype=torch.int64, device=device)])
+    testing = fixed([tpos, tadv], [torch.ones(tpos.shape[0], dtype=torch.int64, device=device),
+                                   torch.zeros(tadv.shape[0], dtype=torch.int64, device=device)])
+    rank, world = hd.world()
+    trainer = WakeWordTrainer(checkpoint_dir=checkpoint_dir, architecture=architecture,
+                              use_half_layers=use_half_layers, use_gating=use_gating, layer_dim=layer_dim,
+                              num_layers=num_layers, device=device)
+    name = safe_name(phrase)
+    if resume:
+        trainer.resume(name)
+    trainer(training=training, validation=validation, testing=testing, activation_threshold=threshold,
+            checkpoint_steps=checkpoint_steps, dynamic_negative_weight=dynamic_negative_weight,
+            high_loss_threshold=high_loss_threshold, learning_rate=learning_rate,
+            max_negative_weight=negative_weight, name=name if rank == 0 else f"{name}_rank{rank}",
+            num_stages=stages, num_steps=steps, target_false_positive_rate=target_false_positive_rate,
+            validation_steps=validation_steps, logging_steps=logging_steps)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

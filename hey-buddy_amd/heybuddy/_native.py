@@ -53,6 +53,8 @@ _PROTOS = {
     "hbk_mel_frames": (_c_int, [_vp, _vp, _c_int64, _c_int64, _c_int64, _vp, _vp]),
     "hbk_embed_plan_create": (_c_int, [_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _vp,
                                        ctypes.c_int32, ctypes.POINTER(_vp)]),
+    "hbk_embed_plan_create_ex": (_c_int, [_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _vp,
+                                          ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(_vp)]),
     "hbk_embed_plan_destroy": (_c_int, [_vp]),
     "hbk_embed_plan_info": (_c_int, [_vp, ctypes.POINTER(ctypes.c_int32),
                                      ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),

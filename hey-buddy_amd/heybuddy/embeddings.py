@@ -25,7 +25,7 @@ import torch
 
 from heybuddy import _native
 from heybuddy.embedding_graph import Graph, se20_graph
-from heybuddy.kernels import EmbedPlan, embed_clips, embed_windows, mel_frames
+from heybuddy.kernels import EmbedPlan, default_embed_precision, embed_clips, embed_windows, mel_frames
 from heybuddy.spectrogram import HOP, MelSpectrogramModel, N_FFT, default_mel_plan
 from heybuddy.util import audio_to_bct_tensor, logger
 
@@ -52,14 +52,16 @@ def set_default_graph(graph: Graph) -> None:
     _EMBED_PLANS.clear()
 
 
-_EMBED_PLANS: Dict[Tuple[int, Tuple[int, ...], int], EmbedPlan] = {}
+_EMBED_PLANS: Dict[Tuple[int, Tuple[int, ...], int, str], EmbedPlan] = {}
 
 
-def embed_plan(device: torch.device, starts: Sequence[int], graph: Optional[Graph] = None) -> EmbedPlan:
+def embed_plan(device: torch.device, starts: Sequence[int], graph: Optional[Graph] = None,
+               precision: Optional[str] = None) -> EmbedPlan:
     graph = default_graph() if graph is None else graph
-    key = (device.index, tuple(starts), id(graph))
+    precision = default_embed_precision() if precision is None else precision
+    key = (device.index, tuple(starts), id(graph), precision)
     if key not in _EMBED_PLANS:
-        _EMBED_PLANS[key] = EmbedPlan(graph, starts=tuple(starts), device=device)
+        _EMBED_PLANS[key] = EmbedPlan(graph, starts=tuple(starts), device=device, precision=precision)
     return _EMBED_PLANS[key]
 
 

@@ -9,6 +9,7 @@ torch op. Nothing here computes on the CPU.
 from __future__ import annotations
 
 import ctypes
+import os
 import itertools
 import threading
 from typing import Dict
@@ -110,16 +111,33 @@ def _aligned_copy(x: torch.Tensor) -> torch.Tensor:
     return buf[:, :t]
 
 
+EMBED_PRECISIONS = {"split": 0, "exact": 1}  # hbk_precision
+
+
+def default_embed_precision() -> str:
+    """HEYBUDDY_EMBED_PRECISION: 'split' (fp16 hi/lo pairs on the f16 MFMA,
+    ~2^-21 relative; default) or 'exact' (f32 MFMA, bitwise fmaf chain)."""
+    p = os.environ.get("HEYBUDDY_EMBED_PRECISION", "split")
+    if p not in EMBED_PRECISIONS:
+        raise ValueError(f"HEYBUDDY_EMBED_PRECISION must be one of {sorted(EMBED_PRECISIONS)}")
+    return p
+
+
 class EmbedPlan:
-    """Device plan of the speech-embedding graph (hbk_embed_plan_create).
+    """Device plan of the speech-embedding graph (hbk_embed_plan_create_ex).
 
     ``graph`` is a heybuddy.embedding_graph.Graph; ``starts`` are the window
-    start frames of the clip path (the reference's 16 windows by default).
+    start frames of the clip path (the reference's 16 windows by default);
+    ``precision`` is 'split' or 'exact' (see include/hbk.h, hbk_precision).
     """
 
-    def __init__(self, graph, starts=None, device: torch.device | int | None = None) -> None:
+    def __init__(self, graph, starts=None, device: torch.device | int | None = None,
+                 precision: str | None = None) -> None:
         from heybuddy.embedding_graph import WINDOW_STARTS, Conv
         self.device = _native.require_device(device)
+        self.precision = default_embed_precision() if precision is None else precision
+        if self.precision not in EMBED_PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(EMBED_PRECISIONS)}")
         self.graph = graph
         self.starts = tuple(WINDOW_STARTS if starts is None else starts)
         ops = (_native.GraphOp * len(graph.ops))()
@@ -138,8 +156,9 @@ class EmbedPlan:
         h, w, _ = graph.in_shape
         handle = ctypes.c_void_p()
         with torch.cuda.device(self.device):
-            check(lib().hbk_embed_plan_create(ops, len(graph.ops), h, w, st, len(self.starts),
-                                              ctypes.byref(handle)), "hbk_embed_plan_create")
+            check(lib().hbk_embed_plan_create_ex(ops, len(graph.ops), h, w, st, len(self.starts),
+                                                 EMBED_PRECISIONS[self.precision], ctypes.byref(handle)),
+                  "hbk_embed_plan_create_ex")
         self._handle = handle
         self._keep = []
         od, npre, nch, sf = (ctypes.c_int32() for _ in range(4))

@@ -85,3 +85,37 @@ def noise_bank(n: int = 64, seed: int = 0, device: torch.device | str = "cpu") -
         x = x / x.pow(2).mean().sqrt() * 0.1
         out.append(x.to(torch.float32).to(device))
     return out
+
+
+def phrase_clips(phrase: str, n: int, length: int = CLIP_SAMPLES, seed: int = 0,
+                 device: torch.device | str = "cpu") -> torch.Tensor:
+    """[n, length] stand-ins for TTS renderings of one phrase: a sequence of
+    4-7 tone "syllables" whose pitches and durations are fixed by the phrase
+    text, rendered per clip with a random onset, tempo (0.85-1.15x), pitch
+    shift (+-5%), gain and 0.01 N(0, 1) noise. Distinct phrases give distinct
+    templates, so a classifier can learn one against synthetic_clips()."""
+    import zlib
+    device = torch.device(device)
+    h = torch.Generator().manual_seed(zlib.crc32(phrase.encode("utf-8")))
+    k = int(torch.randint(4, 8, (1,), generator=h))
+    f0 = torch.rand((k,), generator=h) * 1500.0 + 200.0        # syllable pitch
+    d0 = torch.rand((k,), generator=h) * 0.08 + 0.06           # syllable seconds
+    g = torch.Generator(device=device).manual_seed(seed)
+    t = torch.arange(length, device=device, dtype=torch.float32) / SAMPLE_RATE
+    tempo = torch.rand((n, 1), generator=g, device=device) * 0.3 + 0.85
+    shift = torch.rand((n, 1), generator=g, device=device) * 0.1 + 0.95
+    total = float(d0.sum()) * 1.15
+    onset = torch.rand((n, 1), generator=g, device=device) * max(length / SAMPLE_RATE - total - 0.05, 0.0)
+    gain = torch.rand((n, 1), generator=g, device=device) * 0.3 + 0.2
+    x = torch.zeros((n, length), device=device)
+    start = onset.clone()
+    for j in range(k):
+        dur = float(d0[j]) * tempo
+        u = ((t[None, :] - start) / dur)
+        env = torch.where((u >= 0) & (u <= 1), 0.5 - 0.5 * torch.cos(2 * math.pi * u.clamp(0, 1)),
+                          torch.zeros_like(u))
+        f = float(f0[j]) * shift
+        x += env * (torch.sin(2 * math.pi * f * t[None, :]) + 0.5 * torch.sin(4 * math.pi * f * t[None, :]))
+        start = start + dur
+    x = gain * x + 0.01 * torch.randn((n, length), generator=g, device=device)
+    return x.clamp_(-1.0, 1.0)

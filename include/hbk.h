@@ -107,6 +107,18 @@ int hbk_embed_plan_create(const hbk_graph_op* ops, int32_t n_ops, int32_t in_h, 
                           const int32_t* win_start, int32_t n_win, hbk_embed_plan** plan);
 int hbk_embed_plan_destroy(hbk_embed_plan* plan);
 
+/* Arithmetic of the conv GEMMs.
+ * SPLIT_F16 (default of hbk_embed_plan_create): every activation and weight is
+ *   held as an fp16 pair x = hi + 2^-11 lo and each product as
+ *   hi*hi + 2^-11 (hi*lo + lo*hi) on v_mfma_f32_32x32x16_f16 with f32
+ *   accumulation: ~2^-21 relative per operand (f32 is 2^-24), at 16x the MFMA
+ *   rate of f32 input. Requires |activations| and |weights| < 65504.
+ * EXACT_F32: v_mfma_f32_16x16x4f32, bitwise an fmaf chain in f32. */
+typedef enum { HBK_PREC_SPLIT_F16 = 0, HBK_PREC_EXACT_F32 = 1 } hbk_precision;
+int hbk_embed_plan_create_ex(const hbk_graph_op* ops, int32_t n_ops, int32_t in_h, int32_t in_w,
+                             const int32_t* win_start, int32_t n_win, int32_t precision,
+                             hbk_embed_plan** plan);
+
 /* out_dim; number of ops shared per clip; fused chains (clip path); MACs per
  * clip (shared prefix, algorithmic) and per window (tail). */
 int hbk_embed_plan_info(const hbk_embed_plan* plan, int32_t* out_dim, int32_t* n_prefix_ops,

@@ -4,7 +4,9 @@ The embedding graph is runtime data (heybuddy.embedding_graph); parity is
 against oracle.embed.run_graph, which evaluates every 76-frame window on its
 own exactly as SpeechEmbeddingModel.__call__ does (embeddings.py:32-42) — so
 the GPU clip path's shared-prefix deduplication is checked too.
-Tolerance: fp32 MFMA vs fp64 oracle, |diff| <= 1e-4 * (1 + |ref|).
+Both GEMM precisions of the plan are checked ('split': fp16 hi/lo pairs on
+the f16 MFMA, ~2^-21 relative per operand; 'exact': f32 MFMA).
+Tolerance: vs the fp64 oracle, |diff| <= 1e-4 * (1 + |ref|).
 """
 import numpy as np
 import pytest
@@ -63,12 +65,16 @@ def _close(out, ref, tol=1e-4):
     return (err <= bound).all(), err.max()
 
 
+PRECISIONS = ["split", "exact"]
+
+
 @pytest.mark.gpu
-def test_embed_windows_parity():
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_embed_windows_parity(precision):
     from heybuddy.embedding_graph import se20_graph
     from heybuddy.kernels import EmbedPlan
     g = se20_graph()
-    plan = EmbedPlan(g)
+    plan = EmbedPlan(g, precision=precision)
     rng = np.random.default_rng(5)
     wins = (rng.standard_normal((37, 76, 32)) * 2 + 6).astype(np.float32)
     out = plan.windows(torch.from_numpy(wins).cuda()).cpu().numpy()
@@ -78,11 +84,12 @@ def test_embed_windows_parity():
 
 
 @pytest.mark.gpu
-def test_embed_clips_parity_shared_prefix():
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_embed_clips_parity_shared_prefix(precision):
     from heybuddy.embedding_graph import se20_graph
     from heybuddy.kernels import EmbedPlan
     g = se20_graph()
-    plan = EmbedPlan(g)
+    plan = EmbedPlan(g, precision=precision)
     assert plan.seq_frames == 136 and plan.n_prefix_ops == 13
     mel = _mel_clips(5)
     out = plan.clips(torch.from_numpy(mel).cuda()).cpu().numpy()
@@ -95,15 +102,68 @@ def test_embed_clips_parity_shared_prefix():
 
 
 @pytest.mark.gpu
-def test_embed_clips_ragged_batches():
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_embed_clips_ragged_batches(precision):
     """Clip counts that leave partial task groups, and one clip."""
     from heybuddy.embedding_graph import se20_graph
     from heybuddy.kernels import EmbedPlan
     g = se20_graph()
-    plan = EmbedPlan(g)
+    plan = EmbedPlan(g, precision=precision)
     mel = _mel_clips(3, seed=11)
     ref = _oracle_clip_embeddings(g, mel)
     for n in (1, 3):
         out = plan.clips(torch.from_numpy(mel[:n]).cuda()).cpu().numpy()
         ok, worst = _close(out, ref[:n])
         assert ok, f"n={n}: max |diff| {worst}"
+
+
+def _generic_graph(seed=9):
+    """Shapes the SE20 stand-in does not have: cin 1 with a 2x3 kernel, channel
+    counts that are not multiples of 8 / 32 (12, 40, 70, 33), a 1x1 conv, a
+    (1, 2) pool and a kernel that spans the whole remaining image."""
+    from heybuddy.embedding_graph import Conv, Graph, MaxPool
+    rng = np.random.default_rng(seed)
+
+    def conv(kh, kw, ci, co, act="leaky_relu"):
+        w = rng.standard_normal((kh, kw, ci, co)) * np.sqrt(2.0 / (kh * kw * ci))
+        return Conv(kh, kw, ci, co, w.astype(np.float32), (rng.standard_normal(co) * 0.1).astype(np.float32),
+                    act=act)
+
+    ops = [conv(2, 3, 1, 12), conv(1, 1, 12, 40), MaxPool(2, 2), conv(3, 2, 40, 70), MaxPool(1, 2),
+           conv(7, 2, 70, 33, act=None)]
+    return Graph(ops, (20, 12, 1), name="generic")
+
+
+def test_generic_graph_shapes():
+    g = _generic_graph()
+    assert g.shapes()[-1] == (1, 1, 33)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_embed_generic_graph_parity(precision):
+    from heybuddy.kernels import EmbedPlan
+    g = _generic_graph()
+    plan = EmbedPlan(g, starts=(0,), device=0, precision=precision)
+    rng = np.random.default_rng(2)
+    wins = rng.standard_normal((23, 20, 12)).astype(np.float32)
+    out = plan.windows(torch.from_numpy(wins).cuda()).cpu().numpy()
+    ref = oemb.run_graph(g, wins)
+    ok, worst = _close(out, ref)
+    assert out.shape == (23, 33) and ok, f"max |diff| {worst}"
+
+
+@pytest.mark.gpu
+def test_embed_split_precision_margin():
+    """The split path sits orders of magnitude inside the tolerance: relative
+    error vs the fp64 oracle below 1e-5 over SE20 windows."""
+    from heybuddy.embedding_graph import se20_graph
+    from heybuddy.kernels import EmbedPlan
+    g = se20_graph()
+    plan = EmbedPlan(g, precision="split")
+    rng = np.random.default_rng(8)
+    wins = (rng.standard_normal((64, 76, 32)) * 2 + 6).astype(np.float32)
+    out = plan.windows(torch.from_numpy(wins).cuda()).cpu().numpy()
+    ref = oemb.run_graph(g, wins)
+    rel = np.abs(out - ref).max() / np.abs(ref).max()
+    assert rel < 1e-5, rel
