@@ -40,35 +40,46 @@ def _headers_mtime() -> float:
     return max((os.path.getmtime(h) for h in hs), default=0.0)
 
 
-def _compile(src: str, force: bool) -> str:
-    obj = os.path.join(OBJ, os.path.basename(src) + ".o")
+def _compile(src: str, force: bool, obj_dir: str = OBJ, extra: tuple = ()) -> str:
+    obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
     if not force and os.path.exists(obj):
         if os.path.getmtime(obj) >= max(os.path.getmtime(src), _headers_mtime()):
             return obj
     lang = ["-x", "hip"] if src.endswith(".hip") else []
-    cmd = [HIPCC, *CFLAGS, *lang, "-c", src, "-o", obj]
+    cmd = [HIPCC, *CFLAGS, *extra, *lang, "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
     return obj
 
 
-def build(force: bool = False) -> str:
-    os.makedirs(OBJ, exist_ok=True)
+VARIANTS = {  # profiling builds (load with HBK_LIB=hey-buddy_amd/lib/<name>)
+    "phase": ("libhbk_phase.so", ("-DHBK_PHASE_TIMING",)),  # s_memtime phase counters + ablation
+    "ablate": ("libhbk_ablate.so", ("-DHBK_ABLATE",)),      # HBK_DEBUG_SKIP phase ablation only
+    "trace": ("libhbk_trace.so", ("-DHBK_TRACE",)),         # per-wave s_memtime timeline
+}
+
+
+def build(force: bool = False, variant: str | None = None) -> str:
+    obj_dir = OBJ + (f"_{variant}" if variant else "")
+    lib = os.path.join(LIB_DIR, VARIANTS[variant][0]) if variant else LIB
+    extra = VARIANTS[variant][1] if variant else ()
+    os.makedirs(obj_dir, exist_ok=True)
     os.makedirs(LIB_DIR, exist_ok=True)
     srcs = sources()
     with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-        objs = list(ex.map(lambda s: _compile(s, force), srcs))
-    if (not force and os.path.exists(LIB)
-            and os.path.getmtime(LIB) >= max(os.path.getmtime(o) for o in objs)):
-        return LIB
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", LIB + ".tmp"]
+        objs = list(ex.map(lambda s: _compile(s, force, obj_dir, extra), srcs))
+    if (not force and os.path.exists(lib)
+            and os.path.getmtime(lib) >= max(os.path.getmtime(o) for o in objs)):
+        return lib
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", lib + ".tmp"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(lib + ".tmp", lib)
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv))
+    var = next((a[len("--variant="):] for a in sys.argv if a.startswith("--variant=")), None)
+    print(build(force="--force" in sys.argv, variant=var))

@@ -20,6 +20,7 @@
 //     the per-window "tail". The per-window API runs every layer per window.
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <numeric>
 #include <vector>
 
@@ -233,10 +234,12 @@ __global__ void __launch_bounds__(kThreads) conv_chain_kernel(ChainArgs a) {
 
 // ------------------------------------------------- split-f16 conv chain ----
 // Same task structure as conv_chain_kernel; the arithmetic is an fp16 pair per
-// value, x = hi + 2^-11 lo (lo = fp16((x - hi) * 2^11), hi rounded toward
-// zero), and each GEMM is
-//   acc_h = W_hi X_hi,  acc_x = W_hi X_lo + W_lo X_hi,  out = acc_h + 2^-11 acc_x
-// on v_mfma_f32_32x32x16_f16 (f32 accumulation), with the WEIGHTS as the A
+// value, x = hi + lo (hi = x with its 13 low mantissa bits cleared, i.e. x
+// rounded toward zero to fp16's 11 bits; lo = fp16(x - hi)), and each GEMM is
+//   acc = W_hi X_hi + W_hi X_lo + W_lo X_hi
+// on v_mfma_f32_32x32x16_f16 (f32 accumulation): ~2^-22 relative per operand
+// (lo loses bits only below fp16's subnormal step, 2^-24 absolute; the
+// dropped W_lo X_lo is 2^-22 relative). WEIGHTS are the A
 // operand (32 output channels) and 32 output POSITIONS as the B operand, so a
 // lane of the accumulator holds 4 consecutive channels of one position: the
 // epilogue packs them (v_cvt_pkrtz) and stores 8 B per plane.
@@ -250,8 +253,6 @@ __global__ void __launch_bounds__(kThreads) conv_chain_kernel(ChainArgs a) {
 // unit) so no integer division runs per element.
 constexpr int kXThreads = 256;
 constexpr int kXWaves = kXThreads / 64;
-constexpr float kLoScale = 2048.f;
-constexpr float kLoInv = 1.f / 2048.f;
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef __fp16 h2 __attribute__((ext_vector_type(2)));
@@ -278,6 +279,8 @@ struct XArgs {
   const _Float16* wblob;   // global weights (WG mode reads them here)
   const float* bblob;      // biases [per stage nblk * 32]
   const int* ktab;         // group offsets, all stages
+  const int* i2c_off;      // im2col: raw-row offset of tap k = (dh kw + dw) C + ci
+  int i2c_n;
   int64_t n_img;
   int64_t src_clip_stride;
   int src_row_stride;
@@ -289,18 +292,93 @@ struct XArgs {
   int out_ph, out_pw, H_out, W_out, C_out;
   int64_t out_img_stride;
   int vec_out;             // C_out % 4 == 0 and 16-B aligned output: float4 stores
+  int raw_vec;             // im2col staging reads float4 (in_pw == 1, aligned rows)
   int G, band, n_bands, shrink, n_stages;
   XStage st[kMaxStages];
   int w_halfs;             // resident weights (0: WG mode)
   int b_floats, kt_n;
   int lds_x, lds_y, lds_w, lds_b, lds_k;  // byte offsets into dynamic LDS
+  int dbg_slot;            // phase-timing slot (chain index mod 4; profiling build only)
+  int dbg_skip;            // profiling build only: bit 0 stages, 1 im2col, 2 store, 3 staging
 };
 
-// hi (round toward zero) and lo = (v - hi) * 2^11 for two values, packed
+#if defined(HBK_PHASE_TIMING) || defined(HBK_ABLATE)
+#define HBK_SKIP(bit) (a.dbg_skip & (1 << (bit)))
+#else
+#define HBK_SKIP(bit) false
+#endif
+#ifdef HBK_PHASE_TIMING
+// Profiling build only (build.py --phase-timing): wave 0 of every block adds
+// the s_memtime cycles of each task phase (staging, im2col, stage s, store;
+// barrier waits included in the phase before them) into g_phase_cycles.
+__device__ unsigned long long g_phase_cycles[64];  // [chain slot (4)][phase (16)]
+#define HBK_PHASE(i)                                                          \
+  do {                                                                        \
+    if (threadIdx.x == 0) {                                                   \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime();             \
+      atomicAdd(&g_phase_cycles[a.dbg_slot * 16 + (i)], t_ - phase_t0);      \
+      phase_t0 = t_;                                                          \
+    }                                                                         \
+  } while (0)
+#else
+#define HBK_PHASE(i) \
+  do {               \
+  } while (0)
+#endif
+
+#ifdef HBK_TRACE
+// Tracing build only: lane 0 of waves of the first 4 blocks records
+// s_memtime at marks of the first tasks into g_trace[block][wave][event].
+__device__ unsigned long long g_trace[4][4][256];
+__device__ int g_trace_n[4][4];
+#define HBK_MARK(id)                                                                        \
+  do {                                                                                      \
+    if (blockIdx.x < 4 && (threadIdx.x & 63) == 0) {                                        \
+      const int w_ = threadIdx.x >> 6, b_ = blockIdx.x;                                     \
+      const int n_ = g_trace_n[b_][w_];                                                     \
+      if (n_ < 255) {                                                                       \
+        g_trace[b_][w_][n_] = (__builtin_amdgcn_s_memtime() << 8) | static_cast<unsigned>(id); \
+        g_trace_n[b_][w_] = n_ + 1;                                                         \
+      }                                                                                     \
+    }                                                                                       \
+  } while (0)
+#else
+#define HBK_MARK(id) \
+  do {               \
+  } while (0)
+#endif
+
+constexpr int kXStageInts = sizeof(XStage) / 4;
+constexpr int kI2cLds = 256;  // im2col tap table entries kept in LDS
+
+// A stage descriptor from the block's LDS copy, as uniform (scalar) values.
+__device__ __forceinline__ XStage lds_stage(const int* p) {
+  XStage S;
+  int* d = reinterpret_cast<int*>(&S);
+#pragma unroll
+  for (int i = 0; i < kXStageInts; ++i) d[i] = __builtin_amdgcn_readfirstlane(p[i]);
+  return S;
+}
+
+// q = n / d for 0 <= n < 2^24, d >= 1, from a float reciprocal (one
+// correction step covers its rounding); inv = 1.f / d
+__device__ __forceinline__ int div_small(int n, int d, float inv) {
+  int q = static_cast<int>(static_cast<float>(n) * inv);
+  const int r = n - q * d;
+  q += (r >= d) ? 1 : 0;
+  q -= (r < 0) ? 1 : 0;
+  return q;
+}
+
+// hi = v rounded toward zero to 11 significant bits (exact in fp16 for
+// |v| in fp16's normal range), lo = v - hi; two values, packed
+__device__ __forceinline__ float hi_part(float v) {
+  return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, v) & 0xFFFFE000u);
+}
 __device__ __forceinline__ void split2(float a, float b, h2& hi, h2& lo) {
-  hi = __builtin_amdgcn_cvt_pkrtz(a, b);
-  lo = __builtin_amdgcn_cvt_pkrtz((a - static_cast<float>(hi.x)) * kLoScale,
-                                  (b - static_cast<float>(hi.y)) * kLoScale);
+  const float ha = hi_part(a), hb = hi_part(b);
+  hi = __builtin_amdgcn_cvt_pkrtz(ha, hb);
+  lo = __builtin_amdgcn_cvt_pkrtz(a - ha, b - hb);
 }
 
 __device__ __forceinline__ uint32_t h2_bits(h2 v) { return __builtin_bit_cast(uint32_t, v); }
@@ -327,59 +405,102 @@ struct RowMap {
   }
 };
 
+// Yf != nullptr: the chain's last stage, written as f32 [m][coutr] for the
+// pooled store (no split / reconstruct).
 template <int NB, int RB>
 __device__ __forceinline__ void xstage(const _Float16* __restrict__ Xh, const _Float16* __restrict__ Xl,
                                        _Float16* __restrict__ Yh, _Float16* __restrict__ Yl,
-                                       const _Float16* __restrict__ Wh, const int* __restrict__ kt,
-                                       const float* __restrict__ bias, int M, int hA, int wA, int ho,
-                                       int wo, const XStage& S, int lane, int wave) {
+                                       float* __restrict__ Yf, const _Float16* __restrict__ Wh,
+                                       const int* __restrict__ kt, const float* __restrict__ bias, int M,
+                                       int hA, int wA, int ho, int wo, const XStage& S, int lane, int wave) {
   const int img_pos = ho * wo;
   const int nrb = (M + 31) >> 5;
   const int r32 = lane & 31, khalf = lane >> 5;
   const _Float16* wp = Wh + r32 * S.wrow + khalf * 8;
   const int cstride = 32 * S.wrow;
+  // input position of output m = (g, y, x): with ytot = g ho + y = m / wo,
+  // (g hA + y) wA + x = m + ytot (wA - wo) + g (hA - ho) wA
+  const float inv_wo = 1.f / static_cast<float>(wo), inv_ho = 1.f / static_cast<float>(ho);
+  const bool one_img = M <= img_pos;
+  // this lane's biases, channels n = 32 c + 8 q + 4 khalf + j (register 4 q + j)
+  f16x bl[NB];
+#pragma unroll
+  for (int c = 0; c < NB; ++c)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 b = *reinterpret_cast<const float4*>(bias + c * 32 + 8 * q + 4 * khalf);
+      bl[c][4 * q] = b.x;
+      bl[c][4 * q + 1] = b.y;
+      bl[c][4 * q + 2] = b.z;
+      bl[c][4 * q + 3] = b.w;
+    }
   for (int rb0 = wave * RB; rb0 < nrb; rb0 += kXWaves * RB) {
+    HBK_MARK(10);
     int xoff[RB];
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
       const int m = min((rb0 + r) * 32 + r32, M - 1);
-      const int g = m / img_pos;
-      const int rem = m - g * img_pos;
-      const int y = rem / wo;
-      const int x = rem - y * wo;
-      xoff[r] = ((g * hA + y) * wA + x) * S.cs_in;
+      const int ytot = div_small(m, wo, inv_wo);
+      const int g = one_img ? 0 : div_small(ytot, ho, inv_ho);
+      xoff[r] = (m + ytot * (wA - wo) + g * (hA - ho) * wA) * S.cs_in;
     }
-    f16x acc_h[RB][NB], acc_x[RB][NB];
-#pragma unroll
-    for (int r = 0; r < RB; ++r)
-#pragma unroll
-      for (int c = 0; c < NB; ++c) {
-        acc_h[r][c] = f16x{};
-        acc_x[r][c] = f16x{};
-      }
-#pragma unroll 2
-    for (int ks = 0; ks < S.ksteps; ++ks) {
+    (void)img_pos;
+    f16x acc[RB][NB];
+    // software-pipelined K loop over two fragment sets: the LDS reads of step
+    // ks + 1 are in flight while the MFMAs of step ks run (the prefetch index
+    // is clamped, so the last step re-reads its own fragments harmlessly)
+    struct Frag {
+      h8 xh[RB], xl[RB], wh[NB], wl[NB];
+    };
+    auto load = [&](Frag& f, int ks) {
       const int ko = kt[2 * ks + khalf];
-      h8 xh[RB], xl[RB];
 #pragma unroll
       for (int r = 0; r < RB; ++r) {
-        xh[r] = *reinterpret_cast<const h8*>(Xh + xoff[r] + ko);
-        xl[r] = *reinterpret_cast<const h8*>(Xl + xoff[r] + ko);
+        f.xh[r] = *reinterpret_cast<const h8*>(Xh + xoff[r] + ko);
+        f.xl[r] = *reinterpret_cast<const h8*>(Xl + xoff[r] + ko);
       }
 #pragma unroll
       for (int c = 0; c < NB; ++c) {
-        const h8 wh = *reinterpret_cast<const h8*>(wp + c * cstride + ks * 16);
-        const h8 wl = *reinterpret_cast<const h8*>(wp + S.w_lo + c * cstride + ks * 16);
+        f.wh[c] = *reinterpret_cast<const h8*>(wp + c * cstride + ks * 16);
+        f.wl[c] = *reinterpret_cast<const h8*>(wp + S.w_lo + c * cstride + ks * 16);
+      }
+    };
+    // three products per tile, the tiles interleaved so that consecutive
+    // MFMAs never chain on one accumulator
+    auto mma = [&](const Frag& f, bool first) {
 #pragma unroll
-        for (int r = 0; r < RB; ++r) {
-          acc_h[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xh[r], acc_h[r][c], 0, 0, 0);
-          acc_x[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xl[r], acc_x[r][c], 0, 0, 0);
-        }
+      for (int c = 0; c < NB; ++c) {
 #pragma unroll
         for (int r = 0; r < RB; ++r)
-          acc_x[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, xh[r], acc_x[r][c], 0, 0, 0);
+          acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.wh[c], f.xh[r], first ? f16x{} : acc[r][c], 0, 0,
+                                                              0);
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+          acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.wh[c], f.xl[r], acc[r][c], 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+          acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.wl[c], f.xh[r], acc[r][c], 0, 0, 0);
       }
+    };
+    HBK_MARK(11);
+    const int last = S.ksteps - 1;
+    Frag fa, fb;
+    load(fa, 0);
+    load(fb, min(1, last));
+    mma(fa, true);
+    int ks = 1;
+    for (; ks < last; ks += 2) {
+      load(fa, ks + 1);
+      mma(fb, false);
+      load(fb, min(ks + 2, last));
+      mma(fa, false);
     }
+    if (ks == last) mma(fb, false);
+#ifdef HBK_TRACE
+    // make the mark wait for the accumulators (MFMA completion)
+    asm volatile("" ::"v"(acc[0][0][0]));
+#endif
+    HBK_MARK(12);
     // D[n][m]: this lane holds position m = tile + (lane & 31) and channels
     // n = 32 c + 8 q + 4 (lane >> 5) + j for register i = 4 q + j
 #pragma unroll
@@ -392,16 +513,21 @@ __device__ __forceinline__ void xstage(const _Float16* __restrict__ Xh, const _F
       for (int c = 0; c < NB; ++c)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
+          // coutr is a multiple of 8, so this test is the same for both lane halves (uniform)
+          if (c * 32 + 8 * q >= S.coutr) continue;
           const int n0 = c * 32 + 8 * q + 4 * khalf;
-          if (n0 >= S.coutr) continue;
-          const float4 bb = *reinterpret_cast<const float4*>(bias + n0);
-          float v[4];
+          float v[4] = {acc[r][c][4 * q] + bl[c][4 * q], acc[r][c][4 * q + 1] + bl[c][4 * q + 1],
+                        acc[r][c][4 * q + 2] + bl[c][4 * q + 2], acc[r][c][4 * q + 3] + bl[c][4 * q + 3]};
+          if (S.act == 1) {  // LeakyReLU, 0 <= alpha <= 1: max(v, alpha v) (NaN stays NaN)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            float t = acc_h[r][c][4 * q + j] + acc_x[r][c][4 * q + j] * kLoInv;
-            t += j == 0 ? bb.x : j == 1 ? bb.y : j == 2 ? bb.z : bb.w;
-            if (S.act) t = t >= 0.f ? t : t * S.alpha;
-            v[j] = t;
+            for (int j = 0; j < 4; ++j) v[j] = __builtin_fmaxf(v[j], v[j] * S.alpha);
+          } else if (S.act == 2) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = v[j] >= 0.f ? v[j] : v[j] * S.alpha;
+          }
+          if (Yf) {
+            *reinterpret_cast<float4*>(Yf + m * S.coutr + n0) = float4{v[0], v[1], v[2], v[3]};
+            continue;
           }
           h2 h01, l01, h23, l23;
           split2(v[0], v[1], h01, l01);
@@ -410,11 +536,16 @@ __device__ __forceinline__ void xstage(const _Float16* __restrict__ Xh, const _F
           *reinterpret_cast<uint2*>(yl + n0) = uint2{h2_bits(l01), h2_bits(l23)};
         }
     }
+    HBK_MARK(13);
   }
 }
 
+#ifndef HBK_X3_WAVES_PER_EU
+#define HBK_X3_WAVES_PER_EU 2
+#endif
 template <int NBMAX, bool WG>
-__global__ void __launch_bounds__(kXThreads) conv_chain_x3_kernel(XArgs a) {
+__global__ void __launch_bounds__(kXThreads) __attribute__((amdgpu_waves_per_eu(HBK_X3_WAVES_PER_EU)))
+conv_chain_x3_kernel(XArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char xsmem[];
   unsigned char* Xb = xsmem + a.lds_x;
   unsigned char* Yb = xsmem + a.lds_y;
@@ -422,14 +553,21 @@ __global__ void __launch_bounds__(kXThreads) conv_chain_x3_kernel(XArgs a) {
   float* Bl = reinterpret_cast<float*>(xsmem + a.lds_b);
   int* kt = reinterpret_cast<int*>(xsmem + a.lds_k);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // per-block LDS copies of the stage descriptors and the im2col tap table
+  // (read every task; kernel arguments are not re-read in the task loop)
+  __shared__ int s_st[kMaxStages * kXStageInts];
+  __shared__ int s_i2c[kI2cLds];
+  for (int i = tid; i < a.n_stages * kXStageInts; i += kXThreads)
+    s_st[i] = reinterpret_cast<const int*>(a.st)[i];
+  for (int i = tid; i < kI2cLds; i += kXThreads) s_i2c[i] = a.i2c_off[min(i, a.i2c_n - 1)];
   if (!WG)
     for (int i = tid; i < a.w_halfs / 8; i += kXThreads)
       reinterpret_cast<h8*>(Wl)[i] = reinterpret_cast<const h8*>(a.wblob)[i];
   for (int i = tid; i < a.b_floats; i += kXThreads) Bl[i] = a.bblob[i];
   for (int i = tid; i < a.kt_n; i += kXThreads) kt[i] = a.ktab[i];
 
-  const int64_t n_groups = (a.n_img + a.G - 1) / a.G;
-  const int64_t n_tasks = n_groups * a.n_bands;
+  // task indices fit in 32 bits (at most kChunkClips x 32 windows x bands)
+  const int n_tasks = static_cast<int>((a.n_img + a.G - 1) / a.G) * a.n_bands;
   const int C = a.C_src;
   const XStage& S0 = a.st[0];
   // per-kernel thread mappings
@@ -437,7 +575,8 @@ __global__ void __launch_bounds__(kXThreads) conv_chain_x3_kernel(XArgs a) {
   //  staging (im2col):    raw f32, W_in * C per row
   //  im2col expansion:    positions, wo0 per row
   //  store:               units of 4 channels (vec_out) or 1, W_out * C_out / (4|1) per row
-  const int st_units = a.im2col ? a.W_in * C : a.W_in * (C / 8);
+  const int st_units = a.im2col ? (a.raw_vec ? a.W_in * C / 4 : a.W_in * C) : a.W_in * (C / 8);
+  const int raw_len = a.W_in * C;  // floats per raw row (im2col)
   const RowMap ms(st_units, tid);
   const int st_w = a.im2col ? 0 : ms.t_u / (C / 8);
   const int wo0 = a.W_in - S0.kw + 1;
@@ -446,67 +585,151 @@ __global__ void __launch_bounds__(kXThreads) conv_chain_x3_kernel(XArgs a) {
   const RowMap mo(a.W_out * a.C_out / cu, tid);
   const int o_w = mo.t_u / (a.C_out / cu), o_c = (mo.t_u - o_w * (a.C_out / cu)) * cu;
 
-  for (int64_t task = blockIdx.x; task < n_tasks; task += gridDim.x) {
-    const int64_t grp = task / a.n_bands;
-    const int band = static_cast<int>(task - grp * a.n_bands);
-    const int64_t img0 = grp * a.G;
-    const int G = static_cast<int>(min<int64_t>(a.G, a.n_img - img0));
-    const int orow0 = band * a.band;
-    const int orows = min(a.band, a.H_out - orow0);
-    const int r0 = orow0 * a.out_ph;
-    const int rows_in = orows * a.out_ph + a.shrink;
-    const int nrows = G * rows_in;
+  struct Geo {
+    int64_t img0;
+    int G, orow0, orows, r0, rows_in, nrows;
+  };
+  auto geo = [&](int task) {
+    Geo t;
+    const int grp = task / a.n_bands;
+    const int band = task - grp * a.n_bands;
+    t.img0 = static_cast<int64_t>(grp) * a.G;
+    t.G = static_cast<int>(min<int64_t>(a.G, a.n_img - t.img0));
+    t.orow0 = band * a.band;
+    t.orows = min(a.band, a.H_out - t.orow0);
+    t.r0 = t.orow0 * a.out_ph;
+    t.rows_in = t.orows * a.out_ph + a.shrink;
+    t.nrows = t.G * t.rows_in;
+    return t;
+  };
+  // one staging unit of row `row` (image g, band row r), max-pooled on load:
+  // im2col: 4 raw floats (raw_vec) or 1; otherwise 8 channels of position w
+  auto load_unit = [&](const Geo& t, int row, int u, float4& v0, float4& v1) {
+    const int g = row / t.rows_in;
+    const int r = row - g * t.rows_in;
+    const int64_t im = t.img0 + g;
+    const int64_t clip = im / a.ipc;
+    const int roff = a.row_off[im - clip * a.ipc];
+    const float* srow = a.in + clip * a.src_clip_stride +
+                        static_cast<int64_t>(roff + (t.r0 + r) * a.in_ph) * a.src_row_stride;
+    if (a.im2col) {
+      if (a.raw_vec) {  // in_pw == 1
+        const float* src = srow + u * 4;
+        v0 = *reinterpret_cast<const float4*>(src);
+        for (int i = 1; i < a.in_ph; ++i) {
+          const float4 q = *reinterpret_cast<const float4*>(src + i * a.src_row_stride);
+          v0 = float4{nan_max(v0.x, q.x), nan_max(v0.y, q.y), nan_max(v0.z, q.z), nan_max(v0.w, q.w)};
+        }
+      } else {
+        const int w = u / C, c = u - w * C;
+        const float* src = srow + (w * a.in_pw) * C + c;
+        float v = src[0];
+        for (int i = 0; i < a.in_ph; ++i)
+          for (int j = 0; j < a.in_pw; ++j) v = nan_max(v, src[i * a.src_row_stride + j * C]);
+        v0.x = v;
+      }
+      return;
+    }
+    const int w = (ms.u_step == st_units) ? st_w : u / (C / 8);
+    const int c8 = (u - w * (C / 8)) * 8;
+    const float* src = srow + (w * a.in_pw) * C + c8;
+    v0 = *reinterpret_cast<const float4*>(src);
+    v1 = *reinterpret_cast<const float4*>(src + 4);
+    for (int i = 0; i < a.in_ph; ++i)
+      for (int j = 0; j < a.in_pw; ++j) {
+        if (i == 0 && j == 0) continue;
+        const float* q = src + i * a.src_row_stride + j * C;
+        const float4 p0 = *reinterpret_cast<const float4*>(q);
+        const float4 p1 = *reinterpret_cast<const float4*>(q + 4);
+        v0 = float4{nan_max(v0.x, p0.x), nan_max(v0.y, p0.y), nan_max(v0.z, p0.z), nan_max(v0.w, p0.w)};
+        v1 = float4{nan_max(v1.x, p1.x), nan_max(v1.y, p1.y), nan_max(v1.z, p1.z), nan_max(v1.w, p1.w)};
+      }
+  };
+  auto store_unit = [&](const Geo& t, int row, int u, const float4& v0, const float4& v1) {
+    if (a.im2col) {
+      float* R = reinterpret_cast<float*>(Yb) + row * raw_len;
+      if (a.raw_vec)
+        *reinterpret_cast<float4*>(R + u * 4) = v0;
+      else
+        R[u] = v0.x;
+      return;
+    }
+    const int w = (ms.u_step == st_units) ? st_w : u / (C / 8);
+    const int c8 = (u - w * (C / 8)) * 8;
+    h2 a0, b0, a1, b1, a2, b2, a3, b3;
+    split2(v0.x, v0.y, a0, b0);
+    split2(v0.z, v0.w, a1, b1);
+    split2(v1.x, v1.y, a2, b2);
+    split2(v1.z, v1.w, a3, b3);
+    _Float16* Sh = reinterpret_cast<_Float16*>(Xb);
+    const int idx = (row * a.W_in + w) * a.cs0 + c8;
+    *reinterpret_cast<uint4*>(Sh + idx) = uint4{h2_bits(a0), h2_bits(a1), h2_bits(a2), h2_bits(a3)};
+    *reinterpret_cast<uint4*>(Sh + t.nrows * a.W_in * a.cs0 + idx) =
+        uint4{h2_bits(b0), h2_bits(b1), h2_bits(b2), h2_bits(b3)};
+  };
+  // The first kPF row passes of a task's staging are loaded into registers
+  // one task ahead (their global loads overlap the current task's compute);
+  // further passes, or rows wider than the block, load synchronously.
+#ifndef HBK_X3_PF
+#define HBK_X3_PF (NBMAX == 1 ? 4 : 2)
+#endif
+  constexpr int kPF = HBK_X3_PF;
+  const bool pf_ok = ms.u_step == st_units;
+  float4 pv0[kPF], pv1[kPF];
+  auto prefetch = [&](const Geo& t) {
+#pragma unroll
+    for (int p = 0; p < kPF; ++p) {
+      const int row = ms.t_row + p * ms.rpp;
+      if (row < t.nrows) load_unit(t, row, ms.t_u, pv0[p], pv1[p]);
+    }
+  };
+
+  int task = blockIdx.x;
+  Geo tg{};
+  if (task < n_tasks) {
+    tg = geo(task);
+    if (pf_ok) prefetch(tg);
+  }
+  for (; task < n_tasks; task += gridDim.x) {
+    const Geo t = tg;
+    const int64_t img0 = t.img0;
+    const int G = t.G, orow0 = t.orow0, orows = t.orows, rows_in = t.rows_in;
 
     // 1) stage the band's input rows (max-pooled on the fly)
     __syncthreads();  // previous task's readers of X / Y are done (kt, Wl, Bl on the first task)
-    for (int row = ms.t_row; row < nrows; row += ms.rpp) {
-      const int g = row / rows_in;
-      const int r = row - g * rows_in;
-      const int64_t im = img0 + g;
-      const int64_t clip = im / a.ipc;
-      const int roff = a.row_off[im - clip * a.ipc];
-      const float* srow = a.in + clip * a.src_clip_stride +
-                          static_cast<int64_t>(roff + (r0 + r) * a.in_ph) * a.src_row_stride;
-      for (int u = ms.t_u; u < st_units; u += ms.u_step) {
-        if (a.im2col) {  // raw f32 rows, u = w * C + c
-          const int w = u / C, c = u - w * C;
-          const float* src = srow + (w * a.in_pw) * C + c;
-          float v = src[0];
-          for (int i = 0; i < a.in_ph; ++i)
-            for (int j = 0; j < a.in_pw; ++j) v = nan_max(v, src[i * a.src_row_stride + j * C]);
-          reinterpret_cast<float*>(Yb)[row * st_units + u] = v;
-        } else {         // 8 channels of position w
-          const int w = (ms.u_step == st_units) ? st_w : u / (C / 8);
-          const int c8 = (u - w * (C / 8)) * 8;
-          const float* src = srow + (w * a.in_pw) * C + c8;
-          float4 lo4 = *reinterpret_cast<const float4*>(src);
-          float4 hi4 = *reinterpret_cast<const float4*>(src + 4);
-          for (int i = 0; i < a.in_ph; ++i)
-            for (int j = 0; j < a.in_pw; ++j) {
-              if (i == 0 && j == 0) continue;
-              const float* q = src + i * a.src_row_stride + j * C;
-              const float4 p0 = *reinterpret_cast<const float4*>(q);
-              const float4 p1 = *reinterpret_cast<const float4*>(q + 4);
-              lo4 = float4{nan_max(lo4.x, p0.x), nan_max(lo4.y, p0.y), nan_max(lo4.z, p0.z), nan_max(lo4.w, p0.w)};
-              hi4 = float4{nan_max(hi4.x, p1.x), nan_max(hi4.y, p1.y), nan_max(hi4.z, p1.z), nan_max(hi4.w, p1.w)};
-            }
-          h2 a0, b0, a1, b1, a2, b2, a3, b3;
-          split2(lo4.x, lo4.y, a0, b0);
-          split2(lo4.z, lo4.w, a1, b1);
-          split2(hi4.x, hi4.y, a2, b2);
-          split2(hi4.z, hi4.w, a3, b3);
-          _Float16* Sh = reinterpret_cast<_Float16*>(Xb);
-          const int idx = (row * a.W_in + w) * a.cs0 + c8;
-          *reinterpret_cast<uint4*>(Sh + idx) = uint4{h2_bits(a0), h2_bits(a1), h2_bits(a2), h2_bits(a3)};
-          *reinterpret_cast<uint4*>(Sh + nrows * a.W_in * a.cs0 + idx) =
-              uint4{h2_bits(b0), h2_bits(b1), h2_bits(b2), h2_bits(b3)};
-        }
+#ifdef HBK_PHASE_TIMING
+    unsigned long long phase_t0 = __builtin_amdgcn_s_memtime();
+#endif
+    HBK_MARK(1);
+    if (HBK_SKIP(3)) {
+    } else if (pf_ok) {
+#pragma unroll
+      for (int p = 0; p < kPF; ++p) {
+        const int row = ms.t_row + p * ms.rpp;
+        if (row < t.nrows) store_unit(t, row, ms.t_u, pv0[p], pv1[p]);
       }
+      for (int row = ms.t_row + kPF * ms.rpp; row < t.nrows; row += ms.rpp) {
+        float4 v0, v1;
+        load_unit(t, row, ms.t_u, v0, v1);
+        store_unit(t, row, ms.t_u, v0, v1);
+      }
+    } else {
+      for (int row = ms.t_row; row < t.nrows; row += ms.rpp)
+        for (int u = ms.t_u; u < st_units; u += ms.u_step) {
+          float4 v0, v1;
+          load_unit(t, row, u, v0, v1);
+          store_unit(t, row, u, v0, v1);
+        }
+    }
+    if (task + static_cast<int>(gridDim.x) < n_tasks) {
+      tg = geo(task + gridDim.x);
+      if (pf_ok && !HBK_SKIP(3)) prefetch(tg);  // in flight during this task's compute
     }
     int hin = rows_in, win = a.W_in;
-    if (a.im2col) {
+    if (a.im2col && !HBK_SKIP(1)) {
       // expand stage 0's taps: position (g, y, x) of its OUTPUT holds k = (dh kw + dw) C + ci
       __syncthreads();
+      HBK_PHASE(0);
       const int ho = hin - S0.kh + 1;
       const int K0 = S0.kh * S0.kw * C, K8 = (K0 + 7) & ~7;
       const float* R = reinterpret_cast<const float*>(Yb);
@@ -518,24 +741,22 @@ __global__ void __launch_bounds__(kXThreads) conv_chain_x3_kernel(XArgs a) {
         const float* base = R + ((g * rows_in + y) * win + x) * C;
         _Float16* dh_ = Ih + (prow * wo0 + x) * a.cs0;
         _Float16* dl_ = Il + (prow * wo0 + x) * a.cs0;
-        int dh = 0, dw = 0, ci = 0;
-        for (int k = 0; k < K8; k += 2) {
-          float v[2];
+        for (int k8 = 0; k8 < K8; k8 += 8) {  // one 8-channel group: 16 B per plane
+          uint32_t hb[4], lb[4];
 #pragma unroll
-          for (int t = 0; t < 2; ++t) {
-            v[t] = (k + t < K0) ? base[(dh * win + dw) * C + ci] : 0.f;
-            if (++ci == C) {
-              ci = 0;
-              if (++dw == S0.kw) {
-                dw = 0;
-                ++dh;
-              }
-            }
+          for (int p = 0; p < 4; ++p) {
+            const int k = k8 + 2 * p;  // tap offsets: uniform table (scalar loads)
+            const int o0 = k < kI2cLds ? s_i2c[k] : a.i2c_off[k];
+            const int o1 = k + 1 < kI2cLds ? s_i2c[k + 1] : a.i2c_off[k + 1];
+            const float v0 = k < K0 ? base[o0] : 0.f;
+            const float v1 = k + 1 < K0 ? base[o1] : 0.f;
+            h2 hh, ll;
+            split2(v0, v1, hh, ll);
+            hb[p] = h2_bits(hh);
+            lb[p] = h2_bits(ll);
           }
-          h2 hh, ll;
-          split2(v[0], v[1], hh, ll);
-          *reinterpret_cast<uint32_t*>(dh_ + k) = h2_bits(hh);
-          *reinterpret_cast<uint32_t*>(dl_ + k) = h2_bits(ll);
+          *reinterpret_cast<uint4*>(dh_ + k8) = uint4{hb[0], hb[1], hb[2], hb[3]};
+          *reinterpret_cast<uint4*>(dl_ + k8) = uint4{lb[0], lb[1], lb[2], lb[3]};
         }
       }
     }
@@ -544,12 +765,15 @@ __global__ void __launch_bounds__(kXThreads) conv_chain_x3_kernel(XArgs a) {
     unsigned char* cur = Xb;
     unsigned char* nxt = Yb;
     for (int s = 0; s < a.n_stages; ++s) {
-      const XStage S = a.st[s];
+      const XStage S = lds_stage(s_st + s * kXStageInts);
       const int ho = hin - S.kh + 1, wo = win - S.kw + 1;
       const bool i2c = a.im2col && s == 0;
       const int hA = i2c ? ho : hin, wA = i2c ? wo : win;
       const int M = G * ho * wo;
+      HBK_MARK(19);
       __syncthreads();  // stage input complete
+      HBK_PHASE(s == 0 ? 1 : 1 + s);
+      HBK_MARK(20 + s);
       const _Float16* Xh = reinterpret_cast<const _Float16*>(cur);
       const _Float16* Xl = Xh + G * hA * wA * S.cs_in;
       _Float16* Yh = reinterpret_cast<_Float16*>(nxt);
@@ -557,27 +781,32 @@ __global__ void __launch_bounds__(kXThreads) conv_chain_x3_kernel(XArgs a) {
       const _Float16* Wst = WG ? a.wblob + S.w_off : Wl + S.w_off;
       const int* kts = kt + S.kt_off;
       const float* bs = Bl + S.b_off;
-      // RB x NB tiles of two 16-register accumulators: keep RB * NB <= 3 (2 waves / SIMD)
+      float* Yf = s + 1 == a.n_stages ? reinterpret_cast<float*>(nxt) : nullptr;
+      if (HBK_SKIP(0)) {
+      } else
+      // RB x NB tiles of one 16-register accumulator each
       if (NBMAX >= 3 && S.nblk == 3)
-        xstage<3, 1>(Xh, Xl, Yh, Yl, Wst, kts, bs, M, hA, wA, ho, wo, S, lane, wave);
+        xstage<3, 1>(Xh, Xl, Yh, Yl, Yf, Wst, kts, bs, M, hA, wA, ho, wo, S, lane, wave);
       else if (NBMAX >= 2 && S.nblk == 2)
-        xstage<2, 1>(Xh, Xl, Yh, Yl, Wst, kts, bs, M, hA, wA, ho, wo, S, lane, wave);
+        xstage<2, 2>(Xh, Xl, Yh, Yl, Yf, Wst, kts, bs, M, hA, wA, ho, wo, S, lane, wave);
       else
-        xstage<1, 2>(Xh, Xl, Yh, Yl, Wst, kts, bs, M, hA, wA, ho, wo, S, lane, wave);
+        xstage<1, 2>(Xh, Xl, Yh, Yl, Yf, Wst, kts, bs, M, hA, wA, ho, wo, S, lane, wave);
       unsigned char* t = cur;
       cur = nxt;
       nxt = t;
       hin = ho;
       win = wo;
     }
+    HBK_MARK(19);
     __syncthreads();
+    HBK_PHASE(1 + a.n_stages);
+    HBK_MARK(5);
 
-    // 3) store the band (max-pooled on the fly), hi + 2^-11 lo back to f32
-    const int cso = a.st[a.n_stages - 1].cs_out;
-    const _Float16* Oh = reinterpret_cast<const _Float16*>(cur);
-    const _Float16* Ol = Oh + G * hin * win * cso;
+    // 3) store the band (max-pooled on the fly) from the last stage's f32 output
+    const int cso = __builtin_amdgcn_readfirstlane(s_st[(a.n_stages - 1) * kXStageInts + 4]);  // coutr
+    const float* O = reinterpret_cast<const float*>(cur);
     const int units = a.W_out * a.C_out / cu;
-    for (int orow = mo.t_row; orow < G * orows; orow += mo.rpp) {
+    for (int orow = HBK_SKIP(2) ? (1 << 30) : mo.t_row; orow < G * orows; orow += mo.rpp) {
       const int g = orow / orows, r = orow - g * orows;
       float* drow = a.out + (img0 + g) * a.out_img_stride + static_cast<int64_t>(orow0 + r) * a.W_out * a.C_out;
       for (int u = mo.t_u; u < units; u += mo.u_step) {
@@ -585,36 +814,24 @@ __global__ void __launch_bounds__(kXThreads) conv_chain_x3_kernel(XArgs a) {
         const int c = (mo.u_step == units) ? o_c : (u - w * (a.C_out / cu)) * cu;
         const int base = ((g * hin + r * a.out_ph) * win + w * a.out_pw) * cso + c;
         if (a.vec_out) {
-          float4 v;
+          float4 v = *reinterpret_cast<const float4*>(O + base);
           for (int i = 0; i < a.out_ph; ++i)
             for (int j = 0; j < a.out_pw; ++j) {
-              const int q = base + (i * win + j) * cso;
-              const uint2 hb = *reinterpret_cast<const uint2*>(Oh + q);
-              const uint2 lb = *reinterpret_cast<const uint2*>(Ol + q);
-              const h2 h0 = __builtin_bit_cast(h2, hb.x), h1 = __builtin_bit_cast(h2, hb.y);
-              const h2 l0 = __builtin_bit_cast(h2, lb.x), l1 = __builtin_bit_cast(h2, lb.y);
-              const float4 t{static_cast<float>(h0.x) + static_cast<float>(l0.x) * kLoInv,
-                             static_cast<float>(h0.y) + static_cast<float>(l0.y) * kLoInv,
-                             static_cast<float>(h1.x) + static_cast<float>(l1.x) * kLoInv,
-                             static_cast<float>(h1.y) + static_cast<float>(l1.y) * kLoInv};
-              if (i == 0 && j == 0)
-                v = t;
-              else
-                v = float4{nan_max(v.x, t.x), nan_max(v.y, t.y), nan_max(v.z, t.z), nan_max(v.w, t.w)};
+              if (i == 0 && j == 0) continue;
+              const float4 t = *reinterpret_cast<const float4*>(O + base + (i * win + j) * cso);
+              v = float4{nan_max(v.x, t.x), nan_max(v.y, t.y), nan_max(v.z, t.z), nan_max(v.w, t.w)};
             }
           *reinterpret_cast<float4*>(drow + w * a.C_out + c) = v;
         } else {
-          float v = 0.f;
+          float v = O[base];
           for (int i = 0; i < a.out_ph; ++i)
-            for (int j = 0; j < a.out_pw; ++j) {
-              const int q = base + (i * win + j) * cso;
-              const float t = static_cast<float>(Oh[q]) + static_cast<float>(Ol[q]) * kLoInv;
-              v = (i == 0 && j == 0) ? t : nan_max(v, t);
-            }
+            for (int j = 0; j < a.out_pw; ++j) v = nan_max(v, O[base + (i * win + j) * cso]);
           drow[w * a.C_out + c] = v;
         }
       }
     }
+    HBK_PHASE(2 + a.n_stages);
+    HBK_MARK(6);
   }
 }
 
@@ -721,6 +938,9 @@ XKernelFn pick_xkernel(int nb, bool wg) {
 int layout_split(const std::vector<OpInfo>& ops, const std::vector<int>& stage_ops, Dims d,
                  const ChainArgs& a, ChainPlan& cp, Dims& od_out) {
   XArgs& x = cp.x;
+  // LDS per block (default 78 KB: two blocks per CU); HBK_EMBED_LDS_KB for tuning
+  int64_t lds_budget = kLdsBudget;
+  if (const char* e = getenv("HBK_EMBED_LDS_KB")) lds_budget = std::min<int64_t>(160, std::max(16, atoi(e))) * 1024;
   x.ipc = a.ipc;
   for (int k = 0; k < kMaxWin; ++k) x.row_off[k] = a.row_off[k];
   x.src_clip_stride = a.src_clip_stride;
@@ -752,7 +972,7 @@ int layout_split(const std::vector<OpInfo>& ops, const std::vector<int>& stage_o
     S.cin = op.cin;
     S.cout = op.cout;
     S.coutr = (op.cout + 7) & ~7;
-    S.act = op.act;
+    S.act = op.act ? ((op.alpha >= 0.f && op.alpha <= 1.f) ? 1 : 2) : 0;
     S.alpha = op.alpha;
     const bool i2c = x.im2col && s == 0;
     const int K0 = op.kh * op.kw * op.cin;
@@ -790,10 +1010,13 @@ int layout_split(const std::vector<OpInfo>& ops, const std::vector<int>& stage_o
         }
         if (src < 0) continue;
         const float v = op.w[size_t(src) * op.cout + n];
-        const _Float16 hi = static_cast<_Float16>(v);
-        wb[S.w_off + size_t(n) * S.wrow + k] = hi;
-        wb[S.w_off + S.w_lo + size_t(n) * S.wrow + k] =
-            static_cast<_Float16>((v - static_cast<float>(hi)) * kLoScale);
+        uint32_t bits;
+        memcpy(&bits, &v, 4);
+        bits &= 0xFFFFE000u;  // hi: v rounded toward zero to 11 bits, as on the device
+        float hv;
+        memcpy(&hv, &bits, 4);
+        wb[S.w_off + size_t(n) * S.wrow + k] = static_cast<_Float16>(hv);
+        wb[S.w_off + S.w_lo + size_t(n) * S.wrow + k] = static_cast<_Float16>(v - hv);
       }
     S.b_off = static_cast<int>(bb.size());
     for (int n = 0; n < rows; ++n) bb.push_back(n < op.cout ? op.b[n] : 0.f);
@@ -816,6 +1039,14 @@ int layout_split(const std::vector<OpInfo>& ops, const std::vector<int>& stage_o
   }
   x.cs0 = x.st[0].cs_in;
   cp.nb = nbmax;
+  std::vector<int> i2c;  // im2col tap offsets into the raw rows (stage-0 input width)
+  if (x.im2col) {
+    const XStage& S = x.st[0];
+    for (int dh = 0; dh < S.kh; ++dh)
+      for (int dw = 0; dw < S.kw; ++dw)
+        for (int ci = 0; ci < S.cin; ++ci) i2c.push_back((dh * d.w + dw) * S.cin + ci);
+  }
+  i2c.push_back(0);
   const Dims od{h / x.out_ph, w / x.out_pw, cin};
   if (od.h <= 0 || od.w <= 0) {
     set_error("hbk: pooling collapses the image");
@@ -877,20 +1108,25 @@ int layout_split(const std::vector<OpInfo>& ops, const std::vector<int>& stage_o
   };
   auto best_band = [&](bool res) {
     for (int b = od.h; b >= 1; --b)
-      if (lds_total(1, b, res) <= kLdsBudget) return b;
+      if (lds_total(1, b, res) <= lds_budget) return b;
     return 0;
   };
   // resident weights unless they cost more than 5 % of the work in halo rows
-  const int band_r = lds_total(1, 1, true) <= kLdsBudget ? best_band(true) : 0;
+  // (HBK_EMBED_WEIGHTS=lds|global overrides, for tuning)
+  const int band_r = lds_total(1, 1, true) <= lds_budget ? best_band(true) : 0;
   const int band_g = best_band(false);
-  const bool resident = band_r > 0 && (band_g == 0 || efficiency(band_r) >= 0.95 * efficiency(band_g));
+  bool resident = band_r > 0 && (band_g == 0 || efficiency(band_r) >= 0.95 * efficiency(band_g));
+  if (const char* wp = getenv("HBK_EMBED_WEIGHTS")) {
+    if (!strcmp(wp, "global") && band_g > 0) resident = false;
+    if (!strcmp(wp, "lds") && band_r > 0) resident = true;
+  }
   int band = resident ? band_r : band_g, G = 1;
   if (band == 0) {
     set_error("hbk: one output row of a chain does not fit in LDS");
     return HBK_ERR_UNSUPPORTED;
   }
   if (band == od.h)
-    while (G < 64 && lds_total(G * 2, band, resident) <= kLdsBudget) G *= 2;
+    while (G < 64 && lds_total(G * 2, band, resident) <= lds_budget) G *= 2;
   x.G = G;
   x.band = band;
   x.n_bands = (od.h + band - 1) / band;
@@ -904,6 +1140,7 @@ int layout_split(const std::vector<OpInfo>& ops, const std::vector<int>& stage_o
   x.w_halfs = resident ? static_cast<int>(wb.size()) : 0;
   x.b_floats = static_cast<int>(bb.size());
   x.vec_out = od.c % 4 == 0;  // cleared at launch for an unaligned output
+  x.raw_vec = x.im2col && x.in_pw == 1 && (x.W_in * x.C_src) % 4 == 0;  // and at launch: alignment
   cp.lds_bytes = size_t(x.lds_k + k_bytes);
   cp.wg = !resident;
   cp.split = true;
@@ -913,17 +1150,21 @@ int layout_split(const std::vector<OpInfo>& ops, const std::vector<int>& stage_o
     return HBK_ERR_UNSUPPORTED;
   }
   // device blob: weights (fp16), biases (f32), group offsets (int)
-  const size_t wsz = wb.size() * 2, bsz = ((bb.size() * 4 + 15) & ~size_t(15)), ksz = kt.size() * 4;
-  hipError_t e = hipMalloc(reinterpret_cast<void**>(&cp.d_blob), wsz + bsz + ksz);
+  const size_t wsz = wb.size() * 2, bsz = ((bb.size() * 4 + 15) & ~size_t(15));
+  const size_t ksz = (kt.size() * 4 + 15) & ~size_t(15), isz = i2c.size() * 4;
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(&cp.d_blob), wsz + bsz + ksz + isz);
   if (e != hipSuccess) return hip_error(e, "hipMalloc chain weights");
   unsigned char* base = reinterpret_cast<unsigned char*>(cp.d_blob);
   e = hipMemcpy(base, wb.data(), wsz, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(base + wsz, bb.data(), bb.size() * 4, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(base + wsz + bsz, kt.data(), ksz, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(base + wsz + bsz, kt.data(), kt.size() * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(base + wsz + bsz + ksz, i2c.data(), isz, hipMemcpyHostToDevice);
   if (e != hipSuccess) return hip_error(e, "copy chain weights");
   x.wblob = reinterpret_cast<const _Float16*>(base);
   x.bblob = reinterpret_cast<const float*>(base + wsz);
   x.ktab = reinterpret_cast<const int*>(base + wsz + bsz);
+  x.i2c_off = reinterpret_cast<const int*>(base + wsz + bsz + ksz);
+  x.i2c_n = static_cast<int>(i2c.size());
   if (cp.lds_bytes > 64 * 1024) {
     e = hipFuncSetAttribute(reinterpret_cast<const void*>(cp.xfn),
                             hipFuncAttributeMaxDynamicSharedMemorySize, int(cp.lds_bytes));
@@ -987,6 +1228,8 @@ int build_segment(const std::vector<OpInfo>& ops, int o0, int o1, Dims in, int i
       Dims od;
       const int rc = layout_split(ops, stage_ops, d, a, cp, od);
       if (rc) return rc;
+      cp.x.dbg_slot = static_cast<int>(prog.chains.size() % 4);
+      if (const char* e = getenv("HBK_DEBUG_SKIP")) cp.x.dbg_skip = atoi(e);
       cp.src_buf = src_buf;
       cp.out_floats = cp.x.out_img_stride * (first ? ipc : 1);
       prog.chains.push_back(cp);
@@ -1172,9 +1415,12 @@ int run_program(const Program& prog, const float* in, int64_t n_units, int64_t i
         }
         x.out = c.dst_buf < 0 ? out + u0 * out_unit_floats : bufs[c.dst_buf];
         if ((reinterpret_cast<uintptr_t>(x.out) & 15) || (x.out_img_stride & 3)) x.vec_out = 0;
+        if ((reinterpret_cast<uintptr_t>(x.in) & 15) || (x.src_clip_stride & 3) || (x.src_row_stride & 3))
+          x.raw_vec = 0;
         x.n_img = nu * imgs_per_unit[k];
         const int64_t tasks = ((x.n_img + x.G - 1) / x.G) * x.n_bands;
-        const int64_t blocks = std::min<int64_t>(tasks, persistent_blocks(2));
+        const int per_cu = std::max<int>(1, std::min<int>(4, int((160 * 1024) / std::max<size_t>(c.lds_bytes, 1))));
+        const int64_t blocks = std::min<int64_t>(tasks, persistent_blocks(per_cu));
         if (blocks <= 0) continue;
         hipLaunchKernelGGL(c.xfn, dim3(unsigned(blocks)), dim3(kXThreads), c.lds_bytes, stream, x);
         HBK_LAUNCH_CHECK("conv_chain_x3_kernel");
@@ -1424,3 +1670,25 @@ int hbk_embed_windows(const hbk_embed_plan* p, const float* windows, int64_t n, 
 }
 
 }  // extern "C"
+
+#ifdef HBK_PHASE_TIMING
+extern "C" int hbk_debug_phase_cycles(unsigned long long* out, int n) {
+  unsigned long long h[64];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(hbk::g_phase_cycles), sizeof(h)) != hipSuccess) return -2;
+  for (int i = 0; i < n && i < 64; ++i) out[i] = h[i];
+  unsigned long long z[64] = {};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(hbk::g_phase_cycles), z, sizeof(z));
+  return 0;
+}
+#endif
+
+#ifdef HBK_TRACE
+extern "C" int hbk_debug_trace(unsigned long long* out, int* counts) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hbk::g_trace), sizeof(unsigned long long) * 4 * 4 * 256) != hipSuccess)
+    return -2;
+  if (hipMemcpyFromSymbol(counts, HIP_SYMBOL(hbk::g_trace_n), sizeof(int) * 16) != hipSuccess) return -2;
+  int z[16] = {};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(hbk::g_trace_n), z, sizeof(z));
+  return 0;
+}
+#endif

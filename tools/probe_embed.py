@@ -12,6 +12,8 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "hey-buddy_amd")]
 os.environ.setdefault("HBK_DEBUG_EMBED", "1")
+if "--phase" in sys.argv:
+    os.environ["HBK_LIB"] = os.path.join(ROOT, "hey-buddy_amd", "lib", "libhbk_phase.so")
 
 import torch  # noqa: E402
 
@@ -24,6 +26,8 @@ def main():
     ap.add_argument("--clips", type=int, default=16384)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--precision", default="both")
+    ap.add_argument("--phase", action="store_true",
+                    help="load lib/libhbk_phase.so and print per-chain phase cycles (wave 0 of each block)")
     a = ap.parse_args()
     g = se20_graph()
     mel = (torch.randn((a.clips, 141, 32), device="cuda") * 2 + 1).contiguous()
@@ -41,6 +45,22 @@ def main():
         tf = 2 * plan.macs_per_clip * a.clips / (ms * 1e-3) / 1e12
         print(f"{p}: {ms:.3f} ms per {a.clips} clips = {tf:.1f} TFLOP/s algorithmic, "
               f"finite={bool(torch.isfinite(out).all())}", flush=True)
+        if a.phase and p == "split":
+            import ctypes
+            from heybuddy._native import lib
+            buf = (ctypes.c_ulonglong * 64)()
+            fn = lib().hbk_debug_phase_cycles
+            fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
+            fn(buf, 64)  # reset after the timed loop
+            plan.clips(mel)
+            torch.cuda.synchronize()
+            fn(buf, 64)
+            for ch in range(4):
+                row = [buf[ch * 16 + i] for i in range(16)]
+                tot = sum(row)
+                if tot:
+                    print(f"chain {ch}: " + " ".join(f"p{i}={v / tot * 100:.1f}%" for i, v in enumerate(row) if v)
+                          + f"  total {tot / 1e6:.1f} Mcyc (sum over blocks, wave 0)", flush=True)
 
 
 if __name__ == "__main__":
