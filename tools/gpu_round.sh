@@ -9,7 +9,7 @@ mkdir -p $OUT
 TAG=${TAG:-r01}
 if [ -z "$SKIP_TESTS" ]; then
   echo "=== tests"
-  timeout -k 10 900 python -m pytest tests -m gpu -x -q > $OUT/tests_$TAG.log 2>&1 || { tail -40 $OUT/tests_$TAG.log; exit 1; }
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/tests_$TAG.log 2>&1 || { tail -40 $OUT/tests_$TAG.log; exit 1; }
   tail -2 $OUT/tests_$TAG.log
   echo "=== smoke"
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$TAG.log 2>&1 || { tail -20 $OUT/smoke_$TAG.log; exit 1; }
