@@ -26,6 +26,10 @@ CFLAGS = [
     "-I", INCLUDE, "-I", CSRC, "-Wall", "-Wno-unused-function",
     "-munsafe-fp-atomics",
 ]
+# Per-file flags. hbk_mel.hip: no SLP vectorisation of scalar f32 code (it packs
+# the mel dot products into v_pk_fma_f32 plus register moves; the complex
+# arithmetic there is already explicit float2 vector code).
+FILE_FLAGS = {"hbk_mel.hip": ("-fno-slp-vectorize",)}
 
 
 def sources() -> list[str]:
@@ -46,7 +50,7 @@ def _compile(src: str, force: bool, obj_dir: str = OBJ, extra: tuple = ()) -> st
         if os.path.getmtime(obj) >= max(os.path.getmtime(src), _headers_mtime()):
             return obj
     lang = ["-x", "hip"] if src.endswith(".hip") else []
-    cmd = [HIPCC, *CFLAGS, *extra, *lang, "-c", src, "-o", obj]
+    cmd = [HIPCC, *CFLAGS, *FILE_FLAGS.get(os.path.basename(src), ()), *extra, *lang, "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

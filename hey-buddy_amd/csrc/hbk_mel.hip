@@ -72,9 +72,31 @@ __device__ __forceinline__ cf w16(int p) {
   }
 }
 
-__device__ __forceinline__ void fft4(cf& a0, cf& a1, cf& a2, cf& a3) {
-  const cf t0 = cadd(a0, a2), t1 = csub(a0, a2);
-  const cf t2 = cadd(a1, a3), t3 = cmul_mi(csub(a1, a3));
+// Scalar-pair complex: the same arithmetic as cf issued as single-lane f32
+// ops instead of v_pk_*_f32 (the v2 kernel picks one with a template argument).
+struct sc {
+  float x, y;
+};
+using hbk::cadd;
+using hbk::cmul;
+using hbk::cmul_mi;
+using hbk::csub;
+__device__ __forceinline__ sc operator+(sc a, sc b) { return {a.x + b.x, a.y + b.y}; }
+__device__ __forceinline__ sc operator-(sc a, sc b) { return {a.x - b.x, a.y - b.y}; }
+__device__ __forceinline__ sc operator*(sc a, sc b) { return {a.x * b.x, a.y * b.y}; }  // elementwise
+__device__ __forceinline__ sc cadd(sc a, sc b) { return a + b; }
+__device__ __forceinline__ sc csub(sc a, sc b) { return a - b; }
+__device__ __forceinline__ sc cmul_mi(sc a) { return {a.y, -a.x}; }
+__device__ __forceinline__ sc cmul(sc a, sc b) {
+  return {fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x)};
+}
+template <class C>
+__device__ __forceinline__ C cpx(cf v) { return C{v.x, v.y}; }
+
+template <class C>
+__device__ __forceinline__ void fft4(C& a0, C& a1, C& a2, C& a3) {
+  const C t0 = cadd(a0, a2), t1 = csub(a0, a2);
+  const C t2 = cadd(a1, a3), t3 = cmul_mi(csub(a1, a3));
   a0 = cadd(t0, t2);
   a2 = csub(t0, t2);
   a1 = cadd(t1, t3);
@@ -82,18 +104,19 @@ __device__ __forceinline__ void fft4(cf& a0, cf& a1, cf& a2, cf& a3) {
 }
 
 // In-register 16-point forward DFT: v[k] <- sum_n v[n] W16^(nk), natural order.
-__device__ __forceinline__ void fft16(cf (&v)[16]) {
+template <class C>
+__device__ __forceinline__ void fft16(C (&v)[16]) {
   // n = 4 m1 + m2: radix-4 over m1 for each m2 -> v[4 l1 + m2] = A[m2][l1]
 #pragma unroll
   for (int m2 = 0; m2 < 4; ++m2) fft4(v[m2], v[4 + m2], v[8 + m2], v[12 + m2]);
 #pragma unroll
   for (int l1 = 1; l1 < 4; ++l1)
 #pragma unroll
-    for (int m2 = 1; m2 < 4; ++m2) v[4 * l1 + m2] = cmul(v[4 * l1 + m2], w16(m2 * l1));
+    for (int m2 = 1; m2 < 4; ++m2) v[4 * l1 + m2] = cmul(v[4 * l1 + m2], cpx<C>(w16(m2 * l1)));
   // radix-4 over m2 for each l1 -> v[4 l1 + l2] = X[l1 + 4 l2]
 #pragma unroll
   for (int l1 = 0; l1 < 4; ++l1) fft4(v[4 * l1 + 0], v[4 * l1 + 1], v[4 * l1 + 2], v[4 * l1 + 3]);
-  cf t[16];
+  C t[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) t[k] = v[4 * (k & 3) + (k >> 2)];
 #pragma unroll
@@ -221,8 +244,211 @@ __global__ void __launch_bounds__(kThreads) mel_frames_kernel(MelArgs a) {
   }
 }
 
+// ------------------------------------------------------------------ v2 ----
+// The same transform, specialised for the filterbanks the reference uses
+// (32 mels reading only bins k < 128, e.g. H0's 60-3800 Hz bank) and cut for
+// LDS traffic / bank conflicts and VALU count, the resources the v1 kernel is
+// bound by (rocprofv3 SQ counters: LDS array busy ~60-75 % of the kernel):
+//  - the window is a per-lane VGPR constant; W256 twiddles, split twiddles
+//    -i W512^k and filter weights are a [entry][lane] LDS table whose b64
+//    reads are conflict-free and broadcast to the wave's 4 frames (v1 reads
+//    its tables with bank conflicts); 8-wave blocks share it, 4 waves / SIMD;
+//  - the real-FFT split's partner Z[256 - k] comes from lane (16 - j) mod 16
+//    of the same frame through two DPP moves (row_mirror, row_ror:1) instead
+//    of a second LDS round trip; lane 0 takes its own register;
+//  - only the 8 blocks of 16 bins the filters read are split and squared;
+//  - a window that is zero on its first and last 32 samples (win_length 400
+//    centred in 512) skips the n1 = 0 and n1 = 15 rows (EDGE0);
+//  - the transpose reads are 16-B ds_read_b128 (rows of 18 complex, frame
+//    regions 9 x 256 B so the two frames of a b128 lane group hit disjoint
+//    banks);
+//  - mel filters are balanced over lanes: lane j computes the narrow filter j
+//    (8 bins) and the wide filter 31 - j (16 bins) from even start bins with
+//    8-B reads; odd frames' power rows
+//    sit 32 dwords up so a lane group's two frames read disjoint banks;
+//  - the 1/2 of the split is folded into the filter weights (x 1/4 on |X|^2,
+//    exact in binary floating point).
+constexpr int kRow2 = 18;
+constexpr int kFrameC2 = 16 * kRow2;  // 288 complex = 2304 B
+constexpr int kTapsA = 8;             // filters 0..15
+constexpr int kTapsB = 16;            // filters 16..31
+constexpr int kBins2 = 128;
+constexpr int kWaves2 = 8;            // 512-thread blocks sharing one constant table
+constexpr int kThreads2 = 64 * kWaves2;
+constexpr int kFramesPerBlock2 = kFramesPerWave * kWaves2;
+constexpr int kBlocksPerCU2 = 2;      // <= 128 VGPRs, 78 KB LDS: 4 waves / SIMD
+
+struct Mel2Args {
+  const float* pcm;
+  float* out;
+  const float* window;  // [512], in_scale folded in
+  const float2* tw256;  // [256] W256^i
+  const float2* twsm;   // [128] -i W512^k
+  const int* mel_lo2;   // [32]: lo(filter j), lo(filter 31 - j) at [j], [16 + j]; even, in-range
+  const float* mel_w2;  // [16][kTapsA] then [16][kTapsB], x 1/4, zero-padded
+  int64_t n_clips;
+  int64_t clip_stride;
+  int64_t n_frames;
+  int hop;
+  float log_floor;
+  float out_scale;  // 10 / out_div
+  float out_add;
+};
+
+// lane j of each 16-lane row receives v from lane (16 - j) mod 16
+__device__ __forceinline__ float from_partner(float v) {
+  int t = __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false);  // row_mirror
+  t = __builtin_amdgcn_mov_dpp(t, 0x121, 0xF, 0xF, false);                               // row_ror:1
+  return __builtin_bit_cast(float, t);
+}
+
+// per-lane constant table in LDS, [entry][lane j] (16-lane rows: conflict-free
+// b64 reads, broadcast over a wave's 4 frames)
+constexpr int kCTw = 0;                   // 16 entries: W256^(j k1)
+constexpr int kCWs = 16;                  // 8 entries: -i W512^(j + 16 k2)
+constexpr int kCWa = 24;                  // kTapsA / 2 pairs: weights of filter j
+constexpr int kCWb = kCWa + kTapsA / 2;   // kTapsB / 2 pairs: weights of filter 31 - j
+constexpr int kCN = kCWb + kTapsB / 2;    // 36 entries = 4.6 KB
+
+template <bool EDGE0, class C>
+__global__ void __launch_bounds__(kThreads2) __attribute__((amdgpu_waves_per_eu(4)))
+mel_frames_v2_kernel(Mel2Args a) {
+  __shared__ __attribute__((aligned(16))) cf s_frame[kFramesPerBlock2 * kFrameC2];
+  __shared__ __attribute__((aligned(16))) cf s_c[kCN * 16];
+
+  const int tid = threadIdx.x;
+  for (int i = tid; i < kCN * 16; i += kThreads2) {
+    const int e = i >> 4, jj = i & 15;
+    cf c;
+    if (e < kCWs) {
+      const float2 t = a.tw256[(jj * e) & 255];
+      c = cf{t.x, t.y};
+    } else if (e < kCWa) {
+      const float2 t = a.twsm[jj + 16 * (e - kCWs)];
+      c = cf{t.x, t.y};
+    } else if (e < kCWb) {
+      c = *reinterpret_cast<const cf*>(a.mel_w2 + jj * kTapsA + 2 * (e - kCWa));
+    } else {
+      c = *reinterpret_cast<const cf*>(a.mel_w2 + 16 * kTapsA + jj * kTapsB + 2 * (e - kCWb));
+    }
+    s_c[i] = c;
+  }
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int slot = wave * kFramesPerWave + (lane >> 4);
+  const int j = lane & 15;
+  const cf* cj = s_c + j;  // entry e of this lane: cj[16 e]
+  C win[16];
+#pragma unroll
+  for (int n1 = 0; n1 < 16; ++n1) win[n1] = cpx<C>(*reinterpret_cast<const cf*>(a.window + 2 * (16 * n1 + j)));
+  __syncthreads();
+
+  const uint32_t total = static_cast<uint32_t>(a.n_clips * a.n_frames);
+  const uint32_t nf = static_cast<uint32_t>(a.n_frames);
+  const uint32_t groups = (total + kFramesPerBlock2 - 1) / kFramesPerBlock2;
+  cf* buf = s_frame + slot * kFrameC2;
+  float* pbuf = reinterpret_cast<float*>(buf) + (slot & 1) * 32;
+  const float* pA = pbuf + a.mel_lo2[j];
+  const float* pB = pbuf + a.mel_lo2[16 + j];
+  constexpr int n1lo = EDGE0 ? 1 : 0, n1hi = EDGE0 ? 15 : 16;
+
+  auto frame_src = [&](uint32_t grp) {
+    uint32_t g = min(grp, groups - 1) * kFramesPerBlock2 + slot;
+    g = g < total ? g : total - 1;
+    const uint32_t clip = g / nf;
+    const uint32_t f = g - clip * nf;
+    return a.pcm + static_cast<int64_t>(clip) * a.clip_stride + static_cast<int64_t>(f) * a.hop + 2 * j;
+  };
+  auto load = [&](const float* src, C (&x)[16]) {
+#pragma unroll
+    for (int n1 = n1lo; n1 < n1hi; ++n1) x[n1] = cpx<C>(*reinterpret_cast<const cf*>(src + 32 * n1));
+  };
+  auto to_log = [&](float acc) {
+    const float c = acc < a.log_floor ? a.log_floor : acc;  // keeps NaN
+    return log10f(c) * a.out_scale + a.out_add;
+  };
+
+  // one group: transform the frames in `cur`, prefetching group grp + stride into `nxt`
+  auto process = [&](uint32_t grp, const C (&cur)[16], C (&nxt)[16]) {
+    C v[16];
+#pragma unroll
+    for (int n1 = 0; n1 < 16; ++n1) v[n1] = (n1 < n1lo || n1 >= n1hi) ? C{0.f, 0.f} : cur[n1] * win[n1];
+    load(frame_src(grp + gridDim.x), nxt);  // prefetch (clamped past the end)
+    fft16(v);
+#pragma unroll
+    for (int k1 = 1; k1 < 16; ++k1) v[k1] = cmul(v[k1], cpx<C>(cj[16 * (kCTw + k1)]));
+#pragma unroll
+    for (int k1 = 0; k1 < 16; ++k1) buf[k1 * kRow2 + j] = cf{v[k1].x, v[k1].y};
+    wave_sync();
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float4 t = *reinterpret_cast<const float4*>(buf + j * kRow2 + 2 * q);
+      v[2 * q] = C{t.x, t.y};
+      v[2 * q + 1] = C{t.z, t.w};
+    }
+    fft16(v);  // v[k2] = Z[j + 16 k2]
+    // 2 X[k] = (Z[k] + Z*[256-k]) + (-i W512^k) (Z[k] - Z*[256-k]),  k = j + 16 k2
+    float p[8];
+#pragma unroll
+    for (int k2 = 0; k2 < 8; ++k2) {
+      const C o = v[15 - k2];
+      C zr = C{from_partner(o.x), from_partner(o.y)};
+      if (j == 0) zr = v[(16 - k2) & 15];
+      const C zc = C{zr.x, -zr.y};  // Z*[256 - k]
+      const C s = v[k2] + zc;
+      const C d = v[k2] - zc;
+      const C X = s + cmul(d, cpx<C>(cj[16 * (kCWs + k2)]));
+      p[k2] = fmaf(X.x, X.x, X.y * X.y);
+    }
+    wave_sync();
+#pragma unroll
+    for (int k2 = 0; k2 < 8; ++k2) pbuf[j + 16 * k2] = p[k2];
+    wave_sync();
+    float accA = 0.f, accB = 0.f;
+#pragma unroll
+    for (int t = 0; t < kTapsA; t += 2) {
+      const float2 pv = *reinterpret_cast<const float2*>(pA + t);
+      const cf w = cj[16 * (kCWa + t / 2)];
+      accA = fmaf(w.x, pv.x, accA);
+      accA = fmaf(w.y, pv.y, accA);
+    }
+#pragma unroll
+    for (int t = 0; t < kTapsB; t += 2) {
+      const float2 pv = *reinterpret_cast<const float2*>(pB + t);
+      const cf w = cj[16 * (kCWb + t / 2)];
+      accB = fmaf(w.x, pv.x, accB);
+      accB = fmaf(w.y, pv.y, accB);
+    }
+    const uint32_t g = grp * kFramesPerBlock2 + slot;
+    if (g < total) {
+      float* o = a.out + static_cast<int64_t>(g) * kMaxMels;
+      o[j] = to_log(accA);
+      o[31 - j] = to_log(accB);
+    }
+    wave_sync();  // the next group's transpose overwrites pbuf
+  };
+
+  // two explicit prefetch buffers (no register copies on the loop back edge)
+  uint32_t grp = blockIdx.x;
+  C xa[16], xb[16];
+  if (grp < groups) load(frame_src(grp), xa);
+  while (grp < groups) {
+    process(grp, xa, xb);
+    grp += gridDim.x;
+    if (grp >= groups) break;
+    process(grp, xb, xa);
+    grp += gridDim.x;
+  }
+}
+
 }  // namespace
 }  // namespace hbk
+
+#ifdef HBK_MEL_PACKED
+#define HBK_MEL_V2(e) (hbk::mel_frames_v2_kernel<e, hbk::cf>)
+#else
+#define HBK_MEL_V2(e) (hbk::mel_frames_v2_kernel<e, hbk::sc>)
+#endif
 
 struct hbk_mel_plan {
   int n_fft, hop, n_mels, taps, nk2, need256;
@@ -232,6 +458,11 @@ struct hbk_mel_plan {
   float2* d_tw512 = nullptr;
   int* d_lo = nullptr;
   float* d_w = nullptr;
+  // v2 (32 mels, bins < 128): -i W512^k, even start bins, x 1/4 weights
+  int v2 = 0, edge0 = 0;
+  float2* d_twsm = nullptr;
+  int* d_lo2 = nullptr;
+  float* d_w2 = nullptr;
 };
 
 extern "C" {
@@ -262,6 +493,29 @@ int hbk_mel_plan_create(const float* window, const float* fbank, int n_fft, int 
     if (hi[m] < 0) { lo[m] = 0; hi[m] = 0; }  // all-zero filter: weights stay 0
     taps = std::max(taps, hi[m] - lo[m] + 1);
   }
+  // v2 layout: 32 mels reading bins < 128 only. Lane j computes filter j from
+  // kTapsA bins and filter 31 - j from kTapsB bins, each from an even start
+  // (8-B LDS pairs) kept inside [0, 128); weights x 1/4, zero outside the filter.
+  int kmax_all = 0;
+  for (int m = 0; m < n_mels; ++m) kmax_all = std::max(kmax_all, hi[m]);
+  bool v2 = n_mels == kMaxMels && kmax_all < kBins2 && !getenv("HBK_MEL_V1");
+  std::vector<int> lo2(kMaxMels, 0);
+  std::vector<float> w2(16 * (kTapsA + kTapsB), 0.f);
+  for (int m = 0; v2 && m < n_mels; ++m) {
+    const int T = m < 16 ? kTapsA : kTapsB;
+    int l = lo[m] & ~1;
+    if (hi[m] - l + 1 > T) {
+      v2 = false;
+      break;
+    }
+    if (l + T > kBins2) l = kBins2 - T;  // even: T is even
+    const int slot_j = m < 16 ? m : 31 - m;
+    lo2[m < 16 ? slot_j : 16 + slot_j] = l;
+    float* w = w2.data() + (m < 16 ? slot_j * kTapsA : 16 * kTapsA + slot_j * kTapsB);
+    for (int t = 0; t < T; ++t) w[t] = 0.25f * fbank[(l + t) * n_mels + m];
+  }
+  bool edge0 = true;
+  for (int i = 0; i < 32; ++i) edge0 = edge0 && window[i] == 0.f && window[n_fft - 1 - i] == 0.f;
   if (taps > kMaxTaps) {
     set_error("hbk: mel filter spans %d bins (> %d supported)", taps, kMaxTaps);
     return HBK_ERR_UNSUPPORTED;
@@ -318,6 +572,24 @@ int hbk_mel_plan_create(const float* window, const float* fbank, int n_fft, int 
     return fail(e, "copy lo");
   if ((e = hipMemcpy(p->d_w, w.data(), w.size() * sizeof(float), hipMemcpyHostToDevice)) != hipSuccess)
     return fail(e, "copy w");
+  if (v2) {
+    std::vector<float2> twsm(kBins2);
+    for (int k = 0; k < kBins2; ++k) {  // -i W512^k = (sin(-2 pi k/512), -cos(-2 pi k/512))
+      const double ang = -2.0 * M_PI * k / 512.0;
+      twsm[k] = make_float2(static_cast<float>(sin(ang)), static_cast<float>(-cos(ang)));
+    }
+    p->v2 = 1;
+    p->edge0 = edge0 ? 1 : 0;
+    if ((e = hipMalloc(&p->d_twsm, kBins2 * sizeof(float2))) != hipSuccess) return fail(e, "hipMalloc twsm");
+    if ((e = hipMalloc(&p->d_lo2, kMaxMels * sizeof(int))) != hipSuccess) return fail(e, "hipMalloc lo2");
+    if ((e = hipMalloc(&p->d_w2, w2.size() * sizeof(float))) != hipSuccess) return fail(e, "hipMalloc w2");
+    if ((e = hipMemcpy(p->d_twsm, twsm.data(), kBins2 * sizeof(float2), hipMemcpyHostToDevice)) != hipSuccess)
+      return fail(e, "copy twsm");
+    if ((e = hipMemcpy(p->d_lo2, lo2.data(), kMaxMels * sizeof(int), hipMemcpyHostToDevice)) != hipSuccess)
+      return fail(e, "copy lo2");
+    if ((e = hipMemcpy(p->d_w2, w2.data(), w2.size() * sizeof(float), hipMemcpyHostToDevice)) != hipSuccess)
+      return fail(e, "copy w2");
+  }
   *plan = p;
   return HBK_OK;
 }
@@ -329,6 +601,9 @@ int hbk_mel_plan_destroy(hbk_mel_plan* p) {
   (void)hipFree(p->d_tw512);
   (void)hipFree(p->d_lo);
   (void)hipFree(p->d_w);
+  (void)hipFree(p->d_twsm);
+  (void)hipFree(p->d_lo2);
+  (void)hipFree(p->d_w2);
   delete p;
   return HBK_OK;
 }
@@ -344,6 +619,36 @@ int hbk_mel_frames(const hbk_mel_plan* plan, const float* pcm, int64_t n_clips, 
   if ((reinterpret_cast<uintptr_t>(pcm) & 7) || (reinterpret_cast<uintptr_t>(out) & 7))
     return arg_error("pcm/out must be 8-byte aligned");
   if (plan->hop * (n_frames - 1) + plan->n_fft > clip_stride) return arg_error("frames exceed clip_stride");
+  const int64_t total = n_clips * n_frames;
+  if (total >= (int64_t(1) << 31)) return arg_error("more than 2^31 frames in one call");
+  if (plan->v2) {
+    const int64_t groups2 = (total + kFramesPerBlock2 - 1) / kFramesPerBlock2;
+    Mel2Args a;
+    a.pcm = pcm;
+    a.out = out;
+    a.window = plan->d_window;
+    a.tw256 = plan->d_tw256;
+    a.twsm = plan->d_twsm;
+    a.mel_lo2 = plan->d_lo2;
+    a.mel_w2 = plan->d_w2;
+    a.n_clips = n_clips;
+    a.clip_stride = clip_stride;
+    a.n_frames = n_frames;
+    a.hop = plan->hop;
+    a.log_floor = plan->log_floor;
+    a.out_scale = 10.f / plan->out_div;
+    a.out_add = plan->out_add;
+    const int64_t blocks = std::min<int64_t>(groups2, persistent_blocks(kBlocksPerCU2));
+    if (plan->edge0)
+      hipLaunchKernelGGL(HBK_MEL_V2(true), dim3(static_cast<unsigned>(blocks)), dim3(kThreads2), 0,
+                         as_stream(stream), a);
+    else
+      hipLaunchKernelGGL(HBK_MEL_V2(false), dim3(static_cast<unsigned>(blocks)), dim3(kThreads2), 0,
+                         as_stream(stream), a);
+    HBK_LAUNCH_CHECK("mel_frames_v2_kernel");
+    return HBK_OK;
+  }
+  const int64_t groups = (total + kFramesPerBlock - 1) / kFramesPerBlock;
   MelArgs a;
   a.pcm = pcm;
   a.out = out;
@@ -363,9 +668,6 @@ int hbk_mel_frames(const hbk_mel_plan* plan, const float* pcm, int64_t n_clips, 
   a.log_floor = plan->log_floor;
   a.out_div = plan->out_div;
   a.out_add = plan->out_add;
-  const int64_t total = n_clips * n_frames;
-  if (total >= (int64_t(1) << 31)) return arg_error("more than 2^31 frames in one call");
-  const int64_t groups = (total + kFramesPerBlock - 1) / kFramesPerBlock;
   const int64_t blocks = std::min<int64_t>(groups, persistent_blocks(kBlocksPerCU));
   hipLaunchKernelGGL(mel_frames_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kThreads), 0,
                      as_stream(stream), a);
