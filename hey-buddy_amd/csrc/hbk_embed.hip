@@ -835,6 +835,299 @@ conv_chain_x3_kernel(XArgs a) {
   }
 }
 
+// ------------------------------------------------------------------- p0 ----
+// Pattern kernel for the chain  conv 3x3 (1 -> C) . conv 1x3 (C -> C) .
+// conv 3x1 (C -> C) . max-pool 2x2  on a fixed input width WI (the SE20
+// prefix's first group: 136 x 32 mel rows -> 66 x 14 x 24, ~55 % of the
+// embedding MACs). Same split-f16 numerics as conv_chain_x3_kernel (3 fp16
+// products per f32-accurate MAC on v_mfma_f32_32x32x16_f16, f32 accumulate),
+// but every shape is a compile-time constant, so the position / tap address
+// math folds to shifts and immediates (the generic kernel spends ~20 VALU
+// instructions per MFMA on runtime index math and SGPR spills):
+//   * stage 0 builds its B fragments straight from the f32 input rows in LDS
+//     (taps 0-4 in the lane's first K half, 5-8 in the second): no im2col
+//     buffer;
+//   * every stage's A fragments (weights) and bias are loaded once per block
+//     and stay in VGPRs (4-wave blocks, 2 waves / SIMD); the bias is the first
+//     MFMA's accumulator input;
+//   * the hi/lo split of each output is v_cvt_pkrtz (hi, round toward zero)
+//     plus v_fma_mix{lo,hi}_f16 (lo = x - hi rounded to fp16);
+//   * one task = one image x BAND pooled rows (4 waves, 32-position tiles
+//     round-robin over the waves), 2 blocks / CU.
+constexpr int kP0Waves = 4;
+constexpr int kP0Threads = 64 * kP0Waves;
+
+struct P0Args {
+  const float* in;          // [img][rows][WI] f32, row stride WI
+  float* out;               // [img][H_out][W2 / 2][C] f32
+  const _Float16* w;        // stage s: hi [32][16 ks_s], lo [32][16 ks_s]
+  const float* bias;        // [3][32] (rows >= C are 0)
+  int64_t n_img;
+  int64_t src_img_stride;   // floats
+  int H_in;                 // valid input rows per image
+  int H_out;                // pooled output rows per image
+  int n_bands;
+  float alpha;              // LeakyReLU slope of all three convs (LEAKY kernels)
+};
+
+template <int WI, int C, int BAND>
+struct P0Geo {
+  static constexpr int W0 = WI - 2, W1 = W0 - 2, W2 = W1;
+  static constexpr int R2 = 2 * BAND, R1 = R2 + 2, R0 = R1, RI = R0 + 2;
+  static constexpr int CS = ((C / 8) % 2 == 0) ? C + 8 : C;  // odd number of 16-B groups per position
+  static constexpr int M0 = R0 * W0, M1 = R1 * W1, M2 = R2 * W2;
+  static constexpr int T0 = (M0 + 31) / 32, T1 = (M1 + 31) / 32, T2 = (M2 + 31) / 32;
+  static constexpr int KS = (3 * C + 15) / 16;  // K steps of stages 1 and 2
+  static constexpr int RAW = RI * WI * 4;
+  static constexpr int S0B = M0 * CS * 4, S1B = M1 * CS * 4, S2B = M2 * C * 4;
+  static constexpr int XB = ((RAW > S1B ? RAW : S1B) + 15) & ~15;  // raw input, then stage-1 output
+  static constexpr int YB = ((S0B > S2B ? S0B : S2B) + 15) & ~15;  // stage-0 output, then stage-2 f32
+  static constexpr int LDS = XB + YB;
+  static constexpr int WOFF1 = 2 * 32 * 16, WOFF2 = WOFF1 + 2 * 32 * 16 * KS;  // fp16 offsets
+  static constexpr int WHALFS = WOFF2 + 2 * 32 * 16 * KS;
+};
+
+// hi = v rounded toward zero to fp16, lo = (v - hi) rounded to fp16; two values, packed
+__device__ __forceinline__ void split2_mix(float a, float b, uint32_t& hi, uint32_t& lo) {
+  hi = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(a, b));
+  uint32_t l = 0;
+  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "+v"(l) : "v"(a), "v"(hi));
+  asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(l) : "v"(b), "v"(hi));
+  lo = l;
+}
+
+// LEAKY: every conv of the chain is LeakyReLU with 0 <= alpha <= 1 (max(v, alpha v)); else identity
+// (v_max_f32 through asm: fmaxf on MFMA results gets a canonicalising v_max in
+// front of it; both operands are NaN for a NaN input, so NaN propagates)
+template <bool LEAKY>
+__device__ __forceinline__ float p0_act(float v, float alpha) {
+  if (!LEAKY) return v;
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(v), "v"(v * alpha));
+  return r;
+}
+
+// bias of this lane's accumulator rows (channels 8 q + 4 khalf + j, register 4 q + j)
+__device__ __forceinline__ f16x p0_bias(const float* b, int khalf) {
+  f16x v;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 t = *reinterpret_cast<const float4*>(b + 8 * q + 4 * khalf);
+    v[4 * q] = t.x;
+    v[4 * q + 1] = t.y;
+    v[4 * q + 2] = t.z;
+    v[4 * q + 3] = t.w;
+  }
+  return v;
+}
+
+// activation + split of a finished tile into the hi / lo planes at position p
+template <int C, int CS, bool LEAKY>
+__device__ __forceinline__ void p0_store_planes(const f16x& acc, int p, int khalf, _Float16* oh, _Float16* ol,
+                                                float alpha) {
+#pragma unroll
+  for (int q = 0; q < C / 8; ++q) {
+    float v[4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) v[jj] = p0_act<LEAKY>(acc[4 * q + jj], alpha);
+    uint32_t h01, l01, h23, l23;
+    split2_mix(v[0], v[1], h01, l01);
+    split2_mix(v[2], v[3], h23, l23);
+    const int o = p * CS + 8 * q + 4 * khalf;
+    *reinterpret_cast<uint2*>(oh + o) = uint2{h01, h23};
+    *reinterpret_cast<uint2*>(ol + o) = uint2{l01, l23};
+  }
+}
+
+// Stage 1 (1x3, ST = 1: grid R0 x W0 -> R1 x W1, planes out) or stage 2
+// (3x1, ST = 2: R1 x W1 -> R2 x W2, f32 out) of a task; K = tap * C + ci.
+// A fragments (hi, lo) and bias of stage ST for this lane, loaded ahead of use
+template <int KS>
+struct P0W {
+  h8 ah[KS], al[KS];
+  f16x bias;
+};
+template <int WI, int C, int BAND, int ST>
+__device__ __forceinline__ P0W<P0Geo<WI, C, BAND>::KS> p0_load_w(const P0Args& a, int r32, int khalf) {
+  using G = P0Geo<WI, C, BAND>;
+  P0W<G::KS> w;
+  const _Float16* wp = a.w + (ST == 1 ? G::WOFF1 : G::WOFF2) + r32 * (16 * G::KS) + 8 * khalf;
+#pragma unroll
+  for (int ks = 0; ks < G::KS; ++ks) {
+    w.ah[ks] = *reinterpret_cast<const h8*>(wp + 16 * ks);
+    w.al[ks] = *reinterpret_cast<const h8*>(wp + 32 * 16 * G::KS + 16 * ks);
+  }
+  w.bias = p0_bias(a.bias + 32 * ST, khalf);
+  return w;
+}
+
+template <int WI, int C, int BAND, int ST, bool LEAKY>
+__device__ __forceinline__ void p0_stage12(const P0Args& a, const P0W<P0Geo<WI, C, BAND>::KS>& W,
+                                           const _Float16* xh_, const _Float16* xl_, _Float16* oh, _Float16* ol,
+                                           float* of, int wave, int r32, int khalf) {
+  using G = P0Geo<WI, C, BAND>;
+  constexpr int M = ST == 1 ? G::M1 : G::M2, T = ST == 1 ? G::T1 : G::T2;
+  constexpr int Wout = ST == 1 ? G::W1 : G::W2, Win = ST == 1 ? G::W0 : G::W1;
+  constexpr int TAPSTRIDE = ST == 1 ? G::CS : G::W1 * G::CS;  // fp16 between taps in the input grid
+  const float alpha = a.alpha;
+  // Software pipeline over this wave's tiles: the epilogue (activation, split,
+  // LDS stores) of tile t - 1 is issued in the same block as tile t's MFMA
+  // chain, so its VALU work fills the MFMA issue gaps.
+  auto load = [&](int t, int ks, h8& xh, h8& xl) {
+    const int p = min(t * 32 + r32, M - 1);
+    const int y = p / Wout, x = p - y * Wout;
+    // this lane's 8-channel group: K = 16 ks + 8 khalf (groups past 3 C read group 0; weights 0)
+    const int ka = 16 * ks < 3 * C ? 16 * ks : 0;
+    const int kb = 16 * ks + 8 < 3 * C ? 16 * ks + 8 : 0;
+    const int oa = (ka / C) * TAPSTRIDE + ka % C, ob = (kb / C) * TAPSTRIDE + kb % C;
+    const int o = (y * Win + x) * G::CS + (khalf ? ob : oa);
+    xh = *reinterpret_cast<const h8*>(xh_ + o);
+    xl = *reinterpret_cast<const h8*>(xl_ + o);
+  };
+  auto epilogue = [&](int t, const f16x& acc) {
+    const int pp = t * 32 + r32;
+    if (pp >= M) return;
+    if (ST == 1) {
+      p0_store_planes<C, G::CS, LEAKY>(acc, pp, khalf, oh, ol, alpha);
+    } else {
+#pragma unroll
+      for (int q = 0; q < C / 8; ++q) {
+        float4 v;
+        v.x = p0_act<LEAKY>(acc[4 * q], alpha);
+        v.y = p0_act<LEAKY>(acc[4 * q + 1], alpha);
+        v.z = p0_act<LEAKY>(acc[4 * q + 2], alpha);
+        v.w = p0_act<LEAKY>(acc[4 * q + 3], alpha);
+        *reinterpret_cast<float4*>(of + pp * C + 8 * q + 4 * khalf) = v;
+      }
+    }
+  };
+  f16x prev;
+  int tprev = -1;
+  for (int t = wave; t < T; t += kP0Waves) {
+    h8 xh[G::KS], xl[G::KS];
+#pragma unroll
+    for (int ks = 0; ks < G::KS; ++ks) load(t, ks, xh[ks], xl[ks]);
+    f16x acc = W.bias;
+#pragma unroll
+    for (int ks = 0; ks < G::KS; ++ks) {
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(W.ah[ks], xh[ks], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(W.ah[ks], xl[ks], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(W.al[ks], xh[ks], acc, 0, 0, 0);
+    }
+    if (tprev >= 0) epilogue(tprev, prev);
+    prev = acc;
+    tprev = t;
+  }
+  if (tprev >= 0) epilogue(tprev, prev);
+}
+
+template <int WI, int C, int BAND, bool LEAKY>
+__global__ void __launch_bounds__(kP0Threads) __attribute__((amdgpu_waves_per_eu(2)))
+p0_chain_kernel(P0Args a) {
+  using G = P0Geo<WI, C, BAND>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char p0mem[];
+  float* raw = reinterpret_cast<float*>(p0mem);
+  _Float16* s1h = reinterpret_cast<_Float16*>(p0mem);
+  _Float16* s1l = s1h + G::M1 * G::CS;
+  _Float16* s0h = reinterpret_cast<_Float16*>(p0mem + G::XB);
+  _Float16* s0l = s0h + G::M0 * G::CS;
+  float* s2 = reinterpret_cast<float*>(p0mem + G::XB);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r32 = lane & 31, khalf = lane >> 5;
+  const int n_tasks = static_cast<int>(a.n_img) * a.n_bands;
+
+  // the task's input rows (RI x WI floats = RI * WI / 4 float4, one per thread
+  // while it fits) are loaded one task ahead into registers
+  constexpr int kRawV = G::RI * WI / 4;
+  constexpr int kRawPer = (kRawV + kP0Threads - 1) / kP0Threads;
+  float4 rawv[kRawPer];
+  auto load_raw = [&](int task) {
+    const int img = task / a.n_bands, band = task - img * a.n_bands;
+    const float* src = a.in + static_cast<int64_t>(img) * a.src_img_stride;
+#pragma unroll
+    for (int u = 0; u < kRawPer; ++u) {
+      const int i = tid + u * kP0Threads;
+      if (i < kRawV) {
+        const int r = i / (WI / 4), c4 = i - r * (WI / 4);
+        const int rr = min(band * G::R2 + r, a.H_in - 1);
+        rawv[u] = *reinterpret_cast<const float4*>(src + static_cast<int64_t>(rr) * WI + 4 * c4);
+      }
+    }
+  };
+  if (static_cast<int>(blockIdx.x) < n_tasks) load_raw(blockIdx.x);
+  // every stage's A fragments and bias stay in VGPRs for the whole kernel
+  const _Float16* wp0 = a.w + r32 * 16 + 8 * khalf;
+  const h8 a0h = *reinterpret_cast<const h8*>(wp0), a0l = *reinterpret_cast<const h8*>(wp0 + 32 * 16);
+  const f16x b0 = p0_bias(a.bias, khalf);
+  const auto W1 = p0_load_w<WI, C, BAND, 1>(a, r32, khalf);
+  const auto W2 = p0_load_w<WI, C, BAND, 2>(a, r32, khalf);
+
+  for (int task = blockIdx.x; task < n_tasks; task += gridDim.x) {
+    const int img = task / a.n_bands, band = task - img * a.n_bands;
+    __syncthreads();  // the previous task's readers are done
+    // 1) input rows [row0, row0 + RI) (clamped to the image) -> raw; prefetch the next task's
+#pragma unroll
+    for (int u = 0; u < kRawPer; ++u) {
+      const int i = tid + u * kP0Threads;
+      if (i < kRawV) *reinterpret_cast<float4*>(raw + 4 * i) = rawv[u];
+    }
+    if (task + static_cast<int>(gridDim.x) < n_tasks) load_raw(task + gridDim.x);
+    __syncthreads();
+    // 2) stage 0: 3x3, 1 -> C; B fragments straight from the f32 rows
+    //    (taps 0-4 in the first K half, 5-8 and a zero in the second)
+    {
+      for (int t = wave; t < G::T0; t += kP0Waves) {
+        const int pp = t * 32 + r32, p = min(pp, G::M0 - 1);
+        const int y = p / G::W0, x = p - y * G::W0;
+        const float* rp = raw + y * WI + x;
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+          const int t1 = 5 + i < 9 ? 5 + i : 0;
+          v[i] = rp[khalf ? (t1 / 3) * WI + t1 % 3 : (i / 3) * WI + i % 3];
+        }
+        if (khalf) v[4] = 0.f;
+        v[5] = v[6] = v[7] = 0.f;
+        uint32_t hb[4], lb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) split2_mix(v[2 * i], v[2 * i + 1], hb[i], lb[i]);
+        const h8 xh = __builtin_bit_cast(h8, uint4{hb[0], hb[1], hb[2], hb[3]});
+        const h8 xl = __builtin_bit_cast(h8, uint4{lb[0], lb[1], lb[2], lb[3]});
+        f16x acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h, xh, b0, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h, xl, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0l, xh, acc, 0, 0, 0);
+        if (pp < G::M0) p0_store_planes<C, G::CS, LEAKY>(acc, p, khalf, s0h, s0l, a.alpha);
+      }
+    }
+    __syncthreads();
+    p0_stage12<WI, C, BAND, 1, LEAKY>(a, W1, s0h, s0l, s1h, s1l, nullptr, wave, r32, khalf);
+    __syncthreads();
+    p0_stage12<WI, C, BAND, 2, LEAKY>(a, W2, s1h, s1l, nullptr, nullptr, s2, wave, r32, khalf);
+    __syncthreads();
+    // 3) 2x2 max-pool of the stage-2 rows -> the band's BAND output rows
+    {
+      constexpr int PW = G::W2 / 2, C4 = C / 4;
+      float* dst = a.out + static_cast<int64_t>(img) * a.H_out * PW * C;
+      for (int i = tid; i < BAND * PW * C4; i += kP0Threads) {
+        const int c4 = i % C4, rest = i / C4, px = rest % PW, py = rest / PW;
+        const int orow = band * BAND + py;
+        if (orow >= a.H_out) continue;
+        const float* q0 = s2 + ((2 * py) * G::W2 + 2 * px) * C + 4 * c4;
+        const float4 v00 = *reinterpret_cast<const float4*>(q0);
+        const float4 v01 = *reinterpret_cast<const float4*>(q0 + C);
+        const float4 v10 = *reinterpret_cast<const float4*>(q0 + G::W2 * C);
+        const float4 v11 = *reinterpret_cast<const float4*>(q0 + G::W2 * C + C);
+        float4 m;
+        m.x = nan_max(nan_max(v00.x, v01.x), nan_max(v10.x, v11.x));
+        m.y = nan_max(nan_max(v00.y, v01.y), nan_max(v10.y, v11.y));
+        m.z = nan_max(nan_max(v00.z, v01.z), nan_max(v10.z, v11.z));
+        m.w = nan_max(nan_max(v00.w, v01.w), nan_max(v10.w, v11.w));
+        *reinterpret_cast<float4*>(dst + (static_cast<int64_t>(orow) * PW + px) * C + 4 * c4) = m;
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ host ----
 
 struct OpInfo {
@@ -863,6 +1156,13 @@ struct ChainPlan {
   int dst_buf = -1;          // -1: the call's output
   int64_t out_floats = 0;    // per source clip (clip path) or per window
   double macs_per_img = 0;   // algorithmic MACs per image of this chain
+  // pattern kernel (p0_chain_kernel) for this chain, if it matches; the split
+  // plan above stays as the fallback for unaligned buffers
+  void (*p0fn)(P0Args) = nullptr;
+  P0Args p0{};
+  size_t p0_lds = 0;
+  int p0_blocks_per_cu = 0;
+  void* d_p0 = nullptr;
 };
 
 struct Program {
@@ -1180,6 +1480,91 @@ int layout_split(const std::vector<OpInfo>& ops, const std::vector<int>& stage_o
   return HBK_OK;
 }
 
+// The p0 pattern: [3x3 (1 -> C), 1x3 (C -> C), 3x1 (C -> C)] + output pool 2x2
+// on input width 32, C = 24, one image per source clip; all convs LeakyReLU
+// with one slope in [0, 1], or all linear. Packs the weights / biases and
+// sizes the grid; returns false (generic kernel) when the chain differs.
+constexpr int kP0W = 32, kP0C = 24, kP0Band = 6;
+using P0G = P0Geo<kP0W, kP0C, kP0Band>;
+
+bool plan_p0(const std::vector<OpInfo>& ops, const std::vector<int>& st, const ChainArgs& a, Dims d, Dims od,
+             ChainPlan& cp) {
+  if (getenv("HBK_EMBED_NO_P0")) return false;
+  if (st.size() != 3 || a.ipc != 1 || a.C_src != 1 || a.in_ph != 1 || a.in_pw != 1) return false;
+  if (a.out_ph != 2 || a.out_pw != 2 || d.w != kP0W || a.src_row_stride != kP0W) return false;
+  const OpInfo &o0 = ops[st[0]], &o1 = ops[st[1]], &o2 = ops[st[2]];
+  const int C = kP0C;
+  if (!(o0.kh == 3 && o0.kw == 3 && o0.cin == 1 && o0.cout == C)) return false;
+  if (!(o1.kh == 1 && o1.kw == 3 && o1.cin == C && o1.cout == C)) return false;
+  if (!(o2.kh == 3 && o2.kw == 1 && o2.cin == C && o2.cout == C)) return false;
+  const bool leaky = o0.act != 0;
+  for (const OpInfo* o : {&o0, &o1, &o2}) {
+    if ((o->act != 0) != leaky) return false;
+    if (leaky && (o->alpha != o0.alpha || !(o->alpha >= 0.f && o->alpha <= 1.f))) return false;
+  }
+  if (od.h != (d.h - 4) / 2 || od.w != (d.w - 4) / 2 || od.c != C) return false;
+  // weights: stage s = hi [32][16 ks_s] then lo; K of stage 0 = taps 0-4 | pad | taps 5-8 | pad
+  std::vector<_Float16> w(P0G::WHALFS, static_cast<_Float16>(0.f));
+  auto put = [&](int off, int ks, int n, int k, float v) {
+    uint32_t bits;
+    memcpy(&bits, &v, 4);
+    bits &= 0xFFFFE000u;
+    float hv;
+    memcpy(&hv, &bits, 4);
+    w[off + n * 16 * ks + k] = static_cast<_Float16>(hv);
+    w[off + 32 * 16 * ks + n * 16 * ks + k] = static_cast<_Float16>(v - hv);
+  };
+  for (int n = 0; n < C; ++n) {
+    for (int k = 0; k < 16; ++k) {
+      const int tap = k < 5 ? k : (k >= 8 && k < 12 ? k - 3 : -1);
+      if (tap >= 0) put(0, 1, n, k, o0.w[size_t(tap) * C + n]);
+    }
+    for (int k = 0; k < 3 * C; ++k) {
+      put(P0G::WOFF1, P0G::KS, n, k, o1.w[size_t(k) * C + n]);  // HWIO: (tap * C + ci) * C + n
+      put(P0G::WOFF2, P0G::KS, n, k, o2.w[size_t(k) * C + n]);
+    }
+  }
+  std::vector<float> b(96, 0.f);
+  for (int n = 0; n < C; ++n) {
+    b[n] = o0.b[n];
+    b[32 + n] = o1.b[n];
+    b[64 + n] = o2.b[n];
+  }
+  const size_t wbytes = (w.size() * 2 + 15) & ~size_t(15);
+  hipError_t e = hipMalloc(&cp.d_p0, wbytes + b.size() * 4);
+  if (e == hipSuccess) e = hipMemcpy(cp.d_p0, w.data(), w.size() * 2, hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = hipMemcpy(static_cast<unsigned char*>(cp.d_p0) + wbytes, b.data(), b.size() * 4, hipMemcpyHostToDevice);
+  cp.p0fn = leaky ? p0_chain_kernel<kP0W, kP0C, kP0Band, true> : p0_chain_kernel<kP0W, kP0C, kP0Band, false>;
+  cp.p0_lds = P0G::LDS;
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(cp.p0fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            int(cp.p0_lds));
+  int per_cu = 0;
+  if (e == hipSuccess)
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(cp.p0fn), kP0Threads,
+                                                     cp.p0_lds);
+  if (e != hipSuccess || per_cu < 1) {
+    (void)hipGetLastError();
+    if (cp.d_p0) (void)hipFree(cp.d_p0);
+    cp.d_p0 = nullptr;
+    cp.p0fn = nullptr;
+    return false;
+  }
+  cp.p0_blocks_per_cu = per_cu;
+  P0Args& p = cp.p0;
+  p.w = static_cast<const _Float16*>(cp.d_p0);
+  p.bias = reinterpret_cast<const float*>(static_cast<unsigned char*>(cp.d_p0) + wbytes);
+  p.H_in = d.h;
+  p.H_out = od.h;
+  p.n_bands = (od.h + kP0Band - 1) / kP0Band;
+  p.alpha = leaky ? o0.alpha : 0.f;
+  if (getenv("HBK_DEBUG_EMBED"))
+    fprintf(stderr, "hbk p0 chain: %dx%dx1 -> %dx%dx%d, band %d (%d bands), LDS %zu B, %d blocks/CU\n", d.h, d.w,
+            od.h, od.w, od.c, kP0Band, p.n_bands, cp.p0_lds, per_cu);
+  return true;
+}
+
 // Builds the chains for ops [o0, o1) applied to images of dims `in`, reading
 // image i from row_off[i % ipc] of source clip i / ipc.
 int build_segment(const std::vector<OpInfo>& ops, int o0, int o1, Dims in, int ipc,
@@ -1228,6 +1613,7 @@ int build_segment(const std::vector<OpInfo>& ops, int o0, int o1, Dims in, int i
       Dims od;
       const int rc = layout_split(ops, stage_ops, d, a, cp, od);
       if (rc) return rc;
+      plan_p0(ops, stage_ops, a, d, od, cp);
       cp.x.dbg_slot = static_cast<int>(prog.chains.size() % 4);
       if (const char* e = getenv("HBK_DEBUG_SKIP")) cp.x.dbg_skip = atoi(e);
       cp.src_buf = src_buf;
@@ -1405,6 +1791,23 @@ int run_program(const Program& prog, const float* in, int64_t n_units, int64_t i
     float* bufs[2] = {ws, ws + chunk * buf_unit_floats[0]};
     for (size_t k = 0; k < prog.chains.size(); ++k) {
       const ChainPlan& c = prog.chains[k];
+      if (c.p0fn) {
+        P0Args pa = c.p0;
+        pa.in = c.src_buf < 0 ? in + u0 * in_unit_stride : bufs[c.src_buf];
+        pa.src_img_stride = c.src_buf < 0 ? in_unit_stride : c.x.src_clip_stride;
+        pa.out = c.dst_buf < 0 ? out + u0 * out_unit_floats : bufs[c.dst_buf];
+        pa.n_img = nu * imgs_per_unit[k];
+        const bool aligned = !(reinterpret_cast<uintptr_t>(pa.in) & 15) && !(pa.src_img_stride & 3) &&
+                             !(reinterpret_cast<uintptr_t>(pa.out) & 15);
+        if (aligned && pa.n_img * pa.n_bands < (int64_t(1) << 31)) {
+          const int64_t tasks = pa.n_img * pa.n_bands;
+          const int64_t blocks = std::min<int64_t>(tasks, persistent_blocks(c.p0_blocks_per_cu));
+          if (blocks <= 0) continue;
+          hipLaunchKernelGGL(c.p0fn, dim3(unsigned(blocks)), dim3(kP0Threads), c.p0_lds, stream, pa);
+          HBK_LAUNCH_CHECK("p0_chain_kernel");
+          continue;
+        }
+      }
       if (c.split) {
         XArgs x = c.x;
         if (c.src_buf < 0) {
@@ -1573,7 +1976,10 @@ int hbk_embed_plan_create_ex(const hbk_graph_op* ops, int32_t n_ops, int32_t in_
 int hbk_embed_plan_destroy(hbk_embed_plan* p) {
   if (!p) return HBK_OK;
   for (auto* prog : {&p->clip_prog, &p->win_prog})
-    for (auto& c : prog->chains) (void)hipFree(c.d_blob);
+    for (auto& c : prog->chains) {
+      (void)hipFree(c.d_blob);
+      if (c.d_p0) (void)hipFree(c.d_p0);
+    }
   delete p;
   return HBK_OK;
 }
