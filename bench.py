@@ -68,13 +68,14 @@ def parse():
 
 
 def load_traffic(path, kernel_substr):
-    """HBM bytes per step of the kernels whose name contains kernel_substr,
-    from a tools/pmc_summary.py JSON (FETCH_SIZE doubled per the gfx950
-    calibration + WRITE_SIZE), or None."""
+    """HBM bytes per step of the kernels whose name contains kernel_substr (a
+    string or a tuple of alternatives), from a tools/pmc_summary.py JSON
+    (FETCH_SIZE doubled per the gfx950 calibration + WRITE_SIZE), or None."""
+    subs = (kernel_substr,) if isinstance(kernel_substr, str) else tuple(kernel_substr)
     try:
         with open(path) as f:
             d = json.load(f)
-        v = [k for name, k in d.get("kernels", {}).items() if kernel_substr in name]
+        v = [k for name, k in d.get("kernels", {}).items() if any(s in name for s in subs)]
         if v:
             return sum(k["hbm_bytes_per_step"] for k in v)
     except (OSError, ValueError, KeyError):
@@ -199,15 +200,16 @@ def setup_featurize(args, dev, rank, world, seed):
 
     def roofline(name, ms, pmc):
         if name == "mel":
-            return roof("mel_frames_kernel (hbk_mel_frames, 1 launch per step)", "hbm",
+            return roof("mel_frames_v2_kernel (hbk_mel_frames, 1 launch per step)", "hbm",
                         n * (MEL_READ_SAMPLES * 4 + N_FRAMES * 32 * 4), ms, "GB/s", load_traffic(pmc, "mel_frames"),
                         algorithmic_bytes_per_clip=MEL_READ_SAMPLES * 4 + N_FRAMES * 32 * 4)
         if name == "embed":
             split = eplan.precision == "split"
-            kname = "conv_chain_x3_kernel" if split else "conv_chain_kernel"
+            kname = "p0_chain_kernel + conv_chain_x3_kernel" if split else "conv_chain_kernel"
             return roof("%s (hbk_embed_clips, %s: %d chained launches per %d-clip chunk)"
                         % (kname, eplan.precision, eplan.n_chains, min(n, 16384)), "mfma",
-                        2.0 * eplan.macs_per_clip * n, ms, "TFLOP/s", load_traffic(pmc, "conv_chain"),
+                        2.0 * eplan.macs_per_clip * n, ms, "TFLOP/s",
+                        load_traffic(pmc, ("conv_chain", "p0_chain")),
                         peak=SPLIT_PEAK_TFLOPS if split else FP32_MFMA_PEAK_TFLOPS,
                         peak_basis=("f16 dense MFMA peak / 3 (hi*hi + hi*lo + lo*hi per f32-accurate MAC)"
                                     if split else "f32-input MFMA dense peak"),
