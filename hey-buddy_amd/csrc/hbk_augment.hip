@@ -8,12 +8,14 @@
 //   load x (and the clip's noise segment, in registers) -> E_x, E_n ->
 //   y = x + 10^((10 log10(E_x/E_n) - snr)/20) n -> a_in = mean|y|
 //   circular convolution with the batch's IR kernel of length T = 23040:
-//     z[n] = y[2n] + i y[2n+1], a 11520-point complex FFT done four-step as
-//     256 x 45 in LDS: 45 column FFT-256s (16 lanes each, FFT16 x FFT16 in
-//     VGPRs), twiddle W_M^(n2 k1), 256 row DFT-45s (one thread each, 5x3x3 in
-//     VGPRs) -> Z in (k1, k2) order; the real-FFT split, * H[k], and the
-//     inverse split on (k, M-k) pairs; the inverse transform with the steps
-//     reversed lands back in natural order.
+//     z[n] = y[2n] + i y[2n+1], an 11520-point complex FFT done in place in
+//     LDS as four mixed-radix decimation-in-frequency passes 16 x 16 x 9 x 5
+//     (720, 720, 1280 and 2304 independent DFTs per pass, one per thread and
+//     round, radix-16 / 9 / 5 in VGPRs); twiddles W_M^e = HI[e >> 7] LO[e & 127]
+//     from two small LDS tables. Z lands in digit-reversed order (zaddr); the
+//     real-FFT split, * H[k] and the inverse split run on (k, M-k) pairs; the
+//     inverse transform is the passes reversed (decimation in time, conjugate
+//     twiddles) and lands back in natural order.
 //   y <- a_in * y / (mean|y| + 1e-14), store.
 // The IR spectrum H (one per batch) comes from the same transform run on the
 // rotated kernel [ir[d:], 0..., ir[:d]] (hbk_reverb_spectrum).
@@ -28,9 +30,7 @@ namespace {
 
 constexpr int kT = 23040;        // clip length (1.44 s @ 16 kHz, augmented.py:31)
 constexpr int kM = kT / 2;       // complex FFT length
-constexpr int kR = 256;          // rows of the four-step matrix (FFT-256 length)
-constexpr int kC = 45;           // columns (DFT-45 length)
-constexpr int kThreads = 512;    // 32 column FFTs (16 lanes each) per pass
+constexpr int kThreads = 1024;   // 16 waves: one clip per CU (92 KB of LDS)
 
 // ---- small DFTs in registers (constant twiddles) --------------------------
 template <bool INV>
@@ -143,98 +143,108 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Column FFT-256 of column n2 (stride kC in z), 16 lanes (j = 0..15).
-// tw256: W_256^e table (or conjugate for INV).
+// Two-level twiddle table in LDS: W_M^e = hi[e >> 7] * lo[e & 127], e < kM.
+constexpr int kTwLo = 128, kTwHi = kM / kTwLo;  // 128 x 90
+static_assert(kTwLo * kTwHi == kM, "twiddle split");
+
 template <bool INV>
-__device__ __forceinline__ void column_fft256(cf* z, int n2, int j, const cf* tw256) {
-  cf v[16];
-#pragma unroll
-  for (int a = 0; a < 16; ++a) v[a] = z[(16 * a + j) * kC + n2];
-  fft16v<INV>(v);
-#pragma unroll
-  for (int k = 1; k < 16; ++k) {
-    const cf w = tw256[j * k];
-    v[k] = cmul(v[k], INV ? cf{w.x, -w.y} : w);
-  }
-  wave_sync();
-#pragma unroll
-  for (int k = 0; k < 16; ++k) z[(16 * k + j) * kC + n2] = v[k];
-  wave_sync();
-#pragma unroll
-  for (int b = 0; b < 16; ++b) v[b] = z[(16 * j + b) * kC + n2];
-  fft16v<INV>(v);
-  wave_sync();
-#pragma unroll
-  for (int k = 0; k < 16; ++k) z[(j + 16 * k) * kC + n2] = v[k];
+__device__ __forceinline__ cf twiddle(const cf* thi, const cf* tlo, int e) {
+  const cf w = cmul(thi[e >> 7], tlo[e & (kTwLo - 1)]);
+  return INV ? cf{w.x, -w.y} : w;
 }
 
-// Row k1: (forward) twiddle W_M^(n2 k1) then DFT-45; (inverse) IDFT-45 then
-// conj twiddle. DFT-45 as 5 x 9 (n = 5p + q, k = r + 9s), reading the row
-// straight from LDS and writing results straight back, so that only the 5 x 9
-// intermediate is live in VGPRs.
-template <bool INV>
-__device__ __forceinline__ void row_dft45(cf* z, int k1, const cf* twm) {
-  cf* row = z + k1 * kC;
-  cf a[5][9];
+template <int R, bool INV>
+__device__ __forceinline__ void dftr(cf (&v)[R]) {
+  if constexpr (R == 16) fft16v<INV>(v);
+  else if constexpr (R == 9) dft9<INV>(v);
+  else dft5<INV>(v);
+}
+
+// One in-place pass of radix R over span L (blocks of R L elements): task
+// (blk, i) owns elements blk R L + i + L m, m < R. Forward (DIF): DFT-R, then
+// output k times W_M^(S i k). Inverse (DIT): input k times conj W_M^(S i k),
+// then the inverse DFT-R. Independent tasks, so one barrier per pass.
+template <int R, int L, int S, bool INV>
+__device__ __forceinline__ void pass(cf* z, const cf* thi, const cf* tlo) {
+  constexpr int kTasks = kM / R;
+  // opaque copy of the thread id: keeps the per-pass index math inside the
+  // clip loop instead of hoisted (as dozens of live VGPRs) out of it
+  int t0;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(t0) : "v"(static_cast<int>(threadIdx.x)));
+  for (int t = t0; t < kTasks; t += kThreads) {
+    const int blk = t / L, i = t - blk * L;
+    cf* q = z + blk * (R * L) + i;
+    cf v[R];
 #pragma unroll
-  for (int q = 0; q < 5; ++q) {
-    cf col[9];
+    for (int m = 0; m < R; ++m) v[m] = q[L * m];
+    cf w[R];  // w[k] = W_M^(S i k) (conjugated for INV)
+    if constexpr (S != 0) {
+      if constexpr (R == 16) {
+        // 4 table lookups (k = 1, 2, 4, 8), the other powers as products (<= 3 deep)
+        w[1] = twiddle<INV>(thi, tlo, S * i);
+        w[2] = twiddle<INV>(thi, tlo, 2 * S * i);
+        w[4] = twiddle<INV>(thi, tlo, 4 * S * i);
+        w[8] = twiddle<INV>(thi, tlo, 8 * S * i);
+        w[3] = cmul(w[1], w[2]);
+        w[5] = cmul(w[1], w[4]);
+        w[6] = cmul(w[2], w[4]);
+        w[7] = cmul(w[3], w[4]);
 #pragma unroll
-    for (int p = 0; p < 9; ++p) {
-      const int n = 5 * p + q;
-      cf v = row[n];
-      if (!INV && n) v = cmul(v, twm[n * k1]);
-      col[p] = v;
-    }
-    dft9<INV>(col);
+        for (int k = 9; k < 16; ++k) w[k] = cmul(w[k - 8], w[8]);
+      } else {
 #pragma unroll
-    for (int r = 0; r < 9; ++r) a[q][r] = (q && r) ? cmul(col[r], tw_const<INV>(double(q * r) / 45.0)) : col[r];
-  }
-#pragma unroll
-  for (int r = 0; r < 9; ++r) {
-    cf v[5];
-#pragma unroll
-    for (int q = 0; q < 5; ++q) v[q] = a[q][r];
-    dft5<INV>(v);
-#pragma unroll
-    for (int s5 = 0; s5 < 5; ++s5) {
-      const int k = r + 9 * s5;
-      cf o = v[s5];
-      if (INV && k) {
-        const cf w = twm[k * k1];
-        o = cmul(o, cf{w.x, -w.y});
+        for (int k = 1; k < R; ++k) w[k] = twiddle<INV>(thi, tlo, S * i * k);
       }
-      row[k] = o;
     }
+    if (INV && S)
+#pragma unroll
+      for (int k = 1; k < R; ++k) v[k] = cmul(v[k], w[k]);
+    dftr<R, INV>(v);
+    if (!INV && S)
+#pragma unroll
+      for (int k = 1; k < R; ++k) v[k] = cmul(v[k], w[k]);
+#pragma unroll
+    for (int m = 0; m < R; ++m) q[L * m] = v[m];
   }
 }
 
-// Forward complex FFT of z (natural order) -> Z[k] at addr(k).
-__device__ __forceinline__ int zaddr(int k) { return (k & (kR - 1)) * kC + (k >> 8); }
-
+// Forward: natural z -> Z[f] at zaddr(f); inverse: the reverse (x kM).
 template <bool INV>
-__device__ __forceinline__ void columns(cf* z, const cf* tw256) {
-  for (int c = threadIdx.x >> 4; c < kC; c += kThreads / 16) column_fft256<INV>(z, c, threadIdx.x & 15, tw256);
-}
-
-template <bool INV>
-__device__ __forceinline__ void rows(cf* z, const cf* twm) {
-  for (int r = threadIdx.x; r < kR; r += kThreads) row_dft45<INV>(z, r, twm);
-}
-
-template <bool INV>
-__device__ __forceinline__ void transform(cf* z, const cf* tw256, const cf* twm) {
+__device__ __forceinline__ void transform(cf* z, const cf* thi, const cf* tlo) {
   if (!INV) {
-    columns<false>(z, tw256);
+    pass<16, 720, 1, false>(z, thi, tlo);
     __syncthreads();
-    rows<false>(z, twm);
+    pass<16, 45, 16, false>(z, thi, tlo);
+    __syncthreads();
+    pass<9, 5, 256, false>(z, thi, tlo);
+    __syncthreads();
+    pass<5, 1, 0, false>(z, thi, tlo);
     __syncthreads();
   } else {
-    rows<true>(z, twm);
+    pass<5, 1, 0, true>(z, thi, tlo);
     __syncthreads();
-    columns<true>(z, tw256);
+    pass<9, 5, 256, true>(z, thi, tlo);
+    __syncthreads();
+    pass<16, 45, 16, true>(z, thi, tlo);
+    __syncthreads();
+    pass<16, 720, 1, true>(z, thi, tlo);
     __syncthreads();
   }
+}
+
+// Position of frequency f = k1 + 16 k2 + 256 k3 + 2304 k4 after the forward
+// passes: 720 k1 + 45 k2 + 5 k3 + k4 (mixed-radix digit reversal).
+__device__ __forceinline__ int zaddr(int f) {
+  const int k1 = f & 15, r = f >> 4;
+  const int k2 = r & 15, r2 = r >> 4;
+  const int k4 = r2 / 9, k3 = r2 - 9 * k4;
+  return 720 * k1 + 45 * k2 + 5 * k3 + k4;
+}
+
+// the twiddle tables into LDS (after z and the reduction slots)
+__device__ __forceinline__ void load_tw(cf* thi, cf* tlo, const float2* ghi, const float2* glo) {
+  for (int i = threadIdx.x; i < kTwHi; i += kThreads) thi[i] = cf{ghi[i].x, ghi[i].y};
+  for (int i = threadIdx.x; i < kTwLo; i += kThreads) tlo[i] = cf{glo[i].x, glo[i].y};
 }
 
 __device__ __forceinline__ float block_sum(float v, float* red) {
@@ -261,32 +271,50 @@ struct AugArgs {
   const float* snr_db;      // per clip
   const float2* spectra;    // [n_spec][kM + 1]
   const int* spec_idx;      // per clip: spectrum index, < 0 = no reverb
-  const float2* tw256;
-  const float2* twm;        // W_M^e, e < kM
+  const float2* thi;        // W_M^(128 h), h < 90
+  const float2* tlo;        // W_M^l, l < 128
   const float2* twn;        // W_N^k, k <= kM
 };
 
 __global__ void __launch_bounds__(kThreads) augment_kernel(AugArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   cf* z = reinterpret_cast<cf*>(smem);                      // kM complex
-  float* red = smem + 2 * kM;                               // 16 floats
-  const cf* tw256 = reinterpret_cast<const cf*>(a.tw256);
-  const cf* twm = reinterpret_cast<const cf*>(a.twm);
+  float* red = smem + 2 * kM;                               // 32 floats
+  cf* thi = reinterpret_cast<cf*>(smem + 2 * kM + 32);
+  cf* tlo = thi + kTwHi;
+  load_tw(thi, tlo, a.thi, a.tlo);
   const cf* twn = reinterpret_cast<const cf*>(a.twn);
   float* zf = smem;
   const int tid = threadIdx.x;
-  for (int64_t clip = blockIdx.x; clip < a.n_clips; clip += gridDim.x) {
+  // the next clip's samples are loaded into registers while this clip's
+  // transforms run (one clip per CU: otherwise every load is exposed); the
+  // noise segment is read twice (energy, then mix; the 2nd read hits L2)
+  constexpr int kPer = (kT + kThreads - 1) / kThreads;
+  float xr[kPer];
+  auto prefetch = [&](int64_t clip) {
     const float* x = a.x + clip * a.x_stride;
-    // 1) load x into LDS, the noise segment into registers
-    float ex = 0.f;
-    for (int s = tid; s < kT; s += kThreads) {
-      const float v = x[s];
-      zf[s] = v;
-      ex += v * v;
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int s = tid + u * kThreads;
+      if (s < kT) xr[u] = x[s];
     }
+  };
+  if (blockIdx.x < a.n_clips) prefetch(blockIdx.x);
+  for (int64_t clip = blockIdx.x; clip < a.n_clips; clip += gridDim.x) {
+    // 1) y = x + scale n into LDS (torchaudio add_noise: snr0 = 10 (log10 Ex - log10 En),
+    //    scale = 10^((snr0 - snr)/20))
     const int64_t noff = a.noise_off[clip];
+    float ex = 0.f;
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int s = tid + u * kThreads;
+      if (s < kT) {
+        ex += xr[u] * xr[u];
+        zf[s] = xr[u];
+      }
+    }
+    if (clip + gridDim.x < a.n_clips) prefetch(clip + gridDim.x);
     if (noff >= 0) {
-      // the noise segment is read twice (energy, then mix); the 2nd read hits L2
       auto noise_at = [&](int s) {
         int64_t r = noff + s;
         if (r >= a.ring_len) r -= a.ring_len;
@@ -299,7 +327,6 @@ __global__ void __launch_bounds__(kThreads) augment_kernel(AugArgs a) {
       }
       const float Ex = block_sum(ex, red);
       const float En = block_sum(en, red);
-      // torchaudio add_noise: snr0 = 10 (log10 Ex - log10 En); scale = 10^((snr0 - snr)/20)
       const float snr0 = 10.f * (log10f(Ex) - log10f(En));
       const float scale = powf(10.f, (snr0 - a.snr_db[clip]) / 20.f);
       for (int s = tid; s < kT; s += kThreads) zf[s] = zf[s] + scale * noise_at(s);
@@ -317,7 +344,7 @@ __global__ void __launch_bounds__(kThreads) augment_kernel(AugArgs a) {
     for (int s = tid; s < kT; s += kThreads) aa += fabsf(zf[s]);
     const float a_in = block_sum(aa, red) / kT;
     // 3) forward FFT (natural -> permuted)
-    transform<false>(z, tw256, twm);
+    transform<false>(z, thi, tlo);
     // 4) split, multiply by H, inverse split, on (k, M-k) pairs
     const cf* H = reinterpret_cast<const cf*>(a.spectra) + static_cast<int64_t>(sp) * (kM + 1);
     for (int k = tid; k <= kM / 2; k += kThreads) {
@@ -351,7 +378,7 @@ __global__ void __launch_bounds__(kThreads) augment_kernel(AugArgs a) {
     }
     __syncthreads();
     // 5) inverse FFT (permuted -> natural), 1/M
-    transform<true>(z, tw256, twm);
+    transform<true>(z, thi, tlo);
     float ay = 0.f;
     for (int s = tid; s < kT; s += kThreads) ay += fabsf(zf[s]);
     const float a_out = block_sum(ay, red) / kT / kM;
@@ -363,17 +390,18 @@ __global__ void __launch_bounds__(kThreads) augment_kernel(AugArgs a) {
 
 // Spectrum of one rotated IR kernel k [kT] -> H[k], k = 0..kM (natural order).
 __global__ void __launch_bounds__(kThreads) spectrum_kernel(const float* kern, int64_t kern_stride,
-                                                            float2* spectra, const float2* tw256_,
-                                                            const float2* twm_, const float2* twn_) {
+                                                            float2* spectra, const float2* thi_,
+                                                            const float2* tlo_, const float2* twn_) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   cf* z = reinterpret_cast<cf*>(smem);
-  const cf* tw256 = reinterpret_cast<const cf*>(tw256_);
-  const cf* twm = reinterpret_cast<const cf*>(twm_);
+  cf* thi = reinterpret_cast<cf*>(smem + 2 * kM + 32);
+  cf* tlo = thi + kTwHi;
+  load_tw(thi, tlo, thi_, tlo_);
   const cf* twn = reinterpret_cast<const cf*>(twn_);
   const float* k = kern + blockIdx.x * kern_stride;
   for (int s = threadIdx.x; s < kT; s += kThreads) smem[s] = k[s];
   __syncthreads();
-  transform<false>(z, tw256, twm);
+  transform<false>(z, thi, tlo);
   float2* H = spectra + static_cast<int64_t>(blockIdx.x) * (kM + 1);
   for (int q = threadIdx.x; q <= kM; q += kThreads) {
     const int qq = q % kM, qc = (kM - q) % kM;
@@ -390,10 +418,14 @@ __global__ void __launch_bounds__(kThreads) spectrum_kernel(const float* kern, i
 }  // namespace hbk
 
 struct hbk_reverb_plan {
-  float2* tw256 = nullptr;
-  float2* twm = nullptr;
+  float2* thi = nullptr;
+  float2* tlo = nullptr;
   float2* twn = nullptr;
 };
+
+namespace {
+constexpr size_t kAugLds = (size_t(2 * hbk::kM + 32) * sizeof(float)) + (hbk::kTwHi + hbk::kTwLo) * sizeof(float2);
+}
 
 extern "C" {
 
@@ -405,14 +437,14 @@ int hbk_reverb_plan_create(int64_t T, hbk_reverb_plan** plan) {
     set_error("hbk: reverb supports clips of %d samples (1.44 s @ 16 kHz), got %lld", kT, (long long)T);
     return HBK_ERR_UNSUPPORTED;
   }
-  std::vector<float2> t256(256), tm(kM), tn(kM + 1);
-  for (int i = 0; i < 256; ++i) {
-    const double a = -2.0 * M_PI * i / 256.0;
-    t256[i] = make_float2(float(cos(a)), float(sin(a)));
+  std::vector<float2> th(kTwHi), tl(kTwLo), tn(kM + 1);
+  for (int i = 0; i < kTwHi; ++i) {
+    const double a = -2.0 * M_PI * (double(i) * kTwLo) / double(kM);
+    th[i] = make_float2(float(cos(a)), float(sin(a)));
   }
-  for (int i = 0; i < kM; ++i) {
+  for (int i = 0; i < kTwLo; ++i) {
     const double a = -2.0 * M_PI * i / double(kM);
-    tm[i] = make_float2(float(cos(a)), float(sin(a)));
+    tl[i] = make_float2(float(cos(a)), float(sin(a)));
   }
   for (int i = 0; i <= kM; ++i) {
     const double a = -2.0 * M_PI * i / double(kT);
@@ -420,16 +452,16 @@ int hbk_reverb_plan_create(int64_t T, hbk_reverb_plan** plan) {
   }
   auto* p = new hbk_reverb_plan();
   hipError_t e;
-  if ((e = hipMalloc(&p->tw256, 256 * sizeof(float2))) != hipSuccess ||
-      (e = hipMalloc(&p->twm, kM * sizeof(float2))) != hipSuccess ||
+  if ((e = hipMalloc(&p->thi, kTwHi * sizeof(float2))) != hipSuccess ||
+      (e = hipMalloc(&p->tlo, kTwLo * sizeof(float2))) != hipSuccess ||
       (e = hipMalloc(&p->twn, (kM + 1) * sizeof(float2))) != hipSuccess ||
-      (e = hipMemcpy(p->tw256, t256.data(), 256 * sizeof(float2), hipMemcpyHostToDevice)) != hipSuccess ||
-      (e = hipMemcpy(p->twm, tm.data(), kM * sizeof(float2), hipMemcpyHostToDevice)) != hipSuccess ||
+      (e = hipMemcpy(p->thi, th.data(), kTwHi * sizeof(float2), hipMemcpyHostToDevice)) != hipSuccess ||
+      (e = hipMemcpy(p->tlo, tl.data(), kTwLo * sizeof(float2), hipMemcpyHostToDevice)) != hipSuccess ||
       (e = hipMemcpy(p->twn, tn.data(), (kM + 1) * sizeof(float2), hipMemcpyHostToDevice)) != hipSuccess) {
     hbk_reverb_plan_destroy(p);
     return hip_error(e, "reverb plan tables");
   }
-  const size_t lds = size_t(2 * kM + 32) * sizeof(float);
+  const size_t lds = kAugLds;
   if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(augment_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, int(lds))) != hipSuccess ||
       (e = hipFuncSetAttribute(reinterpret_cast<const void*>(spectrum_kernel),
@@ -443,8 +475,8 @@ int hbk_reverb_plan_create(int64_t T, hbk_reverb_plan** plan) {
 
 int hbk_reverb_plan_destroy(hbk_reverb_plan* p) {
   if (!p) return HBK_OK;
-  (void)hipFree(p->tw256);
-  (void)hipFree(p->twm);
+  (void)hipFree(p->thi);
+  (void)hipFree(p->tlo);
   (void)hipFree(p->twn);
   delete p;
   return HBK_OK;
@@ -458,9 +490,8 @@ int hbk_reverb_spectrum(const hbk_reverb_plan* p, const float* kernels, int64_t 
   if (n_kernels == 0) return HBK_OK;
   if (!kernels || !spectra) return arg_error("NULL pointer");
   if (stride < kT) return arg_error("kernel stride < 23040");
-  const size_t lds = size_t(2 * kM + 32) * sizeof(float);
-  hipLaunchKernelGGL(spectrum_kernel, dim3(unsigned(n_kernels)), dim3(kThreads), lds, as_stream(stream), kernels,
-                     stride, reinterpret_cast<float2*>(spectra), p->tw256, p->twm, p->twn);
+  hipLaunchKernelGGL(spectrum_kernel, dim3(unsigned(n_kernels)), dim3(kThreads), kAugLds, as_stream(stream),
+                     kernels, stride, reinterpret_cast<float2*>(spectra), p->thi, p->tlo, p->twn);
   HBK_LAUNCH_CHECK("spectrum_kernel");
   return HBK_OK;
 }
@@ -487,12 +518,11 @@ int hbk_augment(const hbk_reverb_plan* p, const float* x, int64_t n_clips, int64
   a.snr_db = snr_db;
   a.spectra = reinterpret_cast<const float2*>(spectra);
   a.spec_idx = spec_idx;
-  a.tw256 = p->tw256;
-  a.twm = p->twm;
+  a.thi = p->thi;
+  a.tlo = p->tlo;
   a.twn = p->twn;
-  const size_t lds = size_t(2 * kM + 32) * sizeof(float);
   const int64_t blocks = std::min<int64_t>(n_clips, persistent_blocks(1));
-  hipLaunchKernelGGL(augment_kernel, dim3(unsigned(blocks)), dim3(kThreads), lds, as_stream(stream), a);
+  hipLaunchKernelGGL(augment_kernel, dim3(unsigned(blocks)), dim3(kThreads), kAugLds, as_stream(stream), a);
   HBK_LAUNCH_CHECK("augment_kernel");
   return HBK_OK;
 }
