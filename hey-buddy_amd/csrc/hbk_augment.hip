@@ -172,7 +172,17 @@ __device__ __forceinline__ void pass(cf* z, const cf* thi, const cf* tlo) {
   int t0;
   asm volatile("v_mov_b32 %0, %1" : "=v"(t0) : "v"(static_cast<int>(threadIdx.x)));
   for (int t = t0; t < kTasks; t += kThreads) {
-    const int blk = t / L, i = t - blk * L;
+    // lanes walk i (contiguous addresses) when L is large, blocks (stride R L =
+    // 45 complex: conflict-free over 32 lanes) when L is the short span of 5
+    constexpr int kBlocks = kM / (R * L);
+    int blk, i;
+    if constexpr (L < 16) {
+      i = t / kBlocks;
+      blk = t - i * kBlocks;
+    } else {
+      blk = t / L;
+      i = t - blk * L;
+    }
     cf* q = z + blk * (R * L) + i;
     cf v[R];
 #pragma unroll
@@ -239,6 +249,14 @@ __device__ __forceinline__ int zaddr(int f) {
   const int k2 = r & 15, r2 = r >> 4;
   const int k4 = r2 / 9, k3 = r2 - 9 * k4;
   return 720 * k1 + 45 * k2 + 5 * k3 + k4;
+}
+
+// Frequency stored at position p (inverse of zaddr).
+__device__ __forceinline__ int zfreq(int p) {
+  const int k1 = p / 720, r = p - 720 * k1;
+  const int k2 = r / 45, r2 = r - 45 * k2;
+  const int k3 = r2 / 5, k4 = r2 - 5 * k3;
+  return k1 + 16 * k2 + 256 * k3 + 2304 * k4;
 }
 
 // the twiddle tables into LDS (after z and the reduction slots)
@@ -347,11 +365,18 @@ __global__ void __launch_bounds__(kThreads) augment_kernel(AugArgs a) {
     transform<false>(z, thi, tlo);
     // 4) split, multiply by H, inverse split, on (k, M-k) pairs
     const cf* H = reinterpret_cast<const cf*>(a.spectra) + static_cast<int64_t>(sp) * (kM + 1);
-    for (int k = tid; k <= kM / 2; k += kThreads) {
+    // one thread per pair (k, M - k), k <= M / 2; consecutive lanes take k in
+    // steps of 16 (k = c + 16 r, c = idx / 361), so their positions zaddr(k)
+    // step by 45 complex instead of 720 (no 16-way bank conflicts)
+    constexpr int kRest = kM / 2 / 16 + 1;  // 361
+    for (int idx = tid; idx < 16 * kRest; idx += kThreads) {
+      const int c = idx / kRest;
+      const int k = c + 16 * (idx - c * kRest);
+      if (k > kM / 2) continue;
       const int kc = (kM - k) % kM;
-      const cf zk = z[zaddr(k)];
+      const int p = zaddr(k);
+      const cf zk = z[p];
       const cf zc = z[zaddr(kc)];
-      // X[k] = Fe + W_N^k Fo, X[M-k] = conj(Fe) + W_N^(M-k) conj(Fo)...: compute both directly
       const cf fe = 0.5f * cf{zk.x + zc.x, zk.y - zc.y};
       const cf fo = 0.5f * cf{zk.y + zc.y, zc.x - zk.x};
       const cf wk = twn[k];
@@ -373,7 +398,7 @@ __global__ void __launch_bounds__(kThreads) augment_kernel(AugArgs a) {
       const cf d2 = 0.5f * cf{Yc.x - Yk.x, Yc.y + Yk.y};
       const cf wd2 = cmul(cf{-wk.x, -wk.y}, d2);
       const cf zc2 = s2 + cf{-wd2.y, wd2.x};
-      z[zaddr(k)] = zk2;
+      z[p] = zk2;
       if (kc != k) z[zaddr(kc)] = zc2;
     }
     __syncthreads();
