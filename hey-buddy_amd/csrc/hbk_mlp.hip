@@ -48,7 +48,9 @@ template <bool TA, bool TB>
 __global__ void __launch_bounds__(256) gemm_kernel(const float* __restrict__ A, const float* __restrict__ B,
                                                    float* __restrict__ C, const float* __restrict__ bias,
                                                    int M, int N, int K, int lda, int ldb, int ldc,
-                                                   int accumulate) {
+                                                   int accumulate, int k_split) {
+  // split-K: block z covers K rows [z k_split, (z + 1) k_split) and atomically
+  // adds its partial product (C pre-zeroed by the host; bias from split 0)
   __shared__ float As[GBK][GBM + 4];
   __shared__ float Bs[GBK][GBN + 4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -60,7 +62,8 @@ __global__ void __launch_bounds__(256) gemm_kernel(const float* __restrict__ A, 
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-  for (int k0 = 0; k0 < K; k0 += GBK) {
+  const int kb = blockIdx.z * k_split, ke = min(K, kb + k_split);
+  for (int k0 = kb; k0 < ke; k0 += GBK) {
     // stage A: 64 x 16 -> As[k][m]; B: 16 x 64 -> Bs[k][n]
 #pragma unroll
     for (int e = tid; e < GBM * GBK; e += 256) {
@@ -68,7 +71,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(const float* __restrict__ A, 
       if (TA) { k = e / GBM; m = e - k * GBM; } else { m = e / GBK; k = e - m * GBK; }
       const int gm = m0 + m, gk = k0 + k;
       float v = 0.f;
-      if (gm < M && gk < K) v = TA ? A[static_cast<int64_t>(gk) * lda + gm] : A[static_cast<int64_t>(gm) * lda + gk];
+      if (gm < M && gk < ke) v = TA ? A[static_cast<int64_t>(gk) * lda + gm] : A[static_cast<int64_t>(gm) * lda + gk];
       As[k][m] = v;
     }
 #pragma unroll
@@ -77,7 +80,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(const float* __restrict__ A, 
       if (TB) { n = e / GBK; k = e - n * GBK; } else { k = e / GBN; n = e - k * GBN; }
       const int gn = n0 + n, gk = k0 + k;
       float v = 0.f;
-      if (gn < N && gk < K) v = TB ? B[static_cast<int64_t>(gn) * ldb + gk] : B[static_cast<int64_t>(gk) * ldb + gn];
+      if (gn < N && gk < ke) v = TB ? B[static_cast<int64_t>(gn) * ldb + gk] : B[static_cast<int64_t>(gk) * ldb + gn];
       Bs[k][n] = v;
     }
     __syncthreads();
@@ -101,14 +104,17 @@ __global__ void __launch_bounds__(256) gemm_kernel(const float* __restrict__ A, 
     for (int j = 0; j < 2; ++j) {
       const int n = n0 + 32 * wc + 16 * j + r16;
       if (n >= N) continue;
-      const float bb = bias ? bias[n] : 0.f;
+      const float bb = (bias && blockIdx.z == 0) ? bias[n] : 0.f;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int m = m0 + 32 * wr + 16 * i + kq * 4 + q;
         if (m < M) {
           float* c = C + static_cast<int64_t>(m) * ldc + n;
           const float v = acc[i][j][q] + bb;
-          *c = accumulate ? *c + v : v;
+          if (gridDim.z > 1)
+            atomicAdd(c, v);
+          else
+            *c = accumulate ? *c + v : v;
         }
       }
     }
@@ -427,8 +433,20 @@ int gemm(const float* A, const float* B, float* C, const float* bias, int M, int
          int ldb, int ldc, bool acc, hipStream_t s) {
   if (M <= 0 || N <= 0) return HBK_OK;
   dim3 grid((N + GBN - 1) / GBN, (M + GBM - 1) / GBM);
+  // Split-K when the output has too few tiles to fill the chip (the weight
+  // gradients: K = batch; the input layer: K = 1536), >= 128 K rows per split.
+  int splits = 1;
+  const int tiles = int(grid.x * grid.y);
+  if (tiles < 256 && K >= 256 && (ldc == N || acc)) splits = std::min(std::max(1, 512 / tiles), K / 128);
+  const int k_split = ((K + splits - 1) / splits + GBK - 1) / GBK * GBK;
+  splits = (K + k_split - 1) / k_split;
+  if (splits > 1 && !acc) {
+    hipError_t e = hipMemsetAsync(C, 0, size_t(M) * N * sizeof(float), s);
+    if (e != hipSuccess) return hip_error(e, "hipMemsetAsync (split-K)");
+  }
+  grid.z = splits;
   hipLaunchKernelGGL((gemm_kernel<TA, TB>), grid, dim3(256), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc,
-                     acc ? 1 : 0);
+                     acc ? 1 : 0, k_split);
   HBK_LAUNCH_CHECK("gemm_kernel");
   return HBK_OK;
 }
