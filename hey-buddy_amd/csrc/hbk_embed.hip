@@ -370,15 +370,24 @@ __device__ __forceinline__ int div_small(int n, int d, float inv) {
   return q;
 }
 
-// hi = v rounded toward zero to 11 significant bits (exact in fp16 for
-// |v| in fp16's normal range), lo = v - hi; two values, packed
-__device__ __forceinline__ float hi_part(float v) {
-  return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, v) & 0xFFFFE000u);
-}
+// hi = v rounded toward zero to fp16 (11 significant bits in fp16's normal
+// range), lo = (v - hi) rounded to fp16 by v_fma_mix{lo,hi}_f16 (v - hi is
+// exact in f32); two values, packed: 3 VALU instructions per pair
 __device__ __forceinline__ void split2(float a, float b, h2& hi, h2& lo) {
-  const float ha = hi_part(a), hb = hi_part(b);
-  hi = __builtin_amdgcn_cvt_pkrtz(ha, hb);
-  lo = __builtin_amdgcn_cvt_pkrtz(a - ha, b - hb);
+  hi = __builtin_amdgcn_cvt_pkrtz(a, b);
+  const uint32_t hb = __builtin_bit_cast(uint32_t, hi);
+  uint32_t l = 0;
+  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "+v"(l) : "v"(a), "v"(hb));
+  asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(l) : "v"(b), "v"(hb));
+  lo = __builtin_bit_cast(h2, l);
+}
+
+// max(v, alpha v) through asm: fmaxf on MFMA results gets a canonicalising
+// v_max in front of it; both operands are NaN for a NaN v, so NaN propagates
+__device__ __forceinline__ float leaky_max(float v, float alpha) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(v), "v"(v * alpha));
+  return r;
 }
 
 __device__ __forceinline__ uint32_t h2_bits(h2 v) { return __builtin_bit_cast(uint32_t, v); }
@@ -472,7 +481,7 @@ __device__ __forceinline__ void xstage(const _Float16* __restrict__ Xh, const _F
       for (int c = 0; c < NB; ++c) {
 #pragma unroll
         for (int r = 0; r < RB; ++r)
-          acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.wh[c], f.xh[r], first ? f16x{} : acc[r][c], 0, 0,
+          acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.wh[c], f.xh[r], first ? bl[c] : acc[r][c], 0, 0,
                                                               0);
 #pragma unroll
         for (int r = 0; r < RB; ++r)
@@ -516,11 +525,11 @@ __device__ __forceinline__ void xstage(const _Float16* __restrict__ Xh, const _F
           // coutr is a multiple of 8, so this test is the same for both lane halves (uniform)
           if (c * 32 + 8 * q >= S.coutr) continue;
           const int n0 = c * 32 + 8 * q + 4 * khalf;
-          float v[4] = {acc[r][c][4 * q] + bl[c][4 * q], acc[r][c][4 * q + 1] + bl[c][4 * q + 1],
-                        acc[r][c][4 * q + 2] + bl[c][4 * q + 2], acc[r][c][4 * q + 3] + bl[c][4 * q + 3]};
+          // (the bias is the first MFMA's accumulator input)
+          float v[4] = {acc[r][c][4 * q], acc[r][c][4 * q + 1], acc[r][c][4 * q + 2], acc[r][c][4 * q + 3]};
           if (S.act == 1) {  // LeakyReLU, 0 <= alpha <= 1: max(v, alpha v) (NaN stays NaN)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = __builtin_fmaxf(v[j], v[j] * S.alpha);
+            for (int j = 0; j < 4; ++j) v[j] = leaky_max(v[j], S.alpha);
           } else if (S.act == 2) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) v[j] = v[j] >= 0.f ? v[j] : v[j] * S.alpha;
