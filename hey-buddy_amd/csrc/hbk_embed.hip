@@ -1137,6 +1137,203 @@ p0_chain_kernel(P0Args a) {
   }
 }
 
+// ------------------------------------------------------------------- p1 ----
+// Pattern kernel for the chain  conv 1x3 (CI -> 32) . conv 3x1 (32 -> 32) .
+// conv 1x3 (32 -> 32) . conv 3x1 (32 -> 32) . max-pool 2x2  on an NHWC f32
+// input of fixed width WI (SE20 chain 1: 66 x 14 x 24 -> 31 x 5 x 32). Same
+// split-f16 numerics and tile / epilogue scheme as p0_chain_kernel; the
+// stage weights do not all fit in VGPRs, so each stage's A fragments are
+// loaded (from L2) one stage ahead, while the previous stage runs.
+constexpr int kP1C = 32;
+
+struct P1Args {
+  const float* in;          // [img][H_in][WI][CI] f32
+  float* out;               // [img][H_out][W4 / 2][32] f32
+  const _Float16* w;        // stage s at woff[s]: hi [32][16 ks_s], lo [32][16 ks_s]
+  const float* bias;        // [4][32]
+  int64_t n_img;
+  int64_t src_img_stride;   // floats
+  int H_in, H_out, n_bands;
+  float alpha;
+};
+
+template <int WI, int CI, int BAND>
+struct P1Geo {
+  static constexpr int C = kP1C;
+  static constexpr int W0 = WI, W1 = WI - 2, W2 = W1, W3 = W1 - 2, W4 = W3;
+  static constexpr int R4 = 2 * BAND, R3 = R4 + 2, R2 = R3, R1 = R2 + 2, R0 = R1;
+  static constexpr int CSI = ((CI / 8) % 2 == 0) ? CI + 8 : CI;
+  static constexpr int CS = ((C / 8) % 2 == 0) ? C + 8 : C;
+  static constexpr int M1 = R1 * W1, M2 = R2 * W2, M3 = R3 * W3, M4 = R4 * W4;
+  static constexpr int KS1 = (3 * CI + 15) / 16, KS = (3 * C + 15) / 16;
+  static constexpr int KSMAX = KS1 > KS ? KS1 : KS;
+  static constexpr int INB = R0 * W0 * CSI * 4, S1B = M1 * CS * 4, S2B = M2 * CS * 4, S3B = M3 * CS * 4,
+                       S4B = M4 * C * 4;
+  static constexpr int mx(int a, int b) { return a > b ? a : b; }
+  static constexpr int XB = (mx(mx(INB, S2B), S4B) + 15) & ~15;  // input, stage-2 out, stage-4 out (f32)
+  static constexpr int YB = (mx(S1B, S3B) + 15) & ~15;            // stage-1 out, stage-3 out
+  static constexpr int LDS = XB + YB;
+  static constexpr int WOFF1 = 0, WOFF2 = WOFF1 + 2 * 32 * 16 * KS1, WOFF3 = WOFF2 + 2 * 32 * 16 * KS,
+                       WOFF4 = WOFF3 + 2 * 32 * 16 * KS, WHALFS = WOFF4 + 2 * 32 * 16 * KS;
+};
+
+template <int KS>
+__device__ __forceinline__ P0W<KS> p1_load_w(const _Float16* w, const float* bias, int r32, int khalf) {
+  P0W<KS> W;
+  const _Float16* wp = w + r32 * (16 * KS) + 8 * khalf;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    W.ah[ks] = *reinterpret_cast<const h8*>(wp + 16 * ks);
+    W.al[ks] = *reinterpret_cast<const h8*>(wp + 32 * 16 * KS + 16 * ks);
+  }
+  W.bias = p0_bias(bias, khalf);
+  return W;
+}
+
+// One conv stage on LDS planes: kernel KH x KW over CIN channels (fp16 stride
+// CSI per position, input grid width WIN), output grid (M positions, width
+// WOUT), 32 output channels -> planes (CSO) or f32 (F32OUT, stride 32).
+template <int KH, int KW, int CIN, int CSI, int WIN, int WOUT, int M, int KS, int CSO, bool F32OUT, bool LEAKY>
+__device__ __forceinline__ void p1_stage(const P0W<KS>& W, const _Float16* xh_, const _Float16* xl_,
+                                         _Float16* oh, _Float16* ol, float* of, float alpha, int wave, int r32,
+                                         int khalf) {
+  constexpr int T = (M + 31) / 32;
+  auto epilogue = [&](int t, const f16x& acc) {
+    const int pp = t * 32 + r32;
+    if (pp >= M) return;
+    if (!F32OUT) {
+      p0_store_planes<kP1C, CSO, LEAKY>(acc, pp, khalf, oh, ol, alpha);
+    } else {
+#pragma unroll
+      for (int q = 0; q < kP1C / 8; ++q) {
+        float4 v;
+        v.x = p0_act<LEAKY>(acc[4 * q], alpha);
+        v.y = p0_act<LEAKY>(acc[4 * q + 1], alpha);
+        v.z = p0_act<LEAKY>(acc[4 * q + 2], alpha);
+        v.w = p0_act<LEAKY>(acc[4 * q + 3], alpha);
+        *reinterpret_cast<float4*>(of + pp * kP1C + 8 * q + 4 * khalf) = v;
+      }
+    }
+  };
+  f16x prev;
+  int tprev = -1;
+  for (int t = wave; t < T; t += kP0Waves) {
+    const int p = min(t * 32 + r32, M - 1);
+    const int y = p / WOUT, x = p - y * WOUT;
+    const int base = (y * WIN + x) * CSI;
+    h8 xh[KS], xl[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      // K = tap * CIN + ci, tap = dy * KW + dx; groups past KH KW CIN read group 0 (weights 0)
+      const int ka = 16 * ks < KH * KW * CIN ? 16 * ks : 0;
+      const int kb = 16 * ks + 8 < KH * KW * CIN ? 16 * ks + 8 : 0;
+      const int ta = ka / CIN, tb = kb / CIN;
+      const int oa = ((ta / KW) * WIN + ta % KW) * CSI + ka % CIN;
+      const int ob = ((tb / KW) * WIN + tb % KW) * CSI + kb % CIN;
+      const int o = base + (khalf ? ob : oa);
+      xh[ks] = *reinterpret_cast<const h8*>(xh_ + o);
+      xl[ks] = *reinterpret_cast<const h8*>(xl_ + o);
+    }
+    f16x acc = W.bias;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(W.ah[ks], xh[ks], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(W.ah[ks], xl[ks], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(W.al[ks], xh[ks], acc, 0, 0, 0);
+    }
+    if (tprev >= 0) epilogue(tprev, prev);
+    prev = acc;
+    tprev = t;
+  }
+  if (tprev >= 0) epilogue(tprev, prev);
+}
+
+template <int WI, int CI, int BAND, bool LEAKY>
+__global__ void __launch_bounds__(kP0Threads) __attribute__((amdgpu_waves_per_eu(2)))
+p1_chain_kernel(P1Args a) {
+  using G = P1Geo<WI, CI, BAND>;
+  constexpr int C = kP1C;
+  extern __shared__ __attribute__((aligned(16))) unsigned char p1mem[];
+  _Float16* inh = reinterpret_cast<_Float16*>(p1mem);
+  _Float16* inl = inh + G::R0 * G::W0 * G::CSI;
+  _Float16* s2h = reinterpret_cast<_Float16*>(p1mem);
+  _Float16* s2l = s2h + G::M2 * G::CS;
+  float* s4 = reinterpret_cast<float*>(p1mem);
+  _Float16* s1h = reinterpret_cast<_Float16*>(p1mem + G::XB);
+  _Float16* s1l = s1h + G::M1 * G::CS;
+  _Float16* s3h = reinterpret_cast<_Float16*>(p1mem + G::XB);
+  _Float16* s3l = s3h + G::M3 * G::CS;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r32 = lane & 31, khalf = lane >> 5;
+  const int n_tasks = static_cast<int>(a.n_img) * a.n_bands;
+  const float alpha = a.alpha;
+
+  P0W<G::KS1> W1 = p1_load_w<G::KS1>(a.w + G::WOFF1, a.bias, r32, khalf);
+  for (int task = blockIdx.x; task < n_tasks; task += gridDim.x) {
+    const int img = task / a.n_bands, band = task - img * a.n_bands;
+    const int row0 = band * G::R4;
+    __syncthreads();  // the previous task's readers are done
+    // 1) input rows [row0, row0 + R0) (clamped) -> hi / lo planes, 8 channels per unit
+    {
+      const float* src = a.in + static_cast<int64_t>(img) * a.src_img_stride;
+      constexpr int U = G::R0 * WI * (CI / 8);
+      for (int u = tid; u < U; u += kP0Threads) {
+        const int c8 = u % (CI / 8), pos = u / (CI / 8);
+        const int r = pos / WI, x = pos - r * WI;
+        const int rr = min(row0 + r, a.H_in - 1);
+        const float* q = src + (static_cast<int64_t>(rr) * WI + x) * CI + 8 * c8;
+        const float4 v0 = *reinterpret_cast<const float4*>(q), v1 = *reinterpret_cast<const float4*>(q + 4);
+        uint32_t h[4], l[4];
+        split2_mix(v0.x, v0.y, h[0], l[0]);
+        split2_mix(v0.z, v0.w, h[1], l[1]);
+        split2_mix(v1.x, v1.y, h[2], l[2]);
+        split2_mix(v1.z, v1.w, h[3], l[3]);
+        const int o = pos * G::CSI + 8 * c8;
+        *reinterpret_cast<uint4*>(inh + o) = uint4{h[0], h[1], h[2], h[3]};
+        *reinterpret_cast<uint4*>(inl + o) = uint4{l[0], l[1], l[2], l[3]};
+      }
+    }
+    __syncthreads();
+    P0W<G::KS> W2 = p1_load_w<G::KS>(a.w + G::WOFF2, a.bias + 32, r32, khalf);
+    p1_stage<1, 3, CI, G::CSI, G::W0, G::W1, G::M1, G::KS1, G::CS, false, LEAKY>(W1, inh, inl, s1h, s1l, nullptr,
+                                                                                  alpha, wave, r32, khalf);
+    __syncthreads();
+    P0W<G::KS> W3 = p1_load_w<G::KS>(a.w + G::WOFF3, a.bias + 64, r32, khalf);
+    p1_stage<3, 1, C, G::CS, G::W1, G::W2, G::M2, G::KS, G::CS, false, LEAKY>(W2, s1h, s1l, s2h, s2l, nullptr,
+                                                                               alpha, wave, r32, khalf);
+    __syncthreads();
+    P0W<G::KS> W4 = p1_load_w<G::KS>(a.w + G::WOFF4, a.bias + 96, r32, khalf);
+    p1_stage<1, 3, C, G::CS, G::W2, G::W3, G::M3, G::KS, G::CS, false, LEAKY>(W3, s2h, s2l, s3h, s3l, nullptr,
+                                                                               alpha, wave, r32, khalf);
+    __syncthreads();
+    W1 = p1_load_w<G::KS1>(a.w + G::WOFF1, a.bias, r32, khalf);  // the next task's stage 1
+    p1_stage<3, 1, C, G::CS, G::W3, G::W4, G::M4, G::KS, G::CS, true, LEAKY>(W4, s3h, s3l, nullptr, nullptr, s4,
+                                                                              alpha, wave, r32, khalf);
+    __syncthreads();
+    // 2x2 max-pool of the stage-4 rows -> BAND output rows
+    {
+      constexpr int PW = G::W4 / 2, C4 = C / 4;
+      float* dst = a.out + static_cast<int64_t>(img) * a.H_out * PW * C;
+      for (int i = tid; i < BAND * PW * C4; i += kP0Threads) {
+        const int c4 = i % C4, rest = i / C4, px = rest % PW, py = rest / PW;
+        const int orow = band * BAND + py;
+        if (orow >= a.H_out) continue;
+        const float* q0 = s4 + ((2 * py) * G::W4 + 2 * px) * C + 4 * c4;
+        const float4 v00 = *reinterpret_cast<const float4*>(q0);
+        const float4 v01 = *reinterpret_cast<const float4*>(q0 + C);
+        const float4 v10 = *reinterpret_cast<const float4*>(q0 + G::W4 * C);
+        const float4 v11 = *reinterpret_cast<const float4*>(q0 + G::W4 * C + C);
+        float4 m;
+        m.x = nan_max(nan_max(v00.x, v01.x), nan_max(v10.x, v11.x));
+        m.y = nan_max(nan_max(v00.y, v01.y), nan_max(v10.y, v11.y));
+        m.z = nan_max(nan_max(v00.z, v01.z), nan_max(v10.z, v11.z));
+        m.w = nan_max(nan_max(v00.w, v01.w), nan_max(v10.w, v11.w));
+        *reinterpret_cast<float4*>(dst + (static_cast<int64_t>(orow) * PW + px) * C + 4 * c4) = m;
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ host ----
 
 struct OpInfo {
@@ -1169,6 +1366,8 @@ struct ChainPlan {
   // plan above stays as the fallback for unaligned buffers
   void (*p0fn)(P0Args) = nullptr;
   P0Args p0{};
+  void (*p1fn)(P1Args) = nullptr;  // p1 pattern (shares d_p0 / p0_lds / p0_blocks_per_cu)
+  P1Args p1{};
   size_t p0_lds = 0;
   int p0_blocks_per_cu = 0;
   void* d_p0 = nullptr;
@@ -1574,6 +1773,81 @@ bool plan_p0(const std::vector<OpInfo>& ops, const std::vector<int>& st, const C
   return true;
 }
 
+// The p1 pattern: [1x3 (CI -> 32), 3x1, 1x3, 3x1 (32 -> 32)] + output pool 2x2,
+// NHWC input of width 14 with CI = 24, one image per source image.
+constexpr int kP1W = 14, kP1CI = 24, kP1Band = 8;
+using P1G = P1Geo<kP1W, kP1CI, kP1Band>;
+
+bool plan_p1(const std::vector<OpInfo>& ops, const std::vector<int>& st, const ChainArgs& a, Dims d, Dims od,
+             ChainPlan& cp) {
+  if (getenv("HBK_EMBED_NO_P1")) return false;
+  if (st.size() != 4 || a.ipc != 1 || a.in_ph != 1 || a.in_pw != 1 || a.out_ph != 2 || a.out_pw != 2) return false;
+  if (d.w != kP1W || d.c != kP1CI || a.C_src != kP1CI || a.src_row_stride != kP1W * kP1CI) return false;
+  const int C = kP1C;
+  const int kh[4] = {1, 3, 1, 3}, kw[4] = {3, 1, 3, 1};
+  bool leaky = ops[st[0]].act != 0;
+  for (int i = 0; i < 4; ++i) {
+    const OpInfo& o = ops[st[i]];
+    if (o.kh != kh[i] || o.kw != kw[i] || o.cin != (i ? C : kP1CI) || o.cout != C) return false;
+    if ((o.act != 0) != leaky) return false;
+    if (leaky && (o.alpha != ops[st[0]].alpha || !(o.alpha >= 0.f && o.alpha <= 1.f))) return false;
+  }
+  if (od.h != (d.h - 4) / 2 || od.w != (d.w - 4) / 2 || od.c != C) return false;
+  std::vector<_Float16> w(P1G::WHALFS, static_cast<_Float16>(0.f));
+  const int woff[4] = {P1G::WOFF1, P1G::WOFF2, P1G::WOFF3, P1G::WOFF4};
+  for (int i = 0; i < 4; ++i) {
+    const OpInfo& o = ops[st[i]];
+    const int ks = i ? P1G::KS : P1G::KS1, K = 3 * o.cin;
+    for (int n = 0; n < C; ++n)
+      for (int k = 0; k < K; ++k) {
+        const float v = o.w[size_t(k) * C + n];  // HWIO: (tap * cin + ci) * cout + n
+        uint32_t bits;
+        memcpy(&bits, &v, 4);
+        bits &= 0xFFFFE000u;
+        float hv;
+        memcpy(&hv, &bits, 4);
+        w[woff[i] + n * 16 * ks + k] = static_cast<_Float16>(hv);
+        w[woff[i] + 32 * 16 * ks + n * 16 * ks + k] = static_cast<_Float16>(v - hv);
+      }
+  }
+  std::vector<float> b(128, 0.f);
+  for (int i = 0; i < 4; ++i)
+    for (int n = 0; n < C; ++n) b[32 * i + n] = ops[st[i]].b[n];
+  const size_t wbytes = (w.size() * 2 + 15) & ~size_t(15);
+  hipError_t e = hipMalloc(&cp.d_p0, wbytes + b.size() * 4);
+  if (e == hipSuccess) e = hipMemcpy(cp.d_p0, w.data(), w.size() * 2, hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = hipMemcpy(static_cast<unsigned char*>(cp.d_p0) + wbytes, b.data(), b.size() * 4, hipMemcpyHostToDevice);
+  cp.p1fn = leaky ? p1_chain_kernel<kP1W, kP1CI, kP1Band, true> : p1_chain_kernel<kP1W, kP1CI, kP1Band, false>;
+  cp.p0_lds = P1G::LDS;
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(cp.p1fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            int(cp.p0_lds));
+  int per_cu = 0;
+  if (e == hipSuccess)
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(cp.p1fn), kP0Threads,
+                                                     cp.p0_lds);
+  if (e != hipSuccess || per_cu < 1) {
+    (void)hipGetLastError();
+    if (cp.d_p0) (void)hipFree(cp.d_p0);
+    cp.d_p0 = nullptr;
+    cp.p1fn = nullptr;
+    return false;
+  }
+  cp.p0_blocks_per_cu = per_cu;
+  P1Args& p = cp.p1;
+  p.w = static_cast<const _Float16*>(cp.d_p0);
+  p.bias = reinterpret_cast<const float*>(static_cast<unsigned char*>(cp.d_p0) + wbytes);
+  p.H_in = d.h;
+  p.H_out = od.h;
+  p.n_bands = (od.h + kP1Band - 1) / kP1Band;
+  p.alpha = leaky ? ops[st[0]].alpha : 0.f;
+  if (getenv("HBK_DEBUG_EMBED"))
+    fprintf(stderr, "hbk p1 chain: %dx%dx%d -> %dx%dx%d, band %d (%d bands), LDS %zu B, %d blocks/CU\n", d.h, d.w,
+            d.c, od.h, od.w, od.c, kP1Band, p.n_bands, cp.p0_lds, per_cu);
+  return true;
+}
+
 // Builds the chains for ops [o0, o1) applied to images of dims `in`, reading
 // image i from row_off[i % ipc] of source clip i / ipc.
 int build_segment(const std::vector<OpInfo>& ops, int o0, int o1, Dims in, int ipc,
@@ -1622,7 +1896,7 @@ int build_segment(const std::vector<OpInfo>& ops, int o0, int o1, Dims in, int i
       Dims od;
       const int rc = layout_split(ops, stage_ops, d, a, cp, od);
       if (rc) return rc;
-      plan_p0(ops, stage_ops, a, d, od, cp);
+      if (!plan_p0(ops, stage_ops, a, d, od, cp)) plan_p1(ops, stage_ops, a, d, od, cp);
       cp.x.dbg_slot = static_cast<int>(prog.chains.size() % 4);
       if (const char* e = getenv("HBK_DEBUG_SKIP")) cp.x.dbg_skip = atoi(e);
       cp.src_buf = src_buf;
@@ -1814,6 +2088,23 @@ int run_program(const Program& prog, const float* in, int64_t n_units, int64_t i
           if (blocks <= 0) continue;
           hipLaunchKernelGGL(c.p0fn, dim3(unsigned(blocks)), dim3(kP0Threads), c.p0_lds, stream, pa);
           HBK_LAUNCH_CHECK("p0_chain_kernel");
+          continue;
+        }
+      }
+      if (c.p1fn) {
+        P1Args pa = c.p1;
+        pa.in = c.src_buf < 0 ? in + u0 * in_unit_stride : bufs[c.src_buf];
+        pa.src_img_stride = c.src_buf < 0 ? in_unit_stride : c.x.src_clip_stride;
+        pa.out = c.dst_buf < 0 ? out + u0 * out_unit_floats : bufs[c.dst_buf];
+        pa.n_img = nu * imgs_per_unit[k];
+        const bool aligned = !(reinterpret_cast<uintptr_t>(pa.in) & 15) && !(pa.src_img_stride & 3) &&
+                             !(reinterpret_cast<uintptr_t>(pa.out) & 15);
+        if (aligned && pa.n_img * pa.n_bands < (int64_t(1) << 31)) {
+          const int64_t tasks = pa.n_img * pa.n_bands;
+          const int64_t blocks = std::min<int64_t>(tasks, persistent_blocks(c.p0_blocks_per_cu));
+          if (blocks <= 0) continue;
+          hipLaunchKernelGGL(c.p1fn, dim3(unsigned(blocks)), dim3(kP0Threads), c.p0_lds, stream, pa);
+          HBK_LAUNCH_CHECK("p1_chain_kernel");
           continue;
         }
       }
