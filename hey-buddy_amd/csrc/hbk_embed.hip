@@ -1634,7 +1634,7 @@ int layout_split(const std::vector<OpInfo>& ops, const std::vector<int>& stage_o
     return HBK_ERR_UNSUPPORTED;
   }
   if (band == od.h)
-    while (G < 64 && lds_total(G * 2, band, resident) <= lds_budget) G *= 2;
+    while (G < 64 && lds_total(G + 1, band, resident) <= lds_budget) ++G;  // any G: fill the LDS budget
   x.G = G;
   x.band = band;
   x.n_bands = (od.h + band - 1) / band;
