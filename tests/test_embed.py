@@ -117,6 +117,34 @@ def test_embed_clips_ragged_batches(precision):
         assert ok, f"n={n}: max |diff| {worst}"
 
 
+@pytest.mark.gpu
+def test_embed_pattern_kernels_match_generic_path(monkeypatch, capfd):
+    """The plan picks the p0 / p1 pattern kernels for SE20's chains 0 and 1;
+    with them disabled the generic split-f16 kernel runs every chain. Both
+    paths match the oracle and each other."""
+    from heybuddy.embedding_graph import se20_graph
+    from heybuddy.kernels import EmbedPlan
+    g = se20_graph()
+    mel = _mel_clips(4, seed=21)
+    ref = _oracle_clip_embeddings(g, mel)
+    monkeypatch.setenv("HBK_DEBUG_EMBED", "1")
+    capfd.readouterr()
+    plan = EmbedPlan(g, precision="split")
+    err = capfd.readouterr().err
+    assert "hbk p0 chain" in err and "hbk p1 chain" in err, err
+    out_p = plan.clips(torch.from_numpy(mel).cuda()).cpu().numpy()
+    monkeypatch.setenv("HBK_EMBED_NO_P0", "1")
+    monkeypatch.setenv("HBK_EMBED_NO_P1", "1")
+    plan_g = EmbedPlan(g, precision="split")
+    err = capfd.readouterr().err
+    assert "hbk p0 chain" not in err and "hbk p1 chain" not in err, err
+    out_g = plan_g.clips(torch.from_numpy(mel).cuda()).cpu().numpy()
+    for out in (out_p, out_g):
+        ok, worst = _close(out, ref)
+        assert ok, f"max |diff| {worst}"
+    assert np.abs(out_p - out_g).max() <= 1e-5 * (1.0 + np.abs(ref).max())
+
+
 def _generic_graph(seed=9):
     """Shapes the SE20 stand-in does not have: cin 1 with a 2x3 kernel, channel
     counts that are not multiples of 8 / 32 (12, 40, 70, 33), a 1x1 conv, a
