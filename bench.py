@@ -10,7 +10,8 @@ Workloads (BASELINE.json configs; --config, default 2 = configs[1]):
      16 reference windows per clip (hbk_embed_clips; SE20 stand-in graph — the
      real ONNX graph is absent offline), NaN-row replacement.
   3  the same after on-device augmentation (configs[2]): background-noise mix
-     + IR reverb with p forced to 1, one IR per 128-clip batch (hbk_augment).
+     + IR reverb with p forced to 1, one IR per 128-clip batch, and the
+     reference's per-batch Gain (p 1.0 by default) (hbk_augment).
   4  classifier training (configs[3]): stage-1 steps at the reference's global
      batch of 1,100 embeddings (50 positive / 50 adversarial / 1,000 negative)
      sampled on the device; metric embeddings/s trained.
@@ -214,7 +215,7 @@ def setup_featurize(args, dev, rank, world, seed):
                         peak_basis=("f16 dense MFMA peak / 3 (hi*hi + hi*lo + lo*hi per f32-accurate MAC)"
                                     if split else "f32-input MFMA dense peak"),
                         algorithmic_flops_per_clip=2.0 * eplan.macs_per_clip)
-        return roof("augment_kernel (hbk_augment: noise mix + 23040-pt circular FFT reverb, 1 launch)",
+        return roof("augment_kernel (hbk_augment: gain + noise mix + 23040-pt circular FFT reverb, 1 launch)",
                     "hbm", n * AUG_T * 4 * 3, ms, "GB/s", load_traffic(pmc, "augment_kernel"),
                     algorithmic_bytes_per_clip=AUG_T * 4 * 3)
 
@@ -247,7 +248,7 @@ def setup_featurize(args, dev, rank, world, seed):
         "metric": "audio clips/sec featurized+trained, 1.5 s @16 kHz, 1/2/4/8 GPU",
         "data": "synthetic 1.5 s @16 kHz clips (seeded), SE20 stand-in embedding graph"
                 + (", synthetic noise bank + IR bank" if augment else ""),
-        "config": {"workload": ("configs[2]: 100k clips on-GPU augment (noise mix + IR reverb, p=1) -> mel -> "
+        "config": {"workload": ("configs[2]: 100k clips on-GPU augment (gain + noise mix + IR reverb, p=1) -> mel -> "
                                 "embed per GPU") if augment else
                    "configs[1]: 100k clips mel-STFT + speech-embedding forward per GPU",
                    "clips_per_rank": n, "clip_samples": int(clips.shape[1]), "mel_frames_per_clip": N_FRAMES,

@@ -276,7 +276,7 @@ constexpr int kBins2 = 128;
 constexpr int kWaves2 = 8;            // 512-thread blocks sharing one constant table
 constexpr int kThreads2 = 64 * kWaves2;
 constexpr int kFramesPerBlock2 = kFramesPerWave * kWaves2;
-constexpr int kBlocksPerCU2 = 2;      // <= 128 VGPRs, 78 KB LDS: 4 waves / SIMD
+constexpr int kBlocksPerCU2 = 2;      // <= 128 VGPRs, 80 KB LDS: 4 waves / SIMD
 
 struct Mel2Args {
   const float* pcm;
@@ -295,11 +295,16 @@ struct Mel2Args {
   float out_add;
 };
 
-// lane j of each 16-lane row receives v from lane (16 - j) mod 16
-__device__ __forceinline__ float from_partner(float v) {
-  int t = __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false);  // row_mirror
-  t = __builtin_amdgcn_mov_dpp(t, 0x121, 0xF, 0xF, false);                               // row_ror:1
-  return __builtin_bit_cast(float, t);
+// lane j >= 1 of each 16-lane row receives v from lane 16 - j; lane 0 keeps
+// `own`: row_mirror (mirror()), then row_shr:1 (shr1_or()) whose out-of-row
+// source leaves lane 0's old value in place (bound_ctrl off). All mirrors of
+// a group are issued before the shifts (no DPP read-after-write nops).
+__device__ __forceinline__ int mirror(float v) {
+  return __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false);
+}
+__device__ __forceinline__ float shr1_or(int t, float own) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, own), t, 0x111,
+                                                               0xF, 0xF, false));
 }
 
 // per-lane constant table in LDS, [entry][lane j] (16-lane rows: conflict-free
@@ -308,8 +313,11 @@ constexpr int kCTw = 0;                   // 16 entries: W256^(j k1)
 constexpr int kCWs = 16;                  // 8 entries: -i W512^(j + 16 k2)
 constexpr int kCWa = 24;                  // kTapsA / 2 pairs: weights of filter j
 constexpr int kCWb = kCWa + kTapsA / 2;   // kTapsB / 2 pairs: weights of filter 31 - j
-constexpr int kCN = kCWb + kTapsB / 2;    // 36 entries = 4.6 KB
+constexpr int kCWin = kCWb + kTapsB / 2;  // 16 entries: window pair (w[32 n1 + 2 j], w[32 n1 + 2 j + 1])
+constexpr int kCN = kCWin + 16;           // 52 entries = 6.5 KB
 
+// (Computing the twiddles from 4 table reads + products, or the split twiddles
+// from one read x W32^k2, trades LDS reads for VALU: measured 2-5 % slower.)
 template <bool EDGE0, class C>
 __global__ void __launch_bounds__(kThreads2) __attribute__((amdgpu_waves_per_eu(4)))
 mel_frames_v2_kernel(Mel2Args a) {
@@ -328,8 +336,10 @@ mel_frames_v2_kernel(Mel2Args a) {
       c = cf{t.x, t.y};
     } else if (e < kCWb) {
       c = *reinterpret_cast<const cf*>(a.mel_w2 + jj * kTapsA + 2 * (e - kCWa));
-    } else {
+    } else if (e < kCWin) {
       c = *reinterpret_cast<const cf*>(a.mel_w2 + 16 * kTapsA + jj * kTapsB + 2 * (e - kCWb));
+    } else {
+      c = *reinterpret_cast<const cf*>(a.window + 2 * (16 * (e - kCWin) + jj));
     }
     s_c[i] = c;
   }
@@ -338,9 +348,6 @@ mel_frames_v2_kernel(Mel2Args a) {
   const int slot = wave * kFramesPerWave + (lane >> 4);
   const int j = lane & 15;
   const cf* cj = s_c + j;  // entry e of this lane: cj[16 e]
-  C win[16];
-#pragma unroll
-  for (int n1 = 0; n1 < 16; ++n1) win[n1] = cpx<C>(*reinterpret_cast<const cf*>(a.window + 2 * (16 * n1 + j)));
   __syncthreads();
 
   const uint32_t total = static_cast<uint32_t>(a.n_clips * a.n_frames);
@@ -370,13 +377,20 @@ mel_frames_v2_kernel(Mel2Args a) {
 
   // one group: transform the frames in `cur`, prefetching group grp + stride into `nxt`
   auto process = [&](uint32_t grp, const C (&cur)[16], C (&nxt)[16]) {
+    // window and twiddles come from the LDS table in two batches of reads
+    // (one wait each) instead of VGPR-resident window + per-use twiddle reads
     C v[16];
 #pragma unroll
-    for (int n1 = 0; n1 < 16; ++n1) v[n1] = (n1 < n1lo || n1 >= n1hi) ? C{0.f, 0.f} : cur[n1] * win[n1];
+    for (int n1 = n1lo; n1 < n1hi; ++n1) v[n1] = cpx<C>(cj[16 * (kCWin + n1)]);
+    C tw[16];
+#pragma unroll
+    for (int k1 = 1; k1 < 16; ++k1) tw[k1] = cpx<C>(cj[16 * (kCTw + k1)]);
+#pragma unroll
+    for (int n1 = 0; n1 < 16; ++n1) v[n1] = (n1 < n1lo || n1 >= n1hi) ? C{0.f, 0.f} : cur[n1] * v[n1];
     load(frame_src(grp + gridDim.x), nxt);  // prefetch (clamped past the end)
     fft16(v);
 #pragma unroll
-    for (int k1 = 1; k1 < 16; ++k1) v[k1] = cmul(v[k1], cpx<C>(cj[16 * (kCTw + k1)]));
+    for (int k1 = 1; k1 < 16; ++k1) v[k1] = cmul(v[k1], tw[k1]);
 #pragma unroll
     for (int k1 = 0; k1 < 16; ++k1) buf[k1 * kRow2 + j] = cf{v[k1].x, v[k1].y};
     wave_sync();
@@ -386,18 +400,26 @@ mel_frames_v2_kernel(Mel2Args a) {
       v[2 * q] = C{t.x, t.y};
       v[2 * q + 1] = C{t.z, t.w};
     }
+    C ws[8];
+#pragma unroll
+    for (int k2 = 0; k2 < 8; ++k2) ws[k2] = cpx<C>(cj[16 * (kCWs + k2)]);
     fft16(v);  // v[k2] = Z[j + 16 k2]
     // 2 X[k] = (Z[k] + Z*[256-k]) + (-i W512^k) (Z[k] - Z*[256-k]),  k = j + 16 k2
     float p[8];
+    int mx[8], my[8];
 #pragma unroll
     for (int k2 = 0; k2 < 8; ++k2) {
-      const C o = v[15 - k2];
-      C zr = C{from_partner(o.x), from_partner(o.y)};
-      if (j == 0) zr = v[(16 - k2) & 15];
+      mx[k2] = mirror(v[15 - k2].x);
+      my[k2] = mirror(v[15 - k2].y);
+    }
+#pragma unroll
+    for (int k2 = 0; k2 < 8; ++k2) {
+      const C own = v[(16 - k2) & 15];  // lane 0: Z[256 - 16 k2] is its own
+      const C zr = C{shr1_or(mx[k2], own.x), shr1_or(my[k2], own.y)};
       const C zc = C{zr.x, -zr.y};  // Z*[256 - k]
       const C s = v[k2] + zc;
       const C d = v[k2] - zc;
-      const C X = s + cmul(d, cpx<C>(cj[16 * (kCWs + k2)]));
+      const C X = s + cmul(d, ws[k2]);
       p[k2] = fmaf(X.x, X.x, X.y * X.y);
     }
     wave_sync();

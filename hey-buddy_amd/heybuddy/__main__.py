@@ -24,7 +24,8 @@ from heybuddy.constants import *  # noqa: F401,F403
 from heybuddy.constants import (DEFAULT_ACTIVATION_THRESHOLD, DEFAULT_ADVERSARIAL_BATCH_SIZE,
                                 DEFAULT_ADVERSARIAL_SAMPLES, DEFAULT_AUGMENT_BACKGROUND_NOISE_MAX_SNR_DB,
                                 DEFAULT_AUGMENT_BACKGROUND_NOISE_MIN_SNR_DB,
-                                DEFAULT_AUGMENT_BACKGROUND_NOISE_PROB, DEFAULT_AUGMENT_REVERB_PROB,
+                                DEFAULT_AUGMENT_BACKGROUND_NOISE_PROB, DEFAULT_AUGMENT_GAIN_PROB,
+                                DEFAULT_AUGMENT_REVERB_PROB,
                                 DEFAULT_CHECKPOINT_STEPS, DEFAULT_HIGH_LOSS_THRESHOLD, DEFAULT_LAYER_DIM,
                                 DEFAULT_LAYERS, DEFAULT_LEARNING_RATE, DEFAULT_LOGGING_STEPS,
                                 DEFAULT_NEGATIVE_BATCH_SIZE, DEFAULT_NEGATIVE_WEIGHT,
@@ -100,6 +101,7 @@ def build_embeddings(n: int, seed: int, device: torch.device, augmenter=None, ch
 @click.option("--augmentation-background-noise-min-snr-db", type=float, default=DEFAULT_AUGMENT_BACKGROUND_NOISE_MIN_SNR_DB, show_default=True)
 @click.option("--augmentation-background-noise-max-snr-db", type=float, default=DEFAULT_AUGMENT_BACKGROUND_NOISE_MAX_SNR_DB, show_default=True)
 @click.option("--augmentation-reverb-prob", type=float, default=DEFAULT_AUGMENT_REVERB_PROB, show_default=True)
+@click.option("--augmentation-gain-prob", type=float, default=DEFAULT_AUGMENT_GAIN_PROB, show_default=True)
 @click.option("--logging-steps", type=int, default=DEFAULT_LOGGING_STEPS, show_default=True)
 @click.option("--validation-steps", type=int, default=DEFAULT_VALIDATION_STEPS, show_default=True)
 @click.option("--checkpoint-steps", type=int, default=DEFAULT_CHECKPOINT_STEPS, show_default=True)
@@ -123,6 +125,7 @@ def train(phrase: str, additional_phrase: List[str], wandb_entity: Optional[str]
           target_false_positive_rate: float, dynamic_negative_weight: bool, negative_weight: float,
           augmentation_background_noise_prob: float, augmentation_background_noise_min_snr_db: float,
           augmentation_background_noise_max_snr_db: float, augmentation_reverb_prob: float,
+          augmentation_gain_prob: float,
           logging_steps: int, validation_steps: int, checkpoint_steps: int, positive_samples: int,
           adversarial_samples: int, negative_samples: int, positive_batch_size: int,
           negative_batch_size: int, adversarial_batch_size: int, validation_samples: int,
@@ -153,7 +156,7 @@ def train(phrase: str, additional_phrase: List[str], wandb_entity: Optional[str]
                          batch_size=128, background_noise_prob=augmentation_background_noise_prob,
                          background_noise_min_snr_db=augmentation_background_noise_min_snr_db,
                          background_noise_max_snr_db=augmentation_background_noise_max_snr_db,
-                         reverb_prob=augmentation_reverb_prob)
+                         reverb_prob=augmentation_reverb_prob, gain_prob=augmentation_gain_prob)
     pos = build_embeddings(positive_samples, seed + 1, device, aug, kind="positive", phrase=phrase)
     adv = build_embeddings(adversarial_samples, seed + 2, device, aug, kind="adversarial")
     neg = build_embeddings(negative_samples, seed + 3, device, aug, kind="negative").half()

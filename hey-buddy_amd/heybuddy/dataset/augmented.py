@@ -8,12 +8,15 @@ Semantics kept from the reference:
 * background noise: consecutive noise clips (cycling through the bank) are
   concatenated until they cover batch * T samples and cut into consecutive
   T-sample segments (:246-267); SNR ~ U[min, max] dB per clip (:269-270);
-* reverb: ONE impulse response per batch, taken in order (:188-192).
+* reverb: ONE impulse response per batch, taken in order (:188-192);
+* gain: torch_audiomentations Gain in per_batch mode (:116-120), one factor
+  10^(g/20), g ~ U[-18, 6] dB, per batch with probability gain_prob (1.0),
+  applied before the noise mix (it is the last transform of augment_batch).
 Differences (by design): the IR spectra are computed once for the whole bank
 instead of once per batch, every batch of a call is one kernel launch, and
 clips never leave the device (the reference copies each clip back to host,
 :419). The other augmentations (7-band EQ, tanh distortion, pitch shift,
-band-stop, colored noise, gain) are not on this path yet.
+band-stop, colored noise) are not on this path yet.
 """
 from __future__ import annotations
 
@@ -24,7 +27,9 @@ import torch
 
 from heybuddy.constants import (DEFAULT_AUGMENT_BACKGROUND_NOISE_MAX_SNR_DB,
                                 DEFAULT_AUGMENT_BACKGROUND_NOISE_MIN_SNR_DB,
-                                DEFAULT_AUGMENT_BACKGROUND_NOISE_PROB, DEFAULT_AUGMENT_REVERB_PROB)
+                                DEFAULT_AUGMENT_BACKGROUND_NOISE_PROB, DEFAULT_AUGMENT_GAIN_MAX_DB,
+                                DEFAULT_AUGMENT_GAIN_MIN_DB, DEFAULT_AUGMENT_GAIN_PROB,
+                                DEFAULT_AUGMENT_REVERB_PROB)
 from heybuddy.kernels import ReverbPlan
 
 __all__ = ["BatchAugmenter"]
@@ -39,7 +44,10 @@ class BatchAugmenter:
                  background_noise_prob: float = DEFAULT_AUGMENT_BACKGROUND_NOISE_PROB,
                  background_noise_min_snr_db: float = DEFAULT_AUGMENT_BACKGROUND_NOISE_MIN_SNR_DB,
                  background_noise_max_snr_db: float = DEFAULT_AUGMENT_BACKGROUND_NOISE_MAX_SNR_DB,
-                 reverb_prob: float = DEFAULT_AUGMENT_REVERB_PROB) -> None:
+                 reverb_prob: float = DEFAULT_AUGMENT_REVERB_PROB,
+                 gain_prob: float = DEFAULT_AUGMENT_GAIN_PROB,
+                 min_gain_in_db: float = DEFAULT_AUGMENT_GAIN_MIN_DB,
+                 max_gain_in_db: float = DEFAULT_AUGMENT_GAIN_MAX_DB) -> None:
         self.plan = ReverbPlan(device)
         self.device = self.plan.device
         if background_noise_prob > 0 and not noise:
@@ -51,6 +59,9 @@ class BatchAugmenter:
         self.p_reverb = float(reverb_prob)
         self.snr_min = float(background_noise_min_snr_db)
         self.snr_max = float(background_noise_max_snr_db)
+        self.p_gain = float(gain_prob)
+        self.gain_min_db = float(min_gain_in_db)
+        self.gain_max_db = float(max_gain_in_db)
         self.ring = None
         self.lengths: List[int] = []
         self.starts: List[int] = []
@@ -67,12 +78,15 @@ class BatchAugmenter:
         self.ir_idx = 0
 
     def plan_batches(self, n: int):
-        """Per-clip noise offsets, SNRs and spectrum indices for n clips (host
-        bookkeeping that mirrors the reference's dataset iteration)."""
+        """Per-clip noise offsets, spectrum indices and gains (dB) for n clips
+        (host bookkeeping that mirrors the reference's dataset iteration)."""
         noise_off = np.full(n, -1, dtype=np.int64)
         spec_idx = np.full(n, -1, dtype=np.int32)
+        gain_db = np.zeros(n, dtype=np.float32)
         for b0 in range(0, n, self.batch_size):
             nb = min(self.batch_size, n - b0)
+            if np.random.rand() < self.p_gain:  # per_batch: one gain for the batch
+                gain_db[b0:b0 + nb] = np.random.uniform(self.gain_min_db, self.gain_max_db)
             if np.random.rand() < self.p_noise and self.ring is not None:
                 noise_off[b0:b0 + nb] = self.starts[self.noise_idx] + np.arange(nb) * T
                 covered = 0
@@ -82,15 +96,18 @@ class BatchAugmenter:
             if np.random.rand() < self.p_reverb and self.spectra is not None:
                 spec_idx[b0:b0 + nb] = self.ir_idx
                 self.ir_idx = (self.ir_idx + 1) % self.spectra.shape[0]
-        return noise_off, spec_idx
+        return noise_off, spec_idx, gain_db
 
     def __call__(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """x [n, >= 23040] f32 on the device -> augmented [n, 23040]."""
         n = x.shape[0]
-        noise_off, spec_idx = self.plan_batches(n)
+        noise_off, spec_idx, gain_db = self.plan_batches(n)
         ring_len = 0 if self.ring is None else self.ring.numel()
         if ring_len:
             noise_off = np.where(noise_off >= 0, noise_off % ring_len, -1)
         snr = torch.rand(n, device=self.device) * (self.snr_max - self.snr_min) + self.snr_min
+        gain = None
+        if self.p_gain > 0:  # torch_audiomentations convert_decibels_to_amplitude_ratio
+            gain = torch.pow(10.0, torch.from_numpy(gain_db) / 20.0)
         return self.plan.augment(x, self.ring, torch.from_numpy(noise_off), snr, self.spectra,
-                                 torch.from_numpy(spec_idx), out=out)
+                                 torch.from_numpy(spec_idx), out=out, gain=gain)

@@ -408,8 +408,9 @@ class ReverbPlan:
 
     def augment(self, x: torch.Tensor, ring: torch.Tensor | None, noise_off: torch.Tensor,
                 snr_db: torch.Tensor, spectra: torch.Tensor | None, spec_idx: torch.Tensor,
-                out: torch.Tensor | None = None) -> torch.Tensor:
-        """x [n, >= T] -> out [n, T]; per clip noise (noise_off >= 0) then reverb (spec_idx >= 0)."""
+                out: torch.Tensor | None = None, gain: torch.Tensor | None = None) -> torch.Tensor:
+        """x [n, >= T] -> out [n, T]; per clip gain (linear factor, if given), then
+        noise (noise_off >= 0), then reverb (spec_idx >= 0)."""
         n = x.shape[0]
         if x.dim() != 2 or x.shape[1] < self.T or x.stride(1) != 1 or x.device != self.device:
             raise ValueError(f"x must be [n, >= {self.T}] f32 rows on {self.device}")
@@ -420,6 +421,10 @@ class ReverbPlan:
         snr_db = snr_db.to(self.device, torch.float32).contiguous()
         if noise_off.numel() != n or spec_idx.numel() != n or snr_db.numel() != n:
             raise ValueError("per-clip arrays must have n entries")
+        if gain is not None:
+            gain = gain.to(self.device, torch.float32).contiguous()
+            if gain.numel() != n:
+                raise ValueError("gain must have n entries")
         if bool((noise_off >= 0).any()) and (ring is None or ring.numel() == 0):
             raise ValueError("noise requested without a noise ring")
         if spectra is not None and bool((spec_idx >= spectra.shape[0]).any()):
@@ -428,7 +433,8 @@ class ReverbPlan:
         check(lib().hbk_augment(self._handle, ptr(x), n, x.stride(0),
                                 ptr(ring) if ring is not None else None, ring_len, ptr(noise_off),
                                 ptr(snr_db), ptr(spectra) if spectra is not None else None,
-                                ptr(spec_idx), ptr(out), out.stride(0), stream_ptr(self.device)),
+                                ptr(spec_idx), ptr(gain) if gain is not None else None, ptr(out),
+                                out.stride(0), stream_ptr(self.device)),
               "hbk_augment")
         return out
 

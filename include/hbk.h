@@ -211,14 +211,16 @@ int hbk_reverb_spectrum(const hbk_reverb_plan* plan, const float* kernels, int64
                         int64_t stride, float* spectra, void* stream);
 
 /* Per clip i of x [n_clips, x_stride] (first T samples used):
+ *   if gain != NULL: x = gain[i] x (torch_audiomentations Gain, applied before the
+ *      noise mix as in the reference's batch chain, augmented.py:114-118, :383-392);
  *   if noise_off[i] >= 0: y = x + 10^((10 log10(|x|^2/|n|^2) - snr_db[i]) / 20) n,
  *      n = noise_ring[(noise_off[i] + t) mod ring_len], t < T;
  *   if spec_idx[i] >= 0: y = mean|y| * c / (mean|c| + 1e-14), c = irfft(rfft(y) * spectra[spec_idx[i]]).
  * out [n_clips, out_stride] (may equal x). All pointers are device pointers. */
 int hbk_augment(const hbk_reverb_plan* plan, const float* x, int64_t n_clips, int64_t x_stride,
                 const float* noise_ring, int64_t ring_len, const int64_t* noise_off,
-                const float* snr_db, const float* spectra, const int32_t* spec_idx, float* out,
-                int64_t out_stride, void* stream);
+                const float* snr_db, const float* spectra, const int32_t* spec_idx,
+                const float* gain, float* out, int64_t out_stride, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,11 +1,15 @@
 """Augmentation oracle (TEST INFRASTRUCTURE ONLY, see oracle/__init__.py).
 
-Restates the two batch augmentations of AugmentedAudioGenerator.execute_augment_batch
-(reference src/python/heybuddy/dataset/augmented.py:383-392). Both live in
+Restates three batch augmentations of AugmentedAudioGenerator.execute_augment_batch
+(reference src/python/heybuddy/dataset/augmented.py:114-118, :383-392). Both live in
 third-party packages that are not installed here, so they are restated from
 their published algorithms at the versions environment.yml pins
 (PARITY UNPINNED at the third-party boundary; the reference holds no fixture):
 
+* torch_audiomentations.Gain (min -18 dB, max 6 dB, mode per_batch, p
+  DEFAULT_AUGMENT_GAIN_PROB = 1.0, constants.py:136): y = 10^(g/20) x with
+  g ~ U[-18, 6] dB; the last transform of the torch_audiomentations chain, so
+  it precedes the noise mix and the reverb;
 * torchaudio.functional.add_noise (torchaudio >= 2.3, environment.yml:28),
   called by add_background_noise_to_batch (augmented.py:234-276):
       E_x = ||x||^2, E_n = ||n||^2 (per clip)
@@ -71,10 +75,18 @@ def reverberate(x: np.ndarray, ir: np.ndarray, dtype=np.float64) -> np.ndarray:
     return a_in * y / (np.abs(y).mean(axis=-1, keepdims=True) + 1e-14)
 
 
-def augment_batch(x, noise=None, snr_db=None, ir=None, dtype=np.float64):
-    """noise mix (if noise is given) then reverb (if ir is given), as
-    execute_augment_batch applies them (augmented.py:383-392)."""
+def db_to_amplitude(db) -> np.ndarray:
+    """torch_audiomentations.utils.dsp.convert_decibels_to_amplitude_ratio."""
+    return 10.0 ** (np.asarray(db, dtype=np.float64) / 20.0)
+
+
+def augment_batch(x, noise=None, snr_db=None, ir=None, dtype=np.float64, gain=None):
+    """gain (linear factor per clip, if given), noise mix (if noise is given),
+    then reverb (if ir is given), as execute_augment_batch applies them
+    (augmented.py:114-118 inside augment_batch, then :383-392)."""
     y = np.asarray(x, dtype=dtype)
+    if gain is not None:
+        y = y * np.asarray(gain, dtype=dtype).reshape(-1, 1)
     if noise is not None:
         y = add_noise(y, noise, snr_db, dtype)
     if ir is not None:

@@ -139,3 +139,70 @@ def test_augment_ring_wraparound_and_long_ir():
     for i in range(2):
         ok, worst = _close(out[i], ref[i])
         assert ok, f"clip {i}: max |diff| {worst}"
+
+
+def test_gain_precedes_and_commutes_with_noise_and_reverb():
+    """torch_audiomentations Gain runs before the noise mix and the reverb
+    (augmented.py:114-118, :383-392); both are scale-equivariant (the SNR is
+    relative to the gained clip, the reverb rescales to mean |input|), so the
+    chain with gain g equals g times the chain without it."""
+    x = _clips(3, seed=6)
+    noises, irs = _bank(seed=7)
+    seg, _ = oaug.noise_segments(noises, 0, 3, T)
+    snr = np.array([-5.0, 2.0, 12.0])
+    g = oaug.db_to_amplitude([-18.0, 0.0, 6.0])
+    np.testing.assert_allclose(g, [10 ** -0.9, 1.0, 10 ** 0.3])
+    y = oaug.augment_batch(x, seg, snr, irs[1], gain=g)
+    ref = g[:, None] * oaug.augment_batch(x, seg, snr, irs[1])
+    np.testing.assert_allclose(y, ref, rtol=1e-9, atol=1e-12 * np.abs(ref).max())
+    np.testing.assert_allclose(oaug.augment_batch(x, gain=g), g[:, None] * x, rtol=0, atol=0)
+
+
+@pytest.mark.gpu
+def test_augment_gain_parity():
+    from heybuddy.kernels import ReverbPlan
+    plan = ReverbPlan()
+    x = _clips(4, seed=12)
+    noises, irs = _bank(seed=13)
+    ring = np.concatenate(noises)
+    # clip 0: gain + noise + reverb; 1: gain + reverb; 2: gain only; 3: gain + noise
+    noise_off = np.array([0, -1, -1, T])
+    snr = np.array([4.0, 0.0, 0.0, -3.0])
+    spec_idx = np.array([0, 0, -1, -1])
+    gain_db = np.array([-18.0, 6.0, -7.25, 1.5], dtype=np.float32)
+    gain = torch.pow(10.0, torch.from_numpy(gain_db) / 20.0)
+    H = plan.spectra(ReverbPlan.rotated_kernel(torch.from_numpy(irs[0]), T)[None].cuda())
+    out = plan.augment(torch.from_numpy(x).float().cuda(), torch.from_numpy(ring).float().cuda(),
+                       torch.from_numpy(noise_off), torch.from_numpy(snr), H,
+                       torch.from_numpy(spec_idx), gain=gain).cpu().numpy()
+    xf = x.astype(np.float32).astype(np.float64)
+    g = gain.numpy().astype(np.float64)
+    r32 = ring.astype(np.float32).astype(np.float64)
+    ref = np.empty_like(xf)
+    ref[0] = oaug.augment_batch(xf[:1], r32[None, :T], snr[:1], irs[0], gain=g[:1])[0]
+    ref[1] = oaug.augment_batch(xf[1:2], ir=irs[0], gain=g[1:2])[0]
+    ref[2] = oaug.augment_batch(xf[2:3], gain=g[2:3])[0]
+    ref[3] = oaug.augment_batch(xf[3:4], r32[None, T:2 * T], snr[3:4], gain=g[3:4])[0]
+    for i in range(4):
+        ok, worst = _close(out[i], ref[i])
+        assert ok, f"clip {i}: max |diff| {worst}"
+
+
+@pytest.mark.gpu
+def test_batch_augmenter_gain_is_per_batch():
+    """mode="per_batch": one gain per batch of 128, 10^(g/20) with g in
+    [-18, 6] dB; gain_prob 0 leaves the clips untouched."""
+    from heybuddy.dataset.augmented import BatchAugmenter
+    x = torch.from_numpy(_clips(300, seed=14)).float().cuda()
+    np.random.seed(5)
+    aug = BatchAugmenter(device=0, batch_size=128, background_noise_prob=0.0, reverb_prob=0.0)
+    out = aug(x)
+    ratio = (out / x).cpu().numpy()
+    xs = x.cpu().numpy()
+    for b0 in range(0, 300, 128):
+        blk = ratio[b0:b0 + 128][np.abs(xs[b0:b0 + 128]) > 1e-3]
+        g = np.median(blk)
+        np.testing.assert_allclose(blk, g, rtol=1e-6)
+        assert 10 ** (-18 / 20) * (1 - 1e-6) <= g <= 10 ** (6 / 20) * (1 + 1e-6)
+    off = BatchAugmenter(device=0, background_noise_prob=0.0, reverb_prob=0.0, gain_prob=0.0)
+    assert torch.equal(off(x), x)

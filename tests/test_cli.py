@@ -21,7 +21,7 @@ REFERENCE_OPTIONS = [
     "--learning-rate", "--high-loss-threshold", "--target-false-positive-rate",
     "--dynamic-negative-weight", "--negative-weight", "--augmentation-background-noise-prob",
     "--augmentation-background-noise-min-snr-db", "--augmentation-background-noise-max-snr-db",
-    "--augmentation-reverb-prob", "--logging-steps", "--validation-steps", "--checkpoint-steps",
+    "--augmentation-reverb-prob", "--augmentation-gain-prob", "--logging-steps", "--validation-steps", "--checkpoint-steps",
     "--positive-samples", "--adversarial-samples", "--positive-batch-size", "--negative-batch-size",
     "--adversarial-batch-size", "--validation-samples", "--testing-positive-samples",
     "--testing-adversarial-samples", "--resume", "--debug",
