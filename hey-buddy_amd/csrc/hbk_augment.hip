@@ -8,15 +8,17 @@
 // (augmented.py:386-392) of AugmentedAudioGenerator.execute_augment_batch.
 //
 // One workgroup (1024 threads) per clip, the whole clip resident in LDS:
-//   load x (and the clip's noise segment, in registers) -> E_x, E_n ->
-//   y = x + 10^((10 log10(E_x/E_n) - snr)/20) n -> a_in = mean|y|
+//   x and the clip's noise segment arrive in registers (loaded after the
+//   previous clip's inverse FFT) -> E_x, E_n ->
+//   y = x + 10^((10 log10(E_x/E_n) - snr)/20) n -> LDS, a_in = mean|y|
 //   circular convolution with the batch's IR kernel of length T = 23040:
 //     z[n] = y[2n] + i y[2n+1], an 11520-point complex FFT done in place in
 //     LDS as four mixed-radix decimation-in-frequency passes 16 x 16 x 9 x 5
 //     (720, 720, 1280 and 2304 independent DFTs per pass, one per thread and
 //     round, radix-16 / 9 / 5 in VGPRs); twiddles W_M^e = HI[e >> 7] LO[e & 127]
 //     from two small LDS tables. Z lands in digit-reversed order (zaddr); the
-//     real-FFT split, * H[k] and the inverse split run on (k, M-k) pairs; the
+//     real-FFT split, * H[k] and the inverse split run on (k, M-k) pairs (H and
+//     W_N^k stored bin-major, [k % 16][k / 16], so those loads coalesce); the
 //     inverse transform is the passes reversed (decimation in time, conjugate
 //     twiddles) and lands back in natural order.
 //   y <- a_in * y / (mean|y| + 1e-14), store.
@@ -221,27 +223,57 @@ __device__ __forceinline__ void pass(cf* z, const cf* thi, const cf* tlo) {
   }
 }
 
+#ifdef HBK_PHASE_TIMING
+// Profiling build only (build.py variant "phase"): thread 0 of every block adds
+// the s_memtime cycles of each augment phase (barrier waits included in the
+// phase before them) into g_aug_phase; read by hbk_debug_aug_phase.
+__device__ unsigned long long g_aug_phase[32];
+#define HBK_APH(i)                                                  \
+  do {                                                              \
+    if (threadIdx.x == 0) {                                         \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime();   \
+      atomicAdd(&g_aug_phase[i], t_ - ph_t0);                       \
+      ph_t0 = t_;                                                   \
+    }                                                               \
+  } while (0)
+#else
+#define HBK_APH(i) \
+  do {             \
+  } while (0)
+#endif
+
 // Forward: natural z -> Z[f] at zaddr(f); inverse: the reverse (x kM).
+// (ph_t0 / ph: phase-timing build only, phases ph .. ph + 3)
 template <bool INV>
-__device__ __forceinline__ void transform(cf* z, const cf* thi, const cf* tlo) {
+__device__ __forceinline__ void transform(cf* z, const cf* thi, const cf* tlo,
+                                          [[maybe_unused]] unsigned long long& ph_t0,
+                                          [[maybe_unused]] int ph) {
   if (!INV) {
     pass<16, 720, 1, false>(z, thi, tlo);
     __syncthreads();
+    HBK_APH(ph);
     pass<16, 45, 16, false>(z, thi, tlo);
     __syncthreads();
+    HBK_APH(ph + 1);
     pass<9, 5, 256, false>(z, thi, tlo);
     __syncthreads();
+    HBK_APH(ph + 2);
     pass<5, 1, 0, false>(z, thi, tlo);
     __syncthreads();
+    HBK_APH(ph + 3);
   } else {
     pass<5, 1, 0, true>(z, thi, tlo);
     __syncthreads();
+    HBK_APH(ph);
     pass<9, 5, 256, true>(z, thi, tlo);
     __syncthreads();
+    HBK_APH(ph + 1);
     pass<16, 45, 16, true>(z, thi, tlo);
     __syncthreads();
+    HBK_APH(ph + 2);
     pass<16, 720, 1, true>(z, thi, tlo);
     __syncthreads();
+    HBK_APH(ph + 3);
   }
 }
 
@@ -268,17 +300,77 @@ __device__ __forceinline__ void load_tw(cf* thi, cf* tlo, const float2* ghi, con
   for (int i = threadIdx.x; i < kTwLo; i += kThreads) tlo[i] = cf{glo[i].x, glo[i].y};
 }
 
+// wave sum through DPP (no lane-index VGPRs, unlike __shfl_xor's bpermute
+// addresses, which the compiler hoists and spills): quad_perm [1,0,3,2],
+// [2,3,0,1], row_half_mirror, row_mirror leave each 16-lane row's sum in all
+// of its lanes; the four rows are added from readlane
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum(float v) {
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x141>(v);
+  v += dpp_f<0x140>(v);
+  const int b = __builtin_bit_cast(int, v);
+  return (__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 0)) +
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 16))) +
+         (__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 32)) +
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 48)));
+}
+
+// (results and the wave index are uniform: SGPRs, so nothing here takes a
+// VGPR that could be spilled and reloaded behind the next clip's prefetch)
+__device__ __forceinline__ float sgpr_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+}
 __device__ __forceinline__ float block_sum(float v, float* red) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   __syncthreads();
   if (lane == 0) red[wave] = v;
   __syncthreads();
   float s = 0.f;
   for (int w = 0; w < kThreads / 64; ++w) s += red[w];
-  return s;
+  return sgpr_f(s);  // summed here, not sunk to the use with 16 live partials
 }
+
+// opaque copy of the thread id: index math derived from it stays inside the
+// clip loop (the compiler otherwise hoists dozens of per-element offsets out of
+// it and spills them)
+__device__ __forceinline__ int opaque_tid() {
+  int t;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"(static_cast<int>(threadIdx.x)));
+  return t;
+}
+
+// two block sums in one barrier round (red holds 2 x 16 wave partials)
+__device__ __forceinline__ void block_sum2(float& a, float& b, float* red) {
+  a = wave_sum(a);
+  b = wave_sum(b);
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  __syncthreads();
+  if (lane == 0) {
+    red[wave] = a;
+    red[16 + wave] = b;
+  }
+  __syncthreads();
+  a = b = 0.f;
+  for (int w = 0; w < kThreads / 64; ++w) {
+    a += red[w];
+    b += red[16 + w];
+  }
+  a = sgpr_f(a);
+  b = sgpr_f(b);
+}
+
+// spectrum / W_N^k slot of bin k <= kM: [k % 16][k / 16] (HBK_REVERB_SPECTRUM_SLOTS):
+// the pair loop's lanes walk k in steps of 16, i.e. consecutive slots
+constexpr int kHRow = kM / 16 + 1;  // 721
+constexpr int kHSlots = 16 * kHRow;
+static_assert(kHSlots == HBK_REVERB_SPECTRUM_SLOTS, "spectrum slot layout");
+__device__ __forceinline__ int hslot(int k) { return (k & 15) * kHRow + (k >> 4); }
 
 struct AugArgs {
   const float* x;
@@ -290,12 +382,12 @@ struct AugArgs {
   int64_t ring_len;
   const int64_t* noise_off; // per clip: ring offset of its segment, < 0 = no noise
   const float* snr_db;      // per clip
-  const float2* spectra;    // [n_spec][kM + 1]
+  const float2* spectra;    // [n_spec][kHSlots], bin k at hslot(k)
   const int* spec_idx;      // per clip: spectrum index, < 0 = no reverb
   const float* gain;        // per clip linear gain, or NULL
   const float2* thi;        // W_M^(128 h), h < 90
   const float2* tlo;        // W_M^l, l < 128
-  const float2* twn;        // W_N^k, k <= kM
+  const float2* twn;        // W_N^k, k <= kM, at hslot(k)
 };
 
 __global__ void __launch_bounds__(kThreads) augment_kernel(AugArgs a) {
@@ -312,88 +404,136 @@ __global__ void __launch_bounds__(kThreads) augment_kernel(AugArgs a) {
   // transforms run (one clip per CU: otherwise every load is exposed); the
   // noise segment is read twice (energy, then mix; the 2nd read hits L2)
   constexpr int kPer = (kT + kThreads - 1) / kThreads;
-  float xr[kPer];
-  auto prefetch = [&](int64_t clip) {
+  float xr[kPer], nr[kPer];
+  // the next clip's samples and noise segment  are loaded after this clip's inverse FFT,
+  // so their latency hides behind the |y| sum and the stores without holding
+  // VGPRs through the FFT passes
+  // (noff: the clip's noise offset, read well before, so that no branch waits
+  // on a load queued behind these; vmcnt retires loads in order)
+  auto prefetch = [&](int64_t clip, int64_t noff) {
+    // uniform base + 32-bit per-lane offsets from an opaque thread id (keeps
+    // the 46 per-load addresses from being hoisted out of the clip loop)
+    const int t = opaque_tid();
     const float* x = a.x + clip * a.x_stride;
+    // 32-bit BYTE offsets from a uniform base: global_load's saddr form, one
+    // VGPR per address (ring_len < 2^30, checked on the host)
+    auto at = [](const float* base, uint32_t i) {
+      return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + (i << 2));
+    };
 #pragma unroll
-    for (int u = 0; u < kPer; ++u) {
-      const int s = tid + u * kThreads;
-      if (s < kT) xr[u] = x[s];
+    for (int u = 0; u < kPer; ++u) xr[u] = at(x, static_cast<uint32_t>(min(t + u * kThreads, kT - 1)));
+    if (noff >= 0) {
+      const uint32_t rlen = static_cast<uint32_t>(a.ring_len), r0 = static_cast<uint32_t>(noff);
+#pragma unroll
+      for (int u = 0; u < kPer; ++u) {
+        uint32_t r = r0 + static_cast<uint32_t>(min(t + u * kThreads, kT - 1));
+        r = r >= rlen ? r - rlen : r;
+        nr[u] = at(a.ring, r);
+      }
     }
   };
-  if (blockIdx.x < a.n_clips) prefetch(blockIdx.x);
+  if (blockIdx.x < a.n_clips) prefetch(blockIdx.x, a.noise_off[blockIdx.x]);
+  unsigned long long ph_t0 = 0;
+#ifdef HBK_PHASE_TIMING
+  ph_t0 = __builtin_amdgcn_s_memtime();
+#endif
   for (int64_t clip = blockIdx.x; clip < a.n_clips; clip += gridDim.x) {
-    // 1) y = x + scale n into LDS (torchaudio add_noise: snr0 = 10 (log10 Ex - log10 En),
-    //    scale = 10^((snr0 - snr)/20))
+    // 1) y = x + scale n (torchaudio add_noise: snr0 = 10 (log10 Ex - log10 En),
+    //    scale = 10^((snr0 - snr)/20)) in registers; y goes to LDS once and
+    //    a_in = mean|y| is summed on the way
     const int64_t noff = a.noise_off[clip];
+    const int sp = a.spec_idx[clip];
     const float gain = a.gain ? a.gain[clip] : 1.f;
-    float ex = 0.f;
+    const bool next = clip + gridDim.x < a.n_clips;
+    const int64_t noff_next = __builtin_amdgcn_readfirstlane(static_cast<int>(next ? a.noise_off[clip + gridDim.x] : -1));
+    float ex = 0.f, aa = 0.f;
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
-      const int s = tid + u * kThreads;
-      if (s < kT) {
-        const float v = xr[u] * gain;
-        ex += v * v;
-        zf[s] = v;
-      }
+      xr[u] *= gain;
+      if (tid + u * kThreads < kT) ex += xr[u] * xr[u];
     }
-    if (clip + gridDim.x < a.n_clips) prefetch(clip + gridDim.x);
+    HBK_APH(0);
     if (noff >= 0) {
-      auto noise_at = [&](int s) {
-        int64_t r = noff + s;
-        if (r >= a.ring_len) r -= a.ring_len;
-        return a.ring[r];
-      };
       float en = 0.f;
-      for (int s = tid; s < kT; s += kThreads) {
-        const float v = noise_at(s);
-        en += v * v;
-      }
-      const float Ex = block_sum(ex, red);
-      const float En = block_sum(en, red);
-      const float snr0 = 10.f * (log10f(Ex) - log10f(En));
+#pragma unroll
+      for (int u = 0; u < kPer; ++u)
+        if (tid + u * kThreads < kT) en += nr[u] * nr[u];
+      HBK_APH(1);
+      block_sum2(ex, en, red);
+      HBK_APH(2);
+      const float snr0 = 10.f * (log10f(ex) - log10f(en));
       const float scale = powf(10.f, (snr0 - a.snr_db[clip]) / 20.f);
-      for (int s = tid; s < kT; s += kThreads) zf[s] = zf[s] + scale * noise_at(s);
+#pragma unroll
+      for (int u = 0; u < kPer; ++u) xr[u] += scale * nr[u];
     }
-    __syncthreads();
-    const int sp = a.spec_idx[clip];
+    {
+      const int t = opaque_tid();
+#pragma unroll
+      for (int u = 0; u < kPer; ++u) {
+        const int s = t + u * kThreads;
+        if (s < kT) {
+          zf[s] = xr[u];
+          aa += fabsf(xr[u]);
+        }
+      }
+    }
+    HBK_APH(3);
     float* out = a.out + clip * a.out_stride;
-    if (sp < 0) {
-      for (int s = tid; s < kT; s += kThreads) out[s] = zf[s];
+    if (sp < 0) {  // no reverb: each thread stores the samples it wrote
+      if (next) prefetch(clip + gridDim.x, noff_next);
+      for (int s = opaque_tid(); s < kT; s += kThreads) out[s] = zf[s];
       __syncthreads();
       continue;
     }
-    // 2) a_in = mean |y|
-    float aa = 0.f;
-    for (int s = tid; s < kT; s += kThreads) aa += fabsf(zf[s]);
+    // 2) a_in = mean |y| (block_sum's first barrier also publishes zf)
     const float a_in = block_sum(aa, red) / kT;
+    HBK_APH(4);
     // 3) forward FFT (natural -> permuted)
-    transform<false>(z, thi, tlo);
+    transform<false>(z, thi, tlo, ph_t0, 5);
     // 4) split, multiply by H, inverse split, on (k, M-k) pairs
-    const cf* H = reinterpret_cast<const cf*>(a.spectra) + static_cast<int64_t>(sp) * (kM + 1);
+    const cf* H = reinterpret_cast<const cf*>(a.spectra) + static_cast<int64_t>(sp) * kHSlots;
     // one thread per pair (k, M - k), k <= M / 2; consecutive lanes take k in
     // steps of 16 (k = c + 16 r, c = idx / 361), so their positions zaddr(k)
     // step by 45 complex instead of 720 (no 16-way bank conflicts)
+    // All of a thread's H[k], H[M - k], W_N^k (L2-resident) are loaded in one
+    // batch before the loop: one exposed latency instead of one per pair.
     constexpr int kRest = kM / 2 / 16 + 1;  // 361
-    for (int idx = tid; idx < 16 * kRest; idx += kThreads) {
+    constexpr int kSplitIt = (16 * kRest + kThreads - 1) / kThreads;
+    cf hk[kSplitIt], hc[kSplitIt], wn[kSplitIt];
+    const int ts = opaque_tid();
+    auto pair_k = [&](int it) {
+      const int idx = min(ts + it * kThreads, 16 * kRest - 1);
+      const int c = idx / kRest;
+      return min(c + 16 * (idx - c * kRest), kM / 2);
+    };
+#pragma unroll
+    for (int it = 0; it < kSplitIt; ++it) {
+      const int k = pair_k(it);
+      hk[it] = H[hslot(k)];
+      hc[it] = H[hslot(kM - k)];
+      wn[it] = twn[hslot(k)];
+    }
+#pragma unroll
+    for (int it = 0; it < kSplitIt; ++it) {
+      const int idx = ts + it * kThreads;
       const int c = idx / kRest;
       const int k = c + 16 * (idx - c * kRest);
-      if (k > kM / 2) continue;
+      if (idx >= 16 * kRest || k > kM / 2) continue;
       const int kc = (kM - k) % kM;
       const int p = zaddr(k);
       const cf zk = z[p];
       const cf zc = z[zaddr(kc)];
       const cf fe = 0.5f * cf{zk.x + zc.x, zk.y - zc.y};
       const cf fo = 0.5f * cf{zk.y + zc.y, zc.x - zk.x};
-      const cf wk = twn[k];
+      const cf wk = wn[it];
       const cf Xk = fe + cmul(wk, fo);
       // partner: Fe' = conj(fe), Fo' = conj(fo), W_N^(M-k) = -conj(W_N^k)
       const cf fe2 = cf{fe.x, -fe.y};
       const cf fo2 = cf{fo.x, -fo.y};
       const cf wk2 = cf{-wk.x, wk.y};
       const cf Xc = fe2 + cmul(wk2, fo2);  // X[M - k] (X[M] when k = 0)
-      const cf Yk = cmul(Xk, H[k]);
-      const cf Yc = cmul(Xc, H[kM - k]);
+      const cf Yk = cmul(Xk, hk[it]);
+      const cf Yc = cmul(Xc, hc[it]);
       // inverse split: Z'[k] = (Y[k] + conj Y[M-k])/2 + i W_N^-k (Y[k] - conj Y[M-k])/2
       const cf s1 = 0.5f * cf{Yk.x + Yc.x, Yk.y - Yc.y};
       const cf d1 = 0.5f * cf{Yk.x - Yc.x, Yk.y + Yc.y};
@@ -408,14 +548,18 @@ __global__ void __launch_bounds__(kThreads) augment_kernel(AugArgs a) {
       if (kc != k) z[zaddr(kc)] = zc2;
     }
     __syncthreads();
+    HBK_APH(9);
     // 5) inverse FFT (permuted -> natural), 1/M
-    transform<true>(z, thi, tlo);
+    transform<true>(z, thi, tlo, ph_t0, 10);
+    if (next) prefetch(clip + gridDim.x, noff_next);
     float ay = 0.f;
-    for (int s = tid; s < kT; s += kThreads) ay += fabsf(zf[s]);
+    for (int s = opaque_tid(); s < kT; s += kThreads) ay += fabsf(zf[s]);
     const float a_out = block_sum(ay, red) / kT / kM;
+    HBK_APH(14);
     const float g = a_in / (a_out + 1e-14f) / kM;
-    for (int s = tid; s < kT; s += kThreads) out[s] = zf[s] * g;
+    for (int s = opaque_tid(); s < kT; s += kThreads) out[s] = zf[s] * g;
     __syncthreads();
+    HBK_APH(15);
   }
 }
 
@@ -432,16 +576,17 @@ __global__ void __launch_bounds__(kThreads) spectrum_kernel(const float* kern, i
   const float* k = kern + blockIdx.x * kern_stride;
   for (int s = threadIdx.x; s < kT; s += kThreads) smem[s] = k[s];
   __syncthreads();
-  transform<false>(z, thi, tlo);
-  float2* H = spectra + static_cast<int64_t>(blockIdx.x) * (kM + 1);
+  unsigned long long ph_t0 = 0;
+  transform<false>(z, thi, tlo, ph_t0, 16);
+  float2* H = spectra + static_cast<int64_t>(blockIdx.x) * kHSlots;
   for (int q = threadIdx.x; q <= kM; q += kThreads) {
     const int qq = q % kM, qc = (kM - q) % kM;
     const cf zk = z[zaddr(qq)];
     const cf zc = z[zaddr(qc)];
     const cf fe = 0.5f * cf{zk.x + zc.x, zk.y - zc.y};
     const cf fo = 0.5f * cf{zk.y + zc.y, zc.x - zk.x};
-    const cf X = fe + cmul(twn[q], fo);
-    H[q] = make_float2(X.x, X.y);
+    const cf X = fe + cmul(twn[hslot(q)], fo);
+    H[hslot(q)] = make_float2(X.x, X.y);
   }
 }
 
@@ -468,7 +613,7 @@ int hbk_reverb_plan_create(int64_t T, hbk_reverb_plan** plan) {
     set_error("hbk: reverb supports clips of %d samples (1.44 s @ 16 kHz), got %lld", kT, (long long)T);
     return HBK_ERR_UNSUPPORTED;
   }
-  std::vector<float2> th(kTwHi), tl(kTwLo), tn(kM + 1);
+  std::vector<float2> th(kTwHi), tl(kTwLo), tn(kHSlots, make_float2(0.f, 0.f));
   for (int i = 0; i < kTwHi; ++i) {
     const double a = -2.0 * M_PI * (double(i) * kTwLo) / double(kM);
     th[i] = make_float2(float(cos(a)), float(sin(a)));
@@ -477,18 +622,18 @@ int hbk_reverb_plan_create(int64_t T, hbk_reverb_plan** plan) {
     const double a = -2.0 * M_PI * i / double(kM);
     tl[i] = make_float2(float(cos(a)), float(sin(a)));
   }
-  for (int i = 0; i <= kM; ++i) {
+  for (int i = 0; i <= kM; ++i) {  // W_N^k at the spectrum slot of bin k
     const double a = -2.0 * M_PI * i / double(kT);
-    tn[i] = make_float2(float(cos(a)), float(sin(a)));
+    tn[(i % 16) * kHRow + i / 16] = make_float2(float(cos(a)), float(sin(a)));
   }
   auto* p = new hbk_reverb_plan();
   hipError_t e;
   if ((e = hipMalloc(&p->thi, kTwHi * sizeof(float2))) != hipSuccess ||
       (e = hipMalloc(&p->tlo, kTwLo * sizeof(float2))) != hipSuccess ||
-      (e = hipMalloc(&p->twn, (kM + 1) * sizeof(float2))) != hipSuccess ||
+      (e = hipMalloc(&p->twn, kHSlots * sizeof(float2))) != hipSuccess ||
       (e = hipMemcpy(p->thi, th.data(), kTwHi * sizeof(float2), hipMemcpyHostToDevice)) != hipSuccess ||
       (e = hipMemcpy(p->tlo, tl.data(), kTwLo * sizeof(float2), hipMemcpyHostToDevice)) != hipSuccess ||
-      (e = hipMemcpy(p->twn, tn.data(), (kM + 1) * sizeof(float2), hipMemcpyHostToDevice)) != hipSuccess) {
+      (e = hipMemcpy(p->twn, tn.data(), kHSlots * sizeof(float2), hipMemcpyHostToDevice)) != hipSuccess) {
     hbk_reverb_plan_destroy(p);
     return hip_error(e, "reverb plan tables");
   }
@@ -538,6 +683,7 @@ int hbk_augment(const hbk_reverb_plan* p, const float* x, int64_t n_clips, int64
   if (!x || !out || !noise_off || !snr_db || !spec_idx) return arg_error("NULL pointer");
   if (x_stride < kT || out_stride < kT) return arg_error("stride < 23040");
   if (!noise_ring && ring_len > 0) return arg_error("noise ring is NULL");
+  if (ring_len >= (int64_t(1) << 30)) return arg_error("noise ring longer than 2^30 samples");
   AugArgs a;
   a.x = x;
   a.x_stride = x_stride;
@@ -561,3 +707,13 @@ int hbk_augment(const hbk_reverb_plan* p, const float* x, int64_t n_clips, int64
 }
 
 }  // extern "C"
+
+#ifdef HBK_PHASE_TIMING
+extern "C" int hbk_debug_aug_phase(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hbk::g_aug_phase), sizeof(unsigned long long) * 32) != hipSuccess)
+    return -2;
+  unsigned long long z[32] = {};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(hbk::g_aug_phase), z, sizeof(z));
+  return 0;
+}
+#endif

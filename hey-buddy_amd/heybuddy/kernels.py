@@ -397,14 +397,24 @@ class ReverbPlan:
         z = torch.zeros(T - ir.shape[0], dtype=ir.dtype, device=ir.device)
         return torch.cat([ir[d:], z, ir[:d]])
 
+    SLOTS = 11536  # HBK_REVERB_SPECTRUM_SLOTS: bin k at slot (k % 16) * 721 + k // 16
+
     def spectra(self, kernels: torch.Tensor) -> torch.Tensor:
-        """[n, T] rotated kernels -> [n, T/2 + 1, 2] f32 (complex interleaved)."""
+        """[n, T] rotated kernels -> [n, SLOTS, 2] f32 (complex interleaved), rfft
+        bin k at slot (k % 16) * 721 + k // 16 (natural_spectrum() undoes it)."""
         kernels = kernels.to(self.device, torch.float32).contiguous()
         n = kernels.shape[0]
-        out = torch.empty((n, self.T // 2 + 1, 2), dtype=torch.float32, device=self.device)
+        out = torch.zeros((n, self.SLOTS, 2), dtype=torch.float32, device=self.device)
         check(lib().hbk_reverb_spectrum(self._handle, ptr(kernels), n, kernels.stride(0), ptr(out),
                                         stream_ptr(self.device)), "hbk_reverb_spectrum")
         return out
+
+    @classmethod
+    def natural_spectrum(cls, spectra: torch.Tensor) -> torch.Tensor:
+        """[n, SLOTS, 2] slot layout -> [n, T/2 + 1, 2] in bin order."""
+        n = spectra.shape[0]
+        rows = spectra.reshape(n, 16, cls.SLOTS // 16, 2)
+        return rows.transpose(1, 2).reshape(n, cls.SLOTS, 2)[:, :cls.T // 2 + 1]
 
     def augment(self, x: torch.Tensor, ring: torch.Tensor | None, noise_off: torch.Tensor,
                 snr_db: torch.Tensor, spectra: torch.Tensor | None, spec_idx: torch.Tensor,
@@ -427,6 +437,10 @@ class ReverbPlan:
                 raise ValueError("gain must have n entries")
         if bool((noise_off >= 0).any()) and (ring is None or ring.numel() == 0):
             raise ValueError("noise requested without a noise ring")
+        if ring is not None and bool((noise_off >= ring.numel()).any()):
+            raise ValueError("noise_off must be < the ring length")
+        if spectra is not None and (spectra.dim() != 3 or spectra.shape[1:] != (self.SLOTS, 2)):
+            raise ValueError(f"spectra must be [n, {self.SLOTS}, 2] (ReverbPlan.spectra's slot layout)")
         if spectra is not None and bool((spec_idx >= spectra.shape[0]).any()):
             raise ValueError("spec_idx out of range")
         ring_len = 0 if ring is None else ring.numel()

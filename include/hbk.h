@@ -204,9 +204,15 @@ typedef struct hbk_reverb_plan hbk_reverb_plan;
 int hbk_reverb_plan_create(int64_t T, hbk_reverb_plan** plan);
 int hbk_reverb_plan_destroy(hbk_reverb_plan* plan);
 
+/* Spectrum slots per IR: bin k (0 <= k <= T/2 = 11520) of rfft(kernel) is
+ * stored at slot (k % 16) * 721 + k / 16 (16 rows of 721; 15 slots unused), so
+ * that hbk_augment's pair loop reads it with coalesced loads. */
+#define HBK_REVERB_SPECTRUM_SLOTS 11536
+
 /* kernels [n_kernels, stride] f32: the ROTATED length-T kernels
  * [ir[d:], zeros(T - L), ir[:d]] (d = argmax |ir|, ir truncated to T first),
- * spectra [n_kernels, T/2 + 1] complex64 (interleaved f32) = rfft(kernel). */
+ * spectra [n_kernels, HBK_REVERB_SPECTRUM_SLOTS] complex64 (interleaved f32):
+ * rfft(kernel) in the slot order above. */
 int hbk_reverb_spectrum(const hbk_reverb_plan* plan, const float* kernels, int64_t n_kernels,
                         int64_t stride, float* spectra, void* stream);
 
@@ -214,7 +220,7 @@ int hbk_reverb_spectrum(const hbk_reverb_plan* plan, const float* kernels, int64
  *   if gain != NULL: x = gain[i] x (torch_audiomentations Gain, applied before the
  *      noise mix as in the reference's batch chain, augmented.py:114-118, :383-392);
  *   if noise_off[i] >= 0: y = x + 10^((10 log10(|x|^2/|n|^2) - snr_db[i]) / 20) n,
- *      n = noise_ring[(noise_off[i] + t) mod ring_len], t < T;
+ *      n = noise_ring[(noise_off[i] + t) mod ring_len], t < T (noise_off[i] < ring_len < 2^30);
  *   if spec_idx[i] >= 0: y = mean|y| * c / (mean|c| + 1e-14), c = irfft(rfft(y) * spectra[spec_idx[i]]).
  * out [n_clips, out_stride] (may equal x). All pointers are device pointers. */
 int hbk_augment(const hbk_reverb_plan* plan, const float* x, int64_t n_clips, int64_t x_stride,

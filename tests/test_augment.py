@@ -69,6 +69,18 @@ def test_reverb_kernel_rotation_and_circularity():
     np.testing.assert_allclose(y, ref, atol=1e-9)
 
 
+def test_spectrum_slot_layout_round_trip():
+    """hbk_reverb_spectrum stores bin k at slot (k % 16) * 721 + k // 16
+    (include/hbk.h); natural_spectrum() restores bin order."""
+    from heybuddy.kernels import ReverbPlan
+    k = np.arange(T // 2 + 1)
+    slots = torch.zeros((1, ReverbPlan.SLOTS, 2))
+    slots[0, (k % 16) * 721 + k // 16, 0] = torch.from_numpy(k).float()
+    nat = ReverbPlan.natural_spectrum(slots)
+    assert nat.shape == (1, T // 2 + 1, 2)
+    np.testing.assert_array_equal(nat[0, :, 0].numpy(), k)
+
+
 def _close(out, ref):
     err = np.abs(out - ref)
     return (err.max() <= 2e-5 * np.abs(ref).max()
@@ -81,7 +93,7 @@ def test_reverb_spectrum_matches_rfft():
     plan = ReverbPlan()
     _, irs = _bank()
     ks = torch.stack([ReverbPlan.rotated_kernel(torch.from_numpy(ir), T) for ir in irs])
-    H = plan.spectra(ks.cuda()).cpu().numpy()
+    H = ReverbPlan.natural_spectrum(plan.spectra(ks.cuda())).cpu().numpy()
     ref = np.fft.rfft(ks.numpy().astype(np.float64), axis=1)
     got = H[..., 0] + 1j * H[..., 1]
     assert np.abs(got - ref).max() <= 2e-5 * np.abs(ref).max()
