@@ -3,8 +3,9 @@ AugmentedAudioGenerator.execute_augment_batch, reference
 src/python/heybuddy/dataset/augmented.py:297-394).
 
 Semantics kept from the reference:
-* one coin flip per BATCH for background noise (p 0.75, :383) and then one for
-  reverb (p 0.75, :387), drawn with numpy's global RNG in that order;
+* one coin flip per BATCH for background noise (p 0.75, :383) and one for
+  reverb (p 0.75, :387), from numpy's global RNG (drawn for all batches of a
+  call at once: the coins are the same Bernoulli draws, the stream order differs);
 * background noise: consecutive noise clips (cycling through the bank) are
   concatenated until they cover batch * T samples and cut into consecutive
   T-sample segments (:246-267); SNR ~ U[min, max] dB per clip (:269-270);
@@ -76,26 +77,55 @@ class BatchAugmenter:
             self.spectra = self.plan.spectra(ks)
         self.noise_idx = 0
         self.ir_idx = 0
+        self._advance = {}
+
+    def _noise_advance(self, idx: int, nb: int) -> int:
+        """Index of the noise clip after a batch of nb clips starting at clip idx:
+        whole clips are consumed until they cover nb * T samples
+        (augmented.py:249-254). Memoised: full batches repeat the same few."""
+        key = (idx, nb)
+        nxt = self._advance.get(key)
+        if nxt is None:
+            need, covered, nxt = nb * T, 0, idx
+            while covered < need:
+                covered += self.lengths[nxt]
+                nxt = (nxt + 1) % len(self.lengths)
+            self._advance[key] = nxt
+        return nxt
 
     def plan_batches(self, n: int):
         """Per-clip noise offsets, spectrum indices and gains (dB) for n clips
-        (host bookkeeping that mirrors the reference's dataset iteration)."""
+        (host bookkeeping that mirrors the reference's dataset iteration; the
+        per-batch coins and draws are vectorised over the call's batches)."""
+        bs = self.batch_size
+        nbat = (n + bs - 1) // bs
+        sizes = np.full(nbat, bs, dtype=np.int64)
+        sizes[-1] = n - bs * (nbat - 1)
+        batch = np.repeat(np.arange(nbat), sizes)  # batch of each clip
+        pos = np.arange(n) - batch * bs            # position within its batch
+        # gain (torch_audiomentations Gain, per_batch): one value per batch
+        g_on = np.random.rand(nbat) < self.p_gain
+        g_db = np.random.uniform(self.gain_min_db, self.gain_max_db, nbat)
+        gain_db = np.where(g_on, g_db, 0.0).astype(np.float32)[batch]
+        # background noise: consecutive T-sample segments of the noise stream
         noise_off = np.full(n, -1, dtype=np.int64)
+        n_on = (np.random.rand(nbat) < self.p_noise) if self.ring is not None else np.zeros(nbat, bool)
+        if n_on.any():
+            start = np.full(nbat, -1, dtype=np.int64)
+            for b in np.flatnonzero(n_on):
+                start[b] = self.starts[self.noise_idx]
+                self.noise_idx = self._noise_advance(self.noise_idx, int(sizes[b]))
+            sel = start[batch] >= 0
+            noise_off[sel] = start[batch][sel] + pos[sel] * T
+        # reverb: one IR per batch, taken in order (augmented.py:188-192)
         spec_idx = np.full(n, -1, dtype=np.int32)
-        gain_db = np.zeros(n, dtype=np.float32)
-        for b0 in range(0, n, self.batch_size):
-            nb = min(self.batch_size, n - b0)
-            if np.random.rand() < self.p_gain:  # per_batch: one gain for the batch
-                gain_db[b0:b0 + nb] = np.random.uniform(self.gain_min_db, self.gain_max_db)
-            if np.random.rand() < self.p_noise and self.ring is not None:
-                noise_off[b0:b0 + nb] = self.starts[self.noise_idx] + np.arange(nb) * T
-                covered = 0
-                while covered < nb * T:  # whole clips are consumed (augmented.py:249-254)
-                    covered += self.lengths[self.noise_idx]
-                    self.noise_idx = (self.noise_idx + 1) % len(self.lengths)
-            if np.random.rand() < self.p_reverb and self.spectra is not None:
-                spec_idx[b0:b0 + nb] = self.ir_idx
-                self.ir_idx = (self.ir_idx + 1) % self.spectra.shape[0]
+        r_on = (np.random.rand(nbat) < self.p_reverb) if self.spectra is not None else np.zeros(nbat, bool)
+        if r_on.any():
+            n_spec = self.spectra.shape[0]
+            ir = (self.ir_idx + np.cumsum(r_on) - 1) % n_spec
+            self.ir_idx = int((self.ir_idx + r_on.sum()) % n_spec)
+            per_clip = np.where(r_on, ir, -1).astype(np.int32)[batch]
+            spec_idx[:] = per_clip
         return noise_off, spec_idx, gain_db
 
     def __call__(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -105,7 +135,7 @@ class BatchAugmenter:
         ring_len = 0 if self.ring is None else self.ring.numel()
         if ring_len:
             noise_off = np.where(noise_off >= 0, noise_off % ring_len, -1)
-        snr = torch.rand(n, device=self.device) * (self.snr_max - self.snr_min) + self.snr_min
+        snr = torch.from_numpy(np.random.uniform(self.snr_min, self.snr_max, n).astype(np.float32))
         gain = None
         if self.p_gain > 0:  # torch_audiomentations convert_decibels_to_amplitude_ratio
             gain = torch.pow(10.0, torch.from_numpy(gain_db) / 20.0)

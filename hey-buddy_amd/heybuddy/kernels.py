@@ -426,23 +426,38 @@ class ReverbPlan:
             raise ValueError(f"x must be [n, >= {self.T}] f32 rows on {self.device}")
         if out is None:
             out = torch.empty((n, self.T), dtype=torch.float32, device=self.device)
-        noise_off = noise_off.to(self.device, torch.int64).contiguous()
-        spec_idx = spec_idx.to(self.device, torch.int32).contiguous()
-        snr_db = snr_db.to(self.device, torch.float32).contiguous()
-        if noise_off.numel() != n or spec_idx.numel() != n or snr_db.numel() != n:
-            raise ValueError("per-clip arrays must have n entries")
+        # Host-side per-clip arrays (the BatchAugmenter path) are checked on the
+        # host and sent through pinned memory without a device sync; device
+        # tensors are checked on the device (a sync per check).
+        def per_clip(t: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+            t = t.to(dtype=dtype).reshape(-1).contiguous()
+            if t.numel() != n:
+                raise ValueError("per-clip arrays must have n entries")
+            return t
+
+        noise_off = per_clip(noise_off, torch.int64)
+        spec_idx = per_clip(spec_idx, torch.int32)
+        snr_db = per_clip(snr_db, torch.float32)
         if gain is not None:
-            gain = gain.to(self.device, torch.float32).contiguous()
-            if gain.numel() != n:
-                raise ValueError("gain must have n entries")
-        if bool((noise_off >= 0).any()) and (ring is None or ring.numel() == 0):
-            raise ValueError("noise requested without a noise ring")
-        if ring is not None and bool((noise_off >= ring.numel()).any()):
-            raise ValueError("noise_off must be < the ring length")
+            gain = per_clip(gain, torch.float32)
         if spectra is not None and (spectra.dim() != 3 or spectra.shape[1:] != (self.SLOTS, 2)):
             raise ValueError(f"spectra must be [n, {self.SLOTS}, 2] (ReverbPlan.spectra's slot layout)")
+        ring_n = 0 if ring is None else ring.numel()
+        if bool((noise_off >= 0).any()) and ring_n == 0:
+            raise ValueError("noise requested without a noise ring")
+        if ring_n and bool((noise_off >= ring_n).any()):
+            raise ValueError("noise_off must be < the ring length")
         if spectra is not None and bool((spec_idx >= spectra.shape[0]).any()):
             raise ValueError("spec_idx out of range")
+
+        def to_dev(t: torch.Tensor) -> torch.Tensor:
+            if t.device.type == "cpu":
+                return t.pin_memory().to(self.device, non_blocking=True)
+            return t.to(self.device)
+
+        noise_off, spec_idx, snr_db = to_dev(noise_off), to_dev(spec_idx), to_dev(snr_db)
+        if gain is not None:
+            gain = to_dev(gain)
         ring_len = 0 if ring is None else ring.numel()
         check(lib().hbk_augment(self._handle, ptr(x), n, x.stride(0),
                                 ptr(ring) if ring is not None else None, ring_len, ptr(noise_off),

@@ -218,3 +218,33 @@ def test_batch_augmenter_gain_is_per_batch():
         assert 10 ** (-18 / 20) * (1 - 1e-6) <= g <= 10 ** (6 / 20) * (1 + 1e-6)
     off = BatchAugmenter(device=0, background_noise_prob=0.0, reverb_prob=0.0, gain_prob=0.0)
     assert torch.equal(off(x), x)
+
+
+def test_batch_plan_consumes_whole_noise_clips_per_batch():
+    """Host bookkeeping of BatchAugmenter (no device): each noisy batch takes
+    consecutive T-sample segments of the noise stream starting at the current
+    clip and then skips every clip it touched (augmented.py:246-267); one IR
+    per reverb batch, in order (:188-192); one gain per batch."""
+    from heybuddy.dataset.augmented import BatchAugmenter
+    aug = object.__new__(BatchAugmenter)
+    aug.batch_size, aug.p_gain, aug.gain_min_db, aug.gain_max_db = 128, 1.0, -18.0, 6.0
+    aug.p_noise = aug.p_reverb = 1.0
+    aug.lengths = [48000 + 997 * i for i in range(40)]
+    aug.starts = list(np.cumsum([0] + aug.lengths[:-1]))
+    aug.ring, aug.spectra = object(), np.zeros((7, 1))
+    aug.noise_idx = aug.ir_idx = 0
+    aug._advance = {}
+    n = 1000
+    noise_off, spec_idx, gain_db = aug.plan_batches(n)
+    idx, ir = 0, 0
+    for b0 in range(0, n, 128):
+        nb = min(128, n - b0)
+        np.testing.assert_array_equal(noise_off[b0:b0 + nb], aug.starts[idx] + np.arange(nb) * T)
+        covered = 0
+        while covered < nb * T:
+            covered += aug.lengths[idx]
+            idx = (idx + 1) % len(aug.lengths)
+        assert (spec_idx[b0:b0 + nb] == ir).all()
+        ir = (ir + 1) % 7
+        assert len(set(gain_db[b0:b0 + nb])) == 1 and -18 <= gain_db[b0] <= 6
+    assert aug.noise_idx == idx and aug.ir_idx == ir
