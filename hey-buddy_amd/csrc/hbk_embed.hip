@@ -33,7 +33,8 @@ constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 constexpr int kMaxStages = 10;
 constexpr int kMaxWin = 32;
-constexpr int kLdsBudget = 78 * 1024;  // bytes per block: 2 blocks per CU
+constexpr int kLdsBudget = 78 * 1024;     // bytes per block: 2 blocks per CU
+constexpr int kLdsBudgetCU = 156 * 1024;  // one block per CU
 constexpr int kChunkClips = 16384;     // clips per workspace chunk
 
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -1440,6 +1441,16 @@ XKernelFn pick_xkernel(int nb, bool wg) {
   }
 }
 
+// Dynamic-LDS limit of a kernel raised to what the CU holds beside its static
+// LDS (set once to the maximum, so plans sharing the kernel never lower it).
+hipError_t set_max_dynamic_lds(const void* fn) {
+  hipFuncAttributes at;
+  hipError_t e = hipFuncGetAttributes(&at, fn);
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             int(160 * 1024 - static_cast<int>(at.sharedSizeBytes)));
+}
+
 // Split-f16 layout of one chain whose source / pooling fields are already in
 // `a`: packs the fp16 weight planes, biases and group-offset tables, and picks
 // images-per-task and band for the LDS budget.
@@ -1447,8 +1458,13 @@ int layout_split(const std::vector<OpInfo>& ops, const std::vector<int>& stage_o
                  const ChainArgs& a, ChainPlan& cp, Dims& od_out) {
   XArgs& x = cp.x;
   // LDS per block (default 78 KB: two blocks per CU); HBK_EMBED_LDS_KB for tuning
+  // (a chain that fits fewer than kMinG whole images per task at that budget
+  // takes a whole CU instead: measured on SE20's chain 2, 2 -> 6 images,
+  // 0.96 -> 0.81 ms per 16384 clips; the tail chain, 30 images, keeps 2 / CU)
+  constexpr int kMinG = 8;
+  const char* lds_env = getenv("HBK_EMBED_LDS_KB");
   int64_t lds_budget = kLdsBudget;
-  if (const char* e = getenv("HBK_EMBED_LDS_KB")) lds_budget = std::min<int64_t>(160, std::max(16, atoi(e))) * 1024;
+  if (lds_env) lds_budget = std::min<int64_t>(160, std::max(16, atoi(lds_env))) * 1024;
   x.ipc = a.ipc;
   for (int k = 0; k < kMaxWin; ++k) x.row_off[k] = a.row_off[k];
   x.src_clip_stride = a.src_clip_stride;
@@ -1619,22 +1635,32 @@ int layout_split(const std::vector<OpInfo>& ops, const std::vector<int>& stage_o
       if (lds_total(1, b, res) <= lds_budget) return b;
     return 0;
   };
-  // resident weights unless they cost more than 5 % of the work in halo rows
-  // (HBK_EMBED_WEIGHTS=lds|global overrides, for tuning)
-  const int band_r = lds_total(1, 1, true) <= lds_budget ? best_band(true) : 0;
-  const int band_g = best_band(false);
-  bool resident = band_r > 0 && (band_g == 0 || efficiency(band_r) >= 0.95 * efficiency(band_g));
-  if (const char* wp = getenv("HBK_EMBED_WEIGHTS")) {
-    if (!strcmp(wp, "global") && band_g > 0) resident = false;
-    if (!strcmp(wp, "lds") && band_r > 0) resident = true;
+  bool resident = false;
+  int band = 0, G = 1;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    // resident weights unless they cost more than 5 % of the work in halo rows
+    // (HBK_EMBED_WEIGHTS=lds|global overrides, for tuning)
+    const int band_r = lds_total(1, 1, true) <= lds_budget ? best_band(true) : 0;
+    const int band_g = best_band(false);
+    resident = band_r > 0 && (band_g == 0 || efficiency(band_r) >= 0.95 * efficiency(band_g));
+    if (const char* wp = getenv("HBK_EMBED_WEIGHTS")) {
+      if (!strcmp(wp, "global") && band_g > 0) resident = false;
+      if (!strcmp(wp, "lds") && band_r > 0) resident = true;
+    }
+    band = resident ? band_r : band_g;
+    G = 1;
+    if (band == 0) {
+      set_error("hbk: one output row of a chain does not fit in LDS");
+      return HBK_ERR_UNSUPPORTED;
+    }
+    if (band == od.h)
+      while (G < 64 && lds_total(G + 1, band, resident) <= lds_budget) ++G;  // any G: fill the LDS budget
+    if (attempt == 0 && !lds_env && band == od.h && G < kMinG) {
+      lds_budget = kLdsBudgetCU;
+      continue;
+    }
+    break;
   }
-  int band = resident ? band_r : band_g, G = 1;
-  if (band == 0) {
-    set_error("hbk: one output row of a chain does not fit in LDS");
-    return HBK_ERR_UNSUPPORTED;
-  }
-  if (band == od.h)
-    while (G < 64 && lds_total(G + 1, band, resident) <= lds_budget) ++G;  // any G: fill the LDS budget
   x.G = G;
   x.band = band;
   x.n_bands = (od.h + band - 1) / band;
@@ -1673,9 +1699,8 @@ int layout_split(const std::vector<OpInfo>& ops, const std::vector<int>& stage_o
   x.ktab = reinterpret_cast<const int*>(base + wsz + bsz);
   x.i2c_off = reinterpret_cast<const int*>(base + wsz + bsz + ksz);
   x.i2c_n = static_cast<int>(i2c.size());
-  if (cp.lds_bytes > 64 * 1024) {
-    e = hipFuncSetAttribute(reinterpret_cast<const void*>(cp.xfn),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, int(cp.lds_bytes));
+  if (cp.lds_bytes > 64 * 1024) {  // the CU maximum: chains sharing a kernel never lower it
+    e = set_max_dynamic_lds(reinterpret_cast<const void*>(cp.xfn));
     if (e != hipSuccess) return hip_error(e, "hipFuncSetAttribute(max dynamic LDS)");
   }
   cp.macs_per_img = macs;
@@ -2038,8 +2063,7 @@ int build_segment(const std::vector<OpInfo>& ops, int o0, int o1, Dims in, int i
     if (e != hipSuccess) return hip_error(e, "copy chain weights");
     a.wblob = cp.d_blob;
     if (cp.lds_bytes > 64 * 1024) {
-      e = hipFuncSetAttribute(reinterpret_cast<const void*>(cp.fn),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, int(cp.lds_bytes));
+      e = set_max_dynamic_lds(reinterpret_cast<const void*>(cp.fn));  // see layout_split
       if (e != hipSuccess) return hip_error(e, "hipFuncSetAttribute(max dynamic LDS)");
     }
     cp.macs_per_img = macs;
