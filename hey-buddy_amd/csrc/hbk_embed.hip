@@ -1074,6 +1074,7 @@ p0_chain_kernel(P0Args a) {
 
   for (int task = blockIdx.x; task < n_tasks; task += gridDim.x) {
     const int img = task / a.n_bands, band = task - img * a.n_bands;
+    HBK_MARK(1);
     __syncthreads();  // the previous task's readers are done
     // 1) input rows [row0, row0 + RI) (clamped to the image) -> raw; prefetch the next task's
 #pragma unroll
@@ -1083,6 +1084,7 @@ p0_chain_kernel(P0Args a) {
     }
     if (task + static_cast<int>(gridDim.x) < n_tasks) load_raw(task + gridDim.x);
     __syncthreads();
+    HBK_MARK(40);
     // 2) stage 0: 3x3, 1 -> C; B fragments straight from the f32 rows
     //    (taps 0-4 in the first K half, 5-8 and a zero in the second)
     {
@@ -1109,11 +1111,17 @@ p0_chain_kernel(P0Args a) {
         if (pp < G::M0) p0_store_planes<C, G::CS, LEAKY>(acc, p, khalf, s0h, s0l, a.alpha);
       }
     }
+    HBK_MARK(50);
     __syncthreads();
+    HBK_MARK(41);
     p0_stage12<WI, C, BAND, 1, LEAKY>(a, W1, s0h, s0l, s1h, s1l, nullptr, wave, r32, khalf);
+    HBK_MARK(51);
     __syncthreads();
+    HBK_MARK(42);
     p0_stage12<WI, C, BAND, 2, LEAKY>(a, W2, s1h, s1l, nullptr, nullptr, s2, wave, r32, khalf);
+    HBK_MARK(52);
     __syncthreads();
+    HBK_MARK(43);
     // 3) 2x2 max-pool of the stage-2 rows -> the band's BAND output rows
     {
       constexpr int PW = G::W2 / 2, C4 = C / 4;
@@ -1135,6 +1143,7 @@ p0_chain_kernel(P0Args a) {
         *reinterpret_cast<float4*>(dst + (static_cast<int64_t>(orow) * PW + px) * C + 4 * c4) = m;
       }
     }
+    HBK_MARK(6);
   }
 }
 

@@ -16,7 +16,8 @@ from heybuddy._native import lib  # noqa: E402
 from heybuddy.embedding_graph import WINDOW_STARTS, se20_graph  # noqa: E402
 from heybuddy.kernels import EmbedPlan  # noqa: E402
 
-NAMES = {1: "task", 19: "bar>", 5: "store", 6: "end", 10: "unit", 11: "pro", 12: "mma", 13: "epi"}
+NAMES = {1: "task", 19: "bar>", 5: "store", 6: "end", 10: "unit", 11: "pro", 12: "mma", 13: "epi",
+         40: "raw|", 50: "s0>", 41: "s0|", 51: "s1>", 42: "s1|", 52: "s2>", 43: "s2|"}  # p0: > done, | after barrier
 
 
 def main():
@@ -40,7 +41,7 @@ def main():
             ev = [(buf[(b * 4 + w) * 256 + i] >> 8, buf[(b * 4 + w) * 256 + i] & 255) for i in range(n)]
             line = []
             prev = t0
-            for t, i in ev[:90]:
+            for t, i in ev[:60]:
                 nm = NAMES.get(i, f"s{i - 20}" if 20 <= i < 40 else str(i))
                 line.append(f"{nm}+{(t - prev)}")
                 prev = t
