@@ -590,6 +590,135 @@ __global__ void __launch_bounds__(kThreads) spectrum_kernel(const float* kern, i
   }
 }
 
+// ---- colored noise --------------------------------------------------------
+// torch_audiomentations AddColoredNoise (the reference's batch chain,
+// augmented.py:107-113; p 0.25 per batch, snr ~ U[10, 30] dB and f_decay ~
+// U[-1, 2] per clip, constants.py:128-132). Per clip:
+//   w ~ N(0, 1) [T]; S = rfft(w) / linspace(1, sqrt(sr / 2), T/2 + 1)^f_decay;
+//   n = irfft(S); n /= rms(n) + 1e-8; y = x + rms(x) / 10^(snr / 20) n.
+// One workgroup per clip on the augment kernel's LDS transform: white noise
+// into LDS, forward FFT, the real-FFT split x mask x inverse split on (k, M-k)
+// pairs, inverse FFT, then rms(n) and rms(x) in one block sum and the mix.
+// White noise comes from the caller (parity tests) or from a counter-based
+// Box-Muller stream (seed, clip, sample): no RNG state, any grid.
+struct ColoredArgs {
+  const float* x;
+  int64_t x_stride;
+  float* out;
+  int64_t out_stride;
+  int64_t n_clips;
+  const float* white;     // [n_clips, white_stride] N(0,1) or NULL (generated from seed)
+  int64_t white_stride;
+  uint64_t seed;
+  const float* f_decay;   // per clip
+  const float* snr_db;    // per clip
+  float lin_step;         // (sqrt(sr / 2) - 1) / (T / 2): linspace step over the T/2 + 1 bins
+  const float2* thi;
+  const float2* tlo;
+  const float2* twn;
+};
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+// standard normal of stream element i (Box-Muller on two 24-bit uniforms)
+__device__ __forceinline__ float gauss(uint64_t seed, uint64_t i) {
+  const uint64_t h = mix64(seed + 0x9E3779B97F4A7C15ull * (i + 1));
+  const float u1 = (static_cast<float>(h >> 40) + 0.5f) * (1.f / 16777216.f);
+  const float u2 = static_cast<float>((h >> 16) & 0xFFFFFF) * (1.f / 16777216.f);
+  return sqrtf(-2.f * __logf(u1)) * __cosf(6.283185307179586f * u2);
+}
+
+__global__ void __launch_bounds__(kThreads) colored_noise_kernel(ColoredArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  cf* z = reinterpret_cast<cf*>(smem);
+  float* red = smem + 2 * kM;
+  cf* thi = reinterpret_cast<cf*>(smem + 2 * kM + 32);
+  cf* tlo = thi + kTwHi;
+  load_tw(thi, tlo, a.thi, a.tlo);
+  const cf* twn = reinterpret_cast<const cf*>(a.twn);
+  float* zf = smem;
+  constexpr int kPer = (kT + kThreads - 1) / kThreads;
+  constexpr int kRest = kM / 2 / 16 + 1;  // 361 pairs per k % 16 class
+  unsigned long long ph_t0 = 0;
+  for (int64_t clip = blockIdx.x; clip < a.n_clips; clip += gridDim.x) {
+    const int tid = opaque_tid();
+    const float snr = a.snr_db[clip];
+    if (snr != snr) {  // NaN: this clip's batch drew no colored noise (uniform per block)
+      if (a.out != a.x || a.out_stride != a.x_stride) {
+        const float* x = a.x + clip * a.x_stride;
+        float* out = a.out + clip * a.out_stride;
+        for (int s = tid; s < kT; s += kThreads) out[s] = x[s];
+      }
+      continue;
+    }
+    // 1) white noise -> LDS (the previous clip's readers finished at its last barrier)
+    if (a.white) {
+      const float* w = a.white + clip * a.white_stride;
+      for (int s = tid; s < kT; s += kThreads) zf[s] = w[s];
+    } else {
+      for (int s = tid; s < kT; s += kThreads) zf[s] = gauss(a.seed, static_cast<uint64_t>(clip) * kT + s);
+    }
+    __syncthreads();
+    transform<false>(z, thi, tlo, ph_t0, 0);
+    // 2) X = split(Z); Y = X / lin^f_decay (a real mask); Z' = inverse split(Y)
+    const float fd = a.f_decay[clip];
+    for (int idx = tid; idx < 16 * kRest; idx += kThreads) {
+      const int c = idx / kRest;
+      const int k = c + 16 * (idx - c * kRest);
+      if (k > kM / 2) continue;
+      const int kc = (kM - k) % kM;
+      const int p = zaddr(k);
+      const cf zk = z[p];
+      const cf zc = z[zaddr(kc)];
+      const cf fe = 0.5f * cf{zk.x + zc.x, zk.y - zc.y};
+      const cf fo = 0.5f * cf{zk.y + zc.y, zc.x - zk.x};
+      const cf wk = twn[hslot(k)];
+      const float mk = powf(fmaf(a.lin_step, static_cast<float>(k), 1.f), -fd);
+      const float mc = powf(fmaf(a.lin_step, static_cast<float>(kM - k), 1.f), -fd);  // bin M - k (M for k = 0)
+      const cf Yk = mk * (fe + cmul(wk, fo));
+      const cf Yc = mc * (cf{fe.x, -fe.y} + cmul(cf{-wk.x, wk.y}, cf{fo.x, -fo.y}));
+      const cf s1 = 0.5f * cf{Yk.x + Yc.x, Yk.y - Yc.y};
+      const cf d1 = 0.5f * cf{Yk.x - Yc.x, Yk.y + Yc.y};
+      const cf wd = cmul(cf{wk.x, -wk.y}, d1);
+      const cf s2 = 0.5f * cf{Yc.x + Yk.x, Yc.y - Yk.y};
+      const cf d2 = 0.5f * cf{Yc.x - Yk.x, Yc.y + Yk.y};
+      const cf wd2 = cmul(cf{-wk.x, -wk.y}, d2);
+      z[p] = s1 + cf{-wd.y, wd.x};
+      if (kc != k) z[zaddr(kc)] = s2 + cf{-wd2.y, wd2.x};
+    }
+    __syncthreads();
+    transform<true>(z, thi, tlo, ph_t0, 0);  // natural order, x kM
+    // 3) rms(n), rms(x) in one block sum, then y = x + rms(x) 10^(-snr/20) n / (rms(n) + 1e-8)
+    const float* x = a.x + clip * a.x_stride;
+    float xr[kPer];
+    float ex = 0.f, en = 0.f;
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int s = tid + u * kThreads;
+      xr[u] = 0.f;
+      if (s < kT) {
+        xr[u] = x[s];
+        const float nv = zf[s] * (1.f / kM);
+        ex += xr[u] * xr[u];
+        en += nv * nv;
+      }
+    }
+    block_sum2(ex, en, red);
+    const float rms_x = sqrtf(ex / kT), rms_n = sqrtf(en / kT);
+    const float scale = rms_x / powf(10.f, snr / 20.f) / (rms_n + 1e-8f) * (1.f / kM);
+    float* out = a.out + clip * a.out_stride;
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int s = tid + u * kThreads;
+      if (s < kT) out[s] = fmaf(scale, zf[s], xr[u]);
+    }
+    __syncthreads();  // zf is rewritten by the next clip
+  }
+}
+
 }  // namespace
 }  // namespace hbk
 
@@ -641,6 +770,8 @@ int hbk_reverb_plan_create(int64_t T, hbk_reverb_plan** plan) {
   if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(augment_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, int(lds))) != hipSuccess ||
       (e = hipFuncSetAttribute(reinterpret_cast<const void*>(spectrum_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, int(lds))) != hipSuccess ||
+      (e = hipFuncSetAttribute(reinterpret_cast<const void*>(colored_noise_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, int(lds))) != hipSuccess) {
     hbk_reverb_plan_destroy(p);
     return hip_error(e, "hipFuncSetAttribute(augment LDS)");
@@ -703,6 +834,38 @@ int hbk_augment(const hbk_reverb_plan* p, const float* x, int64_t n_clips, int64
   const int64_t blocks = std::min<int64_t>(n_clips, persistent_blocks(1));
   hipLaunchKernelGGL(augment_kernel, dim3(unsigned(blocks)), dim3(kThreads), kAugLds, as_stream(stream), a);
   HBK_LAUNCH_CHECK("augment_kernel");
+  return HBK_OK;
+}
+
+int hbk_colored_noise(const hbk_reverb_plan* p, const float* x, int64_t n_clips, int64_t x_stride,
+                      const float* white, int64_t white_stride, uint64_t seed, const float* f_decay,
+                      const float* snr_db, float sample_rate, float* out, int64_t out_stride, void* stream) {
+  using namespace hbk;
+  if (!p) return arg_error("plan is NULL");
+  if (n_clips < 0) return arg_error("negative n_clips");
+  if (n_clips == 0) return HBK_OK;
+  if (!x || !out || !f_decay || !snr_db) return arg_error("NULL pointer");
+  if (x_stride < kT || out_stride < kT) return arg_error("stride < 23040");
+  if (white && white_stride < kT) return arg_error("white_stride < 23040");
+  if (!(sample_rate > 2.f)) return arg_error("sample_rate must be > 2");
+  ColoredArgs a;
+  a.x = x;
+  a.x_stride = x_stride;
+  a.out = out;
+  a.out_stride = out_stride;
+  a.n_clips = n_clips;
+  a.white = white;
+  a.white_stride = white_stride;
+  a.seed = seed;
+  a.f_decay = f_decay;
+  a.snr_db = snr_db;
+  a.lin_step = static_cast<float>((std::sqrt(double(sample_rate) / 2.0) - 1.0) / double(kM));
+  a.thi = p->thi;
+  a.tlo = p->tlo;
+  a.twn = p->twn;
+  const int64_t blocks = std::min<int64_t>(n_clips, persistent_blocks(1));
+  hipLaunchKernelGGL(colored_noise_kernel, dim3(unsigned(blocks)), dim3(kThreads), kAugLds, as_stream(stream), a);
+  HBK_LAUNCH_CHECK("colored_noise_kernel");
   return HBK_OK;
 }
 

@@ -102,6 +102,11 @@ def build_embeddings(n: int, seed: int, device: torch.device, augmenter=None, ch
 @click.option("--augmentation-background-noise-max-snr-db", type=float, default=DEFAULT_AUGMENT_BACKGROUND_NOISE_MAX_SNR_DB, show_default=True)
 @click.option("--augmentation-reverb-prob", type=float, default=DEFAULT_AUGMENT_REVERB_PROB, show_default=True)
 @click.option("--augmentation-gain-prob", type=float, default=DEFAULT_AUGMENT_GAIN_PROB, show_default=True)
+@click.option("--augmentation-colored-noise-prob", type=float, default=DEFAULT_AUGMENT_COLORED_NOISE_PROB, show_default=True)
+@click.option("--augmentation-colored-noise-min-snr-db", type=float, default=DEFAULT_AUGMENT_COLORED_NOISE_MIN_SNR_DB, show_default=True)
+@click.option("--augmentation-colored-noise-max-snr-db", type=float, default=DEFAULT_AUGMENT_COLORED_NOISE_MAX_SNR_DB, show_default=True)
+@click.option("--augmentation-colored-noise-min-f-decay", type=float, default=DEFAULT_AUGMENT_COLORED_NOISE_MIN_F_DECAY, show_default=True)
+@click.option("--augmentation-colored-noise-max-f-decay", type=float, default=DEFAULT_AUGMENT_COLORED_NOISE_MAX_F_DECAY, show_default=True)
 @click.option("--logging-steps", type=int, default=DEFAULT_LOGGING_STEPS, show_default=True)
 @click.option("--validation-steps", type=int, default=DEFAULT_VALIDATION_STEPS, show_default=True)
 @click.option("--checkpoint-steps", type=int, default=DEFAULT_CHECKPOINT_STEPS, show_default=True)
@@ -125,7 +130,9 @@ def train(phrase: str, additional_phrase: List[str], wandb_entity: Optional[str]
           target_false_positive_rate: float, dynamic_negative_weight: bool, negative_weight: float,
           augmentation_background_noise_prob: float, augmentation_background_noise_min_snr_db: float,
           augmentation_background_noise_max_snr_db: float, augmentation_reverb_prob: float,
-          augmentation_gain_prob: float,
+          augmentation_gain_prob: float, augmentation_colored_noise_prob: float,
+          augmentation_colored_noise_min_snr_db: float, augmentation_colored_noise_max_snr_db: float,
+          augmentation_colored_noise_min_f_decay: float, augmentation_colored_noise_max_f_decay: float,
           logging_steps: int, validation_steps: int, checkpoint_steps: int, positive_samples: int,
           adversarial_samples: int, negative_samples: int, positive_batch_size: int,
           negative_batch_size: int, adversarial_batch_size: int, validation_samples: int,
@@ -156,7 +163,12 @@ def train(phrase: str, additional_phrase: List[str], wandb_entity: Optional[str]
                          batch_size=128, background_noise_prob=augmentation_background_noise_prob,
                          background_noise_min_snr_db=augmentation_background_noise_min_snr_db,
                          background_noise_max_snr_db=augmentation_background_noise_max_snr_db,
-                         reverb_prob=augmentation_reverb_prob, gain_prob=augmentation_gain_prob)
+                         reverb_prob=augmentation_reverb_prob, gain_prob=augmentation_gain_prob,
+                         colored_noise_prob=augmentation_colored_noise_prob,
+                         colored_noise_min_snr_db=augmentation_colored_noise_min_snr_db,
+                         colored_noise_max_snr_db=augmentation_colored_noise_max_snr_db,
+                         colored_noise_min_f_decay=augmentation_colored_noise_min_f_decay,
+                         colored_noise_max_f_decay=augmentation_colored_noise_max_f_decay)
     pos = build_embeddings(positive_samples, seed + 1, device, aug, kind="positive", phrase=phrase)
     adv = build_embeddings(adversarial_samples, seed + 2, device, aug, kind="adversarial")
     neg = build_embeddings(negative_samples, seed + 3, device, aug, kind="negative").half()

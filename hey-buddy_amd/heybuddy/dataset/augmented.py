@@ -12,12 +12,17 @@ Semantics kept from the reference:
 * reverb: ONE impulse response per batch, taken in order (:188-192);
 * gain: torch_audiomentations Gain in per_batch mode (:116-120), one factor
   10^(g/20), g ~ U[-18, 6] dB, per batch with probability gain_prob (1.0),
-  applied before the noise mix (it is the last transform of augment_batch).
+  applied before the noise mix (it is the last transform of augment_batch);
+* colored noise: torch_audiomentations AddColoredNoise in per_batch mode
+  (:107-113), before the gain: per batch with probability colored_noise_prob
+  (0.25) one snr ~ U[10, 30] dB and one f_decay ~ U[-1, 2] (per_batch draws
+  one parameter set, as for the gain); white noise per clip from the kernel's
+  counter-based normal stream (seeded from numpy's global RNG).
 Differences (by design): the IR spectra are computed once for the whole bank
 instead of once per batch, every batch of a call is one kernel launch, and
 clips never leave the device (the reference copies each clip back to host,
 :419). The other augmentations (7-band EQ, tanh distortion, pitch shift,
-band-stop, colored noise) are not on this path yet.
+band-stop) are not on this path yet.
 """
 from __future__ import annotations
 
@@ -28,6 +33,10 @@ import torch
 
 from heybuddy.constants import (DEFAULT_AUGMENT_BACKGROUND_NOISE_MAX_SNR_DB,
                                 DEFAULT_AUGMENT_BACKGROUND_NOISE_MIN_SNR_DB,
+                                DEFAULT_AUGMENT_COLORED_NOISE_MAX_F_DECAY,
+                                DEFAULT_AUGMENT_COLORED_NOISE_MAX_SNR_DB,
+                                DEFAULT_AUGMENT_COLORED_NOISE_MIN_F_DECAY,
+                                DEFAULT_AUGMENT_COLORED_NOISE_MIN_SNR_DB, DEFAULT_AUGMENT_COLORED_NOISE_PROB,
                                 DEFAULT_AUGMENT_BACKGROUND_NOISE_PROB, DEFAULT_AUGMENT_GAIN_MAX_DB,
                                 DEFAULT_AUGMENT_GAIN_MIN_DB, DEFAULT_AUGMENT_GAIN_PROB,
                                 DEFAULT_AUGMENT_REVERB_PROB)
@@ -48,7 +57,13 @@ class BatchAugmenter:
                  reverb_prob: float = DEFAULT_AUGMENT_REVERB_PROB,
                  gain_prob: float = DEFAULT_AUGMENT_GAIN_PROB,
                  min_gain_in_db: float = DEFAULT_AUGMENT_GAIN_MIN_DB,
-                 max_gain_in_db: float = DEFAULT_AUGMENT_GAIN_MAX_DB) -> None:
+                 max_gain_in_db: float = DEFAULT_AUGMENT_GAIN_MAX_DB,
+                 colored_noise_prob: float = DEFAULT_AUGMENT_COLORED_NOISE_PROB,
+                 colored_noise_min_snr_db: float = DEFAULT_AUGMENT_COLORED_NOISE_MIN_SNR_DB,
+                 colored_noise_max_snr_db: float = DEFAULT_AUGMENT_COLORED_NOISE_MAX_SNR_DB,
+                 colored_noise_min_f_decay: float = DEFAULT_AUGMENT_COLORED_NOISE_MIN_F_DECAY,
+                 colored_noise_max_f_decay: float = DEFAULT_AUGMENT_COLORED_NOISE_MAX_F_DECAY,
+                 sample_rate: int = 16000) -> None:
         self.plan = ReverbPlan(device)
         self.device = self.plan.device
         if background_noise_prob > 0 and not noise:
@@ -63,6 +78,10 @@ class BatchAugmenter:
         self.p_gain = float(gain_prob)
         self.gain_min_db = float(min_gain_in_db)
         self.gain_max_db = float(max_gain_in_db)
+        self.p_colored = float(colored_noise_prob)
+        self.colored_snr = (float(colored_noise_min_snr_db), float(colored_noise_max_snr_db))
+        self.colored_decay = (float(colored_noise_min_f_decay), float(colored_noise_max_f_decay))
+        self.sample_rate = int(sample_rate)
         self.ring = None
         self.lengths: List[int] = []
         self.starts: List[int] = []
@@ -107,6 +126,12 @@ class BatchAugmenter:
         g_on = np.random.rand(nbat) < self.p_gain
         g_db = np.random.uniform(self.gain_min_db, self.gain_max_db, nbat)
         gain_db = np.where(g_on, g_db, 0.0).astype(np.float32)[batch]
+        # colored noise (AddColoredNoise, per_batch): one (snr, f_decay) per batch; NaN snr = off
+        c_on = np.random.rand(nbat) < self.p_colored
+        c_snr = np.random.uniform(*self.colored_snr, nbat)
+        c_fd = np.random.uniform(*self.colored_decay, nbat)
+        colored_snr = np.where(c_on, c_snr, np.nan).astype(np.float32)[batch]
+        colored_fd = c_fd.astype(np.float32)[batch]
         # background noise: consecutive T-sample segments of the noise stream
         noise_off = np.full(n, -1, dtype=np.int64)
         n_on = (np.random.rand(nbat) < self.p_noise) if self.ring is not None else np.zeros(nbat, bool)
@@ -126,6 +151,7 @@ class BatchAugmenter:
             self.ir_idx = int((self.ir_idx + r_on.sum()) % n_spec)
             per_clip = np.where(r_on, ir, -1).astype(np.int32)[batch]
             spec_idx[:] = per_clip
+        self._colored = (colored_snr, colored_fd)
         return noise_off, spec_idx, gain_db
 
     def __call__(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -139,5 +165,11 @@ class BatchAugmenter:
         gain = None
         if self.p_gain > 0:  # torch_audiomentations convert_decibels_to_amplitude_ratio
             gain = torch.pow(10.0, torch.from_numpy(gain_db) / 20.0)
+        colored_snr, colored_fd = self._colored
+        if not np.isnan(colored_snr).all():  # colored noise precedes the gain (augmented.py:107-118)
+            x = self.plan.colored_noise(x, torch.from_numpy(colored_fd), torch.from_numpy(colored_snr),
+                                        seed=int(np.random.randint(0, 2 ** 62)), out=out,
+                                        sample_rate=self.sample_rate)
+            out = x
         return self.plan.augment(x, self.ring, torch.from_numpy(noise_off), snr, self.spectra,
                                  torch.from_numpy(spec_idx), out=out, gain=gain)

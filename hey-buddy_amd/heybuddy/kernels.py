@@ -467,6 +467,37 @@ class ReverbPlan:
               "hbk_augment")
         return out
 
+    def colored_noise(self, x: torch.Tensor, f_decay: torch.Tensor, snr_db: torch.Tensor,
+                      white: torch.Tensor | None = None, seed: int = 0, out: torch.Tensor | None = None,
+                      sample_rate: int = 16000) -> torch.Tensor:
+        """torch_audiomentations AddColoredNoise on x [n, >= T] -> out [n, T]
+        (hbk_colored_noise): per clip f_decay and snr (dB; NaN leaves the clip
+        unchanged); white noise [n, >= T] N(0,1) if given, else the kernel's
+        counter-based stream from ``seed``."""
+        n = x.shape[0]
+        if x.dim() != 2 or x.shape[1] < self.T or x.stride(1) != 1 or x.device != self.device:
+            raise ValueError(f"x must be [n, >= {self.T}] f32 rows on {self.device}")
+        if white is not None and (white.dim() != 2 or white.shape[0] != n or white.shape[1] < self.T
+                                  or white.stride(1) != 1 or white.device != self.device
+                                  or white.dtype != torch.float32):
+            raise ValueError(f"white must be [n, >= {self.T}] f32 rows on {self.device}")
+        if out is None:
+            out = torch.empty((n, self.T), dtype=torch.float32, device=self.device)
+
+        def per_clip(t: torch.Tensor) -> torch.Tensor:
+            t = t.to(dtype=torch.float32).reshape(-1).contiguous()
+            if t.numel() != n:
+                raise ValueError("per-clip arrays must have n entries")
+            return t.pin_memory().to(self.device, non_blocking=True) if t.device.type == "cpu" else t.to(self.device)
+
+        f_decay, snr_db = per_clip(f_decay), per_clip(snr_db)
+        check(lib().hbk_colored_noise(self._handle, ptr(x), n, x.stride(0),
+                                      ptr(white) if white is not None else None,
+                                      white.stride(0) if white is not None else 0,
+                                      int(seed) & (2 ** 64 - 1), ptr(f_decay), ptr(snr_db), float(sample_rate),
+                                      ptr(out), out.stride(0), stream_ptr(self.device)), "hbk_colored_noise")
+        return out
+
     def __del__(self) -> None:
         h = getattr(self, "_handle", None)
         if h is not None and h.value:

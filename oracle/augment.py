@@ -24,6 +24,13 @@ their published algorithms at the versions environment.yml pins
       k = [ir[d:], zeros(T - L), ir[:d]]
       y = irfft(rfft(x) * rfft(k), n=T)          (circular, length T)
       y = a_in * y / (mean |y| + 1e-14)
+* torch_audiomentations.AddColoredNoise (min/max SNR 10/30 dB, f_decay -1..2,
+  mode per_batch, p 0.25; augmented.py:107-113, constants.py:128-132), between
+  band-stop and gain in the batch chain. Per clip (snr and f_decay per example):
+      w ~ N(0, 1) [T];  S = rfft(w) / linspace(1, sqrt(sr / 2), T/2 + 1)^f_decay
+      n = irfft(S);  n = n / (rms(n) + 1e-8)                 (Audio.rms_normalize)
+      y = x + rms(x) / 10^(snr / 20) * n                     (calculate_rms)
+  The white noise is an explicit input (torch.randn's stream is not reproduced).
 """
 from __future__ import annotations
 
@@ -73,6 +80,20 @@ def reverberate(x: np.ndarray, ir: np.ndarray, dtype=np.float64) -> np.ndarray:
     k = reverb_kernel(ir, T)
     y = np.fft.irfft(np.fft.rfft(x, axis=-1) * np.fft.rfft(k), n=T, axis=-1)
     return a_in * y / (np.abs(y).mean(axis=-1, keepdims=True) + 1e-14)
+
+
+def colored_noise(x, white, f_decay, snr_db, sample_rate: int = 16000, dtype=np.float64) -> np.ndarray:
+    """AddColoredNoise.apply_transform / _gen_noise with the white noise given."""
+    x = np.asarray(x, dtype=dtype)
+    w = np.asarray(white, dtype=dtype)
+    T = x.shape[-1]
+    spec = np.fft.rfft(w, axis=-1)
+    lin = np.linspace(1.0, np.sqrt(sample_rate / 2.0), spec.shape[-1])
+    fd = np.asarray(f_decay, dtype=dtype).reshape(-1, 1)
+    n = np.fft.irfft(spec / lin[None, :] ** fd, n=T, axis=-1)
+    n = n / (np.sqrt((n * n).mean(axis=-1, keepdims=True)) + 1e-8)
+    rms_x = np.sqrt((x * x).mean(axis=-1, keepdims=True))
+    return x + rms_x / 10.0 ** (np.asarray(snr_db, dtype=dtype).reshape(-1, 1) / 20.0) * n
 
 
 def db_to_amplitude(db) -> np.ndarray:

@@ -229,6 +229,7 @@ def test_batch_plan_consumes_whole_noise_clips_per_batch():
     aug = object.__new__(BatchAugmenter)
     aug.batch_size, aug.p_gain, aug.gain_min_db, aug.gain_max_db = 128, 1.0, -18.0, 6.0
     aug.p_noise = aug.p_reverb = 1.0
+    aug.p_colored, aug.colored_snr, aug.colored_decay = 0.5, (10.0, 30.0), (-1.0, 2.0)
     aug.lengths = [48000 + 997 * i for i in range(40)]
     aug.starts = list(np.cumsum([0] + aug.lengths[:-1]))
     aug.ring, aug.spectra = object(), np.zeros((7, 1))
@@ -247,4 +248,97 @@ def test_batch_plan_consumes_whole_noise_clips_per_batch():
         assert (spec_idx[b0:b0 + nb] == ir).all()
         ir = (ir + 1) % 7
         assert len(set(gain_db[b0:b0 + nb])) == 1 and -18 <= gain_db[b0] <= 6
+        c_snr, c_fd = aug._colored[0][b0:b0 + nb], aug._colored[1][b0:b0 + nb]
+        assert len(set(c_fd)) == 1 and -1 <= c_fd[0] <= 2
+        assert np.isnan(c_snr).all() or (len(set(c_snr)) == 1 and 10 <= c_snr[0] <= 30)
     assert aug.noise_idx == idx and aug.ir_idx == ir
+
+
+# ---- colored noise (torch_audiomentations AddColoredNoise, augmented.py:107-113) ----
+# PARITY UNPINNED at the third-party boundary (torch_audiomentations is not
+# installed, no fixture): oracle/augment.py restates AddColoredNoise; the white
+# noise is an explicit input on both sides. Same tolerance as above.
+
+def test_colored_noise_oracle_properties():
+    rng = np.random.default_rng(21)
+    x = _clips(3, seed=21)
+    w = rng.standard_normal((3, T))
+    snr = np.array([10.0, 20.0, 30.0])
+    # f_decay 0: the noise is the white noise, rms-normalised
+    y = oaug.colored_noise(x, w, np.zeros(3), snr)
+    rms = lambda v: np.sqrt((v * v).mean(axis=-1))
+    n = (y - x) / (rms(x) / 10 ** (snr / 20))[:, None]
+    np.testing.assert_allclose(n, w / (rms(w)[:, None] + 1e-8), atol=1e-9)
+    # any f_decay: the added noise sits exactly snr dB below the clip (up to the 1e-8 guard)
+    fd = np.array([-1.0, 0.7, 2.0])
+    y = oaug.colored_noise(x, w, fd, snr)
+    np.testing.assert_allclose(20 * np.log10(rms(x) / rms(y - x)), snr, atol=1e-6)
+    # the noise spectrum is the white spectrum shaped by linspace(1, sqrt(8000), T/2+1)^-f_decay
+    lin = np.linspace(1.0, np.sqrt(8000.0), T // 2 + 1)
+    ratio = np.abs(np.fft.rfft(y - x)) / np.abs(np.fft.rfft(w))
+    for i in range(3):
+        shape = ratio[i] / ratio[i, 1]
+        np.testing.assert_allclose(shape[1:], (lin[1:] / lin[1]) ** -fd[i], rtol=1e-6)
+
+
+@pytest.mark.gpu
+def test_colored_noise_parity():
+    from heybuddy.kernels import ReverbPlan
+    plan = ReverbPlan()
+    x = _clips(5, seed=22)
+    w = np.random.default_rng(23).standard_normal((5, T)).astype(np.float32)
+    fd = np.array([-1.0, 0.0, 0.5, 1.3, 2.0], dtype=np.float32)
+    snr = np.array([10.0, 15.0, 20.0, 25.0, 30.0], dtype=np.float32)
+    out = plan.colored_noise(torch.from_numpy(x).float().cuda(), torch.from_numpy(fd), torch.from_numpy(snr),
+                             white=torch.from_numpy(w).cuda()).cpu().numpy()
+    ref = oaug.colored_noise(x.astype(np.float32), w, fd, snr)
+    for i in range(5):
+        ok, worst = _close(out[i], ref[i])
+        assert ok, f"clip {i}: max |diff| {worst}"
+
+
+@pytest.mark.gpu
+def test_colored_noise_nan_snr_skips_and_generated_stream():
+    from heybuddy.kernels import ReverbPlan
+    plan = ReverbPlan()
+    x = torch.from_numpy(_clips(4, seed=24)).float().cuda()
+    fd = torch.tensor([0.0, 1.0, 0.0, -1.0])
+    snr = torch.tensor([12.0, float("nan"), 25.0, float("nan")])
+    out = plan.colored_noise(x, fd, snr, seed=7)
+    assert torch.equal(out[1], x[1]) and torch.equal(out[3], x[3])
+    again = plan.colored_noise(x, fd, snr, seed=7)
+    other = plan.colored_noise(x, fd, snr, seed=8)
+    assert torch.equal(out, again) and not torch.equal(out[0], other[0])
+    xs, os_ = x.cpu().double().numpy(), out.cpu().double().numpy()
+    rms = lambda v: np.sqrt((v * v).mean())
+    for i, s in ((0, 12.0), (2, 25.0)):
+        n = os_[i] - xs[i]
+        assert abs(20 * np.log10(rms(xs[i]) / rms(n)) - s) < 1e-3
+        # f_decay 0: the generated stream itself, normalised: ~N(0, 1) moments
+        z = n / rms(n)
+        assert abs(z.mean()) < 0.03 and abs((z ** 4).mean() - 3.0) < 0.2
+    # in place (out = x) leaves NaN-snr clips untouched too
+    y = x.clone()
+    plan.colored_noise(y, fd, snr, seed=7, out=y)
+    assert torch.equal(y, out)
+
+
+@pytest.mark.gpu
+def test_batch_augmenter_colored_noise_is_per_batch():
+    """mode="per_batch": one (snr, f_decay) per batch of 128; snr in [10, 30] dB."""
+    from heybuddy.dataset.augmented import BatchAugmenter
+    x = torch.from_numpy(_clips(300, seed=25)).float().cuda()
+    np.random.seed(6)
+    aug = BatchAugmenter(device=0, batch_size=128, background_noise_prob=0.0, reverb_prob=0.0, gain_prob=0.0,
+                         colored_noise_prob=1.0)
+    out = aug(x)
+    xs, os_ = x.cpu().double().numpy(), out.cpu().double().numpy()
+    rms = lambda v: np.sqrt((v * v).mean(axis=-1))
+    snr = 20 * np.log10(rms(xs) / rms(os_ - xs))
+    for b0 in range(0, 300, 128):
+        blk = snr[b0:b0 + 128]
+        assert blk.max() - blk.min() < 1e-3
+        assert 10.0 - 1e-3 <= blk[0] <= 30.0 + 1e-3
+    off = BatchAugmenter(device=0, background_noise_prob=0.0, reverb_prob=0.0, gain_prob=0.0,
+                         colored_noise_prob=0.0)
+    assert torch.equal(off(x), x)
