@@ -171,7 +171,7 @@ def setup_featurize(args, dev, rank, world, seed):
         aug = BatchAugmenter(noise_bank(64, seed=seed + 1, device=dev),
                              impulse_responses(32, seed=seed + 2, device=dev), device=dev, batch_size=128,
                              background_noise_prob=1.0, reverb_prob=1.0,
-                             colored_noise_prob=0.0)  # configs[2] = IR reverb + noise mix (+ gain)
+                             colored_noise_prob=0.0, tanh_distortion_prob=0.0)  # configs[2]: IR reverb + noise mix (+ gain)
         aug_out = torch.empty((n, AUG_T), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
     stages = (["augment"] if augment else []) + ["mel", "embed"]

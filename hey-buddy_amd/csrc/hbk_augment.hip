@@ -719,6 +719,135 @@ __global__ void __launch_bounds__(kThreads) colored_noise_kernel(ColoredArgs a) 
   }
 }
 
+// ---- tanh distortion ------------------------------------------------------
+// audiomentations TanhDistortion (the reference's per-clip Compose,
+// augmented.py:79-90; p 0.25, distortion ~ U[1e-4, 0.1], constants.py:122-124):
+//   q = 100 - 99 amount; th = percentile(|x|, q) (numpy's linear interpolation);
+//   y = tanh(0.5 / (th + 1e-6) x); if rms(x) > 1e-9: y *= rms(x) / rms(y).
+// One workgroup per clip, the clip in registers. The two order statistics of
+// |x| around the percentile come from an LDS radix select over the f32 bit
+// patterns (non-negative floats order like their bits): four 8-bit histogram
+// passes for rank lo, then its successor from one count + min reduction.
+struct TanhArgs {
+  const float* x;
+  int64_t x_stride;
+  float* out;
+  int64_t out_stride;
+  int64_t n_clips;
+  const float* amount;  // per clip; NaN = clip unchanged
+};
+
+__global__ void __launch_bounds__(kThreads) tanh_distortion_kernel(TanhArgs a) {
+  __shared__ unsigned hist[256];
+  __shared__ float red[32];
+  __shared__ unsigned pick[2];  // selected digit, rank left within it
+  constexpr int kPer = (kT + kThreads - 1) / kThreads;
+  for (int64_t clip = blockIdx.x; clip < a.n_clips; clip += gridDim.x) {
+    const int tid = opaque_tid();
+    const float* x = a.x + clip * a.x_stride;
+    float* out = a.out + clip * a.out_stride;
+    const float amt = a.amount[clip];
+    if (amt != amt) {
+      if (out != x)
+        for (int s = tid; s < kT; s += kThreads) out[s] = x[s];
+      continue;
+    }
+    float xr[kPer];
+    unsigned ux[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int s = tid + u * kThreads;
+      xr[u] = s < kT ? x[s] : 0.f;
+      ux[u] = s < kT ? (__builtin_bit_cast(unsigned, xr[u]) & 0x7FFFFFFFu) : 0xFFFFFFFFu;  // past the end: above all
+    }
+    // numpy percentile, method "linear": position q/100 (N - 1)
+    const double pos = (100.0 - 99.0 * static_cast<double>(amt)) / 100.0 * (kT - 1);
+    const int lo = min(max(static_cast<int>(floor(pos)), 0), kT - 1);
+    const double frac = pos - lo;
+    unsigned prefix = 0, mask = 0, rank = static_cast<unsigned>(lo);
+#pragma unroll 1
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      if (tid < 256) hist[tid] = 0;
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < kPer; ++u)
+        if ((ux[u] & mask) == prefix && ux[u] != 0xFFFFFFFFu) atomicAdd(&hist[(ux[u] >> shift) & 255], 1u);
+      __syncthreads();
+      if (tid < 64) {  // wave 0: 4 bins per lane, inclusive scan over lanes, first lane past rank
+        const unsigned h0 = hist[4 * tid], h1 = hist[4 * tid + 1], h2 = hist[4 * tid + 2], h3 = hist[4 * tid + 3];
+        unsigned inc = h0 + h1 + h2 + h3;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const unsigned v = __shfl_up(inc, d, 64);
+          if (tid >= d) inc += v;
+        }
+        const unsigned excl = inc - (h0 + h1 + h2 + h3);
+        const unsigned long long hit = __ballot(inc > rank);
+        const int l = __ffsll(static_cast<long long>(hit)) - 1;
+        if (tid == l) {
+          unsigned r = rank - excl, dsel = 4 * l;
+          if (r >= h0) {
+            r -= h0;
+            ++dsel;
+            if (r >= h1) {
+              r -= h1;
+              ++dsel;
+              if (r >= h2) {
+                r -= h2;
+                ++dsel;
+              }
+            }
+          }
+          pick[0] = dsel;
+          pick[1] = r;
+        }
+      }
+      __syncthreads();
+      prefix |= pick[0] << shift;
+      mask |= 255u << shift;
+      rank = pick[1];
+    }
+    // successor: v_lo again if more than lo + 1 values are <= v_lo, else min{|x| > v_lo}
+    float cnt = 0.f, mg = __builtin_inff();
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      if (ux[u] == 0xFFFFFFFFu) continue;
+      if (ux[u] <= prefix) cnt += 1.f;
+      else mg = fminf(mg, __builtin_bit_cast(float, ux[u]));
+    }
+    cnt = block_sum(cnt, red);
+    {  // block min (wave min through shuffles, then the 16 partials)
+      for (int d = 32; d >= 1; d >>= 1) mg = fminf(mg, __shfl_xor(mg, d, 64));
+      __syncthreads();
+      if ((tid & 63) == 0) red[tid >> 6] = mg;
+      __syncthreads();
+      mg = red[0];
+      for (int w = 1; w < kThreads / 64; ++w) mg = fminf(mg, red[w]);
+    }
+    const double v_lo = __builtin_bit_cast(float, prefix);
+    const double v_hi = (cnt >= lo + 2 || lo + 1 >= kT) ? v_lo : static_cast<double>(mg);
+    const double d = v_hi - v_lo;
+    const double th = frac >= 0.5 ? v_hi - d * (1.0 - frac) : v_lo + d * frac;  // numpy _lerp
+    const float g = static_cast<float>(0.5 / (th + 1e-6));
+    float ex = 0.f, ey = 0.f;
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      ex += xr[u] * xr[u];
+      xr[u] = tanhf(g * xr[u]);  // past-the-end slots hold 0 -> tanh 0 = 0
+      ey += xr[u] * xr[u];
+    }
+    block_sum2(ex, ey, red);
+    const float rms_x = sqrtf(ex / kT);
+    const float post = rms_x > 1e-9f ? rms_x / sqrtf(ey / kT) : 1.f;
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int s = tid + u * kThreads;
+      if (s < kT) out[s] = xr[u] * post;
+    }
+    __syncthreads();  // red / hist reuse by the next clip
+  }
+}
+
 }  // namespace
 }  // namespace hbk
 
@@ -866,6 +995,26 @@ int hbk_colored_noise(const hbk_reverb_plan* p, const float* x, int64_t n_clips,
   const int64_t blocks = std::min<int64_t>(n_clips, persistent_blocks(1));
   hipLaunchKernelGGL(colored_noise_kernel, dim3(unsigned(blocks)), dim3(kThreads), kAugLds, as_stream(stream), a);
   HBK_LAUNCH_CHECK("colored_noise_kernel");
+  return HBK_OK;
+}
+
+int hbk_tanh_distortion(const float* x, int64_t n_clips, int64_t x_stride, const float* amount, float* out,
+                        int64_t out_stride, void* stream) {
+  using namespace hbk;
+  if (n_clips < 0) return arg_error("negative n_clips");
+  if (n_clips == 0) return HBK_OK;
+  if (!x || !out || !amount) return arg_error("NULL pointer");
+  if (x_stride < kT || out_stride < kT) return arg_error("stride < 23040");
+  TanhArgs a;
+  a.x = x;
+  a.x_stride = x_stride;
+  a.out = out;
+  a.out_stride = out_stride;
+  a.n_clips = n_clips;
+  a.amount = amount;
+  const int64_t blocks = std::min<int64_t>(n_clips, persistent_blocks(2));
+  hipLaunchKernelGGL(tanh_distortion_kernel, dim3(unsigned(blocks)), dim3(kThreads), 0, as_stream(stream), a);
+  HBK_LAUNCH_CHECK("tanh_distortion_kernel");
   return HBK_OK;
 }
 

@@ -102,6 +102,9 @@ def build_embeddings(n: int, seed: int, device: torch.device, augmenter=None, ch
 @click.option("--augmentation-background-noise-max-snr-db", type=float, default=DEFAULT_AUGMENT_BACKGROUND_NOISE_MAX_SNR_DB, show_default=True)
 @click.option("--augmentation-reverb-prob", type=float, default=DEFAULT_AUGMENT_REVERB_PROB, show_default=True)
 @click.option("--augmentation-gain-prob", type=float, default=DEFAULT_AUGMENT_GAIN_PROB, show_default=True)
+@click.option("--augmentation-tanh-distortion-prob", type=float, default=DEFAULT_AUGMENT_TANH_DISTORTION_PROB, show_default=True)
+@click.option("--augmentation-tanh-min-distortion", type=float, default=DEFAULT_AUGMENT_TANH_MIN_DISTORTION, show_default=True)
+@click.option("--augmentation-tanh-max-distortion", type=float, default=DEFAULT_AUGMENT_TANH_MAX_DISTORTION, show_default=True)
 @click.option("--augmentation-colored-noise-prob", type=float, default=DEFAULT_AUGMENT_COLORED_NOISE_PROB, show_default=True)
 @click.option("--augmentation-colored-noise-min-snr-db", type=float, default=DEFAULT_AUGMENT_COLORED_NOISE_MIN_SNR_DB, show_default=True)
 @click.option("--augmentation-colored-noise-max-snr-db", type=float, default=DEFAULT_AUGMENT_COLORED_NOISE_MAX_SNR_DB, show_default=True)
@@ -133,6 +136,8 @@ def train(phrase: str, additional_phrase: List[str], wandb_entity: Optional[str]
           augmentation_gain_prob: float, augmentation_colored_noise_prob: float,
           augmentation_colored_noise_min_snr_db: float, augmentation_colored_noise_max_snr_db: float,
           augmentation_colored_noise_min_f_decay: float, augmentation_colored_noise_max_f_decay: float,
+          augmentation_tanh_distortion_prob: float, augmentation_tanh_min_distortion: float,
+          augmentation_tanh_max_distortion: float,
           logging_steps: int, validation_steps: int, checkpoint_steps: int, positive_samples: int,
           adversarial_samples: int, negative_samples: int, positive_batch_size: int,
           negative_batch_size: int, adversarial_batch_size: int, validation_samples: int,
@@ -168,7 +173,10 @@ def train(phrase: str, additional_phrase: List[str], wandb_entity: Optional[str]
                          colored_noise_min_snr_db=augmentation_colored_noise_min_snr_db,
                          colored_noise_max_snr_db=augmentation_colored_noise_max_snr_db,
                          colored_noise_min_f_decay=augmentation_colored_noise_min_f_decay,
-                         colored_noise_max_f_decay=augmentation_colored_noise_max_f_decay)
+                         colored_noise_max_f_decay=augmentation_colored_noise_max_f_decay,
+                         tanh_distortion_prob=augmentation_tanh_distortion_prob,
+                         tanh_min_distortion=augmentation_tanh_min_distortion,
+                         tanh_max_distortion=augmentation_tanh_max_distortion)
     pos = build_embeddings(positive_samples, seed + 1, device, aug, kind="positive", phrase=phrase)
     adv = build_embeddings(adversarial_samples, seed + 2, device, aug, kind="adversarial")
     neg = build_embeddings(negative_samples, seed + 3, device, aug, kind="negative").half()

@@ -17,12 +17,15 @@ Semantics kept from the reference:
   (:107-113), before the gain: per batch with probability colored_noise_prob
   (0.25) one snr ~ U[10, 30] dB and one f_decay ~ U[-1, 2] (per_batch draws
   one parameter set, as for the gain); white noise per clip from the kernel's
-  counter-based normal stream (seeded from numpy's global RNG).
+  counter-based normal stream (seeded from numpy's global RNG);
+* tanh distortion: audiomentations TanhDistortion, per CLIP with probability
+  tanh_distortion_prob (0.25), amount ~ U[1e-4, 0.1] (:79-90), first: the
+  reference applies it on the host before the batch chain (:325-328).
 Differences (by design): the IR spectra are computed once for the whole bank
 instead of once per batch, every batch of a call is one kernel launch, and
 clips never leave the device (the reference copies each clip back to host,
-:419). The other augmentations (7-band EQ, tanh distortion, pitch shift,
-band-stop) are not on this path yet.
+:419). The other augmentations (7-band EQ, pitch shift, band-stop) are not on this
+path yet.
 """
 from __future__ import annotations
 
@@ -37,10 +40,12 @@ from heybuddy.constants import (DEFAULT_AUGMENT_BACKGROUND_NOISE_MAX_SNR_DB,
                                 DEFAULT_AUGMENT_COLORED_NOISE_MAX_SNR_DB,
                                 DEFAULT_AUGMENT_COLORED_NOISE_MIN_F_DECAY,
                                 DEFAULT_AUGMENT_COLORED_NOISE_MIN_SNR_DB, DEFAULT_AUGMENT_COLORED_NOISE_PROB,
+                                DEFAULT_AUGMENT_TANH_DISTORTION_PROB, DEFAULT_AUGMENT_TANH_MAX_DISTORTION,
+                                DEFAULT_AUGMENT_TANH_MIN_DISTORTION,
                                 DEFAULT_AUGMENT_BACKGROUND_NOISE_PROB, DEFAULT_AUGMENT_GAIN_MAX_DB,
                                 DEFAULT_AUGMENT_GAIN_MIN_DB, DEFAULT_AUGMENT_GAIN_PROB,
                                 DEFAULT_AUGMENT_REVERB_PROB)
-from heybuddy.kernels import ReverbPlan
+from heybuddy.kernels import ReverbPlan, tanh_distortion
 
 __all__ = ["BatchAugmenter"]
 
@@ -63,6 +68,9 @@ class BatchAugmenter:
                  colored_noise_max_snr_db: float = DEFAULT_AUGMENT_COLORED_NOISE_MAX_SNR_DB,
                  colored_noise_min_f_decay: float = DEFAULT_AUGMENT_COLORED_NOISE_MIN_F_DECAY,
                  colored_noise_max_f_decay: float = DEFAULT_AUGMENT_COLORED_NOISE_MAX_F_DECAY,
+                 tanh_distortion_prob: float = DEFAULT_AUGMENT_TANH_DISTORTION_PROB,
+                 tanh_min_distortion: float = DEFAULT_AUGMENT_TANH_MIN_DISTORTION,
+                 tanh_max_distortion: float = DEFAULT_AUGMENT_TANH_MAX_DISTORTION,
                  sample_rate: int = 16000) -> None:
         self.plan = ReverbPlan(device)
         self.device = self.plan.device
@@ -82,6 +90,8 @@ class BatchAugmenter:
         self.colored_snr = (float(colored_noise_min_snr_db), float(colored_noise_max_snr_db))
         self.colored_decay = (float(colored_noise_min_f_decay), float(colored_noise_max_f_decay))
         self.sample_rate = int(sample_rate)
+        self.p_tanh = float(tanh_distortion_prob)
+        self.tanh_range = (float(tanh_min_distortion), float(tanh_max_distortion))
         self.ring = None
         self.lengths: List[int] = []
         self.starts: List[int] = []
@@ -152,6 +162,10 @@ class BatchAugmenter:
             per_clip = np.where(r_on, ir, -1).astype(np.int32)[batch]
             spec_idx[:] = per_clip
         self._colored = (colored_snr, colored_fd)
+        # tanh distortion (audiomentations, per clip): NaN amount = off
+        t_on = np.random.rand(n) < getattr(self, "p_tanh", 0.0)
+        t_amt = np.random.uniform(*getattr(self, "tanh_range", (0.0, 0.0)), n)
+        self._tanh = np.where(t_on, t_amt, np.nan).astype(np.float32)
         return noise_off, spec_idx, gain_db
 
     def __call__(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -165,6 +179,9 @@ class BatchAugmenter:
         gain = None
         if self.p_gain > 0:  # torch_audiomentations convert_decibels_to_amplitude_ratio
             gain = torch.pow(10.0, torch.from_numpy(gain_db) / 20.0)
+        if not np.isnan(self._tanh).all():  # per-clip Compose, before the batch chain (augmented.py:325-328)
+            x = tanh_distortion(x, torch.from_numpy(self._tanh), out=out)
+            out = x
         colored_snr, colored_fd = self._colored
         if not np.isnan(colored_snr).all():  # colored noise precedes the gain (augmented.py:107-118)
             x = self.plan.colored_noise(x, torch.from_numpy(colored_fd), torch.from_numpy(colored_snr),

@@ -373,6 +373,25 @@ class MlpPlan:
                                       stream_ptr(params.device)), "hbk_mlp_gate_adam")
 
 
+def tanh_distortion(x: torch.Tensor, amount: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """audiomentations TanhDistortion per clip on x [n, >= 23040] -> out [n, 23040]
+    (hbk_tanh_distortion); amount per clip, NaN leaves the clip unchanged."""
+    T = ReverbPlan.T
+    dev = _native.require_device(x.device)
+    n = x.shape[0]
+    if x.dim() != 2 or x.shape[1] < T or x.stride(1) != 1 or x.dtype != torch.float32:
+        raise ValueError(f"x must be [n, >= {T}] f32 rows on the device")
+    amount = amount.to(dtype=torch.float32).reshape(-1).contiguous()
+    if amount.numel() != n:
+        raise ValueError("amount must have n entries")
+    amount = amount.pin_memory().to(dev, non_blocking=True) if amount.device.type == "cpu" else amount.to(dev)
+    if out is None:
+        out = torch.empty((n, T), dtype=torch.float32, device=dev)
+    check(lib().hbk_tanh_distortion(ptr(x), n, x.stride(0), ptr(amount), ptr(out), out.stride(0),
+                                    stream_ptr(dev)), "hbk_tanh_distortion")
+    return out
+
+
 class ReverbPlan:
     """Batch augmentation on the HIP path (hbk_reverb_* / hbk_augment):
     background-noise mix + IR reverb for clips of 23,040 samples."""

@@ -242,6 +242,17 @@ int hbk_colored_noise(const hbk_reverb_plan* plan, const float* x, int64_t n_cli
                       const float* white, int64_t white_stride, uint64_t seed, const float* f_decay,
                       const float* snr_db, float sample_rate, float* out, int64_t out_stride, void* stream);
 
+/* Tanh distortion: audiomentations TanhDistortion, which the reference applies
+ * per clip with p 0.25 and distortion ~ U[1e-4, 0.1] before the batch chain
+ * (dataset/augmented.py:79-90, :325-328; constants.py:122-124). Per clip i of
+ * x [n_clips, x_stride] (first T = 23040 samples used):
+ *   th = percentile(|x|, 100 - 99 amount[i]) (numpy "linear");
+ *   y = tanh(0.5 / (th + 1e-6) x); if rms(x) > 1e-9: y *= rms(x) / rms(y);
+ *   amount[i] NaN: out[i] = x[i].
+ * out may equal x. Device pointers. */
+int hbk_tanh_distortion(const float* x, int64_t n_clips, int64_t x_stride, const float* amount, float* out,
+                        int64_t out_stride, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -31,6 +31,10 @@ their published algorithms at the versions environment.yml pins
       n = irfft(S);  n = n / (rms(n) + 1e-8)                 (Audio.rms_normalize)
       y = x + rms(x) / 10^(snr / 20) * n                     (calculate_rms)
   The white noise is an explicit input (torch.randn's stream is not reproduced).
+* audiomentations.TanhDistortion (p 0.25 per clip, distortion ~ U[1e-4, 0.1];
+  augmented.py:79-90, constants.py:122-124), in the per-clip Compose before H2D:
+      th = np.percentile(|x|, 100 - 99 amount);  y = tanh(0.5 / (th + 1e-6) x)
+      if rms(x) > 1e-9: y *= rms(x) / rms(y)
 """
 from __future__ import annotations
 
@@ -94,6 +98,20 @@ def colored_noise(x, white, f_decay, snr_db, sample_rate: int = 16000, dtype=np.
     n = n / (np.sqrt((n * n).mean(axis=-1, keepdims=True)) + 1e-8)
     rms_x = np.sqrt((x * x).mean(axis=-1, keepdims=True))
     return x + rms_x / 10.0 ** (np.asarray(snr_db, dtype=dtype).reshape(-1, 1) / 20.0) * n
+
+
+def tanh_distortion(x, amount) -> np.ndarray:
+    """TanhDistortion.apply on float32 clips (audiomentations computes in the clip dtype)."""
+    x = np.asarray(x, dtype=np.float32)
+    out = np.empty_like(x)
+    for i, a in enumerate(np.asarray(amount, dtype=np.float64).reshape(-1)):
+        th = np.percentile(np.abs(x[i]), 100 - 99 * a)
+        y = np.tanh((0.5 / (th + 1e-6)) * x[i]).astype(np.float32)
+        rb = np.sqrt(np.mean(np.square(x[i])))
+        if rb > 1e-9:
+            y = (rb / np.sqrt(np.mean(np.square(y)))) * y
+        out[i] = y
+    return out
 
 
 def db_to_amplitude(db) -> np.ndarray:

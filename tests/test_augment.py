@@ -207,7 +207,8 @@ def test_batch_augmenter_gain_is_per_batch():
     from heybuddy.dataset.augmented import BatchAugmenter
     x = torch.from_numpy(_clips(300, seed=14)).float().cuda()
     np.random.seed(5)
-    aug = BatchAugmenter(device=0, batch_size=128, background_noise_prob=0.0, reverb_prob=0.0)
+    aug = BatchAugmenter(device=0, batch_size=128, background_noise_prob=0.0, reverb_prob=0.0,
+                         colored_noise_prob=0.0, tanh_distortion_prob=0.0)
     out = aug(x)
     ratio = (out / x).cpu().numpy()
     xs = x.cpu().numpy()
@@ -216,7 +217,8 @@ def test_batch_augmenter_gain_is_per_batch():
         g = np.median(blk)
         np.testing.assert_allclose(blk, g, rtol=1e-6)
         assert 10 ** (-18 / 20) * (1 - 1e-6) <= g <= 10 ** (6 / 20) * (1 + 1e-6)
-    off = BatchAugmenter(device=0, background_noise_prob=0.0, reverb_prob=0.0, gain_prob=0.0)
+    off = BatchAugmenter(device=0, background_noise_prob=0.0, reverb_prob=0.0, gain_prob=0.0,
+                         colored_noise_prob=0.0, tanh_distortion_prob=0.0)
     assert torch.equal(off(x), x)
 
 
@@ -230,6 +232,7 @@ def test_batch_plan_consumes_whole_noise_clips_per_batch():
     aug.batch_size, aug.p_gain, aug.gain_min_db, aug.gain_max_db = 128, 1.0, -18.0, 6.0
     aug.p_noise = aug.p_reverb = 1.0
     aug.p_colored, aug.colored_snr, aug.colored_decay = 0.5, (10.0, 30.0), (-1.0, 2.0)
+    aug.p_tanh, aug.tanh_range = 0.25, (1e-4, 0.1)
     aug.lengths = [48000 + 997 * i for i in range(40)]
     aug.starts = list(np.cumsum([0] + aug.lengths[:-1]))
     aug.ring, aug.spectra = object(), np.zeros((7, 1))
@@ -252,6 +255,9 @@ def test_batch_plan_consumes_whole_noise_clips_per_batch():
         assert len(set(c_fd)) == 1 and -1 <= c_fd[0] <= 2
         assert np.isnan(c_snr).all() or (len(set(c_snr)) == 1 and 10 <= c_snr[0] <= 30)
     assert aug.noise_idx == idx and aug.ir_idx == ir
+    amt = aug._tanh  # per clip: NaN (off) or U[1e-4, 0.1]
+    on = ~np.isnan(amt)
+    assert 0.15 < on.mean() < 0.35 and ((amt[on] >= 1e-4) & (amt[on] <= 0.1)).all()
 
 
 # ---- colored noise (torch_audiomentations AddColoredNoise, augmented.py:107-113) ----
@@ -330,7 +336,7 @@ def test_batch_augmenter_colored_noise_is_per_batch():
     x = torch.from_numpy(_clips(300, seed=25)).float().cuda()
     np.random.seed(6)
     aug = BatchAugmenter(device=0, batch_size=128, background_noise_prob=0.0, reverb_prob=0.0, gain_prob=0.0,
-                         colored_noise_prob=1.0)
+                         colored_noise_prob=1.0, tanh_distortion_prob=0.0)
     out = aug(x)
     xs, os_ = x.cpu().double().numpy(), out.cpu().double().numpy()
     rms = lambda v: np.sqrt((v * v).mean(axis=-1))
@@ -340,5 +346,51 @@ def test_batch_augmenter_colored_noise_is_per_batch():
         assert blk.max() - blk.min() < 1e-3
         assert 10.0 - 1e-3 <= blk[0] <= 30.0 + 1e-3
     off = BatchAugmenter(device=0, background_noise_prob=0.0, reverb_prob=0.0, gain_prob=0.0,
-                         colored_noise_prob=0.0)
+                         colored_noise_prob=0.0, tanh_distortion_prob=0.0)
     assert torch.equal(off(x), x)
+
+
+# ---- tanh distortion (audiomentations TanhDistortion, augmented.py:79-90) ----
+# PARITY UNPINNED at the third-party boundary (audiomentations is not
+# installed); oracle/augment.py restates TanhDistortion.apply.
+
+def _tanh_clips():
+    x = _clips(6, seed=31).astype(np.float32)
+    x[3] = 0.0                                                # silent: no post-gain
+    x[4] = np.round(x[4] * 64) / 64                           # heavy ties around the percentile
+    x[5, :100] = 0.9; x[5, 100:] = 1e-3                       # percentile inside a tie run
+    return x
+
+
+def test_tanh_distortion_oracle_properties():
+    x = _tanh_clips()
+    amt = np.array([1e-4, 0.05, 0.1, 0.07, 0.1, 0.004])
+    y = oaug.tanh_distortion(x, amt)
+    rms = lambda v: np.sqrt(np.mean(np.square(v.astype(np.float64)), axis=-1))
+    live = rms(x) > 1e-9
+    np.testing.assert_allclose(rms(y)[live], rms(x)[live], rtol=1e-5)
+    assert not y[3].any()
+    # monotone, odd map of x
+    i = np.argsort(x[0])
+    assert (np.diff(y[0][i]) >= -1e-7).all()
+
+
+@pytest.mark.gpu
+def test_tanh_distortion_parity():
+    from heybuddy.kernels import tanh_distortion
+    x = _tanh_clips()
+    amt = np.array([1e-4, 0.05, 0.1, 0.07, 0.1, 0.004], dtype=np.float32)
+    out = tanh_distortion(torch.from_numpy(x).cuda(), torch.from_numpy(amt)).cpu().numpy()
+    ref = oaug.tanh_distortion(x, amt.astype(np.float64))
+    # f32 tanh / rms on both sides: 1e-5 of the clip's peak
+    for i in range(6):
+        err = np.abs(out[i] - ref[i]).max()
+        assert err <= 1e-5 * max(np.abs(ref[i]).max(), 1e-30), f"clip {i}: max |diff| {err}"
+    # NaN amount: untouched (out of place and in place)
+    nan_amt = torch.tensor([float("nan"), 0.05, float("nan"), 0.1, float("nan"), 0.01])
+    xs = torch.from_numpy(x).cuda()
+    o2 = tanh_distortion(xs, nan_amt)
+    assert torch.equal(o2[0], xs[0]) and torch.equal(o2[2], xs[2]) and torch.equal(o2[4], xs[4])
+    y = xs.clone()
+    tanh_distortion(y, nan_amt, out=y)
+    assert torch.equal(y, o2)
