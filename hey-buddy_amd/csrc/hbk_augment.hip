@@ -676,8 +676,9 @@ __global__ void __launch_bounds__(kThreads) colored_noise_kernel(ColoredArgs a) 
       const cf fe = 0.5f * cf{zk.x + zc.x, zk.y - zc.y};
       const cf fo = 0.5f * cf{zk.y + zc.y, zc.x - zk.x};
       const cf wk = twn[hslot(k)];
-      const float mk = powf(fmaf(a.lin_step, static_cast<float>(k), 1.f), -fd);
-      const float mc = powf(fmaf(a.lin_step, static_cast<float>(kM - k), 1.f), -fd);  // bin M - k (M for k = 0)
+      // lin^-f_decay as exp2(-f_decay log2 lin) on the transcendental unit (lin >= 1)
+      const float mk = exp2f(-fd * __log2f(fmaf(a.lin_step, static_cast<float>(k), 1.f)));
+      const float mc = exp2f(-fd * __log2f(fmaf(a.lin_step, static_cast<float>(kM - k), 1.f)));  // bin M - k
       const cf Yk = mk * (fe + cmul(wk, fo));
       const cf Yc = mc * (cf{fe.x, -fe.y} + cmul(cf{-wk.x, wk.y}, cf{fo.x, -fo.y}));
       const cf s1 = 0.5f * cf{Yk.x + Yc.x, Yk.y - Yc.y};
