@@ -150,7 +150,9 @@ __device__ __forceinline__ float dropped(const float* xr, int64_t base, int i, f
 __global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x, const float* __restrict__ g,
                                                      const float* __restrict__ b, float* __restrict__ y,
                                                      float* __restrict__ xhat, float* __restrict__ rstd,
-                                                     int rows, int D, float drop_p, uint64_t seed) {
+                                                     int rows, int D, float drop_p, uint64_t seed,
+                                                     const double* __restrict__ step_sc) {
+  if (step_sc) seed = static_cast<uint64_t>(step_sc[2]);  // graph replays: per-step seed from the device
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
@@ -256,7 +258,8 @@ __global__ void colsum_kernel(const float* __restrict__ x, float* __restrict__ o
 __global__ void __launch_bounds__(256) loss_kernel(const float* __restrict__ z, const float* __restrict__ y,
                                                    float* __restrict__ prob, float* __restrict__ dz,
                                                    float* __restrict__ stats, int rows, float neg_weight,
-                                                   float thr, float act_thr) {
+                                                   float thr, float act_thr, const double* __restrict__ step_sc) {
+  if (step_sc) neg_weight = static_cast<float>(step_sc[1]);
   __shared__ float red[4][kStats];
   float loc[kStats] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < rows; i += gridDim.x * blockDim.x) {
@@ -354,8 +357,9 @@ __global__ void gate_kernel(const float* __restrict__ stats, float* __restrict__
 // p -= lr / bc1 * m / (sqrt(v) / sqrt(bc2) + eps)
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                             float* __restrict__ v, const float* __restrict__ ctrl, int64_t n, float lr,
-                            float beta1, float beta2, float eps) {
+                            float beta1, float beta2, float eps, const double* __restrict__ step_sc) {
   if (ctrl[0] == 0.f) return;
+  if (step_sc) lr = static_cast<float>(step_sc[0]);
   const float scale = ctrl[1], bc1 = ctrl[2], bc2s = sqrtf(ctrl[3]);
   const float step_size = lr / bc1;
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
@@ -387,6 +391,9 @@ struct hbk_mlp_plan {
   std::vector<hbk::Gmlp> g;  // mlp_in, layers..., mlp_out
   std::vector<hbk::Ln> ln;   // layers' LNs..., norm_out
   int64_t n_params = 0;
+  // hbk_mlp_set_step_scalars: device [lr, neg_weight, seed] read by the train
+  // kernels in place of their by-value arguments (graph-captured steps)
+  const double* step_scalars = nullptr;
 };
 
 namespace hbk {
@@ -461,10 +468,10 @@ inline unsigned ew_grid(int64_t n) { return static_cast<unsigned>(std::min<int64
 
 // Forward pass; fills the workspace (activations kept for backward).
 int forward(const hbk_mlp_plan& p, const float* P, const float* x, int B, float* ws, const Ws& w,
-            float drop_p, uint64_t seed, hipStream_t s) {
+            float drop_p, uint64_t seed, hipStream_t s, const double* step_sc = nullptr) {
   const unsigned lnb = (B + 3) / 4;
   hipLaunchKernelGGL(ln_fwd_kernel, dim3(lnb), dim3(256), 0, s, x, P + p.ln_in.g, P + p.ln_in.b, ws + w.xn_in,
-                     ws + w.xhat_in, ws + w.rstd_in, B, p.d_in, drop_p, seed);
+                     ws + w.xhat_in, ws + w.rstd_in, B, p.d_in, drop_p, seed, step_sc);
   HBK_LAUNCH_CHECK("ln_fwd_kernel");
   const float* in = ws + w.xn_in;
   for (size_t k = 0; k < p.g.size(); ++k) {
@@ -473,7 +480,7 @@ int forward(const hbk_mlp_plan& p, const float* P, const float* x, int B, float*
       const Ln& l = p.ln[k - 1];
       hipLaunchKernelGGL(ln_fwd_kernel, dim3(lnb), dim3(256), 0, s, ws + w.s[k - 1], P + l.g, P + l.b,
                          ws + w.xn[k - 1], ws + w.xhat[k - 1], ws + w.rstd[k - 1], B, l.d, 0.f,
-                         uint64_t(0));
+                         uint64_t(0), static_cast<const double*>(nullptr));
       HBK_LAUNCH_CHECK("ln_fwd_kernel");
       in = ws + w.xn[k - 1];
     }
@@ -606,16 +613,18 @@ int hbk_mlp_train_fwd_bwd(const hbk_mlp_plan* p, const float* params, const floa
   float* ws = static_cast<float*>(workspace);
   const int B = static_cast<int>(batch);
   if (dropout_p < 0.f || dropout_p >= 1.f) return arg_error("dropout_p must be in [0, 1)");
-  HBK_RC(forward(*p, params, x, B, ws, w, dropout_p, seed, s));
+  HBK_RC(forward(*p, params, x, B, ws, w, dropout_p, seed, s, p->step_scalars));
   float* G = bucket;  // gradients, same layout as params
   float* stats = bucket + p->n_params;
   float* pr = prob ? prob : ws + w.prob;
   hipLaunchKernelGGL(loss_kernel, dim3(std::min<unsigned>((B + 255) / 256, 64)), dim3(256), 0, s, ws + w.z, y, pr,
-                     ws + w.dz, stats, B, neg_weight, high_loss_threshold, activation_threshold);
+                     ws + w.dz, stats, B, neg_weight, high_loss_threshold, activation_threshold, p->step_scalars);
   HBK_LAUNCH_CHECK("loss_kernel");
   // backward: dS = d(output of GMLP k) [B, out]
   const float* dS = ws + w.dz;  // [B,1] for mlp_out
-  const int rpb = 32;
+  // rows per block of the column reductions (LN dgamma/dbeta, bias grads): ~256
+  // blocks at the stage batch sizes (32 rows gave 35 blocks at B = 1100)
+  const int rpb = std::max(4, (B + 255) / 256);
   const unsigned cs_grid = (B + rpb - 1) / rpb;
   float* bufA = ws + w.dtmp_a;
   float* bufB = ws + w.dtmp_b;
@@ -655,6 +664,12 @@ int hbk_mlp_train_fwd_bwd(const hbk_mlp_plan* p, const float* params, const floa
   return HBK_OK;
 }
 
+int hbk_mlp_set_step_scalars(hbk_mlp_plan* p, const double* dev_scalars) {
+  if (!p) return hbk::arg_error("plan is NULL");
+  p->step_scalars = dev_scalars;
+  return HBK_OK;
+}
+
 int hbk_mlp_gate_adam(const hbk_mlp_plan* p, float* params, const float* bucket, float* m, float* v,
                       float* state, float* ctrl, float* history, int32_t history_cap, float lr, float beta1,
                       float beta2, float eps, void* stream) {
@@ -665,7 +680,7 @@ int hbk_mlp_gate_adam(const hbk_mlp_plan* p, float* params, const float* bucket,
                      history_cap, beta1, beta2);
   HBK_LAUNCH_CHECK("gate_kernel");
   hipLaunchKernelGGL(adam_kernel, dim3(ew_grid(p->n_params)), dim3(256), 0, s, params, bucket, m, v, ctrl,
-                     p->n_params, lr, beta1, beta2, eps);
+                     p->n_params, lr, beta1, beta2, eps, p->step_scalars);
   HBK_LAUNCH_CHECK("adam_kernel");
   return HBK_OK;
 }

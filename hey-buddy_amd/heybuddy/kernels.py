@@ -318,6 +318,16 @@ class MlpPlan:
         gmlp("mlp_out", self.n_layers + 1, L, 1)
         return out
 
+    def set_step_scalars(self, scalars: torch.Tensor | None) -> None:
+        """Device float64 [lr, neg_weight, seed] that train launches read instead of
+        their arguments (hbk_mlp_set_step_scalars; None = off). The pointer is
+        taken at launch time, so a graph captured while it is set keeps it."""
+        if scalars is not None and (scalars.dtype != torch.float64 or scalars.numel() < 3
+                                    or scalars.device.type != "cuda"):
+            raise ValueError("step scalars must be a float64 [3] device tensor")
+        check(lib().hbk_mlp_set_step_scalars(self._handle, ptr(scalars) if scalars is not None else None),
+              "hbk_mlp_set_step_scalars")
+
     def workspace(self, batch: int, device: torch.device) -> torch.Tensor:
         need = ctypes.c_int64()
         check(lib().hbk_mlp_workspace_size(self._handle, int(batch), ctypes.byref(need)),

@@ -200,12 +200,64 @@ class WakeWordTrainer(Trainer):
         y = y.to(dev, non_blocking=True)
         plan = self.model.plan
         p = self.model.dropout.p if self.model.training else 0.0
+        if dev.type == "cuda" and os.environ.get("HBK_MLP_GRAPHS", "1") != "0":
+            self._graph_step(x, y, lr, neg_weight, threshold, activation_threshold, history,
+                             seed * 1000003 + rank, p, world)
+            return
         plan.train_fwd_bwd(self.model.flat_parameters, x.reshape(x.shape[0], -1), y, self._bucket,
                            neg_weight, threshold, activation_threshold, dropout_p=p,
                            seed=seed * 1000003 + rank)
         distributed.reduce_bucket(self._bucket)
         plan.gate_adam(self.model.flat_parameters, self._bucket, self._m, self._v, self._state, self._ctrl,
                        history, lr, BETAS[0], BETAS[1], EPS)
+
+    def _graph_step(self, x: torch.Tensor, y: torch.Tensor, lr: float, neg_weight: float, threshold: float,
+                    activation_threshold: float, history: Optional[torch.Tensor], seed: int, p: float,
+                    world: int) -> None:
+        """The same step as two captured hipGraphs (forward/loss/backward, then gate +
+        Adam; the all-reduce runs between them when world > 1). lr, neg_weight and
+        the dropout seed change every step, so the kernels read them from a device
+        float64 [3] (hbk_mlp_set_step_scalars) filled before each replay. One
+        capture per (batch size, thresholds, dropout p, buffers): ~45 launches per
+        step become 2 graph launches + 3 fills + the batch copies."""
+        dev = self.device
+        plan = self.model.plan
+        flat = self.model.flat_parameters
+        B = int(x.shape[0])
+        key = (B, float(threshold), float(activation_threshold), float(p), world,
+               tuple(t.data_ptr() for t in (flat, self._m, self._v, self._state, self._ctrl, self._bucket)),
+               None if history is None else (history.data_ptr(), history.shape[0]))
+        graphs = self.__dict__.setdefault("_graphs", {})
+        g = graphs.get(key)
+        if g is None:
+            if getattr(self, "_scalars", None) is None or self._scalars.device != dev:
+                self._scalars = torch.zeros(3, dtype=torch.float64, device=dev)
+            sx = torch.zeros((B, plan.d_in), dtype=torch.float32, device=dev)
+            sy = torch.zeros(B, dtype=torch.float32, device=dev)
+            plan.workspace(B, dev)  # allocated outside the capture
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            fwd, upd = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            plan.set_step_scalars(self._scalars)
+            try:
+                with torch.cuda.graph(fwd, stream=side):
+                    plan.train_fwd_bwd(flat, sx, sy, self._bucket, 1.0, threshold, activation_threshold,
+                                       dropout_p=p, seed=0)
+                with torch.cuda.graph(upd, stream=side):
+                    plan.gate_adam(flat, self._bucket, self._m, self._v, self._state, self._ctrl, history,
+                                   1.0, BETAS[0], BETAS[1], EPS)
+            finally:
+                plan.set_step_scalars(None)  # eager launches keep their by-value arguments
+            torch.cuda.current_stream(dev).wait_stream(side)
+            g = graphs[key] = {"x": sx, "y": sy, "fwd": fwd, "upd": upd}
+        g["x"].copy_(x.reshape(B, -1), non_blocking=True)
+        g["y"].copy_(y, non_blocking=True)
+        self._scalars[0].fill_(float(lr))
+        self._scalars[1].fill_(float(neg_weight))
+        self._scalars[2].fill_(float(seed))  # < 2^53: exact in float64
+        g["fwd"].replay()
+        distributed.reduce_bucket(self._bucket)
+        g["upd"].replay()
 
     @torch.no_grad()
     def _predict_all(self, data: Any) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -189,6 +189,13 @@ int hbk_mlp_gate_adam(const hbk_mlp_plan* plan, float* params, const float* buck
                       float* v, float* state, float* ctrl, float* history, int32_t history_cap,
                       float lr, float beta1, float beta2, float eps, void* stream);
 
+/* Graph-captured training steps: dev_scalars (device, double[3] = lr,
+ * neg_weight, dropout seed; NULL = off) is read by the kernels of
+ * hbk_mlp_train_fwd_bwd and hbk_mlp_gate_adam in place of their lr,
+ * neg_weight and seed arguments, so one captured hipGraph replays every step
+ * of a stage with the schedule's values written before each replay. */
+int hbk_mlp_set_step_scalars(hbk_mlp_plan* plan, const double* dev_scalars);
+
 /* ------------------------------------------------------------------------ *
  * Batch augmentation: background-noise mix + impulse-response reverb
  *

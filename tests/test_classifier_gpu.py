@@ -117,3 +117,37 @@ def test_train_epoch_matches_reference(gold, inputs, tmp_path):
     tr2 = WakeWordTrainer(checkpoint_dir=str(tmp_path))
     tr2.resume("t")
     assert torch.equal(tr2._m, tr._m) and torch.equal(tr2.model.flat_parameters, tr.model.flat_parameters)
+
+
+def test_graph_steps_equal_eager_steps(inputs, tmp_path, monkeypatch):
+    """The captured-hipGraph step (default) and the eager step launch the same
+    kernels; lr (warmup schedule), neg_weight and the dropout seed reach the
+    graph through the device scalars, so 10 steps with dropout on must agree.
+    Not bit for bit: split-K GEMMs and the loss statistics accumulate with
+    float atomics (order varies run to run, eager or not). Loss history to
+    1e-4; parameters: Adam turns fp32-noise-floor gradients into +-lr steps
+    (module docstring), so < 0.1 % of them may differ by more than 1e-5.
+    A wrong lr, neg_weight or dropout seed moves the losses by >> 1e-4."""
+    from heybuddy.trainer import WakeWordTrainer
+    params, _, _, batches = inputs
+    data = [(torch.from_numpy(xb), torch.from_numpy(yb)) for xb, yb in batches][:10]
+    runs = []
+    for graphs in ("1", "0"):
+        monkeypatch.setenv("HBK_MLP_GRAPHS", graphs)
+        tr = WakeWordTrainer(checkpoint_dir=str(tmp_path / graphs))
+        tr.model.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=True)
+        tr.model.dropout.p = 0.1
+        torch.manual_seed(0)
+        import random
+        random.seed(3)  # train_epoch's dropout seed base
+        out = tr.train_epoch(data, num_steps=10, warmup_steps=4, hold_steps=3, validation_steps=1000,
+                             checkpoint_steps=100000, negative_weight_schedule=[1.0, 2.0, 0.5] * 4)
+        torch.cuda.synchronize()
+        runs.append((tr.model.flat_parameters.clone(), tr._m.clone(), tr._v.clone(), out[2].clone(),
+                     len(getattr(tr, "_graphs", {}))))
+    (p1, m1, v1, l1, ng), (p0, m0, v0, l0, _) = runs
+    assert ng >= 1
+    np.testing.assert_allclose(l1.numpy(), l0.numpy(), rtol=1e-4, atol=1e-6)
+    d = (p1 - p0).abs()
+    assert float((d > 1e-5).float().mean()) < 1e-3 and float(d.max()) <= 2e-2
+    assert float(((m1 - m0).abs() > 1e-5 * m0.abs().max()).float().mean()) < 1e-3
