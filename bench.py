@@ -62,6 +62,9 @@ def parse():
     ap.add_argument("--clips", type=int, default=100_000, help="clips per rank per step (configs 2, 3)")
     ap.add_argument("--cpu-sample", type=int, default=None, help="units timed on the host CPU (~10-30 s)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--full-augment", action="store_true",
+                    help="config 3 plus the reference's tanh distortion and colored noise at their default "
+                         "probabilities (0.25 each); not the BASELINE configs[2] workload")
     ap.add_argument("--no-check", action="store_true", help="skip the one-off featurize equality check")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                     help="per-kernel HBM bytes from rocprofv3 --pmc passes (optional)")
@@ -171,7 +174,8 @@ def setup_featurize(args, dev, rank, world, seed):
         aug = BatchAugmenter(noise_bank(64, seed=seed + 1, device=dev),
                              impulse_responses(32, seed=seed + 2, device=dev), device=dev, batch_size=128,
                              background_noise_prob=1.0, reverb_prob=1.0,
-                             colored_noise_prob=0.0, tanh_distortion_prob=0.0)  # configs[2]: IR reverb + noise mix (+ gain)
+                             colored_noise_prob=0.25 if args.full_augment else 0.0,
+                             tanh_distortion_prob=0.25 if args.full_augment else 0.0)  # configs[2]: reverb + noise (+ gain)
         aug_out = torch.empty((n, AUG_T), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
     stages = (["augment"] if augment else []) + ["mel", "embed"]
@@ -249,8 +253,9 @@ def setup_featurize(args, dev, rank, world, seed):
         "metric": "audio clips/sec featurized+trained, 1.5 s @16 kHz, 1/2/4/8 GPU",
         "data": "synthetic 1.5 s @16 kHz clips (seeded), SE20 stand-in embedding graph"
                 + (", synthetic noise bank + IR bank" if augment else ""),
-        "config": {"workload": ("configs[2]: 100k clips on-GPU augment (gain + noise mix + IR reverb, p=1) -> mel -> "
-                                "embed per GPU") if augment else
+        "config": {"workload": ("configs[2]: 100k clips on-GPU augment (gain + noise mix + IR reverb, p=1"
+                                + (", + tanh distortion / colored noise at p=0.25" if args.full_augment else "")
+                                + ") -> mel -> embed per GPU") if augment else
                    "configs[1]: 100k clips mel-STFT + speech-embedding forward per GPU",
                    "clips_per_rank": n, "clip_samples": int(clips.shape[1]), "mel_frames_per_clip": N_FRAMES,
                    "windows_per_clip": len(WINDOW_STARTS),
