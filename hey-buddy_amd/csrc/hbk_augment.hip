@@ -631,6 +631,24 @@ __device__ __forceinline__ float gauss(uint64_t seed, uint64_t i) {
   return sqrtf(-2.f * __logf(u1)) * __cosf(6.283185307179586f * u2);
 }
 
+// a clip copied through registers: all loads issued before the first store
+// (a load -> store loop waits out one memory latency per element, since x and
+// out may alias)
+__device__ __forceinline__ void copy_clip(const float* x, float* out, int tid) {
+  constexpr int kPer = (kT + kThreads - 1) / kThreads;
+  float v[kPer];
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int s = tid + u * kThreads;
+    v[u] = s < kT ? x[s] : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int s = tid + u * kThreads;
+    if (s < kT) out[s] = v[u];
+  }
+}
+
 __global__ void __launch_bounds__(kThreads) colored_noise_kernel(ColoredArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   cf* z = reinterpret_cast<cf*>(smem);
@@ -647,11 +665,8 @@ __global__ void __launch_bounds__(kThreads) colored_noise_kernel(ColoredArgs a) 
     const int tid = opaque_tid();
     const float snr = a.snr_db[clip];
     if (snr != snr) {  // NaN: this clip's batch drew no colored noise (uniform per block)
-      if (a.out != a.x || a.out_stride != a.x_stride) {
-        const float* x = a.x + clip * a.x_stride;
-        float* out = a.out + clip * a.out_stride;
-        for (int s = tid; s < kT; s += kThreads) out[s] = x[s];
-      }
+      if (a.out != a.x || a.out_stride != a.x_stride)
+        copy_clip(a.x + clip * a.x_stride, a.out + clip * a.out_stride, tid);
       continue;
     }
     // 1) white noise -> LDS (the previous clip's readers finished at its last barrier)
@@ -749,8 +764,7 @@ __global__ void __launch_bounds__(kThreads) tanh_distortion_kernel(TanhArgs a) {
     float* out = a.out + clip * a.out_stride;
     const float amt = a.amount[clip];
     if (amt != amt) {
-      if (out != x)
-        for (int s = tid; s < kT; s += kThreads) out[s] = x[s];
+      if (out != x) copy_clip(x, out, tid);
       continue;
     }
     float xr[kPer];
