@@ -634,18 +634,23 @@ __device__ __forceinline__ float gauss(uint64_t seed, uint64_t i) {
 // a clip copied through registers: all loads issued before the first store
 // (a load -> store loop waits out one memory latency per element, since x and
 // out may alias)
+// (groups of 8 slots: few live VGPRs in the 64-VGPR tanh kernel)
 __device__ __forceinline__ void copy_clip(const float* x, float* out, int tid) {
-  constexpr int kPer = (kT + kThreads - 1) / kThreads;
-  float v[kPer];
+  constexpr int kPer = (kT + kThreads - 1) / kThreads, kG = 8;
+#pragma unroll 1
+  for (int u0 = 0; u0 < kPer; u0 += kG) {
+    float v[kG];
 #pragma unroll
-  for (int u = 0; u < kPer; ++u) {
-    const int s = tid + u * kThreads;
-    v[u] = s < kT ? x[s] : 0.f;
-  }
+    for (int u = 0; u < kG; ++u) {
+      const int s = tid + (u0 + u) * kThreads;
+      v[u] = s < kT ? *reinterpret_cast<const float*>(reinterpret_cast<const char*>(x) + (static_cast<uint32_t>(s) << 2))
+                    : 0.f;
+    }
 #pragma unroll
-  for (int u = 0; u < kPer; ++u) {
-    const int s = tid + u * kThreads;
-    if (s < kT) out[s] = v[u];
+    for (int u = 0; u < kG; ++u) {
+      const int s = tid + (u0 + u) * kThreads;
+      if (s < kT) *reinterpret_cast<float*>(reinterpret_cast<char*>(out) + (static_cast<uint32_t>(s) << 2)) = v[u];
+    }
   }
 }
 
@@ -753,7 +758,14 @@ struct TanhArgs {
   const float* amount;  // per clip; NaN = clip unchanged
 };
 
-__global__ void __launch_bounds__(kThreads) tanh_distortion_kernel(TanhArgs a) {
+// |x| bits of slot u (u < kPer), or ~0 past the end of the clip (above every value);
+// recomputed per pass instead of held (2 blocks / CU need <= 64 VGPRs)
+__device__ __forceinline__ unsigned abs_bits(float v, int s) {
+  return s < kT ? (__builtin_bit_cast(unsigned, v) & 0x7FFFFFFFu) : 0xFFFFFFFFu;
+}
+
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8)))
+tanh_distortion_kernel(TanhArgs a) {
   __shared__ unsigned hist[256];
   __shared__ float red[32];
   __shared__ unsigned pick[2];  // selected digit, rank left within it
@@ -767,13 +779,17 @@ __global__ void __launch_bounds__(kThreads) tanh_distortion_kernel(TanhArgs a) {
       if (out != x) copy_clip(x, out, tid);
       continue;
     }
+    // uniform base + 32-bit byte offsets (global_load's saddr form): one VGPR per
+    // address instead of a hoisted 64-bit pointer per slot
     float xr[kPer];
-    unsigned ux[kPer];
+    {
+    const int t = opaque_tid();
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
-      const int s = tid + u * kThreads;
-      xr[u] = s < kT ? x[s] : 0.f;
-      ux[u] = s < kT ? (__builtin_bit_cast(unsigned, xr[u]) & 0x7FFFFFFFu) : 0xFFFFFFFFu;  // past the end: above all
+      const int s = t + u * kThreads;
+      xr[u] = s < kT ? *reinterpret_cast<const float*>(reinterpret_cast<const char*>(x) + (static_cast<uint32_t>(s) << 2))
+                     : 0.f;
+    }
     }
     // numpy percentile, method "linear": position q/100 (N - 1)
     const double pos = (100.0 - 99.0 * static_cast<double>(amt)) / 100.0 * (kT - 1);
@@ -784,9 +800,12 @@ __global__ void __launch_bounds__(kThreads) tanh_distortion_kernel(TanhArgs a) {
     for (int shift = 24; shift >= 0; shift -= 8) {
       if (tid < 256) hist[tid] = 0;
       __syncthreads();
+      const int t = opaque_tid();
 #pragma unroll
-      for (int u = 0; u < kPer; ++u)
-        if ((ux[u] & mask) == prefix && ux[u] != 0xFFFFFFFFu) atomicAdd(&hist[(ux[u] >> shift) & 255], 1u);
+      for (int u = 0; u < kPer; ++u) {
+        const unsigned b = abs_bits(xr[u], t + u * kThreads);
+        if ((b & mask) == prefix && b != 0xFFFFFFFFu) atomicAdd(&hist[(b >> shift) & 255], 1u);
+      }
       __syncthreads();
       if (tid < 64) {  // wave 0: 4 bins per lane, inclusive scan over lanes, first lane past rank
         const unsigned h0 = hist[4 * tid], h1 = hist[4 * tid + 1], h2 = hist[4 * tid + 2], h3 = hist[4 * tid + 3];
@@ -824,11 +843,13 @@ __global__ void __launch_bounds__(kThreads) tanh_distortion_kernel(TanhArgs a) {
     }
     // successor: v_lo again if more than lo + 1 values are <= v_lo, else min{|x| > v_lo}
     float cnt = 0.f, mg = __builtin_inff();
+    const int t2 = opaque_tid();
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
-      if (ux[u] == 0xFFFFFFFFu) continue;
-      if (ux[u] <= prefix) cnt += 1.f;
-      else mg = fminf(mg, __builtin_bit_cast(float, ux[u]));
+      const unsigned b = abs_bits(xr[u], t2 + u * kThreads);
+      if (b == 0xFFFFFFFFu) continue;
+      if (b <= prefix) cnt += 1.f;
+      else mg = fminf(mg, __builtin_bit_cast(float, b));
     }
     cnt = block_sum(cnt, red);
     {  // block min (wave min through shuffles, then the 16 partials)
@@ -851,16 +872,17 @@ __global__ void __launch_bounds__(kThreads) tanh_distortion_kernel(TanhArgs a) {
       // tanh(v) = 1 - 2 / (e^(2v) + 1) on the transcendental unit (+-1 at the
       // overflow ends; absolute error ~1e-7, tanhf's polynomial cost ~4x more);
       // past-the-end slots hold 0 -> 0
-      xr[u] = 1.f - 2.f / (__expf(2.f * g * xr[u]) + 1.f);
+      xr[u] = 1.f - __fdividef(2.f, __expf(2.f * g * xr[u]) + 1.f);
       ey += xr[u] * xr[u];
     }
     block_sum2(ex, ey, red);
     const float rms_x = sqrtf(ex / kT);
     const float post = rms_x > 1e-9f ? rms_x / sqrtf(ey / kT) : 1.f;
+    const int t3 = opaque_tid();
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
-      const int s = tid + u * kThreads;
-      if (s < kT) out[s] = xr[u] * post;
+      const int s = t3 + u * kThreads;
+      if (s < kT) *reinterpret_cast<float*>(reinterpret_cast<char*>(out) + (static_cast<uint32_t>(s) << 2)) = xr[u] * post;
     }
     __syncthreads();  // red / hist reuse by the next clip
   }
