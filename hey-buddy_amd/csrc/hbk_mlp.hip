@@ -632,8 +632,10 @@ int hbk_mlp_train_fwd_bwd(const hbk_mlp_plan* p, const float* params, const floa
     const Gmlp& gm = p->g[k];
     const float* X = (k == 0) ? ws + w.xn_in : ws + w.xn[k - 1];
     // dW_o [out, H] = dS^T U ; db_o = colsum dS
+    // (weight gradients accumulate into the bucket zeroed above: acc = true spares
+    // split-K its own memset of C)
     HBK_RC((gemm<true, false>(dS, ws + w.u[k], G + gm.w_o, nullptr, gm.out, gm.hid, B, gm.out, gm.hid, gm.hid,
-                              false, s)));
+                              true, s)));
     hipLaunchKernelGGL(colsum_kernel, dim3(cs_grid), dim3(128), 0, s, dS, G + gm.b_o, B, gm.out, rpb);
     HBK_LAUNCH_CHECK("colsum_kernel");
     // dU [B, H] = dS W_o
@@ -644,7 +646,7 @@ int hbk_mlp_train_fwd_bwd(const hbk_mlp_plan* p, const float* params, const floa
     HBK_LAUNCH_CHECK("gate_bwd_kernel");
     // dW_hg [2H, in] = dHG^T X ; db_hg = colsum dHG
     HBK_RC((gemm<true, false>(ws + w.dhg, X, G + gm.w_hg, nullptr, 2 * gm.hid, gm.in, B, 2 * gm.hid, gm.in,
-                              gm.in, false, s)));
+                              gm.in, true, s)));
     hipLaunchKernelGGL(colsum_kernel, dim3(cs_grid), dim3(128), 0, s, ws + w.dhg, G + gm.b_hg, B, 2 * gm.hid, rpb);
     HBK_LAUNCH_CHECK("colsum_kernel");
     // dX [B, in] = dHG W_hg
