@@ -441,10 +441,10 @@ int gemm(const float* A, const float* B, float* C, const float* bias, int M, int
   if (M <= 0 || N <= 0) return HBK_OK;
   dim3 grid((N + GBN - 1) / GBN, (M + GBM - 1) / GBM);
   // Split-K when the output has too few tiles to fill the chip (the weight
-  // gradients: K = batch; the input layer: K = 1536), >= 128 K rows per split.
+  // gradients: K = batch; the input layer: K = 1536), >= 16 K rows per split.
   int splits = 1;
   const int tiles = int(grid.x * grid.y);
-  if (tiles < 256 && K >= 256 && (ldc == N || acc)) splits = std::min(std::max(1, 512 / tiles), K / 128);
+  if (tiles < 256 && K >= 256 && (ldc == N || acc)) splits = std::min(std::max(1, 512 / tiles), K / 16);
   const int k_split = ((K + splits - 1) / splits + GBK - 1) / GBK * GBK;
   splits = (K + k_split - 1) / k_split;
   if (splits > 1 && !acc) {
