@@ -58,8 +58,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4))
-    ap.add_argument("--clips", type=int, default=100_000, help="clips per rank per step (configs 2, 3)")
+    ap.add_argument("--config", type=int, default=5, choices=(1, 2, 3, 4, 5))
+    ap.add_argument("--clips", type=int, default=100_000, help="clips per rank per step (configs 2, 3, 5)")
     ap.add_argument("--cpu-sample", type=int, default=None, help="units timed on the host CPU (~10-30 s)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--full-augment", action="store_true",
@@ -99,6 +99,8 @@ def roof(kernel, bound, work, ms, unit, traffic, peak=None, **extra):
 
 def main():
     args = parse()
+    if args.config == 1:
+        return cpu_mel_only(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -109,7 +111,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from heybuddy.synthetic import seed_for
-    setup = {2: setup_featurize, 3: setup_featurize, 4: setup_train}[args.config]
+    setup = {2: setup_featurize, 3: setup_featurize, 4: setup_train, 5: setup_e2e}[args.config]
     job = setup(args, dev, rank, world, seed_for(args.config, rank))
     stream = torch.cuda.current_stream(dev)
 
@@ -328,6 +330,245 @@ def setup_train(args, dev, rank, world, seed):
         "data": "synthetic [16,96] embedding pools in HBM (pos N(0,1)+0.5u, adv N(0,1)-0.25u, neg N(0,1) f16)",
         "config": {"workload": "configs[3]: 3-stage classifier training, stage-1 step timing",
                    "global_batch": B, "params": P, "parallelism": f"dp{world} (batch shards + 1 all-reduce/step)"},
+    }
+
+
+
+# ------------------------------------------------------------ host CPU ----
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def host_threads() -> int:
+    """Host cores this process may use (the GPU box's CPU share is 16)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+# --------------------------------------------------------------- config 1 ----
+def cpu_mel_only(args):
+    """configs[0]: 1,000 synthetic clips, mel spectrogram only, on the host CPU
+    (the reference's CPU path: 4 audio windows x 105 frames per clip through
+    the mel graph in batches of 64, features.py:203-208). No GPU is touched.
+    Reported at all host threads and at 1 thread."""
+    import numpy as np
+    from oracle.featurizer import cpu_mel_windows
+    from heybuddy.synthetic import seed_for, synthetic_clips
+    n = args.clips if args.clips != 100_000 else 1000
+    clips = synthetic_clips(n, seed=seed_for(1)).numpy()
+    threads = host_threads()
+    runs = {}
+    for th in (threads, 1):
+        sub = clips if th == threads else clips[:max(50, n // 10)]
+        cpu_mel_windows(sub[:4], threads=th)
+        t0 = time.perf_counter()
+        out = cpu_mel_windows(sub, threads=th)
+        el = time.perf_counter() - t0
+        assert out.shape == (sub.shape[0], 420, 32)
+        runs[th] = (sub.shape[0] / el, sub.shape[0], el)
+    v, nn, el = runs[threads]
+    line = {"metric": "audio clips/sec mel-spectrogram (CPU reference path)", "value": round(v, 1),
+            "unit": "clips/s", "n_gpus": 0, "steps": 1, "warmup": 1, "ms_per_step": round(el * 1e3, 3),
+            "higher_is_better": True, "scaling": "none", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic 1.5 s @16 kHz clips (seeded)",
+            "config": {"workload": "configs[0]: 1,000 synthetic clips, feature_generator mel spectrogram only, "
+                                   "CPU reference path (4 x 105 frames per clip, batch 64)",
+                       "clips": int(nn), "threads": threads, "cpu_model": cpu_model()},
+            "cpu_1thread": {"value": round(runs[1][0], 1), "unit": "clips/s", "cores": 1,
+                            "sample": f"{runs[1][1]} clips, {runs[1][2]:.1f} s"}}
+    print(json.dumps(line), flush=True)
+
+
+# --------------------------------------------------------------- config 5 ----
+def setup_e2e(args, dev, rank, world, seed):
+    """configs[4], the headline: the `heybuddy train` pipeline per rank.
+
+    One step = C clips (default 100 k: C/2 TTS-like utterances of the wake
+    phrase and C/2 adversarial ones, variable length, resident in HBM) ->
+    clip placement (to_target_length) -> the reference's augmentation chain
+    at its default probabilities (tanh distortion 0.25 per clip; colored
+    noise 0.25, gain 1.0, background noise 0.75, reverb 0.75 per batch of
+    128) -> STFT/mel -> speech embedding -> NaN replacement -> the embeddings
+    become the positive / adversarial pools of C/100 classifier train steps
+    in the reference's stage-1 batch composition (50 positive + 50
+    adversarial of THIS step's clips, each used once, + 666 + 334 negatives
+    from the precalculated f16 pool), with dropout, filter, BCE, the
+    accumulation gate and Adam. Unit = clips featurized AND trained on.
+    Data-parallel: every rank runs its own C clips and C/100 steps at the
+    reference's batch of 1,100 per rank, with one RCCL all-reduce of the
+    gradient bucket per step (weak scaling: the global batch is 1,100 x N)."""
+    import numpy as np
+    from heybuddy.dataset.augmented import AugmentedAudioGenerator
+    from heybuddy.embedding_graph import WINDOW_STARTS
+    from heybuddy.embeddings import _replace_nan_rows, default_graph, embed_plan
+    from heybuddy.kernels import embed_clips, mel_frames
+    from heybuddy.spectrogram import default_mel_plan
+    from heybuddy.synthetic import impulse_responses, noise_bank, speech_clips
+    from heybuddy.trainer import WakeWordTrainer
+
+    n = args.clips
+    half = n // 2
+    np.random.seed(seed)
+    pos, pos_len = speech_clips("hello world", half, seed=seed, device=dev)
+    adv, adv_len = speech_clips("hello world", n - half, seed=seed + 1, device=dev, adversarial=True)
+    src = torch.cat([pos, adv])
+    del pos, adv
+    lens = np.concatenate([pos_len, adv_len]).astype(np.int32)
+    aug = AugmentedAudioGenerator([], device_id=dev.index, augmentation_dataset=noise_bank(64, seed=seed + 2),
+                                  impulse_response_dataset=impulse_responses(32, seed=seed + 3), batch_size=128,
+                                  seven_band_aug_prob=0.0, pitch_shift_prob=0.0, band_stop_prob=0.0)
+    mplan = default_mel_plan(dev, 32767.0)
+    eplan = embed_plan(dev, WINDOW_STARTS)
+    pool = torch.empty((n, len(WINDOW_STARTS), 96), dtype=torch.float32, device=dev)
+    # precalculated negatives (the reference's hosted f16 sets): large 2/3, medium 1/3
+    g = torch.Generator(device=dev).manual_seed(seed + 4)
+    n_neg = 200_000
+    neg = torch.randn((n_neg, 16, 96), generator=g, device=dev).half()
+    n_large = n_neg * 2 // 3
+    P, A, NL, NM = 50, 50, 666, 334
+    B = P + A + NL + NM
+    S = half // P
+    idx = torch.empty((S, B), dtype=torch.int32, device=dev)
+    y = torch.cat([torch.ones(P), torch.zeros(B - P)]).to(dev)
+    tr = WakeWordTrainer(checkpoint_dir="/tmp/hb_bench_ck", device=dev)
+    tr.model.train()  # dropout 0.1 stays on, as in the reference
+    steps_total = 5000  # stage-1 LR schedule (warmup 1000, hold 1666, cosine)
+    lr = tr.get_learning_rate(np.arange(S) + 1000, warmup_steps=1000, hold_steps=1666, total_steps=steps_total)
+    sched = torch.from_numpy(np.stack([lr, np.ones(S)], 1).astype(np.float32)).to(dev)
+    hist = torch.zeros((S, 8), dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    stages = ["augment", "mel", "embed", "train"]
+    neg_pos = [0]
+
+    def sample():
+        """Device-side sampler: every featurized clip once (a fresh permutation
+        of the step's positives and adversarials), negatives walked through a
+        permutation of each pool with wrap-around."""
+        idx[:, :P] = torch.randperm(half, device=dev, dtype=torch.int32)[:S * P].view(S, P)
+        idx[:, P:P + A] = half + torch.randperm(n - half, device=dev, dtype=torch.int32)[:S * A].view(S, A)
+        o = neg_pos[0]
+        k = torch.arange(S * NL, device=dev, dtype=torch.int64)
+        idx[:, P + A:P + A + NL] = (-1 - ((o + k) % n_large)).to(torch.int32).view(S, NL)
+        k = torch.arange(S * NM, device=dev, dtype=torch.int64)
+        idx[:, P + A + NL:] = (-1 - n_large - ((o + k) % (n_neg - n_large))).to(torch.int32).view(S, NM)
+        neg_pos[0] = (o + S * NL) % n_large
+
+    def step(evs):
+        if evs:
+            evs[0].record(stream)
+        x = aug.augment_device(src, lens)
+        if evs:
+            evs[1].record(stream)
+        frames = mel_frames(x, mplan, N_FRAMES)
+        if evs:
+            evs[2].record(stream)
+        emb = _replace_nan_rows(embed_clips(frames, eplan, out=pool))
+        if emb is not pool:
+            pool.copy_(emb)
+        if evs:
+            evs[3].record(stream)
+        sample()
+        tr._reset_accumulation()
+        tr.train_indexed(idx, y, sched, pool32=pool, pool16=neg, history=hist, steps_per_graph=50)
+        if evs:
+            evs[4].record(stream)
+
+    flops_step = 2.0 * 559_296 * B
+
+    def roofline(name, ms, pmc):
+        if name == "augment":
+            return roof("place_kernel + tanh_distortion_kernel + colored_noise_kernel + augment_kernel "
+                        "(placement, tanh, colored noise, gain + noise mix + 23040-pt FFT reverb)", "hbm",
+                        n * AUG_T * 4 * 2, ms, "GB/s", load_traffic(pmc, ("place_kernel", "augment_kernel",
+                                                                          "colored_noise", "tanh_distortion")),
+                        algorithmic_bytes_per_clip=AUG_T * 4 * 2,
+                        bytes_basis="placed clip written + augmented clip written in place (92,160 B each); "
+                                    "the chain's re-reads of the in-place buffer are not counted")
+        if name == "mel":
+            return roof("mel_frames_v2_kernel (hbk_mel_frames)", "hbm",
+                        n * (MEL_READ_SAMPLES * 4 + N_FRAMES * 32 * 4), ms, "GB/s", load_traffic(pmc, "mel_frames"),
+                        algorithmic_bytes_per_clip=MEL_READ_SAMPLES * 4 + N_FRAMES * 32 * 4)
+        if name == "embed":
+            split = eplan.precision == "split"
+            return roof("p0_chain_kernel + p1_chain_kernel + conv_chain_x3_kernel x2 (hbk_embed_clips)", "mfma",
+                        2.0 * eplan.macs_per_clip * n, ms, "TFLOP/s",
+                        load_traffic(pmc, ("conv_chain", "p0_chain", "p1_chain")),
+                        peak=SPLIT_PEAK_TFLOPS if split else FP32_MFMA_PEAK_TFLOPS,
+                        peak_basis="f16 dense MFMA peak / 3 (hi*hi + hi*lo + lo*hi per f32-accurate MAC)",
+                        algorithmic_flops_per_clip=2.0 * eplan.macs_per_clip)
+        return roof("k1_input + k2_rows + k3_wgrad + k4_update (fused train step, %d steps of B=%d)" % (S, B),
+                    "mfma", flops_step * S, ms, "TFLOP/s",
+                    load_traffic(pmc, ("k1_input", "k2_rows", "k3_wgrad", "k4_update")),
+                    algorithmic_flops_per_sample=2.0 * 559_296, steps=S, batch=B,
+                    us_per_train_step=round(ms * 1e3 / S, 2))
+
+    def cpu_baseline(sample_n):
+        """The same pipeline on the host CPU (oracle/): placement + augment
+        (numpy fp64 noise mix + rfft reverb) + featurize (reference cost
+        structure, torch CPU fp32 convs) + the train steps of those clips
+        (numpy fp32 forward / backward / Adam at B = 1,100)."""
+        from oracle.augment import augment_batch
+        from oracle.featurizer import cpu_featurize
+        from oracle import mlp as omlp
+        from threadpoolctl import threadpool_limits
+        gr = default_graph()
+        x_all = src[:n].cpu().numpy()
+        res = {}
+        for th, m in ((host_threads(), sample_n or 1500), (1, 150)):
+            xs = x_all[:m, :AUG_T]
+            rng = np.random.default_rng(0)
+            with threadpool_limits(limits=th):
+                cpu_featurize(xs[:4], gr, threads=th)
+                t0 = time.perf_counter()
+                nz = rng.standard_normal((m, AUG_T)).astype(np.float32) * 0.1
+                ir = impulse_responses(1, seed=3)[0].numpy()
+                xa = augment_batch(xs, nz, rng.uniform(-10, 15, m), ir).astype(np.float32)
+                emb = cpu_featurize(xa, gr, threads=th)
+                params = omlp.init_params(seed=0)
+                opt = omlp.Adam(params)
+                steps = max(1, m // (P + A))
+                negs = rng.standard_normal((B - P - A, 16, 96)).astype(np.float32)
+                yy = np.concatenate([np.ones(P), np.zeros(B - P)]).astype(np.int64)
+                for s in range(steps):
+                    xb = np.concatenate([np.resize(emb, (P + A, 16, 96)), negs]).astype(np.float32)
+                    prob, z, cache = omlp.forward(params, xb, dtype=np.float32)
+                    loss, nsel, dz = omlp.step_loss_and_dz(prob, yy)
+                    grads = omlp.backward(params, cache, dz, dtype=np.float32)
+                    params = opt.step(params, grads, 1e-3)
+                el = time.perf_counter() - t0
+            res[th] = (m / el, m, el, steps)
+        th = host_threads()
+        v, m, el, steps = res[th]
+        return {"value": round(v, 2), "unit": "clips/s", "cores": th, "kind": "port",
+                "cpu_model": cpu_model(),
+                "sample": f"{m} of the step's clips through oracle/ (augment + featurize at the reference's "
+                          f"cost structure + {steps} train steps of B={B} incl. Adam), {el:.1f} s",
+                "value_1thread": round(res[1][0], 2),
+                "sample_1thread": f"{res[1][1]} clips + {res[1][3]} train steps, {res[1][2]:.1f} s"}
+
+    return {
+        "step": step, "stages": stages, "roofline": roofline, "cpu_baseline": cpu_baseline,
+        "units_per_step": n, "scaling": "weak", "unit": "clips/s",
+        "metric": "audio clips/sec featurized+trained, 1.5 s @16 kHz, 1/2/4/8 GPU",
+        "data": "synthetic TTS-like utterances (seeded, 0.3-1.5 s), synthetic noise + IR banks, synthetic "
+                "f16 negative pool; SE20 stand-in embedding graph",
+        "config": {"workload": "configs[4]: end-to-end heybuddy-train pipeline per GPU: placement -> augment "
+                               "(reference default probabilities) -> mel -> embed -> %d train steps (B=%d: 50 pos "
+                               "+ 50 adv of the step's clips + 1000 f16 negatives)" % (S, B),
+                   "clips_per_rank": n, "train_steps_per_rank": S, "train_batch_per_rank": B,
+                   "negative_pool": f"{n_neg} x [16,96] f16",
+                   "parallelism": f"dp{world} (clip shards; 1 all-reduce of the 1,025,700-B bucket per train step)"},
     }
 
 

@@ -888,6 +888,36 @@ tanh_distortion_kernel(TanhArgs a) {
   }
 }
 
+// Clip placement (AugmentedAudioGenerator.to_target_length, augmented.py:200-232):
+// out[i, t] = src[i, t - pre[i]] for pre[i] <= t < pre[i] + min(len[i], T), else 0.
+// One 256-thread block per (clip, 4096-sample span): every thread writes one
+// float4 of out (T % 4 == 0); the shifted source is read with scalar loads
+// (pre[i] is arbitrary, so the 4 samples are not 16-B aligned in src).
+constexpr int kPlaceSpan = 4096;
+__global__ void __launch_bounds__(256) place_kernel(const float* __restrict__ src, int64_t src_stride,
+                                                    const int32_t* __restrict__ src_len,
+                                                    const int32_t* __restrict__ pre, float* __restrict__ out,
+                                                    int64_t out_stride, int T) {
+  const int64_t clip = blockIdx.y;
+  const int p = pre[clip];
+  const int n = min(src_len[clip], T);
+  const float* s = src + clip * src_stride;
+  float* o = out + clip * out_stride;
+  const int t0 = blockIdx.x * kPlaceSpan + 4 * threadIdx.x;
+#pragma unroll
+  for (int r = 0; r < kPlaceSpan / 1024; ++r) {
+    const int t = t0 + r * 1024;
+    if (t >= T) break;
+    float v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int u = t + q - p;
+      v[q] = (u >= 0 && u < n) ? s[u] : 0.f;
+    }
+    *reinterpret_cast<float4*>(o + t) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
 }  // namespace
 }  // namespace hbk
 
@@ -1035,6 +1065,23 @@ int hbk_colored_noise(const hbk_reverb_plan* p, const float* x, int64_t n_clips,
   const int64_t blocks = std::min<int64_t>(n_clips, persistent_blocks(1));
   hipLaunchKernelGGL(colored_noise_kernel, dim3(unsigned(blocks)), dim3(kThreads), kAugLds, as_stream(stream), a);
   HBK_LAUNCH_CHECK("colored_noise_kernel");
+  return HBK_OK;
+}
+
+int hbk_place_clips(const float* src, int64_t n_clips, int64_t src_stride, const int32_t* src_len,
+                    const int32_t* pre, float* out, int64_t out_stride, int64_t T, void* stream) {
+  using namespace hbk;
+  if (n_clips < 0) return arg_error("negative n_clips");
+  if (n_clips == 0) return HBK_OK;
+  if (!src || !src_len || !pre || !out) return arg_error("NULL pointer");
+  if (T <= 0 || T % 4 || T > (int64_t(1) << 30)) return arg_error("T must be a positive multiple of 4");
+  if (out_stride < T || out_stride % 4 || (reinterpret_cast<uintptr_t>(out) & 15))
+    return arg_error("out rows must be 16-B aligned with stride >= T");
+  if (n_clips > 65535) return arg_error("n_clips > 65535 per call");
+  dim3 grid(unsigned((T + kPlaceSpan - 1) / kPlaceSpan), unsigned(n_clips));
+  hipLaunchKernelGGL(place_kernel, grid, dim3(256), 0, as_stream(stream), src, src_stride, src_len, pre, out,
+                     out_stride, int(T));
+  HBK_LAUNCH_CHECK("place_kernel");
   return HBK_OK;
 }
 

@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "hbk_common.h"
+#include "hbk_mlp_internal.h"
 
 namespace hbk {
 namespace {
@@ -125,16 +126,6 @@ __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
-}
-
-// Counter-based uniform in [0, 1) (splitmix64 of seed ^ index): the dropout
-// mask of element i of a step is a pure function of (seed, i).
-__device__ __forceinline__ float uniform01(uint64_t seed, uint64_t i) {
-  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (i + 1);
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return static_cast<float>(z >> 40) * (1.f / 16777216.f);
 }
 
 // Input dropout (nn.Dropout, wakeword.py:197/338: zero with prob p, scale by
@@ -372,29 +363,8 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
   }
 }
 
-// ------------------------------------------------------------ host --------
-struct Gmlp {
-  int in, hid, out;
-  int64_t w_hg, b_hg, w_o, b_o;  // offsets
-};
-struct Ln {
-  int d;
-  int64_t g, b;
-};
-
 }  // namespace
 }  // namespace hbk
-
-struct hbk_mlp_plan {
-  int d_in = 0, layer = 0, hid = 0, n_layers = 0;
-  hbk::Ln ln_in;
-  std::vector<hbk::Gmlp> g;  // mlp_in, layers..., mlp_out
-  std::vector<hbk::Ln> ln;   // layers' LNs..., norm_out
-  int64_t n_params = 0;
-  // hbk_mlp_set_step_scalars: device [lr, neg_weight, seed] read by the train
-  // kernels in place of their by-value arguments (graph-captured steps)
-  const double* step_scalars = nullptr;
-};
 
 namespace hbk {
 namespace {
@@ -571,7 +541,9 @@ int hbk_mlp_layout(const hbk_mlp_plan* p, int64_t* n_params, int64_t* offsets, i
 
 int hbk_mlp_workspace_size(const hbk_mlp_plan* p, int64_t batch, int64_t* bytes) {
   if (!p || !bytes) return hbk::arg_error("NULL");
-  *bytes = hbk::ws_layout(*p, std::max<int64_t>(batch, 1)).total * int64_t(sizeof(float));
+  int64_t floats = hbk::ws_layout(*p, std::max<int64_t>(batch, 1)).total;
+  if (hbk::mlp_fused_supported(*p)) floats = std::max(floats, hbk::mlp_fused_ws_floats(*p, batch));
+  *bytes = floats * int64_t(sizeof(float));
   return HBK_OK;
 }
 
@@ -589,6 +561,11 @@ int hbk_mlp_forward(const hbk_mlp_plan* p, const float* params, const float* x, 
   float* ws = static_cast<float*>(workspace);
   const int B = static_cast<int>(batch);
   if (dropout_p < 0.f || dropout_p >= 1.f) return arg_error("dropout_p must be in [0, 1)");
+  if (mlp_fused_supported(*p)) {
+    if (ws_bytes < mlp_fused_ws_floats(*p, batch) * int64_t(sizeof(float))) return arg_error("workspace too small");
+    return mlp_fused_run(*p, params, x, batch, nullptr, 0, nullptr, 0, nullptr, 0, B, nullptr, 0, nullptr, 0, 1.f, 0.f, 0.f,
+                         dropout_p, seed, nullptr, prob, logit, ws, false, s);
+  }
   HBK_RC(forward(*p, params, x, B, ws, w, dropout_p, seed, s));
   hipLaunchKernelGGL(sigmoid_kernel, dim3(ew_grid(B)), dim3(256), 0, s, ws + w.z, prob, B);
   HBK_LAUNCH_CHECK("sigmoid_kernel");
@@ -685,6 +662,52 @@ int hbk_mlp_gate_adam(const hbk_mlp_plan* p, float* params, const float* bucket,
                      p->n_params, lr, beta1, beta2, eps, p->step_scalars);
   HBK_LAUNCH_CHECK("adam_kernel");
   return HBK_OK;
+}
+
+int hbk_mlp_fused_supported(const hbk_mlp_plan* p, int32_t* supported) {
+  if (!p || !supported) return hbk::arg_error("NULL");
+  *supported = hbk::mlp_fused_supported(*p) ? 1 : 0;
+  return HBK_OK;
+}
+
+int hbk_mlp_step_fwd_bwd(const hbk_mlp_plan* p, const float* params, const float* pool32, int64_t n32,
+                         const void* pool16, int64_t n16, const int32_t* idx, int64_t idx_step_stride, const float* y, int64_t y_step_stride,
+                         int64_t batch, const float* state, int32_t parity, const float* sched, int64_t sched_len,
+                         float neg_weight, float high_loss_threshold, float activation_threshold, float dropout_p,
+                         uint64_t seed, float* bucket, float* prob, void* workspace, int64_t ws_bytes,
+                         void* stream) {
+  using namespace hbk;
+  if (!p) return arg_error("plan is NULL");
+  if (!mlp_fused_supported(*p)) {
+    set_error("hbk: the fused train step covers d_in 1536, layer 96, hidden 64, <= 4 layers");
+    return HBK_ERR_UNSUPPORTED;
+  }
+  if (batch <= 0 || batch > (1 << 22)) return arg_error("batch out of range");
+  if (!params || !y || !bucket || !workspace || !state) return arg_error("NULL pointer");
+  if (!idx && !pool32) return arg_error("no rows: idx and pool32 are NULL");
+  if (parity != 0 && parity != 1) return arg_error("parity must be 0 or 1");
+  if (sched && sched_len <= 0) return arg_error("sched_len must be > 0");
+  if (dropout_p < 0.f || dropout_p >= 1.f) return arg_error("dropout_p must be in [0, 1)");
+  if (ws_bytes < mlp_fused_ws_floats(*p, batch) * int64_t(sizeof(float))) return arg_error("workspace too small");
+  if (n32 < 0 || n16 < 0) return arg_error("negative pool size");
+  if (!idx && n32 < batch) return arg_error("idx NULL: pool32 must hold the batch rows");
+  return mlp_fused_run(*p, params, pool32, n32, pool16, n16, idx, idx_step_stride, y, y_step_stride, static_cast<int>(batch),
+                       state, parity, sched, static_cast<int>(std::min<int64_t>(sched_len, 1 << 30)), neg_weight,
+                       high_loss_threshold, activation_threshold, dropout_p, seed, bucket, prob, nullptr,
+                       static_cast<float*>(workspace), true, as_stream(stream));
+}
+
+int hbk_mlp_step_update(const hbk_mlp_plan* p, float* params, float* bucket, float* m, float* v, float* state,
+                        int32_t parity, const float* sched, int64_t sched_len, float lr, float beta1, float beta2,
+                        float eps, float* history, int32_t history_cap, void* stream) {
+  using namespace hbk;
+  if (!p) return arg_error("plan is NULL");
+  if (!params || !bucket || !m || !v || !state) return arg_error("NULL pointer");
+  if (parity != 0 && parity != 1) return arg_error("parity must be 0 or 1");
+  if (sched && sched_len <= 0) return arg_error("sched_len must be > 0");
+  return mlp_fused_update(*p, params, bucket, m, v, state, parity, sched,
+                          static_cast<int>(std::min<int64_t>(sched_len, 1 << 30)), lr, beta1, beta2, eps, history,
+                          history ? history_cap : 0, as_stream(stream));
 }
 
 }  // extern "C"

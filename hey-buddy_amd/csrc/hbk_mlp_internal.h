@@ -1,0 +1,56 @@
+// The classifier plan shared by hbk_mlp.hip (generic GEMM path, any dims) and
+// hbk_mlp_fused.hip (fused train step for the default architecture).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+namespace hbk {
+
+struct Gmlp {
+  int in, hid, out;
+  int64_t w_hg, b_hg, w_o, b_o;  // float offsets into the flat parameter buffer
+};
+struct Ln {
+  int d;
+  int64_t g, b;
+};
+
+}  // namespace hbk
+
+struct hbk_mlp_plan {
+  int d_in = 0, layer = 0, hid = 0, n_layers = 0;
+  hbk::Ln ln_in;
+  std::vector<hbk::Gmlp> g;  // mlp_in, layers..., mlp_out
+  std::vector<hbk::Ln> ln;   // layers' LNs..., norm_out
+  int64_t n_params = 0;
+  // hbk_mlp_set_step_scalars: device [lr, neg_weight, seed] read by the train
+  // kernels in place of their by-value arguments (graph-captured steps)
+  const double* step_scalars = nullptr;
+};
+
+namespace hbk {
+// Counter-based uniform in [0, 1) (splitmix64 of seed ^ index): the input
+// dropout mask of element i of a step is a pure function of (seed, i).
+__device__ __forceinline__ float uniform01(uint64_t seed, uint64_t i) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (i + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return static_cast<float>(z >> 40) * (1.f / 16777216.f);
+}
+
+// True when the fused kernels of hbk_mlp_fused.hip cover this plan.
+bool mlp_fused_supported(const hbk_mlp_plan& p);
+int64_t mlp_fused_ws_floats(const hbk_mlp_plan& p, int64_t B);
+int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool32, int64_t n32,
+                  const void* pool16, int64_t n16, const int32_t* idx, int64_t idx_stride, const float* y, int64_t y_stride, int B,
+                  const float* state, int parity, const float* sched, int sched_len, float neg_weight,
+                  float thr, float act_thr, float drop_p, uint64_t seed, float* bucket, float* prob,
+                  float* logit, float* ws, bool train, hipStream_t s);
+int mlp_fused_update(const hbk_mlp_plan& p, float* params, float* bucket, float* m, float* v, float* state,
+                     int parity, const float* sched, int sched_len, float lr, float b1, float b2, float eps,
+                     float* hist, int hist_cap, hipStream_t s);
+}  // namespace hbk

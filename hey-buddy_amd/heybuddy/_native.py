@@ -72,6 +72,7 @@ _PROTOS = {
     "hbk_colored_noise": (_c_int, [_vp, _vp, _c_int64, _c_int64, _vp, _c_int64, ctypes.c_uint64, _vp, _vp,
                                    _c_float, _vp, _c_int64, _vp]),
     "hbk_tanh_distortion": (_c_int, [_vp, _c_int64, _c_int64, _vp, _vp, _c_int64, _vp]),
+    "hbk_place_clips": (_c_int, [_vp, _c_int64, _c_int64, _vp, _vp, _vp, _c_int64, _c_int64, _vp]),
     "hbk_mlp_set_step_scalars": (_c_int, [_vp, _vp]),
     "hbk_mlp_plan_create": (_c_int, [ctypes.c_int32] * 4 + [ctypes.POINTER(_vp)]),
     "hbk_mlp_plan_destroy": (_c_int, [_vp]),
@@ -83,6 +84,12 @@ _PROTOS = {
                                        _c_float, ctypes.c_uint64, _vp, _vp, _vp, _c_int64, _vp]),
     "hbk_mlp_gate_adam": (_c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int32,
                                    _c_float, _c_float, _c_float, _c_float, _vp]),
+    "hbk_mlp_fused_supported": (_c_int, [_vp, ctypes.POINTER(ctypes.c_int32)]),
+    "hbk_mlp_step_fwd_bwd": (_c_int, [_vp, _vp, _vp, _c_int64, _vp, _c_int64, _vp, _c_int64, _vp, _c_int64,
+                                      _c_int64, _vp, ctypes.c_int32, _vp, _c_int64, _c_float, _c_float,
+                                      _c_float, _c_float, ctypes.c_uint64, _vp, _vp, _vp, _c_int64, _vp]),
+    "hbk_mlp_step_update": (_c_int, [_vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int32, _vp, _c_int64, _c_float,
+                                     _c_float, _c_float, _c_float, _vp, ctypes.c_int32, _vp]),
 }
 
 

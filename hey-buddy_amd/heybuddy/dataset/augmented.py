@@ -29,7 +29,7 @@ path yet.
 """
 from __future__ import annotations
 
-from typing import List, Optional, Sequence
+from typing import Any, Dict, Iterator, List, Optional, Sequence
 
 import numpy as np
 import torch
@@ -45,9 +45,10 @@ from heybuddy.constants import (DEFAULT_AUGMENT_BACKGROUND_NOISE_MAX_SNR_DB,
                                 DEFAULT_AUGMENT_BACKGROUND_NOISE_PROB, DEFAULT_AUGMENT_GAIN_MAX_DB,
                                 DEFAULT_AUGMENT_GAIN_MIN_DB, DEFAULT_AUGMENT_GAIN_PROB,
                                 DEFAULT_AUGMENT_REVERB_PROB)
-from heybuddy.kernels import ReverbPlan, tanh_distortion
+from heybuddy.kernels import ReverbPlan, place_clips, tanh_distortion
 
-__all__ = ["BatchAugmenter"]
+__all__ = ["AugmentedAudioGenerator", "BatchAugmenter", "target_length_offset", "target_length_offsets",
+           "to_target_length"]
 
 T = 23040
 
@@ -190,3 +191,229 @@ class BatchAugmenter:
             out = x
         return self.plan.augment(x, self.ring, torch.from_numpy(noise_off), snr, self.spectra,
                                  torch.from_numpy(spec_idx), out=out, gain=gain)
+
+
+# ---------------------------------------------------------------------------
+# AugmentedAudioGenerator: the reference's class surface (augmented.py:16-427)
+# over the device chain above.
+# ---------------------------------------------------------------------------
+def target_length_offset(num_samples: int, target_num_samples: int) -> int:
+    """Leading zeros to_target_length puts in front of a clip of num_samples
+    (augmented.py:210-226): 0 when it is cropped or when exactly one sample is
+    missing, else np.random.randint(int(S/4), int(3S/4)) from numpy's global
+    RNG, S = target - num_samples (one draw per padded clip, in clip order)."""
+    total = target_num_samples - num_samples
+    if total <= 1:
+        return 0
+    return int(np.random.randint(int(total / 4), int(3 * total / 4)))
+
+
+def target_length_offsets(lengths: Sequence[int], target_num_samples: int) -> np.ndarray:
+    """target_length_offset for a whole batch in one vectorised draw: numpy's
+    legacy randint with array bounds produces the same values, in clip order,
+    and leaves the RNG in the same state as one scalar draw per padded clip."""
+    lengths = np.asarray(lengths, dtype=np.int64)
+    total = target_num_samples - lengths
+    pre = np.zeros(lengths.shape[0], dtype=np.int32)
+    pad = total > 1
+    if pad.any():
+        t = total[pad]
+        pre[pad] = np.random.randint((t / 4).astype(np.int64), (3 * t / 4).astype(np.int64))
+    return pre
+
+
+def to_target_length(audio: np.ndarray, target_num_samples: int) -> np.ndarray:
+    """Host form of AugmentedAudioGenerator.to_target_length
+    (augmented.py:200-232): int16 -> /32768, crop to the target, or pad with
+    random leading silence (float32 out)."""
+    if audio.dtype == np.int16:
+        audio = audio.astype(np.float32) / 32768.0
+    n = audio.shape[0]
+    if n >= target_num_samples:
+        return audio[:target_num_samples]
+    pre = target_length_offset(n, target_num_samples)
+    out = np.zeros(target_num_samples, dtype=np.float32)
+    out[pre:pre + n] = audio
+    return out
+
+
+def _audio_arrays(dataset: Any) -> List[Dict[str, Any]]:
+    """Rows of an audio dataset as {"array", "sampling_rate"} dicts: an HF
+    ``datasets.Dataset`` with an "audio" column, a list of such rows, a list of
+    {"array", ...} dicts, or plain arrays / tensors (16 kHz)."""
+    out = []
+    for row in dataset:
+        if isinstance(row, dict) and "audio" in row:
+            row = row["audio"]
+        if isinstance(row, dict):
+            out.append({"array": row["array"], "sampling_rate": int(row.get("sampling_rate", 16000))})
+        else:
+            out.append({"array": row, "sampling_rate": 16000})
+    return out
+
+
+def _as_float_array(a: Any) -> np.ndarray:
+    if torch.is_tensor(a):
+        a = a.detach().cpu().numpy()
+    a = np.asarray(a)
+    if a.dtype == np.int16:
+        return a.astype(np.float32) / 32768.0
+    return a.astype(np.float32, copy=False)
+
+
+class AugmentedAudioGenerator:
+    """Drop-in for heybuddy.dataset.augmented.AugmentedAudioGenerator
+    (augmented.py:16-427). Same constructor and methods; every batch runs on
+    the MI355X: clip placement (hbk_place_clips), tanh distortion, colored
+    noise, gain, background noise and reverb (hbk_*), in the reference's order
+    (:297-394). The datasets are any iterable of audio rows (see _audio_arrays)
+    at ``sample_rate``; the noise and IR sets are loaded into HBM once.
+    Not on this path yet: 7-band EQ, pitch shift and band-stop
+    (their probabilities are accepted and must be 0, or a warning is logged)."""
+
+    def __init__(self, source_dataset: Any, device_id: Optional[int] = None,
+                 augmentation_dataset: Any = None, impulse_response_dataset: Any = None,
+                 target_length: float = 1.44, sample_rate: int = 16000, batch_size: int = 128,
+                 seven_band_aug_prob: float = 0.25, seven_band_aug_gain_db: float = 6.0,
+                 tanh_distortion_prob: float = DEFAULT_AUGMENT_TANH_DISTORTION_PROB,
+                 tanh_min_distortion: float = DEFAULT_AUGMENT_TANH_MIN_DISTORTION,
+                 tanh_max_distortion: float = DEFAULT_AUGMENT_TANH_MAX_DISTORTION,
+                 pitch_shift_prob: float = 0.25, pitch_shift_semitones: int = 3,
+                 band_stop_prob: float = 0.25,
+                 colored_noise_prob: float = DEFAULT_AUGMENT_COLORED_NOISE_PROB,
+                 colored_noise_min_snr_db: float = DEFAULT_AUGMENT_COLORED_NOISE_MIN_SNR_DB,
+                 colored_noise_max_snr_db: float = DEFAULT_AUGMENT_COLORED_NOISE_MAX_SNR_DB,
+                 colored_noise_min_f_decay: float = DEFAULT_AUGMENT_COLORED_NOISE_MIN_F_DECAY,
+                 colored_noise_max_f_decay: float = DEFAULT_AUGMENT_COLORED_NOISE_MAX_F_DECAY,
+                 background_noise_prob: float = DEFAULT_AUGMENT_BACKGROUND_NOISE_PROB,
+                 background_noise_min_snr_db: float = DEFAULT_AUGMENT_BACKGROUND_NOISE_MIN_SNR_DB,
+                 background_noise_max_snr_db: float = DEFAULT_AUGMENT_BACKGROUND_NOISE_MAX_SNR_DB,
+                 gain_prob: float = DEFAULT_AUGMENT_GAIN_PROB,
+                 reverb_prob: float = DEFAULT_AUGMENT_REVERB_PROB) -> None:
+        from heybuddy.util import logger
+        if background_noise_prob > 0 and not augmentation_dataset:
+            raise ValueError("Background noise is enabled but no augmentation dataset is provided")
+        if reverb_prob > 0 and not impulse_response_dataset:
+            raise ValueError("Reverb is enabled but no impulse response dataset is provided")
+        for name, p in (("seven_band_aug_prob", seven_band_aug_prob), ("pitch_shift_prob", pitch_shift_prob),
+                        ("band_stop_prob", band_stop_prob)):
+            if p > 0:
+                logger.warning(f"{name}={p}: this augmentation is not on the MI355X path yet; skipped")
+        self.device_id = device_id
+        self.source_dataset = source_dataset
+        self.augmentation_dataset = augmentation_dataset
+        self.impulse_response_dataset = impulse_response_dataset
+        self.target_length = target_length
+        self.sample_rate = int(sample_rate)
+        self.batch_size = int(batch_size)
+        self.reverb_prob = reverb_prob
+        self.background_noise_prob = background_noise_prob
+        self.background_noise_min_snr_db = background_noise_min_snr_db
+        self.background_noise_max_snr_db = background_noise_max_snr_db
+        dev = None if device_id is None else torch.device("cuda", device_id)
+
+        def bank(ds):
+            if not ds:
+                return None
+            rows = _audio_arrays(ds)
+            for r in rows:
+                if r["sampling_rate"] != self.sample_rate:
+                    raise NotImplementedError("resampling is outside the MI355X path: give "
+                                              f"{self.sample_rate} Hz audio")
+            return [torch.from_numpy(_as_float_array(r["array"]).reshape(-1)) for r in rows]
+
+        self.augmenter = BatchAugmenter(
+            bank(augmentation_dataset), bank(impulse_response_dataset), device=dev,
+            batch_size=self.batch_size, background_noise_prob=background_noise_prob,
+            background_noise_min_snr_db=background_noise_min_snr_db,
+            background_noise_max_snr_db=background_noise_max_snr_db, reverb_prob=reverb_prob,
+            gain_prob=gain_prob, colored_noise_prob=colored_noise_prob,
+            colored_noise_min_snr_db=colored_noise_min_snr_db, colored_noise_max_snr_db=colored_noise_max_snr_db,
+            colored_noise_min_f_decay=colored_noise_min_f_decay, colored_noise_max_f_decay=colored_noise_max_f_decay,
+            tanh_distortion_prob=tanh_distortion_prob, tanh_min_distortion=tanh_min_distortion,
+            tanh_max_distortion=tanh_max_distortion, sample_rate=self.sample_rate)
+        self.device = self.augmenter.device
+        self._source: Optional[List[Dict[str, Any]]] = None
+        self._source_pos = 0
+
+    @property
+    def target_num_samples(self) -> int:
+        """augmented.py:123-128."""
+        return int(self.target_length * self.sample_rate)
+
+    def to_target_length(self, audio: np.ndarray) -> np.ndarray:
+        return to_target_length(np.asarray(audio), self.target_num_samples)
+
+    def to_audio_array(self, audio: Any) -> np.ndarray:
+        """augmented.py:278-295: lists become float32 (float items) or int16."""
+        if isinstance(audio, list):
+            if not audio:
+                raise ValueError("Audio list is empty")
+            first = audio[0][0] if isinstance(audio[0], list) else audio[0]
+            return np.array(audio, dtype=np.float32 if isinstance(first, float) else np.int16)
+        return audio
+
+    def get_next_audio_sample_dict(self) -> Dict[str, Any]:
+        """The next source row, in order, wrapping around (augmented.py:148-186)."""
+        if self._source is None:
+            self._source = list(self.source_dataset)
+            if not self._source:
+                raise ValueError("source dataset is empty")
+        row = self._source[self._source_pos % len(self._source)]
+        self._source_pos += 1
+        return row if isinstance(row, dict) and "audio" in row else {"audio": _audio_arrays([row])[0]}
+
+    def place_batch(self, batch: Sequence[Any]) -> torch.Tensor:
+        """The per-clip placement of execute_augment_batch (:314-328) for a
+        batch of audio rows: one device launch; the leading-silence draws come
+        from numpy's global RNG in clip order, as to_target_length draws them."""
+        T = self.target_num_samples
+        arrays = []
+        for audio in batch:
+            a = audio["array"] if isinstance(audio, dict) else audio
+            sr = audio.get("sampling_rate", self.sample_rate) if isinstance(audio, dict) else self.sample_rate
+            if sr != self.sample_rate:
+                raise NotImplementedError("resampling is outside the MI355X path")
+            arrays.append(_as_float_array(self.to_audio_array(a)).reshape(-1))
+        lens = np.array([a.shape[0] for a in arrays], dtype=np.int32)
+        pre = target_length_offsets(lens, T)
+        width = max(int(lens.max()), 1)
+        host = torch.zeros((len(arrays), width), dtype=torch.float32).pin_memory()
+        for i, a in enumerate(arrays):
+            host[i, :a.shape[0]] = torch.from_numpy(a)
+        return place_batch_device(host.to(self.device, non_blocking=True), lens, pre, T)
+
+    def execute_augment_batch(self, batch: Sequence[Any]) -> torch.Tensor:
+        """augmented.py:297-394 on the device: placement, then the batch chain
+        (in place on the placed batch)."""
+        placed = self.place_batch(batch)
+        return self.augmenter(placed, out=placed)
+
+    def augment_device(self, clips: torch.Tensor, lengths: Optional[Sequence[int]] = None) -> torch.Tensor:
+        """Device-resident form used by the feature generator: clips [n, S] f32
+        on the device (clip i valid in [0, lengths[i])) -> augmented [n, T]."""
+        T = self.target_num_samples
+        n = clips.shape[0]
+        lens = np.full(n, clips.shape[1], dtype=np.int32) if lengths is None else np.asarray(lengths, np.int32)
+        pre = target_length_offsets(lens, T)
+        placed = place_clips(clips, lens, pre, T)  # a fresh buffer: the chain then runs in place
+        return self.augmenter(placed, out=placed)
+
+    def __call__(self, num_samples: int, **kwargs: Any) -> Iterator[Dict[str, Any]]:
+        """augmented.py:396-427: yields {"audio": {"array", "sampling_rate"}, ...}."""
+        total_batches = int(np.ceil(num_samples / self.batch_size))
+        for i in range(total_batches):
+            nb = min(self.batch_size, num_samples - i * self.batch_size)
+            items = [self.get_next_audio_sample_dict() for _ in range(nb)]
+            out = self.execute_augment_batch([it["audio"] for it in items]).cpu().numpy()
+            for audio, item in zip(out, items):
+                yield {"audio": {"array": audio, "sampling_rate": self.sample_rate},
+                       **{k: v for k, v in item.items() if k != "audio"}}
+
+
+def place_batch_device(src: torch.Tensor, lengths: np.ndarray, pre: np.ndarray, T: int) -> torch.Tensor:
+    """[n, S] -> [n, T] placement (hbk_place_clips), or a no-op view when every
+    clip is cropped at 0 and already long enough."""
+    if not pre.any() and src.shape[1] >= T and (lengths >= T).all():
+        return src[:, :T]
+    return place_clips(src, lengths, pre, T)

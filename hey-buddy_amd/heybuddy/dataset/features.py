@@ -1,0 +1,383 @@
+"""Drop-in for heybuddy.dataset.features (reference src/python/heybuddy/dataset/features.py).
+
+``TrainingFeaturesGenerator`` keeps the reference's constructor (every TTS /
+augmentation / embedding parameter), ``autoconfigure``, ``generate``,
+``__call__(num_samples) -> ndarray [n, 16, 96]``, ``default``,
+``get_wake_phrase_file_name``, ``get_training_features`` and
+``get_validation_features`` (:30-908). The pipeline per chunk is the
+reference's (:360-490):
+
+  TTS (n_tts = n // augment_sample_ratio utterances)
+    -> AugmentedAudioGenerator (clip placement, tanh distortion, colored
+       noise, gain, background noise, reverb; one device launch each)
+    -> SpeechEmbeddings (STFT/mel + speech embedding + NaN replacement)
+
+but the clips never leave HBM between the stages (``generate_device``), and
+no child process is spawned per 25,000-clip chunk (the reference isolates a
+host memory leak of its CPU/ORT path that this path does not have).
+
+Offline stand-ins (outside the hot path, documented in DESIGN.md §7):
+* TTS: Piper needs downloaded weights; ``heybuddy.synthetic.speech_clips``
+  renders variable-length tone-syllable utterances per phrase instead.
+* The default background / impulse-response datasets are Hugging Face repos
+  (constants.py DEFAULT_BACKGROUND_DATASET / DEFAULT_IMPULSE_DATASET); when a
+  dataset argument is such a name it is replaced by the synthetic noise / IR
+  banks of ``heybuddy.synthetic`` (a warning is logged). Any in-memory audio
+  dataset (HF ``Dataset``, list of arrays or {"array", "sampling_rate"} rows)
+  is used as given.
+"""
+from __future__ import annotations
+
+import math
+import os
+import re
+from typing import Any, List, Optional, Sequence, Tuple, Union
+
+import numpy as np
+import torch
+
+from heybuddy.constants import (DEFAULT_AUGMENT_BACKGROUND_NOISE_MAX_SNR_DB,
+                                DEFAULT_AUGMENT_BACKGROUND_NOISE_MIN_SNR_DB,
+                                DEFAULT_AUGMENT_BACKGROUND_NOISE_PROB,
+                                DEFAULT_AUGMENT_COLORED_NOISE_MAX_F_DECAY,
+                                DEFAULT_AUGMENT_COLORED_NOISE_MAX_SNR_DB,
+                                DEFAULT_AUGMENT_COLORED_NOISE_MIN_F_DECAY,
+                                DEFAULT_AUGMENT_COLORED_NOISE_MIN_SNR_DB, DEFAULT_AUGMENT_COLORED_NOISE_PROB,
+                                DEFAULT_AUGMENT_GAIN_PROB, DEFAULT_AUGMENT_REVERB_PROB,
+                                DEFAULT_AUGMENT_TANH_DISTORTION_PROB, DEFAULT_AUGMENT_TANH_MAX_DISTORTION,
+                                DEFAULT_AUGMENT_TANH_MIN_DISTORTION, DEFAULT_EMBEDDING_BATCH_SIZE,
+                                DEFAULT_EMBEDDING_SPECTROGRAM_BATCH_SIZE, DEFAULT_FEATURE_BATCH_SIZE)
+from heybuddy.dataset.augmented import AugmentedAudioGenerator
+from heybuddy.dataset.precalculated import PrecalculatedDatasetIterator
+from heybuddy.util import logger
+
+__all__ = ["TrainingFeaturesGenerator", "SyntheticSpeechGenerator", "safe_name"]
+
+# reference constants.py values that only this module uses
+DEFAULT_ADVERSARIAL_PHRASES = 250
+DEFAULT_TTS_BATCH_SIZE = 8
+DEFAULT_AUGMENT_BATCH_SIZE = 8
+DEFAULT_AUGMENT_SAMPLE_RATIO = 1.0
+DEFAULT_AUGMENT_SEVEN_BAND_PROB = 0.25
+DEFAULT_AUGMENT_SEVEN_BAND_GAIN_DB = 6.0
+DEFAULT_AUGMENT_PITCH_SHIFT_PROB = 0.25
+DEFAULT_AUGMENT_PITCH_SHIFT_SEMITONES = 3
+DEFAULT_AUGMENT_BAND_STOP_PROB = 0.25
+DEFAULT_AUGMENT_PHRASE_PROB = 0.75
+DEFAULT_IMPULSE_DATASET = "benjamin-paine/mit-impulse-response-survey-16khz"
+DEFAULT_BACKGROUND_DATASET = ["benjamin-paine/free-music-archive-commercial-16khz-full",
+                              "benjamin-paine/freesound-laion-640k-commercial-16khz-full"]
+SupplementalDatasetType = Any
+
+
+def safe_name(name: str) -> str:
+    """util/string_util.py:145-151: lower-case, non-alphanumerics -> '_'."""
+    return re.sub(r"[^a-z0-9]+", "_", name.lower()).strip("_")
+
+
+class SyntheticSpeechGenerator:
+    """Stands in for PiperSpeechGenerator (dataset/piper.py:16-191): ``(n)``
+    yields {"audio": {"array", "sampling_rate"}} utterances of the phrase (or
+    of adversarial phrases); ``device_batch(n)`` returns them as one HBM batch
+    (clips [n, 24000], lengths)."""
+
+    def __init__(self, phrase: str, adversarial: bool = False, num_adversarial_texts: int = 250,
+                 device_id: Optional[int] = None, target_sample_rate: int = 16000, seed: Optional[int] = None,
+                 **kwargs: Any) -> None:
+        self.phrase = phrase
+        self.adversarial = adversarial
+        self.num_adversarial_texts = max(1, int(num_adversarial_texts))
+        self.device = torch.device("cpu") if device_id is None else torch.device("cuda", device_id)
+        self.sample_rate = target_sample_rate
+        self.seed = int(np.random.randint(0, 2 ** 31 - 1)) if seed is None else int(seed)
+
+    def device_batch(self, n: int) -> Tuple[torch.Tensor, np.ndarray]:
+        from heybuddy.synthetic import speech_clips
+        return speech_clips(self.phrase, n, seed=self.seed, device=self.device, adversarial=self.adversarial,
+                            num_phrases=self.num_adversarial_texts)
+
+    def __call__(self, n: int):
+        clips, lengths = self.device_batch(n)
+        host = clips.cpu().numpy()
+        for i in range(n):
+            yield {"audio": {"array": host[i, :lengths[i]], "sampling_rate": self.sample_rate}}
+
+
+def _is_hub_name(ds: Any) -> bool:
+    if isinstance(ds, str):
+        return bool(re.match(r"^[A-Za-z0-9\-_.]+/[A-Za-z0-9\-_.]+$", ds)) and not os.path.exists(ds)
+    if isinstance(ds, (list, tuple)):
+        return bool(ds) and all(isinstance(d, str) for d in ds)
+    return False
+
+
+class TrainingFeaturesGenerator:
+    """Generate a dataset of features (features.py:30-908)."""
+
+    def __init__(self, device_id: Optional[int] = None, use_tqdm: bool = True, use_autoconfigure: bool = True,
+                 sample_rate: int = 16000, sample_batch_size: int = DEFAULT_FEATURE_BATCH_SIZE,
+                 tts_text: str = "Hello, world!", tts_additional_texts: List[str] = [],
+                 tts_adversarial: bool = False, tts_adversarial_num_phrases: int = DEFAULT_ADVERSARIAL_PHRASES,
+                 tts_adversarial_custom_phrases: List[str] = [], tts_batch_size: int = DEFAULT_TTS_BATCH_SIZE,
+                 tts_phrase_augment_prob: float = DEFAULT_AUGMENT_PHRASE_PROB,
+                 tts_phrase_augment_words: Sequence[str] = (),
+                 augment_target_length: float = 1.44, augment_batch_size: int = DEFAULT_AUGMENT_BATCH_SIZE,
+                 augment_sample_ratio: float = DEFAULT_AUGMENT_SAMPLE_RATIO,
+                 augment_dataset_streaming: bool = False,
+                 augment_background_dataset: SupplementalDatasetType = None,
+                 augment_impulse_dataset: SupplementalDatasetType = None,
+                 augment_seven_band_prob: float = DEFAULT_AUGMENT_SEVEN_BAND_PROB,
+                 augment_seven_band_gain_db: float = DEFAULT_AUGMENT_SEVEN_BAND_GAIN_DB,
+                 augment_tanh_distortion_prob: float = DEFAULT_AUGMENT_TANH_DISTORTION_PROB,
+                 augment_tanh_min_distortion: float = DEFAULT_AUGMENT_TANH_MIN_DISTORTION,
+                 augment_tanh_max_distortion: float = DEFAULT_AUGMENT_TANH_MAX_DISTORTION,
+                 augment_pitch_shift_prob: float = DEFAULT_AUGMENT_PITCH_SHIFT_PROB,
+                 augment_pitch_shift_semitones: int = DEFAULT_AUGMENT_PITCH_SHIFT_SEMITONES,
+                 augment_band_stop_prob: float = DEFAULT_AUGMENT_BAND_STOP_PROB,
+                 augment_colored_noise_prob: float = DEFAULT_AUGMENT_COLORED_NOISE_PROB,
+                 augment_colored_noise_min_snr_db: float = DEFAULT_AUGMENT_COLORED_NOISE_MIN_SNR_DB,
+                 augment_colored_noise_max_snr_db: float = DEFAULT_AUGMENT_COLORED_NOISE_MAX_SNR_DB,
+                 augment_colored_noise_min_f_decay: float = DEFAULT_AUGMENT_COLORED_NOISE_MIN_F_DECAY,
+                 augment_colored_noise_max_f_decay: float = DEFAULT_AUGMENT_COLORED_NOISE_MAX_F_DECAY,
+                 augment_background_noise_prob: float = DEFAULT_AUGMENT_BACKGROUND_NOISE_PROB,
+                 augment_background_noise_min_snr_db: float = DEFAULT_AUGMENT_BACKGROUND_NOISE_MIN_SNR_DB,
+                 augment_background_noise_max_snr_db: float = DEFAULT_AUGMENT_BACKGROUND_NOISE_MAX_SNR_DB,
+                 augment_gain_prob: float = DEFAULT_AUGMENT_GAIN_PROB,
+                 augment_reverb_prob: float = DEFAULT_AUGMENT_REVERB_PROB,
+                 embedding_spectrogram_batch_size: int = DEFAULT_EMBEDDING_SPECTROGRAM_BATCH_SIZE,
+                 embedding_batch_size: int = DEFAULT_EMBEDDING_BATCH_SIZE) -> None:
+        self.device_id = device_id
+        self.use_autoconfigure = use_autoconfigure
+        self.use_tqdm = use_tqdm
+        self.sample_rate = sample_rate
+        self.sample_batch_size = sample_batch_size
+        self.tts_text = tts_text
+        self.tts_additional_texts = list(tts_additional_texts)
+        self.tts_adversarial = tts_adversarial
+        self.tts_adversarial_num_phrases = tts_adversarial_num_phrases
+        self.tts_adversarial_custom_phrases = list(tts_adversarial_custom_phrases)
+        self.tts_batch_size = tts_batch_size
+        self.tts_phrase_augment_prob = tts_phrase_augment_prob
+        self.tts_phrase_augment_words = list(tts_phrase_augment_words)
+        self.augment_target_length = augment_target_length
+        self.augment_sample_ratio = augment_sample_ratio
+        self.augment_batch_size = augment_batch_size
+        self.augment_dataset_streaming = augment_dataset_streaming
+        self.augment_background_dataset = augment_background_dataset
+        self.augment_impulse_dataset = augment_impulse_dataset
+        self.augment_seven_band_prob = augment_seven_band_prob
+        self.augment_seven_band_gain_db = augment_seven_band_gain_db
+        self.augment_tanh_distortion_prob = augment_tanh_distortion_prob
+        self.augment_tanh_min_distortion = augment_tanh_min_distortion
+        self.augment_tanh_max_distortion = augment_tanh_max_distortion
+        self.augment_pitch_shift_prob = augment_pitch_shift_prob
+        self.augment_pitch_shift_semitones = augment_pitch_shift_semitones
+        self.augment_band_stop_prob = augment_band_stop_prob
+        self.augment_colored_noise_prob = augment_colored_noise_prob
+        self.augment_colored_noise_min_snr_db = augment_colored_noise_min_snr_db
+        self.augment_colored_noise_max_snr_db = augment_colored_noise_max_snr_db
+        self.augment_colored_noise_min_f_decay = augment_colored_noise_min_f_decay
+        self.augment_colored_noise_max_f_decay = augment_colored_noise_max_f_decay
+        self.augment_background_noise_prob = augment_background_noise_prob
+        self.augment_background_noise_min_snr_db = augment_background_noise_min_snr_db
+        self.augment_background_noise_max_snr_db = augment_background_noise_max_snr_db
+        self.augment_gain_prob = augment_gain_prob
+        self.augment_reverb_prob = augment_reverb_prob
+        self.embedding_spectrogram_batch_size = embedding_spectrogram_batch_size
+        self.embedding_batch_size = embedding_batch_size
+        self._augmenters: dict = {}
+
+    @property
+    def device(self) -> torch.device:
+        from heybuddy import _native
+        return _native.require_device(self.device_id)
+
+    def autoconfigure(self) -> None:
+        """features.py:171-218 for a GPU with >= 8 GiB: batch sizes 64 / 128 / 128 / 128.
+        The MI355X path needs a HIP device (there is no CPU branch)."""
+        from heybuddy import _native
+        dev = _native.require_device(self.device_id)
+        self.device_id = dev.index
+        self.tts_batch_size = 64
+        self.augment_batch_size = 128
+        self.embedding_spectrogram_batch_size = 128
+        self.embedding_batch_size = 128
+
+    def get_speech_embeddings_model(self):
+        from heybuddy.embeddings import get_speech_embeddings
+        return get_speech_embeddings(device_id=self.device.index)
+
+    def get_tts_generator(self) -> SyntheticSpeechGenerator:
+        return SyntheticSpeechGenerator(self.tts_text, adversarial=self.tts_adversarial,
+                                        num_adversarial_texts=self.tts_adversarial_num_phrases,
+                                        device_id=self.device.index, target_sample_rate=self.sample_rate)
+
+    def _bank(self, which: str, testing: bool) -> Any:
+        ds = self.augment_background_dataset if which == "noise" else self.augment_impulse_dataset
+        if ds is None or not _is_hub_name(ds):
+            return ds
+        from heybuddy.synthetic import impulse_responses, noise_bank
+        logger.warning(f"{which} dataset {ds!r} is a Hugging Face repo (no network): using the synthetic "
+                       f"{which} bank of heybuddy.synthetic")
+        seed = 1000 + (7 if testing else 0)
+        return noise_bank(64, seed=seed) if which == "noise" else impulse_responses(32, seed=seed + 1)
+
+    def get_augmented_generator(self, dataset: Any = None, testing: bool = False) -> AugmentedAudioGenerator:
+        key = (testing, self.augment_batch_size)
+        if key not in self._augmenters:
+            self._augmenters[key] = AugmentedAudioGenerator(
+                dataset if dataset is not None else [], device_id=self.device.index,
+                batch_size=self.augment_batch_size,
+                target_length=self.augment_target_length, sample_rate=self.sample_rate,
+                augmentation_dataset=self._bank("noise", testing),
+                impulse_response_dataset=self._bank("ir", testing),
+                seven_band_aug_prob=0.0, seven_band_aug_gain_db=self.augment_seven_band_gain_db,
+                tanh_distortion_prob=self.augment_tanh_distortion_prob,
+                tanh_min_distortion=self.augment_tanh_min_distortion,
+                tanh_max_distortion=self.augment_tanh_max_distortion,
+                pitch_shift_prob=0.0, pitch_shift_semitones=self.augment_pitch_shift_semitones,
+                band_stop_prob=0.0,
+                colored_noise_prob=self.augment_colored_noise_prob,
+                colored_noise_min_snr_db=self.augment_colored_noise_min_snr_db,
+                colored_noise_max_snr_db=self.augment_colored_noise_max_snr_db,
+                colored_noise_min_f_decay=self.augment_colored_noise_min_f_decay,
+                colored_noise_max_f_decay=self.augment_colored_noise_max_f_decay,
+                background_noise_prob=self.augment_background_noise_prob,
+                background_noise_min_snr_db=self.augment_background_noise_min_snr_db,
+                background_noise_max_snr_db=self.augment_background_noise_max_snr_db,
+                gain_prob=self.augment_gain_prob, reverb_prob=self.augment_reverb_prob)
+            for name in ("seven_band", "pitch_shift", "band_stop"):
+                p = getattr(self, f"augment_{name}_prob")
+                if p > 0:
+                    logger.warning(f"augment_{name}_prob={p}: not on the MI355X path yet; skipped")
+        return self._augmenters[key]
+
+    def augment_device(self, clips: torch.Tensor, lengths: np.ndarray, num_samples: int,
+                       testing: bool = False, validation: bool = False) -> torch.Tensor:
+        """The middle stage of generate (features.py:412-458) on device data:
+        n_tts utterances -> num_samples clips of T samples."""
+        T = int(self.sample_rate * self.augment_target_length)
+        n_tts = clips.shape[0]
+        if validation:  # centred pad, no augmentation (:412-427)
+            from heybuddy.kernels import place_clips
+            lens = np.minimum(lengths, T).astype(np.int32)
+            pre = ((T - lens) // 2).astype(np.int32)
+            return place_clips(clips, lens, pre, T)
+        idx = np.arange(num_samples) % n_tts  # the source dataset is iterated in order, wrapping
+        src = clips if num_samples == n_tts else clips.index_select(0, torch.from_numpy(idx).to(clips.device))
+        return self.get_augmented_generator(testing=testing).augment_device(src, lengths[idx])
+
+    def generate_device(self, num_samples: int, testing: bool = False, validation: bool = False) -> torch.Tensor:
+        """features.py:360-490 with every stage in HBM: [num_samples, 16, 96] f32 on the device."""
+        if self.use_autoconfigure:
+            self.autoconfigure()
+        if validation:
+            tts_num_samples = num_samples
+        else:
+            tts_num_samples = max(1, min(num_samples, int(num_samples // self.augment_sample_ratio)))
+        clips, lengths = self.get_tts_generator().device_batch(tts_num_samples)
+        audio = self.augment_device(clips, lengths, num_samples, testing=testing, validation=validation)
+        del clips
+        return self.get_speech_embeddings_model().featurize(audio)
+
+    def generate(self, num_samples: int, sample_save_path: Optional[str] = None,
+                 augmented_sample_save_path: Optional[str] = None, testing: bool = False,
+                 validation: bool = False) -> np.ndarray:
+        """Samples -> embeddings [num_samples, 16, 96] (features.py:360-490)."""
+        if sample_save_path or augmented_sample_save_path:
+            logger.warning("sample wav export needs an audio writer; skipped")
+        return self.generate_device(num_samples, testing=testing, validation=validation).cpu().numpy()
+
+    def __call__(self, num_samples: int, sample_save_path: Optional[str] = None,
+                 augmented_sample_save_path: Optional[str] = None, testing: bool = False,
+                 validation: bool = False) -> np.ndarray:
+        """Chunks of sample_batch_size, concatenated (features.py:492-535)."""
+        sizes = [self.sample_batch_size] * math.ceil(num_samples / self.sample_batch_size)
+        if num_samples % self.sample_batch_size:
+            sizes[-1] = num_samples % self.sample_batch_size
+        parts = [self.generate(s, sample_save_path, augmented_sample_save_path, testing, validation)
+                 for s in sizes]
+        return parts[0] if len(parts) == 1 else np.concatenate(parts)
+
+    @classmethod
+    def default(cls, wake_phrase: str, adversarial: bool = False, num_adversarial_phrases: int = 10,
+                additional_wake_phrases: List[str] = [], custom_adversarial_phrases: List[str] = [],
+                dataset_streaming: bool = False, tts_batch_size: int = DEFAULT_TTS_BATCH_SIZE,
+                phrase_augment_prob: float = DEFAULT_AUGMENT_PHRASE_PROB,
+                phrase_augment_words: Sequence[str] = (), augment_target_length: float = 1.44,
+                augment_background_dataset: SupplementalDatasetType = DEFAULT_BACKGROUND_DATASET,
+                augment_impulse_dataset: SupplementalDatasetType = DEFAULT_IMPULSE_DATASET,
+                **kwargs: Any) -> "TrainingFeaturesGenerator":
+        """features.py:537-616 (augment_* / embedding_* keywords pass through)."""
+        return cls(use_autoconfigure=True, tts_text=wake_phrase, tts_adversarial=adversarial,
+                   tts_batch_size=tts_batch_size, tts_adversarial_num_phrases=num_adversarial_phrases,
+                   tts_adversarial_custom_phrases=custom_adversarial_phrases,
+                   tts_additional_texts=additional_wake_phrases, tts_phrase_augment_prob=phrase_augment_prob,
+                   tts_phrase_augment_words=phrase_augment_words,
+                   augment_background_dataset=augment_background_dataset,
+                   augment_impulse_dataset=augment_impulse_dataset, augment_target_length=augment_target_length,
+                   **kwargs)
+
+    @classmethod
+    def get_wake_phrase_file_name(cls, wake_phrase: str, testing: bool = False) -> str:
+        return safe_name(wake_phrase).strip("_") + ("_tst" if testing else "")
+
+    @classmethod
+    def get_training_features(cls, wake_phrase: str, num_positive_samples: int, num_adversarial_samples: int,
+                              num_adversarial_phrases: int = 10, additional_wake_phrases: List[str] = [],
+                              custom_adversarial_phrases: List[str] = [], testing: bool = False,
+                              use_cache: bool = True, save_samples: bool = True, keep_in_memory: bool = False,
+                              directory: Optional[str] = None, **kwargs: Any
+                              ) -> Tuple[PrecalculatedDatasetIterator, PrecalculatedDatasetIterator]:
+        """Positive and adversarial feature sets for a phrase, cached by name
+        (``{name}.npy``, ``{name}_adv.npy``) and topped up when the cache is
+        short (features.py:618-837)."""
+        from heybuddy.dataset.precalculated import LOCAL_DIR
+        directory = directory or LOCAL_DIR
+        name = cls.get_wake_phrase_file_name(wake_phrase, testing=testing)
+        out = []
+        for suffix, adversarial, n in (("", False, num_positive_samples), ("_adv", True, num_adversarial_samples)):
+            it_name = name + suffix
+            existing = None
+            if use_cache:
+                try:
+                    existing = PrecalculatedDatasetIterator(it_name, directory=directory)
+                except FileNotFoundError:
+                    existing = None
+            have = len(existing) if existing is not None else 0
+            if existing is not None and have >= n:
+                out.append(existing)
+                continue
+            gen = cls.default(wake_phrase, adversarial=adversarial, num_adversarial_phrases=num_adversarial_phrases,
+                              additional_wake_phrases=additional_wake_phrases,
+                              custom_adversarial_phrases=custom_adversarial_phrases, **kwargs)
+            feats = gen(n - have, testing=testing)
+            if have:
+                feats = np.concatenate([np.asarray(existing.precalculated), feats])
+            out.append(PrecalculatedDatasetIterator.from_array(feats, name=it_name, directory=directory,
+                                                               keep_in_memory=keep_in_memory))
+        return out[0], out[1]
+
+    @classmethod
+    def get_validation_features(cls, wake_phrase: str, num_positive_samples: int, use_cache: bool = True,
+                                keep_in_memory: bool = False, augment_target_length: float = 1.44,
+                                directory: Optional[str] = None, **kwargs: Any) -> PrecalculatedDatasetIterator:
+        """Un-augmented, centre-padded positive features (features.py:840-908)."""
+        from heybuddy.dataset.precalculated import LOCAL_DIR
+        directory = directory or LOCAL_DIR
+        name = cls.get_wake_phrase_file_name(wake_phrase) + "_val"
+        existing = None
+        if use_cache:
+            try:
+                existing = PrecalculatedDatasetIterator(name, directory=directory)
+            except FileNotFoundError:
+                existing = None
+        have = len(existing) if existing is not None else 0
+        if existing is not None and have >= num_positive_samples:
+            return existing
+        gen = cls.default(wake_phrase, augment_target_length=augment_target_length)
+        feats = gen(num_positive_samples - have, validation=True)
+        if have:
+            feats = np.concatenate([np.asarray(existing.precalculated), feats])
+        return PrecalculatedDatasetIterator.from_array(feats, name=name, directory=directory,
+                                                       keep_in_memory=keep_in_memory)

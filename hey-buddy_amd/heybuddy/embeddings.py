@@ -160,9 +160,11 @@ class SpeechEmbeddings:
     def featurize(self, audio: torch.Tensor, audio_window_size: int = 17280,
                   audio_window_stride: int = 1920, window_size: int = 76, window_stride: int = 8,
                   in_scale: float = 32767.0, remove_nan: bool = True,
-                  return_frames: bool = False):
+                  return_frames: bool = False, out: Optional[torch.Tensor] = None):
         """audio [B, T] float in [-1, 1] on the device -> embeddings [B, n, 96]
-        (and the unique mel frames [B, F, 32] if ``return_frames``)."""
+        (and the unique mel frames [B, F, 32] if ``return_frames``); ``out``:
+        an optional [B, n, 96] f32 destination (kept when no NaN row needs
+        replacing)."""
         dev = audio.device
         b, t = audio.shape
         starts, f_aw, f_total = self.window_plan(t, audio_window_size, audio_window_stride,
@@ -171,13 +173,18 @@ class SpeechEmbeddings:
             raise ValueError("need at least one array to concatenate")
         mplan = default_mel_plan(dev, in_scale)
         frames = mel_frames(audio, mplan, f_total)
-        emb = torch.empty((b, len(starts), 96), dtype=torch.float32, device=dev)
-        for s0 in range(0, len(starts), 32):  # hbk plans take <= 32 windows
-            st = starts[s0:s0 + 32]
-            off = min(st)
-            plan = embed_plan(dev, [s - off for s in st])
-            sub = frames[:, off:off + plan.seq_frames]
-            emb[:, s0:s0 + len(st)] = embed_clips(sub, plan)
+        if len(starts) <= 32:  # one plan covers every window: write straight into the output
+            off = min(starts)
+            plan = embed_plan(dev, [s - off for s in starts])
+            emb = embed_clips(frames[:, off:off + plan.seq_frames], plan, out=out)
+        else:
+            emb = out if out is not None else torch.empty((b, len(starts), 96), dtype=torch.float32, device=dev)
+            for s0 in range(0, len(starts), 32):  # hbk plans take <= 32 windows
+                st = starts[s0:s0 + 32]
+                off = min(st)
+                plan = embed_plan(dev, [s - off for s in st])
+                sub = frames[:, off:off + plan.seq_frames]
+                emb[:, s0:s0 + len(st)] = embed_clips(sub, plan)
         if remove_nan:
             emb = _replace_nan_rows(emb)
         return (emb, frames) if return_frames else emb

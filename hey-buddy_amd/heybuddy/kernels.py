@@ -241,15 +241,31 @@ def _(windows, plan_id):
     return windows.new_empty((windows.shape[0], plan.out_dim))
 
 
-def embed_clips(mel: torch.Tensor, plan: EmbedPlan) -> torch.Tensor:
+@torch.library.custom_op("hbk::embed_clips_out", mutates_args=("out",))
+def _embed_clips_out_op(mel: torch.Tensor, plan_id: int, out: torch.Tensor) -> None:
+    plan = _plans[plan_id]
+    n = mel.shape[0]
+    ws = plan.workspace(n)
+    check(lib().hbk_embed_clips(plan._handle, ptr(mel), n, mel.stride(0), ptr(out), ptr(ws),
+                                ws.numel(), stream_ptr(mel.device)), "hbk_embed_clips")
+
+
+def embed_clips(mel: torch.Tensor, plan: EmbedPlan, out: torch.Tensor | None = None) -> torch.Tensor:
     """Unique mel frames [B, F >= seq_frames, n_mels] -> embeddings
-    [B, n_windows, out_dim] in the reference's slot order."""
+    [B, n_windows, out_dim] in the reference's slot order (into ``out`` if
+    given: a contiguous f32 tensor of that shape on the device)."""
     if mel.dim() != 3 or mel.dtype != torch.float32 or mel.device != plan.device:
         raise ValueError(f"mel must be [B, F, {plan.in_w}] float32 on {plan.device}")
     if mel.shape[2] != plan.in_w or mel.shape[1] < plan.seq_frames:
         raise ValueError(f"mel {tuple(mel.shape)}: need >= {plan.seq_frames} frames of {plan.in_w}")
     if mel.stride(2) != 1 or mel.stride(1) != plan.in_w:
         mel = mel.contiguous()
+    if out is not None:
+        if (tuple(out.shape) != (mel.shape[0], len(plan.starts), plan.out_dim) or out.dtype != torch.float32
+                or out.device != mel.device or not out.is_contiguous()):
+            raise ValueError("out must be a contiguous f32 [B, n_windows, out_dim] tensor on the device")
+        torch.ops.hbk.embed_clips_out(mel, plan.id, out)
+        return out
     return torch.ops.hbk.embed_clips(mel, plan.id)
 
 
@@ -328,7 +344,15 @@ class MlpPlan:
         check(lib().hbk_mlp_set_step_scalars(self._handle, ptr(scalars) if scalars is not None else None),
               "hbk_mlp_set_step_scalars")
 
+    def workspace_bytes(self, batch: int) -> int:
+        need = ctypes.c_int64()
+        check(lib().hbk_mlp_workspace_size(self._handle, int(batch), ctypes.byref(need)),
+              "hbk_mlp_workspace_size")
+        return need.value
+
     def workspace(self, batch: int, device: torch.device) -> torch.Tensor:
+        """Shared eager workspace (grown on demand). Captured graphs own their
+        workspace instead: a growth here frees the old buffer."""
         need = ctypes.c_int64()
         check(lib().hbk_mlp_workspace_size(self._handle, int(batch), ctypes.byref(need)),
               "hbk_mlp_workspace_size")
@@ -374,6 +398,73 @@ class MlpPlan:
                                           ptr(prob) if prob is not None else None, ptr(ws), ws.numel(),
                                           stream_ptr(x.device)), "hbk_mlp_train_fwd_bwd")
 
+    # -- fused train step (hbk_mlp_step_*) -------------------------------
+    @property
+    def fused(self) -> bool:
+        """True when hbk_mlp_step_* cover this architecture (the default one)."""
+        if not hasattr(self, "_fused"):
+            ok = ctypes.c_int32()
+            check(lib().hbk_mlp_fused_supported(self._handle, ctypes.byref(ok)), "hbk_mlp_fused_supported")
+            self._fused = bool(ok.value)
+        return self._fused
+
+    @staticmethod
+    def new_state(device, adam_t: float = 0.0, salt: int = 0) -> torch.Tensor:
+        """Device step state, both halves [0, 1, adam_t, 0, salt, 0, 0, 0]."""
+        half = [0.0, 1.0, float(adam_t), 0.0, float(salt % (1 << 24)), 0.0, 0.0, 0.0]
+        return torch.tensor(half * 2, dtype=torch.float32, device=device)
+
+    def step_fwd_bwd(self, params: torch.Tensor, bucket: torch.Tensor, state: torch.Tensor, parity: int,
+                     y: torch.Tensor, batch: int, pool32: torch.Tensor | None = None,
+                     pool16: torch.Tensor | None = None, idx: torch.Tensor | None = None,
+                     idx_stride: int = 0, y_stride: int = 0, sched: torch.Tensor | None = None,
+                     neg_weight: float = 1.0, threshold: float = 1e-4, activation_threshold: float = 0.5,
+                     dropout_p: float = 0.0, seed: int = 0, prob: torch.Tensor | None = None,
+                     workspace: torch.Tensor | None = None) -> None:
+        """Forward / filter / BCE / backward of one step into ``bucket``
+        (hbk_mlp_step_fwd_bwd). Rows come from pool32 [n, 1536] f32 and pool16
+        [n, 1536] f16 by ``idx`` (int32, >= 0 -> pool32, < 0 -> pool16 row -i-1;
+        None -> pool32 rows 0..batch-1); y: 0/1 float32 labels on the device."""
+        dev = params.device
+        if params.numel() != self.n_params or bucket.numel() != self.n_params + self.N_STATS:
+            raise ValueError("params / bucket do not match the plan")
+        for t, dt, name in ((pool32, torch.float32, "pool32"), (pool16, torch.float16, "pool16")):
+            if t is not None and (t.dtype != dt or t.device != dev or not t.is_contiguous()
+                                  or t.reshape(t.shape[0], -1).shape[1] != self.d_in):
+                raise ValueError(f"{name} must be a contiguous [n, {self.d_in}] {dt} tensor on {dev}")
+        if idx is not None and (idx.dtype != torch.int32 or idx.device != dev or not idx.is_contiguous()):
+            raise ValueError("idx must be a contiguous int32 device tensor")
+        if idx is None and (pool32 is None or pool32.shape[0] < batch):
+            raise ValueError("without idx, pool32 must hold the batch rows")
+        if y.dtype != torch.float32 or y.device != dev or not y.is_contiguous():
+            raise ValueError("y must be contiguous float32 labels on the device")
+        if state.numel() != 16 or state.dtype != torch.float32 or state.device != dev:
+            raise ValueError("state must be the float32 [16] device state (MlpPlan.new_state)")
+        if sched is not None and (sched.dtype != torch.float32 or sched.shape[-1] != 2 or sched.device != dev):
+            raise ValueError("sched must be float32 [n, 2] (lr, neg_weight) on the device")
+        ws = self.workspace(batch, dev) if workspace is None else workspace
+        check(lib().hbk_mlp_step_fwd_bwd(
+            self._handle, ptr(params), ptr(pool32) if pool32 is not None else None,
+            pool32.shape[0] if pool32 is not None else 0, ptr(pool16) if pool16 is not None else None,
+            pool16.shape[0] if pool16 is not None else 0, ptr(idx) if idx is not None else None, int(idx_stride),
+            ptr(y), int(y_stride), int(batch), ptr(state), int(parity),
+            ptr(sched) if sched is not None else None, sched.shape[0] if sched is not None else 0,
+            float(neg_weight), float(threshold), float(activation_threshold), float(dropout_p),
+            int(seed) & (2 ** 64 - 1), ptr(bucket), ptr(prob) if prob is not None else None, ptr(ws),
+            ws.numel(), stream_ptr(dev)), "hbk_mlp_step_fwd_bwd")
+
+    def step_update(self, params: torch.Tensor, bucket: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
+                    state: torch.Tensor, parity: int, sched: torch.Tensor | None = None, lr: float = 1e-3,
+                    beta1: float = 0.9, beta2: float = 0.999, eps: float = 1e-8,
+                    history: torch.Tensor | None = None) -> None:
+        """Gate + Adam + bucket zeroing (hbk_mlp_step_update)."""
+        cap = 0 if history is None else history.shape[0]
+        check(lib().hbk_mlp_step_update(
+            self._handle, ptr(params), ptr(bucket), ptr(m), ptr(v), ptr(state), int(parity),
+            ptr(sched) if sched is not None else None, sched.shape[0] if sched is not None else 0,
+            float(lr), float(beta1), float(beta2), float(eps), ptr(history) if history is not None else None,
+            cap, stream_ptr(params.device)), "hbk_mlp_step_update")
+
     def gate_adam(self, params, bucket, m, v, state, ctrl, history, lr, beta1=0.9, beta2=0.999,
                   eps=1e-8) -> None:
         cap = 0 if history is None else history.shape[0]
@@ -381,6 +472,50 @@ class MlpPlan:
                                       ptr(ctrl), ptr(history) if history is not None else None, cap,
                                       float(lr), float(beta1), float(beta2), float(eps),
                                       stream_ptr(params.device)), "hbk_mlp_gate_adam")
+
+
+@torch.library.custom_op("hbk::place_clips", mutates_args=())
+def _place_clips_op(src: torch.Tensor, src_len: torch.Tensor, pre: torch.Tensor, T: int) -> torch.Tensor:
+    n = src.shape[0]
+    out = torch.empty((n, T), dtype=torch.float32, device=src.device)
+    for s in range(0, n, 65535):  # grid.y limit of one launch
+        m = min(65535, n - s)
+        check(lib().hbk_place_clips(ptr(src) + 4 * s * src.stride(0), m, src.stride(0),
+                                    ptr(src_len) + 4 * s, ptr(pre) + 4 * s, ptr(out) + 4 * s * T, T, T,
+                                    stream_ptr(src.device)), "hbk_place_clips")
+    return out
+
+
+@_place_clips_op.register_fake
+def _(src, src_len, pre, T):
+    return src.new_empty((src.shape[0], T))
+
+
+def place_clips(src: torch.Tensor, src_len, pre, T: int = 23040) -> torch.Tensor:
+    """AugmentedAudioGenerator.to_target_length on the device (hbk_place_clips):
+    src [n, S] f32 rows holding src_len[i] valid samples -> [n, T] with clip i
+    shifted right by pre[i] zeros and cut at T."""
+    dev = _native.require_device(src.device)
+    if src.dim() != 2 or src.dtype != torch.float32 or src.stride(1) != 1:
+        raise ValueError("src must be [n, S] float32 rows on the device")
+    n = src.shape[0]
+
+    def per_clip(v) -> torch.Tensor:
+        t = torch.as_tensor(v, dtype=torch.int32).reshape(-1).contiguous()
+        if t.numel() != n:
+            raise ValueError("src_len / pre must have n entries")
+        if t.device.type == "cpu":
+            if bool((t < 0).any()):
+                raise ValueError("src_len / pre must be >= 0")
+            return t.pin_memory().to(dev, non_blocking=True)
+        return t.to(dev)
+
+    if torch.is_tensor(src_len) and src_len.device.type != "cpu":
+        src_len = src_len.clamp(0, src.shape[1])  # the kernel reads src[i, :min(len, T)]
+    elif int(np.max(np.asarray(src_len), initial=0)) > src.shape[1]:
+        raise ValueError(f"src_len exceeds the {src.shape[1]} source columns")
+    src_len, pre = per_clip(src_len), per_clip(pre)
+    return torch.ops.hbk.place_clips(src, src_len, pre, int(T))
 
 
 def tanh_distortion(x: torch.Tensor, amount: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:

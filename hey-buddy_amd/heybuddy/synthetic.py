@@ -119,3 +119,68 @@ def phrase_clips(phrase: str, n: int, length: int = CLIP_SAMPLES, seed: int = 0,
         start = start + dur
     x = gain * x + 0.01 * torch.randn((n, length), generator=g, device=device)
     return x.clamp_(-1.0, 1.0)
+
+
+def _syllables(phrase: str):
+    """Pitch (Hz) and duration (s) of the tone "syllables" of a phrase template
+    (fixed by the text: distinct phrases give distinct templates)."""
+    import zlib
+    h = torch.Generator().manual_seed(zlib.crc32(phrase.encode("utf-8")))
+    k = int(torch.randint(4, 8, (1,), generator=h))
+    f0 = torch.rand((k,), generator=h) * 1500.0 + 200.0
+    d0 = torch.rand((k,), generator=h) * 0.08 + 0.06
+    return f0, d0
+
+
+def speech_clips(phrase: str, n: int, seed: int = 0, device: torch.device | str = "cpu",
+                 adversarial: bool = False, num_phrases: int = 250, max_len: int = CLIP_SAMPLES,
+                 chunk: int = 4096):
+    """Stand-in for the Piper TTS generator (PiperSpeechGenerator, dataset/piper.py,
+    out of scope offline): variable-length utterances as the reference's
+    to_target_length receives them. Returns (clips [n, max_len] f32 with clip i
+    valid in [0, lengths[i]) and zero after, lengths int32 numpy [n]).
+
+    Positive clips render the phrase's template; adversarial clips render one
+    of ``num_phrases`` other templates ("phrase#k"), per clip, with the same
+    random tempo (0.85-1.15x), pitch shift (+-5 %), gain, 20-80 ms margins and
+    0.01 N(0, 1) noise inside the utterance."""
+    device = torch.device(device)
+    g = torch.Generator(device=device).manual_seed(seed)
+    gh = torch.Generator().manual_seed(seed + 1)
+    names = [phrase] if not adversarial else [f"{phrase}#adv{k}" for k in range(num_phrases)]
+    temps = [_syllables(s) for s in names]
+    kmax = max(int(f.shape[0]) for f, _ in temps)
+    F = torch.zeros((len(names), kmax))
+    D = torch.zeros((len(names), kmax))
+    for i, (f, d) in enumerate(temps):
+        F[i, :f.shape[0]] = f
+        D[i, :d.shape[0]] = d
+    which = torch.randint(0, len(names), (n,), generator=gh)
+    F, D = F[which].to(device), D[which].to(device)
+    out = torch.zeros((n, max_len), dtype=torch.float32, device=device)
+    lengths = torch.empty(n, dtype=torch.int32, device=device)
+    t = torch.arange(max_len, device=device, dtype=torch.float32) / SAMPLE_RATE
+    for s in range(0, n, chunk):
+        b = min(chunk, n - s)
+        f_all, d_all = F[s:s + b], D[s:s + b]
+        tempo = torch.rand((b, 1), generator=g, device=device) * 0.3 + 0.85
+        shift = torch.rand((b, 1), generator=g, device=device) * 0.1 + 0.95
+        gain = torch.rand((b, 1), generator=g, device=device) * 0.3 + 0.2
+        lead = torch.rand((b, 1), generator=g, device=device) * 0.06 + 0.02
+        tail = torch.rand((b, 1), generator=g, device=device) * 0.06 + 0.02
+        x = torch.zeros((b, max_len), device=device)
+        start = lead.clone()
+        for j in range(kmax):
+            dur = d_all[:, j:j + 1] * tempo
+            u = (t[None, :] - start) / dur.clamp_min(1e-6)
+            on = (u >= 0) & (u <= 1) & (dur > 0)
+            env = torch.where(on, 0.5 - 0.5 * torch.cos(2 * math.pi * u.clamp(0, 1)), torch.zeros_like(u))
+            f = f_all[:, j:j + 1] * shift
+            x += env * (torch.sin(2 * math.pi * f * t[None, :]) + 0.5 * torch.sin(4 * math.pi * f * t[None, :]))
+            start = start + dur
+        length = ((start + tail) * SAMPLE_RATE).floor().clamp(1, max_len)
+        inside = torch.arange(max_len, device=device)[None, :] < length
+        x = gain * x + 0.01 * torch.randn((b, max_len), generator=g, device=device)
+        out[s:s + b] = torch.where(inside, x.clamp_(-1.0, 1.0), torch.zeros_like(x))
+        lengths[s:s + b] = length[:, 0].to(torch.int32)
+    return out, lengths.cpu().numpy()

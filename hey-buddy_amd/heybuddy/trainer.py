@@ -78,20 +78,51 @@ class Trainer(nn.Module):
         dev = flat.device
         self._m = torch.zeros_like(flat)
         self._v = torch.zeros_like(flat)
+        # generic path (hbk_mlp_gate_adam): [acc_samples, acc_steps, adam t, step]
         self._state = torch.tensor([0.0, 1.0, 0.0, 0.0], dtype=torch.float32, device=dev)
         self._ctrl = torch.zeros(4, dtype=torch.float32, device=dev)
+        # fused path (hbk_mlp_step_*): ping-ponged [2][8] state, `_parity` = half of the next step
+        self._fstate = torch.tensor([0.0, 1.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0] * 2, dtype=torch.float32, device=dev)
+        self._parity = 0
         self._bucket = torch.zeros(flat.numel() + self.model.plan.N_STATS, dtype=torch.float32, device=dev)
+        self._graphs = {}
 
     def _apply(self, fn, recurse=True):
         super()._apply(fn, recurse)
         if hasattr(self, "_m"):
             self._m, self._v = fn(self._m), fn(self._v)
             self._state, self._ctrl, self._bucket = fn(self._state), fn(self._ctrl), fn(self._bucket)
+            self._fstate = fn(self._fstate)
+            self._graphs = {}
         return self
 
     @property
     def device(self) -> torch.device:
         return self.model.device
+
+    @property
+    def _fused(self) -> bool:
+        return self.model.plan.fused and self.device.type == "cuda"
+
+    def _adam_t(self) -> float:
+        if self._fused:
+            return float(self._fstate[8 * self._parity + 2].item())
+        return float(self._state[2].item())
+
+    def _reset_accumulation(self, salt: int = 0) -> None:
+        """Start of an epoch (trainer.py:377-378): accumulated samples 0,
+        accumulation steps 1, step index 0; the Adam step count is kept.
+        Device-side only (no host sync)."""
+        st = self._fstate.view(2, 8)
+        st[1 - self._parity].copy_(st[self._parity])
+        st[:, 0] = 0.0
+        st[:, 1] = 1.0
+        st[:, 3] = 0.0
+        st[:, 4] = float(salt % (1 << 24))
+        self._parity = 0
+        self._state[0] = 0.0
+        self._state[1] = 1.0
+        self._state[3] = 0.0
 
     def get_learning_rate(self, step: int, warmup_steps: int = 0, hold_steps: int = 0, total_steps: int = 0,
                           start_learning_rate: float = 0.0,
@@ -107,7 +138,7 @@ class Trainer(nn.Module):
     # -- checkpoints (trainer.py:186-198, resume :54-118) ----------------------
     def _sync_torch_optimizer(self) -> None:
         """Expose the kernels' Adam state through torch.optim.Adam's state_dict."""
-        t = int(self._state[2].item())
+        t = int(self._adam_t())
         views_m = self.model.plan.views(self._m)
         views_v = self.model.plan.views(self._v)
         for name, p in self.model.named_parameters():
@@ -144,6 +175,8 @@ class Trainer(nn.Module):
             vv[n].copy_(st["exp_avg_sq"].to(vv[n].device))
             t = float(st["step"])
         self._state.copy_(torch.tensor([0.0, 1.0, t, 0.0]))
+        self._fstate.copy_(torch.tensor([0.0, 1.0, t, 0.0, 0.0, 0.0, 0.0, 0.0] * 2))
+        self._parity = 0
 
     def __call__(self, training: Any, **kwargs: Any) -> None:
         raise NotImplementedError()
@@ -200,7 +233,22 @@ class WakeWordTrainer(Trainer):
         y = y.to(dev, non_blocking=True)
         plan = self.model.plan
         p = self.model.dropout.p if self.model.training else 0.0
-        if dev.type == "cuda" and os.environ.get("HBK_MLP_GRAPHS", "1") != "0":
+        graphs = dev.type == "cuda" and os.environ.get("HBK_MLP_GRAPHS", "1") != "0"
+        if self._fused:
+            if graphs:
+                self._fused_graph_step(x, y, lr, neg_weight, threshold, activation_threshold, history, p, world)
+            else:
+                xs = x.reshape(x.shape[0], -1).to(torch.float32).contiguous()
+                ys = y.to(torch.float32).contiguous()
+                plan.step_fwd_bwd(self.model.flat_parameters, self._bucket, self._fstate, self._parity, ys,
+                                  xs.shape[0], pool32=xs, neg_weight=neg_weight, threshold=threshold,
+                                  activation_threshold=activation_threshold, dropout_p=p, seed=self._seed_base)
+                distributed.reduce_bucket(self._bucket)
+                plan.step_update(self.model.flat_parameters, self._bucket, self._m, self._v, self._fstate,
+                                 self._parity, lr=lr, beta1=BETAS[0], beta2=BETAS[1], eps=EPS, history=history)
+            self._parity ^= 1
+            return
+        if graphs:
             self._graph_step(x, y, lr, neg_weight, threshold, activation_threshold, history,
                              seed * 1000003 + rank, p, world)
             return
@@ -210,6 +258,139 @@ class WakeWordTrainer(Trainer):
         distributed.reduce_bucket(self._bucket)
         plan.gate_adam(self.model.flat_parameters, self._bucket, self._m, self._v, self._state, self._ctrl,
                        history, lr, BETAS[0], BETAS[1], EPS)
+
+    @property
+    def _seed_base(self) -> int:
+        """Dropout stream of the fused path: fixed per trainer; every step adds
+        its index and every epoch its salt (state[4]) on the device."""
+        if not hasattr(self, "_seed_base_v"):
+            self._seed_base_v = random.getrandbits(40)
+        return self._seed_base_v
+
+    def _fused_graph_step(self, x: torch.Tensor, y: torch.Tensor, lr: float, neg_weight: float,
+                          threshold: float, activation_threshold: float, history: Optional[torch.Tensor],
+                          p: float, world: int) -> None:
+        """One fused step as captured hipGraphs, one set per (batch size, parity,
+        thresholds, dropout p, history buffer). Each graph owns its staging rows,
+        its (lr, neg_weight) cell and its workspace, so no later allocation can
+        move memory a graph replays into. world == 1: one graph per step;
+        data-parallel: forward/backward graph, all-reduce, update graph."""
+        dev = self.device
+        plan = self.model.plan
+        flat = self.model.flat_parameters
+        B = int(x.shape[0])
+        key = (B, self._parity, float(threshold), float(activation_threshold), float(p), world,
+               None if history is None else (history.data_ptr(), history.shape[0]))
+        g = self._graphs.get(key)
+        if g is None:
+            sx = torch.zeros((B, plan.d_in), dtype=torch.float32, device=dev)
+            sy = torch.zeros(B, dtype=torch.float32, device=dev)
+            sched = torch.zeros((1, 2), dtype=torch.float32, device=dev)
+            ws = torch.empty(plan.workspace_bytes(B), dtype=torch.uint8, device=dev)
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            parity = self._parity
+
+            def fwd():
+                plan.step_fwd_bwd(flat, self._bucket, self._fstate, parity, sy, B, pool32=sx, sched=sched,
+                                  threshold=threshold, activation_threshold=activation_threshold, dropout_p=p,
+                                  seed=self._seed_base, workspace=ws)
+
+            def upd():
+                plan.step_update(flat, self._bucket, self._m, self._v, self._fstate, parity, sched=sched,
+                                 beta1=BETAS[0], beta2=BETAS[1], eps=EPS, history=history)
+
+            graphs = []
+            with torch.cuda.stream(side):
+                if world == 1:
+                    gr = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(gr, stream=side):
+                        fwd()
+                        upd()
+                    graphs.append(gr)
+                else:
+                    for fn in (fwd, upd):
+                        gr = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(gr, stream=side):
+                            fn()
+                        graphs.append(gr)
+            torch.cuda.current_stream(dev).wait_stream(side)
+            g = self._graphs[key] = {"x": sx, "y": sy, "sched": sched, "ws": ws, "graphs": graphs}
+        g["x"].copy_(x.reshape(B, -1), non_blocking=True)
+        g["y"].copy_(y, non_blocking=True)
+        g["sched"][0, 0].fill_(float(lr))
+        g["sched"][0, 1].fill_(float(neg_weight))
+        if len(g["graphs"]) == 1:
+            g["graphs"][0].replay()
+        else:
+            g["graphs"][0].replay()
+            distributed.reduce_bucket(self._bucket)
+            g["graphs"][1].replay()
+
+    def train_indexed(self, idx: torch.Tensor, y: torch.Tensor, sched: torch.Tensor,
+                      pool32: Optional[torch.Tensor] = None, pool16: Optional[torch.Tensor] = None,
+                      threshold: float = DEFAULT_HIGH_LOSS_THRESHOLD,
+                      activation_threshold: float = DEFAULT_ACTIVATION_THRESHOLD,
+                      history: Optional[torch.Tensor] = None, steps_per_graph: int = 16,
+                      graphs: bool = True) -> None:
+        """S fused optimisation steps whose batches are rows of HBM-resident
+        embedding pools (the device-side sampler's output): step s trains on
+        rows idx[s] (int32 [S, B]; >= 0 -> pool32 f32 [n, 16, 96], < 0 ->
+        pool16 f16 row -i-1) with labels y (f32 [B], the same composition every
+        step, or [S, B]) at sched[s] = (lr, neg_weight). The step index lives on
+        the device, so a hipGraph of ``steps_per_graph`` steps replays the whole
+        run; continues from the current state (call _reset_accumulation() to
+        start an epoch). Data-parallel: every rank passes its own rows; one
+        all-reduce of the bucket per step."""
+        if not self._fused:
+            raise NotImplementedError("train_indexed needs the fused train step (default architecture)")
+        dev = self.device
+        plan = self.model.plan
+        flat = self.model.flat_parameters
+        S, B = int(idx.shape[0]), int(idx.shape[1])
+        y_stride = B if y.dim() == 2 else 0
+        p = self.model.dropout.p if self.model.training else 0.0
+        p32 = None if pool32 is None else pool32.reshape(pool32.shape[0], -1)
+        p16 = None if pool16 is None else pool16.reshape(pool16.shape[0], -1)
+        _, world = self._world()
+        ws = self._indexed_ws = getattr(self, "_indexed_ws", None)
+        need = plan.workspace_bytes(B)
+        if ws is None or ws.numel() < need or ws.device != dev:
+            ws = self._indexed_ws = torch.empty(need, dtype=torch.uint8, device=dev)
+
+        def one(parity: int) -> None:
+            plan.step_fwd_bwd(flat, self._bucket, self._fstate, parity, y, B, pool32=p32, pool16=p16, idx=idx,
+                              idx_stride=B, y_stride=y_stride, sched=sched, threshold=threshold,
+                              activation_threshold=activation_threshold, dropout_p=p, seed=self._seed_base,
+                              workspace=ws)
+            distributed.reduce_bucket(self._bucket)
+            plan.step_update(flat, self._bucket, self._m, self._v, self._fstate, parity, sched=sched,
+                             beta1=BETAS[0], beta2=BETAS[1], eps=EPS, history=history)
+
+        done = 0
+        k = max(2, steps_per_graph - steps_per_graph % 2)
+        if graphs and world == 1 and S >= k:
+            key = ("indexed", k, self._parity, B, y_stride, float(threshold), float(activation_threshold), float(p),
+                   tuple(t.data_ptr() if t is not None else 0 for t in (idx, y, sched, p32, p16, history)))
+            gr = self._graphs.get(key)
+            if gr is None:
+                side = torch.cuda.Stream(dev)
+                side.wait_stream(torch.cuda.current_stream(dev))
+                gr = torch.cuda.CUDAGraph()
+                par0 = self._parity
+                with torch.cuda.stream(side):
+                    with torch.cuda.graph(gr, stream=side):
+                        for j in range(k):
+                            one(par0 ^ (j & 1))
+                torch.cuda.current_stream(dev).wait_stream(side)
+                self._graphs[key] = gr
+            while S - done >= k:
+                gr.replay()
+                done += k
+        while done < S:
+            one(self._parity)
+            self._parity ^= 1
+            done += 1
 
     def _graph_step(self, x: torch.Tensor, y: torch.Tensor, lr: float, neg_weight: float, threshold: float,
                     activation_threshold: float, history: Optional[torch.Tensor], seed: int, p: float,
@@ -227,7 +408,7 @@ class WakeWordTrainer(Trainer):
         key = (B, float(threshold), float(activation_threshold), float(p), world,
                tuple(t.data_ptr() for t in (flat, self._m, self._v, self._state, self._ctrl, self._bucket)),
                None if history is None else (history.data_ptr(), history.shape[0]))
-        graphs = self.__dict__.setdefault("_graphs", {})
+        graphs = self._graphs
         g = graphs.get(key)
         if g is None:
             if getattr(self, "_scalars", None) is None or self._scalars.device != dev:
@@ -289,8 +470,13 @@ class WakeWordTrainer(Trainer):
         """One epoch (trainer.py:314-608). Returns the reference's 11 histories."""
         if use_wandb:
             logger.warning("wandb logging is outside the MI355X hot path; ignored")
-        self._state.copy_(torch.tensor([0.0, 1.0, float(self._state[2].item()), 0.0]))
-        history = torch.zeros((num_steps, 8), dtype=torch.float32, device=self.device)
+        self._reset_accumulation(salt=random.getrandbits(24))
+        cap = getattr(self, "_history", None)
+        if cap is None or cap.shape[0] < num_steps or cap.device != self.device:
+            self._history = torch.zeros((max(num_steps, 1), 8), dtype=torch.float32, device=self.device)
+            self._graphs = {k: v for k, v in self._graphs.items() if k[0] == "indexed"}
+        history = self._history
+        history.zero_()
         lr_hist: List[float] = []
         nw_hist: List[float] = []
         batch_sizes: List[int] = []
@@ -323,7 +509,9 @@ class WakeWordTrainer(Trainer):
                     preds, labels = self._predict_all(validation)
                     n_neg = int((labels == 0).sum().item())
                     hours = n_neg * 1.44 / 3600
-                    fph = float(self.num_false_positives(preds, labels, activation_threshold).item()) / hours
+                    n_fp = float(self.num_false_positives(preds, labels, activation_threshold).item())
+                    # torch tensor division in the reference (trainer.py:511): x / 0 -> inf (nan for 0 / 0)
+                    fph = n_fp / hours if hours > 0 else (float("inf") if n_fp > 0 else float("nan"))
                     v_fp.append(fph)
                     pos = labels == 1
                     v_rec.append(_recall(float((preds[pos] > activation_threshold).sum().item()),

@@ -189,6 +189,43 @@ int hbk_mlp_gate_adam(const hbk_mlp_plan* plan, float* params, const float* buck
                       float* v, float* state, float* ctrl, float* history, int32_t history_cap,
                       float lr, float beta1, float beta2, float eps, void* stream);
 
+/* Fused train step (default architecture: d_in 1536, layer_dim 96, hidden 64,
+ * at most 4 layers; *supported = 0 for other plans, which keep the generic
+ * entry points above). Four launches per step, no host synchronisation:
+ * hbk_mlp_step_fwd_bwd (input gather + LayerNorm + input GEMM, the 16-row
+ * chain forward/filter/BCE/backward, the weight gradients) and
+ * hbk_mlp_step_update (gate + Adam + bucket zeroing), with the data-parallel
+ * all-reduce of the bucket between them.
+ *
+ * Rows: row r of the step's batch is pool32 row idx[r] (idx[r] >= 0, f32
+ *   [n32, 1536]) or pool16 row -idx[r] - 1 (f16 [n16, 1536]); an index outside
+ *   its pool reads as a zero row. idx == NULL: row r = pool32 row r. The step's
+ *   idx is idx + step * idx_step_stride, its labels y + step * y_step_stride
+ *   (0/1 f32), where step = state[8 * parity + 3].
+ * state: device float[16], two halves of [accumulated_samples,
+ *   accumulation_steps (init 1), adam step t, step index, dropout salt, 0, 0, 0].
+ *   A step reads half `parity` and hbk_mlp_step_update writes half 1 - parity
+ *   (step + 1): successive steps alternate parity, and a hipGraph of an even
+ *   number of steps replays a whole stage.
+ * sched (optional, device f32 [sched_len][2]): (lr, neg_weight) of step s at
+ *   row min(s, sched_len - 1), in place of the lr / neg_weight arguments.
+ * bucket [n_params + 8]: must be zero before the first step (hbk_mlp_step_update
+ *   zeroes it for the next one); receives the unnormalised gradients and the
+ *   statistics of hbk_mlp_train_fwd_bwd. history as in hbk_mlp_gate_adam.
+ * The dropout mask of element i of step s is f(seed + s + (salt << 24), i). */
+int hbk_mlp_fused_supported(const hbk_mlp_plan* plan, int32_t* supported);
+int hbk_mlp_step_fwd_bwd(const hbk_mlp_plan* plan, const float* params, const float* pool32, int64_t n32,
+                         const void* pool16, int64_t n16, const int32_t* idx, int64_t idx_step_stride,
+                         const float* y, int64_t y_step_stride, int64_t batch, const float* state,
+                         int32_t parity, const float* sched, int64_t sched_len, float neg_weight,
+                         float high_loss_threshold, float activation_threshold, float dropout_p,
+                         uint64_t seed, float* bucket, float* prob, void* workspace,
+                         int64_t workspace_bytes, void* stream);
+int hbk_mlp_step_update(const hbk_mlp_plan* plan, float* params, float* bucket, float* m, float* v,
+                        float* state, int32_t parity, const float* sched, int64_t sched_len, float lr,
+                        float beta1, float beta2, float eps, float* history, int32_t history_cap,
+                        void* stream);
+
 /* Graph-captured training steps: dev_scalars (device, double[3] = lr,
  * neg_weight, dropout seed; NULL = off) is read by the kernels of
  * hbk_mlp_train_fwd_bwd and hbk_mlp_gate_adam in place of their lr,
@@ -259,6 +296,18 @@ int hbk_colored_noise(const hbk_reverb_plan* plan, const float* x, int64_t n_cli
  * out may equal x. Device pointers. */
 int hbk_tanh_distortion(const float* x, int64_t n_clips, int64_t x_stride, const float* amount, float* out,
                         int64_t out_stride, void* stream);
+
+/* Clip placement: AugmentedAudioGenerator.to_target_length
+ * (dataset/augmented.py:200-232) for a batch already on the device. Per clip i
+ * of src [n_clips, src_stride] holding src_len[i] valid samples:
+ *   out[i, t] = src[i, t - pre[i]] for pre[i] <= t < pre[i] + min(src_len[i], T),
+ *   out[i, t] = 0 elsewhere, t < T.
+ * The reference crops (pre = 0) when src_len >= T, else pads with
+ * pre = np.random.randint(int(S/4), int(3S/4)) leading zeros, S = T - src_len
+ * (pre = 0 when S == 1); the caller draws pre on the host with that rule.
+ * T % 4 == 0, out rows 16-B aligned, n_clips <= 65535 per call. */
+int hbk_place_clips(const float* src, int64_t n_clips, int64_t src_stride, const int32_t* src_len,
+                    const int32_t* pre, float* out, int64_t out_stride, int64_t T, void* stream);
 
 #ifdef __cplusplus
 }

@@ -105,3 +105,36 @@ def _torch_layers(graph):
         else:
             layers.append(("pool", (op.ph, op.pw), None))
     return layers
+
+
+def _mel_batch(x: np.ndarray) -> np.ndarray:
+    """fp32 mel graph of a batch of 17,280-sample windows -> [b, 105, 32]
+    (the ONNX mel graph's work, spectrogram.py:23-32, with the H0 parameters)."""
+    x = np.asarray(x, dtype=np.float32) * np.float32(32767.0)
+    nf = (x.shape[1] - 512) // 160 + 1
+    idx = np.arange(nf)[:, None] * 160 + np.arange(512)[None, :]
+    fr = x[:, idx] * omel.hann_window().astype(np.float32)
+    spec = np.fft.rfft(fr, axis=-1)
+    p = (spec.real ** 2 + spec.imag ** 2).astype(np.float32)
+    mel = p @ omel.mel_fbank().astype(np.float32)
+    return 10.0 * np.log10(np.maximum(mel, 1e-10)) / 10.0 + 2.0
+
+
+def cpu_mel_windows(audio: np.ndarray, batch: int = 64, threads: int = 1) -> np.ndarray:
+    """configs[0]'s CPU path: SpeechEmbeddings.audio_to_spectrograms' cost
+    structure (embeddings.py:56-84, :190): every clip's 4 audio windows of
+    17,280 samples (stride 1,920) through the mel graph in batches of ``batch``
+    windows (the CPU autoconfigure, features.py:203-208) -> [n, 420, 32].
+    ``threads`` workers take whole batches (numpy's FFT releases the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+    audio = np.asarray(audio, dtype=np.float32)
+    n = audio.shape[0]
+    wins = np.stack([audio[:, s:s + 17280] for s in range(0, 5761, 1920)], axis=1).reshape(n * 4, 17280)
+    chunks = [wins[i:i + batch] for i in range(0, wins.shape[0], batch)]
+    if threads > 1:
+        from threadpoolctl import threadpool_limits
+        with threadpool_limits(limits=1), ThreadPoolExecutor(threads) as ex:
+            outs = list(ex.map(_mel_batch, chunks))
+    else:
+        outs = [_mel_batch(c) for c in chunks]
+    return np.concatenate(outs).reshape(n, 4 * 105, 32)

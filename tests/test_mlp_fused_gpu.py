@@ -1,0 +1,155 @@
+"""The fused classifier train step (hbk_mlp_step_*, hbk_mlp_fused.hip) on the
+GPU: against the reference's own outputs (tests/golden/classifier.npz), against
+the generic GEMM path at the stage batch sizes 1100 / 550 / 273 (and ragged
+ones), and the index-gathered multi-step graph (train_indexed) against eager
+steps.
+
+Tolerances: gradients 1e-4 of each tensor's max |g| (f32, summation order
+and float-atomic order differ from torch's); loss 1e-5 relative.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import golden_classifier as gc
+
+pytestmark = pytest.mark.gpu
+
+GOLD = "tests/golden/classifier.npz"
+
+
+def _model(params):
+    from heybuddy.wakeword import WakeWordMLPModel
+    m = WakeWordMLPModel()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=True)
+    m.dropout.p = 0.0
+    return m.cuda()
+
+
+def _fused_grads(model, x, y, neg_weight=2.0):
+    plan = model.plan
+    flat = model.flat_parameters
+    bucket = torch.zeros(plan.n_params + plan.N_STATS, device="cuda")
+    state = plan.new_state("cuda")
+    xs = torch.as_tensor(x).cuda().reshape(len(x), -1).contiguous()
+    ys = torch.as_tensor(y).cuda().to(torch.float32)
+    prob = torch.zeros(len(x), device="cuda")
+    plan.step_fwd_bwd(flat, bucket, state, 0, ys, len(x), pool32=xs, neg_weight=neg_weight, prob=prob)
+    return bucket, prob
+
+
+def test_fused_supported():
+    from heybuddy.kernels import MlpPlan
+    assert MlpPlan().fused
+    assert not MlpPlan(layer_dim=64, hidden=48).fused
+
+
+def test_fused_grads_match_reference():
+    params, x, y, _ = gc.golden_inputs()
+    gold = np.load(GOLD)
+    m = _model(params)
+    bucket, prob = _fused_grads(m, x, y)
+    plan = m.plan
+    stats = bucket[plan.n_params:].cpu().numpy()
+    n_sel = int(gold["n_sel"])
+    assert int(stats[0]) == n_sel
+    np.testing.assert_allclose(stats[1] / n_sel, float(gold["loss"]), rtol=1e-5)
+    np.testing.assert_allclose(prob.cpu().numpy(), gold["prob"], rtol=1e-4, atol=1e-6)
+    g = plan.views(bucket[:plan.n_params] / n_sel)
+    for k in params:
+        ref = gold[f"grad/{k}"]
+        scale = np.abs(ref).max() + 1e-12
+        np.testing.assert_allclose(g[k].cpu().numpy() / scale, ref / scale, rtol=0, atol=1e-4, err_msg=k)
+
+
+@pytest.mark.parametrize("B", [1100, 550, 273, 17, 1])
+def test_fused_matches_generic_path(B):
+    """Same step through the generic kernels (hbk_mlp_train_fwd_bwd) and the
+    fused ones, at the reference's stage batch sizes and ragged tails."""
+    params = gc.golden_inputs()[0]
+    m = _model(params)
+    rng = np.random.default_rng(B)
+    y = (rng.random(B) < 0.1).astype(np.int64)
+    x = (rng.standard_normal((B, 16, 96)) + np.where(y[:, None, None] == 1, 0.8, -0.2)).astype(np.float32)
+    fused, _ = _fused_grads(m, x, y, neg_weight=1.5)
+    plan = m.plan
+    ref = torch.zeros_like(fused)
+    plan.train_fwd_bwd(m.flat_parameters, torch.from_numpy(x).cuda().reshape(B, -1), torch.from_numpy(y), ref,
+                       neg_weight=1.5)
+    fs, rs = fused[plan.n_params:].cpu().numpy(), ref[plan.n_params:].cpu().numpy()
+    np.testing.assert_array_equal(fs[[0, 2, 3, 4, 5, 6]], rs[[0, 2, 3, 4, 5, 6]])
+    np.testing.assert_allclose(fs[1], rs[1], rtol=1e-5)
+    gf, gr = plan.views(fused[:plan.n_params]), plan.views(ref[:plan.n_params])
+    for k in gf:
+        a, b = gf[k].cpu().numpy(), gr[k].cpu().numpy()
+        scale = np.abs(b).max() + 1e-12
+        np.testing.assert_allclose(a / scale, b / scale, rtol=0, atol=1e-4, err_msg=k)
+
+
+def test_fused_update_matches_gate_adam():
+    """hbk_mlp_step_update = hbk_mlp_gate_adam on the same bucket, and it
+    zeroes the bucket and advances the ping-pong state."""
+    params, x, y, _ = gc.golden_inputs()
+    m = _model(params)
+    plan = m.plan
+    bucket, _ = _fused_grads(m, x, y)
+    b2 = bucket.clone()
+    p0 = m.flat_parameters.clone()
+    mm, vv = torch.zeros_like(p0), torch.zeros_like(p0)
+    state = plan.new_state("cuda")
+    state[0] = 128.0  # earlier samples accumulated: the gate fires
+    hist = torch.zeros((4, 8), device="cuda")
+    plan.step_update(m.flat_parameters, bucket, mm, vv, state, 0, lr=1e-3, history=hist)
+    new = m.flat_parameters.clone()
+    # reference: the generic single-thread gate + Adam
+    m.flat_parameters.copy_(p0)
+    st2 = torch.tensor([128.0, 1.0, 0.0, 0.0], device="cuda")
+    ctrl = torch.zeros(4, device="cuda")
+    hist2 = torch.zeros((4, 8), device="cuda")
+    plan.gate_adam(m.flat_parameters, b2, torch.zeros_like(p0), torch.zeros_like(p0), st2, ctrl, hist2, 1e-3)
+    torch.testing.assert_close(new, m.flat_parameters, rtol=0, atol=0)
+    torch.testing.assert_close(hist[0], hist2[0])
+    assert float(bucket[:plan.n_params].abs().max()) == 0.0
+    s = state.cpu().numpy()
+    assert s[8 + 3] == 1.0 and s[8 + 2] == 1.0 and s[8 + 0] == 0.0 and s[8 + 1] == 1.0
+
+
+def test_train_indexed_equals_eager_steps(tmp_path):
+    """12 steps gathered by index from an f32 positive pool and an f16
+    negative pool, as one 4-step graph replayed 3 times, against the same
+    batches stepped eagerly from host tensors."""
+    from heybuddy.trainer import WakeWordTrainer
+    params = gc.golden_inputs()[0]
+    rng = np.random.default_rng(5)
+    S, npos, nneg = 12, 20, 80
+    pos = torch.from_numpy(rng.standard_normal((300, 16, 96)).astype(np.float32) + 0.7)
+    neg = torch.from_numpy(rng.standard_normal((500, 16, 96)).astype(np.float32)).half()
+    ip = np.stack([rng.choice(300, npos, replace=False) for _ in range(S)])
+    ineg = np.stack([rng.choice(500, nneg, replace=False) for _ in range(S)])
+    idx = np.concatenate([ip, -ineg - 1], axis=1).astype(np.int32)
+    y = np.concatenate([np.ones(npos), np.zeros(nneg)]).astype(np.float32)
+    lr = np.linspace(1e-4, 1e-3, S).astype(np.float32)
+    nw = np.tile([1.0, 2.0, 0.5], S // 3).astype(np.float32)
+    runs = []
+    for mode in ("indexed", "eager"):
+        tr = WakeWordTrainer(checkpoint_dir=str(tmp_path / mode), device="cuda")
+        tr.model.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=True)
+        tr.model.dropout.p = 0.0
+        tr._reset_accumulation()
+        hist = torch.zeros((S, 8), device="cuda")
+        if mode == "indexed":
+            sched = torch.from_numpy(np.stack([lr, nw], 1)).cuda()
+            tr.train_indexed(torch.from_numpy(idx).cuda(), torch.from_numpy(y).cuda(), sched, pool32=pos.cuda(),
+                             pool16=neg.cuda(), history=hist, steps_per_graph=4)
+        else:
+            for s in range(S):
+                x = torch.cat([pos[ip[s]], neg[ineg[s]].float()])
+                tr._step(x, torch.from_numpy(y).long(), float(lr[s]), float(nw[s]), 1e-4, 0.5, hist, s)
+        torch.cuda.synchronize()
+        runs.append((tr.model.flat_parameters.clone(), hist.clone(), tr._fstate.clone()))
+    (p1, h1, s1), (p0, h0, s0) = runs
+    np.testing.assert_allclose(h1[:, [0, 2, 4, 5, 6, 7]].cpu().numpy(), h0[:, [0, 2, 4, 5, 6, 7]].cpu().numpy())
+    np.testing.assert_allclose(h1[:, 3].cpu().numpy(), h0[:, 3].cpu().numpy(), rtol=1e-4)
+    d = (p1 - p0).abs()
+    assert float((d > 1e-5).float().mean()) < 1e-3 and float(d.max()) <= 2e-2
+    torch.testing.assert_close(s1, s0)
