@@ -62,12 +62,53 @@ constexpr int kChunkMax = 384;    // k1 K-chunk
 __device__ __forceinline__ f4 mma(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
-__device__ __forceinline__ float wsum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+// wave sum through DPP: quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror,
+// row_mirror leave each 16-lane row's sum in all of its lanes (rsum16); the
+// four rows are then added from readlane (a bpermute-based __shfl_xor chain
+// costs an LDS round trip per step)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float rsum16(float v) {
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x141>(v);
+  v += dpp_f<0x140>(v);
   return v;
 }
+__device__ __forceinline__ float wsum(float v) {
+  v = rsum16(v);
+  const int b = __builtin_bit_cast(int, v);
+  return (__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 0)) +
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 16))) +
+         (__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 32)) +
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 48)));
+}
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+
+#ifdef HBK_TRACE
+// Tracing build only (lib/libhbk_trace.so, tools/probe_mlp.py): lane 0 of every
+// wave of block 0 records (mark << 56 | s_memtime) at stage marks of k1 / k2 / k3.
+__device__ unsigned long long g_mlp_trace[3][4][128];
+__device__ int g_mlp_trace_n[3][4];
+#define HBK_MT(kern, id)                                                                       \
+  do {                                                                                         \
+    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) {                                          \
+      const int w_ = threadIdx.x >> 6;                                                          \
+      const int n_ = g_mlp_trace_n[kern][w_];                                                   \
+      if (n_ < 128) {                                                                           \
+        g_mlp_trace[kern][w_][n_] = (static_cast<unsigned long long>(id) << 56) |               \
+                                    (__builtin_amdgcn_s_memtime() & 0xFFFFFFFFFFFFFFull);       \
+        g_mlp_trace_n[kern][w_] = n_ + 1;                                                       \
+      }                                                                                         \
+    }                                                                                           \
+  } while (0)
+#else
+#define HBK_MT(kern, id) \
+  do {                   \
+  } while (0)
+#endif
 
 __device__ __forceinline__ int step_of(const float* state, int parity) {
   return state ? static_cast<int>(state[parity * 8 + 3]) : 0;
@@ -88,14 +129,38 @@ struct K1Args {
   float drop_p;
   uint64_t seed;
   float* hg_part;  // [KS][B][128]
-  float* xhat;     // [B][1536]
+  float* xhat;     // TRANSPOSED [1536][Bp] (rows >= B zero)
+  int64_t Bp;
   float* stats;    // bucket tail, zeroed here (k2 accumulates into it); may be NULL
 };
 
+// 32-bit counter hash for the input dropout mask (murmur3's finaliser over
+// the element-pair index mixed with the step's 64-bit seed): one hash gives
+// the 16-bit uniforms of elements 2 i and 2 i + 1 (p resolved to 2^-16).
+__device__ __forceinline__ uint32_t drop_hash(uint32_t s0, uint32_t s1, uint32_t i) {
+  uint32_t h = i * 0x9E3779B1u + s0;
+  h ^= s1;
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+
+// Grid: the KS K-chunks of one 16-row tile run on ONE XCD (blocks b and b + 8
+// share an XCD under round-robin dispatch; speed only, never correctness), so
+// the tile's gathered rows come from that XCD's L2 after the first fetch.
 __global__ void __launch_bounds__(256) k1_input_kernel(K1Args a) {
-  __shared__ __attribute__((aligned(16))) float xn[kR][kChunkMax + 4];
+  __shared__ __attribute__((aligned(16))) float xn[kR][kChunkMax + 4];  // xhat of the chunk
+  __shared__ __attribute__((aligned(16))) float gb[2][kChunkMax];       // norm_in gamma, beta of the chunk
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int rt = blockIdx.x, ks = blockIdx.y;
+  const int KS = kD / a.chunk;
+  const int q = blockIdx.x >> 3;
+  const int ks = q % KS, rt = (q / KS) * 8 + (blockIdx.x & 7);
+  const int n_rt = (a.B + kR - 1) / kR;
+  if (rt >= n_rt) return;
+  HBK_MT(0, 1);
   const int k0 = ks * a.chunk;
   const int step = step_of(a.state, a.parity);
   if (a.stats && rt == 0 && ks == 0 && tid < kStats) a.stats[tid] = 0.f;
@@ -103,86 +168,125 @@ __global__ void __launch_bounds__(256) k1_input_kernel(K1Args a) {
   // per-step dropout stream: base seed + step + the epoch salt (state[4])
   const uint64_t seed = a.seed + static_cast<uint64_t>(step) +
                         (a.state ? static_cast<uint64_t>(a.state[a.parity * 8 + 4]) << 24 : 0);
-  const float* g = a.P + a.g_in;
-  const float* bb = a.P + a.b_in;
+  const uint32_t s0 = static_cast<uint32_t>(seed), s1 = static_cast<uint32_t>(seed >> 32) * 0x27D4EB2Fu;
+  for (int c = tid; c < a.chunk; c += 256) {
+    gb[0][c] = a.P[a.g_in + k0 + c];
+    gb[1][c] = a.P[a.b_in + k0 + c];
+  }
   const float keep = a.drop_p > 0.f ? 1.f / (1.f - a.drop_p) : 1.f;
-  // LayerNorm: wave w normalises rows 4w..4w+3; lane holds elements
-  // c = 4 lane + 256 u + e (u < 6, e < 4)
-  for (int i = 0; i < 4; ++i) {
-    const int rl = wave * 4 + i, r = rt * kR + rl;
-    if (r >= a.B) {
-      for (int c = lane; c < a.chunk; c += 64) xn[rl][c] = 0.f;
-      continue;
-    }
-    const int ix = idx ? idx[r] : r;
-    f4 v[6];
-    if (ix >= 0 ? ix >= a.n32 : -static_cast<int64_t>(ix) - 1 >= a.n16) {
+  // LayerNorm: wave w normalises rows 4w..4w+3 (all four loaded first); lane
+  // holds elements c = 4 lane + 256 u + e (u < 6, e < 4)
+  f4 v[4][6];
 #pragma unroll
-      for (int u = 0; u < 6; ++u) v[u] = f4{0.f, 0.f, 0.f, 0.f};
-    } else if (ix >= 0) {
+  for (int i = 0; i < 4; ++i) {
+    const int r = rt * kR + wave * 4 + i;
+    const int ix = r < a.B ? (idx ? idx[r] : r) : 0;
+    const bool ok = r < a.B && (ix >= 0 ? ix < a.n32 : -static_cast<int64_t>(ix) - 1 < a.n16);
+    if (ok && ix >= 0) {
       const f4* src = reinterpret_cast<const f4*>(a.pool32 + static_cast<int64_t>(ix) * kD);
 #pragma unroll
-      for (int u = 0; u < 6; ++u) v[u] = src[lane + 64 * u];
-    } else {
+      for (int u = 0; u < 6; ++u) v[i][u] = src[lane + 64 * u];
+    } else if (ok) {
       const h4* src = reinterpret_cast<const h4*>(a.pool16 + static_cast<int64_t>(-ix - 1) * kD);
 #pragma unroll
-      for (int u = 0; u < 6; ++u) v[u] = __builtin_convertvector(src[lane + 64 * u], f4);
+      for (int u = 0; u < 6; ++u) v[i][u] = __builtin_convertvector(src[lane + 64 * u], f4);
+    } else {
+#pragma unroll
+      for (int u = 0; u < 6; ++u) v[i][u] = f4{0.f, 0.f, 0.f, 0.f};
     }
+  }
+  // B fragments (W_hg0 rows) of the first 8 K-steps: in flight during the LayerNorm
+  const int m = lane & 15, kq = lane >> 4;
+  const float* w0 = a.P + a.w0 + static_cast<int64_t>(32 * wave + m) * kD + k0 + 4 * kq;
+  const float* w1 = w0 + 16 * kD;
+  const int n16 = a.chunk / 16;
+  f4 rb0[8], rb1[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    if (u < n16) {
+      rb0[u] = *reinterpret_cast<const f4*>(w0 + 16 * u);
+      rb1[u] = *reinterpret_cast<const f4*>(w1 + 16 * u);
+    }
+  }
+  HBK_MT(0, 2);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rl = wave * 4 + i, r = rt * kR + rl;
     if (a.drop_p > 0.f) {  // nn.Dropout on the input (wakeword.py:197, :338)
-      const uint64_t base = static_cast<uint64_t>(r) * kD;
+      const uint32_t base = static_cast<uint32_t>(r) * (kD / 2);
+      const uint32_t thr = static_cast<uint32_t>(a.drop_p * 65536.f + 0.5f);
 #pragma unroll
       for (int u = 0; u < 6; ++u)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const uint64_t c = 4 * lane + 256 * u + e;
-          v[u][e] = uniform01(seed, base + c) < a.drop_p ? 0.f : v[u][e] * keep;
+        for (int e = 0; e < 4; e += 2) {
+          const uint32_t h = drop_hash(s0, s1, base + 2 * lane + 128 * u + e / 2);
+          v[i][u][e] = (h & 0xFFFFu) < thr ? 0.f : v[i][u][e] * keep;
+          v[i][u][e + 1] = (h >> 16) < thr ? 0.f : v[i][u][e + 1] * keep;
         }
     }
-    float s = 0.f;
+    float sm = 0.f;
 #pragma unroll
-    for (int u = 0; u < 6; ++u) s += (v[u][0] + v[u][1]) + (v[u][2] + v[u][3]);
-    const float mu = wsum(s) * (1.f / kD);
-    float q = 0.f;
+    for (int u = 0; u < 6; ++u) sm += (v[i][u][0] + v[i][u][1]) + (v[i][u][2] + v[i][u][3]);
+    const float mu = wsum(sm) * (1.f / kD);
+    float sq = 0.f;
 #pragma unroll
     for (int u = 0; u < 6; ++u)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float d = v[u][e] - mu;
-        q += d * d;
+        const float d = v[i][u][e] - mu;
+        sq += d * d;
       }
-    const float rs = 1.f / sqrtf(wsum(q) * (1.f / kD) + kLnEps);
+    const float rs = 1.f / sqrtf(wsum(sq) * (1.f / kD) + kLnEps);
 #pragma unroll
     for (int u = 0; u < 6; ++u) {
       const int c = 4 * lane + 256 * u;
       if (c >= k0 && c < k0 + a.chunk) {
-        const f4 xh = (v[u] - mu) * rs;
-        *reinterpret_cast<f4*>(a.xhat + static_cast<int64_t>(r) * kD + c) = xh;
-        const f4 gg = *reinterpret_cast<const f4*>(g + c), b4 = *reinterpret_cast<const f4*>(bb + c);
-        *reinterpret_cast<f4*>(&xn[rl][c - k0]) = xh * gg + b4;
+        const f4 xh = r < a.B ? (v[i][u] - mu) * rs : f4{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f4*>(&xn[rl][c - k0]) = xh;
       }
     }
   }
+  HBK_MT(0, 3);
   __syncthreads();
-  // HG0 partial over this K chunk: wave w -> output columns [32 w, 32 w + 32).
-  // MFMA step (i, s) covers k = 16 i + 4 kq + s for lane group kq: A and B
-  // both read float4 runs along k.
-  const int m = lane & 15, kq = lane >> 4;
-  const float* w0 = a.P + a.w0 + static_cast<int64_t>(32 * wave + m) * kD + k0 + 4 * kq;
-  const float* w1 = w0 + 16 * kD;
-  const float* xr = &xn[m][4 * kq];
-  f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-  const int n16 = a.chunk / 16;
-#pragma unroll 4
-  for (int i = 0; i < n16; ++i) {
-    const f4 av = *reinterpret_cast<const f4*>(xr + 16 * i);
-    const f4 b0 = *reinterpret_cast<const f4*>(w0 + 16 * i);
-    const f4 b1 = *reinterpret_cast<const f4*>(w1 + 16 * i);
+  HBK_MT(0, 4);
+  // xhat^T for k3: thread -> one column, the tile's 16 rows as 4 float4 (64 B)
+  if (a.xhat) {
+    for (int c = tid; c < a.chunk; c += 256) {
+      float* dst = a.xhat + static_cast<int64_t>(k0 + c) * a.Bp + rt * kR;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      acc0 = mma(av[s], b0[s], acc0);
-      acc1 = mma(av[s], b1[s], acc1);
+      for (int q4 = 0; q4 < 4; ++q4)
+        *reinterpret_cast<f4*>(dst + 4 * q4) =
+            f4{xn[4 * q4][c], xn[4 * q4 + 1][c], xn[4 * q4 + 2][c], xn[4 * q4 + 3][c]};
     }
   }
+  // HG0 partial over this K chunk: wave w -> output columns [32 w, 32 w + 32).
+  // MFMA step (i, s) covers k = 16 i + 4 kq + s for lane group kq: A and B
+  // both read float4 runs along k. B fragments stream through an 8-step
+  // register ring (the load of step i + 8 is issued when step i is consumed).
+  const float* xr = &xn[m][4 * kq];
+  f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+  for (int i0 = 0; i0 < n16; i0 += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u;
+      if (i < n16) {
+        const f4 gg = *reinterpret_cast<const f4*>(&gb[0][16 * i + 4 * kq]);
+        const f4 be = *reinterpret_cast<const f4*>(&gb[1][16 * i + 4 * kq]);
+        const f4 av = *reinterpret_cast<const f4*>(xr + 16 * i) * gg + be;  // LN output = xhat g + b
+        const f4 b0 = rb0[u], b1 = rb1[u];
+        if (i + 8 < n16) {
+          rb0[u] = *reinterpret_cast<const f4*>(w0 + 16 * (i + 8));
+          rb1[u] = *reinterpret_cast<const f4*>(w1 + 16 * (i + 8));
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          acc0 = mma(av[s], b0[s], acc0);
+          acc1 = mma(av[s], b1[s], acc1);
+        }
+      }
+    }
+  }
+  HBK_MT(0, 5);
   float* out = a.hg_part + static_cast<int64_t>(ks) * a.B * kH2;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -195,40 +299,73 @@ __global__ void __launch_bounds__(256) k1_input_kernel(K1Args a) {
 }
 
 // ------------------------------------------------------------------ k2 ----
-// C[16][N] = A[16][K] (LDS, stride kLd) . op(W) (+ bias), op(W) = W^T for
-// W [N][K] row-major (NT, the forward) or W for W [K][N] (NN, the backward).
-// Waves take 16-column tiles round robin; two accumulation chains per tile.
+// One 16-row tile per workgroup, 4 waves. Every matrix stage is
+// C[16][N] = A[16][K] . op(W) on v_mfma_f32_16x16x4_f32 with A in LDS; wave w
+// owns the 16-column tiles w and w + 4, so a gated MLP's hidden column j and
+// gate column 64 + j land in the same wave and the SiLU gate (forward) and its
+// derivative (backward) run in the GEMM epilogue. The B operands (weights) of
+// the NEXT matrix stage are loaded into registers while the current one runs
+// (one workgroup per CU: the whole 512-VGPR file is available). NT: W [N][K]
+// row-major (forward, y = x W^T); NN: W [K][N] (backward, dx = dy W).
+// MFMA step (i, s) covers k = 16 i + 4 kq + s for lane group kq.
+constexpr int kWRegs = 64;  // 2 tiles x K/4 (K <= 128)
+struct WReg {
+  float v[kWRegs];
+};
+
 template <int K, int N, bool NT>
-__device__ __forceinline__ void rows_gemm(const float* A, const float* __restrict__ W,
-                                          const float* __restrict__ bias, float* C, int wave, int lane) {
+__device__ __forceinline__ void load_w(WReg& w, const float* __restrict__ W, int wave, int lane) {
   constexpr int kTiles = (N + 15) / 16;
   const int m = lane & 15, kq = lane >> 4;
-  for (int t = wave; t < kTiles; t += 4) {
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt) {
+    const int t = wave + 4 * tt;
     const int n = 16 * t + m;
-    const bool nok = n < N;
-    f4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    const bool ok = t < kTiles && n < N;
 #pragma unroll
     for (int i = 0; i < K / 16; ++i) {
-      const f4 av = *reinterpret_cast<const f4*>(A + m * kLd + 16 * i + 4 * kq);
-      f4 bv = {0.f, 0.f, 0.f, 0.f};
-      if (nok) {
-        if (NT) {
-          bv = *reinterpret_cast<const f4*>(W + n * K + 16 * i + 4 * kq);
-        } else {
+      if (NT) {
+        f4 q = {0.f, 0.f, 0.f, 0.f};
+        if (ok) q = *reinterpret_cast<const f4*>(W + n * K + 16 * i + 4 * kq);
 #pragma unroll
-          for (int s = 0; s < 4; ++s) bv[s] = W[(16 * i + 4 * kq + s) * N + n];
-        }
+        for (int s = 0; s < 4; ++s) w.v[tt * (K / 4) + 4 * i + s] = q[s];
+      } else {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) w.v[tt * (K / 4) + 4 * i + s] = ok ? W[(16 * i + 4 * kq + s) * N + n] : 0.f;
       }
-#pragma unroll
-      for (int s = 0; s < 4; ++s) acc[i & 1] = mma(av[s], bv[s], acc[i & 1]);
-    }
-    const f4 r = acc[0] + acc[1];
-    if (nok) {
-      const float b = bias ? bias[n] : 0.f;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) C[(4 * kq + e) * kLd + n] = r[e] + b;
     }
   }
+}
+
+// two tiles (w, w + 4), two interleaved accumulation chains
+template <int K>
+__device__ __forceinline__ void gemm2(const WReg& w, const float* A, int lane, f4& c0, f4& c1) {
+  const int m = lane & 15, kq = lane >> 4;
+  c0 = f4{0.f, 0.f, 0.f, 0.f};
+  c1 = c0;
+#pragma unroll
+  for (int i = 0; i < K / 16; ++i) {
+    const f4 av = *reinterpret_cast<const f4*>(A + m * kLd + 16 * i + 4 * kq);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      c0 = mma(av[s], w.v[4 * i + s], c0);
+      c1 = mma(av[s], w.v[K / 4 + 4 * i + s], c1);
+    }
+  }
+}
+
+// one tile (w), two chains over the even / odd 16-k blocks
+template <int K>
+__device__ __forceinline__ f4 gemm1(const WReg& w, const float* A, int lane) {
+  const int m = lane & 15, kq = lane >> 4;
+  f4 c[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int i = 0; i < K / 16; ++i) {
+    const f4 av = *reinterpret_cast<const f4*>(A + m * kLd + 16 * i + 4 * kq);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) c[i & 1] = mma(av[s], w.v[4 * i + s], c[i & 1]);
+  }
+  return c[0] + c[1];
 }
 
 struct K2Args {
@@ -248,7 +385,9 @@ struct K2Args {
   float* logit;  // [B] or NULL
   float* G;      // gradient bucket (params layout)
   float* stats;  // its statistics tail (8 floats)
-  // activations for k3, [NG][B][width]: U 64, Xn 96 (k >= 1), dS 96 (k = NG-1: column 0), dHG 128
+  // activations for k3, TRANSPOSED [NG][width][Bp] (Bp = B rounded up to 16, pad rows zero):
+  // U 64, Xn 96 (k >= 1), dS 96 (k = NG-1: row 0 = dz), dHG 128
+  int64_t Bp;
   float* U;
   float* Xn;
   float* dS;
@@ -257,80 +396,163 @@ struct K2Args {
 
 template <bool kTrain>
 __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
+  HBK_MT(1, 1);
   __shared__ __attribute__((aligned(16))) float hgS[kMaxG][kR][kLd];
   __shared__ __attribute__((aligned(16))) float xhS[kMaxG - 1][kR][kL + 4];
-  __shared__ __attribute__((aligned(16))) float bufA[kR][kLd];
-  __shared__ __attribute__((aligned(16))) float bufB[kR][kLd];
-  __shared__ __attribute__((aligned(16))) float bufS[kR][kLd];
+  __shared__ __attribute__((aligned(16))) float bX[kR][kLd];   // LN output (forward) / dHG (backward)
+  __shared__ __attribute__((aligned(16))) float bU[kR][kLd];   // gate output (forward) / dXn (backward)
+  __shared__ __attribute__((aligned(16))) float bS[kR][kLd];   // GMLP output (forward) / dS (backward)
   __shared__ float rsS[kMaxG][kR];
   __shared__ float zS[kR], dzS[kR];
-  __shared__ float red[4][kStats];
+  __shared__ float red[kStats];
+  // every bias / LayerNorm affine / the output unit's weights, loaded once
+  __shared__ float sBo[kMaxG][kL], sBhg[kMaxG][kH2], sLg[kMaxG][kL], sLb[kMaxG][kL], sWo[kH];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m = lane & 15, kq = lane >> 4;
   const int r0 = blockIdx.x * kR;
   const int nrow = min(kR, a.B - r0);
   const float* P = a.P;
   const int NG = a.NG;
   const int64_t B = a.B;
-  // HG0 = sum of k1's partials + bias
-  for (int e = tid; e < kR * kH2; e += 256) {
-    const int r = e >> 7, j = e & 127;
-    float v = 0.f;
-    if (r < nrow)
-      for (int s = 0; s < a.KS; ++s) v += a.hg_part[(s * B + r0 + r) * kH2 + j];
-    hgS[0][r][j] = v + P[a.b_hg[0] + j];
-  }
-  __syncthreads();
-  // ---------------------------------------------------------- forward ----
+  WReg wa, wb;
+  load_w<kH, kL, true>(wa, P + a.w_o[0], wave, lane);
   for (int k = 0; k < NG; ++k) {
-    // U = silu(H) * G
-    for (int e = tid; e < kR * kH; e += 256) {
-      const int r = e >> 6, j = e & 63;
-      const float h = hgS[k][r][j], gg = hgS[k][r][kH + j];
-      const float u = h * sigm(h) * gg;
-      bufA[r][j] = u;
-      if (kTrain && r < nrow) a.U[(k * B + r0 + r) * kH + j] = u;
-    }
-    __syncthreads();
-    if (k == NG - 1) break;
-    rows_gemm<kH, kL, true>(&bufA[0][0], P + a.w_o[k], P + a.b_o[k], &bufB[0][0], wave, lane);
-    __syncthreads();
-    // LayerNorm k over 96 columns: wave w -> rows 4w..4w+3, lane -> c, c + 64
-    const float* lg = P + a.ln_g[k];
-    const float* lb = P + a.ln_b[k];
-    for (int i = 0; i < 4; ++i) {
-      const int r = wave * 4 + i;
-      const float v0 = bufB[r][lane], v1 = lane < kL - 64 ? bufB[r][64 + lane] : 0.f;
-      const float mu = wsum(v0 + v1) * (1.f / kL);
-      const float d0 = v0 - mu, d1 = lane < kL - 64 ? v1 - mu : 0.f;
-      const float rs = 1.f / sqrtf(wsum(d0 * d0 + d1 * d1) * (1.f / kL) + kLnEps);
-      const float x0 = d0 * rs, x1 = d1 * rs;
-      xhS[k][r][lane] = x0;
-      const float n0 = x0 * lg[lane] + lb[lane];
-      bufA[r][lane] = n0;
-      if (kTrain && r < nrow) a.Xn[((k + 1) * B + r0 + r) * kL + lane] = n0;
-      if (lane < kL - 64) {
-        xhS[k][r][64 + lane] = x1;
-        const float n1 = x1 * lg[64 + lane] + lb[64 + lane];
-        bufA[r][64 + lane] = n1;
-        if (kTrain && r < nrow) a.Xn[((k + 1) * B + r0 + r) * kL + 64 + lane] = n1;
+    const int out = k + 1 < NG ? kL : 1;
+    for (int c = tid; c < kH2; c += 256) sBhg[k][c] = P[a.b_hg[k] + c];
+    for (int c = tid; c < out; c += 256) sBo[k][c] = P[a.b_o[k] + c];
+    if (k + 1 < NG)
+      for (int c = tid; c < kL; c += 256) {
+        sLg[k][c] = P[a.ln_g[k] + c];
+        sLb[k][c] = P[a.ln_b[k] + c];
       }
-      if (lane == 0) rsS[k][r] = rs;
+  }
+  if (tid < kH) sWo[tid] = P[a.w_o[NG - 1] + tid];
+  // HG0 = sum of k1's KS partial slabs + bias; U0 = silu(H) G. Thread ->
+  // 4 (row, j) pairs; the slab loads are issued 4 slabs at a time.
+  {
+    float h[4] = {0.f, 0.f, 0.f, 0.f}, g[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int s0 = 0; s0 < a.KS; s0 += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (s0 + u < a.KS) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int e = tid + 256 * q, r = e >> 6, j = e & 63;
+            if (r < nrow) {
+              const float* src = a.hg_part + ((s0 + u) * B + r0 + r) * kH2;
+              h[q] += src[j];
+              g[q] += src[kH + j];
+            }
+          }
+        }
+      }
     }
-    __syncthreads();
-    rows_gemm<kL, kH2, true>(&bufA[0][0], P + a.w_hg[k + 1], P + a.b_hg[k + 1], &hgS[k + 1][0][0], wave, lane);
-    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = tid + 256 * q, r = e >> 6, j = e & 63;
+      const float hh = h[q] + P[a.b_hg[0] + j], gg = g[q] + P[a.b_hg[0] + kH + j];
+      hgS[0][r][j] = hh;
+      hgS[0][r][kH + j] = gg;
+      bU[r][j] = hh * sigm(hh) * gg;
+    }
+  }
+  __syncthreads(); HBK_MT(1, 11);
+  const int64_t Bp = a.Bp;
+  // transposed activation stores: 4 consecutive rows of one column per float4
+  auto st4 = [&](float* base, int col, int row4, f4 v) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (r0 + row4 + e >= a.B) v[e] = 0.f;
+    *reinterpret_cast<f4*>(base + col * Bp + r0 + row4) = v;
+  };
+  if (kTrain) {  // U_0 from bU: thread -> column tid & 63, rows 4 (tid >> 6) ..
+    const int j = tid & 63, rg = 4 * (tid >> 6);
+    st4(a.U, j, rg, f4{bU[rg][j], bU[rg + 1][j], bU[rg + 2][j], bU[rg + 3][j]});
+  }
+  // ---------------------------------------------------------- forward ----
+  for (int k = 0; k + 1 < NG; ++k) {
+    // S_k = U_k W_o_k^T + b_o_k  -> bS   (weights in wa; prefetch HG_{k+1}'s into wb)
+    load_w<kL, kH2, true>(wb, P + a.w_hg[k + 1], wave, lane);
+    {
+      f4 c0, c1;
+      gemm2<kH>(wa, &bU[0][0], lane, c0, c1);
+      const int n0 = 16 * wave + m, n1 = 16 * (wave + 4) + m;
+      const float bo0 = sBo[k][n0], bo1 = n1 < kL ? sBo[k][n1] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bS[4 * kq + e][n0] = c0[e] + bo0;
+      if (n1 < kL) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bS[4 * kq + e][n1] = c1[e] + bo1;
+      }
+    }
+    __syncthreads(); HBK_MT(1, 12);
+    // LayerNorm k over 96 columns: wave w -> rows 4w..4w+3, lane -> c, c + 64
+    {
+      const bool hi = lane < kL - 64;
+      const float g0 = sLg[k][lane], b0 = sLb[k][lane];
+      const float g1 = hi ? sLg[k][64 + lane] : 0.f, b1 = hi ? sLb[k][64 + lane] : 0.f;
+      f4 o0, o1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wave * 4 + i;
+        const float v0 = bS[r][lane], v1 = hi ? bS[r][64 + lane] : 0.f;
+        const float mu = wsum(v0 + v1) * (1.f / kL);
+        const float d0 = v0 - mu, d1 = hi ? v1 - mu : 0.f;
+        const float rs = 1.f / sqrtf(wsum(d0 * d0 + d1 * d1) * (1.f / kL) + kLnEps);
+        const float x0 = d0 * rs, x1 = d1 * rs;
+        const float n0 = x0 * g0 + b0;
+        xhS[k][r][lane] = x0;
+        bX[r][lane] = n0;
+        o0[i] = n0;
+        const float n1 = x1 * g1 + b1;
+        o1[i] = n1;
+        if (hi) {
+          xhS[k][r][64 + lane] = x1;
+          bX[r][64 + lane] = n1;
+        }
+        if (lane == 0) rsS[k][r] = rs;
+      }
+      if (kTrain) {
+        float* xt = a.Xn + (k + 1) * kL * Bp;
+        st4(xt, lane, 4 * wave, o0);
+        if (hi) st4(xt, 64 + lane, 4 * wave, o1);
+      }
+    }
+    __syncthreads(); HBK_MT(1, 13);
+    // HG_{k+1} = Xn W_hg^T + b, gate in the epilogue -> hgS[k+1], U_{k+1} -> bU
+    if (k + 2 < NG) load_w<kH, kL, true>(wa, P + a.w_o[k + 1], wave, lane);
+    {
+      f4 ch, cg;
+      gemm2<kL>(wb, &bX[0][0], lane, ch, cg);
+      const int j = 16 * wave + m;
+      const float bh = sBhg[k + 1][j], bg = sBhg[k + 1][kH + j];
+      f4 uo;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int r = 4 * kq + e;
+        const float h = ch[e] + bh, g = cg[e] + bg;
+        hgS[k + 1][r][j] = h;
+        hgS[k + 1][r][kH + j] = g;
+        const float u = h * sigm(h) * g;
+        bU[r][j] = u;
+        uo[e] = u;
+      }
+      if (kTrain) st4(a.U + (k + 1) * kH * Bp, j, 4 * kq, uo);
+    }
+    __syncthreads(); HBK_MT(1, 14);
   }
   // output unit: z = U . w_o + b_o (wave w -> rows 4w..4w+3)
   {
-    const float* wo = P + a.w_o[NG - 1];
-    const float bo = P[a.b_o[NG - 1]];
+    const float bo = sBo[NG - 1][0];
+    const float wl = sWo[lane];
+#pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = wave * 4 + i;
-      const float z = wsum(bufA[r][lane] * wo[lane]) + bo;
+      const float z = wsum(bU[r][lane] * wl) + bo;
       if (lane == 0) zS[r] = z;
     }
   }
-  __syncthreads();
+  __syncthreads(); HBK_MT(1, 15);
   const int step = step_of(a.state, a.parity);
   // sigmoid, high-loss filter (trainer.py:407-424), weighted BCE (:301-312, torch
   // formulas incl. the log clamp at -100 and the 1e-12 in BCE's backward)
@@ -369,119 +591,161 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
     if (kTrain) {
 #pragma unroll
       for (int s = 0; s < kStats; ++s) {
-        float v = loc[s];
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);  // 16-lane sum
-        if (tid == 0) red[0][s] = v;
+        const float v = rsum16(loc[s]);  // lanes 0..15 of wave 0
+        if (tid == 0) red[s] = v;
       }
     }
   }
   if (!kTrain) return;
-  __syncthreads();
-  if (tid < kStats && red[0][tid] != 0.f) atomicAdd(a.stats + tid, red[0][tid]);
+  // backward weights: dU = dS W_o (NN) of GMLP NG-2, dXn = dHG W_hg (NN) of GMLP NG-1
+  load_w<kL, kH, false>(wa, P + a.w_o[NG - 2], wave, lane);
+  load_w<kH2, kL, false>(wb, P + a.w_hg[NG - 1], wave, lane);
+  __syncthreads(); HBK_MT(1, 16);
+  if (tid < kStats && red[tid] != 0.f) atomicAdd(a.stats + tid, red[tid]);
   // ---------------------------------------------------------- backward ---
   float* G = a.G;
-  // dS of the output unit = dz (column 0), its bias gradient = sum dz
-  if (tid < kR) {
-    bufS[tid][0] = dzS[tid];
-    if (tid < nrow) a.dS[((NG - 1) * B + r0 + tid) * kL] = dzS[tid];
-  }
-  if (tid == 0) {
+  if (tid < 4) st4(a.dS + (NG - 1) * kL * Bp, 0, 4 * tid, f4{dzS[4 * tid], dzS[4 * tid + 1], dzS[4 * tid + 2], dzS[4 * tid + 3]});
+  if (tid == 64) {  // output bias gradient = sum dz
     float s = 0.f;
     for (int r = 0; r < kR; ++r) s += dzS[r];
     if (s != 0.f) atomicAdd(G + a.b_o[NG - 1], s);
   }
-  __syncthreads();
-  for (int k = NG - 1; k >= 0; --k) {
-    // dU = dS_k . W_o_k
-    if (k == NG - 1) {
-      const float* wo = P + a.w_o[k];
-      for (int e = tid; e < kR * kH; e += 256) {
-        const int r = e >> 6, j = e & 63;
-        bufA[r][j] = bufS[r][0] * wo[j];
-      }
-    } else {
-      rows_gemm<kL, kH, false>(&bufS[0][0], P + a.w_o[k], nullptr, &bufA[0][0], wave, lane);
-      // bias gradient of output k: column sums of dS_k
-      if (tid < kL) {
-        float s = 0.f;
-        for (int r = 0; r < kR; ++r) s += bufS[r][tid];
-        atomicAdd(G + a.b_o[k] + tid, s);
-      }
-    }
-    __syncthreads();
-    // gate backward: dH = dU G silu'(H), dG = dU silu(H)
-    for (int e = tid; e < kR * kH; e += 256) {
-      const int r = e >> 6, j = e & 63;
-      const float h = hgS[k][r][j], gg = hgS[k][r][kH + j], du = bufA[r][j];
+  // output unit: dU = dz w_o, gate backward -> dHG (bX)
+  {
+    const int k = NG - 1;
+    const int j = tid & 63, rg = 4 * (tid >> 6);
+    const float wj = sWo[j];
+    f4 dho, dgo;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int r = rg + e;
+      const float h = hgS[k][r][j], gg = hgS[k][r][kH + j], du = dzS[r] * wj;
       const float sg = sigm(h);
       const float dh = du * gg * (sg * (1.f + h * (1.f - sg))), dg = du * h * sg;
-      bufB[r][j] = dh;
-      bufB[r][kH + j] = dg;
-      if (r < nrow) {
-        a.dHG[(k * B + r0 + r) * kH2 + j] = dh;
-        a.dHG[(k * B + r0 + r) * kH2 + kH + j] = dg;
-      }
+      bX[r][j] = dh;
+      bX[r][kH + j] = dg;
+      dho[e] = dh;
+      dgo[e] = dg;
     }
-    __syncthreads();
-    if (tid < kH2) {  // bias gradient of hidden + gate k
+    st4(a.dHG + k * kH2 * Bp, j, rg, dho);
+    st4(a.dHG + k * kH2 * Bp, kH + j, rg, dgo);
+  }
+  __syncthreads(); HBK_MT(1, 17);
+  for (int k = NG - 1; k >= 1; --k) {
+    // bias gradient of hidden + gate k: column sums of dHG_k (bX)
+    if (tid < kH2) {
       float s = 0.f;
-      for (int r = 0; r < kR; ++r) s += bufB[r][tid];
+      for (int r = 0; r < kR; ++r) s += bX[r][tid];
       atomicAdd(G + a.b_hg[k] + tid, s);
     }
-    if (k == 0) break;
-    // dXn (input of GMLP k = output of LayerNorm k - 1) = dHG . W_hg_k
-    rows_gemm<kH2, kL, false>(&bufB[0][0], P + a.w_hg[k], nullptr, &bufA[0][0], wave, lane);
-    __syncthreads();
-    // LayerNorm k - 1 backward: gamma / beta column sums, dS_{k-1} per row
+    // dXn = dHG_k W_hg_k (NN: K 128 -> N 96, weights in wb) -> bU
+    {
+      f4 c0, c1;
+      gemm2<kH2>(wb, &bX[0][0], lane, c0, c1);
+      const int n0 = 16 * wave + m, n1 = 16 * (wave + 4) + m;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bU[4 * kq + e][n0] = c0[e];
+      if (n1 < kL) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bU[4 * kq + e][n1] = c1[e];
+      }
+    }
+    __syncthreads(); HBK_MT(1, 18);
+    // LayerNorm k-1 backward: gamma / beta column sums, dS_{k-1} per row -> bS
     {
       const int l = k - 1;
       if (tid < kL) {
         float sg = 0.f, sb = 0.f;
         for (int r = 0; r < kR; ++r) {
-          sg += bufA[r][tid] * xhS[l][r][tid];
-          sb += bufA[r][tid];
+          sg += bU[r][tid] * xhS[l][r][tid];
+          sb += bU[r][tid];
         }
         atomicAdd(G + a.ln_g[l] + tid, sg);
         atomicAdd(G + a.ln_b[l] + tid, sb);
       }
-      const float* lg = P + a.ln_g[l];
+      const bool hi = lane < kL - 64;
+      const float g0 = sLg[l][lane], g1 = hi ? sLg[l][64 + lane] : 0.f;
+      f4 o0, o1;
+#pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = wave * 4 + i;
-        const float t0 = bufA[r][lane] * lg[lane];
-        const float t1 = lane < kL - 64 ? bufA[r][64 + lane] * lg[64 + lane] : 0.f;
-        const float x0 = xhS[l][r][lane], x1 = lane < kL - 64 ? xhS[l][r][64 + lane] : 0.f;
+        const float t0 = bU[r][lane] * g0;
+        const float t1 = hi ? bU[r][64 + lane] * g1 : 0.f;
+        const float x0 = xhS[l][r][lane], x1 = hi ? xhS[l][r][64 + lane] : 0.f;
         const float s1 = wsum(t0 + t1) * (1.f / kL);
         const float s2 = wsum(t0 * x0 + t1 * x1) * (1.f / kL);
         const float rs = rsS[l][r];
         const float d0 = rs * (t0 - s1 - x0 * s2);
-        bufS[r][lane] = d0;
-        if (r < nrow) a.dS[(l * B + r0 + r) * kL + lane] = d0;
-        if (lane < kL - 64) {
-          const float d1 = rs * (t1 - s1 - x1 * s2);
-          bufS[r][64 + lane] = d1;
-          if (r < nrow) a.dS[(l * B + r0 + r) * kL + 64 + lane] = d1;
-        }
+        const float d1 = rs * (t1 - s1 - x1 * s2);
+        bS[r][lane] = d0;
+        o0[i] = d0;
+        o1[i] = d1;
+        if (hi) bS[r][64 + lane] = d1;
       }
+      st4(a.dS + l * kL * Bp, lane, 4 * wave, o0);
+      if (hi) st4(a.dS + l * kL * Bp, 64 + lane, 4 * wave, o1);
     }
-    __syncthreads();
+    __syncthreads(); HBK_MT(1, 19);
+    // GMLP k-1: output bias gradient (column sums of dS), dU = dS W_o (NN: K 96 -> N 64)
+    // with the gate backward in the epilogue -> dHG_{k-1} (bX)
+    {
+      const int kk = k - 1;
+      if (tid < kL) {
+        float s = 0.f;
+        for (int r = 0; r < kR; ++r) s += bS[r][tid];
+        atomicAdd(G + a.b_o[kk] + tid, s);
+      }
+      const f4 du = gemm1<kL>(wa, &bS[0][0], lane);
+      if (kk >= 1) {  // the next iteration's weights
+        load_w<kL, kH, false>(wa, P + a.w_o[kk - 1], wave, lane);
+        load_w<kH2, kL, false>(wb, P + a.w_hg[kk], wave, lane);
+      }
+      const int j = 16 * wave + m;
+      f4 dho, dgo;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int r = 4 * kq + e;
+        const float h = hgS[kk][r][j], gg = hgS[kk][r][kH + j];
+        const float sg = sigm(h);
+        const float dh = du[e] * gg * (sg * (1.f + h * (1.f - sg))), dg = du[e] * h * sg;
+        bX[r][j] = dh;
+        bX[r][kH + j] = dg;
+        dho[e] = dh;
+        dgo[e] = dg;
+      }
+      st4(a.dHG + kk * kH2 * Bp, j, 4 * kq, dho);
+      st4(a.dHG + kk * kH2 * Bp, kH + j, 4 * kq, dgo);
+    }
+    __syncthreads(); HBK_MT(1, 20);
   }
+  // bias gradient of mlp_in's hidden + gate
+  if (tid < kH2) {
+    float s = 0.f;
+    for (int r = 0; r < kR; ++r) s += bX[r][tid];
+    atomicAdd(G + a.b_hg[0] + tid, s);
+  }
+  HBK_MT(1, 99);
 }
 
 // ------------------------------------------------------------------ k3 ----
-// dW [M][N] += X^T Y over a chunk of batch rows: X [B][ldx] (columns = M),
-// Y [B][ldy] (columns = N). Tile 64 x 32, wave w -> rows 16 w..16 w + 15.
+// dW [M][N] += X^T Y over a chunk of batch rows, from k1/k2's TRANSPOSED
+// activations X^T [M][Bp], Y^T [N][Bp] (rows of b contiguous, pad rows zero):
+// lane (m, kq) of MFMA step (i, s) reads k = b = 16 i + 4 kq + s, so A and B
+// are float4 loads along b. Tile 64 x 32, wave w -> M rows 16 w .. 16 w + 15,
+// both 16-column halves; split-K partials are added with float atomics into
+// the bucket (zeroed by the previous step's k4).
 constexpr int kTM = 64, kTN = 32, kMaxJobs = 2 * kMaxG;
 struct WJob {
-  const float* X;
-  const float* Y;
-  float* C;
-  int ldx, ldy, ldc, M, N, tn;
+  const float* X;  // [M][Bp]
+  const float* Y;  // [N][Bp]
+  float* C;        // [M][ldc]
+  int ldc, M, N, tn;
 };
 struct K3Args {
   WJob job[kMaxJobs];
   int start[kMaxJobs + 1];
-  int n_jobs, B, Kc, KS;
+  int n_jobs, Kc, KS;
+  int64_t Bp;
   // input-layer job (job 0): post-op with norm_in's affine and W_hg0
   const float* g_in;
   const float* b_in;
@@ -501,34 +765,52 @@ __global__ void __launch_bounds__(256) k3_wgrad_kernel(K3Args a) {
   const int local = blk - a.start[j];
   const int split = local % a.KS, tile = local / a.KS;
   const int tm = tile / jb.tn, tn = tile - tm * jb.tn;
-  const int rb0 = split * a.Kc, rb1 = min(a.B, rb0 + a.Kc);
+  HBK_MT(2, 1);
+  const int rb0 = split * a.Kc, rb1 = static_cast<int>(min(a.Bp, static_cast<int64_t>(rb0 + a.Kc)));
   const int m = lane & 15, kq = lane >> 4;
-  const int mrow = tm * kTM + 16 * wave;   // first M row of this wave
+  const int mrow = tm * kTM + 16 * wave;  // first M row of this wave
   const int n0 = tn * kTN;
   const bool mok = mrow + m < jb.M;
   const bool nok0 = n0 + m < jb.N, nok1 = n0 + 16 + m < jb.N;
-  f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-  float ssum = 0.f;
-  const float* X = jb.X + mrow + m;
-  const float* Y0 = jb.Y + n0 + m;
-  const float* Y1 = Y0 + 16;
-  for (int b = rb0; b < rb1; b += 32) {
-    float xa[8], ya[8], yb[8];
+  f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, ssum = acc0;
+  const f4 zero = acc0;
+  const float* X = jb.X + static_cast<int64_t>(mok ? mrow + m : 0) * a.Bp + 4 * kq;
+  const float* Y0 = jb.Y + static_cast<int64_t>(nok0 ? n0 + m : 0) * a.Bp + 4 * kq;
+  const float* Y1 = jb.Y + static_cast<int64_t>(nok1 ? n0 + 16 + m : 0) * a.Bp + 4 * kq;
+  // 8-step register ring: the loads of step i + 8 are issued as step i is consumed
+  const int nit = (rb1 - rb0) / 16;
+  f4 rx[8], ry0[8], ry1[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int rb = b + 4 * u + kq;
-      const bool ok = rb < rb1;
-      xa[u] = (ok && mok) ? X[static_cast<int64_t>(rb) * jb.ldx] : 0.f;
-      ya[u] = (ok && nok0) ? Y0[static_cast<int64_t>(rb) * jb.ldy] : 0.f;
-      yb[u] = (ok && nok1) ? Y1[static_cast<int64_t>(rb) * jb.ldy] : 0.f;
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      acc0 = mma(xa[u], ya[u], acc0);
-      acc1 = mma(xa[u], yb[u], acc1);
-      ssum += xa[u];
+  for (int u = 0; u < 8; ++u) {
+    if (u < nit) {
+      const int b = rb0 + 16 * u;
+      rx[u] = mok ? *reinterpret_cast<const f4*>(X + b) : zero;
+      ry0[u] = nok0 ? *reinterpret_cast<const f4*>(Y0 + b) : zero;
+      ry1[u] = nok1 ? *reinterpret_cast<const f4*>(Y1 + b) : zero;
     }
   }
+  for (int i0 = 0; i0 < nit; i0 += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u;
+      if (i < nit) {
+        const f4 xa = rx[u], ya = ry0[u], yb = ry1[u];
+        if (i + 8 < nit) {
+          const int b = rb0 + 16 * (i + 8);
+          rx[u] = mok ? *reinterpret_cast<const f4*>(X + b) : zero;
+          ry0[u] = nok0 ? *reinterpret_cast<const f4*>(Y0 + b) : zero;
+          ry1[u] = nok1 ? *reinterpret_cast<const f4*>(Y1 + b) : zero;
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          acc0 = mma(xa[s], ya[s], acc0);
+          acc1 = mma(xa[s], yb[s], acc1);
+        }
+        ssum += xa;
+      }
+    }
+  }
+  HBK_MT(2, 2);
   if (j != 0) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -540,10 +822,11 @@ __global__ void __launch_bounds__(256) k3_wgrad_kernel(K3Args a) {
     }
     return;
   }
-  // input layer: s_j = sum over the chunk's rows of dHG0[b][j] (lanes m, m+16, m+32, m+48 hold parts)
-  ssum += __shfl_xor(ssum, 16, 64);
-  ssum += __shfl_xor(ssum, 32, 64);
-  if (kq == 0) sS[16 * wave + m] = ssum;
+  // input layer: s_j = sum over the chunk's rows of dHG0[b][j] (lanes m + 16 q hold parts)
+  float sj_part = (ssum[0] + ssum[1]) + (ssum[2] + ssum[3]);
+  sj_part += __shfl_xor(sj_part, 16, 64);
+  sj_part += __shfl_xor(sj_part, 32, 64);
+  if (kq == 0) sS[16 * wave + m] = sj_part;
   __syncthreads();
   float dg0 = 0.f, dg1 = 0.f, dbt0 = 0.f, dbt1 = 0.f;
   const int c0 = n0 + m, c1 = n0 + 16 + m;
@@ -658,10 +941,33 @@ __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
   if (a.sched) lr = a.sched[2 * min(step, a.sched_len - 1)];
   const float bc1 = 1.f - powf(a.b1, t), bc2s = sqrtf(1.f - powf(a.b2, t));
   const float step_size = lr / bc1;
-  for (int64_t i = blockIdx.x * int64_t(256) + threadIdx.x; i < a.n; i += int64_t(gridDim.x) * 256) {
+  const bool on = fire != 0.f;
+  // float4 body (the bucket, params and moments are 16-B aligned torch buffers), scalar tail
+  const int64_t n4 = a.n >> 2;
+  f4* G4 = reinterpret_cast<f4*>(a.G);
+  f4* P4 = reinterpret_cast<f4*>(a.P);
+  f4* M4 = reinterpret_cast<f4*>(a.m);
+  f4* V4 = reinterpret_cast<f4*>(a.v);
+  const f4 z4 = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t i = blockIdx.x * int64_t(256) + threadIdx.x; i < n4; i += int64_t(gridDim.x) * 256) {
+    const f4 g = G4[i];
+    G4[i] = z4;
+    if (on) {
+      const f4 gi = g * scale;
+      const f4 mi = a.b1 * M4[i] + (1.f - a.b1) * gi;
+      const f4 vi = a.b2 * V4[i] + (1.f - a.b2) * gi * gi;
+      M4[i] = mi;
+      V4[i] = vi;
+      f4 p = P4[i];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) p[e] -= step_size * mi[e] / (sqrtf(vi[e]) / bc2s + a.eps);
+      P4[i] = p;
+    }
+  }
+  for (int64_t i = 4 * n4 + blockIdx.x * int64_t(256) + threadIdx.x; i < a.n; i += int64_t(gridDim.x) * 256) {
     const float g = a.G[i];
     a.G[i] = 0.f;
-    if (fire != 0.f) {
+    if (on) {
       const float gi = g * scale;
       const float mi = a.b1 * a.m[i] + (1.f - a.b1) * gi;
       const float vi = a.b2 * a.v[i] + (1.f - a.b2) * gi * gi;
@@ -687,12 +993,13 @@ FusedWs fused_layout(int64_t B, int NG) {
   FusedWs w;
   int64_t o = 0;
   auto take = [&](int64_t n) { const int64_t r = o; o += (n + 63) & ~int64_t(63); return r; };
+  const int64_t Bp = (B + kR - 1) / kR * kR;
   w.hg_part = take(int64_t(24) * B * kH2);
-  w.xhat = take(B * kD);
-  w.U = take(int64_t(NG) * B * kH);
-  w.Xn = take(int64_t(NG) * B * kL);
-  w.dS = take(int64_t(NG) * B * kL);
-  w.dHG = take(int64_t(NG) * B * kH2);
+  w.xhat = take(Bp * kD);
+  w.U = take(int64_t(NG) * Bp * kH);
+  w.Xn = take(int64_t(NG) * Bp * kL);
+  w.dS = take(int64_t(NG) * Bp * kL);
+  w.dHG = take(int64_t(NG) * Bp * kH2);
   w.total = o;
   return w;
 }
@@ -749,11 +1056,14 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
   k1.chunk = kD / KS;
   k1.drop_p = drop_p;
   k1.seed = seed;
+  const int64_t Bp = (B + kR - 1) / kR * kR;
   k1.hg_part = ws + w.hg_part;
-  k1.xhat = ws + w.xhat;
+  k1.xhat = train ? ws + w.xhat : nullptr;
+  k1.Bp = Bp;
   k1.stats = train ? bucket + p.n_params : nullptr;
   const int rt = (B + kR - 1) / kR;
-  hipLaunchKernelGGL(k1_input_kernel, dim3(rt, KS), dim3(256), 0, s, k1);
+  const int rt8 = (rt + 7) / 8 * 8;  // XCD-aware 1-D grid (see k1_input_kernel)
+  hipLaunchKernelGGL(k1_input_kernel, dim3(rt8 * KS), dim3(256), 0, s, k1);
   HBK_LAUNCH_CHECK("k1_input_kernel");
   K2Args k2;
   k2.P = params;
@@ -778,6 +1088,7 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
   k2.Xn = ws + w.Xn;
   k2.dS = ws + w.dS;
   k2.dHG = ws + w.dHG;
+  k2.Bp = Bp;
   if (!train) {
     hipLaunchKernelGGL(k2_rows_kernel<false>, dim3(rt), dim3(256), 0, s, k2);
     HBK_LAUNCH_CHECK("k2_rows_kernel");
@@ -788,14 +1099,12 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
   // k3: job 0 = input layer, then dW_hg of GMLPs 1.., then dW_o of every GMLP
   K3Args k3;
   int nj = 0, blocks = 0;
-  const int KS3 = std::max(1, std::min((B + 127) / 128, 8));
-  const int Kc = ((B + KS3 - 1) / KS3 + 3) / 4 * 4;
-  auto add = [&](const float* X, int ldx, const float* Y, int ldy, float* C, int ldc, int M, int N) {
+  const int KS3 = std::max(1, static_cast<int>((Bp + 287) / 288));
+  const int Kc = static_cast<int>((Bp / kR + KS3 - 1) / KS3) * kR;
+  auto add = [&](const float* X, const float* Y, float* C, int ldc, int M, int N) {
     WJob& j = k3.job[nj];
     j.X = X;
-    j.ldx = ldx;
     j.Y = Y;
-    j.ldy = ldy;
     j.C = C;
     j.ldc = ldc;
     j.M = M;
@@ -806,18 +1115,16 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
     ++nj;
   };
   float* G = bucket;
-  add(ws + w.dHG, kH2, ws + w.xhat, kD, G + p.g[0].w_hg, kD, kH2, kD);
+  add(ws + w.dHG, ws + w.xhat, G + p.g[0].w_hg, kD, kH2, kD);
   for (int k = 1; k < NG; ++k)
-    add(ws + w.dHG + int64_t(k) * B * kH2, kH2, ws + w.Xn + int64_t(k) * B * kL, kL, G + p.g[k].w_hg, kL, kH2,
-        kL);
+    add(ws + w.dHG + int64_t(k) * kH2 * Bp, ws + w.Xn + int64_t(k) * kL * Bp, G + p.g[k].w_hg, kL, kH2, kL);
   for (int k = 0; k < NG; ++k)
-    add(ws + w.dS + int64_t(k) * B * kL, kL, ws + w.U + int64_t(k) * B * kH, kH, G + p.g[k].w_o, kH,
-        p.g[k].out, kH);
+    add(ws + w.dS + int64_t(k) * kL * Bp, ws + w.U + int64_t(k) * kH * Bp, G + p.g[k].w_o, kH, p.g[k].out, kH);
   k3.start[nj] = blocks;
   k3.n_jobs = nj;
-  k3.B = B;
   k3.Kc = Kc;
   k3.KS = KS3;
+  k3.Bp = Bp;
   k3.g_in = params + p.ln_in.g;
   k3.b_in = params + p.ln_in.b;
   k3.W0 = params + p.g[0].w_hg;
@@ -847,10 +1154,21 @@ int mlp_fused_update(const hbk_mlp_plan& p, float* params, float* bucket, float*
   k.eps = eps;
   k.hist = hist;
   k.hist_cap = hist_cap;
-  const int64_t blocks = std::min<int64_t>((p.n_params + 1023) / 1024, 1024);
+  const int64_t blocks = std::min<int64_t>((p.n_params / 4 + 255) / 256, 1024);
   hipLaunchKernelGGL(k4_update_kernel, dim3(unsigned(blocks)), dim3(256), 0, s, k);
   HBK_LAUNCH_CHECK("k4_update_kernel");
   return HBK_OK;
 }
 
 }  // namespace hbk
+
+#ifdef HBK_TRACE
+extern "C" int hbk_debug_mlp_trace(unsigned long long* out, int* counts) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hbk::g_mlp_trace), sizeof(unsigned long long) * 3 * 4 * 128) != hipSuccess)
+    return -2;
+  if (hipMemcpyFromSymbol(counts, HIP_SYMBOL(hbk::g_mlp_trace_n), sizeof(int) * 12) != hipSuccess) return -2;
+  int z[12] = {};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(hbk::g_mlp_trace_n), z, sizeof(z));
+  return 0;
+}
+#endif

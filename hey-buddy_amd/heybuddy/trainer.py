@@ -618,7 +618,8 @@ class WakeWordTrainer(Trainer):
         steps x 2 (at least validation_steps), batch x 0.5, and the last
         validated negative weight carries over."""
         start = perf_counter()
-        hist: Dict[str, List[torch.Tensor]] = {k: [] for k in ("lr", "nw", "loss", "hlr", "recall", "fp")}
+        hist: Dict[str, List[torch.Tensor]] = {k: [] for k in ("lr", "nw", "loss", "hlr", "recall", "fp", "vfp",
+                                                               "vrecall", "tacc", "trecall", "tfp")}
         last = {"loss": 0.0, "recall": 0.0, "fp": 0.0, "vfp": 0.0, "vrec": 0.0, "tacc": 0.0, "trec": 0.0, "tfp": 0.0}
         for hook in ("start",):
             for d in (training, validation, testing):
@@ -646,7 +647,8 @@ class WakeWordTrainer(Trainer):
                 last_testing_false_positive_rate=last["tfp"])
             logger.info(f"Training Stage {i + 1}: {len(lr)} steps in {perf_counter() - t0:.2f} s, "
                         f"final loss {float(loss[-1]) if loss is not None else float('nan'):.5f}")
-            for k, v in zip(("lr", "nw", "loss", "hlr", "recall", "fp"), (lr, nw, loss, hlr, rec, fp)):
+            for k, v in zip(("lr", "nw", "loss", "hlr", "recall", "fp", "vfp", "vrecall", "tacc", "trecall", "tfp"),
+                            (lr, nw, loss, hlr, rec, fp, v_fp, v_rec, t_acc, t_rec, t_fp)):
                 if v is not None:
                     hist[k].append(v)
             last.update(loss=float(loss[-1]), recall=float(rec[-1]), fp=float(fp[-1]))

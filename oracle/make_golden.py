@@ -16,8 +16,13 @@ records its outputs on seeded inputs:
                          orchestration numerically (inputs included).
   classifier.npz         WakeWordMLPModel forward / BCE / backward / Adam and
                          WakeWordTrainer.train_epoch histories (seeded).
+  classifier_stages.npz  WakeWordTrainer.__call__: 3 stages at batch 1100 -> 550
+                         -> 273 with validation / testing and the dynamic
+                         negative weight (histories + final parameters).
+  to_target_length.npz   AugmentedAudioGenerator.to_target_length with numpy's
+                         global RNG seeded (crop, 1-sample pad, random pads).
 
-Usage: python oracle/make_golden.py [--only featurizer|classifier]
+Usage: python oracle/make_golden.py [--only featurizer|classifier|stages|augment]
 """
 from __future__ import annotations
 
@@ -68,6 +73,8 @@ def import_reference():
     import heybuddy.embeddings
     import heybuddy.trainer
     import heybuddy.wakeword
+    import heybuddy.dataset.training
+    import heybuddy.dataset.augmented
     os.chdir(cwd)
     return heybuddy
 
@@ -161,9 +168,13 @@ def main():
     sys.path = [p for p in sys.path if not p.endswith("/src")]
     if args.only in (None, "featurizer"):
         make_featurizer(hb)
+    from oracle import golden_classifier
     if args.only in (None, "classifier"):
-        from oracle import golden_classifier
         golden_classifier.make(hb, GOLDEN)
+    if args.only in (None, "stages"):
+        golden_classifier.make_stages(hb, GOLDEN)
+    if args.only in (None, "augment"):
+        golden_classifier.make_to_target_length(hb, GOLDEN)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,86 @@
+"""Fused classifier train step probe (tuning aid, not a test).
+
+  python tools/probe_mlp.py [steps]          µs per step over `steps` graph-replayed
+                                             steps of B = 1100 (bench composition)
+  python tools/probe_mlp.py --trace          s_memtime stage timeline of block 0's
+                                             waves in k1 / k2 / k3 (libhbk_trace.so)
+"""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "hey-buddy_amd")]
+TRACE = "--trace" in sys.argv
+if TRACE:
+    os.environ["HBK_LIB"] = os.path.join(ROOT, "hey-buddy_amd", "lib", "libhbk_trace.so")
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from heybuddy.trainer import WakeWordTrainer  # noqa: E402
+
+
+def setup(S, B=1100, P=50, A=50):
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(0)
+    pos = torch.randn((50_000, 16, 96), generator=g, device=dev) + 0.3
+    neg = torch.randn((200_000, 16, 96), generator=g, device=dev).half()
+    idx = torch.empty((S, B), dtype=torch.int32, device=dev)
+    idx[:, :P + A] = torch.randint(0, 50_000, (S, P + A), device=dev, dtype=torch.int32)
+    idx[:, P + A:] = -1 - torch.randint(0, 200_000, (S, B - P - A), device=dev, dtype=torch.int32)
+    y = torch.cat([torch.ones(P), torch.zeros(B - P)]).to(dev)
+    sched = torch.tensor([[1e-3, 1.0]] * S, device=dev)
+    tr = WakeWordTrainer(checkpoint_dir="/tmp/probe_ck", device=dev)
+    tr.model.train()
+    return tr, pos, neg, idx, y, sched
+
+
+def timing(S):
+    tr, pos, neg, idx, y, sched = setup(S)
+    hist = torch.zeros((S, 8), device="cuda")
+    for _ in range(2):
+        tr._reset_accumulation()
+        tr.train_indexed(idx, y, sched, pool32=pos, pool16=neg, history=hist, steps_per_graph=50)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(3):
+        tr._reset_accumulation()
+        tr.train_indexed(idx, y, sched, pool32=pos, pool16=neg, history=hist, steps_per_graph=50)
+    e1.record()
+    torch.cuda.synchronize()
+    print(f"{e0.elapsed_time(e1) * 1e3 / (3 * S):.2f} us per train step (B=1100, {S} steps x 3)")
+
+
+def trace():
+    from heybuddy._native import lib
+    tr, pos, neg, idx, y, sched = setup(4)
+    fn = lib().hbk_debug_mlp_trace
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    buf = (ctypes.c_ulonglong * (3 * 4 * 128))()
+    cnt = (ctypes.c_int * 12)()
+    tr._reset_accumulation()
+    tr.train_indexed(idx[:2], y, sched, pool32=pos, pool16=neg, graphs=False)
+    torch.cuda.synchronize()
+    fn(buf, cnt)  # reset
+    tr.train_indexed(idx[2:3], y, sched, pool32=pos, pool16=neg, graphs=False)
+    torch.cuda.synchronize()
+    fn(buf, cnt)
+    for k, name in enumerate(("k1_input", "k2_rows", "k3_wgrad")):
+        evs = []
+        for w in range(4):
+            n = cnt[k * 4 + w]
+            evs.append([(int(buf[(k * 4 + w) * 128 + i]) >> 56, int(buf[(k * 4 + w) * 128 + i]) & ((1 << 56) - 1))
+                        for i in range(n)])
+        t0 = min(e[0][1] for e in evs if e)
+        print(f"--- {name} (block 0; cycles from the first mark)")
+        for w, e in enumerate(evs):
+            print(f"  wave {w}: " + " ".join(f"{m}@{t - t0}" for m, t in e))
+
+
+if __name__ == "__main__":
+    if TRACE:
+        trace()
+    else:
+        timing(int(next((a for a in sys.argv[1:] if a.isdigit()), 200)))
