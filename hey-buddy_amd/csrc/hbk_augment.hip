@@ -607,12 +607,12 @@ struct ColoredArgs {
   float* out;
   int64_t out_stride;
   int64_t n_clips;
-  const float* white;     // [n_clips, white_stride] N(0,1) or NULL (generated from seed)
+  const float* white;     // [n_clips, white_stride >= 16000] N(0,1) or NULL (generated from seed)
   int64_t white_stride;
   uint64_t seed;
   const float* f_decay;   // per clip
   const float* snr_db;    // per clip
-  float lin_step;         // (sqrt(sr / 2) - 1) / (T / 2): linspace step over the T/2 + 1 bins
+  float lin_step;         // (sqrt(8000) - 1) / 8000: linspace step over the 8001 bins
   const float2* thi;
   const float2* tlo;
   const float2* twn;
@@ -654,18 +654,102 @@ __device__ __forceinline__ void copy_clip(const float* x, float* out, int tid) {
   }
 }
 
+// ---- 8000-point complex FFT (the 16,000-sample real FFT of one second of
+// noise): DIF passes 16 x 5 x 5 x 5 x 4 in LDS, twiddles W_8000^e =
+// HI8[e / 100] LO8[e % 100]; frequency f = k1 + 16 k2 + 80 k3 + 400 k4 + 2000 k5
+// lands at 500 k1 + 100 k2 + 20 k3 + 4 k4 + k5.
+constexpr int kN1 = 16000;               // torch_audiomentations' noise length = sample_rate
+constexpr int kM1 = kN1 / 2;             // 8000
+constexpr int kTw8Lo = 100, kTw8Hi = kM1 / kTw8Lo;  // 100 x 80
+
+template <bool INV>
+__device__ __forceinline__ cf twiddle8(const cf* thi, const cf* tlo, int e) {
+  const int h = e / kTw8Lo;
+  const cf w = cmul(thi[h], tlo[e - h * kTw8Lo]);
+  return INV ? cf{w.x, -w.y} : w;
+}
+
+template <int R, int L, int S, bool INV>
+__device__ __forceinline__ void pass8(cf* z, const cf* thi, const cf* tlo) {
+  constexpr int kTasks = kM1 / R;
+  int t0;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(t0) : "v"(static_cast<int>(threadIdx.x)));
+  for (int t = t0; t < kTasks; t += kThreads) {
+    const int blk = t / L, i = t - (t / L) * L;
+    cf* q = z + blk * (R * L) + i;
+    cf v[R];
+#pragma unroll
+    for (int m = 0; m < R; ++m) v[m] = q[L * m];
+    cf w[R];
+    if constexpr (S != 0) {
+#pragma unroll
+      for (int k = 1; k < R; ++k) w[k] = twiddle8<INV>(thi, tlo, S * i * k);
+    }
+    if (INV && S)
+#pragma unroll
+      for (int k = 1; k < R; ++k) v[k] = cmul(v[k], w[k]);
+    if constexpr (R == 16) fft16v<INV>(v);
+    else if constexpr (R == 4) fft4v<INV>(v[0], v[1], v[2], v[3]);
+    else dft5<INV>(v);
+    if (!INV && S)
+#pragma unroll
+      for (int k = 1; k < R; ++k) v[k] = cmul(v[k], w[k]);
+#pragma unroll
+    for (int m = 0; m < R; ++m) q[L * m] = v[m];
+  }
+}
+
+template <bool INV>
+__device__ __forceinline__ void transform8(cf* z, const cf* thi, const cf* tlo) {
+  if (!INV) {
+    pass8<16, 500, 1, false>(z, thi, tlo);
+    __syncthreads();
+    pass8<5, 100, 16, false>(z, thi, tlo);
+    __syncthreads();
+    pass8<5, 20, 80, false>(z, thi, tlo);
+    __syncthreads();
+    pass8<5, 4, 400, false>(z, thi, tlo);
+    __syncthreads();
+    pass8<4, 1, 0, false>(z, thi, tlo);
+    __syncthreads();
+  } else {
+    pass8<4, 1, 0, true>(z, thi, tlo);
+    __syncthreads();
+    pass8<5, 4, 400, true>(z, thi, tlo);
+    __syncthreads();
+    pass8<5, 20, 80, true>(z, thi, tlo);
+    __syncthreads();
+    pass8<5, 100, 16, true>(z, thi, tlo);
+    __syncthreads();
+    pass8<16, 500, 1, true>(z, thi, tlo);
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ int zaddr8(int f) {
+  const int k1 = f & 15, r = f >> 4;  // r = k2 + 5 k3 + 25 k4 + 125 k5
+  const int k2 = r % 5, r2 = r / 5;
+  const int k3 = r2 % 5, r3 = r2 / 5;
+  const int k4 = r3 % 5, k5 = r3 / 5;
+  return 500 * k1 + 100 * k2 + 20 * k3 + 4 * k4 + k5;
+}
+
+// torch_audiomentations AddColoredNoise (per clip, white noise w of ONE second):
+//   n1 = irfft(rfft(w[:16000]) / linspace(1, sqrt(sr/2), 8001)^f_decay)      (16,000)
+//   n1 /= rms(n1) + 1e-8;  noise[t] = n1[t mod 16000], t < T (tiled, not renormalised)
+//   y = x + rms(x) / 10^(snr/20) noise
+// The 16,000 noise samples as 8000 complex pairs in LDS, forward FFT, the
+// real-FFT split x mask x inverse split on (k, M - k) pairs, inverse FFT.
 __global__ void __launch_bounds__(kThreads) colored_noise_kernel(ColoredArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  cf* z = reinterpret_cast<cf*>(smem);
-  float* red = smem + 2 * kM;
-  cf* thi = reinterpret_cast<cf*>(smem + 2 * kM + 32);
-  cf* tlo = thi + kTwHi;
-  load_tw(thi, tlo, a.thi, a.tlo);
-  const cf* twn = reinterpret_cast<const cf*>(a.twn);
+  cf* z = reinterpret_cast<cf*>(smem);                 // kM1 complex
+  float* red = smem + 2 * kM1;                         // 32 floats
+  cf* thi = reinterpret_cast<cf*>(smem + 2 * kM1 + 32);
+  cf* tlo = thi + kTw8Hi;
+  for (int i = threadIdx.x; i < kTw8Hi; i += kThreads) thi[i] = cf{a.thi[i].x, a.thi[i].y};
+  for (int i = threadIdx.x; i < kTw8Lo; i += kThreads) tlo[i] = cf{a.tlo[i].x, a.tlo[i].y};
   float* zf = smem;
   constexpr int kPer = (kT + kThreads - 1) / kThreads;
-  constexpr int kRest = kM / 2 / 16 + 1;  // 361 pairs per k % 16 class
-  unsigned long long ph_t0 = 0;
   for (int64_t clip = blockIdx.x; clip < a.n_clips; clip += gridDim.x) {
     const int tid = opaque_tid();
     const float snr = a.snr_db[clip];
@@ -674,31 +758,27 @@ __global__ void __launch_bounds__(kThreads) colored_noise_kernel(ColoredArgs a) 
         copy_clip(a.x + clip * a.x_stride, a.out + clip * a.out_stride, tid);
       continue;
     }
-    // 1) white noise -> LDS (the previous clip's readers finished at its last barrier)
+    // 1) one second of white noise -> LDS (the previous clip's readers finished at its last barrier)
     if (a.white) {
       const float* w = a.white + clip * a.white_stride;
-      for (int s = tid; s < kT; s += kThreads) zf[s] = w[s];
+      for (int s = tid; s < kN1; s += kThreads) zf[s] = w[s];
     } else {
-      for (int s = tid; s < kT; s += kThreads) zf[s] = gauss(a.seed, static_cast<uint64_t>(clip) * kT + s);
+      for (int s = tid; s < kN1; s += kThreads) zf[s] = gauss(a.seed, static_cast<uint64_t>(clip) * kN1 + s);
     }
     __syncthreads();
-    transform<false>(z, thi, tlo, ph_t0, 0);
-    // 2) X = split(Z); Y = X / lin^f_decay (a real mask); Z' = inverse split(Y)
+    transform8<false>(z, thi, tlo);
+    // 2) X = split(Z); Y = X / lin^f_decay; Z' = inverse split(Y), pairs (k, M - k), k <= M / 2
     const float fd = a.f_decay[clip];
-    for (int idx = tid; idx < 16 * kRest; idx += kThreads) {
-      const int c = idx / kRest;
-      const int k = c + 16 * (idx - c * kRest);
-      if (k > kM / 2) continue;
-      const int kc = (kM - k) % kM;
-      const int p = zaddr(k);
+    for (int k = tid; k <= kM1 / 2; k += kThreads) {
+      const int kc = (kM1 - k) % kM1;
+      const int p = zaddr8(k), pc = zaddr8(kc);
       const cf zk = z[p];
-      const cf zc = z[zaddr(kc)];
+      const cf zc = z[pc];
       const cf fe = 0.5f * cf{zk.x + zc.x, zk.y - zc.y};
       const cf fo = 0.5f * cf{zk.y + zc.y, zc.x - zk.x};
-      const cf wk = twn[hslot(k)];
-      // lin^-f_decay as exp2(-f_decay log2 lin) on the transcendental unit (lin >= 1)
+      const cf wk = cf{a.twn[k].x, a.twn[k].y};  // W_16000^k
       const float mk = exp2f(-fd * __log2f(fmaf(a.lin_step, static_cast<float>(k), 1.f)));
-      const float mc = exp2f(-fd * __log2f(fmaf(a.lin_step, static_cast<float>(kM - k), 1.f)));  // bin M - k
+      const float mc = exp2f(-fd * __log2f(fmaf(a.lin_step, static_cast<float>(kM1 - k), 1.f)));  // bin M - k
       const cf Yk = mk * (fe + cmul(wk, fo));
       const cf Yc = mc * (cf{fe.x, -fe.y} + cmul(cf{-wk.x, wk.y}, cf{fo.x, -fo.y}));
       const cf s1 = 0.5f * cf{Yk.x + Yc.x, Yk.y - Yc.y};
@@ -708,11 +788,11 @@ __global__ void __launch_bounds__(kThreads) colored_noise_kernel(ColoredArgs a) 
       const cf d2 = 0.5f * cf{Yc.x - Yk.x, Yc.y + Yk.y};
       const cf wd2 = cmul(cf{-wk.x, -wk.y}, d2);
       z[p] = s1 + cf{-wd.y, wd.x};
-      if (kc != k) z[zaddr(kc)] = s2 + cf{-wd2.y, wd2.x};
+      if (kc != k) z[pc] = s2 + cf{-wd2.y, wd2.x};
     }
     __syncthreads();
-    transform<true>(z, thi, tlo, ph_t0, 0);  // natural order, x kM
-    // 3) rms(n), rms(x) in one block sum, then y = x + rms(x) 10^(-snr/20) n / (rms(n) + 1e-8)
+    transform8<true>(z, thi, tlo);  // natural order, x kM1
+    // 3) rms(n1) over 16,000 and rms(x) over T in one block sum; tile and mix
     const float* x = a.x + clip * a.x_stride;
     float xr[kPer];
     float ex = 0.f, en = 0.f;
@@ -722,19 +802,21 @@ __global__ void __launch_bounds__(kThreads) colored_noise_kernel(ColoredArgs a) 
       xr[u] = 0.f;
       if (s < kT) {
         xr[u] = x[s];
-        const float nv = zf[s] * (1.f / kM);
         ex += xr[u] * xr[u];
+      }
+      if (s < kN1) {
+        const float nv = zf[s] * (1.f / kM1);
         en += nv * nv;
       }
     }
     block_sum2(ex, en, red);
-    const float rms_x = sqrtf(ex / kT), rms_n = sqrtf(en / kT);
-    const float scale = rms_x / powf(10.f, snr / 20.f) / (rms_n + 1e-8f) * (1.f / kM);
+    const float rms_x = sqrtf(ex / kT), rms_n = sqrtf(en / kN1);
+    const float scale = rms_x / powf(10.f, snr / 20.f) / (rms_n + 1e-8f) * (1.f / kM1);
     float* out = a.out + clip * a.out_stride;
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
       const int s = tid + u * kThreads;
-      if (s < kT) out[s] = fmaf(scale, zf[s], xr[u]);
+      if (s < kT) out[s] = fmaf(scale, zf[s < kN1 ? s : s - kN1], xr[u]);
     }
     __syncthreads();  // zf is rewritten by the next clip
   }
@@ -925,10 +1007,14 @@ struct hbk_reverb_plan {
   float2* thi = nullptr;
   float2* tlo = nullptr;
   float2* twn = nullptr;
+  float2* thi8 = nullptr;  // colored noise: W_8000^(100 h), W_8000^l, W_16000^k (k <= 4000)
+  float2* tlo8 = nullptr;
+  float2* twn16 = nullptr;
 };
 
 namespace {
 constexpr size_t kAugLds = (size_t(2 * hbk::kM + 32) * sizeof(float)) + (hbk::kTwHi + hbk::kTwLo) * sizeof(float2);
+constexpr size_t kColoredLds = (size_t(2 * hbk::kM1 + 32) * sizeof(float)) + (hbk::kTw8Hi + hbk::kTw8Lo) * sizeof(float2);
 }
 
 extern "C" {
@@ -954,6 +1040,19 @@ int hbk_reverb_plan_create(int64_t T, hbk_reverb_plan** plan) {
     const double a = -2.0 * M_PI * i / double(kT);
     tn[(i % 16) * kHRow + i / 16] = make_float2(float(cos(a)), float(sin(a)));
   }
+  std::vector<float2> th8(kTw8Hi), tl8(kTw8Lo), tn16(kM1 / 2 + 1);
+  for (int i = 0; i < kTw8Hi; ++i) {
+    const double a = -2.0 * M_PI * (double(i) * kTw8Lo) / double(kM1);
+    th8[i] = make_float2(float(cos(a)), float(sin(a)));
+  }
+  for (int i = 0; i < kTw8Lo; ++i) {
+    const double a = -2.0 * M_PI * i / double(kM1);
+    tl8[i] = make_float2(float(cos(a)), float(sin(a)));
+  }
+  for (int i = 0; i <= kM1 / 2; ++i) {
+    const double a = -2.0 * M_PI * i / double(kN1);
+    tn16[i] = make_float2(float(cos(a)), float(sin(a)));
+  }
   auto* p = new hbk_reverb_plan();
   hipError_t e;
   if ((e = hipMalloc(&p->thi, kTwHi * sizeof(float2))) != hipSuccess ||
@@ -961,7 +1060,13 @@ int hbk_reverb_plan_create(int64_t T, hbk_reverb_plan** plan) {
       (e = hipMalloc(&p->twn, kHSlots * sizeof(float2))) != hipSuccess ||
       (e = hipMemcpy(p->thi, th.data(), kTwHi * sizeof(float2), hipMemcpyHostToDevice)) != hipSuccess ||
       (e = hipMemcpy(p->tlo, tl.data(), kTwLo * sizeof(float2), hipMemcpyHostToDevice)) != hipSuccess ||
-      (e = hipMemcpy(p->twn, tn.data(), kHSlots * sizeof(float2), hipMemcpyHostToDevice)) != hipSuccess) {
+      (e = hipMemcpy(p->twn, tn.data(), kHSlots * sizeof(float2), hipMemcpyHostToDevice)) != hipSuccess ||
+      (e = hipMalloc(&p->thi8, kTw8Hi * sizeof(float2))) != hipSuccess ||
+      (e = hipMalloc(&p->tlo8, kTw8Lo * sizeof(float2))) != hipSuccess ||
+      (e = hipMalloc(&p->twn16, tn16.size() * sizeof(float2))) != hipSuccess ||
+      (e = hipMemcpy(p->thi8, th8.data(), kTw8Hi * sizeof(float2), hipMemcpyHostToDevice)) != hipSuccess ||
+      (e = hipMemcpy(p->tlo8, tl8.data(), kTw8Lo * sizeof(float2), hipMemcpyHostToDevice)) != hipSuccess ||
+      (e = hipMemcpy(p->twn16, tn16.data(), tn16.size() * sizeof(float2), hipMemcpyHostToDevice)) != hipSuccess) {
     hbk_reverb_plan_destroy(p);
     return hip_error(e, "reverb plan tables");
   }
@@ -971,7 +1076,7 @@ int hbk_reverb_plan_create(int64_t T, hbk_reverb_plan** plan) {
       (e = hipFuncSetAttribute(reinterpret_cast<const void*>(spectrum_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, int(lds))) != hipSuccess ||
       (e = hipFuncSetAttribute(reinterpret_cast<const void*>(colored_noise_kernel),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, int(lds))) != hipSuccess) {
+                               hipFuncAttributeMaxDynamicSharedMemorySize, int(kColoredLds))) != hipSuccess) {
     hbk_reverb_plan_destroy(p);
     return hip_error(e, "hipFuncSetAttribute(augment LDS)");
   }
@@ -984,6 +1089,9 @@ int hbk_reverb_plan_destroy(hbk_reverb_plan* p) {
   (void)hipFree(p->thi);
   (void)hipFree(p->tlo);
   (void)hipFree(p->twn);
+  (void)hipFree(p->thi8);
+  (void)hipFree(p->tlo8);
+  (void)hipFree(p->twn16);
   delete p;
   return HBK_OK;
 }
@@ -1045,8 +1153,11 @@ int hbk_colored_noise(const hbk_reverb_plan* p, const float* x, int64_t n_clips,
   if (n_clips == 0) return HBK_OK;
   if (!x || !out || !f_decay || !snr_db) return arg_error("NULL pointer");
   if (x_stride < kT || out_stride < kT) return arg_error("stride < 23040");
-  if (white && white_stride < kT) return arg_error("white_stride < 23040");
-  if (!(sample_rate > 2.f)) return arg_error("sample_rate must be > 2");
+  if (white && white_stride < kN1) return arg_error("white_stride < 16000");
+  if (sample_rate != float(kN1)) {
+    set_error("hbk: colored noise is generated at 16 kHz (one second = 16000 samples), got %g", double(sample_rate));
+    return HBK_ERR_UNSUPPORTED;
+  }
   ColoredArgs a;
   a.x = x;
   a.x_stride = x_stride;
@@ -1058,12 +1169,12 @@ int hbk_colored_noise(const hbk_reverb_plan* p, const float* x, int64_t n_clips,
   a.seed = seed;
   a.f_decay = f_decay;
   a.snr_db = snr_db;
-  a.lin_step = static_cast<float>((std::sqrt(double(sample_rate) / 2.0) - 1.0) / double(kM));
-  a.thi = p->thi;
-  a.tlo = p->tlo;
-  a.twn = p->twn;
+  a.lin_step = static_cast<float>((std::sqrt(double(kN1) / 2.0) - 1.0) / double(kM1));
+  a.thi = p->thi8;
+  a.tlo = p->tlo8;
+  a.twn = p->twn16;
   const int64_t blocks = std::min<int64_t>(n_clips, persistent_blocks(1));
-  hipLaunchKernelGGL(colored_noise_kernel, dim3(unsigned(blocks)), dim3(kThreads), kAugLds, as_stream(stream), a);
+  hipLaunchKernelGGL(colored_noise_kernel, dim3(unsigned(blocks)), dim3(kThreads), kColoredLds, as_stream(stream), a);
   HBK_LAUNCH_CHECK("colored_noise_kernel");
   return HBK_OK;
 }

@@ -636,15 +636,16 @@ class ReverbPlan:
                       sample_rate: int = 16000) -> torch.Tensor:
         """torch_audiomentations AddColoredNoise on x [n, >= T] -> out [n, T]
         (hbk_colored_noise): per clip f_decay and snr (dB; NaN leaves the clip
-        unchanged); white noise [n, >= T] N(0,1) if given, else the kernel's
-        counter-based stream from ``seed``."""
+        unchanged); one second of white noise per clip ([n, >= 16000] N(0,1))
+        if given, else the kernel's counter-based stream from ``seed``; the
+        coloured second is tiled to T as _gen_noise does."""
         n = x.shape[0]
         if x.dim() != 2 or x.shape[1] < self.T or x.stride(1) != 1 or x.device != self.device:
             raise ValueError(f"x must be [n, >= {self.T}] f32 rows on {self.device}")
-        if white is not None and (white.dim() != 2 or white.shape[0] != n or white.shape[1] < self.T
+        if white is not None and (white.dim() != 2 or white.shape[0] != n or white.shape[1] < 16000
                                   or white.stride(1) != 1 or white.device != self.device
                                   or white.dtype != torch.float32):
-            raise ValueError(f"white must be [n, >= {self.T}] f32 rows on {self.device}")
+            raise ValueError(f"white must be [n, >= 16000] f32 rows on {self.device}")
         if out is None:
             out = torch.empty((n, self.T), dtype=torch.float32, device=self.device)
 

@@ -275,13 +275,15 @@ int hbk_augment(const hbk_reverb_plan* plan, const float* x, int64_t n_clips, in
 /* Colored noise: torch_audiomentations AddColoredNoise, which the reference's
  * batch chain applies per batch with p 0.25 (dataset/augmented.py:107-113,
  * constants.py:128-132). Per clip i of x [n_clips, x_stride] (first T = 23040
- * samples used):
- *   w = white[i] (N(0,1) [T], white_stride >= T) or, if white == NULL, the
- *       counter-based N(0,1) stream (seed, i * T + t);
- *   n = irfft(rfft(w) / linspace(1, sqrt(sample_rate / 2), T/2 + 1)^f_decay[i]);
- *   out[i] = x[i] + rms(x[i]) / 10^(snr_db[i] / 20) * n / (rms(n) + 1e-8);
+ * samples used), the package's _gen_noise / apply_transform:
+ *   w = white[i][0 .. 16000) (N(0,1), white_stride >= 16000) or, if white ==
+ *       NULL, the counter-based N(0,1) stream (seed, i * 16000 + t);
+ *   n1 = irfft(rfft(w) / linspace(1, sqrt(8000), 8001)^f_decay[i], n = 16000);
+ *   n1 /= rms(n1) + 1e-8;  noise[t] = n1[t mod 16000] (tiled to T, not renormalised);
+ *   out[i] = x[i] + rms(x[i]) / 10^(snr_db[i] / 20) * noise;
  *   snr_db[i] NaN: out[i] = x[i] (a batch whose coin came up tails).
- * out may equal x. Uses hbk_reverb_plan's FFT tables. Device pointers. */
+ * sample_rate must be 16000 (the noise is one second long). out may equal x.
+ * Device pointers. */
 int hbk_colored_noise(const hbk_reverb_plan* plan, const float* x, int64_t n_clips, int64_t x_stride,
                       const float* white, int64_t white_stride, uint64_t seed, const float* f_decay,
                       const float* snr_db, float sample_rate, float* out, int64_t out_stride, void* stream);

@@ -86,16 +86,29 @@ def reverberate(x: np.ndarray, ir: np.ndarray, dtype=np.float64) -> np.ndarray:
     return a_in * y / (np.abs(y).mean(axis=-1, keepdims=True) + 1e-14)
 
 
-def colored_noise(x, white, f_decay, snr_db, sample_rate: int = 16000, dtype=np.float64) -> np.ndarray:
-    """AddColoredNoise.apply_transform / _gen_noise with the white noise given."""
-    x = np.asarray(x, dtype=dtype)
-    w = np.asarray(white, dtype=dtype)
-    T = x.shape[-1]
+def gen_colored_noise(white, f_decay, num_samples: int, sample_rate: int = 16000, dtype=np.float64):
+    """torch_audiomentations' _gen_noise (AddColoredNoise, the reference's batch
+    chain, augmented.py:107-113) with the white noise given: ``sample_rate``
+    N(0,1) samples (ONE second), rfft, mask 1 / linspace(1, sqrt(sr/2),
+    sr/2 + 1)^f_decay, irfft (n = sr), RMS-normalise (/ (rms + 1e-8)), then
+    TILE to num_samples (ceil(num_samples / sr) copies, cut). torch_audiomentations
+    is not installed here: restated from its published source (lower bound pinned
+    by the reference's environment.yml); parity unpinned against the package."""
+    w = np.asarray(white, dtype=dtype)[..., :sample_rate]
     spec = np.fft.rfft(w, axis=-1)
     lin = np.linspace(1.0, np.sqrt(sample_rate / 2.0), spec.shape[-1])
     fd = np.asarray(f_decay, dtype=dtype).reshape(-1, 1)
-    n = np.fft.irfft(spec / lin[None, :] ** fd, n=T, axis=-1)
+    n = np.fft.irfft(spec / lin[None, :] ** fd, n=sample_rate, axis=-1)
     n = n / (np.sqrt((n * n).mean(axis=-1, keepdims=True)) + 1e-8)
+    reps = -(-num_samples // sample_rate)
+    return np.concatenate([n] * reps, axis=-1)[..., :num_samples]
+
+
+def colored_noise(x, white, f_decay, snr_db, sample_rate: int = 16000, dtype=np.float64) -> np.ndarray:
+    """AddColoredNoise.apply_transform with the white noise given:
+    y = x + rms(x) / 10^(snr/20) * noise, rms over the clip (calculate_rms)."""
+    x = np.asarray(x, dtype=dtype)
+    n = gen_colored_noise(white, f_decay, x.shape[-1], sample_rate, dtype)
     rms_x = np.sqrt((x * x).mean(axis=-1, keepdims=True))
     return x + rms_x / 10.0 ** (np.asarray(snr_db, dtype=dtype).reshape(-1, 1) / 20.0) * n
 

@@ -265,23 +265,30 @@ def test_batch_plan_consumes_whole_noise_clips_per_batch():
 # installed, no fixture): oracle/augment.py restates AddColoredNoise; the white
 # noise is an explicit input on both sides. Same tolerance as above.
 
+N1 = 16000  # torch_audiomentations _gen_noise: ONE second of noise, tiled to the clip
+
+
 def test_colored_noise_oracle_properties():
     rng = np.random.default_rng(21)
     x = _clips(3, seed=21)
-    w = rng.standard_normal((3, T))
+    w = rng.standard_normal((3, N1))
     snr = np.array([10.0, 20.0, 30.0])
-    # f_decay 0: the noise is the white noise, rms-normalised
-    y = oaug.colored_noise(x, w, np.zeros(3), snr)
     rms = lambda v: np.sqrt((v * v).mean(axis=-1))
+    # f_decay 0: the noise is the white second, rms-normalised, tiled to T
+    y = oaug.colored_noise(x, w, np.zeros(3), snr)
     n = (y - x) / (rms(x) / 10 ** (snr / 20))[:, None]
-    np.testing.assert_allclose(n, w / (rms(w)[:, None] + 1e-8), atol=1e-9)
-    # any f_decay: the added noise sits exactly snr dB below the clip (up to the 1e-8 guard)
+    wn = w / (rms(w)[:, None] + 1e-8)
+    np.testing.assert_allclose(n[:, :N1], wn, atol=1e-9)
+    np.testing.assert_allclose(n[:, N1:], wn[:, :T - N1], atol=1e-9)
+    # any f_decay: period 16,000, and the first second sits exactly snr dB below the clip
     fd = np.array([-1.0, 0.7, 2.0])
     y = oaug.colored_noise(x, w, fd, snr)
-    np.testing.assert_allclose(20 * np.log10(rms(x) / rms(y - x)), snr, atol=1e-6)
-    # the noise spectrum is the white spectrum shaped by linspace(1, sqrt(8000), T/2+1)^-f_decay
-    lin = np.linspace(1.0, np.sqrt(8000.0), T // 2 + 1)
-    ratio = np.abs(np.fft.rfft(y - x)) / np.abs(np.fft.rfft(w))
+    d = y - x
+    np.testing.assert_allclose(d[:, N1:], d[:, :T - N1], rtol=0, atol=1e-12)
+    np.testing.assert_allclose(20 * np.log10(rms(x) / rms(d[:, :N1])), snr, atol=1e-6)
+    # the noise spectrum is the white spectrum shaped by linspace(1, sqrt(8000), 8001)^-f_decay
+    lin = np.linspace(1.0, np.sqrt(8000.0), N1 // 2 + 1)
+    ratio = np.abs(np.fft.rfft(d[:, :N1])) / np.abs(np.fft.rfft(w))
     for i in range(3):
         shape = ratio[i] / ratio[i, 1]
         np.testing.assert_allclose(shape[1:], (lin[1:] / lin[1]) ** -fd[i], rtol=1e-6)
@@ -292,7 +299,7 @@ def test_colored_noise_parity():
     from heybuddy.kernels import ReverbPlan
     plan = ReverbPlan()
     x = _clips(5, seed=22)
-    w = np.random.default_rng(23).standard_normal((5, T)).astype(np.float32)
+    w = np.random.default_rng(23).standard_normal((5, N1)).astype(np.float32)
     fd = np.array([-1.0, 0.0, 0.5, 1.3, 2.0], dtype=np.float32)
     snr = np.array([10.0, 15.0, 20.0, 25.0, 30.0], dtype=np.float32)
     out = plan.colored_noise(torch.from_numpy(x).float().cuda(), torch.from_numpy(fd), torch.from_numpy(snr),
@@ -301,6 +308,9 @@ def test_colored_noise_parity():
     for i in range(5):
         ok, worst = _close(out[i], ref[i])
         assert ok, f"clip {i}: max |diff| {worst}"
+    # the added noise repeats with the 16,000-sample period of torch_audiomentations' one-second noise
+    d = out - x.astype(np.float32)
+    np.testing.assert_allclose(d[:, N1:], d[:, :T - N1], rtol=0, atol=2e-6 * np.abs(d).max())
 
 
 @pytest.mark.gpu
@@ -319,7 +329,7 @@ def test_colored_noise_nan_snr_skips_and_generated_stream():
     rms = lambda v: np.sqrt((v * v).mean())
     for i, s in ((0, 12.0), (2, 25.0)):
         n = os_[i] - xs[i]
-        assert abs(20 * np.log10(rms(xs[i]) / rms(n)) - s) < 1e-3
+        assert abs(20 * np.log10(rms(xs[i]) / rms(n[:N1])) - s) < 1e-3
         # f_decay 0: the generated stream itself, normalised: ~N(0, 1) moments
         z = n / rms(n)
         assert abs(z.mean()) < 0.03 and abs((z ** 4).mean() - 3.0) < 0.2
@@ -340,7 +350,7 @@ def test_batch_augmenter_colored_noise_is_per_batch():
     out = aug(x)
     xs, os_ = x.cpu().double().numpy(), out.cpu().double().numpy()
     rms = lambda v: np.sqrt((v * v).mean(axis=-1))
-    snr = 20 * np.log10(rms(xs) / rms(os_ - xs))
+    snr = 20 * np.log10(rms(xs) / rms((os_ - xs)[:, :N1]))  # the noise's first (normalised) second
     for b0 in range(0, 300, 128):
         blk = snr[b0:b0 + 128]
         assert blk.max() - blk.min() < 1e-3
