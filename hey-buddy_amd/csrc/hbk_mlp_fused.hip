@@ -1,6 +1,6 @@
 // Fused wake-word classifier train step for gfx950 (default architecture:
-// d_in = 16 x 96 = 1536, layer_dim 96, hidden get_normalized_dim(96) = 64, any
-// number of layers up to kMaxG - 2).
+// d_in = 16 x 96 = 1536, layer_dim 96, hidden get_normalized_dim(96) = 64,
+// 0..2 layers; other plans use the generic GEMM path of hbk_mlp.hip).
 //
 // Replaces, per optimisation step of WakeWordTrainer.train_epoch
 // (trainer.py:380-494), the reference's forward (wakeword.py:334-348), the
@@ -53,7 +53,7 @@ typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 
 constexpr int kD = 1536, kL = 96, kH = 64, kH2 = 128;
 constexpr int kR = 16;            // rows per tile = MFMA M
-constexpr int kMaxG = 6;          // gated MLPs held by k2 (n_layers <= 4)
+constexpr int kMaxG = 4;          // gated MLPs held by k2 (n_layers <= 2: the LDS budget)
 constexpr int kStats = 8;
 constexpr float kLnEps = 1e-5f;
 constexpr int kLd = 132;          // LDS row stride of [16][<=128] activation tiles
@@ -313,25 +313,25 @@ struct WReg {
   float v[kWRegs];
 };
 
+// Loads are unconditional: a tile past N reads a clamped (valid) row and its
+// product is discarded by the caller. A load under a lane predicate becomes a
+// branch whose join copies the value, i.e. an s_waitcnt vmcnt(0) right after
+// the load, which serialises the whole prefetch.
 template <int K, int N, bool NT>
 __device__ __forceinline__ void load_w(WReg& w, const float* __restrict__ W, int wave, int lane) {
-  constexpr int kTiles = (N + 15) / 16;
   const int m = lane & 15, kq = lane >> 4;
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt) {
-    const int t = wave + 4 * tt;
-    const int n = 16 * t + m;
-    const bool ok = t < kTiles && n < N;
+    const int n = min(16 * (wave + 4 * tt) + m, N - 1);
 #pragma unroll
     for (int i = 0; i < K / 16; ++i) {
       if (NT) {
-        f4 q = {0.f, 0.f, 0.f, 0.f};
-        if (ok) q = *reinterpret_cast<const f4*>(W + n * K + 16 * i + 4 * kq);
+        const f4 q = *reinterpret_cast<const f4*>(W + n * K + 16 * i + 4 * kq);
 #pragma unroll
         for (int s = 0; s < 4; ++s) w.v[tt * (K / 4) + 4 * i + s] = q[s];
       } else {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) w.v[tt * (K / 4) + 4 * i + s] = ok ? W[(16 * i + 4 * kq + s) * N + n] : 0.f;
+        for (int s = 0; s < 4; ++s) w.v[tt * (K / 4) + 4 * i + s] = W[(16 * i + 4 * kq + s) * N + n];
       }
     }
   }
@@ -394,70 +394,158 @@ struct K2Args {
   float* dHG;
 };
 
-template <bool kTrain>
+// Backward weights go through LDS: W_hg [128][96] and W_o [96][64] are read
+// there as NN B fragments (dx = dy W: one scalar per lane per MFMA, 16 lanes of a
+// k-group on consecutive columns); they are loaded cooperatively with coalesced
+// float4 loads two stages ahead and written to LDS one stage ahead of use.
+constexpr int kWX = kH2 * kL, kWY = kL * kH;  // 12,288 and 6,144 floats
+template <int N>
+__device__ __forceinline__ void coop_load(f4 (&r)[N], const float* __restrict__ src, int tid) {
+#pragma unroll
+  for (int u = 0; u < N; ++u) r[u] = *reinterpret_cast<const f4*>(src + 4 * (tid + 256 * u));
+}
+template <int N>
+__device__ __forceinline__ void coop_store(float* dst, const f4 (&r)[N], int tid) {
+#pragma unroll
+  for (int u = 0; u < N; ++u) *reinterpret_cast<f4*>(dst + 4 * (tid + 256 * u)) = r[u];
+}
+// NN product from an LDS weight matrix W [K][N]: tiles w and w + 4 (two chains)
+template <int K, int N>
+__device__ __forceinline__ void gemm2_lds(const float* W, const float* A, int wave, int lane, f4& c0, f4& c1) {
+  const int m = lane & 15, kq = lane >> 4;
+  const int n0 = 16 * wave + m, n1 = min(16 * (wave + 4) + m, N - 1);  // tile w + 4 past N: discarded
+  c0 = f4{0.f, 0.f, 0.f, 0.f};
+  c1 = c0;
+#pragma unroll
+  for (int i = 0; i < K / 16; ++i) {
+    const f4 av = *reinterpret_cast<const f4*>(A + m * kLd + 16 * i + 4 * kq);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int k = 16 * i + 4 * kq + s;
+      c0 = mma(av[s], W[k * N + n0], c0);
+      c1 = mma(av[s], W[k * N + n1], c1);
+    }
+  }
+}
+// one tile (w), two chains over the even / odd 16-k blocks
+template <int K, int N>
+__device__ __forceinline__ f4 gemm1_lds(const float* W, const float* A, int wave, int lane) {
+  const int m = lane & 15, kq = lane >> 4;
+  const int n0 = 16 * wave + m;
+  f4 c[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int i = 0; i < K / 16; ++i) {
+    const f4 av = *reinterpret_cast<const f4*>(A + m * kLd + 16 * i + 4 * kq);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) c[i & 1] = mma(av[s], W[(16 * i + 4 * kq + s) * N + n0], c[i & 1]);
+  }
+  return c[0] + c[1];
+}
+
+#ifdef HBK_TRACE
+#define K2_MARK(id)                                                                \
+  do {                                                                             \
+    if (blockIdx.x == 0 && lane == 0 && trn < 48)                                  \
+      trS[wave][trn++] = (static_cast<unsigned long long>(id) << 56) |             \
+                         (__builtin_amdgcn_s_memtime() & 0xFFFFFFFFFFFFFFull);     \
+  } while (0)
+#else
+#define K2_MARK(id) \
+  do {              \
+  } while (0)
+#endif
+
+// NG (= n_layers + 2 gated MLPs) is a template argument: every stage below is
+// straight-line code, so the register prefetches and their waits are exact.
+template <bool kTrain, int NG>
 __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
-  HBK_MT(1, 1);
-  __shared__ __attribute__((aligned(16))) float hgS[kMaxG][kR][kLd];
-  __shared__ __attribute__((aligned(16))) float xhS[kMaxG - 1][kR][kL + 4];
+  __shared__ __attribute__((aligned(16))) float hgS[NG][kR][kLd];
+  __shared__ __attribute__((aligned(16))) float xhS[NG - 1][kR][kL + 4];
   __shared__ __attribute__((aligned(16))) float bX[kR][kLd];   // LN output (forward) / dHG (backward)
   __shared__ __attribute__((aligned(16))) float bU[kR][kLd];   // gate output (forward) / dXn (backward)
   __shared__ __attribute__((aligned(16))) float bS[kR][kLd];   // GMLP output (forward) / dS (backward)
-  __shared__ float rsS[kMaxG][kR];
+  __shared__ __attribute__((aligned(16))) float wX[kTrain ? kWX : 4];  // backward W_hg_k
+  __shared__ __attribute__((aligned(16))) float wY[kTrain ? kWY : 4];  // backward W_o_k
+  __shared__ float rsS[NG][kR];
   __shared__ float zS[kR], dzS[kR];
   __shared__ float red[kStats];
-  // every bias / LayerNorm affine / the output unit's weights, loaded once
-  __shared__ float sBo[kMaxG][kL], sBhg[kMaxG][kH2], sLg[kMaxG][kL], sLb[kMaxG][kL], sWo[kH];
+  __shared__ float sBo[NG][kL], sBhg[NG][kH2], sLg[NG][kL], sLb[NG][kL], sWo[kH];
+#ifdef HBK_TRACE
+  __shared__ unsigned long long trS[4][48];
+  int trn = 0;
+#endif
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int m = lane & 15, kq = lane >> 4;
   const int r0 = blockIdx.x * kR;
   const int nrow = min(kR, a.B - r0);
   const float* P = a.P;
-  const int NG = a.NG;
   const int64_t B = a.B;
+  const int64_t Bp = a.Bp;
+  K2_MARK(1);
+  // step, label and negative weight of this workgroup's rows (used by the loss,
+  // loaded now so their two dependent latencies hide under the forward pass)
+  const int step = step_of(a.state, a.parity);
+  float y_pre = 0.f, nw_pre = a.neg_weight;
+  if (kTrain) {
+    y_pre = a.y[static_cast<int64_t>(step) * a.y_stride + min(r0 + (tid & 15), a.B - 1)];
+    if (a.sched) nw_pre = a.sched[2 * min(step, a.sched_len - 1) + 1];
+  }
   WReg wa, wb;
   load_w<kH, kL, true>(wa, P + a.w_o[0], wave, lane);
-  for (int k = 0; k < NG; ++k) {
-    const int out = k + 1 < NG ? kL : 1;
-    for (int c = tid; c < kH2; c += 256) sBhg[k][c] = P[a.b_hg[k] + c];
-    for (int c = tid; c < out; c += 256) sBo[k][c] = P[a.b_o[k] + c];
-    if (k + 1 < NG)
-      for (int c = tid; c < kL; c += 256) {
-        sLg[k][c] = P[a.ln_g[k] + c];
-        sLb[k][c] = P[a.ln_b[k] + c];
+  {  // small parameters: all loads issued unconditionally, then stored
+    const int c2 = tid & (kH2 - 1), c1 = min(tid, kL - 1);
+    float vbhg[NG], vbo[NG], vlg[NG], vlb[NG];
+#pragma unroll
+    for (int k = 0; k < NG; ++k) {
+      vbhg[k] = P[a.b_hg[k] + c2];
+      vbo[k] = P[a.b_o[k] + (k + 1 < NG ? c1 : 0)];
+      vlg[k] = k + 1 < NG ? P[a.ln_g[k] + c1] : 0.f;
+      vlb[k] = k + 1 < NG ? P[a.ln_b[k] + c1] : 0.f;
+    }
+    const float vwo = P[a.w_o[NG - 1] + (tid & (kH - 1))];
+#pragma unroll
+    for (int k = 0; k < NG; ++k) {
+      if (tid < kH2) sBhg[k][tid] = vbhg[k];
+      if (tid < (k + 1 < NG ? kL : 1)) sBo[k][tid] = vbo[k];
+      if (k + 1 < NG && tid < kL) {
+        sLg[k][tid] = vlg[k];
+        sLb[k][tid] = vlb[k];
       }
+    }
+    if (tid < kH) sWo[tid] = vwo;
   }
-  if (tid < kH) sWo[tid] = P[a.w_o[NG - 1] + tid];
   // HG0 = sum of k1's KS partial slabs + bias; U0 = silu(H) G. Thread ->
-  // 4 (row, j) pairs; the slab loads are issued 4 slabs at a time.
+  // 4 (row, j) pairs; the slab loads are issued 4 slabs at a time (rows past B
+  // read row B - 1: their values are finite and every gradient they feed is
+  // multiplied by dz = 0).
   {
     float h[4] = {0.f, 0.f, 0.f, 0.f}, g[4] = {0.f, 0.f, 0.f, 0.f};
     for (int s0 = 0; s0 < a.KS; s0 += 4) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        if (s0 + u < a.KS) {
+        const int sl = min(s0 + u, a.KS - 1);
+        const float on = s0 + u < a.KS ? 1.f : 0.f;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int e = tid + 256 * q, r = e >> 6, j = e & 63;
-            if (r < nrow) {
-              const float* src = a.hg_part + ((s0 + u) * B + r0 + r) * kH2;
-              h[q] += src[j];
-              g[q] += src[kH + j];
-            }
-          }
+        for (int q = 0; q < 4; ++q) {
+          const int e = tid + 256 * q, r = min(e >> 6, nrow - 1), j = e & 63;
+          const float* src = a.hg_part + (sl * B + r0 + r) * kH2;
+          h[q] += on * src[j];
+          g[q] += on * src[kH + j];
         }
       }
     }
+    const float bh = P[a.b_hg[0] + (tid & 63)], bg = P[a.b_hg[0] + kH + (tid & 63)];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int e = tid + 256 * q, r = e >> 6, j = e & 63;
-      const float hh = h[q] + P[a.b_hg[0] + j], gg = g[q] + P[a.b_hg[0] + kH + j];
+      const float hh = h[q] + bh, gg = g[q] + bg;
       hgS[0][r][j] = hh;
       hgS[0][r][kH + j] = gg;
       bU[r][j] = hh * sigm(hh) * gg;
     }
   }
-  __syncthreads(); HBK_MT(1, 11);
-  const int64_t Bp = a.Bp;
+  __syncthreads();
+  K2_MARK(2);
   // transposed activation stores: 4 consecutive rows of one column per float4
   auto st4 = [&](float* base, int col, int row4, f4 v) {
 #pragma unroll
@@ -470,6 +558,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
     st4(a.U, j, rg, f4{bU[rg][j], bU[rg + 1][j], bU[rg + 2][j], bU[rg + 3][j]});
   }
   // ---------------------------------------------------------- forward ----
+#pragma unroll
   for (int k = 0; k + 1 < NG; ++k) {
     // S_k = U_k W_o_k^T + b_o_k  -> bS   (weights in wa; prefetch HG_{k+1}'s into wb)
     load_w<kL, kH2, true>(wb, P + a.w_hg[k + 1], wave, lane);
@@ -485,8 +574,10 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
         for (int e = 0; e < 4; ++e) bS[4 * kq + e][n1] = c1[e] + bo1;
       }
     }
-    __syncthreads(); HBK_MT(1, 12);
+    __syncthreads();
+    K2_MARK(10 + k);
     // LayerNorm k over 96 columns: wave w -> rows 4w..4w+3, lane -> c, c + 64
+    if (k + 2 < NG) load_w<kH, kL, true>(wa, P + a.w_o[k + 1], wave, lane);
     {
       const bool hi = lane < kL - 64;
       const float g0 = sLg[k][lane], b0 = sLb[k][lane];
@@ -500,11 +591,10 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
         const float d0 = v0 - mu, d1 = hi ? v1 - mu : 0.f;
         const float rs = 1.f / sqrtf(wsum(d0 * d0 + d1 * d1) * (1.f / kL) + kLnEps);
         const float x0 = d0 * rs, x1 = d1 * rs;
-        const float n0 = x0 * g0 + b0;
+        const float n0 = x0 * g0 + b0, n1 = x1 * g1 + b1;
         xhS[k][r][lane] = x0;
         bX[r][lane] = n0;
         o0[i] = n0;
-        const float n1 = x1 * g1 + b1;
         o1[i] = n1;
         if (hi) {
           xhS[k][r][64 + lane] = x1;
@@ -518,9 +608,9 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
         if (hi) st4(xt, 64 + lane, 4 * wave, o1);
       }
     }
-    __syncthreads(); HBK_MT(1, 13);
+    __syncthreads();
+    K2_MARK(20 + k);
     // HG_{k+1} = Xn W_hg^T + b, gate in the epilogue -> hgS[k+1], U_{k+1} -> bU
-    if (k + 2 < NG) load_w<kH, kL, true>(wa, P + a.w_o[k + 1], wave, lane);
     {
       f4 ch, cg;
       gemm2<kL>(wb, &bX[0][0], lane, ch, cg);
@@ -539,7 +629,14 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
       }
       if (kTrain) st4(a.U + (k + 1) * kH * Bp, j, 4 * kq, uo);
     }
-    __syncthreads(); HBK_MT(1, 14);
+    __syncthreads();
+    K2_MARK(30 + k);
+  }
+  // backward weights of the first two backward matrix stages: W_hg_{NG-1}, W_o_{NG-2}
+  f4 rX[kWX / 1024], rY[kWY / 1024];
+  if (kTrain) {
+    coop_load(rX, P + a.w_hg[NG - 1], tid);
+    coop_load(rY, P + a.w_o[NG - 2], tid);
   }
   // output unit: z = U . w_o + b_o (wave w -> rows 4w..4w+3)
   {
@@ -552,8 +649,8 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
       if (lane == 0) zS[r] = z;
     }
   }
-  __syncthreads(); HBK_MT(1, 15);
-  const int step = step_of(a.state, a.parity);
+  __syncthreads();
+  K2_MARK(40);
   // sigmoid, high-loss filter (trainer.py:407-424), weighted BCE (:301-312, torch
   // formulas incl. the log clamp at -100 and the 1e-12 in BCE's backward)
   if (tid < kR) {
@@ -565,9 +662,8 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
       if (a.prob) a.prob[r0 + r] = p;
       if (a.logit) a.logit[r0 + r] = z;
       if (kTrain) {
-        float nw = a.neg_weight;
-        if (a.sched) nw = a.sched[2 * min(step, a.sched_len - 1) + 1];
-        const float yy = a.y[static_cast<int64_t>(step) * a.y_stride + r0 + r];
+        const float nw = nw_pre;
+        const float yy = y_pre;
         const bool pos = yy == 1.f;
         const bool sel = pos ? (p < 1.f - a.thr) : (p >= a.thr);
         if (sel) {
@@ -596,11 +692,12 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
       }
     }
   }
-  if (!kTrain) return;
-  // backward weights: dU = dS W_o (NN) of GMLP NG-2, dXn = dHG W_hg (NN) of GMLP NG-1
-  load_w<kL, kH, false>(wa, P + a.w_o[NG - 2], wave, lane);
-  load_w<kH2, kL, false>(wb, P + a.w_hg[NG - 1], wave, lane);
-  __syncthreads(); HBK_MT(1, 16);
+  if constexpr (!kTrain) return;
+  // write the first backward weights (their loads overlapped z and the loss)
+  coop_store(wX, rX, tid);
+  coop_store(wY, rY, tid);
+  __syncthreads();
+  K2_MARK(41);
   if (tid < kStats && red[tid] != 0.f) atomicAdd(a.stats + tid, red[tid]);
   // ---------------------------------------------------------- backward ---
   float* G = a.G;
@@ -630,7 +727,9 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
     st4(a.dHG + k * kH2 * Bp, j, rg, dho);
     st4(a.dHG + k * kH2 * Bp, kH + j, rg, dgo);
   }
-  __syncthreads(); HBK_MT(1, 17);
+  __syncthreads();
+  K2_MARK(42);
+#pragma unroll
   for (int k = NG - 1; k >= 1; --k) {
     // bias gradient of hidden + gate k: column sums of dHG_k (bX)
     if (tid < kH2) {
@@ -638,10 +737,12 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
       for (int r = 0; r < kR; ++r) s += bX[r][tid];
       atomicAdd(G + a.b_hg[k] + tid, s);
     }
-    // dXn = dHG_k W_hg_k (NN: K 128 -> N 96, weights in wb) -> bU
+    // dXn = dHG_k W_hg_k (NN: K 128 -> N 96, W in wX) -> bU
+    if (k < NG - 1) coop_store(wY, rY, tid);    // W_o_{k-1} (wY is free: dU_k is done)
+    if (k - 1 >= 1) coop_load(rX, P + a.w_hg[k - 1], tid);
     {
       f4 c0, c1;
-      gemm2<kH2>(wb, &bX[0][0], lane, c0, c1);
+      gemm2_lds<kH2, kL>(wX, &bX[0][0], wave, lane, c0, c1);
       const int n0 = 16 * wave + m, n1 = 16 * (wave + 4) + m;
 #pragma unroll
       for (int e = 0; e < 4; ++e) bU[4 * kq + e][n0] = c0[e];
@@ -650,8 +751,11 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
         for (int e = 0; e < 4; ++e) bU[4 * kq + e][n1] = c1[e];
       }
     }
-    __syncthreads(); HBK_MT(1, 18);
+    __syncthreads();
+    K2_MARK(50 + k);
     // LayerNorm k-1 backward: gamma / beta column sums, dS_{k-1} per row -> bS
+    if (k - 1 >= 1) coop_store(wX, rX, tid);     // W_hg_{k-1} (wX is free: dXn_k is done)
+    if (k - 2 >= 0) coop_load(rY, P + a.w_o[k - 2], tid);
     {
       const int l = k - 1;
       if (tid < kL) {
@@ -685,9 +789,10 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
       st4(a.dS + l * kL * Bp, lane, 4 * wave, o0);
       if (hi) st4(a.dS + l * kL * Bp, 64 + lane, 4 * wave, o1);
     }
-    __syncthreads(); HBK_MT(1, 19);
-    // GMLP k-1: output bias gradient (column sums of dS), dU = dS W_o (NN: K 96 -> N 64)
-    // with the gate backward in the epilogue -> dHG_{k-1} (bX)
+    __syncthreads();
+    K2_MARK(60 + k);
+    // GMLP k-1: output bias gradient (column sums of dS), dU = dS W_o (NN: K 96 -> N 64,
+    // W in wY) with the gate backward in the epilogue -> dHG_{k-1} (bX)
     {
       const int kk = k - 1;
       if (tid < kL) {
@@ -695,11 +800,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
         for (int r = 0; r < kR; ++r) s += bS[r][tid];
         atomicAdd(G + a.b_o[kk] + tid, s);
       }
-      const f4 du = gemm1<kL>(wa, &bS[0][0], lane);
-      if (kk >= 1) {  // the next iteration's weights
-        load_w<kL, kH, false>(wa, P + a.w_o[kk - 1], wave, lane);
-        load_w<kH2, kL, false>(wb, P + a.w_hg[kk], wave, lane);
-      }
+      const f4 du = gemm1_lds<kL, kH>(wY, &bS[0][0], wave, lane);
       const int j = 16 * wave + m;
       f4 dho, dgo;
 #pragma unroll
@@ -716,7 +817,8 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
       st4(a.dHG + kk * kH2 * Bp, j, 4 * kq, dho);
       st4(a.dHG + kk * kH2 * Bp, kH + j, 4 * kq, dgo);
     }
-    __syncthreads(); HBK_MT(1, 20);
+    __syncthreads();
+    K2_MARK(70 + k);
   }
   // bias gradient of mlp_in's hidden + gate
   if (tid < kH2) {
@@ -724,7 +826,13 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
     for (int r = 0; r < kR; ++r) s += bX[r][tid];
     atomicAdd(G + a.b_hg[0] + tid, s);
   }
-  HBK_MT(1, 99);
+  K2_MARK(99);
+#ifdef HBK_TRACE
+  if (blockIdx.x == 0 && lane == 0) {
+    for (int i = 0; i < trn; ++i) g_mlp_trace[1][wave][i] = trS[wave][i];
+    g_mlp_trace_n[1][wave] = trn;
+  }
+#endif
 }
 
 // ------------------------------------------------------------------ k3 ----
@@ -830,25 +938,32 @@ __global__ void __launch_bounds__(256) k3_wgrad_kernel(K3Args a) {
   __syncthreads();
   float dg0 = 0.f, dg1 = 0.f, dbt0 = 0.f, dbt1 = 0.f;
   const int c0 = n0 + m, c1 = n0 + 16 + m;
-  const float g0 = nok0 ? a.g_in[c0] : 0.f, g1 = nok1 ? a.g_in[c1] : 0.f;
-  const float be0 = nok0 ? a.b_in[c0] : 0.f, be1 = nok1 ? a.b_in[c1] : 0.f;
+  // every epilogue load is issued up front at clamped (valid) addresses, so none
+  // sits behind an atomic in a predicated branch
+  const int c0c = min(c0, jb.N - 1), c1c = min(c1, jb.N - 1);
+  const float g0 = a.g_in[c0c], g1 = a.g_in[c1c];
+  const float be0 = a.b_in[c0c], be1 = a.b_in[c1c];
+  float w0[4], w1[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float* wr = a.W0 + static_cast<int64_t>(min(mrow + 4 * kq + e, jb.M - 1)) * jb.ldc;
+    w0[e] = wr[c0c];
+    w1[e] = wr[c1c];
+  }
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int row = mrow + 4 * kq + e;  // j
     if (row >= jb.M) continue;
     const float sj = sS[16 * wave + 4 * kq + e];
-    const float* wr = a.W0 + static_cast<int64_t>(row) * jb.ldc;
     if (nok0) {
       atomicAdd(jb.C + static_cast<int64_t>(row) * jb.ldc + c0, g0 * acc0[e] + be0 * sj);
-      const float w = wr[c0];
-      dg0 += w * acc0[e];
-      dbt0 += w * sj;
+      dg0 += w0[e] * acc0[e];
+      dbt0 += w0[e] * sj;
     }
     if (nok1) {
       atomicAdd(jb.C + static_cast<int64_t>(row) * jb.ldc + c1, g1 * acc1[e] + be1 * sj);
-      const float w = wr[c1];
-      dg1 += w * acc1[e];
-      dbt1 += w * sj;
+      dg1 += w1[e] * acc1[e];
+      dbt1 += w1[e] * sj;
     }
   }
   // reduce over kq (lanes m + 16 q) then over waves
@@ -899,14 +1014,16 @@ struct K4Args {
 __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
   const float* st = a.state + a.parity * 8;
   const float* stats = a.G + a.n;
-  const float n_sel = stats[0];
+  // statistics read before any store (the history row copies them)
+  const float n_sel = stats[0], s_loss = stats[1], s_neg = stats[2], s_fp = stats[3], s_pos = stats[4],
+              s_tp = stats[5];
   float acc_samples = st[0], acc_steps = st[1], t = st[2];
   const float stepf = st[3];
   const int step = static_cast<int>(stepf);
   float fire = 0.f, scale = 0.f, loss = 0.f;
   const float used = acc_steps;
   if (n_sel > 0.f) {
-    loss = stats[1] / n_sel / acc_steps;
+    loss = s_loss / n_sel / acc_steps;
     acc_samples += n_sel;
     if (acc_samples < 128.f) {
       acc_steps += 1.f;
@@ -931,10 +1048,10 @@ __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
       h[1] = used;
       h[2] = fire;
       h[3] = loss;
-      h[4] = stats[2];
-      h[5] = stats[3];
-      h[6] = stats[4];
-      h[7] = stats[5];
+      h[4] = s_neg;
+      h[5] = s_fp;
+      h[6] = s_pos;
+      h[7] = s_tp;
     }
   }
   float lr = a.lr;
@@ -1089,13 +1206,20 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
   k2.dS = ws + w.dS;
   k2.dHG = ws + w.dHG;
   k2.Bp = Bp;
-  if (!train) {
-    hipLaunchKernelGGL(k2_rows_kernel<false>, dim3(rt), dim3(256), 0, s, k2);
+  {
+    auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(rt), dim3(256), 0, s, k2); };
+    if (train) {
+      if (NG == 2) launch(k2_rows_kernel<true, 2>);
+      else if (NG == 3) launch(k2_rows_kernel<true, 3>);
+      else launch(k2_rows_kernel<true, 4>);
+    } else {
+      if (NG == 2) launch(k2_rows_kernel<false, 2>);
+      else if (NG == 3) launch(k2_rows_kernel<false, 3>);
+      else launch(k2_rows_kernel<false, 4>);
+    }
     HBK_LAUNCH_CHECK("k2_rows_kernel");
-    return HBK_OK;
   }
-  hipLaunchKernelGGL(k2_rows_kernel<true>, dim3(rt), dim3(256), 0, s, k2);
-  HBK_LAUNCH_CHECK("k2_rows_kernel");
+  if (!train) return HBK_OK;
   // k3: job 0 = input layer, then dW_hg of GMLPs 1.., then dW_o of every GMLP
   K3Args k3;
   int nj = 0, blocks = 0;
