@@ -643,6 +643,25 @@ conv_chain_x3_kernel(XArgs a) {
     const int w = (ms.u_step == st_units) ? st_w : u / (C / 8);
     const int c8 = (u - w * (C / 8)) * 8;
     const float* src = srow + (w * a.in_pw) * C + c8;
+    if (a.in_ph <= 2 && a.in_pw <= 2) {
+      // window of at most 2 x 2: all four taps are loaded unconditionally (a tap
+      // outside the window re-reads tap (0, 0); the max is idempotent), so no
+      // load sits in a predicated branch or a runtime loop that would wait on it
+      const int di = a.in_ph > 1 ? a.src_row_stride : 0, dj = a.in_pw > 1 ? C : 0;
+      const float4 p00 = *reinterpret_cast<const float4*>(src), q00 = *reinterpret_cast<const float4*>(src + 4);
+      const float4 p01 = *reinterpret_cast<const float4*>(src + dj);
+      const float4 q01 = *reinterpret_cast<const float4*>(src + dj + 4);
+      const float4 p10 = *reinterpret_cast<const float4*>(src + di);
+      const float4 q10 = *reinterpret_cast<const float4*>(src + di + 4);
+      const float4 p11 = *reinterpret_cast<const float4*>(src + di + dj);
+      const float4 q11 = *reinterpret_cast<const float4*>(src + di + dj + 4);
+      auto mx = [](const float4& x, const float4& y) {
+        return float4{nan_max(x.x, y.x), nan_max(x.y, y.y), nan_max(x.z, y.z), nan_max(x.w, y.w)};
+      };
+      v0 = mx(mx(p00, p01), mx(p10, p11));
+      v1 = mx(mx(q00, q01), mx(q10, q11));
+      return;
+    }
     v0 = *reinterpret_cast<const float4*>(src);
     v1 = *reinterpret_cast<const float4*>(src + 4);
     for (int i = 0; i < a.in_ph; ++i)
@@ -689,8 +708,9 @@ conv_chain_x3_kernel(XArgs a) {
   auto prefetch = [&](const Geo& t) {
 #pragma unroll
     for (int p = 0; p < kPF; ++p) {
-      const int row = ms.t_row + p * ms.rpp;
-      if (row < t.nrows) load_unit(t, row, ms.t_u, pv0[p], pv1[p]);
+      // clamped, not predicated: rows past the task re-read its last row (unused)
+      const int row = min(ms.t_row + p * ms.rpp, t.nrows - 1);
+      load_unit(t, row, ms.t_u, pv0[p], pv1[p]);
     }
   };
 

@@ -216,5 +216,143 @@ def train(phrase: str, additional_phrase: List[str], wandb_entity: Optional[str]
         torch.distributed.destroy_process_group()
 
 
+@main.command()
+@click.argument("name", type=str, nargs=1)
+@click.argument("repo_id", type=str, nargs=1)
+@click.option("--directory", default=None, help="Directory to save the embeddings to (default: precalculated/).")
+@click.option("--config", type=str, default=None)
+@click.option("--split", type=str, default="train", show_default=True)
+@click.option("--audio-key", type=str, default="audio", show_default=True)
+@click.option("--audio-array-key", type=str, default="array", show_default=True)
+@click.option("--audio-sample-rate-key", type=str, default="sampling_rate", show_default=True)
+@click.option("--transcript-key", type=str, default=None,
+              help="Write labeled [N, 17, 96] files (needs a local tokenizer: --tokenizer).")
+@click.option("--tokenizer", type=str, default=None, help="Local transformers tokenizer directory.")
+@click.option("--streaming/--no-streaming", default=True)
+@click.option("--trust-remote-code/--no-trust-remote-code", default=False)
+@click.option("--hours", type=float, default=1000.0, show_default=True)
+@click.option("--samples-per-file", type=int, default=10000, show_default=True)
+@click.option("--device-id", type=int, default=None)
+@click.option("--sample-rate", type=int, default=16000, show_default=True)
+@click.option("--seconds-per-batch", type=float, default=1.44, show_default=True)
+@click.option("--process-batch-size", default=100, show_default=True)
+@click.option("--embedding-batch-size", default=32, show_default=True)
+@click.option("--tokenizer-max-length", default=96, show_default=True)
+@click.option("--debug/--no-debug", default=False)
+def extract(name: str, repo_id: str, directory: Optional[str], config: Optional[str], split: str, audio_key: str,
+            audio_array_key: str, audio_sample_rate_key: str, transcript_key: Optional[str],
+            tokenizer: Optional[str], streaming: bool, trust_remote_code: bool, hours: float,
+            samples_per_file: int, device_id: Optional[int], sample_rate: int, seconds_per_batch: float,
+            process_batch_size: int, embedding_batch_size: int, tokenizer_max_length: int, debug: bool) -> None:
+    """Creates a dataset of speech embeddings from an audio dataset (__main__.py:40-110);
+    REPO_ID is anything datasets.load_dataset opens offline (a local path)."""
+    from heybuddy.dataset import precalculated as pc
+    kw = dict(config_name=config, split=split, audio_key=audio_key, audio_array_key=audio_array_key,
+              audio_sample_rate_key=audio_sample_rate_key, device_id=device_id, sample_rate=sample_rate,
+              seconds_per_batch=seconds_per_batch, process_batch_size=process_batch_size,
+              embedding_batch_size=embedding_batch_size)
+    if transcript_key is not None:
+        tok = None
+        if tokenizer is not None:
+            from transformers import AutoTokenizer
+            t = AutoTokenizer.from_pretrained(tokenizer, local_files_only=True)
+            tok = lambda text: t(text, padding="max_length", truncation=True,  # noqa: E731
+                                 max_length=tokenizer_max_length)["input_ids"]
+        gen = pc.PrecalculatedLabeledTrainingDatasetGenerator(repo_id, transcript_key=transcript_key,
+                                                              tokenizer_max_length=tokenizer_max_length,
+                                                              tokenizer=tok, **kw)
+    else:
+        gen = pc.PrecalculatedTrainingDatasetGenerator(repo_id, **kw)
+    files = gen(name=name, output_dir=directory or pc.LOCAL_DIR, max_hours=hours, dataset_streaming=streaming,
+                trust_remote_code=trust_remote_code, samples_per_file=samples_per_file)
+    click.echo(f"Wrote {len(files)} file(s) to {os.path.join(directory or pc.LOCAL_DIR, name)}")
+
+
+@main.command()
+@click.argument("source", type=str, nargs=-1)
+@click.argument("target", type=str, nargs=1)
+@click.option("--directory", default=None, help="Directory of the embeddings (default: precalculated/).")
+@click.option("--reset/--no-reset", default=True, help="Reset the target file if it already exists.")
+@click.option("--half/--no-half", default=False, help="Store f16 embeddings.")
+@click.option("--delete/--no-delete", default=False, help="Delete source embeddings after combining.")
+@click.option("--batch-size", default=10, show_default=True, help="Files read per append.")
+@click.option("--debug/--no-debug", default=False)
+def combine(source: List[str], target: str, directory: Optional[str], reset: bool, half: bool, delete: bool,
+            batch_size: int, debug: bool) -> None:
+    """Combines the .npy files of one or more extract directories into one
+    appendable .npy (__main__.py:112-169); --half stores f16 (the trainer's
+    f16 negative pool)."""
+    import numpy as np
+    from heybuddy.dataset.precalculated import LOCAL_DIR
+    from heybuddy.util.numpy_util import AppendableNumpyArrayFile
+    directory = directory or LOCAL_DIR
+    target_path = os.path.join(directory, target)
+    if reset and os.path.exists(target_path):
+        os.remove(target_path)
+    dirs = [os.path.join(directory, s) for s in source]
+    files = sorted(os.path.join(d, f) for d in dirs for f in os.listdir(d) if f.endswith(".npy"))
+    with AppendableNumpyArrayFile(target_path, dtype=np.float16 if half else None) as out:
+        for i in range(0, len(files), max(1, batch_size)):
+            group = files[i:i + max(1, batch_size)]
+            out.append(np.concatenate([np.load(f) for f in group], axis=0))
+            if delete:
+                for f in group:
+                    os.remove(f)
+    if delete:
+        for d in dirs:
+            os.rmdir(d)
+    click.echo(f"Combined {len(files)} file(s) into {target_path}")
+
+
+@main.command()
+@click.argument("checkpoint", type=click.Path(exists=True, dir_okay=False, file_okay=True), nargs=1)
+@click.argument("audio", type=click.Path(exists=True, dir_okay=False, file_okay=True), nargs=1)
+@click.option("--threshold", type=float, default=DEFAULT_ACTIVATION_THRESHOLD, show_default=True)
+@click.option("--device-id", type=int, default=None)
+@click.option("--debug/--no-debug", default=False)
+def predict(checkpoint: str, audio: str, threshold: float, device_id: Optional[int], debug: bool) -> None:
+    """Predicts wake word times in an audio file (__main__.py:431-464). AUDIO:
+    a .npy / .wav (PCM) file at 16 kHz or any rate (resampled)."""
+    import numpy as np
+    from heybuddy.wakeword import WakeWordMLPModel
+    device = torch.device("cuda", device_id or 0)
+    model = WakeWordMLPModel.from_file(checkpoint, device=device).eval()
+    if audio.endswith(".npy"):
+        wav, rate = np.load(audio), 16000
+    else:
+        import wave
+        with wave.open(audio, "rb") as w:
+            rate, width, ch = w.getframerate(), w.getsampwidth(), w.getnchannels()
+            raw = np.frombuffer(w.readframes(w.getnframes()), dtype={1: np.uint8, 2: np.int16, 4: np.int32}[width])
+        wav = raw.reshape(-1, ch).T.astype(np.float32)
+        wav = (wav - 128) / 128 if width == 1 else wav / float(2 ** (8 * width - 1))
+    from heybuddy.util import audio_to_bct_tensor
+    x, _ = audio_to_bct_tensor(np.asarray(wav, dtype=np.float32), sample_rate=rate, target_sample_rate=16000)
+    times = model.predict_timecodes(x, threshold=threshold)
+    if not times:
+        click.echo("No wake-word utterances detected")
+    elif len(times) == 1:
+        click.echo(f"Wake-word utterance detected at {times[0]:.1f} second(s)")
+    else:
+        click.echo(f"{len(times)} wake-word utterances detected at the following times:")
+        for t in times:
+            click.echo(f"  {t:.1f} second(s)")
+
+
+@main.command()
+@click.argument("checkpoint", type=click.Path(exists=True, dir_okay=False, file_okay=True), nargs=1)
+@click.option("-v", "--opset-version", type=int, default=19, show_default=True)
+@click.option("-o", "--output", type=click.Path(exists=False, dir_okay=False, file_okay=True), default=None)
+def convert(checkpoint: str, opset_version: int, output: Optional[str]) -> None:
+    """Converts a checkpoint to ONNX (__main__.py:599-625)."""
+    from heybuddy.wakeword import WakeWordMLPModel
+    dest = output or os.path.join(os.path.dirname(checkpoint),
+                                  os.path.splitext(os.path.basename(checkpoint))[0] + ".onnx")
+    if os.path.exists(dest):
+        os.remove(dest)
+    WakeWordMLPModel.from_file(checkpoint).save_onnx(dest, opset_version=opset_version)
+    click.echo(f"Model saved to {dest}")
+
+
 if __name__ == "__main__":
     main()

@@ -38,11 +38,21 @@ def default_graph() -> Graph:
     """The speech-embedding graph. The reference downloads an ONNX file
     (embeddings.py:29-30) that is not available offline; this build uses the
     seeded SE20 stand-in (heybuddy.embedding_graph) unless a graph is
-    registered with ``set_default_graph``."""
+    registered with ``set_default_graph``.
+
+    The stand-in has the reference graph's shapes and cost but seeded random
+    weights: its embeddings are NOT those of the reference's speech-embedding
+    model, so classifiers trained by the reference (e.g. the shipped
+    ``src/js/models/*.onnx`` heads) score meaningless values on them. A
+    warning says so once per process."""
     global _GRAPH
     if _GRAPH is None:
         seed = int(os.environ.get("HEYBUDDY_EMBEDDING_SEED", "1234"))
         _GRAPH = se20_graph(seed)
+        logger.warning(
+            "heybuddy: no speech-embedding weights registered (set_default_graph); using the seeded SE20 "
+            "stand-in graph. Its embeddings are not reference-compatible: performance and pipeline "
+            "behaviour match, model outputs do not.")
     return _GRAPH
 
 

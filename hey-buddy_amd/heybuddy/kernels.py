@@ -385,13 +385,14 @@ class MlpPlan:
 
     def train_fwd_bwd(self, params: torch.Tensor, x: torch.Tensor, y: torch.Tensor, bucket: torch.Tensor,
                       neg_weight: float, threshold: float = 1e-4, activation_threshold: float = 0.5,
-                      dropout_p: float = 0.0, seed: int = 0, prob: torch.Tensor | None = None) -> None:
+                      dropout_p: float = 0.0, seed: int = 0, prob: torch.Tensor | None = None,
+                      workspace: torch.Tensor | None = None) -> None:
         x = self._check(params, x)
         b = x.shape[0]
         y = y.to(device=x.device, dtype=torch.float32).contiguous()
         if y.numel() != b or bucket.numel() != self.n_params + self.N_STATS:
             raise ValueError("bad y / bucket size")
-        ws = self.workspace(b, x.device)
+        ws = self.workspace(b, x.device) if workspace is None else workspace
         check(lib().hbk_mlp_train_fwd_bwd(self._handle, ptr(params), ptr(x), ptr(y), b, float(neg_weight),
                                           float(threshold), float(activation_threshold), float(dropout_p),
                                           int(seed) & (2 ** 64 - 1), ptr(bucket),

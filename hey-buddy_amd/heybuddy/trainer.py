@@ -283,6 +283,7 @@ class WakeWordTrainer(Trainer):
                None if history is None else (history.data_ptr(), history.shape[0]))
         g = self._graphs.get(key)
         if g is None:
+            self._evict_graphs()
             sx = torch.zeros((B, plan.d_in), dtype=torch.float32, device=dev)
             sy = torch.zeros(B, dtype=torch.float32, device=dev)
             sched = torch.zeros((1, 2), dtype=torch.float32, device=dev)
@@ -371,9 +372,11 @@ class WakeWordTrainer(Trainer):
         k = max(2, steps_per_graph - steps_per_graph % 2)
         if graphs and world == 1 and S >= k:
             key = ("indexed", k, self._parity, B, y_stride, float(threshold), float(activation_threshold), float(p),
-                   tuple(t.data_ptr() if t is not None else 0 for t in (idx, y, sched, p32, p16, history)))
-            gr = self._graphs.get(key)
+                   tuple(t.data_ptr() if t is not None else 0 for t in (idx, y, sched, p32, p16, history, ws)))
+            entry = self._graphs.get(key)
+            gr = None if entry is None else entry[0]
             if gr is None:
+                self._evict_graphs()
                 side = torch.cuda.Stream(dev)
                 side.wait_stream(torch.cuda.current_stream(dev))
                 gr = torch.cuda.CUDAGraph()
@@ -383,7 +386,7 @@ class WakeWordTrainer(Trainer):
                         for j in range(k):
                             one(par0 ^ (j & 1))
                 torch.cuda.current_stream(dev).wait_stream(side)
-                self._graphs[key] = gr
+                self._graphs[key] = (gr, ws)  # the entry keeps the baked-in workspace alive
             while S - done >= k:
                 gr.replay()
                 done += k
@@ -391,6 +394,16 @@ class WakeWordTrainer(Trainer):
             one(self._parity)
             self._parity ^= 1
             done += 1
+
+    _MAX_GRAPHS = 8
+
+    def _evict_graphs(self) -> None:
+        """Bound the capture cache: each captured graph holds its staging
+        buffers, workspace and memory pool, and the per-epoch keys (history
+        buffer, stage batch size) would otherwise accumulate for the
+        trainer's lifetime. Oldest captures go first."""
+        while len(self._graphs) >= self._MAX_GRAPHS:
+            self._graphs.pop(next(iter(self._graphs)))
 
     def _graph_step(self, x: torch.Tensor, y: torch.Tensor, lr: float, neg_weight: float, threshold: float,
                     activation_threshold: float, history: Optional[torch.Tensor], seed: int, p: float,
@@ -411,11 +424,14 @@ class WakeWordTrainer(Trainer):
         graphs = self._graphs
         g = graphs.get(key)
         if g is None:
+            self._evict_graphs()
             if getattr(self, "_scalars", None) is None or self._scalars.device != dev:
                 self._scalars = torch.zeros(3, dtype=torch.float64, device=dev)
             sx = torch.zeros((B, plan.d_in), dtype=torch.float32, device=dev)
             sy = torch.zeros(B, dtype=torch.float32, device=dev)
-            plan.workspace(B, dev)  # allocated outside the capture
+            # the graph owns its workspace: the plan's shared eager one may be
+            # reallocated by a larger (validation) batch after the capture
+            ws = torch.empty(plan.workspace_bytes(B), dtype=torch.uint8, device=dev)
             side = torch.cuda.Stream(dev)
             side.wait_stream(torch.cuda.current_stream(dev))
             fwd, upd = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
@@ -423,14 +439,14 @@ class WakeWordTrainer(Trainer):
             try:
                 with torch.cuda.graph(fwd, stream=side):
                     plan.train_fwd_bwd(flat, sx, sy, self._bucket, 1.0, threshold, activation_threshold,
-                                       dropout_p=p, seed=0)
+                                       dropout_p=p, seed=0, workspace=ws)
                 with torch.cuda.graph(upd, stream=side):
                     plan.gate_adam(flat, self._bucket, self._m, self._v, self._state, self._ctrl, history,
                                    1.0, BETAS[0], BETAS[1], EPS)
             finally:
                 plan.set_step_scalars(None)  # eager launches keep their by-value arguments
             torch.cuda.current_stream(dev).wait_stream(side)
-            g = graphs[key] = {"x": sx, "y": sy, "fwd": fwd, "upd": upd}
+            g = graphs[key] = {"x": sx, "y": sy, "ws": ws, "fwd": fwd, "upd": upd}
         g["x"].copy_(x.reshape(B, -1), non_blocking=True)
         g["y"].copy_(y, non_blocking=True)
         self._scalars[0].fill_(float(lr))

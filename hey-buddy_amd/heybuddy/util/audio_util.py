@@ -2,7 +2,8 @@
 
 Mirrors ``audio_to_bct_tensor`` (reference util/audio_util.py:73-145) for the
 in-memory inputs the hot path receives (lists, numpy arrays, torch tensors);
-file / URI / bytes decoding and resampling are outside this build's scope.
+file / URI / bytes decoding is outside this build's scope. ``resample`` is
+the band-limited resampler the extract path needs (torchaudio's, restated).
 Quirks kept on purpose: a list is cropped to its shortest member; a 2-D
 array/tensor [C, T] is ONE clip with C channels (it gets a batch dim, not a
 channel dim), which SpeechEmbeddings then averages (embeddings.py:183-184).
@@ -10,6 +11,9 @@ channel dim), which SpeechEmbeddings then averages (embeddings.py:183-184).
 from __future__ import annotations
 
 from typing import Any, Optional, Sequence, Tuple, Union
+
+import math
+from functools import lru_cache
 
 import numpy as np
 import torch
@@ -46,9 +50,46 @@ def audio_to_bct_tensor(input_data: AudioType, sample_rate: Optional[int] = None
     elif waveform.dtype is torch.int8:
         waveform = (waveform.float() - 128) / 128.0
     if target_sample_rate is not None and sample_rate != target_sample_rate:
-        raise NotImplementedError("resampling is outside the MI355X hot path")
+        waveform = resample(waveform.float(), int(sample_rate), int(target_sample_rate))
+        sample_rate = target_sample_rate
     if waveform.dim() == 1:
         waveform = waveform.unsqueeze(0)
     if waveform.dim() == 2:
         waveform = waveform.unsqueeze(0)
     return waveform, sample_rate
+
+
+@lru_cache(maxsize=16)
+def _sinc_kernel(orig: int, new: int, width_zc: int = 6, rolloff: float = 0.99) -> Tuple[torch.Tensor, int]:
+    """Polyphase windowed-sinc filters [new, 1, taps] of torchaudio's
+    Resample(orig, new) (sinc_interp_hann, lowpass_filter_width 6, rolloff
+    0.99; torchaudio is not installed here, so parity is unpinned): one row per
+    output phase, cut off at rolloff x the lower Nyquist frequency."""
+    base = min(orig, new) * rolloff
+    width = math.ceil(width_zc * orig / base)
+    idx = torch.arange(-width, width + orig, dtype=torch.float64)[None, None] / orig
+    t = (torch.arange(0, -new, -1, dtype=torch.float64)[:, None, None] / new + idx) * base
+    t = t.clamp(-width_zc, width_zc)
+    window = torch.cos(t * math.pi / width_zc / 2) ** 2
+    t = t * math.pi
+    k = torch.where(t == 0, torch.ones_like(t), torch.sin(t) / torch.where(t == 0, torch.ones_like(t), t))
+    return (k * window * (base / orig)).float(), width
+
+
+def resample(waveform: torch.Tensor, orig_freq: int, new_freq: int) -> torch.Tensor:
+    """Resample the last axis from orig_freq to new_freq (any leading shape),
+    on the tensor's device: pad, strided conv with the polyphase filters,
+    interleave phases, keep ceil(new * T / orig) samples."""
+    if orig_freq == new_freq:
+        return waveform
+    g = math.gcd(int(orig_freq), int(new_freq))
+    orig, new = int(orig_freq) // g, int(new_freq) // g
+    kernel, width = _sinc_kernel(orig, new)
+    kernel = kernel.to(waveform.device)
+    shape = waveform.shape
+    x = waveform.reshape(-1, shape[-1]).float()
+    n = x.shape[-1]
+    x = torch.nn.functional.pad(x, (width, width + orig))
+    y = torch.nn.functional.conv1d(x[:, None], kernel, stride=orig)  # [b, new, steps]
+    y = y.transpose(1, 2).reshape(x.shape[0], -1)[:, :math.ceil(new * n / orig)]
+    return y.reshape(*shape[:-1], y.shape[-1])

@@ -7,9 +7,9 @@ header helpers :108-300) and trains from memory maps of such files
 This module keeps that file format and API:
 
 * the header is a format-1.0 ``.npy`` header whose text is padded so that the
-  growth axis (axis 0, or the last axis for Fortran order) can reach 21 digits
-  without the header growing; appending rewrites the shape in place, so the
-  file is a valid ``.npy`` after every append (``numpy.load`` reads it);
+  row count (axis 0) can reach 21 digits without the header growing; appends
+  are positional writes at the end of the data followed by an in-place rewrite
+  of the row count, so the file is a valid ``.npy`` after every append;
 * ``load_to_device`` streams a (memory-mapped) feature file into a device
   tensor through a pinned staging buffer in chunks, so a 72 GB negative pool
   never needs to fit in host RAM at once; the trainer then samples it on the
@@ -27,41 +27,56 @@ import numpy as np
 __all__ = ["AppendableNumpyArrayFile", "read_npy_header", "load_to_device"]
 
 _MAGIC = b"\x93NUMPY"
-_GROWTH_DIGITS = 21  # room for the growth axis (fits any int64 length)
+_RESERVE = 21  # growth-axis digits the header always has room for (any int64 row count)
+_ALIGN = 64    # numpy pads the header so the data starts 64-B aligned
 
 
-def _header_bytes(shape: Tuple[int, ...], fortran_order: bool, descr: Any, header_len: Optional[int] = None) -> bytes:
-    text = "{'descr': %r, 'fortran_order': %r, 'shape': %r, }" % (descr, fortran_order, tuple(shape))
-    if shape:
-        grow = shape[-1] if fortran_order else shape[0]
-        text += " " * max(0, _GROWTH_DIGITS - len(repr(grow)))
-    # magic (6) + version (2) + length (2) + text + "\n", padded to a multiple of 64
-    base = len(_MAGIC) + 2 + 2
-    if header_len is None:
-        total = -(-(base + len(text) + 1) // 64) * 64
-    else:
-        total = header_len
-        if base + len(text) + 1 > total:
-            raise ValueError("header does not fit in the reserved length")
-    text = text + " " * (total - base - len(text) - 1) + "\n"
-    if len(text) > 0xFFFF:
-        raise ValueError("header too long for format 1.0")
-    return _MAGIC + bytes([1, 0]) + struct.pack("<H", len(text)) + text.encode("latin1")
+def _render_header(rows: int, tail: Tuple[int, ...], descr: str, size: Optional[int] = None) -> bytes:
+    """Format-1.0 header for a C-order array of shape (rows, *tail).
+
+    The dict text is followed by enough spaces that ``rows`` can grow to
+    ``_RESERVE`` digits without the header (hence the data offset) moving.
+    ``size`` pins the total header size of an existing file."""
+    shape = (rows, *tail)
+    body = "{'descr': %r, 'fortran_order': False, 'shape': %r, }" % (descr, shape)
+    body += " " * (_RESERVE - len(str(rows)))
+    fixed = len(_MAGIC) + 4  # magic, version (1, 0), uint16 header length
+    need = fixed + len(body) + 1
+    if size is None:
+        size = (need + _ALIGN - 1) // _ALIGN * _ALIGN
+    elif need > size:
+        raise ValueError(f"shape {shape} no longer fits the file's {size}-byte header")
+    body = body.ljust(size - fixed - 1) + "\n"
+    if len(body) > 0xFFFF:
+        raise ValueError("array header exceeds the .npy 1.0 limit")
+    return _MAGIC + b"\x01\x00" + struct.pack("<H", len(body)) + body.encode("latin1")
 
 
 def read_npy_header(fp) -> Tuple[Tuple[int, ...], bool, np.dtype, int]:
     """(shape, fortran_order, dtype, data offset) of an open ``.npy`` file."""
     fp.seek(0)
-    version = np.lib.format.read_magic(fp)
-    if version == (1, 0):
-        shape, fortran, dtype = np.lib.format.read_array_header_1_0(fp)
-    else:
-        shape, fortran, dtype = np.lib.format.read_array_header_2_0(fp)
+    major, _ = np.lib.format.read_magic(fp)
+    reader = np.lib.format.read_array_header_1_0 if major == 1 else np.lib.format.read_array_header_2_0
+    shape, fortran, dtype = reader(fp)
     return tuple(shape), bool(fortran), dtype, fp.tell()
 
 
+def _pwrite_all(fd: int, buf, offset: int) -> None:
+    view = memoryview(buf)
+    while len(view):  # one pwrite moves at most ~2 GiB on Linux
+        n = os.pwrite(fd, view, offset)
+        view, offset = view[n:], offset + n
+
+
 class AppendableNumpyArrayFile:
-    """Append arrays to one ``.npy`` file (reference numpy_util.py:395-564).
+    """A ``.npy`` file that grows along axis 0 (the reference's feature-file
+    writer, numpy_util.py:395-564; same constructor and ``append`` / ``close``
+    surface, C order only).
+
+    The file is a valid ``.npy`` after every append when
+    ``rewrite_header_on_append`` is set (else after ``close``): data goes to the
+    end with positional writes and only the row count in the fixed-size
+    header changes.
 
     >>> import numpy, tempfile
     >>> tf = tempfile.NamedTemporaryFile(suffix=".npy")
@@ -77,72 +92,79 @@ class AppendableNumpyArrayFile:
         self.filename = filename
         self.rewrite_header_on_append = rewrite_header_on_append
         self.lock = threading.Lock()
-        self.initialized = False
-        self.fp = None
         self.dtype = None if dtype is None else np.dtype(dtype)
+        self.shape: Optional[Tuple[int, ...]] = None
+        self.header_length = 0
+        self._fd: Optional[int] = None
+        self._end = 0  # byte offset of the end of the data
+        if os.path.exists(filename) and (delete_if_exists or os.path.getsize(filename) == 0):
+            os.unlink(filename)
         if os.path.exists(filename):
-            if os.path.getsize(filename) == 0 or delete_if_exists:
-                os.unlink(filename)
-            else:
-                self.initialize_file()
+            self._open_existing()
 
-    def initialize_file(self) -> None:
-        self.fp = open(self.filename, "rb+")
-        self.shape, self.fortran_order, dtype, self.header_length = read_npy_header(self.fp)
+    @property
+    def initialized(self) -> bool:
+        return self._fd is not None
+
+    def _open_existing(self) -> None:
+        with open(self.filename, "rb") as fp:
+            shape, fortran, dtype, offset = read_npy_header(fp)
+        if fortran:
+            raise ValueError(f"{self.filename}: Fortran-order feature files are not appendable here")
         if dtype.hasobject:
-            raise ValueError("Object arrays cannot be appended to")
-        if self.dtype is not None and dtype != self.dtype:
-            raise ValueError(f"{self.filename} holds {dtype}, not {self.dtype}")
-        self.dtype = dtype
-        if len(_header_bytes(self.shape, self.fortran_order, np.lib.format.dtype_to_descr(dtype))) > self.header_length:
-            raise ValueError(f"Header of {self.filename} not appendable")
-        self.fp.seek(0, os.SEEK_END)
-        if self.fp.tell() - self.header_length != int(np.prod(self.shape)) * dtype.itemsize:
-            raise ValueError(f"Cannot append to {self.filename}, needs recovery (data length != header shape)")
-        self.initialized = True
+            raise ValueError(f"{self.filename}: object dtype cannot be appended to")
+        if self.dtype is not None and self.dtype != dtype:
+            raise ValueError(f"{self.filename} stores {dtype}; {self.dtype} was requested")
+        if not shape:
+            raise ValueError(f"{self.filename}: a 0-d array has no axis to grow")
+        _render_header(shape[0], shape[1:], np.lib.format.dtype_to_descr(dtype), offset)  # room to grow?
+        size = os.path.getsize(self.filename)
+        expect = offset + int(np.prod(shape)) * dtype.itemsize
+        if size != expect:
+            raise ValueError(f"{self.filename} holds {size - offset} data bytes but its header says "
+                             f"{expect - offset}: the file needs recovery before appending")
+        self.dtype, self.shape, self.header_length, self._end = dtype, shape, offset, size
+        self._fd = os.open(self.filename, os.O_RDWR)
 
-    def _write_array_header(self) -> None:
-        if self.fp is None:
-            return
-        self.fp.seek(0, os.SEEK_SET)
-        self.fp.write(_header_bytes(self.shape, self.fortran_order, np.lib.format.dtype_to_descr(self.dtype),
-                                    self.header_length))
+    def _header(self) -> bytes:
+        return _render_header(self.shape[0], self.shape[1:], np.lib.format.dtype_to_descr(self.dtype),
+                              self.header_length)
 
     def update_header(self) -> None:
         with self.lock:
-            self._write_array_header()
+            if self._fd is not None:
+                os.pwrite(self._fd, self._header(), 0)
 
     def append(self, arr: np.ndarray) -> None:
         arr = np.asarray(arr)
+        if arr.ndim == 0:
+            raise ValueError("cannot append a 0-d array")
         with self.lock:
-            if not self.initialized:
-                dtype = self.dtype if self.dtype is not None else arr.dtype
-                data = np.ascontiguousarray(arr, dtype=dtype)
-                with open(self.filename, "wb") as fp:
-                    fp.write(_header_bytes(data.shape, False, np.lib.format.dtype_to_descr(data.dtype)))
-                    data.tofile(fp)
-                self.initialize_file()
-                return
-            c = -1 if self.fortran_order else 1
-            if self.shape[::c][1:] != arr.shape[::c][1:]:
-                raise ValueError(f"Shapes {self.shape[::c][1:][::c]} and {arr.shape[::c][1:][::c]} do not match")
-            self.fp.seek(0, os.SEEK_END)
-            arr.astype(self.dtype, copy=False).flatten(order="F" if self.fortran_order else "C").tofile(self.fp)
-            if self.fortran_order:
-                self.shape = (*self.shape[:-1], self.shape[-1] + arr.shape[-1])
-            else:
-                self.shape = (self.shape[0] + arr.shape[0], *self.shape[1:])
+            if self._fd is None:  # first append creates the file
+                self.dtype = self.dtype or arr.dtype
+                self.shape = (0, *arr.shape[1:])
+                self._fd = os.open(self.filename, os.O_RDWR | os.O_CREAT | os.O_TRUNC, 0o644)
+                self.header_length = len(_render_header(0, self.shape[1:], np.lib.format.dtype_to_descr(self.dtype)))
+                self._end = self.header_length
+                os.pwrite(self._fd, self._header(), 0)
+            if tuple(arr.shape[1:]) != tuple(self.shape[1:]):
+                raise ValueError(f"cannot append rows of shape {arr.shape[1:]} to {self.filename}, "
+                                 f"whose rows are {self.shape[1:]}")
+            data = np.ascontiguousarray(arr, dtype=self.dtype)
+            if data.nbytes:
+                _pwrite_all(self._fd, data.reshape(-1).view(np.uint8), self._end)
+            self._end += data.nbytes
+            self.shape = (self.shape[0] + arr.shape[0], *self.shape[1:])
             if self.rewrite_header_on_append:
-                self._write_array_header()
+                os.pwrite(self._fd, self._header(), 0)
 
     def close(self) -> None:
         with self.lock:
-            if self.initialized:
-                if not self.rewrite_header_on_append:
-                    self._write_array_header()
-                self.fp.close()
-                self.fp = None
-                self.initialized = False
+            if self._fd is None:
+                return
+            os.pwrite(self._fd, self._header(), 0)
+            os.close(self._fd)
+            self._fd = None
 
     def __del__(self) -> None:
         try:

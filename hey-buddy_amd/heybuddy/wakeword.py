@@ -2,8 +2,9 @@
 src/python/heybuddy/wakeword.py:171-348).
 
 ``WakeWordMLPModel`` keeps the reference's constructor, state_dict names and
-shapes (checkpoints and the shipped src/js/models/*.onnx weights load with
-strict=True), ``from_file`` and ``predict``, but its parameters are views into
+shapes (checkpoints and the shipped src/js/models/*.onnx heads load with
+strict=True, through heybuddy.util.onnx_util), ``from_file``, ``predict``,
+``predict_timecodes`` and ``save_onnx``, but its parameters are views into
 ONE flat f32 buffer laid out for libhbk.so, and ``forward`` runs the fused HIP
 forward (hbk_mlp_forward). Training goes through the fused HIP train step
 (heybuddy.trainer), not autograd. Only the default architecture is on the MI355X
@@ -13,7 +14,7 @@ from __future__ import annotations
 
 import random
 from collections import OrderedDict
-from typing import Any, List, Optional, Tuple, Union
+from typing import Any, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
 import torch
@@ -148,8 +149,14 @@ class WakeWordMLPModel(nn.Module):
 
     @classmethod
     def from_file(cls, path: str, device: Optional[torch.device] = None) -> "WakeWordMLPModel":
-        """wakeword.py:249-276: infer layer_dim / num_layers from the state_dict."""
-        state_dict = torch.load(path, weights_only=True, map_location="cpu")
+        """wakeword.py:249-276: infer layer_dim / num_layers from the state_dict.
+        ``.onnx`` heads (the reference's shipped src/js/models/*.onnx, or
+        ``save_onnx`` output) load from their initializers."""
+        if str(path).lower().endswith(".onnx"):
+            from heybuddy.util.onnx_util import read_initializers
+            state_dict = {k: torch.from_numpy(v) for k, v in read_initializers(path).items()}
+        else:
+            state_dict = torch.load(path, weights_only=True, map_location="cpu")
         layer_dim = state_dict["norm_out.weight"].shape[0]
         num_layers = 0
         while f"layers.{num_layers}.0.weight" in state_dict:
@@ -159,6 +166,13 @@ class WakeWordMLPModel(nn.Module):
         if device is not None:
             model.to(device)
         return model
+
+    def save_onnx(self, path: str, opset_version: int = 19) -> None:
+        """wakeword.py:316-332: the head as an ONNX file with the exporter's
+        graph (input ``input`` [1, 16, 96], output ``output`` [1, 1])."""
+        from heybuddy.util.onnx_util import write_wakeword_onnx
+        sd = OrderedDict((k, v.detach().float().cpu().numpy()) for k, v in self.state_dict().items())
+        write_wakeword_onnx(path, sd, self.num_layers, self.input_shape, opset_version=opset_version)
 
     # -- WakeWordInferenceMixin.predict (wakeword.py:129-169) ---------------
     @property
@@ -187,3 +201,50 @@ class WakeWordMLPModel(nn.Module):
         if return_scores:
             return tuple(pred.flatten())
         return tuple(pred > threshold)
+
+    @staticmethod
+    def timecode_windows(audio_tensor: torch.Tensor) -> torch.Tensor:
+        """wakeword.py:59-90: mono [t] -> 2-s windows every 1 s [n, 1, 32000]
+        (padded to whole seconds, 1 s of silence on both ends)."""
+        if audio_tensor.dim() == 3:
+            _, c, _ = audio_tensor.shape
+            audio_tensor = audio_tensor[0, 0, :] if c == 1 else audio_tensor[0, :, :].mean(dim=0)
+        t = audio_tensor.shape[0]
+        rem = t % 16000
+        z = lambda n: torch.zeros(n, dtype=audio_tensor.dtype, device=audio_tensor.device)  # noqa: E731
+        if rem > 0:
+            audio_tensor = torch.cat([audio_tensor, z(16000 - rem)])
+        audio_tensor = torch.cat([z(16000), audio_tensor, z(16000)])
+        starts = range(0, audio_tensor.shape[0] - 16000, 16000)
+        return torch.stack([audio_tensor[i:i + 32000] for i in starts]).unsqueeze(1)
+
+    @staticmethod
+    def timecodes(predictions: Sequence[bool]) -> List[float]:
+        """wakeword.py:99-110: a positive window i is reported at i + 0.5 when
+        window i + 1 is positive too, skipped when it is the last window and
+        follows a positive one, else at i."""
+        out: List[float] = []
+        n = len(predictions)
+        for i, hit in enumerate(predictions):
+            if not hit:
+                continue
+            if i < n - 1 and predictions[i + 1]:
+                out.append(i + 0.5)
+            elif i == n - 1 and predictions[i - 1]:
+                continue
+            else:
+                out.append(i)
+        return out
+
+    @torch.no_grad()
+    def predict_timecodes(self, audio: Any, threshold: float = 0.5, embedding_spectrogram_batch_size: int = 32,
+                          embedding_batch_size: int = 32) -> List[float]:
+        """Per-second detections in one clip (wakeword.py:50-110): every 2-s
+        window goes through the HIP featurizer and head in one batch."""
+        from heybuddy.util import audio_to_bct_tensor
+        audio_tensor, _ = audio_to_bct_tensor(audio, sample_rate=16000)
+        windows = self.timecode_windows(audio_tensor)
+        preds = self.predict(windows, threshold=threshold,
+                             embedding_spectrogram_batch_size=embedding_spectrogram_batch_size,
+                             embedding_batch_size=embedding_batch_size)
+        return self.timecodes(preds)

@@ -21,8 +21,10 @@ records its outputs on seeded inputs:
                          negative weight (histories + final parameters).
   to_target_length.npz   AugmentedAudioGenerator.to_target_length with numpy's
                          global RNG seeded (crop, 1-sample pad, random pads).
+  onnx_heads.npz         the shipped src/js/models/*.onnx heads through the
+                         reference WakeWordMLPModel (zeros KAT + seeded inputs).
 
-Usage: python oracle/make_golden.py [--only featurizer|classifier|stages|augment]
+Usage: python oracle/make_golden.py [--only featurizer|classifier|stages|augment|onnx]
 """
 from __future__ import annotations
 
@@ -175,6 +177,8 @@ def main():
         golden_classifier.make_stages(hb, GOLDEN)
     if args.only in (None, "augment"):
         golden_classifier.make_to_target_length(hb, GOLDEN)
+    if args.only in (None, "onnx"):
+        golden_classifier.make_onnx_heads(hb, GOLDEN)
 
 
 if __name__ == "__main__":
