@@ -22,9 +22,22 @@ from heybuddy._native import check, lib, ptr, stream_ptr
 
 __all__ = ["MelPlan", "mel_frames"]
 
-_plans: Dict[int, "MelPlan"] = {}
+_plans: Dict[int, object] = {}
 _plan_ids = itertools.count(1)
 _plans_lock = threading.Lock()
+
+
+def _register(plan) -> int:
+    """Plans are handed to the torch.library ops by id (ops take no opaque objects)."""
+    with _plans_lock:
+        pid = next(_plan_ids)
+        _plans[pid] = plan
+    return pid
+
+
+def _u64_to_i64(v: int) -> int:
+    v &= 2 ** 64 - 1
+    return v - 2 ** 64 if v >= 2 ** 63 else v
 
 
 class MelPlan:
@@ -52,9 +65,7 @@ class MelPlan:
                 float(in_scale), float(log_floor), float(out_div), float(out_add),
                 ctypes.byref(handle)), "hbk_mel_plan_create")
         self._handle = handle
-        with _plans_lock:
-            self.id = next(_plan_ids)
-            _plans[self.id] = self
+        self.id = _register(self)
 
     def n_frames(self, n_samples: int) -> int:
         return 0 if n_samples < self.n_fft else (n_samples - self.n_fft) // self.hop + 1
@@ -174,9 +185,7 @@ class EmbedPlan:
         self.seq_frames = sf.value
         self.in_h, self.in_w = h, w
         self._ws: torch.Tensor | None = None
-        with _plans_lock:
-            self.id = next(_plan_ids)
-            _plans[self.id] = self
+        self.id = _register(self)
 
     @property
     def macs_per_clip(self) -> float:
@@ -298,6 +307,7 @@ class MlpPlan:
         self.n_params = n.value
         self.offsets = list(offs)
         self._ws: Dict[torch.device, torch.Tensor] = {}
+        self.id = _register(self)
 
     def views(self, flat: torch.Tensor) -> "Dict[str, torch.Tensor]":
         """state_dict-named views (reference names and shapes) into ``flat``."""
@@ -373,14 +383,8 @@ class MlpPlan:
     def forward(self, params: torch.Tensor, x: torch.Tensor, dropout_p: float = 0.0, seed: int = 0,
                 logits: bool = False):
         x = self._check(params, x)
-        b = x.shape[0]
-        prob = torch.empty(b, dtype=torch.float32, device=x.device)
-        logit = torch.empty(b, dtype=torch.float32, device=x.device) if logits else None
-        ws = self.workspace(b, x.device)
-        check(lib().hbk_mlp_forward(self._handle, ptr(params), ptr(x), b, ptr(prob),
-                                    ptr(logit) if logit is not None else None, float(dropout_p),
-                                    int(seed) & (2 ** 64 - 1), ptr(ws), ws.numel(),
-                                    stream_ptr(x.device)), "hbk_mlp_forward")
+        ws = self.workspace(x.shape[0], x.device)
+        prob, logit = torch.ops.hbk.mlp_forward(params, x, ws, float(dropout_p), _u64_to_i64(seed), self.id)
         return (prob, logit) if logits else prob
 
     def train_fwd_bwd(self, params: torch.Tensor, x: torch.Tensor, y: torch.Tensor, bucket: torch.Tensor,
@@ -444,27 +448,18 @@ class MlpPlan:
         if sched is not None and (sched.dtype != torch.float32 or sched.shape[-1] != 2 or sched.device != dev):
             raise ValueError("sched must be float32 [n, 2] (lr, neg_weight) on the device")
         ws = self.workspace(batch, dev) if workspace is None else workspace
-        check(lib().hbk_mlp_step_fwd_bwd(
-            self._handle, ptr(params), ptr(pool32) if pool32 is not None else None,
-            pool32.shape[0] if pool32 is not None else 0, ptr(pool16) if pool16 is not None else None,
-            pool16.shape[0] if pool16 is not None else 0, ptr(idx) if idx is not None else None, int(idx_stride),
-            ptr(y), int(y_stride), int(batch), ptr(state), int(parity),
-            ptr(sched) if sched is not None else None, sched.shape[0] if sched is not None else 0,
-            float(neg_weight), float(threshold), float(activation_threshold), float(dropout_p),
-            int(seed) & (2 ** 64 - 1), ptr(bucket), ptr(prob) if prob is not None else None, ptr(ws),
-            ws.numel(), stream_ptr(dev)), "hbk_mlp_step_fwd_bwd")
+        torch.ops.hbk.mlp_step_fwd_bwd(params, bucket, state, int(parity), y, int(batch), pool32, pool16, idx,
+                                       int(idx_stride), int(y_stride), sched, float(neg_weight), float(threshold),
+                                       float(activation_threshold), float(dropout_p), _u64_to_i64(seed), prob, ws,
+                                       self.id)
 
     def step_update(self, params: torch.Tensor, bucket: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
                     state: torch.Tensor, parity: int, sched: torch.Tensor | None = None, lr: float = 1e-3,
                     beta1: float = 0.9, beta2: float = 0.999, eps: float = 1e-8,
                     history: torch.Tensor | None = None) -> None:
         """Gate + Adam + bucket zeroing (hbk_mlp_step_update)."""
-        cap = 0 if history is None else history.shape[0]
-        check(lib().hbk_mlp_step_update(
-            self._handle, ptr(params), ptr(bucket), ptr(m), ptr(v), ptr(state), int(parity),
-            ptr(sched) if sched is not None else None, sched.shape[0] if sched is not None else 0,
-            float(lr), float(beta1), float(beta2), float(eps), ptr(history) if history is not None else None,
-            cap, stream_ptr(params.device)), "hbk_mlp_step_update")
+        torch.ops.hbk.mlp_step_update(params, bucket, m, v, state, int(parity), sched, float(lr), float(beta1),
+                                      float(beta2), float(eps), history, self.id)
 
     def gate_adam(self, params, bucket, m, v, state, ctrl, history, lr, beta1=0.9, beta2=0.999,
                   eps=1e-8) -> None:
@@ -473,6 +468,53 @@ class MlpPlan:
                                       ptr(ctrl), ptr(history) if history is not None else None, cap,
                                       float(lr), float(beta1), float(beta2), float(eps),
                                       stream_ptr(params.device)), "hbk_mlp_gate_adam")
+
+
+@torch.library.custom_op("hbk::mlp_forward", mutates_args=("ws",))
+def _mlp_forward_op(params: torch.Tensor, x: torch.Tensor, ws: torch.Tensor, dropout_p: float, seed: int,
+                    plan_id: int) -> tuple[torch.Tensor, torch.Tensor]:
+    plan = _plans[plan_id]
+    b = x.shape[0]
+    prob = torch.empty(b, dtype=torch.float32, device=x.device)
+    logit = torch.empty(b, dtype=torch.float32, device=x.device)
+    check(lib().hbk_mlp_forward(plan._handle, ptr(params), ptr(x), b, ptr(prob), ptr(logit), float(dropout_p),
+                                int(seed) & (2 ** 64 - 1), ptr(ws), ws.numel(), stream_ptr(x.device)),
+          "hbk_mlp_forward")
+    return prob, logit
+
+
+@_mlp_forward_op.register_fake
+def _(params, x, ws, dropout_p, seed, plan_id):
+    return x.new_empty(x.shape[0]), x.new_empty(x.shape[0])
+
+
+@torch.library.custom_op("hbk::mlp_step_fwd_bwd", mutates_args=("bucket", "prob", "ws"))
+def _mlp_step_fwd_bwd_op(params: torch.Tensor, bucket: torch.Tensor, state: torch.Tensor, parity: int,
+                         y: torch.Tensor, batch: int, pool32: torch.Tensor | None, pool16: torch.Tensor | None,
+                         idx: torch.Tensor | None, idx_stride: int, y_stride: int, sched: torch.Tensor | None,
+                         neg_weight: float, threshold: float, activation_threshold: float, dropout_p: float,
+                         seed: int, prob: torch.Tensor | None, ws: torch.Tensor, plan_id: int) -> None:
+    plan = _plans[plan_id]
+    opt = lambda t: ptr(t) if t is not None else None  # noqa: E731
+    check(lib().hbk_mlp_step_fwd_bwd(
+        plan._handle, ptr(params), opt(pool32), pool32.shape[0] if pool32 is not None else 0, opt(pool16),
+        pool16.shape[0] if pool16 is not None else 0, opt(idx), idx_stride, ptr(y), y_stride, batch, ptr(state),
+        parity, opt(sched), sched.shape[0] if sched is not None else 0, neg_weight, threshold,
+        activation_threshold, dropout_p, seed & (2 ** 64 - 1), ptr(bucket), opt(prob), ptr(ws), ws.numel(),
+        stream_ptr(params.device)), "hbk_mlp_step_fwd_bwd")
+
+
+@torch.library.custom_op("hbk::mlp_step_update", mutates_args=("params", "bucket", "m", "v", "state", "history"))
+def _mlp_step_update_op(params: torch.Tensor, bucket: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
+                        state: torch.Tensor, parity: int, sched: torch.Tensor | None, lr: float, beta1: float,
+                        beta2: float, eps: float, history: torch.Tensor | None, plan_id: int) -> None:
+    plan = _plans[plan_id]
+    cap = 0 if history is None else history.shape[0]
+    check(lib().hbk_mlp_step_update(
+        plan._handle, ptr(params), ptr(bucket), ptr(m), ptr(v), ptr(state), parity,
+        ptr(sched) if sched is not None else None, sched.shape[0] if sched is not None else 0, lr, beta1, beta2,
+        eps, ptr(history) if history is not None else None, cap, stream_ptr(params.device)),
+          "hbk_mlp_step_update")
 
 
 @torch.library.custom_op("hbk::place_clips", mutates_args=())
@@ -533,9 +575,14 @@ def tanh_distortion(x: torch.Tensor, amount: torch.Tensor, out: torch.Tensor | N
     amount = amount.pin_memory().to(dev, non_blocking=True) if amount.device.type == "cpu" else amount.to(dev)
     if out is None:
         out = torch.empty((n, T), dtype=torch.float32, device=dev)
-    check(lib().hbk_tanh_distortion(ptr(x), n, x.stride(0), ptr(amount), ptr(out), out.stride(0),
-                                    stream_ptr(dev)), "hbk_tanh_distortion")
+    torch.ops.hbk.tanh_distortion_(x, amount, out)
     return out
+
+
+@torch.library.custom_op("hbk::tanh_distortion_", mutates_args=("out",))
+def _tanh_distortion_op(x: torch.Tensor, amount: torch.Tensor, out: torch.Tensor) -> None:
+    check(lib().hbk_tanh_distortion(ptr(x), x.shape[0], x.stride(0), ptr(amount), ptr(out), out.stride(0),
+                                    stream_ptr(x.device)), "hbk_tanh_distortion")
 
 
 class ReverbPlan:
@@ -550,6 +597,7 @@ class ReverbPlan:
         with torch.cuda.device(self.device):
             check(lib().hbk_reverb_plan_create(self.T, ctypes.byref(handle)), "hbk_reverb_plan_create")
         self._handle = handle
+        self.id = _register(self)
 
     @staticmethod
     def rotated_kernel(ir: torch.Tensor, T: int = 23040) -> torch.Tensor:
@@ -570,8 +618,7 @@ class ReverbPlan:
         kernels = kernels.to(self.device, torch.float32).contiguous()
         n = kernels.shape[0]
         out = torch.zeros((n, self.SLOTS, 2), dtype=torch.float32, device=self.device)
-        check(lib().hbk_reverb_spectrum(self._handle, ptr(kernels), n, kernels.stride(0), ptr(out),
-                                        stream_ptr(self.device)), "hbk_reverb_spectrum")
+        torch.ops.hbk.reverb_spectrum_(kernels, out, self.id)
         return out
 
     @classmethod
@@ -623,13 +670,7 @@ class ReverbPlan:
         noise_off, spec_idx, snr_db = to_dev(noise_off), to_dev(spec_idx), to_dev(snr_db)
         if gain is not None:
             gain = to_dev(gain)
-        ring_len = 0 if ring is None else ring.numel()
-        check(lib().hbk_augment(self._handle, ptr(x), n, x.stride(0),
-                                ptr(ring) if ring is not None else None, ring_len, ptr(noise_off),
-                                ptr(snr_db), ptr(spectra) if spectra is not None else None,
-                                ptr(spec_idx), ptr(gain) if gain is not None else None, ptr(out),
-                                out.stride(0), stream_ptr(self.device)),
-              "hbk_augment")
+        torch.ops.hbk.augment_(x, ring, noise_off, snr_db, spectra, spec_idx, gain, out, self.id)
         return out
 
     def colored_noise(self, x: torch.Tensor, f_decay: torch.Tensor, snr_db: torch.Tensor,
@@ -657,11 +698,7 @@ class ReverbPlan:
             return t.pin_memory().to(self.device, non_blocking=True) if t.device.type == "cpu" else t.to(self.device)
 
         f_decay, snr_db = per_clip(f_decay), per_clip(snr_db)
-        check(lib().hbk_colored_noise(self._handle, ptr(x), n, x.stride(0),
-                                      ptr(white) if white is not None else None,
-                                      white.stride(0) if white is not None else 0,
-                                      int(seed) & (2 ** 64 - 1), ptr(f_decay), ptr(snr_db), float(sample_rate),
-                                      ptr(out), out.stride(0), stream_ptr(self.device)), "hbk_colored_noise")
+        torch.ops.hbk.colored_noise_(x, white, f_decay, snr_db, _u64_to_i64(seed), float(sample_rate), out, self.id)
         return out
 
     def __del__(self) -> None:
@@ -672,3 +709,32 @@ class ReverbPlan:
             except Exception:
                 pass
             self._handle = None
+
+
+@torch.library.custom_op("hbk::reverb_spectrum_", mutates_args=("out",))
+def _reverb_spectrum_op(kernels: torch.Tensor, out: torch.Tensor, plan_id: int) -> None:
+    plan = _plans[plan_id]
+    check(lib().hbk_reverb_spectrum(plan._handle, ptr(kernels), kernels.shape[0], kernels.stride(0), ptr(out),
+                                    stream_ptr(kernels.device)), "hbk_reverb_spectrum")
+
+
+@torch.library.custom_op("hbk::augment_", mutates_args=("out",))
+def _augment_op(x: torch.Tensor, ring: torch.Tensor | None, noise_off: torch.Tensor, snr_db: torch.Tensor,
+                spectra: torch.Tensor | None, spec_idx: torch.Tensor, gain: torch.Tensor | None, out: torch.Tensor,
+                plan_id: int) -> None:
+    plan = _plans[plan_id]
+    opt = lambda t: ptr(t) if t is not None else None  # noqa: E731
+    check(lib().hbk_augment(plan._handle, ptr(x), x.shape[0], x.stride(0), opt(ring),
+                            0 if ring is None else ring.numel(), ptr(noise_off), ptr(snr_db), opt(spectra),
+                            ptr(spec_idx), opt(gain), ptr(out), out.stride(0), stream_ptr(x.device)), "hbk_augment")
+
+
+@torch.library.custom_op("hbk::colored_noise_", mutates_args=("out",))
+def _colored_noise_op(x: torch.Tensor, white: torch.Tensor | None, f_decay: torch.Tensor, snr_db: torch.Tensor,
+                      seed: int, sample_rate: float, out: torch.Tensor, plan_id: int) -> None:
+    plan = _plans[plan_id]
+    check(lib().hbk_colored_noise(plan._handle, ptr(x), x.shape[0], x.stride(0),
+                                  ptr(white) if white is not None else None,
+                                  white.stride(0) if white is not None else 0, seed & (2 ** 64 - 1), ptr(f_decay),
+                                  ptr(snr_db), sample_rate, ptr(out), out.stride(0), stream_ptr(x.device)),
+          "hbk_colored_noise")
