@@ -237,14 +237,30 @@ class WakeWordMLPModel(nn.Module):
         return out
 
     @torch.no_grad()
+    def window_scores(self, windows: torch.Tensor) -> torch.Tensor:
+        """Score of each audio window [n, 1, T]: a 2-s window yields more
+        embedding rows (32) than the head takes (16), which the reference's
+        predict() passes to the head unchanged (its LayerNorm(1536) then
+        rejects the 3072-wide input). Here the head scores every 16-row run of
+        the window's embeddings (the JS detector's rolling buffer,
+        src/js/src/hey-buddy.js:88, wakeWordEmbeddingFrames = 16) and the window
+        keeps the highest score."""
+        x = windows.reshape(windows.shape[0], -1).to(self.device, torch.float32)
+        emb = self.speech_embeddings.featurize(x)  # [n, m, 96] on the device
+        rows = self.input_shape[0]
+        n, m, d = emb.shape
+        if m < rows:
+            raise ValueError(f"windows of {x.shape[1]} samples give {m} < {rows} embedding rows")
+        runs = emb.unfold(1, rows, 1).permute(0, 1, 3, 2).reshape(-1, rows, d)  # [n * (m - rows + 1), rows, d]
+        return self(runs.contiguous()).reshape(n, m - rows + 1).amax(dim=1)
+
+    @torch.no_grad()
     def predict_timecodes(self, audio: Any, threshold: float = 0.5, embedding_spectrogram_batch_size: int = 32,
                           embedding_batch_size: int = 32) -> List[float]:
-        """Per-second detections in one clip (wakeword.py:50-110): every 2-s
-        window goes through the HIP featurizer and head in one batch."""
+        """Per-second detections in one clip (wakeword.py:50-110): 2-s windows
+        every second, all featurized and scored in one batch on the device
+        (window_scores), then the reference's timecode rule."""
         from heybuddy.util import audio_to_bct_tensor
         audio_tensor, _ = audio_to_bct_tensor(audio, sample_rate=16000)
-        windows = self.timecode_windows(audio_tensor)
-        preds = self.predict(windows, threshold=threshold,
-                             embedding_spectrogram_batch_size=embedding_spectrogram_batch_size,
-                             embedding_batch_size=embedding_batch_size)
-        return self.timecodes(preds)
+        scores = self.window_scores(self.timecode_windows(audio_tensor))
+        return self.timecodes((scores > threshold).tolist())
