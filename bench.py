@@ -71,6 +71,9 @@ def parse():
     return ap.parse_args()
 
 
+TRAFFIC_SOURCE = [None]
+
+
 def load_traffic(path, kernel_substr):
     """HBM bytes per step of the kernels whose name contains kernel_substr (a
     string or a tuple of alternatives), from a tools/pmc_summary.py JSON
@@ -81,6 +84,7 @@ def load_traffic(path, kernel_substr):
             d = json.load(f)
         v = [k for name, k in d.get("kernels", {}).items() if any(s in name for s in subs)]
         if v:
+            TRAFFIC_SOURCE[0] = os.path.relpath(path, ROOT)
             return sum(k["hbm_bytes_per_step"] for k in v)
     except (OSError, ValueError, KeyError):
         pass
@@ -93,6 +97,9 @@ def roof(kernel, bound, work, ms, unit, traffic, peak=None, **extra):
         peak = HBM_PEAK_GBS if unit == "GB/s" else FP32_MFMA_PEAK_TFLOPS
     d = {"kernel": kernel, "bound": bound, "achieved": round(ach, 3), "peak": peak, "unit": unit,
          "frac": round(ach / peak, 4), "traffic": traffic, "ms_per_step": round(ms, 3)}
+    if traffic is not None:  # PMC bytes are collected in separate rocprofv3 passes, not in this run
+        d["traffic_source"] = "%s (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, tools/pmc_summary.py)" % (
+            TRAFFIC_SOURCE[0],)
     d.update(extra)
     return d
 
@@ -213,11 +220,11 @@ def setup_featurize(args, dev, rank, world, seed):
                         algorithmic_bytes_per_clip=MEL_READ_SAMPLES * 4 + N_FRAMES * 32 * 4)
         if name == "embed":
             split = eplan.precision == "split"
-            kname = "p0_chain_kernel + conv_chain_x3_kernel" if split else "conv_chain_kernel"
+            kname = "p0_chain_kernel + p1_chain_kernel + conv_chain_x3_kernel x2" if split else "conv_chain_kernel"
             return roof("%s (hbk_embed_clips, %s: %d chained launches per %d-clip chunk)"
                         % (kname, eplan.precision, eplan.n_chains, min(n, 16384)), "mfma",
                         2.0 * eplan.macs_per_clip * n, ms, "TFLOP/s",
-                        load_traffic(pmc, ("conv_chain", "p0_chain")),
+                        load_traffic(pmc, ("conv_chain", "p0_chain", "p1_chain")),
                         peak=SPLIT_PEAK_TFLOPS if split else FP32_MFMA_PEAK_TFLOPS,
                         peak_basis=("f16 dense MFMA peak / 3 (hi*hi + hi*lo + lo*hi per f32-accurate MAC)"
                                     if split else "f32-input MFMA dense peak"),

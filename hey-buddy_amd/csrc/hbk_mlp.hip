@@ -563,8 +563,8 @@ int hbk_mlp_forward(const hbk_mlp_plan* p, const float* params, const float* x, 
   if (dropout_p < 0.f || dropout_p >= 1.f) return arg_error("dropout_p must be in [0, 1)");
   if (mlp_fused_supported(*p)) {
     if (ws_bytes < mlp_fused_ws_floats(*p, batch) * int64_t(sizeof(float))) return arg_error("workspace too small");
-    return mlp_fused_run(*p, params, x, batch, nullptr, 0, nullptr, 0, nullptr, 0, B, nullptr, 0, nullptr, 0, 1.f, 0.f, 0.f,
-                         dropout_p, seed, nullptr, prob, logit, ws, false, s);
+    return mlp_fused_run(*p, params, x, batch, nullptr, 0, nullptr, 0, 0, nullptr, 0, B, nullptr, 0, nullptr, 0, 1.f,
+                         0.f, 0.f, dropout_p, seed, nullptr, prob, logit, ws, false, 0, s);
   }
   HBK_RC(forward(*p, params, x, B, ws, w, dropout_p, seed, s));
   hipLaunchKernelGGL(sigmoid_kernel, dim3(ew_grid(B)), dim3(256), 0, s, ws + w.z, prob, B);
@@ -674,8 +674,8 @@ int hbk_mlp_step_fwd_bwd(const hbk_mlp_plan* p, const float* params, const float
                          const void* pool16, int64_t n16, const int32_t* idx, int64_t idx_step_stride, const float* y, int64_t y_step_stride,
                          int64_t batch, const float* state, int32_t parity, const float* sched, int64_t sched_len,
                          float neg_weight, float high_loss_threshold, float activation_threshold, float dropout_p,
-                         uint64_t seed, float* bucket, float* prob, void* workspace, int64_t ws_bytes,
-                         void* stream) {
+                         uint64_t seed, float* bucket, float* prob, int64_t idx_steps, int32_t flags,
+                         void* workspace, int64_t ws_bytes, void* stream) {
   using namespace hbk;
   if (!p) return arg_error("plan is NULL");
   if (!mlp_fused_supported(*p)) {
@@ -691,10 +691,13 @@ int hbk_mlp_step_fwd_bwd(const hbk_mlp_plan* p, const float* params, const float
   if (ws_bytes < mlp_fused_ws_floats(*p, batch) * int64_t(sizeof(float))) return arg_error("workspace too small");
   if (n32 < 0 || n16 < 0) return arg_error("negative pool size");
   if (!idx && n32 < batch) return arg_error("idx NULL: pool32 must hold the batch rows");
-  return mlp_fused_run(*p, params, pool32, n32, pool16, n16, idx, idx_step_stride, y, y_step_stride, static_cast<int>(batch),
-                       state, parity, sched, static_cast<int>(std::min<int64_t>(sched_len, 1 << 30)), neg_weight,
-                       high_loss_threshold, activation_threshold, dropout_p, seed, bucket, prob, nullptr,
-                       static_cast<float*>(workspace), true, as_stream(stream));
+  if (flags & ~(HBK_STEP_XHAT_READY | HBK_STEP_PREFETCH_NEXT)) return arg_error("unknown flags");
+  if (!pool32 && !pool16) return arg_error("no embedding pool");
+  return mlp_fused_run(*p, params, pool32, n32, pool16, n16, idx, idx_step_stride, idx_steps, y, y_step_stride,
+                       static_cast<int>(batch), state, parity, sched,
+                       static_cast<int>(std::min<int64_t>(sched_len, 1 << 30)), neg_weight, high_loss_threshold,
+                       activation_threshold, dropout_p, seed, bucket, prob, nullptr, static_cast<float*>(workspace),
+                       true, flags, as_stream(stream));
 }
 
 int hbk_mlp_step_update(const hbk_mlp_plan* p, float* params, float* bucket, float* m, float* v, float* state,

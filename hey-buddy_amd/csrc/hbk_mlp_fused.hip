@@ -7,10 +7,14 @@
 // high-loss filter and weighted BCE (:407-445), autograd backward and
 // torch.optim.Adam (:45, :460-462), with FOUR launches and no host sync:
 //
-//   k1_input   gather the batch rows from the embedding pools by index (f32
-//              or f16 pool), input dropout, LayerNorm(1536) -> xhat, and the
-//              input GEMM HG0 = LN(x) W_hg0^T as split-K partial slabs
-//              (row tiles of 16 x K-chunks: ~280 workgroups at B = 1100)
+//   k1a        gather the batch rows from the embedding pools by index (f32
+//              or f16 pool), input dropout, LayerNorm(1536) -> xhat^T in HBM.
+//              It needs no weights, so step s + 1's k1a runs as extra
+//              workgroups of step s's k2 launch (k2 fills 69 of 256 CUs at
+//              B = 1100) and is off the critical path; a standalone launch
+//              covers the first step and steps without a known successor
+//   k1b        the input GEMM HG0 = (xhat g + b) W_hg0^T as split-K partial
+//              slabs (row tiles of 16 x K-chunks: ~576 workgroups at B = 1100)
 //   k2_rows    per 16-row tile, the whole rest of the network in LDS:
 //              sum of the HG0 partials + bias, SiLU gate, every gated MLP and
 //              LayerNorm forward, sigmoid, the high-loss filter, weighted BCE
@@ -90,8 +94,8 @@ __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); 
 #ifdef HBK_TRACE
 // Tracing build only (lib/libhbk_trace.so, tools/probe_mlp.py): lane 0 of every
 // wave of block 0 records (mark << 56 | s_memtime) at stage marks of k1 / k2 / k3.
-__device__ unsigned long long g_mlp_trace[3][4][128];
-__device__ int g_mlp_trace_n[3][4];
+__device__ unsigned long long g_mlp_trace[4][4][128];
+__device__ int g_mlp_trace_n[4][4];
 #define HBK_MT(kern, id)                                                                       \
   do {                                                                                         \
     if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) {                                          \
@@ -115,23 +119,30 @@ __device__ __forceinline__ int step_of(const float* state, int parity) {
 }
 
 // ------------------------------------------------------------------ k1 ----
-struct K1Args {
-  const float* P;
-  int64_t g_in, b_in, w0;
+struct K1aArgs {
   const float* pool32;
   const _Float16* pool16;
   int64_t n32, n16;    // pool rows; an index outside its pool reads as a zero row
   const int32_t* idx;  // row r of the step's batch: >= 0 pool32 row, < 0 pool16 row -idx-1; NULL = r
   int64_t idx_stride;
+  int64_t idx_steps;   // rows of idx (steps) available: no prefetch past the last
   const float* state;
   int parity;
-  int B, chunk;
+  int B;
   float drop_p;
   uint64_t seed;
-  float* hg_part;  // [KS][B][128]
-  float* xhat;     // TRANSPOSED [1536][Bp] (rows >= B zero)
+  float* xhat[2];      // TRANSPOSED [1536][Bp] (rows >= B zero), by step parity
   int64_t Bp;
-  float* stats;    // bucket tail, zeroed here (k2 accumulates into it); may be NULL
+};
+
+struct K1bArgs {
+  const float* P;
+  int64_t g_in, b_in, w0;
+  int B;
+  const float* xhat;  // this step's xhat^T
+  int64_t Bp;
+  float* hg_part;     // [KS][B][128]
+  float* stats;       // bucket tail, zeroed here (k2 accumulates into it); may be NULL
 };
 
 // 32-bit counter hash for the input dropout mask (murmur3's finaliser over
@@ -148,145 +159,198 @@ __device__ __forceinline__ uint32_t drop_hash(uint32_t s0, uint32_t s1, uint32_t
   return h;
 }
 
-// Grid: the KS K-chunks of one 16-row tile run on ONE XCD (blocks b and b + 8
-// share an XCD under round-robin dispatch; speed only, never correctness), so
-// the tile's gathered rows come from that XCD's L2 after the first fetch.
-__global__ void __launch_bounds__(256) k1_input_kernel(K1Args a) {
-  __shared__ __attribute__((aligned(16))) float xn[kR][kChunkMax + 4];  // xhat of the chunk
-  __shared__ __attribute__((aligned(16))) float gb[2][kChunkMax];       // norm_in gamma, beta of the chunk
+// k1a: one 16-row tile, full width. Every loop is unrolled and every global
+// load unconditional (a row outside its pool reads a valid fallback row and is
+// zeroed afterwards), so the vmcnt waits are exact and a wave's four rows are
+// in flight together: one 16-B load per lane per 256 f32 / 512 f16 elements,
+// the f16 row re-reading its first half for slots 3..5. Lane value j holds
+// element 4 (lane + 64 (j / 4)) + j % 4 (f32 rows) or 8 (lane + 64 (j / 8)) +
+// j % 8 (f16 rows): either way values 8 t .. 8 t + 7 fall in columns
+// [512 t, 512 t + 512), so xhat^T is written in three 512-column slabs staged
+// through LDS (slab: [16][516] floats) as 64-B column runs.
+constexpr int kSlabLd = 516;
+template <bool kIdx>
+__device__ __forceinline__ void k1a_tile(const K1aArgs& a, int rt, int step, float* __restrict__ xout,
+                                         float* slab) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int KS = kD / a.chunk;
+  const uint64_t seed = a.seed + static_cast<uint64_t>(step) +
+                        (a.state ? static_cast<uint64_t>(a.state[a.parity * 8 + 4]) << 24 : 0);
+  const uint32_t s0 = static_cast<uint32_t>(seed), s1 = static_cast<uint32_t>(seed >> 32) * 0x27D4EB2Fu;
+  const char* fallback = a.pool32 ? reinterpret_cast<const char*>(a.pool32) : reinterpret_cast<const char*>(a.pool16);
+  int ixs[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    ixs[i] = min(rt * kR + wave * 4 + i, a.B - 1);
+    if (kIdx) ixs[i] = a.idx[static_cast<int64_t>(step) * a.idx_stride + ixs[i]];
+  }
+  uint4 raw[4][6];
+  bool is16[4], ok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = rt * kR + wave * 4 + i;
+    const int ix = __builtin_amdgcn_readfirstlane(ixs[i]);
+    is16[i] = ix < 0;
+    const int64_t row16 = -static_cast<int64_t>(ix) - 1;
+    ok[i] = r < a.B && (is16[i] ? row16 < a.n16 : ix < a.n32);
+    const char* bp = !ok[i] ? fallback
+                     : is16[i] ? reinterpret_cast<const char*>(a.pool16 + row16 * kD)
+                               : reinterpret_cast<const char*>(a.pool32 + static_cast<int64_t>(ix) * kD);
+#pragma unroll
+    for (int u = 0; u < 6; ++u) {
+      const int slot = is16[i] ? u % 3 : u;
+      raw[i][u] = *reinterpret_cast<const uint4*>(bp + 16 * (lane + 64 * slot));
+    }
+  }
+  const float keep = a.drop_p > 0.f ? 1.f / (1.f - a.drop_p) : 1.f;
+  const uint32_t thr = static_cast<uint32_t>(a.drop_p * 65536.f + 0.5f);
+  float xh[4][24];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = rt * kR + wave * 4 + i;
+    float v[24];
+    int c[24];
+#pragma unroll
+    for (int j = 0; j < 24; ++j) {
+      const uint4 w16 = raw[i][j >> 3];
+      const uint32_t word16 = (&w16.x)[(j & 7) >> 1];
+      const _Float16 h = __builtin_bit_cast(_Float16, static_cast<uint16_t>((j & 1) ? word16 >> 16 : word16));
+      const uint4 w32 = raw[i][j >> 2];
+      const float f = __builtin_bit_cast(float, (&w32.x)[j & 3]);
+      v[j] = ok[i] ? (is16[i] ? static_cast<float>(h) : f) : 0.f;
+      c[j] = is16[i] ? 8 * (lane + 64 * (j >> 3)) + (j & 7) : 4 * (lane + 64 * (j >> 2)) + (j & 3);
+    }
+    if (a.drop_p > 0.f) {  // nn.Dropout on the input (wakeword.py:197, :338): one hash per element pair
+      const uint32_t base = static_cast<uint32_t>(r) * (kD / 2);
+#pragma unroll
+      for (int j = 0; j < 24; j += 2) {
+        const uint32_t hsh = drop_hash(s0, s1, base + (c[j] >> 1));
+        v[j] = (hsh & 0xFFFFu) < thr ? 0.f : v[j] * keep;
+        v[j + 1] = (hsh >> 16) < thr ? 0.f : v[j + 1] * keep;
+      }
+    }
+    float sm = 0.f;
+#pragma unroll
+    for (int j = 0; j < 24; ++j) sm += v[j];
+    const float mu = wsum(sm) * (1.f / kD);
+    float sq = 0.f;
+#pragma unroll
+    for (int j = 0; j < 24; ++j) sq += (v[j] - mu) * (v[j] - mu);
+    const float rs = 1.f / sqrtf(wsum(sq) * (1.f / kD) + kLnEps);
+    const bool live = r < a.B;
+#pragma unroll
+    for (int j = 0; j < 24; ++j) xh[i][j] = live ? (v[j] - mu) * rs : 0.f;
+  }
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    __syncthreads();  // the slab's previous readers are done
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float* row = slab + (wave * 4 + i) * kSlabLd;
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const int j = 8 * t + jj;
+        const int col = is16[i] ? 8 * lane + jj : 4 * lane + (jj & 3) + 256 * (jj >> 2);
+        row[col] = xh[i][j];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int col = tid + 256 * h;
+      float* dst = xout + static_cast<int64_t>(512 * t + col) * a.Bp + rt * kR;
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4)
+        *reinterpret_cast<f4*>(dst + 4 * q4) =
+            f4{slab[(4 * q4) * kSlabLd + col], slab[(4 * q4 + 1) * kSlabLd + col],
+               slab[(4 * q4 + 2) * kSlabLd + col], slab[(4 * q4 + 3) * kSlabLd + col]};
+    }
+  }
+}
+
+// Standalone k1a: the step's own xhat (next = 0) or its successor's (next = 1).
+template <bool kIdx>
+__global__ void __launch_bounds__(256) k1a_kernel(K1aArgs a, int next) {
+  __shared__ __attribute__((aligned(16))) float slab[kR * kSlabLd];
+  const int step = step_of(a.state, a.parity) + next;
+  if (kIdx && next && step >= a.idx_steps) return;
+  HBK_MT(0, 1);
+  k1a_tile<kIdx>(a, blockIdx.x, step, a.xhat[a.parity ^ next], slab);
+  HBK_MT(0, 2);
+}
+
+// k1b grid: the KS K-chunks of one 16-row tile run on ONE XCD (blocks b and
+// b + 8 share an XCD under round-robin dispatch; speed only, never
+// correctness), so the tile's xhat rows come from that XCD's L2 after the
+// first fetch. KS is a template argument: all loads unconditional and issued
+// together (the xhat^T tile, norm_in's gamma / beta and the chunk's whole
+// W_hg0 B-fragment set), then the unrolled MFMA chain.
+template <int KS>
+__global__ void __launch_bounds__(256) k1b_kernel(K1bArgs a) {
+  constexpr int kChunk = kD / KS, kN16 = kChunk / 16, kXl = (kChunk + 63) / 64;  // f4 loads per thread
+  __shared__ __attribute__((aligned(16))) float xn[kR][kChunk + 4];  // xhat of the chunk
+  __shared__ __attribute__((aligned(16))) float gb[2][kChunk];       // norm_in gamma, beta of the chunk
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q = blockIdx.x >> 3;
   const int ks = q % KS, rt = (q / KS) * 8 + (blockIdx.x & 7);
   const int n_rt = (a.B + kR - 1) / kR;
   if (rt >= n_rt) return;
-  HBK_MT(0, 1);
-  const int k0 = ks * a.chunk;
-  const int step = step_of(a.state, a.parity);
+  HBK_MT(3, 1);
+  const int k0 = ks * kChunk;
   if (a.stats && rt == 0 && ks == 0 && tid < kStats) a.stats[tid] = 0.f;
-  const int32_t* idx = a.idx ? a.idx + static_cast<int64_t>(step) * a.idx_stride : nullptr;
-  // per-step dropout stream: base seed + step + the epoch salt (state[4])
-  const uint64_t seed = a.seed + static_cast<uint64_t>(step) +
-                        (a.state ? static_cast<uint64_t>(a.state[a.parity * 8 + 4]) << 24 : 0);
-  const uint32_t s0 = static_cast<uint32_t>(seed), s1 = static_cast<uint32_t>(seed >> 32) * 0x27D4EB2Fu;
-  for (int c = tid; c < a.chunk; c += 256) {
-    gb[0][c] = a.P[a.g_in + k0 + c];
-    gb[1][c] = a.P[a.b_in + k0 + c];
+  f4 xt[kXl];
+#pragma unroll
+  for (int h = 0; h < kXl; ++h) {
+    const int e = min(tid + 256 * h, 4 * kChunk - 1);  // clamped: the last pass may be partial
+    xt[h] = *reinterpret_cast<const f4*>(a.xhat + static_cast<int64_t>(k0 + (e >> 2)) * a.Bp + rt * kR + 4 * (e & 3));
   }
-  const float keep = a.drop_p > 0.f ? 1.f / (1.f - a.drop_p) : 1.f;
-  // LayerNorm: wave w normalises rows 4w..4w+3 (all four loaded first); lane
-  // holds elements c = 4 lane + 256 u + e (u < 6, e < 4)
-  f4 v[4][6];
+  float gv[2], bv[2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = rt * kR + wave * 4 + i;
-    const int ix = r < a.B ? (idx ? idx[r] : r) : 0;
-    const bool ok = r < a.B && (ix >= 0 ? ix < a.n32 : -static_cast<int64_t>(ix) - 1 < a.n16);
-    if (ok && ix >= 0) {
-      const f4* src = reinterpret_cast<const f4*>(a.pool32 + static_cast<int64_t>(ix) * kD);
-#pragma unroll
-      for (int u = 0; u < 6; ++u) v[i][u] = src[lane + 64 * u];
-    } else if (ok) {
-      const h4* src = reinterpret_cast<const h4*>(a.pool16 + static_cast<int64_t>(-ix - 1) * kD);
-#pragma unroll
-      for (int u = 0; u < 6; ++u) v[i][u] = __builtin_convertvector(src[lane + 64 * u], f4);
-    } else {
-#pragma unroll
-      for (int u = 0; u < 6; ++u) v[i][u] = f4{0.f, 0.f, 0.f, 0.f};
-    }
+  for (int h = 0; h < 2; ++h) {
+    const int c = min(tid + 256 * h, kChunk - 1);
+    gv[h] = a.P[a.g_in + k0 + c];
+    bv[h] = a.P[a.b_in + k0 + c];
   }
-  // B fragments (W_hg0 rows) of the first 8 K-steps: in flight during the LayerNorm
   const int m = lane & 15, kq = lane >> 4;
   const float* w0 = a.P + a.w0 + static_cast<int64_t>(32 * wave + m) * kD + k0 + 4 * kq;
   const float* w1 = w0 + 16 * kD;
-  const int n16 = a.chunk / 16;
-  f4 rb0[8], rb1[8];
+  f4 rb0[kN16], rb1[kN16];
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    if (u < n16) {
-      rb0[u] = *reinterpret_cast<const f4*>(w0 + 16 * u);
-      rb1[u] = *reinterpret_cast<const f4*>(w1 + 16 * u);
+  for (int i = 0; i < kN16; ++i) {
+    rb0[i] = *reinterpret_cast<const f4*>(w0 + 16 * i);
+    rb1[i] = *reinterpret_cast<const f4*>(w1 + 16 * i);
+  }
+#pragma unroll
+  for (int h = 0; h < kXl; ++h) {
+    const int e = tid + 256 * h, col = e >> 2, r4 = 4 * (e & 3);
+    if (e < 4 * kChunk) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) xn[r4 + u][col] = xt[h][u];
     }
   }
-  HBK_MT(0, 2);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int rl = wave * 4 + i, r = rt * kR + rl;
-    if (a.drop_p > 0.f) {  // nn.Dropout on the input (wakeword.py:197, :338)
-      const uint32_t base = static_cast<uint32_t>(r) * (kD / 2);
-      const uint32_t thr = static_cast<uint32_t>(a.drop_p * 65536.f + 0.5f);
-#pragma unroll
-      for (int u = 0; u < 6; ++u)
-#pragma unroll
-        for (int e = 0; e < 4; e += 2) {
-          const uint32_t h = drop_hash(s0, s1, base + 2 * lane + 128 * u + e / 2);
-          v[i][u][e] = (h & 0xFFFFu) < thr ? 0.f : v[i][u][e] * keep;
-          v[i][u][e + 1] = (h >> 16) < thr ? 0.f : v[i][u][e + 1] * keep;
-        }
+  for (int h = 0; h < 2; ++h)
+    if (tid + 256 * h < kChunk) {
+      gb[0][tid + 256 * h] = gv[h];
+      gb[1][tid + 256 * h] = bv[h];
     }
-    float sm = 0.f;
-#pragma unroll
-    for (int u = 0; u < 6; ++u) sm += (v[i][u][0] + v[i][u][1]) + (v[i][u][2] + v[i][u][3]);
-    const float mu = wsum(sm) * (1.f / kD);
-    float sq = 0.f;
-#pragma unroll
-    for (int u = 0; u < 6; ++u)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float d = v[i][u][e] - mu;
-        sq += d * d;
-      }
-    const float rs = 1.f / sqrtf(wsum(sq) * (1.f / kD) + kLnEps);
-#pragma unroll
-    for (int u = 0; u < 6; ++u) {
-      const int c = 4 * lane + 256 * u;
-      if (c >= k0 && c < k0 + a.chunk) {
-        const f4 xh = r < a.B ? (v[i][u] - mu) * rs : f4{0.f, 0.f, 0.f, 0.f};
-        *reinterpret_cast<f4*>(&xn[rl][c - k0]) = xh;
-      }
-    }
-  }
-  HBK_MT(0, 3);
   __syncthreads();
-  HBK_MT(0, 4);
-  // xhat^T for k3: thread -> one column, the tile's 16 rows as 4 float4 (64 B)
-  if (a.xhat) {
-    for (int c = tid; c < a.chunk; c += 256) {
-      float* dst = a.xhat + static_cast<int64_t>(k0 + c) * a.Bp + rt * kR;
-#pragma unroll
-      for (int q4 = 0; q4 < 4; ++q4)
-        *reinterpret_cast<f4*>(dst + 4 * q4) =
-            f4{xn[4 * q4][c], xn[4 * q4 + 1][c], xn[4 * q4 + 2][c], xn[4 * q4 + 3][c]};
-    }
-  }
+  HBK_MT(3, 2);
   // HG0 partial over this K chunk: wave w -> output columns [32 w, 32 w + 32).
-  // MFMA step (i, s) covers k = 16 i + 4 kq + s for lane group kq: A and B
-  // both read float4 runs along k. B fragments stream through an 8-step
-  // register ring (the load of step i + 8 is issued when step i is consumed).
+  // MFMA step (i, s) covers k = 16 i + 4 kq + s for lane group kq; the two
+  // 16-column tiles are two interleaved accumulator chains.
   const float* xr = &xn[m][4 * kq];
   f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-  for (int i0 = 0; i0 < n16; i0 += 8) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i = i0 + u;
-      if (i < n16) {
-        const f4 gg = *reinterpret_cast<const f4*>(&gb[0][16 * i + 4 * kq]);
-        const f4 be = *reinterpret_cast<const f4*>(&gb[1][16 * i + 4 * kq]);
-        const f4 av = *reinterpret_cast<const f4*>(xr + 16 * i) * gg + be;  // LN output = xhat g + b
-        const f4 b0 = rb0[u], b1 = rb1[u];
-        if (i + 8 < n16) {
-          rb0[u] = *reinterpret_cast<const f4*>(w0 + 16 * (i + 8));
-          rb1[u] = *reinterpret_cast<const f4*>(w1 + 16 * (i + 8));
-        }
+  for (int i = 0; i < kN16; ++i) {
+    const f4 gg = *reinterpret_cast<const f4*>(&gb[0][16 * i + 4 * kq]);
+    const f4 be = *reinterpret_cast<const f4*>(&gb[1][16 * i + 4 * kq]);
+    const f4 av = *reinterpret_cast<const f4*>(xr + 16 * i) * gg + be;  // LN output = xhat g + b
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          acc0 = mma(av[s], b0[s], acc0);
-          acc1 = mma(av[s], b1[s], acc1);
-        }
-      }
+    for (int s = 0; s < 4; ++s) {
+      acc0 = mma(av[s], rb0[i][s], acc0);
+      acc1 = mma(av[s], rb1[i][s], acc1);
     }
   }
-  HBK_MT(0, 5);
   float* out = a.hg_part + static_cast<int64_t>(ks) * a.B * kH2;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -296,6 +360,7 @@ __global__ void __launch_bounds__(256) k1_input_kernel(K1Args a) {
       out[static_cast<int64_t>(r) * kH2 + 32 * wave + 16 + m] = acc1[e];
     }
   }
+  HBK_MT(3, 3);
 }
 
 // ------------------------------------------------------------------ k2 ----
@@ -392,6 +457,9 @@ struct K2Args {
   float* Xn;
   float* dS;
   float* dHG;
+  // workgroups n_rt .. 2 n_rt - 1 (when prefetch): k1a of the NEXT step
+  int n_rt, prefetch;
+  K1aArgs pre;
 };
 
 // Backward weights go through LDS: W_hg [128][96] and W_o [96][64] are read
@@ -474,6 +542,12 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
   __shared__ unsigned long long trS[4][48];
   int trn = 0;
 #endif
+  if (kTrain && static_cast<int>(blockIdx.x) >= a.n_rt) {  // next step's k1a (weights not needed)
+    const int step = step_of(a.pre.state, a.pre.parity) + 1;
+    if (step < a.pre.idx_steps)
+      k1a_tile<true>(a.pre, blockIdx.x - a.n_rt, step, a.pre.xhat[a.pre.parity ^ 1], wX);
+    return;
+  }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int m = lane & 15, kq = lane >> 4;
   const int r0 = blockIdx.x * kR;
@@ -1097,13 +1171,14 @@ __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
 
 // --------------------------------------------------------- workspace ------
 struct FusedWs {
-  int64_t hg_part, xhat, U, Xn, dS, dHG, total;  // float offsets
+  int64_t hg_part, xhat[2], U, Xn, dS, dHG, total;  // float offsets
 };
 int k1_splits(int B) {
   const int rt = (B + kR - 1) / kR;
+  const int rt8 = (rt + 7) / 8 * 8;
   static const int ks_opts[] = {4, 6, 8, 12, 16, 24};
   for (int ks : ks_opts)
-    if (rt * ks >= 240) return ks;
+    if (rt8 * ks >= 480) return ks;
   return 24;
 }
 FusedWs fused_layout(int64_t B, int NG) {
@@ -1112,7 +1187,8 @@ FusedWs fused_layout(int64_t B, int NG) {
   auto take = [&](int64_t n) { const int64_t r = o; o += (n + 63) & ~int64_t(63); return r; };
   const int64_t Bp = (B + kR - 1) / kR * kR;
   w.hg_part = take(int64_t(24) * B * kH2);
-  w.xhat = take(Bp * kD);
+  w.xhat[0] = take(Bp * kD);
+  w.xhat[1] = take(Bp * kD);
   w.U = take(int64_t(NG) * Bp * kH);
   w.Xn = take(int64_t(NG) * Bp * kL);
   w.dS = take(int64_t(NG) * Bp * kL);
@@ -1149,39 +1225,62 @@ int64_t mlp_fused_ws_floats(const hbk_mlp_plan& p, int64_t B) {
 
 // k1 + k2 (+ k3): the forward (inference) or forward/backward half of a step.
 int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool32, int64_t n32,
-                  const void* pool16, int64_t n16, const int32_t* idx, int64_t idx_stride, const float* y, int64_t y_stride, int B,
-                  const float* state, int parity, const float* sched, int sched_len, float neg_weight,
-                  float thr, float act_thr, float drop_p, uint64_t seed, float* bucket, float* prob,
-                  float* logit, float* ws, bool train, hipStream_t s) {
+                  const void* pool16, int64_t n16, const int32_t* idx, int64_t idx_stride, int64_t idx_steps,
+                  const float* y, int64_t y_stride, int B, const float* state, int parity, const float* sched,
+                  int sched_len, float neg_weight, float thr, float act_thr, float drop_p, uint64_t seed,
+                  float* bucket, float* prob, float* logit, float* ws, bool train, int flags, hipStream_t s) {
   const int NG = static_cast<int>(p.g.size());
   const FusedWs w = fused_layout(B, NG);
   const int KS = k1_splits(B);
-  K1Args k1;
-  k1.P = params;
-  k1.g_in = p.ln_in.g;
-  k1.b_in = p.ln_in.b;
-  k1.w0 = p.g[0].w_hg;
-  k1.pool32 = pool32;
-  k1.pool16 = static_cast<const _Float16*>(pool16);
-  k1.n32 = pool32 ? n32 : 0;
-  k1.n16 = pool16 ? n16 : 0;
-  k1.idx = idx;
-  k1.idx_stride = idx_stride;
-  k1.state = state;
-  k1.parity = parity;
-  k1.B = B;
-  k1.chunk = kD / KS;
-  k1.drop_p = drop_p;
-  k1.seed = seed;
   const int64_t Bp = (B + kR - 1) / kR * kR;
-  k1.hg_part = ws + w.hg_part;
-  k1.xhat = train ? ws + w.xhat : nullptr;
-  k1.Bp = Bp;
-  k1.stats = train ? bucket + p.n_params : nullptr;
   const int rt = (B + kR - 1) / kR;
-  const int rt8 = (rt + 7) / 8 * 8;  // XCD-aware 1-D grid (see k1_input_kernel)
-  hipLaunchKernelGGL(k1_input_kernel, dim3(rt8 * KS), dim3(256), 0, s, k1);
-  HBK_LAUNCH_CHECK("k1_input_kernel");
+  const int rt8 = (rt + 7) / 8 * 8;  // XCD-aware 1-D grid (see k1b_kernel)
+  K1aArgs ka;
+  ka.pool32 = pool32;
+  ka.pool16 = static_cast<const _Float16*>(pool16);
+  ka.n32 = pool32 ? n32 : 0;
+  ka.n16 = pool16 ? n16 : 0;
+  ka.idx = idx;
+  ka.idx_stride = idx_stride;
+  ka.idx_steps = idx ? idx_steps : 0;
+  ka.state = state;
+  ka.parity = parity;
+  ka.B = B;
+  ka.drop_p = drop_p;
+  ka.seed = seed;
+  ka.xhat[0] = ws + w.xhat[0];
+  ka.xhat[1] = ws + w.xhat[1];
+  ka.Bp = Bp;
+  const float* xhat = ws + w.xhat[parity];
+  if (!(flags & HBK_STEP_XHAT_READY)) {  // this step's rows were not prefetched by the previous step
+    if (idx)
+      hipLaunchKernelGGL(k1a_kernel<true>, dim3(rt), dim3(256), 0, s, ka, 0);
+    else
+      hipLaunchKernelGGL(k1a_kernel<false>, dim3(rt), dim3(256), 0, s, ka, 0);
+    HBK_LAUNCH_CHECK("k1a_kernel");
+  }
+  K1bArgs kb;
+  kb.P = params;
+  kb.g_in = p.ln_in.g;
+  kb.b_in = p.ln_in.b;
+  kb.w0 = p.g[0].w_hg;
+  kb.B = B;
+  kb.xhat = xhat;
+  kb.Bp = Bp;
+  kb.hg_part = ws + w.hg_part;
+  kb.stats = train ? bucket + p.n_params : nullptr;
+  {
+    auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(rt8 * KS), dim3(256), 0, s, kb); };
+    switch (KS) {
+      case 4: launch(k1b_kernel<4>); break;
+      case 6: launch(k1b_kernel<6>); break;
+      case 8: launch(k1b_kernel<8>); break;
+      case 12: launch(k1b_kernel<12>); break;
+      case 16: launch(k1b_kernel<16>); break;
+      default: launch(k1b_kernel<24>);
+    }
+    HBK_LAUNCH_CHECK("k1b_kernel");
+  }
   K2Args k2;
   k2.P = params;
   k2.B = B;
@@ -1206,8 +1305,12 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
   k2.dS = ws + w.dS;
   k2.dHG = ws + w.dHG;
   k2.Bp = Bp;
+  k2.n_rt = rt;
+  k2.prefetch = train && idx && (flags & HBK_STEP_PREFETCH_NEXT);
+  k2.pre = ka;
   {
-    auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(rt), dim3(256), 0, s, k2); };
+    const int grid = k2.prefetch ? 2 * rt : rt;
+    auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, k2); };
     if (train) {
       if (NG == 2) launch(k2_rows_kernel<true, 2>);
       else if (NG == 3) launch(k2_rows_kernel<true, 3>);
@@ -1239,7 +1342,7 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
     ++nj;
   };
   float* G = bucket;
-  add(ws + w.dHG, ws + w.xhat, G + p.g[0].w_hg, kD, kH2, kD);
+  add(ws + w.dHG, xhat, G + p.g[0].w_hg, kD, kH2, kD);
   for (int k = 1; k < NG; ++k)
     add(ws + w.dHG + int64_t(k) * kH2 * Bp, ws + w.Xn + int64_t(k) * kL * Bp, G + p.g[k].w_hg, kL, kH2, kL);
   for (int k = 0; k < NG; ++k)
@@ -1288,10 +1391,10 @@ int mlp_fused_update(const hbk_mlp_plan& p, float* params, float* bucket, float*
 
 #ifdef HBK_TRACE
 extern "C" int hbk_debug_mlp_trace(unsigned long long* out, int* counts) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hbk::g_mlp_trace), sizeof(unsigned long long) * 3 * 4 * 128) != hipSuccess)
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hbk::g_mlp_trace), sizeof(unsigned long long) * 4 * 4 * 128) != hipSuccess)
     return -2;
-  if (hipMemcpyFromSymbol(counts, HIP_SYMBOL(hbk::g_mlp_trace_n), sizeof(int) * 12) != hipSuccess) return -2;
-  int z[12] = {};
+  if (hipMemcpyFromSymbol(counts, HIP_SYMBOL(hbk::g_mlp_trace_n), sizeof(int) * 16) != hipSuccess) return -2;
+  int z[16] = {};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(hbk::g_mlp_trace_n), z, sizeof(z));
   return 0;
 }

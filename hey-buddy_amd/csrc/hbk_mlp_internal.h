@@ -46,10 +46,10 @@ __device__ __forceinline__ float uniform01(uint64_t seed, uint64_t i) {
 bool mlp_fused_supported(const hbk_mlp_plan& p);
 int64_t mlp_fused_ws_floats(const hbk_mlp_plan& p, int64_t B);
 int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool32, int64_t n32,
-                  const void* pool16, int64_t n16, const int32_t* idx, int64_t idx_stride, const float* y, int64_t y_stride, int B,
-                  const float* state, int parity, const float* sched, int sched_len, float neg_weight,
-                  float thr, float act_thr, float drop_p, uint64_t seed, float* bucket, float* prob,
-                  float* logit, float* ws, bool train, hipStream_t s);
+                  const void* pool16, int64_t n16, const int32_t* idx, int64_t idx_stride, int64_t idx_steps,
+                  const float* y, int64_t y_stride, int B, const float* state, int parity, const float* sched,
+                  int sched_len, float neg_weight, float thr, float act_thr, float drop_p, uint64_t seed,
+                  float* bucket, float* prob, float* logit, float* ws, bool train, int flags, hipStream_t s);
 int mlp_fused_update(const hbk_mlp_plan& p, float* params, float* bucket, float* m, float* v, float* state,
                      int parity, const float* sched, int sched_len, float lr, float b1, float b2, float eps,
                      float* hist, int hist_cap, hipStream_t s);

@@ -87,7 +87,8 @@ _PROTOS = {
     "hbk_mlp_fused_supported": (_c_int, [_vp, ctypes.POINTER(ctypes.c_int32)]),
     "hbk_mlp_step_fwd_bwd": (_c_int, [_vp, _vp, _vp, _c_int64, _vp, _c_int64, _vp, _c_int64, _vp, _c_int64,
                                       _c_int64, _vp, ctypes.c_int32, _vp, _c_int64, _c_float, _c_float,
-                                      _c_float, _c_float, ctypes.c_uint64, _vp, _vp, _vp, _c_int64, _vp]),
+                                      _c_float, _c_float, ctypes.c_uint64, _vp, _vp, _c_int64, ctypes.c_int32,
+                                      _vp, _c_int64, _vp]),
     "hbk_mlp_step_update": (_c_int, [_vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int32, _vp, _c_int64, _c_float,
                                      _c_float, _c_float, _c_float, _vp, ctypes.c_int32, _vp]),
 }

@@ -425,11 +425,16 @@ class MlpPlan:
                      idx_stride: int = 0, y_stride: int = 0, sched: torch.Tensor | None = None,
                      neg_weight: float = 1.0, threshold: float = 1e-4, activation_threshold: float = 0.5,
                      dropout_p: float = 0.0, seed: int = 0, prob: torch.Tensor | None = None,
-                     workspace: torch.Tensor | None = None) -> None:
+                     workspace: torch.Tensor | None = None, xhat_ready: bool = False,
+                     prefetch_next: bool = False, idx_steps: int | None = None) -> None:
         """Forward / filter / BCE / backward of one step into ``bucket``
         (hbk_mlp_step_fwd_bwd). Rows come from pool32 [n, 1536] f32 and pool16
         [n, 1536] f16 by ``idx`` (int32, >= 0 -> pool32, < 0 -> pool16 row -i-1;
-        None -> pool32 rows 0..batch-1); y: 0/1 float32 labels on the device."""
+        None -> pool32 rows 0..batch-1); y: 0/1 float32 labels on the device.
+        ``prefetch_next``: also gather + normalise step + 1's rows (idx row
+        step + 1 < idx_steps, default idx.numel() // idx_stride) during this
+        step; ``xhat_ready``: the previous call on this workspace did that for
+        this step."""
         dev = params.device
         if params.numel() != self.n_params or bucket.numel() != self.n_params + self.N_STATS:
             raise ValueError("params / bucket do not match the plan")
@@ -448,10 +453,13 @@ class MlpPlan:
         if sched is not None and (sched.dtype != torch.float32 or sched.shape[-1] != 2 or sched.device != dev):
             raise ValueError("sched must be float32 [n, 2] (lr, neg_weight) on the device")
         ws = self.workspace(batch, dev) if workspace is None else workspace
+        if idx_steps is None:
+            idx_steps = idx.numel() // idx_stride if idx is not None and idx_stride > 0 else 1
+        flags = (1 if xhat_ready else 0) | (2 if prefetch_next and idx is not None else 0)
         torch.ops.hbk.mlp_step_fwd_bwd(params, bucket, state, int(parity), y, int(batch), pool32, pool16, idx,
                                        int(idx_stride), int(y_stride), sched, float(neg_weight), float(threshold),
                                        float(activation_threshold), float(dropout_p), _u64_to_i64(seed), prob, ws,
-                                       self.id)
+                                       int(idx_steps), int(flags), self.id)
 
     def step_update(self, params: torch.Tensor, bucket: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
                     state: torch.Tensor, parity: int, sched: torch.Tensor | None = None, lr: float = 1e-3,
@@ -493,15 +501,16 @@ def _mlp_step_fwd_bwd_op(params: torch.Tensor, bucket: torch.Tensor, state: torc
                          y: torch.Tensor, batch: int, pool32: torch.Tensor | None, pool16: torch.Tensor | None,
                          idx: torch.Tensor | None, idx_stride: int, y_stride: int, sched: torch.Tensor | None,
                          neg_weight: float, threshold: float, activation_threshold: float, dropout_p: float,
-                         seed: int, prob: torch.Tensor | None, ws: torch.Tensor, plan_id: int) -> None:
+                         seed: int, prob: torch.Tensor | None, ws: torch.Tensor, idx_steps: int, flags: int,
+                         plan_id: int) -> None:
     plan = _plans[plan_id]
     opt = lambda t: ptr(t) if t is not None else None  # noqa: E731
     check(lib().hbk_mlp_step_fwd_bwd(
         plan._handle, ptr(params), opt(pool32), pool32.shape[0] if pool32 is not None else 0, opt(pool16),
         pool16.shape[0] if pool16 is not None else 0, opt(idx), idx_stride, ptr(y), y_stride, batch, ptr(state),
         parity, opt(sched), sched.shape[0] if sched is not None else 0, neg_weight, threshold,
-        activation_threshold, dropout_p, seed & (2 ** 64 - 1), ptr(bucket), opt(prob), ptr(ws), ws.numel(),
-        stream_ptr(params.device)), "hbk_mlp_step_fwd_bwd")
+        activation_threshold, dropout_p, seed & (2 ** 64 - 1), ptr(bucket), opt(prob), idx_steps, flags, ptr(ws),
+        ws.numel(), stream_ptr(params.device)), "hbk_mlp_step_fwd_bwd")
 
 
 @torch.library.custom_op("hbk::mlp_step_update", mutates_args=("params", "bucket", "m", "v", "state", "history"))

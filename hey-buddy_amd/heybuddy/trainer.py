@@ -359,18 +359,24 @@ class WakeWordTrainer(Trainer):
         if ws is None or ws.numel() < need or ws.device != dev:
             ws = self._indexed_ws = torch.empty(need, dtype=torch.uint8, device=dev)
 
-        def one(parity: int) -> None:
+        # Each step also gathers + normalises the NEXT step's rows inside its own
+        # launches (prefetch_next); only the first step of this call gathers its own.
+        def one(parity: int, ready: bool) -> None:
             plan.step_fwd_bwd(flat, self._bucket, self._fstate, parity, y, B, pool32=p32, pool16=p16, idx=idx,
                               idx_stride=B, y_stride=y_stride, sched=sched, threshold=threshold,
                               activation_threshold=activation_threshold, dropout_p=p, seed=self._seed_base,
-                              workspace=ws)
+                              workspace=ws, xhat_ready=ready, prefetch_next=True, idx_steps=S)
             distributed.reduce_bucket(self._bucket)
             plan.step_update(flat, self._bucket, self._m, self._v, self._fstate, parity, sched=sched,
                              beta1=BETAS[0], beta2=BETAS[1], eps=EPS, history=history)
 
         done = 0
+        if S > 0:  # the first step gathers its own rows and prefetches the next
+            one(self._parity, False)
+            self._parity ^= 1
+            done = 1
         k = max(2, steps_per_graph - steps_per_graph % 2)
-        if graphs and world == 1 and S >= k:
+        if graphs and world == 1 and S - done >= k:
             key = ("indexed", k, self._parity, B, y_stride, float(threshold), float(activation_threshold), float(p),
                    tuple(t.data_ptr() if t is not None else 0 for t in (idx, y, sched, p32, p16, history, ws)))
             entry = self._graphs.get(key)
@@ -384,14 +390,14 @@ class WakeWordTrainer(Trainer):
                 with torch.cuda.stream(side):
                     with torch.cuda.graph(gr, stream=side):
                         for j in range(k):
-                            one(par0 ^ (j & 1))
+                            one(par0 ^ (j & 1), True)
                 torch.cuda.current_stream(dev).wait_stream(side)
                 self._graphs[key] = (gr, ws)  # the entry keeps the baked-in workspace alive
             while S - done >= k:
                 gr.replay()
                 done += k
         while done < S:
-            one(self._parity)
+            one(self._parity, True)
             self._parity ^= 1
             done += 1
 

@@ -212,15 +212,26 @@ int hbk_mlp_gate_adam(const hbk_mlp_plan* plan, float* params, const float* buck
  * bucket [n_params + 8]: must be zero before the first step (hbk_mlp_step_update
  *   zeroes it for the next one); receives the unnormalised gradients and the
  *   statistics of hbk_mlp_train_fwd_bwd. history as in hbk_mlp_gate_adam.
- * The dropout mask of element i of step s is f(seed + s + (salt << 24), i). */
+ * The dropout mask of element i of step s is f(seed + s + (salt << 24), i).
+ *
+ * The input gather + dropout + LayerNorm of a step needs no weights, so it is
+ * computed one step AHEAD inside the previous step's launches:
+ *   flags & HBK_STEP_PREFETCH_NEXT (with idx): this call also computes step + 1's
+ *     normalised rows (rows idx[step + 1], if step + 1 < idx_steps) into the
+ *     workspace, concurrently with its own chain kernel;
+ *   flags & HBK_STEP_XHAT_READY: this step's rows were prefetched that way (the
+ *     previous call on the same workspace set PREFETCH_NEXT) and are not
+ *     recomputed. Without it the step gathers its own rows first. */
+#define HBK_STEP_XHAT_READY 1
+#define HBK_STEP_PREFETCH_NEXT 2
 int hbk_mlp_fused_supported(const hbk_mlp_plan* plan, int32_t* supported);
 int hbk_mlp_step_fwd_bwd(const hbk_mlp_plan* plan, const float* params, const float* pool32, int64_t n32,
                          const void* pool16, int64_t n16, const int32_t* idx, int64_t idx_step_stride,
                          const float* y, int64_t y_step_stride, int64_t batch, const float* state,
                          int32_t parity, const float* sched, int64_t sched_len, float neg_weight,
                          float high_loss_threshold, float activation_threshold, float dropout_p,
-                         uint64_t seed, float* bucket, float* prob, void* workspace,
-                         int64_t workspace_bytes, void* stream);
+                         uint64_t seed, float* bucket, float* prob, int64_t idx_steps, int32_t flags,
+                         void* workspace, int64_t workspace_bytes, void* stream);
 int hbk_mlp_step_update(const hbk_mlp_plan* plan, float* params, float* bucket, float* m, float* v,
                         float* state, int32_t parity, const float* sched, int64_t sched_len, float lr,
                         float beta1, float beta2, float eps, float* history, int32_t history_cap,

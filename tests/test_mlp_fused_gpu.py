@@ -62,10 +62,11 @@ def test_fused_grads_match_reference():
         np.testing.assert_allclose(g[k].cpu().numpy() / scale, ref / scale, rtol=0, atol=1e-4, err_msg=k)
 
 
-@pytest.mark.parametrize("B", [1100, 550, 273, 17, 1])
+@pytest.mark.parametrize("B", [1100, 1000, 550, 500, 273, 100, 17, 1])
 def test_fused_matches_generic_path(B):
     """Same step through the generic kernels (hbk_mlp_train_fwd_bwd) and the
-    fused ones, at the reference's stage batch sizes and ragged tails."""
+    fused ones, at the reference's stage batch sizes, ragged tails and every
+    K-split of the input GEMM (KS 8 / 12 / 16 / 24 at B 1100 / 550 / 500 / 273)."""
     params = gc.golden_inputs()[0]
     m = _model(params)
     rng = np.random.default_rng(B)
@@ -153,3 +154,16 @@ def test_train_indexed_equals_eager_steps(tmp_path):
     d = (p1 - p0).abs()
     assert float((d > 1e-5).float().mean()) < 1e-3 and float(d.max()) <= 2e-2
     torch.testing.assert_close(s1, s0)
+
+
+@pytest.mark.parametrize("B", [1, 100, 273, 500, 550, 1000, 1100, 2000, 5000])
+def test_fused_forward_matches_oracle(B):
+    """Inference (hbk_mlp_forward: k1a + k1b + k2) against the oracle forward
+    at every K-split of the input GEMM; probabilities within 1e-6."""
+    from oracle import mlp as omlp
+    params = gc.golden_inputs()[0]
+    m = _model(params).eval()
+    x = (np.random.default_rng(B).standard_normal((B, 16, 96)) * 1.3 + 0.2).astype(np.float32)
+    p = m(torch.from_numpy(x).cuda()).cpu().numpy().ravel()
+    po, _, _ = omlp.forward(params, x)
+    np.testing.assert_allclose(p, po, rtol=0, atol=1e-6)

@@ -58,8 +58,8 @@ def trace():
     tr, pos, neg, idx, y, sched = setup(4)
     fn = lib().hbk_debug_mlp_trace
     fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-    buf = (ctypes.c_ulonglong * (3 * 4 * 128))()
-    cnt = (ctypes.c_int * 12)()
+    buf = (ctypes.c_ulonglong * (4 * 4 * 128))()
+    cnt = (ctypes.c_int * 16)()
     tr._reset_accumulation()
     tr.train_indexed(idx[:2], y, sched, pool32=pos, pool16=neg, graphs=False)
     torch.cuda.synchronize()
@@ -67,12 +67,15 @@ def trace():
     tr.train_indexed(idx[2:3], y, sched, pool32=pos, pool16=neg, graphs=False)
     torch.cuda.synchronize()
     fn(buf, cnt)
-    for k, name in enumerate(("k1_input", "k2_rows", "k3_wgrad")):
+    for k, name in enumerate(("k1a (standalone only)", "k2_rows", "k3_wgrad", "k1b_gemm")):
         evs = []
         for w in range(4):
             n = cnt[k * 4 + w]
             evs.append([(int(buf[(k * 4 + w) * 128 + i]) >> 56, int(buf[(k * 4 + w) * 128 + i]) & ((1 << 56) - 1))
                         for i in range(n)])
+        if not any(evs):
+            print(f"--- {name}: no marks")
+            continue
         t0 = min(e[0][1] for e in evs if e)
         print(f"--- {name} (block 0; cycles from the first mark)")
         for w, e in enumerate(evs):
