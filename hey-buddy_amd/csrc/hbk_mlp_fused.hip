@@ -89,6 +89,17 @@ __device__ __forceinline__ float wsum(float v) {
          (__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 32)) +
           __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 48)));
 }
+__device__ __forceinline__ float wmax(float v) {
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x141>(v));
+  v = fmaxf(v, dpp_f<0x140>(v));
+  const int b = __builtin_bit_cast(int, v);
+  return fmaxf(fmaxf(__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 0)),
+                     __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 16))),
+               fmaxf(__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 32)),
+                     __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 48))));
+}
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
 
 #ifdef HBK_TRACE
@@ -278,30 +289,69 @@ __global__ void __launch_bounds__(256) k1a_kernel(K1aArgs a, int next) {
   HBK_MT(0, 2);
 }
 
-// k1b grid: the KS K-chunks of one 16-row tile run on ONE XCD (blocks b and
-// b + 8 share an XCD under round-robin dispatch; speed only, never
-// correctness), so the tile's xhat rows come from that XCD's L2 after the
-// first fetch. KS is a template argument: all loads unconditional and issued
-// together (the xhat^T tile, norm_in's gamma / beta and the chunk's whole
-// W_hg0 B-fragment set), then the unrolled MFMA chain.
+// Split-f16 products on v_mfma_f32_16x16x32_f16: v = hi + lo with hi = v
+// rounded toward zero to f16 and lo = f16(v - hi) (v - hi is exact in f32), so
+// a . b ~ hi_a hi_b + hi_a lo_b + lo_a hi_b (the dropped lo_a lo_b is
+// ~2^-22 relative): three f16 MFMAs (16 cycles each per 16x16x32) for the 8
+// f32 MFMAs (32 cycles each) of the same 32-deep product. Two values per
+// 3 VALU instructions (v_cvt_pkrtz + two v_fma_mix).
+typedef __fp16 hh2 __attribute__((ext_vector_type(2)));
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ void split_pair(float a, float b, uint32_t& hi, uint32_t& lo) {
+  const hh2 h = __builtin_amdgcn_cvt_pkrtz(a, b);
+  hi = __builtin_bit_cast(uint32_t, h);
+  uint32_t l = 0;
+  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "+v"(l) : "v"(a), "v"(hi));
+  asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(l) : "v"(b), "v"(hi));
+  lo = l;
+}
+// 8 floats (two f4) -> hi / lo h8
+__device__ __forceinline__ void split8(const f4& x0, const f4& x1, h8& hi, h8& lo) {
+  uint32_t h[4], l[4];
+  split_pair(x0[0], x0[1], h[0], l[0]);
+  split_pair(x0[2], x0[3], h[1], l[1]);
+  split_pair(x1[0], x1[1], h[2], l[2]);
+  split_pair(x1[2], x1[3], h[3], l[3]);
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  hi = __builtin_bit_cast(h8, u4{h[0], h[1], h[2], h[3]});
+  lo = __builtin_bit_cast(h8, u4{l[0], l[1], l[2], l[3]});
+}
+__device__ __forceinline__ f4 mma3(const h8& ah, const h8& al, const h8& bh, const h8& bl, f4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, c, 0, 0, 0);
+}
+
+// k1b: HG0 partials for 64 rows x one K-chunk per workgroup (4 MFMA row tiles
+// share each W fragment: W is read from L2 ceil(B / 64) times per step, not
+// ceil(B / 16)). Grid: the KS chunks of one 64-row block run on ONE XCD
+// (blocks b and b + 8 share an XCD under round-robin dispatch; speed only).
+// KS is a template argument: all loads unconditional and issued together (the
+// xhat^T tile, norm_in's gamma / beta, the chunk's W_hg0 fragments), then the
+// unrolled split-f16 chain. W is scaled by 16 before the split (keeps lo of
+// |W| ~ 1e-2 in f16's normal range); the sums are scaled back exactly.
+constexpr int kRB = 64;
 template <int KS>
 __global__ void __launch_bounds__(256) k1b_kernel(K1bArgs a) {
-  constexpr int kChunk = kD / KS, kN16 = kChunk / 16, kXl = (kChunk + 63) / 64;  // f4 loads per thread
-  __shared__ __attribute__((aligned(16))) float xn[kR][kChunk + 4];  // xhat of the chunk
-  __shared__ __attribute__((aligned(16))) float gb[2][kChunk];       // norm_in gamma, beta of the chunk
+  constexpr int kChunk = kD / KS, kN32 = kChunk / 32, kXl = kChunk / 16;  // xhat^T f4 loads per thread
+  __shared__ __attribute__((aligned(16))) float xn[kRB][kChunk + 4];  // xhat of the chunk
+  __shared__ __attribute__((aligned(16))) float gb[2][kChunk];        // norm_in gamma, beta of the chunk
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q = blockIdx.x >> 3;
-  const int ks = q % KS, rt = (q / KS) * 8 + (blockIdx.x & 7);
-  const int n_rt = (a.B + kR - 1) / kR;
-  if (rt >= n_rt) return;
+  const int ks = q % KS, rb = (q / KS) * 8 + (blockIdx.x & 7);
+  const int r0 = rb * kRB;
+  if (r0 >= a.B) return;
   HBK_MT(3, 1);
   const int k0 = ks * kChunk;
-  if (a.stats && rt == 0 && ks == 0 && tid < kStats) a.stats[tid] = 0.f;
+  if (a.stats && rb == 0 && ks == 0 && tid < kStats) a.stats[tid] = 0.f;
+  // xhat^T: column c holds the block's 64 rows as 16 float4; rows past Bp read
+  // a clamped (valid) run, their outputs are never stored
   f4 xt[kXl];
 #pragma unroll
   for (int h = 0; h < kXl; ++h) {
-    const int e = min(tid + 256 * h, 4 * kChunk - 1);  // clamped: the last pass may be partial
-    xt[h] = *reinterpret_cast<const f4*>(a.xhat + static_cast<int64_t>(k0 + (e >> 2)) * a.Bp + rt * kR + 4 * (e & 3));
+    const int e = tid + 256 * h, col = e >> 4;
+    const int row = min(r0 + 4 * (e & 15), static_cast<int>(a.Bp) - 4);
+    xt[h] = *reinterpret_cast<const f4*>(a.xhat + static_cast<int64_t>(k0 + col) * a.Bp + row);
   }
   float gv[2], bv[2];
 #pragma unroll
@@ -310,22 +360,23 @@ __global__ void __launch_bounds__(256) k1b_kernel(K1bArgs a) {
     gv[h] = a.P[a.g_in + k0 + c];
     bv[h] = a.P[a.b_in + k0 + c];
   }
+  // W fragments: lane (n = m, kq) of column tile c holds W[32 w + 16 c + m][k0 + 32 i + 8 kq .. + 7]
   const int m = lane & 15, kq = lane >> 4;
-  const float* w0 = a.P + a.w0 + static_cast<int64_t>(32 * wave + m) * kD + k0 + 4 * kq;
-  const float* w1 = w0 + 16 * kD;
-  f4 rb0[kN16], rb1[kN16];
+  f4 wr[2][kN32][2];
 #pragma unroll
-  for (int i = 0; i < kN16; ++i) {
-    rb0[i] = *reinterpret_cast<const f4*>(w0 + 16 * i);
-    rb1[i] = *reinterpret_cast<const f4*>(w1 + 16 * i);
+  for (int c = 0; c < 2; ++c) {
+    const float* wp = a.P + a.w0 + static_cast<int64_t>(32 * wave + 16 * c + m) * kD + k0 + 8 * kq;
+#pragma unroll
+    for (int i = 0; i < kN32; ++i) {
+      wr[c][i][0] = *reinterpret_cast<const f4*>(wp + 32 * i);
+      wr[c][i][1] = *reinterpret_cast<const f4*>(wp + 32 * i + 4);
+    }
   }
 #pragma unroll
   for (int h = 0; h < kXl; ++h) {
-    const int e = tid + 256 * h, col = e >> 2, r4 = 4 * (e & 3);
-    if (e < 4 * kChunk) {
+    const int e = tid + 256 * h, col = e >> 4, r4 = 4 * (e & 15);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) xn[r4 + u][col] = xt[h][u];
-    }
+    for (int u = 0; u < 4; ++u) xn[r4 + u][col] = xt[h][u];
   }
 #pragma unroll
   for (int h = 0; h < 2; ++h)
@@ -333,33 +384,45 @@ __global__ void __launch_bounds__(256) k1b_kernel(K1bArgs a) {
       gb[0][tid + 256 * h] = gv[h];
       gb[1][tid + 256 * h] = bv[h];
     }
+  h8 whi[2][kN32], wlo[2][kN32];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int i = 0; i < kN32; ++i) split8(wr[c][i][0] * 16.f, wr[c][i][1] * 16.f, whi[c][i], wlo[c][i]);
   __syncthreads();
   HBK_MT(3, 2);
-  // HG0 partial over this K chunk: wave w -> output columns [32 w, 32 w + 32).
-  // MFMA step (i, s) covers k = 16 i + 4 kq + s for lane group kq; the two
-  // 16-column tiles are two interleaved accumulator chains.
-  const float* xr = &xn[m][4 * kq];
-  f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+  // wave w -> output columns [32 w, 32 w + 32) of all 64 rows: 4 row tiles x 2
+  // column tiles, A = LN output = xhat g + b from LDS (k = 32 i + 8 kq ..)
+  f4 acc[4][2];
 #pragma unroll
-  for (int i = 0; i < kN16; ++i) {
-    const f4 gg = *reinterpret_cast<const f4*>(&gb[0][16 * i + 4 * kq]);
-    const f4 be = *reinterpret_cast<const f4*>(&gb[1][16 * i + 4 * kq]);
-    const f4 av = *reinterpret_cast<const f4*>(xr + 16 * i) * gg + be;  // LN output = xhat g + b
+  for (int t = 0; t < 4; ++t) acc[t][0] = acc[t][1] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      acc0 = mma(av[s], rb0[i][s], acc0);
-      acc1 = mma(av[s], rb1[i][s], acc1);
+  for (int i = 0; i < kN32; ++i) {
+    const int kk = 32 * i + 8 * kq;
+    const f4 g0 = *reinterpret_cast<const f4*>(&gb[0][kk]), g1 = *reinterpret_cast<const f4*>(&gb[0][kk + 4]);
+    const f4 b0 = *reinterpret_cast<const f4*>(&gb[1][kk]), b1 = *reinterpret_cast<const f4*>(&gb[1][kk + 4]);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float* xr = &xn[16 * t + m][kk];
+      const f4 a0 = *reinterpret_cast<const f4*>(xr) * g0 + b0;
+      const f4 a1 = *reinterpret_cast<const f4*>(xr + 4) * g1 + b1;
+      h8 ah, al;
+      split8(a0, a1, ah, al);
+      acc[t][0] = mma3(ah, al, whi[0][i], wlo[0][i], acc[t][0]);
+      acc[t][1] = mma3(ah, al, whi[1][i], wlo[1][i], acc[t][1]);
     }
   }
   float* out = a.hg_part + static_cast<int64_t>(ks) * a.B * kH2;
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int r = rt * kR + 4 * kq + e;
-    if (r < a.B) {
-      out[static_cast<int64_t>(r) * kH2 + 32 * wave + m] = acc0[e];
-      out[static_cast<int64_t>(r) * kH2 + 32 * wave + 16 + m] = acc1[e];
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int r = r0 + 16 * t + 4 * kq + e;
+      if (r < a.B) {
+        out[static_cast<int64_t>(r) * kH2 + 32 * wave + m] = acc[t][0][e] * (1.f / 16.f);
+        out[static_cast<int64_t>(r) * kH2 + 32 * wave + 16 + m] = acc[t][1][e] * (1.f / 16.f);
+      }
     }
-  }
   HBK_MT(3, 3);
 }
 
@@ -588,23 +651,32 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
     }
     if (tid < kH) sWo[tid] = vwo;
   }
-  // HG0 = sum of k1's KS partial slabs + bias; U0 = silu(H) G. Thread ->
-  // 4 (row, j) pairs; the slab loads are issued 4 slabs at a time (rows past B
-  // read row B - 1: their values are finite and every gradient they feed is
-  // multiplied by dz = 0).
+  // HG0 = sum of k1b's KS partial slabs + bias; U0 = silu(H) G. Thread ->
+  // 4 (row, j) pairs; up to 12 slabs' loads are issued together (unrolled,
+  // clamped: slabs past KS are re-reads weighted 0; rows past B read row B - 1,
+  // whose values are finite and whose every gradient is multiplied by dz = 0).
   {
     float h[4] = {0.f, 0.f, 0.f, 0.f}, g[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int s0 = 0; s0 < a.KS; s0 += 4) {
+    for (int s0 = 0; s0 < a.KS; s0 += 12) {
+      float lh[12][4], lg[12][4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 12; ++u) {
         const int sl = min(s0 + u, a.KS - 1);
-        const float on = s0 + u < a.KS ? 1.f : 0.f;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int e = tid + 256 * q, r = min(e >> 6, nrow - 1), j = e & 63;
           const float* src = a.hg_part + (sl * B + r0 + r) * kH2;
-          h[q] += on * src[j];
-          g[q] += on * src[kH + j];
+          lh[u][q] = src[j];
+          lg[u][q] = src[kH + j];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 12; ++u) {
+        const float on = s0 + u < a.KS ? 1.f : 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          h[q] += on * lh[u][q];
+          g[q] += on * lg[u][q];
         }
       }
     }
@@ -910,13 +982,22 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
 }
 
 // ------------------------------------------------------------------ k3 ----
-// dW [M][N] += X^T Y over a chunk of batch rows, from k1/k2's TRANSPOSED
-// activations X^T [M][Bp], Y^T [N][Bp] (rows of b contiguous, pad rows zero):
-// lane (m, kq) of MFMA step (i, s) reads k = b = 16 i + 4 kq + s, so A and B
-// are float4 loads along b. Tile 64 x 32, wave w -> M rows 16 w .. 16 w + 15,
-// both 16-column halves; split-K partials are added with float atomics into
-// the bucket (zeroed by the previous step's k4).
-constexpr int kTM = 64, kTN = 32, kMaxJobs = 2 * kMaxG;
+// dW [M][N] += X^T Y over a split of batch rows, from k1a/k2's TRANSPOSED
+// activations X^T [M][Bp] (a gradient: dHG or dS), Y^T [N][Bp] (an
+// activation: xhat, Xn or U); rows of b contiguous, pad rows zero. Split-f16
+// products on v_mfma_f32_16x16x32_f16 (hi*hi + hi*lo + lo*hi, f32
+// accumulation): lane (m, kq) of step u holds b = 32 u + 8 kq .. + 7, so A and B
+// are two float4 runs along b. Gradients can be arbitrarily small, so X is
+// scaled by a power of two per workgroup (its tile's max |X| into [2^14, 2^15):
+// no f16 overflow, lo parts in f16's normal range) and the sums are scaled
+// back exactly. Tile 128 x 32: wave w owns M rows 32 w .. 32 w + 31 (two MFMA
+// row tiles, X in registers, all loads in flight together) and both 16-column
+// halves; the split's Y^T tile (32 x 288) is loaded once per workgroup, split
+// into f16 hi / lo planes in LDS and shared by the four waves. Split-K partials
+// are added with float atomics into the bucket (zeroed by the previous k4).
+constexpr int kTM = 128, kTN = 32, kMaxJobs = 2 * kMaxG;
+constexpr int kK3Steps = 9, kK3Rows = 32 * kK3Steps;  // batch rows per split (B = 1100: 4 splits)
+constexpr int kYLdH = kK3Rows + 8;                    // LDS row stride (halves) of the Y planes
 struct WJob {
   const float* X;  // [M][Bp]
   const float* Y;  // [N][Bp]
@@ -926,7 +1007,7 @@ struct WJob {
 struct K3Args {
   WJob job[kMaxJobs];
   int start[kMaxJobs + 1];
-  int n_jobs, Kc, KS;
+  int n_jobs, KS;
   int64_t Bp;
   // input-layer job (job 0): post-op with norm_in's affine and W_hg0
   const float* g_in;
@@ -937,8 +1018,11 @@ struct K3Args {
 };
 
 __global__ void __launch_bounds__(256) k3_wgrad_kernel(K3Args a) {
+  __shared__ __attribute__((aligned(16))) _Float16 yh[kTN * kYLdH];
+  __shared__ __attribute__((aligned(16))) _Float16 yl[kTN * kYLdH];
   __shared__ float sS[kTM];
   __shared__ float red[2][4][kTN];
+  __shared__ float smax[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int blk = blockIdx.x;
   int j = 0;
@@ -948,67 +1032,116 @@ __global__ void __launch_bounds__(256) k3_wgrad_kernel(K3Args a) {
   const int split = local % a.KS, tile = local / a.KS;
   const int tm = tile / jb.tn, tn = tile - tm * jb.tn;
   HBK_MT(2, 1);
-  const int rb0 = split * a.Kc, rb1 = static_cast<int>(min(a.Bp, static_cast<int64_t>(rb0 + a.Kc)));
+  const int rb0 = split * kK3Rows;
+  const int Bp = static_cast<int>(a.Bp);
   const int m = lane & 15, kq = lane >> 4;
-  const int mrow = tm * kTM + 16 * wave;  // first M row of this wave
+  const int mrow = tm * kTM + 32 * wave;  // first M row of this wave (two 16-row tiles)
   const int n0 = tn * kTN;
-  const bool mok = mrow + m < jb.M;
-  const bool nok0 = n0 + m < jb.N, nok1 = n0 + 16 + m < jb.N;
-  f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, ssum = acc0;
-  const f4 zero = acc0;
-  const float* X = jb.X + static_cast<int64_t>(mok ? mrow + m : 0) * a.Bp + 4 * kq;
-  const float* Y0 = jb.Y + static_cast<int64_t>(nok0 ? n0 + m : 0) * a.Bp + 4 * kq;
-  const float* Y1 = jb.Y + static_cast<int64_t>(nok1 ? n0 + 16 + m : 0) * a.Bp + 4 * kq;
-  // 8-step register ring: the loads of step i + 8 are issued as step i is consumed
-  const int nit = (rb1 - rb0) / 16;
-  f4 rx[8], ry0[8], ry1[8];
+  // Y^T tile: 32 columns x 288 rows = 72 float4 per column; rows past Bp are
+  // zeroed (their loads read a clamped valid run). Columns past N read a
+  // clamped row: their products only reach outputs that are never stored.
+  constexpr int kYv = kTN * kK3Rows / 4 / 256;  // float4 per thread (9)
+  f4 yv[kYv];
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    if (u < nit) {
-      const int b = rb0 + 16 * u;
-      rx[u] = mok ? *reinterpret_cast<const f4*>(X + b) : zero;
-      ry0[u] = nok0 ? *reinterpret_cast<const f4*>(Y0 + b) : zero;
-      ry1[u] = nok1 ? *reinterpret_cast<const f4*>(Y1 + b) : zero;
+  for (int h = 0; h < kYv; ++h) {
+    const int e = tid + 256 * h, col = e / (kK3Rows / 4), off = 4 * (e % (kK3Rows / 4));
+    const int b = min(rb0 + off, Bp - 4);
+    yv[h] = *reinterpret_cast<const f4*>(jb.Y + static_cast<int64_t>(min(n0 + col, jb.N - 1)) * Bp + b);
+  }
+  // X: rows past M read a clamped row (discarded outputs); this lane's 8 batch
+  // rows past Bp (8-row granularity: Bp is a multiple of 16) read the last 8
+  // rows and are zeroed
+  const float* X0 = jb.X + static_cast<int64_t>(min(mrow + m, jb.M - 1)) * Bp;
+  const float* X1 = jb.X + static_cast<int64_t>(min(mrow + 16 + m, jb.M - 1)) * Bp;
+  f4 rx[2][kK3Steps][2];
+#pragma unroll
+  for (int u = 0; u < kK3Steps; ++u) {
+    const int b = min(rb0 + 32 * u + 8 * kq, Bp - 8);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      rx[0][u][h] = *reinterpret_cast<const f4*>(X0 + b + 4 * h);
+      rx[1][u][h] = *reinterpret_cast<const f4*>(X1 + b + 4 * h);
     }
   }
-  for (int i0 = 0; i0 < nit; i0 += 8) {
+  const f4 z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i = i0 + u;
-      if (i < nit) {
-        const f4 xa = rx[u], ya = ry0[u], yb = ry1[u];
-        if (i + 8 < nit) {
-          const int b = rb0 + 16 * (i + 8);
-          rx[u] = mok ? *reinterpret_cast<const f4*>(X + b) : zero;
-          ry0[u] = nok0 ? *reinterpret_cast<const f4*>(Y0 + b) : zero;
-          ry1[u] = nok1 ? *reinterpret_cast<const f4*>(Y1 + b) : zero;
-        }
+  for (int h = 0; h < kYv; ++h) {
+    const int e = tid + 256 * h, col = e / (kK3Rows / 4), off = 4 * (e % (kK3Rows / 4));
+    const f4 v = rb0 + off < Bp ? yv[h] : z;
+    uint32_t h0, l0, h1, l1;
+    split_pair(v[0], v[1], h0, l0);
+    split_pair(v[2], v[3], h1, l1);
+    *reinterpret_cast<uint2*>(&yh[col * kYLdH + off]) = uint2{h0, h1};
+    *reinterpret_cast<uint2*>(&yl[col * kYLdH + off]) = uint2{l0, l1};
+  }
+  // zero the dead batch rows of X, row sums (input job) and the tile's max |X|
+  f4 ssum[2] = {z, z};
+  float mx = 0.f;
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          acc0 = mma(xa[s], ya[s], acc0);
-          acc1 = mma(xa[s], yb[s], acc1);
-        }
-        ssum += xa;
+  for (int u = 0; u < kK3Steps; ++u) {
+    const bool live = rb0 + 32 * u + 8 * kq < Bp;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        rx[t][u][h] = live ? rx[t][u][h] : z;
+        ssum[t] += rx[t][u][h];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) mx = fmaxf(mx, fabsf(rx[t][u][h][e]));
       }
+  }
+  mx = wmax(mx);
+  if (lane == 0) smax[wave] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
+  // scale = 2^(14 - floor(log2 max)): max |X| * scale in [2^14, 2^15)
+  const int ex = mx > 0.f ? min(14 - ilogbf(mx), 126) : 0;
+  const float scale = ldexpf(1.f, ex), unscale = ldexpf(1.f, -ex);
+  f4 acc[2][2] = {{z, z}, {z, z}};
+  const _Float16* y0h = &yh[m * kYLdH + 8 * kq];
+  const _Float16* y0l = &yl[m * kYLdH + 8 * kq];
+  const _Float16* y1h = &yh[(16 + m) * kYLdH + 8 * kq];
+  const _Float16* y1l = &yl[(16 + m) * kYLdH + 8 * kq];
+#pragma unroll
+  for (int u = 0; u < kK3Steps; ++u) {
+    const h8 bh0 = *reinterpret_cast<const h8*>(y0h + 32 * u), bl0 = *reinterpret_cast<const h8*>(y0l + 32 * u);
+    const h8 bh1 = *reinterpret_cast<const h8*>(y1h + 32 * u), bl1 = *reinterpret_cast<const h8*>(y1l + 32 * u);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      h8 ah, al;
+      split8(rx[t][u][0] * scale, rx[t][u][1] * scale, ah, al);
+      acc[t][0] = mma3(ah, al, bh0, bl0, acc[t][0]);
+      acc[t][1] = mma3(ah, al, bh1, bl1, acc[t][1]);
     }
   }
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    acc[t][0] *= unscale;
+    acc[t][1] *= unscale;
+  }
+  const bool nok0 = n0 + m < jb.N, nok1 = n0 + 16 + m < jb.N;
   HBK_MT(2, 2);
   if (j != 0) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int row = mrow + 4 * kq + e;
-      if (row < jb.M) {
-        if (nok0) atomicAdd(jb.C + static_cast<int64_t>(row) * jb.ldc + n0 + m, acc0[e]);
-        if (nok1) atomicAdd(jb.C + static_cast<int64_t>(row) * jb.ldc + n0 + 16 + m, acc1[e]);
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = mrow + 16 * t + 4 * kq + e;
+        if (row < jb.M) {
+          if (nok0) atomicAdd(jb.C + static_cast<int64_t>(row) * jb.ldc + n0 + m, acc[t][0][e]);
+          if (nok1) atomicAdd(jb.C + static_cast<int64_t>(row) * jb.ldc + n0 + 16 + m, acc[t][1][e]);
+        }
       }
-    }
     return;
   }
-  // input layer: s_j = sum over the chunk's rows of dHG0[b][j] (lanes m + 16 q hold parts)
-  float sj_part = (ssum[0] + ssum[1]) + (ssum[2] + ssum[3]);
-  sj_part += __shfl_xor(sj_part, 16, 64);
-  sj_part += __shfl_xor(sj_part, 32, 64);
-  if (kq == 0) sS[16 * wave + m] = sj_part;
+  // input layer: s_j = sum over the split's rows of dHG0[b][j] (lanes m + 16 q hold parts)
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    float sj_part = (ssum[t][0] + ssum[t][1]) + (ssum[t][2] + ssum[t][3]);
+    sj_part += __shfl_xor(sj_part, 16, 64);
+    sj_part += __shfl_xor(sj_part, 32, 64);
+    if (kq == 0) sS[32 * wave + 16 * t + m] = sj_part;
+  }
   __syncthreads();
   float dg0 = 0.f, dg1 = 0.f, dbt0 = 0.f, dbt1 = 0.f;
   const int c0 = n0 + m, c1 = n0 + 16 + m;
@@ -1017,29 +1150,33 @@ __global__ void __launch_bounds__(256) k3_wgrad_kernel(K3Args a) {
   const int c0c = min(c0, jb.N - 1), c1c = min(c1, jb.N - 1);
   const float g0 = a.g_in[c0c], g1 = a.g_in[c1c];
   const float be0 = a.b_in[c0c], be1 = a.b_in[c1c];
-  float w0[4], w1[4];
+  float w0[2][4], w1[2][4];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const float* wr = a.W0 + static_cast<int64_t>(min(mrow + 4 * kq + e, jb.M - 1)) * jb.ldc;
-    w0[e] = wr[c0c];
-    w1[e] = wr[c1c];
-  }
+  for (int t = 0; t < 2; ++t)
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int row = mrow + 4 * kq + e;  // j
-    if (row >= jb.M) continue;
-    const float sj = sS[16 * wave + 4 * kq + e];
-    if (nok0) {
-      atomicAdd(jb.C + static_cast<int64_t>(row) * jb.ldc + c0, g0 * acc0[e] + be0 * sj);
-      dg0 += w0[e] * acc0[e];
-      dbt0 += w0[e] * sj;
+    for (int e = 0; e < 4; ++e) {
+      const float* wr = a.W0 + static_cast<int64_t>(min(mrow + 16 * t + 4 * kq + e, jb.M - 1)) * jb.ldc;
+      w0[t][e] = wr[c0c];
+      w1[t][e] = wr[c1c];
     }
-    if (nok1) {
-      atomicAdd(jb.C + static_cast<int64_t>(row) * jb.ldc + c1, g1 * acc1[e] + be1 * sj);
-      dg1 += w1[e] * acc1[e];
-      dbt1 += w1[e] * sj;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = mrow + 16 * t + 4 * kq + e;  // j
+      if (row >= jb.M) continue;
+      const float sj = sS[32 * wave + 16 * t + 4 * kq + e];
+      if (nok0) {
+        atomicAdd(jb.C + static_cast<int64_t>(row) * jb.ldc + c0, g0 * acc[t][0][e] + be0 * sj);
+        dg0 += w0[t][e] * acc[t][0][e];
+        dbt0 += w0[t][e] * sj;
+      }
+      if (nok1) {
+        atomicAdd(jb.C + static_cast<int64_t>(row) * jb.ldc + c1, g1 * acc[t][1][e] + be1 * sj);
+        dg1 += w1[t][e] * acc[t][1][e];
+        dbt1 += w1[t][e] * sj;
+      }
     }
-  }
   // reduce over kq (lanes m + 16 q) then over waves
 #pragma unroll
   for (int o = 16; o < 64; o <<= 1) {
@@ -1141,15 +1278,17 @@ __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
   f4* V4 = reinterpret_cast<f4*>(a.v);
   const f4 z4 = {0.f, 0.f, 0.f, 0.f};
   for (int64_t i = blockIdx.x * int64_t(256) + threadIdx.x; i < n4; i += int64_t(gridDim.x) * 256) {
-    const f4 g = G4[i];
+    // all four loads unconditional (issued together, no wait behind the gate
+    // decision, which itself waits on the statistics)
+    const f4 g = G4[i], m0 = M4[i], v0 = V4[i];
+    f4 p = P4[i];
     G4[i] = z4;
     if (on) {
       const f4 gi = g * scale;
-      const f4 mi = a.b1 * M4[i] + (1.f - a.b1) * gi;
-      const f4 vi = a.b2 * V4[i] + (1.f - a.b2) * gi * gi;
+      const f4 mi = a.b1 * m0 + (1.f - a.b1) * gi;
+      const f4 vi = a.b2 * v0 + (1.f - a.b2) * gi * gi;
       M4[i] = mi;
       V4[i] = vi;
-      f4 p = P4[i];
 #pragma unroll
       for (int e = 0; e < 4; ++e) p[e] -= step_size * mi[e] / (sqrtf(vi[e]) / bc2s + a.eps);
       P4[i] = p;
@@ -1173,12 +1312,11 @@ __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
 struct FusedWs {
   int64_t hg_part, xhat[2], U, Xn, dS, dHG, total;  // float offsets
 };
+int k1_blocks(int B) { return ((B + kRB - 1) / kRB + 7) / 8 * 8; }  // row blocks, XCD-aware
 int k1_splits(int B) {
-  const int rt = (B + kR - 1) / kR;
-  const int rt8 = (rt + 7) / 8 * 8;
   static const int ks_opts[] = {4, 6, 8, 12, 16, 24};
   for (int ks : ks_opts)
-    if (rt8 * ks >= 480) return ks;
+    if (k1_blocks(B) * ks >= 256) return ks;
   return 24;
 }
 FusedWs fused_layout(int64_t B, int NG) {
@@ -1234,7 +1372,6 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
   const int KS = k1_splits(B);
   const int64_t Bp = (B + kR - 1) / kR * kR;
   const int rt = (B + kR - 1) / kR;
-  const int rt8 = (rt + 7) / 8 * 8;  // XCD-aware 1-D grid (see k1b_kernel)
   K1aArgs ka;
   ka.pool32 = pool32;
   ka.pool16 = static_cast<const _Float16*>(pool16);
@@ -1270,7 +1407,7 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
   kb.hg_part = ws + w.hg_part;
   kb.stats = train ? bucket + p.n_params : nullptr;
   {
-    auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(rt8 * KS), dim3(256), 0, s, kb); };
+    auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(k1_blocks(B) * KS), dim3(256), 0, s, kb); };
     switch (KS) {
       case 4: launch(k1b_kernel<4>); break;
       case 6: launch(k1b_kernel<6>); break;
@@ -1326,8 +1463,7 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
   // k3: job 0 = input layer, then dW_hg of GMLPs 1.., then dW_o of every GMLP
   K3Args k3;
   int nj = 0, blocks = 0;
-  const int KS3 = std::max(1, static_cast<int>((Bp + 287) / 288));
-  const int Kc = static_cast<int>((Bp / kR + KS3 - 1) / KS3) * kR;
+  const int KS3 = static_cast<int>((Bp + kK3Rows - 1) / kK3Rows);
   auto add = [&](const float* X, const float* Y, float* C, int ldc, int M, int N) {
     WJob& j = k3.job[nj];
     j.X = X;
@@ -1349,7 +1485,6 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
     add(ws + w.dS + int64_t(k) * kL * Bp, ws + w.U + int64_t(k) * kH * Bp, G + p.g[k].w_o, kH, p.g[k].out, kH);
   k3.start[nj] = blocks;
   k3.n_jobs = nj;
-  k3.Kc = Kc;
   k3.KS = KS3;
   k3.Bp = Bp;
   k3.g_in = params + p.ln_in.g;

@@ -195,3 +195,24 @@ def test_embed_split_precision_margin():
     ref = oemb.run_graph(g, wins)
     rel = np.abs(out - ref).max() / np.abs(ref).max()
     assert rel < 1e-5, rel
+
+
+@pytest.mark.gpu
+def test_featurize_across_the_16384_clip_chunk():
+    """hbk_embed_clips works through the batch in 16,384-clip workspace chunks
+    (hbk_embed.hip kChunkClips): 16,390 clips cross one boundary. The clips on
+    both sides of it (and the first / last) against the oracle mel + graph."""
+    from heybuddy.embedding_graph import se20_graph
+    from heybuddy.embeddings import SpeechEmbeddings
+    from heybuddy.synthetic import synthetic_clips
+    n = 16390
+    clips = synthetic_clips(n, seed=21, device="cuda")
+    se = SpeechEmbeddings(device_id=0)
+    out, frames = se.featurize(clips, return_frames=True)
+    pick = [0, 16381, 16382, 16383, 16384, 16385, 16386, n - 1]
+    sub = clips[pick].cpu().numpy()
+    mel_ref, _, _ = omel.mel_frames(sub, frames.shape[1])
+    np.testing.assert_allclose(frames[pick].cpu().numpy(), mel_ref, rtol=1e-4, atol=1e-4)
+    ref = _oracle_clip_embeddings(se20_graph(), mel_ref)
+    ok, worst = _close(out[pick].cpu().numpy(), ref)
+    assert out.shape == (n, 16, 96) and ok, f"max |diff| {worst}"
