@@ -1000,6 +1000,89 @@ __global__ void __launch_bounds__(256) place_kernel(const float* __restrict__ sr
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Seven-band parametric EQ: audiomentations SevenBandParametricEQ, the
+// reference's per-clip transform ahead of tanh (dataset/augmented.py:79-84):
+// seven RBJ biquads in series (low shelf, five peaks, high shelf), each the
+// direct form II transposed recursion of scipy sosfilt in float64 with its
+// output rounded to float32 before the next stage (audiomentations casts each
+// filter's output). One lane per clip: the recursion is sequential in time,
+// and clips are the parallel axis. A wave owns 64 clips; 64-sample tiles are
+// loaded coalesced (16 lanes per clip row, float4), transposed through LDS to
+// [sample][clip] (conflict-free column reads), filtered in place and stored
+// back the same way; the next tile's loads are issued before the current one
+// is filtered. A clip whose first b0 is NaN is copied.
+constexpr int kEqTile = 64;
+struct EqArgs {
+  const float* x;
+  int64_t x_stride;
+  const double* coef;  // [n][7][5]: b0, b1, b2, a1, a2 (a0 = 1)
+  float* out;
+  int64_t out_stride;
+  int64_t n;
+};
+
+__global__ void __launch_bounds__(64) eq_kernel(EqArgs a) {
+  __shared__ float tile[kEqTile][kEqTile + 1];
+  const int lane = threadIdx.x;
+  const int64_t c0 = static_cast<int64_t>(blockIdx.x) * 64;
+  const int64_t cl = min(c0 + lane, a.n - 1);
+  double co[35];
+#pragma unroll
+  for (int i = 0; i < 35; ++i) co[i] = a.coef[cl * 35 + i];
+  const bool skip = c0 + lane >= a.n || co[0] != co[0];
+  double s1[7], s2[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) s1[k] = s2[k] = 0.0;
+  // cooperative mapping: item i of this lane -> clip row (lane + 64 i) / 16, samples 4 ((lane + 64 i) % 16) ..
+  const float* rows[16];
+  float4 pre[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int e = lane + 64 * i;
+    rows[i] = a.x + min(c0 + (e >> 4), a.n - 1) * a.x_stride + 4 * (e & 15);
+    pre[i] = *reinterpret_cast<const float4*>(rows[i]);
+  }
+  for (int t0 = 0; t0 < kT; t0 += kEqTile) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int e = lane + 64 * i, r = e >> 4, q = 4 * (e & 15);
+      tile[q][r] = pre[i].x;
+      tile[q + 1][r] = pre[i].y;
+      tile[q + 2][r] = pre[i].z;
+      tile[q + 3][r] = pre[i].w;
+    }
+    __syncthreads();
+    const int tn = min(t0 + kEqTile, kT - kEqTile);  // next tile (the last iteration re-reads its own)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) pre[i] = *reinterpret_cast<const float4*>(rows[i] + tn);
+    if (!skip) {
+      for (int s = 0; s < kEqTile; ++s) {
+        float v = tile[s][lane];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+          const double vd = v;
+          const double y = fma(co[5 * k], vd, s1[k]);
+          s1[k] = fma(co[5 * k + 1], vd, fma(-co[5 * k + 3], y, s2[k]));
+          s2[k] = fma(co[5 * k + 2], vd, -co[5 * k + 4] * y);
+          v = static_cast<float>(y);
+        }
+        tile[s][lane] = v;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int e = lane + 64 * i, r = e >> 4, q = 4 * (e & 15);
+      if (c0 + r < a.n)
+        *reinterpret_cast<float4*>(a.out + (c0 + r) * a.out_stride + t0 + q) =
+            float4{tile[q][r], tile[q + 1][r], tile[q + 2][r], tile[q + 3][r]};
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
 }  // namespace hbk
 
@@ -1213,6 +1296,27 @@ int hbk_tanh_distortion(const float* x, int64_t n_clips, int64_t x_stride, const
   const int64_t blocks = std::min<int64_t>(n_clips, persistent_blocks(2));
   hipLaunchKernelGGL(tanh_distortion_kernel, dim3(unsigned(blocks)), dim3(kThreads), 0, as_stream(stream), a);
   HBK_LAUNCH_CHECK("tanh_distortion_kernel");
+  return HBK_OK;
+}
+
+int hbk_seven_band_eq(const float* x, int64_t n_clips, int64_t x_stride, const double* coef, float* out,
+                      int64_t out_stride, void* stream) {
+  using namespace hbk;
+  if (n_clips < 0) return arg_error("negative n_clips");
+  if (n_clips == 0) return HBK_OK;
+  if (!x || !out || !coef) return arg_error("NULL pointer");
+  if (x_stride < kT || out_stride < kT) return arg_error("stride < 23040");
+  if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out)) % 16 || x_stride % 4 || out_stride % 4)
+    return arg_error("x / out rows must be 16-B aligned");
+  EqArgs a;
+  a.x = x;
+  a.x_stride = x_stride;
+  a.coef = coef;
+  a.out = out;
+  a.out_stride = out_stride;
+  a.n = n_clips;
+  hipLaunchKernelGGL(eq_kernel, dim3(unsigned((n_clips + 63) / 64)), dim3(64), 0, as_stream(stream), a);
+  HBK_LAUNCH_CHECK("eq_kernel");
   return HBK_OK;
 }
 

@@ -18,14 +18,19 @@ Semantics kept from the reference:
   (0.25) one snr ~ U[10, 30] dB and one f_decay ~ U[-1, 2] (per_batch draws
   one parameter set, as for the gain); white noise per clip from the kernel's
   counter-based normal stream (seeded from numpy's global RNG);
+* seven-band EQ: audiomentations SevenBandParametricEQ, per CLIP with
+  probability seven_band_prob (0.25), gains ~ U[-6, 6] dB (:79-84): first in the
+  per-clip Compose; the per-clip filter parameters (center mel-uniform in each
+  band's range, gain, Q ~ U[0.5, 1.33]) are drawn here and turned into RBJ
+  biquad coefficients (eq_coefficients), the cascade runs on the device;
 * tanh distortion: audiomentations TanhDistortion, per CLIP with probability
-  tanh_distortion_prob (0.25), amount ~ U[1e-4, 0.1] (:79-90), first: the
-  reference applies it on the host before the batch chain (:325-328).
+  tanh_distortion_prob (0.25), amount ~ U[1e-4, 0.1] (:79-90), after the EQ: the
+  reference applies both on the host before the batch chain (:325-328).
 Differences (by design): the IR spectra are computed once for the whole bank
 instead of once per batch, every batch of a call is one kernel launch, and
 clips never leave the device (the reference copies each clip back to host,
-:419). The other augmentations (7-band EQ, pitch shift, band-stop) are not on this
-path yet.
+:419). Pitch shift and band-stop (the first two transforms of the batch chain) are
+not on this path yet.
 """
 from __future__ import annotations
 
@@ -44,13 +49,54 @@ from heybuddy.constants import (DEFAULT_AUGMENT_BACKGROUND_NOISE_MAX_SNR_DB,
                                 DEFAULT_AUGMENT_TANH_MIN_DISTORTION,
                                 DEFAULT_AUGMENT_BACKGROUND_NOISE_PROB, DEFAULT_AUGMENT_GAIN_MAX_DB,
                                 DEFAULT_AUGMENT_GAIN_MIN_DB, DEFAULT_AUGMENT_GAIN_PROB,
-                                DEFAULT_AUGMENT_REVERB_PROB)
-from heybuddy.kernels import ReverbPlan, place_clips, tanh_distortion
+                                DEFAULT_AUGMENT_REVERB_PROB, DEFAULT_AUGMENT_SEVEN_BAND_GAIN_DB,
+                                DEFAULT_AUGMENT_SEVEN_BAND_PROB)
+from heybuddy.kernels import ReverbPlan, place_clips, seven_band_eq, tanh_distortion
 
-__all__ = ["AugmentedAudioGenerator", "BatchAugmenter", "target_length_offset", "target_length_offsets",
-           "to_target_length"]
+__all__ = ["AugmentedAudioGenerator", "BatchAugmenter", "eq_coefficients", "eq_parameters",
+           "target_length_offset", "target_length_offsets", "to_target_length"]
 
 T = 23040
+
+# SevenBandParametricEQ: low shelf, five peaking filters, high shelf; center
+# frequency ranges (Hz) and the Q range of audiomentations' documentation
+EQ_BANDS = ((42.0, 95.0), (91.0, 204.0), (196.0, 441.0), (421.0, 948.0), (909.0, 2045.0),
+            (1957.0, 4404.0), (4216.0, 9486.0))
+EQ_Q_RANGE = (0.5, 1.33)
+
+
+def eq_parameters(n: int, gain_db: float, sample_rate: int = 16000) -> np.ndarray:
+    """(center Hz, gain dB, Q) [n, 7, 3] from numpy's global RNG: centers
+    uniform on the mel scale within each band (the high shelf clamped to 0.95
+    Nyquist), gains ~ U[-gain_db, gain_db], Q ~ U[0.5, 1.33]."""
+    mel = lambda f: 2595.0 * np.log10(1.0 + np.asarray(f) / 700.0)  # noqa: E731
+    lo, hi = mel([b[0] for b in EQ_BANDS]), mel([b[1] for b in EQ_BANDS])
+    f0 = 700.0 * (10.0 ** (np.random.uniform(lo, hi, (n, 7)) / 2595.0) - 1.0)
+    f0[:, 6] = np.minimum(f0[:, 6], (sample_rate // 2) * 0.95)
+    g = np.random.uniform(-gain_db, gain_db, (n, 7))
+    q = np.random.uniform(*EQ_Q_RANGE, (n, 7))
+    return np.stack([f0, g, q], axis=-1)
+
+
+def eq_coefficients(params: np.ndarray, sample_rate: int = 16000) -> np.ndarray:
+    """RBJ audio-EQ-cookbook biquads (b0, b1, b2, a1, a2) / a0, float64 [..., 7, 5]:
+    filter 0 low shelf, 1-5 peaking, 6 high shelf; A = 10^(gain / 40),
+    w0 = 2 pi f0 / sr, alpha = sin(w0) / (2 Q)."""
+    p = np.asarray(params, dtype=np.float64)
+    A = 10.0 ** (p[..., 1] / 40.0)
+    w0 = 2.0 * np.pi * p[..., 0] / sample_rate
+    c, al = np.cos(w0), np.sin(w0) / (2.0 * p[..., 2])
+    r = 2.0 * np.sqrt(A) * al
+    Ap, Am = A + 1.0, A - 1.0
+    peak = (1 + al * A, -2 * c, 1 - al * A, 1 + al / A, -2 * c, 1 - al / A)
+    low = (A * (Ap - Am * c + r), 2 * A * (Am - Ap * c), A * (Ap - Am * c - r),
+           Ap + Am * c + r, -2 * (Am + Ap * c), Ap + Am * c - r)
+    high = (A * (Ap + Am * c + r), -2 * A * (Am + Ap * c), A * (Ap + Am * c - r),
+            Ap - Am * c + r, 2 * (Am - Ap * c), Ap - Am * c - r)
+    kind = np.arange(7)
+    b0, b1, b2, a0, a1, a2 = (np.where(kind == 0, lo_, np.where(kind == 6, hi_, pk_))
+                              for lo_, hi_, pk_ in zip(low, high, peak))
+    return np.stack([b0 / a0, b1 / a0, b2 / a0, a1 / a0, a2 / a0], axis=-1)
 
 
 class BatchAugmenter:
@@ -72,6 +118,8 @@ class BatchAugmenter:
                  tanh_distortion_prob: float = DEFAULT_AUGMENT_TANH_DISTORTION_PROB,
                  tanh_min_distortion: float = DEFAULT_AUGMENT_TANH_MIN_DISTORTION,
                  tanh_max_distortion: float = DEFAULT_AUGMENT_TANH_MAX_DISTORTION,
+                 seven_band_prob: float = DEFAULT_AUGMENT_SEVEN_BAND_PROB,
+                 seven_band_gain_db: float = DEFAULT_AUGMENT_SEVEN_BAND_GAIN_DB,
                  sample_rate: int = 16000) -> None:
         self.plan = ReverbPlan(device)
         self.device = self.plan.device
@@ -93,6 +141,8 @@ class BatchAugmenter:
         self.sample_rate = int(sample_rate)
         self.p_tanh = float(tanh_distortion_prob)
         self.tanh_range = (float(tanh_min_distortion), float(tanh_max_distortion))
+        self.p_eq = float(seven_band_prob)
+        self.eq_gain_db = float(seven_band_gain_db)
         self.ring = None
         self.lengths: List[int] = []
         self.starts: List[int] = []
@@ -163,6 +213,12 @@ class BatchAugmenter:
             per_clip = np.where(r_on, ir, -1).astype(np.int32)[batch]
             spec_idx[:] = per_clip
         self._colored = (colored_snr, colored_fd)
+        # seven-band EQ (audiomentations, per clip): NaN b0 = off
+        e_on = np.random.rand(n) < getattr(self, "p_eq", 0.0)
+        sr = getattr(self, "sample_rate", 16000)
+        coef = eq_coefficients(eq_parameters(n, getattr(self, "eq_gain_db", 0.0), sr), sr)
+        coef[~e_on, 0, 0] = np.nan
+        self._eq = coef
         # tanh distortion (audiomentations, per clip): NaN amount = off
         t_on = np.random.rand(n) < getattr(self, "p_tanh", 0.0)
         t_amt = np.random.uniform(*getattr(self, "tanh_range", (0.0, 0.0)), n)
@@ -180,6 +236,9 @@ class BatchAugmenter:
         gain = None
         if self.p_gain > 0:  # torch_audiomentations convert_decibels_to_amplitude_ratio
             gain = torch.pow(10.0, torch.from_numpy(gain_db) / 20.0)
+        if not np.isnan(self._eq[:, 0, 0]).all():  # per-clip Compose: EQ, then tanh (augmented.py:79-90)
+            x = seven_band_eq(x, torch.from_numpy(self._eq), out=out)
+            out = x
         if not np.isnan(self._tanh).all():  # per-clip Compose, before the batch chain (augmented.py:325-328)
             x = tanh_distortion(x, torch.from_numpy(self._tanh), out=out)
             out = x
@@ -264,17 +323,19 @@ def _as_float_array(a: Any) -> np.ndarray:
 class AugmentedAudioGenerator:
     """Drop-in for heybuddy.dataset.augmented.AugmentedAudioGenerator
     (augmented.py:16-427). Same constructor and methods; every batch runs on
-    the MI355X: clip placement (hbk_place_clips), tanh distortion, colored
-    noise, gain, background noise and reverb (hbk_*), in the reference's order
-    (:297-394). The datasets are any iterable of audio rows (see _audio_arrays)
-    at ``sample_rate``; the noise and IR sets are loaded into HBM once.
-    Not on this path yet: 7-band EQ, pitch shift and band-stop
-    (their probabilities are accepted and must be 0, or a warning is logged)."""
+    the MI355X: clip placement (hbk_place_clips), seven-band EQ, tanh
+    distortion, colored noise, gain, background noise and reverb (hbk_*), in
+    the reference's order (:297-394). The datasets are any iterable of audio
+    rows (see _audio_arrays); clips at another rate are resampled (torchaudio's
+    band-limited resampler, restated). The noise and IR sets are loaded into
+    HBM once. Not on this path yet: pitch shift and band-stop
+    (their probabilities are accepted; a warning is logged when > 0)."""
 
     def __init__(self, source_dataset: Any, device_id: Optional[int] = None,
                  augmentation_dataset: Any = None, impulse_response_dataset: Any = None,
                  target_length: float = 1.44, sample_rate: int = 16000, batch_size: int = 128,
-                 seven_band_aug_prob: float = 0.25, seven_band_aug_gain_db: float = 6.0,
+                 seven_band_aug_prob: float = DEFAULT_AUGMENT_SEVEN_BAND_PROB,
+                 seven_band_aug_gain_db: float = DEFAULT_AUGMENT_SEVEN_BAND_GAIN_DB,
                  tanh_distortion_prob: float = DEFAULT_AUGMENT_TANH_DISTORTION_PROB,
                  tanh_min_distortion: float = DEFAULT_AUGMENT_TANH_MIN_DISTORTION,
                  tanh_max_distortion: float = DEFAULT_AUGMENT_TANH_MAX_DISTORTION,
@@ -295,8 +356,7 @@ class AugmentedAudioGenerator:
             raise ValueError("Background noise is enabled but no augmentation dataset is provided")
         if reverb_prob > 0 and not impulse_response_dataset:
             raise ValueError("Reverb is enabled but no impulse response dataset is provided")
-        for name, p in (("seven_band_aug_prob", seven_band_aug_prob), ("pitch_shift_prob", pitch_shift_prob),
-                        ("band_stop_prob", band_stop_prob)):
+        for name, p in (("pitch_shift_prob", pitch_shift_prob), ("band_stop_prob", band_stop_prob)):
             if p > 0:
                 logger.warning(f"{name}={p}: this augmentation is not on the MI355X path yet; skipped")
         self.device_id = device_id
@@ -315,12 +375,10 @@ class AugmentedAudioGenerator:
         def bank(ds):
             if not ds:
                 return None
+            from heybuddy.util import resample
             rows = _audio_arrays(ds)
-            for r in rows:
-                if r["sampling_rate"] != self.sample_rate:
-                    raise NotImplementedError("resampling is outside the MI355X path: give "
-                                              f"{self.sample_rate} Hz audio")
-            return [torch.from_numpy(_as_float_array(r["array"]).reshape(-1)) for r in rows]
+            return [resample(torch.from_numpy(_as_float_array(r["array"]).reshape(-1)), int(r["sampling_rate"]),
+                             self.sample_rate) for r in rows]
 
         self.augmenter = BatchAugmenter(
             bank(augmentation_dataset), bank(impulse_response_dataset), device=dev,
@@ -331,7 +389,8 @@ class AugmentedAudioGenerator:
             colored_noise_min_snr_db=colored_noise_min_snr_db, colored_noise_max_snr_db=colored_noise_max_snr_db,
             colored_noise_min_f_decay=colored_noise_min_f_decay, colored_noise_max_f_decay=colored_noise_max_f_decay,
             tanh_distortion_prob=tanh_distortion_prob, tanh_min_distortion=tanh_min_distortion,
-            tanh_max_distortion=tanh_max_distortion, sample_rate=self.sample_rate)
+            tanh_max_distortion=tanh_max_distortion, seven_band_prob=seven_band_aug_prob,
+            seven_band_gain_db=seven_band_aug_gain_db, sample_rate=self.sample_rate)
         self.device = self.augmenter.device
         self._source: Optional[List[Dict[str, Any]]] = None
         self._source_pos = 0
@@ -366,15 +425,20 @@ class AugmentedAudioGenerator:
     def place_batch(self, batch: Sequence[Any]) -> torch.Tensor:
         """The per-clip placement of execute_augment_batch (:314-328) for a
         batch of audio rows: one device launch; the leading-silence draws come
-        from numpy's global RNG in clip order, as to_target_length draws them."""
+        from numpy's global RNG in clip order, as to_target_length draws them.
+        Clips at another rate are resampled first (util.resample; the reference
+        resamples them in a second pass, :330-360, so in a mixed-rate batch its
+        draws come in a different order)."""
+        from heybuddy.util import resample
         T = self.target_num_samples
         arrays = []
         for audio in batch:
             a = audio["array"] if isinstance(audio, dict) else audio
             sr = audio.get("sampling_rate", self.sample_rate) if isinstance(audio, dict) else self.sample_rate
+            a = _as_float_array(self.to_audio_array(a)).reshape(-1)
             if sr != self.sample_rate:
-                raise NotImplementedError("resampling is outside the MI355X path")
-            arrays.append(_as_float_array(self.to_audio_array(a)).reshape(-1))
+                a = resample(torch.from_numpy(a), int(sr), self.sample_rate).numpy()
+            arrays.append(a)
         lens = np.array([a.shape[0] for a in arrays], dtype=np.int32)
         pre = target_length_offsets(lens, T)
         width = max(int(lens.max()), 1)

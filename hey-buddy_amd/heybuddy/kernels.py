@@ -588,6 +588,32 @@ def tanh_distortion(x: torch.Tensor, amount: torch.Tensor, out: torch.Tensor | N
     return out
 
 
+def seven_band_eq(x: torch.Tensor, coef: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """audiomentations SevenBandParametricEQ per clip on x [n, >= 23040] -> out
+    [n, 23040] (hbk_seven_band_eq): coef [n, 7, 5] float64 (b0, b1, b2, a1, a2
+    of the low shelf, five peaks and high shelf, normalised by a0); a NaN
+    coef[i, 0, 0] leaves clip i unchanged."""
+    T = ReverbPlan.T
+    dev = _native.require_device(x.device)
+    n = x.shape[0]
+    if x.dim() != 2 or x.shape[1] < T or x.stride(1) != 1 or x.dtype != torch.float32:
+        raise ValueError(f"x must be [n, >= {T}] f32 rows on the device")
+    if x.stride(0) % 4 or x.data_ptr() % 16:
+        raise ValueError("x rows must be 16-B aligned")
+    coef = coef.to(dtype=torch.float64).reshape(n, 7, 5).contiguous()
+    coef = coef.pin_memory().to(dev, non_blocking=True) if coef.device.type == "cpu" else coef.to(dev)
+    if out is None:
+        out = torch.empty((n, T), dtype=torch.float32, device=dev)
+    torch.ops.hbk.seven_band_eq_(x, coef, out)
+    return out
+
+
+@torch.library.custom_op("hbk::seven_band_eq_", mutates_args=("out",))
+def _seven_band_eq_op(x: torch.Tensor, coef: torch.Tensor, out: torch.Tensor) -> None:
+    check(lib().hbk_seven_band_eq(ptr(x), x.shape[0], x.stride(0), ptr(coef), ptr(out), out.stride(0),
+                                  stream_ptr(x.device)), "hbk_seven_band_eq")
+
+
 @torch.library.custom_op("hbk::tanh_distortion_", mutates_args=("out",))
 def _tanh_distortion_op(x: torch.Tensor, amount: torch.Tensor, out: torch.Tensor) -> None:
     check(lib().hbk_tanh_distortion(ptr(x), x.shape[0], x.stride(0), ptr(amount), ptr(out), out.stride(0),

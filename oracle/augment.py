@@ -35,10 +35,22 @@ their published algorithms at the versions environment.yml pins
   augmented.py:79-90, constants.py:122-124), in the per-clip Compose before H2D:
       th = np.percentile(|x|, 100 - 99 amount);  y = tanh(0.5 / (th + 1e-6) x)
       if rms(x) > 1e-9: y *= rms(x) / rms(y)
+* audiomentations.SevenBandParametricEQ (p 0.25 per clip, gains +-6 dB;
+  augmented.py:79-84, constants.py:120-121), first in the per-clip Compose:
+  a low shelf, five peaking filters and a high shelf (RBJ audio-EQ-cookbook
+  biquads, each applied with scipy sosfilt = direct form II transposed in
+  float64, its output cast back to float32 before the next filter). Per filter
+  k: center frequency mel-uniform in the band's range (low shelf 42-95 Hz,
+  peaks 91-204, 196-441, 421-948, 909-2045, 1957-4404 Hz, high shelf
+  4216-9486 Hz, clamped to 0.95 Nyquist), gain ~ U[-g, g] dB, Q ~ U[0.5, 1.33];
+      A = 10^(gain/40), w0 = 2 pi f0 / sr, alpha = sin(w0) / (2 Q)
+  (the band ranges, Q range and draw distributions are restated from the
+  package's documentation: PARITY UNPINNED, no fixture exists).
 """
 from __future__ import annotations
 
 import numpy as np
+from scipy.signal import sosfilt
 
 
 def add_noise(x: np.ndarray, noise: np.ndarray, snr_db: np.ndarray, dtype=np.float64) -> np.ndarray:
@@ -144,3 +156,76 @@ def augment_batch(x, noise=None, snr_db=None, ir=None, dtype=np.float64, gain=No
     if ir is not None:
         y = reverberate(y, ir, dtype)
     return y
+
+
+# --------------------------------------------------------------------------
+# SevenBandParametricEQ
+EQ_BANDS = ((42.0, 95.0), (91.0, 204.0), (196.0, 441.0), (421.0, 948.0), (909.0, 2045.0),
+            (1957.0, 4404.0), (4216.0, 9486.0))  # low shelf, 5 peaks, high shelf
+EQ_Q = (0.5, 1.33)
+
+
+def hz_to_mel(f):
+    return 2595.0 * np.log10(1.0 + np.asarray(f, dtype=np.float64) / 700.0)
+
+
+def mel_to_hz(m):
+    return 700.0 * (10.0 ** (np.asarray(m, dtype=np.float64) / 2595.0) - 1.0)
+
+
+def eq_draw(rng, n: int, gain_db: float, sample_rate: int = 16000):
+    """(center Hz, gain dB, Q) [n, 7, 3] for n clips."""
+    lo = hz_to_mel([b[0] for b in EQ_BANDS])
+    hi = hz_to_mel([b[1] for b in EQ_BANDS])
+    f0 = mel_to_hz(rng.uniform(lo, hi, (n, 7)))
+    f0[:, 6] = np.minimum(f0[:, 6], (sample_rate // 2) * 0.95)
+    g = rng.uniform(-gain_db, gain_db, (n, 7))
+    q = rng.uniform(EQ_Q[0], EQ_Q[1], (n, 7))
+    return np.stack([f0, g, q], axis=-1)
+
+
+def eq_sos(params, sample_rate: int = 16000) -> np.ndarray:
+    """RBJ biquads [..., 7, 6] (b0, b1, b2, 1, a1, a2; normalised by a0) from
+    eq_draw parameters [..., 7, 3]: filter 0 low shelf, 1-5 peaking, 6 high shelf."""
+    params = np.asarray(params, dtype=np.float64)
+    f0, gdb, q = params[..., 0], params[..., 1], params[..., 2]
+    A = 10.0 ** (gdb / 40.0)
+    w0 = 2.0 * np.pi * f0 / sample_rate
+    c, al = np.cos(w0), np.sin(w0) / (2.0 * q)
+    sA = np.sqrt(A)
+    # peaking
+    pb = np.stack([1 + al * A, -2 * c, 1 - al * A], -1)
+    pa = np.stack([1 + al / A, -2 * c, 1 - al / A], -1)
+    # low shelf
+    lb = np.stack([A * ((A + 1) - (A - 1) * c + 2 * sA * al), 2 * A * ((A - 1) - (A + 1) * c),
+                   A * ((A + 1) - (A - 1) * c - 2 * sA * al)], -1)
+    la = np.stack([(A + 1) + (A - 1) * c + 2 * sA * al, -2 * ((A - 1) + (A + 1) * c),
+                   (A + 1) + (A - 1) * c - 2 * sA * al], -1)
+    # high shelf
+    hb = np.stack([A * ((A + 1) + (A - 1) * c + 2 * sA * al), -2 * A * ((A - 1) + (A + 1) * c),
+                   A * ((A + 1) + (A - 1) * c - 2 * sA * al)], -1)
+    ha = np.stack([(A + 1) - (A - 1) * c + 2 * sA * al, 2 * ((A - 1) - (A + 1) * c),
+                   (A + 1) - (A - 1) * c - 2 * sA * al], -1)
+    k = np.arange(7)
+    b = np.where((k == 0)[:, None], lb, np.where((k == 6)[:, None], hb, pb))
+    a = np.where((k == 0)[:, None], la, np.where((k == 6)[:, None], ha, pa))
+    a0 = a[..., :1]
+    return np.concatenate([b / a0, np.ones_like(a0), a[..., 1:] / a0], axis=-1)
+
+
+def seven_band_eq(x, sos) -> np.ndarray:
+    """The cascade on float32 clips x [n, T] with per-clip sos [n, 7, 6]; a NaN
+    b0 in filter 0 leaves the clip unchanged (the transform's coin came up
+    tails). Each stage: DF2T in float64 on the float32 input, output cast to
+    float32 (audiomentations: sosfilt(...).astype(np.float32))."""
+    x = np.asarray(x, dtype=np.float32)
+    out = x.copy()
+    sos = np.asarray(sos, dtype=np.float64)
+    for i in range(x.shape[0]):
+        if np.isnan(sos[i, 0, 0]):
+            continue
+        y = x[i]
+        for k in range(7):  # scipy.signal.sosfilt: the DF2T recursion audiomentations calls
+            y = sosfilt(sos[i, k][None], y).astype(np.float32)
+        out[i] = y
+    return out

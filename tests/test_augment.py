@@ -208,7 +208,7 @@ def test_batch_augmenter_gain_is_per_batch():
     x = torch.from_numpy(_clips(300, seed=14)).float().cuda()
     np.random.seed(5)
     aug = BatchAugmenter(device=0, batch_size=128, background_noise_prob=0.0, reverb_prob=0.0,
-                         colored_noise_prob=0.0, tanh_distortion_prob=0.0)
+                         colored_noise_prob=0.0, tanh_distortion_prob=0.0, seven_band_prob=0.0)
     out = aug(x)
     ratio = (out / x).cpu().numpy()
     xs = x.cpu().numpy()
@@ -218,7 +218,7 @@ def test_batch_augmenter_gain_is_per_batch():
         np.testing.assert_allclose(blk, g, rtol=1e-6)
         assert 10 ** (-18 / 20) * (1 - 1e-6) <= g <= 10 ** (6 / 20) * (1 + 1e-6)
     off = BatchAugmenter(device=0, background_noise_prob=0.0, reverb_prob=0.0, gain_prob=0.0,
-                         colored_noise_prob=0.0, tanh_distortion_prob=0.0)
+                         colored_noise_prob=0.0, tanh_distortion_prob=0.0, seven_band_prob=0.0)
     assert torch.equal(off(x), x)
 
 
@@ -346,7 +346,7 @@ def test_batch_augmenter_colored_noise_is_per_batch():
     x = torch.from_numpy(_clips(300, seed=25)).float().cuda()
     np.random.seed(6)
     aug = BatchAugmenter(device=0, batch_size=128, background_noise_prob=0.0, reverb_prob=0.0, gain_prob=0.0,
-                         colored_noise_prob=1.0, tanh_distortion_prob=0.0)
+                         colored_noise_prob=1.0, tanh_distortion_prob=0.0, seven_band_prob=0.0)
     out = aug(x)
     xs, os_ = x.cpu().double().numpy(), out.cpu().double().numpy()
     rms = lambda v: np.sqrt((v * v).mean(axis=-1))
@@ -356,7 +356,7 @@ def test_batch_augmenter_colored_noise_is_per_batch():
         assert blk.max() - blk.min() < 1e-3
         assert 10.0 - 1e-3 <= blk[0] <= 30.0 + 1e-3
     off = BatchAugmenter(device=0, background_noise_prob=0.0, reverb_prob=0.0, gain_prob=0.0,
-                         colored_noise_prob=0.0, tanh_distortion_prob=0.0)
+                         colored_noise_prob=0.0, tanh_distortion_prob=0.0, seven_band_prob=0.0)
     assert torch.equal(off(x), x)
 
 
@@ -404,3 +404,44 @@ def test_tanh_distortion_parity():
     y = xs.clone()
     tanh_distortion(y, nan_amt, out=y)
     assert torch.equal(y, o2)
+
+
+# ---------------------------------------------------------------------------
+# Seven-band parametric EQ (audiomentations SevenBandParametricEQ, parity unpinned)
+def test_eq_coefficients_match_oracle_and_gains():
+    """The product's RBJ coefficients equal the oracle's, and each filter's
+    gain at its center frequency (peaks) / far side (shelves) is the drawn gain."""
+    import scipy.signal as ss
+    from heybuddy.dataset.augmented import eq_coefficients
+    rng = np.random.default_rng(3)
+    prm = oaug.eq_draw(rng, 5, 6.0)
+    ours = eq_coefficients(prm)
+    sos = oaug.eq_sos(prm)
+    np.testing.assert_allclose(ours, sos[..., [0, 1, 2, 4, 5]], rtol=1e-12, atol=1e-14)
+    for i in range(5):
+        for k in range(1, 6):  # peaks: |H(f0)| = gain
+            _, h = ss.sosfreqz(sos[i, k][None], worN=[prm[i, k, 0]], fs=16000)
+            np.testing.assert_allclose(20 * np.log10(abs(h[0])), prm[i, k, 1], atol=1e-6)
+        _, h = ss.sosfreqz(sos[i, 0][None], worN=[1e-3], fs=16000)  # low shelf at DC
+        np.testing.assert_allclose(20 * np.log10(abs(h[0])), prm[i, 0, 1], atol=1e-3)
+        _, h = ss.sosfreqz(sos[i, 6][None], worN=[7999.0], fs=16000)  # high shelf near Nyquist
+        np.testing.assert_allclose(20 * np.log10(abs(h[0])), prm[i, 6, 1], atol=0.05)
+    assert (prm[:, 6, 0] <= 7600.0).all() and (prm[:, :, 2] >= 0.5).all() and (prm[:, :, 2] <= 1.33).all()
+
+
+@pytest.mark.gpu
+def test_seven_band_eq_kernel_matches_oracle():
+    from heybuddy.dataset.augmented import eq_coefficients, eq_parameters
+    from heybuddy.kernels import seven_band_eq
+    rng = np.random.default_rng(4)
+    n = 70  # a full 64-clip wave and a ragged one
+    x = (rng.standard_normal((n, 24000)) * 0.2).astype(np.float32)
+    np.random.seed(9)
+    coef = eq_coefficients(eq_parameters(n, 6.0))
+    coef[[3, 65], 0, 0] = np.nan  # coin tails: copied
+    sos = np.concatenate([coef[..., :3], np.ones_like(coef[..., :1]), coef[..., 3:]], axis=-1)
+    ref = oaug.seven_band_eq(x[:, :23040], sos)
+    out = seven_band_eq(torch.from_numpy(x).cuda(), torch.from_numpy(coef)).cpu().numpy()
+    scale = np.abs(ref).max(axis=1, keepdims=True)
+    np.testing.assert_allclose(out / scale, ref / scale, rtol=0, atol=2e-6)
+    np.testing.assert_array_equal(out[[3, 65]], x[[3, 65], :23040])
