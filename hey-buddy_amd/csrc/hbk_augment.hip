@@ -1018,6 +1018,7 @@ struct EqArgs {
   const float* x;
   int64_t x_stride;
   const double* coef;  // [n][7][5]: b0, b1, b2, a1, a2 (a0 = 1)
+  const int32_t* idx;  // clip of entry j (NULL: j)
   float* out;
   int64_t out_stride;
   int64_t n;
@@ -1026,24 +1027,29 @@ struct EqArgs {
 __global__ void __launch_bounds__(64) eq_kernel(EqArgs a) {
   __shared__ float tile[kEqTile][kEqTile + 1];
   const int lane = threadIdx.x;
-  const int64_t c0 = static_cast<int64_t>(blockIdx.x) * 64;
-  const int64_t cl = min(c0 + lane, a.n - 1);
+  const int64_t j0 = static_cast<int64_t>(blockIdx.x) * 64;
+  const int64_t jl = min(j0 + lane, a.n - 1);
   double co[35];
 #pragma unroll
-  for (int i = 0; i < 35; ++i) co[i] = a.coef[cl * 35 + i];
-  const bool skip = c0 + lane >= a.n || co[0] != co[0];
+  for (int i = 0; i < 35; ++i) co[i] = a.coef[jl * 35 + i];
+  const bool skip = j0 + lane >= a.n || co[0] != co[0];
   double s1[7], s2[7];
 #pragma unroll
   for (int k = 0; k < 7; ++k) s1[k] = s2[k] = 0.0;
-  // cooperative mapping: item i of this lane -> clip row (lane + 64 i) / 16, samples 4 ((lane + 64 i) % 16) ..
-  const float* rows[16];
+  // cooperative mapping: item i of this lane -> entry row (lane + 64 i) / 16,
+  // samples 4 ((lane + 64 i) % 16) .. of the tile; entries past n re-read the
+  // last entry's clip and are never stored
+  int64_t clip[16];
   float4 pre[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int e = lane + 64 * i;
-    rows[i] = a.x + min(c0 + (e >> 4), a.n - 1) * a.x_stride + 4 * (e & 15);
-    pre[i] = *reinterpret_cast<const float4*>(rows[i]);
+    const int64_t j = min(j0 + (e >> 4), a.n - 1);
+    clip[i] = a.idx ? static_cast<int64_t>(a.idx[j]) : j;
   }
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    pre[i] = *reinterpret_cast<const float4*>(a.x + clip[i] * a.x_stride + 4 * ((lane + 64 * i) & 15));
   for (int t0 = 0; t0 < kT; t0 += kEqTile) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -1056,7 +1062,8 @@ __global__ void __launch_bounds__(64) eq_kernel(EqArgs a) {
     __syncthreads();
     const int tn = min(t0 + kEqTile, kT - kEqTile);  // next tile (the last iteration re-reads its own)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) pre[i] = *reinterpret_cast<const float4*>(rows[i] + tn);
+    for (int i = 0; i < 16; ++i)
+      pre[i] = *reinterpret_cast<const float4*>(a.x + clip[i] * a.x_stride + tn + 4 * ((lane + 64 * i) & 15));
     if (!skip) {
       for (int s = 0; s < kEqTile; ++s) {
         float v = tile[s][lane];
@@ -1075,8 +1082,8 @@ __global__ void __launch_bounds__(64) eq_kernel(EqArgs a) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int e = lane + 64 * i, r = e >> 4, q = 4 * (e & 15);
-      if (c0 + r < a.n)
-        *reinterpret_cast<float4*>(a.out + (c0 + r) * a.out_stride + t0 + q) =
+      if (j0 + r < a.n)
+        *reinterpret_cast<float4*>(a.out + clip[i] * a.out_stride + t0 + q) =
             float4{tile[q][r], tile[q + 1][r], tile[q + 2][r], tile[q + 3][r]};
     }
     __syncthreads();
@@ -1299,11 +1306,12 @@ int hbk_tanh_distortion(const float* x, int64_t n_clips, int64_t x_stride, const
   return HBK_OK;
 }
 
-int hbk_seven_band_eq(const float* x, int64_t n_clips, int64_t x_stride, const double* coef, float* out,
-                      int64_t out_stride, void* stream) {
+int hbk_seven_band_eq(const float* x, int64_t n_clips, int64_t x_stride, const double* coef, const int32_t* idx,
+                      int64_t n_entries, float* out, int64_t out_stride, void* stream) {
   using namespace hbk;
-  if (n_clips < 0) return arg_error("negative n_clips");
-  if (n_clips == 0) return HBK_OK;
+  if (n_clips < 0 || n_entries < 0) return arg_error("negative count");
+  if (!idx) n_entries = n_clips;
+  if (n_entries == 0) return HBK_OK;
   if (!x || !out || !coef) return arg_error("NULL pointer");
   if (x_stride < kT || out_stride < kT) return arg_error("stride < 23040");
   if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out)) % 16 || x_stride % 4 || out_stride % 4)
@@ -1312,10 +1320,11 @@ int hbk_seven_band_eq(const float* x, int64_t n_clips, int64_t x_stride, const d
   a.x = x;
   a.x_stride = x_stride;
   a.coef = coef;
+  a.idx = idx;
   a.out = out;
   a.out_stride = out_stride;
-  a.n = n_clips;
-  hipLaunchKernelGGL(eq_kernel, dim3(unsigned((n_clips + 63) / 64)), dim3(64), 0, as_stream(stream), a);
+  a.n = n_entries;
+  hipLaunchKernelGGL(eq_kernel, dim3(unsigned((n_entries + 63) / 64)), dim3(64), 0, as_stream(stream), a);
   HBK_LAUNCH_CHECK("eq_kernel");
   return HBK_OK;
 }

@@ -213,12 +213,12 @@ class BatchAugmenter:
             per_clip = np.where(r_on, ir, -1).astype(np.int32)[batch]
             spec_idx[:] = per_clip
         self._colored = (colored_snr, colored_fd)
-        # seven-band EQ (audiomentations, per clip): NaN b0 = off
+        # seven-band EQ (audiomentations, per clip): the clips whose coin came up
+        # and their filters (parameters drawn for those clips only)
         e_on = np.random.rand(n) < getattr(self, "p_eq", 0.0)
         sr = getattr(self, "sample_rate", 16000)
-        coef = eq_coefficients(eq_parameters(n, getattr(self, "eq_gain_db", 0.0), sr), sr)
-        coef[~e_on, 0, 0] = np.nan
-        self._eq = coef
+        eq_idx = np.nonzero(e_on)[0].astype(np.int32)
+        self._eq = (eq_idx, eq_coefficients(eq_parameters(eq_idx.size, getattr(self, "eq_gain_db", 0.0), sr), sr))
         # tanh distortion (audiomentations, per clip): NaN amount = off
         t_on = np.random.rand(n) < getattr(self, "p_tanh", 0.0)
         t_amt = np.random.uniform(*getattr(self, "tanh_range", (0.0, 0.0)), n)
@@ -236,9 +236,13 @@ class BatchAugmenter:
         gain = None
         if self.p_gain > 0:  # torch_audiomentations convert_decibels_to_amplitude_ratio
             gain = torch.pow(10.0, torch.from_numpy(gain_db) / 20.0)
-        if not np.isnan(self._eq[:, 0, 0]).all():  # per-clip Compose: EQ, then tanh (augmented.py:79-90)
-            x = seven_band_eq(x, torch.from_numpy(self._eq), out=out)
-            out = x
+        eq_idx, eq_coef = self._eq
+        if eq_idx.size:  # per-clip Compose: EQ, then tanh (augmented.py:79-90), in place on out
+            if out is None:
+                out = torch.empty((n, T), dtype=torch.float32, device=x.device)
+            if out.data_ptr() != x.data_ptr():
+                out.copy_(x[:, :T])
+            x = seven_band_eq(out, torch.from_numpy(eq_coef), idx=torch.from_numpy(eq_idx))
         if not np.isnan(self._tanh).all():  # per-clip Compose, before the batch chain (augmented.py:325-328)
             x = tanh_distortion(x, torch.from_numpy(self._tanh), out=out)
             out = x

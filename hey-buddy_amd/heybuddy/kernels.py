@@ -588,11 +588,14 @@ def tanh_distortion(x: torch.Tensor, amount: torch.Tensor, out: torch.Tensor | N
     return out
 
 
-def seven_band_eq(x: torch.Tensor, coef: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-    """audiomentations SevenBandParametricEQ per clip on x [n, >= 23040] -> out
-    [n, 23040] (hbk_seven_band_eq): coef [n, 7, 5] float64 (b0, b1, b2, a1, a2
-    of the low shelf, five peaks and high shelf, normalised by a0); a NaN
-    coef[i, 0, 0] leaves clip i unchanged."""
+def seven_band_eq(x: torch.Tensor, coef: torch.Tensor, out: torch.Tensor | None = None,
+                  idx: torch.Tensor | None = None) -> torch.Tensor:
+    """audiomentations SevenBandParametricEQ per clip (hbk_seven_band_eq).
+    Without ``idx``: every clip of x [n, >= 23040] -> out [n, 23040], coef
+    [n, 7, 5] float64 (b0, b1, b2, a1, a2 of the low shelf, five peaks and high
+    shelf, normalised by a0), a NaN coef[i, 0, 0] copies clip i. With ``idx``
+    (int32 [m]): only clips idx[j] with coef [m, 7, 5], written into out
+    (default: in place into x)."""
     T = ReverbPlan.T
     dev = _native.require_device(x.device)
     n = x.shape[0]
@@ -600,17 +603,30 @@ def seven_band_eq(x: torch.Tensor, coef: torch.Tensor, out: torch.Tensor | None 
         raise ValueError(f"x must be [n, >= {T}] f32 rows on the device")
     if x.stride(0) % 4 or x.data_ptr() % 16:
         raise ValueError("x rows must be 16-B aligned")
-    coef = coef.to(dtype=torch.float64).reshape(n, 7, 5).contiguous()
-    coef = coef.pin_memory().to(dev, non_blocking=True) if coef.device.type == "cpu" else coef.to(dev)
-    if out is None:
+
+    def to_dev(t: torch.Tensor) -> torch.Tensor:
+        return t.pin_memory().to(dev, non_blocking=True) if t.device.type == "cpu" else t.to(dev)
+
+    m = n if idx is None else int(idx.numel())
+    coef = to_dev(coef.to(dtype=torch.float64).reshape(m, 7, 5).contiguous())
+    if idx is not None:
+        idx = idx.to(dtype=torch.int32).reshape(-1).contiguous()
+        if idx.device.type == "cpu" and m and (int(idx.min()) < 0 or int(idx.max()) >= n):
+            raise ValueError("idx out of range")
+        idx = to_dev(idx)
+        if out is None:
+            out = x
+    elif out is None:
         out = torch.empty((n, T), dtype=torch.float32, device=dev)
-    torch.ops.hbk.seven_band_eq_(x, coef, out)
+    if m:
+        torch.ops.hbk.seven_band_eq_(x, coef, idx, out)
     return out
 
 
 @torch.library.custom_op("hbk::seven_band_eq_", mutates_args=("out",))
-def _seven_band_eq_op(x: torch.Tensor, coef: torch.Tensor, out: torch.Tensor) -> None:
-    check(lib().hbk_seven_band_eq(ptr(x), x.shape[0], x.stride(0), ptr(coef), ptr(out), out.stride(0),
+def _seven_band_eq_op(x: torch.Tensor, coef: torch.Tensor, idx: torch.Tensor | None, out: torch.Tensor) -> None:
+    check(lib().hbk_seven_band_eq(ptr(x), x.shape[0], x.stride(0), ptr(coef), ptr(idx) if idx is not None else None,
+                                  idx.numel() if idx is not None else x.shape[0], ptr(out), out.stride(0),
                                   stream_ptr(x.device)), "hbk_seven_band_eq")
 
 

@@ -309,15 +309,17 @@ int hbk_colored_noise(const hbk_reverb_plan* plan, const float* x, int64_t n_cli
  * out may equal x. Device pointers. */
 /* Seven-band parametric EQ: audiomentations SevenBandParametricEQ, which the
  * reference applies per clip with p 0.25 and gains in +-6 dB, first in its
- * per-clip Compose (dataset/augmented.py:79-84; constants.py:120-121). Per clip
- * i of x [n_clips, x_stride] (first T = 23040 samples): seven biquads in
- * series, coef[i][k] = (b0, b1, b2, a1, a2) normalised by a0 (f64; low shelf,
- * five peaks, high shelf from the RBJ cookbook, built by the caller), each run
- * as direct form II transposed in f64 from a zero state with its output
- * rounded to f32 (scipy sosfilt + astype(float32) per filter). coef[i][0][0]
- * NaN: out[i] = x[i]. Rows 16-B aligned; out may equal x. Device pointers. */
-int hbk_seven_band_eq(const float* x, int64_t n_clips, int64_t x_stride, const double* coef, float* out,
-                      int64_t out_stride, void* stream);
+ * per-clip Compose (dataset/augmented.py:79-84; constants.py:120-121). For
+ * entry j < n_entries, clip c = idx[j] (idx NULL: every clip, c = j,
+ * n_entries = n_clips) of x [., x_stride] (first T = 23040 samples): seven
+ * biquads in series, coef[j][k] = (b0, b1, b2, a1, a2) normalised by a0 (f64;
+ * low shelf, five peaks, high shelf from the RBJ cookbook, built by the
+ * caller), each run as direct form II transposed in f64 from a zero state with
+ * its output rounded to f32 (scipy sosfilt + astype(float32) per filter), into
+ * out[c]. coef[j][0][0] NaN: out[c] = x[c]. Clips not listed are not touched:
+ * with idx, run it in place (out == x). Rows 16-B aligned. Device pointers. */
+int hbk_seven_band_eq(const float* x, int64_t n_clips, int64_t x_stride, const double* coef, const int32_t* idx,
+                      int64_t n_entries, float* out, int64_t out_stride, void* stream);
 
 int hbk_tanh_distortion(const float* x, int64_t n_clips, int64_t x_stride, const float* amount, float* out,
                         int64_t out_stride, void* stream);

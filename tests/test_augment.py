@@ -445,3 +445,10 @@ def test_seven_band_eq_kernel_matches_oracle():
     scale = np.abs(ref).max(axis=1, keepdims=True)
     np.testing.assert_allclose(out / scale, ref / scale, rtol=0, atol=2e-6)
     np.testing.assert_array_equal(out[[3, 65]], x[[3, 65], :23040])
+    # indexed, in place: only the listed clips change
+    sel = np.array([5, 0, 69, 40], dtype=np.int32)
+    xd = torch.from_numpy(x).cuda()
+    got = seven_band_eq(xd, torch.from_numpy(coef[sel]), idx=torch.from_numpy(sel)).cpu().numpy()
+    keep = np.setdiff1d(np.arange(n), sel)
+    np.testing.assert_array_equal(got[keep], x[keep])
+    np.testing.assert_allclose(got[sel, :23040] / scale[sel], ref[sel] / scale[sel], rtol=0, atol=2e-6)
