@@ -496,9 +496,9 @@ def setup_e2e(args, dev, rank, world, seed):
 
     def roofline(name, ms, pmc):
         if name == "augment":
-            return roof("place_kernel + tanh_distortion_kernel + colored_noise_kernel + augment_kernel "
-                        "(placement, tanh, colored noise, gain + noise mix + 23040-pt FFT reverb)", "hbm",
-                        n * AUG_T * 4 * 2, ms, "GB/s", load_traffic(pmc, ("place_kernel", "augment_kernel",
+            return roof("place_kernel + eq_kernel + tanh_distortion_kernel + colored_noise_kernel + augment_kernel "
+                        "(placement, 7-band EQ, tanh, colored noise, gain + noise mix + 23040-pt FFT reverb)", "hbm",
+                        n * AUG_T * 4 * 2, ms, "GB/s", load_traffic(pmc, ("place_kernel", "augment_kernel", "eq_kernel",
                                                                           "colored_noise", "tanh_distortion")),
                         algorithmic_bytes_per_clip=AUG_T * 4 * 2,
                         bytes_basis="placed clip written + augmented clip written in place (92,160 B each); "
