@@ -699,6 +699,14 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
       if (r0 + row4 + e >= a.B) v[e] = 0.f;
     *reinterpret_cast<f4*>(base + col * Bp + r0 + row4) = v;
   };
+  // a [16][kLd] LDS tile's first ncols columns -> base^T (4 rows per float4)
+  auto store_t = [&](float* base, const float* src, int ncols) {
+    for (int e = tid; e < 4 * ncols; e += 256) {
+      const int col = e >> 2, r4 = 4 * (e & 3);
+      st4(base, col, r4,
+          f4{src[r4 * kLd + col], src[(r4 + 1) * kLd + col], src[(r4 + 2) * kLd + col], src[(r4 + 3) * kLd + col]});
+    }
+  };
   if (kTrain) {  // U_0 from bU: thread -> column tid & 63, rows 4 (tid >> 6) ..
     const int j = tid & 63, rg = 4 * (tid >> 6);
     st4(a.U, j, rg, f4{bU[rg][j], bU[rg + 1][j], bU[rg + 2][j], bU[rg + 3][j]});
@@ -722,41 +730,33 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
     }
     __syncthreads();
     K2_MARK(10 + k);
-    // LayerNorm k over 96 columns: wave w -> rows 4w..4w+3, lane -> c, c + 64
+    // LayerNorm k over 96 columns: 16 lanes per row (wave w -> rows 4w..4w+3,
+    // lane -> row 4w + lane / 16, columns 6 (lane % 16) ..), both reductions of
+    // the four rows in parallel within 16-lane DPP rows (rsum16: no cross-row
+    // steps); Xn^T goes to HBM from LDS in the next stage
     if (k + 2 < NG) load_w<kH, kL, true>(wa, P + a.w_o[k + 1], wave, lane);
     {
-      const bool hi = lane < kL - 64;
-      const float g0 = sLg[k][lane], b0 = sLb[k][lane];
-      const float g1 = hi ? sLg[k][64 + lane] : 0.f, b1 = hi ? sLb[k][64 + lane] : 0.f;
-      f4 o0, o1;
+      const int r = wave * 4 + (lane >> 4), c0 = 6 * (lane & 15);
+      float v[6];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = wave * 4 + i;
-        const float v0 = bS[r][lane], v1 = hi ? bS[r][64 + lane] : 0.f;
-        const float mu = wsum(v0 + v1) * (1.f / kL);
-        const float d0 = v0 - mu, d1 = hi ? v1 - mu : 0.f;
-        const float rs = 1.f / sqrtf(wsum(d0 * d0 + d1 * d1) * (1.f / kL) + kLnEps);
-        const float x0 = d0 * rs, x1 = d1 * rs;
-        const float n0 = x0 * g0 + b0, n1 = x1 * g1 + b1;
-        xhS[k][r][lane] = x0;
-        bX[r][lane] = n0;
-        o0[i] = n0;
-        o1[i] = n1;
-        if (hi) {
-          xhS[k][r][64 + lane] = x1;
-          bX[r][64 + lane] = n1;
-        }
-        if (lane == 0) rsS[k][r] = rs;
+      for (int e = 0; e < 6; ++e) v[e] = bS[r][c0 + e];
+      const float mu = rsum16(((v[0] + v[1]) + (v[2] + v[3])) + (v[4] + v[5])) * (1.f / kL);
+      float sq = 0.f;
+#pragma unroll
+      for (int e = 0; e < 6; ++e) sq += (v[e] - mu) * (v[e] - mu);
+      const float rs = 1.f / sqrtf(rsum16(sq) * (1.f / kL) + kLnEps);
+#pragma unroll
+      for (int e = 0; e < 6; ++e) {
+        const float x = (v[e] - mu) * rs;
+        xhS[k][r][c0 + e] = x;
+        bX[r][c0 + e] = x * sLg[k][c0 + e] + sLb[k][c0 + e];
       }
-      if (kTrain) {
-        float* xt = a.Xn + (k + 1) * kL * Bp;
-        st4(xt, lane, 4 * wave, o0);
-        if (hi) st4(xt, 64 + lane, 4 * wave, o1);
-      }
+      if ((lane & 15) == 0) rsS[k][r] = rs;
     }
     __syncthreads();
     K2_MARK(20 + k);
     // HG_{k+1} = Xn W_hg^T + b, gate in the epilogue -> hgS[k+1], U_{k+1} -> bU
+    if (kTrain) store_t(a.Xn + (k + 1) * kL * Bp, &bX[0][0], kL);
     {
       f4 ch, cg;
       gemm2<kL>(wb, &bX[0][0], lane, ch, cg);
@@ -913,27 +913,22 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
         atomicAdd(G + a.ln_g[l] + tid, sg);
         atomicAdd(G + a.ln_b[l] + tid, sb);
       }
-      const bool hi = lane < kL - 64;
-      const float g0 = sLg[l][lane], g1 = hi ? sLg[l][64 + lane] : 0.f;
-      f4 o0, o1;
+      // 16 lanes per row, as in the forward LayerNorm; dS^T goes to HBM from
+      // LDS in the next stage
+      const int r = wave * 4 + (lane >> 4), c0 = 6 * (lane & 15);
+      float t[6], x[6];
+      float p1 = 0.f, p2 = 0.f;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = wave * 4 + i;
-        const float t0 = bU[r][lane] * g0;
-        const float t1 = hi ? bU[r][64 + lane] * g1 : 0.f;
-        const float x0 = xhS[l][r][lane], x1 = hi ? xhS[l][r][64 + lane] : 0.f;
-        const float s1 = wsum(t0 + t1) * (1.f / kL);
-        const float s2 = wsum(t0 * x0 + t1 * x1) * (1.f / kL);
-        const float rs = rsS[l][r];
-        const float d0 = rs * (t0 - s1 - x0 * s2);
-        const float d1 = rs * (t1 - s1 - x1 * s2);
-        bS[r][lane] = d0;
-        o0[i] = d0;
-        o1[i] = d1;
-        if (hi) bS[r][64 + lane] = d1;
+      for (int e = 0; e < 6; ++e) {
+        t[e] = bU[r][c0 + e] * sLg[l][c0 + e];
+        x[e] = xhS[l][r][c0 + e];
+        p1 += t[e];
+        p2 += t[e] * x[e];
       }
-      st4(a.dS + l * kL * Bp, lane, 4 * wave, o0);
-      if (hi) st4(a.dS + l * kL * Bp, 64 + lane, 4 * wave, o1);
+      const float s1 = rsum16(p1) * (1.f / kL), s2 = rsum16(p2) * (1.f / kL);
+      const float rs = rsS[l][r];
+#pragma unroll
+      for (int e = 0; e < 6; ++e) bS[r][c0 + e] = rs * (t[e] - s1 - x[e] * s2);
     }
     __syncthreads();
     K2_MARK(60 + k);
@@ -941,6 +936,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
     // W in wY) with the gate backward in the epilogue -> dHG_{k-1} (bX)
     {
       const int kk = k - 1;
+      store_t(a.dS + kk * kL * Bp, &bS[0][0], kL);
       if (tid < kL) {
         float s = 0.f;
         for (int r = 0; r < kR; ++r) s += bS[r][tid];
