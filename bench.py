@@ -281,6 +281,7 @@ def setup_train(args, dev, rank, world, seed):
     k1a/k1b/k2/k3/k4 per step, hipGraph-replayed). A bench step = one pass of
     STEPS_1 stage-1 steps, 2 STEPS_1 stage-2 steps and 4 STEPS_1 stage-3 steps;
     units = embeddings trained (sum of the stages' batches)."""
+    import numpy as np
     from heybuddy.trainer import WakeWordTrainer
 
     g = torch.Generator(device=dev).manual_seed(seed)
