@@ -66,6 +66,11 @@ def parse():
                     help="config 3 plus the reference's tanh distortion and colored noise at their default "
                          "probabilities (0.25 each); not the BASELINE configs[2] workload")
     ap.add_argument("--no-check", action="store_true", help="skip the one-off featurize equality check")
+    ap.add_argument("--overlap", default="off",
+                    help="config 5: train chunk s while chunk s + 1 is featurized on a second stream "
+                         "(heybuddy.pipeline policies: off, prio, split:N, spill:N)")
+    ap.add_argument("--stage-steps", type=int, default=2,
+                    help="overlapped runs: sequential (untimed) steps that time the stages for the rooflines")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                     help="per-kernel HBM bytes from rocprofv3 --pmc passes (optional)")
     return ap.parse_args()
@@ -122,17 +127,23 @@ def main():
     job = setup(args, dev, rank, world, seed_for(args.config, rank))
     stream = torch.cuda.current_stream(dev)
 
+    staged = job.get("staged_step")  # overlapped stages: timed per stage in separate sequential steps
+    n_ev = args.stage_steps if staged else args.steps
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(len(job["stages"]) + 1)] for _ in range(n_ev)]
+    if staged:  # before the pipelined warmup, which leaves the next chunk's features pending
+        staged(None)
+        for k in range(n_ev):
+            staged(evs[k])
+        torch.cuda.synchronize(dev)
     for _ in range(args.warmup):
         job["step"](None)
     torch.cuda.synchronize(dev)
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(len(job["stages"]) + 1)]
-           for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(args.steps):
-        job["step"](evs[k])
+        job["step"](None if staged else evs[k])
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -141,7 +152,7 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    stage_ms = [sum(e[i].elapsed_time(e[i + 1]) for e in evs) / args.steps for i in range(len(job["stages"]))]
+    stage_ms = [sum(e[i].elapsed_time(e[i + 1]) for e in evs) / n_ev for i in range(len(job["stages"]))]
     roofs = [job["roofline"](name, ms, args.pmc) for name, ms in zip(job["stages"], stage_ms)]
     dom = max(range(len(roofs)), key=lambda i: stage_ms[i])
 
@@ -448,7 +459,7 @@ def setup_e2e(args, dev, rank, world, seed):
     import numpy as np
     from heybuddy.dataset.augmented import AugmentedAudioGenerator
     from heybuddy.embedding_graph import WINDOW_STARTS
-    from heybuddy.embeddings import _replace_nan_rows, default_graph, embed_plan
+    from heybuddy.embeddings import default_graph, embed_plan, replace_nan_rows_device
     from heybuddy.kernels import embed_clips, mel_frames
     from heybuddy.spectrogram import default_mel_plan
     from heybuddy.synthetic import impulse_responses, noise_bank, speech_clips
@@ -468,6 +479,7 @@ def setup_e2e(args, dev, rank, world, seed):
     mplan = default_mel_plan(dev, 32767.0)
     eplan = embed_plan(dev, WINDOW_STARTS)
     pool = torch.empty((n, len(WINDOW_STARTS), 96), dtype=torch.float32, device=dev)
+    raw = torch.empty_like(pool)  # embed output before the NaN replacement gathers it into the pool
     # precalculated negatives (the reference's hosted f16 sets): large 2/3, medium 1/3
     g = torch.Generator(device=dev).manual_seed(seed + 4)
     n_neg = 200_000
@@ -502,17 +514,17 @@ def setup_e2e(args, dev, rank, world, seed):
         neg_pos[0] = (o + S * NL) % n_large
 
     def step(evs):
+        stream = torch.cuda.current_stream(dev)
+        prep = aug.prepare_device(src, lens)  # host draws first: the stage events time device work
         if evs:
             evs[0].record(stream)
-        x = aug.augment_device(src, lens)
+        x = aug.augment_device(src, lens, prepared=prep)
         if evs:
             evs[1].record(stream)
         frames = mel_frames(x, mplan, N_FRAMES)
         if evs:
             evs[2].record(stream)
-        emb = _replace_nan_rows(embed_clips(frames, eplan, out=pool))
-        if emb is not pool:
-            pool.copy_(emb)
+        replace_nan_rows_device(embed_clips(frames, eplan, out=raw), out=pool)  # no host sync
         if evs:
             evs[3].record(stream)
         sample()
@@ -520,6 +532,52 @@ def setup_e2e(args, dev, rank, world, seed):
         tr.train_indexed(idx, y, sched, pool32=pool, pool16=neg, history=hist, steps_per_graph=50)
         if evs:
             evs[4].record(stream)
+
+    staged_step = None
+    if args.overlap != "off":
+        # heybuddy.pipeline: train(s) on the train stream while featurize(s + 1)
+        # runs on the feature stream; two embedding pools
+        from heybuddy.pipeline import make_streams
+        fs, ts, keep = make_streams(dev, args.overlap)
+        pools = [pool, torch.empty_like(pool)]
+        feat_done = [torch.cuda.Event(), torch.cuda.Event()]
+        train_done = [torch.cuda.Event(), torch.cuda.Event()]
+        count = [0]
+        staged_step = step
+
+        host_log = os.environ.get("HBK_BENCH_HOSTTIME")
+
+        def featurize(c):
+            b = c % 2
+            with torch.cuda.stream(fs):
+                fs.wait_event(train_done[b])  # train(c - 2) has finished reading pools[b]
+                x = aug.augment_device(src, lens)
+                frames = mel_frames(x, mplan, N_FRAMES)
+                replace_nan_rows_device(embed_clips(frames, eplan, out=raw), out=pools[b])
+                feat_done[b].record(fs)
+
+        def step(evs):  # noqa: F811
+            # chunk c+1 is featurized while chunk c trains; its work is queued
+            # FIRST: 1,000 train steps are ~5,000 packets, and a full hardware
+            # queue blocks the host until the device drains it
+            c = count[0]
+            count[0] += 1
+            if c == 0:
+                featurize(0)  # pipeline fill (first warmup step)
+            h0 = time.perf_counter()
+            featurize(c + 1)
+            h1 = time.perf_counter()
+            b = c % 2
+            with torch.cuda.stream(ts):
+                ts.wait_event(feat_done[b])
+                sample()
+                tr._reset_accumulation()
+                tr.train_indexed(idx, y, sched, pool32=pools[b], pool16=neg, history=hist, steps_per_graph=50)
+                train_done[b].record(ts)
+            if host_log:
+                print("host ms: featurize enqueue %.1f, train enqueue %.1f" % (
+                    1e3 * (h1 - h0), 1e3 * (time.perf_counter() - h1)), file=sys.stderr, flush=True)
+        step.keep = keep  # the CU-masked streams live as long as the step
 
     flops_step = 2.0 * 559_296 * B
 
@@ -595,8 +653,8 @@ def setup_e2e(args, dev, rank, world, seed):
                 "sample_1thread": f"{res[1][1]} clips + {res[1][3]} train steps, {res[1][2]:.1f} s"}
 
     return {
-        "step": step, "stages": stages, "roofline": roofline, "cpu_baseline": cpu_baseline,
-        "units_per_step": n, "scaling": "weak", "unit": "clips/s",
+        "step": step, "staged_step": staged_step, "stages": stages, "roofline": roofline,
+        "cpu_baseline": cpu_baseline, "units_per_step": n, "scaling": "weak", "unit": "clips/s",
         "metric": "audio clips/sec featurized+trained, 1.5 s @16 kHz, 1/2/4/8 GPU",
         "data": "synthetic TTS-like utterances (seeded, 0.3-1.5 s), synthetic noise + IR banks, synthetic "
                 "f16 negative pool; SE20 stand-in embedding graph",

@@ -31,8 +31,10 @@
 //   k4_update  the < 128-sample accumulation gate, Adam, and zeroing of the
 //              bucket for the next step
 //
-// All arithmetic is f32 (GEMMs on v_mfma_f32_16x16x4_f32, bitwise an fmaf
-// chain); results differ from the reference only in summation order.
+// GEMMs are split-f16 products (hi*hi + hi*lo + lo*hi of f16 hi / lo parts,
+// f32 accumulation, operands power-of-two scaled into the f16 range): ~22-bit
+// products, so results differ from the f32 reference at the level of its own
+// summation-order differences; everything else is f32.
 //
 // Step state lives on the device and is PING-PONGED: state[2][8] floats
 // (acc_samples, acc_steps, adam_t, step, -, -, -, -); step s reads half
@@ -291,19 +293,23 @@ __global__ void __launch_bounds__(256) k1a_kernel(K1aArgs a, int next) {
 
 // Split-f16 products on v_mfma_f32_16x16x32_f16: v = hi + lo with hi = v
 // rounded toward zero to f16 and lo = f16(v - hi) (v - hi is exact in f32), so
-// a . b ~ hi_a hi_b + hi_a lo_b + lo_a hi_b (the dropped lo_a lo_b is
-// ~2^-22 relative): three f16 MFMAs (16 cycles each per 16x16x32) for the 8
-// f32 MFMAs (32 cycles each) of the same 32-deep product. Two values per
-// 3 VALU instructions (v_cvt_pkrtz + two v_fma_mix).
-typedef __fp16 hh2 __attribute__((ext_vector_type(2)));
+// a . b ~ hi_a hi_b + hi_a lo_b + lo_a hi_b: three f16 MFMAs (16 cycles each
+// per 16x16x32) for the 8 f32 MFMAs (32 cycles each) of the same 32-deep
+// product. hi is rounded to nearest (v_cvt_pk_f16_f32), so |lo| <= 2^-11 |x|
+// with either sign and the dropped lo_a lo_b is an unbiased ~2^-22 relative
+// term (a round-toward-zero hi makes it up to 2^-20 and one-signed, a bias that
+// survives long sums). lo = x - hi is exact in f32 before its rounding to f16.
+// Plain vector code (cvt_pk, two cvt back, pk_fma, cvt_pk per pair): the
+// compiler sees every operand and places the wait states itself. Callers keep
+// |x| < 2^15.
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+typedef float f2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void split_pair(float a, float b, uint32_t& hi, uint32_t& lo) {
-  const hh2 h = __builtin_amdgcn_cvt_pkrtz(a, b);
+  const h2v h = __builtin_convertvector(f2v{a, b}, h2v);
+  const f2v r = f2v{a, b} - __builtin_convertvector(h, f2v);
   hi = __builtin_bit_cast(uint32_t, h);
-  uint32_t l = 0;
-  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "+v"(l) : "v"(a), "v"(hi));
-  asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(l) : "v"(b), "v"(hi));
-  lo = l;
+  lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, h2v));
 }
 // 8 floats (two f4) -> hi / lo h8
 __device__ __forceinline__ void split8(const f4& x0, const f4& x1, h8& hi, h8& lo) {
@@ -428,14 +434,22 @@ __global__ void __launch_bounds__(256) k1b_kernel(K1bArgs a) {
 
 // ------------------------------------------------------------------ k2 ----
 // One 16-row tile per workgroup, 4 waves. Every matrix stage is
-// C[16][N] = A[16][K] . op(W) on v_mfma_f32_16x16x4_f32 with A in LDS; wave w
-// owns the 16-column tiles w and w + 4, so a gated MLP's hidden column j and
-// gate column 64 + j land in the same wave and the SiLU gate (forward) and its
+// C[16][N] = A[16][K] . op(W) with A in LDS, as split-f16 products on
+// v_mfma_f32_16x16x32_f16 (hi*hi + hi*lo + lo*hi, f32 accumulation, as in k1b
+// and k3: a fifth of the MFMA cycles of the f32 16x16x4 chain). Wave w owns
+// the 16-column tiles w and w + 4, so a gated MLP's hidden column j and gate
+// column 64 + j land in the same wave and the SiLU gate (forward) and its
 // derivative (backward) run in the GEMM epilogue. The B operands (weights) of
 // the NEXT matrix stage are loaded into registers while the current one runs
-// (one workgroup per CU: the whole 512-VGPR file is available). NT: W [N][K]
-// row-major (forward, y = x W^T); NN: W [K][N] (backward, dx = dy W).
-// MFMA step (i, s) covers k = 16 i + 4 kq + s for lane group kq.
+// (one workgroup per CU: the whole 512-VGPR file is available) and split just
+// before use. NT: W [N][K] row-major (forward, y = x W^T); NN: W [K][N] in LDS
+// (backward, dx = dy W). MFMA block i covers k = 32 i + 8 kq .. + 7 for lane
+// group kq.
+// Range: every wave reads the whole A tile (16 rows x K) for its fragments, so
+// it takes the tile's max |A| itself (DPP + readlane, no LDS round trip) and
+// scales A by a power of two into [2^14, 2^15) before the split; W is scaled by
+// 16 (as in k1b). The sums are scaled back exactly. Gradients (multiples of dz)
+// can be arbitrarily small and activations large: neither leaves f16's range.
 constexpr int kWRegs = 64;  // 2 tiles x K/4 (K <= 128)
 struct WReg {
   float v[kWRegs];
@@ -444,56 +458,85 @@ struct WReg {
 // Loads are unconditional: a tile past N reads a clamped (valid) row and its
 // product is discarded by the caller. A load under a lane predicate becomes a
 // branch whose join copies the value, i.e. an s_waitcnt vmcnt(0) right after
-// the load, which serialises the whole prefetch.
-template <int K, int N, bool NT>
+// the load, which serialises the whole prefetch. Layout: v[tt K/4 + 8 i + e] =
+// W[n][32 i + 8 kq + e].
+template <int K, int N>
 __device__ __forceinline__ void load_w(WReg& w, const float* __restrict__ W, int wave, int lane) {
   const int m = lane & 15, kq = lane >> 4;
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt) {
     const int n = min(16 * (wave + 4 * tt) + m, N - 1);
 #pragma unroll
-    for (int i = 0; i < K / 16; ++i) {
-      if (NT) {
-        const f4 q = *reinterpret_cast<const f4*>(W + n * K + 16 * i + 4 * kq);
+    for (int i = 0; i < K / 32; ++i) {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) w.v[tt * (K / 4) + 4 * i + s] = q[s];
-      } else {
+      for (int h = 0; h < 2; ++h) {
+        const f4 q = *reinterpret_cast<const f4*>(W + n * K + 32 * i + 8 * kq + 4 * h);
 #pragma unroll
-        for (int s = 0; s < 4; ++s) w.v[tt * (K / 4) + 4 * i + s] = W[(16 * i + 4 * kq + s) * N + n];
+        for (int s = 0; s < 4; ++s) w.v[tt * (K / 4) + 8 * i + 4 * h + s] = q[s];
       }
     }
   }
 }
 
+// 2^p and 2^-p with max |a| 2^p in [2^14, 2^15) (p clamped to +-100: a zero tile
+// gets 2^100; inf / NaN propagate through the products)
+__device__ __forceinline__ void pow2_scale(float amax, float& s, float& inv) {
+  const int e = (__builtin_bit_cast(int, amax) >> 23) & 255;
+  const int p = max(-100, min(100, 141 - e));
+  s = __builtin_bit_cast(float, (127 + p) << 23);
+  inv = __builtin_bit_cast(float, (127 - p) << 23);
+}
+
+// split-f16 A fragments of a [16][kLd] f32 LDS tile; inv undoes the A scale and
+// the 16 on W
+template <int K>
+struct AFrag {
+  h8 h[K / 32], l[K / 32];
+  float inv;
+};
+template <int K>
+__device__ __forceinline__ AFrag<K> load_a(const float* A, int lane) {
+  const int m = lane & 15, kq = lane >> 4;
+  f4 v[K / 32][2];
+  float mx = 0.f;
+#pragma unroll
+  for (int i = 0; i < K / 32; ++i) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      v[i][h] = *reinterpret_cast<const f4*>(A + m * kLd + 32 * i + 8 * kq + 4 * h);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) mx = fmaxf(mx, fabsf(v[i][h][s]));
+    }
+  }
+  float sc, inv;
+  pow2_scale(wmax(mx), sc, inv);
+  AFrag<K> f;
+  f.inv = inv * (1.f / 16.f);
+#pragma unroll
+  for (int i = 0; i < K / 32; ++i) split8(v[i][0] * sc, v[i][1] * sc, f.h[i], f.l[i]);
+  return f;
+}
+
+// W fragment (8 consecutive k of one column, x16) -> hi / lo
+__device__ __forceinline__ void split_w(const float* v, h8& hi, h8& lo) {
+  split8(f4{v[0], v[1], v[2], v[3]} * 16.f, f4{v[4], v[5], v[6], v[7]} * 16.f, hi, lo);
+}
+
 // two tiles (w, w + 4), two interleaved accumulation chains
 template <int K>
-__device__ __forceinline__ void gemm2(const WReg& w, const float* A, int lane, f4& c0, f4& c1) {
-  const int m = lane & 15, kq = lane >> 4;
+__device__ __forceinline__ void gemm2(const WReg& w, const AFrag<K>& a, f4& c0, f4& c1) {
   c0 = f4{0.f, 0.f, 0.f, 0.f};
   c1 = c0;
 #pragma unroll
-  for (int i = 0; i < K / 16; ++i) {
-    const f4 av = *reinterpret_cast<const f4*>(A + m * kLd + 16 * i + 4 * kq);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      c0 = mma(av[s], w.v[4 * i + s], c0);
-      c1 = mma(av[s], w.v[K / 4 + 4 * i + s], c1);
-    }
+  for (int i = 0; i < K / 32; ++i) {
+    h8 bh0, bl0, bh1, bl1;
+    split_w(&w.v[8 * i], bh0, bl0);
+    split_w(&w.v[K / 4 + 8 * i], bh1, bl1);
+    c0 = mma3(a.h[i], a.l[i], bh0, bl0, c0);
+    c1 = mma3(a.h[i], a.l[i], bh1, bl1, c1);
   }
-}
-
-// one tile (w), two chains over the even / odd 16-k blocks
-template <int K>
-__device__ __forceinline__ f4 gemm1(const WReg& w, const float* A, int lane) {
-  const int m = lane & 15, kq = lane >> 4;
-  f4 c[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-  for (int i = 0; i < K / 16; ++i) {
-    const f4 av = *reinterpret_cast<const f4*>(A + m * kLd + 16 * i + 4 * kq);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) c[i & 1] = mma(av[s], w.v[4 * i + s], c[i & 1]);
-  }
-  return c[0] + c[1];
+  c0 *= a.inv;
+  c1 *= a.inv;
 }
 
 struct K2Args {
@@ -540,37 +583,45 @@ __device__ __forceinline__ void coop_store(float* dst, const f4 (&r)[N], int tid
 #pragma unroll
   for (int u = 0; u < N; ++u) *reinterpret_cast<f4*>(dst + 4 * (tid + 256 * u)) = r[u];
 }
+// NN fragment from an LDS weight matrix W [K][N]: column n, k = 32 i + 8 kq ..
+template <int N>
+__device__ __forceinline__ void lds_w(const float* W, int i, int kq, int n, h8& hi, h8& lo) {
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = W[(32 * i + 8 * kq + e) * N + n];
+  split_w(v, hi, lo);
+}
 // NN product from an LDS weight matrix W [K][N]: tiles w and w + 4 (two chains)
 template <int K, int N>
-__device__ __forceinline__ void gemm2_lds(const float* W, const float* A, int wave, int lane, f4& c0, f4& c1) {
+__device__ __forceinline__ void gemm2_lds(const float* W, const AFrag<K>& a, int wave, int lane, f4& c0, f4& c1) {
   const int m = lane & 15, kq = lane >> 4;
   const int n0 = 16 * wave + m, n1 = min(16 * (wave + 4) + m, N - 1);  // tile w + 4 past N: discarded
   c0 = f4{0.f, 0.f, 0.f, 0.f};
   c1 = c0;
 #pragma unroll
-  for (int i = 0; i < K / 16; ++i) {
-    const f4 av = *reinterpret_cast<const f4*>(A + m * kLd + 16 * i + 4 * kq);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int k = 16 * i + 4 * kq + s;
-      c0 = mma(av[s], W[k * N + n0], c0);
-      c1 = mma(av[s], W[k * N + n1], c1);
-    }
+  for (int i = 0; i < K / 32; ++i) {
+    h8 bh0, bl0, bh1, bl1;
+    lds_w<N>(W, i, kq, n0, bh0, bl0);
+    lds_w<N>(W, i, kq, n1, bh1, bl1);
+    c0 = mma3(a.h[i], a.l[i], bh0, bl0, c0);
+    c1 = mma3(a.h[i], a.l[i], bh1, bl1, c1);
   }
+  c0 *= a.inv;
+  c1 *= a.inv;
 }
-// one tile (w), two chains over the even / odd 16-k blocks
+// one tile (w), two chains over the even / odd k blocks
 template <int K, int N>
-__device__ __forceinline__ f4 gemm1_lds(const float* W, const float* A, int wave, int lane) {
+__device__ __forceinline__ f4 gemm1_lds(const float* W, const AFrag<K>& a, int wave, int lane) {
   const int m = lane & 15, kq = lane >> 4;
   const int n0 = 16 * wave + m;
   f4 c[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-  for (int i = 0; i < K / 16; ++i) {
-    const f4 av = *reinterpret_cast<const f4*>(A + m * kLd + 16 * i + 4 * kq);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) c[i & 1] = mma(av[s], W[(16 * i + 4 * kq + s) * N + n0], c[i & 1]);
+  for (int i = 0; i < K / 32; ++i) {
+    h8 bh, bl;
+    lds_w<N>(W, i, kq, n0, bh, bl);
+    c[i & 1] = mma3(a.h[i], a.l[i], bh, bl, c[i & 1]);
   }
-  return c[0] + c[1];
+  return (c[0] + c[1]) * a.inv;
 }
 
 #ifdef HBK_TRACE
@@ -628,7 +679,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
     if (a.sched) nw_pre = a.sched[2 * min(step, a.sched_len - 1) + 1];
   }
   WReg wa, wb;
-  load_w<kH, kL, true>(wa, P + a.w_o[0], wave, lane);
+  load_w<kH, kL>(wa, P + a.w_o[0], wave, lane);
   {  // small parameters: all loads issued unconditionally, then stored
     const int c2 = tid & (kH2 - 1), c1 = min(tid, kL - 1);
     float vbhg[NG], vbo[NG], vlg[NG], vlb[NG];
@@ -715,10 +766,10 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
 #pragma unroll
   for (int k = 0; k + 1 < NG; ++k) {
     // S_k = U_k W_o_k^T + b_o_k  -> bS   (weights in wa; prefetch HG_{k+1}'s into wb)
-    load_w<kL, kH2, true>(wb, P + a.w_hg[k + 1], wave, lane);
+    load_w<kL, kH2>(wb, P + a.w_hg[k + 1], wave, lane);
     {
       f4 c0, c1;
-      gemm2<kH>(wa, &bU[0][0], lane, c0, c1);
+      gemm2<kH>(wa, load_a<kH>(&bU[0][0], lane), c0, c1);
       const int n0 = 16 * wave + m, n1 = 16 * (wave + 4) + m;
       const float bo0 = sBo[k][n0], bo1 = n1 < kL ? sBo[k][n1] : 0.f;
 #pragma unroll
@@ -734,7 +785,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
     // lane -> row 4w + lane / 16, columns 6 (lane % 16) ..), both reductions of
     // the four rows in parallel within 16-lane DPP rows (rsum16: no cross-row
     // steps); Xn^T goes to HBM from LDS in the next stage
-    if (k + 2 < NG) load_w<kH, kL, true>(wa, P + a.w_o[k + 1], wave, lane);
+    if (k + 2 < NG) load_w<kH, kL>(wa, P + a.w_o[k + 1], wave, lane);
     {
       const int r = wave * 4 + (lane >> 4), c0 = 6 * (lane & 15);
       float v[6];
@@ -759,7 +810,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
     if (kTrain) store_t(a.Xn + (k + 1) * kL * Bp, &bX[0][0], kL);
     {
       f4 ch, cg;
-      gemm2<kL>(wb, &bX[0][0], lane, ch, cg);
+      gemm2<kL>(wb, load_a<kL>(&bX[0][0], lane), ch, cg);
       const int j = 16 * wave + m;
       const float bh = sBhg[k + 1][j], bg = sBhg[k + 1][kH + j];
       f4 uo;
@@ -888,7 +939,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
     if (k - 1 >= 1) coop_load(rX, P + a.w_hg[k - 1], tid);
     {
       f4 c0, c1;
-      gemm2_lds<kH2, kL>(wX, &bX[0][0], wave, lane, c0, c1);
+      gemm2_lds<kH2, kL>(wX, load_a<kH2>(&bX[0][0], lane), wave, lane, c0, c1);
       const int n0 = 16 * wave + m, n1 = 16 * (wave + 4) + m;
 #pragma unroll
       for (int e = 0; e < 4; ++e) bU[4 * kq + e][n0] = c0[e];
@@ -942,7 +993,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
         for (int r = 0; r < kR; ++r) s += bS[r][tid];
         atomicAdd(G + a.b_o[kk] + tid, s);
       }
-      const f4 du = gemm1_lds<kL, kH>(wY, &bS[0][0], wave, lane);
+      const f4 du = gemm1_lds<kL, kH>(wY, load_a<kL>(&bS[0][0], lane), wave, lane);
       const int j = 16 * wave + m;
       f4 dho, dgo;
 #pragma unroll

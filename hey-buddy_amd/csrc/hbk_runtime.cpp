@@ -55,4 +55,19 @@ int hbk_device_count(int* count) {
   return HBK_OK;
 }
 
+int hbk_stream_create_cu_mask(const uint32_t* cu_mask, int n_words, void** stream) {
+  if (!cu_mask || n_words <= 0 || !stream) return hbk::arg_error("cu_mask / n_words / stream");
+  hipStream_t s = nullptr;
+  hipError_t e = hipExtStreamCreateWithCUMask(&s, static_cast<uint32_t>(n_words), cu_mask);
+  if (e != hipSuccess) return hbk::hip_error(e, "hipExtStreamCreateWithCUMask");
+  *stream = s;
+  return HBK_OK;
+}
+
+int hbk_stream_destroy(void* stream) {
+  if (!stream) return hbk::arg_error("stream is NULL");
+  hipError_t e = hipStreamDestroy(static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? HBK_OK : hbk::hip_error(e, "hipStreamDestroy");
+}
+
 }  // extern "C"

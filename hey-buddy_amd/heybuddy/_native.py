@@ -47,6 +47,8 @@ _PROTOS = {
     "hbk_version": (ctypes.c_char_p, []),
     "hbk_last_error": (ctypes.c_char_p, []),
     "hbk_device_count": (_c_int, [ctypes.POINTER(_c_int)]),
+    "hbk_stream_create_cu_mask": (_c_int, [_vp, _c_int, ctypes.POINTER(_vp)]),
+    "hbk_stream_destroy": (_c_int, [_vp]),
     "hbk_mel_plan_create": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int, _c_float, _c_float,
                                      _c_float, _c_float, ctypes.POINTER(_vp)]),
     "hbk_mel_plan_destroy": (_c_int, [_vp]),

@@ -99,6 +99,11 @@ def eq_coefficients(params: np.ndarray, sample_rate: int = 16000) -> np.ndarray:
     return np.stack([b0 / a0, b1 / a0, b2 / a0, a1 / a0, a2 / a0], axis=-1)
 
 
+def _pinned(t: torch.Tensor) -> torch.Tensor:
+    """Page-locked copy for an asynchronous upload (as is on a GPU-less host)."""
+    return t.pin_memory() if torch.cuda.is_available() else t
+
+
 class BatchAugmenter:
     def __init__(self, noise: Optional[Sequence[torch.Tensor]] = None,
                  impulse_responses: Optional[Sequence[torch.Tensor]] = None,
@@ -225,9 +230,11 @@ class BatchAugmenter:
         self._tanh = np.where(t_on, t_amt, np.nan).astype(np.float32)
         return noise_off, spec_idx, gain_db
 
-    def __call__(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """x [n, >= 23040] f32 on the device -> augmented [n, 23040]."""
-        n = x.shape[0]
+    def prepare(self, n: int) -> Dict[str, Any]:
+        """Every host-side draw of one call over n clips (plan_batches, the
+        background SNRs, the colored-noise seed) in the order __call__ makes
+        them, with the EQ filters already in pinned memory: a pipelined caller
+        prepares chunk s + 1 while the device works, then launches."""
         noise_off, spec_idx, gain_db = self.plan_batches(n)
         ring_len = 0 if self.ring is None else self.ring.numel()
         if ring_len:
@@ -237,23 +244,39 @@ class BatchAugmenter:
         if self.p_gain > 0:  # torch_audiomentations convert_decibels_to_amplitude_ratio
             gain = torch.pow(10.0, torch.from_numpy(gain_db) / 20.0)
         eq_idx, eq_coef = self._eq
-        if eq_idx.size:  # per-clip Compose: EQ, then tanh (augmented.py:79-90), in place on out
+        eq = None
+        if eq_idx.size:
+            eq = (_pinned(torch.from_numpy(eq_coef)), _pinned(torch.from_numpy(eq_idx)))
+        tanh = None if np.isnan(self._tanh).all() else torch.from_numpy(self._tanh)
+        colored_snr, colored_fd = self._colored
+        colored = None
+        if not np.isnan(colored_snr).all():
+            colored = (torch.from_numpy(colored_fd), torch.from_numpy(colored_snr), int(np.random.randint(0, 2 ** 62)))
+        return {"n": n, "noise_off": torch.from_numpy(noise_off), "spec_idx": torch.from_numpy(spec_idx),
+                "snr": snr, "gain": gain, "eq": eq, "tanh": tanh, "colored": colored}
+
+    def __call__(self, x: torch.Tensor, out: Optional[torch.Tensor] = None,
+                 prepared: Optional[Dict[str, Any]] = None) -> torch.Tensor:
+        """x [n, >= 23040] f32 on the device -> augmented [n, 23040]."""
+        n = x.shape[0]
+        pr = self.prepare(n) if prepared is None else prepared
+        if pr["n"] != n:
+            raise ValueError(f"prepared for {pr['n']} clips, called with {n}")
+        if pr["eq"] is not None:  # per-clip Compose: EQ, then tanh (augmented.py:79-90), in place on out
             if out is None:
                 out = torch.empty((n, T), dtype=torch.float32, device=x.device)
             if out.data_ptr() != x.data_ptr():
                 out.copy_(x[:, :T])
-            x = seven_band_eq(out, torch.from_numpy(eq_coef), idx=torch.from_numpy(eq_idx))
-        if not np.isnan(self._tanh).all():  # per-clip Compose, before the batch chain (augmented.py:325-328)
-            x = tanh_distortion(x, torch.from_numpy(self._tanh), out=out)
+            x = seven_band_eq(out, pr["eq"][0], idx=pr["eq"][1])
+        if pr["tanh"] is not None:  # per-clip Compose, before the batch chain (augmented.py:325-328)
+            x = tanh_distortion(x, pr["tanh"], out=out)
             out = x
-        colored_snr, colored_fd = self._colored
-        if not np.isnan(colored_snr).all():  # colored noise precedes the gain (augmented.py:107-118)
-            x = self.plan.colored_noise(x, torch.from_numpy(colored_fd), torch.from_numpy(colored_snr),
-                                        seed=int(np.random.randint(0, 2 ** 62)), out=out,
-                                        sample_rate=self.sample_rate)
+        if pr["colored"] is not None:  # colored noise precedes the gain (augmented.py:107-118)
+            fd, csnr, seed = pr["colored"]
+            x = self.plan.colored_noise(x, fd, csnr, seed=seed, out=out, sample_rate=self.sample_rate)
             out = x
-        return self.plan.augment(x, self.ring, torch.from_numpy(noise_off), snr, self.spectra,
-                                 torch.from_numpy(spec_idx), out=out, gain=gain)
+        return self.plan.augment(x, self.ring, pr["noise_off"], pr["snr"], self.spectra, pr["spec_idx"],
+                                 out=out, gain=pr["gain"])
 
 
 # ---------------------------------------------------------------------------
@@ -457,15 +480,22 @@ class AugmentedAudioGenerator:
         placed = self.place_batch(batch)
         return self.augmenter(placed, out=placed)
 
-    def augment_device(self, clips: torch.Tensor, lengths: Optional[Sequence[int]] = None) -> torch.Tensor:
-        """Device-resident form used by the feature generator: clips [n, S] f32
-        on the device (clip i valid in [0, lengths[i])) -> augmented [n, T]."""
-        T = self.target_num_samples
+    def prepare_device(self, clips: torch.Tensor, lengths: Optional[Sequence[int]] = None) -> Dict[str, Any]:
+        """The host-side draws of one augment_device call (placement offsets,
+        then BatchAugmenter.prepare), so that a pipelined caller can make them
+        ahead of the launch."""
         n = clips.shape[0]
         lens = np.full(n, clips.shape[1], dtype=np.int32) if lengths is None else np.asarray(lengths, np.int32)
-        pre = target_length_offsets(lens, T)
-        placed = place_clips(clips, lens, pre, T)  # a fresh buffer: the chain then runs in place
-        return self.augmenter(placed, out=placed)
+        return {"lens": lens, "pre": target_length_offsets(lens, self.target_num_samples),
+                "chain": self.augmenter.prepare(n)}
+
+    def augment_device(self, clips: torch.Tensor, lengths: Optional[Sequence[int]] = None,
+                       prepared: Optional[Dict[str, Any]] = None) -> torch.Tensor:
+        """Device-resident form used by the feature generator: clips [n, S] f32
+        on the device (clip i valid in [0, lengths[i])) -> augmented [n, T]."""
+        pr = self.prepare_device(clips, lengths) if prepared is None else prepared
+        placed = place_clips(clips, pr["lens"], pr["pre"], self.target_num_samples)  # the chain runs in place
+        return self.augmenter(placed, out=placed, prepared=pr["chain"])
 
     def __call__(self, num_samples: int, **kwargs: Any) -> Iterator[Dict[str, Any]]:
         """augmented.py:396-427: yields {"audio": {"array", "sampling_rate"}, ...}."""

@@ -255,6 +255,25 @@ def _replace_nan_rows(emb: torch.Tensor) -> torch.Tensor:
     return torch.from_numpy(host).to(emb.device)
 
 
+def replace_nan_rows_device(emb: torch.Tensor, out: torch.Tensor,
+                            generator: Optional[torch.Generator] = None) -> torch.Tensor:
+    """The NaN replacement of embeddings.py:213-227 with no host
+    synchronisation, for pipelined featurization: every clip (row of emb
+    [n, ...]) holding a NaN takes the embeddings of a uniformly drawn NaN-free
+    clip (device RNG in place of np.random.choice), all zeros when every clip
+    is NaN; the result is gathered into out (same shape, not emb). The
+    reference's warning needs the count on the host and is not emitted here
+    (_replace_nan_rows is the logging form)."""
+    n = emb.shape[0]
+    bad = torch.isnan(emb.reshape(n, -1)).any(dim=1)
+    order = torch.argsort(bad.to(torch.uint8), stable=True)  # NaN-free clips first
+    n_good = n - bad.sum()
+    r = (torch.rand(n, device=emb.device, generator=generator) * n_good).long().clamp_(max=n - 1)
+    src = torch.where(bad, order[r], torch.arange(n, device=emb.device))
+    torch.index_select(emb.reshape(n, -1), 0, src, out=out.view(n, -1))
+    return out.masked_fill_((n_good == 0).reshape([1] * out.dim()), 0.0)
+
+
 def _replace_nan_rows_host(embeddings: np.ndarray) -> Optional[np.ndarray]:
     """Any clip with a NaN gets a random non-NaN clip's embeddings
     (np.random.choice, as embeddings.py:227); None if every clip is NaN."""

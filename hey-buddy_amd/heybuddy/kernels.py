@@ -605,7 +605,7 @@ def seven_band_eq(x: torch.Tensor, coef: torch.Tensor, out: torch.Tensor | None 
         raise ValueError("x rows must be 16-B aligned")
 
     def to_dev(t: torch.Tensor) -> torch.Tensor:
-        return t.pin_memory().to(dev, non_blocking=True) if t.device.type == "cpu" else t.to(dev)
+        return (t if t.is_pinned() else t.pin_memory()).to(dev, non_blocking=True) if t.device.type == "cpu" else t.to(dev)
 
     m = n if idx is None else int(idx.numel())
     coef = to_dev(coef.to(dtype=torch.float64).reshape(m, 7, 5).contiguous())

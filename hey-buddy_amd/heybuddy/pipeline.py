@@ -1,0 +1,102 @@
+"""Overlapping featurization with classifier training on one GPU.
+
+The reference runs the two phases of ``heybuddy train`` one after the other:
+every clip is augmented and featurized first, then the classifier trains on
+the stored features (__main__.py:245-429, features.py:492-535,
+trainer.py:764-1007). On MI355X the train step at the reference's batch of
+1,100 rows is a latency-bound chain that fills a fraction of the 256 CUs
+(k2 runs one workgroup per 16-row tile: 69 workgroups), while featurization is
+throughput work that fills any CU it is given. So the pipelined driver trains
+on chunk s while chunk s + 1 is augmented and featurized beside it, on a
+second stream, with two embedding pools:
+
+  feature stream:  featurize(s + 1) -> pool[(s + 1) % 2]   (waits train(s - 1))
+  train stream:    train(s) on pool[s % 2]                 (waits featurize(s))
+
+The work is the same as the sequential order (every clip featurized once and
+trained on once, the model updated in the same step order); only the
+placement in time changes. How the two streams share the CUs is a policy:
+
+  "prio"       both streams on the whole device, the train stream at high
+               priority (the dispatcher prefers its waiting workgroups);
+  "split:N"    the train stream on N CUs of its own, featurization on the rest
+               (hipExtStreamCreateWithCUMask, hbk_stream_create_cu_mask);
+  "spill:N"    featurization on all but N CUs, the train stream on the whole
+               device at high priority (its wide launches spill into the
+               featurization CUs as their workgroups retire).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Tuple
+
+import torch
+
+__all__ = ["train_cu_set", "cu_mask_words", "masked_stream", "make_streams"]
+
+
+def train_cu_set(n_cu: int, n_train: int, n_xcd: int = 8) -> List[int]:
+    """n_train CU ids spread evenly over the XCDs whether the mask's bit i maps
+    to XCD i // (n_cu / n_xcd) or to XCD i % n_xcd: XCD x takes the k = n_train
+    / n_xcd ids x * per + (floor(j per / k) + x) mod per (per = CUs per XCD)."""
+    per = n_cu // n_xcd
+    k = max(1, min(per, n_train // n_xcd))
+    return sorted(x * per + ((j * per // k + x) % per) for x in range(n_xcd) for j in range(k))
+
+
+def cu_mask_words(cus, n_cu: int) -> List[int]:
+    words = [0] * ((n_cu + 31) // 32)
+    for c in cus:
+        words[c // 32] |= 1 << (c % 32)
+    return words
+
+
+class _MaskedStream:
+    """A hipExtStreamCreateWithCUMask stream wrapped as a torch ExternalStream
+    (destroyed with this object)."""
+
+    def __init__(self, device: torch.device, cus):
+        from . import _native
+        self._lib = _native.lib()
+        n_cu = torch.cuda.get_device_properties(device).multi_processor_count
+        words = cu_mask_words(cus, n_cu)
+        arr = (ctypes.c_uint32 * len(words))(*words)
+        handle = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            _native.check(self._lib.hbk_stream_create_cu_mask(arr, len(words), ctypes.byref(handle)))
+        self.handle = handle
+        self.stream = torch.cuda.ExternalStream(handle.value, device=device)
+        self.cus = list(cus)
+
+    def __del__(self):
+        try:
+            if self.handle:
+                torch.cuda.synchronize()
+                self._lib.hbk_stream_destroy(self.handle)
+        except Exception:
+            pass
+
+
+def masked_stream(device: torch.device, cus) -> "_MaskedStream":
+    return _MaskedStream(device, cus)
+
+
+def make_streams(device: torch.device, policy: str) -> Tuple[torch.cuda.Stream, torch.cuda.Stream, list]:
+    """(feature stream, train stream, keep-alive objects) for a policy string
+    ("prio", "split:N", "spill:N")."""
+    n_cu = torch.cuda.get_device_properties(device).multi_processor_count
+    keep: list = []
+    if policy == "prio":
+        return torch.cuda.Stream(device), torch.cuda.Stream(device, priority=-1), keep
+    kind, _, n = policy.partition(":")
+    n = int(n)
+    if kind not in ("split", "spill") or not 0 < n < n_cu:
+        raise ValueError(f"unknown overlap policy {policy!r}")
+    train = train_cu_set(n_cu, n)
+    feat = masked_stream(device, sorted(set(range(n_cu)) - set(train)))
+    keep.append(feat)
+    if kind == "split":
+        ts = masked_stream(device, train)
+        keep.append(ts)
+        return feat.stream, ts.stream, keep
+    return feat.stream, torch.cuda.Stream(device, priority=-1), keep

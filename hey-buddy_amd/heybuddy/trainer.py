@@ -376,26 +376,41 @@ class WakeWordTrainer(Trainer):
             self._parity ^= 1
             done = 1
         k = max(2, steps_per_graph - steps_per_graph % 2)
-        if graphs and world == 1 and S - done >= k:
-            key = ("indexed", k, self._parity, B, y_stride, float(threshold), float(activation_threshold), float(p),
-                   tuple(t.data_ptr() if t is not None else 0 for t in (idx, y, sched, p32, p16, history, ws)))
+        ptrs = tuple(t.data_ptr() if t is not None else 0 for t in (idx, y, sched, p32, p16, history, ws))
+
+        def graph_of(n: int) -> "torch.cuda.CUDAGraph":
+            """The captured graph of n (even) steps from the current parity."""
+            key = ("indexed", n, self._parity, B, y_stride, float(threshold), float(activation_threshold), float(p),
+                   ptrs)
             entry = self._graphs.get(key)
-            gr = None if entry is None else entry[0]
-            if gr is None:
-                self._evict_graphs()
-                side = torch.cuda.Stream(dev)
-                side.wait_stream(torch.cuda.current_stream(dev))
-                gr = torch.cuda.CUDAGraph()
-                par0 = self._parity
-                with torch.cuda.stream(side):
-                    with torch.cuda.graph(gr, stream=side):
-                        for j in range(k):
-                            one(par0 ^ (j & 1), True)
-                torch.cuda.current_stream(dev).wait_stream(side)
-                self._graphs[key] = (gr, ws)  # the entry keeps the baked-in workspace alive
-            while S - done >= k:
-                gr.replay()
-                done += k
+            if entry is not None:
+                return entry[0]
+            self._evict_graphs()
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            gr = torch.cuda.CUDAGraph()
+            par0 = self._parity
+            with torch.cuda.stream(side):
+                with torch.cuda.graph(gr, stream=side):
+                    for j in range(n):
+                        one(par0 ^ (j & 1), True)
+            torch.cuda.current_stream(dev).wait_stream(side)
+            self._graphs[key] = (gr, ws)  # the entry keeps the baked-in workspace alive
+            return gr
+
+        if graphs and world == 1 and S - done >= 2:
+            # k-step graphs, then one graph for the even remainder: at most one
+            # more eager step (each eager step is ~1 ms of host time, a graph
+            # replay a few us, and the host must stay ahead of the device)
+            if S - done >= k:
+                gr = graph_of(k)
+                while S - done >= k:
+                    gr.replay()
+                    done += k
+            tail = (S - done) - (S - done) % 2
+            if tail >= 2:
+                graph_of(tail).replay()
+                done += tail
         while done < S:
             one(self._parity, True)
             self._parity ^= 1

@@ -36,6 +36,14 @@ const char* hbk_version(void);
 const char* hbk_last_error(void);
 /* Number of HIP devices visible to the library (0 on a GPU-less host). */
 int hbk_device_count(int* count);
+/* A stream whose kernels run only on the compute units set in cu_mask (bit i
+ * of word i / 32 = CU i; n_words 32-bit words; hipExtStreamCreateWithCUMask).
+ * The pipelined train driver (heybuddy.pipeline) gives the latency-bound
+ * classifier step a CU partition of its own while the next chunk of clips is
+ * featurized on the rest; no reference interface (the reference runs the two
+ * phases one after the other, __main__.py:245-429). */
+int hbk_stream_create_cu_mask(const uint32_t* cu_mask, int n_words, void** stream);
+int hbk_stream_destroy(void* stream);
 
 /* ------------------------------------------------------------------------ *
  * Mel spectrogram (STFT -> |.|^2 -> mel filterbank -> 10 log10 -> x/10 + 2)
