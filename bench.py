@@ -1,28 +1,35 @@
 #!/usr/bin/env python
 """bench.py — the BASELINE.json metric on the MI355X hot path.
 
-Metric: audio clips/sec featurized (1.5 s @ 16 kHz synthetic clips), at N GPUs.
+Metric: audio clips/sec featurized+trained (1.5 s @ 16 kHz clips), at N GPUs.
 
-Workloads (BASELINE.json configs; --config, default 2 = configs[1]):
-  2  per rank, 100 k clips resident in HBM are featurized exactly as
-     SpeechEmbeddings.__call__ does (reference embeddings.py:153-234):
+Workloads (BASELINE.json configs; --config, default 5 = the headline):
+  1  configs[0]: the reference's CPU mel-only case (host oracle, no GPU).
+  2  configs[1]: per rank, 100 k clips resident in HBM are featurized exactly
+     as SpeechEmbeddings.__call__ does (reference embeddings.py:153-234):
      STFT + 32-bin log-mel (hbk_mel_frames), the speech-embedding graph on the
      16 reference windows per clip (hbk_embed_clips; SE20 stand-in graph — the
      real ONNX graph is absent offline), NaN-row replacement.
-  3  the same after on-device augmentation (configs[2]): background-noise mix
+  3  configs[2]: the same after on-device augmentation: background-noise mix
      + IR reverb with p forced to 1, one IR per 128-clip batch, and the
      reference's per-batch Gain (p 1.0 by default) (hbk_augment).
-  4  classifier training (configs[3]): stage-1 steps at the reference's global
-     batch of 1,100 embeddings (50 positive / 50 adversarial / 1,000 negative)
-     sampled on the device; metric embeddings/s trained.
-One step = one pass of the hot path over one batch (100 k clips; 1 train step).
+  4  configs[3]: classifier training, the reference's 3-stage schedule at
+     batch 1,100 / 550 / 275 sampled on the device; embeddings/s trained.
+  5  configs[4]: the `heybuddy train` pipeline per rank: placement, the
+     reference's augmentation chain at its default probabilities, mel, embed,
+     then 1,000 train steps on those clips; clips/s featurized AND trained.
+     By default chunk s + 1 is featurized on one stream while chunk s trains
+     on another (heybuddy.pipeline, --overlap split:96); the per-stage
+     rooflines come from untimed sequential steps.
+One step = one pass of the hot path over one batch (100 k clips; for config 4
+one 3-stage run).
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
-torch.distributed.run (one process per GPU, RCCL). Featurization shards the
-clips with no data-path collective ("weak": every rank featurizes its own
-100 k clips); training splits each global batch over the ranks with one
-all-reduce of the gradient bucket per step ("strong"). The timed region is
-bracketed by barrier + synchronize and the max over ranks is reported.
+torch.distributed.run (one process per GPU, RCCL). Clips are sharded with no
+data-path collective ("weak": every rank featurizes its own 100 k clips);
+training runs the reference's batch per rank with one all-reduce of the
+gradient bucket per step. The timed region is bracketed by barrier +
+synchronize and the max over ranks is reported.
 
 rank 0 prints ONE JSON line: the metric, ``roofline`` for the dominant kernel
 (algorithmic work / its average duration, timed live with HIP events on the
@@ -66,9 +73,10 @@ def parse():
                     help="config 3 plus the reference's tanh distortion and colored noise at their default "
                          "probabilities (0.25 each); not the BASELINE configs[2] workload")
     ap.add_argument("--no-check", action="store_true", help="skip the one-off featurize equality check")
-    ap.add_argument("--overlap", default="off",
+    ap.add_argument("--overlap", default="split:96",
                     help="config 5: train chunk s while chunk s + 1 is featurized on a second stream "
-                         "(heybuddy.pipeline policies: off, prio, split:N, spill:N)")
+                         "(heybuddy.pipeline policies: off, prio, split:N, spill:N; N a multiple of 32, "
+                         "i.e. whole CUs of every shader engine of every XCD)")
     ap.add_argument("--stage-steps", type=int, default=2,
                     help="overlapped runs: sequential (untimed) steps that time the stages for the rooflines")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
@@ -664,7 +672,10 @@ def setup_e2e(args, dev, rank, world, seed):
                                "+ 50 adv of the step's clips + 1000 f16 negatives)" % (S, B),
                    "clips_per_rank": n, "train_steps_per_rank": S, "train_batch_per_rank": B,
                    "negative_pool": f"{n_neg} x [16,96] f16",
-                   "parallelism": f"dp{world} (clip shards; 1 all-reduce of the 1,025,700-B bucket per train step)"},
+                   "parallelism": f"dp{world} (clip shards; 1 all-reduce of the 1,025,700-B bucket per train step)",
+                   "schedule": ("sequential: featurize(s) then train(s)" if args.overlap == "off" else
+                                f"pipelined (heybuddy.pipeline {args.overlap}): featurize(s + 1) on one stream while "
+                                f"train(s) runs on another; per-stage ms from {args.stage_steps} sequential steps")},
     }
 
 

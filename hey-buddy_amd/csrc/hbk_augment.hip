@@ -1228,7 +1228,7 @@ int hbk_augment(const hbk_reverb_plan* p, const float* x, int64_t n_clips, int64
   a.thi = p->thi;
   a.tlo = p->tlo;
   a.twn = p->twn;
-  const int64_t blocks = std::min<int64_t>(n_clips, persistent_blocks(1));
+  const int64_t blocks = std::min<int64_t>(n_clips, persistent_blocks(1, stream));
   hipLaunchKernelGGL(augment_kernel, dim3(unsigned(blocks)), dim3(kThreads), kAugLds, as_stream(stream), a);
   HBK_LAUNCH_CHECK("augment_kernel");
   return HBK_OK;
@@ -1263,7 +1263,7 @@ int hbk_colored_noise(const hbk_reverb_plan* p, const float* x, int64_t n_clips,
   a.thi = p->thi8;
   a.tlo = p->tlo8;
   a.twn = p->twn16;
-  const int64_t blocks = std::min<int64_t>(n_clips, persistent_blocks(1));
+  const int64_t blocks = std::min<int64_t>(n_clips, persistent_blocks(1, stream));
   hipLaunchKernelGGL(colored_noise_kernel, dim3(unsigned(blocks)), dim3(kThreads), kColoredLds, as_stream(stream), a);
   HBK_LAUNCH_CHECK("colored_noise_kernel");
   return HBK_OK;
@@ -1300,7 +1300,7 @@ int hbk_tanh_distortion(const float* x, int64_t n_clips, int64_t x_stride, const
   a.out_stride = out_stride;
   a.n_clips = n_clips;
   a.amount = amount;
-  const int64_t blocks = std::min<int64_t>(n_clips, persistent_blocks(2));
+  const int64_t blocks = std::min<int64_t>(n_clips, persistent_blocks(2, stream));
   hipLaunchKernelGGL(tanh_distortion_kernel, dim3(unsigned(blocks)), dim3(kThreads), 0, as_stream(stream), a);
   HBK_LAUNCH_CHECK("tanh_distortion_kernel");
   return HBK_OK;

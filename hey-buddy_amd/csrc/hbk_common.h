@@ -36,8 +36,11 @@ int hip_error(hipError_t e, const char* where);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
-// Grid size for a persistent (grid-stride) kernel on the current device.
-int64_t persistent_blocks(int blocks_per_cu);
+// Grid of a persistent (grid-stride) kernel: blocks_per_cu x the CUs the
+// stream may use (its CU mask when created by hbk_stream_create_cu_mask, else
+// the device's): a grid sized for more CUs than the stream owns leaves a tail
+// wave of workgroups running alone.
+int64_t persistent_blocks(int blocks_per_cu, const void* stream);
 
 // ---------------------------------------------------------------- device ----
 // Complex float as a 2-lane vector so adds / multiplies lower to the packed

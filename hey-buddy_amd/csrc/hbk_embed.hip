@@ -2137,7 +2137,7 @@ int run_program(const Program& prog, const float* in, int64_t n_units, int64_t i
                              !(reinterpret_cast<uintptr_t>(pa.out) & 15);
         if (aligned && pa.n_img * pa.n_bands < (int64_t(1) << 31)) {
           const int64_t tasks = pa.n_img * pa.n_bands;
-          const int64_t blocks = std::min<int64_t>(tasks, persistent_blocks(c.p0_blocks_per_cu));
+          const int64_t blocks = std::min<int64_t>(tasks, persistent_blocks(c.p0_blocks_per_cu, stream));
           if (blocks <= 0) continue;
           hipLaunchKernelGGL(c.p0fn, dim3(unsigned(blocks)), dim3(kP0Threads), c.p0_lds, stream, pa);
           HBK_LAUNCH_CHECK("p0_chain_kernel");
@@ -2154,7 +2154,7 @@ int run_program(const Program& prog, const float* in, int64_t n_units, int64_t i
                              !(reinterpret_cast<uintptr_t>(pa.out) & 15);
         if (aligned && pa.n_img * pa.n_bands < (int64_t(1) << 31)) {
           const int64_t tasks = pa.n_img * pa.n_bands;
-          const int64_t blocks = std::min<int64_t>(tasks, persistent_blocks(c.p0_blocks_per_cu));
+          const int64_t blocks = std::min<int64_t>(tasks, persistent_blocks(c.p0_blocks_per_cu, stream));
           if (blocks <= 0) continue;
           hipLaunchKernelGGL(c.p1fn, dim3(unsigned(blocks)), dim3(kP0Threads), c.p0_lds, stream, pa);
           HBK_LAUNCH_CHECK("p1_chain_kernel");
@@ -2176,7 +2176,7 @@ int run_program(const Program& prog, const float* in, int64_t n_units, int64_t i
         x.n_img = nu * imgs_per_unit[k];
         const int64_t tasks = ((x.n_img + x.G - 1) / x.G) * x.n_bands;
         const int per_cu = std::max<int>(1, std::min<int>(4, int((160 * 1024) / std::max<size_t>(c.lds_bytes, 1))));
-        const int64_t blocks = std::min<int64_t>(tasks, persistent_blocks(per_cu));
+        const int64_t blocks = std::min<int64_t>(tasks, persistent_blocks(per_cu, stream));
         if (blocks <= 0) continue;
         hipLaunchKernelGGL(c.xfn, dim3(unsigned(blocks)), dim3(kXThreads), c.lds_bytes, stream, x);
         HBK_LAUNCH_CHECK("conv_chain_x3_kernel");
@@ -2192,7 +2192,7 @@ int run_program(const Program& prog, const float* in, int64_t n_units, int64_t i
       a.out = c.dst_buf < 0 ? out + u0 * out_unit_floats : bufs[c.dst_buf];
       a.n_img = nu * imgs_per_unit[k];
       const int64_t tasks = ((a.n_img + a.G - 1) / a.G) * a.n_bands;
-      const int64_t blocks = std::min<int64_t>(tasks, persistent_blocks(2));
+      const int64_t blocks = std::min<int64_t>(tasks, persistent_blocks(2, stream));
       if (blocks <= 0) continue;
       hipLaunchKernelGGL(c.fn, dim3(unsigned(blocks)), dim3(kThreads), c.lds_bytes, stream, a);
       HBK_LAUNCH_CHECK("conv_chain_kernel");

@@ -660,7 +660,7 @@ int hbk_mel_frames(const hbk_mel_plan* plan, const float* pcm, int64_t n_clips, 
     a.log_floor = plan->log_floor;
     a.out_scale = 10.f / plan->out_div;
     a.out_add = plan->out_add;
-    const int64_t blocks = std::min<int64_t>(groups2, persistent_blocks(kBlocksPerCU2));
+    const int64_t blocks = std::min<int64_t>(groups2, persistent_blocks(kBlocksPerCU2, stream));
     if (plan->edge0)
       hipLaunchKernelGGL(HBK_MEL_V2(true), dim3(static_cast<unsigned>(blocks)), dim3(kThreads2), 0,
                          as_stream(stream), a);
@@ -690,7 +690,7 @@ int hbk_mel_frames(const hbk_mel_plan* plan, const float* pcm, int64_t n_clips, 
   a.log_floor = plan->log_floor;
   a.out_div = plan->out_div;
   a.out_add = plan->out_add;
-  const int64_t blocks = std::min<int64_t>(groups, persistent_blocks(kBlocksPerCU));
+  const int64_t blocks = std::min<int64_t>(groups, persistent_blocks(kBlocksPerCU, stream));
   hipLaunchKernelGGL(mel_frames_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kThreads), 0,
                      as_stream(stream), a);
   HBK_LAUNCH_CHECK("mel_frames_kernel");

@@ -19,7 +19,7 @@ int hip_error(hipError_t e, const char* where) {
   return HBK_ERR_HIP;
 }
 
-int64_t persistent_blocks(int blocks_per_cu) {
+int64_t persistent_blocks(int blocks_per_cu, const void* stream) {
   static thread_local int cached_dev = -1;
   static thread_local int cached_cus = 256;
   int dev = 0;
@@ -30,7 +30,18 @@ int64_t persistent_blocks(int blocks_per_cu) {
       cached_cus = cus;
     cached_dev = dev;
   }
-  return int64_t(cached_cus) * blocks_per_cu;
+  int cus = cached_cus;
+  if (stream) {
+    uint32_t mask[32] = {};
+    if (hipExtStreamGetCUMask(static_cast<hipStream_t>(const_cast<void*>(stream)), 32, mask) == hipSuccess) {
+      int n = 0;
+      for (uint32_t w : mask) n += __builtin_popcount(w);
+      if (n > 0 && n < cus) cus = n;
+    } else {
+      (void)hipGetLastError();
+    }
+  }
+  return int64_t(cus) * blocks_per_cu;
 }
 
 }  // namespace hbk
