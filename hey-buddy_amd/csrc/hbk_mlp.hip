@@ -691,7 +691,8 @@ int hbk_mlp_step_fwd_bwd(const hbk_mlp_plan* p, const float* params, const float
   if (ws_bytes < mlp_fused_ws_floats(*p, batch) * int64_t(sizeof(float))) return arg_error("workspace too small");
   if (n32 < 0 || n16 < 0) return arg_error("negative pool size");
   if (!idx && n32 < batch) return arg_error("idx NULL: pool32 must hold the batch rows");
-  if (flags & ~(HBK_STEP_XHAT_READY | HBK_STEP_PREFETCH_NEXT)) return arg_error("unknown flags");
+  if (flags & ~(HBK_STEP_XHAT_READY | HBK_STEP_PREFETCH_NEXT | HBK_STEP_WEIGHTS_READY))
+    return arg_error("unknown flags");
   if (!pool32 && !pool16) return arg_error("no embedding pool");
   return mlp_fused_run(*p, params, pool32, n32, pool16, n16, idx, idx_step_stride, idx_steps, y, y_step_stride,
                        static_cast<int>(batch), state, parity, sched,
@@ -702,15 +703,18 @@ int hbk_mlp_step_fwd_bwd(const hbk_mlp_plan* p, const float* params, const float
 
 int hbk_mlp_step_update(const hbk_mlp_plan* p, float* params, float* bucket, float* m, float* v, float* state,
                         int32_t parity, const float* sched, int64_t sched_len, float lr, float beta1, float beta2,
-                        float eps, float* history, int32_t history_cap, void* stream) {
+                        float eps, float* history, int32_t history_cap, void* workspace, int64_t ws_bytes,
+                        void* stream) {
   using namespace hbk;
   if (!p) return arg_error("plan is NULL");
   if (!params || !bucket || !m || !v || !state) return arg_error("NULL pointer");
   if (parity != 0 && parity != 1) return arg_error("parity must be 0 or 1");
   if (sched && sched_len <= 0) return arg_error("sched_len must be > 0");
+  if (workspace && (!mlp_fused_supported(*p) || ws_bytes < mlp_fused_ws_floats(*p, 1) * int64_t(sizeof(float))))
+    return arg_error("workspace: fused plans only, and at least the weight cache");
   return mlp_fused_update(*p, params, bucket, m, v, state, parity, sched,
                           static_cast<int>(std::min<int64_t>(sched_len, 1 << 30)), lr, beta1, beta2, eps, history,
-                          history ? history_cap : 0, as_stream(stream));
+                          history ? history_cap : 0, static_cast<float*>(workspace), as_stream(stream));
 }
 
 }  // extern "C"

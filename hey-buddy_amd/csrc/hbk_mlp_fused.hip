@@ -291,8 +291,8 @@ __global__ void __launch_bounds__(256) k1a_kernel(K1aArgs a, int next) {
   HBK_MT(0, 2);
 }
 
-// Split-f16 products on v_mfma_f32_16x16x32_f16: v = hi + lo with hi = v
-// rounded toward zero to f16 and lo = f16(v - hi) (v - hi is exact in f32), so
+// Split-f16 products on v_mfma_f32_16x16x32_f16: v = hi + lo with hi = f16(v)
+// and lo = f16(v - hi) (v - hi is exact in f32), so
 // a . b ~ hi_a hi_b + hi_a lo_b + lo_a hi_b: three f16 MFMAs (16 cycles each
 // per 16x16x32) for the 8 f32 MFMAs (32 cycles each) of the same 32-deep
 // product. hi is rounded to nearest (v_cvt_pk_f16_f32), so |lo| <= 2^-11 |x|
@@ -450,30 +450,27 @@ __global__ void __launch_bounds__(256) k1b_kernel(K1bArgs a) {
 // scales A by a power of two into [2^14, 2^15) before the split; W is scaled by
 // 16 (as in k1b). The sums are scaled back exactly. Gradients (multiples of dz)
 // can be arbitrarily small and activations large: neither leaves f16's range.
-constexpr int kWRegs = 64;  // 2 tiles x K/4 (K <= 128)
-struct WReg {
-  float v[kWRegs];
+// Weight fragments come pre-split from the step's weight cache (WSplit below:
+// f16 hi / lo planes of 16 W, written by k4 with every update): T tiles of a
+// [N][K] matrix (k contiguous), lane (n, kq) of block i holding k = 32 i + 8 kq
+// .. + 7 of row n. Loads are unconditional: a tile past N reads a clamped
+// (valid) row and its product is discarded by the caller. A load under a lane
+// predicate becomes a branch whose join copies the value, i.e. an s_waitcnt
+// vmcnt(0) right after the load, which serialises the whole prefetch.
+template <int K, int T>
+struct WFrag {
+  h8 h[T][K / 32], l[T][K / 32];
 };
-
-// Loads are unconditional: a tile past N reads a clamped (valid) row and its
-// product is discarded by the caller. A load under a lane predicate becomes a
-// branch whose join copies the value, i.e. an s_waitcnt vmcnt(0) right after
-// the load, which serialises the whole prefetch. Layout: v[tt K/4 + 8 i + e] =
-// W[n][32 i + 8 kq + e].
-template <int K, int N>
-__device__ __forceinline__ void load_w(WReg& w, const float* __restrict__ W, int wave, int lane) {
+template <int K, int N, int T>
+__device__ __forceinline__ void load_wf(WFrag<K, T>& w, const _Float16* __restrict__ hi, int wave, int lane) {
   const int m = lane & 15, kq = lane >> 4;
 #pragma unroll
-  for (int tt = 0; tt < 2; ++tt) {
+  for (int tt = 0; tt < T; ++tt) {
     const int n = min(16 * (wave + 4 * tt) + m, N - 1);
 #pragma unroll
     for (int i = 0; i < K / 32; ++i) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const f4 q = *reinterpret_cast<const f4*>(W + n * K + 32 * i + 8 * kq + 4 * h);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) w.v[tt * (K / 4) + 8 * i + 4 * h + s] = q[s];
-      }
+      w.h[tt][i] = *reinterpret_cast<const h8*>(hi + n * K + 32 * i + 8 * kq);
+      w.l[tt][i] = *reinterpret_cast<const h8*>(hi + N * K + n * K + 32 * i + 8 * kq);
     }
   }
 }
@@ -517,26 +514,82 @@ __device__ __forceinline__ AFrag<K> load_a(const float* A, int lane) {
   return f;
 }
 
-// W fragment (8 consecutive k of one column, x16) -> hi / lo
-__device__ __forceinline__ void split_w(const float* v, h8& hi, h8& lo) {
-  split8(f4{v[0], v[1], v[2], v[3]} * 16.f, f4{v[4], v[5], v[6], v[7]} * 16.f, hi, lo);
-}
-
 // two tiles (w, w + 4), two interleaved accumulation chains
 template <int K>
-__device__ __forceinline__ void gemm2(const WReg& w, const AFrag<K>& a, f4& c0, f4& c1) {
+__device__ __forceinline__ void gemm2(const WFrag<K, 2>& w, const AFrag<K>& a, f4& c0, f4& c1) {
   c0 = f4{0.f, 0.f, 0.f, 0.f};
   c1 = c0;
 #pragma unroll
   for (int i = 0; i < K / 32; ++i) {
-    h8 bh0, bl0, bh1, bl1;
-    split_w(&w.v[8 * i], bh0, bl0);
-    split_w(&w.v[K / 4 + 8 * i], bh1, bl1);
-    c0 = mma3(a.h[i], a.l[i], bh0, bl0, c0);
-    c1 = mma3(a.h[i], a.l[i], bh1, bl1, c1);
+    c0 = mma3(a.h[i], a.l[i], w.h[0][i], w.l[0][i], c0);
+    c1 = mma3(a.h[i], a.l[i], w.h[1][i], w.l[1][i], c1);
   }
   c0 *= a.inv;
   c1 *= a.inv;
+}
+// one tile (w), two chains over the even / odd k blocks
+template <int K>
+__device__ __forceinline__ f4 gemm1(const WFrag<K, 1>& w, const AFrag<K>& a) {
+  f4 c[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int i = 0; i < K / 32; ++i) c[i & 1] = mma3(a.h[i], a.l[i], w.h[0][i], w.l[0][i], c[i & 1]);
+  return (c[0] + c[1]) * a.inv;
+}
+
+// The step's weight cache: the matrices k2 multiplies by (W_o_k, k < NG - 1:
+// [96][64]; W_hg_k, k >= 1: [128][96]) as f16 hi / lo planes of 16 W, each
+// twice: as stored ([N][K], the forward's NT operand) and transposed (the
+// backward's NN operand dx = dy W, again with k contiguous). Segment s at
+// halves dst: hi [R][C], lo [R][C], hi^T [C][R], lo^T [C][R]. Written from the
+// parameters by k0_wsplit (a step whose predecessor did not run k4 on this
+// workspace) and by k4 with every update, so k2 reads its fragments with no
+// conversion (the split of the f32 weights used to cost each of the ~70
+// workgroups ~700 VALU cycles per matrix stage).
+constexpr int kMaxSeg = 2 * kMaxG;
+struct WSeg {
+  int64_t src;  // float offset of the matrix in the parameters
+  int rows, cols;
+  int64_t dst;  // halves from the cache base
+  int64_t q0;   // first float4 of the segment in the k0 grid
+};
+struct WSplit {
+  int n;
+  WSeg s[kMaxSeg];
+};
+__device__ __forceinline__ void wsplit_store4(const WSplit& w, _Float16* __restrict__ base, int64_t i4, f4 p) {
+#pragma unroll
+  for (int sg = 0; sg < kMaxSeg; ++sg) {
+    if (sg >= w.n) break;
+    const WSeg g = w.s[sg];
+    const int64_t rc = int64_t(g.rows) * g.cols, off = i4 - g.src;
+    if (off < 0 || off >= rc) continue;
+    uint32_t h[2], l[2];
+    split_pair(16.f * p[0], 16.f * p[1], h[0], l[0]);
+    split_pair(16.f * p[2], 16.f * p[3], h[1], l[1]);
+    _Float16* d = base + g.dst;
+    *reinterpret_cast<uint2*>(d + off) = uint2{h[0], h[1]};
+    *reinterpret_cast<uint2*>(d + rc + off) = uint2{l[0], l[1]};
+    const int r = static_cast<int>(off / g.cols), c = static_cast<int>(off - int64_t(r) * g.cols);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t he = (e & 1) ? h[e >> 1] >> 16 : h[e >> 1] & 0xFFFFu;
+      const uint32_t le = (e & 1) ? l[e >> 1] >> 16 : l[e >> 1] & 0xFFFFu;
+      d[2 * rc + int64_t(c + e) * g.rows + r] = __builtin_bit_cast(_Float16, static_cast<uint16_t>(he));
+      d[3 * rc + int64_t(c + e) * g.rows + r] = __builtin_bit_cast(_Float16, static_cast<uint16_t>(le));
+    }
+  }
+}
+// k0: the cache from the parameters (grid-stride over the segments' float4s)
+__global__ void __launch_bounds__(256) k0_wsplit_kernel(WSplit w, const float* __restrict__ P,
+                                                         _Float16* __restrict__ base, int64_t n4) {
+  for (int64_t q = blockIdx.x * int64_t(256) + threadIdx.x; q < n4; q += int64_t(gridDim.x) * 256) {
+    int sg = 0;
+#pragma unroll
+    for (int t = 1; t < kMaxSeg; ++t)
+      if (t < w.n && q >= w.s[t].q0) sg = t;
+    const int64_t i4 = w.s[sg].src + 4 * (q - w.s[sg].q0);
+    wsplit_store4(w, base, i4, *reinterpret_cast<const f4*>(P + i4));
+  }
 }
 
 struct K2Args {
@@ -566,63 +619,10 @@ struct K2Args {
   // workgroups n_rt .. 2 n_rt - 1 (when prefetch): k1a of the NEXT step
   int n_rt, prefetch;
   K1aArgs pre;
+  // weight cache (WSplit): hi planes of W_o_k / W_hg_k as stored and transposed
+  const _Float16* wc;
+  int64_t c_o[kMaxG], c_hg[kMaxG], c_oT[kMaxG], c_hgT[kMaxG];
 };
-
-// Backward weights go through LDS: W_hg [128][96] and W_o [96][64] are read
-// there as NN B fragments (dx = dy W: one scalar per lane per MFMA, 16 lanes of a
-// k-group on consecutive columns); they are loaded cooperatively with coalesced
-// float4 loads two stages ahead and written to LDS one stage ahead of use.
-constexpr int kWX = kH2 * kL, kWY = kL * kH;  // 12,288 and 6,144 floats
-template <int N>
-__device__ __forceinline__ void coop_load(f4 (&r)[N], const float* __restrict__ src, int tid) {
-#pragma unroll
-  for (int u = 0; u < N; ++u) r[u] = *reinterpret_cast<const f4*>(src + 4 * (tid + 256 * u));
-}
-template <int N>
-__device__ __forceinline__ void coop_store(float* dst, const f4 (&r)[N], int tid) {
-#pragma unroll
-  for (int u = 0; u < N; ++u) *reinterpret_cast<f4*>(dst + 4 * (tid + 256 * u)) = r[u];
-}
-// NN fragment from an LDS weight matrix W [K][N]: column n, k = 32 i + 8 kq ..
-template <int N>
-__device__ __forceinline__ void lds_w(const float* W, int i, int kq, int n, h8& hi, h8& lo) {
-  float v[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) v[e] = W[(32 * i + 8 * kq + e) * N + n];
-  split_w(v, hi, lo);
-}
-// NN product from an LDS weight matrix W [K][N]: tiles w and w + 4 (two chains)
-template <int K, int N>
-__device__ __forceinline__ void gemm2_lds(const float* W, const AFrag<K>& a, int wave, int lane, f4& c0, f4& c1) {
-  const int m = lane & 15, kq = lane >> 4;
-  const int n0 = 16 * wave + m, n1 = min(16 * (wave + 4) + m, N - 1);  // tile w + 4 past N: discarded
-  c0 = f4{0.f, 0.f, 0.f, 0.f};
-  c1 = c0;
-#pragma unroll
-  for (int i = 0; i < K / 32; ++i) {
-    h8 bh0, bl0, bh1, bl1;
-    lds_w<N>(W, i, kq, n0, bh0, bl0);
-    lds_w<N>(W, i, kq, n1, bh1, bl1);
-    c0 = mma3(a.h[i], a.l[i], bh0, bl0, c0);
-    c1 = mma3(a.h[i], a.l[i], bh1, bl1, c1);
-  }
-  c0 *= a.inv;
-  c1 *= a.inv;
-}
-// one tile (w), two chains over the even / odd k blocks
-template <int K, int N>
-__device__ __forceinline__ f4 gemm1_lds(const float* W, const AFrag<K>& a, int wave, int lane) {
-  const int m = lane & 15, kq = lane >> 4;
-  const int n0 = 16 * wave + m;
-  f4 c[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-  for (int i = 0; i < K / 32; ++i) {
-    h8 bh, bl;
-    lds_w<N>(W, i, kq, n0, bh, bl);
-    c[i & 1] = mma3(a.h[i], a.l[i], bh, bl, c[i & 1]);
-  }
-  return (c[0] + c[1]) * a.inv;
-}
 
 #ifdef HBK_TRACE
 #define K2_MARK(id)                                                                \
@@ -641,17 +641,19 @@ __device__ __forceinline__ f4 gemm1_lds(const float* W, const AFrag<K>& a, int w
 // straight-line code, so the register prefetches and their waits are exact.
 template <bool kTrain, int NG>
 __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
-  __shared__ __attribute__((aligned(16))) float hgS[NG][kR][kLd];
+  // hgS, or the k1a slab of a prefetch workgroup (<= 80 KB in all: two
+  // workgroups per CU, so the 2 n_rt-workgroup launch fits n_rt CUs)
+  constexpr int kHgF = NG * kR * kLd > kR * kSlabLd ? NG * kR * kLd : kR * kSlabLd;
+  __shared__ __attribute__((aligned(16))) float hgRaw[kHgF];
+  float (*hgS)[kR][kLd] = reinterpret_cast<float (*)[kR][kLd]>(hgRaw);
   __shared__ __attribute__((aligned(16))) float xhS[NG - 1][kR][kL + 4];
   __shared__ __attribute__((aligned(16))) float bX[kR][kLd];   // LN output (forward) / dHG (backward)
   __shared__ __attribute__((aligned(16))) float bU[kR][kLd];   // gate output (forward) / dXn (backward)
   __shared__ __attribute__((aligned(16))) float bS[kR][kLd];   // GMLP output (forward) / dS (backward)
-  __shared__ __attribute__((aligned(16))) float wX[kTrain ? kWX : 4];  // backward W_hg_k
-  __shared__ __attribute__((aligned(16))) float wY[kTrain ? kWY : 4];  // backward W_o_k
   __shared__ float rsS[NG][kR];
   __shared__ float zS[kR], dzS[kR];
   __shared__ float red[kStats];
-  __shared__ float sBo[NG][kL], sBhg[NG][kH2], sLg[NG][kL], sLb[NG][kL], sWo[kH];
+  __shared__ float sBhg[NG][kH2], sWo[kH];
 #ifdef HBK_TRACE
   __shared__ unsigned long long trS[4][48];
   int trn = 0;
@@ -659,7 +661,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
   if (kTrain && static_cast<int>(blockIdx.x) >= a.n_rt) {  // next step's k1a (weights not needed)
     const int step = step_of(a.pre.state, a.pre.parity) + 1;
     if (step < a.pre.idx_steps)
-      k1a_tile<true>(a.pre, blockIdx.x - a.n_rt, step, a.pre.xhat[a.pre.parity ^ 1], wX);
+      k1a_tile<true>(a.pre, blockIdx.x - a.n_rt, step, a.pre.xhat[a.pre.parity ^ 1], hgRaw);
     return;
   }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -678,28 +680,32 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
     y_pre = a.y[static_cast<int64_t>(step) * a.y_stride + min(r0 + (tid & 15), a.B - 1)];
     if (a.sched) nw_pre = a.sched[2 * min(step, a.sched_len - 1) + 1];
   }
-  WReg wa, wb;
-  load_w<kH, kL>(wa, P + a.w_o[0], wave, lane);
-  {  // small parameters: all loads issued unconditionally, then stored
-    const int c2 = tid & (kH2 - 1), c1 = min(tid, kL - 1);
-    float vbhg[NG], vbo[NG], vlg[NG], vlb[NG];
+  WFrag<kH, 2> wa;
+  WFrag<kL, 2> wb;
+  load_wf<kH, kL, 2>(wa, a.wc + a.c_o[0], wave, lane);
+  // small parameters, all loads issued unconditionally: the HG biases and the
+  // output weights to LDS; this lane's output biases (columns n0, n1 of the
+  // S GEMMs) and LayerNorm gamma / beta (columns c0 .. c0 + 5) to registers
+  const int lc0 = 6 * (lane & 15);
+  float bo0[NG], bo1[NG], lg[NG][6], lb[NG][6];
+  {
+    const int c2 = tid & (kH2 - 1);
+    float vbhg[NG];
 #pragma unroll
     for (int k = 0; k < NG; ++k) {
       vbhg[k] = P[a.b_hg[k] + c2];
-      vbo[k] = P[a.b_o[k] + (k + 1 < NG ? c1 : 0)];
-      vlg[k] = k + 1 < NG ? P[a.ln_g[k] + c1] : 0.f;
-      vlb[k] = k + 1 < NG ? P[a.ln_b[k] + c1] : 0.f;
+      bo0[k] = P[a.b_o[k] + (k + 1 < NG ? 16 * wave + m : 0)];
+      bo1[k] = P[a.b_o[k] + (k + 1 < NG ? min(16 * (wave + 4) + m, kL - 1) : 0)];
+#pragma unroll
+      for (int e = 0; e < 6; ++e) {
+        lg[k][e] = k + 1 < NG ? P[a.ln_g[k] + lc0 + e] : 0.f;
+        lb[k][e] = k + 1 < NG ? P[a.ln_b[k] + lc0 + e] : 0.f;
+      }
     }
     const float vwo = P[a.w_o[NG - 1] + (tid & (kH - 1))];
 #pragma unroll
-    for (int k = 0; k < NG; ++k) {
+    for (int k = 0; k < NG; ++k)
       if (tid < kH2) sBhg[k][tid] = vbhg[k];
-      if (tid < (k + 1 < NG ? kL : 1)) sBo[k][tid] = vbo[k];
-      if (k + 1 < NG && tid < kL) {
-        sLg[k][tid] = vlg[k];
-        sLb[k][tid] = vlb[k];
-      }
-    }
     if (tid < kH) sWo[tid] = vwo;
   }
   // HG0 = sum of k1b's KS partial slabs + bias; U0 = silu(H) G. Thread ->
@@ -766,17 +772,17 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
 #pragma unroll
   for (int k = 0; k + 1 < NG; ++k) {
     // S_k = U_k W_o_k^T + b_o_k  -> bS   (weights in wa; prefetch HG_{k+1}'s into wb)
-    load_w<kL, kH2>(wb, P + a.w_hg[k + 1], wave, lane);
+    load_wf<kL, kH2, 2>(wb, a.wc + a.c_hg[k + 1], wave, lane);
     {
       f4 c0, c1;
       gemm2<kH>(wa, load_a<kH>(&bU[0][0], lane), c0, c1);
       const int n0 = 16 * wave + m, n1 = 16 * (wave + 4) + m;
-      const float bo0 = sBo[k][n0], bo1 = n1 < kL ? sBo[k][n1] : 0.f;
+      const float bo0_ = bo0[k], bo1_ = bo1[k];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) bS[4 * kq + e][n0] = c0[e] + bo0;
+      for (int e = 0; e < 4; ++e) bS[4 * kq + e][n0] = c0[e] + bo0_;
       if (n1 < kL) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) bS[4 * kq + e][n1] = c1[e] + bo1;
+        for (int e = 0; e < 4; ++e) bS[4 * kq + e][n1] = c1[e] + bo1_;
       }
     }
     __syncthreads();
@@ -785,7 +791,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
     // lane -> row 4w + lane / 16, columns 6 (lane % 16) ..), both reductions of
     // the four rows in parallel within 16-lane DPP rows (rsum16: no cross-row
     // steps); Xn^T goes to HBM from LDS in the next stage
-    if (k + 2 < NG) load_w<kH, kL>(wa, P + a.w_o[k + 1], wave, lane);
+    if (k + 2 < NG) load_wf<kH, kL, 2>(wa, a.wc + a.c_o[k + 1], wave, lane);
     {
       const int r = wave * 4 + (lane >> 4), c0 = 6 * (lane & 15);
       float v[6];
@@ -800,7 +806,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
       for (int e = 0; e < 6; ++e) {
         const float x = (v[e] - mu) * rs;
         xhS[k][r][c0 + e] = x;
-        bX[r][c0 + e] = x * sLg[k][c0 + e] + sLb[k][c0 + e];
+        bX[r][c0 + e] = x * lg[k][e] + lb[k][e];
       }
       if ((lane & 15) == 0) rsS[k][r] = rs;
     }
@@ -829,15 +835,17 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
     __syncthreads();
     K2_MARK(30 + k);
   }
-  // backward weights of the first two backward matrix stages: W_hg_{NG-1}, W_o_{NG-2}
-  f4 rX[kWX / 1024], rY[kWY / 1024];
+  // backward weight fragments of the first two backward matrix stages (from
+  // the transposed cache): W_hg_{NG-1}, W_o_{NG-2}
+  WFrag<kH2, 2> fx;
+  WFrag<kL, 1> fy;
   if (kTrain) {
-    coop_load(rX, P + a.w_hg[NG - 1], tid);
-    coop_load(rY, P + a.w_o[NG - 2], tid);
+    load_wf<kH2, kL, 2>(fx, a.wc + a.c_hgT[NG - 1], wave, lane);
+    load_wf<kL, kH, 1>(fy, a.wc + a.c_oT[NG - 2], wave, lane);
   }
   // output unit: z = U . w_o + b_o (wave w -> rows 4w..4w+3)
   {
-    const float bo = sBo[NG - 1][0];
+    const float bo = bo0[NG - 1];
     const float wl = sWo[lane];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -890,9 +898,6 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
     }
   }
   if constexpr (!kTrain) return;
-  // write the first backward weights (their loads overlapped z and the loss)
-  coop_store(wX, rX, tid);
-  coop_store(wY, rY, tid);
   __syncthreads();
   K2_MARK(41);
   if (tid < kStats && red[tid] != 0.f) atomicAdd(a.stats + tid, red[tid]);
@@ -934,12 +939,11 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
       for (int r = 0; r < kR; ++r) s += bX[r][tid];
       atomicAdd(G + a.b_hg[k] + tid, s);
     }
-    // dXn = dHG_k W_hg_k (NN: K 128 -> N 96, W in wX) -> bU
-    if (k < NG - 1) coop_store(wY, rY, tid);    // W_o_{k-1} (wY is free: dU_k is done)
-    if (k - 1 >= 1) coop_load(rX, P + a.w_hg[k - 1], tid);
+    // dXn = dHG_k W_hg_k (NN: K 128 -> N 96, fragments fx) -> bU; then W_hg_{k-1}'s
     {
       f4 c0, c1;
-      gemm2_lds<kH2, kL>(wX, load_a<kH2>(&bX[0][0], lane), wave, lane, c0, c1);
+      gemm2<kH2>(fx, load_a<kH2>(&bX[0][0], lane), c0, c1);
+      if (k - 1 >= 1) load_wf<kH2, kL, 2>(fx, a.wc + a.c_hgT[k - 1], wave, lane);
       const int n0 = 16 * wave + m, n1 = 16 * (wave + 4) + m;
 #pragma unroll
       for (int e = 0; e < 4; ++e) bU[4 * kq + e][n0] = c0[e];
@@ -951,8 +955,6 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
     __syncthreads();
     K2_MARK(50 + k);
     // LayerNorm k-1 backward: gamma / beta column sums, dS_{k-1} per row -> bS
-    if (k - 1 >= 1) coop_store(wX, rX, tid);     // W_hg_{k-1} (wX is free: dXn_k is done)
-    if (k - 2 >= 0) coop_load(rY, P + a.w_o[k - 2], tid);
     {
       const int l = k - 1;
       if (tid < kL) {
@@ -971,7 +973,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
       float p1 = 0.f, p2 = 0.f;
 #pragma unroll
       for (int e = 0; e < 6; ++e) {
-        t[e] = bU[r][c0 + e] * sLg[l][c0 + e];
+        t[e] = bU[r][c0 + e] * lg[l][e];
         x[e] = xhS[l][r][c0 + e];
         p1 += t[e];
         p2 += t[e] * x[e];
@@ -984,7 +986,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
     __syncthreads();
     K2_MARK(60 + k);
     // GMLP k-1: output bias gradient (column sums of dS), dU = dS W_o (NN: K 96 -> N 64,
-    // W in wY) with the gate backward in the epilogue -> dHG_{k-1} (bX)
+    // fragments fy) with the gate backward in the epilogue -> dHG_{k-1} (bX)
     {
       const int kk = k - 1;
       store_t(a.dS + kk * kL * Bp, &bS[0][0], kL);
@@ -993,7 +995,8 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
         for (int r = 0; r < kR; ++r) s += bS[r][tid];
         atomicAdd(G + a.b_o[kk] + tid, s);
       }
-      const f4 du = gemm1_lds<kL, kH>(wY, load_a<kL>(&bS[0][0], lane), wave, lane);
+      const f4 du = gemm1<kL>(fy, load_a<kL>(&bS[0][0], lane));
+      if (k - 2 >= 0) load_wf<kL, kH, 1>(fy, a.wc + a.c_oT[k - 2], wave, lane);
       const int j = 16 * wave + m;
       f4 dho, dgo;
 #pragma unroll
@@ -1249,6 +1252,7 @@ __global__ void __launch_bounds__(256) k3_wgrad_kernel(K3Args a) {
 }
 
 // ------------------------------------------------------------------ k4 ----
+constexpr int kTileR = 16, kMaxTiles = 48;
 struct K4Args {
   float* P;
   float* G;  // gradient bucket; the statistics follow at G[n]
@@ -1262,6 +1266,13 @@ struct K4Args {
   float lr, b1, b2, eps;
   float* hist;
   int hist_cap;
+  WSplit w;       // weight cache kept current with the update (wc NULL: not kept)
+  _Float16* wc;
+  // with wc: workgroups 0 .. n_tiles - 1 update the cached matrices in tiles of
+  // kTileR rows (tile t: segment tile_seg[t], first row tile_r0[t]) and write the
+  // transposed planes from LDS as 16-B column runs; the rest do everything else
+  int n_tiles;
+  int tile_seg[kMaxTiles], tile_r0[kMaxTiles];
 };
 
 // The accumulation gate (trainer.py:443-465), computed identically by every
@@ -1324,9 +1335,10 @@ __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
   f4* M4 = reinterpret_cast<f4*>(a.m);
   f4* V4 = reinterpret_cast<f4*>(a.v);
   const f4 z4 = {0.f, 0.f, 0.f, 0.f};
-  for (int64_t i = blockIdx.x * int64_t(256) + threadIdx.x; i < n4; i += int64_t(gridDim.x) * 256) {
-    // all four loads unconditional (issued together, no wait behind the gate
-    // decision, which itself waits on the statistics)
+  // one float4: all four loads unconditional (issued together, no wait behind
+  // the gate decision, which itself waits on the statistics); the parameters
+  // after the step are returned
+  auto adam4 = [&](int64_t i) -> f4 {
     const f4 g = G4[i], m0 = M4[i], v0 = V4[i];
     f4 p = P4[i];
     G4[i] = z4;
@@ -1340,8 +1352,86 @@ __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
       for (int e = 0; e < 4; ++e) p[e] -= step_size * mi[e] / (sqrtf(vi[e]) / bc2s + a.eps);
       P4[i] = p;
     }
+    return p;
+  };
+  const int t0 = a.wc ? a.n_tiles : 0;
+  if (static_cast<int>(blockIdx.x) < t0) {  // a tile of a cached matrix
+    __shared__ float tileS[kTileR][kL + 1];
+    const WSeg g = a.w.s[a.tile_seg[blockIdx.x]];
+    const int r0 = a.tile_r0[blockIdx.x], C = g.cols, C4 = g.cols / 4;
+    const int rows = min(kTileR, g.rows - r0);
+    const int64_t rc = int64_t(g.rows) * C;
+    _Float16* d = a.wc + g.dst;
+    // <= kTileR * kL / 4 / 256 float4s per thread (2), all loads issued first
+    // (clamped indices) so the tile costs one memory latency, not several
+    constexpr int kIt = (kTileR * kL / 4 + 255) / 256;
+    f4 lg_[kIt], lm_[kIt], lv_[kIt], lp_[kIt];
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int q = min(static_cast<int>(threadIdx.x) + 256 * it, rows * C4 - 1);
+      const int r = q / C4, c4 = q - r * C4;
+      const int64_t i = (g.src + int64_t(r0 + r) * C + 4 * c4) >> 2;
+      lg_[it] = G4[i];
+      lm_[it] = M4[i];
+      lv_[it] = V4[i];
+      lp_[it] = P4[i];
+    }
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int q = static_cast<int>(threadIdx.x) + 256 * it;
+      if (q >= rows * C4) break;
+      const int r = q / C4, c4 = q - r * C4;
+      const int64_t off = int64_t(r0 + r) * C + 4 * c4;
+      const int64_t i = (g.src + off) >> 2;
+      f4 p = lp_[it];
+      G4[i] = z4;
+      if (on) {
+        const f4 gi = lg_[it] * scale;
+        const f4 mi = a.b1 * lm_[it] + (1.f - a.b1) * gi;
+        const f4 vi = a.b2 * lv_[it] + (1.f - a.b2) * gi * gi;
+        M4[i] = mi;
+        V4[i] = vi;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) p[e] -= step_size * mi[e] / (sqrtf(vi[e]) / bc2s + a.eps);
+        P4[i] = p;
+      }
+      if (on) {
+        uint32_t h[2], l[2];
+        split_pair(16.f * p[0], 16.f * p[1], h[0], l[0]);
+        split_pair(16.f * p[2], 16.f * p[3], h[1], l[1]);
+        *reinterpret_cast<uint2*>(d + off) = uint2{h[0], h[1]};
+        *reinterpret_cast<uint2*>(d + rc + off) = uint2{l[0], l[1]};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) tileS[r][4 * c4 + e] = p[e];
+      }
+    }
+    if (!on) return;  // the gate is the same in every thread: parameters and cache unchanged
+    __syncthreads();
+    for (int u = threadIdx.x; u < C * (kTileR / 8); u += 256) {
+      const int c = u / (kTileR / 8), rb = 8 * (u % (kTileR / 8));
+      if (rb >= rows) continue;
+      h8 hi, lo;
+      split8(f4{tileS[rb][c], tileS[rb + 1][c], tileS[rb + 2][c], tileS[rb + 3][c]} * 16.f,
+             f4{tileS[rb + 4][c], tileS[rb + 5][c], tileS[rb + 6][c], tileS[rb + 7][c]} * 16.f, hi, lo);
+      const int64_t o = int64_t(c) * g.rows + r0 + rb;
+      *reinterpret_cast<h8*>(d + 2 * rc + o) = hi;
+      *reinterpret_cast<h8*>(d + 3 * rc + o) = lo;
+    }
+    return;
   }
-  for (int64_t i = 4 * n4 + blockIdx.x * int64_t(256) + threadIdx.x; i < a.n; i += int64_t(gridDim.x) * 256) {
+  const int64_t b0 = static_cast<int64_t>(blockIdx.x) - t0, nb = static_cast<int64_t>(gridDim.x) - t0;
+  for (int64_t i = b0 * 256 + threadIdx.x; i < n4; i += nb * 256) {
+    if (t0) {  // cached matrices are the tile workgroups'
+      bool cached = false;
+#pragma unroll
+      for (int sg = 0; sg < kMaxSeg; ++sg)
+        cached |= sg < a.w.n && 4 * i >= a.w.s[sg].src &&
+                  4 * i < a.w.s[sg].src + int64_t(a.w.s[sg].rows) * a.w.s[sg].cols;
+      if (cached) continue;
+    }
+    adam4(i);
+  }
+  for (int64_t i = 4 * n4 + b0 * 256 + threadIdx.x; i < a.n; i += nb * 256) {
     const float g = a.G[i];
     a.G[i] = 0.f;
     if (on) {
@@ -1357,8 +1447,28 @@ __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
 
 // --------------------------------------------------------- workspace ------
 struct FusedWs {
-  int64_t hg_part, xhat[2], U, Xn, dS, dHG, total;  // float offsets
+  int64_t wsplit, hg_part, xhat[2], U, Xn, dS, dHG, total;  // float offsets
 };
+// the weight cache's segments (WSplit) for plan p: W_o_k (k < NG - 1), then W_hg_k (k >= 1)
+WSplit make_wsplit(const hbk_mlp_plan& p) {
+  const int NG = static_cast<int>(p.g.size());
+  WSplit w{};
+  int64_t dst = 0, q = 0;
+  auto add = [&](int64_t src, int rows, int cols) {
+    WSeg& g = w.s[w.n++];
+    g.src = src;
+    g.rows = rows;
+    g.cols = cols;
+    g.dst = dst;
+    g.q0 = q;
+    dst += 4 * int64_t(rows) * cols;
+    q += int64_t(rows) * cols / 4;
+  };
+  for (int k = 0; k + 1 < NG; ++k) add(p.g[k].w_o, p.g[k].out, p.g[k].hid);
+  for (int k = 1; k < NG; ++k) add(p.g[k].w_hg, 2 * p.g[k].hid, p.g[k].in);
+  return w;
+}
+int64_t wsplit_halves(int NG) { return int64_t(NG - 1) * 4 * (kL * kH + kH2 * kL); }
 int k1_blocks(int B) { return ((B + kRB - 1) / kRB + 7) / 8 * 8; }  // row blocks, XCD-aware
 int k1_splits(int B) {
   static const int ks_opts[] = {4, 6, 8, 12, 16, 24};
@@ -1371,6 +1481,7 @@ FusedWs fused_layout(int64_t B, int NG) {
   int64_t o = 0;
   auto take = [&](int64_t n) { const int64_t r = o; o += (n + 63) & ~int64_t(63); return r; };
   const int64_t Bp = (B + kR - 1) / kR * kR;
+  w.wsplit = take(wsplit_halves(NG) / 2);  // first: its offset does not depend on B
   w.hg_part = take(int64_t(24) * B * kH2);
   w.xhat[0] = take(Bp * kD);
   w.xhat[1] = take(Bp * kD);
@@ -1436,6 +1547,14 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
   ka.xhat[1] = ws + w.xhat[1];
   ka.Bp = Bp;
   const float* xhat = ws + w.xhat[parity];
+  const WSplit wsp = make_wsplit(p);
+  _Float16* wc = reinterpret_cast<_Float16*>(ws + w.wsplit);
+  if (!(flags & HBK_STEP_WEIGHTS_READY)) {  // the previous step's k4 did not leave the cache current
+    const int64_t n4 = wsplit_halves(NG) / 16;  // float4s of the segments
+    hipLaunchKernelGGL(k0_wsplit_kernel, dim3(unsigned(std::min<int64_t>((n4 + 255) / 256, 256))), dim3(256), 0,
+                       s, wsp, params, wc, n4);
+    HBK_LAUNCH_CHECK("k0_wsplit_kernel");
+  }
   if (!(flags & HBK_STEP_XHAT_READY)) {  // this step's rows were not prefetched by the previous step
     if (idx)
       hipLaunchKernelGGL(k1a_kernel<true>, dim3(rt), dim3(256), 0, s, ka, 0);
@@ -1492,6 +1611,16 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
   k2.n_rt = rt;
   k2.prefetch = train && idx && (flags & HBK_STEP_PREFETCH_NEXT);
   k2.pre = ka;
+  k2.wc = wc;
+  for (int k = 0; k < NG; ++k) k2.c_o[k] = k2.c_oT[k] = k2.c_hg[k] = k2.c_hgT[k] = 0;
+  for (int sg = 0; sg < wsp.n; ++sg) {
+    const WSeg& g = wsp.s[sg];
+    const int64_t rc = int64_t(g.rows) * g.cols;
+    const bool is_o = sg < NG - 1;
+    const int k = is_o ? sg : sg - (NG - 1) + 1;
+    (is_o ? k2.c_o : k2.c_hg)[k] = g.dst;
+    (is_o ? k2.c_oT : k2.c_hgT)[k] = g.dst + 2 * rc;
+  }
   {
     const int grid = k2.prefetch ? 2 * rt : rt;
     auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, k2); };
@@ -1546,8 +1675,16 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
 
 int mlp_fused_update(const hbk_mlp_plan& p, float* params, float* bucket, float* m, float* v, float* state,
                      int parity, const float* sched, int sched_len, float lr, float b1, float b2, float eps,
-                     float* hist, int hist_cap, hipStream_t s) {
+                     float* hist, int hist_cap, float* ws, hipStream_t s) {
   K4Args k;
+  k.w = make_wsplit(p);
+  k.wc = ws ? reinterpret_cast<_Float16*>(ws + fused_layout(1, static_cast<int>(p.g.size())).wsplit) : nullptr;
+  k.n_tiles = 0;
+  for (int sg = 0; sg < k.w.n; ++sg)
+    for (int r0 = 0; r0 < k.w.s[sg].rows && k.n_tiles < kMaxTiles; r0 += kTileR) {
+      k.tile_seg[k.n_tiles] = sg;
+      k.tile_r0[k.n_tiles++] = r0;
+    }
   k.P = params;
   k.G = bucket;
   k.m = m;
@@ -1563,7 +1700,7 @@ int mlp_fused_update(const hbk_mlp_plan& p, float* params, float* bucket, float*
   k.eps = eps;
   k.hist = hist;
   k.hist_cap = hist_cap;
-  const int64_t blocks = std::min<int64_t>((p.n_params / 4 + 255) / 256, 1024);
+  const int64_t blocks = (k.wc ? k.n_tiles : 0) + std::min<int64_t>((p.n_params / 4 + 255) / 256, 1024);
   hipLaunchKernelGGL(k4_update_kernel, dim3(unsigned(blocks)), dim3(256), 0, s, k);
   HBK_LAUNCH_CHECK("k4_update_kernel");
   return HBK_OK;

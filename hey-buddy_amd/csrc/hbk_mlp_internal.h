@@ -52,5 +52,5 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
                   float* bucket, float* prob, float* logit, float* ws, bool train, int flags, hipStream_t s);
 int mlp_fused_update(const hbk_mlp_plan& p, float* params, float* bucket, float* m, float* v, float* state,
                      int parity, const float* sched, int sched_len, float lr, float b1, float b2, float eps,
-                     float* hist, int hist_cap, hipStream_t s);
+                     float* hist, int hist_cap, float* ws, hipStream_t s);
 }  // namespace hbk

@@ -93,7 +93,7 @@ _PROTOS = {
                                       _c_float, _c_float, ctypes.c_uint64, _vp, _vp, _c_int64, ctypes.c_int32,
                                       _vp, _c_int64, _vp]),
     "hbk_mlp_step_update": (_c_int, [_vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int32, _vp, _c_int64, _c_float,
-                                     _c_float, _c_float, _c_float, _vp, ctypes.c_int32, _vp]),
+                                     _c_float, _c_float, _c_float, _vp, ctypes.c_int32, _vp, _c_int64, _vp]),
 }
 
 

@@ -426,7 +426,8 @@ class MlpPlan:
                      neg_weight: float = 1.0, threshold: float = 1e-4, activation_threshold: float = 0.5,
                      dropout_p: float = 0.0, seed: int = 0, prob: torch.Tensor | None = None,
                      workspace: torch.Tensor | None = None, xhat_ready: bool = False,
-                     prefetch_next: bool = False, idx_steps: int | None = None) -> None:
+                     prefetch_next: bool = False, idx_steps: int | None = None,
+                     weights_ready: bool = False) -> None:
         """Forward / filter / BCE / backward of one step into ``bucket``
         (hbk_mlp_step_fwd_bwd). Rows come from pool32 [n, 1536] f32 and pool16
         [n, 1536] f16 by ``idx`` (int32, >= 0 -> pool32, < 0 -> pool16 row -i-1;
@@ -434,7 +435,8 @@ class MlpPlan:
         ``prefetch_next``: also gather + normalise step + 1's rows (idx row
         step + 1 < idx_steps, default idx.numel() // idx_stride) during this
         step; ``xhat_ready``: the previous call on this workspace did that for
-        this step."""
+        this step; ``weights_ready``: the previous step_update got this
+        workspace, so its weight cache is current (else it is refreshed)."""
         dev = params.device
         if params.numel() != self.n_params or bucket.numel() != self.n_params + self.N_STATS:
             raise ValueError("params / bucket do not match the plan")
@@ -455,7 +457,8 @@ class MlpPlan:
         ws = self.workspace(batch, dev) if workspace is None else workspace
         if idx_steps is None:
             idx_steps = idx.numel() // idx_stride if idx is not None and idx_stride > 0 else 1
-        flags = (1 if xhat_ready else 0) | (2 if prefetch_next and idx is not None else 0)
+        flags = (1 if xhat_ready else 0) | (2 if prefetch_next and idx is not None else 0) | (
+            4 if weights_ready else 0)
         torch.ops.hbk.mlp_step_fwd_bwd(params, bucket, state, int(parity), y, int(batch), pool32, pool16, idx,
                                        int(idx_stride), int(y_stride), sched, float(neg_weight), float(threshold),
                                        float(activation_threshold), float(dropout_p), _u64_to_i64(seed), prob, ws,
@@ -464,10 +467,12 @@ class MlpPlan:
     def step_update(self, params: torch.Tensor, bucket: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
                     state: torch.Tensor, parity: int, sched: torch.Tensor | None = None, lr: float = 1e-3,
                     beta1: float = 0.9, beta2: float = 0.999, eps: float = 1e-8,
-                    history: torch.Tensor | None = None) -> None:
-        """Gate + Adam + bucket zeroing (hbk_mlp_step_update)."""
+                    history: torch.Tensor | None = None, workspace: torch.Tensor | None = None) -> None:
+        """Gate + Adam + bucket zeroing (hbk_mlp_step_update); with the step's
+        ``workspace`` it also keeps the weight cache there current, so the next
+        step_fwd_bwd on it may pass weights_ready."""
         torch.ops.hbk.mlp_step_update(params, bucket, m, v, state, int(parity), sched, float(lr), float(beta1),
-                                      float(beta2), float(eps), history, self.id)
+                                      float(beta2), float(eps), history, workspace, self.id)
 
     def gate_adam(self, params, bucket, m, v, state, ctrl, history, lr, beta1=0.9, beta2=0.999,
                   eps=1e-8) -> None:
@@ -513,17 +518,19 @@ def _mlp_step_fwd_bwd_op(params: torch.Tensor, bucket: torch.Tensor, state: torc
         ws.numel(), stream_ptr(params.device)), "hbk_mlp_step_fwd_bwd")
 
 
-@torch.library.custom_op("hbk::mlp_step_update", mutates_args=("params", "bucket", "m", "v", "state", "history"))
+@torch.library.custom_op("hbk::mlp_step_update",
+                         mutates_args=("params", "bucket", "m", "v", "state", "history", "ws"))
 def _mlp_step_update_op(params: torch.Tensor, bucket: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
                         state: torch.Tensor, parity: int, sched: torch.Tensor | None, lr: float, beta1: float,
-                        beta2: float, eps: float, history: torch.Tensor | None, plan_id: int) -> None:
+                        beta2: float, eps: float, history: torch.Tensor | None, ws: torch.Tensor | None,
+                        plan_id: int) -> None:
     plan = _plans[plan_id]
     cap = 0 if history is None else history.shape[0]
     check(lib().hbk_mlp_step_update(
         plan._handle, ptr(params), ptr(bucket), ptr(m), ptr(v), ptr(state), parity,
         ptr(sched) if sched is not None else None, sched.shape[0] if sched is not None else 0, lr, beta1, beta2,
-        eps, ptr(history) if history is not None else None, cap, stream_ptr(params.device)),
-          "hbk_mlp_step_update")
+        eps, ptr(history) if history is not None else None, cap, ptr(ws) if ws is not None else None,
+        ws.numel() if ws is not None else 0, stream_ptr(params.device)), "hbk_mlp_step_update")
 
 
 @torch.library.custom_op("hbk::place_clips", mutates_args=())

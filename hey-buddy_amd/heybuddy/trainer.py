@@ -365,10 +365,10 @@ class WakeWordTrainer(Trainer):
             plan.step_fwd_bwd(flat, self._bucket, self._fstate, parity, y, B, pool32=p32, pool16=p16, idx=idx,
                               idx_stride=B, y_stride=y_stride, sched=sched, threshold=threshold,
                               activation_threshold=activation_threshold, dropout_p=p, seed=self._seed_base,
-                              workspace=ws, xhat_ready=ready, prefetch_next=True, idx_steps=S)
+                              workspace=ws, xhat_ready=ready, prefetch_next=True, idx_steps=S, weights_ready=ready)
             distributed.reduce_bucket(self._bucket)
             plan.step_update(flat, self._bucket, self._m, self._v, self._fstate, parity, sched=sched,
-                             beta1=BETAS[0], beta2=BETAS[1], eps=EPS, history=history)
+                             beta1=BETAS[0], beta2=BETAS[1], eps=EPS, history=history, workspace=ws)
 
         done = 0
         if S > 0:  # the first step gathers its own rows and prefetches the next

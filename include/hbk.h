@@ -229,9 +229,15 @@ int hbk_mlp_gate_adam(const hbk_mlp_plan* plan, float* params, const float* buck
  *     workspace, concurrently with its own chain kernel;
  *   flags & HBK_STEP_XHAT_READY: this step's rows were prefetched that way (the
  *     previous call on the same workspace set PREFETCH_NEXT) and are not
- *     recomputed. Without it the step gathers its own rows first. */
+ *     recomputed. Without it the step gathers its own rows first.
+ * The chain kernel reads its weight matrices as pre-split f16 hi / lo planes
+ * (plain and transposed) from a cache at the start of the workspace:
+ *   flags & HBK_STEP_WEIGHTS_READY: the previous hbk_mlp_step_update got the same
+ *     workspace and left the cache current (it rewrites the cached matrices with
+ *     every update); without it the step refreshes the cache from params first. */
 #define HBK_STEP_XHAT_READY 1
 #define HBK_STEP_PREFETCH_NEXT 2
+#define HBK_STEP_WEIGHTS_READY 4
 int hbk_mlp_fused_supported(const hbk_mlp_plan* plan, int32_t* supported);
 int hbk_mlp_step_fwd_bwd(const hbk_mlp_plan* plan, const float* params, const float* pool32, int64_t n32,
                          const void* pool16, int64_t n16, const int32_t* idx, int64_t idx_step_stride,
@@ -243,7 +249,7 @@ int hbk_mlp_step_fwd_bwd(const hbk_mlp_plan* plan, const float* params, const fl
 int hbk_mlp_step_update(const hbk_mlp_plan* plan, float* params, float* bucket, float* m, float* v,
                         float* state, int32_t parity, const float* sched, int64_t sched_len, float lr,
                         float beta1, float beta2, float eps, float* history, int32_t history_cap,
-                        void* stream);
+                        void* workspace, int64_t workspace_bytes, void* stream);
 
 /* Graph-captured training steps: dev_scalars (device, double[3] = lr,
  * neg_weight, dropout seed; NULL = off) is read by the kernels of
