@@ -10,9 +10,10 @@
 //   k1a        gather the batch rows from the embedding pools by index (f32
 //              or f16 pool), input dropout, LayerNorm(1536) -> xhat^T in HBM.
 //              It needs no weights, so step s + 1's k1a runs as extra
-//              workgroups of step s's k2 launch (k2 fills 69 of 256 CUs at
-//              B = 1100) and is off the critical path; a standalone launch
-//              covers the first step and steps without a known successor
+//              workgroups of step s's k2 launch, two row tiles each (k2 fills
+//              35 of 256 CUs at B = 1100, two workgroups per CU) and is off
+//              the critical path; a standalone launch covers the first step
+//              and steps without a known successor
 //   k1b        the input GEMM HG0 = (xhat g + b) W_hg0^T as split-K partial
 //              slabs (row tiles of 16 x K-chunks: ~576 workgroups at B = 1100)
 //   k2_rows    per 16-row tile, the whole rest of the network in LDS:
@@ -182,6 +183,7 @@ __device__ __forceinline__ uint32_t drop_hash(uint32_t s0, uint32_t s1, uint32_t
 // [512 t, 512 t + 512), so xhat^T is written in three 512-column slabs staged
 // through LDS (slab: [16][516] floats) as 64-B column runs.
 constexpr int kSlabLd = 516;
+constexpr int kPreTiles = 2;  // k1a row tiles per prefetch workgroup of k2
 template <bool kIdx>
 __device__ __forceinline__ void k1a_tile(const K1aArgs& a, int rt, int step, float* __restrict__ xout,
                                          float* slab) {
@@ -659,9 +661,17 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
   int trn = 0;
 #endif
   if (kTrain && static_cast<int>(blockIdx.x) >= a.n_rt) {  // next step's k1a (weights not needed)
+    // kPreTiles row tiles per workgroup: about as long as a chain workgroup, and
+    // the launch needs n_rt + n_rt / kPreTiles slots (two per CU)
     const int step = step_of(a.pre.state, a.pre.parity) + 1;
-    if (step < a.pre.idx_steps)
-      k1a_tile<true>(a.pre, blockIdx.x - a.n_rt, step, a.pre.xhat[a.pre.parity ^ 1], hgRaw);
+    if (step < a.pre.idx_steps) {
+      for (int t = 0; t < kPreTiles; ++t) {
+        const int rt = (blockIdx.x - a.n_rt) * kPreTiles + t;
+        if (rt >= a.n_rt) break;
+        if (t) __syncthreads();  // the slab's previous readers are done
+        k1a_tile<true>(a.pre, rt, step, a.pre.xhat[a.pre.parity ^ 1], hgRaw);
+      }
+    }
     return;
   }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1622,7 +1632,7 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
     (is_o ? k2.c_oT : k2.c_hgT)[k] = g.dst + 2 * rc;
   }
   {
-    const int grid = k2.prefetch ? 2 * rt : rt;
+    const int grid = k2.prefetch ? rt + (rt + kPreTiles - 1) / kPreTiles : rt;
     auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, k2); };
     if (train) {
       if (NG == 2) launch(k2_rows_kernel<true, 2>);

@@ -36,7 +36,16 @@ def setup(S, B=1100, P=50, A=50):
     return tr, pos, neg, idx, y, sched
 
 
-def timing(S):
+def timing(S, n_cus=0):
+    """n_cus > 0: on a stream masked to that many CUs (heybuddy.pipeline)."""
+    if n_cus:
+        from heybuddy.pipeline import masked_stream, train_cu_set
+        ms = masked_stream(torch.device("cuda", 0), train_cu_set(torch.cuda.get_device_properties(0).multi_processor_count, n_cus))
+        with torch.cuda.stream(ms.stream):
+            timing(S)
+        torch.cuda.synchronize()
+        print(f"  (above: stream masked to {n_cus} CUs)")
+        return
     tr, pos, neg, idx, y, sched = setup(S)
     hist = torch.zeros((S, 8), device="cuda")
     for _ in range(2):
@@ -86,4 +95,5 @@ if __name__ == "__main__":
     if TRACE:
         trace()
     else:
-        timing(int(next((a for a in sys.argv[1:] if a.isdigit()), 200)))
+        cus = next((int(a[6:]) for a in sys.argv[1:] if a.startswith("--cus=")), 0)
+        timing(int(next((a for a in sys.argv[1:] if a.isdigit()), 200)), cus)
