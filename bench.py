@@ -85,16 +85,21 @@ def parse():
 
 
 TRAFFIC_SOURCE = [None]
+CURRENT_CONFIG = [None]
 
 
 def load_traffic(path, kernel_substr):
     """HBM bytes per step of the kernels whose name contains kernel_substr (a
     string or a tuple of alternatives), from a tools/pmc_summary.py JSON
-    (FETCH_SIZE doubled per the gfx950 calibration + WRITE_SIZE), or None."""
+    (FETCH_SIZE doubled per the gfx950 calibration + WRITE_SIZE), or None. A
+    summary recorded for another --config (its "config" field) is not used:
+    per-step bytes belong to one workload."""
     subs = (kernel_substr,) if isinstance(kernel_substr, str) else tuple(kernel_substr)
     try:
         with open(path) as f:
             d = json.load(f)
+        if d.get("config") not in (None, CURRENT_CONFIG[0]):
+            return None
         v = [k for name, k in d.get("kernels", {}).items() if any(s in name for s in subs)]
         if v:
             TRAFFIC_SOURCE[0] = os.path.relpath(path, ROOT)
@@ -119,6 +124,7 @@ def roof(kernel, bound, work, ms, unit, traffic, peak=None, **extra):
 
 def main():
     args = parse()
+    CURRENT_CONFIG[0] = args.config
     if args.config == 1:
         return cpu_mel_only(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -6,7 +6,9 @@ Each pass must profile ONE bench step (bench.py --steps 1 --warmup 0 --no-cpu
 one pass on gfx950). Per MI355X_MICROARCH.md §HBM, FETCH_SIZE reports half the
 bytes of a wide coalesced read on gfx950, so
     hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024     (counters in KiB)
-Usage: python tools/pmc_summary.py FETCH_DIR WRITE_DIR OUT.json
+Usage: python tools/pmc_summary.py FETCH_DIR WRITE_DIR OUT.json [CONFIG]
+(CONFIG: the bench.py --config the passes ran; bench.py only uses a summary
+for the same workload.)
 """
 import csv
 import glob
@@ -33,6 +35,7 @@ def load(dirpath, counter):
 
 def main():
     fdir, wdir, out = sys.argv[1:4]
+    config = int(sys.argv[4]) if len(sys.argv) > 4 else None
     fetch, fcalls = load(fdir, "FETCH_SIZE")
     write, _ = load(wdir, "WRITE_SIZE")
     res = {}
@@ -42,7 +45,7 @@ def main():
                      "hbm_bytes_per_step": (2.0 * f + w) * 1024.0}
     with open(out, "w") as fh:
         json.dump({"formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 per step (gfx950 FETCH_SIZE = 1/2 bytes)",
-                   "kernels": res}, fh, indent=1)
+                   "config": config, "kernels": res}, fh, indent=1)
     for name, v in res.items():
         if v["hbm_bytes_per_step"] > 1e6:
             print(f"{v['hbm_bytes_per_step'] / 1e9:10.3f} GB  {name[:100]}")

@@ -38,7 +38,7 @@ if [ -n "$PMC" ]; then
     echo "=== pmc config $C"
     timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/pmcf_${TAG}_c$C -o run -- python3 bench.py --config $C --steps 1 --warmup 0 --no-cpu --no-check --overlap off > $OUT/pmcf_${TAG}_c$C.log 2>&1 || { tail -20 $OUT/pmcf_${TAG}_c$C.log; exit 1; }
     timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -f csv -d $OUT/pmcw_${TAG}_c$C -o run -- python3 bench.py --config $C --steps 1 --warmup 0 --no-cpu --no-check --overlap off > $OUT/pmcw_${TAG}_c$C.log 2>&1 || { tail -20 $OUT/pmcw_${TAG}_c$C.log; exit 1; }
-    python tools/pmc_summary.py $OUT/pmcf_${TAG}_c$C $OUT/pmcw_${TAG}_c$C $OUT/pmc_${TAG}_c$C.json
+    python tools/pmc_summary.py $OUT/pmcf_${TAG}_c$C $OUT/pmcw_${TAG}_c$C $OUT/pmc_${TAG}_c$C.json $C
   done
 fi
 echo "=== done"
