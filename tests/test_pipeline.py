@@ -1,0 +1,95 @@
+"""heybuddy.pipeline: CU partitions for featurizing beside training.
+
+CPU: the train CU set is spread evenly over the XCDs whether the mask's bit i
+maps to XCD i // 32 or to XCD i % 8, and the mask words hold exactly that set.
+GPU: on a CU-masked stream (persistent grids sized to the mask) the embedding
+chain gives the same bits as on the default stream, and the mel frames agree to
+the last bit or two (the persistent mel kernel's frame-group-to-workgroup
+assignment follows the grid size; measured max |d| 1.9e-6 on log-mel values);
+the sync-free NaN-row replacement keeps clean rows and fills NaN rows from
+NaN-free ones.
+"""
+import numpy as np
+import pytest
+import torch
+
+from heybuddy.pipeline import cu_mask_words, train_cu_set
+
+
+@pytest.mark.parametrize("n_train", [32, 64, 96, 128])
+def test_train_cu_set_even_over_xcds(n_train):
+    cus = train_cu_set(256, n_train)
+    assert len(cus) == len(set(cus)) == n_train and all(0 <= c < 256 for c in cus)
+    contiguous = np.bincount([c // 32 for c in cus], minlength=8)
+    interleaved = np.bincount([c % 8 for c in cus], minlength=8)
+    assert (contiguous == n_train // 8).all()
+    assert (interleaved == n_train // 8).all()
+
+
+def test_cu_mask_words():
+    cus = train_cu_set(256, 64)
+    words = cu_mask_words(cus, 256)
+    assert len(words) == 8
+    back = [32 * w + b for w, word in enumerate(words) for b in range(32) if word >> b & 1]
+    assert back == sorted(cus)
+    rest = sorted(set(range(256)) - set(cus))
+    assert sum(bin(w).count("1") for w in cu_mask_words(rest, 256)) == 192
+
+
+def test_replace_nan_rows_device_cpu_semantics():
+    from heybuddy.embeddings import replace_nan_rows_device
+    g = torch.Generator().manual_seed(0)
+    e = torch.randn(12, 16, 96, generator=g)
+    e[2, 5, 7] = float("nan")
+    e[9] = float("nan")
+    out = torch.empty_like(e)
+    replace_nan_rows_device(e, out, generator=torch.Generator().manual_seed(1))
+    clean = [i for i in range(12) if i not in (2, 9)]
+    assert not torch.isnan(out).any()
+    for i in clean:
+        assert torch.equal(out[i], e[i])
+    for i in (2, 9):
+        assert any(torch.equal(out[i], e[j]) for j in clean)
+    allnan = torch.full((3, 16, 96), float("nan"))
+    assert (replace_nan_rows_device(allnan, torch.empty_like(allnan)) == 0).all()
+
+
+@pytest.mark.gpu
+def test_masked_stream_same_bits():
+    from heybuddy.embedding_graph import WINDOW_STARTS
+    from heybuddy.embeddings import embed_plan
+    from heybuddy.kernels import embed_clips, mel_frames
+    from heybuddy.pipeline import make_streams
+    from heybuddy.spectrogram import default_mel_plan
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(3)
+    clips = torch.randn((300, 24000), generator=g, device=dev) * 0.1
+    mplan = default_mel_plan(dev, 32767.0)
+    eplan = embed_plan(dev, WINDOW_STARTS)
+    mel_ref = mel_frames(clips, mplan, 141).clone()
+    ref = embed_clips(mel_ref, eplan).clone()
+    fs, ts, keep = make_streams(dev, "split:64")
+    for st in (fs, ts):
+        st.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(st):
+            mel = mel_frames(clips, mplan, 141)
+            out = embed_clips(mel_ref, eplan)
+        torch.cuda.current_stream(dev).wait_stream(st)
+        torch.cuda.synchronize()
+        assert (mel - mel_ref).abs().max().item() <= 1e-5
+        assert torch.equal(out, ref)
+    del keep
+
+
+@pytest.mark.gpu
+def test_replace_nan_rows_device_gpu():
+    from heybuddy.embeddings import replace_nan_rows_device
+    dev = torch.device("cuda", 0)
+    e = torch.randn(64, 16, 96, device=dev)
+    e[5, 0, 0] = float("nan")
+    e[40] = float("nan")
+    out = torch.empty_like(e)
+    replace_nan_rows_device(e, out)
+    assert not torch.isnan(out).any()
+    keep = [i for i in range(64) if i not in (5, 40)]
+    assert torch.equal(out[keep], e[keep])
