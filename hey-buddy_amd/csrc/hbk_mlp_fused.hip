@@ -1056,7 +1056,12 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
 // into f16 hi / lo planes in LDS and shared by the four waves. Split-K partials
 // are added with float atomics into the bucket (zeroed by the previous k4).
 constexpr int kTM = 128, kTN = 32, kMaxJobs = 2 * kMaxG;
-constexpr int kK3Steps = 9, kK3Rows = 32 * kK3Steps;  // batch rows per split (B = 1100: 4 splits)
+// batch rows per split: measured 4 / 5 / 6 / 9 steps (124 / 152 / 180 / 248 VGPRs) at 60.2 / 60.3 /
+// 61.6 / 58.9 us per step on 256 CUs and 88.7 / 88.9 / 94.8 / 92.1 on a 64-CU stream
+#ifndef HBK_K3_STEPS
+#define HBK_K3_STEPS 9
+#endif
+constexpr int kK3Steps = HBK_K3_STEPS, kK3Rows = 32 * kK3Steps;  // batch rows per split (B = 1100: 4 splits)
 constexpr int kYLdH = kK3Rows + 8;                    // LDS row stride (halves) of the Y planes
 struct WJob {
   const float* X;  // [M][Bp]
