@@ -301,6 +301,7 @@ struct XArgs {
   int lds_x, lds_y, lds_w, lds_b, lds_k;  // byte offsets into dynamic LDS
   int dbg_slot;            // phase-timing slot (chain index mod 4; profiling build only)
   int dbg_skip;            // profiling build only: bit 0 stages, 1 im2col, 2 store, 3 staging
+  int* range_flag;         // set to 1 when an f16-split value reaches kF16Max
 };
 
 #if defined(HBK_PHASE_TIMING) || defined(HBK_ABLATE)
@@ -374,6 +375,25 @@ __device__ __forceinline__ int div_small(int n, int d, float inv) {
 // hi = v rounded toward zero to fp16 (11 significant bits in fp16's normal
 // range), lo = (v - hi) rounded to fp16 by v_fma_mix{lo,hi}_f16 (v - hi is
 // exact in f32); two values, packed: 3 VALU instructions per pair
+// The f16 planes hold |v| < 65504 (kF16Max): amax keeps the largest |v| a
+// thread split (one v_max3 per pair; fmaxf drops NaN, which is not a range
+// fault) and the kernel raises its plan's range flag when it reaches kF16Max.
+constexpr float kF16Max = 65504.f;
+// (one v_max3 through asm: fmaxf / fabsf put canonicalising v_max ops in front)
+__device__ __forceinline__ void track(float& amax, float a, float b) {
+  asm("v_max3_f32 %0, %0, |%1|, |%2|" : "+v"(amax) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void raise_range(int* flag, float amax) {
+  if (amax >= kF16Max) *flag = 1;  // vector store: any writer, same value
+}
+// (the generic kernel runs at its VGPR cap: it checks each group of values
+// where it splits them instead of carrying amax, guard4)
+__device__ __forceinline__ void guard4(int* flag, float a, float b, float c, float d) {
+  float m = 0.f;
+  track(m, a, b);
+  track(m, c, d);
+  if (m >= kF16Max) *flag = 1;
+}
 __device__ __forceinline__ void split2(float a, float b, h2& hi, h2& lo) {
   hi = __builtin_amdgcn_cvt_pkrtz(a, b);
   const uint32_t hb = __builtin_bit_cast(uint32_t, hi);
@@ -422,7 +442,8 @@ __device__ __forceinline__ void xstage(const _Float16* __restrict__ Xh, const _F
                                        _Float16* __restrict__ Yh, _Float16* __restrict__ Yl,
                                        float* __restrict__ Yf, const _Float16* __restrict__ Wh,
                                        const int* __restrict__ kt, const float* __restrict__ bias, int M,
-                                       int hA, int wA, int ho, int wo, const XStage& S, int lane, int wave) {
+                                       int hA, int wA, int ho, int wo, const XStage& S, int lane, int wave,
+                                       int* flag) {
   const int img_pos = ho * wo;
   const int nrb = (M + 31) >> 5;
   const int r32 = lane & 31, khalf = lane >> 5;
@@ -513,6 +534,7 @@ __device__ __forceinline__ void xstage(const _Float16* __restrict__ Xh, const _F
     HBK_MARK(12);
     // D[n][m]: this lane holds position m = tile + (lane & 31) and channels
     // n = 32 c + 8 q + 4 (lane >> 5) + j for register i = 4 q + j
+    float m4 = 0.f;  // range guard over this epilogue's split values
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
       const int m = (rb0 + r) * 32 + r32;
@@ -540,12 +562,15 @@ __device__ __forceinline__ void xstage(const _Float16* __restrict__ Xh, const _F
             continue;
           }
           h2 h01, l01, h23, l23;
+          track(m4, v[0], v[1]);
+          track(m4, v[2], v[3]);
           split2(v[0], v[1], h01, l01);
           split2(v[2], v[3], h23, l23);
           *reinterpret_cast<uint2*>(yh + n0) = uint2{h2_bits(h01), h2_bits(h23)};
           *reinterpret_cast<uint2*>(yl + n0) = uint2{h2_bits(l01), h2_bits(l23)};
         }
     }
+    if (m4 >= kF16Max) *flag = 1;
     HBK_MARK(13);
   }
 }
@@ -686,6 +711,8 @@ conv_chain_x3_kernel(XArgs a) {
     const int w = (ms.u_step == st_units) ? st_w : u / (C / 8);
     const int c8 = (u - w * (C / 8)) * 8;
     h2 a0, b0, a1, b1, a2, b2, a3, b3;
+    guard4(a.range_flag, v0.x, v0.y, v0.z, v0.w);
+    guard4(a.range_flag, v1.x, v1.y, v1.z, v1.w);
     split2(v0.x, v0.y, a0, b0);
     split2(v0.z, v0.w, a1, b1);
     split2(v1.x, v1.y, a2, b2);
@@ -773,6 +800,7 @@ conv_chain_x3_kernel(XArgs a) {
         _Float16* dl_ = Il + (prow * wo0 + x) * a.cs0;
         for (int k8 = 0; k8 < K8; k8 += 8) {  // one 8-channel group: 16 B per plane
           uint32_t hb[4], lb[4];
+          float m = 0.f;
 #pragma unroll
           for (int p = 0; p < 4; ++p) {
             const int k = k8 + 2 * p;  // tap offsets: uniform table (scalar loads)
@@ -781,10 +809,12 @@ conv_chain_x3_kernel(XArgs a) {
             const float v0 = k < K0 ? base[o0] : 0.f;
             const float v1 = k + 1 < K0 ? base[o1] : 0.f;
             h2 hh, ll;
+            track(m, v0, v1);
             split2(v0, v1, hh, ll);
             hb[p] = h2_bits(hh);
             lb[p] = h2_bits(ll);
           }
+          if (m >= kF16Max) *a.range_flag = 1;
           *reinterpret_cast<uint4*>(dh_ + k8) = uint4{hb[0], hb[1], hb[2], hb[3]};
           *reinterpret_cast<uint4*>(dl_ + k8) = uint4{lb[0], lb[1], lb[2], lb[3]};
         }
@@ -816,11 +846,11 @@ conv_chain_x3_kernel(XArgs a) {
       } else
       // RB x NB tiles of one 16-register accumulator each
       if (NBMAX >= 3 && S.nblk == 3)
-        xstage<3, 1>(Xh, Xl, Yh, Yl, Yf, Wst, kts, bs, M, hA, wA, ho, wo, S, lane, wave);
+        xstage<3, 1>(Xh, Xl, Yh, Yl, Yf, Wst, kts, bs, M, hA, wA, ho, wo, S, lane, wave, a.range_flag);
       else if (NBMAX >= 2 && S.nblk == 2)
-        xstage<2, 2>(Xh, Xl, Yh, Yl, Yf, Wst, kts, bs, M, hA, wA, ho, wo, S, lane, wave);
+        xstage<2, 2>(Xh, Xl, Yh, Yl, Yf, Wst, kts, bs, M, hA, wA, ho, wo, S, lane, wave, a.range_flag);
       else
-        xstage<1, 2>(Xh, Xl, Yh, Yl, Yf, Wst, kts, bs, M, hA, wA, ho, wo, S, lane, wave);
+        xstage<1, 2>(Xh, Xl, Yh, Yl, Yf, Wst, kts, bs, M, hA, wA, ho, wo, S, lane, wave, a.range_flag);
       unsigned char* t = cur;
       cur = nxt;
       nxt = t;
@@ -898,6 +928,7 @@ struct P0Args {
   int H_out;                // pooled output rows per image
   int n_bands;
   float alpha;              // LeakyReLU slope of all three convs (LEAKY kernels)
+  int* range_flag;          // set to 1 when an f16-split value reaches kF16Max
 };
 
 template <int WI, int C, int BAND>
@@ -918,7 +949,8 @@ struct P0Geo {
 };
 
 // hi = v rounded toward zero to fp16, lo = (v - hi) rounded to fp16; two values, packed
-__device__ __forceinline__ void split2_mix(float a, float b, uint32_t& hi, uint32_t& lo) {
+__device__ __forceinline__ void split2_mix(float a, float b, uint32_t& hi, uint32_t& lo, float& amax) {
+  track(amax, a, b);
   hi = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(a, b));
   uint32_t l = 0;
   asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "+v"(l) : "v"(a), "v"(hi));
@@ -954,15 +986,15 @@ __device__ __forceinline__ f16x p0_bias(const float* b, int khalf) {
 // activation + split of a finished tile into the hi / lo planes at position p
 template <int C, int CS, bool LEAKY>
 __device__ __forceinline__ void p0_store_planes(const f16x& acc, int p, int khalf, _Float16* oh, _Float16* ol,
-                                                float alpha) {
+                                                float alpha, float& amax) {
 #pragma unroll
   for (int q = 0; q < C / 8; ++q) {
     float v[4];
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) v[jj] = p0_act<LEAKY>(acc[4 * q + jj], alpha);
     uint32_t h01, l01, h23, l23;
-    split2_mix(v[0], v[1], h01, l01);
-    split2_mix(v[2], v[3], h23, l23);
+    split2_mix(v[0], v[1], h01, l01, amax);
+    split2_mix(v[2], v[3], h23, l23, amax);
     const int o = p * CS + 8 * q + 4 * khalf;
     *reinterpret_cast<uint2*>(oh + o) = uint2{h01, h23};
     *reinterpret_cast<uint2*>(ol + o) = uint2{l01, l23};
@@ -994,7 +1026,7 @@ __device__ __forceinline__ P0W<P0Geo<WI, C, BAND>::KS> p0_load_w(const P0Args& a
 template <int WI, int C, int BAND, int ST, bool LEAKY>
 __device__ __forceinline__ void p0_stage12(const P0Args& a, const P0W<P0Geo<WI, C, BAND>::KS>& W,
                                            const _Float16* xh_, const _Float16* xl_, _Float16* oh, _Float16* ol,
-                                           float* of, int wave, int r32, int khalf) {
+                                           float* of, int wave, int r32, int khalf, float& amax) {
   using G = P0Geo<WI, C, BAND>;
   constexpr int M = ST == 1 ? G::M1 : G::M2, T = ST == 1 ? G::T1 : G::T2;
   constexpr int Wout = ST == 1 ? G::W1 : G::W2, Win = ST == 1 ? G::W0 : G::W1;
@@ -1018,7 +1050,7 @@ __device__ __forceinline__ void p0_stage12(const P0Args& a, const P0W<P0Geo<WI, 
     const int pp = t * 32 + r32;
     if (pp >= M) return;
     if (ST == 1) {
-      p0_store_planes<C, G::CS, LEAKY>(acc, pp, khalf, oh, ol, alpha);
+      p0_store_planes<C, G::CS, LEAKY>(acc, pp, khalf, oh, ol, alpha, amax);
     } else {
 #pragma unroll
       for (int q = 0; q < C / 8; ++q) {
@@ -1091,6 +1123,7 @@ p0_chain_kernel(P0Args a) {
   const f16x b0 = p0_bias(a.bias, khalf);
   const auto W1 = p0_load_w<WI, C, BAND, 1>(a, r32, khalf);
   const auto W2 = p0_load_w<WI, C, BAND, 2>(a, r32, khalf);
+  float amax = 0.f;
 
   for (int task = blockIdx.x; task < n_tasks; task += gridDim.x) {
     const int img = task / a.n_bands, band = task - img * a.n_bands;
@@ -1122,23 +1155,23 @@ p0_chain_kernel(P0Args a) {
         v[5] = v[6] = v[7] = 0.f;
         uint32_t hb[4], lb[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) split2_mix(v[2 * i], v[2 * i + 1], hb[i], lb[i]);
+        for (int i = 0; i < 4; ++i) split2_mix(v[2 * i], v[2 * i + 1], hb[i], lb[i], amax);
         const h8 xh = __builtin_bit_cast(h8, uint4{hb[0], hb[1], hb[2], hb[3]});
         const h8 xl = __builtin_bit_cast(h8, uint4{lb[0], lb[1], lb[2], lb[3]});
         f16x acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h, xh, b0, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h, xl, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0l, xh, acc, 0, 0, 0);
-        if (pp < G::M0) p0_store_planes<C, G::CS, LEAKY>(acc, p, khalf, s0h, s0l, a.alpha);
+        if (pp < G::M0) p0_store_planes<C, G::CS, LEAKY>(acc, p, khalf, s0h, s0l, a.alpha, amax);
       }
     }
     HBK_MARK(50);
     __syncthreads();
     HBK_MARK(41);
-    p0_stage12<WI, C, BAND, 1, LEAKY>(a, W1, s0h, s0l, s1h, s1l, nullptr, wave, r32, khalf);
+    p0_stage12<WI, C, BAND, 1, LEAKY>(a, W1, s0h, s0l, s1h, s1l, nullptr, wave, r32, khalf, amax);
     HBK_MARK(51);
     __syncthreads();
     HBK_MARK(42);
-    p0_stage12<WI, C, BAND, 2, LEAKY>(a, W2, s1h, s1l, nullptr, nullptr, s2, wave, r32, khalf);
+    p0_stage12<WI, C, BAND, 2, LEAKY>(a, W2, s1h, s1l, nullptr, nullptr, s2, wave, r32, khalf, amax);
     HBK_MARK(52);
     __syncthreads();
     HBK_MARK(43);
@@ -1165,6 +1198,7 @@ p0_chain_kernel(P0Args a) {
     }
     HBK_MARK(6);
   }
+  raise_range(a.range_flag, amax);
 }
 
 // ------------------------------------------------------------------- p1 ----
@@ -1185,6 +1219,7 @@ struct P1Args {
   int64_t src_img_stride;   // floats
   int H_in, H_out, n_bands;
   float alpha;
+  int* range_flag;          // set to 1 when an f16-split value reaches kF16Max
 };
 
 template <int WI, int CI, int BAND>
@@ -1226,13 +1261,13 @@ __device__ __forceinline__ P0W<KS> p1_load_w(const _Float16* w, const float* bia
 template <int KH, int KW, int CIN, int CSI, int WIN, int WOUT, int M, int KS, int CSO, bool F32OUT, bool LEAKY>
 __device__ __forceinline__ void p1_stage(const P0W<KS>& W, const _Float16* xh_, const _Float16* xl_,
                                          _Float16* oh, _Float16* ol, float* of, float alpha, int wave, int r32,
-                                         int khalf) {
+                                         int khalf, float& amax) {
   constexpr int T = (M + 31) / 32;
   auto epilogue = [&](int t, const f16x& acc) {
     const int pp = t * 32 + r32;
     if (pp >= M) return;
     if (!F32OUT) {
-      p0_store_planes<kP1C, CSO, LEAKY>(acc, pp, khalf, oh, ol, alpha);
+      p0_store_planes<kP1C, CSO, LEAKY>(acc, pp, khalf, oh, ol, alpha, amax);
     } else {
 #pragma unroll
       for (int q = 0; q < kP1C / 8; ++q) {
@@ -1299,6 +1334,7 @@ p1_chain_kernel(P1Args a) {
   const float alpha = a.alpha;
 
   P0W<G::KS1> W1 = p1_load_w<G::KS1>(a.w + G::WOFF1, a.bias, r32, khalf);
+  float amax = 0.f;
   for (int task = blockIdx.x; task < n_tasks; task += gridDim.x) {
     const int img = task / a.n_bands, band = task - img * a.n_bands;
     const int row0 = band * G::R4;
@@ -1314,10 +1350,10 @@ p1_chain_kernel(P1Args a) {
         const float* q = src + (static_cast<int64_t>(rr) * WI + x) * CI + 8 * c8;
         const float4 v0 = *reinterpret_cast<const float4*>(q), v1 = *reinterpret_cast<const float4*>(q + 4);
         uint32_t h[4], l[4];
-        split2_mix(v0.x, v0.y, h[0], l[0]);
-        split2_mix(v0.z, v0.w, h[1], l[1]);
-        split2_mix(v1.x, v1.y, h[2], l[2]);
-        split2_mix(v1.z, v1.w, h[3], l[3]);
+        split2_mix(v0.x, v0.y, h[0], l[0], amax);
+        split2_mix(v0.z, v0.w, h[1], l[1], amax);
+        split2_mix(v1.x, v1.y, h[2], l[2], amax);
+        split2_mix(v1.z, v1.w, h[3], l[3], amax);
         const int o = pos * G::CSI + 8 * c8;
         *reinterpret_cast<uint4*>(inh + o) = uint4{h[0], h[1], h[2], h[3]};
         *reinterpret_cast<uint4*>(inl + o) = uint4{l[0], l[1], l[2], l[3]};
@@ -1326,19 +1362,19 @@ p1_chain_kernel(P1Args a) {
     __syncthreads();
     P0W<G::KS> W2 = p1_load_w<G::KS>(a.w + G::WOFF2, a.bias + 32, r32, khalf);
     p1_stage<1, 3, CI, G::CSI, G::W0, G::W1, G::M1, G::KS1, G::CS, false, LEAKY>(W1, inh, inl, s1h, s1l, nullptr,
-                                                                                  alpha, wave, r32, khalf);
+                                                                                  alpha, wave, r32, khalf, amax);
     __syncthreads();
     P0W<G::KS> W3 = p1_load_w<G::KS>(a.w + G::WOFF3, a.bias + 64, r32, khalf);
     p1_stage<3, 1, C, G::CS, G::W1, G::W2, G::M2, G::KS, G::CS, false, LEAKY>(W2, s1h, s1l, s2h, s2l, nullptr,
-                                                                               alpha, wave, r32, khalf);
+                                                                               alpha, wave, r32, khalf, amax);
     __syncthreads();
     P0W<G::KS> W4 = p1_load_w<G::KS>(a.w + G::WOFF4, a.bias + 96, r32, khalf);
     p1_stage<1, 3, C, G::CS, G::W2, G::W3, G::M3, G::KS, G::CS, false, LEAKY>(W3, s2h, s2l, s3h, s3l, nullptr,
-                                                                               alpha, wave, r32, khalf);
+                                                                               alpha, wave, r32, khalf, amax);
     __syncthreads();
     W1 = p1_load_w<G::KS1>(a.w + G::WOFF1, a.bias, r32, khalf);  // the next task's stage 1
     p1_stage<3, 1, C, G::CS, G::W3, G::W4, G::M4, G::KS, G::CS, true, LEAKY>(W4, s3h, s3l, nullptr, nullptr, s4,
-                                                                              alpha, wave, r32, khalf);
+                                                                              alpha, wave, r32, khalf, amax);
     __syncthreads();
     // 2x2 max-pool of the stage-4 rows -> BAND output rows
     {
@@ -1362,6 +1398,7 @@ p1_chain_kernel(P1Args a) {
       }
     }
   }
+  raise_range(a.range_flag, amax);
 }
 
 // ------------------------------------------------------------------ host ----
@@ -1441,6 +1478,7 @@ struct hbk_embed_plan {
   bool split_f16 = true;
   double prefix_macs = 0, tail_macs = 0;
   hbk::Program clip_prog, win_prog;
+  int* d_range = nullptr;  // range flag of the split-f16 kernels (hbk_embed_range_status)
 };
 
 namespace hbk {
@@ -2121,7 +2159,8 @@ void assign_buffers(Program& prog, int64_t units_per_first_img_ratio) {
 
 int run_program(const Program& prog, const float* in, int64_t n_units, int64_t in_unit_stride,
                 float* out, int64_t out_unit_floats, float* ws, int64_t chunk, hipStream_t stream,
-                const std::vector<int64_t>& imgs_per_unit, const std::vector<int64_t>& buf_unit_floats) {
+                const std::vector<int64_t>& imgs_per_unit, const std::vector<int64_t>& buf_unit_floats,
+                int* range_flag) {
   for (int64_t u0 = 0; u0 < n_units; u0 += chunk) {
     const int64_t nu = std::min(chunk, n_units - u0);
     float* bufs[2] = {ws, ws + chunk * buf_unit_floats[0]};
@@ -2129,6 +2168,7 @@ int run_program(const Program& prog, const float* in, int64_t n_units, int64_t i
       const ChainPlan& c = prog.chains[k];
       if (c.p0fn) {
         P0Args pa = c.p0;
+        pa.range_flag = range_flag;
         pa.in = c.src_buf < 0 ? in + u0 * in_unit_stride : bufs[c.src_buf];
         pa.src_img_stride = c.src_buf < 0 ? in_unit_stride : c.x.src_clip_stride;
         pa.out = c.dst_buf < 0 ? out + u0 * out_unit_floats : bufs[c.dst_buf];
@@ -2146,6 +2186,7 @@ int run_program(const Program& prog, const float* in, int64_t n_units, int64_t i
       }
       if (c.p1fn) {
         P1Args pa = c.p1;
+        pa.range_flag = range_flag;
         pa.in = c.src_buf < 0 ? in + u0 * in_unit_stride : bufs[c.src_buf];
         pa.src_img_stride = c.src_buf < 0 ? in_unit_stride : c.x.src_clip_stride;
         pa.out = c.dst_buf < 0 ? out + u0 * out_unit_floats : bufs[c.dst_buf];
@@ -2163,6 +2204,7 @@ int run_program(const Program& prog, const float* in, int64_t n_units, int64_t i
       }
       if (c.split) {
         XArgs x = c.x;
+        x.range_flag = range_flag;
         if (c.src_buf < 0) {
           x.in = in + u0 * in_unit_stride;
           x.src_clip_stride = in_unit_stride;
@@ -2229,6 +2271,11 @@ int hbk_embed_plan_create_ex(const hbk_graph_op* ops, int32_t n_ops, int32_t in_
   p->in_h = in_h;
   p->in_w = in_w;
   p->split_f16 = precision == HBK_PREC_SPLIT_F16;
+  {
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&p->d_range), sizeof(int));
+    if (e == hipSuccess) e = hipMemset(p->d_range, 0, sizeof(int));
+    if (e != hipSuccess) return fail(hip_error(e, "hipMalloc range flag"));
+  }
   for (int i = 0; i < n_win; ++i) {
     if (win_start[i] < 0) return fail(arg_error("negative window start"));
     p->starts.push_back(win_start[i]);
@@ -2243,6 +2290,13 @@ int hbk_embed_plan_create_ex(const hbk_graph_op* ops, int32_t n_ops, int32_t in_
       if (o.cin != d.c || o.cout <= 0 || !o.weight || !o.bias) return fail(arg_error("bad conv op"));
       op.w.assign(o.weight, o.weight + size_t(o.kh) * o.kw * o.cin * o.cout);
       op.b.assign(o.bias, o.bias + o.cout);
+      if (p->split_f16)
+        for (float w : op.w)
+          if (!(std::fabs(w) < kF16Max)) {
+            set_error("hbk: op %d has a weight |w| >= 65504 (or NaN), outside the split-f16 range; "
+                      "use HBK_PREC_EXACT_F32", i);
+            return fail(HBK_ERR_UNSUPPORTED);
+          }
       d = Dims{d.h - o.kh + 1, d.w - o.kw + 1, o.cout};
     } else if (o.kind == HBK_OP_MAXPOOL) {
       d = Dims{d.h / o.kh, d.w / o.kw, d.c};
@@ -2333,6 +2387,7 @@ int hbk_embed_plan_destroy(hbk_embed_plan* p) {
       (void)hipFree(c.d_blob);
       if (c.d_p0) (void)hipFree(c.d_p0);
     }
+  if (p->d_range) (void)hipFree(p->d_range);
   delete p;
   return HBK_OK;
 }
@@ -2408,7 +2463,7 @@ int hbk_embed_clips(const hbk_embed_plan* p, const float* mel, int64_t n_clips, 
   const int64_t chunk = std::min<int64_t>(n_clips, kChunkClips);
   return run_program(p->clip_prog, mel, n_clips, mel_clip_stride, out,
                      int64_t(p->starts.size()) * p->out_dim, static_cast<float*>(workspace), chunk,
-                     as_stream(stream), imgs, bufs);
+                     as_stream(stream), imgs, bufs, p->d_range);
 }
 
 int hbk_embed_windows(const hbk_embed_plan* p, const float* windows, int64_t n, float* out,
@@ -2425,7 +2480,19 @@ int hbk_embed_windows(const hbk_embed_plan* p, const float* windows, int64_t n, 
   program_geometry(p->win_prog, false, 1, imgs, bufs);
   const int64_t chunk = std::min<int64_t>(n, int64_t(kChunkClips));
   return run_program(p->win_prog, windows, n, int64_t(p->in_h) * p->in_w, out, p->out_dim,
-                     static_cast<float*>(workspace), chunk, as_stream(stream), imgs, bufs);
+                     static_cast<float*>(workspace), chunk, as_stream(stream), imgs, bufs, p->d_range);
+}
+
+int hbk_embed_range_status(const hbk_embed_plan* p, int32_t* tripped, int32_t reset, void* stream) {
+  using namespace hbk;
+  if (!p || !tripped) return arg_error("plan/tripped is NULL");
+  int32_t h = 0;
+  hipError_t e = hipMemcpyAsync(&h, p->d_range, sizeof(int32_t), hipMemcpyDeviceToHost, as_stream(stream));
+  if (e == hipSuccess) e = hipStreamSynchronize(as_stream(stream));
+  if (e == hipSuccess && reset && h) e = hipMemsetAsync(p->d_range, 0, sizeof(int32_t), as_stream(stream));
+  if (e != hipSuccess) return hip_error(e, "hbk_embed_range_status");
+  *tripped = h;
+  return HBK_OK;
 }
 
 }  // extern "C"

@@ -90,8 +90,8 @@ class SpeechEmbeddingModel:
     def device(self) -> torch.device:
         return _native.require_device(self.device_id)
 
-    def plan(self, starts: Sequence[int] = (0,)) -> EmbedPlan:
-        return embed_plan(self.device, starts, self.graph)
+    def plan(self, starts: Sequence[int] = (0,), precision: Optional[str] = None) -> EmbedPlan:
+        return embed_plan(self.device, starts, self.graph, precision)
 
     def load(self) -> None:
         self.plan()
@@ -102,8 +102,24 @@ class SpeechEmbeddingModel:
 
     def __call__(self, spectrograms: np.ndarray[Any, Any]) -> np.ndarray[Any, Any]:
         x = torch.as_tensor(np.ascontiguousarray(spectrograms, dtype=np.float32), device=self.device)
-        out = embed_windows(x.reshape(x.shape[0], x.shape[1], x.shape[2]), self.plan())
+        x = x.reshape(x.shape[0], x.shape[1], x.shape[2])
+        out = range_checked(lambda prec: embed_windows(x, self.plan(precision=prec)),
+                            lambda: [self.plan()])
         return out.reshape(out.shape[0], 1, 1, -1).cpu().numpy().squeeze()
+
+
+def range_checked(run: Callable[[Optional[str]], Any], plans: Callable[[], List[EmbedPlan]]) -> Any:
+    """run(None) on the default plans; if a split-f16 plan's range guard
+    tripped (an activation reached fp16's 65504, include/hbk.h
+    hbk_embed_range_status), warn and return run('exact') instead. Waits for
+    the device: for the host-returning entry points only."""
+    out = run(None)
+    tripped = [p.range_tripped() for p in plans() if p.precision == "split"]
+    if any(tripped):
+        logger.warning("speech embedding: an activation left the split-f16 range (|x| >= 65504); "
+                       "recomputing this call in exact f32")
+        out = run("exact")
+    return out
 
 
 class SpeechEmbeddings:
@@ -147,7 +163,8 @@ class SpeechEmbeddings:
         x = torch.as_tensor(np.ascontiguousarray(spectrograms, dtype=np.float32), device=self.device)
         wins = x.unfold(1, window_size, window_stride)[:, :n]        # [b, n, m, ws]
         wins = wins.permute(0, 1, 3, 2).reshape(b * n, window_size, m)
-        out = embed_windows(wins, self.embeddings.plan())
+        out = range_checked(lambda prec: embed_windows(wins, self.embeddings.plan(precision=prec)),
+                            lambda: [self.embeddings.plan()])
         if on_progress is not None:
             on_progress(b * n, b * n)
         return out.reshape(b, n, embedding_dim).cpu().numpy()
@@ -170,11 +187,13 @@ class SpeechEmbeddings:
     def featurize(self, audio: torch.Tensor, audio_window_size: int = 17280,
                   audio_window_stride: int = 1920, window_size: int = 76, window_stride: int = 8,
                   in_scale: float = 32767.0, remove_nan: bool = True,
-                  return_frames: bool = False, out: Optional[torch.Tensor] = None):
+                  return_frames: bool = False, out: Optional[torch.Tensor] = None,
+                  check_range: bool = False):
         """audio [B, T] float in [-1, 1] on the device -> embeddings [B, n, 96]
         (and the unique mel frames [B, F, 32] if ``return_frames``); ``out``:
         an optional [B, n, 96] f32 destination (kept when no NaN row needs
-        replacing)."""
+        replacing). ``check_range``: wait for the device and recompute in exact
+        f32 if a split-f16 kernel saw |x| >= 65504 (range_checked)."""
         dev = audio.device
         b, t = audio.shape
         starts, f_aw, f_total = self.window_plan(t, audio_window_size, audio_window_stride,
@@ -183,18 +202,24 @@ class SpeechEmbeddings:
             raise ValueError("need at least one array to concatenate")
         mplan = default_mel_plan(dev, in_scale)
         frames = mel_frames(audio, mplan, f_total)
-        if len(starts) <= 32:  # one plan covers every window: write straight into the output
-            off = min(starts)
-            plan = embed_plan(dev, [s - off for s in starts])
-            emb = embed_clips(frames[:, off:off + plan.seq_frames], plan, out=out)
-        else:
+        groups = [starts[s0:s0 + 32] for s0 in range(0, len(starts), 32)]  # hbk plans take <= 32 windows
+
+        def run(prec: Optional[str]) -> torch.Tensor:
+            if len(groups) == 1:  # one plan covers every window: write straight into the output
+                off = min(starts)
+                plan = embed_plan(dev, [s - off for s in starts], precision=prec)
+                return embed_clips(frames[:, off:off + plan.seq_frames], plan, out=out)
             emb = out if out is not None else torch.empty((b, len(starts), 96), dtype=torch.float32, device=dev)
-            for s0 in range(0, len(starts), 32):  # hbk plans take <= 32 windows
-                st = starts[s0:s0 + 32]
+            for s0, st in zip(range(0, len(starts), 32), groups):
                 off = min(st)
-                plan = embed_plan(dev, [s - off for s in st])
-                sub = frames[:, off:off + plan.seq_frames]
-                emb[:, s0:s0 + len(st)] = embed_clips(sub, plan)
+                plan = embed_plan(dev, [s - off for s in st], precision=prec)
+                emb[:, s0:s0 + len(st)] = embed_clips(frames[:, off:off + plan.seq_frames], plan)
+            return emb
+
+        if check_range:
+            emb = range_checked(run, lambda: [embed_plan(dev, [s - min(st) for s in st]) for st in groups])
+        else:
+            emb = run(None)
         if remove_nan:
             emb = _replace_nan_rows(emb)
         return (emb, frames) if return_frames else emb
@@ -220,7 +245,7 @@ class SpeechEmbeddings:
             raise ValueError("the MI355X featurizer is built for 32 mel bins and 96-d embeddings")
         emb, frames = self.featurize(x.contiguous(), audio_window_size, audio_window_stride,
                                      window_size, window_stride, in_scale=scale,
-                                     remove_nan=False, return_frames=True)
+                                     remove_nan=False, return_frames=True, check_range=True)
         b, n = emb.shape[0], emb.shape[1]
         if on_spectrogram_progress is not None:
             on_spectrogram_progress(b, b)

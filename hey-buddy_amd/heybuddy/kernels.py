@@ -187,6 +187,18 @@ class EmbedPlan:
         self._ws: torch.Tensor | None = None
         self.id = _register(self)
 
+    def range_tripped(self, reset: bool = True) -> bool:
+        """Range guard of a 'split' plan (hbk_embed_range_status): True if a
+        kernel of this plan split an activation with |x| >= 65504 since the
+        last reset, i.e. outputs since then are not f32-accurate. Waits for the
+        current stream. An 'exact' plan never trips."""
+        t = ctypes.c_int32()
+        with torch.cuda.device(self.device):
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            check(lib().hbk_embed_range_status(self._handle, ctypes.byref(t), int(reset), ctypes.c_void_p(stream)),
+                  "hbk_embed_range_status")
+        return bool(t.value)
+
     @property
     def macs_per_clip(self) -> float:
         """Algorithmic MACs of the clip path (shared prefix + per-window tail)."""

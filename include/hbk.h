@@ -120,7 +120,10 @@ int hbk_embed_plan_destroy(hbk_embed_plan* plan);
  *   held as an fp16 pair x = hi + 2^-11 lo and each product as
  *   hi*hi + 2^-11 (hi*lo + lo*hi) on v_mfma_f32_32x32x16_f16 with f32
  *   accumulation: ~2^-21 relative per operand (f32 is 2^-24), at 16x the MFMA
- *   rate of f32 input. Requires |activations| and |weights| < 65504.
+ *   rate of f32 input. Requires |activations| and |weights| < 65504: a plan
+ *   whose weights reach it is refused (HBK_ERR_UNSUPPORTED: use EXACT_F32), and
+ *   every kernel that splits an activation raises the plan's range flag when one
+ *   reaches it (hbk_embed_range_status).
  * EXACT_F32: v_mfma_f32_16x16x4f32, bitwise an fmaf chain in f32. */
 typedef enum { HBK_PREC_SPLIT_F16 = 0, HBK_PREC_EXACT_F32 = 1 } hbk_precision;
 int hbk_embed_plan_create_ex(const hbk_graph_op* ops, int32_t n_ops, int32_t in_h, int32_t in_w,
@@ -145,6 +148,13 @@ int hbk_embed_clips(const hbk_embed_plan* plan, const float* mel, int64_t n_clip
 /* Per-window API of the reference: windows [n, in_h, in_w] f32 -> out [n, out_dim]. */
 int hbk_embed_windows(const hbk_embed_plan* plan, const float* windows, int64_t n, float* out,
                       void* workspace, int64_t workspace_bytes, void* stream);
+
+/* Range guard of SPLIT_F16 plans (no reference counterpart: the ONNX graph runs
+ * in f32). *tripped = 1 if any split kernel of this plan saw an activation with
+ * |x| >= 65504 since the flag was last cleared (those outputs are not
+ * f32-accurate: recompute them with an EXACT_F32 plan), else 0. Waits for the
+ * work queued on `stream`; reset != 0 clears the flag. */
+int hbk_embed_range_status(const hbk_embed_plan* plan, int32_t* tripped, int32_t reset, void* stream);
 
 /* ------------------------------------------------------------------------ *
  * Wake-word classifier: gated MLP forward and the fused train step

@@ -216,3 +216,46 @@ def test_featurize_across_the_16384_clip_chunk():
     ref = _oracle_clip_embeddings(se20_graph(), mel_ref)
     ok, worst = _close(out[pick].cpu().numpy(), ref)
     assert out.shape == (n, 16, 96) and ok, f"max |diff| {worst}"
+
+
+@pytest.mark.gpu
+def test_embed_split_range_guard():
+    """Split-f16 range guard (include/hbk.h, hbk_embed_range_status): every
+    kernel that splits an activation into f16 hi / lo raises the plan's flag
+    at |x| >= 65504; the host-returning entry points then recompute in exact
+    f32. A plan whose weights leave the f16 range is refused."""
+    from heybuddy.embedding_graph import Conv, Graph, se20_graph
+    from heybuddy.embeddings import SpeechEmbeddingModel
+    from heybuddy.kernels import EmbedPlan
+    from heybuddy._native import HBKError
+    g = se20_graph()
+    split, exact = EmbedPlan(g, precision="split"), EmbedPlan(g, precision="exact")
+    rng = np.random.default_rng(4)
+    wins = (rng.standard_normal((9, 76, 32)) * 2 + 6).astype(np.float32)
+    mel = _mel_clips(2, seed=5)
+    split.windows(torch.from_numpy(wins).cuda())
+    split.clips(torch.from_numpy(mel).cuda())
+    assert not split.range_tripped()  # realistic inputs stay inside the range
+    # per-window path (generic kernel) and clip path (p0 / p1 / x3) with inputs past 65504
+    split.windows(torch.from_numpy(wins * 2e4).cuda())
+    assert split.range_tripped()
+    assert not split.range_tripped()  # the read cleared it
+    split.clips(torch.from_numpy(mel * 1e5).cuda())
+    assert split.range_tripped()
+    assert not exact.range_tripped()
+    # the reference-shaped entry point returns the exact-f32 result when tripped
+    model = SpeechEmbeddingModel(device_id=0, graph=g)
+    big = wins * 2e4
+    out = model(big[:, :, :, None])
+    ref = exact.windows(torch.from_numpy(big).cuda()).cpu().numpy()
+    np.testing.assert_array_equal(out, ref)
+    # weights outside the f16 range: refused in split, fine in exact
+    ops = list(g.ops)
+    c0 = ops[0]
+    w = c0.weight.copy()
+    w.flat[0] = 7e4
+    ops[0] = Conv(c0.kh, c0.kw, c0.cin, c0.cout, w, c0.bias, act=c0.act, alpha=c0.alpha)
+    g_big = Graph(ops, g.in_shape, name="se20-bigw")
+    with pytest.raises(HBKError, match="65504"):
+        EmbedPlan(g_big, precision="split")
+    EmbedPlan(g_big, precision="exact")

@@ -14,6 +14,8 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "hey-buddy_amd")]
 os.environ.setdefault("HBK_DEBUG_EMBED", "1")
 if "--phase" in sys.argv:
     os.environ["HBK_LIB"] = os.path.join(ROOT, "hey-buddy_amd", "lib", "libhbk_phase.so")
+if "--lib" in sys.argv:  # A/B against another build: prototypes it does not export are dropped
+    os.environ["HBK_LIB"] = os.path.abspath(sys.argv[sys.argv.index("--lib") + 1])
 
 import torch  # noqa: E402
 
@@ -26,9 +28,16 @@ def main():
     ap.add_argument("--clips", type=int, default=16384)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--precision", default="both")
+    ap.add_argument("--lib", default=None, help="load this libhbk build instead (A/B timing)")
     ap.add_argument("--phase", action="store_true",
                     help="load lib/libhbk_phase.so and print per-chain phase cycles (wave 0 of each block)")
     a = ap.parse_args()
+    if a.lib:
+        import ctypes
+        from heybuddy import _native
+        h = ctypes.CDLL(os.environ["HBK_LIB"])
+        for name in [n for n in _native._PROTOS if not hasattr(h, n)]:
+            _native._PROTOS.pop(name)
     g = se20_graph()
     mel = (torch.randn((a.clips, 141, 32), device="cuda") * 2 + 1).contiguous()
     precs = ["split", "exact"] if a.precision == "both" else [a.precision]
