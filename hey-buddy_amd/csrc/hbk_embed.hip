@@ -82,6 +82,9 @@ __device__ __forceinline__ void conv_stage(const float* __restrict__ X, float* _
   const int img_pos = ho * wo, M = G * img_pos;
   const int nrb = (M + 15) >> 4;
   const int r16 = lane & 15, kq = lane >> 4;
+  // output channels in groups of NB 16-column blocks (more than NB * 16 channels: several passes)
+  const int nblk = (S.cout + 15) >> 4;
+  for (int cb = 0; cb < nblk; cb += NB)
   for (int rb0 = wave * RB; rb0 < nrb; rb0 += kWaves * RB) {
     int moff[RB];
 #pragma unroll
@@ -98,7 +101,7 @@ __device__ __forceinline__ void conv_stage(const float* __restrict__ X, float* _
     for (int r = 0; r < RB; ++r)
 #pragma unroll
       for (int c = 0; c < NB; ++c) acc[r][c] = f4{0.f, 0.f, 0.f, 0.f};
-    const float* wp = Wst + kq * wstride + r16;
+    const float* wp = Wst + kq * wstride + cb * 16 + r16;
 #pragma unroll 2
     for (int ks = 0; ks < S.ksteps; ++ks) {
       const int koff = ktab[ks * 4 + kq];
@@ -106,7 +109,7 @@ __device__ __forceinline__ void conv_stage(const float* __restrict__ X, float* _
 #pragma unroll
       for (int r = 0; r < RB; ++r) av[r] = X[moff[r] + koff];
 #pragma unroll
-      for (int c = 0; c < NB; ++c) bv[c] = wp[ks * 4 * wstride + c * 16];
+      for (int c = 0; c < NB; ++c) bv[c] = wp[ks * 4 * wstride + min(c, nblk - 1 - cb) * 16];
 #pragma unroll
       for (int r = 0; r < RB; ++r)
 #pragma unroll
@@ -116,7 +119,7 @@ __device__ __forceinline__ void conv_stage(const float* __restrict__ X, float* _
     // C/D layout: row (lane >> 4) * 4 + i, column lane & 15
 #pragma unroll
     for (int c = 0; c < NB; ++c) {
-      const int n = c * 16 + r16;
+      const int n = (cb + c) * 16 + r16;
       if (n >= S.cout) continue;
       const float bb = bias[n];
 #pragma unroll
@@ -443,12 +446,13 @@ __device__ __forceinline__ void xstage(const _Float16* __restrict__ Xh, const _F
                                        float* __restrict__ Yf, const _Float16* __restrict__ Wh,
                                        const int* __restrict__ kt, const float* __restrict__ bias, int M,
                                        int hA, int wA, int ho, int wo, const XStage& S, int lane, int wave,
-                                       int* flag) {
+                                       int* flag, int cb) {
+  // output channels 32 (cb + c) + ..., c < NB: one group of at most 3 blocks of a wider stage
   const int img_pos = ho * wo;
   const int nrb = (M + 31) >> 5;
   const int r32 = lane & 31, khalf = lane >> 5;
-  const _Float16* wp = Wh + r32 * S.wrow + khalf * 8;
   const int cstride = 32 * S.wrow;
+  const _Float16* wp = Wh + cb * cstride + r32 * S.wrow + khalf * 8;
   // input position of output m = (g, y, x): with ytot = g ho + y = m / wo,
   // (g hA + y) wA + x = m + ytot (wA - wo) + g (hA - ho) wA
   const float inv_wo = 1.f / static_cast<float>(wo), inv_ho = 1.f / static_cast<float>(ho);
@@ -459,7 +463,7 @@ __device__ __forceinline__ void xstage(const _Float16* __restrict__ Xh, const _F
   for (int c = 0; c < NB; ++c)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float4 b = *reinterpret_cast<const float4*>(bias + c * 32 + 8 * q + 4 * khalf);
+      const float4 b = *reinterpret_cast<const float4*>(bias + (cb + c) * 32 + 8 * q + 4 * khalf);
       bl[c][4 * q] = b.x;
       bl[c][4 * q + 1] = b.y;
       bl[c][4 * q + 2] = b.z;
@@ -546,8 +550,8 @@ __device__ __forceinline__ void xstage(const _Float16* __restrict__ Xh, const _F
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           // coutr is a multiple of 8, so this test is the same for both lane halves (uniform)
-          if (c * 32 + 8 * q >= S.coutr) continue;
-          const int n0 = c * 32 + 8 * q + 4 * khalf;
+          if ((cb + c) * 32 + 8 * q >= S.coutr) continue;
+          const int n0 = (cb + c) * 32 + 8 * q + 4 * khalf;
           // (the bias is the first MFMA's accumulator input)
           float v[4] = {acc[r][c][4 * q], acc[r][c][4 * q + 1], acc[r][c][4 * q + 2], acc[r][c][4 * q + 3]};
           if (S.act == 1) {  // LeakyReLU, 0 <= alpha <= 1: max(v, alpha v) (NaN stays NaN)
@@ -842,15 +846,28 @@ conv_chain_x3_kernel(XArgs a) {
       const int* kts = kt + S.kt_off;
       const float* bs = Bl + S.b_off;
       float* Yf = s + 1 == a.n_stages ? reinterpret_cast<float*>(nxt) : nullptr;
+      // RB x NB tiles of one 16-register accumulator each. NBMAX 4 (plans with
+      // a stage wider than 96 channels): groups of 3 blocks, each re-reading
+      // the stage input (a separate instantiation: the loop costs the others
+      // spills)
       if (HBK_SKIP(0)) {
-      } else
-      // RB x NB tiles of one 16-register accumulator each
-      if (NBMAX >= 3 && S.nblk == 3)
-        xstage<3, 1>(Xh, Xl, Yh, Yl, Yf, Wst, kts, bs, M, hA, wA, ho, wo, S, lane, wave, a.range_flag);
-      else if (NBMAX >= 2 && S.nblk == 2)
-        xstage<2, 2>(Xh, Xl, Yh, Yl, Yf, Wst, kts, bs, M, hA, wA, ho, wo, S, lane, wave, a.range_flag);
-      else
-        xstage<1, 2>(Xh, Xl, Yh, Yl, Yf, Wst, kts, bs, M, hA, wA, ho, wo, S, lane, wave, a.range_flag);
+      } else if constexpr (NBMAX > 3) {
+        for (int cb = 0; cb < S.nblk; cb += 3) {
+          const int nb = min(3, S.nblk - cb);
+          if (nb == 3)
+            xstage<3, 1>(Xh, Xl, Yh, Yl, Yf, Wst, kts, bs, M, hA, wA, ho, wo, S, lane, wave, a.range_flag, cb);
+          else if (nb == 2)
+            xstage<2, 2>(Xh, Xl, Yh, Yl, Yf, Wst, kts, bs, M, hA, wA, ho, wo, S, lane, wave, a.range_flag, cb);
+          else
+            xstage<1, 2>(Xh, Xl, Yh, Yl, Yf, Wst, kts, bs, M, hA, wA, ho, wo, S, lane, wave, a.range_flag, cb);
+        }
+      } else if (NBMAX >= 3 && S.nblk == 3) {
+        xstage<3, 1>(Xh, Xl, Yh, Yl, Yf, Wst, kts, bs, M, hA, wA, ho, wo, S, lane, wave, a.range_flag, 0);
+      } else if (NBMAX >= 2 && S.nblk == 2) {
+        xstage<2, 2>(Xh, Xl, Yh, Yl, Yf, Wst, kts, bs, M, hA, wA, ho, wo, S, lane, wave, a.range_flag, 0);
+      } else {
+        xstage<1, 2>(Xh, Xl, Yh, Yl, Yf, Wst, kts, bs, M, hA, wA, ho, wo, S, lane, wave, a.range_flag, 0);
+      }
       unsigned char* t = cur;
       cur = nxt;
       nxt = t;
@@ -1458,8 +1475,7 @@ KernelFn pick_kernel(int nb, bool wg) {
     case 3: return wg ? kernel_for<3, 4, true>() : kernel_for<3, 4, false>();
     case 4: return wg ? kernel_for<4, 2, true>() : kernel_for<4, 2, false>();
     case 5: return wg ? kernel_for<5, 2, true>() : kernel_for<5, 2, false>();
-    case 6: return wg ? kernel_for<6, 2, true>() : kernel_for<6, 2, false>();
-    default: return nullptr;
+    default: return wg ? kernel_for<6, 2, true>() : kernel_for<6, 2, false>();
   }
 }
 
@@ -1504,7 +1520,7 @@ XKernelFn pick_xkernel(int nb, bool wg) {
     case 1: return wg ? xkernel_for<1, true>() : xkernel_for<1, false>();
     case 2: return wg ? xkernel_for<2, true>() : xkernel_for<2, false>();
     case 3: return wg ? xkernel_for<3, true>() : xkernel_for<3, false>();
-    default: return nullptr;
+    default: return wg ? xkernel_for<4, true>() : xkernel_for<4, false>();  // > 3 blocks: groups of 3
   }
 }
 
@@ -1746,10 +1762,6 @@ int layout_split(const std::vector<OpInfo>& ops, const std::vector<int>& stage_o
   cp.wg = !resident;
   cp.split = true;
   cp.xfn = pick_xkernel(nbmax, cp.wg);
-  if (!cp.xfn) {
-    set_error("hbk: conv with more than 96 output channels is not supported");
-    return HBK_ERR_UNSUPPORTED;
-  }
   // device blob: weights (fp16), biases (f32), group offsets (int)
   const size_t wsz = wb.size() * 2, bsz = ((bb.size() * 4 + 15) & ~size_t(15));
   const size_t ksz = (kt.size() * 4 + 15) & ~size_t(15), isz = i2c.size() * 4;
@@ -2035,11 +2047,7 @@ int build_segment(const std::vector<OpInfo>& ops, int o0, int o1, Dims in, int i
       macs += double(h) * w * op.cout * S.K;
       cin = op.cout;
     }
-    if (nb > 6) {
-      set_error("hbk: conv with more than 96 output channels is not supported");
-      return HBK_ERR_UNSUPPORTED;
-    }
-    cp.nb = nb;
+    cp.nb = nb;  // > 6 blocks: the 6-block kernel loops over channel groups
     a.wstride = nb * 16 + ((nb * 16) % 32 == 0 ? 16 : 0);  // kq rows on different bank halves
     // pack weights: per stage [ksteps*4][wstride] then bias [nb*16]
     std::vector<float> blob;

@@ -181,6 +181,38 @@ def test_embed_generic_graph_parity(precision):
     assert out.shape == (23, 33) and ok, f"max |diff| {worst}"
 
 
+def _wide_graph(seed=13):
+    """Convs wider than 96 output channels (130 inside a chain, 100 at a
+    chain's end): the kernels run them in groups of output-channel blocks."""
+    from heybuddy.embedding_graph import Conv, Graph, MaxPool
+    rng = np.random.default_rng(seed)
+
+    def conv(kh, kw, ci, co, act="leaky_relu"):
+        w = rng.standard_normal((kh, kw, ci, co)) * np.sqrt(2.0 / (kh * kw * ci))
+        return Conv(kh, kw, ci, co, w.astype(np.float32), (rng.standard_normal(co) * 0.1).astype(np.float32),
+                    act=act)
+
+    ops = [conv(3, 3, 1, 40), conv(1, 3, 40, 130), MaxPool(2, 2), conv(3, 3, 130, 100), MaxPool(1, 2),
+           conv(7, 1, 100, 33, act=None)]
+    return Graph(ops, (20, 12, 1), name="wide")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_embed_wide_channels_parity(precision):
+    """More than 96 output channels (round 1 refused them), against the oracle."""
+    from heybuddy.kernels import EmbedPlan
+    g = _wide_graph()
+    assert g.shapes()[-1] == (1, 1, 33)
+    plan = EmbedPlan(g, starts=(0,), device=0, precision=precision)
+    rng = np.random.default_rng(6)
+    wins = rng.standard_normal((29, 20, 12)).astype(np.float32)
+    out = plan.windows(torch.from_numpy(wins).cuda()).cpu().numpy()
+    ref = oemb.run_graph(g, wins)
+    ok, worst = _close(out, ref)
+    assert out.shape == (29, 33) and ok, f"max |diff| {worst}"
+
+
 @pytest.mark.gpu
 def test_embed_split_precision_margin():
     """The split path sits orders of magnitude inside the tolerance: relative
