@@ -130,11 +130,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # HBK_BENCH_REHEARSE=1: every rank on cuda:0 over gloo, so that the N > 1
+    # code paths (shards, the per-step all-reduce, max-over-ranks timing) run on
+    # a one-GPU box; its numbers are not a measurement
+    rehearse = os.environ.get("HBK_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from heybuddy.synthetic import seed_for
     setup = {2: setup_featurize, 3: setup_featurize, 4: setup_train, 5: setup_e2e}[args.config]
