@@ -219,7 +219,8 @@ def setup_featurize(args, dev, rank, world, seed):
                              background_noise_prob=1.0, reverb_prob=1.0,
                              colored_noise_prob=0.25 if args.full_augment else 0.0,
                              tanh_distortion_prob=0.25 if args.full_augment else 0.0,
-                             seven_band_prob=0.25 if args.full_augment else 0.0)  # configs[2]: reverb + noise (+ gain)
+                             seven_band_prob=0.25 if args.full_augment else 0.0,
+                             band_stop_prob=0.25 if args.full_augment else 0.0)  # configs[2]: reverb + noise (+ gain)
         aug_out = torch.empty((n, AUG_T), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
     stages = (["augment"] if augment else []) + ["mel", "embed"]
@@ -498,7 +499,7 @@ def setup_e2e(args, dev, rank, world, seed):
     lens = np.concatenate([pos_len, adv_len]).astype(np.int32)
     aug = AugmentedAudioGenerator([], device_id=dev.index, augmentation_dataset=noise_bank(64, seed=seed + 2),
                                   impulse_response_dataset=impulse_responses(32, seed=seed + 3), batch_size=128,
-                                  pitch_shift_prob=0.0, band_stop_prob=0.0)  # EQ, tanh, colored, gain at defaults
+                                  pitch_shift_prob=0.0)  # EQ, tanh, band-stop, colored, gain at defaults
     mplan = default_mel_plan(dev, 32767.0)
     eplan = embed_plan(dev, WINDOW_STARTS)
     pool = torch.empty((n, len(WINDOW_STARTS), 96), dtype=torch.float32, device=dev)
@@ -606,10 +607,12 @@ def setup_e2e(args, dev, rank, world, seed):
 
     def roofline(name, ms, pmc):
         if name == "augment":
-            return roof("place_kernel + eq_kernel + tanh_distortion_kernel + colored_noise_kernel + augment_kernel "
-                        "(placement, 7-band EQ, tanh, colored noise, gain + noise mix + 23040-pt FFT reverb)", "hbm",
+            return roof("place_kernel + eq_kernel + tanh_distortion_kernel + band_stop_kernel + colored_noise_kernel + "
+                        "augment_kernel (placement, 7-band EQ, tanh, band-stop, colored noise, gain + noise mix + "
+                        "23040-pt FFT reverb)", "hbm",
                         n * AUG_T * 4 * 2, ms, "GB/s", load_traffic(pmc, ("place_kernel", "augment_kernel", "eq_kernel",
-                                                                          "colored_noise", "tanh_distortion")),
+                                                                          "band_stop", "colored_noise",
+                                                                          "tanh_distortion")),
                         algorithmic_bytes_per_clip=AUG_T * 4 * 2,
                         bytes_basis="placed clip written + augmented clip written in place (92,160 B each); "
                                     "the chain's re-reads of the in-place buffer are not counted")
@@ -682,8 +685,8 @@ def setup_e2e(args, dev, rank, world, seed):
         "data": "synthetic TTS-like utterances (seeded, 0.3-1.5 s), synthetic noise + IR banks, synthetic "
                 "f16 negative pool; SE20 stand-in embedding graph",
         "config": {"workload": "configs[4]: end-to-end heybuddy-train pipeline per GPU: placement -> augment "
-                               "(reference default probabilities: 7-band EQ, tanh, colored noise, gain, background noise, reverb; "
-                               "pitch shift and band-stop not on the path yet) -> mel -> embed -> %d train steps (B=%d: 50 pos "
+                               "(reference default probabilities: 7-band EQ, tanh, band-stop, colored noise, gain, background noise, "
+                               "reverb; pitch shift not on the path yet) -> mel -> embed -> %d train steps (B=%d: 50 pos "
                                "+ 50 adv of the step's clips + 1000 f16 negatives)" % (S, B),
                    "clips_per_rank": n, "train_steps_per_rank": S, "train_batch_per_rank": B,
                    "negative_pool": f"{n_neg} x [16,96] f16",

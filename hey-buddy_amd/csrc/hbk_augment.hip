@@ -590,6 +590,157 @@ __global__ void __launch_bounds__(kThreads) spectrum_kernel(const float* kern, i
   }
 }
 
+// ---- band-stop ------------------------------------------------------------
+// torch_audiomentations BandStopFilter (the reference's batch chain,
+// augmented.py:101-105; p 0.25 per batch, parameters per clip):
+//   y = x - julius.bandpass_filter(x, cut_lo, cut_hi)
+// julius: the difference of two windowed-sinc lowpasses of half size
+// h = int(8 / cut_lo / 2) over the clip padded by h replicated edge samples,
+//   f_c[t] = 2 c hann[t + h] sinc(2 pi c t) / sum, t in [-h, h]
+// (taps in float32 arithmetic, as torch computes them).
+// One workgroup per selected clip; the clip is first copied to a per-block
+// global scratch row (the output may alias the input). The filter
+// f[k] = g[k - h], k < L = 2h + 1, is cut into partitions of kBsPart taps; for
+// partition p: kernel kappa[0] = f_p[0], kappa[N - k] = f_p[k] -> spectrum H_p
+// (the reverb transform, into the block's scratch); for each output half b:
+// segment s[j] = xpad[11520 b + p kBsPart + j] (xpad[m] = x[clamp(m - h, 0,
+// T - 1)]) -> forward transform, x H_p, inverse: samples 0..11519 of the
+// circular convolution are the partition's correlation sum for
+// n = 11520 b + i (overlap-save: i + k < 23040, nothing wraps).
+// y[n] = x[n] - sum_p c_p[n]; 5 transforms per partition (one partition for
+// h <= 5760, 99 % of the reference's draws).
+constexpr int kBsHalf = kT / 2;             // outputs per block
+constexpr int kBsPart = kT - kBsHalf + 1;   // 11521 taps per partition
+constexpr int64_t kBsScratch = kT + 2 * int64_t(kHSlots);  // floats per block: clip, then H
+
+struct BandStopArgs {
+  const float* x;
+  int64_t x_stride;
+  float* out;
+  int64_t out_stride;
+  int64_t n;               // selected clips
+  const int32_t* idx;      // clip row of entry i
+  const float* cut_lo;     // per entry, fraction of the sample rate
+  const float* cut_hi;
+  const int32_t* half;     // per entry: julius half_size
+  float* scratch;          // [gridDim.x][kBsScratch]
+  const float2* thi;
+  const float2* tlo;
+  const float2* twn;
+};
+
+// unnormalised julius lowpass tap t in [-h, h] (float32 as torch: hann from
+// arange * f32(2 pi / (2h)), arg = f32(2 pi c) * t, 2c * w * sinc)
+__device__ __forceinline__ float bs_tap(float two_c, float two_pi_c, float wstep, int h, int t) {
+  const float w = 0.5f - 0.5f * cosf(static_cast<float>(t + h) * wstep);
+  const float arg = two_pi_c * static_cast<float>(t);
+  const float sinc = arg == 0.f ? 1.f : sinf(arg) / arg;
+  return two_c * w * sinc;
+}
+
+__global__ void __launch_bounds__(kThreads) band_stop_kernel(BandStopArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  cf* z = reinterpret_cast<cf*>(smem);
+  float* red = smem + 2 * kM;
+  cf* thi = reinterpret_cast<cf*>(smem + 2 * kM + 32);
+  cf* tlo = thi + kTwHi;
+  load_tw(thi, tlo, a.thi, a.tlo);
+  const cf* twn = reinterpret_cast<const cf*>(a.twn);
+  float* zf = smem;
+  float* xs = a.scratch + static_cast<int64_t>(blockIdx.x) * kBsScratch;
+  cf* Hs = reinterpret_cast<cf*>(xs + kT);
+  unsigned long long ph_t0 = 0;
+  for (int64_t e = blockIdx.x; e < a.n; e += gridDim.x) {
+    const int64_t clip = a.idx[e];
+    const float* x = a.x + clip * a.x_stride;
+    float* out = a.out + clip * a.out_stride;
+    const int h = a.half[e];
+    const int L = 2 * h + 1;
+    const float cl = a.cut_lo[e], ch = a.cut_hi[e];
+    const float two_cl = static_cast<float>(2.0 * double(cl)), two_ch = static_cast<float>(2.0 * double(ch));
+    const float tpi_l = static_cast<float>(2.0 * double(cl) * M_PI), tpi_h = static_cast<float>(2.0 * double(ch) * M_PI);
+    const float wstep = static_cast<float>(2.0 * M_PI / double(L - 1));
+    // 1) the clip -> scratch; the two lowpass sums (float32 taps, float64 per-thread sums)
+    __syncthreads();  // the previous clip's readers of xs / H are done
+    for (int s = opaque_tid(); s < kT; s += kThreads) xs[s] = x[s];
+    double sl = 0.0, sh = 0.0;
+    for (int t = opaque_tid() - h; t <= h; t += kThreads) {
+      sl += bs_tap(two_cl, tpi_l, wstep, h, t);
+      sh += bs_tap(two_ch, tpi_h, wstep, h, t);
+    }
+    float fsl = static_cast<float>(sl), fsh = static_cast<float>(sh);
+    block_sum2(fsl, fsh, red);  // (its barriers also publish xs)
+    const int parts = (L + kBsPart - 1) / kBsPart;
+    for (int p = 0; p < parts; ++p) {
+      // 2) kernel of partition p into LDS, its spectrum into the scratch
+      __syncthreads();  // the previous partition's output loop is done reading zf
+      for (int m = opaque_tid(); m < kT; m += kThreads) {
+        const int k = m == 0 ? 0 : kT - m;  // kappa[m] = f_p[(-m) mod N]
+        const int kk = p * kBsPart + k;     // filter tap index, t = kk - h
+        float v = 0.f;
+        if (k < kBsPart && kk < L) {
+          const int t = kk - h;
+          v = bs_tap(two_ch, tpi_h, wstep, h, t) / fsh - bs_tap(two_cl, tpi_l, wstep, h, t) / fsl;
+        }
+        zf[m] = v;
+      }
+      __syncthreads();
+      transform<false>(z, thi, tlo, ph_t0, 16);
+      for (int q = opaque_tid(); q <= kM; q += kThreads) {
+        const int qq = q % kM, qc = (kM - q) % kM;
+        const cf zk = z[zaddr(qq)];
+        const cf zc = z[zaddr(qc)];
+        const cf fe = 0.5f * cf{zk.x + zc.x, zk.y - zc.y};
+        const cf fo = 0.5f * cf{zk.y + zc.y, zc.x - zk.x};
+        Hs[hslot(q)] = fe + cmul(twn[hslot(q)], fo);
+      }
+      // 3) the two output halves
+      for (int b = 0; b < 2; ++b) {
+        __syncthreads();  // H complete; the previous transform's readers of z are done
+        const int base = b * kBsHalf + p * kBsPart - h;
+        for (int j = opaque_tid(); j < kT; j += kThreads) zf[j] = xs[min(max(base + j, 0), kT - 1)];
+        __syncthreads();
+        transform<false>(z, thi, tlo, ph_t0, 16);
+        // split, x H, inverse split on (k, M - k) pairs (as augment_kernel)
+        const int ts = opaque_tid();
+        constexpr int kRest = kM / 2 / 16 + 1;
+        for (int idx = ts; idx < 16 * kRest; idx += kThreads) {
+          const int c = idx / kRest;
+          const int k = c + 16 * (idx - c * kRest);
+          if (k > kM / 2) continue;
+          const int kc = (kM - k) % kM;
+          const int pz = zaddr(k);
+          const cf zk = z[pz];
+          const cf zc = z[zaddr(kc)];
+          const cf fe = 0.5f * cf{zk.x + zc.x, zk.y - zc.y};
+          const cf fo = 0.5f * cf{zk.y + zc.y, zc.x - zk.x};
+          const cf wk = twn[hslot(k)];
+          const cf Xk = fe + cmul(wk, fo);
+          const cf Xc = cf{fe.x, -fe.y} + cmul(cf{-wk.x, wk.y}, cf{fo.x, -fo.y});
+          const cf Yk = cmul(Xk, Hs[hslot(k)]);
+          const cf Yc = cmul(Xc, Hs[hslot(kM - k)]);
+          const cf s1 = 0.5f * cf{Yk.x + Yc.x, Yk.y - Yc.y};
+          const cf d1 = 0.5f * cf{Yk.x - Yc.x, Yk.y + Yc.y};
+          const cf wd = cmul(cf{wk.x, -wk.y}, d1);
+          const cf s2 = 0.5f * cf{Yc.x + Yk.x, Yc.y - Yk.y};
+          const cf d2 = 0.5f * cf{Yc.x - Yk.x, Yc.y + Yk.y};
+          const cf wd2 = cmul(cf{-wk.x, -wk.y}, d2);
+          z[pz] = s1 + cf{-wd.y, wd.x};
+          if (kc != k) z[zaddr(kc)] = s2 + cf{-wd2.y, wd2.x};
+        }
+        __syncthreads();
+        transform<true>(z, thi, tlo, ph_t0, 16);
+        // y = x - sum_p c_p: each thread revisits only the samples it wrote before
+        for (int i = opaque_tid(); i < kBsHalf; i += kThreads) {
+          const int n = b * kBsHalf + i;
+          const float c = zf[i] * (1.f / kM);
+          out[n] = (p == 0 ? xs[n] : out[n]) - c;
+        }
+      }
+    }
+  }
+}
+
 // ---- colored noise --------------------------------------------------------
 // torch_audiomentations AddColoredNoise (the reference's batch chain,
 // augmented.py:107-113; p 0.25 per batch, snr ~ U[10, 30] dB and f_decay ~
@@ -1165,6 +1316,8 @@ int hbk_reverb_plan_create(int64_t T, hbk_reverb_plan** plan) {
                                hipFuncAttributeMaxDynamicSharedMemorySize, int(lds))) != hipSuccess ||
       (e = hipFuncSetAttribute(reinterpret_cast<const void*>(spectrum_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, int(lds))) != hipSuccess ||
+      (e = hipFuncSetAttribute(reinterpret_cast<const void*>(band_stop_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, int(lds))) != hipSuccess ||
       (e = hipFuncSetAttribute(reinterpret_cast<const void*>(colored_noise_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, int(kColoredLds))) != hipSuccess) {
     hbk_reverb_plan_destroy(p);
@@ -1266,6 +1419,43 @@ int hbk_colored_noise(const hbk_reverb_plan* p, const float* x, int64_t n_clips,
   const int64_t blocks = std::min<int64_t>(n_clips, persistent_blocks(1, stream));
   hipLaunchKernelGGL(colored_noise_kernel, dim3(unsigned(blocks)), dim3(kThreads), kColoredLds, as_stream(stream), a);
   HBK_LAUNCH_CHECK("colored_noise_kernel");
+  return HBK_OK;
+}
+
+int64_t hbk_band_stop_workspace_size(int64_t n, void* stream) {
+  using namespace hbk;
+  if (n <= 0) return 0;
+  return std::min<int64_t>(n, persistent_blocks(1, stream)) * kBsScratch * int64_t(sizeof(float));
+}
+
+int hbk_band_stop(const hbk_reverb_plan* p, const float* x, int64_t x_stride, const int32_t* idx, int64_t n,
+                  const float* cut_lo, const float* cut_hi, const int32_t* half, float* out, int64_t out_stride,
+                  void* workspace, int64_t workspace_bytes, void* stream) {
+  using namespace hbk;
+  if (!p) return arg_error("plan is NULL");
+  if (n < 0) return arg_error("negative n");
+  if (n == 0) return HBK_OK;
+  if (!x || !idx || !cut_lo || !cut_hi || !half || !out || !workspace) return arg_error("NULL pointer");
+  if (x_stride < kT || out_stride < kT) return arg_error("stride < 23040");
+  const int64_t blocks = std::min<int64_t>(n, persistent_blocks(1, stream));
+  if (workspace_bytes < blocks * kBsScratch * int64_t(sizeof(float)))
+    return arg_error("workspace too small (hbk_band_stop_workspace_size)");
+  BandStopArgs a;
+  a.x = x;
+  a.x_stride = x_stride;
+  a.out = out;
+  a.out_stride = out_stride;
+  a.n = n;
+  a.idx = idx;
+  a.cut_lo = cut_lo;
+  a.cut_hi = cut_hi;
+  a.half = half;
+  a.scratch = static_cast<float*>(workspace);
+  a.thi = p->thi;
+  a.tlo = p->tlo;
+  a.twn = p->twn;
+  hipLaunchKernelGGL(band_stop_kernel, dim3(unsigned(blocks)), dim3(kThreads), kAugLds, as_stream(stream), a);
+  HBK_LAUNCH_CHECK("band_stop_kernel");
   return HBK_OK;
 }
 

@@ -26,11 +26,17 @@ Semantics kept from the reference:
 * tanh distortion: audiomentations TanhDistortion, per CLIP with probability
   tanh_distortion_prob (0.25), amount ~ U[1e-4, 0.1] (:79-90), after the EQ: the
   reference applies both on the host before the batch chain (:325-328).
+* band-stop: torch_audiomentations BandStopFilter in per_batch mode (:101-105),
+  second in the batch chain (before the colored noise): per batch with
+  probability band_stop_prob (0.25) one center frequency (mel-uniform in
+  [200, 4000] Hz) and one bandwidth fraction (U[0.5, 1.99]); julius'
+  windowed-sinc band-pass subtracted from each clip of the batch on the device
+  (hbk_band_stop).
 Differences (by design): the IR spectra are computed once for the whole bank
 instead of once per batch, every batch of a call is one kernel launch, and
 clips never leave the device (the reference copies each clip back to host,
-:419). Pitch shift and band-stop (the first two transforms of the batch chain) are
-not on this path yet.
+:419). Pitch shift (the first transform of the batch chain) is not on this path
+yet.
 """
 from __future__ import annotations
 
@@ -40,7 +46,7 @@ import numpy as np
 import torch
 
 from heybuddy.constants import (DEFAULT_AUGMENT_BACKGROUND_NOISE_MAX_SNR_DB,
-                                DEFAULT_AUGMENT_BACKGROUND_NOISE_MIN_SNR_DB,
+                                DEFAULT_AUGMENT_BACKGROUND_NOISE_MIN_SNR_DB, DEFAULT_AUGMENT_BAND_STOP_PROB,
                                 DEFAULT_AUGMENT_COLORED_NOISE_MAX_F_DECAY,
                                 DEFAULT_AUGMENT_COLORED_NOISE_MAX_SNR_DB,
                                 DEFAULT_AUGMENT_COLORED_NOISE_MIN_F_DECAY,
@@ -53,7 +59,7 @@ from heybuddy.constants import (DEFAULT_AUGMENT_BACKGROUND_NOISE_MAX_SNR_DB,
                                 DEFAULT_AUGMENT_SEVEN_BAND_PROB)
 from heybuddy.kernels import ReverbPlan, place_clips, seven_band_eq, tanh_distortion
 
-__all__ = ["AugmentedAudioGenerator", "BatchAugmenter", "eq_coefficients", "eq_parameters",
+__all__ = ["AugmentedAudioGenerator", "BatchAugmenter", "bandstop_cutoffs", "eq_coefficients", "eq_parameters",
            "target_length_offset", "target_length_offsets", "to_target_length"]
 
 T = 23040
@@ -99,6 +105,22 @@ def eq_coefficients(params: np.ndarray, sample_rate: int = 16000) -> np.ndarray:
     return np.stack([b0 / a0, b1 / a0, b2 / a0, a1 / a0, a2 / a0], axis=-1)
 
 
+def bandstop_cutoffs(n: int, sample_rate: int = 16000):
+    """n (cut_lo, cut_hi) pairs of torch_audiomentations BandStopFilter (float32
+    fractions of the sample rate): center mel-uniform in [200, 4000] Hz (its
+    convert_frequencies_to_mels: 2595 log10(1 + f / 700)), bandwidth fraction
+    U[0.5, 1.99], cut = f_c (1 -+ bw / 2) / sr; numpy's global RNG."""
+    def mel(f):
+        return 2595.0 * np.log10(1.0 + f / 700.0)
+    m = np.random.uniform(mel(200.0), mel(4000.0), n).astype(np.float32)
+    fc = (np.float32(700.0) * (np.float32(10.0) ** (m / np.float32(2595.0)) - np.float32(1.0))).astype(np.float32)
+    bw = np.random.uniform(0.5, 1.99, n).astype(np.float32)
+    sr = np.float32(sample_rate)
+    lo = (fc * (np.float32(1.0) - bw / np.float32(2.0)) / sr).astype(np.float32)
+    hi = (fc * (np.float32(1.0) + bw / np.float32(2.0)) / sr).astype(np.float32)
+    return lo, hi
+
+
 def _pinned(t: torch.Tensor) -> torch.Tensor:
     """Page-locked copy for an asynchronous upload (as is on a GPU-less host)."""
     return t.pin_memory() if torch.cuda.is_available() else t
@@ -125,6 +147,7 @@ class BatchAugmenter:
                  tanh_max_distortion: float = DEFAULT_AUGMENT_TANH_MAX_DISTORTION,
                  seven_band_prob: float = DEFAULT_AUGMENT_SEVEN_BAND_PROB,
                  seven_band_gain_db: float = DEFAULT_AUGMENT_SEVEN_BAND_GAIN_DB,
+                 band_stop_prob: float = DEFAULT_AUGMENT_BAND_STOP_PROB,
                  sample_rate: int = 16000) -> None:
         self.plan = ReverbPlan(device)
         self.device = self.plan.device
@@ -148,6 +171,7 @@ class BatchAugmenter:
         self.tanh_range = (float(tanh_min_distortion), float(tanh_max_distortion))
         self.p_eq = float(seven_band_prob)
         self.eq_gain_db = float(seven_band_gain_db)
+        self.p_bandstop = float(band_stop_prob)
         self.ring = None
         self.lengths: List[int] = []
         self.starts: List[int] = []
@@ -218,6 +242,14 @@ class BatchAugmenter:
             per_clip = np.where(r_on, ir, -1).astype(np.int32)[batch]
             spec_idx[:] = per_clip
         self._colored = (colored_snr, colored_fd)
+        # band-stop (BandStopFilter, per_batch): one (center, bandwidth) per batch
+        # whose coin came up; the filtered clips and their cutoffs
+        b_on = np.random.rand(nbat) < getattr(self, "p_bandstop", 0.0)
+        lo, hi = bandstop_cutoffs(int(b_on.sum()), getattr(self, "sample_rate", 16000))
+        sel = b_on[batch]
+        per = np.full(nbat, -1, dtype=np.int64)
+        per[b_on] = np.arange(int(b_on.sum()))
+        self._bandstop = (np.flatnonzero(sel).astype(np.int32), lo[per[batch][sel]], hi[per[batch][sel]])
         # seven-band EQ (audiomentations, per clip): the clips whose coin came up
         # and their filters (parameters drawn for those clips only)
         e_on = np.random.rand(n) < getattr(self, "p_eq", 0.0)
@@ -248,12 +280,16 @@ class BatchAugmenter:
         if eq_idx.size:
             eq = (_pinned(torch.from_numpy(eq_coef)), _pinned(torch.from_numpy(eq_idx)))
         tanh = None if np.isnan(self._tanh).all() else torch.from_numpy(self._tanh)
+        bs_idx, bs_lo, bs_hi = self._bandstop
+        bandstop = None
+        if bs_idx.size:
+            bandstop = (torch.from_numpy(bs_idx), torch.from_numpy(bs_lo), torch.from_numpy(bs_hi))
         colored_snr, colored_fd = self._colored
         colored = None
         if not np.isnan(colored_snr).all():
             colored = (torch.from_numpy(colored_fd), torch.from_numpy(colored_snr), int(np.random.randint(0, 2 ** 62)))
         return {"n": n, "noise_off": torch.from_numpy(noise_off), "spec_idx": torch.from_numpy(spec_idx),
-                "snr": snr, "gain": gain, "eq": eq, "tanh": tanh, "colored": colored}
+                "snr": snr, "gain": gain, "eq": eq, "tanh": tanh, "bandstop": bandstop, "colored": colored}
 
     def __call__(self, x: torch.Tensor, out: Optional[torch.Tensor] = None,
                  prepared: Optional[Dict[str, Any]] = None) -> torch.Tensor:
@@ -271,6 +307,12 @@ class BatchAugmenter:
         if pr["tanh"] is not None:  # per-clip Compose, before the batch chain (augmented.py:325-328)
             x = tanh_distortion(x, pr["tanh"], out=out)
             out = x
+        if pr.get("bandstop") is not None:  # batch chain: band-stop, then colored noise (augmented.py:101-113)
+            if out is None:
+                out = x[:, :T].clone()
+            elif out.data_ptr() != x.data_ptr():
+                out.copy_(x[:, :T])
+            x = self.plan.band_stop(out, *pr["bandstop"], out=out)
         if pr["colored"] is not None:  # colored noise precedes the gain (augmented.py:107-118)
             fd, csnr, seed = pr["colored"]
             x = self.plan.colored_noise(x, fd, csnr, seed=seed, out=out, sample_rate=self.sample_rate)
@@ -383,9 +425,8 @@ class AugmentedAudioGenerator:
             raise ValueError("Background noise is enabled but no augmentation dataset is provided")
         if reverb_prob > 0 and not impulse_response_dataset:
             raise ValueError("Reverb is enabled but no impulse response dataset is provided")
-        for name, p in (("pitch_shift_prob", pitch_shift_prob), ("band_stop_prob", band_stop_prob)):
-            if p > 0:
-                logger.warning(f"{name}={p}: this augmentation is not on the MI355X path yet; skipped")
+        if pitch_shift_prob > 0:
+            logger.warning(f"pitch_shift_prob={pitch_shift_prob}: pitch shift is not on the MI355X path yet; skipped")
         self.device_id = device_id
         self.source_dataset = source_dataset
         self.augmentation_dataset = augmentation_dataset
@@ -417,7 +458,7 @@ class AugmentedAudioGenerator:
             colored_noise_min_f_decay=colored_noise_min_f_decay, colored_noise_max_f_decay=colored_noise_max_f_decay,
             tanh_distortion_prob=tanh_distortion_prob, tanh_min_distortion=tanh_min_distortion,
             tanh_max_distortion=tanh_max_distortion, seven_band_prob=seven_band_aug_prob,
-            seven_band_gain_db=seven_band_aug_gain_db, sample_rate=self.sample_rate)
+            seven_band_gain_db=seven_band_aug_gain_db, band_stop_prob=band_stop_prob, sample_rate=self.sample_rate)
         self.device = self.augmenter.device
         self._source: Optional[List[Dict[str, Any]]] = None
         self._source_pos = 0

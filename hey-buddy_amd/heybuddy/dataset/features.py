@@ -231,12 +231,13 @@ class TrainingFeaturesGenerator:
                 target_length=self.augment_target_length, sample_rate=self.sample_rate,
                 augmentation_dataset=self._bank("noise", testing),
                 impulse_response_dataset=self._bank("ir", testing),
-                seven_band_aug_prob=0.0, seven_band_aug_gain_db=self.augment_seven_band_gain_db,
+                seven_band_aug_prob=self.augment_seven_band_prob,
+                seven_band_aug_gain_db=self.augment_seven_band_gain_db,
                 tanh_distortion_prob=self.augment_tanh_distortion_prob,
                 tanh_min_distortion=self.augment_tanh_min_distortion,
                 tanh_max_distortion=self.augment_tanh_max_distortion,
                 pitch_shift_prob=0.0, pitch_shift_semitones=self.augment_pitch_shift_semitones,
-                band_stop_prob=0.0,
+                band_stop_prob=self.augment_band_stop_prob,
                 colored_noise_prob=self.augment_colored_noise_prob,
                 colored_noise_min_snr_db=self.augment_colored_noise_min_snr_db,
                 colored_noise_max_snr_db=self.augment_colored_noise_max_snr_db,
@@ -246,10 +247,9 @@ class TrainingFeaturesGenerator:
                 background_noise_min_snr_db=self.augment_background_noise_min_snr_db,
                 background_noise_max_snr_db=self.augment_background_noise_max_snr_db,
                 gain_prob=self.augment_gain_prob, reverb_prob=self.augment_reverb_prob)
-            for name in ("seven_band", "pitch_shift", "band_stop"):
-                p = getattr(self, f"augment_{name}_prob")
-                if p > 0:
-                    logger.warning(f"augment_{name}_prob={p}: not on the MI355X path yet; skipped")
+            if self.augment_pitch_shift_prob > 0:
+                logger.warning(f"augment_pitch_shift_prob={self.augment_pitch_shift_prob}: "
+                               "not on the MI355X path yet; skipped")
         return self._augmenters[key]
 
     def augment_device(self, clips: torch.Tensor, lengths: np.ndarray, num_samples: int,

@@ -667,6 +667,7 @@ class ReverbPlan:
         with torch.cuda.device(self.device):
             check(lib().hbk_reverb_plan_create(self.T, ctypes.byref(handle)), "hbk_reverb_plan_create")
         self._handle = handle
+        self._bs_ws: torch.Tensor | None = None  # band-stop workspace (grows)
         self.id = _register(self)
 
     @staticmethod
@@ -771,6 +772,42 @@ class ReverbPlan:
         torch.ops.hbk.colored_noise_(x, white, f_decay, snr_db, _u64_to_i64(seed), float(sample_rate), out, self.id)
         return out
 
+    def band_stop(self, x: torch.Tensor, idx: torch.Tensor, cut_lo: torch.Tensor, cut_hi: torch.Tensor,
+                  out: torch.Tensor | None = None) -> torch.Tensor:
+        """torch_audiomentations BandStopFilter on rows idx of x [n, >= T] ->
+        out [n, T] (hbk_band_stop): out[idx[e]] = x[idx[e]] - julius
+        bandpass(cut_lo[e], cut_hi[e]) (fractions of the sample rate); other
+        rows of out are left as they are (out may be x)."""
+        n = x.shape[0]
+        if x.dim() != 2 or x.shape[1] < self.T or x.stride(1) != 1 or x.device != self.device:
+            raise ValueError(f"x must be [n, >= {self.T}] f32 rows on {self.device}")
+        if out is None:
+            out = x[:, :self.T].clone()
+        e = idx.numel()
+        if cut_lo.numel() != e or cut_hi.numel() != e:
+            raise ValueError("idx, cut_lo and cut_hi must have one entry per filtered clip")
+        if e == 0:
+            return out
+        lo_h = cut_lo.detach().to("cpu", torch.float32).reshape(-1)
+        hi_h = cut_hi.detach().to("cpu", torch.float32).reshape(-1)
+        if not bool(((lo_h > 0) & (lo_h <= hi_h) & (hi_h <= 0.5)).all()):
+            raise ValueError("band-stop cutoffs must satisfy 0 < cut_lo <= cut_hi <= 0.5")
+        idx_h = idx.detach().to("cpu", torch.int32).reshape(-1)
+        if bool(((idx_h < 0) | (idx_h >= n)).any()):
+            raise ValueError("idx out of range")
+        # julius LowPassFilters.half_size = int(zeros / min(cutoffs) / 2), zeros = 8
+        half = torch.tensor([int(8 / float(c) / 2) for c in lo_h.tolist()], dtype=torch.int32)
+
+        def to_dev(t: torch.Tensor) -> torch.Tensor:
+            return t.contiguous().pin_memory().to(self.device, non_blocking=True)
+
+        ws_bytes = int(lib().hbk_band_stop_workspace_size(e, stream_ptr(self.device)))
+        if self._bs_ws is None or self._bs_ws.numel() < ws_bytes:
+            self._bs_ws = torch.empty(ws_bytes, dtype=torch.uint8, device=self.device)
+        torch.ops.hbk.band_stop_(x, to_dev(idx_h), to_dev(lo_h), to_dev(hi_h), to_dev(half), out, self._bs_ws,
+                                 self.id)
+        return out
+
     def __del__(self) -> None:
         h = getattr(self, "_handle", None)
         if h is not None and h.value:
@@ -808,3 +845,12 @@ def _colored_noise_op(x: torch.Tensor, white: torch.Tensor | None, f_decay: torc
                                   white.stride(0) if white is not None else 0, seed & (2 ** 64 - 1), ptr(f_decay),
                                   ptr(snr_db), sample_rate, ptr(out), out.stride(0), stream_ptr(x.device)),
           "hbk_colored_noise")
+
+
+@torch.library.custom_op("hbk::band_stop_", mutates_args=("out", "workspace"))
+def _band_stop_op(x: torch.Tensor, idx: torch.Tensor, cut_lo: torch.Tensor, cut_hi: torch.Tensor,
+                  half: torch.Tensor, out: torch.Tensor, workspace: torch.Tensor, plan_id: int) -> None:
+    plan = _plans[plan_id]
+    check(lib().hbk_band_stop(plan._handle, ptr(x), x.stride(0), ptr(idx), idx.numel(), ptr(cut_lo), ptr(cut_hi),
+                              ptr(half), ptr(out), out.stride(0), ptr(workspace), workspace.numel(),
+                              stream_ptr(x.device)), "hbk_band_stop")

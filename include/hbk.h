@@ -323,6 +323,22 @@ int hbk_colored_noise(const hbk_reverb_plan* plan, const float* x, int64_t n_cli
                       const float* white, int64_t white_stride, uint64_t seed, const float* f_decay,
                       const float* snr_db, float sample_rate, float* out, int64_t out_stride, void* stream);
 
+/* Band-stop: torch_audiomentations BandStopFilter, which the reference applies
+ * in its batch chain with p 0.25 per batch and parameters per clip (center
+ * mel-uniform in [200, 4000] Hz, bandwidth fraction U[0.5, 1.99];
+ * dataset/augmented.py:101-105, constants.py:127). For entry e < n, clip row
+ * r = idx[e] of x [*, x_stride] (first T = 23040 samples):
+ *   out[r] = x[r] - julius.bandpass_filter(x[r], cut_lo[e], cut_hi[e])
+ * with julius' windowed-sinc lowpasses of half size half[e] = int(8 / cut_lo / 2)
+ * over the replicate-padded clip (cutoffs as fractions of the sample rate).
+ * Rows not listed are not touched; out may equal x. workspace: at least
+ * hbk_band_stop_workspace_size(n, stream) bytes (one clip + one spectrum per
+ * resident workgroup). Device pointers. */
+int64_t hbk_band_stop_workspace_size(int64_t n, void* stream);
+int hbk_band_stop(const hbk_reverb_plan* plan, const float* x, int64_t x_stride, const int32_t* idx, int64_t n,
+                  const float* cut_lo, const float* cut_hi, const int32_t* half, float* out, int64_t out_stride,
+                  void* workspace, int64_t workspace_bytes, void* stream);
+
 /* Tanh distortion: audiomentations TanhDistortion, which the reference applies
  * per clip with p 0.25 and distortion ~ U[1e-4, 0.1] before the batch chain
  * (dataset/augmented.py:79-90, :325-328; constants.py:122-124). Per clip i of

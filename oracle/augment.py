@@ -46,6 +46,19 @@ their published algorithms at the versions environment.yml pins
       A = 10^(gain/40), w0 = 2 pi f0 / sr, alpha = sin(w0) / (2 Q)
   (the band ranges, Q range and draw distributions are restated from the
   package's documentation: PARITY UNPINNED, no fixture exists).
+* torch_audiomentations.BandStopFilter (torch_audiomentations >= 0.11,
+  environment.yml:27; p 0.25, mode per_batch: one coin per batch, parameters
+  per clip; augmented.py:101-105, constants.py:127), second in the batch chain
+  (after PitchShift, before AddColoredNoise). Per clip: center frequency
+  mel-uniform in [200, 4000] Hz, bandwidth fraction ~ U[0.5, 1.99],
+      cut_lo = f_c (1 - bw/2) / sr,  cut_hi = f_c (1 + bw/2) / sr   (float32)
+  and y = x - julius.bandpass_filter(x, cut_lo, cut_hi) with julius's
+  LowPassFilters([cut_lo, cut_hi], zeros=8): half_size h = int(8 / cut_lo / 2),
+  taps t in [-h, h], window hann(2h + 1, periodic=False),
+      f_c[t] = 2 c w[t] sinc(2 pi c t),  f_c /= sum(f_c)        (float32 math)
+      bandpass = conv1d(pad(x, h, 'replicate'), f_hi) - (same with f_lo)
+  (julius switches to an FFT convolution for h > 32: the same linear
+  convolution up to rounding). PARITY UNPINNED: neither package is installed.
 """
 from __future__ import annotations
 
@@ -228,4 +241,59 @@ def seven_band_eq(x, sos) -> np.ndarray:
         for k in range(7):  # scipy.signal.sosfilt: the DF2T recursion audiomentations calls
             y = sosfilt(sos[i, k][None], y).astype(np.float32)
         out[i] = y
+    return out
+
+
+# --------------------------------------------------------------------------
+# BandStopFilter
+BANDSTOP_CENTER = (200.0, 4000.0)
+BANDSTOP_BANDWIDTH = (0.5, 1.99)
+
+
+def bandstop_draw(rng, n: int, sample_rate: int = 16000):
+    """(cut_lo, cut_hi) [n] float32 fractions of the sample rate: f_c
+    mel-uniform in BANDSTOP_CENTER, bandwidth fraction uniform (float32 math,
+    as torch_audiomentations' tensors)."""
+    lo, hi = hz_to_mel(BANDSTOP_CENTER)
+    fc = mel_to_hz(rng.uniform(lo, hi, n)).astype(np.float32)
+    bw = rng.uniform(*BANDSTOP_BANDWIDTH, n).astype(np.float32)
+    sr = np.float32(sample_rate)
+    return (fc * (np.float32(1) - bw / np.float32(2)) / sr).astype(np.float32), \
+        (fc * (np.float32(1) + bw / np.float32(2)) / sr).astype(np.float32)
+
+
+def bandstop_half_size(cut_lo) -> int:
+    """julius LowPassFilters.half_size = int(zeros / min(cutoffs) / 2), zeros 8."""
+    return int(8 / float(cut_lo) / 2)
+
+
+def lowpass_taps(cutoff, half: int) -> np.ndarray:
+    """julius' windowed-sinc lowpass [2 half + 1] in float32 arithmetic:
+    2 c hann[t] sinc(2 pi c t), normalised to unit sum."""
+    n = 2 * half + 1
+    k = np.arange(n, dtype=np.float32)
+    hann = (np.float32(0.5) - np.float32(0.5) * np.cos(k * np.float32(2.0 * np.pi / (n - 1)))).astype(np.float32) \
+        if n > 1 else np.ones(1, np.float32)
+    t = np.arange(-half, half + 1).astype(np.float32)
+    arg = (np.float32(2.0 * float(cutoff) * np.pi) * t).astype(np.float32)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        sinc = np.where(arg == 0, np.float32(1), (np.sin(arg) / arg).astype(np.float32))
+    f = (np.float32(2.0 * float(cutoff)) * hann * sinc).astype(np.float32)
+    return (f / f.astype(np.float64).sum().astype(np.float32)).astype(np.float32)
+
+
+def band_stop(x, cut_lo, cut_hi) -> np.ndarray:
+    """x [n, T] float32 -> x - bandpass(x), per-clip cutoffs (float64
+    convolution of the float32 taps; a NaN cut_lo leaves the clip unchanged)."""
+    from scipy.signal import fftconvolve
+    x = np.asarray(x, dtype=np.float32)
+    out = x.copy()
+    for i in range(x.shape[0]):
+        if np.isnan(cut_lo[i]):
+            continue
+        h = bandstop_half_size(cut_lo[i])
+        g = lowpass_taps(cut_hi[i], h).astype(np.float64) - lowpass_taps(cut_lo[i], h).astype(np.float64)
+        xp = np.pad(x[i].astype(np.float64), h, mode="edge")
+        bp = fftconvolve(xp, g[::-1], mode="valid")  # conv1d is a correlation; g is symmetric anyway
+        out[i] = (x[i] - bp).astype(np.float32)
     return out

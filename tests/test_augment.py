@@ -208,7 +208,8 @@ def test_batch_augmenter_gain_is_per_batch():
     x = torch.from_numpy(_clips(300, seed=14)).float().cuda()
     np.random.seed(5)
     aug = BatchAugmenter(device=0, batch_size=128, background_noise_prob=0.0, reverb_prob=0.0,
-                         colored_noise_prob=0.0, tanh_distortion_prob=0.0, seven_band_prob=0.0)
+                         colored_noise_prob=0.0, tanh_distortion_prob=0.0, seven_band_prob=0.0,
+                         band_stop_prob=0.0)
     out = aug(x)
     ratio = (out / x).cpu().numpy()
     xs = x.cpu().numpy()
@@ -218,7 +219,8 @@ def test_batch_augmenter_gain_is_per_batch():
         np.testing.assert_allclose(blk, g, rtol=1e-6)
         assert 10 ** (-18 / 20) * (1 - 1e-6) <= g <= 10 ** (6 / 20) * (1 + 1e-6)
     off = BatchAugmenter(device=0, background_noise_prob=0.0, reverb_prob=0.0, gain_prob=0.0,
-                         colored_noise_prob=0.0, tanh_distortion_prob=0.0, seven_band_prob=0.0)
+                         colored_noise_prob=0.0, tanh_distortion_prob=0.0, seven_band_prob=0.0,
+                         band_stop_prob=0.0)
     assert torch.equal(off(x), x)
 
 
@@ -346,7 +348,8 @@ def test_batch_augmenter_colored_noise_is_per_batch():
     x = torch.from_numpy(_clips(300, seed=25)).float().cuda()
     np.random.seed(6)
     aug = BatchAugmenter(device=0, batch_size=128, background_noise_prob=0.0, reverb_prob=0.0, gain_prob=0.0,
-                         colored_noise_prob=1.0, tanh_distortion_prob=0.0, seven_band_prob=0.0)
+                         colored_noise_prob=1.0, tanh_distortion_prob=0.0, seven_band_prob=0.0,
+                         band_stop_prob=0.0)
     out = aug(x)
     xs, os_ = x.cpu().double().numpy(), out.cpu().double().numpy()
     rms = lambda v: np.sqrt((v * v).mean(axis=-1))
@@ -356,7 +359,8 @@ def test_batch_augmenter_colored_noise_is_per_batch():
         assert blk.max() - blk.min() < 1e-3
         assert 10.0 - 1e-3 <= blk[0] <= 30.0 + 1e-3
     off = BatchAugmenter(device=0, background_noise_prob=0.0, reverb_prob=0.0, gain_prob=0.0,
-                         colored_noise_prob=0.0, tanh_distortion_prob=0.0, seven_band_prob=0.0)
+                         colored_noise_prob=0.0, tanh_distortion_prob=0.0, seven_band_prob=0.0,
+                         band_stop_prob=0.0)
     assert torch.equal(off(x), x)
 
 
@@ -452,3 +456,79 @@ def test_seven_band_eq_kernel_matches_oracle():
     keep = np.setdiff1d(np.arange(n), sel)
     np.testing.assert_array_equal(got[keep], x[keep])
     np.testing.assert_allclose(got[sel, :23040] / scale[sel], ref[sel] / scale[sel], rtol=0, atol=2e-6)
+
+
+# ---- band-stop (torch_audiomentations BandStopFilter, augmented.py:101-105) ----
+# PARITY UNPINNED at the third-party boundary (torch_audiomentations / julius are
+# not installed); oracle/augment.py restates julius' bandpass_filter.
+
+def test_bandstop_oracle_properties():
+    """The restated filter: each lowpass sums to 1 (a constant clip passes the
+    band-stop unchanged), an in-band tone is removed, an out-of-band one kept,
+    and the half size is julius' int(8 / cut_lo / 2)."""
+    assert oaug.bandstop_half_size(0.1) == 40
+    assert oaug.bandstop_half_size(np.float32(0.1)) == 39  # the float32 cutoff is 0.1000000015
+    for c, h in ((0.03, 133), (0.3, 40)):
+        np.testing.assert_allclose(oaug.lowpass_taps(c, h).astype(np.float64).sum(), 1.0, rtol=1e-6)
+    n = np.arange(T)
+    x = np.stack([np.full(T, 0.3), np.sin(2 * np.pi * 1000 / 16000 * n), np.sin(2 * np.pi * 3000 / 16000 * n)])
+    lo, hi = np.float32(700 / 16000), np.float32(1400 / 16000)
+    y = oaug.band_stop(x.astype(np.float32), np.full(3, lo), np.full(3, hi))
+    np.testing.assert_allclose(y[0], x[0], atol=1e-6)
+    assert np.abs(y[1, 4000:-4000]).max() < 2e-3
+    np.testing.assert_allclose(y[2, 4000:-4000], x[2, 4000:-4000], atol=2e-3)
+    r = np.random.default_rng(3)
+    lo, hi = oaug.bandstop_draw(r, 1000)
+    assert (lo > 0).all() and (lo <= hi).all() and (hi < 0.5).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("inplace", [False, True])
+def test_band_stop_matches_oracle(inplace):
+    """hbk_band_stop against the oracle over filter lengths from 43 taps to
+    the longest the reference draws (half size 64,000: 12 partitions of the
+    overlap-save scheme), a step clip (replicate padding) and an unlisted clip."""
+    from heybuddy.kernels import ReverbPlan
+    x = _clips(8, seed=41).astype(np.float32)
+    x[6] = np.where(np.arange(T) < T // 3, 0.4, -0.2)          # step: the padded edges matter
+    cut_lo = np.array([0.1875, 0.03, 2.0e-3, 6.0e-4, 3.3e-4, 1.3e-4, 0.01, np.nan], np.float32)
+    cut_hi = np.array([0.45, 0.2, 0.1, 0.05, 2.0e-3, 0.4987, 0.03, np.nan], np.float32)
+    sel = np.flatnonzero(~np.isnan(cut_lo)).astype(np.int32)   # clip 7 is not listed
+    ref = oaug.band_stop(x, cut_lo, cut_hi)
+    plan = ReverbPlan(0)
+    xd = torch.from_numpy(x).cuda()
+    out = plan.band_stop(xd, torch.from_numpy(sel), torch.from_numpy(cut_lo[sel]), torch.from_numpy(cut_hi[sel]),
+                         out=xd if inplace else None).cpu().numpy()
+    for i in range(8):
+        tol = 2e-5 * max(np.abs(x[i]).max(), np.abs(ref[i]).max())
+        err = np.abs(out[i] - ref[i]).max()
+        assert err <= tol, f"clip {i} (half size {oaug.bandstop_half_size(cut_lo[i]) if i < 7 else 0}): {err} > {tol}"
+    np.testing.assert_array_equal(out[7], x[7])
+
+
+@pytest.mark.gpu
+def test_batch_augmenter_band_stop_is_per_batch():
+    """BatchAugmenter: band-stop per batch of 128 (one cutoff pair per batch
+    whose coin came up) between the per-clip chain and the colored noise; the
+    device result equals the oracle on the drawn cutoffs."""
+    from heybuddy.dataset.augmented import BatchAugmenter
+    x = torch.from_numpy(_clips(300, seed=43)).float().cuda()
+    np.random.seed(9)
+    aug = BatchAugmenter(device=0, batch_size=128, background_noise_prob=0.0, reverb_prob=0.0, gain_prob=0.0,
+                         colored_noise_prob=0.0, tanh_distortion_prob=0.0, seven_band_prob=0.0,
+                         band_stop_prob=1.0)
+    pr = aug.prepare(300)
+    idx, lo, hi = (t.numpy() for t in pr["bandstop"])
+    np.testing.assert_array_equal(idx, np.arange(300))
+    for b0 in range(0, 300, 128):
+        assert np.unique(lo[b0:b0 + 128]).size == 1 and np.unique(hi[b0:b0 + 128]).size == 1
+    out = aug(x, prepared=pr).cpu().numpy()
+    xs = x.cpu().numpy()
+    pick = [0, 127, 128, 299]
+    ref = oaug.band_stop(xs[pick], lo[pick], hi[pick])
+    for j, i in enumerate(pick):
+        assert np.abs(out[i] - ref[j]).max() <= 2e-5 * np.abs(xs[i]).max()
+    off = BatchAugmenter(device=0, background_noise_prob=0.0, reverb_prob=0.0, gain_prob=0.0,
+                         colored_noise_prob=0.0, tanh_distortion_prob=0.0, seven_band_prob=0.0,
+                         band_stop_prob=0.0)
+    assert off.prepare(300)["bandstop"] is None
