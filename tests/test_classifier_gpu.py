@@ -106,12 +106,17 @@ def test_train_epoch_matches_reference(gold, inputs, tmp_path):
     np.testing.assert_allclose(lr, gold["epoch/lr"], rtol=1e-6)
     np.testing.assert_allclose(hlr, gold["epoch/hlr"], rtol=1e-6)
     assert loss.shape == gold["epoch/loss"].shape
-    np.testing.assert_allclose(loss, gold["epoch/loss"], rtol=2e-3, atol=1e-5)
+    # the oracle's bounds (test_classifier_oracle.py): loss 2e-4; final
+    # parameters within 2e-4 except Adam's sign flips where a gradient sits at
+    # the fp32 noise floor (each flip moves a weight by up to 2 lr): at most
+    # 0.5 % of the 256,417 parameters, as in test_stages_gpu.py
+    np.testing.assert_allclose(loss, gold["epoch/loss"], rtol=2e-4, atol=1e-7)
     np.testing.assert_allclose(rec, gold["epoch/recall"], atol=1e-6)
     np.testing.assert_allclose(fp, gold["epoch/fp"], atol=1e-6)
     sd = tr.model.state_dict()
-    worst = max(np.abs(sd[k].cpu().numpy() - gold[f"epoch_final/{k}"]).max() for k in params)
-    assert worst <= 5e-3, worst
+    diffs = np.concatenate([np.abs(sd[k].cpu().numpy() - gold[f"epoch_final/{k}"]).ravel() for k in params])
+    assert (diffs > 2e-4).mean() <= 5e-3, (diffs > 2e-4).mean()
+    assert diffs.max() <= 5e-3, diffs.max()  # a flipped element: a few lr-sized steps at most
     # checkpoint + resume round trip keeps the Adam state
     tr.save_checkpoint("t")
     tr2 = WakeWordTrainer(checkpoint_dir=str(tmp_path))
