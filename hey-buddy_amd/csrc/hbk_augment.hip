@@ -592,142 +592,242 @@ __global__ void __launch_bounds__(kThreads) spectrum_kernel(const float* kern, i
 
 // ---- band-stop ------------------------------------------------------------
 // torch_audiomentations BandStopFilter (the reference's batch chain,
-// augmented.py:101-105; p 0.25 per batch, parameters per clip):
+// augmented.py:101-105; p 0.25 per batch, one parameter set per batch):
 //   y = x - julius.bandpass_filter(x, cut_lo, cut_hi)
 // julius: the difference of two windowed-sinc lowpasses of half size
 // h = int(8 / cut_lo / 2) over the clip padded by h replicated edge samples,
 //   f_c[t] = 2 c hann[t + h] sinc(2 pi c t) / sum, t in [-h, h]
-// (taps in float32 arithmetic, as torch computes them).
-// One workgroup per selected clip; the clip is first copied to a per-block
-// global scratch row (the output may alias the input). The filter
-// f[k] = g[k - h], k < L = 2h + 1, is cut into partitions of kBsPart taps; for
-// partition p: kernel kappa[0] = f_p[0], kappa[N - k] = f_p[k] -> spectrum H_p
-// (the reverb transform, into the block's scratch); for each output half b:
-// segment s[j] = xpad[11520 b + p kBsPart + j] (xpad[m] = x[clamp(m - h, 0,
-// T - 1)]) -> forward transform, x H_p, inverse: samples 0..11519 of the
-// circular convolution are the partition's correlation sum for
-// n = 11520 b + i (overlap-save: i + k < 23040, nothing wraps).
-// y[n] = x[n] - sum_p c_p[n]; 5 transforms per partition (one partition for
-// h <= 5760, 99 % of the reference's draws).
-constexpr int kBsHalf = kT / 2;             // outputs per block
+// (taps in float32 arithmetic, as torch computes them); g = f_hi - f_lo.
+// Three launches per call: per filter (batch) the two lowpass sums and, for
+// short filters, the taps g[0..h]; per filter spectrum (the reverb transform);
+// per clip the convolution:
+//  * h <= HBK_BAND_STOP_CIRCULAR_MAX_HALF (about 80 % of the reference's draws):
+//    the clip's circular convolution with g (one forward and one inverse
+//    transform, like the reverb), then the 2h edge samples corrected directly:
+//    for n < h the taps that wrapped to the clip's end are replaced by the
+//    replicated first sample, sum_{d < -n} g[d] (x[0] - x[T + n + d]), and
+//    likewise at the other end;
+//  * longer filters: overlap-save. f[k] = g[k - h], k < 2h + 1, in partitions
+//    of kBsPart taps, each with its own spectrum; for partition p and output
+//    half b the segment s[j] = xpad[11520 b + p kBsPart + j] (xpad[m] =
+//    x[clamp(m - h, 0, T - 1)]) is transformed, multiplied, transformed back:
+//    samples 0..11519 are the partition's sum for n = 11520 b + i (i + k <
+//    23040: nothing wraps); the clip sits in a per-block global scratch row
+//    (the output may alias the input).
+constexpr int kBsHalf = kT / 2;             // outputs per overlap-save block
 constexpr int kBsPart = kT - kBsHalf + 1;   // 11521 taps per partition
-constexpr int64_t kBsScratch = kT + 2 * int64_t(kHSlots);  // floats per block: clip, then H
+constexpr int kBsCirc = HBK_BAND_STOP_CIRCULAR_MAX_HALF;
+static_assert(2 * kBsCirc <= kThreads, "one edge sample per thread");
+
+// unnormalised julius lowpass tap t in [-h, h] (float32 as torch: hann from
+// arange * f32(2 pi / (2h)), arg = f32(2 pi c) * t, 2c * w * sinc)
+struct BsLowpass {
+  float two_c, two_pi_c, wstep;
+  int h;
+  __device__ __forceinline__ BsLowpass(float c, int h_) : h(h_) {
+    two_c = static_cast<float>(2.0 * double(c));
+    two_pi_c = static_cast<float>(2.0 * double(c) * M_PI);
+    wstep = static_cast<float>(2.0 * M_PI / double(2 * h_));
+  }
+  __device__ __forceinline__ float tap(int t) const {
+    const float w = 0.5f - 0.5f * cosf(static_cast<float>(t + h) * wstep);
+    const float arg = two_pi_c * static_cast<float>(t);
+    const float sinc = arg == 0.f ? 1.f : sinf(arg) / arg;
+    return two_c * w * sinc;
+  }
+};
 
 struct BandStopArgs {
   const float* x;
   int64_t x_stride;
   float* out;
   int64_t out_stride;
-  int64_t n;               // selected clips
-  const int32_t* idx;      // clip row of entry i
-  const float* cut_lo;     // per entry, fraction of the sample rate
-  const float* cut_hi;
-  const int32_t* half;     // per entry: julius half_size
-  float* scratch;          // [gridDim.x][kBsScratch]
+  int64_t n;               // filtered clips
+  const int32_t* idx;      // clip row of entry e
+  const int32_t* filt;     // filter of entry e
+  int n_filters;
+  const float* f_lo;       // per filter: cutoffs (fraction of the sample rate), half size,
+  const float* f_hi;       //   first spectrum slot
+  const int32_t* f_half;
+  const int32_t* f_spec0;
+  int n_spectra;
+  const int32_t* s_filt;   // per spectrum: filter, partition (-1: circular kernel)
+  const int32_t* s_part;
+  float2* sums;            // [n_filters]: the two lowpass sums (lo, hi)
+  float* taps;             // [n_filters][kBsCirc + 1]: g[0..h] of circular filters
+  float2* spectra;         // [n_spectra][kHSlots]
+  float* scratch;          // [gridDim.x][kT]: overlap-save clips
   const float2* thi;
   const float2* tlo;
   const float2* twn;
 };
 
-// unnormalised julius lowpass tap t in [-h, h] (float32 as torch: hann from
-// arange * f32(2 pi / (2h)), arg = f32(2 pi c) * t, 2c * w * sinc)
-__device__ __forceinline__ float bs_tap(float two_c, float two_pi_c, float wstep, int h, int t) {
-  const float w = 0.5f - 0.5f * cosf(static_cast<float>(t + h) * wstep);
-  const float arg = two_pi_c * static_cast<float>(t);
-  const float sinc = arg == 0.f ? 1.f : sinf(arg) / arg;
-  return two_c * w * sinc;
+// g[t] from the normalised lowpasses
+__device__ __forceinline__ float bs_g(const BsLowpass& lo, const BsLowpass& hi, float2 s, int t) {
+  return hi.tap(t) / s.y - lo.tap(t) / s.x;
 }
 
-__global__ void __launch_bounds__(kThreads) band_stop_kernel(BandStopArgs a) {
+// launch 1: one block per filter
+__global__ void __launch_bounds__(kThreads) band_stop_sums_kernel(BandStopArgs a) {
+  __shared__ float red[32];
+  const int f = blockIdx.x;
+  const int h = a.f_half[f];
+  const BsLowpass lo(a.f_lo[f], h), hi(a.f_hi[f], h);
+  double sl = 0.0, sh = 0.0;
+  for (int t = static_cast<int>(threadIdx.x) - h; t <= h; t += kThreads) {
+    sl += lo.tap(t);
+    sh += hi.tap(t);
+  }
+  float fl = static_cast<float>(sl), fh = static_cast<float>(sh);
+  block_sum2(fl, fh, red);
+  const float2 sm = make_float2(fl, fh);
+  if (threadIdx.x == 0) a.sums[f] = sm;
+  if (h <= kBsCirc)
+    for (int t = threadIdx.x; t <= h; t += kThreads) a.taps[int64_t(f) * (kBsCirc + 1) + t] = bs_g(lo, hi, sm, t);
+}
+
+// launch 2: one block per spectrum: circular kernel kappa[m] = g[(-m) mod T]
+// (|t| <= h) or overlap-save partition p: kappa[0] = f_p[0], kappa[T - k] = f_p[k]
+__global__ void __launch_bounds__(kThreads) band_stop_spectrum_kernel(BandStopArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   cf* z = reinterpret_cast<cf*>(smem);
-  float* red = smem + 2 * kM;
   cf* thi = reinterpret_cast<cf*>(smem + 2 * kM + 32);
   cf* tlo = thi + kTwHi;
   load_tw(thi, tlo, a.thi, a.tlo);
   const cf* twn = reinterpret_cast<const cf*>(a.twn);
+  const int sidx = blockIdx.x, f = a.s_filt[sidx], p = a.s_part[sidx];
+  const int h = a.f_half[f], L = 2 * h + 1;
+  const BsLowpass lo(a.f_lo[f], h), hi(a.f_hi[f], h);
+  const float2 sm = a.sums[f];
+  for (int m = threadIdx.x; m < kT; m += kThreads) {
+    float v = 0.f;
+    if (p < 0) {  // circular: tap t = -m or T - m
+      const int t = m <= kT / 2 ? -m : kT - m;
+      if (t >= -h && t <= h) v = bs_g(lo, hi, sm, t);
+    } else {
+      const int k = m == 0 ? 0 : kT - m;
+      const int kk = p * kBsPart + k;
+      if (k < kBsPart && kk < L) v = bs_g(lo, hi, sm, kk - h);
+    }
+    smem[m] = v;
+  }
+  __syncthreads();
+  unsigned long long ph_t0 = 0;
+  transform<false>(z, thi, tlo, ph_t0, 16);
+  cf* H = reinterpret_cast<cf*>(a.spectra) + static_cast<int64_t>(sidx) * kHSlots;
+  for (int q = threadIdx.x; q <= kM; q += kThreads) {
+    const int qq = q % kM, qc = (kM - q) % kM;
+    const cf zk = z[zaddr(qq)];
+    const cf zc = z[zaddr(qc)];
+    const cf fe = 0.5f * cf{zk.x + zc.x, zk.y - zc.y};
+    const cf fo = 0.5f * cf{zk.y + zc.y, zc.x - zk.x};
+    H[hslot(q)] = fe + cmul(twn[hslot(q)], fo);
+  }
+}
+
+// the split, x H, inverse split on (k, M - k) pairs (as augment_kernel)
+__device__ __forceinline__ void bs_multiply(cf* z, const cf* H, const cf* twn) {
+  constexpr int kRest = kM / 2 / 16 + 1;
+  for (int idx = opaque_tid(); idx < 16 * kRest; idx += kThreads) {
+    const int c = idx / kRest;
+    const int k = c + 16 * (idx - c * kRest);
+    if (k > kM / 2) continue;
+    const int kc = (kM - k) % kM;
+    const int pz = zaddr(k);
+    const cf zk = z[pz];
+    const cf zc = z[zaddr(kc)];
+    const cf fe = 0.5f * cf{zk.x + zc.x, zk.y - zc.y};
+    const cf fo = 0.5f * cf{zk.y + zc.y, zc.x - zk.x};
+    const cf wk = twn[hslot(k)];
+    const cf Xk = fe + cmul(wk, fo);
+    const cf Xc = cf{fe.x, -fe.y} + cmul(cf{-wk.x, wk.y}, cf{fo.x, -fo.y});
+    const cf Yk = cmul(Xk, H[hslot(k)]);
+    const cf Yc = cmul(Xc, H[hslot(kM - k)]);
+    const cf s1 = 0.5f * cf{Yk.x + Yc.x, Yk.y - Yc.y};
+    const cf d1 = 0.5f * cf{Yk.x - Yc.x, Yk.y + Yc.y};
+    const cf wd = cmul(cf{wk.x, -wk.y}, d1);
+    const cf s2 = 0.5f * cf{Yc.x + Yk.x, Yc.y - Yk.y};
+    const cf d2 = 0.5f * cf{Yc.x - Yk.x, Yc.y + Yk.y};
+    const cf wd2 = cmul(cf{-wk.x, -wk.y}, d2);
+    z[pz] = s1 + cf{-wd.y, wd.x};
+    if (kc != k) z[zaddr(kc)] = s2 + cf{-wd2.y, wd2.x};
+  }
+}
+
+// launch 3: one block per clip (grid-strided)
+__global__ void __launch_bounds__(kThreads) band_stop_kernel(BandStopArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  cf* z = reinterpret_cast<cf*>(smem);
+  cf* thi = reinterpret_cast<cf*>(smem + 2 * kM + 32);
+  cf* tlo = thi + kTwHi;
+  float* gt = reinterpret_cast<float*>(tlo + kTwLo);  // [kBsCirc + 1] taps g[0..h]
+  float* xe = gt + kBsCirc + 1;                        // [4 kBsCirc]: x[0, 2h), x[T - 2h, T)
+  load_tw(thi, tlo, a.thi, a.tlo);
+  const cf* twn = reinterpret_cast<const cf*>(a.twn);
   float* zf = smem;
-  float* xs = a.scratch + static_cast<int64_t>(blockIdx.x) * kBsScratch;
-  cf* Hs = reinterpret_cast<cf*>(xs + kT);
+  float* xs = a.scratch + static_cast<int64_t>(blockIdx.x) * kT;
   unsigned long long ph_t0 = 0;
   for (int64_t e = blockIdx.x; e < a.n; e += gridDim.x) {
     const int64_t clip = a.idx[e];
     const float* x = a.x + clip * a.x_stride;
     float* out = a.out + clip * a.out_stride;
-    const int h = a.half[e];
-    const int L = 2 * h + 1;
-    const float cl = a.cut_lo[e], ch = a.cut_hi[e];
-    const float two_cl = static_cast<float>(2.0 * double(cl)), two_ch = static_cast<float>(2.0 * double(ch));
-    const float tpi_l = static_cast<float>(2.0 * double(cl) * M_PI), tpi_h = static_cast<float>(2.0 * double(ch) * M_PI);
-    const float wstep = static_cast<float>(2.0 * M_PI / double(L - 1));
-    // 1) the clip -> scratch; the two lowpass sums (float32 taps, float64 per-thread sums)
-    __syncthreads();  // the previous clip's readers of xs / H are done
-    for (int s = opaque_tid(); s < kT; s += kThreads) xs[s] = x[s];
-    double sl = 0.0, sh = 0.0;
-    for (int t = opaque_tid() - h; t <= h; t += kThreads) {
-      sl += bs_tap(two_cl, tpi_l, wstep, h, t);
-      sh += bs_tap(two_ch, tpi_h, wstep, h, t);
-    }
-    float fsl = static_cast<float>(sl), fsh = static_cast<float>(sh);
-    block_sum2(fsl, fsh, red);  // (its barriers also publish xs)
-    const int parts = (L + kBsPart - 1) / kBsPart;
-    for (int p = 0; p < parts; ++p) {
-      // 2) kernel of partition p into LDS, its spectrum into the scratch
-      __syncthreads();  // the previous partition's output loop is done reading zf
-      for (int m = opaque_tid(); m < kT; m += kThreads) {
-        const int k = m == 0 ? 0 : kT - m;  // kappa[m] = f_p[(-m) mod N]
-        const int kk = p * kBsPart + k;     // filter tap index, t = kk - h
-        float v = 0.f;
-        if (k < kBsPart && kk < L) {
-          const int t = kk - h;
-          v = bs_tap(two_ch, tpi_h, wstep, h, t) / fsh - bs_tap(two_cl, tpi_l, wstep, h, t) / fsl;
-        }
-        zf[m] = v;
+    const int f = a.filt[e];
+    const int h = a.f_half[f];
+    const cf* H0 = reinterpret_cast<const cf*>(a.spectra) + static_cast<int64_t>(a.f_spec0[f]) * kHSlots;
+    __syncthreads();  // the previous clip's readers of LDS / xs are done
+    if (h <= kBsCirc) {
+      // circular convolution + direct correction of the 2h edge samples
+      for (int s = opaque_tid(); s < kT; s += kThreads) zf[s] = x[s];
+      for (int t = threadIdx.x; t <= h; t += kThreads) gt[t] = a.taps[int64_t(f) * (kBsCirc + 1) + t];
+      for (int i = threadIdx.x; i < 2 * h; i += kThreads) {
+        xe[i] = x[i];
+        xe[2 * kBsCirc + i] = x[kT - 2 * h + i];
       }
       __syncthreads();
-      transform<false>(z, thi, tlo, ph_t0, 16);
-      for (int q = opaque_tid(); q <= kM; q += kThreads) {
-        const int qq = q % kM, qc = (kM - q) % kM;
-        const cf zk = z[zaddr(qq)];
-        const cf zc = z[zaddr(qc)];
-        const cf fe = 0.5f * cf{zk.x + zc.x, zk.y - zc.y};
-        const cf fo = 0.5f * cf{zk.y + zc.y, zc.x - zk.x};
-        Hs[hslot(q)] = fe + cmul(twn[hslot(q)], fo);
+      // edge sample of this thread (n < h, or n >= T - h), computed before the
+      // transform overwrites nothing it needs (x edges and taps live apart from z)
+      const int tid = threadIdx.x;
+      float corr = 0.f;
+      int n_edge = -1;
+      if (tid < 2 * h) {
+        const float* xb = xe + 2 * kBsCirc;  // xb[j] = x[T - 2h + j]
+        if (tid < h) {  // n = tid: taps d = -h .. -n-1 wrapped to x[T + n + d]
+          n_edge = tid;
+          const float x0 = xe[0];
+          for (int d = -h; d < -n_edge; ++d) corr += gt[-d] * (x0 - xb[2 * h + n_edge + d]);
+        } else {  // n = T - 2h + tid: taps d = T - n .. h wrapped to x[n + d - T]
+          n_edge = kT - 2 * h + tid;
+          const float x1 = xb[2 * h - 1];
+          for (int d = kT - n_edge; d <= h; ++d) corr += gt[d] * (x1 - xe[n_edge + d - kT]);
+        }
       }
-      // 3) the two output halves
+      transform<false>(z, thi, tlo, ph_t0, 16);
+      bs_multiply(z, H0, twn);
+      __syncthreads();
+      transform<true>(z, thi, tlo, ph_t0, 16);
+      // out = x - conv (x re-read from global: each thread reads then writes only its own samples)
+      for (int s = opaque_tid(); s < kT; s += kThreads) {
+        const bool edge = s < h || s >= kT - h;
+        if (!edge) out[s] = x[s] - zf[s] * (1.f / kM);
+      }
+      if (n_edge >= 0) {
+        const float xv = n_edge < h ? xe[n_edge] : xe[2 * kBsCirc + n_edge - (kT - 2 * h)];
+        out[n_edge] = xv - (zf[n_edge] * (1.f / kM) + corr);
+      }
+      continue;
+    }
+    // overlap-save over partitions of kBsPart taps
+    for (int s = opaque_tid(); s < kT; s += kThreads) xs[s] = x[s];
+    const int parts = (2 * h + 1 + kBsPart - 1) / kBsPart;
+    for (int p = 0; p < parts; ++p) {
+      const cf* Hp = H0 + static_cast<int64_t>(p) * kHSlots;
       for (int b = 0; b < 2; ++b) {
-        __syncthreads();  // H complete; the previous transform's readers of z are done
+        __syncthreads();  // xs published; the previous transform's readers of z are done
         const int base = b * kBsHalf + p * kBsPart - h;
         for (int j = opaque_tid(); j < kT; j += kThreads) zf[j] = xs[min(max(base + j, 0), kT - 1)];
         __syncthreads();
         transform<false>(z, thi, tlo, ph_t0, 16);
-        // split, x H, inverse split on (k, M - k) pairs (as augment_kernel)
-        const int ts = opaque_tid();
-        constexpr int kRest = kM / 2 / 16 + 1;
-        for (int idx = ts; idx < 16 * kRest; idx += kThreads) {
-          const int c = idx / kRest;
-          const int k = c + 16 * (idx - c * kRest);
-          if (k > kM / 2) continue;
-          const int kc = (kM - k) % kM;
-          const int pz = zaddr(k);
-          const cf zk = z[pz];
-          const cf zc = z[zaddr(kc)];
-          const cf fe = 0.5f * cf{zk.x + zc.x, zk.y - zc.y};
-          const cf fo = 0.5f * cf{zk.y + zc.y, zc.x - zk.x};
-          const cf wk = twn[hslot(k)];
-          const cf Xk = fe + cmul(wk, fo);
-          const cf Xc = cf{fe.x, -fe.y} + cmul(cf{-wk.x, wk.y}, cf{fo.x, -fo.y});
-          const cf Yk = cmul(Xk, Hs[hslot(k)]);
-          const cf Yc = cmul(Xc, Hs[hslot(kM - k)]);
-          const cf s1 = 0.5f * cf{Yk.x + Yc.x, Yk.y - Yc.y};
-          const cf d1 = 0.5f * cf{Yk.x - Yc.x, Yk.y + Yc.y};
-          const cf wd = cmul(cf{wk.x, -wk.y}, d1);
-          const cf s2 = 0.5f * cf{Yc.x + Yk.x, Yc.y - Yk.y};
-          const cf d2 = 0.5f * cf{Yc.x - Yk.x, Yc.y + Yk.y};
-          const cf wd2 = cmul(cf{-wk.x, -wk.y}, d2);
-          z[pz] = s1 + cf{-wd.y, wd.x};
-          if (kc != k) z[zaddr(kc)] = s2 + cf{-wd2.y, wd2.x};
-        }
+        bs_multiply(z, Hp, twn);
         __syncthreads();
         transform<true>(z, thi, tlo, ph_t0, 16);
         // y = x - sum_p c_p: each thread revisits only the samples it wrote before
@@ -1255,6 +1355,7 @@ struct hbk_reverb_plan {
 
 namespace {
 constexpr size_t kAugLds = (size_t(2 * hbk::kM + 32) * sizeof(float)) + (hbk::kTwHi + hbk::kTwLo) * sizeof(float2);
+constexpr size_t kBandStopLds = kAugLds + (5 * hbk::kBsCirc + 1) * sizeof(float);  // + taps g[0..h], the edges
 constexpr size_t kColoredLds = (size_t(2 * hbk::kM1 + 32) * sizeof(float)) + (hbk::kTw8Hi + hbk::kTw8Lo) * sizeof(float2);
 }
 
@@ -1317,6 +1418,8 @@ int hbk_reverb_plan_create(int64_t T, hbk_reverb_plan** plan) {
       (e = hipFuncSetAttribute(reinterpret_cast<const void*>(spectrum_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, int(lds))) != hipSuccess ||
       (e = hipFuncSetAttribute(reinterpret_cast<const void*>(band_stop_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, int(kBandStopLds))) != hipSuccess ||
+      (e = hipFuncSetAttribute(reinterpret_cast<const void*>(band_stop_spectrum_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, int(lds))) != hipSuccess ||
       (e = hipFuncSetAttribute(reinterpret_cast<const void*>(colored_noise_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, int(kColoredLds))) != hipSuccess) {
@@ -1422,24 +1525,33 @@ int hbk_colored_noise(const hbk_reverb_plan* p, const float* x, int64_t n_clips,
   return HBK_OK;
 }
 
-int64_t hbk_band_stop_workspace_size(int64_t n, void* stream) {
+int64_t hbk_band_stop_workspace_size(int64_t n, int32_t n_filters, int32_t n_spectra, void* stream) {
   using namespace hbk;
   if (n <= 0) return 0;
-  return std::min<int64_t>(n, persistent_blocks(1, stream)) * kBsScratch * int64_t(sizeof(float));
+  const int64_t blocks = std::min<int64_t>(n, persistent_blocks(1, stream));
+  int64_t b = ((int64_t(n_filters) * 8 + 255) & ~int64_t(255));                          // sums
+  b += ((int64_t(n_filters) * (kBsCirc + 1) * 4 + 255) & ~int64_t(255));                 // taps
+  b += int64_t(n_spectra) * kHSlots * 8;                                                  // spectra
+  b += blocks * kT * 4;                                                                   // clips
+  return b;
 }
 
-int hbk_band_stop(const hbk_reverb_plan* p, const float* x, int64_t x_stride, const int32_t* idx, int64_t n,
-                  const float* cut_lo, const float* cut_hi, const int32_t* half, float* out, int64_t out_stride,
-                  void* workspace, int64_t workspace_bytes, void* stream) {
+int hbk_band_stop(const hbk_reverb_plan* p, const float* x, int64_t x_stride, int64_t n, const int32_t* idx,
+                  const int32_t* filt, int32_t n_filters, const float* f_lo, const float* f_hi,
+                  const int32_t* f_half, const int32_t* f_spec0, int32_t n_spectra, const int32_t* s_filt,
+                  const int32_t* s_part, float* out, int64_t out_stride, void* workspace, int64_t workspace_bytes,
+                  void* stream) {
   using namespace hbk;
   if (!p) return arg_error("plan is NULL");
-  if (n < 0) return arg_error("negative n");
+  if (n < 0 || n_filters < 0 || n_spectra < 0) return arg_error("negative count");
   if (n == 0) return HBK_OK;
-  if (!x || !idx || !cut_lo || !cut_hi || !half || !out || !workspace) return arg_error("NULL pointer");
+  if (n_filters == 0 || n_spectra < n_filters) return arg_error("every filter needs at least one spectrum");
+  if (!x || !idx || !filt || !f_lo || !f_hi || !f_half || !f_spec0 || !s_filt || !s_part || !out || !workspace)
+    return arg_error("NULL pointer");
   if (x_stride < kT || out_stride < kT) return arg_error("stride < 23040");
-  const int64_t blocks = std::min<int64_t>(n, persistent_blocks(1, stream));
-  if (workspace_bytes < blocks * kBsScratch * int64_t(sizeof(float)))
+  if (workspace_bytes < hbk_band_stop_workspace_size(n, n_filters, n_spectra, stream))
     return arg_error("workspace too small (hbk_band_stop_workspace_size)");
+  const int64_t blocks = std::min<int64_t>(n, persistent_blocks(1, stream));
   BandStopArgs a;
   a.x = x;
   a.x_stride = x_stride;
@@ -1447,14 +1559,32 @@ int hbk_band_stop(const hbk_reverb_plan* p, const float* x, int64_t x_stride, co
   a.out_stride = out_stride;
   a.n = n;
   a.idx = idx;
-  a.cut_lo = cut_lo;
-  a.cut_hi = cut_hi;
-  a.half = half;
-  a.scratch = static_cast<float*>(workspace);
+  a.filt = filt;
+  a.n_filters = n_filters;
+  a.f_lo = f_lo;
+  a.f_hi = f_hi;
+  a.f_half = f_half;
+  a.f_spec0 = f_spec0;
+  a.n_spectra = n_spectra;
+  a.s_filt = s_filt;
+  a.s_part = s_part;
+  unsigned char* w = static_cast<unsigned char*>(workspace);
+  a.sums = reinterpret_cast<float2*>(w);
+  w += (int64_t(n_filters) * 8 + 255) & ~int64_t(255);
+  a.taps = reinterpret_cast<float*>(w);
+  w += (int64_t(n_filters) * (kBsCirc + 1) * 4 + 255) & ~int64_t(255);
+  a.spectra = reinterpret_cast<float2*>(w);
+  w += int64_t(n_spectra) * kHSlots * 8;
+  a.scratch = reinterpret_cast<float*>(w);
   a.thi = p->thi;
   a.tlo = p->tlo;
   a.twn = p->twn;
-  hipLaunchKernelGGL(band_stop_kernel, dim3(unsigned(blocks)), dim3(kThreads), kAugLds, as_stream(stream), a);
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(band_stop_sums_kernel, dim3(unsigned(n_filters)), dim3(kThreads), 0, st, a);
+  HBK_LAUNCH_CHECK("band_stop_sums_kernel");
+  hipLaunchKernelGGL(band_stop_spectrum_kernel, dim3(unsigned(n_spectra)), dim3(kThreads), kAugLds, st, a);
+  HBK_LAUNCH_CHECK("band_stop_spectrum_kernel");
+  hipLaunchKernelGGL(band_stop_kernel, dim3(unsigned(blocks)), dim3(kThreads), kBandStopLds, st, a);
   HBK_LAUNCH_CHECK("band_stop_kernel");
   return HBK_OK;
 }

@@ -655,6 +655,9 @@ def _tanh_distortion_op(x: torch.Tensor, amount: torch.Tensor, out: torch.Tensor
                                     stream_ptr(x.device)), "hbk_tanh_distortion")
 
 
+BAND_STOP_CIRCULAR_MAX_HALF = 512  # HBK_BAND_STOP_CIRCULAR_MAX_HALF (include/hbk.h)
+
+
 class ReverbPlan:
     """Batch augmentation on the HIP path (hbk_reverb_* / hbk_augment):
     background-noise mix + IR reverb for clips of 23,040 samples."""
@@ -795,16 +798,26 @@ class ReverbPlan:
         idx_h = idx.detach().to("cpu", torch.int32).reshape(-1)
         if bool(((idx_h < 0) | (idx_h >= n)).any()):
             raise ValueError("idx out of range")
+        # one filter per distinct cutoff pair (a batch's clips share theirs)
+        pairs, filt = np.unique(np.stack([lo_h.numpy(), hi_h.numpy()], 1), axis=0, return_inverse=True)
         # julius LowPassFilters.half_size = int(zeros / min(cutoffs) / 2), zeros = 8
-        half = torch.tensor([int(8 / float(c) / 2) for c in lo_h.tolist()], dtype=torch.int32)
+        half = np.array([int(8 / float(c) / 2) for c in pairs[:, 0].tolist()], dtype=np.int32)
+        nspec = np.where(half <= BAND_STOP_CIRCULAR_MAX_HALF, 1, (2 * half + 1 + 11520) // 11521).astype(np.int32)
+        spec0 = np.concatenate([[0], np.cumsum(nspec)[:-1]]).astype(np.int32)
+        s_filt = np.repeat(np.arange(len(pairs), dtype=np.int32), nspec)
+        s_part = np.concatenate([[-1] if h <= BAND_STOP_CIRCULAR_MAX_HALF else np.arange(k)
+                                 for h, k in zip(half, nspec)]).astype(np.int32)
 
-        def to_dev(t: torch.Tensor) -> torch.Tensor:
-            return t.contiguous().pin_memory().to(self.device, non_blocking=True)
+        def to_dev(a) -> torch.Tensor:
+            return torch.from_numpy(np.ascontiguousarray(a)).pin_memory().to(self.device, non_blocking=True)
 
-        ws_bytes = int(lib().hbk_band_stop_workspace_size(e, stream_ptr(self.device)))
+        nf, ns = len(pairs), int(nspec.sum())
+        ws_bytes = int(lib().hbk_band_stop_workspace_size(e, nf, ns, stream_ptr(self.device)))
         if self._bs_ws is None or self._bs_ws.numel() < ws_bytes:
             self._bs_ws = torch.empty(ws_bytes, dtype=torch.uint8, device=self.device)
-        torch.ops.hbk.band_stop_(x, to_dev(idx_h), to_dev(lo_h), to_dev(hi_h), to_dev(half), out, self._bs_ws,
+        torch.ops.hbk.band_stop_(x, to_dev(idx_h.numpy()), to_dev(filt.astype(np.int32).reshape(-1)),
+                                 to_dev(pairs[:, 0].astype(np.float32)), to_dev(pairs[:, 1].astype(np.float32)),
+                                 to_dev(half), to_dev(spec0), to_dev(s_filt), to_dev(s_part), out, self._bs_ws,
                                  self.id)
         return out
 
@@ -848,9 +861,11 @@ def _colored_noise_op(x: torch.Tensor, white: torch.Tensor | None, f_decay: torc
 
 
 @torch.library.custom_op("hbk::band_stop_", mutates_args=("out", "workspace"))
-def _band_stop_op(x: torch.Tensor, idx: torch.Tensor, cut_lo: torch.Tensor, cut_hi: torch.Tensor,
-                  half: torch.Tensor, out: torch.Tensor, workspace: torch.Tensor, plan_id: int) -> None:
+def _band_stop_op(x: torch.Tensor, idx: torch.Tensor, filt: torch.Tensor, f_lo: torch.Tensor, f_hi: torch.Tensor,
+                  f_half: torch.Tensor, f_spec0: torch.Tensor, s_filt: torch.Tensor, s_part: torch.Tensor,
+                  out: torch.Tensor, workspace: torch.Tensor, plan_id: int) -> None:
     plan = _plans[plan_id]
-    check(lib().hbk_band_stop(plan._handle, ptr(x), x.stride(0), ptr(idx), idx.numel(), ptr(cut_lo), ptr(cut_hi),
-                              ptr(half), ptr(out), out.stride(0), ptr(workspace), workspace.numel(),
+    check(lib().hbk_band_stop(plan._handle, ptr(x), x.stride(0), idx.numel(), ptr(idx), ptr(filt), f_lo.numel(),
+                              ptr(f_lo), ptr(f_hi), ptr(f_half), ptr(f_spec0), s_filt.numel(), ptr(s_filt),
+                              ptr(s_part), ptr(out), out.stride(0), ptr(workspace), workspace.numel(),
                               stream_ptr(x.device)), "hbk_band_stop")

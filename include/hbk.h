@@ -324,20 +324,27 @@ int hbk_colored_noise(const hbk_reverb_plan* plan, const float* x, int64_t n_cli
                       const float* snr_db, float sample_rate, float* out, int64_t out_stride, void* stream);
 
 /* Band-stop: torch_audiomentations BandStopFilter, which the reference applies
- * in its batch chain with p 0.25 per batch and parameters per clip (center
- * mel-uniform in [200, 4000] Hz, bandwidth fraction U[0.5, 1.99];
- * dataset/augmented.py:101-105, constants.py:127). For entry e < n, clip row
- * r = idx[e] of x [*, x_stride] (first T = 23040 samples):
- *   out[r] = x[r] - julius.bandpass_filter(x[r], cut_lo[e], cut_hi[e])
- * with julius' windowed-sinc lowpasses of half size half[e] = int(8 / cut_lo / 2)
- * over the replicate-padded clip (cutoffs as fractions of the sample rate).
- * Rows not listed are not touched; out may equal x. workspace: at least
- * hbk_band_stop_workspace_size(n, stream) bytes (one clip + one spectrum per
- * resident workgroup). Device pointers. */
-int64_t hbk_band_stop_workspace_size(int64_t n, void* stream);
-int hbk_band_stop(const hbk_reverb_plan* plan, const float* x, int64_t x_stride, const int32_t* idx, int64_t n,
-                  const float* cut_lo, const float* cut_hi, const int32_t* half, float* out, int64_t out_stride,
-                  void* workspace, int64_t workspace_bytes, void* stream);
+ * in its batch chain with p 0.25 per batch, one parameter set per batch
+ * (center mel-uniform in [200, 4000] Hz, bandwidth fraction U[0.5, 1.99];
+ * dataset/augmented.py:101-105, constants.py:127). Filter f: cutoffs f_lo[f],
+ * f_hi[f] (fractions of the sample rate) and julius' half size
+ * f_half[f] = int(8 / f_lo / 2); its spectra are slots f_spec0[f] .. of the
+ * n_spectra listed in s_filt / s_part: ONE slot with s_part = -1 when
+ * f_half <= HBK_BAND_STOP_CIRCULAR_MAX_HALF (circular convolution + direct edge
+ * correction), else ceil((2 f_half + 1) / 11521) slots with s_part = 0, 1, ..
+ * (overlap-save partitions). For entry e < n, clip row r = idx[e] of x
+ * [*, x_stride] (first T = 23040 samples):
+ *   out[r] = x[r] - julius.bandpass_filter(x[r], f_lo[filt[e]], f_hi[filt[e]])
+ * (windowed-sinc lowpasses over the replicate-padded clip). Rows not listed are
+ * not touched; out may equal x. workspace: hbk_band_stop_workspace_size bytes.
+ * Device pointers. */
+#define HBK_BAND_STOP_CIRCULAR_MAX_HALF 512
+int64_t hbk_band_stop_workspace_size(int64_t n, int32_t n_filters, int32_t n_spectra, void* stream);
+int hbk_band_stop(const hbk_reverb_plan* plan, const float* x, int64_t x_stride, int64_t n, const int32_t* idx,
+                  const int32_t* filt, int32_t n_filters, const float* f_lo, const float* f_hi,
+                  const int32_t* f_half, const int32_t* f_spec0, int32_t n_spectra, const int32_t* s_filt,
+                  const int32_t* s_part, float* out, int64_t out_stride, void* workspace, int64_t workspace_bytes,
+                  void* stream);
 
 /* Tanh distortion: audiomentations TanhDistortion, which the reference applies
  * per clip with p 0.25 and distortion ~ U[1e-4, 0.1] before the batch chain

@@ -489,20 +489,25 @@ def test_band_stop_matches_oracle(inplace):
     the longest the reference draws (half size 64,000: 12 partitions of the
     overlap-save scheme), a step clip (replicate padding) and an unlisted clip."""
     from heybuddy.kernels import ReverbPlan
-    x = _clips(8, seed=41).astype(np.float32)
+    x = _clips(10, seed=41).astype(np.float32)
     x[6] = np.where(np.arange(T) < T // 3, 0.4, -0.2)          # step: the padded edges matter
-    cut_lo = np.array([0.1875, 0.03, 2.0e-3, 6.0e-4, 3.3e-4, 1.3e-4, 0.01, np.nan], np.float32)
-    cut_hi = np.array([0.45, 0.2, 0.1, 0.05, 2.0e-3, 0.4987, 0.03, np.nan], np.float32)
+    x[8] = np.where(np.arange(T) > T - 300, 0.5, x[8])         # a step inside the last h samples
+    # half sizes 21, 133 (circular path), 2000, 6666, 12121, 30769 (1, 2, 3, 6
+    # overlap-save partitions), 400 (circular), -, 512 (largest circular), 513
+    cut_lo = np.array([0.1875, 0.03, 2.0e-3, 6.0e-4, 3.3e-4, 1.3e-4, 0.01, np.nan, 0.0078125, 0.00779],
+                      np.float32)
+    cut_hi = np.array([0.45, 0.2, 0.1, 0.05, 2.0e-3, 0.4987, 0.03, np.nan, 0.02, 0.3], np.float32)
     sel = np.flatnonzero(~np.isnan(cut_lo)).astype(np.int32)   # clip 7 is not listed
     ref = oaug.band_stop(x, cut_lo, cut_hi)
     plan = ReverbPlan(0)
     xd = torch.from_numpy(x).cuda()
     out = plan.band_stop(xd, torch.from_numpy(sel), torch.from_numpy(cut_lo[sel]), torch.from_numpy(cut_hi[sel]),
                          out=xd if inplace else None).cpu().numpy()
-    for i in range(8):
+    assert [oaug.bandstop_half_size(c) for c in cut_lo[8:]] == [512, 513]
+    for i in range(10):
         tol = 2e-5 * max(np.abs(x[i]).max(), np.abs(ref[i]).max())
         err = np.abs(out[i] - ref[i]).max()
-        assert err <= tol, f"clip {i} (half size {oaug.bandstop_half_size(cut_lo[i]) if i < 7 else 0}): {err} > {tol}"
+        assert err <= tol, f"clip {i} (half size {oaug.bandstop_half_size(cut_lo[i]) if i != 7 else 0}): {err} > {tol}"
     np.testing.assert_array_equal(out[7], x[7])
 
 
