@@ -864,6 +864,8 @@ struct ColoredArgs {
   const float* f_decay;   // per clip
   const float* snr_db;    // per clip
   float lin_step;         // (sqrt(8000) - 1) / 8000: linspace step over the 8001 bins
+  const int32_t* idx;     // NULL: every clip; else the n_entries listed clip rows (balanced launch)
+  int64_t n_entries;
   const float2* thi;
   const float2* tlo;
   const float2* twn;
@@ -1001,7 +1003,9 @@ __global__ void __launch_bounds__(kThreads) colored_noise_kernel(ColoredArgs a) 
   for (int i = threadIdx.x; i < kTw8Lo; i += kThreads) tlo[i] = cf{a.tlo[i].x, a.tlo[i].y};
   float* zf = smem;
   constexpr int kPer = (kT + kThreads - 1) / kThreads;
-  for (int64_t clip = blockIdx.x; clip < a.n_clips; clip += gridDim.x) {
+  const int64_t n_iter = a.idx ? a.n_entries : a.n_clips;
+  for (int64_t e = blockIdx.x; e < n_iter; e += gridDim.x) {
+    const int64_t clip = a.idx ? a.idx[e] : e;
     const int tid = opaque_tid();
     const float snr = a.snr_db[clip];
     if (snr != snr) {  // NaN: this clip's batch drew no colored noise (uniform per block)
@@ -1089,6 +1093,8 @@ struct TanhArgs {
   int64_t out_stride;
   int64_t n_clips;
   const float* amount;  // per clip; NaN = clip unchanged
+  const int32_t* idx;   // NULL: every clip; else the n_entries listed clip rows (balanced launch)
+  int64_t n_entries;
 };
 
 // |x| bits of slot u (u < kPer), or ~0 past the end of the clip (above every value);
@@ -1103,7 +1109,9 @@ tanh_distortion_kernel(TanhArgs a) {
   __shared__ float red[32];
   __shared__ unsigned pick[2];  // selected digit, rank left within it
   constexpr int kPer = (kT + kThreads - 1) / kThreads;
-  for (int64_t clip = blockIdx.x; clip < a.n_clips; clip += gridDim.x) {
+  const int64_t n_iter = a.idx ? a.n_entries : a.n_clips;
+  for (int64_t e = blockIdx.x; e < n_iter; e += gridDim.x) {
+    const int64_t clip = a.idx ? a.idx[e] : e;
     const int tid = opaque_tid();
     const float* x = a.x + clip * a.x_stride;
     float* out = a.out + clip * a.out_stride;
@@ -1492,7 +1500,8 @@ int hbk_augment(const hbk_reverb_plan* p, const float* x, int64_t n_clips, int64
 
 int hbk_colored_noise(const hbk_reverb_plan* p, const float* x, int64_t n_clips, int64_t x_stride,
                       const float* white, int64_t white_stride, uint64_t seed, const float* f_decay,
-                      const float* snr_db, float sample_rate, float* out, int64_t out_stride, void* stream) {
+                      const float* snr_db, float sample_rate, const int32_t* idx, int64_t n_entries, float* out,
+                      int64_t out_stride, void* stream) {
   using namespace hbk;
   if (!p) return arg_error("plan is NULL");
   if (n_clips < 0) return arg_error("negative n_clips");
@@ -1516,10 +1525,13 @@ int hbk_colored_noise(const hbk_reverb_plan* p, const float* x, int64_t n_clips,
   a.f_decay = f_decay;
   a.snr_db = snr_db;
   a.lin_step = static_cast<float>((std::sqrt(double(kN1) / 2.0) - 1.0) / double(kM1));
+  a.idx = idx;
+  a.n_entries = idx ? n_entries : n_clips;
   a.thi = p->thi8;
   a.tlo = p->tlo8;
   a.twn = p->twn16;
-  const int64_t blocks = std::min<int64_t>(n_clips, persistent_blocks(1, stream));
+  if (a.n_entries <= 0) return n_entries < 0 ? arg_error("negative n_entries") : HBK_OK;
+  const int64_t blocks = std::min<int64_t>(a.n_entries, persistent_blocks(1, stream));
   hipLaunchKernelGGL(colored_noise_kernel, dim3(unsigned(blocks)), dim3(kThreads), kColoredLds, as_stream(stream), a);
   HBK_LAUNCH_CHECK("colored_noise_kernel");
   return HBK_OK;
@@ -1606,8 +1618,8 @@ int hbk_place_clips(const float* src, int64_t n_clips, int64_t src_stride, const
   return HBK_OK;
 }
 
-int hbk_tanh_distortion(const float* x, int64_t n_clips, int64_t x_stride, const float* amount, float* out,
-                        int64_t out_stride, void* stream) {
+int hbk_tanh_distortion(const float* x, int64_t n_clips, int64_t x_stride, const float* amount,
+                        const int32_t* idx, int64_t n_entries, float* out, int64_t out_stride, void* stream) {
   using namespace hbk;
   if (n_clips < 0) return arg_error("negative n_clips");
   if (n_clips == 0) return HBK_OK;
@@ -1620,7 +1632,10 @@ int hbk_tanh_distortion(const float* x, int64_t n_clips, int64_t x_stride, const
   a.out_stride = out_stride;
   a.n_clips = n_clips;
   a.amount = amount;
-  const int64_t blocks = std::min<int64_t>(n_clips, persistent_blocks(2, stream));
+  a.idx = idx;
+  a.n_entries = idx ? n_entries : n_clips;
+  if (a.n_entries <= 0) return n_entries < 0 ? arg_error("negative n_entries") : HBK_OK;
+  const int64_t blocks = std::min<int64_t>(a.n_entries, persistent_blocks(2, stream));
   hipLaunchKernelGGL(tanh_distortion_kernel, dim3(unsigned(blocks)), dim3(kThreads), 0, as_stream(stream), a);
   HBK_LAUNCH_CHECK("tanh_distortion_kernel");
   return HBK_OK;

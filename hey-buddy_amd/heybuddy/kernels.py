@@ -589,9 +589,18 @@ def place_clips(src: torch.Tensor, src_len, pre, T: int = 23040) -> torch.Tensor
     return torch.ops.hbk.place_clips(src, src_len, pre, int(T))
 
 
+def _active_rows(values: torch.Tensor) -> torch.Tensor | None:
+    """int32 rows whose per-clip parameter is not NaN (a host tensor: the
+    indexed, balanced launch), or None for a device tensor (every row)."""
+    if values.device.type != "cpu":
+        return None
+    return torch.from_numpy(np.flatnonzero(~np.isnan(values.numpy())).astype(np.int32))
+
+
 def tanh_distortion(x: torch.Tensor, amount: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     """audiomentations TanhDistortion per clip on x [n, >= 23040] -> out [n, 23040]
-    (hbk_tanh_distortion); amount per clip, NaN leaves the clip unchanged."""
+    (hbk_tanh_distortion); amount per clip, NaN leaves the clip unchanged. A
+    host ``amount`` launches over the clips it switches on only."""
     T = ReverbPlan.T
     dev = _native.require_device(x.device)
     n = x.shape[0]
@@ -600,10 +609,18 @@ def tanh_distortion(x: torch.Tensor, amount: torch.Tensor, out: torch.Tensor | N
     amount = amount.to(dtype=torch.float32).reshape(-1).contiguous()
     if amount.numel() != n:
         raise ValueError("amount must have n entries")
+    rows = _active_rows(amount)
     amount = amount.pin_memory().to(dev, non_blocking=True) if amount.device.type == "cpu" else amount.to(dev)
     if out is None:
         out = torch.empty((n, T), dtype=torch.float32, device=dev)
-    torch.ops.hbk.tanh_distortion_(x, amount, out)
+    if rows is not None:
+        if out.data_ptr() != x.data_ptr():
+            out.copy_(x[:, :T])  # the indexed launch writes the listed rows only
+            x = out
+        if rows.numel() == 0:
+            return out
+        rows = rows.pin_memory().to(dev, non_blocking=True)
+    torch.ops.hbk.tanh_distortion_(x, amount, rows, out)
     return out
 
 
@@ -650,9 +667,10 @@ def _seven_band_eq_op(x: torch.Tensor, coef: torch.Tensor, idx: torch.Tensor | N
 
 
 @torch.library.custom_op("hbk::tanh_distortion_", mutates_args=("out",))
-def _tanh_distortion_op(x: torch.Tensor, amount: torch.Tensor, out: torch.Tensor) -> None:
-    check(lib().hbk_tanh_distortion(ptr(x), x.shape[0], x.stride(0), ptr(amount), ptr(out), out.stride(0),
-                                    stream_ptr(x.device)), "hbk_tanh_distortion")
+def _tanh_distortion_op(x: torch.Tensor, amount: torch.Tensor, rows: torch.Tensor | None, out: torch.Tensor) -> None:
+    check(lib().hbk_tanh_distortion(ptr(x), x.shape[0], x.stride(0), ptr(amount),
+                                    ptr(rows) if rows is not None else None, rows.numel() if rows is not None else 0,
+                                    ptr(out), out.stride(0), stream_ptr(x.device)), "hbk_tanh_distortion")
 
 
 BAND_STOP_CIRCULAR_MAX_HALF = 512  # HBK_BAND_STOP_CIRCULAR_MAX_HALF (include/hbk.h)
@@ -769,10 +787,23 @@ class ReverbPlan:
             t = t.to(dtype=torch.float32).reshape(-1).contiguous()
             if t.numel() != n:
                 raise ValueError("per-clip arrays must have n entries")
-            return t.pin_memory().to(self.device, non_blocking=True) if t.device.type == "cpu" else t.to(self.device)
+            return t
 
         f_decay, snr_db = per_clip(f_decay), per_clip(snr_db)
-        torch.ops.hbk.colored_noise_(x, white, f_decay, snr_db, _u64_to_i64(seed), float(sample_rate), out, self.id)
+        rows = _active_rows(snr_db)  # host snr: launch over the clips whose batch drew noise only
+        if rows is not None:
+            if out.data_ptr() != x.data_ptr():
+                out.copy_(x[:, :self.T])  # the indexed launch writes the listed rows only
+                x = out
+            if rows.numel() == 0:
+                return out
+            rows = rows.pin_memory().to(self.device, non_blocking=True)
+
+        def to_dev(t: torch.Tensor) -> torch.Tensor:
+            return t.pin_memory().to(self.device, non_blocking=True) if t.device.type == "cpu" else t.to(self.device)
+
+        torch.ops.hbk.colored_noise_(x, white, to_dev(f_decay), to_dev(snr_db), _u64_to_i64(seed),
+                                     float(sample_rate), rows, out, self.id)
         return out
 
     def band_stop(self, x: torch.Tensor, idx: torch.Tensor, cut_lo: torch.Tensor, cut_hi: torch.Tensor,
@@ -851,13 +882,15 @@ def _augment_op(x: torch.Tensor, ring: torch.Tensor | None, noise_off: torch.Ten
 
 @torch.library.custom_op("hbk::colored_noise_", mutates_args=("out",))
 def _colored_noise_op(x: torch.Tensor, white: torch.Tensor | None, f_decay: torch.Tensor, snr_db: torch.Tensor,
-                      seed: int, sample_rate: float, out: torch.Tensor, plan_id: int) -> None:
+                      seed: int, sample_rate: float, rows: torch.Tensor | None, out: torch.Tensor,
+                      plan_id: int) -> None:
     plan = _plans[plan_id]
     check(lib().hbk_colored_noise(plan._handle, ptr(x), x.shape[0], x.stride(0),
                                   ptr(white) if white is not None else None,
                                   white.stride(0) if white is not None else 0, seed & (2 ** 64 - 1), ptr(f_decay),
-                                  ptr(snr_db), sample_rate, ptr(out), out.stride(0), stream_ptr(x.device)),
-          "hbk_colored_noise")
+                                  ptr(snr_db), sample_rate, ptr(rows) if rows is not None else None,
+                                  rows.numel() if rows is not None else 0, ptr(out), out.stride(0),
+                                  stream_ptr(x.device)), "hbk_colored_noise")
 
 
 @torch.library.custom_op("hbk::band_stop_", mutates_args=("out", "workspace"))

@@ -321,7 +321,8 @@ int hbk_augment(const hbk_reverb_plan* plan, const float* x, int64_t n_clips, in
  * Device pointers. */
 int hbk_colored_noise(const hbk_reverb_plan* plan, const float* x, int64_t n_clips, int64_t x_stride,
                       const float* white, int64_t white_stride, uint64_t seed, const float* f_decay,
-                      const float* snr_db, float sample_rate, float* out, int64_t out_stride, void* stream);
+                      const float* snr_db, float sample_rate, const int32_t* idx, int64_t n_entries, float* out,
+                      int64_t out_stride, void* stream);
 
 /* Band-stop: torch_audiomentations BandStopFilter, which the reference applies
  * in its batch chain with p 0.25 per batch, one parameter set per batch
@@ -368,8 +369,12 @@ int hbk_band_stop(const hbk_reverb_plan* plan, const float* x, int64_t x_stride,
 int hbk_seven_band_eq(const float* x, int64_t n_clips, int64_t x_stride, const double* coef, const int32_t* idx,
                       int64_t n_entries, float* out, int64_t out_stride, void* stream);
 
-int hbk_tanh_distortion(const float* x, int64_t n_clips, int64_t x_stride, const float* amount, float* out,
-                        int64_t out_stride, void* stream);
+/* (tanh distortion and colored noise) idx: NULL runs every clip of
+ * [0, n_clips); else only the n_entries clip rows it lists (the clips or
+ * batches whose coin came up, so the grid's work is balanced), in place or into
+ * out's same rows (the other rows of out are not written). */
+int hbk_tanh_distortion(const float* x, int64_t n_clips, int64_t x_stride, const float* amount,
+                        const int32_t* idx, int64_t n_entries, float* out, int64_t out_stride, void* stream);
 
 /* Clip placement: AugmentedAudioGenerator.to_target_length
  * (dataset/augmented.py:200-232) for a batch already on the device. Per clip i
