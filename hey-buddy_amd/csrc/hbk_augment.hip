@@ -1283,67 +1283,85 @@ struct EqArgs {
   int64_t n;
 };
 
+// Systolic over the cascade: a wave filters 8 clips, 8 lanes per clip; lane
+// s < 7 holds section s's coefficients and state and, at step t, filters sample
+// t - s: its input is section s - 1's output of step t - 1 (DPP row_shr:1),
+// section 0 reads x[t] from the LDS tile, section 6's output is y[t - 6]. Each
+// section runs the same float64 recursion, in the same order, as a one-lane
+// cascade (float32 between sections), so the result is bitwise that of the
+// sequential filter; eight times as many waves fill the chip (the filter is
+// sequential in time, so one lane per clip left most SIMDs idle). A clip whose
+// coefficients are NaN passes through an identity cascade (a copy).
+constexpr int kEqClips = 8;  // clips per wave
 __global__ void __launch_bounds__(64) eq_kernel(EqArgs a) {
-  __shared__ float tile[kEqTile][kEqTile + 1];
-  const int lane = threadIdx.x;
-  const int64_t j0 = static_cast<int64_t>(blockIdx.x) * 64;
-  const int64_t jl = min(j0 + lane, a.n - 1);
-  double co[35];
-#pragma unroll
-  for (int i = 0; i < 35; ++i) co[i] = a.coef[jl * 35 + i];
-  const bool skip = j0 + lane >= a.n || co[0] != co[0];
-  double s1[7], s2[7];
-#pragma unroll
-  for (int k = 0; k < 7; ++k) s1[k] = s2[k] = 0.0;
-  // cooperative mapping: item i of this lane -> entry row (lane + 64 i) / 16,
-  // samples 4 ((lane + 64 i) % 16) .. of the tile; entries past n re-read the
-  // last entry's clip and are never stored
-  int64_t clip[16];
-  float4 pre[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int e = lane + 64 * i;
-    const int64_t j = min(j0 + (e >> 4), a.n - 1);
-    clip[i] = a.idx ? static_cast<int64_t>(a.idx[j]) : j;
-  }
-#pragma unroll
-  for (int i = 0; i < 16; ++i)
-    pre[i] = *reinterpret_cast<const float4*>(a.x + clip[i] * a.x_stride + 4 * ((lane + 64 * i) & 15));
-  for (int t0 = 0; t0 < kT; t0 += kEqTile) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int e = lane + 64 * i, r = e >> 4, q = 4 * (e & 15);
-      tile[q][r] = pre[i].x;
-      tile[q + 1][r] = pre[i].y;
-      tile[q + 2][r] = pre[i].z;
-      tile[q + 3][r] = pre[i].w;
-    }
+  constexpr int kRow = kEqTile + 4;  // 16-B aligned rows (b128 reads / writes of 8 steps)
+  __shared__ __attribute__((aligned(16))) float tin[kEqClips][kRow];
+  __shared__ __attribute__((aligned(16))) float tout[kEqClips][kRow];
+  const int lane = threadIdx.x, c = lane >> 3, sec = lane & 7;
+  const int64_t j0 = static_cast<int64_t>(blockIdx.x) * kEqClips;
+  const int64_t jc = min(j0 + c, a.n - 1);
+  const double* cf0 = a.coef + jc * 35;
+  const bool copy = cf0[0] != cf0[0];
+  const int k = min(sec, 6);
+  double b0 = cf0[5 * k], b1 = cf0[5 * k + 1], b2 = cf0[5 * k + 2], a1 = cf0[5 * k + 3], a2 = cf0[5 * k + 4];
+  if (copy) b0 = 1.0, b1 = b2 = a1 = a2 = 0.0;
+  double s1 = 0.0, s2 = 0.0;
+  // tile I/O mapping: lane -> clip lc = lane >> 3, float4 column lq = lane & 7 (samples 4 lq, 32 + 4 lq)
+  const int lc = lane >> 3, lq = lane & 7;
+  const int64_t jl = min(j0 + lc, a.n - 1);
+  const int64_t clip_l = a.idx ? static_cast<int64_t>(a.idx[jl]) : jl;
+  const float* xl = a.x + clip_l * a.x_stride;
+  float* ol = a.out + clip_l * a.out_stride;
+  const bool store_l = j0 + lc < a.n;
+  float4 p0 = *reinterpret_cast<const float4*>(xl + 4 * lq);
+  float4 p1 = *reinterpret_cast<const float4*>(xl + 32 + 4 * lq);
+  float prev = 0.f;
+  for (int t0 = 0; t0 <= kT; t0 += kEqTile) {  // the last tile only drains the pipeline
+    tin[lc][4 * lq] = p0.x;
+    tin[lc][4 * lq + 1] = p0.y;
+    tin[lc][4 * lq + 2] = p0.z;
+    tin[lc][4 * lq + 3] = p0.w;
+    tin[lc][32 + 4 * lq] = p1.x;
+    tin[lc][32 + 4 * lq + 1] = p1.y;
+    tin[lc][32 + 4 * lq + 2] = p1.z;
+    tin[lc][32 + 4 * lq + 3] = p1.w;
     __syncthreads();
-    const int tn = min(t0 + kEqTile, kT - kEqTile);  // next tile (the last iteration re-reads its own)
+    const int tn = min(t0 + kEqTile, kT - kEqTile);  // next tile (clamped: the drain re-reads the last)
+    p0 = *reinterpret_cast<const float4*>(xl + tn + 4 * lq);
+    p1 = *reinterpret_cast<const float4*>(xl + tn + 32 + 4 * lq);
+    // 8 steps per group: their section-0 inputs read ahead (two b128 reads, one
+    // wait), section 6's outputs written after (branch-free steps in between)
+    for (int st0 = 0; st0 < kEqTile; st0 += 8) {
+      const float4 ia = *reinterpret_cast<const float4*>(&tin[c][st0]);
+      const float4 ib = *reinterpret_cast<const float4*>(&tin[c][st0 + 4]);
+      const float in8[8] = {ia.x, ia.y, ia.z, ia.w, ib.x, ib.y, ib.z, ib.w};
+      float o8[8];
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
-      pre[i] = *reinterpret_cast<const float4*>(a.x + clip[i] * a.x_stride + tn + 4 * ((lane + 64 * i) & 15));
-    if (!skip) {
-      for (int s = 0; s < kEqTile; ++s) {
-        float v = tile[s][lane];
-#pragma unroll
-        for (int k = 0; k < 7; ++k) {
-          const double vd = v;
-          const double y = fma(co[5 * k], vd, s1[k]);
-          s1[k] = fma(co[5 * k + 1], vd, fma(-co[5 * k + 3], y, s2[k]));
-          s2[k] = fma(co[5 * k + 2], vd, -co[5 * k + 4] * y);
-          v = static_cast<float>(y);
-        }
-        tile[s][lane] = v;
+      for (int q = 0; q < 8; ++q) {
+        const float u = sec == 0 ? in8[q] : prev;
+        const double vd = u;
+        const double y = fma(b0, vd, s1);
+        s1 = fma(b1, vd, fma(-a1, y, s2));
+        s2 = fma(b2, vd, -a2 * y);
+        const float v = static_cast<float>(y);
+        o8[q] = v;  // section 6: sample t0 + st0 + q - 6
+        prev = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, prev),
+                                                                     __builtin_bit_cast(int, v), 0x111, 0xF, 0xF,
+                                                                     false));
+      }
+      if (sec == 6) {
+        *reinterpret_cast<float4*>(&tout[c][st0]) = float4{o8[0], o8[1], o8[2], o8[3]};
+        *reinterpret_cast<float4*>(&tout[c][st0 + 4]) = float4{o8[4], o8[5], o8[6], o8[7]};
       }
     }
     __syncthreads();
+    if (store_l) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int e = lane + 64 * i, r = e >> 4, q = 4 * (e & 15);
-      if (j0 + r < a.n)
-        *reinterpret_cast<float4*>(a.out + clip[i] * a.out_stride + t0 + q) =
-            float4{tile[q][r], tile[q + 1][r], tile[q + 2][r], tile[q + 3][r]};
+      for (int m = 0; m < 8; ++m) {
+        const int kk = lq + 8 * m;
+        const int n = t0 - 6 + kk;
+        if (n >= 0 && n < kT) ol[n] = tout[lc][kk];
+      }
     }
     __syncthreads();
   }
@@ -1659,7 +1677,8 @@ int hbk_seven_band_eq(const float* x, int64_t n_clips, int64_t x_stride, const d
   a.out = out;
   a.out_stride = out_stride;
   a.n = n_entries;
-  hipLaunchKernelGGL(eq_kernel, dim3(unsigned((n_entries + 63) / 64)), dim3(64), 0, as_stream(stream), a);
+  hipLaunchKernelGGL(eq_kernel, dim3(unsigned((n_entries + kEqClips - 1) / kEqClips)), dim3(64), 0,
+                     as_stream(stream), a);
   HBK_LAUNCH_CHECK("eq_kernel");
   return HBK_OK;
 }

@@ -1063,6 +1063,7 @@ constexpr int kTM = 128, kTN = 32, kMaxJobs = 2 * kMaxG;
 #endif
 constexpr int kK3Steps = HBK_K3_STEPS, kK3Rows = 32 * kK3Steps;  // batch rows per split (B = 1100: 4 splits)
 constexpr int kYLdH = kK3Rows + 8;                    // LDS row stride (halves) of the Y planes
+constexpr int kK3StepsNarrow = 4, kK3NarrowCUs = 96;
 struct WJob {
   const float* X;  // [M][Bp]
   const float* Y;  // [N][Bp]
@@ -1082,7 +1083,12 @@ struct K3Args {
   float* db_in;
 };
 
+// STEPS: batch rows per split / 32 (the grid's split count follows); the launch
+// takes kK3Steps on a wide stream and kK3StepsNarrow on a CU-masked one of at
+// most kK3NarrowCUs CUs (fewer, longer workgroups: see kK3Steps' sweep)
+template <int STEPS>
 __global__ void __launch_bounds__(256) k3_wgrad_kernel(K3Args a) {
+  constexpr int kK3Steps = STEPS, kK3Rows = 32 * STEPS, kYLdH = kK3Rows + 8;
   __shared__ __attribute__((aligned(16))) _Float16 yh[kTN * kYLdH];
   __shared__ __attribute__((aligned(16))) _Float16 yl[kTN * kYLdH];
   __shared__ float sS[kTM];
@@ -1654,7 +1660,9 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
   // k3: job 0 = input layer, then dW_hg of GMLPs 1.., then dW_o of every GMLP
   K3Args k3;
   int nj = 0, blocks = 0;
-  const int KS3 = static_cast<int>((Bp + kK3Rows - 1) / kK3Rows);
+  const bool narrow = persistent_blocks(1, s) <= kK3NarrowCUs;
+  const int rows3 = 32 * (narrow ? kK3StepsNarrow : kK3Steps);
+  const int KS3 = static_cast<int>((Bp + rows3 - 1) / rows3);
   auto add = [&](const float* X, const float* Y, float* C, int ldc, int M, int N) {
     WJob& j = k3.job[nj];
     j.X = X;
@@ -1683,7 +1691,10 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
   k3.W0 = params + p.g[0].w_hg;
   k3.dg_in = G + p.ln_in.g;
   k3.db_in = G + p.ln_in.b;
-  hipLaunchKernelGGL(k3_wgrad_kernel, dim3(blocks), dim3(256), 0, s, k3);
+  if (narrow)
+    hipLaunchKernelGGL(k3_wgrad_kernel<kK3StepsNarrow>, dim3(blocks), dim3(256), 0, s, k3);
+  else
+    hipLaunchKernelGGL(k3_wgrad_kernel<kK3Steps>, dim3(blocks), dim3(256), 0, s, k3);
   HBK_LAUNCH_CHECK("k3_wgrad_kernel");
   return HBK_OK;
 }

@@ -67,18 +67,37 @@ class _MaskedStream:
         self.handle = handle
         self.stream = torch.cuda.ExternalStream(handle.value, device=device)
         self.cus = list(cus)
+        self.device = device
+        _MASKS[handle.value] = self.cus
 
     def __del__(self):
         try:
             if self.handle:
+                _MASKS.pop(self.handle.value, None)
                 torch.cuda.synchronize()
                 self._lib.hbk_stream_destroy(self.handle)
         except Exception:
             pass
 
 
+_MASKS: dict = {}  # raw stream handle -> its CU set (the live _MaskedStreams)
+
+
 def masked_stream(device: torch.device, cus) -> "_MaskedStream":
     return _MaskedStream(device, cus)
+
+
+def capture_stream(device: torch.device):
+    """A side stream for capturing work that will replay on the current
+    stream: with the current stream's CU mask if it has one, so that kernels
+    sizing their grids (or picking a variant) by the stream's CUs at capture
+    time see the CUs they will replay on. Returns (stream, keep-alive)."""
+    cur = torch.cuda.current_stream(device)
+    cus = _MASKS.get(cur.cuda_stream)
+    if cus is None:
+        return torch.cuda.Stream(device), None
+    ms = _MaskedStream(device, cus)
+    return ms.stream, ms
 
 
 def make_streams(device: torch.device, policy: str) -> Tuple[torch.cuda.Stream, torch.cuda.Stream, list]:

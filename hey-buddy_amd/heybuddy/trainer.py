@@ -43,6 +43,7 @@ from heybuddy.constants import (DEFAULT_ACTIVATION_THRESHOLD, DEFAULT_ARCHITECTU
                                 DEFAULT_TARGET_FALSE_POSITIVE_RATE, DEFAULT_VALIDATION_STEPS,
                                 DEFAULT_WARMUP_STEPS)
 from heybuddy import distributed
+from heybuddy.pipeline import capture_stream
 from heybuddy.util import logger
 from heybuddy.wakeword import WakeWordMLPModel
 
@@ -381,12 +382,12 @@ class WakeWordTrainer(Trainer):
         def graph_of(n: int) -> "torch.cuda.CUDAGraph":
             """The captured graph of n (even) steps from the current parity."""
             key = ("indexed", n, self._parity, B, y_stride, float(threshold), float(activation_threshold), float(p),
-                   ptrs)
+                   ptrs, torch.cuda.current_stream(dev).cuda_stream)
             entry = self._graphs.get(key)
             if entry is not None:
                 return entry[0]
             self._evict_graphs()
-            side = torch.cuda.Stream(dev)
+            side, keep = capture_stream(dev)  # the replay stream's CU mask, if any
             side.wait_stream(torch.cuda.current_stream(dev))
             gr = torch.cuda.CUDAGraph()
             par0 = self._parity
@@ -395,7 +396,7 @@ class WakeWordTrainer(Trainer):
                     for j in range(n):
                         one(par0 ^ (j & 1), True)
             torch.cuda.current_stream(dev).wait_stream(side)
-            self._graphs[key] = (gr, ws)  # the entry keeps the baked-in workspace alive
+            self._graphs[key] = (gr, ws, keep)  # the entry keeps the baked-in workspace alive
             return gr
 
         if graphs and world == 1 and S - done >= 2:
