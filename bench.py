@@ -570,15 +570,39 @@ def setup_e2e(args, dev, rank, world, seed):
         staged_step = step
 
         host_log = os.environ.get("HBK_BENCH_HOSTTIME")
+        # HBK_BENCH_PARTITION=1: each partition's device time per step (events on
+        # its own stream, from its first kernel to its last), printed at exit
+        part = [] if os.environ.get("HBK_BENCH_PARTITION") else None
+        if part is not None:
+            import atexit
+
+            def _report():
+                torch.cuda.synchronize(dev)
+                for name in ("featurize", "train"):
+                    ms = [a.elapsed_time(b) for k, a, b in part if k == name][2:]  # past the warmup
+                    if ms:
+                        print("partition %s: %.2f ms per step (%d steps)" % (name, sum(ms) / len(ms), len(ms)),
+                              file=sys.stderr, flush=True)
+            atexit.register(_report)
+
+        def mark(name, stream):
+            if part is None:
+                return None
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(stream)
+            return e
 
         def featurize(c):
             b = c % 2
             with torch.cuda.stream(fs):
                 fs.wait_event(train_done[b])  # train(c - 2) has finished reading pools[b]
+                e0 = mark("featurize", fs)
                 x = aug.augment_device(src, lens)
                 frames = mel_frames(x, mplan, N_FRAMES)
                 replace_nan_rows_device(embed_clips(frames, eplan, out=raw), out=pools[b])
                 feat_done[b].record(fs)
+                if part is not None:
+                    part.append(("featurize", e0, mark("featurize", fs)))
 
         def step(evs):  # noqa: F811
             # chunk c+1 is featurized while chunk c trains; its work is queued
@@ -594,10 +618,13 @@ def setup_e2e(args, dev, rank, world, seed):
             b = c % 2
             with torch.cuda.stream(ts):
                 ts.wait_event(feat_done[b])
+                e0 = mark("train", ts)
                 sample()
                 tr._reset_accumulation()
                 tr.train_indexed(idx, y, sched, pool32=pools[b], pool16=neg, history=hist, steps_per_graph=50)
                 train_done[b].record(ts)
+                if part is not None:
+                    part.append(("train", e0, mark("train", ts)))
             if host_log:
                 print("host ms: featurize enqueue %.1f, train enqueue %.1f" % (
                     1e3 * (h1 - h0), 1e3 * (time.perf_counter() - h1)), file=sys.stderr, flush=True)
