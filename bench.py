@@ -179,6 +179,7 @@ def main():
     roofs = [job["roofline"](name, ms, args.pmc) for name, ms in zip(job["stages"], stage_ms)]
     dom = max(range(len(roofs)), key=lambda i: stage_ms[i])
 
+    extra = job["extra_rooflines"]() if "extra_rooflines" in job and world == 1 else []
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = job["cpu_baseline"](args.cpu_sample)
@@ -191,7 +192,7 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": job["scaling"], "vs_baseline": None, "dtype": "f32",
             "data": job["data"], "config": job["config"], "roofline": roofs[dom],
-            "roofline_other": [r for i, r in enumerate(roofs) if i != dom], "cpu_baseline": cpu,
+            "roofline_other": [r for i, r in enumerate(roofs) if i != dom] + extra, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -705,8 +706,40 @@ def setup_e2e(args, dev, rank, world, seed):
                 "value_1thread": round(res[1][0], 2),
                 "sample_1thread": f"{res[1][1]} clips + {res[1][3]} train steps, {res[1][2]:.1f} s"}
 
+    def extra_rooflines():
+        """Untimed, after the measurement: the embedding on the generic
+        split-f16 chain kernel alone (HBK_EMBED_NO_P0 / NO_P1: what a graph
+        without SE20's chain shapes would run), on one 16,384-clip chunk."""
+        from heybuddy.kernels import EmbedPlan
+        m = min(n, 16384)
+        frames = mel_frames(aug.augment_device(src[:m], lens[:m]), mplan, N_FRAMES)
+        saved = {k: os.environ.get(k) for k in ("HBK_EMBED_NO_P0", "HBK_EMBED_NO_P1")}
+        os.environ.update({"HBK_EMBED_NO_P0": "1", "HBK_EMBED_NO_P1": "1"})
+        try:
+            gplan = EmbedPlan(default_graph(), starts=WINDOW_STARTS, device=dev, precision=eplan.precision)
+        finally:
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+        out = torch.empty((m, len(WINDOW_STARTS), 96), dtype=torch.float32, device=dev)
+        embed_clips(frames, gplan, out=out)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(3):
+            embed_clips(frames, gplan, out=out)
+        e1.record()
+        torch.cuda.synchronize(dev)
+        ms = e0.elapsed_time(e1) / 3
+        return [roof("conv_chain_x3_kernel only (HBK_EMBED_NO_P0=1 HBK_EMBED_NO_P1=1: the generic split-f16 chain "
+                     "kernel on every chain, as for a graph without SE20's chain shapes; %d clips, untimed)" % m,
+                     "mfma", 2.0 * gplan.macs_per_clip * m, ms, "TFLOP/s", None, peak=SPLIT_PEAK_TFLOPS,
+                     peak_basis="f16 dense MFMA peak / 3", clips=m)]
+
     return {
         "step": step, "staged_step": staged_step, "stages": stages, "roofline": roofline,
+        "extra_rooflines": extra_rooflines,
         "cpu_baseline": cpu_baseline, "units_per_step": n, "scaling": "weak", "unit": "clips/s",
         "metric": "audio clips/sec featurized+trained, 1.5 s @16 kHz, 1/2/4/8 GPU",
         "data": "synthetic TTS-like utterances (seeded, 0.3-1.5 s), synthetic noise + IR banks, synthetic "

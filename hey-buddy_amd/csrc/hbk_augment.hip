@@ -876,12 +876,16 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   return z ^ (z >> 31);
 }
-// standard normal of stream element i (Box-Muller on two 24-bit uniforms)
-__device__ __forceinline__ float gauss(uint64_t seed, uint64_t i) {
+// standard normals 2i and 2i + 1 of the stream (Box-Muller on two 24-bit
+// uniforms of one hash: both the cosine and the sine branch)
+__device__ __forceinline__ float2 gauss2(uint64_t seed, uint64_t i) {
   const uint64_t h = mix64(seed + 0x9E3779B97F4A7C15ull * (i + 1));
   const float u1 = (static_cast<float>(h >> 40) + 0.5f) * (1.f / 16777216.f);
   const float u2 = static_cast<float>((h >> 16) & 0xFFFFFF) * (1.f / 16777216.f);
-  return sqrtf(-2.f * __logf(u1)) * __cosf(6.283185307179586f * u2);
+  const float r = sqrtf(-2.f * __logf(u1));
+  float sn, cs;
+  __sincosf(6.283185307179586f * u2, &sn, &cs);
+  return make_float2(r * cs, r * sn);
 }
 
 // a clip copied through registers: all loads issued before the first store
@@ -1018,7 +1022,10 @@ __global__ void __launch_bounds__(kThreads) colored_noise_kernel(ColoredArgs a) 
       const float* w = a.white + clip * a.white_stride;
       for (int s = tid; s < kN1; s += kThreads) zf[s] = w[s];
     } else {
-      for (int s = tid; s < kN1; s += kThreads) zf[s] = gauss(a.seed, static_cast<uint64_t>(clip) * kN1 + s);
+      for (int q = tid; q < kN1 / 2; q += kThreads) {
+        const float2 g = gauss2(a.seed, static_cast<uint64_t>(clip) * (kN1 / 2) + q);
+        *reinterpret_cast<float2*>(zf + 2 * q) = g;
+      }
     }
     __syncthreads();
     transform8<false>(z, thi, tlo);

@@ -312,7 +312,8 @@ int hbk_augment(const hbk_reverb_plan* plan, const float* x, int64_t n_clips, in
  * constants.py:128-132). Per clip i of x [n_clips, x_stride] (first T = 23040
  * samples used), the package's _gen_noise / apply_transform:
  *   w = white[i][0 .. 16000) (N(0,1), white_stride >= 16000) or, if white ==
- *       NULL, the counter-based N(0,1) stream (seed, i * 16000 + t);
+ *       NULL, the counter-based N(0,1) stream: samples 2q, 2q + 1 of clip i are the
+ *       Box-Muller pair of hash (seed, i * 8000 + q);
  *   n1 = irfft(rfft(w) / linspace(1, sqrt(8000), 8001)^f_decay[i], n = 16000);
  *   n1 /= rms(n1) + 1e-8;  noise[t] = n1[t mod 16000] (tiled to T, not renormalised);
  *   out[i] = x[i] + rms(x[i]) / 10^(snr_db[i] / 20) * noise;
