@@ -1796,12 +1796,12 @@ int layout_split(const std::vector<OpInfo>& ops, const std::vector<int>& stage_o
 // on input width 32, C = 24, one image per source clip; all convs LeakyReLU
 // with one slope in [0, 1], or all linear. Packs the weights / biases and
 // sizes the grid; returns false (generic kernel) when the chain differs.
-constexpr int kP0W = 32, kP0C = 24, kP0Band = 6;
-using P0G = P0Geo<kP0W, kP0C, kP0Band>;
+constexpr int kP0W = 32, kP0C = 24;
 
-bool plan_p0(const std::vector<OpInfo>& ops, const std::vector<int>& st, const ChainArgs& a, Dims d, Dims od,
-             ChainPlan& cp) {
-  if (getenv("HBK_EMBED_NO_P0")) return false;
+template <int kP0Band>
+bool plan_p0_band(const std::vector<OpInfo>& ops, const std::vector<int>& st, const ChainArgs& a, Dims d, Dims od,
+                  ChainPlan& cp) {
+  using P0G = P0Geo<kP0W, kP0C, kP0Band>;
   if (st.size() != 3 || a.ipc != 1 || a.C_src != 1 || a.in_ph != 1 || a.in_pw != 1) return false;
   if (a.out_ph != 2 || a.out_pw != 2 || d.w != kP0W || a.src_row_stride != kP0W) return false;
   const OpInfo &o0 = ops[st[0]], &o1 = ops[st[1]], &o2 = ops[st[2]];
@@ -1875,6 +1875,17 @@ bool plan_p0(const std::vector<OpInfo>& ops, const std::vector<int>& st, const C
     fprintf(stderr, "hbk p0 chain: %dx%dx1 -> %dx%dx%d, band %d (%d bands), LDS %zu B, %d blocks/CU\n", d.h, d.w,
             od.h, od.w, od.c, kP0Band, p.n_bands, cp.p0_lds, per_cu);
   return true;
+}
+
+// pooled rows per task: 6 (78 KB of LDS, two blocks per CU); HBK_P0_BAND=5|7 for tuning
+bool plan_p0(const std::vector<OpInfo>& ops, const std::vector<int>& st, const ChainArgs& a, Dims d, Dims od,
+             ChainPlan& cp) {
+  if (getenv("HBK_EMBED_NO_P0")) return false;
+  const char* bs = getenv("HBK_P0_BAND");
+  const int band = bs ? atoi(bs) : 6;
+  if (band == 5) return plan_p0_band<5>(ops, st, a, d, od, cp);
+  if (band == 7) return plan_p0_band<7>(ops, st, a, d, od, cp);
+  return plan_p0_band<6>(ops, st, a, d, od, cp);
 }
 
 // The p1 pattern: [1x3 (CI -> 32), 3x1, 1x3, 3x1 (32 -> 32)] + output pool 2x2,
