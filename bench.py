@@ -221,7 +221,8 @@ def setup_featurize(args, dev, rank, world, seed):
                              colored_noise_prob=0.25 if args.full_augment else 0.0,
                              tanh_distortion_prob=0.25 if args.full_augment else 0.0,
                              seven_band_prob=0.25 if args.full_augment else 0.0,
-                             band_stop_prob=0.25 if args.full_augment else 0.0)  # configs[2]: reverb + noise (+ gain)
+                             band_stop_prob=0.25 if args.full_augment else 0.0,
+                             pitch_shift_prob=0.25 if args.full_augment else 0.0)  # configs[2]: reverb + noise (+ gain)
         aug_out = torch.empty((n, AUG_T), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
     stages = (["augment"] if augment else []) + ["mel", "embed"]

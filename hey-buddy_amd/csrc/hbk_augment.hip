@@ -26,6 +26,7 @@
 // rotated kernel [ir[d:], 0..., ir[:d]] (hbk_reverb_spectrum).
 #include <algorithm>
 #include <cmath>
+#include <numeric>
 #include <vector>
 
 #include "hbk_common.h"
@@ -1374,6 +1375,308 @@ __global__ void __launch_bounds__(64) eq_kernel(EqArgs a) {
   }
 }
 
+// ----------------------------------------------------------------------------
+// PitchShift (torch_audiomentations PitchShift -> torch_pitch_shift.pitch_shift,
+// augmented.py:93-100): stft (n_fft 250, hop 7, rectangular window, center,
+// reflect) -> phase vocoder (torchaudio TimeStretch, rate = 1 / shift) ->
+// istft -> sinc resample (torchaudio Resample(sr, int(sr / shift))), cropped or
+// zero-padded to the clip length. One ratio per call (per_batch mode).
+//
+// Frame spectra are computed by a sliding DFT (hop 7: seven samples enter and
+// leave per frame, O(bins) per frame instead of an FFT), restarted by a direct
+// DFT every kPsRestart frames; an all-zero frame is exactly zero (angle 0) as in
+// the FFT. The istft needs no per-frame inverse transform either: with Z_t[k] =
+// Y_t[k] e^{-2 pi i k 7 t / 250}, sample p of the overlap-add is
+//   (1/250) sum_k c_k Re(e^{2 pi i k p / 250} W_p[k]),  W_p = sum of Z_t over the
+// <= 36 frames covering p, a sliding window sum per bin.
+//   ps_stft_kernel       (segment of 64 input frames, clip): angle, |X| per frame
+//   ps_phase_sum_kernel  (segment, clip): sum of the vocoder's phase increments of
+//                        the output frames whose source frame is in the segment
+//   ps_synth_kernel      (segment, clip): prefix phase (f64), vocoder frames, the
+//                        windowed sums, a bin reduction through LDS -> istft samples
+//   ps_resample_kernel   (frame group, clip): polyphase sinc, taps in registers
+constexpr int kPsFft = 250, kPsHop = 7, kPsBins = kPsFft / 2 + 1, kPsPad = kPsFft / 2;
+constexpr int kPsSeg = 64;                             // input frames per segment
+constexpr int kPsRestart = 16;                         // direct DFT every 16 frames
+constexpr int kPsWin = (kPsFft + kPsHop - 1) / kPsHop;  // 36 frames cover a sample
+constexpr int kPsChunk = 8;                            // output frames per bin reduction
+constexpr int kPsTapMax = HBK_PITCH_SHIFT_MAX_TAPS;    // 2 width + orig (142 / 139 at 16 kHz)
+constexpr int kPsPhaseMax = 128;                       // new (resampler phases)
+constexpr int kPsResFrames = 32;                       // resampler frames per workgroup
+constexpr int kPsLd = 128;                             // bins stored per frame (126 used)
+
+struct PitchArgs {
+  const float* x;
+  int64_t x_stride;
+  const int32_t* idx;
+  float* out;
+  int64_t out_stride;
+  int L, f_in, f_out, l1, nseg, orig, nw, width, target;
+  double rate;
+  float* ang;     // [n][f_in + 2][kPsLd]
+  float* mag;     // [n][f_in + 2][kPsLd]
+  double* segsum; // [n][nseg][kPsLd]
+  float* y;       // [n][l1]
+  float* taps;    // [nw][kPsTapMax]
+};
+
+__device__ __forceinline__ int ps_i0(const PitchArgs& a, int t, float& alpha) {
+  // torch.arange(0, f_in, rate, dtype=float32): start + step * i in double, cast
+  const float ts = static_cast<float>(static_cast<double>(t) * a.rate);
+  const float fl = floorf(ts);
+  alpha = ts - fl;
+  return static_cast<int>(fl);
+}
+
+// first output frame whose source frame i0 is >= f
+__device__ int ps_first_t(const PitchArgs& a, int f) {
+  if (f <= 0) return 0;
+  int t = max(0, static_cast<int>(static_cast<double>(f) / a.rate) - 2);
+  float al;
+  while (t < a.f_out && ps_i0(a, t, al) < f) ++t;
+  return t;
+}
+
+// the vocoder's phase increment of output frame t, bin k (torchaudio phase_vocoder)
+__device__ __forceinline__ double ps_phase(const float* ang, int i0, int k) {
+  const double adv = (M_PI * kPsHop) * k / (kPsBins - 1);
+  double ph = static_cast<double>(ang[(i0 + 1) * kPsLd]) - static_cast<double>(ang[i0 * kPsLd]) - adv;
+  ph -= (2.0 * M_PI) * rint(ph * (0.5 / M_PI));
+  return ph + adv;
+}
+
+__device__ __forceinline__ void ps_twiddles(float2* tw) {
+  for (int q = threadIdx.x; q < kPsFft; q += blockDim.x) {
+    double s, c;
+    sincospi(2.0 * q / kPsFft, &s, &c);
+    tw[q] = make_float2(static_cast<float>(c), static_cast<float>(s));
+  }
+}
+
+__global__ void __launch_bounds__(128) ps_stft_kernel(PitchArgs a) {
+  __shared__ float2 tw[kPsFft];
+  __shared__ float xs[kPsHop * (kPsSeg - 1) + kPsFft];
+  __shared__ int zf[kPsSeg];
+  const int k = threadIdx.x, s = blockIdx.x, e = blockIdx.y;
+  const float* x = a.x + static_cast<int64_t>(a.idx[e]) * a.x_stride;
+  ps_twiddles(tw);
+  const int f0 = s * kPsSeg, nf = min(kPsSeg, a.f_in - f0);
+  const int q0 = f0 * kPsHop, nq = kPsHop * (nf - 1) + kPsFft;
+  for (int q = k; q < nq; q += 128) {  // reflect padding by n_fft / 2
+    int i = q0 + q - kPsPad;
+    i = i < 0 ? -i : i;
+    i = i >= a.L ? 2 * (a.L - 1) - i : i;
+    xs[q] = x[i];
+  }
+  __syncthreads();
+  if (k < nf) {
+    bool any = false;
+    for (int j = 0; j < kPsFft; ++j) any |= xs[kPsHop * k + j] != 0.f;
+    zf[k] = any;
+  }
+  __syncthreads();
+  const int64_t frame0 = static_cast<int64_t>(e) * (a.f_in + 2);
+  float* ang = a.ang + (frame0 + f0) * kPsLd + k;
+  float* mag = a.mag + (frame0 + f0) * kPsLd + k;
+  if (k < kPsBins) {
+    const float2 rot = tw[(kPsHop * k) % kPsFft];
+    float xr = 0.f, xi = 0.f;
+    for (int f = 0; f < nf; ++f) {
+      const float* xf = xs + kPsHop * f;
+      if (f % kPsRestart == 0) {  // X = sum_n x[n] e^{-2 pi i k n / 250}
+        float re = 0.f, im = 0.f;
+        int q = 0;
+        for (int j = 0; j < kPsFft; ++j) {
+          const float v = xf[j];
+          const float2 w = tw[q];
+          re = fmaf(v, w.x, re);
+          im = fmaf(-v, w.y, im);
+          q += k;
+          q -= q >= kPsFft ? kPsFft : 0;
+        }
+        xr = re;
+        xi = im;
+      } else {  // X_f = e^{2 pi i k 7 / 250} (X_{f-1} + sum_j (x_in[j] - x_out[j]) e^{-2 pi i k j / 250})
+        float dr = 0.f, di = 0.f;
+        int q = 0;
+#pragma unroll
+        for (int j = 0; j < kPsHop; ++j) {
+          const float d = xf[kPsFft - kPsHop + j] - xf[j - kPsHop];
+          const float2 w = tw[q];
+          dr = fmaf(d, w.x, dr);
+          di = fmaf(-d, w.y, di);
+          q += k;
+          q -= q >= kPsFft ? kPsFft : 0;
+        }
+        const float ar = xr + dr, ai = xi + di;
+        xr = ar * rot.x - ai * rot.y;
+        xi = ar * rot.y + ai * rot.x;
+      }
+      if (!zf[f]) xr = xi = 0.f;
+      ang[f * kPsLd] = atan2f(xi, xr);
+      mag[f * kPsLd] = sqrtf(xr * xr + xi * xi);
+    }
+  }
+  if (s == a.nseg - 1) {  // the vocoder's two zero frames past the end
+    float* az = a.ang + (frame0 + a.f_in) * kPsLd + k;
+    float* mz = a.mag + (frame0 + a.f_in) * kPsLd + k;
+    az[0] = az[kPsLd] = 0.f;
+    mz[0] = mz[kPsLd] = 0.f;
+  }
+}
+
+__global__ void __launch_bounds__(128) ps_phase_sum_kernel(PitchArgs a) {
+  const int k = threadIdx.x, s = blockIdx.x, e = blockIdx.y;
+  const int t0 = ps_first_t(a, s * kPsSeg);
+  const int t1 = s + 1 < a.nseg ? ps_first_t(a, (s + 1) * kPsSeg) : a.f_out;
+  const float* ang = a.ang + static_cast<int64_t>(e) * (a.f_in + 2) * kPsLd + k;
+  double acc = 0.0;
+  if (k < kPsBins) {
+    for (int t = t0; t < t1; ++t) {
+      float al;
+      acc += ps_phase(ang, ps_i0(a, t, al), k);
+    }
+  }
+  a.segsum[(static_cast<int64_t>(e) * a.nseg + s) * kPsLd + k] = acc;
+}
+
+__global__ void __launch_bounds__(128) ps_synth_kernel(PitchArgs a) {
+  __shared__ float2 tw[kPsFft];
+  __shared__ float2 ring[kPsWin][kPsLd];
+  __shared__ float cb[kPsChunk * kPsHop][kPsLd + 1];
+  const int k = threadIdx.x, s = blockIdx.x, e = blockIdx.y;
+  ps_twiddles(tw);
+  for (int i = k; i < kPsWin * kPsLd; i += 128) ring[i / kPsLd][i % kPsLd] = make_float2(0.f, 0.f);
+  const int t_lo = ps_first_t(a, s * kPsSeg);
+  const bool last = s + 1 == a.nseg;
+  const int t_hi = last ? a.f_out : ps_first_t(a, (s + 1) * kPsSeg);
+  // samples p = 7 j + r of this segment: j in [t_lo, j_end); the last segment
+  // runs past the last frame to the last istft sample (p = n_fft/2 + l1 - 1)
+  const int j_end = last ? (a.l1 + kPsPad - 1) / kPsHop + 1 : t_hi;
+  const int t_a = max(0, t_lo - (kPsWin - 1));
+  const int64_t frame0 = static_cast<int64_t>(e) * (a.f_in + 2);
+  const float* ang = a.ang + frame0 * kPsLd + k;
+  const float* mag = a.mag + frame0 * kPsLd + k;
+  double acc = 0.0;  // accumulated phase of frame t (float64: |acc| reaches 7e4 rad)
+  if (k < kPsBins) {
+    acc = ang[0];
+    const double* ss = a.segsum + static_cast<int64_t>(e) * a.nseg * kPsLd + k;
+    for (int q = 0; q < s; ++q) acc += ss[q * kPsLd];
+    for (int t = t_a; t < t_lo; ++t) {
+      float al;
+      acc -= ps_phase(ang, ps_i0(a, t, al), k);
+    }
+  }
+  __syncthreads();
+  const float ck = (k == 0 || k == kPsBins - 1) ? 1.f : (k < kPsBins ? 2.f : 0.f);
+  const int kq = k < kPsBins ? k : 0;
+  float wr = 0.f, wi = 0.f;
+  int row = 0, jc = t_lo;
+  float* y = a.y + static_cast<int64_t>(e) * a.l1;
+  for (int t = t_a; t < j_end; ++t) {
+    float zr = 0.f, zi = 0.f;
+    if (k < kPsBins && t < a.f_out) {
+      float al;
+      const int i0 = ps_i0(a, t, al);
+      const float m = al * mag[(i0 + 1) * kPsLd] + (1.f - al) * mag[i0 * kPsLd];
+      double th = acc - (2.0 * M_PI / kPsFft) * ((kPsHop * static_cast<int64_t>(t) * k) % kPsFft);
+      th -= (2.0 * M_PI) * rint(th * (0.5 / M_PI));
+      float sn, cs;
+      sincosf(static_cast<float>(th), &sn, &cs);
+      zr = m * cs;
+      zi = m * sn;
+      acc += ps_phase(ang, i0, k);
+    }
+    const int slot = t % kPsWin;
+    const float2 old = ring[slot][k];
+    wr += zr - old.x;
+    wi += zi - old.y;
+    ring[slot][k] = make_float2(zr, zi);
+    if (t >= t_lo) {
+      const float2 z35 = ring[(t + 1) % kPsWin][k];  // Z_{t-35}
+      int q = (kq * ((kPsHop * t) % kPsFft)) % kPsFft;
+#pragma unroll
+      for (int r = 0; r < kPsHop; ++r) {
+        // frames t-35 .. t cover p = 7 t + r for r <= 4, t-34 .. t for r = 5, 6
+        const float vr = r <= 4 ? wr : wr - z35.x, vi = r <= 4 ? wi : wi - z35.y;
+        const float2 w = tw[q];
+        cb[row * kPsHop + r][k] = ck * (w.x * vr - w.y * vi);
+        q += kq;
+        q -= q >= kPsFft ? kPsFft : 0;
+      }
+      ++row;
+      if (row == kPsChunk || t == j_end - 1) {
+        __syncthreads();
+        if (k < row * kPsHop) {
+          const int p = kPsHop * jc + k;
+          const int m = p - kPsPad;
+          if (m >= 0 && m < a.l1) {
+            float acc2 = 0.f;
+            for (int b = 0; b < kPsBins; ++b) acc2 += cb[k][b];
+            const int j = p / kPsHop;
+            const int lo = max(0, j - (kPsWin - 1) + (p % kPsHop >= 5 ? 1 : 0));
+            const int hi = min(a.f_out - 1, j);
+            y[m] = acc2 / (static_cast<float>(kPsFft) * static_cast<float>(hi - lo + 1));
+          }
+        }
+        __syncthreads();
+        row = 0;
+        jc = t + 1;
+      }
+    }
+  }
+}
+
+__global__ void ps_taps_kernel(PitchArgs a) {
+  // torchaudio _get_sinc_resample_kernel: sinc_interp_hann, width 6, rolloff 0.99
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.nw * kPsTapMax) return;
+  const int ph = i / kPsTapMax, q = i % kPsTapMax;
+  float v = 0.f;
+  if (q < 2 * a.width + a.orig) {
+    const double lpw = 6.0, base = min(a.orig, a.nw) * 0.99;
+    double t = static_cast<double>(static_cast<float>(-ph) / static_cast<float>(a.nw)) +
+               static_cast<double>(q - a.width) / a.orig;
+    t = fmin(fmax(t * base, -lpw), lpw);
+    const double c = cos(t * M_PI / lpw / 2);
+    t *= M_PI;
+    v = static_cast<float>((t == 0.0 ? 1.0 : sin(t) / t) * c * c * (base / a.orig));
+  }
+  a.taps[i] = v;
+}
+
+__global__ void __launch_bounds__(128) ps_resample_kernel(PitchArgs a) {
+  __shared__ float ys[kPsResFrames * kPsPhaseMax + kPsTapMax];
+  const int ph = threadIdx.x, e = blockIdx.y;
+  const int f0 = blockIdx.x * kPsResFrames;
+  const float* y = a.y + static_cast<int64_t>(e) * a.l1;
+  // y padded by (width, width + orig) zeros; frame f reads ypad[f orig + q]
+  // (the window is read to kPsTapMax, past 2 width + orig, against zero taps)
+  const int j0 = f0 * a.orig - a.width, nj = (kPsResFrames - 1) * a.orig + kPsTapMax;
+  for (int j = ph; j < nj; j += 128) {
+    const int src = j0 + j;
+    ys[j] = (src >= 0 && src < a.l1) ? y[src] : 0.f;
+  }
+  float tp[kPsTapMax];
+  const float* tr = a.taps + min(ph, a.nw - 1) * kPsTapMax;
+#pragma unroll
+  for (int q = 0; q < kPsTapMax; ++q) tp[q] = tr[q];
+  __syncthreads();
+  if (ph >= a.nw) return;
+  float* out = a.out + static_cast<int64_t>(a.idx[e]) * a.out_stride;
+  for (int f = 0; f < kPsResFrames; ++f) {
+    const int i = (f0 + f) * a.nw + ph;
+    if (i >= a.L) break;
+    float v = 0.f;
+    if (i < a.target) {
+      const float* w = ys + f * a.orig;
+#pragma unroll
+      for (int q = 0; q < kPsTapMax; ++q) v = fmaf(tp[q], w[q], v);
+    }
+    out[i] = v;
+  }
+}
+
 }  // namespace
 }  // namespace hbk
 
@@ -1687,6 +1990,97 @@ int hbk_seven_band_eq(const float* x, int64_t n_clips, int64_t x_stride, const d
   hipLaunchKernelGGL(eq_kernel, dim3(unsigned((n_entries + kEqClips - 1) / kEqClips)), dim3(64), 0,
                      as_stream(stream), a);
   HBK_LAUNCH_CHECK("eq_kernel");
+  return HBK_OK;
+}
+
+static int ps_geometry(int64_t L, int32_t sample_rate, int32_t num, int32_t den, hbk::PitchArgs& a) {
+  using namespace hbk;
+  if (sample_rate != 16000) {
+    set_error("hbk: pitch shift supports 16 kHz (n_fft 250, hop 7), got %d", sample_rate);
+    return HBK_ERR_UNSUPPORTED;
+  }
+  if (num <= 0 || den <= 0) return arg_error("shift num / den must be positive");
+  if (L <= kPsPad || L > (int64_t(1) << 24)) return arg_error("clip length must be in (125, 2^24]");
+  a.L = static_cast<int>(L);
+  a.rate = double(den) / double(num);
+  a.f_in = 1 + a.L / kPsHop;
+  a.f_out = static_cast<int>(std::ceil(double(a.f_in) / a.rate));
+  a.l1 = kPsHop * (a.f_out - 1);
+  a.nseg = (a.f_in + kPsSeg - 1) / kPsSeg;
+  const int64_t new_sr = int64_t(sample_rate) * den / num;
+  const int64_t g = std::gcd(int64_t(sample_rate), new_sr);
+  if (new_sr <= 0 || g <= 0) return arg_error("shift out of range");
+  a.orig = static_cast<int>(sample_rate / g);
+  a.nw = static_cast<int>(new_sr / g);
+  a.width = static_cast<int>(std::ceil(6.0 * a.orig / (std::min(a.orig, a.nw) * 0.99)));
+  a.target = static_cast<int>(std::ceil(double(a.nw) * a.l1 / a.orig));
+  if (a.nw > kPsPhaseMax || 2 * a.width + a.orig > kPsTapMax || a.l1 <= 0) {
+    set_error("hbk: pitch shift %d/%d resamples %d -> %d (%d taps): the kernel holds <= %d phases of <= %d taps "
+              "(torch_pitch_shift's fast shifts at 16 kHz)", num, den, a.orig, a.nw, 2 * a.width + a.orig,
+              kPsPhaseMax, kPsTapMax);
+    return HBK_ERR_UNSUPPORTED;
+  }
+  return HBK_OK;
+}
+
+static int64_t ps_bytes(const hbk::PitchArgs& a, int64_t n, int64_t* off) {
+  using namespace hbk;
+  auto up = [](int64_t b) { return (b + 255) & ~int64_t(255); };
+  const int64_t spec = up(n * (a.f_in + 2) * kPsLd * 4);
+  off[0] = 0;                                      // ang
+  off[1] = spec;                                   // mag
+  off[2] = 2 * spec;                               // segsum
+  off[3] = off[2] + up(n * a.nseg * kPsLd * 8);    // y
+  off[4] = off[3] + up(n * a.l1 * 4);              // taps
+  return off[4] + up(int64_t(kPsPhaseMax) * kPsTapMax * 4);
+}
+
+int64_t hbk_pitch_shift_workspace_size(int64_t n, int64_t T, int32_t sample_rate, int32_t num, int32_t den) {
+  hbk::PitchArgs a{};
+  if (n <= 0 || ps_geometry(T, sample_rate, num, den, a) != HBK_OK) return 0;
+  int64_t off[5];
+  return ps_bytes(a, n, off);
+}
+
+int hbk_pitch_shift(const float* x, int64_t x_stride, int64_t n, const int32_t* idx, int64_t T, int32_t sample_rate,
+                    int32_t num, int32_t den, float* out, int64_t out_stride, void* workspace,
+                    int64_t workspace_bytes, void* stream) {
+  using namespace hbk;
+  if (n < 0) return arg_error("negative n");
+  if (n == 0) return HBK_OK;
+  if (n > 65535) return arg_error("n > 65535 per call");
+  if (!x || !idx || !out || !workspace) return arg_error("NULL pointer");
+  PitchArgs a{};
+  const int rc = ps_geometry(T, sample_rate, num, den, a);
+  if (rc != HBK_OK) return rc;
+  if (x_stride < T || out_stride < T) return arg_error("stride < T");
+  int64_t off[5];
+  if (workspace_bytes < ps_bytes(a, n, off)) return arg_error("workspace too small (hbk_pitch_shift_workspace_size)");
+  unsigned char* w = static_cast<unsigned char*>(workspace);
+  a.x = x;
+  a.x_stride = x_stride;
+  a.idx = idx;
+  a.out = out;
+  a.out_stride = out_stride;
+  a.ang = reinterpret_cast<float*>(w + off[0]);
+  a.mag = reinterpret_cast<float*>(w + off[1]);
+  a.segsum = reinterpret_cast<double*>(w + off[2]);
+  a.y = reinterpret_cast<float*>(w + off[3]);
+  a.taps = reinterpret_cast<float*>(w + off[4]);
+  hipStream_t st = as_stream(stream);
+  const dim3 seg(unsigned(a.nseg), unsigned(n));
+  hipLaunchKernelGGL(ps_taps_kernel, dim3(unsigned((a.nw * kPsTapMax + 255) / 256)), dim3(256), 0, st, a);
+  HBK_LAUNCH_CHECK("ps_taps_kernel");
+  hipLaunchKernelGGL(ps_stft_kernel, seg, dim3(128), 0, st, a);
+  HBK_LAUNCH_CHECK("ps_stft_kernel");
+  hipLaunchKernelGGL(ps_phase_sum_kernel, seg, dim3(128), 0, st, a);
+  HBK_LAUNCH_CHECK("ps_phase_sum_kernel");
+  hipLaunchKernelGGL(ps_synth_kernel, seg, dim3(128), 0, st, a);
+  HBK_LAUNCH_CHECK("ps_synth_kernel");
+  const int res_frames = (a.L + a.nw - 1) / a.nw;
+  hipLaunchKernelGGL(ps_resample_kernel, dim3(unsigned((res_frames + kPsResFrames - 1) / kPsResFrames), unsigned(n)),
+                     dim3(128), 0, st, a);
+  HBK_LAUNCH_CHECK("ps_resample_kernel");
   return HBK_OK;
 }
 

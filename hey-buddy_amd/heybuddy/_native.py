@@ -78,6 +78,10 @@ _PROTOS = {
     "hbk_band_stop_workspace_size": (_c_int64, [_c_int64, ctypes.c_int32, ctypes.c_int32, _vp]),
     "hbk_band_stop": (_c_int, [_vp, _vp, _c_int64, _c_int64, _vp, _vp, ctypes.c_int32, _vp, _vp, _vp, _vp,
                                ctypes.c_int32, _vp, _vp, _vp, _c_int64, _vp, _c_int64, _vp]),
+    "hbk_pitch_shift_workspace_size": (_c_int64, [_c_int64, _c_int64, ctypes.c_int32, ctypes.c_int32,
+                                                  ctypes.c_int32]),
+    "hbk_pitch_shift": (_c_int, [_vp, _c_int64, _c_int64, _vp, _c_int64, ctypes.c_int32, ctypes.c_int32,
+                                 ctypes.c_int32, _vp, _c_int64, _vp, _c_int64, _vp]),
     "hbk_seven_band_eq": (_c_int, [_vp, _c_int64, _c_int64, _vp, _vp, _c_int64, _vp, _c_int64, _vp]),
     "hbk_place_clips": (_c_int, [_vp, _c_int64, _c_int64, _vp, _vp, _vp, _c_int64, _c_int64, _vp]),
     "hbk_mlp_set_step_scalars": (_c_int, [_vp, _vp]),

@@ -35,8 +35,12 @@ Semantics kept from the reference:
 Differences (by design): the IR spectra are computed once for the whole bank
 instead of once per batch, every batch of a call is one kernel launch, and
 clips never leave the device (the reference copies each clip back to host,
-:419). Pitch shift (the first transform of the batch chain) is not on this path
-yet.
+:419).
+* pitch shift: torch_audiomentations PitchShift in per_batch mode (:93-100),
+  first in the batch chain: per batch with probability pitch_shift_prob (0.25)
+  one of torch_pitch_shift's fast shifts within +-pitch_shift_semitones (at
+  16 kHz and 3 semitones: 125/128 and 128/125), drawn uniformly; stft, phase
+  vocoder, istft and the sinc resampler on the device (hbk_pitch_shift).
 """
 from __future__ import annotations
 
@@ -51,13 +55,14 @@ from heybuddy.constants import (DEFAULT_AUGMENT_BACKGROUND_NOISE_MAX_SNR_DB,
                                 DEFAULT_AUGMENT_COLORED_NOISE_MAX_SNR_DB,
                                 DEFAULT_AUGMENT_COLORED_NOISE_MIN_F_DECAY,
                                 DEFAULT_AUGMENT_COLORED_NOISE_MIN_SNR_DB, DEFAULT_AUGMENT_COLORED_NOISE_PROB,
+                                DEFAULT_AUGMENT_PITCH_SHIFT_PROB, DEFAULT_AUGMENT_PITCH_SHIFT_SEMITONES,
                                 DEFAULT_AUGMENT_TANH_DISTORTION_PROB, DEFAULT_AUGMENT_TANH_MAX_DISTORTION,
                                 DEFAULT_AUGMENT_TANH_MIN_DISTORTION,
                                 DEFAULT_AUGMENT_BACKGROUND_NOISE_PROB, DEFAULT_AUGMENT_GAIN_MAX_DB,
                                 DEFAULT_AUGMENT_GAIN_MIN_DB, DEFAULT_AUGMENT_GAIN_PROB,
                                 DEFAULT_AUGMENT_REVERB_PROB, DEFAULT_AUGMENT_SEVEN_BAND_GAIN_DB,
                                 DEFAULT_AUGMENT_SEVEN_BAND_PROB)
-from heybuddy.kernels import ReverbPlan, place_clips, seven_band_eq, tanh_distortion
+from heybuddy.kernels import ReverbPlan, pitch_shift, place_clips, seven_band_eq, tanh_distortion
 
 __all__ = ["AugmentedAudioGenerator", "BatchAugmenter", "bandstop_cutoffs", "eq_coefficients", "eq_parameters",
            "target_length_offset", "target_length_offsets", "to_target_length"]
@@ -126,6 +131,24 @@ def _pinned(t: torch.Tensor) -> torch.Tensor:
     return t.pin_memory() if torch.cuda.is_available() else t
 
 
+def fast_shifts(sample_rate: int = 16000, semitones: float = DEFAULT_AUGMENT_PITCH_SHIFT_SEMITONES) -> list:
+    """torch_pitch_shift.get_fast_shifts as torch_audiomentations PitchShift
+    calls it: every ratio i / j (i, j products of sample_rate's prime factors)
+    in [2^(-semitones/12), 2^(semitones/12)] except 1, ascending."""
+    from fractions import Fraction
+    from itertools import combinations
+    from math import prod
+    fac, n, d = [], int(sample_rate), 2
+    while n > 1:
+        while n % d == 0:
+            fac.append(d)
+            n //= d
+        d += 1
+    products = {prod(c) for r in range(1, len(fac) + 1) for c in combinations(fac, r)}
+    lo, hi = Fraction(2.0 ** (-semitones / 12.0)), Fraction(2.0 ** (semitones / 12.0))
+    return sorted({Fraction(i, j) for i in products for j in products if lo <= Fraction(i, j) <= hi} - {1})
+
+
 class BatchAugmenter:
     def __init__(self, noise: Optional[Sequence[torch.Tensor]] = None,
                  impulse_responses: Optional[Sequence[torch.Tensor]] = None,
@@ -148,7 +171,9 @@ class BatchAugmenter:
                  seven_band_prob: float = DEFAULT_AUGMENT_SEVEN_BAND_PROB,
                  seven_band_gain_db: float = DEFAULT_AUGMENT_SEVEN_BAND_GAIN_DB,
                  band_stop_prob: float = DEFAULT_AUGMENT_BAND_STOP_PROB,
-                 sample_rate: int = 16000) -> None:
+                 sample_rate: int = 16000,
+                 pitch_shift_prob: float = DEFAULT_AUGMENT_PITCH_SHIFT_PROB,
+                 pitch_shift_semitones: float = DEFAULT_AUGMENT_PITCH_SHIFT_SEMITONES) -> None:
         self.plan = ReverbPlan(device)
         self.device = self.plan.device
         if background_noise_prob > 0 and not noise:
@@ -172,6 +197,10 @@ class BatchAugmenter:
         self.p_eq = float(seven_band_prob)
         self.eq_gain_db = float(seven_band_gain_db)
         self.p_bandstop = float(band_stop_prob)
+        self.p_pitch = float(pitch_shift_prob)
+        self.pitch_shifts = fast_shifts(self.sample_rate, pitch_shift_semitones) if self.p_pitch > 0 else []
+        if self.p_pitch > 0 and not self.pitch_shifts:
+            raise ValueError(f"no fast pitch shift within +-{pitch_shift_semitones} semitones at {sample_rate} Hz")
         self.ring = None
         self.lengths: List[int] = []
         self.starts: List[int] = []
@@ -250,6 +279,16 @@ class BatchAugmenter:
         per = np.full(nbat, -1, dtype=np.int64)
         per[b_on] = np.arange(int(b_on.sum()))
         self._bandstop = (np.flatnonzero(sel).astype(np.int32), lo[per[batch][sel]], hi[per[batch][sel]])
+        # pitch shift (PitchShift, per_batch): one fast shift per batch whose coin
+        # came up (random.choices over the shifts); the clips of each shift
+        self._pitch = []
+        if getattr(self, "p_pitch", 0.0) > 0:
+            p_on = np.random.rand(nbat) < self.p_pitch
+            p_pick = np.random.randint(0, len(self.pitch_shifts), nbat)
+            for j, f in enumerate(self.pitch_shifts):
+                clips = np.flatnonzero((p_on & (p_pick == j))[batch]).astype(np.int32)
+                if clips.size:
+                    self._pitch.append((f.numerator, f.denominator, clips))
         # seven-band EQ (audiomentations, per clip): the clips whose coin came up
         # and their filters (parameters drawn for those clips only)
         e_on = np.random.rand(n) < getattr(self, "p_eq", 0.0)
@@ -289,7 +328,8 @@ class BatchAugmenter:
         if not np.isnan(colored_snr).all():
             colored = (torch.from_numpy(colored_fd), torch.from_numpy(colored_snr), int(np.random.randint(0, 2 ** 62)))
         return {"n": n, "noise_off": torch.from_numpy(noise_off), "spec_idx": torch.from_numpy(spec_idx),
-                "snr": snr, "gain": gain, "eq": eq, "tanh": tanh, "bandstop": bandstop, "colored": colored}
+                "snr": snr, "gain": gain, "eq": eq, "tanh": tanh, "bandstop": bandstop, "colored": colored,
+                "pitch": [(a, b, _pinned(torch.from_numpy(c))) for a, b, c in getattr(self, "_pitch", [])]}
 
     def __call__(self, x: torch.Tensor, out: Optional[torch.Tensor] = None,
                  prepared: Optional[Dict[str, Any]] = None) -> torch.Tensor:
@@ -307,7 +347,11 @@ class BatchAugmenter:
         if pr["tanh"] is not None:  # per-clip Compose, before the batch chain (augmented.py:325-328)
             x = tanh_distortion(x, pr["tanh"], out=out)
             out = x
-        if pr.get("bandstop") is not None:  # batch chain: band-stop, then colored noise (augmented.py:101-113)
+        for num, den, clips in pr.get("pitch") or []:  # batch chain: pitch shift first (augmented.py:93-100)
+            if out is None:
+                out = torch.empty((n, T), dtype=torch.float32, device=x.device)
+            x = pitch_shift(x, clips, num, den, out=out, sample_rate=self.sample_rate)
+        if pr.get("bandstop") is not None:  # then band-stop, then colored noise (augmented.py:101-113)
             if out is None:
                 out = x[:, :T].clone()
             elif out.data_ptr() != x.data_ptr():
@@ -397,8 +441,7 @@ class AugmentedAudioGenerator:
     the reference's order (:297-394). The datasets are any iterable of audio
     rows (see _audio_arrays); clips at another rate are resampled (torchaudio's
     band-limited resampler, restated). The noise and IR sets are loaded into
-    HBM once. Not on this path yet: pitch shift and band-stop
-    (their probabilities are accepted; a warning is logged when > 0)."""
+    HBM once. Every augmentation of the reference's chain runs on the device."""
 
     def __init__(self, source_dataset: Any, device_id: Optional[int] = None,
                  augmentation_dataset: Any = None, impulse_response_dataset: Any = None,
@@ -420,13 +463,10 @@ class AugmentedAudioGenerator:
                  background_noise_max_snr_db: float = DEFAULT_AUGMENT_BACKGROUND_NOISE_MAX_SNR_DB,
                  gain_prob: float = DEFAULT_AUGMENT_GAIN_PROB,
                  reverb_prob: float = DEFAULT_AUGMENT_REVERB_PROB) -> None:
-        from heybuddy.util import logger
         if background_noise_prob > 0 and not augmentation_dataset:
             raise ValueError("Background noise is enabled but no augmentation dataset is provided")
         if reverb_prob > 0 and not impulse_response_dataset:
             raise ValueError("Reverb is enabled but no impulse response dataset is provided")
-        if pitch_shift_prob > 0:
-            logger.warning(f"pitch_shift_prob={pitch_shift_prob}: pitch shift is not on the MI355X path yet; skipped")
         self.device_id = device_id
         self.source_dataset = source_dataset
         self.augmentation_dataset = augmentation_dataset
@@ -458,7 +498,8 @@ class AugmentedAudioGenerator:
             colored_noise_min_f_decay=colored_noise_min_f_decay, colored_noise_max_f_decay=colored_noise_max_f_decay,
             tanh_distortion_prob=tanh_distortion_prob, tanh_min_distortion=tanh_min_distortion,
             tanh_max_distortion=tanh_max_distortion, seven_band_prob=seven_band_aug_prob,
-            seven_band_gain_db=seven_band_aug_gain_db, band_stop_prob=band_stop_prob, sample_rate=self.sample_rate)
+            seven_band_gain_db=seven_band_aug_gain_db, band_stop_prob=band_stop_prob, sample_rate=self.sample_rate,
+            pitch_shift_prob=pitch_shift_prob, pitch_shift_semitones=pitch_shift_semitones)
         self.device = self.augmenter.device
         self._source: Optional[List[Dict[str, Any]]] = None
         self._source_pos = 0

@@ -236,7 +236,8 @@ class TrainingFeaturesGenerator:
                 tanh_distortion_prob=self.augment_tanh_distortion_prob,
                 tanh_min_distortion=self.augment_tanh_min_distortion,
                 tanh_max_distortion=self.augment_tanh_max_distortion,
-                pitch_shift_prob=0.0, pitch_shift_semitones=self.augment_pitch_shift_semitones,
+                pitch_shift_prob=self.augment_pitch_shift_prob,
+                pitch_shift_semitones=self.augment_pitch_shift_semitones,
                 band_stop_prob=self.augment_band_stop_prob,
                 colored_noise_prob=self.augment_colored_noise_prob,
                 colored_noise_min_snr_db=self.augment_colored_noise_min_snr_db,
@@ -247,9 +248,6 @@ class TrainingFeaturesGenerator:
                 background_noise_min_snr_db=self.augment_background_noise_min_snr_db,
                 background_noise_max_snr_db=self.augment_background_noise_max_snr_db,
                 gain_prob=self.augment_gain_prob, reverb_prob=self.augment_reverb_prob)
-            if self.augment_pitch_shift_prob > 0:
-                logger.warning(f"augment_pitch_shift_prob={self.augment_pitch_shift_prob}: "
-                               "not on the MI355X path yet; skipped")
         return self._augmenters[key]
 
     def augment_device(self, clips: torch.Tensor, lengths: np.ndarray, num_samples: int,

@@ -624,6 +624,54 @@ def tanh_distortion(x: torch.Tensor, amount: torch.Tensor, out: torch.Tensor | N
     return out
 
 
+PITCH_SHIFT_CHUNK = 256  # clips per hbk_pitch_shift call (~3.4 MB of workspace each)
+_PS_WS: dict = {}
+
+
+def pitch_shift(x: torch.Tensor, idx: torch.Tensor, num: int, den: int, out: torch.Tensor | None = None,
+                sample_rate: int = 16000) -> torch.Tensor:
+    """torch_pitch_shift.pitch_shift(x[idx], Fraction(num, den), sample_rate)
+    (hbk_pitch_shift; torch_audiomentations PitchShift per batch,
+    dataset/augmented.py:93-100) on rows idx of x [n, >= 23040] -> out [n, 23040].
+    Rows not listed are copied from x when out is a different buffer."""
+    T = ReverbPlan.T
+    dev = _native.require_device(x.device)
+    if x.dim() != 2 or x.shape[1] < T or x.stride(1) != 1 or x.dtype != torch.float32:
+        raise ValueError(f"x must be [n, >= {T}] f32 rows on the device")
+    n = x.shape[0]
+    if out is None:
+        out = torch.empty((n, T), dtype=torch.float32, device=dev)
+    if out.data_ptr() != x.data_ptr():
+        out.copy_(x[:, :T])
+        x = out
+    idx = idx.to(dtype=torch.int32).reshape(-1)
+    if idx.numel() == 0:
+        return out
+    if idx.device.type == "cpu":
+        if int(idx.min()) < 0 or int(idx.max()) >= n:
+            raise ValueError("idx out of range")
+        idx = idx.pin_memory().to(dev, non_blocking=True)
+    chunk = min(PITCH_SHIFT_CHUNK, idx.numel())
+    need = int(lib().hbk_pitch_shift_workspace_size(chunk, T, sample_rate, num, den))
+    if need <= 0:
+        raise ValueError(f"unsupported pitch shift {num}/{den} at {sample_rate} Hz")
+    ws = _PS_WS.get(dev)
+    if ws is None or ws.numel() < need:
+        ws = torch.empty(need, dtype=torch.uint8, device=dev)
+        _PS_WS[dev] = ws
+    for c0 in range(0, idx.numel(), chunk):
+        torch.ops.hbk.pitch_shift_(x, idx[c0:c0 + chunk], num, den, sample_rate, out, ws)
+    return out
+
+
+@torch.library.custom_op("hbk::pitch_shift_", mutates_args=("out", "workspace"))
+def _pitch_shift_op(x: torch.Tensor, idx: torch.Tensor, num: int, den: int, sample_rate: int, out: torch.Tensor,
+                    workspace: torch.Tensor) -> None:
+    check(lib().hbk_pitch_shift(ptr(x), x.stride(0), idx.numel(), ptr(idx), ReverbPlan.T, sample_rate, num, den,
+                                ptr(out), out.stride(0), ptr(workspace), workspace.numel(), stream_ptr(x.device)),
+          "hbk_pitch_shift")
+
+
 def seven_band_eq(x: torch.Tensor, coef: torch.Tensor, out: torch.Tensor | None = None,
                   idx: torch.Tensor | None = None) -> torch.Tensor:
     """audiomentations SevenBandParametricEQ per clip (hbk_seven_band_eq).

@@ -348,6 +348,25 @@ int hbk_band_stop(const hbk_reverb_plan* plan, const float* x, int64_t x_stride,
                   const int32_t* s_part, float* out, int64_t out_stride, void* workspace, int64_t workspace_bytes,
                   void* stream);
 
+/* Pitch shift: torch_audiomentations PitchShift (+-3 semitones, mode per_batch,
+ * p 0.25; dataset/augmented.py:93-100, constants.py:125-126), which calls
+ * torch_pitch_shift.pitch_shift(x, Fraction(num, den), sample_rate): at 16 kHz
+ * its "fast shifts" within +-3 semitones are 125/128 and 128/125. For entry
+ * e < n, clip row r = idx[e] of x [*, x_stride] (first T samples):
+ *   X = stft(x[r], n_fft 250, hop 7, rectangular window, center, reflect)
+ *   Y = phase_vocoder(X, rate = den / num, adv = linspace(0, 7 pi, 126))
+ *   out[r] = Resample(16000, 16000 den / num)(istft(Y)), cropped / zero-padded to T
+ * Rows not listed are not touched; out may equal x (all reads of x precede
+ * the writes). HBK_ERR_UNSUPPORTED for sample_rate != 16000 or a ratio whose
+ * resampler needs more than 128 phases or HBK_PITCH_SHIFT_MAX_TAPS taps.
+ * workspace: hbk_pitch_shift_workspace_size bytes (~3.4 MB per entry at
+ * T = 23040; 0 for an unsupported geometry). Device pointers. */
+#define HBK_PITCH_SHIFT_MAX_TAPS 144
+int64_t hbk_pitch_shift_workspace_size(int64_t n, int64_t T, int32_t sample_rate, int32_t num, int32_t den);
+int hbk_pitch_shift(const float* x, int64_t x_stride, int64_t n, const int32_t* idx, int64_t T, int32_t sample_rate,
+                    int32_t num, int32_t den, float* out, int64_t out_stride, void* workspace,
+                    int64_t workspace_bytes, void* stream);
+
 /* Tanh distortion: audiomentations TanhDistortion, which the reference applies
  * per clip with p 0.25 and distortion ~ U[1e-4, 0.1] before the batch chain
  * (dataset/augmented.py:79-90, :325-328; constants.py:122-124). Per clip i of

@@ -297,3 +297,122 @@ def band_stop(x, cut_lo, cut_hi) -> np.ndarray:
         bp = fftconvolve(xp, g[::-1], mode="valid")  # conv1d is a correlation; g is symmetric anyway
         out[i] = (x[i] - bp).astype(np.float32)
     return out
+
+
+# PitchShift (torch_audiomentations PitchShift, mode per_batch, p 0.25, +-3
+# semitones; augmented.py:93-100, constants.py:125-126) -> torch_pitch_shift
+# (>= 1.2, unpinned: not in environment.yml's explicit list) -> torch.stft /
+# torchaudio TimeStretch (phase_vocoder) / torch.istft / torchaudio Resample.
+# PARITY UNPINNED: none of these packages is installed; the restatement below
+# follows their published algorithms and computes in float64 throughout (the
+# reference runs them in float32, whose phase cumsum alone carries ~1e-2 rad of
+# rounding at the top bins).
+
+def _prime_factors(n: int) -> list:
+    out, d = [], 2
+    while n > 1:
+        while n % d == 0:
+            out.append(d)
+            n //= d
+        d += 1
+    return out
+
+
+def pitch_fast_shifts(sample_rate: int = 16000, semitones: float = 3.0) -> list:
+    """torch_pitch_shift.get_fast_shifts(sample_rate, lo <= f <= hi and f != 1)
+    with lo / hi = Fraction(2 ** (-+semitones / 12)) (semitones_to_ratio): the
+    ratios i / j of products of sample_rate's prime factors. At 16 kHz and +-3
+    semitones that is {125/128, 128/125} (+-0.41 semitones)."""
+    from fractions import Fraction
+    from itertools import combinations
+    from math import prod
+    fac = _prime_factors(sample_rate)
+    products = {prod(c) for r in range(1, len(fac) + 1) for c in combinations(fac, r)}
+    lo, hi = Fraction(2.0 ** (-semitones / 12.0)), Fraction(2.0 ** (semitones / 12.0))
+    return sorted({Fraction(i, j) for i in products for j in products if lo <= Fraction(i, j) <= hi} - {1})
+
+
+def pitch_shift_geometry(length: int, num: int, den: int, sample_rate: int = 16000) -> dict:
+    """Frame counts and resampler shape of pitch_shift(x, Fraction(num, den))."""
+    from math import ceil, gcd
+    n_fft = sample_rate // 64
+    hop = n_fft // 32
+    f_in = 1 + length // hop                       # torch.stft, center=True
+    rate = float(den) / float(num)                 # TimeStretch(fixed_rate = float(1 / shift))
+    f_out = int(ceil(f_in / rate))                 # torch.arange(0, f_in, rate).numel()
+    l1 = hop * (f_out - 1)                         # torch.istft, center=True, length=None
+    new_sr = (sample_rate * den) // num            # int(sample_rate / shift)
+    g = gcd(sample_rate, new_sr)
+    orig, new = sample_rate // g, new_sr // g
+    width = int(ceil(6 * orig / (min(orig, new) * 0.99)))
+    target = int(ceil(new * l1 / orig))
+    return dict(n_fft=n_fft, hop=hop, f_in=f_in, rate=rate, f_out=f_out, l1=l1, orig=orig, new=new,
+                width=width, target=target)
+
+
+def resample_taps(orig: int, new: int) -> tuple:
+    """torchaudio _get_sinc_resample_kernel (sinc_interp_hann, lowpass_filter_width
+    6, rolloff 0.99, dtype None: float64 math, float32 taps) -> ([new, 2w + orig], w)."""
+    from math import ceil
+    lpw = 6.0
+    base = min(orig, new) * 0.99
+    width = int(ceil(lpw * orig / base))
+    idx = np.arange(-width, width + orig, dtype=np.float64)[None] / orig
+    t = (np.arange(0, -new, -1) / new).astype(np.float32).astype(np.float64)[:, None] + idx
+    t = np.clip(t * base, -lpw, lpw)
+    window = np.cos(t * np.pi / lpw / 2) ** 2
+    t = t * np.pi
+    with np.errstate(invalid="ignore", divide="ignore"):
+        k = np.where(t == 0, 1.0, np.sin(t) / t)
+    return (k * window * (base / orig)).astype(np.float32), width
+
+
+def pitch_shift(x, num: int, den: int, sample_rate: int = 16000) -> np.ndarray:
+    """torch_pitch_shift.pitch_shift(x, Fraction(num, den), sample_rate) per clip
+    (rows of x), float64:
+      X = stft(x, n_fft = sr // 64, hop = n_fft // 32)   rectangular window,
+          center, reflect padding, onesided
+      phase_vocoder(X, rate = den / num, adv_k = linspace(0, pi hop, n_fft/2 + 1)):
+          ts = arange(0, F, rate) (float32), i0 = int(ts), a = ts % 1
+          X padded with 2 zero frames; ph = angle(X[i0+1]) - angle(X[i0]) - adv
+          ph -= 2 pi round(ph / 2 pi); ph += adv
+          acc = cumsum([angle(X[0]), ph[:-1]]);  Y = (a |X[i0+1]| + (1-a) |X[i0]|) e^(i acc)
+      y = istft(Y)  (overlap-add / frame count, trimmed by n_fft // 2)
+      y = Resample(sr, int(sr / shift))(y), cropped or zero-padded to len(x)."""
+    x = np.atleast_2d(np.asarray(x, dtype=np.float64))
+    n, L = x.shape
+    g = pitch_shift_geometry(L, num, den, sample_rate)
+    n_fft, hop, f_in, f_out = g["n_fft"], g["hop"], g["f_in"], g["f_out"]
+    pad = n_fft // 2
+    nb = n_fft // 2 + 1
+    xp = np.pad(x, ((0, 0), (pad, pad)), mode="reflect")
+    fidx = hop * np.arange(f_in)[:, None] + np.arange(n_fft)[None]
+    X = np.fft.rfft(xp[:, fidx], axis=-1)                                # [n, f_in, nb]
+    ts = (np.arange(f_out, dtype=np.float64) * g["rate"]).astype(np.float32)
+    i0 = ts.astype(np.int64)
+    alpha = (ts - np.floor(ts)).astype(np.float64)[None, :, None]
+    Xp = np.concatenate([X, np.zeros((n, 2, nb), X.dtype)], axis=1)
+    X0, X1 = Xp[:, i0], Xp[:, i0 + 1]
+    adv = np.linspace(0.0, np.pi * hop, nb)
+    ph = np.angle(X1) - np.angle(X0) - adv
+    ph = ph - 2 * np.pi * np.round(ph / (2 * np.pi)) + adv
+    ph = np.concatenate([np.angle(X[:, :1]), ph[:, :-1]], axis=1)
+    acc = np.cumsum(ph, axis=1)
+    Y = (alpha * np.abs(X1) + (1.0 - alpha) * np.abs(X0)) * np.exp(1j * acc)
+    frames = np.fft.irfft(Y, n=n_fft, axis=-1)                           # [n, f_out, n_fft]
+    full = np.zeros((n, n_fft + hop * (f_out - 1)))
+    env = np.zeros(full.shape[1])
+    for t in range(f_out):
+        full[:, hop * t:hop * t + n_fft] += frames[:, t]
+        env[hop * t:hop * t + n_fft] += 1.0
+    y = full[:, pad:pad + g["l1"]] / env[pad:pad + g["l1"]]
+    taps, w = resample_taps(g["orig"], g["new"])
+    orig, new = g["orig"], g["new"]
+    ypad = np.pad(y, ((0, 0), (w, w + orig)))
+    nfr = g["l1"] // orig + 1
+    win = orig * np.arange(nfr)[:, None] + np.arange(2 * w + orig)[None]
+    res = np.einsum("nfq,pq->nfp", ypad[:, win], taps.astype(np.float64)).reshape(n, -1)[:, :g["target"]]
+    out = np.zeros((n, L))
+    m = min(L, res.shape[1])
+    out[:, :m] = res[:, :m]
+    return out

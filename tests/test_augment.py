@@ -209,7 +209,7 @@ def test_batch_augmenter_gain_is_per_batch():
     np.random.seed(5)
     aug = BatchAugmenter(device=0, batch_size=128, background_noise_prob=0.0, reverb_prob=0.0,
                          colored_noise_prob=0.0, tanh_distortion_prob=0.0, seven_band_prob=0.0,
-                         band_stop_prob=0.0)
+                         band_stop_prob=0.0, pitch_shift_prob=0.0)
     out = aug(x)
     ratio = (out / x).cpu().numpy()
     xs = x.cpu().numpy()
@@ -220,7 +220,7 @@ def test_batch_augmenter_gain_is_per_batch():
         assert 10 ** (-18 / 20) * (1 - 1e-6) <= g <= 10 ** (6 / 20) * (1 + 1e-6)
     off = BatchAugmenter(device=0, background_noise_prob=0.0, reverb_prob=0.0, gain_prob=0.0,
                          colored_noise_prob=0.0, tanh_distortion_prob=0.0, seven_band_prob=0.0,
-                         band_stop_prob=0.0)
+                         band_stop_prob=0.0, pitch_shift_prob=0.0)
     assert torch.equal(off(x), x)
 
 
@@ -349,7 +349,7 @@ def test_batch_augmenter_colored_noise_is_per_batch():
     np.random.seed(6)
     aug = BatchAugmenter(device=0, batch_size=128, background_noise_prob=0.0, reverb_prob=0.0, gain_prob=0.0,
                          colored_noise_prob=1.0, tanh_distortion_prob=0.0, seven_band_prob=0.0,
-                         band_stop_prob=0.0)
+                         band_stop_prob=0.0, pitch_shift_prob=0.0)
     out = aug(x)
     xs, os_ = x.cpu().double().numpy(), out.cpu().double().numpy()
     rms = lambda v: np.sqrt((v * v).mean(axis=-1))
@@ -360,7 +360,7 @@ def test_batch_augmenter_colored_noise_is_per_batch():
         assert 10.0 - 1e-3 <= blk[0] <= 30.0 + 1e-3
     off = BatchAugmenter(device=0, background_noise_prob=0.0, reverb_prob=0.0, gain_prob=0.0,
                          colored_noise_prob=0.0, tanh_distortion_prob=0.0, seven_band_prob=0.0,
-                         band_stop_prob=0.0)
+                         band_stop_prob=0.0, pitch_shift_prob=0.0)
     assert torch.equal(off(x), x)
 
 
@@ -521,7 +521,7 @@ def test_batch_augmenter_band_stop_is_per_batch():
     np.random.seed(9)
     aug = BatchAugmenter(device=0, batch_size=128, background_noise_prob=0.0, reverb_prob=0.0, gain_prob=0.0,
                          colored_noise_prob=0.0, tanh_distortion_prob=0.0, seven_band_prob=0.0,
-                         band_stop_prob=1.0)
+                         band_stop_prob=1.0, pitch_shift_prob=0.0)
     pr = aug.prepare(300)
     idx, lo, hi = (t.numpy() for t in pr["bandstop"])
     np.testing.assert_array_equal(idx, np.arange(300))
@@ -535,5 +535,119 @@ def test_batch_augmenter_band_stop_is_per_batch():
         assert np.abs(out[i] - ref[j]).max() <= 2e-5 * np.abs(xs[i]).max()
     off = BatchAugmenter(device=0, background_noise_prob=0.0, reverb_prob=0.0, gain_prob=0.0,
                          colored_noise_prob=0.0, tanh_distortion_prob=0.0, seven_band_prob=0.0,
-                         band_stop_prob=0.0)
+                         band_stop_prob=0.0, pitch_shift_prob=0.0)
     assert off.prepare(300)["bandstop"] is None
+
+
+# ------------------------------------------------------------------ pitch shift
+
+def test_pitch_shift_oracle_properties():
+    """The restated torch_pitch_shift: the fast shifts at 16 kHz within +-3
+    semitones, the frame / resampler geometry, and a tone moving by the ratio."""
+    from fractions import Fraction
+    assert oaug.pitch_fast_shifts(16000, 3) == [Fraction(125, 128), Fraction(128, 125)]
+    g = oaug.pitch_shift_geometry(T, 128, 125)
+    assert (g["f_in"], g["f_out"], g["l1"], g["orig"], g["new"], g["width"], g["target"]) == \
+        (3292, 3372, 23597, 128, 125, 7, 23044)
+    g = oaug.pitch_shift_geometry(T, 125, 128)
+    assert (g["f_out"], g["l1"], g["orig"], g["new"], g["target"]) == (3215, 22498, 125, 128, 23038)
+    taps, w = oaug.resample_taps(128, 125)
+    assert taps.shape == (125, 2 * w + 128) and taps.dtype == np.float32
+    np.testing.assert_allclose(taps.sum(axis=1), 1.0, rtol=2e-2)   # ~unit DC gain per output phase
+    t = np.arange(T) / 16000.0
+    for num, den in ((128, 125), (125, 128)):
+        y = oaug.pitch_shift(0.5 * np.sin(2 * np.pi * 1000.0 * t), num, den)[0]
+        s = np.abs(np.fft.rfft(y[2000:18384] * np.hanning(16384)))
+        assert abs(np.argmax(s) * 16000 / 16384 - 1000.0 * num / den) < 1.5
+    assert not oaug.pitch_shift(np.zeros(T), 128, 125).any()
+
+
+def test_pitch_shift_workspace_geometry():
+    """hbk_pitch_shift_workspace_size (host only): 0 for an unsupported rate
+    or ratio, ~3.4 MB per clip at 23,040 samples."""
+    from heybuddy._native import lib
+    h = lib()
+    one = h.hbk_pitch_shift_workspace_size(1, T, 16000, 128, 125)
+    assert 3_000_000 < one < 4_000_000
+    assert h.hbk_pitch_shift_workspace_size(4, T, 16000, 125, 128) > 3 * one
+    assert h.hbk_pitch_shift_workspace_size(1, T, 22050, 128, 125) == 0
+    assert h.hbk_pitch_shift_workspace_size(1, T, 16000, 3, 2) == 0      # 16000 -> 10666: not a fast shift
+
+
+def _pitch_clips():
+    x = _clips(8, seed=57).astype(np.float32)
+    t = np.arange(T) / 16000.0
+    x[1] = 0.3 * np.sin(2 * np.pi * 440.0 * t) + 0.1 * np.sin(2 * np.pi * 3100.0 * t)
+    x[2, :9000] = 0.0                   # leading silence (all-zero frames: angle 0 in the FFT)
+    x[3, 15000:] = 0.0                  # trailing silence
+    x[4] = 0.0                          # silent clip stays silent
+    # a chirp. (No piecewise-constant clip: its constant frames have exactly zero
+    # energy off DC, so the vocoder phase carried across a step is rounding noise
+    # in every implementation, the reference's float32 FFT included.)
+    x[6] = 0.3 * np.sin(2 * np.pi * (100.0 + 1500.0 * t) * t)
+    return x
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("num,den,inplace", [(128, 125, False), (125, 128, True)])
+def test_pitch_shift_matches_oracle(num, den, inplace):
+    """hbk_pitch_shift against the float64 restatement for both fast shifts:
+    speech-like clips, two tones, leading / trailing silence, a silent clip, a
+    chirp, and an unlisted clip (7) left untouched. Tolerance: per clip, L2 error
+    <= 1e-4 of the reference's L2 and max error <= 1e-3 of its peak (sliding DFT
+    in float32 against numpy's float64 FFT; the phase cumsum is float64 in both)."""
+    from heybuddy.kernels import pitch_shift
+    x = _pitch_clips()
+    sel = np.array([0, 1, 2, 3, 4, 5, 6], np.int32)
+    ref = oaug.pitch_shift(x[sel], num, den)
+    xd = torch.from_numpy(x).cuda()
+    out = pitch_shift(xd, torch.from_numpy(sel), num, den, out=xd if inplace else None).cpu().numpy()
+    for j, i in enumerate(sel):
+        r = ref[j]
+        if not r.any():
+            assert not out[i].any(), f"clip {i}: silent input, non-zero output"
+            continue
+        l2 = np.sqrt(((out[i] - r) ** 2).sum()) / np.sqrt((r ** 2).sum())
+        mx = np.abs(out[i] - r).max() / np.abs(r).max()
+        assert l2 <= 1e-4 and mx <= 1e-3, f"clip {i}: rel L2 {l2:.2e}, rel max {mx:.2e}"
+    np.testing.assert_array_equal(out[7], x[7])
+
+
+def test_fast_shifts_match_oracle():
+    """The package's fast-shift list (BatchAugmenter's draw set) equals the
+    oracle's restatement of torch_pitch_shift.get_fast_shifts."""
+    from heybuddy.dataset.augmented import fast_shifts
+    for sr, semi in ((16000, 3), (16000, 12), (22050, 2), (8000, 5)):
+        assert fast_shifts(sr, semi) == oaug.pitch_fast_shifts(sr, semi)
+
+
+@pytest.mark.gpu
+def test_batch_augmenter_pitch_shift_is_per_batch():
+    """BatchAugmenter: pitch shift per batch of 128 (one fast shift per batch
+    whose coin came up), first in the batch chain; the device result equals
+    the oracle on the drawn shift."""
+    from heybuddy.dataset.augmented import BatchAugmenter
+    x = torch.from_numpy(_clips(300, seed=61)).float().cuda()
+    np.random.seed(13)
+    aug = BatchAugmenter(device=0, batch_size=128, background_noise_prob=0.0, reverb_prob=0.0, gain_prob=0.0,
+                         colored_noise_prob=0.0, tanh_distortion_prob=0.0, seven_band_prob=0.0,
+                         band_stop_prob=0.0, pitch_shift_prob=1.0)
+    pr = aug.prepare(300)
+    groups = pr["pitch"]
+    assert sorted(np.concatenate([g[2].numpy() for g in groups]).tolist()) == list(range(300))
+    shift_of = {}
+    for num, den, clips in groups:
+        assert (num, den) in ((125, 128), (128, 125))
+        for c in clips.numpy():
+            shift_of[int(c)] = (num, den)
+    for b0 in range(0, 300, 128):
+        assert len({shift_of[c] for c in range(b0, min(b0 + 128, 300))}) == 1
+    out = aug(x, prepared=pr).cpu().numpy()
+    xs = x.cpu().numpy()
+    for i in (0, 127, 128, 299):
+        r = oaug.pitch_shift(xs[i], *shift_of[i])[0]
+        assert np.sqrt(((out[i] - r) ** 2).sum() / (r ** 2).sum()) <= 1e-4
+    off = BatchAugmenter(device=0, background_noise_prob=0.0, reverb_prob=0.0, gain_prob=0.0,
+                         colored_noise_prob=0.0, tanh_distortion_prob=0.0, seven_band_prob=0.0,
+                         band_stop_prob=0.0, pitch_shift_prob=0.0)
+    assert off.prepare(300)["pitch"] == []

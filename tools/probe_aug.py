@@ -16,7 +16,7 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 100000
 dev = torch.device("cuda", 0)
 x = synthetic_clips(n, seed=1, device=dev)
 aug = BatchAugmenter(noise_bank(64, seed=2, device=dev), impulse_responses(32, seed=3, device=dev), device=dev,
-                     batch_size=128, background_noise_prob=1.0, reverb_prob=1.0)
+                     batch_size=128, background_noise_prob=1.0, reverb_prob=1.0, pitch_shift_prob=0.0)
 out = torch.empty((n, 23040), dtype=torch.float32, device=dev)
 for _ in range(2):
     aug(x, out=out)
