@@ -73,6 +73,8 @@ def parse():
                     help="config 3 plus the reference's tanh distortion and colored noise at their default "
                          "probabilities (0.25 each); not the BASELINE configs[2] workload")
     ap.add_argument("--no-check", action="store_true", help="skip the one-off featurize equality check")
+    ap.add_argument("--pitch-prob", type=float, default=0.25,
+                    help="config 5: PitchShift probability per batch (the reference's default 0.25)")
     ap.add_argument("--overlap", default="split:64",
                     help="config 5: train chunk s while chunk s + 1 is featurized on a second stream "
                          "(heybuddy.pipeline policies: off, prio, split:N, spill:N; N a multiple of 32, "
@@ -501,7 +503,7 @@ def setup_e2e(args, dev, rank, world, seed):
     lens = np.concatenate([pos_len, adv_len]).astype(np.int32)
     aug = AugmentedAudioGenerator([], device_id=dev.index, augmentation_dataset=noise_bank(64, seed=seed + 2),
                                   impulse_response_dataset=impulse_responses(32, seed=seed + 3), batch_size=128,
-                                  pitch_shift_prob=0.0)  # EQ, tanh, band-stop, colored, gain at defaults
+                                  pitch_shift_prob=args.pitch_prob)  # every augmentation at its default
     mplan = default_mel_plan(dev, 32767.0)
     eplan = embed_plan(dev, WINDOW_STARTS)
     pool = torch.empty((n, len(WINDOW_STARTS), 96), dtype=torch.float32, device=dev)
@@ -636,11 +638,11 @@ def setup_e2e(args, dev, rank, world, seed):
 
     def roofline(name, ms, pmc):
         if name == "augment":
-            return roof("place_kernel + eq_kernel + tanh_distortion_kernel + band_stop_kernel + colored_noise_kernel + "
-                        "augment_kernel (placement, 7-band EQ, tanh, band-stop, colored noise, gain + noise mix + "
-                        "23040-pt FFT reverb)", "hbm",
+            return roof("place_kernel + eq_kernel + tanh_distortion_kernel + ps_*_kernel + band_stop_kernel + "
+                        "colored_noise_kernel + augment_kernel (placement, 7-band EQ, tanh, pitch shift, band-stop, "
+                        "colored noise, gain + noise mix + 23040-pt FFT reverb)", "hbm",
                         n * AUG_T * 4 * 2, ms, "GB/s", load_traffic(pmc, ("place_kernel", "augment_kernel", "eq_kernel",
-                                                                          "band_stop", "colored_noise",
+                                                                          "band_stop", "colored_noise", "ps_",
                                                                           "tanh_distortion")),
                         algorithmic_bytes_per_clip=AUG_T * 4 * 2,
                         bytes_basis="placed clip written + augmented clip written in place (92,160 B each); "
@@ -746,9 +748,9 @@ def setup_e2e(args, dev, rank, world, seed):
         "data": "synthetic TTS-like utterances (seeded, 0.3-1.5 s), synthetic noise + IR banks, synthetic "
                 "f16 negative pool; SE20 stand-in embedding graph",
         "config": {"workload": "configs[4]: end-to-end heybuddy-train pipeline per GPU: placement -> augment "
-                               "(reference default probabilities: 7-band EQ, tanh, band-stop, colored noise, gain, background noise, "
-                               "reverb; pitch shift not on the path yet) -> mel -> embed -> %d train steps (B=%d: 50 pos "
-                               "+ 50 adv of the step's clips + 1000 f16 negatives)" % (S, B),
+                               "(reference default probabilities: 7-band EQ, tanh, pitch shift p=%g, band-stop, colored "
+                               "noise, gain, background noise, reverb) -> mel -> embed -> %d train steps (B=%d: 50 pos "
+                               "+ 50 adv of the step's clips + 1000 f16 negatives)" % (args.pitch_prob, S, B),
                    "clips_per_rank": n, "train_steps_per_rank": S, "train_batch_per_rank": B,
                    "negative_pool": f"{n_neg} x [16,96] f16",
                    "parallelism": f"dp{world} (clip shards; 1 all-reduce of the 1,025,700-B bucket per train step)",

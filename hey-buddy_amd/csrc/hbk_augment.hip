@@ -1389,21 +1389,26 @@ __global__ void __launch_bounds__(64) eq_kernel(EqArgs a) {
 // Y_t[k] e^{-2 pi i k 7 t / 250}, sample p of the overlap-add is
 //   (1/250) sum_k c_k Re(e^{2 pi i k p / 250} W_p[k]),  W_p = sum of Z_t over the
 // <= 36 frames covering p, a sliding window sum per bin.
-//   ps_stft_kernel       (segment of 64 input frames, clip): angle, |X| per frame
-//   ps_phase_sum_kernel  (segment, clip): sum of the vocoder's phase increments of
-//                        the output frames whose source frame is in the segment
-//   ps_synth_kernel      (segment, clip): prefix phase (f64), vocoder frames, the
-//                        windowed sums, a bin reduction through LDS -> istft samples
+// No spectrogram is stored: both passes slide the DFT over their own frames
+// from the clip samples in LDS (a frame depends on its index alone, see PsFrames).
+//   ps_phase_sum_kernel  (segment of 128 input frames, clip): sums of the vocoder's
+//                        phase increments of the output frames whose source frame
+//                        is in the segment (all, and the last 35)
+//   ps_synth_kernel      (segment, clip): prefix phase (f64) from those sums, the
+//                        vocoder frames, the windowed sums, a bin reduction
+//                        through LDS -> istft samples
 //   ps_resample_kernel   (frame group, clip): polyphase sinc, taps in registers
 constexpr int kPsFft = 250, kPsHop = 7, kPsBins = kPsFft / 2 + 1, kPsPad = kPsFft / 2;
-constexpr int kPsSeg = 64;                             // input frames per segment
-constexpr int kPsRestart = 16;                         // direct DFT every 16 frames
+constexpr int kPsSeg = 128;                            // input frames per segment
+constexpr int kPsRestart = 64;                         // direct DFT at every 64th frame (absolute index)
 constexpr int kPsWin = (kPsFft + kPsHop - 1) / kPsHop;  // 36 frames cover a sample
-constexpr int kPsChunk = 8;                            // output frames per bin reduction
+constexpr int kPsChunk = 4;                            // output frames per bin reduction
 constexpr int kPsTapMax = HBK_PITCH_SHIFT_MAX_TAPS;    // 2 width + orig (142 / 139 at 16 kHz)
 constexpr int kPsPhaseMax = 128;                       // new (resampler phases)
 constexpr int kPsResFrames = 32;                       // resampler frames per workgroup
-constexpr int kPsLd = 128;                             // bins stored per frame (126 used)
+constexpr int kPsLd = 128;                             // bins per row of the phase sums (126 used)
+constexpr int kPsFrames = 240;                         // input frames a workgroup may touch
+constexpr int kPsXs = kPsHop * (kPsFrames - 1) + kPsFft;
 
 struct PitchArgs {
   const float* x;
@@ -1413,9 +1418,8 @@ struct PitchArgs {
   int64_t out_stride;
   int L, f_in, f_out, l1, nseg, orig, nw, width, target;
   double rate;
-  float* ang;     // [n][f_in + 2][kPsLd]
-  float* mag;     // [n][f_in + 2][kPsLd]
-  double* segsum; // [n][nseg][kPsLd]
+  double* segsum; // [n][nseg][kPsLd]: phase increments of the segment's output frames (+ angle of frame 0 in 0)
+  double* osum;   // [n][nseg][kPsLd]: ... of its last kPsWin - 1 output frames
   float* y;       // [n][l1]
   float* taps;    // [nw][kPsTapMax]
 };
@@ -1437,10 +1441,10 @@ __device__ int ps_first_t(const PitchArgs& a, int f) {
   return t;
 }
 
-// the vocoder's phase increment of output frame t, bin k (torchaudio phase_vocoder)
-__device__ __forceinline__ double ps_phase(const float* ang, int i0, int k) {
+// the vocoder's phase increment between source frames with angles a0, a1 (bin k)
+__device__ __forceinline__ double ps_phase(float a0, float a1, int k) {
   const double adv = (M_PI * kPsHop) * k / (kPsBins - 1);
-  double ph = static_cast<double>(ang[(i0 + 1) * kPsLd]) - static_cast<double>(ang[i0 * kPsLd]) - adv;
+  double ph = static_cast<double>(a1) - static_cast<double>(a0) - adv;
   ph -= (2.0 * M_PI) * rint(ph * (0.5 / M_PI));
   return ph + adv;
 }
@@ -1453,176 +1457,240 @@ __device__ __forceinline__ void ps_twiddles(float2* tw) {
   }
 }
 
-__global__ void __launch_bounds__(128) ps_stft_kernel(PitchArgs a) {
-  __shared__ float2 tw[kPsFft];
-  __shared__ float xs[kPsHop * (kPsSeg - 1) + kPsFft];
-  __shared__ int zf[kPsSeg];
-  const int k = threadIdx.x, s = blockIdx.x, e = blockIdx.y;
-  const float* x = a.x + static_cast<int64_t>(a.idx[e]) * a.x_stride;
-  ps_twiddles(tw);
-  const int f0 = s * kPsSeg, nf = min(kPsSeg, a.f_in - f0);
-  const int q0 = f0 * kPsHop, nq = kPsHop * (nf - 1) + kPsFft;
-  for (int q = k; q < nq; q += 128) {  // reflect padding by n_fft / 2
-    int i = q0 + q - kPsPad;
+// Frames [fb, fe] of one clip in LDS: the reflect-padded samples and the
+// all-zero flags. Every frame is a function of its index alone (direct DFT at
+// multiples of kPsRestart, slides in between), so both kernels see identical
+// spectra. fb must be a multiple of kPsRestart, fe - fb < kPsFrames.
+struct PsFrames {
+  const float* xs;
+  const int* zf;
+  const float2* tw;
+  float2 rot;
+  int k, fb, f_in;
+  // X_f from X_{f-1} (xr, xi)
+  __device__ __forceinline__ void next(int f, float& xr, float& xi) const {
+    if (f >= f_in) {  // the vocoder's zero frames past the end
+      xr = xi = 0.f;
+      return;
+    }
+    const float* xf = xs + kPsHop * (f - fb);
+    if (f % kPsRestart == 0) {  // X = sum_n x[n] e^{-2 pi i k n / 250}
+      float re = 0.f, im = 0.f;
+      int q = 0;
+      for (int j = 0; j < kPsFft; ++j) {
+        const float v = xf[j];
+        const float2 w = tw[q];
+        re = fmaf(v, w.x, re);
+        im = fmaf(-v, w.y, im);
+        q += k;
+        q -= q >= kPsFft ? kPsFft : 0;
+      }
+      xr = re;
+      xi = im;
+    } else {  // X_f = e^{2 pi i k 7 / 250} (X_{f-1} + sum_j (x_in[j] - x_out[j]) e^{-2 pi i k j / 250})
+      float dr = 0.f, di = 0.f;
+      int q = 0;
+#pragma unroll
+      for (int j = 0; j < kPsHop; ++j) {
+        const float d = xf[kPsFft - kPsHop + j] - xf[j - kPsHop];
+        const float2 w = tw[q];
+        dr = fmaf(d, w.x, dr);
+        di = fmaf(-d, w.y, di);
+        q += k;
+        q -= q >= kPsFft ? kPsFft : 0;
+      }
+      const float ar = xr + dr, ai = xi + di;
+      xr = ar * rot.x - ai * rot.y;
+      xi = ar * rot.y + ai * rot.x;
+    }
+    if (!zf[f - fb]) xr = xi = 0.f;
+  }
+};
+
+__device__ __forceinline__ void ps_load_frames(const PitchArgs& a, const float* x, int fb, int fe, float* xs,
+                                               int* zf) {
+  const int nq = kPsHop * (fe - fb) + kPsFft;
+  for (int q = threadIdx.x; q < nq; q += blockDim.x) {  // reflect padding by n_fft / 2
+    int i = kPsHop * fb + q - kPsPad;
     i = i < 0 ? -i : i;
     i = i >= a.L ? 2 * (a.L - 1) - i : i;
     xs[q] = x[i];
   }
   __syncthreads();
-  if (k < nf) {
+  for (int f = threadIdx.x; f <= fe - fb; f += blockDim.x) {
+    const float* xf = xs + kPsHop * f;
     bool any = false;
-    for (int j = 0; j < kPsFft; ++j) any |= xs[kPsHop * k + j] != 0.f;
-    zf[k] = any;
+    for (int j = 0; j < kPsFft; ++j) any |= xf[j] != 0.f;
+    zf[f] = any;
   }
   __syncthreads();
-  const int64_t frame0 = static_cast<int64_t>(e) * (a.f_in + 2);
-  float* ang = a.ang + (frame0 + f0) * kPsLd + k;
-  float* mag = a.mag + (frame0 + f0) * kPsLd + k;
-  if (k < kPsBins) {
-    const float2 rot = tw[(kPsHop * k) % kPsFft];
-    float xr = 0.f, xi = 0.f;
-    for (int f = 0; f < nf; ++f) {
-      const float* xf = xs + kPsHop * f;
-      if (f % kPsRestart == 0) {  // X = sum_n x[n] e^{-2 pi i k n / 250}
-        float re = 0.f, im = 0.f;
-        int q = 0;
-        for (int j = 0; j < kPsFft; ++j) {
-          const float v = xf[j];
-          const float2 w = tw[q];
-          re = fmaf(v, w.x, re);
-          im = fmaf(-v, w.y, im);
-          q += k;
-          q -= q >= kPsFft ? kPsFft : 0;
-        }
-        xr = re;
-        xi = im;
-      } else {  // X_f = e^{2 pi i k 7 / 250} (X_{f-1} + sum_j (x_in[j] - x_out[j]) e^{-2 pi i k j / 250})
-        float dr = 0.f, di = 0.f;
-        int q = 0;
-#pragma unroll
-        for (int j = 0; j < kPsHop; ++j) {
-          const float d = xf[kPsFft - kPsHop + j] - xf[j - kPsHop];
-          const float2 w = tw[q];
-          dr = fmaf(d, w.x, dr);
-          di = fmaf(-d, w.y, di);
-          q += k;
-          q -= q >= kPsFft ? kPsFft : 0;
-        }
-        const float ar = xr + dr, ai = xi + di;
-        xr = ar * rot.x - ai * rot.y;
-        xi = ar * rot.y + ai * rot.x;
-      }
-      if (!zf[f]) xr = xi = 0.f;
-      ang[f * kPsLd] = atan2f(xi, xr);
-      mag[f * kPsLd] = sqrtf(xr * xr + xi * xi);
-    }
-  }
-  if (s == a.nseg - 1) {  // the vocoder's two zero frames past the end
-    float* az = a.ang + (frame0 + a.f_in) * kPsLd + k;
-    float* mz = a.mag + (frame0 + a.f_in) * kPsLd + k;
-    az[0] = az[kPsLd] = 0.f;
-    mz[0] = mz[kPsLd] = 0.f;
-  }
 }
 
-__global__ void __launch_bounds__(128) ps_phase_sum_kernel(PitchArgs a) {
-  const int k = threadIdx.x, s = blockIdx.x, e = blockIdx.y;
-  const int t0 = ps_first_t(a, s * kPsSeg);
-  const int t1 = s + 1 < a.nseg ? ps_first_t(a, (s + 1) * kPsSeg) : a.f_out;
-  const float* ang = a.ang + static_cast<int64_t>(e) * (a.f_in + 2) * kPsLd + k;
-  double acc = 0.0;
-  if (k < kPsBins) {
-    for (int t = t0; t < t1; ++t) {
-      float al;
-      acc += ps_phase(ang, ps_i0(a, t, al), k);
+// a frame producer: (X, angle, |X|) of the current source frame c and of c + 1
+struct PsCursor {
+  float cr, ci, ca, cm;  // frame c
+  float nr, ni, na, nm;  // frame c + 1
+  int c;
+  // frames F.fb .. i slid without their angles, then frames i and i + 1
+  __device__ __forceinline__ void seek(const PsFrames& F, int i) {
+    F.next(F.fb, cr, ci);
+    for (int f = F.fb + 1; f <= i; ++f) F.next(f, cr, ci);
+    c = i;
+    nr = cr;
+    ni = ci;
+    F.next(c + 1, nr, ni);
+    ca = atan2f(ci, cr);
+    cm = sqrtf(cr * cr + ci * ci);
+    na = atan2f(ni, nr);
+    nm = sqrtf(nr * nr + ni * ni);
+  }
+  __device__ __forceinline__ void advance_to(const PsFrames& F, int i0) {
+    while (c < i0) {
+      ++c;
+      cr = nr;
+      ci = ni;
+      ca = na;
+      cm = nm;
+      F.next(c + 1, nr, ni);
+      na = atan2f(ni, nr);
+      nm = sqrtf(nr * nr + ni * ni);
     }
   }
-  a.segsum[(static_cast<int64_t>(e) * a.nseg + s) * kPsLd + k] = acc;
+};
+
+__global__ void __launch_bounds__(128) ps_phase_sum_kernel(PitchArgs a) {
+  __shared__ float2 tw[kPsFft];
+  __shared__ float xs[kPsXs];
+  __shared__ int zf[kPsFrames];
+  const int k = threadIdx.x, s = blockIdx.x, e = blockIdx.y;
+  ps_twiddles(tw);
+  const int f0 = s * kPsSeg, fe = min(f0 + kPsSeg, a.f_in - 1);
+  ps_load_frames(a, a.x + static_cast<int64_t>(a.idx[e]) * a.x_stride, f0, fe, xs, zf);
+  const int t0 = ps_first_t(a, f0);
+  const int t1 = s + 1 < a.nseg ? ps_first_t(a, f0 + kPsSeg) : a.f_out;
+  const int kq = min(k, kPsBins - 1);
+  PsFrames F{xs, zf, tw, tw[(kPsHop * kq) % kPsFft], kq, f0, a.f_in};
+  PsCursor cur;
+  cur.seek(F, f0);
+  double acc = s == 0 ? static_cast<double>(cur.ca) : 0.0, osum = 0.0;
+  for (int t = t0; t < t1; ++t) {
+    float al;
+    cur.advance_to(F, ps_i0(a, t, al));
+    const double ph = ps_phase(cur.ca, cur.na, kq);
+    acc += ph;
+    if (t >= t1 - (kPsWin - 1)) osum += ph;
+  }
+  const int64_t o = (static_cast<int64_t>(e) * a.nseg + s) * kPsLd + k;
+  a.segsum[o] = k < kPsBins ? acc : 0.0;
+  a.osum[o] = k < kPsBins ? osum : 0.0;
 }
 
 __global__ void __launch_bounds__(128) ps_synth_kernel(PitchArgs a) {
   __shared__ float2 tw[kPsFft];
-  __shared__ float2 ring[kPsWin][kPsLd];
   __shared__ float cb[kPsChunk * kPsHop][kPsLd + 1];
+  __shared__ float xs[kPsXs];
+  __shared__ int zf[kPsFrames];
   const int k = threadIdx.x, s = blockIdx.x, e = blockIdx.y;
   ps_twiddles(tw);
-  for (int i = k; i < kPsWin * kPsLd; i += 128) ring[i / kPsLd][i % kPsLd] = make_float2(0.f, 0.f);
   const int t_lo = ps_first_t(a, s * kPsSeg);
   const bool last = s + 1 == a.nseg;
   const int t_hi = last ? a.f_out : ps_first_t(a, (s + 1) * kPsSeg);
   // samples p = 7 j + r of this segment: j in [t_lo, j_end); the last segment
   // runs past the last frame to the last istft sample (p = n_fft/2 + l1 - 1)
   const int j_end = last ? (a.l1 + kPsPad - 1) / kPsHop + 1 : t_hi;
-  const int t_a = max(0, t_lo - (kPsWin - 1));
-  const int64_t frame0 = static_cast<int64_t>(e) * (a.f_in + 2);
-  const float* ang = a.ang + frame0 * kPsLd + k;
-  const float* mag = a.mag + frame0 * kPsLd + k;
-  double acc = 0.0;  // accumulated phase of frame t (float64: |acc| reaches 7e4 rad)
-  if (k < kPsBins) {
-    acc = ang[0];
+  const int t_a = s == 0 ? 0 : t_lo - (kPsWin - 1);
+  float al;
+  const int i_a = ps_i0(a, t_a, al);
+  const int fb = i_a - i_a % kPsRestart;
+  const int fe = min(ps_i0(a, min(j_end, a.f_out) - 1, al) + 1, a.f_in - 1);
+  ps_load_frames(a, a.x + static_cast<int64_t>(a.idx[e]) * a.x_stride, fb, fe, xs, zf);
+  const int kq = min(k, kPsBins - 1);
+  PsFrames F{xs, zf, tw, tw[(kPsHop * kq) % kPsFft], kq, fb, a.f_in};
+  PsCursor cur;
+  cur.seek(F, i_a);
+  // accumulated phase of frame t_a (float64: |acc| reaches 7e4 rad)
+  double acc = 0.0;
+  if (s == 0) {
+    acc = cur.ca;
+  } else {
     const double* ss = a.segsum + static_cast<int64_t>(e) * a.nseg * kPsLd + k;
     for (int q = 0; q < s; ++q) acc += ss[q * kPsLd];
-    for (int t = t_a; t < t_lo; ++t) {
-      float al;
-      acc -= ps_phase(ang, ps_i0(a, t, al), k);
-    }
+    acc -= a.osum[(static_cast<int64_t>(e) * a.nseg + s - 1) * kPsLd + k];
   }
-  __syncthreads();
   const float ck = (k == 0 || k == kPsBins - 1) ? 1.f : (k < kPsBins ? 2.f : 0.f);
-  const int kq = k < kPsBins ? k : 0;
   float wr = 0.f, wi = 0.f;
   int row = 0, jc = t_lo;
+  // qz = k 7 t mod 250: Z_t = Y_t e^{-2 pi i qz / 250}, and sample p = 7 t + r
+  // takes e^{+2 pi i (qz + k r) / 250}
+  int qz = (kq * ((kPsHop * t_a) % kPsFft)) % kPsFft;
+  const int dq = (kPsHop * kq) % kPsFft;
   float* y = a.y + static_cast<int64_t>(e) * a.l1;
-  for (int t = t_a; t < j_end; ++t) {
-    float zr = 0.f, zi = 0.f;
-    if (k < kPsBins && t < a.f_out) {
-      float al;
-      const int i0 = ps_i0(a, t, al);
-      const float m = al * mag[(i0 + 1) * kPsLd] + (1.f - al) * mag[i0 * kPsLd];
-      double th = acc - (2.0 * M_PI / kPsFft) * ((kPsHop * static_cast<int64_t>(t) * k) % kPsFft);
-      th -= (2.0 * M_PI) * rint(th * (0.5 / M_PI));
-      float sn, cs;
-      sincosf(static_cast<float>(th), &sn, &cs);
-      zr = m * cs;
-      zi = m * sn;
-      acc += ps_phase(ang, i0, k);
-    }
-    const int slot = t % kPsWin;
-    const float2 old = ring[slot][k];
-    wr += zr - old.x;
-    wi += zi - old.y;
-    ring[slot][k] = make_float2(zr, zi);
-    if (t >= t_lo) {
-      const float2 z35 = ring[(t + 1) % kPsWin][k];  // Z_{t-35}
-      int q = (kq * ((kPsHop * t) % kPsFft)) % kPsFft;
+  // this bin's last kPsWin vocoder frames Z in registers, oldest first (a
+  // shift per frame keeps every index static)
+  float2 zq[kPsWin];
 #pragma unroll
-      for (int r = 0; r < kPsHop; ++r) {
-        // frames t-35 .. t cover p = 7 t + r for r <= 4, t-34 .. t for r = 5, 6
-        const float vr = r <= 4 ? wr : wr - z35.x, vi = r <= 4 ? wi : wi - z35.y;
-        const float2 w = tw[q];
-        cb[row * kPsHop + r][k] = ck * (w.x * vr - w.y * vi);
-        q += kq;
-        q -= q >= kPsFft ? kPsFft : 0;
+  for (int u = 0; u < kPsWin; ++u) zq[u] = make_float2(0.f, 0.f);
+  for (int t = t_a; t < j_end; ++t) {
+    {
+      float zr = 0.f, zi = 0.f;
+      if (t < a.f_out) {
+        cur.advance_to(F, ps_i0(a, t, al));
+        const float m = al * cur.nm + (1.f - al) * cur.cm;
+        const double th = acc - (2.0 * M_PI) * rint(acc * (0.5 / M_PI));
+        float sn, cs;
+        __sincosf(static_cast<float>(th), &sn, &cs);
+        const float2 w = tw[qz];
+        const float yr = m * cs, yi = m * sn;
+        zr = yr * w.x + yi * w.y;
+        zi = yi * w.x - yr * w.y;
+        acc += ps_phase(cur.ca, cur.na, kq);
       }
-      ++row;
-      if (row == kPsChunk || t == j_end - 1) {
-        __syncthreads();
-        if (k < row * kPsHop) {
-          const int p = kPsHop * jc + k;
-          const int m = p - kPsPad;
-          if (m >= 0 && m < a.l1) {
-            float acc2 = 0.f;
-            for (int b = 0; b < kPsBins; ++b) acc2 += cb[k][b];
-            const int j = p / kPsHop;
-            const int lo = max(0, j - (kPsWin - 1) + (p % kPsHop >= 5 ? 1 : 0));
-            const int hi = min(a.f_out - 1, j);
-            y[m] = acc2 / (static_cast<float>(kPsFft) * static_cast<float>(hi - lo + 1));
-          }
+      wr += zr - zq[0].x;  // Z_{t-36} leaves the window
+      wi += zi - zq[0].y;
+#pragma unroll
+      for (int u = 0; u + 1 < kPsWin; ++u) zq[u] = zq[u + 1];
+      zq[kPsWin - 1] = make_float2(zr, zi);
+      if (t >= t_lo) {
+        const float z35r = zq[0].x, z35i = zq[0].y;  // Z_{t-35}
+        int q = qz;
+#pragma unroll
+        for (int r = 0; r < kPsHop; ++r) {
+          // frames t-35 .. t cover p = 7 t + r for r <= 4, t-34 .. t for r = 5, 6
+          const float vr = r <= 4 ? wr : wr - z35r, vi = r <= 4 ? wi : wi - z35i;
+          const float2 w = tw[q];
+          cb[row * kPsHop + r][k] = ck * (w.x * vr - w.y * vi);
+          q += kq;
+          q -= q >= kPsFft ? kPsFft : 0;
         }
-        __syncthreads();
-        row = 0;
-        jc = t + 1;
+        ++row;
+        if (row == kPsChunk || t == j_end - 1) {
+          __syncthreads();
+          // two lanes per sample row (63 bins each), combined by a lane swap
+          const int rw = k >> 1, h = k & 1;
+          float part = 0.f;
+          if (rw < row * kPsHop) {
+            const float* c = cb[rw] + h * 63;
+#pragma unroll 9
+            for (int b = 0; b < 63; ++b) part += c[b];
+          }
+          part += __shfl_xor(part, 1);
+          if (h == 0 && rw < row * kPsHop) {
+            const int p = kPsHop * jc + rw;
+            const int m = p - kPsPad;
+            if (m >= 0 && m < a.l1) {
+              const int j = p / kPsHop;
+              const int lo = max(0, j - (kPsWin - 1) + (p % kPsHop >= 5 ? 1 : 0));
+              const int hi = min(a.f_out - 1, j);
+              y[m] = part / (static_cast<float>(kPsFft) * static_cast<float>(hi - lo + 1));
+            }
+          }
+          __syncthreads();
+          row = 0;
+          jc = t + 1;
+        }
       }
+      qz += dq;
+      qz -= qz >= kPsFft ? kPsFft : 0;
     }
   }
 }
@@ -2014,7 +2082,8 @@ static int ps_geometry(int64_t L, int32_t sample_rate, int32_t num, int32_t den,
   a.nw = static_cast<int>(new_sr / g);
   a.width = static_cast<int>(std::ceil(6.0 * a.orig / (std::min(a.orig, a.nw) * 0.99)));
   a.target = static_cast<int>(std::ceil(double(a.nw) * a.l1 / a.orig));
-  if (a.nw > kPsPhaseMax || 2 * a.width + a.orig > kPsTapMax || a.l1 <= 0) {
+  const int span = kPsSeg + static_cast<int>(std::ceil((kPsWin - 1) * a.rate)) + kPsRestart + 4;
+  if (a.nw > kPsPhaseMax || 2 * a.width + a.orig > kPsTapMax || a.l1 <= 0 || span > kPsFrames) {
     set_error("hbk: pitch shift %d/%d resamples %d -> %d (%d taps): the kernel holds <= %d phases of <= %d taps "
               "(torch_pitch_shift's fast shifts at 16 kHz)", num, den, a.orig, a.nw, 2 * a.width + a.orig,
               kPsPhaseMax, kPsTapMax);
@@ -2026,11 +2095,10 @@ static int ps_geometry(int64_t L, int32_t sample_rate, int32_t num, int32_t den,
 static int64_t ps_bytes(const hbk::PitchArgs& a, int64_t n, int64_t* off) {
   using namespace hbk;
   auto up = [](int64_t b) { return (b + 255) & ~int64_t(255); };
-  const int64_t spec = up(n * (a.f_in + 2) * kPsLd * 4);
-  off[0] = 0;                                      // ang
-  off[1] = spec;                                   // mag
-  off[2] = 2 * spec;                               // segsum
-  off[3] = off[2] + up(n * a.nseg * kPsLd * 8);    // y
+  off[0] = 0;                                      // segsum
+  off[1] = up(n * a.nseg * kPsLd * 8);             // osum
+  off[2] = 2 * off[1];
+  off[3] = off[2];                                 // y
   off[4] = off[3] + up(n * a.l1 * 4);              // taps
   return off[4] + up(int64_t(kPsPhaseMax) * kPsTapMax * 4);
 }
@@ -2062,17 +2130,14 @@ int hbk_pitch_shift(const float* x, int64_t x_stride, int64_t n, const int32_t* 
   a.idx = idx;
   a.out = out;
   a.out_stride = out_stride;
-  a.ang = reinterpret_cast<float*>(w + off[0]);
-  a.mag = reinterpret_cast<float*>(w + off[1]);
-  a.segsum = reinterpret_cast<double*>(w + off[2]);
+  a.segsum = reinterpret_cast<double*>(w + off[0]);
+  a.osum = reinterpret_cast<double*>(w + off[1]);
   a.y = reinterpret_cast<float*>(w + off[3]);
   a.taps = reinterpret_cast<float*>(w + off[4]);
   hipStream_t st = as_stream(stream);
   const dim3 seg(unsigned(a.nseg), unsigned(n));
   hipLaunchKernelGGL(ps_taps_kernel, dim3(unsigned((a.nw * kPsTapMax + 255) / 256)), dim3(256), 0, st, a);
   HBK_LAUNCH_CHECK("ps_taps_kernel");
-  hipLaunchKernelGGL(ps_stft_kernel, seg, dim3(128), 0, st, a);
-  HBK_LAUNCH_CHECK("ps_stft_kernel");
   hipLaunchKernelGGL(ps_phase_sum_kernel, seg, dim3(128), 0, st, a);
   HBK_LAUNCH_CHECK("ps_phase_sum_kernel");
   hipLaunchKernelGGL(ps_synth_kernel, seg, dim3(128), 0, st, a);

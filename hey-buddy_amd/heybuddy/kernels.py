@@ -624,7 +624,7 @@ def tanh_distortion(x: torch.Tensor, amount: torch.Tensor, out: torch.Tensor | N
     return out
 
 
-PITCH_SHIFT_CHUNK = 256  # clips per hbk_pitch_shift call (~3.4 MB of workspace each)
+PITCH_SHIFT_CHUNK = 2048  # clips per hbk_pitch_shift call (~0.2 MB of workspace each)
 _PS_WS: dict = {}
 
 

@@ -359,7 +359,7 @@ int hbk_band_stop(const hbk_reverb_plan* plan, const float* x, int64_t x_stride,
  * Rows not listed are not touched; out may equal x (all reads of x precede
  * the writes). HBK_ERR_UNSUPPORTED for sample_rate != 16000 or a ratio whose
  * resampler needs more than 128 phases or HBK_PITCH_SHIFT_MAX_TAPS taps.
- * workspace: hbk_pitch_shift_workspace_size bytes (~3.4 MB per entry at
+ * workspace: hbk_pitch_shift_workspace_size bytes (~0.2 MB per entry at
  * T = 23040; 0 for an unsupported geometry). Device pointers. */
 #define HBK_PITCH_SHIFT_MAX_TAPS 144
 int64_t hbk_pitch_shift_workspace_size(int64_t n, int64_t T, int32_t sample_rate, int32_t num, int32_t den);

@@ -564,12 +564,12 @@ def test_pitch_shift_oracle_properties():
 
 def test_pitch_shift_workspace_geometry():
     """hbk_pitch_shift_workspace_size (host only): 0 for an unsupported rate
-    or ratio, ~3.4 MB per clip at 23,040 samples."""
+    or ratio, ~0.2 MB per clip at 23,040 samples (no spectrogram is stored)."""
     from heybuddy._native import lib
     h = lib()
     one = h.hbk_pitch_shift_workspace_size(1, T, 16000, 128, 125)
-    assert 3_000_000 < one < 4_000_000
-    assert h.hbk_pitch_shift_workspace_size(4, T, 16000, 125, 128) > 3 * one
+    assert 100_000 < one < 400_000
+    assert h.hbk_pitch_shift_workspace_size(4, T, 16000, 125, 128) > 2 * one
     assert h.hbk_pitch_shift_workspace_size(1, T, 22050, 128, 125) == 0
     assert h.hbk_pitch_shift_workspace_size(1, T, 16000, 3, 2) == 0      # 16000 -> 10666: not a fast shift
 
