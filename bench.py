@@ -75,15 +75,19 @@ def parse():
     ap.add_argument("--no-check", action="store_true", help="skip the one-off featurize equality check")
     ap.add_argument("--pitch-prob", type=float, default=0.25,
                     help="config 5: PitchShift probability per batch (the reference's default 0.25)")
-    ap.add_argument("--overlap", default="split:64",
-                    help="config 5: train chunk s while chunk s + 1 is featurized on a second stream "
+    ap.add_argument("--overlap", default=None,
+                    help="config 5 (default split:32 with pitch shift on, split:64 without): "
+                         "train chunk s while chunk s + 1 is featurized on a second stream "
                          "(heybuddy.pipeline policies: off, prio, split:N, spill:N; N a multiple of 32, "
                          "i.e. whole CUs of every shader engine of every XCD)")
     ap.add_argument("--stage-steps", type=int, default=2,
                     help="overlapped runs: sequential (untimed) steps that time the stages for the rooflines")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                     help="per-kernel HBM bytes from rocprofv3 --pmc passes (optional)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.overlap is None:  # pitch shift makes featurization ~3x heavier: give it 224 CUs (r02ag)
+        args.overlap = "split:32" if args.pitch_prob > 0 else "split:64"
+    return args
 
 
 TRAFFIC_SOURCE = [None]
