@@ -639,6 +639,8 @@ def setup_e2e(args, dev, rank, world, seed):
         step.keep = keep  # the CU-masked streams live as long as the step
 
     flops_step = 2.0 * 559_296 * B
+    _fft = 2.5 * 250 * np.log2(250)
+    PITCH_FLOP_PER_CLIP = 3292 * _fft + 3372 * 126 * 16 + 3372 * (_fft + 250) + 23044 * 2 * 142
 
     def roofline(name, ms, pmc):
         if name == "augment":
@@ -739,10 +741,31 @@ def setup_e2e(args, dev, rank, world, seed):
         e1.record()
         torch.cuda.synchronize(dev)
         ms = e0.elapsed_time(e1) / 3
-        return [roof("conv_chain_x3_kernel only (HBK_EMBED_NO_P0=1 HBK_EMBED_NO_P1=1: the generic split-f16 chain "
-                     "kernel on every chain, as for a graph without SE20's chain shapes; %d clips, untimed)" % m,
-                     "mfma", 2.0 * gplan.macs_per_clip * m, ms, "TFLOP/s", None, peak=SPLIT_PEAK_TFLOPS,
-                     peak_basis="f16 dense MFMA peak / 3", clips=m)]
+        extra = [roof("conv_chain_x3_kernel only (HBK_EMBED_NO_P0=1 HBK_EMBED_NO_P1=1: the generic split-f16 chain "
+                      "kernel on every chain, as for a graph without SE20's chain shapes; %d clips, untimed)" % m,
+                      "mfma", 2.0 * gplan.macs_per_clip * m, ms, "TFLOP/s", None, peak=SPLIT_PEAK_TFLOPS,
+                      peak_basis="f16 dense MFMA peak / 3", clips=m)]
+        # pitch shift alone (the largest part of the augment stage when it is on): both fast shifts
+        # over the same clips, against the f32 VALU peak, with the FFT-based FLOP count of the
+        # reference's algorithm (stft + vocoder + istft + resample) as the algorithmic work
+        from heybuddy.kernels import pitch_shift
+        x = aug.augment_device(src[:m], lens[:m])
+        rows = torch.arange(m, dtype=torch.int32, device=dev)
+        pitch_shift(x, rows, 128, 125, out=x)
+        e0.record()
+        for num, den in ((128, 125), (125, 128), (128, 125), (125, 128)):
+            pitch_shift(x, rows, num, den, out=x)
+        e1.record()
+        torch.cuda.synchronize(dev)
+        ms = e0.elapsed_time(e1) / 4
+        extra.append(roof("ps_phase_sum_kernel + ps_synth_kernel + ps_resample_kernel (hbk_pitch_shift, both fast "
+                          "shifts alternately; %d clips, untimed)" % m, "valu", PITCH_FLOP_PER_CLIP * m, ms,
+                          "TFLOP/s", None, peak=157.3, peak_basis="f32 vector peak (MI355X_MICROARCH.md)",
+                          flops_basis="FFT-based count of the reference's algorithm per clip: stft 3,292 x 2.5 N "
+                                      "log2 N (N = 250) + vocoder 3,372 x 126 x 16 + istft 3,372 x (2.5 N log2 N + "
+                                      "250) + resample 23,044 x 2 x 142 = %.1f MFLOP" % (PITCH_FLOP_PER_CLIP / 1e6),
+                          clips=m))
+        return extra
 
     return {
         "step": step, "staged_step": staged_step, "stages": stages, "roofline": roofline,
