@@ -1402,7 +1402,7 @@ constexpr int kPsFft = 250, kPsHop = 7, kPsBins = kPsFft / 2 + 1, kPsPad = kPsFf
 constexpr int kPsSeg = 128;                            // input frames per segment
 constexpr int kPsRestart = 64;                         // direct DFT at every 64th frame (absolute index)
 constexpr int kPsWin = (kPsFft + kPsHop - 1) / kPsHop;  // 36 frames cover a sample
-constexpr int kPsChunk = 4;                            // output frames per bin reduction
+constexpr int kPsChunk = 2;                            // output frames per bin reduction
 constexpr int kPsTapMax = HBK_PITCH_SHIFT_MAX_TAPS;    // 2 width + orig (142 / 139 at 16 kHz)
 constexpr int kPsPhaseMax = 128;                       // new (resampler phases)
 constexpr int kPsResFrames = 32;                       // resampler frames per workgroup
@@ -1526,6 +1526,28 @@ __device__ __forceinline__ void ps_load_frames(const PitchArgs& a, const float* 
   __syncthreads();
 }
 
+// atan2 for the vocoder's angles: a degree-15 odd polynomial for atan on [0, 1]
+// (least-squares fit, max error 1.2e-7 rad in float32, as libm's atan2f) and
+// the octant reflections; atan2(0, 0) = 0 as in torch
+__device__ __forceinline__ float ps_atan2(float y, float x) {
+  const float ax = fabsf(x), ay = fabsf(y);
+  const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+  const float a = mx > 0.f ? mn * __builtin_amdgcn_rcpf(mx) : 0.f;
+  const float s = a * a;
+  float r = -0.004051558673381805f;
+  r = fmaf(r, s, 0.021852469071745872f);
+  r = fmaf(r, s, -0.05589785426855087f);
+  r = fmaf(r, s, 0.09641194343566895f);
+  r = fmaf(r, s, -0.1390826404094696f);
+  r = fmaf(r, s, 0.19946499168872833f);
+  r = fmaf(r, s, -0.33329856395721436f);
+  r = fmaf(r, s, 0.9999993443489075f);
+  r *= a;
+  r = ay > ax ? 1.5707963267948966f - r : r;
+  r = x < 0.f ? 3.141592653589793f - r : r;
+  return copysignf(r, y);
+}
+
 // a frame producer: (X, angle, |X|) of the current source frame c and of c + 1
 struct PsCursor {
   float cr, ci, ca, cm;  // frame c
@@ -1539,9 +1561,9 @@ struct PsCursor {
     nr = cr;
     ni = ci;
     F.next(c + 1, nr, ni);
-    ca = atan2f(ci, cr);
+    ca = ps_atan2(ci, cr);
     cm = sqrtf(cr * cr + ci * ci);
-    na = atan2f(ni, nr);
+    na = ps_atan2(ni, nr);
     nm = sqrtf(nr * nr + ni * ni);
   }
   __device__ __forceinline__ void advance_to(const PsFrames& F, int i0) {
@@ -1552,7 +1574,7 @@ struct PsCursor {
       ca = na;
       cm = nm;
       F.next(c + 1, nr, ni);
-      na = atan2f(ni, nr);
+      na = ps_atan2(ni, nr);
       nm = sqrtf(nr * nr + ni * ni);
     }
   }
@@ -1585,7 +1607,7 @@ __global__ void __launch_bounds__(128) ps_phase_sum_kernel(PitchArgs a) {
   a.osum[o] = k < kPsBins ? osum : 0.0;
 }
 
-__global__ void __launch_bounds__(128) ps_synth_kernel(PitchArgs a) {
+__global__ void __launch_bounds__(128, 4) ps_synth_kernel(PitchArgs a) {
   __shared__ float2 tw[kPsFft];
   __shared__ float cb[kPsChunk * kPsHop][kPsLd + 1];
   __shared__ float xs[kPsXs];
@@ -1653,12 +1675,13 @@ __global__ void __launch_bounds__(128) ps_synth_kernel(PitchArgs a) {
       if (t >= t_lo) {
         const float z35r = zq[0].x, z35i = zq[0].y;  // Z_{t-35}
         int q = qz;
+        const float cwr = ck * wr, cwi = ck * wi, cvr = ck * (wr - z35r), cvi = ck * (wi - z35i);
 #pragma unroll
         for (int r = 0; r < kPsHop; ++r) {
           // frames t-35 .. t cover p = 7 t + r for r <= 4, t-34 .. t for r = 5, 6
-          const float vr = r <= 4 ? wr : wr - z35r, vi = r <= 4 ? wi : wi - z35i;
+          const float vr = r <= 4 ? cwr : cvr, vi = r <= 4 ? cwi : cvi;
           const float2 w = tw[q];
-          cb[row * kPsHop + r][k] = ck * (w.x * vr - w.y * vi);
+          cb[row * kPsHop + r][k] = w.x * vr - w.y * vi;
           q += kq;
           q -= q >= kPsFft ? kPsFft : 0;
         }
