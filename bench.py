@@ -128,6 +128,16 @@ def roof(kernel, bound, work, ms, unit, traffic, peak=None, **extra):
     return d
 
 
+def prof_mark(tag, dev):
+    """hbk_profile_mark_kernel on the current stream, behind a device
+    synchronize (outside the timed region): rocprofv3 traces and counter
+    passes keep the dispatches between two marks (tools/prof_summary.py)."""
+    from heybuddy import _native
+    torch.cuda.synchronize(dev)
+    _native.check(_native.lib().hbk_profile_mark(tag, _native.stream_ptr(dev)), "hbk_profile_mark")
+    torch.cuda.synchronize(dev)
+
+
 def main():
     args = parse()
     CURRENT_CONFIG[0] = args.config
@@ -161,14 +171,17 @@ def main():
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(len(job["stages"]) + 1)] for _ in range(n_ev)]
     if staged:  # before the pipelined warmup, which leaves the next chunk's features pending
         staged(None)
+        prof_mark(3, dev)
         for k in range(n_ev):
             staged(evs[k])
         torch.cuda.synchronize(dev)
+        prof_mark(4, dev)
     for _ in range(args.warmup):
         job["step"](None)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
+    prof_mark(1, dev)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(args.steps):
@@ -177,6 +190,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    prof_mark(2, dev)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -672,48 +686,63 @@ def setup_e2e(args, dev, rank, world, seed):
                     us_per_train_step=round(ms * 1e3 / S, 2))
 
     def cpu_baseline(sample_n):
-        """The same pipeline on the host CPU (oracle/): placement + augment
-        (numpy fp64 noise mix + rfft reverb) + featurize (reference cost
-        structure, torch CPU fp32 convs) + the train steps of those clips
-        (numpy fp32 forward / backward / Adam at B = 1,100)."""
-        from oracle.augment import augment_batch
+        """The same pipeline on the host CPU (oracle/): placement, the
+        reference's whole augmentation chain (oracle.augment.augment_chain:
+        7-band EQ and tanh per clip; pitch shift, band-stop, colored noise,
+        gain, background noise and reverb per batch of 128, at the default
+        probabilities, each per-batch coin stratified so that the sample holds
+        round(p * batches) of each), featurize at the reference's cost
+        structure, then the train steps of exactly those clips (50 positives +
+        50 adversarials of the sample per step + 1,000 negatives, numpy fp32
+        forward / backward / Adam at B = 1,100)."""
+        from oracle.augment import augment_chain
         from oracle.featurizer import cpu_featurize
         from oracle import mlp as omlp
         from threadpoolctl import threadpool_limits
         gr = default_graph()
-        x_all = src[:n].cpu().numpy()
+        nb_cpu = [v.numpy() for v in noise_bank(64, seed=seed + 2)]
+        ir_cpu = [v.numpy() for v in impulse_responses(32, seed=seed + 3)]
         res = {}
-        for th, m in ((host_threads(), sample_n or 1500), (1, 150)):
-            xs = x_all[:m, :AUG_T]
+        for th, m in ((host_threads(), sample_n or 512), (1, 128)):
+            # half positives, half adversarials, as the step's clips
+            rows = np.concatenate([np.arange(m // 2), half + np.arange(m - m // 2)])
+            xs, ls = src[rows].cpu().numpy(), lens[rows]
             rng = np.random.default_rng(0)
             with threadpool_limits(limits=th):
-                cpu_featurize(xs[:4], gr, threads=th)
+                torch.set_num_threads(th)
+                cpu_featurize(xs[:4, :AUG_T], gr, threads=th)
                 t0 = time.perf_counter()
-                nz = rng.standard_normal((m, AUG_T)).astype(np.float32) * 0.1
-                ir = impulse_responses(1, seed=3)[0].numpy()
-                xa = augment_batch(xs, nz, rng.uniform(-10, 15, m), ir).astype(np.float32)
+                xa, counts = augment_chain(xs, ls, rng, nb_cpu, ir_cpu, stratify=True, fast_pitch=True)
                 emb = cpu_featurize(xa, gr, threads=th)
                 params = omlp.init_params(seed=0)
                 opt = omlp.Adam(params)
-                steps = max(1, m // (P + A))
-                negs = rng.standard_normal((B - P - A, 16, 96)).astype(np.float32)
+                steps = max(1, (m // 2) // P)
                 yy = np.concatenate([np.ones(P), np.zeros(B - P)]).astype(np.int64)
-                for s in range(steps):
-                    xb = np.concatenate([np.resize(emb, (P + A, 16, 96)), negs]).astype(np.float32)
+                for s_ in range(steps):
+                    pos_ = emb[s_ * P:(s_ + 1) * P]
+                    adv_ = emb[m // 2 + s_ * A:m // 2 + (s_ + 1) * A]
+                    negs = rng.standard_normal((B - P - A, 16, 96)).astype(np.float16).astype(np.float32)
+                    xb = np.concatenate([pos_, adv_, negs]).astype(np.float32)
                     prob, z, cache = omlp.forward(params, xb, dtype=np.float32)
                     loss, nsel, dz = omlp.step_loss_and_dz(prob, yy)
                     grads = omlp.backward(params, cache, dz, dtype=np.float32)
                     params = opt.step(params, grads, 1e-3)
                 el = time.perf_counter() - t0
-            res[th] = (m / el, m, el, steps)
+            res[th] = (m / el, m, el, steps, counts)
+        torch.set_num_threads(host_threads())
         th = host_threads()
-        v, m, el, steps = res[th]
+        v, m, el, steps, counts = res[th]
         return {"value": round(v, 2), "unit": "clips/s", "cores": th, "kind": "port",
                 "cpu_model": cpu_model(),
-                "sample": f"{m} of the step's clips through oracle/ (augment + featurize at the reference's "
-                          f"cost structure + {steps} train steps of B={B} incl. Adam), {el:.1f} s",
+                "sample": f"{m} of the step's clips through oracle/: placement + the full augmentation chain "
+                          f"(7-band EQ, tanh, pitch shift [float32 torch.stft/istft + phase vocoder + sinc "
+                          f"resample], band-stop, colored noise, gain, background noise, reverb; applied: "
+                          f"{counts}) + featurize at the reference's cost structure (4 x 105 mel frames, "
+                          f"16 windows per clip, batch 64) + {steps} train steps of B={B} on those clips' "
+                          f"embeddings incl. Adam, {el:.1f} s",
                 "value_1thread": round(res[1][0], 2),
-                "sample_1thread": f"{res[1][1]} clips + {res[1][3]} train steps, {res[1][2]:.1f} s"}
+                "sample_1thread": f"{res[1][1]} clips (same chain, {res[1][4]}) + {res[1][3]} train steps, "
+                                  f"{res[1][2]:.1f} s"}
 
     def extra_rooflines():
         """Untimed, after the measurement: the embedding on the generic

@@ -862,6 +862,7 @@ struct ColoredArgs {
   const float* white;     // [n_clips, white_stride >= 16000] N(0,1) or NULL (generated from seed)
   int64_t white_stride;
   uint64_t seed;
+  int64_t group;          // clips per white-noise vector (per_batch: the batch size)
   const float* f_decay;   // per clip
   const float* snr_db;    // per clip
   float lin_step;         // (sqrt(8000) - 1) / 8000: linspace step over the 8001 bins
@@ -1019,12 +1020,13 @@ __global__ void __launch_bounds__(kThreads) colored_noise_kernel(ColoredArgs a) 
       continue;
     }
     // 1) one second of white noise -> LDS (the previous clip's readers finished at its last barrier)
+    const int64_t grp = clip / a.group;  // clips of one batch share the noise vector (per_batch)
     if (a.white) {
-      const float* w = a.white + clip * a.white_stride;
+      const float* w = a.white + grp * a.white_stride;
       for (int s = tid; s < kN1; s += kThreads) zf[s] = w[s];
     } else {
       for (int q = tid; q < kN1 / 2; q += kThreads) {
-        const float2 g = gauss2(a.seed, static_cast<uint64_t>(clip) * (kN1 / 2) + q);
+        const float2 g = gauss2(a.seed, static_cast<uint64_t>(grp) * (kN1 / 2) + q);
         *reinterpret_cast<float2*>(zf + 2 * q) = g;
       }
     }
@@ -1918,9 +1920,9 @@ int hbk_augment(const hbk_reverb_plan* p, const float* x, int64_t n_clips, int64
 }
 
 int hbk_colored_noise(const hbk_reverb_plan* p, const float* x, int64_t n_clips, int64_t x_stride,
-                      const float* white, int64_t white_stride, uint64_t seed, const float* f_decay,
-                      const float* snr_db, float sample_rate, const int32_t* idx, int64_t n_entries, float* out,
-                      int64_t out_stride, void* stream) {
+                      const float* white, int64_t white_stride, uint64_t seed, int64_t clips_per_noise,
+                      const float* f_decay, const float* snr_db, float sample_rate, const int32_t* idx,
+                      int64_t n_entries, float* out, int64_t out_stride, void* stream) {
   using namespace hbk;
   if (!p) return arg_error("plan is NULL");
   if (n_clips < 0) return arg_error("negative n_clips");
@@ -1928,6 +1930,7 @@ int hbk_colored_noise(const hbk_reverb_plan* p, const float* x, int64_t n_clips,
   if (!x || !out || !f_decay || !snr_db) return arg_error("NULL pointer");
   if (x_stride < kT || out_stride < kT) return arg_error("stride < 23040");
   if (white && white_stride < kN1) return arg_error("white_stride < 16000");
+  if (clips_per_noise < 1) return arg_error("clips_per_noise < 1");
   if (sample_rate != float(kN1)) {
     set_error("hbk: colored noise is generated at 16 kHz (one second = 16000 samples), got %g", double(sample_rate));
     return HBK_ERR_UNSUPPORTED;
@@ -1941,6 +1944,7 @@ int hbk_colored_noise(const hbk_reverb_plan* p, const float* x, int64_t n_clips,
   a.white = white;
   a.white_stride = white_stride;
   a.seed = seed;
+  a.group = clips_per_noise;
   a.f_decay = f_decay;
   a.snr_db = snr_db;
   a.lin_step = static_cast<float>((std::sqrt(double(kN1) / 2.0) - 1.0) / double(kM1));

@@ -44,6 +44,11 @@ int64_t persistent_blocks(int blocks_per_cu, const void* stream) {
   return int64_t(cus) * blocks_per_cu;
 }
 
+__device__ int32_t g_profile_mark[64];
+
+// One wave; the store keeps the launch from being optimised into nothing.
+__global__ void hbk_profile_mark_kernel(int32_t tag) { g_profile_mark[threadIdx.x] = tag; }
+
 }  // namespace hbk
 
 extern "C" {
@@ -72,6 +77,12 @@ int hbk_stream_create_cu_mask(const uint32_t* cu_mask, int n_words, void** strea
   hipError_t e = hipExtStreamCreateWithCUMask(&s, static_cast<uint32_t>(n_words), cu_mask);
   if (e != hipSuccess) return hbk::hip_error(e, "hipExtStreamCreateWithCUMask");
   *stream = s;
+  return HBK_OK;
+}
+
+int hbk_profile_mark(int32_t tag, void* stream) {
+  hipLaunchKernelGGL(hbk::hbk_profile_mark_kernel, dim3(1), dim3(64), 0, hbk::as_stream(stream), tag);
+  HBK_LAUNCH_CHECK("hbk_profile_mark_kernel");
   return HBK_OK;
 }
 

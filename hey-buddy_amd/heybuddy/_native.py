@@ -49,6 +49,7 @@ _PROTOS = {
     "hbk_device_count": (_c_int, [ctypes.POINTER(_c_int)]),
     "hbk_stream_create_cu_mask": (_c_int, [_vp, _c_int, ctypes.POINTER(_vp)]),
     "hbk_stream_destroy": (_c_int, [_vp]),
+    "hbk_profile_mark": (_c_int, [ctypes.c_int32, _vp]),
     "hbk_mel_plan_create": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int, _c_float, _c_float,
                                      _c_float, _c_float, ctypes.POINTER(_vp)]),
     "hbk_mel_plan_destroy": (_c_int, [_vp]),
@@ -72,8 +73,8 @@ _PROTOS = {
     "hbk_reverb_spectrum": (_c_int, [_vp, _vp, _c_int64, _c_int64, _vp, _vp]),
     "hbk_augment": (_c_int, [_vp, _vp, _c_int64, _c_int64, _vp, _c_int64, _vp, _vp, _vp, _vp, _vp,
                              _vp, _c_int64, _vp]),
-    "hbk_colored_noise": (_c_int, [_vp, _vp, _c_int64, _c_int64, _vp, _c_int64, ctypes.c_uint64, _vp, _vp,
-                                   _c_float, _vp, _c_int64, _vp, _c_int64, _vp]),
+    "hbk_colored_noise": (_c_int, [_vp, _vp, _c_int64, _c_int64, _vp, _c_int64, ctypes.c_uint64, _c_int64, _vp,
+                                   _vp, _c_float, _vp, _c_int64, _vp, _c_int64, _vp]),
     "hbk_tanh_distortion": (_c_int, [_vp, _c_int64, _c_int64, _vp, _vp, _c_int64, _vp, _c_int64, _vp]),
     "hbk_band_stop_workspace_size": (_c_int64, [_c_int64, ctypes.c_int32, ctypes.c_int32, _vp]),
     "hbk_band_stop": (_c_int, [_vp, _vp, _c_int64, _c_int64, _vp, _vp, ctypes.c_int32, _vp, _vp, _vp, _vp,

@@ -15,9 +15,12 @@ Semantics kept from the reference:
   applied before the noise mix (it is the last transform of augment_batch);
 * colored noise: torch_audiomentations AddColoredNoise in per_batch mode
   (:107-113), before the gain: per batch with probability colored_noise_prob
-  (0.25) one snr ~ U[10, 30] dB and one f_decay ~ U[-1, 2] (per_batch draws
-  one parameter set, as for the gain); white noise per clip from the kernel's
-  counter-based normal stream (seeded from numpy's global RNG);
+  (0.25) one snr ~ U[10, 30] dB and one f_decay ~ U[-1, 2]; torch_audiomentations
+  runs a per_batch transform on the batch reshaped to (1, batch * channels, T)
+  (BaseWaveformTransform.forward), so ONE parameter set and ONE noise vector
+  serve the whole batch, scaled per clip by its own rms; the white noise comes
+  from the kernel's counter-based normal stream (seeded from numpy's global RNG),
+  one vector per batch;
 * seven-band EQ: audiomentations SevenBandParametricEQ, per CLIP with
   probability seven_band_prob (0.25), gains ~ U[-6, 6] dB (:79-84): first in the
   per-clip Compose; the per-clip filter parameters (center mel-uniform in each
@@ -359,7 +362,8 @@ class BatchAugmenter:
             x = self.plan.band_stop(out, *pr["bandstop"], out=out)
         if pr["colored"] is not None:  # colored noise precedes the gain (augmented.py:107-118)
             fd, csnr, seed = pr["colored"]
-            x = self.plan.colored_noise(x, fd, csnr, seed=seed, out=out, sample_rate=self.sample_rate)
+            x = self.plan.colored_noise(x, fd, csnr, seed=seed, out=out, sample_rate=self.sample_rate,
+                                        clips_per_noise=self.batch_size)
             out = x
         return self.plan.augment(x, self.ring, pr["noise_off"], pr["snr"], self.spectra, pr["spec_idx"],
                                  out=out, gain=pr["gain"])

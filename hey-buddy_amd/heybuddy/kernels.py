@@ -815,19 +815,24 @@ class ReverbPlan:
 
     def colored_noise(self, x: torch.Tensor, f_decay: torch.Tensor, snr_db: torch.Tensor,
                       white: torch.Tensor | None = None, seed: int = 0, out: torch.Tensor | None = None,
-                      sample_rate: int = 16000) -> torch.Tensor:
+                      sample_rate: int = 16000, clips_per_noise: int = 1) -> torch.Tensor:
         """torch_audiomentations AddColoredNoise on x [n, >= T] -> out [n, T]
         (hbk_colored_noise): per clip f_decay and snr (dB; NaN leaves the clip
-        unchanged); one second of white noise per clip ([n, >= 16000] N(0,1))
-        if given, else the kernel's counter-based stream from ``seed``; the
-        coloured second is tiled to T as _gen_noise does."""
+        unchanged); one second of white noise per group of ``clips_per_noise``
+        consecutive clips (per_batch mode shares one vector across the batch;
+        [ceil(n / clips_per_noise), >= 16000] N(0,1)) if given, else the
+        kernel's counter-based stream from ``seed``; the coloured second is
+        tiled to T as _gen_noise does."""
         n = x.shape[0]
         if x.dim() != 2 or x.shape[1] < self.T or x.stride(1) != 1 or x.device != self.device:
             raise ValueError(f"x must be [n, >= {self.T}] f32 rows on {self.device}")
-        if white is not None and (white.dim() != 2 or white.shape[0] != n or white.shape[1] < 16000
+        groups = (n + clips_per_noise - 1) // max(1, clips_per_noise)
+        if clips_per_noise < 1:
+            raise ValueError("clips_per_noise must be >= 1")
+        if white is not None and (white.dim() != 2 or white.shape[0] != groups or white.shape[1] < 16000
                                   or white.stride(1) != 1 or white.device != self.device
                                   or white.dtype != torch.float32):
-            raise ValueError(f"white must be [n, >= 16000] f32 rows on {self.device}")
+            raise ValueError(f"white must be [{groups}, >= 16000] f32 rows on {self.device}")
         if out is None:
             out = torch.empty((n, self.T), dtype=torch.float32, device=self.device)
 
@@ -851,7 +856,7 @@ class ReverbPlan:
             return t.pin_memory().to(self.device, non_blocking=True) if t.device.type == "cpu" else t.to(self.device)
 
         torch.ops.hbk.colored_noise_(x, white, to_dev(f_decay), to_dev(snr_db), _u64_to_i64(seed),
-                                     float(sample_rate), rows, out, self.id)
+                                     int(clips_per_noise), float(sample_rate), rows, out, self.id)
         return out
 
     def band_stop(self, x: torch.Tensor, idx: torch.Tensor, cut_lo: torch.Tensor, cut_hi: torch.Tensor,
@@ -930,12 +935,13 @@ def _augment_op(x: torch.Tensor, ring: torch.Tensor | None, noise_off: torch.Ten
 
 @torch.library.custom_op("hbk::colored_noise_", mutates_args=("out",))
 def _colored_noise_op(x: torch.Tensor, white: torch.Tensor | None, f_decay: torch.Tensor, snr_db: torch.Tensor,
-                      seed: int, sample_rate: float, rows: torch.Tensor | None, out: torch.Tensor,
-                      plan_id: int) -> None:
+                      seed: int, clips_per_noise: int, sample_rate: float, rows: torch.Tensor | None,
+                      out: torch.Tensor, plan_id: int) -> None:
     plan = _plans[plan_id]
     check(lib().hbk_colored_noise(plan._handle, ptr(x), x.shape[0], x.stride(0),
                                   ptr(white) if white is not None else None,
-                                  white.stride(0) if white is not None else 0, seed & (2 ** 64 - 1), ptr(f_decay),
+                                  white.stride(0) if white is not None else 0, seed & (2 ** 64 - 1),
+                                  clips_per_noise, ptr(f_decay),
                                   ptr(snr_db), sample_rate, ptr(rows) if rows is not None else None,
                                   rows.numel() if rows is not None else 0, ptr(out), out.stride(0),
                                   stream_ptr(x.device)), "hbk_colored_noise")

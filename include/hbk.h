@@ -45,6 +45,14 @@ int hbk_device_count(int* count);
 int hbk_stream_create_cu_mask(const uint32_t* cu_mask, int n_words, void** stream);
 int hbk_stream_destroy(void* stream);
 
+/* Profiling marker (no reference counterpart): enqueues hbk_profile_mark_kernel,
+ * a one-wave kernel that stores `tag`, on `stream`. bench.py brackets its timed
+ * region with tags 1 / 2 (and its sequential stage-timing steps with 3 / 4),
+ * each behind a device synchronize, so a rocprofv3 kernel trace or counter pass
+ * can keep exactly the dispatches that fall between two markers
+ * (tools/prof_summary.py). */
+int hbk_profile_mark(int32_t tag, void* stream);
+
 /* ------------------------------------------------------------------------ *
  * Mel spectrogram (STFT -> |.|^2 -> mel filterbank -> 10 log10 -> x/10 + 2)
  *
@@ -310,10 +318,13 @@ int hbk_augment(const hbk_reverb_plan* plan, const float* x, int64_t n_clips, in
 /* Colored noise: torch_audiomentations AddColoredNoise, which the reference's
  * batch chain applies per batch with p 0.25 (dataset/augmented.py:107-113,
  * constants.py:128-132). Per clip i of x [n_clips, x_stride] (first T = 23040
- * samples used), the package's _gen_noise / apply_transform:
- *   w = white[i][0 .. 16000) (N(0,1), white_stride >= 16000) or, if white ==
- *       NULL, the counter-based N(0,1) stream: samples 2q, 2q + 1 of clip i are the
- *       Box-Muller pair of hash (seed, i * 8000 + q);
+ * samples used), the package's _gen_noise / apply_transform, with the white
+ * noise shared by each group of clips_per_noise consecutive clips, g = i /
+ * clips_per_noise (per_batch mode runs the transform on the batch reshaped to
+ * (1, batch, T): one noise vector for the whole batch; 1 = a vector per clip):
+ *   w = white[g][0 .. 16000) (N(0,1), white_stride >= 16000) or, if white ==
+ *       NULL, the counter-based N(0,1) stream: samples 2q, 2q + 1 of group g are
+ *       the Box-Muller pair of hash (seed, g * 8000 + q);
  *   n1 = irfft(rfft(w) / linspace(1, sqrt(8000), 8001)^f_decay[i], n = 16000);
  *   n1 /= rms(n1) + 1e-8;  noise[t] = n1[t mod 16000] (tiled to T, not renormalised);
  *   out[i] = x[i] + rms(x[i]) / 10^(snr_db[i] / 20) * noise;
@@ -321,9 +332,9 @@ int hbk_augment(const hbk_reverb_plan* plan, const float* x, int64_t n_clips, in
  * sample_rate must be 16000 (the noise is one second long). out may equal x.
  * Device pointers. */
 int hbk_colored_noise(const hbk_reverb_plan* plan, const float* x, int64_t n_clips, int64_t x_stride,
-                      const float* white, int64_t white_stride, uint64_t seed, const float* f_decay,
-                      const float* snr_db, float sample_rate, const int32_t* idx, int64_t n_entries, float* out,
-                      int64_t out_stride, void* stream);
+                      const float* white, int64_t white_stride, uint64_t seed, int64_t clips_per_noise,
+                      const float* f_decay, const float* snr_db, float sample_rate, const int32_t* idx,
+                      int64_t n_entries, float* out, int64_t out_stride, void* stream);
 
 /* Band-stop: torch_audiomentations BandStopFilter, which the reference applies
  * in its batch chain with p 0.25 per batch, one parameter set per batch

@@ -26,7 +26,11 @@ their published algorithms at the versions environment.yml pins
       y = a_in * y / (mean |y| + 1e-14)
 * torch_audiomentations.AddColoredNoise (min/max SNR 10/30 dB, f_decay -1..2,
   mode per_batch, p 0.25; augmented.py:107-113, constants.py:128-132), between
-  band-stop and gain in the batch chain. Per clip (snr and f_decay per example):
+  band-stop and gain in the batch chain. per_batch mode: torch_audiomentations'
+  BaseWaveformTransform.forward reshapes the batch to (1, batch * channels, T)
+  before randomize_parameters / apply_transform, so ONE (snr, f_decay) and ONE
+  noise vector serve the whole batch (the same holds for Gain, BandStopFilter
+  and PitchShift: one parameter set per batch); rms(x) stays per clip:
       w ~ N(0, 1) [T];  S = rfft(w) / linspace(1, sqrt(sr / 2), T/2 + 1)^f_decay
       n = irfft(S);  n = n / (rms(n) + 1e-8)                 (Audio.rms_normalize)
       y = x + rms(x) / 10^(snr / 20) * n                     (calculate_rms)
@@ -47,9 +51,10 @@ their published algorithms at the versions environment.yml pins
   (the band ranges, Q range and draw distributions are restated from the
   package's documentation: PARITY UNPINNED, no fixture exists).
 * torch_audiomentations.BandStopFilter (torch_audiomentations >= 0.11,
-  environment.yml:27; p 0.25, mode per_batch: one coin per batch, parameters
-  per clip; augmented.py:101-105, constants.py:127), second in the batch chain
-  (after PitchShift, before AddColoredNoise). Per clip: center frequency
+  environment.yml:27; p 0.25, mode per_batch: one coin AND one parameter set
+  per batch (the (1, batch * channels, T) reshape above); augmented.py:101-105,
+  constants.py:127), second in the batch chain (after PitchShift, before
+  AddColoredNoise). Per batch: center frequency
   mel-uniform in [200, 4000] Hz, bandwidth fraction ~ U[0.5, 1.99],
       cut_lo = f_c (1 - bw/2) / sr,  cut_hi = f_c (1 + bw/2) / sr   (float32)
   and y = x - julius.bandpass_filter(x, cut_lo, cut_hi) with julius's
@@ -416,3 +421,124 @@ def pitch_shift(x, num: int, den: int, sample_rate: int = 16000) -> np.ndarray:
     m = min(L, res.shape[1])
     out[:, :m] = res[:, :m]
     return out
+
+
+def pitch_shift_torch(x, num: int, den: int, sample_rate: int = 16000) -> np.ndarray:
+    """pitch_shift in float32 torch CPU ops, as the reference's packages run it
+    (torch.stft / torch.istft, torchaudio's phase_vocoder and Resample written
+    out): the timed CPU baseline's pitch shift (bench.py config 5); the float64
+    pitch_shift above stays the parity oracle."""
+    import math
+    import torch
+    import torch.nn.functional as F
+    x = torch.as_tensor(np.atleast_2d(np.asarray(x, dtype=np.float32)))
+    n, L = x.shape
+    g = pitch_shift_geometry(L, num, den, sample_rate)
+    n_fft, hop = g["n_fft"], g["hop"]
+    X = torch.stft(x, n_fft, hop, window=torch.ones(n_fft), center=True, pad_mode="reflect",
+                   return_complex=True)  # [n, nb, f_in]; torch_pitch_shift passes no window: rectangular
+    nb = X.shape[1]
+    adv = torch.linspace(0, math.pi * hop, nb)[:, None]
+    ts = torch.arange(0, X.shape[-1], g["rate"], dtype=torch.float32)
+    alpha = ts % 1.0
+    ph0 = X[..., :1].angle()
+    Xp = F.pad(X, [0, 2])
+    X0, X1 = Xp.index_select(-1, ts.long()), Xp.index_select(-1, (ts + 1).long())
+    ph = X1.angle() - X0.angle() - adv
+    ph = ph - 2 * math.pi * torch.round(ph / (2 * math.pi)) + adv
+    acc = torch.cumsum(torch.cat([ph0, ph[..., :-1]], -1), -1)
+    Y = torch.polar(alpha * X1.abs() + (1 - alpha) * X0.abs(), acc)
+    y = torch.istft(Y, n_fft, hop, window=torch.ones(n_fft), center=True)
+    taps, w = resample_taps(g["orig"], g["new"])
+    orig = g["orig"]
+    yp = F.pad(y[:, None], (w, w + orig))
+    res = F.conv1d(yp, torch.from_numpy(taps)[:, None], stride=orig).transpose(1, 2).reshape(n, -1)[:, :g["target"]]
+    out = torch.zeros((n, L))
+    m = min(L, res.shape[1])
+    out[:, :m] = res[:, :m]
+    return out.numpy()
+
+
+# --------------------------------------------------------------------------
+# The whole chain of AugmentedAudioGenerator.execute_augment_batch
+# (augmented.py:297-394), used as bench.py's CPU baseline (config 5) and by
+# tests: placement (to_target_length, :200-232), per clip [7-band EQ p .25,
+# tanh p .25] (:79-90, :314-328), per batch [pitch shift p .25, band-stop
+# p .25, colored noise p .25, gain p 1.0] (:93-121, :368-380), background
+# noise p .75 (:383-384), reverb p .75 (:386-392).
+def place(clip, length: int, T: int, rng) -> np.ndarray:
+    """to_target_length: crop to T, or pad with U[S/4, 3S/4) leading zeros."""
+    x = np.asarray(clip[:length], dtype=np.float32)
+    if length >= T:
+        return x[:T].copy()
+    out = np.zeros(T, np.float32)
+    s = T - length
+    pre = int(rng.integers(s // 4, max(s // 4 + 1, 3 * s // 4)))
+    out[pre:pre + length] = x
+    return out
+
+
+def augment_chain(src, lengths, rng, noise_bank, irs, T: int = 23040, batch: int = 128,
+                  p_eq=0.25, p_tanh=0.25, p_pitch=0.25, p_bandstop=0.25, p_colored=0.25, p_gain=1.0,
+                  p_noise=0.75, p_reverb=0.75, stratify: bool = False, fast_pitch: bool = False):
+    """src [n, >= T] utterances with valid lengths -> augmented [n, T] float32.
+    Per-batch coins from ``rng``; stratify=True turns each per-batch coin into
+    exactly round(p * n_batches) batches (a random subset), so a small sample
+    carries the chain's expected cost; fast_pitch: the float32 torch pitch
+    shift (the reference's own cost) instead of the float64 restatement.
+    Returns (y, counts of applied stages)."""
+    n = len(src)
+    x = np.stack([place(src[i], int(lengths[i]), T, rng) for i in range(n)])
+    cnt = {}
+    e_on = rng.random(n) < p_eq
+    if e_on.any():
+        sos = np.full((n, 7, 6), np.nan)
+        sos[e_on] = eq_sos(eq_draw(rng, int(e_on.sum()), 6.0))
+        x = seven_band_eq(x, sos)
+    t_on = rng.random(n) < p_tanh
+    for i in np.flatnonzero(t_on):
+        x[i] = tanh_distortion(x[i:i + 1], rng.uniform(1e-4, 0.1))[0]
+    cnt["eq_clips"], cnt["tanh_clips"] = int(e_on.sum()), int(t_on.sum())
+    nb = (n + batch - 1) // batch
+
+    def coins(p):
+        if stratify:
+            on = np.zeros(nb, bool)
+            on[rng.permutation(nb)[:int(round(p * nb))]] = True
+            return on
+        return rng.random(nb) < p
+
+    c_pitch, c_bs, c_col, c_gain, c_noise, c_rev = (coins(p) for p in (p_pitch, p_bandstop, p_colored, p_gain,
+                                                                       p_noise, p_reverb))
+    ring = np.concatenate([np.asarray(v, np.float32) for v in noise_bank])
+    ring_pos = 0
+    shifts = ((125, 128), (128, 125))
+    for b in range(nb):
+        sl = slice(b * batch, min(n, (b + 1) * batch))
+        y = x[sl].astype(np.float64)
+        m = y.shape[0]
+        if c_pitch[b]:
+            num, den = shifts[int(rng.integers(0, 2))]
+            for s in range(0, m, 32):
+                y[s:s + 32] = (pitch_shift_torch if fast_pitch else pitch_shift)(y[s:s + 32], num, den)
+        if c_bs[b]:
+            lo, hi = bandstop_draw(rng, 1)
+            y = band_stop(y.astype(np.float32), np.repeat(lo, m), np.repeat(hi, m)).astype(np.float64)
+        if c_col[b]:
+            w = np.repeat(rng.standard_normal((1, 16000)), m, axis=0)
+            y = colored_noise(y, w, np.full(m, rng.uniform(-1, 2)), np.full(m, rng.uniform(10, 30)))
+        gain = db_to_amplitude(np.full(m, rng.uniform(-18, 6))) if c_gain[b] else None
+        noise = snr = ir = None
+        if c_noise[b]:
+            idx = (ring_pos + np.arange(m * T)) % ring.size
+            noise = ring[idx].reshape(m, T)
+            ring_pos = (ring_pos + m * T) % ring.size
+            snr = rng.uniform(-10, 15, m)
+        if c_rev[b]:
+            ir = np.asarray(irs[b % len(irs)], np.float64)
+        x[sl] = augment_batch(y, noise, snr, ir, gain=gain).astype(np.float32)
+    for k, v in (("pitch", c_pitch), ("bandstop", c_bs), ("colored", c_col), ("gain", c_gain),
+                 ("noise", c_noise), ("reverb", c_rev)):
+        cnt[k + "_batches"] = int(v.sum())
+    cnt["batches"] = nb
+    return x, cnt

@@ -313,6 +313,13 @@ def test_colored_noise_parity():
     # the added noise repeats with the 16,000-sample period of torch_audiomentations' one-second noise
     d = out - x.astype(np.float32)
     np.testing.assert_allclose(d[:, N1:], d[:, :T - N1], rtol=0, atol=2e-6 * np.abs(d).max())
+    # per_batch sharing: clips_per_noise = 2 -> groups {0, 1}, {2, 3}, {4} read white rows 0, 1, 2
+    out2 = plan.colored_noise(torch.from_numpy(x).float().cuda(), torch.from_numpy(fd), torch.from_numpy(snr),
+                              white=torch.from_numpy(w[:3]).cuda(), clips_per_noise=2).cpu().numpy()
+    ref2 = oaug.colored_noise(x.astype(np.float32), w[[0, 0, 1, 1, 2]], fd, snr)
+    for i in range(5):
+        ok, worst = _close(out2[i], ref2[i])
+        assert ok, f"shared noise, clip {i}: max |diff| {worst}"
 
 
 @pytest.mark.gpu
@@ -343,7 +350,9 @@ def test_colored_noise_nan_snr_skips_and_generated_stream():
 
 @pytest.mark.gpu
 def test_batch_augmenter_colored_noise_is_per_batch():
-    """mode="per_batch": one (snr, f_decay) per batch of 128; snr in [10, 30] dB."""
+    """mode="per_batch": one (snr, f_decay) AND one noise vector per batch of 128
+    (torch_audiomentations runs the transform on the batch reshaped to
+    (1, batch, T)); snr in [10, 30] dB."""
     from heybuddy.dataset.augmented import BatchAugmenter
     x = torch.from_numpy(_clips(300, seed=25)).float().cuda()
     np.random.seed(6)
@@ -358,6 +367,11 @@ def test_batch_augmenter_colored_noise_is_per_batch():
         blk = snr[b0:b0 + 128]
         assert blk.max() - blk.min() < 1e-3
         assert 10.0 - 1e-3 <= blk[0] <= 30.0 + 1e-3
+        # the normalised noise is the same vector for every clip of the batch
+        z = (os_ - xs)[b0:b0 + 128]
+        z = z / rms(z)[:, None]
+        np.testing.assert_allclose(z, np.broadcast_to(z[:1], z.shape), rtol=0, atol=1e-4 * np.abs(z).max())
+    assert not np.allclose((os_ - xs)[0] / rms(os_ - xs)[0], (os_ - xs)[128] / rms(os_ - xs)[128])
     off = BatchAugmenter(device=0, background_noise_prob=0.0, reverb_prob=0.0, gain_prob=0.0,
                          colored_noise_prob=0.0, tanh_distortion_prob=0.0, seven_band_prob=0.0,
                          band_stop_prob=0.0, pitch_shift_prob=0.0)
