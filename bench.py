@@ -80,6 +80,10 @@ def parse():
                          "train chunk s while chunk s + 1 is featurized on a second stream "
                          "(heybuddy.pipeline policies: off, prio, split:N, spill:N; N a multiple of 32, "
                          "i.e. whole CUs of every shader engine of every XCD)")
+    ap.add_argument("--train-batch", choices=("per-rank", "global"), default="per-rank",
+                    help="config 5 at N > 1: the reference's batch of 1,100 per rank (weak: global batch "
+                         "1,100 N, 1,000 steps per rank) or split over the ranks (global batch 1,100, "
+                         "N x 1,000 steps per rank)")
     ap.add_argument("--stage-steps", type=int, default=2,
                     help="overlapped runs: sequential (untimed) steps that time the stages for the rooflines")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
@@ -138,11 +142,30 @@ def prof_mark(tag, dev):
     torch.cuda.synchronize(dev)
 
 
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` run directly (no WORLD_SIZE in the environment):
+    start N ranks under torch.distributed.run as a CHILD process and return
+    its exit code. Nothing here touches the GPU (torch is imported, no HIP
+    call is made), so the ranks own their devices from the start."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
     CURRENT_CONFIG[0] = args.config
     if args.config == 1:
         return cpu_mel_only(args)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -534,6 +557,13 @@ def setup_e2e(args, dev, rank, world, seed):
     P, A, NL, NM = 50, 50, 666, 334
     B = P + A + NL + NM
     S = half // P
+    if args.train_batch == "global" and world > 1:
+        # the reference's batch of 1,100 is the GLOBAL batch: each rank takes a
+        # class-stratified stride-world share of it; all ranks' clips are trained on once on average
+        # over world x 1,000 global steps (each rank's positives / adversarials permuted with wrap)
+        P, A, NL, NM = (len(range(rank, k, world)) for k in (50, 50, 666, 334))
+        B = P + A + NL + NM
+        S = (half * world) // 50
     idx = torch.empty((S, B), dtype=torch.int32, device=dev)
     y = torch.cat([torch.ones(P), torch.zeros(B - P)]).to(dev)
     tr = WakeWordTrainer(checkpoint_dir="/tmp/hb_bench_ck", device=dev)
@@ -550,8 +580,10 @@ def setup_e2e(args, dev, rank, world, seed):
         """Device-side sampler: every featurized clip once (a fresh permutation
         of the step's positives and adversarials), negatives walked through a
         permutation of each pool with wrap-around."""
-        idx[:, :P] = torch.randperm(half, device=dev, dtype=torch.int32)[:S * P].view(S, P)
-        idx[:, P:P + A] = half + torch.randperm(n - half, device=dev, dtype=torch.int32)[:S * A].view(S, A)
+        k = torch.arange(S * P, device=dev) % half
+        idx[:, :P] = torch.randperm(half, device=dev, dtype=torch.int32)[k].view(S, P)
+        k = torch.arange(S * A, device=dev) % (n - half)
+        idx[:, P:P + A] = half + torch.randperm(n - half, device=dev, dtype=torch.int32)[k].view(S, A)
         o = neg_pos[0]
         k = torch.arange(S * NL, device=dev, dtype=torch.int64)
         idx[:, P + A:P + A + NL] = (-1 - ((o + k) % n_large)).to(torch.int32).view(S, NL)
@@ -808,6 +840,9 @@ def setup_e2e(args, dev, rank, world, seed):
                                "noise, gain, background noise, reverb) -> mel -> embed -> %d train steps (B=%d: 50 pos "
                                "+ 50 adv of the step's clips + 1000 f16 negatives)" % (args.pitch_prob, S, B),
                    "clips_per_rank": n, "train_steps_per_rank": S, "train_batch_per_rank": B,
+                   "train_batch_mode": ("global: the reference's 1,100 split over the ranks" if
+                                        args.train_batch == "global" and world > 1 else
+                                        "per-rank: 1,100 per rank (global batch 1,100 x N)"),
                    "negative_pool": f"{n_neg} x [16,96] f16",
                    "parallelism": f"dp{world} (clip shards; 1 all-reduce of the 1,025,700-B bucket per train step)",
                    "schedule": ("sequential: featurize(s) then train(s)" if args.overlap == "off" else

@@ -14,6 +14,7 @@ backend "nccl" = RCCL over xGMI on the MI355X box, "gloo" in CPU tests).
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -39,8 +40,27 @@ def shard_batch(x: torch.Tensor, y: torch.Tensor, rank: int, world_size: int):
     return x[rank::world_size], y[rank::world_size]
 
 
+def force_reduce() -> bool:
+    """HBK_DP_REDUCE_ALWAYS=1: run the bucket all-reduce even on a one-rank
+    group (a single-GPU check that the RCCL call captures into the train
+    step's hipGraph and replays; the sum over one rank is the identity)."""
+    return os.environ.get("HBK_DP_REDUCE_ALWAYS") == "1" and dist.is_available() and dist.is_initialized()
+
+
+def graph_capturable(world_size: int) -> bool:
+    """Can the train step's all-reduce be captured into its hipGraph? RCCL
+    (backend "nccl") collectives can be stream-captured; gloo stages through
+    the host and cannot. HBK_DP_GRAPHS=0 forces the eager per-step path."""
+    if world_size == 1 and not force_reduce():
+        return True
+    if os.environ.get("HBK_DP_GRAPHS", "1") == "0":
+        return False
+    return dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl"
+
+
 def reduce_bucket(bucket: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
-    """Sum the gradient + statistics bucket over the data-parallel ranks."""
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+    """Sum the gradient + statistics bucket over the data-parallel ranks (one
+    all-reduce of the 1,025,700-B bucket; capturable into a hipGraph on RCCL)."""
+    if dist.is_available() and dist.is_initialized() and (dist.get_world_size(group) > 1 or force_reduce()):
         dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=group)
     return bucket

@@ -8,7 +8,8 @@ step is the fused HIP train step of libhbk.so:
 
   hbk_mlp_train_fwd_bwd  forward (+ input dropout), high-loss filter, weighted
                          BCE, backward -> gradient bucket + statistics
-  all_reduce(bucket)     RCCL, only when torch.distributed is initialised:
+  all_reduce(bucket)     RCCL, only when torch.distributed is initialised
+                         (captured into the step's hipGraph on RCCL):
                          every rank trains on a 1/world slice of each batch
   hbk_mlp_gate_adam      the reference's < 128-sample accumulation gate on the
                          global statistics, then Adam iff it fires
@@ -281,7 +282,7 @@ class WakeWordTrainer(Trainer):
         flat = self.model.flat_parameters
         B = int(x.shape[0])
         key = (B, self._parity, float(threshold), float(activation_threshold), float(p), world,
-               None if history is None else (history.data_ptr(), history.shape[0]))
+               None if history is None else (history.data_ptr(), history.shape[0]), self._state_ptrs())
         g = self._graphs.get(key)
         if g is None:
             self._evict_graphs()
@@ -304,10 +305,11 @@ class WakeWordTrainer(Trainer):
 
             graphs = []
             with torch.cuda.stream(side):
-                if world == 1:
+                if distributed.graph_capturable(world):  # one graph per step, the RCCL all-reduce inside
                     gr = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(gr, stream=side):
                         fwd()
+                        distributed.reduce_bucket(self._bucket)
                         upd()
                     graphs.append(gr)
                 else:
@@ -378,6 +380,7 @@ class WakeWordTrainer(Trainer):
             done = 1
         k = max(2, steps_per_graph - steps_per_graph % 2)
         ptrs = tuple(t.data_ptr() if t is not None else 0 for t in (idx, y, sched, p32, p16, history, ws))
+        ptrs += self._state_ptrs()
 
         def graph_of(n: int) -> "torch.cuda.CUDAGraph":
             """The captured graph of n (even) steps from the current parity."""
@@ -399,10 +402,11 @@ class WakeWordTrainer(Trainer):
             self._graphs[key] = (gr, ws, keep)  # the entry keeps the baked-in workspace alive
             return gr
 
-        if graphs and world == 1 and S - done >= 2:
+        if graphs and distributed.graph_capturable(world) and S - done >= 2:
             # k-step graphs, then one graph for the even remainder: at most one
             # more eager step (each eager step is ~1 ms of host time, a graph
-            # replay a few us, and the host must stay ahead of the device)
+            # replay a few us, and the host must stay ahead of the device).
+            # Data-parallel on RCCL: every step's all-reduce is captured too.
             if S - done >= k:
                 gr = graph_of(k)
                 while S - done >= k:
@@ -418,6 +422,14 @@ class WakeWordTrainer(Trainer):
             done += 1
 
     _MAX_GRAPHS = 8
+
+    def _state_ptrs(self) -> tuple:
+        """Addresses a captured step bakes in besides its own buffers: the flat
+        parameters, Adam moments, gradient bucket and step state. Part of every
+        graph key, so a re-flattened or moved model never replays into freed
+        memory."""
+        return tuple(t.data_ptr() for t in (self.model.flat_parameters, self._m, self._v, self._bucket,
+                                            self._fstate))
 
     def _evict_graphs(self) -> None:
         """Bound the capture cache: each captured graph holds its staging

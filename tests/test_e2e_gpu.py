@@ -4,9 +4,11 @@ against the oracle: the `heybuddy train` hot path of the reference
 synthetic utterances.
 
   placement (to_target_length)   bit-exact vs the numpy restatement
-  7-band EQ, tanh, band-stop,    each stage's HIP output against the oracle
-  colored noise, gain + noise    applied to the HIP output of the stage before
-  + reverb                       (so an error is attributed to its stage)
+  7-band EQ, tanh, pitch shift,  each stage's HIP output against the oracle
+  band-stop, colored noise,      applied to the HIP output of the stage before
+  gain + noise + reverb          (so an error is attributed to its stage), in
+                                 the reference's order (augmented.py:79-121,
+                                 :368-392); pitch shift first in the batch chain
   mel frames                     1e-4 vs oracle.mel on the augmented clips
   speech embedding               1e-4 (1 + |ref|) vs oracle.embed on the HIP mel
   NaN replacement                the device gather leaves finite rows alone
@@ -52,7 +54,8 @@ def test_headline_pipeline_stagewise():
     from heybuddy.dataset.augmented import bandstop_cutoffs, eq_coefficients, eq_parameters, target_length_offsets
     from heybuddy.embedding_graph import WINDOW_STARTS, se20_graph
     from heybuddy.embeddings import embed_plan, replace_nan_rows_device
-    from heybuddy.kernels import ReverbPlan, embed_clips, mel_frames, place_clips, seven_band_eq, tanh_distortion
+    from heybuddy.kernels import (ReverbPlan, embed_clips, mel_frames, pitch_shift, place_clips, seven_band_eq,
+                                  tanh_distortion)
     from heybuddy.spectrogram import default_mel_plan
     from heybuddy.synthetic import impulse_responses, noise_bank, speech_clips
     from heybuddy.trainer import WakeWordTrainer
@@ -87,7 +90,29 @@ def test_headline_pipeline_stagewise():
     x = tanh_distortion(x, torch.from_numpy(amount).to(dev))
     _check_stage("tanh", x.cpu().numpy(), oaug.tanh_distortion(x_in, amount), rows)
 
-    # 3) batch chain: band-stop (one cutoff pair per batch of 128), colored noise, gain + noise + reverb
+    # 3) batch chain (augmented.py:93-121): pitch shift first, one fast shift per batch of 128
+    #    (batch 0: 125/128, batch 1: 128/125, batch 2: unshifted), vs the float64 restatement at
+    #    the pitch tests' bound (per clip L2 <= 1e-4 of the reference's, max <= 1e-3 of its peak)
+    x_in = x.cpu().numpy()
+    shifted = {}
+    for (num, den), b in (((125, 128), 0), ((128, 125), 1)):
+        sel = np.arange(b * 128, min(N, (b + 1) * 128), dtype=np.int32)
+        x = pitch_shift(x, torch.from_numpy(sel), num, den, out=x)
+        for i in rows:
+            if sel[0] <= i <= sel[-1]:
+                shifted[i] = (num, den)
+    out_h = x.cpu().numpy()
+    for i in rows:
+        if i not in shifted:
+            np.testing.assert_array_equal(out_h[i], x_in[i])
+            continue
+        r = oaug.pitch_shift(x_in[i:i + 1].astype(np.float64), *shifted[i])[0]
+        l2 = np.sqrt(((out_h[i] - r) ** 2).sum()) / np.sqrt((r ** 2).sum())
+        mx = np.abs(out_h[i] - r).max() / np.abs(r).max()
+        assert l2 <= 1e-4 and mx <= 1e-3, f"pitch shift {shifted[i]}: clip {i}: L2 {l2:.2e}, max {mx:.2e}"
+    assert len(shifted) >= 8
+
+    #    then band-stop (one cutoff pair per batch of 128), colored noise, gain + noise + reverb
     plan = ReverbPlan(dev)
     lo_b, hi_b = bandstop_cutoffs(3)
     batch = np.arange(N) // 128

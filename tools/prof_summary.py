@@ -46,9 +46,10 @@ def rows(d, pattern):
 
 def short(name):
     """Kernel name without namespaces / argument lists, template args kept."""
-    n = re.sub(r"\(.*$", "", name)          # argument list
+    n = name.replace("(anonymous namespace)::", "")
+    n = re.sub(r"\(.*$", "", n)             # argument list
     n = re.sub(r"^void ", "", n)
-    n = re.sub(r"hbk::\(anonymous namespace\)::|hbk::", "", n)
+    n = re.sub(r"^hbk::", "", n)
     return n.strip()
 
 

@@ -44,4 +44,6 @@ python3 tools/prof_summary.py --fetch $OUT/${TAG}_pmcfetch_c$C --write $OUT/${TA
   --steps 1 --stage-steps 1 --config $C \
   --label "$TAG counter passes: bench.py --steps 1 --warmup 1 --stage-steps 1 --no-cpu --no-check $BA" \
   --out $OUT/${TAG}_pmc_c$C.json
+# the raw per-dispatch CSVs exceed gpurun's 64 MiB copy-back: keep the summaries and kernel_stats
+rm -rf $OUT/${TAG}_trace_c$C $OUT/${TAG}_pmcfetch_c$C $OUT/${TAG}_pmcwrite_c$C $OUT/${TAG}_pmcsq_c$C
 echo "=== done"
