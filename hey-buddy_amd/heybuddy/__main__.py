@@ -21,6 +21,7 @@ import click
 import torch
 
 from heybuddy.constants import *  # noqa: F401,F403
+from heybuddy.dataset.training import OFFLINE_NEGATIVE_SAMPLES, OFFLINE_VALIDATION_NEGATIVE_SAMPLES
 from heybuddy.constants import (DEFAULT_ACTIVATION_THRESHOLD, DEFAULT_ADVERSARIAL_BATCH_SIZE,
                                 DEFAULT_ADVERSARIAL_SAMPLES, DEFAULT_AUGMENT_BACKGROUND_NOISE_MAX_SNR_DB,
                                 DEFAULT_AUGMENT_BACKGROUND_NOISE_MIN_SNR_DB,
@@ -46,109 +47,141 @@ def main() -> None:
     """hey-buddy (MI355X hot path)."""
 
 
-def build_embeddings(n: int, seed: int, device: torch.device, augmenter=None, chunk: int = 65536,
-                     kind: str = "positive", phrase: str = "") -> torch.Tensor:
-    """Synthetic clips of one class -> [n, 16, 96] embeddings on the device,
-    featurized (and augmented, if given) in chunks, sharded over the ranks.
-    positive: phrase_clips(phrase); adversarial: random tone bursts;
-    negative: the same at 0.3x level."""
-    from heybuddy import distributed as hd
-    from heybuddy.embeddings import SpeechEmbeddings
-    from heybuddy.synthetic import phrase_clips, synthetic_clips
-    rank, world = hd.world()
-    lo, hi = hd.clip_range(n, rank, world)
-    se = SpeechEmbeddings(device_id=device.index)
-    parts = []
-    for s in range(lo, hi, chunk):
-        m = min(chunk, hi - s)
-        if kind == "positive":
-            clips = phrase_clips(phrase, m, seed=seed * 7919 + s, device=device)
-        else:
-            clips = synthetic_clips(m, seed=seed * 7919 + s, device=device)
-        if kind == "negative":  # noise-like negatives: random tones at low level, no burst
-            clips.mul_(0.3)
-        if augmenter is not None:
-            clips = augmenter(clips)
-        parts.append(se.featurize(clips))
-    local = torch.cat(parts) if parts else torch.empty((0, 16, 96), device=device)
-    if world == 1:
-        return local
-    sizes = [hd.clip_range(n, r, world) for r in range(world)]
-    buf = [torch.empty((b - a, 16, 96), device=device) for a, b in sizes]
-    torch.distributed.all_gather(buf, local.contiguous())
-    return torch.cat(buf)
-
-
 @main.command()
 @click.argument("phrase", type=str, nargs=1)
-@click.option("--additional-phrase", type=str, default=None, multiple=True)
-@click.option("--wandb-entity", type=str, default=None)
-@click.option("--perceptron", "architecture", flag_value="perceptron", default=True)
-@click.option("--transformer", "architecture", flag_value="transformer")
-@click.option("--use-half-layers/--no-use-half-layers", default=DEFAULT_USE_HALF_LAYERS)
-@click.option("--use-gating/--no-use-gating", default=DEFAULT_USE_GATING)
-@click.option("--layer-dim", type=int, default=DEFAULT_LAYER_DIM, show_default=True)
-@click.option("--num-layers", type=int, default=DEFAULT_LAYERS, show_default=True)
-@click.option("--steps", type=int, default=DEFAULT_STEPS, show_default=True)
-@click.option("--stages", type=int, default=DEFAULT_STAGES, show_default=True)
-@click.option("--threshold", type=float, default=DEFAULT_ACTIVATION_THRESHOLD, show_default=True)
-@click.option("--learning-rate", type=float, default=DEFAULT_LEARNING_RATE, show_default=True)
-@click.option("--high-loss-threshold", type=float, default=DEFAULT_HIGH_LOSS_THRESHOLD, show_default=True)
-@click.option("--target-false-positive-rate", type=float, default=DEFAULT_TARGET_FALSE_POSITIVE_RATE, show_default=True)
-@click.option("--dynamic-negative-weight/--no-dynamic-negative-weight", default=True)
-@click.option("--negative-weight", type=float, default=DEFAULT_NEGATIVE_WEIGHT, show_default=True)
-@click.option("--augmentation-background-noise-prob", type=float, default=DEFAULT_AUGMENT_BACKGROUND_NOISE_PROB, show_default=True)
-@click.option("--augmentation-background-noise-min-snr-db", type=float, default=DEFAULT_AUGMENT_BACKGROUND_NOISE_MIN_SNR_DB, show_default=True)
-@click.option("--augmentation-background-noise-max-snr-db", type=float, default=DEFAULT_AUGMENT_BACKGROUND_NOISE_MAX_SNR_DB, show_default=True)
-@click.option("--augmentation-reverb-prob", type=float, default=DEFAULT_AUGMENT_REVERB_PROB, show_default=True)
-@click.option("--augmentation-gain-prob", type=float, default=DEFAULT_AUGMENT_GAIN_PROB, show_default=True)
-@click.option("--augmentation-tanh-distortion-prob", type=float, default=DEFAULT_AUGMENT_TANH_DISTORTION_PROB, show_default=True)
-@click.option("--augmentation-tanh-min-distortion", type=float, default=DEFAULT_AUGMENT_TANH_MIN_DISTORTION, show_default=True)
-@click.option("--augmentation-tanh-max-distortion", type=float, default=DEFAULT_AUGMENT_TANH_MAX_DISTORTION, show_default=True)
-@click.option("--augmentation-colored-noise-prob", type=float, default=DEFAULT_AUGMENT_COLORED_NOISE_PROB, show_default=True)
-@click.option("--augmentation-colored-noise-min-snr-db", type=float, default=DEFAULT_AUGMENT_COLORED_NOISE_MIN_SNR_DB, show_default=True)
-@click.option("--augmentation-colored-noise-max-snr-db", type=float, default=DEFAULT_AUGMENT_COLORED_NOISE_MAX_SNR_DB, show_default=True)
-@click.option("--augmentation-colored-noise-min-f-decay", type=float, default=DEFAULT_AUGMENT_COLORED_NOISE_MIN_F_DECAY, show_default=True)
-@click.option("--augmentation-colored-noise-max-f-decay", type=float, default=DEFAULT_AUGMENT_COLORED_NOISE_MAX_F_DECAY, show_default=True)
-@click.option("--logging-steps", type=int, default=DEFAULT_LOGGING_STEPS, show_default=True)
-@click.option("--validation-steps", type=int, default=DEFAULT_VALIDATION_STEPS, show_default=True)
-@click.option("--checkpoint-steps", type=int, default=DEFAULT_CHECKPOINT_STEPS, show_default=True)
-@click.option("--positive-samples", type=int, default=DEFAULT_POSITIVE_SAMPLES, show_default=True)
-@click.option("--adversarial-samples", type=int, default=DEFAULT_ADVERSARIAL_SAMPLES, show_default=True)
-@click.option("--negative-samples", type=int, default=200_000, show_default=True,
-              help="Synthetic negatives featurized in place of the hosted precalculated sets.")
-@click.option("--positive-batch-size", type=int, default=DEFAULT_POSITIVE_BATCH_SIZE, show_default=True)
-@click.option("--negative-batch-size", type=int, default=DEFAULT_NEGATIVE_BATCH_SIZE, show_default=True)
-@click.option("--adversarial-batch-size", type=int, default=DEFAULT_ADVERSARIAL_BATCH_SIZE, show_default=True)
-@click.option("--validation-samples", type=int, default=DEFAULT_VALIDATION_SAMPLES, show_default=True)
-@click.option("--testing-positive-samples", type=int, default=DEFAULT_TESTING_POSITIVE_SAMPLES, show_default=True)
-@click.option("--testing-adversarial-samples", type=int, default=DEFAULT_TESTING_ADVERSARIAL_SAMPLES, show_default=True)
+@click.option("--additional-phrase", type=str, default=None, multiple=True, help="Additional phrases to use for training.", show_default=True)
+@click.option("--wandb-entity", type=str, default=None, help="W&B entity to use for logging (outside the hot path: ignored).", show_default=True)
+@click.option("--perceptron", "architecture", flag_value="perceptron", default=DEFAULT_ARCHITECTURE == "perceptron", help="Use a perceptron architecture.", show_default=True)
+@click.option("--transformer", "architecture", flag_value="transformer", default=DEFAULT_ARCHITECTURE == "transformer", help="Use a transformer architecture (not implemented on the MI355X path).", show_default=True)
+@click.option("--use-half-layers/--no-use-half-layers", default=DEFAULT_USE_HALF_LAYERS, is_flag=True, help="Use enumerated striped-attention layers for the perceptron model.", show_default=True)
+@click.option("--use-gating/--no-use-gating", default=DEFAULT_USE_GATING, is_flag=True, help="Use gated MLP layers for the perceptron model.", show_default=True)
+@click.option("--layer-dim", type=int, default=DEFAULT_LAYER_DIM, help="Dimension of the linear layers to use for the model.", show_default=True)
+@click.option("--num-layers", type=int, default=DEFAULT_LAYERS, help="The number of perceptron blocks.", show_default=True)
+@click.option("--num-heads", type=int, default=DEFAULT_HEADS, help="The number of attention heads to use when using the transformer model.", show_default=True)
+@click.option("--steps", type=int, default=DEFAULT_STEPS, help="Number of optimization steps to take.", show_default=True)
+@click.option("--stages", type=int, default=DEFAULT_STAGES, help="Number of training stages.", show_default=True)
+@click.option("--threshold", type=float, default=DEFAULT_ACTIVATION_THRESHOLD, help="Threshold to use for wake-word detection.", show_default=True)
+@click.option("--learning-rate", type=float, default=DEFAULT_LEARNING_RATE, help="Learning rate for the optimizer.", show_default=True)
+@click.option("--high-loss-threshold", type=float, default=DEFAULT_HIGH_LOSS_THRESHOLD, help="Threshold for high loss values.", show_default=True)
+@click.option("--target-false-positive-rate", type=float, default=DEFAULT_TARGET_FALSE_POSITIVE_RATE, help="Target false positive rate for the model.", show_default=True)
+@click.option("--dynamic-negative-weight/--no-dynamic-negative-weight", default=True, is_flag=True, help="Dynamically adjust the negative weight at each validation step.", show_default=True)
+@click.option("--negative-weight", type=float, default=DEFAULT_NEGATIVE_WEIGHT, help="Negative weight for the loss function.", show_default=True)
+@click.option("--training-full-default-dataset", "training_default_size", flag_value="full", help="Use the full precalculated default training set.", default=True, show_default=True)
+@click.option("--training-large-default-dataset", "training_default_size", flag_value="large", help="Use the large precalculated default training set.", default=False, show_default=True)
+@click.option("--training-medium-default-dataset", "training_default_size", flag_value="medium", help="Use the medium precalculated default training set.", default=False, show_default=True)
+@click.option("--training-no-default-dataset", "training_default_size", flag_value="none", help="Do not use a precalculated default training set.", default=False, show_default=True)
+@click.option("--training-dataset", type=click.Path(exists=True, dir_okay=False, file_okay=True), default=None, help="Use a custom precalculated training set.", show_default=True)
+@click.option("--augment-phrase-prob", type=float, default=DEFAULT_AUGMENT_PHRASE_PROB, help="Probability of augmenting the phrase.", show_default=True)
+@click.option("--augment-phrase-default-words/--augment-phrase-no-default-words", default=True, is_flag=True, help="Use the default words for augmentation.", show_default=True)
+@click.option("--augment-phrase-word", type=str, default=None, multiple=True, help="Custom words to use for augmentation.", show_default=True)
+@click.option("--augmentation-default-background-dataset/--augmentation-no-default-background-dataset", default=True, is_flag=True, help="Use the default background dataset for augmentation.", show_default=True)
+@click.option("--augmentation-background-dataset", default=None, multiple=True, help="Use a custom background dataset for augmentation.", show_default=True)
+@click.option("--augmentation-default-impulse-dataset/--augmentation-no-default-impulse-dataset", default=True, is_flag=True, help="Use the default impulse dataset for augmentation.", show_default=True)
+@click.option("--augmentation-impulse-dataset", default=None, multiple=True, help="Use a custom impulse dataset for augmentation.", show_default=True)
+@click.option("--augmentation-dataset-streaming/--augmentation-dataset-no-streaming", default=False, is_flag=True, help="Stream the augmentation datasets, instead of downloading first.", show_default=True)
+@click.option("--augmentation-seven-band-prob", type=float, default=DEFAULT_AUGMENT_SEVEN_BAND_PROB, help="Probability of applying the seven band equalization augmentation.", show_default=True)
+@click.option("--augmentation-seven-band-gain-db", type=float, default=DEFAULT_AUGMENT_SEVEN_BAND_GAIN_DB, help="Gain in decibels for the seven band equalization augmentation.", show_default=True)
+@click.option("--augmentation-tanh-distortion-prob", type=float, default=DEFAULT_AUGMENT_TANH_DISTORTION_PROB, help="Probability of applying the tanh distortion augmentation.", show_default=True)
+@click.option("--augmentation-tanh-distortion-min", type=float, default=DEFAULT_AUGMENT_TANH_MIN_DISTORTION, help="Minimum value for the tanh distortion augmentation.", show_default=True)
+@click.option("--augmentation-tanh-distortion-max", type=float, default=DEFAULT_AUGMENT_TANH_MAX_DISTORTION, help="Maximum value for the tanh distortion augmentation.", show_default=True)
+@click.option("--augmentation-pitch-shift-prob", type=float, default=DEFAULT_AUGMENT_PITCH_SHIFT_PROB, help="Probability of applying the pitch shift augmentation.", show_default=True)
+@click.option("--augmentation-pitch-shift-semitones", type=int, default=DEFAULT_AUGMENT_PITCH_SHIFT_SEMITONES, help="Number of semitones to shift the pitch for the pitch shift augmentation.", show_default=True)
+@click.option("--augmentation-band-stop-prob", type=float, default=DEFAULT_AUGMENT_BAND_STOP_PROB, help="Probability of applying the band stop filter augmentation.", show_default=True)
+@click.option("--augmentation-colored-noise-prob", type=float, default=DEFAULT_AUGMENT_COLORED_NOISE_PROB, help="Probability of applying the colored noise augmentation.", show_default=True)
+@click.option("--augmentation-colored-noise-min-snr-db", type=float, default=DEFAULT_AUGMENT_COLORED_NOISE_MIN_SNR_DB, help="Minimum signal-to-noise ratio for the colored noise augmentation.", show_default=True)
+@click.option("--augmentation-colored-noise-max-snr-db", type=float, default=DEFAULT_AUGMENT_COLORED_NOISE_MAX_SNR_DB, help="Maximum signal-to-noise ratio for the colored noise augmentation.", show_default=True)
+@click.option("--augmentation-colored-noise-min-f-decay", type=float, default=DEFAULT_AUGMENT_COLORED_NOISE_MIN_F_DECAY, help="Minimum frequency decay for the colored noise augmentation.", show_default=True)
+@click.option("--augmentation-colored-noise-max-f-decay", type=float, default=DEFAULT_AUGMENT_COLORED_NOISE_MAX_F_DECAY, help="Maximum frequency decay for the colored noise augmentation.", show_default=True)
+@click.option("--augmentation-background-noise-prob", type=float, default=DEFAULT_AUGMENT_BACKGROUND_NOISE_PROB, help="Probability of applying the background noise augmentation.", show_default=True)
+@click.option("--augmentation-background-noise-min-snr-db", type=float, default=DEFAULT_AUGMENT_BACKGROUND_NOISE_MIN_SNR_DB, help="Minimum signal-to-noise ratio for the background noise augmentation.", show_default=True)
+@click.option("--augmentation-background-noise-max-snr-db", type=float, default=DEFAULT_AUGMENT_BACKGROUND_NOISE_MAX_SNR_DB, help="Maximum signal-to-noise ratio for the background noise augmentation.", show_default=True)
+@click.option("--augmentation-gain-prob", type=float, default=DEFAULT_AUGMENT_GAIN_PROB, help="Probability of applying the gain augmentation.", show_default=True)
+@click.option("--augmentation-reverb-prob", type=float, default=DEFAULT_AUGMENT_REVERB_PROB, help="Probability of applying the reverb augmentation.", show_default=True)
+@click.option("--logging-steps", type=int, default=DEFAULT_LOGGING_STEPS, help="How often to log step details.", show_default=True)
+@click.option("--validation-steps", type=int, default=DEFAULT_VALIDATION_STEPS, help="How often to validate the model.", show_default=True)
+@click.option("--checkpoint-steps", type=int, default=DEFAULT_CHECKPOINT_STEPS, help="How often to save the model.", show_default=True)
+@click.option("--positive-samples", type=int, default=DEFAULT_POSITIVE_SAMPLES, help="Number of positive samples to use for training.", show_default=True)
+@click.option("--adversarial-samples", type=int, default=DEFAULT_ADVERSARIAL_SAMPLES, help="Number of adversarial samples to use for training.", show_default=True)
+@click.option("--adversarial-phrases", type=int, default=DEFAULT_ADVERSARIAL_PHRASES, help="Number of adversarial phrases to use for training.", show_default=True)
+@click.option("--adversarial-phrase-custom", type=str, default=None, multiple=True, help="Custom adversarial phrases to use for training.", show_default=True)
+@click.option("--positive-batch-size", type=int, default=DEFAULT_POSITIVE_BATCH_SIZE, help="The number of positive samples in each training batch.", show_default=True)
+@click.option("--negative-batch-size", type=int, default=DEFAULT_NEGATIVE_BATCH_SIZE, help="The number of negative samples in each training batch.", show_default=True)
+@click.option("--adversarial-batch-size", type=int, default=DEFAULT_ADVERSARIAL_BATCH_SIZE, help="The number of adversarial samples in each training batch.", show_default=True)
+@click.option("--num-batch-threads", type=int, default=DEFAULT_BATCH_THREADS, help="Batch threads (batches are sampled on the device here: accepted, unused).", show_default=True)
+@click.option("--validation-positive-batch-size", type=int, default=DEFAULT_VALIDATION_POSITIVE_BATCH_SIZE, help="The number of positive samples in each validation batch.", show_default=True)
+@click.option("--validation-negative-batch-size", type=int, default=DEFAULT_VALIDATION_NEGATIVE_BATCH_SIZE, help="The number of negative samples in each validation batch.", show_default=True)
+@click.option("--validation-samples", type=int, default=DEFAULT_VALIDATION_SAMPLES, help="The number of samples to use for validation.", show_default=True)
+@click.option("--validation-num-batch-threads", type=int, default=1, help="Validation batch threads (accepted, unused).", show_default=True)
+@click.option("--validation-default-dataset/--validation-no-default-dataset", default=True, is_flag=True, help="Use the default validation dataset.", show_default=True)
+@click.option("--validation-dataset", type=click.Path(exists=True, dir_okay=False, file_okay=True), default=None, help="Use a custom precalculated validation set.", show_default=True)
+@click.option("--testing-positive-samples", type=int, default=DEFAULT_TESTING_POSITIVE_SAMPLES, help="The number of positive samples to use for testing.", show_default=True)
+@click.option("--testing-adversarial-samples", type=int, default=DEFAULT_TESTING_ADVERSARIAL_SAMPLES, help="The number of adversarial samples to use for testing.", show_default=True)
+@click.option("--testing-positive-batch-size", type=int, default=None, help="Positive samples per testing batch (default: the training size).", show_default=True)
+@click.option("--testing-adversarial-batch-size", type=int, default=None, help="Adversarial samples per testing batch (default: the training size).", show_default=True)
+@click.option("--testing-num-batch-threads", type=int, default=1, help="Testing batch threads (accepted, unused).", show_default=True)
+@click.option("--resume/--no-resume", default=False, is_flag=True, help="Resume training from the last checkpoint.", show_default=True)
+@click.option("--debug/--no-debug", default=False, is_flag=True, help="Enable debug logging.", show_default=True)
+# MI355X-path additions (offline stand-ins and run control; not in the reference)
+@click.option("--negative-samples", type=int, default=OFFLINE_NEGATIVE_SAMPLES, show_default=True,
+              help="Synthetic negatives featurized when the hosted precalculated sets are not on disk.")
+@click.option("--validation-negative-samples", type=int, default=OFFLINE_VALIDATION_NEGATIVE_SAMPLES, show_default=True,
+              help="Synthetic validation negatives when the hosted validation set is not on disk.")
 @click.option("--checkpoint-dir", type=str, default="./checkpoints", show_default=True)
 @click.option("--seed", type=int, default=0, show_default=True)
-@click.option("--resume/--no-resume", default=False)
-@click.option("--debug/--no-debug", default=False)
-def train(phrase: str, additional_phrase: List[str], wandb_entity: Optional[str], architecture: str,
-          use_half_layers: bool, use_gating: bool, layer_dim: int, num_layers: int, steps: int, stages: int,
-          threshold: float, learning_rate: float, high_loss_threshold: float,
-          target_false_positive_rate: float, dynamic_negative_weight: bool, negative_weight: float,
-          augmentation_background_noise_prob: float, augmentation_background_noise_min_snr_db: float,
-          augmentation_background_noise_max_snr_db: float, augmentation_reverb_prob: float,
-          augmentation_gain_prob: float, augmentation_colored_noise_prob: float,
-          augmentation_colored_noise_min_snr_db: float, augmentation_colored_noise_max_snr_db: float,
-          augmentation_colored_noise_min_f_decay: float, augmentation_colored_noise_max_f_decay: float,
-          augmentation_tanh_distortion_prob: float, augmentation_tanh_min_distortion: float,
-          augmentation_tanh_max_distortion: float,
-          logging_steps: int, validation_steps: int, checkpoint_steps: int, positive_samples: int,
-          adversarial_samples: int, negative_samples: int, positive_batch_size: int,
-          negative_batch_size: int, adversarial_batch_size: int, validation_samples: int,
-          testing_positive_samples: int, testing_adversarial_samples: int, checkpoint_dir: str, seed: int,
-          resume: bool, debug: bool) -> None:
-    """Trains a wake word detection model (synthetic data on the device)."""
+def train(phrase: str, additional_phrase: List[str] = [], wandb_entity: Optional[str] = None,
+          architecture: str = DEFAULT_ARCHITECTURE, use_half_layers: bool = DEFAULT_USE_HALF_LAYERS,
+          use_gating: bool = DEFAULT_USE_GATING, layer_dim: int = DEFAULT_LAYER_DIM, num_layers: int = DEFAULT_LAYERS,
+          num_heads: int = DEFAULT_HEADS, steps: int = DEFAULT_STEPS, stages: int = DEFAULT_STAGES,
+          threshold: float = DEFAULT_ACTIVATION_THRESHOLD, learning_rate: float = DEFAULT_LEARNING_RATE,
+          high_loss_threshold: float = DEFAULT_HIGH_LOSS_THRESHOLD,
+          target_false_positive_rate: float = DEFAULT_TARGET_FALSE_POSITIVE_RATE,
+          dynamic_negative_weight: bool = True, negative_weight: float = DEFAULT_NEGATIVE_WEIGHT,
+          training_default_size: str = "full", training_dataset: Optional[str] = None,
+          augment_phrase_prob: float = DEFAULT_AUGMENT_PHRASE_PROB, augment_phrase_default_words: bool = True,
+          augment_phrase_word: List[str] = [], augmentation_default_background_dataset: bool = True,
+          augmentation_background_dataset: List[str] = [], augmentation_default_impulse_dataset: bool = True,
+          augmentation_impulse_dataset: List[str] = [], augmentation_dataset_streaming: bool = False,
+          augmentation_seven_band_prob: float = DEFAULT_AUGMENT_SEVEN_BAND_PROB,
+          augmentation_seven_band_gain_db: float = DEFAULT_AUGMENT_SEVEN_BAND_GAIN_DB,
+          augmentation_tanh_distortion_prob: float = DEFAULT_AUGMENT_TANH_DISTORTION_PROB,
+          augmentation_tanh_distortion_min: float = DEFAULT_AUGMENT_TANH_MIN_DISTORTION,
+          augmentation_tanh_distortion_max: float = DEFAULT_AUGMENT_TANH_MAX_DISTORTION,
+          augmentation_pitch_shift_prob: float = DEFAULT_AUGMENT_PITCH_SHIFT_PROB,
+          augmentation_pitch_shift_semitones: int = DEFAULT_AUGMENT_PITCH_SHIFT_SEMITONES,
+          augmentation_band_stop_prob: float = DEFAULT_AUGMENT_BAND_STOP_PROB,
+          augmentation_colored_noise_prob: float = DEFAULT_AUGMENT_COLORED_NOISE_PROB,
+          augmentation_colored_noise_min_snr_db: float = DEFAULT_AUGMENT_COLORED_NOISE_MIN_SNR_DB,
+          augmentation_colored_noise_max_snr_db: float = DEFAULT_AUGMENT_COLORED_NOISE_MAX_SNR_DB,
+          augmentation_colored_noise_min_f_decay: float = DEFAULT_AUGMENT_COLORED_NOISE_MIN_F_DECAY,
+          augmentation_colored_noise_max_f_decay: float = DEFAULT_AUGMENT_COLORED_NOISE_MAX_F_DECAY,
+          augmentation_background_noise_prob: float = DEFAULT_AUGMENT_BACKGROUND_NOISE_PROB,
+          augmentation_background_noise_min_snr_db: float = DEFAULT_AUGMENT_BACKGROUND_NOISE_MIN_SNR_DB,
+          augmentation_background_noise_max_snr_db: float = DEFAULT_AUGMENT_BACKGROUND_NOISE_MAX_SNR_DB,
+          augmentation_gain_prob: float = DEFAULT_AUGMENT_GAIN_PROB,
+          augmentation_reverb_prob: float = DEFAULT_AUGMENT_REVERB_PROB,
+          logging_steps: int = DEFAULT_LOGGING_STEPS, validation_steps: int = DEFAULT_VALIDATION_STEPS,
+          checkpoint_steps: int = DEFAULT_CHECKPOINT_STEPS, positive_samples: int = DEFAULT_POSITIVE_SAMPLES,
+          adversarial_samples: int = DEFAULT_ADVERSARIAL_SAMPLES, adversarial_phrases: int = DEFAULT_ADVERSARIAL_PHRASES,
+          adversarial_phrase_custom: List[str] = [], positive_batch_size: int = DEFAULT_POSITIVE_BATCH_SIZE,
+          negative_batch_size: int = DEFAULT_NEGATIVE_BATCH_SIZE,
+          adversarial_batch_size: int = DEFAULT_ADVERSARIAL_BATCH_SIZE, num_batch_threads: int = DEFAULT_BATCH_THREADS,
+          validation_positive_batch_size: int = DEFAULT_VALIDATION_POSITIVE_BATCH_SIZE,
+          validation_negative_batch_size: int = DEFAULT_VALIDATION_NEGATIVE_BATCH_SIZE,
+          validation_samples: int = DEFAULT_VALIDATION_SAMPLES, validation_num_batch_threads: int = 1,
+          validation_default_dataset: bool = True, validation_dataset: Optional[str] = None,
+          testing_positive_samples: int = DEFAULT_TESTING_POSITIVE_SAMPLES,
+          testing_adversarial_samples: int = DEFAULT_TESTING_ADVERSARIAL_SAMPLES,
+          testing_positive_batch_size: Optional[int] = None, testing_adversarial_batch_size: Optional[int] = None,
+          testing_num_batch_threads: int = 1, resume: bool = False, debug: bool = False,
+          negative_samples: int = OFFLINE_NEGATIVE_SAMPLES,
+          validation_negative_samples: int = OFFLINE_VALIDATION_NEGATIVE_SAMPLES,
+          checkpoint_dir: str = "./checkpoints", seed: int = 0) -> None:
+    """Trains a wake word detection model (reference __main__.py:245-429):
+    WakeWordTrainingDatasetIterator.all -> WakeWordTrainer(...)(...), with the
+    featurization and every train step on the device."""
     import numpy as np
     from heybuddy import distributed as hd
-    from heybuddy.dataset.augmented import BatchAugmenter
-    from heybuddy.dataset.training import DevicePool, TrainingDatasetIterator, WakeWordTrainingDatasetIterator
-    from heybuddy.synthetic import impulse_responses, noise_bank
+    from heybuddy.dataset.training import WakeWordTrainingDatasetIterator
     from heybuddy.trainer import WakeWordTrainer
     from heybuddy.util import logger
 
@@ -159,50 +192,65 @@ def train(phrase: str, additional_phrase: List[str], wandb_entity: Optional[str]
     device = torch.device("cuda", torch.cuda.current_device())
     torch.manual_seed(seed)
     np.random.seed(seed)
-    if additional_phrase:
-        logger.warning("additional phrases need TTS; the synthetic positives stand in for every phrase")
     if wandb_entity:
         logger.warning("wandb logging is outside the MI355X hot path; ignored")
-    aug = BatchAugmenter(noise_bank(64, seed=seed + 11, device=device),
-                         impulse_responses(32, seed=seed + 12, device=device), device=device,
-                         batch_size=128, background_noise_prob=augmentation_background_noise_prob,
-                         background_noise_min_snr_db=augmentation_background_noise_min_snr_db,
-                         background_noise_max_snr_db=augmentation_background_noise_max_snr_db,
-                         reverb_prob=augmentation_reverb_prob, gain_prob=augmentation_gain_prob,
-                         colored_noise_prob=augmentation_colored_noise_prob,
-                         colored_noise_min_snr_db=augmentation_colored_noise_min_snr_db,
-                         colored_noise_max_snr_db=augmentation_colored_noise_max_snr_db,
-                         colored_noise_min_f_decay=augmentation_colored_noise_min_f_decay,
-                         colored_noise_max_f_decay=augmentation_colored_noise_max_f_decay,
-                         tanh_distortion_prob=augmentation_tanh_distortion_prob,
-                         tanh_min_distortion=augmentation_tanh_min_distortion,
-                         tanh_max_distortion=augmentation_tanh_max_distortion)
-    pos = build_embeddings(positive_samples, seed + 1, device, aug, kind="positive", phrase=phrase)
-    adv = build_embeddings(adversarial_samples, seed + 2, device, aug, kind="adversarial")
-    neg = build_embeddings(negative_samples, seed + 3, device, aug, kind="negative").half()
-    vpos = build_embeddings(validation_samples // 10 or 1, seed + 4, device, aug, kind="positive", phrase=phrase)
-    vneg = build_embeddings(validation_samples, seed + 5, device, aug, kind="negative")
-    tpos = build_embeddings(testing_positive_samples, seed + 6, device, aug, kind="positive", phrase=phrase)
-    tadv = build_embeddings(testing_adversarial_samples, seed + 7, device, aug, kind="adversarial")
-    g = torch.Generator(device=device).manual_seed(seed + 99)  # identical batches on every rank
-    half = int(negative_samples * 2 / 3)
-    training = WakeWordTrainingDatasetIterator.default(
-        pos, adv, neg[:half], neg[half:], positive_per_batch=positive_batch_size,
-        adversarial_per_batch=adversarial_batch_size, negative_per_batch=negative_batch_size, generator=g)
 
-    def fixed(xs, ys, bs=1000):
-        x = torch.cat(xs)
-        y = torch.cat(ys)
-        return [(x[i:i + bs], y[i:i + bs]) for i in range(0, x.shape[0], bs)]
+    phrase_augment_words: List[str] = []
+    if augment_phrase_default_words:
+        phrase_augment_words.extend(DEFAULT_AUGMENT_PHRASE_WORDS)
+    phrase_augment_words.extend(augment_phrase_word or [])
+    background: List[str] = []
+    if augmentation_default_background_dataset:
+        background.extend([DEFAULT_BACKGROUND_DATASET] if isinstance(DEFAULT_BACKGROUND_DATASET, str)
+                          else DEFAULT_BACKGROUND_DATASET)
+    background.extend(augmentation_background_dataset or [])
+    impulse: List[str] = []
+    if augmentation_default_impulse_dataset:
+        impulse.extend([DEFAULT_IMPULSE_DATASET] if isinstance(DEFAULT_IMPULSE_DATASET, str)
+                       else DEFAULT_IMPULSE_DATASET)
+    impulse.extend(augmentation_impulse_dataset or [])
 
-    validation = fixed([vpos, vneg], [torch.ones(vpos.shape[0], dtype=torch.int64, device=device),
-                                      torch.zeros(vneg.shape[0], dtype=torch.int64, device=device)])
-    testing = fixed([tpos, tadv], [torch.ones(tpos.shape[0], dtype=torch.int64, device=device),
-                                   torch.zeros(tadv.shape[0], dtype=torch.int64, device=device)])
+    training, validation, testing = WakeWordTrainingDatasetIterator.all(
+        wake_phrase=phrase, additional_wake_phrases=list(additional_phrase or []),
+        adversarial_per_batch=adversarial_batch_size, augment_background_dataset=background,
+        augment_background_noise_max_snr_db=augmentation_background_noise_max_snr_db,
+        augment_background_noise_min_snr_db=augmentation_background_noise_min_snr_db,
+        augment_background_noise_prob=augmentation_background_noise_prob,
+        augment_band_stop_prob=augmentation_band_stop_prob,
+        augment_colored_noise_max_f_decay=augmentation_colored_noise_max_f_decay,
+        augment_colored_noise_max_snr_db=augmentation_colored_noise_max_snr_db,
+        augment_colored_noise_min_f_decay=augmentation_colored_noise_min_f_decay,
+        augment_colored_noise_min_snr_db=augmentation_colored_noise_min_snr_db,
+        augment_colored_noise_prob=augmentation_colored_noise_prob,
+        augment_dataset_streaming=augmentation_dataset_streaming, augment_gain_prob=augmentation_gain_prob,
+        augment_impulse_dataset=impulse, augment_pitch_shift_prob=augmentation_pitch_shift_prob,
+        augment_pitch_shift_semitones=augmentation_pitch_shift_semitones,
+        augment_reverb_prob=augmentation_reverb_prob, augment_seven_band_gain_db=augmentation_seven_band_gain_db,
+        augment_seven_band_prob=augmentation_seven_band_prob,
+        augment_tanh_distortion_prob=augmentation_tanh_distortion_prob,
+        augment_tanh_max_distortion=augmentation_tanh_distortion_max,
+        augment_tanh_min_distortion=augmentation_tanh_distortion_min,
+        custom_adversarial_phrases=list(adversarial_phrase_custom or []), custom_training=training_dataset,
+        large_training=training_default_size in ["full", "large"],
+        medium_training=training_default_size in ["full", "medium"], negative_per_batch=negative_batch_size,
+        num_adversarial_phrases=adversarial_phrases, num_adversarial_samples=adversarial_samples,
+        num_batch_threads=num_batch_threads, num_positive_samples=positive_samples,
+        phrase_augment_prob=augment_phrase_prob, phrase_augment_words=phrase_augment_words,
+        positive_per_batch=positive_batch_size, testing_adversarial_per_batch=testing_adversarial_batch_size,
+        testing_num_adversarial_samples=testing_adversarial_samples,
+        testing_num_batch_threads=testing_num_batch_threads, testing_num_positive_samples=testing_positive_samples,
+        testing_positive_per_batch=testing_positive_batch_size, validation_custom=validation_dataset,
+        validation_include_precalculated=validation_default_dataset,
+        validation_negative_batch_size=validation_negative_batch_size,
+        validation_num_batch_threads=validation_num_batch_threads, validation_num_positive_samples=validation_samples,
+        validation_positive_batch_size=validation_positive_batch_size,
+        device_id=device.index, seed=seed, offline_negative_samples=negative_samples,
+        offline_validation_negative_samples=validation_negative_samples)
+
     rank, world = hd.world()
     trainer = WakeWordTrainer(checkpoint_dir=checkpoint_dir, architecture=architecture,
                               use_half_layers=use_half_layers, use_gating=use_gating, layer_dim=layer_dim,
-                              num_layers=num_layers, device=device)
+                              num_layers=num_layers, num_heads=num_heads, device=device)
     name = safe_name(phrase)
     if resume:
         trainer.resume(name)
@@ -211,7 +259,7 @@ def train(phrase: str, additional_phrase: List[str], wandb_entity: Optional[str]
             high_loss_threshold=high_loss_threshold, learning_rate=learning_rate,
             max_negative_weight=negative_weight, name=name if rank == 0 else f"{name}_rank{rank}",
             num_stages=stages, num_steps=steps, target_false_positive_rate=target_false_positive_rate,
-            validation_steps=validation_steps, logging_steps=logging_steps)
+            validation_steps=validation_steps, logging_steps=logging_steps, wandb_entity=wandb_entity)
     if world > 1:
         torch.distributed.destroy_process_group()
 

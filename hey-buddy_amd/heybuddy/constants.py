@@ -62,3 +62,35 @@ DEFAULT_AUGMENT_SEVEN_BAND_GAIN_DB = 6.0
 DEFAULT_AUGMENT_PITCH_SHIFT_PROB = 0.25
 DEFAULT_AUGMENT_PITCH_SHIFT_SEMITONES = 3
 DEFAULT_AUGMENT_BAND_STOP_PROB = 0.25
+
+# The remaining defaults of the reference's constants.py (TTS, batch threads,
+# the hosted augmentation datasets and the phrase-augmentation words); the
+# values are checked against tests/golden/cli_train_options.json.
+DEFAULT_ADVERSARIAL_PHRASES = 250
+DEFAULT_BATCH_THREADS = 12
+DEFAULT_LISTEN_BUFFER_SIZE = 4096
+DEFAULT_NOISE_BATCH_SIZE = 1000
+DEFAULT_TTS_BATCH_SIZE = 8
+DEFAULT_TTS_SLERP_WEIGHTS = (0.00, 0.25, 0.50, 0.75)
+DEFAULT_TTS_LENGTH_SCALES = (0.75, 1.00, 1.25, 1.50)
+DEFAULT_TTS_NOISE_SCALES = (0.667, 1.0)
+DEFAULT_TTS_NOISE_SCALE_WEIGHTS = (0.8, 1.0)
+DEFAULT_AUGMENT_SAMPLE_RATIO = 1.0
+DEFAULT_IMPULSE_DATASET = "benjamin-paine/mit-impulse-response-survey-16khz"
+DEFAULT_BACKGROUND_DATASET = [
+    "benjamin-paine/free-music-archive-commercial-16khz-full",
+    "benjamin-paine/freesound-laion-640k-commercial-16khz-full",
+]
+DEFAULT_AUGMENT_PHRASE_PROB = 0.75
+DEFAULT_AUGMENT_PHRASE_WORDS = [  # 100 words
+    "can", "where", "who", "what", "when", "why", "how", "is", "are", "do",
+    "will", "would", "should", "could", "may", "might", "please", "tell", "give", "show",
+    "explain", "find", "list", "make", "play", "call", "set", "remind", "start", "stop",
+    "pause", "open", "close", "turn", "begin", "continue", "send", "search", "answer", "read",
+    "repeat", "check", "update", "add", "remove", "delete", "connect", "save", "load", "launch",
+    "bring", "print", "identify", "translate", "record", "forward", "rewind", "increase", "decrease", "switch",
+    "change", "describe", "access", "review", "manage", "organize", "move", "select", "toggle", "control",
+    "copy", "paste", "schedule", "arrange", "integrate", "collaborate", "prepare", "track", "navigate", "compile",
+    "prioritize", "compare", "summarize", "highlight", "visualize", "analyze", "optimize", "clarify", "verify", "monitor",
+    "explore", "enhance", "expand", "customize", "format", "generate", "calculate", "configure", "recommend", "build",
+]

@@ -36,7 +36,7 @@ from typing import Any, List, Optional, Sequence, Tuple, Union
 import numpy as np
 import torch
 
-from heybuddy.constants import (DEFAULT_AUGMENT_BACKGROUND_NOISE_MAX_SNR_DB,
+from heybuddy.constants import (DEFAULT_ADVERSARIAL_PHRASES, DEFAULT_AUGMENT_BACKGROUND_NOISE_MAX_SNR_DB,
                                 DEFAULT_AUGMENT_BACKGROUND_NOISE_MIN_SNR_DB,
                                 DEFAULT_AUGMENT_BACKGROUND_NOISE_PROB,
                                 DEFAULT_AUGMENT_COLORED_NOISE_MAX_F_DECAY,
@@ -46,28 +46,108 @@ from heybuddy.constants import (DEFAULT_AUGMENT_BACKGROUND_NOISE_MAX_SNR_DB,
                                 DEFAULT_AUGMENT_GAIN_PROB, DEFAULT_AUGMENT_REVERB_PROB,
                                 DEFAULT_AUGMENT_TANH_DISTORTION_PROB, DEFAULT_AUGMENT_TANH_MAX_DISTORTION,
                                 DEFAULT_AUGMENT_TANH_MIN_DISTORTION, DEFAULT_EMBEDDING_BATCH_SIZE,
-                                DEFAULT_EMBEDDING_SPECTROGRAM_BATCH_SIZE, DEFAULT_FEATURE_BATCH_SIZE)
+                                DEFAULT_EMBEDDING_SPECTROGRAM_BATCH_SIZE, DEFAULT_FEATURE_BATCH_SIZE,
+                                DEFAULT_AUGMENT_BATCH_SIZE, DEFAULT_AUGMENT_BAND_STOP_PROB,
+                                DEFAULT_AUGMENT_PHRASE_PROB, DEFAULT_AUGMENT_PITCH_SHIFT_PROB,
+                                DEFAULT_AUGMENT_PITCH_SHIFT_SEMITONES, DEFAULT_AUGMENT_SAMPLE_RATIO,
+                                DEFAULT_AUGMENT_SEVEN_BAND_GAIN_DB, DEFAULT_AUGMENT_SEVEN_BAND_PROB,
+                                DEFAULT_BACKGROUND_DATASET, DEFAULT_IMPULSE_DATASET, DEFAULT_TTS_BATCH_SIZE)
 from heybuddy.dataset.augmented import AugmentedAudioGenerator
 from heybuddy.dataset.precalculated import PrecalculatedDatasetIterator
 from heybuddy.util import logger
 
-__all__ = ["TrainingFeaturesGenerator", "SyntheticSpeechGenerator", "safe_name"]
+__all__ = ["TrainingFeaturesGenerator", "SyntheticSpeechGenerator", "safe_name", "synthetic_negative_features"]
 
-# reference constants.py values that only this module uses
-DEFAULT_ADVERSARIAL_PHRASES = 250
-DEFAULT_TTS_BATCH_SIZE = 8
-DEFAULT_AUGMENT_BATCH_SIZE = 8
-DEFAULT_AUGMENT_SAMPLE_RATIO = 1.0
-DEFAULT_AUGMENT_SEVEN_BAND_PROB = 0.25
-DEFAULT_AUGMENT_SEVEN_BAND_GAIN_DB = 6.0
-DEFAULT_AUGMENT_PITCH_SHIFT_PROB = 0.25
-DEFAULT_AUGMENT_PITCH_SHIFT_SEMITONES = 3
-DEFAULT_AUGMENT_BAND_STOP_PROB = 0.25
-DEFAULT_AUGMENT_PHRASE_PROB = 0.75
-DEFAULT_IMPULSE_DATASET = "benjamin-paine/mit-impulse-response-survey-16khz"
-DEFAULT_BACKGROUND_DATASET = ["benjamin-paine/free-music-archive-commercial-16khz-full",
-                              "benjamin-paine/freesound-laion-640k-commercial-16khz-full"]
 SupplementalDatasetType = Any
+
+
+def _gather_rows(local: torch.Tensor, n: int) -> torch.Tensor:
+    """Every rank's contiguous share [clip_range(n, r, W)] of an [n, ...] device
+    tensor, all-gathered (padded to equal sizes: uneven all_gather is not
+    portable across backends) -> the whole [n, ...] on every rank."""
+    import torch.distributed as dist
+    from heybuddy import distributed as hd
+    rank, world = hd.world()
+    sizes = [b - a for a, b in (hd.clip_range(n, r, world) for r in range(world))]
+    m = max(sizes)
+    cpu = dist.get_backend() == "gloo"
+    pad = torch.zeros((m,) + tuple(local.shape[1:]), dtype=local.dtype, device="cpu" if cpu else local.device)
+    pad[:local.shape[0]] = local.to(pad.device)
+    bufs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(bufs, pad)
+    return torch.cat([b[:k] for b, k in zip(bufs, sizes)]).to(local.device)
+
+
+def _sharded(fn, n: int) -> np.ndarray:
+    """fn(m) -> [m, 16, 96] device features; under torch.distributed every
+    rank featurizes its share (numpy's global RNG offset by the rank, so the
+    shards differ) and the shares are all-gathered: the result is the same
+    [n, 16, 96] array on every rank."""
+    from heybuddy import distributed as hd
+    rank, world = hd.world()
+    if world == 1:
+        return fn(n).cpu().numpy()
+    lo, hi = hd.clip_range(n, rank, world)
+    state = np.random.get_state()
+    np.random.seed((int(state[1][0]) + 7919 * (rank + 1)) % (2 ** 32))
+    try:
+        local = fn(hi - lo)
+    finally:
+        np.random.set_state(state)
+    return _gather_rows(local, n).cpu().numpy()
+
+
+def _save_then_open(array: np.ndarray, name: str, directory: str, keep_in_memory: bool = False,
+                    **kwargs: Any) -> PrecalculatedDatasetIterator:
+    """PrecalculatedDatasetIterator.from_array, written by rank 0 only (every
+    rank holds the same array), the other ranks open it after a barrier."""
+    from heybuddy import distributed as hd
+    rank, world = hd.world()
+    if world == 1 or rank == 0:
+        it = PrecalculatedDatasetIterator.from_array(array, name=name, directory=directory,
+                                                     keep_in_memory=keep_in_memory, **kwargs)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+        if rank != 0:
+            it = PrecalculatedDatasetIterator(name, directory=directory, data=array if keep_in_memory else None,
+                                              **kwargs)
+    return it
+
+
+def synthetic_negative_features(name: str, num_samples: int, device_id: Optional[int] = None, seed: int = 0,
+                                directory: Optional[str] = None) -> PrecalculatedDatasetIterator:
+    """Offline stand-in for a hosted negative set (precalculated.py:620-649,
+    a download): ``num_samples`` synthetic tone-burst clips at 0.3 level
+    featurized on the device, stored f16 as ``{directory}/{name}.npy`` (the
+    combine --half layout) and reused while large enough."""
+    from heybuddy import _native
+    from heybuddy.dataset.precalculated import LOCAL_DIR
+    from heybuddy.embeddings import SpeechEmbeddings
+    from heybuddy.synthetic import synthetic_clips
+    directory = directory or LOCAL_DIR
+    try:
+        it = PrecalculatedDatasetIterator(name, directory=directory)
+        if len(it) >= num_samples:
+            return it
+    except FileNotFoundError:
+        pass
+    dev = _native.require_device(device_id)
+    se = SpeechEmbeddings(device_id=dev.index)
+    base = [0]
+
+    def fn(m: int) -> torch.Tensor:
+        parts = []
+        off = int(np.random.randint(0, 2 ** 30))
+        for s in range(0, m, 65536):
+            k = min(65536, m - s)
+            clips = synthetic_clips(k, seed=seed * 1_000_003 + off + s, device=dev).mul_(0.3)
+            parts.append(se.featurize(clips))
+        base[0] += m
+        return torch.cat(parts) if parts else torch.empty((0, 16, 96), device=dev)
+
+    feats = _sharded(fn, num_samples).astype(np.float16)
+    return _save_then_open(feats, name, directory)
 
 
 def safe_name(name: str) -> str:
@@ -297,6 +377,16 @@ class TrainingFeaturesGenerator:
                  for s in sizes]
         return parts[0] if len(parts) == 1 else np.concatenate(parts)
 
+    def call_device(self, num_samples: int, testing: bool = False, validation: bool = False) -> torch.Tensor:
+        """__call__ without the host copy: [num_samples, 16, 96] f32 in HBM."""
+        sizes = [self.sample_batch_size] * math.ceil(num_samples / self.sample_batch_size)
+        if num_samples % self.sample_batch_size:
+            sizes[-1] = num_samples % self.sample_batch_size
+        parts = [self.generate_device(s, testing=testing, validation=validation) for s in sizes]
+        if not parts:
+            return torch.empty((0, 16, 96), dtype=torch.float32, device=self.device)
+        return parts[0] if len(parts) == 1 else torch.cat(parts)
+
     @classmethod
     def default(cls, wake_phrase: str, adversarial: bool = False, num_adversarial_phrases: int = 10,
                 additional_wake_phrases: List[str] = [], custom_adversarial_phrases: List[str] = [],
@@ -307,6 +397,11 @@ class TrainingFeaturesGenerator:
                 augment_impulse_dataset: SupplementalDatasetType = DEFAULT_IMPULSE_DATASET,
                 **kwargs: Any) -> "TrainingFeaturesGenerator":
         """features.py:537-616 (augment_* / embedding_* keywords pass through)."""
+        kwargs.pop("use_cache", None)
+        if augment_background_dataset is None:
+            augment_background_dataset = DEFAULT_BACKGROUND_DATASET
+        if augment_impulse_dataset is None:
+            augment_impulse_dataset = DEFAULT_IMPULSE_DATASET
         return cls(use_autoconfigure=True, tts_text=wake_phrase, tts_adversarial=adversarial,
                    tts_batch_size=tts_batch_size, tts_adversarial_num_phrases=num_adversarial_phrases,
                    tts_adversarial_custom_phrases=custom_adversarial_phrases,
@@ -325,11 +420,12 @@ class TrainingFeaturesGenerator:
                               num_adversarial_phrases: int = 10, additional_wake_phrases: List[str] = [],
                               custom_adversarial_phrases: List[str] = [], testing: bool = False,
                               use_cache: bool = True, save_samples: bool = True, keep_in_memory: bool = False,
-                              directory: Optional[str] = None, **kwargs: Any
+                              directory: Optional[str] = None, device_id: Optional[int] = None, **kwargs: Any
                               ) -> Tuple[PrecalculatedDatasetIterator, PrecalculatedDatasetIterator]:
         """Positive and adversarial feature sets for a phrase, cached by name
         (``{name}.npy``, ``{name}_adv.npy``) and topped up when the cache is
-        short (features.py:618-837)."""
+        short (features.py:618-837). Under torch.distributed each rank
+        featurizes its share of the missing rows; rank 0 writes the cache."""
         from heybuddy.dataset.precalculated import LOCAL_DIR
         directory = directory or LOCAL_DIR
         name = cls.get_wake_phrase_file_name(wake_phrase, testing=testing)
@@ -348,18 +444,18 @@ class TrainingFeaturesGenerator:
                 continue
             gen = cls.default(wake_phrase, adversarial=adversarial, num_adversarial_phrases=num_adversarial_phrases,
                               additional_wake_phrases=additional_wake_phrases,
-                              custom_adversarial_phrases=custom_adversarial_phrases, **kwargs)
-            feats = gen(n - have, testing=testing)
+                              custom_adversarial_phrases=custom_adversarial_phrases, device_id=device_id, **kwargs)
+            feats = _sharded(lambda m: gen.call_device(m, testing=testing), n - have)
             if have:
                 feats = np.concatenate([np.asarray(existing.precalculated), feats])
-            out.append(PrecalculatedDatasetIterator.from_array(feats, name=it_name, directory=directory,
-                                                               keep_in_memory=keep_in_memory))
+            out.append(_save_then_open(feats, it_name, directory, keep_in_memory=keep_in_memory))
         return out[0], out[1]
 
     @classmethod
     def get_validation_features(cls, wake_phrase: str, num_positive_samples: int, use_cache: bool = True,
                                 keep_in_memory: bool = False, augment_target_length: float = 1.44,
-                                directory: Optional[str] = None, **kwargs: Any) -> PrecalculatedDatasetIterator:
+                                directory: Optional[str] = None, device_id: Optional[int] = None,
+                                **kwargs: Any) -> PrecalculatedDatasetIterator:
         """Un-augmented, centre-padded positive features (features.py:840-908)."""
         from heybuddy.dataset.precalculated import LOCAL_DIR
         directory = directory or LOCAL_DIR
@@ -373,9 +469,8 @@ class TrainingFeaturesGenerator:
         have = len(existing) if existing is not None else 0
         if existing is not None and have >= num_positive_samples:
             return existing
-        gen = cls.default(wake_phrase, augment_target_length=augment_target_length)
-        feats = gen(num_positive_samples - have, validation=True)
+        gen = cls.default(wake_phrase, augment_target_length=augment_target_length, device_id=device_id)
+        feats = _sharded(lambda m: gen.call_device(m, validation=True), num_positive_samples - have)
         if have:
             feats = np.concatenate([np.asarray(existing.precalculated), feats])
-        return PrecalculatedDatasetIterator.from_array(feats, name=name, directory=directory,
-                                                       keep_in_memory=keep_in_memory)
+        return _save_then_open(feats, name, directory, keep_in_memory=keep_in_memory)

@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import math
 import os
+import re
 from typing import Any, Callable, Dict, Iterable, Iterator, List, Optional, Tuple
 
 import numpy as np
@@ -33,19 +34,25 @@ import numpy as np
 from heybuddy.util import logger
 
 __all__ = ["LOCAL_DIR", "PrecalculatedDatasetIterator", "PrecalculatedTrainingDatasetGenerator",
-           "PrecalculatedLabeledTrainingDatasetGenerator"]
+           "PrecalculatedLabeledTrainingDatasetGenerator", "HostedPrecalculatedDatasetIterator",
+           "PrecalculatedTrainingDatasetLarge", "PrecalculatedTrainingDatasetMedium", "PrecalculatedValidationDataset"]
 
 LOCAL_DIR = os.path.abspath(os.environ.get("HEYBUDDY_PRECALCULATED_DIR",
                                            os.path.join(os.getcwd(), "precalculated")))
 
 
 class PrecalculatedDatasetIterator:
-    def __init__(self, name: str, directory: str = LOCAL_DIR, exclude_phrase: Optional[str] = None,
+    def __init__(self, name: str, directory: Optional[str] = None, exclude_phrase: Optional[str] = None,
                  ordered: bool = False, labeled: bool = False, use_mem_map: bool = True,
-                 shuffle: bool = True, data: Optional[np.ndarray] = None) -> None:
-        if exclude_phrase is not None:
-            raise NotImplementedError("token exclusion needs the BERT tokenizer download (out of scope)")
-        self.directory = directory
+                 shuffle: bool = True, data: Optional[np.ndarray] = None,
+                 exclude_tokens: Optional[Iterable[int]] = None) -> None:
+        """exclude_phrase (labeled sets, precalculated.py:519-531): rows whose
+        token row shares a token with the phrase are skipped. The reference
+        tokenizes the phrase with bert-base-uncased (a download); here the token
+        ids come from ``exclude_tokens`` (or HEYBUDDY_EXCLUDE_TOKENIZER, a local
+        tokenizer directory); without either the phrase is not excluded (a
+        warning is logged)."""
+        self.directory = directory or LOCAL_DIR  # resolved per call: LOCAL_DIR may be re-pointed
         self.name = name
         self.exclude_phrase = exclude_phrase
         self.index = 0
@@ -57,6 +64,9 @@ class PrecalculatedDatasetIterator:
             self._precalculated = data
         if not os.path.exists(self.precalculated_path):
             raise FileNotFoundError(f"Could not find precalculated features at {self.precalculated_path}.")
+        self.exclude_tokens = set(int(t) for t in exclude_tokens) if exclude_tokens is not None else None
+        if exclude_phrase is not None and labeled and self.exclude_tokens is None:
+            self.exclude_tokens = _phrase_tokens(exclude_phrase)
         if shuffle and not ordered:
             self.shuffle()
 
@@ -77,9 +87,10 @@ class PrecalculatedDatasetIterator:
         return self._indexes
 
     @classmethod
-    def from_array(cls, array: np.ndarray, name: str, directory: str = LOCAL_DIR, ordered: bool = False,
+    def from_array(cls, array: np.ndarray, name: str, directory: Optional[str] = None, ordered: bool = False,
                    keep_in_memory: bool = False) -> "PrecalculatedDatasetIterator":
         """Save ``array`` as ``{directory}/{name}.npy`` and open it (precalculated.py:471-491)."""
+        directory = directory or LOCAL_DIR
         os.makedirs(directory, exist_ok=True)
         np.save(os.path.join(directory, f"{name}.npy"), array)
         return cls(name, directory=directory, data=array if keep_in_memory else None, ordered=ordered)
@@ -100,7 +111,13 @@ class PrecalculatedDatasetIterator:
         else:
             self.index += n
         if self.labeled:
+            if self.exclude_tokens:
+                keep = np.array([self.exclude_tokens.isdisjoint(set(np.asarray(r[-1]).astype(np.int64).ravel()))
+                                 for r in batch], dtype=bool)
+                batch = batch[keep]
             batch = batch[:, :-1]
+            if batch.shape[0] < n:  # refill what the exclusion removed
+                batch = np.concatenate([batch, self.take(n - batch.shape[0])])
         self.total_taken += n
         return batch
 
@@ -113,6 +130,10 @@ class PrecalculatedDatasetIterator:
         import torch
         arr = np.asarray(self.precalculated)
         if self.labeled:
+            if self.exclude_tokens:
+                tok = arr[:, -1].astype(np.int64)
+                keep = ~np.isin(tok, np.fromiter(self.exclude_tokens, np.int64)).any(axis=1)
+                arr = arr[keep]
             arr = arr[:, :-1]
         t = torch.from_numpy(np.ascontiguousarray(arr)).to(device)
         return t if dtype is None else t.to(dtype)
@@ -129,6 +150,60 @@ class PrecalculatedDatasetIterator:
 
     def __repr__(self) -> str:
         return f"{type(self).__name__}(num_samples={len(self)})"
+
+
+def _phrase_tokens(phrase: str) -> Optional[set]:
+    """The phrase's token ids (precalculated.py:398-434: special characters to
+    spaces, BERT uncased), from a local tokenizer directory in
+    HEYBUDDY_EXCLUDE_TOKENIZER; None (and a warning) when there is none."""
+    text = re.sub(r"\s+", " ", re.sub(r"[^a-zA-Z0-9]", " ", phrase.replace("'", ""))).strip()
+    path = os.environ.get("HEYBUDDY_EXCLUDE_TOKENIZER")
+    if path:
+        from transformers import AutoTokenizer
+        tok = AutoTokenizer.from_pretrained(path, local_files_only=True)
+        return set(int(t) for t in tok(text)["input_ids"])
+    logger.warning(f"no local tokenizer (HEYBUDDY_EXCLUDE_TOKENIZER): rows containing {phrase!r} are not excluded")
+    return None
+
+
+class HostedPrecalculatedDatasetIterator(PrecalculatedDatasetIterator):
+    """A hosted feature set (precalculated.py:563-616): labeled, memory-mapped,
+    named after its URL's file. The reference downloads it into the
+    precalculated directory; offline the file must already be there
+    (FileNotFoundError otherwise)."""
+    precalculated_url: str = ""
+    precalculated_ordered: bool = False
+    precalculated_labeled: bool = True
+    precalculated_use_mem_map: bool = True
+
+    @classmethod
+    def file_name(cls) -> str:
+        return cls.precalculated_url.rsplit("/", 1)[-1]
+
+    def __init__(self, directory: Optional[str] = None, exclude_phrase: Optional[str] = None,
+                 exclude_tokens: Optional[Iterable[int]] = None) -> None:
+        super().__init__(name=os.path.splitext(self.file_name())[0], directory=directory,
+                         ordered=self.precalculated_ordered, labeled=self.precalculated_labeled,
+                         exclude_phrase=exclude_phrase, use_mem_map=self.precalculated_use_mem_map,
+                         exclude_tokens=exclude_tokens)
+
+
+_HOSTED = "https://huggingface.co/datasets/benjamin-paine/hey-buddy/resolve/main/precalculated/common/"
+
+
+class PrecalculatedTrainingDatasetLarge(HostedPrecalculatedDatasetIterator):
+    """In-the-wild negatives for training (precalculated.py:618-626)."""
+    precalculated_url = _HOSTED + "training-large.npy"
+
+
+class PrecalculatedTrainingDatasetMedium(HostedPrecalculatedDatasetIterator):
+    """In-the-wild negatives for training (precalculated.py:628-636)."""
+    precalculated_url = _HOSTED + "training-medium.npy"
+
+
+class PrecalculatedValidationDataset(HostedPrecalculatedDatasetIterator):
+    """In-the-wild speech for the validation false-positive rate (precalculated.py:638-649)."""
+    precalculated_url = _HOSTED + "validation.npy"
 
 
 class PrecalculatedTrainingDatasetGenerator:

@@ -14,25 +14,56 @@ from click.testing import CliRunner
 from heybuddy.__main__ import main, safe_name
 from heybuddy.synthetic import phrase_clips
 
-# Options of the reference's `train` on the hot path (__main__.py:171-300).
-REFERENCE_OPTIONS = [
-    "--additional-phrase", "--wandb-entity", "--perceptron", "--transformer", "--use-half-layers",
-    "--use-gating", "--layer-dim", "--num-layers", "--steps", "--stages", "--threshold",
-    "--learning-rate", "--high-loss-threshold", "--target-false-positive-rate",
-    "--dynamic-negative-weight", "--negative-weight", "--augmentation-background-noise-prob",
-    "--augmentation-background-noise-min-snr-db", "--augmentation-background-noise-max-snr-db",
-    "--augmentation-reverb-prob", "--augmentation-gain-prob", "--logging-steps", "--validation-steps", "--checkpoint-steps",
-    "--positive-samples", "--adversarial-samples", "--positive-batch-size", "--negative-batch-size",
-    "--adversarial-batch-size", "--validation-samples", "--testing-positive-samples",
-    "--testing-adversarial-samples", "--resume", "--debug",
-]
+GOLDEN_OPTIONS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "cli_train_options.json")
+
+
+def _train_params():
+    from heybuddy.__main__ import train
+    out = {}
+    for p in train.params:
+        for f in list(p.opts) + list(p.secondary_opts):
+            out[f] = p
+    return out
+
+
+def test_train_has_every_reference_option_with_its_default():
+    """The reference's `train` surface (__main__.py:171-244), read from its
+    decorators into tests/golden/cli_train_options.json (oracle/make_cli_fixture.py):
+    every flag, the same destination for the architecture / dataset-size flag
+    groups, and the same default (expressions over DEFAULT_* evaluated against
+    this package's constants, which must equal the reference's values)."""
+    import json
+    import heybuddy.constants as C
+    gold = json.load(open(GOLDEN_OPTIONS))
+    for name, val in gold["constants"].items():
+        mine = getattr(C, name)
+        assert (list(mine) if isinstance(mine, tuple) else mine) == val, name
+    params = _train_params()
+    from heybuddy.__main__ import train
+    assert [p.name for p in train.params if p.param_type_name == "argument"] == gold["arguments"]
+    for opt in gold["options"]:
+        for flag in opt["flags"]:
+            for f in flag.split("/"):
+                assert f in params, f
+        p = params[opt["flags"][0].split("/")[0]]
+        if opt["dest"]:
+            assert p.name == opt["dest"], (opt["flags"], p.name)
+        if opt["flag_value"] is not None:
+            assert p.flag_value == opt["flag_value"], opt["flags"]
+        assert bool(p.multiple) == opt["multiple"], opt["flags"]
+        if opt["default"] is not None and opt["flag_value"] is None:
+            want = eval(opt["default"], {"__builtins__": {}}, vars(C))
+            got = p.default
+            assert got == want or (got is None and want is None), (opt["flags"], got, want)
+        if opt["flag_value"] is not None:  # the group's default member
+            want = eval(opt["default"], {"__builtins__": {}}, vars(C))
+            assert bool(p.default) == bool(want), opt["flags"]
 
 
 def test_train_help_lists_reference_options():
     res = CliRunner().invoke(main, ["train", "--help"])
     assert res.exit_code == 0, res.output
-    for opt in REFERENCE_OPTIONS:
-        assert opt in res.output, opt
+    assert "--augmentation-tanh-distortion-min" in res.output and "--training-no-default-dataset" in res.output
 
 
 def test_safe_name():
@@ -51,11 +82,13 @@ def test_phrase_clips_deterministic_and_distinct():
 
 
 @pytest.mark.gpu
-def test_train_cli_short_run(tmp_path):
+def test_train_cli_short_run(tmp_path, monkeypatch):
     ckpt = tmp_path / "ckpt"
+    from heybuddy.dataset import precalculated as pc
+    monkeypatch.setattr(pc, "LOCAL_DIR", str(tmp_path / "precalculated"))  # feature cache + offline negatives
     args = ["train", "hey buddy", "--steps", "40", "--stages", "2", "--validation-steps", "20",
             "--checkpoint-steps", "40", "--positive-samples", "3000", "--adversarial-samples", "3000",
-            "--negative-samples", "6000", "--validation-samples", "2000",
+            "--negative-samples", "6000", "--validation-negative-samples", "2000", "--validation-samples", "500",
             "--testing-positive-samples", "1000", "--testing-adversarial-samples", "1000",
             "--logging-steps", "20", "--checkpoint-dir", str(ckpt), "--seed", "5"]
     res = CliRunner().invoke(main, args, catch_exceptions=False)
@@ -63,6 +96,14 @@ def test_train_cli_short_run(tmp_path):
     files = os.listdir(ckpt)
     assert any(f.startswith("hey_buddy") and f.endswith(".pt") and not f.endswith("_optimizer.pt")
                for f in files), files
+    # the reference's feature caches (features.py:686-760): positives, adversarials, testing, validation
+    cached = set(os.listdir(pc.LOCAL_DIR))
+    for f in ("hey_buddy.npy", "hey_buddy_adv.npy", "hey_buddy_tst.npy", "hey_buddy_tst_adv.npy", "hey_buddy_val.npy",
+              "synthetic-large.npy", "synthetic-medium.npy", "synthetic-validation.npy"):
+        assert f in cached, (f, cached)
+    import numpy as np
+    assert np.load(os.path.join(pc.LOCAL_DIR, "hey_buddy.npy"), mmap_mode="r").shape == (3000, 16, 96)
+    assert np.load(os.path.join(pc.LOCAL_DIR, "hey_buddy_val.npy"), mmap_mode="r").shape == (500, 16, 96)
 
 
 def test_combine_half_and_delete(tmp_path):
