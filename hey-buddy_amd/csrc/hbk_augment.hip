@@ -1384,45 +1384,47 @@ __global__ void __launch_bounds__(64) eq_kernel(EqArgs a) {
 // istft -> sinc resample (torchaudio Resample(sr, int(sr / shift))), cropped or
 // zero-padded to the clip length. One ratio per call (per_batch mode).
 //
-// Frame spectra are computed by a sliding DFT (hop 7: seven samples enter and
-// leave per frame, O(bins) per frame instead of an FFT), restarted by a direct
-// DFT every kPsRestart frames; an all-zero frame is exactly zero (angle 0) as in
-// the FFT. The istft needs no per-frame inverse transform either: with Z_t[k] =
-// Y_t[k] e^{-2 pi i k 7 t / 250}, sample p of the overlap-add is
-//   (1/250) sum_k c_k Re(e^{2 pi i k p / 250} W_p[k]),  W_p = sum of Z_t over the
-// <= 36 frames covering p, a sliding window sum per bin.
-// No spectrogram is stored: both passes slide the DFT over their own frames
-// from the clip samples in LDS (a frame depends on its index alone, see PsFrames).
-//   ps_phase_sum_kernel  (segment of 128 input frames, clip): sums of the vocoder's
-//                        phase increments of the output frames whose source frame
-//                        is in the segment (all, and the last 35)
-//   ps_synth_kernel      (segment, clip): prefix phase (f64) from those sums, the
-//                        vocoder frames, the windowed sums, a bin reduction
-//                        through LDS -> istft samples
-//   ps_resample_kernel   (frame group, clip): polyphase sinc, taps in registers
+// ps_vocoder_kernel: ONE pass per clip, 128 lanes = 126 bins, sequential over
+// the clip's frames (kPvClips clips per workgroup in lockstep: every clip of a
+// call has the same frame geometry). No spectrogram is stored, no segment is
+// recomputed:
+//  * analysis: a sliding DFT in float64 (hop 7: X_f = w^-7 (X_{f-1} + sum_j d_j
+//    w^j), d_j = xp[7f+243+j] - xp[7f-7+j] exact in f64, w = e^{-2 pi i k/250});
+//    float64 keeps the recursion's error at ~1e-16 of the clip's level, so it
+//    is never restarted, and a frame whose 250 samples are all zero is exactly
+//    0 (angle 0) as in the FFT (a running count of non-zero samples);
+//  * vocoder: the phase in revolutions, accR_{t+1} = accR_t + wrap((a1 - a0) /
+//    2 pi - 7k/250): the phase advance adv_k = 2 pi 7k/250 cancels against the
+//    istft's frame rotation, so Z_t = Y_t e^{-2 pi i 7kt/250} = m_t e^{2 pi i accR_t};
+//  * synthesis without inverse transforms: with Q_t = sum_{t' <= t} Z_t' (a
+//    prefix per bin) and G(t, s) = Re sum_k c_k e^{2 pi i k (7t + s)/250} Q_t[k],
+//    s < 9, the overlap-added istft sample p = 7t + r is
+//      (G(t, r) - G(t - 36, r + 2)) / (250 env)   r <= 4 (frames t-35 .. t)
+//      (G(t, r) - G(t - 35, r - 5)) / (250 env)   r = 5, 6 (frames t-34 .. t)
+//    so a bin keeps no window of past frames: per frame it stages
+//    V_t = c_k Q_t e^{2 pi i 7kt/250} in LDS, and every kPvGroup frames the
+//    workgroup reduces the 9 x kPvGroup G values over the bins (packed f32 FMAs).
+// ps_resample_kernel (frame group, clip): polyphase sinc, taps in registers.
 constexpr int kPsFft = 250, kPsHop = 7, kPsBins = kPsFft / 2 + 1, kPsPad = kPsFft / 2;
-constexpr int kPsSeg = 128;                            // input frames per segment
-constexpr int kPsRestart = 64;                         // direct DFT at every 64th frame (absolute index)
-constexpr int kPsWin = (kPsFft + kPsHop - 1) / kPsHop;  // 36 frames cover a sample
-constexpr int kPsChunk = 2;                            // output frames per bin reduction
 constexpr int kPsTapMax = HBK_PITCH_SHIFT_MAX_TAPS;    // 2 width + orig (142 / 139 at 16 kHz)
 constexpr int kPsPhaseMax = 128;                       // new (resampler phases)
 constexpr int kPsResFrames = 32;                       // resampler frames per workgroup
-constexpr int kPsLd = 128;                             // bins per row of the phase sums (126 used)
-constexpr int kPsFrames = 240;                         // input frames a workgroup may touch
-constexpr int kPsXs = kPsHop * (kPsFrames - 1) + kPsFft;
+constexpr int kPvClips = 4;                            // clips per workgroup (128 lanes each)
+constexpr int kPvGroup = 7;                            // output frames per bin reduction
+constexpr int kPvRows = 64;                            // input frames of d rows held in LDS
+constexpr int kPvGh = 64;                              // ring of G(t, .) rows (>= 36 + kPvGroup)
+constexpr int kPvLd = 130;                             // LDS row pitch (float2) of the bin rows
 
 struct PitchArgs {
   const float* x;
   int64_t x_stride;
   const int32_t* idx;
+  int n;
   float* out;
   int64_t out_stride;
-  int L, f_in, f_out, l1, nseg, orig, nw, width, target;
+  int L, f_in, f_out, l1, orig, nw, width, target;
   double rate;
-  double* segsum; // [n][nseg][kPsLd]: phase increments of the segment's output frames (+ angle of frame 0 in 0)
-  double* osum;   // [n][nseg][kPsLd]: ... of its last kPsWin - 1 output frames
-  float* y;       // [n][l1]
+  float* y;       // [n][l1]: istft output (resampler input)
   float* taps;    // [nw][kPsTapMax]
 };
 
@@ -1432,100 +1434,6 @@ __device__ __forceinline__ int ps_i0(const PitchArgs& a, int t, float& alpha) {
   const float fl = floorf(ts);
   alpha = ts - fl;
   return static_cast<int>(fl);
-}
-
-// first output frame whose source frame i0 is >= f
-__device__ int ps_first_t(const PitchArgs& a, int f) {
-  if (f <= 0) return 0;
-  int t = max(0, static_cast<int>(static_cast<double>(f) / a.rate) - 2);
-  float al;
-  while (t < a.f_out && ps_i0(a, t, al) < f) ++t;
-  return t;
-}
-
-// the vocoder's phase increment between source frames with angles a0, a1 (bin k)
-__device__ __forceinline__ double ps_phase(float a0, float a1, int k) {
-  const double adv = (M_PI * kPsHop) * k / (kPsBins - 1);
-  double ph = static_cast<double>(a1) - static_cast<double>(a0) - adv;
-  ph -= (2.0 * M_PI) * rint(ph * (0.5 / M_PI));
-  return ph + adv;
-}
-
-__device__ __forceinline__ void ps_twiddles(float2* tw) {
-  for (int q = threadIdx.x; q < kPsFft; q += blockDim.x) {
-    double s, c;
-    sincospi(2.0 * q / kPsFft, &s, &c);
-    tw[q] = make_float2(static_cast<float>(c), static_cast<float>(s));
-  }
-}
-
-// Frames [fb, fe] of one clip in LDS: the reflect-padded samples and the
-// all-zero flags. Every frame is a function of its index alone (direct DFT at
-// multiples of kPsRestart, slides in between), so both kernels see identical
-// spectra. fb must be a multiple of kPsRestart, fe - fb < kPsFrames.
-struct PsFrames {
-  const float* xs;
-  const int* zf;
-  const float2* tw;
-  float2 rot;
-  int k, fb, f_in;
-  // X_f from X_{f-1} (xr, xi)
-  __device__ __forceinline__ void next(int f, float& xr, float& xi) const {
-    if (f >= f_in) {  // the vocoder's zero frames past the end
-      xr = xi = 0.f;
-      return;
-    }
-    const float* xf = xs + kPsHop * (f - fb);
-    if (f % kPsRestart == 0) {  // X = sum_n x[n] e^{-2 pi i k n / 250}
-      float re = 0.f, im = 0.f;
-      int q = 0;
-      for (int j = 0; j < kPsFft; ++j) {
-        const float v = xf[j];
-        const float2 w = tw[q];
-        re = fmaf(v, w.x, re);
-        im = fmaf(-v, w.y, im);
-        q += k;
-        q -= q >= kPsFft ? kPsFft : 0;
-      }
-      xr = re;
-      xi = im;
-    } else {  // X_f = e^{2 pi i k 7 / 250} (X_{f-1} + sum_j (x_in[j] - x_out[j]) e^{-2 pi i k j / 250})
-      float dr = 0.f, di = 0.f;
-      int q = 0;
-#pragma unroll
-      for (int j = 0; j < kPsHop; ++j) {
-        const float d = xf[kPsFft - kPsHop + j] - xf[j - kPsHop];
-        const float2 w = tw[q];
-        dr = fmaf(d, w.x, dr);
-        di = fmaf(-d, w.y, di);
-        q += k;
-        q -= q >= kPsFft ? kPsFft : 0;
-      }
-      const float ar = xr + dr, ai = xi + di;
-      xr = ar * rot.x - ai * rot.y;
-      xi = ar * rot.y + ai * rot.x;
-    }
-    if (!zf[f - fb]) xr = xi = 0.f;
-  }
-};
-
-__device__ __forceinline__ void ps_load_frames(const PitchArgs& a, const float* x, int fb, int fe, float* xs,
-                                               int* zf) {
-  const int nq = kPsHop * (fe - fb) + kPsFft;
-  for (int q = threadIdx.x; q < nq; q += blockDim.x) {  // reflect padding by n_fft / 2
-    int i = kPsHop * fb + q - kPsPad;
-    i = i < 0 ? -i : i;
-    i = i >= a.L ? 2 * (a.L - 1) - i : i;
-    xs[q] = x[i];
-  }
-  __syncthreads();
-  for (int f = threadIdx.x; f <= fe - fb; f += blockDim.x) {
-    const float* xf = xs + kPsHop * f;
-    bool any = false;
-    for (int j = 0; j < kPsFft; ++j) any |= xf[j] != 0.f;
-    zf[f] = any;
-  }
-  __syncthreads();
 }
 
 // atan2 for the vocoder's angles: a degree-15 odd polynomial for atan on [0, 1]
@@ -1550,172 +1458,224 @@ __device__ __forceinline__ float ps_atan2(float y, float x) {
   return copysignf(r, y);
 }
 
-// a frame producer: (X, angle, |X|) of the current source frame c and of c + 1
-struct PsCursor {
-  float cr, ci, ca, cm;  // frame c
-  float nr, ni, na, nm;  // frame c + 1
-  int c;
-  // frames F.fb .. i slid without their angles, then frames i and i + 1
-  __device__ __forceinline__ void seek(const PsFrames& F, int i) {
-    F.next(F.fb, cr, ci);
-    for (int f = F.fb + 1; f <= i; ++f) F.next(f, cr, ci);
-    c = i;
-    nr = cr;
-    ni = ci;
-    F.next(c + 1, nr, ni);
-    ca = ps_atan2(ci, cr);
-    cm = sqrtf(cr * cr + ci * ci);
-    na = ps_atan2(ni, nr);
-    nm = sqrtf(nr * nr + ni * ni);
-  }
-  __device__ __forceinline__ void advance_to(const PsFrames& F, int i0) {
-    while (c < i0) {
-      ++c;
-      cr = nr;
-      ci = ni;
-      ca = na;
-      cm = nm;
-      F.next(c + 1, nr, ni);
-      na = ps_atan2(ni, nr);
-      nm = sqrtf(nr * nr + ni * ni);
-    }
-  }
+struct PvClip {
+  double d[kPvRows][8];       // row f - fb: d_j (j < 7) of frame f, [7] = the non-zero-count change
+  cf v[kPvGroup][kPvLd];      // V_t[k] of the group's frames (k >= 126: 0)
+  float gh[kPvGh][9];         // G(t, s), row t mod kPvGh
+  float xs[256];              // xp[0, 250) (frame 0's direct DFT)
+  int cnt0;
+};
+struct PvShared {
+  cf et[9][kPvLd];            // e^{+2 pi i k s / 250}
+  cf tw[256];                 // e^{+2 pi i q / 250}
+  double tw64[256][2];        // e^{-2 pi i q / 250}, float64
+  PvClip c[kPvClips];
 };
 
-__global__ void __launch_bounds__(128) ps_phase_sum_kernel(PitchArgs a) {
-  __shared__ float2 tw[kPsFft];
-  __shared__ float xs[kPsXs];
-  __shared__ int zf[kPsFrames];
-  const int k = threadIdx.x, s = blockIdx.x, e = blockIdx.y;
-  ps_twiddles(tw);
-  const int f0 = s * kPsSeg, fe = min(f0 + kPsSeg, a.f_in - 1);
-  ps_load_frames(a, a.x + static_cast<int64_t>(a.idx[e]) * a.x_stride, f0, fe, xs, zf);
-  const int t0 = ps_first_t(a, f0);
-  const int t1 = s + 1 < a.nseg ? ps_first_t(a, f0 + kPsSeg) : a.f_out;
-  const int kq = min(k, kPsBins - 1);
-  PsFrames F{xs, zf, tw, tw[(kPsHop * kq) % kPsFft], kq, f0, a.f_in};
-  PsCursor cur;
-  cur.seek(F, f0);
-  double acc = s == 0 ? static_cast<double>(cur.ca) : 0.0, osum = 0.0;
-  for (int t = t0; t < t1; ++t) {
-    float al;
-    cur.advance_to(F, ps_i0(a, t, al));
-    const double ph = ps_phase(cur.ca, cur.na, kq);
-    acc += ph;
-    if (t >= t1 - (kPsWin - 1)) osum += ph;
-  }
-  const int64_t o = (static_cast<int64_t>(e) * a.nseg + s) * kPsLd + k;
-  a.segsum[o] = k < kPsBins ? acc : 0.0;
-  a.osum[o] = k < kPsBins ? osum : 0.0;
+// padded sample p of clip row xr (reflect padding by n_fft / 2)
+__device__ __forceinline__ float ps_xp(const float* xr, int L, int p) {
+  int i = p - kPsPad;
+  i = i < 0 ? -i : i;
+  i = i >= L ? 2 * (L - 1) - i : i;
+  return xr[i];
 }
 
-__global__ void __launch_bounds__(128, 4) ps_synth_kernel(PitchArgs a) {
-  __shared__ float2 tw[kPsFft];
-  __shared__ float cb[kPsChunk * kPsHop][kPsLd + 1];
-  __shared__ float xs[kPsXs];
-  __shared__ int zf[kPsFrames];
-  const int k = threadIdx.x, s = blockIdx.x, e = blockIdx.y;
-  ps_twiddles(tw);
-  const int t_lo = ps_first_t(a, s * kPsSeg);
-  const bool last = s + 1 == a.nseg;
-  const int t_hi = last ? a.f_out : ps_first_t(a, (s + 1) * kPsSeg);
-  // samples p = 7 j + r of this segment: j in [t_lo, j_end); the last segment
-  // runs past the last frame to the last istft sample (p = n_fft/2 + l1 - 1)
-  const int j_end = last ? (a.l1 + kPsPad - 1) / kPsHop + 1 : t_hi;
-  const int t_a = s == 0 ? 0 : t_lo - (kPsWin - 1);
-  float al;
-  const int i_a = ps_i0(a, t_a, al);
-  const int fb = i_a - i_a % kPsRestart;
-  const int fe = min(ps_i0(a, min(j_end, a.f_out) - 1, al) + 1, a.f_in - 1);
-  ps_load_frames(a, a.x + static_cast<int64_t>(a.idx[e]) * a.x_stride, fb, fe, xs, zf);
-  const int kq = min(k, kPsBins - 1);
-  PsFrames F{xs, zf, tw, tw[(kPsHop * kq) % kPsFft], kq, fb, a.f_in};
-  PsCursor cur;
-  cur.seek(F, i_a);
-  // accumulated phase of frame t_a (float64: |acc| reaches 7e4 rad)
-  double acc = 0.0;
-  if (s == 0) {
-    acc = cur.ca;
-  } else {
-    const double* ss = a.segsum + static_cast<int64_t>(e) * a.nseg * kPsLd + k;
-    for (int q = 0; q < s; ++q) acc += ss[q * kPsLd];
-    acc -= a.osum[(static_cast<int64_t>(e) * a.nseg + s - 1) * kPsLd + k];
+// rows [fb, fb + kPvRows) of every clip of the workgroup (frames >= f_in: zero rows)
+__device__ __forceinline__ void pv_load_rows(const PitchArgs& a, PvShared& sh, const float* xr, int cl, int lane,
+                                             int fb) {
+  for (int q = lane; q < 2 * kPvRows; q += 128) {
+    const int row = q >> 1, h = q & 1, f = fb + row;
+    double* dr = sh.c[cl].d[row];
+    if (f >= a.f_in) {
+      for (int j = 4 * h; j < 4 * h + 4; ++j) dr[j] = 0.0;
+      continue;
+    }
+    if (h == 0) {
+      for (int j = 0; j < 4; ++j)
+        dr[j] = static_cast<double>(ps_xp(xr, a.L, 7 * f + 243 + j)) - static_cast<double>(ps_xp(xr, a.L, 7 * f - 7 + j));
+    } else {
+      int delta = 0;
+      for (int j = 0; j < 7; ++j) {
+        const float vin = ps_xp(xr, a.L, 7 * f + 243 + j), vout = ps_xp(xr, a.L, 7 * f - 7 + j);
+        delta += (vin != 0.f) - (vout != 0.f);
+        if (j >= 4) dr[j] = static_cast<double>(vin) - static_cast<double>(vout);
+      }
+      dr[7] = static_cast<double>(delta);
+    }
   }
-  const float ck = (k == 0 || k == kPsBins - 1) ? 1.f : (k < kPsBins ? 2.f : 0.f);
-  float wr = 0.f, wi = 0.f;
-  int row = 0, jc = t_lo;
-  // qz = k 7 t mod 250: Z_t = Y_t e^{-2 pi i qz / 250}, and sample p = 7 t + r
-  // takes e^{+2 pi i (qz + k r) / 250}
-  int qz = (kq * ((kPsHop * t_a) % kPsFft)) % kPsFft;
-  const int dq = (kPsHop * kq) % kPsFft;
+}
+
+__global__ void __launch_bounds__(128 * kPvClips) ps_vocoder_kernel(PitchArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char pv_smem[];
+  PvShared& sh = *reinterpret_cast<PvShared*>(pv_smem);
+  const int tid = threadIdx.x, cl = tid >> 7, lane = tid & 127;
+  const int e = min(static_cast<int>(blockIdx.x) * kPvClips + cl, a.n - 1);  // padding slots repeat the last clip
+  const bool live = static_cast<int>(blockIdx.x) * kPvClips + cl < a.n;
+  const float* xr = a.x + static_cast<int64_t>(a.idx[e]) * a.x_stride;
+  PvClip& C = sh.c[cl];
+  // tables
+  for (int q = tid; q < 256; q += blockDim.x) {
+    double sn, cs;
+    sincospi(2.0 * q / kPsFft, &sn, &cs);
+    sh.tw[q] = cf{static_cast<float>(cs), static_cast<float>(sn)};
+    sh.tw64[q][0] = cs;
+    sh.tw64[q][1] = -sn;
+  }
+  for (int q = tid; q < 9 * kPvLd; q += blockDim.x) {
+    const int s = q / kPvLd, k = q % kPvLd;
+    double sn, cs;
+    sincospi(2.0 * ((k * s) % kPsFft) / kPsFft, &sn, &cs);
+    sh.et[s][k] = k < kPsBins ? cf{static_cast<float>(cs), static_cast<float>(sn)} : cf{0.f, 0.f};
+  }
+  if (lane == 0) C.cnt0 = 0;
+  __syncthreads();
+  int nz = 0;
+  for (int q = lane; q < kPsFft; q += 128) {
+    const float v = ps_xp(xr, a.L, q);
+    C.xs[q] = v;
+    nz += v != 0.f;
+  }
+  if (nz) atomicAdd(&C.cnt0, nz);
+  int fb = 1;
+  pv_load_rows(a, sh, xr, cl, lane, fb);
+  __syncthreads();
+
+  const int k = min(lane, kPsBins - 1);
+  // per-bin constants: w^j (j < 7) and w^-7 in float64, the synthesis weight
+  double wr[7], wi[7];
+#pragma unroll
+  for (int j = 0; j < 7; ++j) {
+    const int q = (k * j) % kPsFft;
+    wr[j] = sh.tw64[q][0];
+    wi[j] = sh.tw64[q][1];
+  }
+  const int q7 = (7 * k) % kPsFft;
+  const double rr = sh.tw64[q7][0], ri = -sh.tw64[q7][1];
+  const float ck = lane < kPsBins ? ((lane == 0 || lane == kPsBins - 1) ? 1.f : 2.f) : 0.f;
+  const double kadv = static_cast<double>(7 * k) / kPsFft;  // the phase advance, in revolutions
+  // frame 0: direct DFT (float64)
+  double xre = 0.0, xim = 0.0;
+  {
+    int q = 0;
+    for (int n = 0; n < kPsFft; ++n) {
+      const double v = static_cast<double>(C.xs[n]);
+      xre = fma(v, sh.tw64[q][0], xre);
+      xim = fma(v, sh.tw64[q][1], xim);
+      q += k;
+      q -= q >= kPsFft ? kPsFft : 0;
+    }
+  }
+  int cnt = C.cnt0;
+  if (cnt == 0) xre = xim = 0.0;
+  int sf = 0;  // last slid frame
+  // slide to frame sf + 1 (its d row must be resident)
+  auto slide = [&]() {
+    ++sf;
+    if (sf >= a.f_in) {
+      xre = xim = 0.0;
+      return;
+    }
+    const double* dr = C.d[sf - fb];
+    double dre = 0.0, dim = 0.0;
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      dre = fma(dr[j], wr[j], dre);
+      dim = fma(dr[j], wi[j], dim);
+    }
+    cnt += static_cast<int>(dr[7]);
+    const double ar = xre + dre, ai = xim + dim;
+    xre = ar * rr - ai * ri;
+    xim = ar * ri + ai * rr;
+    if (cnt == 0) xre = xim = 0.0;
+  };
+  auto polar = [&](float& ang, float& mag) {
+    const float fr = static_cast<float>(xre), fi = static_cast<float>(xim);
+    ang = ps_atan2(fi, fr);
+    mag = sqrtf(fmaf(fr, fr, fi * fi));
+  };
+  float ca, cm, na, nm;
+  polar(ca, cm);
+  slide();
+  polar(na, nm);
+  int c = 0;  // frames c and c + 1 = sf are in (ca, cm), (na, nm)
+  double accR = static_cast<double>(ca) * (0.5 / M_PI);
+  cf Q = {0.f, 0.f};
+  int qz = 0;
+  const int dq = q7;
+  const int jmax = (a.l1 + kPsPad - 1) / kPsHop;  // the frame of the last istft sample
   float* y = a.y + static_cast<int64_t>(e) * a.l1;
-  // this bin's last kPsWin vocoder frames Z in registers, oldest first (a
-  // shift per frame keeps every index static)
-  float2 zq[kPsWin];
-#pragma unroll
-  for (int u = 0; u < kPsWin; ++u) zq[u] = make_float2(0.f, 0.f);
-  for (int t = t_a; t < j_end; ++t) {
+
+  for (int t0 = 0; t0 <= jmax; t0 += kPvGroup) {
+    // the group's source frames must be resident: refill the d rows from the next unslid frame
     {
-      float zr = 0.f, zi = 0.f;
+      float al;
+      const int tl = min(t0 + kPvGroup - 1, a.f_out - 1);
+      const int need = t0 < a.f_out ? min(ps_i0(a, tl, al) + 1, a.f_in - 1) : 0;
+      if (need >= fb + kPvRows) {  // uniform across the workgroup
+        __syncthreads();
+        fb = sf + 1;
+        pv_load_rows(a, sh, xr, cl, lane, fb);
+        __syncthreads();
+      }
+    }
+    for (int u = 0; u < kPvGroup; ++u) {
+      const int t = t0 + u;
       if (t < a.f_out) {
-        cur.advance_to(F, ps_i0(a, t, al));
-        const float m = al * cur.nm + (1.f - al) * cur.cm;
-        const double th = acc - (2.0 * M_PI) * rint(acc * (0.5 / M_PI));
-        float sn, cs;
-        __sincosf(static_cast<float>(th), &sn, &cs);
-        const float2 w = tw[qz];
-        const float yr = m * cs, yi = m * sn;
-        zr = yr * w.x + yi * w.y;
-        zi = yi * w.x - yr * w.y;
-        acc += ps_phase(cur.ca, cur.na, kq);
-      }
-      wr += zr - zq[0].x;  // Z_{t-36} leaves the window
-      wi += zi - zq[0].y;
-#pragma unroll
-      for (int u = 0; u + 1 < kPsWin; ++u) zq[u] = zq[u + 1];
-      zq[kPsWin - 1] = make_float2(zr, zi);
-      if (t >= t_lo) {
-        const float z35r = zq[0].x, z35i = zq[0].y;  // Z_{t-35}
-        int q = qz;
-        const float cwr = ck * wr, cwi = ck * wi, cvr = ck * (wr - z35r), cvi = ck * (wi - z35i);
-#pragma unroll
-        for (int r = 0; r < kPsHop; ++r) {
-          // frames t-35 .. t cover p = 7 t + r for r <= 4, t-34 .. t for r = 5, 6
-          const float vr = r <= 4 ? cwr : cvr, vi = r <= 4 ? cwi : cvi;
-          const float2 w = tw[q];
-          cb[row * kPsHop + r][k] = w.x * vr - w.y * vi;
-          q += kq;
-          q -= q >= kPsFft ? kPsFft : 0;
+        float al;
+        const int i0 = ps_i0(a, t, al);
+        while (c < i0) {
+          ++c;
+          ca = na;
+          cm = nm;
+          slide();
+          polar(na, nm);
         }
-        ++row;
-        if (row == kPsChunk || t == j_end - 1) {
-          __syncthreads();
-          // two lanes per sample row (63 bins each), combined by a lane swap
-          const int rw = k >> 1, h = k & 1;
-          float part = 0.f;
-          if (rw < row * kPsHop) {
-            const float* c = cb[rw] + h * 63;
-#pragma unroll 9
-            for (int b = 0; b < 63; ++b) part += c[b];
-          }
-          part += __shfl_xor(part, 1);
-          if (h == 0 && rw < row * kPsHop) {
-            const int p = kPsHop * jc + rw;
-            const int m = p - kPsPad;
-            if (m >= 0 && m < a.l1) {
-              const int j = p / kPsHop;
-              const int lo = max(0, j - (kPsWin - 1) + (p % kPsHop >= 5 ? 1 : 0));
-              const int hi = min(a.f_out - 1, j);
-              y[m] = part / (static_cast<float>(kPsFft) * static_cast<float>(hi - lo + 1));
-            }
-          }
-          __syncthreads();
-          row = 0;
-          jc = t + 1;
-        }
+        const float m = fmaf(al, nm - cm, cm);
+        const double fr = accR - rint(accR);
+        const float frf = static_cast<float>(fr);
+        const float sn = __builtin_amdgcn_sinf(frf), cs = __builtin_amdgcn_cosf(frf);
+        Q += cf{m * cs, m * sn};
+        double inc = (static_cast<double>(na) - static_cast<double>(ca)) * (0.5 / M_PI) - kadv;
+        inc -= rint(inc);
+        accR += inc;
       }
+      C.v[u][lane] = ck * cmul(Q, sh.tw[qz]);
       qz += dq;
       qz -= qz >= kPsFft ? kPsFft : 0;
+    }
+    __syncthreads();
+    // G(t, s) of the group: 63 values, two lanes each (bins [0, 64) and [64, 128))
+    if (lane < 2 * 9 * kPvGroup) {
+      const int o = lane >> 1, h = lane & 1, u = o / 9, s = o % 9;
+      const float4* vp = reinterpret_cast<const float4*>(&C.v[u][64 * h]);
+      const float4* ep = reinterpret_cast<const float4*>(&sh.et[s][64 * h]);
+      cf acc0 = {0.f, 0.f}, acc1 = {0.f, 0.f};
+#pragma unroll 8
+      for (int i = 0; i < 32; ++i) {
+        const float4 v4 = vp[i], e4 = ep[i];
+        acc0 = __builtin_elementwise_fma(cf{v4.x, v4.y}, cf{e4.x, e4.y}, acc0);
+        acc1 = __builtin_elementwise_fma(cf{v4.z, v4.w}, cf{e4.z, e4.w}, acc1);
+      }
+      float g = (acc0.x - acc0.y) + (acc1.x - acc1.y);
+      g += __shfl_xor(g, 1);
+      if (h == 0) C.gh[(t0 + u) % kPvGh][s] = g;
+    }
+    __syncthreads();
+    // the group's istft samples p = 7 t + r
+    if (lane < kPsHop * kPvGroup && live) {
+      const int t = t0 + lane / kPsHop, r = lane % kPsHop;
+      const int m = kPsHop * t + r - kPsPad;
+      if (t <= jmax && m >= 0 && m < a.l1) {
+        const float g1 = C.gh[t % kPvGh][r];
+        float g2 = 0.f;
+        if (r <= 4) {
+          if (t >= 36) g2 = C.gh[(t - 36) % kPvGh][r + 2];
+        } else if (t >= 35) {
+          g2 = C.gh[(t - 35) % kPvGh][r - 5];
+        }
+        const int lo = max(0, t - 35 + (r >= 5 ? 1 : 0)), hi = min(a.f_out - 1, t);
+        y[m] = (g1 - g2) / (static_cast<float>(kPsFft) * static_cast<float>(hi - lo + 1));
+      }
     }
   }
 }
@@ -2101,7 +2061,6 @@ static int ps_geometry(int64_t L, int32_t sample_rate, int32_t num, int32_t den,
   a.f_in = 1 + a.L / kPsHop;
   a.f_out = static_cast<int>(std::ceil(double(a.f_in) / a.rate));
   a.l1 = kPsHop * (a.f_out - 1);
-  a.nseg = (a.f_in + kPsSeg - 1) / kPsSeg;
   const int64_t new_sr = int64_t(sample_rate) * den / num;
   const int64_t g = std::gcd(int64_t(sample_rate), new_sr);
   if (new_sr <= 0 || g <= 0) return arg_error("shift out of range");
@@ -2109,8 +2068,9 @@ static int ps_geometry(int64_t L, int32_t sample_rate, int32_t num, int32_t den,
   a.nw = static_cast<int>(new_sr / g);
   a.width = static_cast<int>(std::ceil(6.0 * a.orig / (std::min(a.orig, a.nw) * 0.99)));
   a.target = static_cast<int>(std::ceil(double(a.nw) * a.l1 / a.orig));
-  const int span = kPsSeg + static_cast<int>(std::ceil((kPsWin - 1) * a.rate)) + kPsRestart + 4;
-  if (a.nw > kPsPhaseMax || 2 * a.width + a.orig > kPsTapMax || a.l1 <= 0 || span > kPsFrames) {
+  // a group of kPvGroup output frames reads at most rate * kPvGroup + 2 new source frames
+  if (a.nw > kPsPhaseMax || 2 * a.width + a.orig > kPsTapMax || a.l1 <= 0 ||
+      a.rate * kPvGroup + 3 > kPvRows) {
     set_error("hbk: pitch shift %d/%d resamples %d -> %d (%d taps): the kernel holds <= %d phases of <= %d taps "
               "(torch_pitch_shift's fast shifts at 16 kHz)", num, den, a.orig, a.nw, 2 * a.width + a.orig,
               kPsPhaseMax, kPsTapMax);
@@ -2122,11 +2082,8 @@ static int ps_geometry(int64_t L, int32_t sample_rate, int32_t num, int32_t den,
 static int64_t ps_bytes(const hbk::PitchArgs& a, int64_t n, int64_t* off) {
   using namespace hbk;
   auto up = [](int64_t b) { return (b + 255) & ~int64_t(255); };
-  off[0] = 0;                                      // segsum
-  off[1] = up(n * a.nseg * kPsLd * 8);             // osum
-  off[2] = 2 * off[1];
-  off[3] = off[2];                                 // y
-  off[4] = off[3] + up(n * a.l1 * 4);              // taps
+  off[0] = off[1] = off[2] = off[3] = 0;           // y
+  off[4] = up(n * a.l1 * 4);                       // taps
   return off[4] + up(int64_t(kPsPhaseMax) * kPsTapMax * 4);
 }
 
@@ -2157,18 +2114,21 @@ int hbk_pitch_shift(const float* x, int64_t x_stride, int64_t n, const int32_t* 
   a.idx = idx;
   a.out = out;
   a.out_stride = out_stride;
-  a.segsum = reinterpret_cast<double*>(w + off[0]);
-  a.osum = reinterpret_cast<double*>(w + off[1]);
+  a.n = static_cast<int>(n);
   a.y = reinterpret_cast<float*>(w + off[3]);
   a.taps = reinterpret_cast<float*>(w + off[4]);
   hipStream_t st = as_stream(stream);
-  const dim3 seg(unsigned(a.nseg), unsigned(n));
   hipLaunchKernelGGL(ps_taps_kernel, dim3(unsigned((a.nw * kPsTapMax + 255) / 256)), dim3(256), 0, st, a);
   HBK_LAUNCH_CHECK("ps_taps_kernel");
-  hipLaunchKernelGGL(ps_phase_sum_kernel, seg, dim3(128), 0, st, a);
-  HBK_LAUNCH_CHECK("ps_phase_sum_kernel");
-  hipLaunchKernelGGL(ps_synth_kernel, seg, dim3(128), 0, st, a);
-  HBK_LAUNCH_CHECK("ps_synth_kernel");
+  static bool lds_set = false;  // > 64 KB of dynamic LDS needs the opt-in (per process, idempotent)
+  if (!lds_set) {
+    HBK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(ps_vocoder_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, int(sizeof(PvShared))));
+    lds_set = true;
+  }
+  hipLaunchKernelGGL(ps_vocoder_kernel, dim3(unsigned((n + kPvClips - 1) / kPvClips)), dim3(128 * kPvClips),
+                     sizeof(PvShared), st, a);
+  HBK_LAUNCH_CHECK("ps_vocoder_kernel");
   const int res_frames = (a.L + a.nw - 1) / a.nw;
   hipLaunchKernelGGL(ps_resample_kernel, dim3(unsigned((res_frames + kPsResFrames - 1) / kPsResFrames), unsigned(n)),
                      dim3(128), 0, st, a);

@@ -185,11 +185,17 @@ def train(phrase: str, additional_phrase: List[str] = [], wandb_entity: Optional
     from heybuddy.trainer import WakeWordTrainer
     from heybuddy.util import logger
 
+    # flag groups sharing a destination (--perceptron / --transformer, --training-*-default-dataset):
+    # click >= 8.2 gives such a group the LAST member's default ("False") when no flag is passed
+    if architecture not in ("perceptron", "transformer"):
+        architecture = DEFAULT_ARCHITECTURE
+    if training_default_size not in ("full", "large", "medium", "none"):
+        training_default_size = "full"
     if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) > 1 and not torch.distributed.is_initialized():
         local = int(os.environ.get("LOCAL_RANK", "0"))
         torch.cuda.set_device(local)
         torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = torch.device("cuda", torch.cuda.current_device())
+    device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
     torch.manual_seed(seed)
     np.random.seed(seed)
     if wandb_entity:

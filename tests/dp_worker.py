@@ -52,6 +52,14 @@ def main():
         os.environ["HBK_DP_REDUCE_ALWAYS"] = "1"
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     from heybuddy.trainer import WakeWordTrainer
+    calls = [0]
+    real = dist.all_reduce
+
+    def counted(*a, **k):  # host calls: one per eager step, one per step while capturing a graph
+        calls[0] += 1
+        return real(*a, **k)
+
+    dist.all_reduce = counted
     pool32, pool16, idx, y, sched = inputs()
     if mode == "gloo":
         idx, y = idx[:, rank::world], y[rank::world]
@@ -64,7 +72,8 @@ def main():
                      torch.from_numpy(sched).to(dev), pool32=torch.from_numpy(pool32).to(dev),
                      pool16=torch.from_numpy(pool16).to(dev), history=hist, steps_per_graph=8)
     torch.cuda.synchronize()
-    np.savez(out, flat=tr.model.flat_parameters.detach().cpu().numpy(), hist=hist.cpu().numpy())
+    np.savez(out, flat=tr.model.flat_parameters.detach().cpu().numpy(), hist=hist.cpu().numpy(),
+             reduce_calls=np.array(calls[0]))
     if dist.is_initialized():
         dist.destroy_process_group()
     print("dp worker ok", mode, rank, world, flush=True)

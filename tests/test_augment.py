@@ -599,6 +599,7 @@ def _pitch_clips():
     # energy off DC, so the vocoder phase carried across a step is rounding noise
     # in every implementation, the reference's float32 FFT included.)
     x[6] = 0.3 * np.sin(2 * np.pi * (100.0 + 1500.0 * t) * t)
+    x[5, 8000:12000] = 0.0              # an exact-zero gap inside a clip (all-zero frames mid-clip)
     return x
 
 
@@ -606,16 +607,21 @@ def _pitch_clips():
 @pytest.mark.parametrize("num,den,inplace", [(128, 125, False), (125, 128, True)])
 def test_pitch_shift_matches_oracle(num, den, inplace):
     """hbk_pitch_shift against the float64 restatement for both fast shifts:
-    speech-like clips, two tones, leading / trailing silence, a silent clip, a
-    chirp, and an unlisted clip (7) left untouched. Tolerance: per clip, L2 error
-    <= 1e-4 of the reference's L2 and max error <= 1e-3 of its peak (sliding DFT
-    in float32 against numpy's float64 FFT; the phase cumsum is float64 in both)."""
+    speech-like clips, two tones, leading / trailing silence, a silent clip, an
+    exact-zero gap inside a clip, a chirp, and an unlisted clip (7) left
+    untouched. The kernel's analysis is a float64 sliding DFT (exact zeros kept
+    exact), its phase float64, its synthesis float32: per clip, L2 error <= 1e-5
+    of the reference's L2 and max error <= 1e-4 of its peak (a simulation of the
+    same arithmetic measured <= 1.9e-6 / 3.4e-6; the reference's own float32
+    torch.stft path differs from the float64 restatement by up to 5e-4, see
+    test_pitch_shift_oracle_vs_torch_stft_restatement)."""
     from heybuddy.kernels import pitch_shift
     x = _pitch_clips()
     sel = np.array([0, 1, 2, 3, 4, 5, 6], np.int32)
     ref = oaug.pitch_shift(x[sel], num, den)
     xd = torch.from_numpy(x).cuda()
     out = pitch_shift(xd, torch.from_numpy(sel), num, den, out=xd if inplace else None).cpu().numpy()
+    worst = (0.0, 0.0)
     for j, i in enumerate(sel):
         r = ref[j]
         if not r.any():
@@ -623,7 +629,9 @@ def test_pitch_shift_matches_oracle(num, den, inplace):
             continue
         l2 = np.sqrt(((out[i] - r) ** 2).sum()) / np.sqrt((r ** 2).sum())
         mx = np.abs(out[i] - r).max() / np.abs(r).max()
-        assert l2 <= 1e-4 and mx <= 1e-3, f"clip {i}: rel L2 {l2:.2e}, rel max {mx:.2e}"
+        worst = (max(worst[0], l2), max(worst[1], mx))
+        assert l2 <= 1e-5 and mx <= 1e-4, f"clip {i}: rel L2 {l2:.2e}, rel max {mx:.2e}"
+    print(f"pitch shift {num}/{den}: worst rel L2 {worst[0]:.2e}, worst rel max {worst[1]:.2e}")
     np.testing.assert_array_equal(out[7], x[7])
 
 

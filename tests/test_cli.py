@@ -60,6 +60,43 @@ def test_train_has_every_reference_option_with_its_default():
             assert bool(p.default) == bool(want), opt["flags"]
 
 
+def test_train_routes_through_dataset_iterator_all(monkeypatch):
+    """`heybuddy train PHRASE` builds its data exactly as the reference does
+    (__main__.py:294-386): WakeWordTrainingDatasetIterator.all with the
+    reference's keyword mapping (the tanh pair, dataset-size flags, phrase
+    words, default background / impulse datasets), then WakeWordTrainer."""
+    import heybuddy.constants as C
+    from heybuddy.dataset.training import WakeWordTrainingDatasetIterator
+    seen = {}
+
+    class Stop(Exception):
+        pass
+
+    def fake_all(**kw):
+        seen.update(kw)
+        raise Stop()
+
+    monkeypatch.setattr(WakeWordTrainingDatasetIterator, "all", staticmethod(fake_all))
+    args = ["train", "hey buddy", "--augmentation-tanh-distortion-min", "0.01", "--augmentation-tanh-distortion-max",
+            "0.2", "--training-large-default-dataset", "--augment-phrase-word", "yo", "--adversarial-phrases", "7",
+            "--augmentation-no-default-impulse-dataset", "--augmentation-impulse-dataset", "my/irs",
+            "--testing-positive-batch-size", "20"]
+    res = CliRunner().invoke(main, args)
+    assert isinstance(res.exception, Stop), res.output
+    assert seen["wake_phrase"] == "hey buddy"
+    assert seen["augment_tanh_min_distortion"] == 0.01 and seen["augment_tanh_max_distortion"] == 0.2
+    assert seen["large_training"] and not seen["medium_training"]
+    assert seen["phrase_augment_words"] == list(C.DEFAULT_AUGMENT_PHRASE_WORDS) + ["yo"]
+    assert seen["augment_background_dataset"] == list(C.DEFAULT_BACKGROUND_DATASET)
+    assert seen["augment_impulse_dataset"] == ["my/irs"]
+    assert seen["num_adversarial_phrases"] == 7 and seen["testing_positive_per_batch"] == 20
+    assert seen["negative_per_batch"] == C.DEFAULT_NEGATIVE_BATCH_SIZE
+    assert seen["validation_num_positive_samples"] == C.DEFAULT_VALIDATION_SAMPLES
+    seen.clear()
+    res = CliRunner().invoke(main, ["train", "hey buddy"])  # no dataset-size flag: the full default set
+    assert isinstance(res.exception, Stop) and seen["large_training"] and seen["medium_training"]
+
+
 def test_train_help_lists_reference_options():
     res = CliRunner().invoke(main, ["train", "--help"])
     assert res.exit_code == 0, res.output
