@@ -219,8 +219,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     stage_ms = [sum(e[i].elapsed_time(e[i + 1]) for e in evs) / n_ev for i in range(len(job["stages"]))]
-    roofs = [job["roofline"](name, ms, args.pmc) for name, ms in zip(job["stages"], stage_ms)]
-    dom = max(range(len(roofs)), key=lambda i: stage_ms[i])
+    if "rooflines" in job:  # per kernel group (sub-stages timed on their own); the dominant one leads
+        roofs = job["rooflines"](dict(zip(job["stages"], stage_ms)), args.pmc)
+    else:
+        roofs = [job["roofline"](name, ms, args.pmc) for name, ms in zip(job["stages"], stage_ms)]
+    dom = max(range(len(roofs)), key=lambda i: roofs[i]["ms_per_step"])
 
     extra = job["extra_rooflines"]() if "extra_rooflines" in job and world == 1 else []
     cpu = None
@@ -591,14 +594,28 @@ def setup_e2e(args, dev, rank, world, seed):
         idx[:, P + A + NL:] = (-1 - n_large - ((o + k) % (n_neg - n_large))).to(torch.int32).view(S, NM)
         neg_pos[0] = (o + S * NL) % n_large
 
+    sub_events = []   # per staged step: (sub-stage, start, end) events of the augment chain
+    plan_counts = []  # per staged step: clips each augmentation was applied to
+
     def step(evs):
         stream = torch.cuda.current_stream(dev)
         prep = aug.prepare_device(src, lens)  # host draws first: the stage events time device work
         if evs:
+            ch = prep["chain"]
+            plan_counts.append({
+                "pitch": sum(int(c.numel()) for _, _, c in ch["pitch"]),
+                "eq": 0 if ch["eq"] is None else int(ch["eq"][1].numel()),
+                "tanh": 0 if ch["tanh"] is None else int((~torch.isnan(ch["tanh"])).sum()),
+                "bandstop": 0 if ch["bandstop"] is None else int(ch["bandstop"][0].numel()),
+                "colored": 0 if ch["colored"] is None else int((~torch.isnan(ch["colored"][1])).sum()),
+                "mix_reverb": n})
+            aug.augmenter.timing = []
             evs[0].record(stream)
         x = aug.augment_device(src, lens, prepared=prep)
         if evs:
             evs[1].record(stream)
+            sub_events.append(aug.augmenter.timing)
+            aug.augmenter.timing = None
         frames = mel_frames(x, mplan, N_FRAMES)
         if evs:
             evs[2].record(stream)
@@ -688,9 +705,51 @@ def setup_e2e(args, dev, rank, world, seed):
     _fft = 2.5 * 250 * np.log2(250)
     PITCH_FLOP_PER_CLIP = 3292 * _fft + 3372 * 126 * 16 + 3372 * (_fft + 250) + 23044 * 2 * 142
 
+    def rooflines(stage_ms, pmc):
+        """Per kernel group, each against its own bound: the augment chain's
+        sub-stages (timed by their own events on the stream they run on), mel,
+        embed and the train step; the whole augment stage is kept as a summary
+        entry. Algorithmic work per unit is stated in each entry."""
+        torch.cuda.synchronize(dev)
+        sub_ms, cnt = {}, {}
+        for evl, pc in zip(sub_events, plan_counts):
+            for name, a, b in evl:
+                sub_ms[name] = sub_ms.get(name, 0.0) + a.elapsed_time(b) / len(sub_events)
+            for k_, v_ in pc.items():
+                cnt[k_] = cnt.get(k_, 0) + v_ / len(plan_counts)
+        out = []
+        if sub_ms.get("pitch"):
+            m = cnt["pitch"]
+            out.append(roof("ps_vocoder_kernel + ps_resample_kernel (hbk_pitch_shift: %.0f clips shifted per step, "
+                            "p = %g per batch of 128)" % (m, args.pitch_prob), "valu", PITCH_FLOP_PER_CLIP * m,
+                            sub_ms["pitch"], "TFLOP/s", load_traffic(pmc, ("ps_vocoder", "ps_resample", "ps_taps")),
+                            peak=157.3, peak_basis="f32 vector peak (MI355X_MICROARCH.md)",
+                            algorithmic_flops_per_clip=round(PITCH_FLOP_PER_CLIP),
+                            flops_basis="FFT-based count of the reference's algorithm per shifted clip: stft 3,292 x "
+                                        "2.5 N log2 N (N = 250) + vocoder 3,372 x 126 x 16 + istft 3,372 x (2.5 N log2 N "
+                                        "+ 250) + resample 23,044 x 2 x 142", clips=round(m)))
+        per_clip = {"mix_reverb": (AUG_T * 4 * 3, "augment_kernel (gain + noise mix + 23040-pt FFT reverb, every clip)",
+                                   ("augment_kernel",), "x + noise read, y written"),
+                    "eq": (AUG_T * 4 * 2, "eq_kernel (7-band EQ, the clips whose coin came up)", ("eq_kernel",),
+                           "x read + y written"),
+                    "tanh": (AUG_T * 4 * 2, "tanh_distortion_kernel (the clips whose coin came up)",
+                             ("tanh_distortion",), "x read + y written"),
+                    "bandstop": (AUG_T * 4 * 2, "band_stop_kernel (+ sums / spectrum, the batches whose coin came up)",
+                                 ("band_stop",), "x read + y written"),
+                    "colored": (AUG_T * 4 * 2, "colored_noise_kernel (the batches whose coin came up)",
+                                ("colored_noise",), "x read + y written")}
+        for name, (bpc, kname, subs, basis) in per_clip.items():
+            if sub_ms.get(name):
+                m = cnt.get(name, n)
+                out.append(roof(kname, "hbm", bpc * m, sub_ms[name], "GB/s", load_traffic(pmc, subs),
+                                algorithmic_bytes_per_clip=bpc, bytes_basis=basis, clips=round(m)))
+        for name in ("augment", "mel", "embed", "train"):
+            out.append(roofline(name, stage_ms[name], pmc))
+        return out
+
     def roofline(name, ms, pmc):
         if name == "augment":
-            return roof("place_kernel + eq_kernel + tanh_distortion_kernel + ps_*_kernel + band_stop_kernel + "
+            return roof("augment stage (summary; its kernels are listed on their own): place_kernel + eq_kernel + tanh_distortion_kernel + ps_*_kernel + band_stop_kernel + "
                         "colored_noise_kernel + augment_kernel (placement, 7-band EQ, tanh, pitch shift, band-stop, "
                         "colored noise, gain + noise mix + 23040-pt FFT reverb)", "hbm",
                         n * AUG_T * 4 * 2, ms, "GB/s", load_traffic(pmc, ("place_kernel", "augment_kernel", "eq_kernel",
@@ -806,30 +865,10 @@ def setup_e2e(args, dev, rank, world, seed):
                       "kernel on every chain, as for a graph without SE20's chain shapes; %d clips, untimed)" % m,
                       "mfma", 2.0 * gplan.macs_per_clip * m, ms, "TFLOP/s", None, peak=SPLIT_PEAK_TFLOPS,
                       peak_basis="f16 dense MFMA peak / 3", clips=m)]
-        # pitch shift alone (the largest part of the augment stage when it is on): both fast shifts
-        # over the same clips, against the f32 VALU peak, with the FFT-based FLOP count of the
-        # reference's algorithm (stft + vocoder + istft + resample) as the algorithmic work
-        from heybuddy.kernels import pitch_shift
-        x = aug.augment_device(src[:m], lens[:m])
-        rows = torch.arange(m, dtype=torch.int32, device=dev)
-        pitch_shift(x, rows, 128, 125, out=x)
-        e0.record()
-        for num, den in ((128, 125), (125, 128), (128, 125), (125, 128)):
-            pitch_shift(x, rows, num, den, out=x)
-        e1.record()
-        torch.cuda.synchronize(dev)
-        ms = e0.elapsed_time(e1) / 4
-        extra.append(roof("ps_phase_sum_kernel + ps_synth_kernel + ps_resample_kernel (hbk_pitch_shift, both fast "
-                          "shifts alternately; %d clips, untimed)" % m, "valu", PITCH_FLOP_PER_CLIP * m, ms,
-                          "TFLOP/s", None, peak=157.3, peak_basis="f32 vector peak (MI355X_MICROARCH.md)",
-                          flops_basis="FFT-based count of the reference's algorithm per clip: stft 3,292 x 2.5 N "
-                                      "log2 N (N = 250) + vocoder 3,372 x 126 x 16 + istft 3,372 x (2.5 N log2 N + "
-                                      "250) + resample 23,044 x 2 x 142 = %.1f MFLOP" % (PITCH_FLOP_PER_CLIP / 1e6),
-                          clips=m))
         return extra
 
     return {
-        "step": step, "staged_step": staged_step, "stages": stages, "roofline": roofline,
+        "step": step, "staged_step": staged_step, "stages": stages, "roofline": roofline, "rooflines": rooflines,
         "extra_rooflines": extra_rooflines,
         "cpu_baseline": cpu_baseline, "units_per_step": n, "scaling": "weak", "unit": "clips/s",
         "metric": "audio clips/sec featurized+trained, 1.5 s @16 kHz, 1/2/4/8 GPU",

@@ -1568,36 +1568,60 @@ __global__ void __launch_bounds__(128 * kPvClips) ps_vocoder_kernel(PitchArgs a)
   int cnt = C.cnt0;
   if (cnt == 0) xre = xim = 0.0;
   int sf = 0;  // last slid frame
-  // slide to frame sf + 1 (its d row must be resident)
-  auto slide = [&]() {
-    ++sf;
-    if (sf >= a.f_in) {
-      xre = xim = 0.0;
+  // the sliding DFT's next frame (sf + 1) from the current state, as a candidate
+  // (xre, xim, cnt are committed by the caller): two partial sums per component
+  // keep the float64 dependency chain short
+  auto slide_to = [&](double& nre, double& nim, int& ncnt) {
+    const int f = sf + 1;
+    if (f >= a.f_in) {
+      nre = nim = 0.0;
+      ncnt = cnt;
       return;
     }
-    const double* dr = C.d[sf - fb];
-    double dre = 0.0, dim = 0.0;
-#pragma unroll
-    for (int j = 0; j < 7; ++j) {
-      dre = fma(dr[j], wr[j], dre);
-      dim = fma(dr[j], wi[j], dim);
-    }
-    cnt += static_cast<int>(dr[7]);
-    const double ar = xre + dre, ai = xim + dim;
-    xre = ar * rr - ai * ri;
-    xim = ar * ri + ai * rr;
-    if (cnt == 0) xre = xim = 0.0;
+    const double* dr = C.d[f - fb];
+    double r0 = dr[0] * wr[0], r1 = dr[1] * wr[1], i0 = dr[0] * wi[0], i1 = dr[1] * wi[1];
+    r0 = fma(dr[2], wr[2], r0);
+    i0 = fma(dr[2], wi[2], i0);
+    r1 = fma(dr[3], wr[3], r1);
+    i1 = fma(dr[3], wi[3], i1);
+    r0 = fma(dr[4], wr[4], r0);
+    i0 = fma(dr[4], wi[4], i0);
+    r1 = fma(dr[5], wr[5], r1);
+    i1 = fma(dr[5], wi[5], i1);
+    r0 = fma(dr[6], wr[6], r0);
+    i0 = fma(dr[6], wi[6], i0);
+    ncnt = cnt + static_cast<int>(dr[7]);
+    const double ar = xre + (r0 + r1), ai = xim + (i0 + i1);
+    nre = ar * rr - ai * ri;
+    nim = ar * ri + ai * rr;
+    if (ncnt == 0) nre = nim = 0.0;
   };
-  auto polar = [&](float& ang, float& mag) {
-    const float fr = static_cast<float>(xre), fi = static_cast<float>(xim);
+  auto commit = [&](double nre, double nim, int ncnt) {
+    xre = nre;
+    xim = nim;
+    cnt = ncnt;
+    ++sf;
+  };
+  auto polar_of = [&](double re, double im, float& ang, float& mag) {
+    const float fr = static_cast<float>(re), fi = static_cast<float>(im);
     ang = ps_atan2(fi, fr);
     mag = sqrtf(fmaf(fr, fr, fi * fi));
   };
-  float ca, cm, na, nm;
+  auto polar = [&](float& ang, float& mag) { polar_of(xre, xim, ang, mag); };
+  // frames c, c + 1 in (ca, cm), (na, nm); frame c + 2 = sf ahead in (pa, pm)
+  float ca, cm, na, nm, pa, pm;
   polar(ca, cm);
-  slide();
-  polar(na, nm);
-  int c = 0;  // frames c and c + 1 = sf are in (ca, cm), (na, nm)
+  {
+    double nre, nim;
+    int ncnt;
+    slide_to(nre, nim, ncnt);
+    commit(nre, nim, ncnt);
+    polar(na, nm);
+    slide_to(nre, nim, ncnt);
+    commit(nre, nim, ncnt);
+    polar(pa, pm);
+  }
+  int c = 0;
   double accR = static_cast<double>(ca) * (0.5 / M_PI);
   cf Q = {0.f, 0.f};
   int qz = 0;
@@ -1606,11 +1630,11 @@ __global__ void __launch_bounds__(128 * kPvClips) ps_vocoder_kernel(PitchArgs a)
   float* y = a.y + static_cast<int64_t>(e) * a.l1;
 
   for (int t0 = 0; t0 <= jmax; t0 += kPvGroup) {
-    // the group's source frames must be resident: refill the d rows from the next unslid frame
+    // the group's source frames (and one ahead) must be resident: refill the d rows
     {
       float al;
       const int tl = min(t0 + kPvGroup - 1, a.f_out - 1);
-      const int need = t0 < a.f_out ? min(ps_i0(a, tl, al) + 1, a.f_in - 1) : 0;
+      const int need = t0 < a.f_out ? min(ps_i0(a, tl, al) + 3, a.f_in - 1) : 0;
       if (need >= fb + kPvRows) {  // uniform across the workgroup
         __syncthreads();
         fb = sf + 1;
@@ -1623,13 +1647,31 @@ __global__ void __launch_bounds__(128 * kPvClips) ps_vocoder_kernel(PitchArgs a)
       if (t < a.f_out) {
         float al;
         const int i0 = ps_i0(a, t, al);
-        while (c < i0) {
+        if (i0 > c + 1) {  // rate > 1: a second source frame this step (rare)
           ++c;
           ca = na;
           cm = nm;
-          slide();
-          polar(na, nm);
+          na = pa;
+          nm = pm;
+          double nre, nim;
+          int ncnt;
+          slide_to(nre, nim, ncnt);
+          commit(nre, nim, ncnt);
+          polar(pa, pm);
         }
+        // the common step (i0 = c + 1) as selects, so that the vocoder of frame t and the
+        // look-ahead slide of the next source frame form one block the scheduler interleaves
+        const bool step = i0 > c;
+        c += step ? 1 : 0;
+        ca = step ? na : ca;
+        cm = step ? nm : cm;
+        na = step ? pa : na;
+        nm = step ? pm : nm;
+        double nre, nim;
+        int ncnt;
+        slide_to(nre, nim, ncnt);  // candidate frame sf + 1 and its polar form, kept only when stepping
+        float qa, qm;
+        polar_of(nre, nim, qa, qm);
         const float m = fmaf(al, nm - cm, cm);
         const double fr = accR - rint(accR);
         const float frf = static_cast<float>(fr);
@@ -1638,6 +1680,12 @@ __global__ void __launch_bounds__(128 * kPvClips) ps_vocoder_kernel(PitchArgs a)
         double inc = (static_cast<double>(na) - static_cast<double>(ca)) * (0.5 / M_PI) - kadv;
         inc -= rint(inc);
         accR += inc;
+        xre = step ? nre : xre;
+        xim = step ? nim : xim;
+        cnt = step ? ncnt : cnt;
+        sf += step ? 1 : 0;
+        pa = step ? qa : pa;
+        pm = step ? qm : pm;
       }
       C.v[u][lane] = ck * cmul(Q, sh.tw[qz]);
       qz += dq;

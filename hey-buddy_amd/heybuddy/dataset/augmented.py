@@ -219,6 +219,20 @@ class BatchAugmenter:
         self.noise_idx = 0
         self.ir_idx = 0
         self._advance = {}
+        # a list: __call__ appends (sub-stage, start event, end event) per stage it
+        # launches (timing events on the current stream; bench.py's per-kernel rooflines)
+        self.timing: Optional[list] = None
+
+    def _tick(self, name: str, start: Optional[Any]) -> Optional[Any]:
+        """Close the sub-stage started by ``start`` (an event or None) as
+        ``name`` and open the next one; no-op unless self.timing is a list."""
+        if self.timing is None:
+            return None
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        if start is not None and name:
+            self.timing.append((name, start, ev))
+        return ev
 
     def _noise_advance(self, idx: int, nb: int) -> int:
         """Index of the noise clip after a batch of nb clips starting at clip idx:
@@ -341,32 +355,40 @@ class BatchAugmenter:
         pr = self.prepare(n) if prepared is None else prepared
         if pr["n"] != n:
             raise ValueError(f"prepared for {pr['n']} clips, called with {n}")
+        ev = self._tick("", None)
         if pr["eq"] is not None:  # per-clip Compose: EQ, then tanh (augmented.py:79-90), in place on out
             if out is None:
                 out = torch.empty((n, T), dtype=torch.float32, device=x.device)
             if out.data_ptr() != x.data_ptr():
                 out.copy_(x[:, :T])
             x = seven_band_eq(out, pr["eq"][0], idx=pr["eq"][1])
+            ev = self._tick("eq", ev)
         if pr["tanh"] is not None:  # per-clip Compose, before the batch chain (augmented.py:325-328)
             x = tanh_distortion(x, pr["tanh"], out=out)
             out = x
+            ev = self._tick("tanh", ev)
         for num, den, clips in pr.get("pitch") or []:  # batch chain: pitch shift first (augmented.py:93-100)
             if out is None:
                 out = torch.empty((n, T), dtype=torch.float32, device=x.device)
             x = pitch_shift(x, clips, num, den, out=out, sample_rate=self.sample_rate)
+            ev = self._tick("pitch", ev)
         if pr.get("bandstop") is not None:  # then band-stop, then colored noise (augmented.py:101-113)
             if out is None:
                 out = x[:, :T].clone()
             elif out.data_ptr() != x.data_ptr():
                 out.copy_(x[:, :T])
             x = self.plan.band_stop(out, *pr["bandstop"], out=out)
+            ev = self._tick("bandstop", ev)
         if pr["colored"] is not None:  # colored noise precedes the gain (augmented.py:107-118)
             fd, csnr, seed = pr["colored"]
             x = self.plan.colored_noise(x, fd, csnr, seed=seed, out=out, sample_rate=self.sample_rate,
                                         clips_per_noise=self.batch_size)
             out = x
-        return self.plan.augment(x, self.ring, pr["noise_off"], pr["snr"], self.spectra, pr["spec_idx"],
-                                 out=out, gain=pr["gain"])
+            ev = self._tick("colored", ev)
+        y = self.plan.augment(x, self.ring, pr["noise_off"], pr["snr"], self.spectra, pr["spec_idx"],
+                              out=out, gain=pr["gain"])
+        self._tick("mix_reverb", ev)
+        return y
 
 
 # ---------------------------------------------------------------------------

@@ -624,7 +624,9 @@ def tanh_distortion(x: torch.Tensor, amount: torch.Tensor, out: torch.Tensor | N
     return out
 
 
-PITCH_SHIFT_CHUNK = 2048  # clips per hbk_pitch_shift call (~0.2 MB of workspace each)
+PITCH_SHIFT_CHUNK = 16384  # clips per hbk_pitch_shift call (~0.1 MB of workspace each)
+# workspace per (device, stream): calls on one stream are ordered, so they may
+# share one; a call on another stream gets its own (no cross-stream reuse)
 _PS_WS: dict = {}
 
 
@@ -655,10 +657,11 @@ def pitch_shift(x: torch.Tensor, idx: torch.Tensor, num: int, den: int, out: tor
     need = int(lib().hbk_pitch_shift_workspace_size(chunk, T, sample_rate, num, den))
     if need <= 0:
         raise ValueError(f"unsupported pitch shift {num}/{den} at {sample_rate} Hz")
-    ws = _PS_WS.get(dev)
+    key = (dev, stream_ptr(dev))
+    ws = _PS_WS.get(key)
     if ws is None or ws.numel() < need:
-        ws = torch.empty(need, dtype=torch.uint8, device=dev)
-        _PS_WS[dev] = ws
+        ws = torch.empty(need, dtype=torch.uint8, device=dev)  # allocated on this stream: no record_stream needed
+        _PS_WS[key] = ws
     for c0 in range(0, idx.numel(), chunk):
         torch.ops.hbk.pitch_shift_(x, idx[c0:c0 + chunk], num, den, sample_rate, out, ws)
     return out

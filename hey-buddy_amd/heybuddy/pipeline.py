@@ -74,13 +74,14 @@ class _MaskedStream:
         try:
             if self.handle:
                 _MASKS.pop(self.handle.value, None)
-                torch.cuda.synchronize()
+                self.stream.synchronize()  # this stream only: no device-wide stall
                 self._lib.hbk_stream_destroy(self.handle)
         except Exception:
             pass
 
 
 _MASKS: dict = {}  # raw stream handle -> its CU set (the live _MaskedStreams)
+_CAPTURE: dict = {}  # (device, CU set) -> the one masked capture stream kept for it
 
 
 def masked_stream(device: torch.device, cus) -> "_MaskedStream":
@@ -96,7 +97,10 @@ def capture_stream(device: torch.device):
     cus = _MASKS.get(cur.cuda_stream)
     if cus is None:
         return torch.cuda.Stream(device), None
-    ms = _MaskedStream(device, cus)
+    key = (str(device), tuple(cus))
+    ms = _CAPTURE.get(key)  # one per CU set, reused: no stream create / destroy per capture
+    if ms is None:
+        ms = _CAPTURE[key] = _MaskedStream(device, cus)
     return ms.stream, ms
 
 

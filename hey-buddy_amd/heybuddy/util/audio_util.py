@@ -68,7 +68,8 @@ def _sinc_kernel(orig: int, new: int, width_zc: int = 6, rolloff: float = 0.99) 
     base = min(orig, new) * rolloff
     width = math.ceil(width_zc * orig / base)
     idx = torch.arange(-width, width + orig, dtype=torch.float64)[None, None] / orig
-    t = (torch.arange(0, -new, -1, dtype=torch.float64)[:, None, None] / new + idx) * base
+    # torchaudio builds the phase offsets with arange(dtype=None), i.e. float32, before adding idx (float64)
+    t = ((torch.arange(0, -new, -1, dtype=torch.float32)[:, None, None] / new).double() + idx) * base
     t = t.clamp(-width_zc, width_zc)
     window = torch.cos(t * math.pi / width_zc / 2) ** 2
     t = t * math.pi

@@ -689,3 +689,23 @@ def test_pitch_shift_oracle_vs_torch_stft_restatement():
         b = oaug.pitch_shift_torch(x, num, den)
         for i in range(len(x)):
             assert np.linalg.norm(a[i] - b[i]) <= 1e-3 * np.linalg.norm(a[i]), (num, den, i)
+
+
+def test_resample_taps_match_oracle():
+    """util.resample's polyphase filters (torchaudio _get_sinc_resample_kernel,
+    float32 phase offsets as with dtype=None) equal oracle.augment.resample_taps,
+    and util.resample equals the oracle's polyphase resampling."""
+    from heybuddy.util.audio_util import _sinc_kernel, resample
+    for orig, new in ((125, 128), (128, 125), (3, 2), (441, 160)):
+        k, w = _sinc_kernel(orig, new)
+        kr, wr = oaug.resample_taps(orig, new)
+        assert w == wr
+        np.testing.assert_array_equal(k[:, 0].numpy(), kr)
+    x = _clips(2, seed=71)[:, :5000].astype(np.float32)
+    y = resample(torch.from_numpy(x), 128, 125).numpy()
+    taps, w = oaug.resample_taps(128, 125)
+    xp = np.pad(x.astype(np.float64), ((0, 0), (w, w + 128)))
+    nfr = 5000 // 128 + 1
+    win = 128 * np.arange(nfr)[:, None] + np.arange(2 * w + 128)[None]
+    ref = np.einsum("nfq,pq->nfp", xp[:, win], taps.astype(np.float64)).reshape(2, -1)[:, :y.shape[1]]
+    np.testing.assert_allclose(y, ref, rtol=0, atol=2e-6)
