@@ -86,9 +86,12 @@ def parse():
                          "N x 1,000 steps per rank)")
     ap.add_argument("--stage-steps", type=int, default=2,
                     help="overlapped runs: sequential (untimed) steps that time the stages for the rooflines")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
-                    help="per-kernel HBM bytes from rocprofv3 --pmc passes (optional)")
+    ap.add_argument("--pmc", default=None,
+                    help="per-kernel HBM bytes per step from rocprofv3 --pmc passes (tools/prof_summary.py JSON; "
+                         "default profiles/pmc_c<config>_latest.json)")
     args = ap.parse_args()
+    if args.pmc is None:
+        args.pmc = os.path.join(ROOT, "profiles", f"pmc_c{args.config}_latest.json")
     if args.overlap is None:  # pitch shift makes featurization ~3x heavier: give it 224 CUs (r02ag)
         args.overlap = "split:32" if args.pitch_prob > 0 else "split:64"
     return args
@@ -100,17 +103,19 @@ CURRENT_CONFIG = [None]
 
 def load_traffic(path, kernel_substr):
     """HBM bytes per step of the kernels whose name contains kernel_substr (a
-    string or a tuple of alternatives), from a tools/pmc_summary.py JSON
-    (FETCH_SIZE doubled per the gfx950 calibration + WRITE_SIZE), or None. A
-    summary recorded for another --config (its "config" field) is not used:
-    per-step bytes belong to one workload."""
+    string or a tuple of alternatives), from a tools/prof_summary.py JSON
+    ((2 FETCH_SIZE + WRITE_SIZE) KiB per the gfx950 calibration, counted over
+    the dispatches of one timed bench step only: between bench.py's profiling
+    markers), or None. A summary recorded for another --config (its "config"
+    field) is not used: per-step bytes belong to one workload."""
     subs = (kernel_substr,) if isinstance(kernel_substr, str) else tuple(kernel_substr)
     try:
         with open(path) as f:
             d = json.load(f)
         if d.get("config") not in (None, CURRENT_CONFIG[0]):
             return None
-        v = [k for name, k in d.get("kernels", {}).items() if any(s in name for s in subs)]
+        kernels = d.get("kernels") or d["regions"]["timed"]["kernels"]
+        v = [k for name, k in kernels.items() if any(s in name for s in subs) and "hbm_bytes_per_step" in k]
         if v:
             TRAFFIC_SOURCE[0] = os.path.relpath(path, ROOT)
             return sum(k["hbm_bytes_per_step"] for k in v)
@@ -126,8 +131,8 @@ def roof(kernel, bound, work, ms, unit, traffic, peak=None, **extra):
     d = {"kernel": kernel, "bound": bound, "achieved": round(ach, 3), "peak": peak, "unit": unit,
          "frac": round(ach / peak, 4), "traffic": traffic, "ms_per_step": round(ms, 3)}
     if traffic is not None:  # PMC bytes are collected in separate rocprofv3 passes, not in this run
-        d["traffic_source"] = "%s (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, tools/pmc_summary.py)" % (
-            TRAFFIC_SOURCE[0],)
+        d["traffic_source"] = ("%s (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over one timed step, "
+                               "tools/prof_summary.py)" % (TRAFFIC_SOURCE[0],))
     d.update(extra)
     return d
 

@@ -61,6 +61,7 @@ VARIANTS = {  # profiling builds (load with HBK_LIB=hey-buddy_amd/lib/<name>)
     "phase": ("libhbk_phase.so", ("-DHBK_PHASE_TIMING",)),  # s_memtime phase counters + ablation
     "ablate": ("libhbk_ablate.so", ("-DHBK_ABLATE",)),      # HBK_DEBUG_SKIP phase ablation only
     "trace": ("libhbk_trace.so", ("-DHBK_TRACE",)),         # per-wave s_memtime timeline
+    "pvpair": ("libhbk_pvpair.so", ("-DHBK_PV_PAIR",)),      # pitch vocoder: lane-pair bin reduction (A/B)
 }
 
 

@@ -1458,6 +1458,8 @@ __device__ __forceinline__ float ps_atan2(float y, float x) {
   return copysignf(r, y);
 }
 
+#ifdef HBK_PV_PAIR
+// bin reduction by lane pairs: output (u, s) summed by two lanes over 64 bins each
 struct PvClip {
   double d[kPvRows][8];       // row f - fb: d_j (j < 7) of frame f, [7] = the non-zero-count change
   cf v[kPvGroup][kPvLd];      // V_t[k] of the group's frames (k >= 126: 0)
@@ -1471,6 +1473,30 @@ struct PvShared {
   double tw64[256][2];        // e^{-2 pi i q / 250}, float64
   PvClip c[kPvClips];
 };
+__device__ __forceinline__ cf& pv_v(cf (*v)[kPvLd], int u, int k) { return v[u][k]; }
+#else
+// bin reduction with broadcast weights: lane 8u + p of each wave sums bins
+// [16p, 16p + 16) of frame u for its wave's s values; the 8 lanes of a part p
+// read the same e^{2 pi i k s / 250} (one LDS broadcast), then 3 lane-xor steps
+// add the 8 parts. Part pitch 18 complex (36 banks) and row pitch 144 complex
+// (== 32 banks mod 64) keep every 16-lane phase of a b128 read conflict-free.
+constexpr int kPvPart = 18;
+struct PvClip {
+  double d[kPvRows][8];       // row f - fb: d_j (j < 7) of frame f, [7] = the non-zero-count change
+  union {
+    cf v[8][8][kPvPart];      // V_t[k] of the group's frames: [u][k / 16][k % 16] (u = 7, k >= 126: 0)
+    float xs[256];            // init only: xp[0, 250) (frame 0's direct DFT)
+  };
+  float gh[kPvGh][9];         // G(t, s), row t mod kPvGh
+  int cnt0;
+};
+struct PvShared {
+  cf et[9][8][kPvPart];       // e^{+2 pi i k s / 250}, [s][k / 16][k % 16]
+  cf tw[256];                 // e^{+2 pi i q / 250}
+  double tw64[256][2];        // e^{-2 pi i q / 250}, float64
+  PvClip c[kPvClips];
+};
+#endif
 
 // padded sample p of clip row xr (reflect padding by n_fft / 2)
 __device__ __forceinline__ float ps_xp(const float* xr, int L, int p) {
@@ -1505,7 +1531,8 @@ __device__ __forceinline__ void pv_load_rows(const PitchArgs& a, PvShared& sh, c
   }
 }
 
-__global__ void __launch_bounds__(128 * kPvClips) ps_vocoder_kernel(PitchArgs a) {
+__global__ void __launch_bounds__(128 * kPvClips) __attribute__((amdgpu_waves_per_eu(4)))
+ps_vocoder_kernel(PitchArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char pv_smem[];
   PvShared& sh = *reinterpret_cast<PvShared*>(pv_smem);
   const int tid = threadIdx.x, cl = tid >> 7, lane = tid & 127;
@@ -1521,11 +1548,16 @@ __global__ void __launch_bounds__(128 * kPvClips) ps_vocoder_kernel(PitchArgs a)
     sh.tw64[q][0] = cs;
     sh.tw64[q][1] = -sn;
   }
-  for (int q = tid; q < 9 * kPvLd; q += blockDim.x) {
-    const int s = q / kPvLd, k = q % kPvLd;
+  for (int q = tid; q < 9 * 128; q += blockDim.x) {
+    const int s = q / 128, k = q % 128;
     double sn, cs;
     sincospi(2.0 * ((k * s) % kPsFft) / kPsFft, &sn, &cs);
-    sh.et[s][k] = k < kPsBins ? cf{static_cast<float>(cs), static_cast<float>(sn)} : cf{0.f, 0.f};
+    const cf ev = k < kPsBins ? cf{static_cast<float>(cs), static_cast<float>(sn)} : cf{0.f, 0.f};
+#ifdef HBK_PV_PAIR
+    sh.et[s][k] = ev;
+#else
+    sh.et[s][k >> 4][k & 15] = ev;
+#endif
   }
   if (lane == 0) C.cnt0 = 0;
   __syncthreads();
@@ -1628,6 +1660,7 @@ __global__ void __launch_bounds__(128 * kPvClips) ps_vocoder_kernel(PitchArgs a)
   const int dq = q7;
   const int jmax = (a.l1 + kPsPad - 1) / kPsHop;  // the frame of the last istft sample
   float* y = a.y + static_cast<int64_t>(e) * a.l1;
+  __syncthreads();  // xs (frame 0's samples) shares LDS with the V rows the first group writes
 
   for (int t0 = 0; t0 <= jmax; t0 += kPvGroup) {
     // the group's source frames (and one ahead) must be resident: refill the d rows
@@ -1687,11 +1720,16 @@ __global__ void __launch_bounds__(128 * kPvClips) ps_vocoder_kernel(PitchArgs a)
         pa = step ? qa : pa;
         pm = step ? qm : pm;
       }
+#ifdef HBK_PV_PAIR
       C.v[u][lane] = ck * cmul(Q, sh.tw[qz]);
+#else
+      C.v[u][lane >> 4][lane & 15] = ck * cmul(Q, sh.tw[qz]);
+#endif
       qz += dq;
       qz -= qz >= kPsFft ? kPsFft : 0;
     }
     __syncthreads();
+#ifdef HBK_PV_PAIR
     // G(t, s) of the group: 63 values, two lanes each (bins [0, 64) and [64, 128))
     if (lane < 2 * 9 * kPvGroup) {
       const int o = lane >> 1, h = lane & 1, u = o / 9, s = o % 9;
@@ -1708,6 +1746,42 @@ __global__ void __launch_bounds__(128 * kPvClips) ps_vocoder_kernel(PitchArgs a)
       g += __shfl_xor(g, 1);
       if (h == 0) C.gh[(t0 + u) % kPvGh][s] = g;
     }
+#else
+    {
+      // wave 0 of the clip: s = 0..4, wave 1: s = 5..8; lane 8u + p: frame u, bins [16p, 16p + 16)
+      const int w = lane >> 6, u = (lane >> 3) & 7, p = lane & 7;
+      const float4* vp = reinterpret_cast<const float4*>(C.v[u][p]);
+      const int s0 = 5 * w, ns = 5 - w;
+      // two passes over the part's bins (s0 .. s0+2, then s0+3, s0+4): fewer live accumulators
+#pragma unroll
+      for (int pass = 0; pass < 2; ++pass) {
+        constexpr int kJ = 3;
+        cf acc[kJ][2];
+#pragma unroll
+        for (int j = 0; j < kJ; ++j) acc[j][0] = acc[j][1] = cf{0.f, 0.f};
+        const int sb = s0 + kJ * pass;
+#pragma unroll 2
+        for (int i = 0; i < 8; ++i) {
+          const float4 v4 = vp[i];
+#pragma unroll
+          for (int j = 0; j < kJ; ++j) {
+            const float4 e4 = reinterpret_cast<const float4*>(sh.et[min(sb + j, 8)][p])[i];
+            acc[j][0] = __builtin_elementwise_fma(cf{v4.x, v4.y}, cf{e4.x, e4.y}, acc[j][0]);
+            acc[j][1] = __builtin_elementwise_fma(cf{v4.z, v4.w}, cf{e4.z, e4.w}, acc[j][1]);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < kJ; ++j) {
+          float gj = (acc[j][0].x - acc[j][0].y) + (acc[j][1].x - acc[j][1].y);
+          gj += __shfl_xor(gj, 1);
+          gj += __shfl_xor(gj, 2);
+          gj += __shfl_xor(gj, 4);
+          const int jj = kJ * pass + j;
+          if (p == 0 && u < kPvGroup && jj < ns) C.gh[(t0 + u) % kPvGh][s0 + jj] = gj;
+        }
+      }
+    }
+#endif
     __syncthreads();
     // the group's istft samples p = 7 t + r
     if (lane < kPsHop * kPvGroup && live) {
