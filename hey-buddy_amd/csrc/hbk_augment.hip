@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <cmath>
 #include <numeric>
+#include <type_traits>
 #include <vector>
 
 #include "hbk_common.h"
@@ -1398,22 +1399,32 @@ __global__ void __launch_bounds__(64) eq_kernel(EqArgs a) {
 //    istft's frame rotation, so Z_t = Y_t e^{-2 pi i 7kt/250} = m_t e^{2 pi i accR_t};
 //  * synthesis without inverse transforms: with Q_t = sum_{t' <= t} Z_t' (a
 //    prefix per bin) and G(t, s) = Re sum_k c_k e^{2 pi i k (7t + s)/250} Q_t[k],
-//    s < 9, the overlap-added istft sample p = 7t + r is
+//    s < 7, the overlap-added istft sample p = 7t + r is
 //      (G(t, r) - G(t - 36, r + 2)) / (250 env)   r <= 4 (frames t-35 .. t)
 //      (G(t, r) - G(t - 35, r - 5)) / (250 env)   r = 5, 6 (frames t-34 .. t)
-//    so a bin keeps no window of past frames: per frame it stages
-//    V_t = c_k Q_t e^{2 pi i 7kt/250} in LDS, and every kPvGroup frames the
-//    workgroup reduces the 9 x kPvGroup G values over the bins (packed f32 FMAs).
+//    so a bin keeps no window of past frames. The 7 G(t, .) of a frame are
+//    reduced over the bins in registers: lane k forms its 7 products
+//    Re(Q_t e^{2 pi i 7kt/250} c_k e^{2 pi i ks/250}) and an 8-lane
+//    reduce-scatter by DPP leaves s = g(lane & 7) on each lane; after the
+//    group's 8 frames a reduce-scatter over the octets (DPP row_ror:8,
+//    v_permlane16/32_swap) leaves frame u of the wave's 64 bins on octet u. No
+//    LDS in the per-frame path; per kPvGroup frames one float per lane goes to
+//    LDS for the istft samples.
 // ps_resample_kernel (frame group, clip): polyphase sinc, taps in registers.
 constexpr int kPsFft = 250, kPsHop = 7, kPsBins = kPsFft / 2 + 1, kPsPad = kPsFft / 2;
 constexpr int kPsTapMax = HBK_PITCH_SHIFT_MAX_TAPS;    // 2 width + orig (142 / 139 at 16 kHz)
 constexpr int kPsPhaseMax = 128;                       // new (resampler phases)
 constexpr int kPsResFrames = 32;                       // resampler frames per workgroup
-constexpr int kPvClips = 4;                            // clips per workgroup (128 lanes each)
-constexpr int kPvGroup = 7;                            // output frames per bin reduction
+#ifndef HBK_PV_ABLATE
+#define HBK_PV_ABLATE 0  // profiling builds: 1 skips the bin reduction, 2 the per-bin vocoder
+#endif
+#ifndef HBK_PV_CLIPS
+#define HBK_PV_CLIPS 2  // measured: 1.79 us/clip at 2, 1.95 at 4, 2.33 at 1 (12,800 clips)
+#endif
+constexpr int kPvClips = HBK_PV_CLIPS;                 // clips per workgroup (128 lanes each)
+constexpr int kPvGroup = 8;                            // output frames per istft step (lane 8u + .: frame u)
 constexpr int kPvRows = 64;                            // input frames of d rows held in LDS
 constexpr int kPvGh = 64;                              // ring of G(t, .) rows (>= 36 + kPvGroup)
-constexpr int kPvLd = 130;                             // LDS row pitch (float2) of the bin rows
 
 struct PitchArgs {
   const float* x;
@@ -1458,45 +1469,41 @@ __device__ __forceinline__ float ps_atan2(float y, float x) {
   return copysignf(r, y);
 }
 
-#ifdef HBK_PV_PAIR
-// bin reduction by lane pairs: output (u, s) summed by two lanes over 64 bins each
 struct PvClip {
   double d[kPvRows][8];       // row f - fb: d_j (j < 7) of frame f, [7] = the non-zero-count change
-  cf v[kPvGroup][kPvLd];      // V_t[k] of the group's frames (k >= 126: 0)
-  float gh[kPvGh][9];         // G(t, s), row t mod kPvGh
   float xs[256];              // xp[0, 250) (frame 0's direct DFT)
+  float gh[2][kPvGh][8];      // G(t, s) over wave w's 64 bins, row t mod kPvGh (s = 7: unused)
   int cnt0;
 };
 struct PvShared {
-  cf et[9][kPvLd];            // e^{+2 pi i k s / 250}
   cf tw[256];                 // e^{+2 pi i q / 250}
   double tw64[256][2];        // e^{-2 pi i q / 250}, float64
+  double2 wt[6][128];         // w^j (j = 1 .. 6) of bin lane, float64, lane-major (one ds_read_b128 per wave)
   PvClip c[kPvClips];
 };
-__device__ __forceinline__ cf& pv_v(cf (*v)[kPvLd], int u, int k) { return v[u][k]; }
-#else
-// bin reduction with broadcast weights: lane 8u + p of each wave sums bins
-// [16p, 16p + 16) of frame u for its wave's s values; the 8 lanes of a part p
-// read the same e^{2 pi i k s / 250} (one LDS broadcast), then 3 lane-xor steps
-// add the 8 parts. Part pitch 18 complex (36 banks) and row pitch 144 complex
-// (== 32 banks mod 64) keep every 16-lane phase of a b128 read conflict-free.
-constexpr int kPvPart = 18;
-struct PvClip {
-  double d[kPvRows][8];       // row f - fb: d_j (j < 7) of frame f, [7] = the non-zero-count change
-  union {
-    cf v[8][8][kPvPart];      // V_t[k] of the group's frames: [u][k / 16][k % 16] (u = 7, k >= 126: 0)
-    float xs[256];            // init only: xp[0, 250) (frame 0's direct DFT)
-  };
-  float gh[kPvGh][9];         // G(t, s), row t mod kPvGh
-  int cnt0;
-};
-struct PvShared {
-  cf et[9][8][kPvPart];       // e^{+2 pi i k s / 250}, [s][k / 16][k % 16]
-  cf tw[256];                 // e^{+2 pi i q / 250}
-  double tw64[256][2];        // e^{-2 pi i q / 250}, float64
-  PvClip c[kPvClips];
-};
-#endif
+
+// the s of register r on lane b (b = lane & 7) is r ^ pv_g(b): with partners
+// b ^ 1, b ^ 2, b ^ 7 (DPP quad_perm / row_half_mirror) each reduce-scatter step
+// pairs equal s (pv_g(1) = 1, pv_g(2) = 2, pv_g(7) = 4), and lane b ends with s = pv_g(b)
+__device__ __forceinline__ int pv_g(int b) { return (b & 3) ^ ((b & 4) ? 7 : 0); }
+
+template <int kCtrl>
+__device__ __forceinline__ float pv_dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), kCtrl, 0xF, 0xF, true));
+}
+
+// reduce-scatter of (x, y) across lane ^ 16 (kSwap16) or lane ^ 32: lanes with
+// that bit clear get x + x', the others y + y'. (inline asm: the compiler's
+// builtin for the swap returns one register for both results in this
+// toolchain; s_nop covers the VALU-write -> permlane hazard)
+template <bool kSwap16>
+__device__ __forceinline__ float pv_swap_add(float x, float y) {
+  if (kSwap16)
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(x), "+v"(y));
+  else
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(x), "+v"(y));
+  return x + y;
+}
 
 // padded sample p of clip row xr (reflect padding by n_fft / 2)
 __device__ __forceinline__ float ps_xp(const float* xr, int L, int p) {
@@ -1531,8 +1538,26 @@ __device__ __forceinline__ void pv_load_rows(const PitchArgs& a, PvShared& sh, c
   }
 }
 
+#ifdef HBK_PHASE_TIMING
+// profiling build: wave 0 of each block sums the s_memtime cycles of the
+// vocoder's phases locally, adds them to g_aug_phase[16 + i] at the end
+#define HBK_PVT(i)                                     \
+  do {                                                 \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    pvt[i] += t_ - pvt_t0;                             \
+    pvt_t0 = t_;                                       \
+  } while (0)
+#else
+#define HBK_PVT(i) \
+  do {             \
+  } while (0)
+#endif
+
 __global__ void __launch_bounds__(128 * kPvClips) __attribute__((amdgpu_waves_per_eu(4)))
 ps_vocoder_kernel(PitchArgs a) {
+#ifdef HBK_PHASE_TIMING
+  unsigned long long pvt[5] = {0, 0, 0, 0, 0}, pvt_t0 = __builtin_amdgcn_s_memtime();
+#endif
   extern __shared__ __attribute__((aligned(16))) unsigned char pv_smem[];
   PvShared& sh = *reinterpret_cast<PvShared*>(pv_smem);
   const int tid = threadIdx.x, cl = tid >> 7, lane = tid & 127;
@@ -1548,17 +1573,6 @@ ps_vocoder_kernel(PitchArgs a) {
     sh.tw64[q][0] = cs;
     sh.tw64[q][1] = -sn;
   }
-  for (int q = tid; q < 9 * 128; q += blockDim.x) {
-    const int s = q / 128, k = q % 128;
-    double sn, cs;
-    sincospi(2.0 * ((k * s) % kPsFft) / kPsFft, &sn, &cs);
-    const cf ev = k < kPsBins ? cf{static_cast<float>(cs), static_cast<float>(sn)} : cf{0.f, 0.f};
-#ifdef HBK_PV_PAIR
-    sh.et[s][k] = ev;
-#else
-    sh.et[s][k >> 4][k & 15] = ev;
-#endif
-  }
   if (lane == 0) C.cnt0 = 0;
   __syncthreads();
   int nz = 0;
@@ -1568,22 +1582,30 @@ ps_vocoder_kernel(PitchArgs a) {
     nz += v != 0.f;
   }
   if (nz) atomicAdd(&C.cnt0, nz);
+  for (int q = tid; q < 6 * 128; q += blockDim.x) {
+    const int j = q / 128 + 1, kk = min(q % 128, kPsBins - 1), qq = (kk * j) % kPsFft;
+    sh.wt[j - 1][q % 128] = double2{sh.tw64[qq][0], sh.tw64[qq][1]};
+  }
   int fb = 1;
   pv_load_rows(a, sh, xr, cl, lane, fb);
   __syncthreads();
 
   const int k = min(lane, kPsBins - 1);
-  // per-bin constants: w^j (j < 7) and w^-7 in float64, the synthesis weight
-  double wr[7], wi[7];
-#pragma unroll
-  for (int j = 0; j < 7; ++j) {
-    const int q = (k * j) % kPsFft;
-    wr[j] = sh.tw64[q][0];
-    wi[j] = sh.tw64[q][1];
-  }
+  // per-bin constants: w^-7 in float64 (w^j, j < 7, read from sh.wt per slide), the synthesis weight
   const int q7 = (7 * k) % kPsFft;
   const double rr = sh.tw64[q7][0], ri = -sh.tw64[q7][1];
   const float ck = lane < kPsBins ? ((lane == 0 || lane == kPsBins - 1) ? 1.f : 2.f) : 0.f;
+  // synthesis weights c_k e^{2 pi i k s / 250} of the lane's registers (s = r ^ pv_g(lane & 7); s = 7: 0)
+  const int gb = pv_g(lane & 7), w = lane >> 6, ou = (lane >> 3) & 7;
+  cf esr[4], esi[4];  // (re, im) of registers 2j, 2j + 1 as pairs (packed products)
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int sr = r ^ gb;
+    const cf ev = sr < kPsHop ? ck * sh.tw[(k * sr) % kPsFft] : cf{0.f, 0.f};
+    esr[r >> 1][r & 1] = ev.x;
+    esi[r >> 1][r & 1] = -ev.y;
+  }
+  const bool b3 = lane & 8;
   const double kadv = static_cast<double>(7 * k) / kPsFft;  // the phase advance, in revolutions
   // frame 0: direct DFT (float64)
   double xre = 0.0, xim = 0.0;
@@ -1611,17 +1633,25 @@ ps_vocoder_kernel(PitchArgs a) {
       return;
     }
     const double* dr = C.d[f - fb];
-    double r0 = dr[0] * wr[0], r1 = dr[1] * wr[1], i0 = dr[0] * wi[0], i1 = dr[1] * wi[1];
-    r0 = fma(dr[2], wr[2], r0);
-    i0 = fma(dr[2], wi[2], i0);
-    r1 = fma(dr[3], wr[3], r1);
-    i1 = fma(dr[3], wi[3], i1);
-    r0 = fma(dr[4], wr[4], r0);
-    i0 = fma(dr[4], wi[4], i0);
-    r1 = fma(dr[5], wr[5], r1);
-    i1 = fma(dr[5], wi[5], i1);
-    r0 = fma(dr[6], wr[6], r0);
-    i0 = fma(dr[6], wi[6], i0);
+    int wl = lane;
+    asm volatile("" : "+v"(wl));  // opaque: keeps the (loop-invariant) table reads in the loop, out of VGPRs
+    double2 wj[6];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) wj[j] = sh.wt[j][wl];
+    double r0 = dr[0], r1 = dr[1] * wj[0].x, i1 = dr[1] * wj[0].y;  // w^0 = 1
+    double i0 = dr[2] * wj[1].y;
+    r0 = fma(dr[2], wj[1].x, r0);
+    r1 = fma(dr[3], wj[2].x, r1);
+    i1 = fma(dr[3], wj[2].y, i1);
+    __builtin_amdgcn_sched_barrier(0);  // half the w^j reads in flight at a time (VGPRs)
+#pragma unroll
+    for (int j = 3; j < 6; ++j) wj[j] = sh.wt[j][wl];
+    r0 = fma(dr[4], wj[3].x, r0);
+    i0 = fma(dr[4], wj[3].y, i0);
+    r1 = fma(dr[5], wj[4].x, r1);
+    i1 = fma(dr[5], wj[4].y, i1);
+    r0 = fma(dr[6], wj[5].x, r0);
+    i0 = fma(dr[6], wj[5].y, i0);
     ncnt = cnt + static_cast<int>(dr[7]);
     const double ar = xre + (r0 + r1), ai = xim + (i0 + i1);
     nre = ar * rr - ai * ri;
@@ -1660,7 +1690,7 @@ ps_vocoder_kernel(PitchArgs a) {
   const int dq = q7;
   const int jmax = (a.l1 + kPsPad - 1) / kPsHop;  // the frame of the last istft sample
   float* y = a.y + static_cast<int64_t>(e) * a.l1;
-  __syncthreads();  // xs (frame 0's samples) shares LDS with the V rows the first group writes
+  HBK_PVT(0);  // init: tables, frame 0, the first rows
 
   for (int t0 = 0; t0 <= jmax; t0 += kPvGroup) {
     // the group's source frames (and one ahead) must be resident: refill the d rows
@@ -1675,12 +1705,26 @@ ps_vocoder_kernel(PitchArgs a) {
         __syncthreads();
       }
     }
-    for (int u = 0; u < kPvGroup; ++u) {
+    HBK_PVT(1);  // row refills
+    float gr[kPvGroup];  // frame u: G(t0 + u, pv_g(lane & 7)) over the lane's octet
+    // one output frame; FULL: t < f_out and i0(t) <= c + 1 are known for the whole
+    // group, so the 7 frames are one straight-line block the scheduler can interleave
+    auto frame = [&](int u, auto full) {
+      constexpr bool FULL = decltype(full)::value;
       const int t = t0 + u;
+#if HBK_PV_ABLATE & 2  // profiling build: the per-bin vocoder replaced by a stand-in
       if (t < a.f_out) {
         float al;
+        ps_i0(a, t, al);
+        Q.x += al;
+      }
+      if (false) {
+#else
+      if (FULL || t < a.f_out) {
+#endif
+        float al;
         const int i0 = ps_i0(a, t, al);
-        if (i0 > c + 1) {  // rate > 1: a second source frame this step (rare)
+        if (!FULL && i0 > c + 1) {  // rate > 1: a second source frame this step (rare)
           ++c;
           ca = na;
           cm = nm;
@@ -1693,7 +1737,7 @@ ps_vocoder_kernel(PitchArgs a) {
           polar(pa, pm);
         }
         // the common step (i0 = c + 1) as selects, so that the vocoder of frame t and the
-        // look-ahead slide of the next source frame form one block the scheduler interleaves
+        // look-ahead slide of the next source frame form one block
         const bool step = i0 > c;
         c += step ? 1 : 0;
         ca = step ? na : ca;
@@ -1720,86 +1764,78 @@ ps_vocoder_kernel(PitchArgs a) {
         pa = step ? qa : pa;
         pm = step ? qm : pm;
       }
-#ifdef HBK_PV_PAIR
-      C.v[u][lane] = ck * cmul(Q, sh.tw[qz]);
+      // G(t, .) over the wave's bins: 7 products, reduce-scatter over the lane octet,
+      // all-reduce over the 8 octets
+      const cf vq = cmul(Q, sh.tw[qz]);
+#if HBK_PV_ABLATE & 1  // profiling build: no bin reduction
+      gr[u] = vq.x * esr[u & 3].x;
 #else
-      C.v[u][lane >> 4][lane & 15] = ck * cmul(Q, sh.tw[qz]);
+      cf pr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pr[j] = __builtin_elementwise_fma(cf{vq.x, vq.x}, esr[j], cf{vq.y, vq.y} * esi[j]);
+      const float q0 = pr[0].x + pv_dpp<0xB1>(pr[0].y), q1 = pr[1].x + pv_dpp<0xB1>(pr[1].y);  // lane ^ 1
+      const float q2 = pr[2].x + pv_dpp<0xB1>(pr[2].y), q3 = pr[3].x + pv_dpp<0xB1>(pr[3].y);
+      const float h0 = q0 + pv_dpp<0x4E>(q1), h1 = q2 + pv_dpp<0x4E>(q3);                     // lane ^ 2
+      const float gv = h0 + pv_dpp<0x141>(h1);                                                 // lane ^ 7
+      if (FULL) {
+        gr[u] = gv;  // u is a constant of the unrolled group
+      } else {
+#pragma unroll
+        for (int j = 0; j < kPvGroup; ++j) gr[j] = j == u ? gv : gr[j];
+      }
 #endif
+      __builtin_amdgcn_sched_barrier(0);  // frames stay in order: the unrolled group would spill
       qz += dq;
       qz -= qz >= kPsFft ? kPsFft : 0;
+    };
+    bool full = t0 + kPvGroup <= a.f_out;
+    if (full) {  // rate > 1 steps by >= 1 per frame: a double step makes the total advance exceed 7
+      float al;
+      full = ps_i0(a, t0 + kPvGroup - 1, al) - c <= kPvGroup;
     }
+    if (full) {
+#pragma unroll
+      for (int u = 0; u < kPvGroup; ++u) frame(u, std::true_type{});
+    } else {  // tail or double-step group: not unrolled
+#pragma unroll 1
+      for (int u = 0; u < kPvGroup; ++u) frame(u, std::false_type{});
+    }
+    // reduce-scatter over the octets: octet o keeps frame o (lane ^ 8, ^ 16, ^ 32)
+    float h[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float keep = b3 ? gr[2 * i + 1] : gr[2 * i], send = b3 ? gr[2 * i] : gr[2 * i + 1];
+      h[i] = keep + pv_dpp<0x128>(send);  // frame 2i + b3
+    }
+    const float h02 = pv_swap_add<true>(h[0], h[1]), h13 = pv_swap_add<true>(h[2], h[3]);
+    const float gsum = pv_swap_add<false>(h02, h13);
+    HBK_PVT(2);  // the group's frames
+    // rows t0 .. t0 + 7 of the ring; the previous group's istft step read other rows
+    if (gb < kPsHop) C.gh[w][(t0 + ou) % kPvGh][gb] = gsum;
     __syncthreads();
-#ifdef HBK_PV_PAIR
-    // G(t, s) of the group: 63 values, two lanes each (bins [0, 64) and [64, 128))
-    if (lane < 2 * 9 * kPvGroup) {
-      const int o = lane >> 1, h = lane & 1, u = o / 9, s = o % 9;
-      const float4* vp = reinterpret_cast<const float4*>(&C.v[u][64 * h]);
-      const float4* ep = reinterpret_cast<const float4*>(&sh.et[s][64 * h]);
-      cf acc0 = {0.f, 0.f}, acc1 = {0.f, 0.f};
-#pragma unroll 8
-      for (int i = 0; i < 32; ++i) {
-        const float4 v4 = vp[i], e4 = ep[i];
-        acc0 = __builtin_elementwise_fma(cf{v4.x, v4.y}, cf{e4.x, e4.y}, acc0);
-        acc1 = __builtin_elementwise_fma(cf{v4.z, v4.w}, cf{e4.z, e4.w}, acc1);
-      }
-      float g = (acc0.x - acc0.y) + (acc1.x - acc1.y);
-      g += __shfl_xor(g, 1);
-      if (h == 0) C.gh[(t0 + u) % kPvGh][s] = g;
-    }
-#else
-    {
-      // wave 0 of the clip: s = 0..4, wave 1: s = 5..8; lane 8u + p: frame u, bins [16p, 16p + 16)
-      const int w = lane >> 6, u = (lane >> 3) & 7, p = lane & 7;
-      const float4* vp = reinterpret_cast<const float4*>(C.v[u][p]);
-      const int s0 = 5 * w, ns = 5 - w;
-      // two passes over the part's bins (s0 .. s0+2, then s0+3, s0+4): fewer live accumulators
-#pragma unroll
-      for (int pass = 0; pass < 2; ++pass) {
-        constexpr int kJ = 3;
-        cf acc[kJ][2];
-#pragma unroll
-        for (int j = 0; j < kJ; ++j) acc[j][0] = acc[j][1] = cf{0.f, 0.f};
-        const int sb = s0 + kJ * pass;
-#pragma unroll 2
-        for (int i = 0; i < 8; ++i) {
-          const float4 v4 = vp[i];
-#pragma unroll
-          for (int j = 0; j < kJ; ++j) {
-            const float4 e4 = reinterpret_cast<const float4*>(sh.et[min(sb + j, 8)][p])[i];
-            acc[j][0] = __builtin_elementwise_fma(cf{v4.x, v4.y}, cf{e4.x, e4.y}, acc[j][0]);
-            acc[j][1] = __builtin_elementwise_fma(cf{v4.z, v4.w}, cf{e4.z, e4.w}, acc[j][1]);
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < kJ; ++j) {
-          float gj = (acc[j][0].x - acc[j][0].y) + (acc[j][1].x - acc[j][1].y);
-          gj += __shfl_xor(gj, 1);
-          gj += __shfl_xor(gj, 2);
-          gj += __shfl_xor(gj, 4);
-          const int jj = kJ * pass + j;
-          if (p == 0 && u < kPvGroup && jj < ns) C.gh[(t0 + u) % kPvGh][s0 + jj] = gj;
-        }
-      }
-    }
-#endif
-    __syncthreads();
+    HBK_PVT(3);  // G rows to LDS + barrier wait
     // the group's istft samples p = 7 t + r
     if (lane < kPsHop * kPvGroup && live) {
       const int t = t0 + lane / kPsHop, r = lane % kPsHop;
       const int m = kPsHop * t + r - kPsPad;
       if (t <= jmax && m >= 0 && m < a.l1) {
-        const float g1 = C.gh[t % kPvGh][r];
+        const float g1 = C.gh[0][t % kPvGh][r] + C.gh[1][t % kPvGh][r];
         float g2 = 0.f;
         if (r <= 4) {
-          if (t >= 36) g2 = C.gh[(t - 36) % kPvGh][r + 2];
+          if (t >= 36) g2 = C.gh[0][(t - 36) % kPvGh][r + 2] + C.gh[1][(t - 36) % kPvGh][r + 2];
         } else if (t >= 35) {
-          g2 = C.gh[(t - 35) % kPvGh][r - 5];
+          g2 = C.gh[0][(t - 35) % kPvGh][r - 5] + C.gh[1][(t - 35) % kPvGh][r - 5];
         }
         const int lo = max(0, t - 35 + (r >= 5 ? 1 : 0)), hi = min(a.f_out - 1, t);
         y[m] = (g1 - g2) / (static_cast<float>(kPsFft) * static_cast<float>(hi - lo + 1));
       }
     }
+    HBK_PVT(4);  // istft samples
   }
+#ifdef HBK_PHASE_TIMING
+  if (tid == 0)
+    for (int i = 0; i < 5; ++i) atomicAdd(&g_aug_phase[16 + i], pvt[i]);
+#endif
 }
 
 __global__ void ps_taps_kernel(PitchArgs a) {

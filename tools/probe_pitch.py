@@ -25,3 +25,18 @@ for num, den in ((128, 125), (125, 128)):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / iters
     print(f"pitch {num}/{den}: {n} clips {ms:.3f} ms -> {ms * 1e3 / n:.2f} us/clip", flush=True)
+    if os.environ.get("HBK_LIB", "").endswith("libhbk_phase.so"):  # vocoder phase cycles (wave 0 per block)
+        import ctypes
+        from heybuddy._native import lib
+        buf = (ctypes.c_ulonglong * 32)()
+        fn = lib().hbk_debug_aug_phase
+        fn.argtypes = [ctypes.c_void_p]
+        fn(buf)
+        pitch_shift(x, idx, num, den, out=x)
+        torch.cuda.synchronize()
+        fn(buf)
+        names = ["init", "refill", "frames", "G->LDS+barrier", "istft"]
+        tot = sum(buf[16 + i] for i in range(5))
+        blocks = (n + 1) // 2  # HBK_PV_CLIPS (2)
+        print("  vocoder phases: " + " ".join(f"{names[i]}={buf[16 + i] / tot * 100:.1f}%" for i in range(5))
+              + f"  {tot / blocks:.0f} cyc/block (wave 0)", flush=True)
