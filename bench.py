@@ -76,7 +76,7 @@ def parse():
     ap.add_argument("--pitch-prob", type=float, default=0.25,
                     help="config 5: PitchShift probability per batch (the reference's default 0.25)")
     ap.add_argument("--overlap", default=None,
-                    help="config 5 (default split:32 with pitch shift on, split:64 without): "
+                    help="config 5 (default split:64: 64 CUs train while 192 featurize): "
                          "train chunk s while chunk s + 1 is featurized on a second stream "
                          "(heybuddy.pipeline policies: off, prio, split:N, spill:N; N a multiple of 32, "
                          "i.e. whole CUs of every shader engine of every XCD)")
@@ -92,8 +92,8 @@ def parse():
     args = ap.parse_args()
     if args.pmc is None:
         args.pmc = os.path.join(ROOT, "profiles", f"pmc_c{args.config}_latest.json")
-    if args.overlap is None:  # pitch shift makes featurization ~3x heavier: give it 224 CUs (r02ag)
-        args.overlap = "split:32" if args.pitch_prob > 0 else "split:64"
+    if args.overlap is None:  # r03j: split:64 652k clips/s vs split:32 617k with pitch shift on
+        args.overlap = "split:64"
     return args
 
 
