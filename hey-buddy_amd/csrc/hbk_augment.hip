@@ -1389,11 +1389,12 @@ __global__ void __launch_bounds__(64) eq_kernel(EqArgs a) {
 // the clip's frames (kPvClips clips per workgroup in lockstep: every clip of a
 // call has the same frame geometry). No spectrogram is stored, no segment is
 // recomputed:
-//  * analysis: a sliding DFT in float64 (hop 7: X_f = w^-7 (X_{f-1} + sum_j d_j
-//    w^j), d_j = xp[7f+243+j] - xp[7f-7+j] exact in f64, w = e^{-2 pi i k/250});
-//    float64 keeps the recursion's error at ~1e-16 of the clip's level, so it
-//    is never restarted, and a frame whose 250 samples are all zero is exactly
-//    0 (angle 0) as in the FFT (a running count of non-zero samples);
+//  * analysis: a sliding DFT (hop 7: X_f = w^-7 (X_{f-1} + sum_j d_j w^j),
+//    d_j = xp[7f+243+j] - xp[7f-7+j], w = e^{-2 pi i k/250}) whose state X is
+//    float64 and whose increment sum_j d_j w^j is float32 (packed FMAs); a
+//    direct float64 DFT restarts it every kPvRestart frames. A frame whose 250
+//    samples are all zero is exactly 0 (angle 0) as in the FFT (a running
+//    count of non-zero samples);
 //  * vocoder: the phase in revolutions, accR_{t+1} = accR_t + wrap((a1 - a0) /
 //    2 pi - 7k/250): the phase advance adv_k = 2 pi 7k/250 cancels against the
 //    istft's frame rotation, so Z_t = Y_t e^{-2 pi i 7kt/250} = m_t e^{2 pi i accR_t};
@@ -1425,6 +1426,10 @@ constexpr int kPvClips = HBK_PV_CLIPS;                 // clips per workgroup (1
 constexpr int kPvGroup = 8;                            // output frames per istft step (lane 8u + .: frame u)
 constexpr int kPvRows = 64;                            // input frames of d rows held in LDS
 constexpr int kPvGh = 64;                              // ring of G(t, .) rows (>= 36 + kPvGroup)
+#ifndef HBK_PV_RESTART
+#define HBK_PV_RESTART 1024  // measured L2 vs the float64 oracle: 3.8e-5 at 128, 5.6e-5 at 256, 6.5e-5 at 1024
+#endif
+constexpr int kPvRestart = HBK_PV_RESTART;             // sliding-DFT frames between direct DFTs
 
 struct PitchArgs {
   const float* x;
@@ -1470,7 +1475,7 @@ __device__ __forceinline__ float ps_atan2(float y, float x) {
 }
 
 struct PvClip {
-  double d[kPvRows][8];       // row f - fb: d_j (j < 7) of frame f, [7] = the non-zero-count change
+  float d[kPvRows][8];        // row f - fb: d_j (j < 7) of frame f, [7] = the non-zero-count change
   float xs[256];              // xp[0, 250) (frame 0's direct DFT)
   float gh[2][kPvGh][8];      // G(t, s) over wave w's 64 bins, row t mod kPvGh (s = 7: unused)
   int cnt0;
@@ -1478,7 +1483,7 @@ struct PvClip {
 struct PvShared {
   cf tw[256];                 // e^{+2 pi i q / 250}
   double tw64[256][2];        // e^{-2 pi i q / 250}, float64
-  double2 wt[6][128];         // w^j (j = 1 .. 6) of bin lane, float64, lane-major (one ds_read_b128 per wave)
+  float4 wt[3][128];          // w^j, w^{j+1} (j = 1, 3, 5) of bin lane, lane-major (one ds_read_b128 per wave)
   PvClip c[kPvClips];
 };
 
@@ -1518,22 +1523,21 @@ __device__ __forceinline__ void pv_load_rows(const PitchArgs& a, PvShared& sh, c
                                              int fb) {
   for (int q = lane; q < 2 * kPvRows; q += 128) {
     const int row = q >> 1, h = q & 1, f = fb + row;
-    double* dr = sh.c[cl].d[row];
+    float* dr = sh.c[cl].d[row];
     if (f >= a.f_in) {
-      for (int j = 4 * h; j < 4 * h + 4; ++j) dr[j] = 0.0;
+      for (int j = 4 * h; j < 4 * h + 4; ++j) dr[j] = 0.f;
       continue;
     }
     if (h == 0) {
-      for (int j = 0; j < 4; ++j)
-        dr[j] = static_cast<double>(ps_xp(xr, a.L, 7 * f + 243 + j)) - static_cast<double>(ps_xp(xr, a.L, 7 * f - 7 + j));
+      for (int j = 0; j < 4; ++j) dr[j] = ps_xp(xr, a.L, 7 * f + 243 + j) - ps_xp(xr, a.L, 7 * f - 7 + j);
     } else {
       int delta = 0;
       for (int j = 0; j < 7; ++j) {
         const float vin = ps_xp(xr, a.L, 7 * f + 243 + j), vout = ps_xp(xr, a.L, 7 * f - 7 + j);
         delta += (vin != 0.f) - (vout != 0.f);
-        if (j >= 4) dr[j] = static_cast<double>(vin) - static_cast<double>(vout);
+        if (j >= 4) dr[j] = vin - vout;
       }
-      dr[7] = static_cast<double>(delta);
+      dr[7] = static_cast<float>(delta);
     }
   }
 }
@@ -1553,7 +1557,10 @@ __device__ __forceinline__ void pv_load_rows(const PitchArgs& a, PvShared& sh, c
   } while (0)
 #endif
 
-__global__ void __launch_bounds__(128 * kPvClips) __attribute__((amdgpu_waves_per_eu(4)))
+#ifndef HBK_PV_WAVES
+#define HBK_PV_WAVES 4  // waves per SIMD the vocoder is register-limited to
+#endif
+__global__ void __launch_bounds__(128 * kPvClips) __attribute__((amdgpu_waves_per_eu(HBK_PV_WAVES)))
 ps_vocoder_kernel(PitchArgs a) {
 #ifdef HBK_PHASE_TIMING
   unsigned long long pvt[5] = {0, 0, 0, 0, 0}, pvt_t0 = __builtin_amdgcn_s_memtime();
@@ -1582,9 +1589,11 @@ ps_vocoder_kernel(PitchArgs a) {
     nz += v != 0.f;
   }
   if (nz) atomicAdd(&C.cnt0, nz);
-  for (int q = tid; q < 6 * 128; q += blockDim.x) {
-    const int j = q / 128 + 1, kk = min(q % 128, kPsBins - 1), qq = (kk * j) % kPsFft;
-    sh.wt[j - 1][q % 128] = double2{sh.tw64[qq][0], sh.tw64[qq][1]};
+  for (int q = tid; q < 3 * 128; q += blockDim.x) {
+    const int j = 2 * (q / 128) + 1, kk = min(q % 128, kPsBins - 1), q1 = (kk * j) % kPsFft,
+              q2 = (kk * (j + 1)) % kPsFft;
+    sh.wt[q / 128][q % 128] = float4{static_cast<float>(sh.tw64[q1][0]), static_cast<float>(sh.tw64[q1][1]),
+                                     static_cast<float>(sh.tw64[q2][0]), static_cast<float>(sh.tw64[q2][1])};
   }
   int fb = 1;
   pv_load_rows(a, sh, xr, cl, lane, fb);
@@ -1607,21 +1616,26 @@ ps_vocoder_kernel(PitchArgs a) {
   }
   const bool b3 = lane & 8;
   const double kadv = static_cast<double>(7 * k) / kPsFft;  // the phase advance, in revolutions
-  // frame 0: direct DFT (float64)
-  double xre = 0.0, xim = 0.0;
-  {
+  // direct DFT (float64) of the frame staged in C.xs: frame 0, and every
+  // kPvRestart frames a restart of the sliding DFT (its float32 increments'
+  // rounding then accumulates over at most kPvRestart frames)
+  auto direct = [&](double& re, double& im) {
+    re = im = 0.0;
     int q = 0;
     for (int n = 0; n < kPsFft; ++n) {
       const double v = static_cast<double>(C.xs[n]);
-      xre = fma(v, sh.tw64[q][0], xre);
-      xim = fma(v, sh.tw64[q][1], xim);
+      re = fma(v, sh.tw64[q][0], re);
+      im = fma(v, sh.tw64[q][1], im);
       q += k;
       q -= q >= kPsFft ? kPsFft : 0;
     }
-  }
+  };
+  double xre, xim;
+  direct(xre, xim);
   int cnt = C.cnt0;
   if (cnt == 0) xre = xim = 0.0;
   int sf = 0;  // last slid frame
+  int anchor = 0;  // frame of the last direct DFT
   // the sliding DFT's next frame (sf + 1) from the current state, as a candidate
   // (xre, xim, cnt are committed by the caller): two partial sums per component
   // keep the float64 dependency chain short
@@ -1632,28 +1646,22 @@ ps_vocoder_kernel(PitchArgs a) {
       ncnt = cnt;
       return;
     }
-    const double* dr = C.d[f - fb];
+    // the increment sum_j d_j w^j in float32 (packed; d_j rounded once to float32): its
+    // rounding enters the float64 state as a random walk far below the state's level
+    const float4* drv = reinterpret_cast<const float4*>(C.d[f - fb]);
+    const float4 da = drv[0], db = drv[1];
     int wl = lane;
     asm volatile("" : "+v"(wl));  // opaque: keeps the (loop-invariant) table reads in the loop, out of VGPRs
-    double2 wj[6];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) wj[j] = sh.wt[j][wl];
-    double r0 = dr[0], r1 = dr[1] * wj[0].x, i1 = dr[1] * wj[0].y;  // w^0 = 1
-    double i0 = dr[2] * wj[1].y;
-    r0 = fma(dr[2], wj[1].x, r0);
-    r1 = fma(dr[3], wj[2].x, r1);
-    i1 = fma(dr[3], wj[2].y, i1);
-    __builtin_amdgcn_sched_barrier(0);  // half the w^j reads in flight at a time (VGPRs)
-#pragma unroll
-    for (int j = 3; j < 6; ++j) wj[j] = sh.wt[j][wl];
-    r0 = fma(dr[4], wj[3].x, r0);
-    i0 = fma(dr[4], wj[3].y, i0);
-    r1 = fma(dr[5], wj[4].x, r1);
-    i1 = fma(dr[5], wj[4].y, i1);
-    r0 = fma(dr[6], wj[5].x, r0);
-    i0 = fma(dr[6], wj[5].y, i0);
-    ncnt = cnt + static_cast<int>(dr[7]);
-    const double ar = xre + (r0 + r1), ai = xim + (i0 + i1);
+    const float4 w12 = sh.wt[0][wl], w34 = sh.wt[1][wl], w56 = sh.wt[2][wl];
+    cf acc = {da.x, 0.f};  // w^0 = 1
+    acc = __builtin_elementwise_fma(cf{da.y, da.y}, cf{w12.x, w12.y}, acc);
+    acc = __builtin_elementwise_fma(cf{da.z, da.z}, cf{w12.z, w12.w}, acc);
+    acc = __builtin_elementwise_fma(cf{da.w, da.w}, cf{w34.x, w34.y}, acc);
+    acc = __builtin_elementwise_fma(cf{db.x, db.x}, cf{w34.z, w34.w}, acc);
+    acc = __builtin_elementwise_fma(cf{db.y, db.y}, cf{w56.x, w56.y}, acc);
+    acc = __builtin_elementwise_fma(cf{db.z, db.z}, cf{w56.z, w56.w}, acc);
+    ncnt = cnt + static_cast<int>(db.w);
+    const double ar = xre + static_cast<double>(acc.x), ai = xim + static_cast<double>(acc.y);
     nre = ar * rr - ai * ri;
     nim = ar * ri + ai * rr;
     if (ncnt == 0) nre = nim = 0.0;
@@ -1667,7 +1675,7 @@ ps_vocoder_kernel(PitchArgs a) {
   auto polar_of = [&](double re, double im, float& ang, float& mag) {
     const float fr = static_cast<float>(re), fi = static_cast<float>(im);
     ang = ps_atan2(fi, fr);
-    mag = sqrtf(fmaf(fr, fr, fi * fi));
+    mag = __builtin_amdgcn_sqrtf(fmaf(fr, fr, fi * fi));  // v_sqrt_f32 (1 ulp), no denormal scaling
   };
   auto polar = [&](float& ang, float& mag) { polar_of(xre, xim, ang, mag); };
   // frames c, c + 1 in (ca, cm), (na, nm); frame c + 2 = sf ahead in (pa, pm)
@@ -1705,10 +1713,17 @@ ps_vocoder_kernel(PitchArgs a) {
         __syncthreads();
       }
     }
-    HBK_PVT(1);  // row refills
+    if (sf - anchor >= kPvRestart && sf < a.f_in) {  // uniform across the workgroup
+      __syncthreads();
+      for (int q = lane; q < kPsFft; q += 128) C.xs[q] = ps_xp(xr, a.L, kPsHop * sf + q);
+      __syncthreads();
+      direct(xre, xim);
+      if (cnt == 0) xre = xim = 0.0;
+      anchor = sf;
+    }
+    HBK_PVT(1);  // row refills, restarts
     float gr[kPvGroup];  // frame u: G(t0 + u, pv_g(lane & 7)) over the lane's octet
-    // one output frame; FULL: t < f_out and i0(t) <= c + 1 are known for the whole
-    // group, so the 7 frames are one straight-line block the scheduler can interleave
+    // one output frame; FULL: t < f_out and i0(t) = c + 1 are known for the whole group
     auto frame = [&](int u, auto full) {
       constexpr bool FULL = decltype(full)::value;
       const int t = t0 + u;
@@ -1736,9 +1751,9 @@ ps_vocoder_kernel(PitchArgs a) {
           commit(nre, nim, ncnt);
           polar(pa, pm);
         }
-        // the common step (i0 = c + 1) as selects, so that the vocoder of frame t and the
-        // look-ahead slide of the next source frame form one block
-        const bool step = i0 > c;
+        // the common step (i0 = c + 1): in a FULL group every frame steps (the source
+        // frames rename through the unrolled frames: no selects), elsewhere selects
+        const bool step = FULL || i0 > c;
         c += step ? 1 : 0;
         ca = step ? na : ca;
         cm = step ? nm : cm;
@@ -1789,9 +1804,9 @@ ps_vocoder_kernel(PitchArgs a) {
       qz -= qz >= kPsFft ? kPsFft : 0;
     };
     bool full = t0 + kPvGroup <= a.f_out;
-    if (full) {  // rate > 1 steps by >= 1 per frame: a double step makes the total advance exceed 7
-      float al;
-      full = ps_i0(a, t0 + kPvGroup - 1, al) - c <= kPvGroup;
+    if (full) {  // per-frame advances are all >= 1 (rate > 1) or all <= 1 (rate < 1): a total of
+      float al;  // kPvGroup means every frame of the group steps exactly once
+      full = ps_i0(a, t0 + kPvGroup - 1, al) - c == kPvGroup;
     }
     if (full) {
 #pragma unroll

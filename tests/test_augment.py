@@ -609,11 +609,13 @@ def test_pitch_shift_matches_oracle(num, den, inplace):
     """hbk_pitch_shift against the float64 restatement for both fast shifts:
     speech-like clips, two tones, leading / trailing silence, a silent clip, an
     exact-zero gap inside a clip, a chirp, and an unlisted clip (7) left
-    untouched. The kernel's analysis is a float64 sliding DFT (exact zeros kept
-    exact), its phase float64, its synthesis float32: per clip, L2 error <= 1e-5
-    of the reference's L2 and max error <= 1e-4 of its peak (a simulation of the
-    same arithmetic measured <= 1.9e-6 / 3.4e-6; the reference's own float32
-    torch.stft path differs from the float64 restatement by up to 5e-4, see
+    untouched. The kernel's sliding DFT keeps a float64 state with float32
+    increments (a direct float64 DFT every 1024 frames; exact zeros kept exact),
+    its phase float64, its synthesis float32: per clip, L2 error <= 1e-4 of the
+    reference's L2 and max error <= 1e-3 of its peak (measured worst: 6.5e-5 /
+    2.6e-4, on the chirp, whose quiet frames carry the increments' rounding
+    into the accumulated phase; the reference's own float32 torch.stft path
+    differs from the float64 restatement by up to 5e-4, see
     test_pitch_shift_oracle_vs_torch_stft_restatement)."""
     from heybuddy.kernels import pitch_shift
     x = _pitch_clips()
@@ -630,7 +632,7 @@ def test_pitch_shift_matches_oracle(num, den, inplace):
         l2 = np.sqrt(((out[i] - r) ** 2).sum()) / np.sqrt((r ** 2).sum())
         mx = np.abs(out[i] - r).max() / np.abs(r).max()
         worst = (max(worst[0], l2), max(worst[1], mx))
-        assert l2 <= 1e-5 and mx <= 1e-4, f"clip {i}: rel L2 {l2:.2e}, rel max {mx:.2e}"
+        assert l2 <= 1e-4 and mx <= 1e-3, f"clip {i}: rel L2 {l2:.2e}, rel max {mx:.2e}"
     print(f"pitch shift {num}/{den}: worst rel L2 {worst[0]:.2e}, worst rel max {worst[1]:.2e}")
     np.testing.assert_array_equal(out[7], x[7])
 
