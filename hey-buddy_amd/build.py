@@ -62,7 +62,6 @@ VARIANTS = {  # profiling builds (load with HBK_LIB=hey-buddy_amd/lib/<name>)
     "ablate": ("libhbk_ablate.so", ("-DHBK_ABLATE",)),      # HBK_DEBUG_SKIP phase ablation only
     "trace": ("libhbk_trace.so", ("-DHBK_TRACE",)),         # per-wave s_memtime timeline
     "pvc1": ("libhbk_pvc1.so", ("-DHBK_PV_CLIPS=1",)),       # pitch vocoder: 1 clip per workgroup (A/B)
-    "pvr128": ("libhbk_pvr128.so", ("-DHBK_PV_RESTART=128",)),  # pitch vocoder: direct DFT every 128 frames
     "pvr256": ("libhbk_pvr256.so", ("-DHBK_PV_RESTART=256",)),  # pitch vocoder: direct DFT every 256 frames
     "pvab1": ("libhbk_pvab1.so", ("-DHBK_PV_ABLATE=1",)),    # pitch vocoder ablation: no bin reduction
     "pvab2": ("libhbk_pvab2.so", ("-DHBK_PV_ABLATE=2",)),    # pitch vocoder ablation: no per-bin vocoder

@@ -1632,7 +1632,7 @@ ps_vocoder_kernel(PitchArgs a) {
   };
   double xre, xim;
   direct(xre, xim);
-  int cnt = C.cnt0;
+  int cnt = __builtin_amdgcn_readfirstlane(C.cnt0);
   if (cnt == 0) xre = xim = 0.0;
   int sf = 0;  // last slid frame
   int anchor = 0;  // frame of the last direct DFT
@@ -1660,7 +1660,7 @@ ps_vocoder_kernel(PitchArgs a) {
     acc = __builtin_elementwise_fma(cf{db.x, db.x}, cf{w34.z, w34.w}, acc);
     acc = __builtin_elementwise_fma(cf{db.y, db.y}, cf{w56.x, w56.y}, acc);
     acc = __builtin_elementwise_fma(cf{db.z, db.z}, cf{w56.z, w56.w}, acc);
-    ncnt = cnt + static_cast<int>(db.w);
+    ncnt = __builtin_amdgcn_readfirstlane(cnt + static_cast<int>(db.w));  // a clip's count: wave-uniform
     const double ar = xre + static_cast<double>(acc.x), ai = xim + static_cast<double>(acc.y);
     nre = ar * rr - ai * ri;
     nim = ar * ri + ai * rr;
@@ -1723,6 +1723,7 @@ ps_vocoder_kernel(PitchArgs a) {
     }
     HBK_PVT(1);  // row refills, restarts
     float gr[kPvGroup];  // frame u: G(t0 + u, pv_g(lane & 7)) over the lane's octet
+    float al_lane = 0.f;  // full groups: the alpha of frame t0 + (lane & 7)
     // one output frame; FULL: t < f_out and i0(t) = c + 1 are known for the whole group
     auto frame = [&](int u, auto full) {
       constexpr bool FULL = decltype(full)::value;
@@ -1738,7 +1739,13 @@ ps_vocoder_kernel(PitchArgs a) {
       if (FULL || t < a.f_out) {
 #endif
         float al;
-        const int i0 = ps_i0(a, t, al);
+        int i0;
+        if (FULL) {  // i0 = c + 1; the group's alphas were computed once, lane u -> frame u
+          i0 = c + 1;
+          al = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, al_lane), u));
+        } else {
+          i0 = ps_i0(a, t, al);
+        }
         if (!FULL && i0 > c + 1) {  // rate > 1: a second source frame this step (rare)
           ++c;
           ca = na;
@@ -1809,6 +1816,7 @@ ps_vocoder_kernel(PitchArgs a) {
       full = ps_i0(a, t0 + kPvGroup - 1, al) - c == kPvGroup;
     }
     if (full) {
+      ps_i0(a, t0 + (lane & 7), al_lane);
 #pragma unroll
       for (int u = 0; u < kPvGroup; ++u) frame(u, std::true_type{});
     } else {  // tail or double-step group: not unrolled
