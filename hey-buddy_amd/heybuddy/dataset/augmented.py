@@ -67,10 +67,59 @@ from heybuddy.constants import (DEFAULT_AUGMENT_BACKGROUND_NOISE_MAX_SNR_DB,
                                 DEFAULT_AUGMENT_SEVEN_BAND_PROB)
 from heybuddy.kernels import ReverbPlan, pitch_shift, place_clips, seven_band_eq, tanh_distortion
 
-__all__ = ["AugmentedAudioGenerator", "BatchAugmenter", "bandstop_cutoffs", "eq_coefficients", "eq_parameters",
-           "target_length_offset", "target_length_offsets", "to_target_length"]
+__all__ = ["AugmentedAudioGenerator", "BatchAugmenter", "SourceOrder", "bandstop_cutoffs", "eq_coefficients",
+           "eq_parameters", "hf_shuffle_permutation", "source_plan", "target_length_offset", "target_length_offsets",
+           "to_target_length"]
 
 T = 23040
+
+# Random streams. numpy's global RNG carries exactly the draws the reference's
+# own code makes from it, in its order: the leading silence of each placed clip
+# (augmented.py:219-223), the re-shuffle of a dataset iterator when it runs out
+# (augmented.py:148-162 -> datasets.Dataset.shuffle(), seeded from numpy's
+# state), and the background-noise and reverb coins of every batch
+# (augmented.py:370-392). The augmentation parameters come from torch's CPU
+# generator (torch_audiomentations draws from torch; audiomentations from
+# Python's random): with a seeded numpy the clip placement and dataset order
+# equal the reference's for any augmentation probabilities.
+
+
+def _u(shape, lo: float = 0.0, hi: float = 1.0) -> np.ndarray:
+    """Uniform [lo, hi) float64 draws from torch's CPU generator."""
+    return (torch.rand(shape, dtype=torch.float64) * (hi - lo) + lo).numpy()
+
+
+def hf_shuffle_permutation(n: int) -> np.ndarray:
+    """The permutation datasets.Dataset.shuffle() (no seed) applies: a seed
+    taken from numpy's global state (key[pos]), one np.random.random() step,
+    then default_rng(seed).permutation(n) (datasets 5.x arrow_dataset.shuffle)."""
+    _, keys, pos, *_ = np.random.get_state()
+    seed = keys[pos] if pos < 624 else keys[0]
+    np.random.random()
+    return np.random.default_rng(seed).permutation(n)
+
+
+class SourceOrder:
+    """The row order of AudioDatasetGenerator.get_next_dataset_value
+    (augmented.py:148-162) over a dataset of n rows: in order first
+    (shuffle_first=False), then a fresh shuffle() each time it runs out."""
+
+    def __init__(self, n: int) -> None:
+        if n <= 0:
+            raise ValueError("source dataset is empty")
+        self.n = int(n)
+        self.perm = np.arange(self.n)
+        self.pos = 0
+
+    def take(self, m: int) -> np.ndarray:
+        out = np.empty(int(m), dtype=np.int64)
+        for i in range(int(m)):
+            if self.pos == self.n:
+                self.perm = hf_shuffle_permutation(self.n)
+                self.pos = 0
+            out[i] = self.perm[self.pos]
+            self.pos += 1
+        return out
 
 # SevenBandParametricEQ: low shelf, five peaking filters, high shelf; center
 # frequency ranges (Hz) and the Q range of audiomentations' documentation
@@ -80,15 +129,15 @@ EQ_Q_RANGE = (0.5, 1.33)
 
 
 def eq_parameters(n: int, gain_db: float, sample_rate: int = 16000) -> np.ndarray:
-    """(center Hz, gain dB, Q) [n, 7, 3] from numpy's global RNG: centers
+    """(center Hz, gain dB, Q) [n, 7, 3] from torch's CPU generator: centers
     uniform on the mel scale within each band (the high shelf clamped to 0.95
     Nyquist), gains ~ U[-gain_db, gain_db], Q ~ U[0.5, 1.33]."""
     mel = lambda f: 2595.0 * np.log10(1.0 + np.asarray(f) / 700.0)  # noqa: E731
     lo, hi = mel([b[0] for b in EQ_BANDS]), mel([b[1] for b in EQ_BANDS])
-    f0 = 700.0 * (10.0 ** (np.random.uniform(lo, hi, (n, 7)) / 2595.0) - 1.0)
+    f0 = 700.0 * (10.0 ** ((lo + _u((n, 7)) * (hi - lo)) / 2595.0) - 1.0)
     f0[:, 6] = np.minimum(f0[:, 6], (sample_rate // 2) * 0.95)
-    g = np.random.uniform(-gain_db, gain_db, (n, 7))
-    q = np.random.uniform(*EQ_Q_RANGE, (n, 7))
+    g = _u((n, 7), -gain_db, gain_db)
+    q = _u((n, 7), *EQ_Q_RANGE)
     return np.stack([f0, g, q], axis=-1)
 
 
@@ -117,12 +166,12 @@ def bandstop_cutoffs(n: int, sample_rate: int = 16000):
     """n (cut_lo, cut_hi) pairs of torch_audiomentations BandStopFilter (float32
     fractions of the sample rate): center mel-uniform in [200, 4000] Hz (its
     convert_frequencies_to_mels: 2595 log10(1 + f / 700)), bandwidth fraction
-    U[0.5, 1.99], cut = f_c (1 -+ bw / 2) / sr; numpy's global RNG."""
+    U[0.5, 1.99], cut = f_c (1 -+ bw / 2) / sr; torch's CPU generator."""
     def mel(f):
         return 2595.0 * np.log10(1.0 + f / 700.0)
-    m = np.random.uniform(mel(200.0), mel(4000.0), n).astype(np.float32)
+    m = _u(n, mel(200.0), mel(4000.0)).astype(np.float32)
     fc = (np.float32(700.0) * (np.float32(10.0) ** (m / np.float32(2595.0)) - np.float32(1.0))).astype(np.float32)
-    bw = np.random.uniform(0.5, 1.99, n).astype(np.float32)
+    bw = _u(n, 0.5, 1.99).astype(np.float32)
     sr = np.float32(sample_rate)
     lo = (fc * (np.float32(1.0) - bw / np.float32(2.0)) / sr).astype(np.float32)
     hi = (fc * (np.float32(1.0) + bw / np.float32(2.0)) / sr).astype(np.float32)
@@ -248,29 +297,42 @@ class BatchAugmenter:
             self._advance[key] = nxt
         return nxt
 
-    def plan_batches(self, n: int):
+    def plan_batches(self, n: int, coins: Optional[np.ndarray] = None):
         """Per-clip noise offsets, spectrum indices and gains (dB) for n clips
-        (host bookkeeping that mirrors the reference's dataset iteration; the
-        per-batch coins and draws are vectorised over the call's batches)."""
+        (host bookkeeping that mirrors the reference's dataset iteration).
+        coins [nbat, 2]: each batch's background-noise and reverb draws from
+        numpy's global RNG (augmented.py:370-392; AugmentedAudioGenerator
+        interleaves them with the batches' placement draws, as the reference
+        does); drawn here, batch by batch, when not given. Every other draw
+        comes from torch's CPU generator, only for augmentations whose
+        probability is non-zero."""
         bs = self.batch_size
         nbat = (n + bs - 1) // bs
         sizes = np.full(nbat, bs, dtype=np.int64)
         sizes[-1] = n - bs * (nbat - 1)
         batch = np.repeat(np.arange(nbat), sizes)  # batch of each clip
         pos = np.arange(n) - batch * bs            # position within its batch
+        if coins is None:
+            coins = np.random.rand(nbat, 2)
+        coins = np.asarray(coins, dtype=np.float64).reshape(nbat, 2)
         # gain (torch_audiomentations Gain, per_batch): one value per batch
-        g_on = np.random.rand(nbat) < self.p_gain
-        g_db = np.random.uniform(self.gain_min_db, self.gain_max_db, nbat)
-        gain_db = np.where(g_on, g_db, 0.0).astype(np.float32)[batch]
+        gain_db = np.zeros(n, dtype=np.float32)
+        if self.p_gain > 0:
+            g_on = _u(nbat) < self.p_gain
+            g_db = _u(nbat, self.gain_min_db, self.gain_max_db)
+            gain_db = np.where(g_on, g_db, 0.0).astype(np.float32)[batch]
         # colored noise (AddColoredNoise, per_batch): one (snr, f_decay) per batch; NaN snr = off
-        c_on = np.random.rand(nbat) < self.p_colored
-        c_snr = np.random.uniform(*self.colored_snr, nbat)
-        c_fd = np.random.uniform(*self.colored_decay, nbat)
-        colored_snr = np.where(c_on, c_snr, np.nan).astype(np.float32)[batch]
-        colored_fd = c_fd.astype(np.float32)[batch]
+        colored_snr = np.full(n, np.nan, dtype=np.float32)
+        colored_fd = np.zeros(n, dtype=np.float32)
+        if self.p_colored > 0:
+            c_on = _u(nbat) < self.p_colored
+            c_snr = _u(nbat, *self.colored_snr)
+            c_fd = _u(nbat, *self.colored_decay)
+            colored_snr = np.where(c_on, c_snr, np.nan).astype(np.float32)[batch]
+            colored_fd = c_fd.astype(np.float32)[batch]
         # background noise: consecutive T-sample segments of the noise stream
         noise_off = np.full(n, -1, dtype=np.int64)
-        n_on = (np.random.rand(nbat) < self.p_noise) if self.ring is not None else np.zeros(nbat, bool)
+        n_on = (coins[:, 0] < self.p_noise) if self.ring is not None else np.zeros(nbat, bool)
         if n_on.any():
             start = np.full(nbat, -1, dtype=np.int64)
             for b in np.flatnonzero(n_on):
@@ -280,7 +342,7 @@ class BatchAugmenter:
             noise_off[sel] = start[batch][sel] + pos[sel] * T
         # reverb: one IR per batch, taken in order (augmented.py:188-192)
         spec_idx = np.full(n, -1, dtype=np.int32)
-        r_on = (np.random.rand(nbat) < self.p_reverb) if self.spectra is not None else np.zeros(nbat, bool)
+        r_on = (coins[:, 1] < self.p_reverb) if self.spectra is not None else np.zeros(nbat, bool)
         if r_on.any():
             n_spec = self.spectra.shape[0]
             ir = (self.ir_idx + np.cumsum(r_on) - 1) % n_spec
@@ -290,7 +352,8 @@ class BatchAugmenter:
         self._colored = (colored_snr, colored_fd)
         # band-stop (BandStopFilter, per_batch): one (center, bandwidth) per batch
         # whose coin came up; the filtered clips and their cutoffs
-        b_on = np.random.rand(nbat) < getattr(self, "p_bandstop", 0.0)
+        p_bs = getattr(self, "p_bandstop", 0.0)
+        b_on = (_u(nbat) < p_bs) if p_bs > 0 else np.zeros(nbat, bool)
         lo, hi = bandstop_cutoffs(int(b_on.sum()), getattr(self, "sample_rate", 16000))
         sel = b_on[batch]
         per = np.full(nbat, -1, dtype=np.int64)
@@ -300,34 +363,40 @@ class BatchAugmenter:
         # came up (random.choices over the shifts); the clips of each shift
         self._pitch = []
         if getattr(self, "p_pitch", 0.0) > 0:
-            p_on = np.random.rand(nbat) < self.p_pitch
-            p_pick = np.random.randint(0, len(self.pitch_shifts), nbat)
+            p_on = _u(nbat) < self.p_pitch
+            p_pick = torch.randint(0, len(self.pitch_shifts), (nbat,)).numpy()
             for j, f in enumerate(self.pitch_shifts):
                 clips = np.flatnonzero((p_on & (p_pick == j))[batch]).astype(np.int32)
                 if clips.size:
                     self._pitch.append((f.numerator, f.denominator, clips))
         # seven-band EQ (audiomentations, per clip): the clips whose coin came up
         # and their filters (parameters drawn for those clips only)
-        e_on = np.random.rand(n) < getattr(self, "p_eq", 0.0)
+        p_eq = getattr(self, "p_eq", 0.0)
+        e_on = (_u(n) < p_eq) if p_eq > 0 else np.zeros(n, bool)
         sr = getattr(self, "sample_rate", 16000)
         eq_idx = np.nonzero(e_on)[0].astype(np.int32)
         self._eq = (eq_idx, eq_coefficients(eq_parameters(eq_idx.size, getattr(self, "eq_gain_db", 0.0), sr), sr))
         # tanh distortion (audiomentations, per clip): NaN amount = off
-        t_on = np.random.rand(n) < getattr(self, "p_tanh", 0.0)
-        t_amt = np.random.uniform(*getattr(self, "tanh_range", (0.0, 0.0)), n)
-        self._tanh = np.where(t_on, t_amt, np.nan).astype(np.float32)
+        p_tanh = getattr(self, "p_tanh", 0.0)
+        self._tanh = np.full(n, np.nan, dtype=np.float32)
+        if p_tanh > 0:
+            t_on = _u(n) < p_tanh
+            t_amt = _u(n, *getattr(self, "tanh_range", (0.0, 0.0)))
+            self._tanh = np.where(t_on, t_amt, np.nan).astype(np.float32)
         return noise_off, spec_idx, gain_db
 
-    def prepare(self, n: int) -> Dict[str, Any]:
+    def prepare(self, n: int, coins: Optional[np.ndarray] = None) -> Dict[str, Any]:
         """Every host-side draw of one call over n clips (plan_batches, the
         background SNRs, the colored-noise seed) in the order __call__ makes
         them, with the EQ filters already in pinned memory: a pipelined caller
         prepares chunk s + 1 while the device works, then launches."""
-        noise_off, spec_idx, gain_db = self.plan_batches(n)
+        noise_off, spec_idx, gain_db = self.plan_batches(n, coins)
         ring_len = 0 if self.ring is None else self.ring.numel()
         if ring_len:
             noise_off = np.where(noise_off >= 0, noise_off % ring_len, -1)
-        snr = torch.from_numpy(np.random.uniform(self.snr_min, self.snr_max, n).astype(np.float32))
+        snr = torch.zeros(n, dtype=torch.float32)
+        if (noise_off >= 0).any():  # torchaudio add_noise's snr: torch.rand in the reference (:271-272)
+            snr = torch.from_numpy(_u(n, self.snr_min, self.snr_max).astype(np.float32))
         gain = None
         if self.p_gain > 0:  # torch_audiomentations convert_decibels_to_amplitude_ratio
             gain = torch.pow(10.0, torch.from_numpy(gain_db) / 20.0)
@@ -343,7 +412,8 @@ class BatchAugmenter:
         colored_snr, colored_fd = self._colored
         colored = None
         if not np.isnan(colored_snr).all():
-            colored = (torch.from_numpy(colored_fd), torch.from_numpy(colored_snr), int(np.random.randint(0, 2 ** 62)))
+            colored = (torch.from_numpy(colored_fd), torch.from_numpy(colored_snr),
+                       int(torch.randint(0, 2 ** 62, (1,)).item()))
         return {"n": n, "noise_off": torch.from_numpy(noise_off), "spec_idx": torch.from_numpy(spec_idx),
                 "snr": snr, "gain": gain, "eq": eq, "tanh": tanh, "bandstop": bandstop, "colored": colored,
                 "pitch": [(a, b, _pinned(torch.from_numpy(c))) for a, b, c in getattr(self, "_pitch", [])]}
@@ -395,6 +465,29 @@ class BatchAugmenter:
 # AugmentedAudioGenerator: the reference's class surface (augmented.py:16-427)
 # over the device chain above.
 # ---------------------------------------------------------------------------
+def source_plan(source_lengths: Sequence[int], num_samples: int, batch_size: int, target_num_samples: int):
+    """numpy's draws when an AugmentedAudioGenerator built over a source
+    dataset of len(source_lengths) rows yields num_samples clips (the
+    reference builds a new one per TrainingFeaturesGenerator.generate call,
+    features.py:434-440): per batch of batch_size, the rows (a fresh
+    SourceOrder: in order, re-shuffled when it runs out), each padded clip's
+    leading silence (to_target_length), then the background-noise and reverb
+    coins (augmented.py:396-427 -> :297-394). Returns (rows [num_samples],
+    leading silence [num_samples], coins [nbat, 2])."""
+    src = np.asarray(source_lengths, dtype=np.int64)
+    order = SourceOrder(src.shape[0])
+    rows, pres, coins = [], [], []
+    for b0 in range(0, int(num_samples), int(batch_size)):
+        r = order.take(min(int(batch_size), int(num_samples) - b0))
+        rows.append(r)
+        pres.append(target_length_offsets(src[r], target_num_samples))
+        coins.append(np.random.rand(2))
+    if not rows:
+        return np.zeros(0, np.int64), np.zeros(0, np.int32), np.zeros((0, 2))
+    return (np.concatenate(rows), np.concatenate(pres).astype(np.int32),
+            np.array(coins, dtype=np.float64).reshape(-1, 2))
+
+
 def target_length_offset(num_samples: int, target_num_samples: int) -> int:
     """Leading zeros to_target_length puts in front of a clip of num_samples
     (augmented.py:210-226): 0 when it is cropped or when exactly one sample is
@@ -528,7 +621,7 @@ class AugmentedAudioGenerator:
             pitch_shift_prob=pitch_shift_prob, pitch_shift_semitones=pitch_shift_semitones)
         self.device = self.augmenter.device
         self._source: Optional[List[Dict[str, Any]]] = None
-        self._source_pos = 0
+        self._order: Optional[SourceOrder] = None
 
     @property
     def target_num_samples(self) -> int:
@@ -548,13 +641,12 @@ class AugmentedAudioGenerator:
         return audio
 
     def get_next_audio_sample_dict(self) -> Dict[str, Any]:
-        """The next source row, in order, wrapping around (augmented.py:148-186)."""
+        """The next source row: in order, then re-shuffled each time the
+        dataset runs out (augmented.py:148-186; SourceOrder)."""
         if self._source is None:
             self._source = list(self.source_dataset)
-            if not self._source:
-                raise ValueError("source dataset is empty")
-        row = self._source[self._source_pos % len(self._source)]
-        self._source_pos += 1
+            self._order = SourceOrder(len(self._source))
+        row = self._source[int(self._order.take(1)[0])]
         return row if isinstance(row, dict) and "audio" in row else {"audio": _audio_arrays([row])[0]}
 
     def place_batch(self, batch: Sequence[Any]) -> torch.Tensor:
@@ -588,14 +680,33 @@ class AugmentedAudioGenerator:
         placed = self.place_batch(batch)
         return self.augmenter(placed, out=placed)
 
+    def plan_batches(self, lens: Sequence[int]):
+        """numpy's draws for consecutive batches of batch_size clips of the
+        given lengths, in the reference's order (augmented.py:396-427 ->
+        :297-394): per batch, each padded clip's leading silence, then the
+        background-noise and reverb coins. Returns (leading silence per clip,
+        coins [nbat, 2])."""
+        lens = np.asarray(lens, dtype=np.int64)
+        pres, coins = [], []
+        for b0 in range(0, lens.shape[0], self.batch_size):
+            pres.append(target_length_offsets(lens[b0:b0 + self.batch_size], self.target_num_samples))
+            coins.append(np.random.rand(2))
+        pre = np.concatenate(pres).astype(np.int32) if pres else np.zeros(0, np.int32)
+        return pre, np.array(coins, dtype=np.float64).reshape(-1, 2)
+
+    def plan_source(self, source_lengths: Sequence[int], num_samples: int):
+        """source_plan with this generator's batch size and target length."""
+        return source_plan(source_lengths, num_samples, self.batch_size, self.target_num_samples)
+
     def prepare_device(self, clips: torch.Tensor, lengths: Optional[Sequence[int]] = None) -> Dict[str, Any]:
-        """The host-side draws of one augment_device call (placement offsets,
-        then BatchAugmenter.prepare), so that a pipelined caller can make them
-        ahead of the launch."""
+        """The host-side draws of one augment_device call (per batch: the
+        placement offsets, then the two coins; then BatchAugmenter.prepare's
+        torch draws), so that a pipelined caller can make them ahead of the
+        launch."""
         n = clips.shape[0]
         lens = np.full(n, clips.shape[1], dtype=np.int32) if lengths is None else np.asarray(lengths, np.int32)
-        return {"lens": lens, "pre": target_length_offsets(lens, self.target_num_samples),
-                "chain": self.augmenter.prepare(n)}
+        pre, coins = self.plan_batches(lens)
+        return {"lens": lens, "pre": pre, "chain": self.augmenter.prepare(n, coins)}
 
     def augment_device(self, clips: torch.Tensor, lengths: Optional[Sequence[int]] = None,
                        prepared: Optional[Dict[str, Any]] = None) -> torch.Tensor:

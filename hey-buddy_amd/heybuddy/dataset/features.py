@@ -30,8 +30,10 @@ from __future__ import annotations
 
 import math
 import os
+import random
 import re
-from typing import Any, List, Optional, Sequence, Tuple, Union
+import zlib
+from typing import Any, Callable, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
 import torch
@@ -169,7 +171,8 @@ class SyntheticSpeechGenerator:
         self.num_adversarial_texts = max(1, int(num_adversarial_texts))
         self.device = torch.device("cpu") if device_id is None else torch.device("cuda", device_id)
         self.sample_rate = target_sample_rate
-        self.seed = int(np.random.randint(0, 2 ** 31 - 1)) if seed is None else int(seed)
+        # not from numpy's global RNG: its stream carries exactly the reference's draws
+        self.seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if seed is None else int(seed)
 
     def device_batch(self, n: int) -> Tuple[torch.Tensor, np.ndarray]:
         from heybuddy.synthetic import speech_clips
@@ -288,9 +291,13 @@ class TrainingFeaturesGenerator:
         return get_speech_embeddings(device_id=self.device.index)
 
     def get_tts_generator(self) -> SyntheticSpeechGenerator:
+        # the stand-in's seed counts the calls (distinct utterances per chunk, and no draw
+        # from the RNG states __call__ restores per chunk)
+        self._tts_calls = getattr(self, "_tts_calls", 0) + 1
+        seed = (zlib.crc32(f"{self.tts_text}|{self.tts_adversarial}".encode()) + 7919 * self._tts_calls) % (2 ** 31 - 1)
         return SyntheticSpeechGenerator(self.tts_text, adversarial=self.tts_adversarial,
                                         num_adversarial_texts=self.tts_adversarial_num_phrases,
-                                        device_id=self.device.index, target_sample_rate=self.sample_rate)
+                                        device_id=self.device.index, target_sample_rate=self.sample_rate, seed=seed)
 
     def _bank(self, which: str, testing: bool) -> Any:
         ds = self.augment_background_dataset if which == "noise" else self.augment_impulse_dataset
@@ -341,9 +348,16 @@ class TrainingFeaturesGenerator:
             lens = np.minimum(lengths, T).astype(np.int32)
             pre = ((T - lens) // 2).astype(np.int32)
             return place_clips(clips, lens, pre, T)
-        idx = np.arange(num_samples) % n_tts  # the source dataset is iterated in order, wrapping
-        src = clips if num_samples == n_tts else clips.index_select(0, torch.from_numpy(idx).to(clips.device))
-        return self.get_augmented_generator(testing=testing).augment_device(src, lengths[idx])
+        # a fresh AugmentedAudioGenerator per call in the reference (:434-440): the source
+        # rows in order, re-shuffled when they run out; the noise / IR iteration from the start
+        aug = self.get_augmented_generator(testing=testing)
+        aug.augmenter.noise_idx = aug.augmenter.ir_idx = 0
+        rows, pre, coins = aug.plan_source(lengths, num_samples)
+        lens = np.asarray(lengths)[rows].astype(np.int32)
+        same = num_samples == n_tts and np.array_equal(rows, np.arange(n_tts))
+        src = clips if same else clips.index_select(0, torch.from_numpy(rows).to(clips.device))
+        prepared = {"lens": lens, "pre": pre, "chain": aug.augmenter.prepare(num_samples, coins)}
+        return aug.augment_device(src, lens, prepared=prepared)
 
     def generate_device(self, num_samples: int, testing: bool = False, validation: bool = False) -> torch.Tensor:
         """features.py:360-490 with every stage in HBM: [num_samples, 16, 96] f32 on the device."""
@@ -366,23 +380,40 @@ class TrainingFeaturesGenerator:
             logger.warning("sample wav export needs an audio writer; skipped")
         return self.generate_device(num_samples, testing=testing, validation=validation).cpu().numpy()
 
+    def _chunks(self, num_samples: int, fn: Callable[[int], Any]) -> List[Any]:
+        """fn over chunks of sample_batch_size (features.py:492-535). The
+        reference runs each chunk in a forked ProcessPoolExecutor worker: every
+        chunk starts from the caller's numpy / torch / random states and none
+        of its draws reach the caller. The same here: the states are restored
+        before each chunk and after the last."""
+        sizes = [self.sample_batch_size] * math.ceil(num_samples / self.sample_batch_size)
+        if num_samples % self.sample_batch_size:
+            sizes[-1] = num_samples % self.sample_batch_size
+        states = (np.random.get_state(), torch.random.get_rng_state(), random.getstate())
+        parts = []
+        try:
+            for size in sizes:
+                np.random.set_state(states[0])
+                torch.random.set_rng_state(states[1])
+                random.setstate(states[2])
+                parts.append(fn(size))
+        finally:
+            np.random.set_state(states[0])
+            torch.random.set_rng_state(states[1])
+            random.setstate(states[2])
+        return parts
+
     def __call__(self, num_samples: int, sample_save_path: Optional[str] = None,
                  augmented_sample_save_path: Optional[str] = None, testing: bool = False,
                  validation: bool = False) -> np.ndarray:
         """Chunks of sample_batch_size, concatenated (features.py:492-535)."""
-        sizes = [self.sample_batch_size] * math.ceil(num_samples / self.sample_batch_size)
-        if num_samples % self.sample_batch_size:
-            sizes[-1] = num_samples % self.sample_batch_size
-        parts = [self.generate(s, sample_save_path, augmented_sample_save_path, testing, validation)
-                 for s in sizes]
+        parts = self._chunks(num_samples, lambda s: self.generate(s, sample_save_path, augmented_sample_save_path,
+                                                                 testing, validation))
         return parts[0] if len(parts) == 1 else np.concatenate(parts)
 
     def call_device(self, num_samples: int, testing: bool = False, validation: bool = False) -> torch.Tensor:
         """__call__ without the host copy: [num_samples, 16, 96] f32 in HBM."""
-        sizes = [self.sample_batch_size] * math.ceil(num_samples / self.sample_batch_size)
-        if num_samples % self.sample_batch_size:
-            sizes[-1] = num_samples % self.sample_batch_size
-        parts = [self.generate_device(s, testing=testing, validation=validation) for s in sizes]
+        parts = self._chunks(num_samples, lambda s: self.generate_device(s, testing=testing, validation=validation))
         if not parts:
             return torch.empty((0, 16, 96), dtype=torch.float32, device=self.device)
         return parts[0] if len(parts) == 1 else torch.cat(parts)

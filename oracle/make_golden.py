@@ -23,8 +23,11 @@ records its outputs on seeded inputs:
                          global RNG seeded (crop, 1-sample pad, random pads).
   onnx_heads.npz         the shipped src/js/models/*.onnx heads through the
                          reference WakeWordMLPModel (zeros KAT + seeded inputs).
+  extract_driver.npz,    PrecalculatedTrainingDatasetGenerator.__call__ and
+  extract_numeric.npz,   TrainingFeaturesGenerator.__call__ runs (see
+  features_driver.npz    oracle/golden_drivers.py).
 
-Usage: python oracle/make_golden.py [--only featurizer|classifier|stages|augment|onnx]
+Usage: python oracle/make_golden.py [--only featurizer|classifier|stages|augment|onnx|drivers]
 """
 from __future__ import annotations
 
@@ -179,6 +182,10 @@ def main():
         golden_classifier.make_to_target_length(hb, GOLDEN)
     if args.only in (None, "onnx"):
         golden_classifier.make_onnx_heads(hb, GOLDEN)
+    if args.only in (None, "drivers"):
+        from oracle import golden_drivers
+        golden_drivers.make_extract(hb, GOLDEN)
+        golden_drivers.make_features(hb, GOLDEN)
 
 
 if __name__ == "__main__":

@@ -2,10 +2,12 @@
 dataset/features.py:360-535, :628-908) against the oracle composition.
 
 The generator's inputs are recorded as it runs (the TTS stand-in's clips and
-the placement offsets it draws from numpy's global RNG), and the expected
-features are recomputed from them on the host: to_target_length placement
-(augmented.py:200-232) of source clip i mod n_tts (the augment_sample_ratio
-wrap of features.py:430-446), then oracle.featurizer.featurize (the
+the source rows and placement offsets it draws from numpy's global RNG), and
+the expected features are recomputed from them on the host: to_target_length
+placement (augmented.py:200-232) of the recorded source row (in order, then
+re-shuffled when the utterances run out: the augment_sample_ratio wrap of
+features.py:430-446; the draws themselves are pinned against a reference run
+in test_drivers_reference.py), then oracle.featurizer.featurize (the
 reference's SpeechEmbeddings.__call__ orchestration with the oracle mel /
 embedding; embeddings.py:153-234). Checked: chunking by sample_batch_size
 (features.py:492-535), the wrap, placement, featurization and the row order
@@ -30,9 +32,15 @@ OFF = dict(augment_seven_band_prob=0.0, augment_tanh_distortion_prob=0.0, augmen
 def _record(monkeypatch):
     from heybuddy.dataset import augmented as A
     from heybuddy.dataset import features as F
-    rec = {"tts": [], "pre": []}
+    rec = {"tts": [], "pre": [], "rows": []}
     real_batch = F.SyntheticSpeechGenerator.device_batch
     real_off = A.target_length_offsets
+    real_plan = A.source_plan
+
+    def plan(*a, **k):
+        out = real_plan(*a, **k)
+        rec["rows"].append(out[0].copy())
+        return out
 
     def device_batch(self, n):
         clips, lens = real_batch(self, n)
@@ -46,6 +54,7 @@ def _record(monkeypatch):
 
     monkeypatch.setattr(F.SyntheticSpeechGenerator, "device_batch", device_batch)
     monkeypatch.setattr(A, "target_length_offsets", offsets)
+    monkeypatch.setattr(A, "source_plan", plan)
     return rec
 
 
@@ -73,15 +82,15 @@ def test_feature_generator_chunks_wrap_and_placement(monkeypatch):
     assert got.shape == (110, 16, 96) and got.dtype == np.float32
     assert [c.shape[0] for c, _ in rec["tts"]] == [24, 24, 7]
     audio = []
-    for (clips, lens), pre, m in zip(rec["tts"], rec["pre"], (48, 48, 14)):
-        idx = np.arange(m) % clips.shape[0]
-        assert pre.shape == (m,)
+    for (clips, lens), pre, idx, m in zip(rec["tts"], rec["pre"], rec["rows"], (48, 48, 14)):
+        assert pre.shape == (m,) and idx.shape == (m,)
+        n_tts = clips.shape[0]
+        assert (idx[:n_tts] == np.arange(n_tts)).all()        # the first pass in order
+        if m >= 2 * n_tts:                                      # then a permutation of the utterances
+            assert sorted(idx[n_tts:2 * n_tts].tolist()) == list(range(n_tts))
         audio += [_place(clips[j], lens[j], pre[i]) for i, j in enumerate(idx)]
     audio = np.stack(audio)
     _check(got, audio, [0, 5, 23, 24, 47, 48, 60, 95, 96, 101, 109])
-    # the wrapped rows reuse the same utterance, with their own placement draw
-    same = np.array_equal(audio[0], audio[24])
-    assert not same or rec["pre"][0][0] == rec["pre"][0][24]
 
 
 def test_validation_features_centre_padded(monkeypatch):
