@@ -400,8 +400,8 @@ __device__ __forceinline__ void guard4(int* flag, float a, float b, float c, flo
 __device__ __forceinline__ void split2(float a, float b, h2& hi, h2& lo) {
   hi = __builtin_amdgcn_cvt_pkrtz(a, b);
   const uint32_t hb = __builtin_bit_cast(uint32_t, hi);
-  uint32_t l = 0;
-  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "+v"(l) : "v"(a), "v"(hb));
+  uint32_t l;  // mixlo writes bits 15:0, mixhi bits 31:16: no initial value needed
+  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(l) : "v"(a), "v"(hb));
   asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(l) : "v"(b), "v"(hb));
   lo = __builtin_bit_cast(h2, l);
 }
@@ -969,8 +969,8 @@ struct P0Geo {
 __device__ __forceinline__ void split2_mix(float a, float b, uint32_t& hi, uint32_t& lo, float& amax) {
   track(amax, a, b);
   hi = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(a, b));
-  uint32_t l = 0;
-  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "+v"(l) : "v"(a), "v"(hi));
+  uint32_t l;  // mixlo writes bits 15:0, mixhi bits 31:16: no initial value needed
+  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(l) : "v"(a), "v"(hi));
   asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(l) : "v"(b), "v"(hi));
   lo = l;
 }
@@ -1418,6 +1418,510 @@ p1_chain_kernel(P1Args a) {
   raise_range(a.range_flag, amax);
 }
 
+// ------------------------------------------------------------------ p0s ----
+// Streaming form of the p0 chain (SE20 chain 0 on a 32-wide mel image:
+// 3x3 1 -> 24, 1x3 24 -> 24, 3x1 24 -> 24, max-pool 2x2): ONE WAVE PER CLIP,
+// the clip's rows streamed top to bottom, no halo recomputation and no
+// workgroup barrier. A tile is one row (32 positions; 30 / 28 / 28 valid).
+// Iteration y runs three independent MFMA chains:
+//   stage 0 of row y      B from the raw rows in registers      -> s0[y & 1]
+//   stage 1 of row y - 1  B from s0[(y - 1) & 1] (LDS)          -> s1[(y - 1) & 3]
+//   stage 2 of row y - 4  B from s1 rows y - 4 .. y - 2 (LDS)   -> registers
+// Every LDS row an iteration reads was written by an earlier iteration of the
+// same wave, and a wave's LDS instructions execute in order, so a compiler
+// barrier between iterations is the only synchronisation. Stage-2 rows 2i and
+// 2i + 1 are max-pooled in registers, the column pairs by a DPP lane swap,
+// and the pooled row is stored as f32 [66][14][24] (the p1 chain's input).
+// Raw rows: one dword per lane per row, loaded 8-11 rows ahead; the three
+// column taps come from two DPP wave shifts. Biases ride in a padding slot
+// of K whose B value is 1 (hi 1, lo 0), so every accumulator starts at 0.
+constexpr int kP0sWaves = 4;
+constexpr int kP0sThreads = 64 * kP0sWaves;
+constexpr int kP0sCS = 24;                         // fp16 per position (3 odd 16-B groups)
+constexpr int kP0sS0Plane = 34 * kP0sCS;           // positions 0..33 (x + tap <= 33)
+constexpr int kP0sS1Plane = 32 * kP0sCS;
+constexpr int kP0sOnes = 4 * kP0sS0Plane + 8 * kP0sS1Plane;  // fp16 offset of the ones / zeros slots
+constexpr int kP0sWaveHalfs = kP0sOnes + 16;
+constexpr int kP0sLds = kP0sWaves * kP0sWaveHalfs * 2;
+constexpr int kP0sKS = 5;                          // K steps of stages 1 and 2 (72 + bias slot)
+constexpr int kP0sRows = 136, kP0sHout = 66, kP0sWout = 14, kP0sC = 24;
+
+struct P0sW {
+  h8 h[kP0sKS], l[kP0sKS];
+};
+
+__device__ __forceinline__ float wave_shl1(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xf, 0xf, false));
+}
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// LeakyReLU of two values: one packed multiply, two maxes (NaN stays NaN)
+template <bool LEAKY>
+__device__ __forceinline__ void p0s_act2(float& a, float& b, float alpha) {
+  if (!LEAKY) return;
+  const f2v m = f2v{a, b} * alpha;
+  asm("v_max_f32 %0, %0, %1" : "+v"(a) : "v"(m.x));
+  asm("v_max_f32 %0, %0, %1" : "+v"(b) : "v"(m.y));
+}
+
+// activation, split and LDS store of one finished stage-0 / stage-1 tile
+template <bool LEAKY>
+__device__ __forceinline__ void p0s_store(const f16x& acc, _Float16* oh, int x, int khalf, float alpha, bool track_it,
+                                          float& amax, int plane) {
+  float m = 0.f;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    float v[4] = {acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]};
+    p0s_act2<LEAKY>(v[0], v[1], alpha);
+    p0s_act2<LEAKY>(v[2], v[3], alpha);
+    uint32_t h01, l01, h23, l23;
+    split2_mix(v[0], v[1], h01, l01, m);
+    split2_mix(v[2], v[3], h23, l23, m);
+    const int o = x * kP0sCS + 8 * q + 4 * khalf;
+    *reinterpret_cast<uint2*>(oh + o) = uint2{h01, h23};
+    *reinterpret_cast<uint2*>(oh + plane + o) = uint2{l01, l23};
+  }
+  asm("v_max_f32 %0, %0, %1" : "+v"(amax) : "v"(track_it ? m : 0.f));
+}
+
+template <bool LEAKY>
+struct P0sCtx {
+  h8 a0h, a0l;
+  P0sW w1, w2;
+  float r[2][3];   // raw rows y + khalf, y + 1 + khalf at columns x, x + 1, x + 2
+  float q[8];      // raw rows loaded ahead (column x; row + khalf)
+  f16x pool;       // stage-2 row 2i (even) awaiting its partner
+  float amax;
+  float alpha;
+};
+
+template <int PAR, bool LEAKY>
+__device__ __forceinline__ void p0s_iter(P0sCtx<LEAKY>& c, int y, int qi, _Float16* wl, float* orow_base, int x,
+                                         int khalf) {
+  // raw window: rows y + khalf, y + 1 + khalf (the second from the load queue)
+  c.r[0][0] = c.r[1][0]; c.r[0][1] = c.r[1][1]; c.r[0][2] = c.r[1][2];
+  c.r[1][0] = c.q[qi];
+  c.r[1][1] = wave_shl1(c.r[1][0]);
+  c.r[1][2] = wave_shl1(c.r[1][1]);
+
+  _Float16* s0w = wl + (PAR & 1) * 2 * kP0sS0Plane;        // stage 0 writes row y
+  _Float16* s0r = wl + ((PAR + 1) & 1) * 2 * kP0sS0Plane;  // stage 1 reads row y - 1
+  _Float16* s1 = wl + 4 * kP0sS0Plane;
+
+  // B fragments of stage 1 (row y - 1) and stage 2 (row y - 4), one K step
+  // ahead of their MFMAs (two sets live). Stage 1: K group g = 2 ks + khalf =
+  // tap * 3 + c sits at s0 fp16 offset 24 (x + tap) + 8 c = 24 x + 8 g, one
+  // per-lane base plus immediates; group 9 is the bias slot (B = 1). Stage 2:
+  // the groups (dy, c) are paired within a row for ks < 3 (khalf = c), then
+  // (0, 2) | (1, 2) and (2, 2) | bias (kP0sG2, mirrored by plan_p0s's packing).
+  const _Float16* base1 = s0r + x * kP0sCS + 8 * khalf;
+  const _Float16* base2 = s1 + x * kP0sCS + 8 * khalf;
+  auto load = [&](int ks, h8& b1h, h8& b1l, h8& b2h, h8& b2l) {
+    const _Float16* p1 = base1 + 16 * ks;
+    const _Float16* p2;
+    if (ks < 3) {
+      p2 = base2 + ((PAR + ks) & 3) * 2 * kP0sS1Plane;
+    } else if (ks == 3) {
+      p2 = s1 + x * kP0sCS + 16 + (khalf ? ((PAR + 1) & 3) : (PAR & 3)) * 2 * kP0sS1Plane;
+    } else {
+      p1 = khalf ? wl + kP0sOnes : p1;
+      p2 = khalf ? wl + kP0sOnes : s1 + x * kP0sCS + 16 + ((PAR + 2) & 3) * 2 * kP0sS1Plane;
+    }
+    const bool one1 = ks == 4 && khalf, one2 = ks == 4 && khalf;
+    b1h = *reinterpret_cast<const h8*>(p1);
+    b1l = *reinterpret_cast<const h8*>(p1 + (one1 ? 8 : kP0sS0Plane));
+    b2h = *reinterpret_cast<const h8*>(p2);
+    b2l = *reinterpret_cast<const h8*>(p2 + (one2 ? 8 : kP0sS1Plane));
+  };
+  h8 f[2][4];
+  load(0, f[0][0], f[0][1], f[0][2], f[0][3]);
+
+  // stage 0 (row y): K slots {r0[0..2], r1[0..2], 1, 0} in both lane halves, the
+  // window one row lower in the upper half (taps (0, *), (1, 0), (1, 1) and the
+  // bias in the lower half's weights, (1, 2), (2, *) in the upper half's)
+  uint32_t hb[3], lb[3];
+  float m0 = 0.f;
+  split2_mix(c.r[0][0], c.r[0][1], hb[0], lb[0], m0);
+  split2_mix(c.r[0][2], c.r[1][0], hb[1], lb[1], m0);
+  split2_mix(c.r[1][1], c.r[1][2], hb[2], lb[2], m0);
+  const h8 xh = __builtin_bit_cast(h8, uint4{hb[0], hb[1], hb[2], 0x3C00u});  // slot 6 = 1.0 (f16)
+  const h8 xl = __builtin_bit_cast(h8, uint4{lb[0], lb[1], lb[2], 0u});
+  const f16x zero = {};
+  f16x acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(c.a0h, xh, zero, 0, 0, 0);
+  acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(c.a0h, xl, acc0, 0, 0, 0);
+  acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(c.a0l, xh, acc0, 0, 0, 0);
+
+  // stage 2 accumulates into c.pool for an even row y - 4 (held for its odd partner)
+  f16x acc1 = zero, acc2 = zero;
+  f16x& a2 = (PAR & 1) == 0 ? c.pool : acc2;
+  a2 = zero;
+#pragma unroll
+  for (int ks = 0; ks < kP0sKS; ++ks) {
+    h8* cur = f[ks & 1];
+    if (ks + 1 < kP0sKS) {
+      h8* nx = f[(ks + 1) & 1];
+      load(ks + 1, nx[0], nx[1], nx[2], nx[3]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(c.w1.h[ks], cur[0], acc1, 0, 0, 0);
+    a2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(c.w2.h[ks], cur[2], a2, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(c.w1.h[ks], cur[1], acc1, 0, 0, 0);
+    a2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(c.w2.h[ks], cur[3], a2, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(c.w1.l[ks], cur[0], acc1, 0, 0, 0);
+    a2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(c.w2.l[ks], cur[2], a2, 0, 0, 0);
+  }
+
+  // epilogues: stage 0 -> s0[y & 1] (rows < 134, positions < 30 tracked),
+  // stage 1 -> s1[(y - 1) & 3] (rows 0 .. 133, positions < 28 tracked)
+  const bool raw_ok = y < kP0sRows - 2;
+  asm("v_max_f32 %0, %0, %1" : "+v"(c.amax) : "v"(raw_ok ? m0 : 0.f));
+  p0s_store<LEAKY>(acc0, s0w, x, khalf, c.alpha, raw_ok && x < 30, c.amax, kP0sS0Plane);
+  p0s_store<LEAKY>(acc1, s1 + ((PAR + 3) & 3) * 2 * kP0sS1Plane, x, khalf, c.alpha,
+                   y >= 1 && y <= kP0sRows - 2 && x < 28, c.amax, kP0sS1Plane);
+
+  // stage 2 (row y - 4): rows 2i and 2i + 1 pooled (max commutes with the
+  // monotone activation; v_maximum3 propagates NaN, as the reference's max-pool)
+  if ((PAR & 1) == 1) {
+    float pv[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      const float t = __builtin_elementwise_maximum(c.pool[i], acc2[i]);
+      // column pair (x, x ^ 1): DPP quad_perm [1, 0, 3, 2]
+      const float u = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, t), 0xB1, 0xf, 0xf,
+                                                                         false));
+      pv[i] = __builtin_elementwise_maximum(t, u);
+    }
+#pragma unroll
+    for (int i = 0; i < 12; i += 2) p0s_act2<LEAKY>(pv[i], pv[i + 1], c.alpha);
+    if (y >= 5 && !(x & 1) && x < 28) {
+      float* o = orow_base + static_cast<int64_t>((y - 4) >> 1) * (kP0sWout * kP0sC) + (x >> 1) * kP0sC + 4 * khalf;
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        *reinterpret_cast<float4*>(o + 8 * q) = float4{pv[4 * q], pv[4 * q + 1], pv[4 * q + 2], pv[4 * q + 3]};
+    }
+  }
+  asm volatile("" ::: "memory");  // this iteration's LDS writes before the next one's reads (in-order LDS)
+}
+
+template <bool LEAKY>
+__global__ void __launch_bounds__(kP0sThreads) __attribute__((amdgpu_waves_per_eu(2)))
+p0s_chain_kernel(P0Args a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char p0smem[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int x = lane & 31, khalf = lane >> 5;
+  _Float16* wl = reinterpret_cast<_Float16*>(p0smem) + wave * kP0sWaveHalfs;
+  // constant slots: hi {1, 0, ..} and lo {0, ..}; s0 positions 32, 33 (never written) = 0
+  if (lane < 16) wl[kP0sOnes + lane] = static_cast<_Float16>(lane == 0 ? 1.f : 0.f);
+  for (int i = lane; i < 2 * 2 * 2 * kP0sCS; i += 64) {  // [buffer][plane][pos 32, 33][24]
+    const int b = i / (4 * kP0sCS), rest = i - b * 4 * kP0sCS, pl = rest / (2 * kP0sCS);
+    wl[b * 2 * kP0sS0Plane + pl * kP0sS0Plane + 32 * kP0sCS + rest % (2 * kP0sCS)] = static_cast<_Float16>(0.f);
+  }
+  P0sCtx<LEAKY> c;
+  c.alpha = a.alpha;
+  c.amax = 0.f;
+  {
+    const _Float16* w0 = a.w + x * 16 + 8 * khalf;
+    c.a0h = *reinterpret_cast<const h8*>(w0);
+    c.a0l = *reinterpret_cast<const h8*>(w0 + 32 * 16);
+    const _Float16* w1 = a.w + 2 * 32 * 16 + x * (16 * kP0sKS) + 8 * khalf;
+    const _Float16* w2 = w1 + 2 * 32 * 16 * kP0sKS;
+#pragma unroll
+    for (int ks = 0; ks < kP0sKS; ++ks) {
+      c.w1.h[ks] = *reinterpret_cast<const h8*>(w1 + 16 * ks);
+      c.w1.l[ks] = *reinterpret_cast<const h8*>(w1 + 32 * 16 * kP0sKS + 16 * ks);
+      c.w2.h[ks] = *reinterpret_cast<const h8*>(w2 + 16 * ks);
+      c.w2.l[ks] = *reinterpret_cast<const h8*>(w2 + 32 * 16 * kP0sKS + 16 * ks);
+    }
+  }
+  asm volatile("" ::: "memory");
+  const int64_t stride_w = static_cast<int64_t>(gridDim.x) * kP0sWaves;
+  for (int64_t img = static_cast<int64_t>(blockIdx.x) * kP0sWaves + wave; img < a.n_img; img += stride_w) {
+    const float* src = a.in + img * a.src_img_stride + x;
+    const int hmax = a.H_in - 1;
+    auto raw = [&](int row) { return src[min(row, hmax) * 32]; };
+    float* orow_base = a.out + img * (static_cast<int64_t>(kP0sHout) * kP0sWout * kP0sC);
+    // window row khalf (the first iteration shifts it down and brings row 1 + khalf); queue rows 1 .. 4 (+ khalf)
+    c.r[1][0] = raw(khalf);
+    c.r[1][1] = wave_shl1(c.r[1][0]);
+    c.r[1][2] = wave_shl1(c.r[1][1]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) c.q[i] = raw(1 + khalf + i);
+    for (int y0 = 0; y0 < kP0sRows; y0 += 4) {
+      // rows y0 + 5 .. y0 + 8 (+ khalf; the next four iterations') into the queue's second half
+#pragma unroll
+      for (int i = 0; i < 4; ++i) c.q[4 + i] = raw(y0 + 5 + khalf + i);
+      p0s_iter<0, LEAKY>(c, y0, 0, wl, orow_base, x, khalf);
+      p0s_iter<1, LEAKY>(c, y0 + 1, 1, wl, orow_base, x, khalf);
+      p0s_iter<2, LEAKY>(c, y0 + 2, 2, wl, orow_base, x, khalf);
+      p0s_iter<3, LEAKY>(c, y0 + 3, 3, wl, orow_base, x, khalf);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) c.q[i] = c.q[i + 4];
+    }
+  }
+  raise_range(a.range_flag, c.amax);
+}
+
+// ------------------------------------------------------------------ p1s ----
+// Streaming form of the p1 chain (SE20 chain 1 on the 66 x 14 x 24 chain-0
+// output: 1x3 24 -> 32, 3x1, 1x3, 3x1 32 -> 32, max-pool 2x2 -> 31 x 5 x 32),
+// rows streamed top to bottom through a TWO-WAVE STAGE PIPELINE per clip:
+// wave 0 runs stages a and b, wave 1 stages c and d, so each wave keeps only
+// its two stages' weights in VGPRs (96) and a CU runs two waves per SIMD.
+// v_mfma_f32_16x16x32_f16 with a tile of one row (16 positions; 12 / 12 /
+// 10 / 10 valid: a 32-position tile would be under half full) and two
+// 16-channel output blocks. Iteration y (one workgroup barrier after it):
+//   wave 0: stage input row y + 1; a(y) -> A[y & 3]; b(y - 3) -> B[(y - 3) & 1]
+//   wave 1: c(y - 4) from B[(y - 4) & 1] -> C[(y - 4) & 3]; d(y - 7), pooled
+// Every row a wave reads was written before the previous barrier or earlier
+// by itself (a wave's LDS instructions execute in order). Stage a's bias
+// rides in its K padding (slot 72, B = 1); b, c and d start their
+// accumulators at the bias. K groups of 8 (g = 4 ks + kq, kq = lane / 16):
+//   a: g = tap * 3 + c   -> input position x + tap, channels 8 c   (24 x + 8 g)
+//   b: g = dy * 4 + c    -> A row (r + dy), position x, channels 8 c
+//   c: g = dx * 4 + c    -> B position x + dx, channels 8 c
+//   d: g = dy * 4 + c    -> C row (r + dy), position x, channels 8 c
+constexpr int kP1sThreads = 128;
+constexpr int kP1sCSI = 24, kP1sCS = 40;          // fp16 per position: input (24 ch), stage outputs (32 ch)
+constexpr int kP1sInPlane = 18 * kP1sCSI;         // 18 positions (14 valid; x + tap <= 17)
+constexpr int kP1sInSlot = 2 * kP1sInPlane + 32;  // hi, lo, then ones (hi 8, lo 8) and zeros (hi 8, lo 8)
+constexpr int kP1sPlane = 16 * kP1sCS;            // A / C rows
+constexpr int kP1sBPlane = 18 * kP1sCS;           // B rows (c reads x + dx <= 17)
+constexpr int kP1sIn = 0, kP1sA = kP1sIn + 2 * kP1sInSlot, kP1sB = kP1sA + 4 * 2 * kP1sPlane,
+              kP1sCr = kP1sB + 2 * 2 * kP1sBPlane;
+constexpr int kP1sHalfs = kP1sCr + 4 * 2 * kP1sPlane;
+constexpr int kP1sLds = kP1sHalfs * 2;
+constexpr int kP1sHin = 66, kP1sHout = 31, kP1sWi = 14, kP1sWo = 5, kP1sCo = 32;
+constexpr int kP1sStageHalfs = 2 * 32 * 96;       // weights per stage: hi [32][96], lo [32][96]
+
+struct P1sW {
+  h8 h[2][3], l[2][3];  // [output block][K step]
+};
+
+struct P1sCtx {
+  P1sW w[2];           // this wave's two stages
+  f4 bias[2][2];       // wave 0: [b][mb] in bias[1]; wave 1: c, d
+  float4 q[4][2];      // wave 0: input rows y + 1 .. y + 4 (two float4 per lane)
+  f4 pool[2];          // wave 1: stage-d row 2i awaiting its partner
+  float amax, alpha;
+};
+
+// one stage of one row: 2 output blocks x 3 K steps x 3 products
+__device__ __forceinline__ void p1s_mma(f4 (&acc)[2], const P1sW& w, const h8 (&bh)[3], const h8 (&bl)[3]) {
+#pragma unroll
+  for (int ks = 0; ks < 3; ++ks)
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+      acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w.h[mb][ks], bh[ks], acc[mb], 0, 0, 0);
+      acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w.h[mb][ks], bl[ks], acc[mb], 0, 0, 0);
+      acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w.l[mb][ks], bh[ks], acc[mb], 0, 0, 0);
+    }
+}
+
+// activation, split and LDS store of a finished stage row (channels 16 mb + 4 kq + j at position x)
+template <bool LEAKY>
+__device__ __forceinline__ void p1s_store(const f4 (&acc)[2], _Float16* oh, int plane, int x, int kq, float alpha,
+                                          bool track_it, float& amax) {
+  float m = 0.f;
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb) {
+    float v[4] = {acc[mb][0], acc[mb][1], acc[mb][2], acc[mb][3]};
+    p0s_act2<LEAKY>(v[0], v[1], alpha);
+    p0s_act2<LEAKY>(v[2], v[3], alpha);
+    uint32_t h01, l01, h23, l23;
+    split2_mix(v[0], v[1], h01, l01, m);
+    split2_mix(v[2], v[3], h23, l23, m);
+    const int o = x * kP1sCS + 16 * mb + 4 * kq;
+    *reinterpret_cast<uint2*>(oh + o) = uint2{h01, h23};
+    *reinterpret_cast<uint2*>(oh + plane + o) = uint2{l01, l23};
+  }
+  asm("v_max_f32 %0, %0, %1" : "+v"(amax) : "v"(track_it ? m : 0.f));
+}
+
+// the input row in registers (two float4 per lane: entries lane, lane + 64 of 84) -> hi / lo planes
+__device__ __forceinline__ void p1s_stage_row(const float4 (&v)[2], _Float16* in_w, int lane, float& amx) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = lane + 64 * u;
+    if (u == 0 || lane < kP1sWi * 6 - 64) {
+      uint32_t h01, l01, h23, l23;
+      split2_mix(v[u].x, v[u].y, h01, l01, amx);
+      split2_mix(v[u].z, v[u].w, h23, l23, amx);
+      const int o = (i / 6) * kP1sCSI + (i % 6) * 4;
+      *reinterpret_cast<uint2*>(in_w + o) = uint2{h01, h23};
+      *reinterpret_cast<uint2*>(in_w + kP1sInPlane + o) = uint2{l01, l23};
+    }
+  }
+}
+
+// wave 0, iteration y: stage input row y + 1, a(y), b(y - 3)
+template <int PAR, bool LEAKY>
+__device__ __forceinline__ void p1s_iter0(P1sCtx& c, int y, _Float16* sm, const float* src, int hmax, int x, int kq,
+                                          int lane, int a2h, int a2l) {
+  const _Float16* in_r = sm + kP1sIn + (PAR & 1) * kP1sInSlot;
+  _Float16* A = sm + kP1sA;
+  h8 bh[2][3], bl[2][3];
+#pragma unroll
+  for (int ks = 0; ks < 3; ++ks) {
+    const int oa = ks < 2 ? x * kP1sCSI + 32 * ks + 8 * kq : a2h;  // 24 x + 8 g; ks 2: the lane's slot
+    const int la = ks < 2 ? kP1sInPlane : a2l;
+    bh[0][ks] = *reinterpret_cast<const h8*>(in_r + oa);
+    bl[0][ks] = *reinterpret_cast<const h8*>(in_r + oa + la);
+    const _Float16* pb = A + ((PAR + 1 + ks) & 3) * 2 * kP1sPlane + x * kP1sCS + 8 * kq;  // row y - 3 + ks
+    bh[1][ks] = *reinterpret_cast<const h8*>(pb);
+    bl[1][ks] = *reinterpret_cast<const h8*>(pb + kP1sPlane);
+  }
+  {  // input row y + 1 (loaded four iterations ago) -> the other input slot; load row y + 5
+    const int slot = (PAR + 1) & 3;
+    float amx = 0.f;
+    p1s_stage_row(c.q[slot], sm + kP1sIn + ((PAR + 1) & 1) * kP1sInSlot, lane, amx);
+    asm("v_max_f32 %0, %0, %1" : "+v"(c.amax) : "v"(y + 1 < kP1sHin ? amx : 0.f));
+    const float* r = src + static_cast<int64_t>(min(y + 5, hmax)) * (kP1sWi * kP1sCSI);
+    c.q[slot][0] = *reinterpret_cast<const float4*>(r + 4 * lane);
+    c.q[slot][1] = *reinterpret_cast<const float4*>(r + 4 * min(lane + 64, kP1sWi * 6 - 1));
+  }
+  const f4 zero = {};
+  f4 acca[2] = {zero, zero}, accb[2] = {c.bias[1][0], c.bias[1][1]};
+  p1s_mma(acca, c.w[0], bh[0], bl[0]);
+  p1s_mma(accb, c.w[1], bh[1], bl[1]);
+  p1s_store<LEAKY>(acca, A + (PAR & 3) * 2 * kP1sPlane, kP1sPlane, x, kq, c.alpha, y < kP1sHin && x < 12, c.amax);
+  p1s_store<LEAKY>(accb, sm + kP1sB + ((PAR + 1) & 1) * 2 * kP1sBPlane, kP1sBPlane, x, kq, c.alpha,
+                   y >= 3 && y - 3 < kP1sHin - 2 && x < 12, c.amax);
+}
+
+// wave 1, iteration y: c(y - 4), d(y - 7) pooled with row y - 8 when y - 7 is odd
+template <int PAR, bool LEAKY>
+__device__ __forceinline__ void p1s_iter1(P1sCtx& c, int y, _Float16* sm, float* obase, int x, int kq) {
+  const _Float16* B = sm + kP1sB + (PAR & 1) * 2 * kP1sBPlane;  // row y - 4
+  _Float16* C = sm + kP1sCr;
+  h8 bh[2][3], bl[2][3];
+#pragma unroll
+  for (int ks = 0; ks < 3; ++ks) {
+    const _Float16* pc = B + (x + ks) * kP1sCS + 8 * kq;
+    bh[0][ks] = *reinterpret_cast<const h8*>(pc);
+    bl[0][ks] = *reinterpret_cast<const h8*>(pc + kP1sBPlane);
+    const _Float16* pd = C + ((PAR + 1 + ks) & 3) * 2 * kP1sPlane + x * kP1sCS + 8 * kq;  // row y - 7 + ks
+    bh[1][ks] = *reinterpret_cast<const h8*>(pd);
+    bl[1][ks] = *reinterpret_cast<const h8*>(pd + kP1sPlane);
+  }
+  f4 accc[2] = {c.bias[0][0], c.bias[0][1]};
+  f4 accd_odd[2] = {c.bias[1][0], c.bias[1][1]};
+  f4(&accd)[2] = ((PAR & 1) == 1) ? c.pool : accd_odd;  // row y - 7 even (y odd): accumulate into the pool
+  if ((PAR & 1) == 1) {
+    c.pool[0] = c.bias[1][0];
+    c.pool[1] = c.bias[1][1];
+  }
+  p1s_mma(accc, c.w[0], bh[0], bl[0]);
+  p1s_mma(accd, c.w[1], bh[1], bl[1]);
+  p1s_store<LEAKY>(accc, C + (PAR & 3) * 2 * kP1sPlane, kP1sPlane, x, kq, c.alpha,
+                   y >= 4 && y - 4 < kP1sHin - 2 && x < 10, c.amax);
+  if ((PAR & 1) == 0) {  // row y - 7 odd: pool with row y - 8, store pooled row (y - 8) / 2
+    float pv[2][4];
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float t = __builtin_elementwise_maximum(c.pool[mb][j], accd[mb][j]);
+        const float u = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, t), 0xB1, 0xf, 0xf,
+                                                                           false));
+        pv[mb][j] = __builtin_elementwise_maximum(t, u);
+      }
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+      p0s_act2<LEAKY>(pv[mb][0], pv[mb][1], c.alpha);
+      p0s_act2<LEAKY>(pv[mb][2], pv[mb][3], c.alpha);
+    }
+    if (y >= 8 && y - 8 < 2 * kP1sHout && !(x & 1) && x < 2 * kP1sWo) {
+      float* o = obase + static_cast<int64_t>((y - 8) >> 1) * (kP1sWo * kP1sCo) + (x >> 1) * kP1sCo + 4 * kq;
+#pragma unroll
+      for (int mb = 0; mb < 2; ++mb)
+        *reinterpret_cast<float4*>(o + 16 * mb) = float4{pv[mb][0], pv[mb][1], pv[mb][2], pv[mb][3]};
+    }
+  }
+}
+
+template <bool LEAKY>
+__global__ void __launch_bounds__(kP1sThreads) __attribute__((amdgpu_waves_per_eu(2)))
+p1s_chain_kernel(P1Args a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char p1smem[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int x = lane & 15, kq = lane >> 4;
+  _Float16* sm = reinterpret_cast<_Float16*>(p1smem);
+  // never-written positions: input 14 .. 17 (both slots, planes), B 16, 17; the ones / zeros slots
+  for (int i = threadIdx.x; i < 2 * 2 * 4 * kP1sCSI; i += kP1sThreads) {
+    const int s = i / (8 * kP1sCSI), rest = i - s * 8 * kP1sCSI, pl = rest / (4 * kP1sCSI);
+    sm[kP1sIn + s * kP1sInSlot + pl * kP1sInPlane + 14 * kP1sCSI + rest % (4 * kP1sCSI)] = static_cast<_Float16>(0.f);
+  }
+  for (int i = threadIdx.x; i < 2 * 2 * 2 * kP1sCS; i += kP1sThreads) {
+    const int s = i / (4 * kP1sCS), rest = i - s * 4 * kP1sCS, pl = rest / (2 * kP1sCS);
+    sm[kP1sB + s * 2 * kP1sBPlane + pl * kP1sBPlane + 16 * kP1sCS + rest % (2 * kP1sCS)] = static_cast<_Float16>(0.f);
+  }
+  if (threadIdx.x < 64) {
+    const int s = lane >> 5, k = lane & 31;
+    sm[kP1sIn + s * kP1sInSlot + 2 * kP1sInPlane + k] = static_cast<_Float16>(k == 0 ? 1.f : 0.f);
+  }
+  // stage a's K step 2: lanes kq 0 read group 8 (tap 2, c 2), kq 1 the ones slot (bias), kq 2, 3 zeros
+  const int a2h = kq == 0 ? x * kP1sCSI + 64 : 2 * kP1sInPlane + (kq == 1 ? 0 : 16);
+  const int a2l = kq == 0 ? kP1sInPlane : 8;
+  P1sCtx c;
+  c.alpha = a.alpha;
+  c.amax = 0.f;
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) {
+        const _Float16* wp = a.w + (2 * wave + s) * kP1sStageHalfs + (16 * mb + x) * 96 + 32 * ks + 8 * kq;
+        c.w[s].h[mb][ks] = *reinterpret_cast<const h8*>(wp);
+        c.w[s].l[mb][ks] = *reinterpret_cast<const h8*>(wp + 32 * 96);
+      }
+  // biases of stages b, c, d ([3][32]): wave 0 keeps b's in bias[1], wave 1 c's and d's
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+      const int st = wave == 0 ? 0 : s + 1;
+      const float4 b = *reinterpret_cast<const float4*>(a.bias + 32 * st + 16 * mb + 4 * kq);
+      c.bias[wave == 0 ? 1 : s][mb] = f4{b.x, b.y, b.z, b.w};
+    }
+  __syncthreads();
+  const int hmax = a.H_in - 1;
+  for (int64_t img = blockIdx.x; img < a.n_img; img += gridDim.x) {
+    const float* src = a.in + img * a.src_img_stride;
+    float* obase = a.out + img * (static_cast<int64_t>(kP1sHout) * kP1sWo * kP1sCo);
+    if (wave == 0) {  // input row 0 straight into slot 0; rows 1 .. 4 into the queue (slot = row & 3)
+      float4 v[2];
+      v[0] = *reinterpret_cast<const float4*>(src + 4 * lane);
+      v[1] = *reinterpret_cast<const float4*>(src + 4 * min(lane + 64, kP1sWi * 6 - 1));
+      float amx = 0.f;
+      p1s_stage_row(v, sm + kP1sIn, lane, amx);
+      asm("v_max_f32 %0, %0, %1" : "+v"(c.amax) : "v"(amx));
+#pragma unroll
+      for (int r = 1; r <= 4; ++r) {
+        const float* rp = src + static_cast<int64_t>(min(r, hmax)) * (kP1sWi * kP1sCSI);
+        c.q[r & 3][0] = *reinterpret_cast<const float4*>(rp + 4 * lane);
+        c.q[r & 3][1] = *reinterpret_cast<const float4*>(rp + 4 * min(lane + 64, kP1sWi * 6 - 1));
+      }
+    }
+    __syncthreads();
+    for (int y0 = 0; y0 < 72; y0 += 4) {
+#define HBK_P1S_STEP(P)                                                              \
+  if (wave == 0)                                                                     \
+    p1s_iter0<P, LEAKY>(c, y0 + P, sm, src, hmax, x, kq, lane, a2h, a2l);            \
+  else                                                                               \
+    p1s_iter1<P, LEAKY>(c, y0 + P, sm, obase, x, kq);                                \
+  __syncthreads();
+      HBK_P1S_STEP(0)
+      HBK_P1S_STEP(1)
+      HBK_P1S_STEP(2)
+      HBK_P1S_STEP(3)
+#undef HBK_P1S_STEP
+    }
+  }
+  raise_range(a.range_flag, c.amax);
+}
+
 // ------------------------------------------------------------------ host ----
 
 struct OpInfo {
@@ -1450,6 +1954,8 @@ struct ChainPlan {
   // plan above stays as the fallback for unaligned buffers
   void (*p0fn)(P0Args) = nullptr;
   P0Args p0{};
+  bool p0s = false;  // p0fn is the streaming p0s_chain_kernel (one wave per image)
+  bool p1s = false;  // p1fn is the streaming p1s_chain_kernel (one wave per image)
   void (*p1fn)(P1Args) = nullptr;  // p1 pattern (shares d_p0 / p0_lds / p0_blocks_per_cu)
   P1Args p1{};
   size_t p0_lds = 0;
@@ -1877,10 +2383,94 @@ bool plan_p0_band(const std::vector<OpInfo>& ops, const std::vector<int>& st, co
   return true;
 }
 
+// The streaming p0 form (p0s_chain_kernel): the same chain on a 136-row input,
+// one wave per clip. Weights as plan_p0_band's (hi / lo of 16 W rounded toward
+// zero), with each stage's bias in K slot 12 (stage 0) or 72 (stages 1, 2).
+bool plan_p0s(const std::vector<OpInfo>& ops, const std::vector<int>& st, const ChainArgs& a, Dims d, Dims od,
+              ChainPlan& cp) {
+  if (getenv("HBK_EMBED_NO_P0S")) return false;
+  if (st.size() != 3 || a.ipc != 1 || a.C_src != 1 || a.in_ph != 1 || a.in_pw != 1) return false;
+  if (a.out_ph != 2 || a.out_pw != 2 || d.w != kP0W || a.src_row_stride != kP0W || d.h != kP0sRows) return false;
+  const OpInfo &o0 = ops[st[0]], &o1 = ops[st[1]], &o2 = ops[st[2]];
+  const int C = kP0C;
+  if (!(o0.kh == 3 && o0.kw == 3 && o0.cin == 1 && o0.cout == C)) return false;
+  if (!(o1.kh == 1 && o1.kw == 3 && o1.cin == C && o1.cout == C)) return false;
+  if (!(o2.kh == 3 && o2.kw == 1 && o2.cin == C && o2.cout == C)) return false;
+  const bool leaky = o0.act != 0;
+  for (const OpInfo* o : {&o0, &o1, &o2}) {
+    if ((o->act != 0) != leaky) return false;
+    if (leaky && (o->alpha != o0.alpha || !(o->alpha >= 0.f && o->alpha <= 1.f))) return false;
+  }
+  if (od.h != kP0sHout || od.w != kP0sWout || od.c != C) return false;
+  const int woff1 = 2 * 32 * 16, woff2 = woff1 + 2 * 32 * 16 * kP0sKS, total = woff2 + 2 * 32 * 16 * kP0sKS;
+  std::vector<_Float16> w(total, static_cast<_Float16>(0.f));
+  auto put = [&](int off, int ks, int n, int k, float v) {
+    uint32_t bits;
+    memcpy(&bits, &v, 4);
+    bits &= 0xFFFFE000u;
+    float hv;
+    memcpy(&hv, &bits, 4);
+    w[off + n * 16 * ks + k] = static_cast<_Float16>(hv);
+    w[off + 32 * 16 * ks + n * 16 * ks + k] = static_cast<_Float16>(v - hv);
+  };
+  for (int n = 0; n < C; ++n) {
+    // K slots (p0s_iter): lower half 0-5 = window (y, y + 1) x (dx 0-2), upper half 8-13 = window
+    // (y + 1, y + 2); taps 0-4 in the lower half, 5-8 in the upper, the bias in slot 6 (B = 1)
+    for (int k = 0; k < 16; ++k) {
+      const int tap = k < 5 ? k : (k >= 10 && k < 14 ? k - 5 : -1);
+      if (tap >= 0) put(0, 1, n, k, o0.w[size_t(tap) * C + n]);
+    }
+    put(0, 1, n, 6, o0.b[n]);
+    for (int k = 0; k < 3 * C; ++k) put(woff1, kP0sKS, n, k, o1.w[size_t(k) * C + n]);  // HWIO: (tap C + ci) C + n
+    put(woff1, kP0sKS, n, 3 * C, o1.b[n]);
+    // stage 2: K step ks, lane half h holds group (dy, c) = G2[ks][h] (p0s_iter), channels 8 c .. 8 c + 7
+    static const int G2[5][2][2] = {{{0, 0}, {0, 1}}, {{1, 0}, {1, 1}}, {{2, 0}, {2, 1}}, {{0, 2}, {1, 2}},
+                                    {{2, 2}, {-1, -1}}};
+    for (int ks = 0; ks < kP0sKS; ++ks)
+      for (int h = 0; h < 2; ++h)
+        for (int i = 0; i < 8; ++i) {
+          const int k = 16 * ks + 8 * h + i, dy = G2[ks][h][0], cg = G2[ks][h][1];
+          put(woff2, kP0sKS, n, k, dy < 0 ? (i == 0 ? o2.b[n] : 0.f) : o2.w[size_t(dy * C + 8 * cg + i) * C + n]);
+        }
+  }
+  hipError_t e = hipMalloc(&cp.d_p0, w.size() * 2);
+  if (e == hipSuccess) e = hipMemcpy(cp.d_p0, w.data(), w.size() * 2, hipMemcpyHostToDevice);
+  cp.p0fn = leaky ? p0s_chain_kernel<true> : p0s_chain_kernel<false>;
+  cp.p0_lds = kP0sLds;
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(cp.p0fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            int(cp.p0_lds));
+  int per_cu = 0;
+  if (e == hipSuccess)
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(cp.p0fn), kP0sThreads,
+                                                     cp.p0_lds);
+  if (e != hipSuccess || per_cu < 1) {
+    (void)hipGetLastError();
+    if (cp.d_p0) (void)hipFree(cp.d_p0);
+    cp.d_p0 = nullptr;
+    cp.p0fn = nullptr;
+    return false;
+  }
+  cp.p0s = true;
+  cp.p0_blocks_per_cu = per_cu;
+  P0Args& p = cp.p0;
+  p.w = static_cast<const _Float16*>(cp.d_p0);
+  p.bias = nullptr;
+  p.H_in = d.h;
+  p.H_out = od.h;
+  p.n_bands = 1;
+  p.alpha = leaky ? o0.alpha : 0.f;
+  if (getenv("HBK_DEBUG_EMBED"))
+    fprintf(stderr, "hbk p0s chain: %dx%dx1 -> %dx%dx%d, one wave per clip, LDS %zu B, %d blocks/CU\n", d.h, d.w,
+            od.h, od.w, od.c, cp.p0_lds, per_cu);
+  return true;
+}
+
 // pooled rows per task: 6 (78 KB of LDS, two blocks per CU); HBK_P0_BAND=5|7 for tuning
 bool plan_p0(const std::vector<OpInfo>& ops, const std::vector<int>& st, const ChainArgs& a, Dims d, Dims od,
              ChainPlan& cp) {
   if (getenv("HBK_EMBED_NO_P0")) return false;
+  if (plan_p0s(ops, st, a, d, od, cp)) return true;
   const char* bs = getenv("HBK_P0_BAND");
   const int band = bs ? atoi(bs) : 6;
   if (band == 5) return plan_p0_band<5>(ops, st, a, d, od, cp);
@@ -1893,9 +2483,86 @@ bool plan_p0(const std::vector<OpInfo>& ops, const std::vector<int>& st, const C
 constexpr int kP1W = 14, kP1CI = 24, kP1Band = 8;
 using P1G = P1Geo<kP1W, kP1CI, kP1Band>;
 
+// The streaming p1 form (p1s_chain_kernel) for a 66-row input: weights per
+// stage s as hi / lo [32][96] (K = tap * cin + ci; stage a's bias at K 72),
+// biases of stages b, c, d as [3][32] f32.
+bool plan_p1s(const std::vector<OpInfo>& ops, const std::vector<int>& st, const ChainArgs& a, Dims d, Dims od,
+              ChainPlan& cp) {
+  if (getenv("HBK_EMBED_NO_P1S")) return false;
+  if (st.size() != 4 || a.ipc != 1 || a.in_ph != 1 || a.in_pw != 1 || a.out_ph != 2 || a.out_pw != 2) return false;
+  if (d.h != kP1sHin || d.w != kP1sWi || d.c != kP1sCSI || a.C_src != kP1sCSI || a.src_row_stride != kP1sWi * kP1sCSI)
+    return false;
+  const int kh[4] = {1, 3, 1, 3}, kw[4] = {3, 1, 3, 1};
+  const bool leaky = ops[st[0]].act != 0;
+  for (int i = 0; i < 4; ++i) {
+    const OpInfo& o = ops[st[i]];
+    if (o.kh != kh[i] || o.kw != kw[i] || o.cin != (i ? kP1sCo : kP1sCSI) || o.cout != kP1sCo) return false;
+    if ((o.act != 0) != leaky) return false;
+    if (leaky && (o.alpha != ops[st[0]].alpha || !(o.alpha >= 0.f && o.alpha <= 1.f))) return false;
+  }
+  if (od.h != kP1sHout || od.w != kP1sWo || od.c != kP1sCo) return false;
+  std::vector<_Float16> w(4 * kP1sStageHalfs, static_cast<_Float16>(0.f));
+  auto put = [&](int s, int n, int k, float v) {
+    uint32_t bits;
+    memcpy(&bits, &v, 4);
+    bits &= 0xFFFFE000u;
+    float hv;
+    memcpy(&hv, &bits, 4);
+    w[s * kP1sStageHalfs + n * 96 + k] = static_cast<_Float16>(hv);
+    w[s * kP1sStageHalfs + 32 * 96 + n * 96 + k] = static_cast<_Float16>(v - hv);
+  };
+  for (int s = 0; s < 4; ++s) {
+    const OpInfo& o = ops[st[s]];
+    const int K = 3 * o.cin;
+    for (int n = 0; n < kP1sCo; ++n) {
+      for (int k = 0; k < K; ++k) put(s, n, k, o.w[size_t(k) * kP1sCo + n]);  // HWIO: (tap cin + ci) cout + n
+      if (s == 0) put(0, n, K, o.b[n]);
+    }
+  }
+  std::vector<float> b(3 * 32, 0.f);
+  for (int s = 1; s < 4; ++s)
+    for (int n = 0; n < kP1sCo; ++n) b[32 * (s - 1) + n] = ops[st[s]].b[n];
+  const size_t wbytes = (w.size() * 2 + 15) & ~size_t(15);
+  hipError_t e = hipMalloc(&cp.d_p0, wbytes + b.size() * 4);
+  if (e == hipSuccess) e = hipMemcpy(cp.d_p0, w.data(), w.size() * 2, hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = hipMemcpy(static_cast<unsigned char*>(cp.d_p0) + wbytes, b.data(), b.size() * 4, hipMemcpyHostToDevice);
+  cp.p1fn = leaky ? p1s_chain_kernel<true> : p1s_chain_kernel<false>;
+  cp.p0_lds = kP1sLds;
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(cp.p1fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            int(cp.p0_lds));
+  int per_cu = 0;
+  if (e == hipSuccess)
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(cp.p1fn), kP1sThreads,
+                                                     cp.p0_lds);
+  if (e != hipSuccess || per_cu < 1) {
+    (void)hipGetLastError();
+    if (cp.d_p0) (void)hipFree(cp.d_p0);
+    cp.d_p0 = nullptr;
+    cp.p1fn = nullptr;
+    return false;
+  }
+  cp.p1s = true;
+  cp.p0_blocks_per_cu = per_cu;
+  P1Args& p = cp.p1;
+  p.w = static_cast<const _Float16*>(cp.d_p0);
+  p.bias = reinterpret_cast<const float*>(static_cast<unsigned char*>(cp.d_p0) + wbytes);
+  p.H_in = d.h;
+  p.H_out = od.h;
+  p.n_bands = 1;
+  p.alpha = leaky ? ops[st[0]].alpha : 0.f;
+  if (getenv("HBK_DEBUG_EMBED"))
+    fprintf(stderr, "hbk p1s chain: %dx%dx%d -> %dx%dx%d, two-wave stage pipeline per clip, LDS %zu B, %d blocks/CU\n",
+            d.h, d.w,
+            d.c, od.h, od.w, od.c, cp.p0_lds, per_cu);
+  return true;
+}
+
 bool plan_p1(const std::vector<OpInfo>& ops, const std::vector<int>& st, const ChainArgs& a, Dims d, Dims od,
              ChainPlan& cp) {
   if (getenv("HBK_EMBED_NO_P1")) return false;
+  if (plan_p1s(ops, st, a, d, od, cp)) return true;
   if (st.size() != 4 || a.ipc != 1 || a.in_ph != 1 || a.in_pw != 1 || a.out_ph != 2 || a.out_pw != 2) return false;
   if (d.w != kP1W || d.c != kP1CI || a.C_src != kP1CI || a.src_row_stride != kP1W * kP1CI) return false;
   const int C = kP1C;
@@ -2195,7 +2862,7 @@ int run_program(const Program& prog, const float* in, int64_t n_units, int64_t i
         const bool aligned = !(reinterpret_cast<uintptr_t>(pa.in) & 15) && !(pa.src_img_stride & 3) &&
                              !(reinterpret_cast<uintptr_t>(pa.out) & 15);
         if (aligned && pa.n_img * pa.n_bands < (int64_t(1) << 31)) {
-          const int64_t tasks = pa.n_img * pa.n_bands;
+          const int64_t tasks = c.p0s ? (pa.n_img + kP0sWaves - 1) / kP0sWaves : pa.n_img * pa.n_bands;
           const int64_t blocks = std::min<int64_t>(tasks, persistent_blocks(c.p0_blocks_per_cu, stream));
           if (blocks <= 0) continue;
           hipLaunchKernelGGL(c.p0fn, dim3(unsigned(blocks)), dim3(kP0Threads), c.p0_lds, stream, pa);
@@ -2213,10 +2880,10 @@ int run_program(const Program& prog, const float* in, int64_t n_units, int64_t i
         const bool aligned = !(reinterpret_cast<uintptr_t>(pa.in) & 15) && !(pa.src_img_stride & 3) &&
                              !(reinterpret_cast<uintptr_t>(pa.out) & 15);
         if (aligned && pa.n_img * pa.n_bands < (int64_t(1) << 31)) {
-          const int64_t tasks = pa.n_img * pa.n_bands;
+          const int64_t tasks = c.p1s ? pa.n_img : pa.n_img * pa.n_bands;
           const int64_t blocks = std::min<int64_t>(tasks, persistent_blocks(c.p0_blocks_per_cu, stream));
           if (blocks <= 0) continue;
-          hipLaunchKernelGGL(c.p1fn, dim3(unsigned(blocks)), dim3(kP0Threads), c.p0_lds, stream, pa);
+          hipLaunchKernelGGL(c.p1fn, dim3(unsigned(blocks)), dim3(c.p1s ? kP1sThreads : kP0Threads), c.p0_lds, stream, pa);
           HBK_LAUNCH_CHECK("p1_chain_kernel");
           continue;
         }

@@ -119,30 +119,38 @@ def test_embed_clips_ragged_batches(precision):
 
 @pytest.mark.gpu
 def test_embed_pattern_kernels_match_generic_path(monkeypatch, capfd):
-    """The plan picks the p0 / p1 pattern kernels for SE20's chains 0 and 1;
-    with them disabled the generic split-f16 kernel runs every chain. Both
-    paths match the oracle and each other."""
+    """The plan picks the streaming p0s kernel (one wave per clip) for SE20's
+    chain 0 and the p1 pattern kernel for chain 1; HBK_EMBED_NO_P0S=1 falls
+    back to the banded p0 kernel, and with every pattern disabled the generic
+    split-f16 kernel runs every chain. All three paths match the oracle and
+    each other."""
     from heybuddy.embedding_graph import se20_graph
     from heybuddy.kernels import EmbedPlan
     g = se20_graph()
-    mel = _mel_clips(4, seed=21)
+    mel = _mel_clips(9, seed=21)  # 9 clips: waves with 3 and 2 clips, idle waves in the last block
     ref = _oracle_clip_embeddings(g, mel)
     monkeypatch.setenv("HBK_DEBUG_EMBED", "1")
     capfd.readouterr()
-    plan = EmbedPlan(g, precision="split")
-    err = capfd.readouterr().err
-    assert "hbk p0 chain" in err and "hbk p1 chain" in err, err
-    out_p = plan.clips(torch.from_numpy(mel).cuda()).cpu().numpy()
-    monkeypatch.setenv("HBK_EMBED_NO_P0", "1")
-    monkeypatch.setenv("HBK_EMBED_NO_P1", "1")
-    plan_g = EmbedPlan(g, precision="split")
-    err = capfd.readouterr().err
-    assert "hbk p0 chain" not in err and "hbk p1 chain" not in err, err
-    out_g = plan_g.clips(torch.from_numpy(mel).cuda()).cpu().numpy()
-    for out in (out_p, out_g):
+    outs = {}
+    for name, env, want in (("p0s", {}, ("hbk p0s chain", "hbk p1 chain")),
+                            ("p0", {"HBK_EMBED_NO_P0S": "1"}, ("hbk p0 chain", "hbk p1 chain")),
+                            ("generic", {"HBK_EMBED_NO_P0": "1", "HBK_EMBED_NO_P1": "1"}, ())):
+        for k in ("HBK_EMBED_NO_P0S", "HBK_EMBED_NO_P0", "HBK_EMBED_NO_P1"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        plan = EmbedPlan(g, precision="split")
+        err = capfd.readouterr().err
+        for w in want:
+            assert w + ":" in err, (name, err)
+        if not want:
+            assert "hbk p0" not in err and "hbk p1 chain" not in err, err
+        outs[name] = plan.clips(torch.from_numpy(mel).cuda()).cpu().numpy()
+    for name, out in outs.items():
         ok, worst = _close(out, ref)
-        assert ok, f"max |diff| {worst}"
-    assert np.abs(out_p - out_g).max() <= 1e-5 * (1.0 + np.abs(ref).max())
+        assert ok, f"{name}: max |diff| {worst}"
+    for name in ("p0", "generic"):
+        assert np.abs(outs["p0s"] - outs[name]).max() <= 1e-5 * (1.0 + np.abs(ref).max()), name
 
 
 def _generic_graph(seed=9):
