@@ -97,6 +97,11 @@ def parse():
     return args
 
 
+# the split-f16 embedding path's kernels (SE20): streaming chain 0, two-wave chain 1,
+# the generic kernel on chain 2 and on the phase-deduplicated tail, the window gather
+EMBED_KERNELS = ("p0s_chain_kernel + p1s_chain_kernel + conv_chain_x3_kernel x2 (chain 2; tail on 2 phase images "
+                 "per clip) + embed_gather_kernel")
+EMBED_KERNEL_SUBSTR = ("conv_chain", "p0_chain", "p1_chain", "p0s_chain", "p1s_chain", "embed_gather")
 TRAFFIC_SOURCE = [None]
 CURRENT_CONFIG = [None]
 
@@ -309,11 +314,11 @@ def setup_featurize(args, dev, rank, world, seed):
                         algorithmic_bytes_per_clip=MEL_READ_SAMPLES * 4 + N_FRAMES * 32 * 4)
         if name == "embed":
             split = eplan.precision == "split"
-            kname = "p0_chain_kernel + p1_chain_kernel + conv_chain_x3_kernel x2" if split else "conv_chain_kernel"
+            kname = (EMBED_KERNELS if split else "conv_chain_kernel")
             return roof("%s (hbk_embed_clips, %s: %d chained launches per %d-clip chunk)"
                         % (kname, eplan.precision, eplan.n_chains, min(n, 16384)), "mfma",
                         2.0 * eplan.macs_per_clip * n, ms, "TFLOP/s",
-                        load_traffic(pmc, ("conv_chain", "p0_chain", "p1_chain")),
+                        load_traffic(pmc, EMBED_KERNEL_SUBSTR),
                         peak=SPLIT_PEAK_TFLOPS if split else FP32_MFMA_PEAK_TFLOPS,
                         peak_basis=("f16 dense MFMA peak / 3 (hi*hi + hi*lo + lo*hi per f32-accurate MAC)"
                                     if split else "f32-input MFMA dense peak"),
@@ -769,9 +774,9 @@ def setup_e2e(args, dev, rank, world, seed):
                         algorithmic_bytes_per_clip=MEL_READ_SAMPLES * 4 + N_FRAMES * 32 * 4)
         if name == "embed":
             split = eplan.precision == "split"
-            return roof("p0_chain_kernel + p1_chain_kernel + conv_chain_x3_kernel x2 (hbk_embed_clips)", "mfma",
+            return roof("%s (hbk_embed_clips)" % EMBED_KERNELS, "mfma",
                         2.0 * eplan.macs_per_clip * n, ms, "TFLOP/s",
-                        load_traffic(pmc, ("conv_chain", "p0_chain", "p1_chain")),
+                        load_traffic(pmc, EMBED_KERNEL_SUBSTR),
                         peak=SPLIT_PEAK_TFLOPS if split else FP32_MFMA_PEAK_TFLOPS,
                         peak_basis="f16 dense MFMA peak / 3 (hi*hi + hi*lo + lo*hi per f32-accurate MAC)",
                         algorithmic_flops_per_clip=2.0 * eplan.macs_per_clip)

@@ -1966,6 +1966,11 @@ struct ChainPlan {
 struct Program {
   std::vector<ChainPlan> chains;
   int64_t buf_floats[2] = {0, 0};  // per unit (clip or window)
+  // phase-deduplicated tail: the last chain writes [n_src rows][out_dim] per clip
+  // into workspace buffer gather_buf; output row i is source row gather_src[i]
+  int gather_buf = -1, n_src = 0;
+  std::vector<int> gather_src;
+  int* d_gather = nullptr;
 };
 
 template <int NB, int RB, bool WG>
@@ -2839,7 +2844,25 @@ void assign_buffers(Program& prog, int64_t units_per_first_img_ratio) {
   for (size_t k = 0; k < n; ++k) {
     ChainPlan& c = prog.chains[k];
     c.src_buf = (k == 0) ? -1 : int((k - 1) % 2);
-    c.dst_buf = (k + 1 == n) ? -1 : int(k % 2);
+    c.dst_buf = (k + 1 == n && prog.gather_src.empty()) ? -1 : int(k % 2);
+  }
+  if (!prog.gather_src.empty()) prog.gather_buf = int((n - 1) % 2);
+}
+
+// out[u][i][:] = src[u][gather_src[i]][:] (rows of `row` floats, row % 4 == 0);
+// one wave per unit, all of a unit's reads ahead of its writes (distinct buffers)
+__global__ void __launch_bounds__(256) embed_gather_kernel(const float* __restrict__ src, float* __restrict__ out,
+                                                           const int* __restrict__ map, int64_t n_units, int n_src,
+                                                           int n_out, int row) {
+  const int lane = threadIdx.x & 63;
+  const int64_t u = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (u >= n_units) return;
+  const int r4 = row / 4, n4 = n_out * r4;
+  const float4* s = reinterpret_cast<const float4*>(src + u * n_src * row);
+  float4* d = reinterpret_cast<float4*>(out + u * n_out * row);
+  for (int f = lane; f < n4; f += 64) {
+    const int i = f / r4, c = f - i * r4;
+    d[f] = s[map[i] * r4 + c];
   }
 }
 
@@ -2924,6 +2947,13 @@ int run_program(const Program& prog, const float* in, int64_t n_units, int64_t i
       if (blocks <= 0) continue;
       hipLaunchKernelGGL(c.fn, dim3(unsigned(blocks)), dim3(kThreads), c.lds_bytes, stream, a);
       HBK_LAUNCH_CHECK("conv_chain_kernel");
+    }
+    if (prog.gather_buf >= 0) {
+      const int n_out = static_cast<int>(prog.gather_src.size());
+      const int row = static_cast<int>(out_unit_floats / n_out);
+      hipLaunchKernelGGL(embed_gather_kernel, dim3(unsigned((nu + 3) / 4)), dim3(256), 0, stream,
+                         bufs[prog.gather_buf], out + u0 * out_unit_floats, prog.d_gather, nu, prog.n_src, n_out, row);
+      HBK_LAUNCH_CHECK("embed_gather_kernel");
     }
   }
   return HBK_OK;
@@ -3044,14 +3074,67 @@ int hbk_embed_plan_create_ex(const hbk_graph_op* ops, int32_t n_ops, int32_t in_
     for (int r : roff)
       if (r + wd.h > pre.h) return fail(arg_error("window start beyond the frame sequence"));
     const size_t n_pre = p->clip_prog.chains.size();
-    rc = build_segment(p->ops, split, n_ops, Dims{wd.h, wd.w, wd.c}, n_win, roff,
-                       int64_t(pre.h) * pre.w * pre.c, pre.w * pre.c, 0, p->split_f16, p->clip_prog,
-                       nullptr);
+    // Phase deduplication of the tail: with S = the tail's cumulative pool
+    // stride, windows whose prefix-row offsets are congruent mod S see the same
+    // pool grid, and the tail's valid convs are translation-equivariant, so
+    // ONE "phase image" per residue (rows [phi, phi + H)) yields every such
+    // window as output row (r - phi) / S. Used when the phase images' output
+    // fits the per-clip output (n_phase x rows <= n_win) and HBK_EMBED_NO_DEDUP
+    // is unset; the output rows are gathered into window order afterwards.
+    std::vector<int> phases, win_src;
+    int H = 0;
+    {
+      int S = 1;
+      for (int i = split; i < n_ops; ++i)
+        if (p->ops[i].kind == HBK_OP_MAXPOOL) S *= p->ops[i].kh;
+      for (int r : roff)
+        if (std::find(phases.begin(), phases.end(), r % S) == phases.end()) phases.push_back(r % S);
+      std::sort(phases.begin(), phases.end());
+      for (int r : roff) H = std::max(H, r - r % S + wd.h);
+      bool ok = S > 1 && !getenv("HBK_EMBED_NO_DEDUP") && int(phases.size()) < n_win;
+      for (int ph : phases) ok = ok && ph + H <= pre.h;
+      // tail output rows for an H-row phase image
+      Dims t{H, wd.w, wd.c};
+      for (int i = split; i < n_ops && ok; ++i) {
+        const OpInfo& o = p->ops[i];
+        t = o.kind == HBK_OP_CONV ? Dims{t.h - o.kh + 1, t.w - o.kw + 1, o.cout} : Dims{t.h / o.kh, t.w / o.kw, t.c};
+        ok = t.h > 0 && t.w > 0;
+      }
+      ok = ok && t.w == 1 && int(phases.size()) * t.h <= n_win;
+      if (ok) {
+        for (int r : roff) {
+          const int ph = int(std::find(phases.begin(), phases.end(), r % S) - phases.begin());
+          const int row = (r - r % S) / S;
+          ok = ok && row < t.h;
+          win_src.push_back(ph * t.h + row);
+        }
+        p->clip_prog.n_src = int(phases.size()) * t.h;
+      }
+      if (!ok) phases.clear();
+    }
+    if (!phases.empty()) {
+      p->clip_prog.gather_src = win_src;
+      hipError_t e = hipMalloc(reinterpret_cast<void**>(&p->clip_prog.d_gather), win_src.size() * sizeof(int));
+      if (e == hipSuccess)
+        e = hipMemcpy(p->clip_prog.d_gather, win_src.data(), win_src.size() * sizeof(int), hipMemcpyHostToDevice);
+      if (e != hipSuccess) return fail(hip_error(e, "embed gather map"));
+      rc = build_segment(p->ops, split, n_ops, Dims{H, wd.w, wd.c}, int(phases.size()), phases,
+                         int64_t(pre.h) * pre.w * pre.c, pre.w * pre.c, 0, p->split_f16, p->clip_prog, nullptr);
+      if (getenv("HBK_DEBUG_EMBED"))
+        fprintf(stderr, "hbk tail dedup: %zu phase images of %d rows per clip for %d windows\n", phases.size(), H,
+                n_win);
+    } else {
+      rc = build_segment(p->ops, split, n_ops, Dims{wd.h, wd.w, wd.c}, n_win, roff,
+                         int64_t(pre.h) * pre.w * pre.c, pre.w * pre.c, 0, p->split_f16, p->clip_prog,
+                         nullptr);
+    }
     if (rc) return fail(rc);
     for (size_t k = 0; k < p->clip_prog.chains.size(); ++k) {
       if (k < n_pre) p->prefix_macs += p->clip_prog.chains[k].macs_per_img;
       else p->tail_macs += p->clip_prog.chains[k].macs_per_img;
     }
+    // tail_macs is reported per window: with phase images, their MACs per clip / n_win
+    if (!phases.empty()) p->tail_macs *= double(phases.size()) / double(n_win);
     assign_buffers(p->clip_prog, 1);
   }
   // ---- window program: every op per window ----
@@ -3068,11 +3151,13 @@ int hbk_embed_plan_create_ex(const hbk_graph_op* ops, int32_t n_ops, int32_t in_
 
 int hbk_embed_plan_destroy(hbk_embed_plan* p) {
   if (!p) return HBK_OK;
-  for (auto* prog : {&p->clip_prog, &p->win_prog})
+  for (auto* prog : {&p->clip_prog, &p->win_prog}) {
     for (auto& c : prog->chains) {
       (void)hipFree(c.d_blob);
       if (c.d_p0) (void)hipFree(c.d_p0);
     }
+    if (prog->d_gather) (void)hipFree(prog->d_gather);
+  }
   if (p->d_range) (void)hipFree(p->d_range);
   delete p;
   return HBK_OK;
@@ -3103,12 +3188,16 @@ void program_geometry(const Program& prog, bool clip_path, int n_win, std::vecto
   imgs.clear();
   bufs.assign(2, 0);
   bool tail = false;
+  int tail_imgs = n_win;
   for (size_t k = 0; k < prog.chains.size(); ++k) {
     const ChainPlan& c = prog.chains[k];
     const int ipc = c.split ? c.x.ipc : c.args.ipc;
     const int64_t ois = c.split ? c.x.out_img_stride : c.args.out_img_stride;
-    if (clip_path && ipc > 1) tail = true;
-    imgs.push_back(tail ? n_win : 1);
+    if (clip_path && ipc > 1 && !tail) {
+      tail = true;
+      tail_imgs = ipc;  // n_win, or the phase images of a deduplicated tail
+    }
+    imgs.push_back(tail ? tail_imgs : 1);
     if (c.dst_buf >= 0) bufs[c.dst_buf] = std::max(bufs[c.dst_buf], ois * imgs.back());
   }
 }

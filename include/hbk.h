@@ -139,7 +139,9 @@ int hbk_embed_plan_create_ex(const hbk_graph_op* ops, int32_t n_ops, int32_t in_
                              hbk_embed_plan** plan);
 
 /* out_dim; number of ops shared per clip; fused chains (clip path); MACs per
- * clip (shared prefix, algorithmic) and per window (tail). */
+ * clip (shared prefix, algorithmic) and per window (tail; when the tail runs
+ * on deduplicated phase images -- windows whose offsets agree modulo the
+ * tail's pool stride share one -- the phase images' MACs per clip / n_win). */
 int hbk_embed_plan_info(const hbk_embed_plan* plan, int32_t* out_dim, int32_t* n_prefix_ops,
                         int32_t* n_chains, double* prefix_macs_per_clip,
                         double* tail_macs_per_window, int32_t* seq_frames);
