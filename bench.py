@@ -233,7 +233,9 @@ def main():
         roofs = job["rooflines"](dict(zip(job["stages"], stage_ms)), args.pmc)
     else:
         roofs = [job["roofline"](name, ms, args.pmc) for name, ms in zip(job["stages"], stage_ms)]
-    dom = max(range(len(roofs)), key=lambda i: roofs[i]["ms_per_step"])
+    # the dominant kernel group by device time (a stage summary that only aggregates
+    # groups listed on their own is never the headline entry)
+    dom = max(range(len(roofs)), key=lambda i: (not roofs[i].get("summary"), roofs[i]["ms_per_step"]))
 
     extra = job["extra_rooflines"]() if "extra_rooflines" in job and world == 1 else []
     cpu = None
@@ -765,7 +767,7 @@ def setup_e2e(args, dev, rank, world, seed):
                         n * AUG_T * 4 * 2, ms, "GB/s", load_traffic(pmc, ("place_kernel", "augment_kernel", "eq_kernel",
                                                                           "band_stop", "colored_noise", "ps_",
                                                                           "tanh_distortion")),
-                        algorithmic_bytes_per_clip=AUG_T * 4 * 2,
+                        algorithmic_bytes_per_clip=AUG_T * 4 * 2, summary=True,
                         bytes_basis="placed clip written + augmented clip written in place (92,160 B each); "
                                     "the chain's re-reads of the in-place buffer are not counted")
         if name == "mel":
