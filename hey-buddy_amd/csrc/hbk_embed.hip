@@ -1510,32 +1510,34 @@ __device__ __forceinline__ void p0s_iter(P0sCtx<LEAKY>& c, int y, int qi, _Float
   _Float16* s1 = wl + 4 * kP0sS0Plane;
 
   // B fragments of stage 1 (row y - 1) and stage 2 (row y - 4), one K step
-  // ahead of their MFMAs (two sets live). Stage 1: K group g = 2 ks + khalf =
-  // tap * 3 + c sits at s0 fp16 offset 24 (x + tap) + 8 c = 24 x + 8 g, one
-  // per-lane base plus immediates; group 9 is the bias slot (B = 1). Stage 2:
-  // the groups (dy, c) are paired within a row for ks < 3 (khalf = c), then
-  // (0, 2) | (1, 2) and (2, 2) | bias (kP0sG2, mirrored by plan_p0s's packing).
+  // ahead of their MFMAs. Stage 1: K group g = 2 ks + khalf = tap * 3 + c sits
+  // at s0 fp16 offset 24 (x + tap) + 8 c = 24 x + 8 g, one per-lane base plus
+  // immediates; group 9 is the bias slot (B = 1). Stage 2: the groups (dy, c)
+  // are paired within a row for ks < 3 (khalf = c), then (0, 2) | (1, 2) and
+  // (2, 2) | bias (mirrored by plan_p0s's packing).
   const _Float16* base1 = s0r + x * kP0sCS + 8 * khalf;
   const _Float16* base2 = s1 + x * kP0sCS + 8 * khalf;
-  auto load = [&](int ks, h8& b1h, h8& b1l, h8& b2h, h8& b2l) {
-    const _Float16* p1 = base1 + 16 * ks;
+  auto load1 = [&](int ks, h8& bh, h8& bl) {
+    const bool one = ks == 4 && khalf;
+    const _Float16* p1 = one ? wl + kP0sOnes : base1 + 16 * ks;
+    bh = *reinterpret_cast<const h8*>(p1);
+    bl = *reinterpret_cast<const h8*>(p1 + (one ? 8 : kP0sS0Plane));
+  };
+  auto load2 = [&](int ks, h8& bh, h8& bl) {
     const _Float16* p2;
     if (ks < 3) {
       p2 = base2 + ((PAR + ks) & 3) * 2 * kP0sS1Plane;
     } else if (ks == 3) {
       p2 = s1 + x * kP0sCS + 16 + (khalf ? ((PAR + 1) & 3) : (PAR & 3)) * 2 * kP0sS1Plane;
     } else {
-      p1 = khalf ? wl + kP0sOnes : p1;
       p2 = khalf ? wl + kP0sOnes : s1 + x * kP0sCS + 16 + ((PAR + 2) & 3) * 2 * kP0sS1Plane;
     }
-    const bool one1 = ks == 4 && khalf, one2 = ks == 4 && khalf;
-    b1h = *reinterpret_cast<const h8*>(p1);
-    b1l = *reinterpret_cast<const h8*>(p1 + (one1 ? 8 : kP0sS0Plane));
-    b2h = *reinterpret_cast<const h8*>(p2);
-    b2l = *reinterpret_cast<const h8*>(p2 + (one2 ? 8 : kP0sS1Plane));
+    const bool one = ks == 4 && khalf;
+    bh = *reinterpret_cast<const h8*>(p2);
+    bl = *reinterpret_cast<const h8*>(p2 + (one ? 8 : kP0sS1Plane));
   };
-  h8 f[2][4];
-  load(0, f[0][0], f[0][1], f[0][2], f[0][3]);
+  h8 f[2][2];
+  load1(0, f[0][0], f[0][1]);
 
   // stage 0 (row y): K slots {r0[0..2], r1[0..2], 1, 0} in both lane halves, the
   // window one row lower in the upper half (taps (0, *), (1, 0), (1, 1) and the
@@ -1551,34 +1553,54 @@ __device__ __forceinline__ void p0s_iter(P0sCtx<LEAKY>& c, int y, int qi, _Float
   f16x acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(c.a0h, xh, zero, 0, 0, 0);
   acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(c.a0h, xl, acc0, 0, 0, 0);
   acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(c.a0l, xh, acc0, 0, 0, 0);
+  const bool raw_ok = y < kP0sRows - 2;
 
+  // The three stages' MFMA chains run one after another (stage 1, then stage
+  // 2), and each finished stage's epilogue is issued between the next stage's
+  // MFMAs (sched_group_barrier: 1 MFMA, then up to 5 VALU), so a wave keeps its
+  // own matrix pipe busy while it activates, splits and stores: stage 0's
+  // epilogue beside stage 1's MFMAs, stage 1's beside stage 2's.
+  f16x acc1 = zero;
+#pragma unroll
+  for (int ks = 0; ks < kP0sKS; ++ks) {
+    h8* cur = f[ks & 1];
+    if (ks + 1 < kP0sKS) load1(ks + 1, f[(ks + 1) & 1][0], f[(ks + 1) & 1][1]);
+    else load2(0, f[(ks + 1) & 1][0], f[(ks + 1) & 1][1]);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(c.w1.h[ks], cur[0], acc1, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(c.w1.h[ks], cur[1], acc1, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(c.w1.l[ks], cur[0], acc1, 0, 0, 0);
+    if (ks == 1) {
+      asm("v_max_f32 %0, %0, %1" : "+v"(c.amax) : "v"(raw_ok ? m0 : 0.f));
+      p0s_store<LEAKY>(acc0, s0w, x, khalf, c.alpha, raw_ok && x < 30, c.amax, kP0sS0Plane);
+    }
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+    }
+  }
   // stage 2 accumulates into c.pool for an even row y - 4 (held for its odd partner)
-  f16x acc1 = zero, acc2 = zero;
+  f16x acc2 = zero;
   f16x& a2 = (PAR & 1) == 0 ? c.pool : acc2;
   a2 = zero;
 #pragma unroll
   for (int ks = 0; ks < kP0sKS; ++ks) {
-    h8* cur = f[ks & 1];
-    if (ks + 1 < kP0sKS) {
-      h8* nx = f[(ks + 1) & 1];
-      load(ks + 1, nx[0], nx[1], nx[2], nx[3]);
+    h8* cur = f[(ks + kP0sKS) & 1];
+    if (ks + 1 < kP0sKS) load2(ks + 1, f[(ks + 1 + kP0sKS) & 1][0], f[(ks + 1 + kP0sKS) & 1][1]);
+    a2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(c.w2.h[ks], cur[0], a2, 0, 0, 0);
+    a2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(c.w2.h[ks], cur[1], a2, 0, 0, 0);
+    a2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(c.w2.l[ks], cur[0], a2, 0, 0, 0);
+    if (ks == 0)
+      p0s_store<LEAKY>(acc1, s1 + ((PAR + 3) & 3) * 2 * kP0sS1Plane, x, khalf, c.alpha,
+                       y >= 1 && y <= kP0sRows - 2 && x < 28, c.amax, kP0sS1Plane);
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
     }
-    __builtin_amdgcn_sched_barrier(0);
-    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(c.w1.h[ks], cur[0], acc1, 0, 0, 0);
-    a2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(c.w2.h[ks], cur[2], a2, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(c.w1.h[ks], cur[1], acc1, 0, 0, 0);
-    a2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(c.w2.h[ks], cur[3], a2, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(c.w1.l[ks], cur[0], acc1, 0, 0, 0);
-    a2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(c.w2.l[ks], cur[2], a2, 0, 0, 0);
   }
-
-  // epilogues: stage 0 -> s0[y & 1] (rows < 134, positions < 30 tracked),
-  // stage 1 -> s1[(y - 1) & 3] (rows 0 .. 133, positions < 28 tracked)
-  const bool raw_ok = y < kP0sRows - 2;
-  asm("v_max_f32 %0, %0, %1" : "+v"(c.amax) : "v"(raw_ok ? m0 : 0.f));
-  p0s_store<LEAKY>(acc0, s0w, x, khalf, c.alpha, raw_ok && x < 30, c.amax, kP0sS0Plane);
-  p0s_store<LEAKY>(acc1, s1 + ((PAR + 3) & 3) * 2 * kP0sS1Plane, x, khalf, c.alpha,
-                   y >= 1 && y <= kP0sRows - 2 && x < 28, c.amax, kP0sS1Plane);
 
   // stage 2 (row y - 4): rows 2i and 2i + 1 pooled (max commutes with the
   // monotone activation; v_maximum3 propagates NaN, as the reference's max-pool)
