@@ -1944,6 +1944,283 @@ p1s_chain_kernel(P1Args a) {
   raise_range(a.range_flag, c.amax);
 }
 
+// ------------------------------------------------------------------ p2s ----
+// Streaming form of SE20's chain 2 (the prefix's last chain, no output pool:
+// 31 x 5 x 32 -> 1x3 32 -> 48 -> 3x1 -> 1x3 -> 3x1 48 -> 48 -> 27 x 1 x 48).
+// Its rows are 3 or 1 positions wide, so a tile packs CLIPS: a workgroup
+// streams the rows of 16 clips at once, and a 16-position tile of
+// v_mfma_f32_16x16x32_f16 is (clip, column) for stages a, b (48 positions: 3
+// tiles) and the clip for stages c, d (1 tile). Eight waves, one unit each,
+// with that unit's weights in VGPRs: waves 0-2 stage a tiles 0-2, waves 3-5
+// stage b tiles 0-2, wave 6 stage c, wave 7 stage d. Tick y (one workgroup
+// barrier after it): a(y), b(y - 3), c(y - 4), d(y - 7), and every wave
+// stages its share of input row y + 1. Rings as in p1s. K groups of 8
+// (g = 4 ks + kq): a: g = dx * 4 + c (32 input channels); b, c, d: g = tap * 6
+// + c (48 channels), g = 18 the bias slot (B = 1), g = 19 zeros; stage a
+// starts its accumulators at the bias.
+constexpr int kP2sThreads = 512, kP2sClips = 16;
+constexpr int kP2sHin = 31, kP2sWi = 5, kP2sCi = 32, kP2sCo = 48, kP2sHout = 27;
+constexpr int kP2sCSI = 40, kP2sCS = 56;                      // fp16 per position (odd 16-B groups)
+constexpr int kP2sInPlane = kP2sClips * kP2sWi * kP2sCSI;     // one input row of 16 clips
+constexpr int kP2sAPlane = kP2sClips * 3 * kP2sCS;            // stage a / b output rows (3 columns)
+constexpr int kP2sCPlane = kP2sClips * kP2sCS;                // stage c output rows (1 column)
+constexpr int kP2sIn = 0, kP2sA = kP2sIn + 2 * 2 * kP2sInPlane, kP2sB = kP2sA + 4 * 2 * kP2sAPlane,
+              kP2sC = kP2sB + 2 * 2 * kP2sAPlane, kP2sOnes = kP2sC + 4 * 2 * kP2sCPlane;
+constexpr int kP2sHalfs = kP2sOnes + 32;
+constexpr int kP2sLds = kP2sHalfs * 2;
+constexpr int kP2sKa = 96, kP2sK = 160;                       // packed K of stage a / stages b, c, d
+constexpr int kP2sTicks = 36;                                 // rows 0 .. 30 through a 7-tick pipeline
+
+struct P2sArgs {
+  const float* in;        // [img][31][5][32] f32
+  float* out;             // [img][27][48] f32
+  const _Float16* w;      // a: hi / lo [48][96]; b, c, d: hi / lo [48][160]
+  const float* bias_a;    // [48]
+  int64_t n_img, src_img_stride;
+  float alpha;
+  int* range_flag;
+};
+
+// the wave's weights: [output block][K step] hi / lo
+template <int KS>
+struct P2sW {
+  h8 h[3][KS], l[3][KS];
+};
+
+template <int KS>
+__device__ __forceinline__ void p2s_mma(f4 (&acc)[3], const P2sW<KS>& w, int ks, const h8& bh, const h8& bl) {
+#pragma unroll
+  for (int mb = 0; mb < 3; ++mb) {
+    acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w.h[mb][ks], bh, acc[mb], 0, 0, 0);
+    acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w.h[mb][ks], bl, acc[mb], 0, 0, 0);
+    acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w.l[mb][ks], bh, acc[mb], 0, 0, 0);
+  }
+}
+
+// activation, split and LDS store of a finished tile (channels 16 mb + 4 kq + j at position p)
+template <bool LEAKY>
+__device__ __forceinline__ void p2s_store(const f4 (&acc)[3], _Float16* oh, int plane, int p, int kq, float alpha,
+                                          bool track_it, float& amax) {
+  float m = 0.f;
+#pragma unroll
+  for (int mb = 0; mb < 3; ++mb) {
+    float v[4] = {acc[mb][0], acc[mb][1], acc[mb][2], acc[mb][3]};
+    p0s_act2<LEAKY>(v[0], v[1], alpha);
+    p0s_act2<LEAKY>(v[2], v[3], alpha);
+    uint32_t h01, l01, h23, l23;
+    split2_mix(v[0], v[1], h01, l01, m);
+    split2_mix(v[2], v[3], h23, l23, m);
+    const int o = p * kP2sCS + 16 * mb + 4 * kq;
+    *reinterpret_cast<uint2*>(oh + o) = uint2{h01, h23};
+    *reinterpret_cast<uint2*>(oh + plane + o) = uint2{l01, l23};
+  }
+  asm("v_max_f32 %0, %0, %1" : "+v"(amax) : "v"(track_it ? m : 0.f));
+}
+
+// every thread's share of input row `row` of the group's clips (640 float4): load / stage
+struct P2sRow {
+  float4 v[2];
+};
+__device__ __forceinline__ void p2s_load_row(P2sRow& r, const P2sArgs& a, int64_t img0, int row, int tid) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = min(tid + kP2sThreads * u, kP2sClips * kP2sWi * kP2sCi / 4 - 1);
+    const int c = i / 40, rem = i - 40 * c;
+    const int64_t img = min(img0 + c, a.n_img - 1);
+    r.v[u] = *reinterpret_cast<const float4*>(a.in + img * a.src_img_stride + min(row, kP2sHin - 1) *
+                                              (kP2sWi * kP2sCi) + 4 * rem);
+  }
+}
+__device__ __forceinline__ void p2s_stage_row(const P2sRow& r, _Float16* slot, int tid, float& amax) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = tid + kP2sThreads * u;
+    if (u == 0 || i < kP2sClips * kP2sWi * kP2sCi / 4) {
+      const int c = i / 40, rem = i - 40 * c, col = rem >> 3, c4 = rem & 7;
+      uint32_t h01, l01, h23, l23;
+      split2_mix(r.v[u].x, r.v[u].y, h01, l01, amax);
+      split2_mix(r.v[u].z, r.v[u].w, h23, l23, amax);
+      const int o = (c * kP2sWi + col) * kP2sCSI + 4 * c4;
+      *reinterpret_cast<uint2*>(slot + o) = uint2{h01, h23};
+      *reinterpret_cast<uint2*>(slot + kP2sInPlane + o) = uint2{l01, l23};
+    }
+  }
+}
+
+template <bool LEAKY>
+__global__ void __launch_bounds__(kP2sThreads) __attribute__((amdgpu_waves_per_eu(2)))
+p2s_chain_kernel(P2sArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char p2smem[];
+  _Float16* sm = reinterpret_cast<_Float16*>(p2smem);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int pl = lane & 15, kq = lane >> 4;
+  if (tid < 32) sm[kP2sOnes + tid] = static_cast<_Float16>(tid == 0 ? 1.f : 0.f);  // ones (hi, lo), zeros
+  const int64_t n_groups = (a.n_img + kP2sClips - 1) / kP2sClips;
+  float amax = 0.f;
+  const float alpha = a.alpha;
+  const _Float16* ones = sm + kP2sOnes;
+  // K groups g = 4 ks + kq of stages b, c, d: tap g / 6, channel group g % 6; g >= 18: bias / zeros slot
+  auto tap_of = [&](int ks) { return (4 * ks + kq) / 6; };
+  auto cg_of = [&](int ks) { return (4 * ks + kq) % 6; };
+
+  if (wave < 3) {  // ---------------- stage a, tile t = wave: positions p = 3 clip + column
+    const int t = wave, p = 16 * t + pl, c = p / 3, x = p - 3 * c;
+    P2sW<3> W;
+#pragma unroll
+    for (int mb = 0; mb < 3; ++mb)
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) {
+        const _Float16* wp = a.w + (16 * mb + pl) * kP2sKa + 32 * ks + 8 * kq;
+        W.h[mb][ks] = *reinterpret_cast<const h8*>(wp);
+        W.l[mb][ks] = *reinterpret_cast<const h8*>(wp + kP2sCo * kP2sKa);
+      }
+    f4 bias[3];
+#pragma unroll
+    for (int mb = 0; mb < 3; ++mb) {
+      const float4 b = *reinterpret_cast<const float4*>(a.bias_a + 16 * mb + 4 * kq);
+      bias[mb] = f4{b.x, b.y, b.z, b.w};
+    }
+    const int base = (c * kP2sWi + x) * kP2sCSI + 8 * kq;  // + 40 ks: column x + ks, channels 8 kq
+    for (int64_t gi = blockIdx.x; gi < n_groups; gi += gridDim.x) {
+      const int64_t img0 = gi * kP2sClips;
+      P2sRow q0, q1;
+      p2s_load_row(q0, a, img0, 0, tid);
+      p2s_load_row(q1, a, img0, 1, tid);
+      p2s_stage_row(q0, sm + kP2sIn, tid, amax);
+      p2s_load_row(q0, a, img0, 2, tid);
+      __syncthreads();
+      for (int y = 0; y < kP2sTicks; ++y) {
+        const _Float16* in = sm + kP2sIn + (y & 1) * 2 * kP2sInPlane;
+        h8 bh[3], bl[3];
+#pragma unroll
+        for (int ks = 0; ks < 3; ++ks) {
+          bh[ks] = *reinterpret_cast<const h8*>(in + base + kP2sCSI * ks);
+          bl[ks] = *reinterpret_cast<const h8*>(in + kP2sInPlane + base + kP2sCSI * ks);
+        }
+        {  // input row y + 1 (loaded a tick ago) -> the other slot; load row y + 3
+          float m = 0.f;
+          p2s_stage_row((y & 1) ? q0 : q1, sm + kP2sIn + ((y + 1) & 1) * 2 * kP2sInPlane, tid, m);
+          asm("v_max_f32 %0, %0, %1" : "+v"(amax) : "v"(y + 1 < kP2sHin ? m : 0.f));
+          if (y & 1) p2s_load_row(q0, a, img0, y + 3, tid);
+          else p2s_load_row(q1, a, img0, y + 3, tid);
+        }
+        f4 acc[3] = {bias[0], bias[1], bias[2]};
+#pragma unroll
+        for (int ks = 0; ks < 3; ++ks) p2s_mma<3>(acc, W, ks, bh[ks], bl[ks]);
+        p2s_store<LEAKY>(acc, sm + kP2sA + (y & 3) * 2 * kP2sAPlane, kP2sAPlane, p, kq, alpha, y < kP2sHin, amax);
+        __syncthreads();
+      }
+    }
+  } else if (wave < 6) {  // ---------------- stage b (3x1 on the A ring), tile t = wave - 3
+    const int t = wave - 3, p = 16 * t + pl;
+    P2sW<5> W;
+#pragma unroll
+    for (int mb = 0; mb < 3; ++mb)
+#pragma unroll
+      for (int ks = 0; ks < 5; ++ks) {
+        const _Float16* wp = a.w + 2 * kP2sCo * kP2sKa + (16 * mb + pl) * kP2sK + 32 * ks + 8 * kq;
+        W.h[mb][ks] = *reinterpret_cast<const h8*>(wp);
+        W.l[mb][ks] = *reinterpret_cast<const h8*>(wp + kP2sCo * kP2sK);
+      }
+    for (int64_t gi = blockIdx.x; gi < n_groups; gi += gridDim.x) {
+      const int64_t img0 = gi * kP2sClips;
+      P2sRow q0, q1;
+      p2s_load_row(q0, a, img0, 0, tid);
+      p2s_load_row(q1, a, img0, 1, tid);
+      p2s_stage_row(q0, sm + kP2sIn, tid, amax);
+      p2s_load_row(q0, a, img0, 2, tid);
+      __syncthreads();
+      for (int y = 0; y < kP2sTicks; ++y) {
+        f4 acc[3] = {};
+#pragma unroll
+        for (int ks = 0; ks < 5; ++ks) {
+          const int tap = tap_of(ks), cg = cg_of(ks);
+          const bool bias_slot = 4 * ks + kq >= 18;
+          const _Float16* pb = bias_slot ? ones + (kq == 2 ? 0 : 16)
+                                         : sm + kP2sA + ((y + 1 + tap) & 3) * 2 * kP2sAPlane + p * kP2sCS + 8 * cg;
+          const int lo = bias_slot ? 8 : kP2sAPlane;
+          const h8 bh = *reinterpret_cast<const h8*>(pb), bl = *reinterpret_cast<const h8*>(pb + lo);
+          p2s_mma<5>(acc, W, ks, bh, bl);
+        }
+        {
+          float m = 0.f;
+          p2s_stage_row((y & 1) ? q0 : q1, sm + kP2sIn + ((y + 1) & 1) * 2 * kP2sInPlane, tid, m);
+          asm("v_max_f32 %0, %0, %1" : "+v"(amax) : "v"(y + 1 < kP2sHin ? m : 0.f));
+          if (y & 1) p2s_load_row(q0, a, img0, y + 3, tid);
+          else p2s_load_row(q1, a, img0, y + 3, tid);
+        }
+        p2s_store<LEAKY>(acc, sm + kP2sB + ((y + 1) & 1) * 2 * kP2sAPlane, kP2sAPlane, p, kq, alpha,
+                         y >= 3 && y - 3 < kP2sHin - 2, amax);
+        __syncthreads();
+      }
+    }
+  } else {  // ---------------- stage c (wave 6: 1x3 on B) or d (wave 7: 3x1 on the C ring); position = clip
+    const bool is_c = wave == 6;
+    P2sW<5> W;
+#pragma unroll
+    for (int mb = 0; mb < 3; ++mb)
+#pragma unroll
+      for (int ks = 0; ks < 5; ++ks) {
+        const _Float16* wp = a.w + 2 * kP2sCo * kP2sKa + (is_c ? 1 : 2) * 2 * kP2sCo * kP2sK + (16 * mb + pl) * kP2sK +
+                             32 * ks + 8 * kq;
+        W.h[mb][ks] = *reinterpret_cast<const h8*>(wp);
+        W.l[mb][ks] = *reinterpret_cast<const h8*>(wp + kP2sCo * kP2sK);
+      }
+    for (int64_t gi = blockIdx.x; gi < n_groups; gi += gridDim.x) {
+      const int64_t img0 = gi * kP2sClips;
+      P2sRow q0, q1;
+      p2s_load_row(q0, a, img0, 0, tid);
+      p2s_load_row(q1, a, img0, 1, tid);
+      p2s_stage_row(q0, sm + kP2sIn, tid, amax);
+      p2s_load_row(q0, a, img0, 2, tid);
+      __syncthreads();
+      for (int y = 0; y < kP2sTicks; ++y) {
+        f4 acc[3] = {};
+#pragma unroll
+        for (int ks = 0; ks < 5; ++ks) {
+          const int tap = tap_of(ks), cg = cg_of(ks);
+          const bool bias_slot = 4 * ks + kq >= 18;
+          const _Float16* src;
+          int lo;
+          if (is_c) {  // B row y - 4, position (clip, tap), channels 8 cg
+            src = sm + kP2sB + (y & 1) * 2 * kP2sAPlane + (3 * pl + tap) * kP2sCS + 8 * cg;
+            lo = kP2sAPlane;
+          } else {     // C ring row y - 7 + tap, position clip
+            src = sm + kP2sC + ((y + 1 + tap) & 3) * 2 * kP2sCPlane + pl * kP2sCS + 8 * cg;
+            lo = kP2sCPlane;
+          }
+          const _Float16* pb = bias_slot ? ones + (kq == 2 ? 0 : 16) : src;
+          if (bias_slot) lo = 8;
+          const h8 bh = *reinterpret_cast<const h8*>(pb), bl = *reinterpret_cast<const h8*>(pb + lo);
+          p2s_mma<5>(acc, W, ks, bh, bl);
+        }
+        {
+          float m = 0.f;
+          p2s_stage_row((y & 1) ? q0 : q1, sm + kP2sIn + ((y + 1) & 1) * 2 * kP2sInPlane, tid, m);
+          asm("v_max_f32 %0, %0, %1" : "+v"(amax) : "v"(y + 1 < kP2sHin ? m : 0.f));
+          if (y & 1) p2s_load_row(q0, a, img0, y + 3, tid);
+          else p2s_load_row(q1, a, img0, y + 3, tid);
+        }
+        if (is_c) {
+          p2s_store<LEAKY>(acc, sm + kP2sC + (y & 3) * 2 * kP2sCPlane, kP2sCPlane, pl, kq, alpha,
+                           y >= 4 && y - 4 < kP2sHin - 2, amax);
+        } else if (y >= 7 && y - 7 < kP2sHout && img0 + pl < a.n_img) {
+          float* o = a.out + (img0 + pl) * (kP2sHout * kP2sCo) + (y - 7) * kP2sCo + 4 * kq;
+#pragma unroll
+          for (int mb = 0; mb < 3; ++mb) {
+            float v[4] = {acc[mb][0], acc[mb][1], acc[mb][2], acc[mb][3]};
+            p0s_act2<LEAKY>(v[0], v[1], alpha);
+            p0s_act2<LEAKY>(v[2], v[3], alpha);
+            *reinterpret_cast<float4*>(o + 16 * mb) = float4{v[0], v[1], v[2], v[3]};
+          }
+        }
+        __syncthreads();
+      }
+    }
+  }
+  raise_range(a.range_flag, amax);
+}
+
 // ------------------------------------------------------------------ host ----
 
 struct OpInfo {
@@ -1978,6 +2255,8 @@ struct ChainPlan {
   P0Args p0{};
   bool p0s = false;  // p0fn is the streaming p0s_chain_kernel (one wave per image)
   bool p1s = false;  // p1fn is the streaming p1s_chain_kernel (one wave per image)
+  void (*p2fn)(P2sArgs) = nullptr;  // p2s pattern (SE20 chain 2; shares d_p0 / p0_lds / p0_blocks_per_cu)
+  P2sArgs p2{};
   void (*p1fn)(P1Args) = nullptr;  // p1 pattern (shares d_p0 / p0_lds / p0_blocks_per_cu)
   P1Args p1{};
   size_t p0_lds = 0;
@@ -2586,6 +2865,78 @@ bool plan_p1s(const std::vector<OpInfo>& ops, const std::vector<int>& st, const 
   return true;
 }
 
+// The p2s pattern (SE20 chain 2): [1x3 (32 -> 48), 3x1, 1x3, 3x1 (48 -> 48)] on a
+// 31 x 5 x 32 input, no output pool, one image per source image. Weights hi /
+// lo [48][96] (stage a) and [48][160] (b, c, d: K = tap * 48 + ci, the bias at
+// K 144); stage a's bias as f32.
+bool plan_p2s(const std::vector<OpInfo>& ops, const std::vector<int>& st, const ChainArgs& a, Dims d, Dims od,
+              ChainPlan& cp) {
+  if (getenv("HBK_EMBED_NO_P2S")) return false;
+  if (st.size() != 4 || a.ipc != 1 || a.in_ph != 1 || a.in_pw != 1 || a.out_ph != 1 || a.out_pw != 1) return false;
+  if (d.h != kP2sHin || d.w != kP2sWi || d.c != kP2sCi || a.C_src != kP2sCi || a.src_row_stride != kP2sWi * kP2sCi)
+    return false;
+  const int kh[4] = {1, 3, 1, 3}, kw[4] = {3, 1, 3, 1};
+  const bool leaky = ops[st[0]].act != 0;
+  for (int i = 0; i < 4; ++i) {
+    const OpInfo& o = ops[st[i]];
+    if (o.kh != kh[i] || o.kw != kw[i] || o.cin != (i ? kP2sCo : kP2sCi) || o.cout != kP2sCo) return false;
+    if ((o.act != 0) != leaky) return false;
+    if (leaky && (o.alpha != ops[st[0]].alpha || !(o.alpha >= 0.f && o.alpha <= 1.f))) return false;
+  }
+  if (od.h != kP2sHout || od.w != 1 || od.c != kP2sCo) return false;
+  const size_t wa = size_t(2) * kP2sCo * kP2sKa, wsz = size_t(2) * kP2sCo * kP2sK;
+  std::vector<_Float16> w(wa + 3 * wsz, static_cast<_Float16>(0.f));
+  auto put = [&](size_t off, int Kp, int n, int k, float v) {
+    uint32_t bits;
+    memcpy(&bits, &v, 4);
+    bits &= 0xFFFFE000u;
+    float hv;
+    memcpy(&hv, &bits, 4);
+    w[off + size_t(n) * Kp + k] = static_cast<_Float16>(hv);
+    w[off + size_t(kP2sCo) * Kp + size_t(n) * Kp + k] = static_cast<_Float16>(v - hv);
+  };
+  for (int s2 = 0; s2 < 4; ++s2) {
+    const OpInfo& o = ops[st[s2]];
+    const size_t off = s2 == 0 ? 0 : wa + (s2 - 1) * wsz;
+    const int Kp = s2 == 0 ? kP2sKa : kP2sK, K = 3 * o.cin;
+    for (int n = 0; n < kP2sCo; ++n) {
+      for (int k = 0; k < K; ++k) put(off, Kp, n, k, o.w[size_t(k) * kP2sCo + n]);  // HWIO: (tap cin + ci) cout + n
+      if (s2 > 0) put(off, Kp, n, K, o.b[n]);
+    }
+  }
+  const size_t wbytes = (w.size() * 2 + 15) & ~size_t(15);
+  hipError_t e = hipMalloc(&cp.d_p0, wbytes + kP2sCo * 4);
+  if (e == hipSuccess) e = hipMemcpy(cp.d_p0, w.data(), w.size() * 2, hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = hipMemcpy(static_cast<unsigned char*>(cp.d_p0) + wbytes, ops[st[0]].b.data(), kP2sCo * 4,
+                  hipMemcpyHostToDevice);
+  cp.p2fn = leaky ? p2s_chain_kernel<true> : p2s_chain_kernel<false>;
+  cp.p0_lds = kP2sLds;
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(cp.p2fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            int(cp.p0_lds));
+  int per_cu = 0;
+  if (e == hipSuccess)
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(cp.p2fn), kP2sThreads,
+                                                     cp.p0_lds);
+  if (e != hipSuccess || per_cu < 1) {
+    (void)hipGetLastError();
+    if (cp.d_p0) (void)hipFree(cp.d_p0);
+    cp.d_p0 = nullptr;
+    cp.p2fn = nullptr;
+    return false;
+  }
+  cp.p0_blocks_per_cu = per_cu;
+  P2sArgs& p = cp.p2;
+  p.w = static_cast<const _Float16*>(cp.d_p0);
+  p.bias_a = reinterpret_cast<const float*>(static_cast<unsigned char*>(cp.d_p0) + wbytes);
+  p.alpha = leaky ? ops[st[0]].alpha : 0.f;
+  if (getenv("HBK_DEBUG_EMBED"))
+    fprintf(stderr, "hbk p2s chain: %dx%dx%d -> %dx%dx%d, %d clips per workgroup, LDS %zu B, %d blocks/CU\n", d.h,
+            d.w, d.c, od.h, od.w, od.c, kP2sClips, cp.p0_lds, per_cu);
+  return true;
+}
+
 bool plan_p1(const std::vector<OpInfo>& ops, const std::vector<int>& st, const ChainArgs& a, Dims d, Dims od,
              ChainPlan& cp) {
   if (getenv("HBK_EMBED_NO_P1")) return false;
@@ -2705,7 +3056,8 @@ int build_segment(const std::vector<OpInfo>& ops, int o0, int o1, Dims in, int i
       Dims od;
       const int rc = layout_split(ops, stage_ops, d, a, cp, od);
       if (rc) return rc;
-      if (!plan_p0(ops, stage_ops, a, d, od, cp)) plan_p1(ops, stage_ops, a, d, od, cp);
+      if (!plan_p0(ops, stage_ops, a, d, od, cp) && !plan_p1(ops, stage_ops, a, d, od, cp))
+        plan_p2s(ops, stage_ops, a, d, od, cp);
       cp.x.dbg_slot = static_cast<int>(prog.chains.size() % 4);
       if (const char* e = getenv("HBK_DEBUG_SKIP")) cp.x.dbg_skip = atoi(e);
       cp.src_buf = src_buf;
@@ -2930,6 +3282,24 @@ int run_program(const Program& prog, const float* in, int64_t n_units, int64_t i
           if (blocks <= 0) continue;
           hipLaunchKernelGGL(c.p1fn, dim3(unsigned(blocks)), dim3(c.p1s ? kP1sThreads : kP0Threads), c.p0_lds, stream, pa);
           HBK_LAUNCH_CHECK("p1_chain_kernel");
+          continue;
+        }
+      }
+      if (c.p2fn) {
+        P2sArgs pa = c.p2;
+        pa.range_flag = range_flag;
+        pa.in = c.src_buf < 0 ? in + u0 * in_unit_stride : bufs[c.src_buf];
+        pa.src_img_stride = c.src_buf < 0 ? in_unit_stride : c.x.src_clip_stride;
+        pa.out = c.dst_buf < 0 ? out + u0 * out_unit_floats : bufs[c.dst_buf];
+        pa.n_img = nu * imgs_per_unit[k];
+        const bool aligned = !(reinterpret_cast<uintptr_t>(pa.in) & 15) && !(pa.src_img_stride & 3) &&
+                             !(reinterpret_cast<uintptr_t>(pa.out) & 15);
+        if (aligned) {
+          const int64_t groups = (pa.n_img + kP2sClips - 1) / kP2sClips;
+          const int64_t blocks = std::min<int64_t>(groups, persistent_blocks(c.p0_blocks_per_cu, stream));
+          if (blocks <= 0) continue;
+          hipLaunchKernelGGL(c.p2fn, dim3(unsigned(blocks)), dim3(kP2sThreads), c.p0_lds, stream, pa);
+          HBK_LAUNCH_CHECK("p2s_chain_kernel");
           continue;
         }
       }
