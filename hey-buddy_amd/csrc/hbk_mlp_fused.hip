@@ -1660,7 +1660,10 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
   // k3: job 0 = input layer, then dW_hg of GMLPs 1.., then dW_o of every GMLP
   K3Args k3;
   int nj = 0, blocks = 0;
-  const bool narrow = persistent_blocks(1, s) <= kK3NarrowCUs;
+  // HBK_K3_WIDE=1: the 288-row splits on narrow streams too (4 instead of 9
+  // splits at B = 1100: fewer partial-sum atomics, more time on a small partition)
+  static const bool k3_wide = getenv("HBK_K3_WIDE") != nullptr;
+  const bool narrow = !k3_wide && persistent_blocks(1, s) <= kK3NarrowCUs;
   const int rows3 = 32 * (narrow ? kK3StepsNarrow : kK3Steps);
   const int KS3 = static_cast<int>((Bp + rows3 - 1) / rows3);
   auto add = [&](const float* X, const float* Y, float* C, int ldc, int M, int N) {
