@@ -1395,9 +1395,11 @@ __global__ void __launch_bounds__(64) eq_kernel(EqArgs a) {
 //    direct float64 DFT restarts it every kPvRestart frames. A frame whose 250
 //    samples are all zero is exactly 0 (angle 0) as in the FFT (a running
 //    count of non-zero samples);
-//  * vocoder: the phase in revolutions, accR_{t+1} = accR_t + wrap((a1 - a0) /
-//    2 pi - 7k/250): the phase advance adv_k = 2 pi 7k/250 cancels against the
+//  * vocoder: the phase in revolutions, accR_{t+1} = accR_t + (a1 - a0) / 2 pi
+//    - 7k/250 (mod 1): the phase advance adv_k = 2 pi 7k/250 cancels against the
 //    istft's frame rotation, so Z_t = Y_t e^{-2 pi i 7kt/250} = m_t e^{2 pi i accR_t};
+//    accR_t = D_t - qz_t / 250 with the angle sum D wrapped in float32 and
+//    qz_t = 7kt mod 250 an exact integer counter;
 //  * synthesis without inverse transforms: with Q_t = sum_{t' <= t} Z_t' (a
 //    prefix per bin) and G(t, s) = Re sum_k c_k e^{2 pi i k (7t + s)/250} Q_t[k],
 //    s < 7, the overlap-added istft sample p = 7t + r is
@@ -1615,7 +1617,6 @@ ps_vocoder_kernel(PitchArgs a) {
     esi[r >> 1][r & 1] = -ev.y;
   }
   const bool b3 = lane & 8;
-  const double kadv = static_cast<double>(7 * k) / kPsFft;  // the phase advance, in revolutions
   // direct DFT (float64) of the frame staged in C.xs: frame 0, and every
   // kPvRestart frames a restart of the sliding DFT (its float32 increments'
   // rounding then accumulates over at most kPvRestart frames)
@@ -1692,7 +1693,13 @@ ps_vocoder_kernel(PitchArgs a) {
     polar(pa, pm);
   }
   int c = 0;
-  double accR = static_cast<double>(ca) * (0.5 / M_PI);
+  // The accumulated phase (revolutions) at frame t is accR_t = D_t - t * 7k / 250
+  // (mod 1), D_t = ca_0 / 2 pi + the sum of the steps' angle differences / 2 pi.
+  // D is kept wrapped to [-1/2, 1/2] in float32 (each addition rounds by at most
+  // 2^-25: a random walk), and t * 7k / 250 mod 1 = qz_t / 250 comes from the
+  // integer counter qz exactly, so no float32 bias accumulates over the frames.
+  float D = ca * static_cast<float>(0.5 / M_PI);
+  D -= rintf(D);
   cf Q = {0.f, 0.f};
   int qz = 0;
   const int dq = q7;
@@ -1772,13 +1779,12 @@ ps_vocoder_kernel(PitchArgs a) {
         float qa, qm;
         polar_of(nre, nim, qa, qm);
         const float m = fmaf(al, nm - cm, cm);
-        const double fr = accR - rint(accR);
-        const float frf = static_cast<float>(fr);
+        float frf = fmaf(static_cast<float>(qz), -1.f / kPsFft, D);  // accR_t = D_t - qz_t / 250
+        frf -= rintf(frf);
         const float sn = __builtin_amdgcn_sinf(frf), cs = __builtin_amdgcn_cosf(frf);
         Q += cf{m * cs, m * sn};
-        double inc = (static_cast<double>(na) - static_cast<double>(ca)) * (0.5 / M_PI) - kadv;
-        inc -= rint(inc);
-        accR += inc;
+        D = fmaf(na - ca, static_cast<float>(0.5 / M_PI), D);
+        D -= rintf(D);
         xre = step ? nre : xre;
         xim = step ? nim : xim;
         cnt = step ? ncnt : cnt;
