@@ -84,6 +84,10 @@ def parse():
                     help="config 5 at N > 1: the reference's batch of 1,100 per rank (weak: global batch "
                          "1,100 N, 1,000 steps per rank) or split over the ranks (global batch 1,100, "
                          "N x 1,000 steps per rank)")
+    ap.add_argument("--embed-split", type=int, default=2,
+                    help="config 5, pipelined: the embedding's first K fused chains run on the featurize stream, "
+                         "the rest (and the NaN replacement) on the train stream after its steps "
+                         "(hbk_embed_clips_front / _back; 0: the whole embedding on the featurize stream)")
     ap.add_argument("--stage-steps", type=int, default=2,
                     help="overlapped runs: sequential (untimed) steps that time the stages for the rooflines")
     ap.add_argument("--pmc", default=None,
@@ -675,17 +679,37 @@ def setup_e2e(args, dev, rank, world, seed):
             e.record(stream)
             return e
 
+        # --embed-split K: the partitions are unbalanced (featurize ~127 ms on 192 CUs,
+        # train ~93 ms on 64 at split:64), so the embedding's last chains of chunk c + 1
+        # run on the train stream after train(c): its front half writes mid[b] on the
+        # feature stream, its back half reads it on the train stream
+        K = args.embed_split if 0 < args.embed_split < eplan.n_chains else 0
+        mids = [torch.empty((n, eplan.mid_floats(K)), dtype=torch.float32, device=dev) for _ in range(2)] if K else []
+        front_done = [torch.cuda.Event(), torch.cuda.Event()]
+
         def featurize(c):
             b = c % 2
             with torch.cuda.stream(fs):
-                fs.wait_event(train_done[b])  # train(c - 2) has finished reading pools[b]
+                fs.wait_event(train_done[b])  # train(c - 2) has finished reading pools[b] (and back(c - 2) mids[b])
                 e0 = mark("featurize", fs)
                 x = aug.augment_device(src, lens)
                 frames = mel_frames(x, mplan, N_FRAMES)
-                replace_nan_rows_device(embed_clips(frames, eplan, out=raw), out=pools[b])
-                feat_done[b].record(fs)
+                if K:
+                    eplan.clips_front(frames, K, mids[b])
+                    front_done[b].record(fs)
+                else:
+                    replace_nan_rows_device(embed_clips(frames, eplan, out=raw), out=pools[b])
+                    feat_done[b].record(fs)
                 if part is not None:
                     part.append(("featurize", e0, mark("featurize", fs)))
+
+        def featurize_back(c):
+            """Chunk c's embedding back half + NaN replacement on the train stream."""
+            b = c % 2
+            with torch.cuda.stream(ts):
+                ts.wait_event(front_done[b])
+                replace_nan_rows_device(eplan.clips_back(mids[b], n, K, raw), out=pools[b])
+                feat_done[b].record(ts)
 
         def step(evs):  # noqa: F811
             # chunk c+1 is featurized while chunk c trains; its work is queued
@@ -695,6 +719,8 @@ def setup_e2e(args, dev, rank, world, seed):
             count[0] += 1
             if c == 0:
                 featurize(0)  # pipeline fill (first warmup step)
+                if K:
+                    featurize_back(0)
             h0 = time.perf_counter()
             featurize(c + 1)
             h1 = time.perf_counter()
@@ -706,8 +732,10 @@ def setup_e2e(args, dev, rank, world, seed):
                 tr._reset_accumulation()
                 tr.train_indexed(idx, y, sched, pool32=pools[b], pool16=neg, history=hist, steps_per_graph=50)
                 train_done[b].record(ts)
-                if part is not None:
-                    part.append(("train", e0, mark("train", ts)))
+            if K:
+                featurize_back(c + 1)
+            if part is not None:
+                part.append(("train", e0, mark("train", ts)))
             if host_log:
                 print("host ms: featurize enqueue %.1f, train enqueue %.1f" % (
                     1e3 * (h1 - h0), 1e3 * (time.perf_counter() - h1)), file=sys.stderr, flush=True)
@@ -898,7 +926,10 @@ def setup_e2e(args, dev, rank, world, seed):
                    "parallelism": f"dp{world} (clip shards; 1 all-reduce of the 1,025,700-B bucket per train step)",
                    "schedule": ("sequential: featurize(s) then train(s)" if args.overlap == "off" else
                                 f"pipelined (heybuddy.pipeline {args.overlap}): featurize(s + 1) on one stream while "
-                                f"train(s) runs on another; per-stage ms from {args.stage_steps} sequential steps")},
+                                f"train(s) runs on another"
+                                + (f", then the embedding's chains >= {args.embed_split} of chunk s + 1 on the train "
+                                   "stream (hbk_embed_clips_back)" if args.embed_split > 0 else "")
+                                + f"; per-stage ms from {args.stage_steps} sequential steps")},
     }
 
 

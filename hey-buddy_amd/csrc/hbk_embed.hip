@@ -3240,20 +3240,28 @@ __global__ void __launch_bounds__(256) embed_gather_kernel(const float* __restri
   }
 }
 
+// Runs chains [k_begin, k_end) of the program (k_end < 0: to the end). The
+// first chain run reads `in` (the call's input, or for k_begin > 0 the output
+// of chain k_begin - 1 in its workspace layout); the last writes `out` (for
+// k_end < n: chain k_end - 1's output in its workspace layout, no gather).
 int run_program(const Program& prog, const float* in, int64_t n_units, int64_t in_unit_stride,
                 float* out, int64_t out_unit_floats, float* ws, int64_t chunk, hipStream_t stream,
                 const std::vector<int64_t>& imgs_per_unit, const std::vector<int64_t>& buf_unit_floats,
-                int* range_flag) {
+                int* range_flag, int k_begin = 0, int k_end = -1) {
+  const int n_ch = static_cast<int>(prog.chains.size());
+  if (k_end < 0) k_end = n_ch;
   for (int64_t u0 = 0; u0 < n_units; u0 += chunk) {
     const int64_t nu = std::min(chunk, n_units - u0);
     float* bufs[2] = {ws, ws + chunk * buf_unit_floats[0]};
-    for (size_t k = 0; k < prog.chains.size(); ++k) {
-      const ChainPlan& c = prog.chains[k];
+    for (int k = k_begin; k < k_end; ++k) {
+      ChainPlan c = prog.chains[k];
+      if (k == k_begin && k_begin > 0) c.src_buf = -1;  // the caller's copy of chain k - 1's output
+      if (k == k_end - 1 && k_end < n_ch) c.dst_buf = -1;  // handed to the caller (no gather)
       if (c.p0fn) {
         P0Args pa = c.p0;
         pa.range_flag = range_flag;
         pa.in = c.src_buf < 0 ? in + u0 * in_unit_stride : bufs[c.src_buf];
-        pa.src_img_stride = c.src_buf < 0 ? in_unit_stride : c.x.src_clip_stride;
+        pa.src_img_stride = c.src_buf < 0 ? in_unit_stride : c.x.src_clip_stride;  // (in_unit_stride == it past chain 0)
         pa.out = c.dst_buf < 0 ? out + u0 * out_unit_floats : bufs[c.dst_buf];
         pa.n_img = nu * imgs_per_unit[k];
         const bool aligned = !(reinterpret_cast<uintptr_t>(pa.in) & 15) && !(pa.src_img_stride & 3) &&
@@ -3271,7 +3279,7 @@ int run_program(const Program& prog, const float* in, int64_t n_units, int64_t i
         P1Args pa = c.p1;
         pa.range_flag = range_flag;
         pa.in = c.src_buf < 0 ? in + u0 * in_unit_stride : bufs[c.src_buf];
-        pa.src_img_stride = c.src_buf < 0 ? in_unit_stride : c.x.src_clip_stride;
+        pa.src_img_stride = c.src_buf < 0 ? in_unit_stride : c.x.src_clip_stride;  // (in_unit_stride == it past chain 0)
         pa.out = c.dst_buf < 0 ? out + u0 * out_unit_floats : bufs[c.dst_buf];
         pa.n_img = nu * imgs_per_unit[k];
         const bool aligned = !(reinterpret_cast<uintptr_t>(pa.in) & 15) && !(pa.src_img_stride & 3) &&
@@ -3289,7 +3297,7 @@ int run_program(const Program& prog, const float* in, int64_t n_units, int64_t i
         P2sArgs pa = c.p2;
         pa.range_flag = range_flag;
         pa.in = c.src_buf < 0 ? in + u0 * in_unit_stride : bufs[c.src_buf];
-        pa.src_img_stride = c.src_buf < 0 ? in_unit_stride : c.x.src_clip_stride;
+        pa.src_img_stride = c.src_buf < 0 ? in_unit_stride : c.x.src_clip_stride;  // (in_unit_stride == it past chain 0)
         pa.out = c.dst_buf < 0 ? out + u0 * out_unit_floats : bufs[c.dst_buf];
         pa.n_img = nu * imgs_per_unit[k];
         const bool aligned = !(reinterpret_cast<uintptr_t>(pa.in) & 15) && !(pa.src_img_stride & 3) &&
@@ -3340,7 +3348,7 @@ int run_program(const Program& prog, const float* in, int64_t n_units, int64_t i
       hipLaunchKernelGGL(c.fn, dim3(unsigned(blocks)), dim3(kThreads), c.lds_bytes, stream, a);
       HBK_LAUNCH_CHECK("conv_chain_kernel");
     }
-    if (prog.gather_buf >= 0) {
+    if (prog.gather_buf >= 0 && k_end == n_ch) {
       const int n_out = static_cast<int>(prog.gather_src.size());
       const int row = static_cast<int>(out_unit_floats / n_out);
       hipLaunchKernelGGL(embed_gather_kernel, dim3(unsigned((nu + 3) / 4)), dim3(256), 0, stream,
@@ -3631,6 +3639,57 @@ int hbk_embed_clips(const hbk_embed_plan* p, const float* mel, int64_t n_clips, 
   return run_program(p->clip_prog, mel, n_clips, mel_clip_stride, out,
                      int64_t(p->starts.size()) * p->out_dim, static_cast<float*>(workspace), chunk,
                      as_stream(stream), imgs, bufs, p->d_range);
+}
+
+int hbk_embed_split_info(const hbk_embed_plan* p, int32_t n_front, int64_t* mid_floats_per_clip) {
+  using namespace hbk;
+  if (!p || !mid_floats_per_clip) return arg_error("plan/mid_floats_per_clip is NULL");
+  const int n = static_cast<int>(p->clip_prog.chains.size());
+  if (n_front < 1 || n_front >= n) return arg_error("n_front must be in [1, n_chains - 1]");
+  std::vector<int64_t> imgs, bufs;
+  program_geometry(p->clip_prog, true, int(p->starts.size()), imgs, bufs);
+  const ChainPlan& c = p->clip_prog.chains[n_front - 1];
+  *mid_floats_per_clip = (c.split ? c.x.out_img_stride : c.args.out_img_stride) * imgs[n_front - 1];
+  return HBK_OK;
+}
+
+int hbk_embed_clips_front(const hbk_embed_plan* p, const float* mel, int64_t n_clips, int64_t mel_clip_stride,
+                          int32_t n_front, float* mid, void* workspace, int64_t workspace_bytes, void* stream) {
+  using namespace hbk;
+  int64_t mid_floats = 0;
+  int rc = hbk_embed_split_info(p, n_front, &mid_floats);
+  if (rc) return rc;
+  if (n_clips < 0) return arg_error("negative n_clips");
+  if (n_clips == 0) return HBK_OK;
+  if (!mel || !mid || !workspace) return arg_error("NULL pointer");
+  if (mel_clip_stride < int64_t(p->seq_frames) * p->in_w) return arg_error("mel_clip_stride < seq_frames * in_w");
+  int64_t need = 0;
+  hbk_embed_workspace_size(p, n_clips, &need);
+  if (workspace_bytes < need) return arg_error("workspace too small");
+  std::vector<int64_t> imgs, bufs;
+  program_geometry(p->clip_prog, true, int(p->starts.size()), imgs, bufs);
+  const int64_t chunk = std::min<int64_t>(n_clips, kChunkClips);
+  return run_program(p->clip_prog, mel, n_clips, mel_clip_stride, mid, mid_floats, static_cast<float*>(workspace),
+                     chunk, as_stream(stream), imgs, bufs, p->d_range, 0, n_front);
+}
+
+int hbk_embed_clips_back(const hbk_embed_plan* p, const float* mid, int64_t n_clips, int32_t n_front, float* out,
+                         void* workspace, int64_t workspace_bytes, void* stream) {
+  using namespace hbk;
+  int64_t mid_floats = 0;
+  int rc = hbk_embed_split_info(p, n_front, &mid_floats);
+  if (rc) return rc;
+  if (n_clips < 0) return arg_error("negative n_clips");
+  if (n_clips == 0) return HBK_OK;
+  if (!mid || !out || !workspace) return arg_error("NULL pointer");
+  int64_t need = 0;
+  hbk_embed_workspace_size(p, n_clips, &need);
+  if (workspace_bytes < need) return arg_error("workspace too small");
+  std::vector<int64_t> imgs, bufs;
+  program_geometry(p->clip_prog, true, int(p->starts.size()), imgs, bufs);
+  const int64_t chunk = std::min<int64_t>(n_clips, kChunkClips);
+  return run_program(p->clip_prog, mid, n_clips, mid_floats, out, int64_t(p->starts.size()) * p->out_dim,
+                     static_cast<float*>(workspace), chunk, as_stream(stream), imgs, bufs, p->d_range, n_front, -1);
 }
 
 int hbk_embed_windows(const hbk_embed_plan* p, const float* windows, int64_t n, float* out,

@@ -204,13 +204,47 @@ class EmbedPlan:
         """Algorithmic MACs of the clip path (shared prefix + per-window tail)."""
         return self.prefix_macs_per_clip + len(self.starts) * self.tail_macs_per_window
 
-    def workspace(self, n: int) -> torch.Tensor:
+    def workspace(self, n: int, slot: int = 0) -> torch.Tensor:
+        """The plan's workspace for n clips; slot 1 is a second one, for the
+        back half of a split call running beside a front half (clips_back)."""
         need = ctypes.c_int64()
         check(lib().hbk_embed_workspace_size(self._handle, int(n), ctypes.byref(need)),
               "hbk_embed_workspace_size")
-        if self._ws is None or self._ws.numel() < need.value:
-            self._ws = torch.empty(need.value, dtype=torch.uint8, device=self.device)
-        return self._ws
+        attr = "_ws" if slot == 0 else "_ws_back"
+        ws = getattr(self, attr, None)
+        if ws is None or ws.numel() < need.value:
+            ws = torch.empty(need.value, dtype=torch.uint8, device=self.device)
+            setattr(self, attr, ws)
+        return ws
+
+    def mid_floats(self, n_front: int) -> int:
+        """Floats per clip of the front half's output (hbk_embed_split_info)."""
+        v = ctypes.c_int64()
+        check(lib().hbk_embed_split_info(self._handle, int(n_front), ctypes.byref(v)), "hbk_embed_split_info")
+        return v.value
+
+    def clips_front(self, mel: torch.Tensor, n_front: int, mid: torch.Tensor) -> torch.Tensor:
+        """The first n_front fused chains of the clip path (hbk_embed_clips_front)
+        on the current stream: mel [B, F, n_mels] -> mid [B, mid_floats(n_front)]."""
+        n = mel.shape[0]
+        if not (mel.is_cuda and mel.dtype == torch.float32 and mel.stride(-1) == 1 and mid.is_contiguous()
+                and mid.dtype == torch.float32 and mid.numel() >= n * self.mid_floats(n_front)):
+            raise ValueError("clips_front: bad mel / mid tensors")
+        ws = self.workspace(n)
+        check(lib().hbk_embed_clips_front(self._handle, ptr(mel), n, mel.stride(0), int(n_front), ptr(mid), ptr(ws),
+                                          ws.numel(), stream_ptr(mel.device)), "hbk_embed_clips_front")
+        return mid
+
+    def clips_back(self, mid: torch.Tensor, n: int, n_front: int, out: torch.Tensor) -> torch.Tensor:
+        """The remaining chains (hbk_embed_clips_back) on the current stream, with
+        the plan's second workspace: mid -> out [n, n_windows, out_dim]."""
+        if not (mid.is_cuda and mid.is_contiguous() and out.is_contiguous() and out.dtype == torch.float32
+                and out.shape == (n, len(self.starts), self.out_dim)):
+            raise ValueError("clips_back: bad mid / out tensors")
+        ws = self.workspace(n, slot=1)
+        check(lib().hbk_embed_clips_back(self._handle, ptr(mid), n, int(n_front), ptr(out), ptr(ws), ws.numel(),
+                                         stream_ptr(mid.device)), "hbk_embed_clips_back")
+        return out
 
     def clips(self, mel: torch.Tensor) -> torch.Tensor:
         return embed_clips(mel, self)

@@ -155,6 +155,21 @@ int hbk_embed_clips(const hbk_embed_plan* plan, const float* mel, int64_t n_clip
                     int64_t mel_clip_stride, float* out, void* workspace,
                     int64_t workspace_bytes, void* stream);
 
+/* hbk_embed_clips in two calls on two streams (no reference counterpart: a
+ * scheduling split, e.g. the tail of featurisation on the training stream's
+ * CUs). The front runs the clip program's first n_front fused chains
+ * (1 <= n_front < n_chains) and writes chain n_front - 1's output to mid
+ * ([n_clips, mid_floats_per_clip] f32, hbk_embed_split_info); the back runs
+ * the remaining chains from mid into out. Front + back == hbk_embed_clips.
+ * Each call needs its own workspace (hbk_embed_workspace_size) when the two
+ * can run concurrently. */
+int hbk_embed_split_info(const hbk_embed_plan* plan, int32_t n_front, int64_t* mid_floats_per_clip);
+int hbk_embed_clips_front(const hbk_embed_plan* plan, const float* mel, int64_t n_clips,
+                          int64_t mel_clip_stride, int32_t n_front, float* mid, void* workspace,
+                          int64_t workspace_bytes, void* stream);
+int hbk_embed_clips_back(const hbk_embed_plan* plan, const float* mid, int64_t n_clips, int32_t n_front,
+                         float* out, void* workspace, int64_t workspace_bytes, void* stream);
+
 /* Per-window API of the reference: windows [n, in_h, in_w] f32 -> out [n, out_dim]. */
 int hbk_embed_windows(const hbk_embed_plan* plan, const float* windows, int64_t n, float* out,
                       void* workspace, int64_t workspace_bytes, void* stream);

@@ -306,3 +306,30 @@ def test_embed_split_range_guard():
     with pytest.raises(HBKError, match="65504"):
         EmbedPlan(g_big, precision="split")
     EmbedPlan(g_big, precision="exact")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_front", [1, 2, 3])
+def test_embed_clips_front_back_split(n_front):
+    """hbk_embed_clips_front + hbk_embed_clips_back (the scheduling split the
+    pipelined bench uses: the last chains on the training stream) equal
+    hbk_embed_clips bit for bit, at every split point of SE20's clip program,
+    each half on its own stream and workspace."""
+    from heybuddy.embedding_graph import se20_graph
+    from heybuddy.kernels import EmbedPlan
+    plan = EmbedPlan(se20_graph(), precision="split")
+    assert 1 <= n_front < plan.n_chains
+    mel = torch.from_numpy(_mel_clips(9, seed=5)).cuda()
+    ref = plan.clips(mel)
+    mid = torch.empty((9, plan.mid_floats(n_front)), device="cuda")
+    out = torch.empty_like(ref)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    s1.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s1):
+        plan.clips_front(mel, n_front, mid)
+    s2.wait_stream(s1)
+    with torch.cuda.stream(s2):
+        plan.clips_back(mid, 9, n_front, out)
+    torch.cuda.current_stream().wait_stream(s2)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
