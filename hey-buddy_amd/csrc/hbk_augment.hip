@@ -1395,11 +1395,14 @@ __global__ void __launch_bounds__(64) eq_kernel(EqArgs a) {
 //    direct float64 DFT restarts it every kPvRestart frames. A frame whose 250
 //    samples are all zero is exactly 0 (angle 0) as in the FFT (a running
 //    count of non-zero samples);
-//  * vocoder: the phase in revolutions, accR_{t+1} = accR_t + (a1 - a0) / 2 pi
-//    - 7k/250 (mod 1): the phase advance adv_k = 2 pi 7k/250 cancels against the
-//    istft's frame rotation, so Z_t = Y_t e^{-2 pi i 7kt/250} = m_t e^{2 pi i accR_t};
-//    accR_t = D_t - qz_t / 250 with the angle sum D wrapped in float32 and
-//    qz_t = 7kt mod 250 an exact integer counter;
+//  * vocoder without angles: the accumulated phase e^{i phi_t} is kept as a unit
+//    complex P_t = u_0 prod (u_{i0+1} conj u_{i0}) of the frames' unit vectors
+//    u = X / |X| (u = 1 for X = 0, angle 0 as in torch), since
+//    e^{i (angle(X1) - angle(X0))} = u_1 conj u_0 whatever 2 pi wrap the
+//    reference applies; the phase advance 2 pi 7k/250 cancels against the istft's
+//    frame rotation, so Z_t = Y_t e^{-2 pi i 7kt/250} = m_t P_t e^{-2 pi i qz_t/250}
+//    with qz_t = 7kt mod 250 an exact integer counter (no atan2, no sin / cos;
+//    P is renormalised once per frame group);
 //  * synthesis without inverse transforms: with Q_t = sum_{t' <= t} Z_t' (a
 //    prefix per bin) and G(t, s) = Re sum_k c_k e^{2 pi i k (7t + s)/250} Q_t[k],
 //    s < 7, the overlap-added istft sample p = 7t + r is
@@ -1452,28 +1455,6 @@ __device__ __forceinline__ int ps_i0(const PitchArgs& a, int t, float& alpha) {
   const float fl = floorf(ts);
   alpha = ts - fl;
   return static_cast<int>(fl);
-}
-
-// atan2 for the vocoder's angles: a degree-15 odd polynomial for atan on [0, 1]
-// (least-squares fit, max error 1.2e-7 rad in float32, as libm's atan2f) and
-// the octant reflections; atan2(0, 0) = 0 as in torch
-__device__ __forceinline__ float ps_atan2(float y, float x) {
-  const float ax = fabsf(x), ay = fabsf(y);
-  const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
-  const float a = mx > 0.f ? mn * __builtin_amdgcn_rcpf(mx) : 0.f;
-  const float s = a * a;
-  float r = -0.004051558673381805f;
-  r = fmaf(r, s, 0.021852469071745872f);
-  r = fmaf(r, s, -0.05589785426855087f);
-  r = fmaf(r, s, 0.09641194343566895f);
-  r = fmaf(r, s, -0.1390826404094696f);
-  r = fmaf(r, s, 0.19946499168872833f);
-  r = fmaf(r, s, -0.33329856395721436f);
-  r = fmaf(r, s, 0.9999993443489075f);
-  r *= a;
-  r = ay > ax ? 1.5707963267948966f - r : r;
-  r = x < 0.f ? 3.141592653589793f - r : r;
-  return copysignf(r, y);
 }
 
 struct PvClip {
@@ -1673,14 +1654,19 @@ ps_vocoder_kernel(PitchArgs a) {
     cnt = ncnt;
     ++sf;
   };
-  auto polar_of = [&](double re, double im, float& ang, float& mag) {
+  // unit vector and magnitude of a frame's bin (X = 0: u = 1, |X| = 0)
+  auto polar_of = [&](double re, double im, cf& u, float& mag) {
     const float fr = static_cast<float>(re), fi = static_cast<float>(im);
-    ang = ps_atan2(fi, fr);
-    mag = __builtin_amdgcn_sqrtf(fmaf(fr, fr, fi * fi));  // v_sqrt_f32 (1 ulp), no denormal scaling
+    const float n2 = fmaf(fr, fr, fi * fi);
+    const float rs = __builtin_amdgcn_rsqf(n2);  // v_rsq_f32 (1 ulp)
+    const bool nz = n2 > 0.f;
+    u = nz ? cf{fr, fi} * rs : cf{1.f, 0.f};
+    mag = nz ? n2 * rs : 0.f;
   };
-  auto polar = [&](float& ang, float& mag) { polar_of(xre, xim, ang, mag); };
+  auto polar = [&](cf& u, float& mag) { polar_of(xre, xim, u, mag); };
   // frames c, c + 1 in (ca, cm), (na, nm); frame c + 2 = sf ahead in (pa, pm)
-  float ca, cm, na, nm, pa, pm;
+  cf ca, na, pa;
+  float cm, nm, pm;
   polar(ca, cm);
   {
     double nre, nim;
@@ -1693,13 +1679,11 @@ ps_vocoder_kernel(PitchArgs a) {
     polar(pa, pm);
   }
   int c = 0;
-  // The accumulated phase (revolutions) at frame t is accR_t = D_t - t * 7k / 250
-  // (mod 1), D_t = ca_0 / 2 pi + the sum of the steps' angle differences / 2 pi.
-  // D is kept wrapped to [-1/2, 1/2] in float32 (each addition rounds by at most
-  // 2^-25: a random walk), and t * 7k / 250 mod 1 = qz_t / 250 comes from the
-  // integer counter qz exactly, so no float32 bias accumulates over the frames.
-  float D = ca * static_cast<float>(0.5 / M_PI);
-  D -= rintf(D);
+  // The accumulated phase at frame t is e^{i phi_t} = P_t e^{-2 pi i qz_t / 250}:
+  // P_0 = u_0, then P <- P u_n conj u_c after each output frame (the float32
+  // products' rounding is a random walk; |P| is reset to 1 once per group), and
+  // t * 7k / 250 mod 1 = qz_t / 250 comes from the integer counter qz exactly.
+  cf P = ca;
   cf Q = {0.f, 0.f};
   int qz = 0;
   const int dq = q7;
@@ -1729,17 +1713,19 @@ ps_vocoder_kernel(PitchArgs a) {
       anchor = sf;
     }
     HBK_PVT(1);  // row refills, restarts
+    P *= __builtin_amdgcn_rsqf(fmaf(P.x, P.x, P.y * P.y));
     float gr[kPvGroup];  // frame u: G(t0 + u, pv_g(lane & 7)) over the lane's octet
     float al_lane = 0.f;  // full groups: the alpha of frame t0 + (lane & 7)
     // one output frame; FULL: t < f_out and i0(t) = c + 1 are known for the whole group
     auto frame = [&](int u, auto full) {
       constexpr bool FULL = decltype(full)::value;
       const int t = t0 + u;
+      const cf tz = sh.tw[qz];  // e^{+2 pi i qz / 250}
 #if HBK_PV_ABLATE & 2  // profiling build: the per-bin vocoder replaced by a stand-in
       if (t < a.f_out) {
         float al;
         ps_i0(a, t, al);
-        Q.x += al;
+        Q.x += al * tz.x;
       }
       if (false) {
 #else
@@ -1776,15 +1762,12 @@ ps_vocoder_kernel(PitchArgs a) {
         double nre, nim;
         int ncnt;
         slide_to(nre, nim, ncnt);  // candidate frame sf + 1 and its polar form, kept only when stepping
-        float qa, qm;
+        cf qa;
+        float qm;
         polar_of(nre, nim, qa, qm);
         const float m = fmaf(al, nm - cm, cm);
-        float frf = fmaf(static_cast<float>(qz), -1.f / kPsFft, D);  // accR_t = D_t - qz_t / 250
-        frf -= rintf(frf);
-        const float sn = __builtin_amdgcn_sinf(frf), cs = __builtin_amdgcn_cosf(frf);
-        Q += cf{m * cs, m * sn};
-        D = fmaf(na - ca, static_cast<float>(0.5 / M_PI), D);
-        D -= rintf(D);
+        Q = __builtin_elementwise_fma(cf{m, m}, cmul_conj(P, tz), Q);  // Z_t = m P e^{-2 pi i qz / 250}
+        P = cmul(P, cmul_conj(na, ca));
         xre = step ? nre : xre;
         xim = step ? nim : xim;
         cnt = step ? ncnt : cnt;
@@ -1794,7 +1777,7 @@ ps_vocoder_kernel(PitchArgs a) {
       }
       // G(t, .) over the wave's bins: 7 products, reduce-scatter over the lane octet,
       // all-reduce over the 8 octets
-      const cf vq = cmul(Q, sh.tw[qz]);
+      const cf vq = cmul(Q, tz);
 #if HBK_PV_ABLATE & 1  // profiling build: no bin reduction
       gr[u] = vq.x * esr[u & 3].x;
 #else

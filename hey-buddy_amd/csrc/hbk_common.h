@@ -57,6 +57,11 @@ __device__ __forceinline__ cf cmul(cf a, cf b) {
 // max that propagates NaN (torch / numpy max-pool semantics; fmaxf drops NaN)
 __device__ __forceinline__ float nan_max(float a, float b) { return (b > a || b != b) ? b : a; }
 
+// a conj(b) = a.x (b.x, -b.y) + a.y (b.y, b.x)
+__device__ __forceinline__ cf cmul_conj(cf a, cf b) {
+  return __builtin_elementwise_fma(cf{a.y, a.y}, cf{b.y, b.x}, cf{a.x, a.x} * cf{b.x, -b.y});
+}
+
 // multiply by -i
 __device__ __forceinline__ cf cmul_mi(cf a) { return cf{a.y, -a.x}; }
 
