@@ -1399,10 +1399,13 @@ __global__ void __launch_bounds__(64) eq_kernel(EqArgs a) {
 //    complex P_t = u_0 prod (u_{i0+1} conj u_{i0}) of the frames' unit vectors
 //    u = X / |X| (u = 1 for X = 0, angle 0 as in torch), since
 //    e^{i (angle(X1) - angle(X0))} = u_1 conj u_0 whatever 2 pi wrap the
-//    reference applies; the phase advance 2 pi 7k/250 cancels against the istft's
-//    frame rotation, so Z_t = Y_t e^{-2 pi i 7kt/250} = m_t P_t e^{-2 pi i qz_t/250}
-//    with qz_t = 7kt mod 250 an exact integer counter (no atan2, no sin / cos;
-//    P is renormalised once per frame group);
+//    reference applies. The product telescopes while the source frame steps by
+//    one: P_t = R u_{i0(t)} with R constant, changed only by a repeated source
+//    frame (R *= u_{i0+1} conj u_{i0}) or a double step. The phase advance
+//    2 pi 7k/250 cancels against the istft's frame rotation, so
+//    Z_t = Y_t e^{-2 pi i 7kt/250} = m_t P_t e^{-2 pi i qz_t/250} with
+//    qz_t = 7kt mod 250 an exact integer counter (no atan2, no sin / cos; R is
+//    renormalised once per frame group);
 //  * synthesis without inverse transforms: with Q_t = sum_{t' <= t} Z_t' (a
 //    prefix per bin) and G(t, s) = Re sum_k c_k e^{2 pi i k (7t + s)/250} Q_t[k],
 //    s < 7, the overlap-added istft sample p = 7t + r is
@@ -1465,6 +1468,7 @@ struct PvClip {
 };
 struct PvShared {
   cf tw[256];                 // e^{+2 pi i q / 250}
+  float4 tw4[256];            // (x, y, -y, x) of tw[q]: complex products by tw[q] or its conjugate without negations
   double tw64[256][2];        // e^{-2 pi i q / 250}, float64
   float4 wt[3][128];          // w^j, w^{j+1} (j = 1, 3, 5) of bin lane, lane-major (one ds_read_b128 per wave)
   PvClip c[kPvClips];
@@ -1560,6 +1564,7 @@ ps_vocoder_kernel(PitchArgs a) {
     double sn, cs;
     sincospi(2.0 * q / kPsFft, &sn, &cs);
     sh.tw[q] = cf{static_cast<float>(cs), static_cast<float>(sn)};
+    sh.tw4[q] = float4{static_cast<float>(cs), static_cast<float>(sn), -static_cast<float>(sn), static_cast<float>(cs)};
     sh.tw64[q][0] = cs;
     sh.tw64[q][1] = -sn;
   }
@@ -1679,11 +1684,12 @@ ps_vocoder_kernel(PitchArgs a) {
     polar(pa, pm);
   }
   int c = 0;
-  // The accumulated phase at frame t is e^{i phi_t} = P_t e^{-2 pi i qz_t / 250}:
-  // P_0 = u_0, then P <- P u_n conj u_c after each output frame (the float32
-  // products' rounding is a random walk; |P| is reset to 1 once per group), and
-  // t * 7k / 250 mod 1 = qz_t / 250 comes from the integer counter qz exactly.
-  cf P = ca;
+  // The accumulated phase at frame t is e^{i phi_t} = P_t e^{-2 pi i qz_t / 250} with
+  // P_t = R u_c (P_0 = u_0: R = 1); R changes only when the source frame repeats or
+  // double-steps (the float32 products' rounding is a random walk; |R| is reset to 1
+  // once per group), and t * 7k / 250 mod 1 = qz_t / 250 comes from the integer
+  // counter qz exactly.
+  cf R = {1.f, 0.f};
   cf Q = {0.f, 0.f};
   int qz = 0;
   const int dq = q7;
@@ -1713,14 +1719,14 @@ ps_vocoder_kernel(PitchArgs a) {
       anchor = sf;
     }
     HBK_PVT(1);  // row refills, restarts
-    P *= __builtin_amdgcn_rsqf(fmaf(P.x, P.x, P.y * P.y));
+    R *= __builtin_amdgcn_rsqf(fmaf(R.x, R.x, R.y * R.y));
     float gr[kPvGroup];  // frame u: G(t0 + u, pv_g(lane & 7)) over the lane's octet
     float al_lane = 0.f;  // full groups: the alpha of frame t0 + (lane & 7)
     // one output frame; FULL: t < f_out and i0(t) = c + 1 are known for the whole group
     auto frame = [&](int u, auto full) {
       constexpr bool FULL = decltype(full)::value;
       const int t = t0 + u;
-      const cf tz = sh.tw[qz];  // e^{+2 pi i qz / 250}
+      const float4 tz = sh.tw4[qz];  // e^{+2 pi i qz / 250} as (x, y, -y, x)
 #if HBK_PV_ABLATE & 2  // profiling build: the per-bin vocoder replaced by a stand-in
       if (t < a.f_out) {
         float al;
@@ -1745,6 +1751,7 @@ ps_vocoder_kernel(PitchArgs a) {
           cm = nm;
           na = pa;
           nm = pm;
+          R = cmul(R, cmul_conj(ca, na));  // P_t = P_{t-1} u_{c+1} conj u_c = R u_{c+1}, and c + 2 becomes the frame
           double nre, nim;
           int ncnt;
           slide_to(nre, nim, ncnt);
@@ -1754,6 +1761,7 @@ ps_vocoder_kernel(PitchArgs a) {
         // the common step (i0 = c + 1): in a FULL group every frame steps (the source
         // frames rename through the unrolled frames: no selects), elsewhere selects
         const bool step = FULL || i0 > c;
+        if (!FULL && !step && t > 0) R = cmul(R, cmul_conj(na, ca));  // the source frame repeats (uniform)
         c += step ? 1 : 0;
         ca = step ? na : ca;
         cm = step ? nm : cm;
@@ -1766,8 +1774,10 @@ ps_vocoder_kernel(PitchArgs a) {
         float qm;
         polar_of(nre, nim, qa, qm);
         const float m = fmaf(al, nm - cm, cm);
-        Q = __builtin_elementwise_fma(cf{m, m}, cmul_conj(P, tz), Q);  // Z_t = m P e^{-2 pi i qz / 250}
-        P = cmul(P, cmul_conj(na, ca));
+        const cf P = cmul(R, ca);
+        // Z_t = m P e^{-2 pi i qz / 250} = m (P.x (x, -y) + P.y (y, x))
+        const cf Z = __builtin_elementwise_fma(cf{P.y, P.y}, cf{tz.y, tz.x}, cf{P.x, P.x} * cf{tz.w, tz.z});
+        Q = __builtin_elementwise_fma(cf{m, m}, Z, Q);
         xre = step ? nre : xre;
         xim = step ? nim : xim;
         cnt = step ? ncnt : cnt;
@@ -1777,7 +1787,7 @@ ps_vocoder_kernel(PitchArgs a) {
       }
       // G(t, .) over the wave's bins: 7 products, reduce-scatter over the lane octet,
       // all-reduce over the 8 octets
-      const cf vq = cmul(Q, tz);
+      const cf vq = __builtin_elementwise_fma(cf{Q.y, Q.y}, cf{tz.z, tz.w}, cf{Q.x, Q.x} * cf{tz.x, tz.y});  // Q tw[qz]
 #if HBK_PV_ABLATE & 1  // profiling build: no bin reduction
       gr[u] = vq.x * esr[u & 3].x;
 #else
@@ -1795,7 +1805,6 @@ ps_vocoder_kernel(PitchArgs a) {
         for (int j = 0; j < kPvGroup; ++j) gr[j] = j == u ? gv : gr[j];
       }
 #endif
-      __builtin_amdgcn_sched_barrier(0);  // frames stay in order: the unrolled group would spill
       qz += dq;
       qz -= qz >= kPsFft ? kPsFft : 0;
     };
