@@ -88,6 +88,9 @@ def parse():
                     help="config 5, pipelined: the embedding's first K fused chains run on the featurize stream, "
                          "the rest (and the NaN replacement) on the train stream after its steps "
                          "(hbk_embed_clips_front / _back; 0: the whole embedding on the featurize stream)")
+    ap.add_argument("--embed-split-frac", type=float, default=0.0,
+                    help="with --embed-split K: this fraction of each chunk's clips is split after K - 1 "
+                         "chains instead (a finer balance of the two streams)")
     ap.add_argument("--stage-steps", type=int, default=2,
                     help="overlapped runs: sequential (untimed) steps that time the stages for the rooflines")
     ap.add_argument("--pmc", default=None,
@@ -684,7 +687,13 @@ def setup_e2e(args, dev, rank, world, seed):
         # run on the train stream after train(c): its front half writes mid[b] on the
         # feature stream, its back half reads it on the train stream
         K = args.embed_split if 0 < args.embed_split < eplan.n_chains else 0
-        mids = [torch.empty((n, eplan.mid_floats(K)), dtype=torch.float32, device=dev) for _ in range(2)] if K else []
+        # --embed-split-frac f: clips [0, a1) split after K - 1 chains, the rest after K
+        a1 = int(round(n * args.embed_split_frac)) if K > 1 else 0
+        a1 = min(max(a1, 0), n)
+        mids = [torch.empty((n - a1, eplan.mid_floats(K)), dtype=torch.float32, device=dev)
+                for _ in range(2)] if K else []
+        mids1 = [torch.empty((a1, eplan.mid_floats(K - 1)), dtype=torch.float32, device=dev)
+                 for _ in range(2)] if a1 else []
         front_done = [torch.cuda.Event(), torch.cuda.Event()]
 
         def featurize(c):
@@ -695,7 +704,10 @@ def setup_e2e(args, dev, rank, world, seed):
                 x = aug.augment_device(src, lens)
                 frames = mel_frames(x, mplan, N_FRAMES)
                 if K:
-                    eplan.clips_front(frames, K, mids[b])
+                    if a1:
+                        eplan.clips_front(frames[:a1], K - 1, mids1[b])
+                    if a1 < n:
+                        eplan.clips_front(frames[a1:], K, mids[b])
                     front_done[b].record(fs)
                 else:
                     replace_nan_rows_device(embed_clips(frames, eplan, out=raw), out=pools[b])
@@ -708,7 +720,11 @@ def setup_e2e(args, dev, rank, world, seed):
             b = c % 2
             with torch.cuda.stream(ts):
                 ts.wait_event(front_done[b])
-                replace_nan_rows_device(eplan.clips_back(mids[b], n, K, raw), out=pools[b])
+                if a1:
+                    eplan.clips_back(mids1[b], a1, K - 1, raw[:a1])
+                if a1 < n:
+                    eplan.clips_back(mids[b], n - a1, K, raw[a1:])
+                replace_nan_rows_device(raw, out=pools[b])
                 feat_done[b].record(ts)
 
         def step(evs):  # noqa: F811
@@ -929,6 +945,8 @@ def setup_e2e(args, dev, rank, world, seed):
                                 f"train(s) runs on another"
                                 + (f", then the embedding's chains >= {args.embed_split} of chunk s + 1 on the train "
                                    "stream (hbk_embed_clips_back)" if args.embed_split > 0 else "")
+                                + (f" (chains >= {args.embed_split - 1} for {args.embed_split_frac:.0%} of the clips)"
+                                   if args.embed_split > 1 and args.embed_split_frac > 0 else "")
                                 + f"; per-stage ms from {args.stage_steps} sequential steps")},
     }
 
