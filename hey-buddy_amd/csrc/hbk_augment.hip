@@ -1693,6 +1693,10 @@ ps_vocoder_kernel(PitchArgs a) {
   cf Q = {0.f, 0.f};
   int qz = 0;
   const int dq = q7;
+  // the istft rotation tw[qz] advances by e7 = tw[7k mod 250] per frame: rotated in registers
+  // (tz and i tz), re-read from the table once per group (no drift, no scattered LDS read per frame)
+  const float4 e74 = sh.tw4[q7];
+  const cf e7 = {e74.x, e74.y}, e7r = {e74.z, e74.w};
   const int jmax = (a.l1 + kPsPad - 1) / kPsHop;  // the frame of the last istft sample
   float* y = a.y + static_cast<int64_t>(e) * a.l1;
   HBK_PVT(0);  // init: tables, frame 0, the first rows
@@ -1720,18 +1724,20 @@ ps_vocoder_kernel(PitchArgs a) {
     }
     HBK_PVT(1);  // row refills, restarts
     R *= __builtin_amdgcn_rsqf(fmaf(R.x, R.x, R.y * R.y));
+    const float4 tz0 = sh.tw4[qz];
+    cf tz = {tz0.x, tz0.y}, tzr = {tz0.z, tz0.w};  // tw[qz] and i tw[qz]
     float gr[kPvGroup];  // frame u: G(t0 + u, pv_g(lane & 7)) over the lane's octet
     float al_lane = 0.f;  // full groups: the alpha of frame t0 + (lane & 7)
     // one output frame; FULL: t < f_out and i0(t) = c + 1 are known for the whole group
     auto frame = [&](int u, auto full) {
       constexpr bool FULL = decltype(full)::value;
       const int t = t0 + u;
-      const float4 tz = sh.tw4[qz];  // e^{+2 pi i qz / 250} as (x, y, -y, x)
+      const float4 tw = {tz.x, tz.y, tzr.x, tzr.y};  // e^{+2 pi i qz / 250} as (x, y, -y, x)
 #if HBK_PV_ABLATE & 2  // profiling build: the per-bin vocoder replaced by a stand-in
       if (t < a.f_out) {
         float al;
         ps_i0(a, t, al);
-        Q.x += al * tz.x;
+        Q.x += al * tw.x;
       }
       if (false) {
 #else
@@ -1776,7 +1782,7 @@ ps_vocoder_kernel(PitchArgs a) {
         const float m = fmaf(al, nm - cm, cm);
         const cf P = cmul(R, ca);
         // Z_t = m P e^{-2 pi i qz / 250} = m (P.x (x, -y) + P.y (y, x))
-        const cf Z = __builtin_elementwise_fma(cf{P.y, P.y}, cf{tz.y, tz.x}, cf{P.x, P.x} * cf{tz.w, tz.z});
+        const cf Z = __builtin_elementwise_fma(cf{P.y, P.y}, cf{tw.y, tw.x}, cf{P.x, P.x} * cf{tw.w, tw.z});
         Q = __builtin_elementwise_fma(cf{m, m}, Z, Q);
         xre = step ? nre : xre;
         xim = step ? nim : xim;
@@ -1787,7 +1793,7 @@ ps_vocoder_kernel(PitchArgs a) {
       }
       // G(t, .) over the wave's bins: 7 products, reduce-scatter over the lane octet,
       // all-reduce over the 8 octets
-      const cf vq = __builtin_elementwise_fma(cf{Q.y, Q.y}, cf{tz.z, tz.w}, cf{Q.x, Q.x} * cf{tz.x, tz.y});  // Q tw[qz]
+      const cf vq = __builtin_elementwise_fma(cf{Q.y, Q.y}, cf{tw.z, tw.w}, cf{Q.x, Q.x} * cf{tw.x, tw.y});  // Q tw[qz]
 #if HBK_PV_ABLATE & 1  // profiling build: no bin reduction
       gr[u] = vq.x * esr[u & 3].x;
 #else
@@ -1807,6 +1813,8 @@ ps_vocoder_kernel(PitchArgs a) {
 #endif
       qz += dq;
       qz -= qz >= kPsFft ? kPsFft : 0;
+      tz = __builtin_elementwise_fma(cf{tz.y, tz.y}, e7r, cf{tz.x, tz.x} * e7);
+      tzr = __builtin_elementwise_fma(cf{tzr.y, tzr.y}, e7r, cf{tzr.x, tzr.x} * e7);
     };
     bool full = t0 + kPvGroup <= a.f_out;
     if (full) {  // per-frame advances are all >= 1 (rate > 1) or all <= 1 (rate < 1): a total of
