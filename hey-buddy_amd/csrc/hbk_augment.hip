@@ -1886,16 +1886,21 @@ __global__ void ps_taps_kernel(PitchArgs a) {
 }
 
 __global__ void __launch_bounds__(128) ps_resample_kernel(PitchArgs a) {
-  __shared__ float ys[kPsResFrames * kPsPhaseMax + kPsTapMax];
+  // frames in pairs (f, f + 1): ys2[p] interleaves their windows, (f q, f+1 q, f q+1, f+1 q+1) per
+  // float4, so one packed FMA per tap serves both frames (the taps of a phase are the same)
+  static_assert(kPsTapMax % 2 == 0 && kPsResFrames % 2 == 0, "resampler pairs");
+  constexpr int kPairs = kPsResFrames / 2;
+  __shared__ __attribute__((aligned(16))) float ys2[kPairs][2 * kPsTapMax];
   const int ph = threadIdx.x, e = blockIdx.y;
   const int f0 = blockIdx.x * kPsResFrames;
   const float* y = a.y + static_cast<int64_t>(e) * a.l1;
   // y padded by (width, width + orig) zeros; frame f reads ypad[f orig + q]
   // (the window is read to kPsTapMax, past 2 width + orig, against zero taps)
-  const int j0 = f0 * a.orig - a.width, nj = (kPsResFrames - 1) * a.orig + kPsTapMax;
-  for (int j = ph; j < nj; j += 128) {
-    const int src = j0 + j;
-    ys[j] = (src >= 0 && src < a.l1) ? y[src] : 0.f;
+  const int j0 = f0 * a.orig - a.width;
+  for (int el = ph; el < kPsResFrames * kPsTapMax; el += 128) {
+    const int fr = el / kPsTapMax, q = el - fr * kPsTapMax;  // q fastest: coalesced reads
+    const int src = j0 + fr * a.orig + q;
+    ys2[fr >> 1][2 * q + (fr & 1)] = (src >= 0 && src < a.l1) ? y[src] : 0.f;
   }
   float tp[kPsTapMax];
   const float* tr = a.taps + min(ph, a.nw - 1) * kPsTapMax;
@@ -1904,16 +1909,21 @@ __global__ void __launch_bounds__(128) ps_resample_kernel(PitchArgs a) {
   __syncthreads();
   if (ph >= a.nw) return;
   float* out = a.out + static_cast<int64_t>(a.idx[e]) * a.out_stride;
-  for (int f = 0; f < kPsResFrames; ++f) {
-    const int i = (f0 + f) * a.nw + ph;
+  for (int p = 0; p < kPairs; ++p) {
+    const int i = (f0 + 2 * p) * a.nw + ph, i1 = i + a.nw;
     if (i >= a.L) break;
-    float v = 0.f;
+    cf v = {0.f, 0.f};
     if (i < a.target) {
-      const float* w = ys + f * a.orig;
+      const float4* w = reinterpret_cast<const float4*>(ys2[p]);
 #pragma unroll
-      for (int q = 0; q < kPsTapMax; ++q) v = fmaf(tp[q], w[q], v);
+      for (int q2 = 0; q2 < kPsTapMax / 2; ++q2) {
+        const float4 ww = w[q2];
+        v = __builtin_elementwise_fma(cf{tp[2 * q2], tp[2 * q2]}, cf{ww.x, ww.y}, v);
+        v = __builtin_elementwise_fma(cf{tp[2 * q2 + 1], tp[2 * q2 + 1]}, cf{ww.z, ww.w}, v);
+      }
     }
-    out[i] = v;
+    out[i] = v.x;
+    if (i1 < a.L) out[i1] = i1 < a.target ? v.y : 0.f;
   }
 }
 
