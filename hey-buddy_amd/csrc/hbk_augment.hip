@@ -872,6 +872,12 @@ struct ColoredArgs {
   const float2* thi;
   const float2* tlo;
   const float2* twn;
+  // group path (clips_per_noise > 1, hbk_colored_noise_ws): colored_group_kernel writes each
+  // group's coloured second (x kM1) and its rms; a clip whose f_decay equals its group's first
+  // clip's mixes from it (NULL: every clip colours its own second)
+  float* gbuf;            // [n_groups][kN1]
+  float* grms;            // [n_groups]: rms of the coloured second, NaN where not made
+  int64_t n_groups;
 };
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
@@ -994,6 +1000,50 @@ __device__ __forceinline__ int zaddr8(int f) {
   return 500 * k1 + 100 * k2 + 20 * k3 + 4 * k4 + k5;
 }
 
+// 1) + 2): group grp's second of white noise -> LDS, forward FFT, the real-FFT split x the
+// 1 / linspace^f_decay mask x inverse split, inverse FFT: zf = the coloured second x kM1
+// (natural order). Entered and left at a barrier.
+__device__ __forceinline__ void colored_second(const ColoredArgs& a, cf* z, const cf* thi, const cf* tlo, int tid,
+                                               int64_t grp, float fd) {
+  float* zf = reinterpret_cast<float*>(z);
+  // 1) one second of white noise -> LDS (the previous clip's readers finished at its last barrier)
+  if (a.white) {
+    const float* w = a.white + grp * a.white_stride;
+    for (int s = tid; s < kN1; s += kThreads) zf[s] = w[s];
+  } else {
+    for (int q = tid; q < kN1 / 2; q += kThreads) {
+      const float2 g = gauss2(a.seed, static_cast<uint64_t>(grp) * (kN1 / 2) + q);
+      *reinterpret_cast<float2*>(zf + 2 * q) = g;
+    }
+  }
+  __syncthreads();
+  transform8<false>(z, thi, tlo);
+  // 2) X = split(Z); Y = X / lin^f_decay; Z' = inverse split(Y), pairs (k, M - k), k <= M / 2
+  for (int k = tid; k <= kM1 / 2; k += kThreads) {
+    const int kc = (kM1 - k) % kM1;
+    const int p = zaddr8(k), pc = zaddr8(kc);
+    const cf zk = z[p];
+    const cf zc = z[pc];
+    const cf fe = 0.5f * cf{zk.x + zc.x, zk.y - zc.y};
+    const cf fo = 0.5f * cf{zk.y + zc.y, zc.x - zk.x};
+    const cf wk = cf{a.twn[k].x, a.twn[k].y};  // W_16000^k
+    const float mk = exp2f(-fd * __log2f(fmaf(a.lin_step, static_cast<float>(k), 1.f)));
+    const float mc = exp2f(-fd * __log2f(fmaf(a.lin_step, static_cast<float>(kM1 - k), 1.f)));  // bin M - k
+    const cf Yk = mk * (fe + cmul(wk, fo));
+    const cf Yc = mc * (cf{fe.x, -fe.y} + cmul(cf{-wk.x, wk.y}, cf{fo.x, -fo.y}));
+    const cf s1 = 0.5f * cf{Yk.x + Yc.x, Yk.y - Yc.y};
+    const cf d1 = 0.5f * cf{Yk.x - Yc.x, Yk.y + Yc.y};
+    const cf wd = cmul(cf{wk.x, -wk.y}, d1);
+    const cf s2 = 0.5f * cf{Yc.x + Yk.x, Yc.y - Yk.y};
+    const cf d2 = 0.5f * cf{Yc.x - Yk.x, Yc.y + Yk.y};
+    const cf wd2 = cmul(cf{-wk.x, -wk.y}, d2);
+    z[p] = s1 + cf{-wd.y, wd.x};
+    if (kc != k) z[pc] = s2 + cf{-wd2.y, wd2.x};
+  }
+  __syncthreads();
+  transform8<true>(z, thi, tlo);  // natural order, x kM1
+}
+
 // torch_audiomentations AddColoredNoise (per clip, white noise w of ONE second):
 //   n1 = irfft(rfft(w[:16000]) / linspace(1, sqrt(sr/2), 8001)^f_decay)      (16,000)
 //   n1 /= rms(n1) + 1e-8;  noise[t] = n1[t mod 16000], t < T (tiled, not renormalised)
@@ -1020,44 +1070,11 @@ __global__ void __launch_bounds__(kThreads) colored_noise_kernel(ColoredArgs a) 
         copy_clip(a.x + clip * a.x_stride, a.out + clip * a.out_stride, tid);
       continue;
     }
-    // 1) one second of white noise -> LDS (the previous clip's readers finished at its last barrier)
     const int64_t grp = clip / a.group;  // clips of one batch share the noise vector (per_batch)
-    if (a.white) {
-      const float* w = a.white + grp * a.white_stride;
-      for (int s = tid; s < kN1; s += kThreads) zf[s] = w[s];
-    } else {
-      for (int q = tid; q < kN1 / 2; q += kThreads) {
-        const float2 g = gauss2(a.seed, static_cast<uint64_t>(grp) * (kN1 / 2) + q);
-        *reinterpret_cast<float2*>(zf + 2 * q) = g;
-      }
-    }
-    __syncthreads();
-    transform8<false>(z, thi, tlo);
-    // 2) X = split(Z); Y = X / lin^f_decay; Z' = inverse split(Y), pairs (k, M - k), k <= M / 2
-    const float fd = a.f_decay[clip];
-    for (int k = tid; k <= kM1 / 2; k += kThreads) {
-      const int kc = (kM1 - k) % kM1;
-      const int p = zaddr8(k), pc = zaddr8(kc);
-      const cf zk = z[p];
-      const cf zc = z[pc];
-      const cf fe = 0.5f * cf{zk.x + zc.x, zk.y - zc.y};
-      const cf fo = 0.5f * cf{zk.y + zc.y, zc.x - zk.x};
-      const cf wk = cf{a.twn[k].x, a.twn[k].y};  // W_16000^k
-      const float mk = exp2f(-fd * __log2f(fmaf(a.lin_step, static_cast<float>(k), 1.f)));
-      const float mc = exp2f(-fd * __log2f(fmaf(a.lin_step, static_cast<float>(kM1 - k), 1.f)));  // bin M - k
-      const cf Yk = mk * (fe + cmul(wk, fo));
-      const cf Yc = mc * (cf{fe.x, -fe.y} + cmul(cf{-wk.x, wk.y}, cf{fo.x, -fo.y}));
-      const cf s1 = 0.5f * cf{Yk.x + Yc.x, Yk.y - Yc.y};
-      const cf d1 = 0.5f * cf{Yk.x - Yc.x, Yk.y + Yc.y};
-      const cf wd = cmul(cf{wk.x, -wk.y}, d1);
-      const cf s2 = 0.5f * cf{Yc.x + Yk.x, Yc.y - Yk.y};
-      const cf d2 = 0.5f * cf{Yc.x - Yk.x, Yc.y + Yk.y};
-      const cf wd2 = cmul(cf{-wk.x, -wk.y}, d2);
-      z[p] = s1 + cf{-wd.y, wd.x};
-      if (kc != k) z[pc] = s2 + cf{-wd2.y, wd2.x};
-    }
-    __syncthreads();
-    transform8<true>(z, thi, tlo);  // natural order, x kM1
+    float rms_g = __builtin_nanf("");
+    if (a.grms && a.f_decay[clip] == a.f_decay[grp * a.group]) rms_g = a.grms[grp];  // uniform per block
+    if (rms_g == rms_g) continue;  // the group's coloured second is made: colored_mix_kernel mixes it
+    colored_second(a, z, thi, tlo, tid, grp, a.f_decay[clip]);
     // 3) rms(n1) over 16,000 and rms(x) over T in one block sum; tile and mix
     const float* x = a.x + clip * a.x_stride;
     float xr[kPer];
@@ -1085,6 +1102,93 @@ __global__ void __launch_bounds__(kThreads) colored_noise_kernel(ColoredArgs a) 
       if (s < kT) out[s] = fmaf(scale, zf[s < kN1 ? s : s - kN1], xr[u]);
     }
     __syncthreads();  // zf is rewritten by the next clip
+  }
+}
+
+// The coloured second of every group whose first clip draws noise (clips_per_noise > 1:
+// per_batch mode shares the white noise and, in the reference's chain, f_decay across the
+// batch), with its rms computed exactly as the clip kernel does.
+__global__ void __launch_bounds__(kThreads) colored_group_kernel(ColoredArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  cf* z = reinterpret_cast<cf*>(smem);
+  float* red = smem + 2 * kM1;
+  cf* thi = reinterpret_cast<cf*>(smem + 2 * kM1 + 32);
+  cf* tlo = thi + kTw8Hi;
+  for (int i = threadIdx.x; i < kTw8Hi; i += kThreads) thi[i] = cf{a.thi[i].x, a.thi[i].y};
+  for (int i = threadIdx.x; i < kTw8Lo; i += kThreads) tlo[i] = cf{a.tlo[i].x, a.tlo[i].y};
+  const float* zf = smem;
+  constexpr int kPer = (kT + kThreads - 1) / kThreads;
+  for (int64_t g = blockIdx.x; g < a.n_groups; g += gridDim.x) {
+    const int tid = opaque_tid();
+    const int64_t c0 = g * a.group;
+    if (a.snr_db[c0] != a.snr_db[c0]) {  // the group's first clip draws no noise: not made
+      if (tid == 0) a.grms[g] = __builtin_nanf("");
+      continue;
+    }
+    __syncthreads();  // tables loaded / the previous group's readers of zf are done
+    colored_second(a, z, thi, tlo, tid, g, a.f_decay[c0]);
+    float ex = 0.f, en = 0.f;
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int s = tid + u * kThreads;
+      if (s < kN1) {
+        const float nv = zf[s] * (1.f / kM1);
+        en += nv * nv;
+      }
+    }
+    block_sum2(ex, en, red);
+    float* gb = a.gbuf + g * kN1;
+    for (int s = tid; s < kN1; s += kThreads) gb[s] = zf[s];
+    if (tid == 0) a.grms[g] = sqrtf(en / kN1);
+    __syncthreads();
+  }
+}
+
+// The clips of made groups (colored_group_kernel): rms(x) and the mix, from the group's
+// coloured second in global memory (L2-resident across its clips). The same per-thread
+// order and block sum as colored_noise_kernel, so the result is bit-identical; no
+// transform LDS, so two 1024-thread blocks (two clips in flight) per CU.
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8))) colored_mix_kernel(ColoredArgs a) {
+  __shared__ float red[32];
+  constexpr int kPer = (kT + kThreads - 1) / kThreads;
+  const int64_t n_iter = a.idx ? a.n_entries : a.n_clips;
+  for (int64_t e = blockIdx.x; e < n_iter; e += gridDim.x) {
+    const int64_t clip = a.idx ? a.idx[e] : e;
+    const int tid = opaque_tid();
+    const float snr = a.snr_db[clip];
+    const int64_t grp = clip / a.group;
+    float rms_g = __builtin_nanf("");
+    if (snr == snr && a.f_decay[clip] == a.f_decay[grp * a.group]) rms_g = a.grms[grp];
+    if (rms_g != rms_g) continue;  // uniform per block: colored_noise_kernel's clip
+    const float* gb = a.gbuf + grp * kN1;
+    const float* x = a.x + clip * a.x_stride;
+    float xr[kPer];
+    float ex = 0.f, en = 0.f;
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int s = tid + u * kThreads;
+      xr[u] = 0.f;
+      if (s < kT) {  // 32-bit byte offsets on uniform bases (few VGPRs: two blocks per CU)
+        xr[u] = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(x) + (static_cast<uint32_t>(s) << 2));
+        ex += xr[u] * xr[u];
+      }
+    }
+    block_sum2(ex, en, red);
+    const float rms_x = sqrtf(ex / kT);
+    const float scale = rms_x / powf(10.f, snr / 20.f) / (rms_g + 1e-8f) * (1.f / kM1);
+    float* out = a.out + clip * a.out_stride;
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int s = tid + u * kThreads;
+      if (s < kT) {
+        const int sn = s < kN1 ? s : s - kN1;
+        const float nv =
+            *reinterpret_cast<const float*>(reinterpret_cast<const char*>(gb) + (static_cast<uint32_t>(sn) << 2));
+        *reinterpret_cast<float*>(reinterpret_cast<char*>(out) + (static_cast<uint32_t>(s) << 2)) =
+            fmaf(scale, nv, xr[u]);
+      }
+    }
+    __syncthreads();  // red is reused by the next clip
   }
 }
 
@@ -2008,6 +2112,8 @@ int hbk_reverb_plan_create(int64_t T, hbk_reverb_plan** plan) {
       (e = hipFuncSetAttribute(reinterpret_cast<const void*>(band_stop_spectrum_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, int(lds))) != hipSuccess ||
       (e = hipFuncSetAttribute(reinterpret_cast<const void*>(colored_noise_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, int(kColoredLds))) != hipSuccess ||
+      (e = hipFuncSetAttribute(reinterpret_cast<const void*>(colored_group_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, int(kColoredLds))) != hipSuccess) {
     hbk_reverb_plan_destroy(p);
     return hip_error(e, "hipFuncSetAttribute(augment LDS)");
@@ -2076,10 +2182,28 @@ int hbk_augment(const hbk_reverb_plan* p, const float* x, int64_t n_clips, int64
   return HBK_OK;
 }
 
+static int64_t colored_groups(int64_t n_clips, int64_t clips_per_noise) {
+  return clips_per_noise > 1 && n_clips > 0 ? (n_clips + clips_per_noise - 1) / clips_per_noise : 0;
+}
+
+int64_t hbk_colored_noise_workspace_size(int64_t n_clips, int64_t clips_per_noise) {
+  const int64_t g = colored_groups(n_clips, clips_per_noise);
+  return g ? g * hbk::kN1 * int64_t(sizeof(float)) + ((g * int64_t(sizeof(float)) + 255) & ~int64_t(255)) : 0;
+}
+
 int hbk_colored_noise(const hbk_reverb_plan* p, const float* x, int64_t n_clips, int64_t x_stride,
                       const float* white, int64_t white_stride, uint64_t seed, int64_t clips_per_noise,
                       const float* f_decay, const float* snr_db, float sample_rate, const int32_t* idx,
                       int64_t n_entries, float* out, int64_t out_stride, void* stream) {
+  return hbk_colored_noise_ws(p, x, n_clips, x_stride, white, white_stride, seed, clips_per_noise, f_decay, snr_db,
+                              sample_rate, idx, n_entries, out, out_stride, nullptr, 0, stream);
+}
+
+int hbk_colored_noise_ws(const hbk_reverb_plan* p, const float* x, int64_t n_clips, int64_t x_stride,
+                         const float* white, int64_t white_stride, uint64_t seed, int64_t clips_per_noise,
+                         const float* f_decay, const float* snr_db, float sample_rate, const int32_t* idx,
+                         int64_t n_entries, float* out, int64_t out_stride, void* workspace, int64_t workspace_bytes,
+                         void* stream) {
   using namespace hbk;
   if (!p) return arg_error("plan is NULL");
   if (n_clips < 0) return arg_error("negative n_clips");
@@ -2110,7 +2234,25 @@ int hbk_colored_noise(const hbk_reverb_plan* p, const float* x, int64_t n_clips,
   a.thi = p->thi8;
   a.tlo = p->tlo8;
   a.twn = p->twn16;
+  a.gbuf = a.grms = nullptr;
+  a.n_groups = 0;
   if (a.n_entries <= 0) return n_entries < 0 ? arg_error("negative n_entries") : HBK_OK;
+  const int64_t need = hbk_colored_noise_workspace_size(n_clips, clips_per_noise);
+  if (workspace && need > 0) {
+    if (workspace_bytes < need) return arg_error("workspace too small (hbk_colored_noise_workspace_size)");
+    a.n_groups = colored_groups(n_clips, clips_per_noise);
+    a.gbuf = static_cast<float*>(workspace);
+    a.grms = a.gbuf + a.n_groups * kN1;
+    const int64_t gblocks = std::min<int64_t>(a.n_groups, persistent_blocks(1, stream));
+    hipLaunchKernelGGL(colored_group_kernel, dim3(unsigned(gblocks)), dim3(kThreads), kColoredLds, as_stream(stream),
+                       a);
+    HBK_LAUNCH_CHECK("colored_group_kernel");
+  }
+  if (a.grms) {
+    const int64_t mblocks = std::min<int64_t>(a.n_entries, persistent_blocks(2, stream));
+    hipLaunchKernelGGL(colored_mix_kernel, dim3(unsigned(mblocks)), dim3(kThreads), 0, as_stream(stream), a);
+    HBK_LAUNCH_CHECK("colored_mix_kernel");
+  }
   const int64_t blocks = std::min<int64_t>(a.n_entries, persistent_blocks(1, stream));
   hipLaunchKernelGGL(colored_noise_kernel, dim3(unsigned(blocks)), dim3(kThreads), kColoredLds, as_stream(stream), a);
   HBK_LAUNCH_CHECK("colored_noise_kernel");

@@ -774,6 +774,7 @@ class ReverbPlan:
             check(lib().hbk_reverb_plan_create(self.T, ctypes.byref(handle)), "hbk_reverb_plan_create")
         self._handle = handle
         self._bs_ws: torch.Tensor | None = None  # band-stop workspace (grows)
+        self._cn_ws: torch.Tensor | None = None  # colored-noise group seconds (grows)
         self.id = _register(self)
 
     @staticmethod
@@ -892,8 +893,18 @@ class ReverbPlan:
         def to_dev(t: torch.Tensor) -> torch.Tensor:
             return t.pin_memory().to(self.device, non_blocking=True) if t.device.type == "cpu" else t.to(self.device)
 
+        # clips_per_noise > 1: each group's coloured second is made once (hbk_colored_noise_ws)
+        ws_bytes = int(lib().hbk_colored_noise_workspace_size(n, int(clips_per_noise)))
+        if os.environ.get("HBK_COLORED_NO_GROUP"):  # A/B: every clip colours its own second
+            ws_bytes = 0
+        ws = None
+        if ws_bytes > 0:
+            ws = self._cn_ws
+            if ws is None or ws.numel() < ws_bytes:
+                ws = torch.empty(ws_bytes, dtype=torch.uint8, device=self.device)
+                self._cn_ws = ws
         torch.ops.hbk.colored_noise_(x, white, to_dev(f_decay), to_dev(snr_db), _u64_to_i64(seed),
-                                     int(clips_per_noise), float(sample_rate), rows, out, self.id)
+                                     int(clips_per_noise), float(sample_rate), rows, out, ws, self.id)
         return out
 
     def band_stop(self, x: torch.Tensor, idx: torch.Tensor, cut_lo: torch.Tensor, cut_hi: torch.Tensor,
@@ -970,18 +981,20 @@ def _augment_op(x: torch.Tensor, ring: torch.Tensor | None, noise_off: torch.Ten
                             ptr(spec_idx), opt(gain), ptr(out), out.stride(0), stream_ptr(x.device)), "hbk_augment")
 
 
-@torch.library.custom_op("hbk::colored_noise_", mutates_args=("out",))
+@torch.library.custom_op("hbk::colored_noise_", mutates_args=("out", "workspace"))
 def _colored_noise_op(x: torch.Tensor, white: torch.Tensor | None, f_decay: torch.Tensor, snr_db: torch.Tensor,
                       seed: int, clips_per_noise: int, sample_rate: float, rows: torch.Tensor | None,
-                      out: torch.Tensor, plan_id: int) -> None:
+                      out: torch.Tensor, workspace: torch.Tensor | None, plan_id: int) -> None:
     plan = _plans[plan_id]
-    check(lib().hbk_colored_noise(plan._handle, ptr(x), x.shape[0], x.stride(0),
-                                  ptr(white) if white is not None else None,
-                                  white.stride(0) if white is not None else 0, seed & (2 ** 64 - 1),
-                                  clips_per_noise, ptr(f_decay),
-                                  ptr(snr_db), sample_rate, ptr(rows) if rows is not None else None,
-                                  rows.numel() if rows is not None else 0, ptr(out), out.stride(0),
-                                  stream_ptr(x.device)), "hbk_colored_noise")
+    check(lib().hbk_colored_noise_ws(plan._handle, ptr(x), x.shape[0], x.stride(0),
+                                     ptr(white) if white is not None else None,
+                                     white.stride(0) if white is not None else 0, seed & (2 ** 64 - 1),
+                                     clips_per_noise, ptr(f_decay),
+                                     ptr(snr_db), sample_rate, ptr(rows) if rows is not None else None,
+                                     rows.numel() if rows is not None else 0, ptr(out), out.stride(0),
+                                     ptr(workspace) if workspace is not None else None,
+                                     workspace.numel() if workspace is not None else 0,
+                                     stream_ptr(x.device)), "hbk_colored_noise_ws")
 
 
 @torch.library.custom_op("hbk::band_stop_", mutates_args=("out", "workspace"))

@@ -352,6 +352,17 @@ int hbk_colored_noise(const hbk_reverb_plan* plan, const float* x, int64_t n_cli
                       const float* white, int64_t white_stride, uint64_t seed, int64_t clips_per_noise,
                       const float* f_decay, const float* snr_db, float sample_rate, const int32_t* idx,
                       int64_t n_entries, float* out, int64_t out_stride, void* stream);
+/* The same with a workspace of hbk_colored_noise_workspace_size(n_clips,
+ * clips_per_noise) bytes (0 when clips_per_noise is 1): each group's coloured
+ * second is made once (from its first clip's f_decay) and every clip of the
+ * group with that f_decay mixes from it, bit-identical to the per-clip path
+ * (per_batch mode draws one f_decay per batch). */
+int64_t hbk_colored_noise_workspace_size(int64_t n_clips, int64_t clips_per_noise);
+int hbk_colored_noise_ws(const hbk_reverb_plan* plan, const float* x, int64_t n_clips, int64_t x_stride,
+                         const float* white, int64_t white_stride, uint64_t seed, int64_t clips_per_noise,
+                         const float* f_decay, const float* snr_db, float sample_rate, const int32_t* idx,
+                         int64_t n_entries, float* out, int64_t out_stride, void* workspace, int64_t workspace_bytes,
+                         void* stream);
 
 /* Band-stop: torch_audiomentations BandStopFilter, which the reference applies
  * in its batch chain with p 0.25 per batch, one parameter set per batch

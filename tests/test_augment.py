@@ -320,6 +320,23 @@ def test_colored_noise_parity():
     for i in range(5):
         ok, worst = _close(out2[i], ref2[i])
         assert ok, f"shared noise, clip {i}: max |diff| {worst}"
+    # group path (hbk_colored_noise_ws): f_decay shared within each group -> one coloured second per
+    # group, bit-identical to colouring each clip's own copy of its group's noise
+    xt = torch.from_numpy(x).float().cuda()
+    fd_g = torch.tensor([0.5, 0.5, 1.3, 1.3, -1.0])
+    out3 = plan.colored_noise(xt, fd_g, torch.from_numpy(snr), white=torch.from_numpy(w[:3]).cuda(),
+                              clips_per_noise=2)
+    out4 = plan.colored_noise(xt, fd_g, torch.from_numpy(snr), white=torch.from_numpy(w[[0, 0, 1, 1, 2]]).cuda())
+    assert torch.equal(out3, out4)
+    # the same for the generated stream: the group path against the per-clip call (hbk_colored_noise)
+    from heybuddy._native import lib
+    from heybuddy.kernels import ptr, stream_ptr
+    out5 = plan.colored_noise(xt, fd_g, torch.from_numpy(snr), seed=11, clips_per_noise=2)
+    out6 = torch.empty_like(xt)
+    fd_d, snr_d = fd_g.cuda(), torch.from_numpy(snr).cuda()
+    assert lib().hbk_colored_noise(plan._handle, ptr(xt), 5, xt.stride(0), None, 0, 11, 2, ptr(fd_d), ptr(snr_d),
+                                   16000.0, None, 0, ptr(out6), out6.stride(0), stream_ptr(xt.device)) == 0
+    assert torch.equal(out5, out6)
 
 
 @pytest.mark.gpu
