@@ -570,7 +570,10 @@ def setup_e2e(args, dev, rank, world, seed):
     mplan = default_mel_plan(dev, 32767.0)
     eplan = embed_plan(dev, WINDOW_STARTS)
     pool = torch.empty((n, len(WINDOW_STARTS), 96), dtype=torch.float32, device=dev)
-    raw = torch.empty_like(pool)  # embed output before the NaN replacement gathers it into the pool
+    # embed output before the NaN replacement gathers it into the pool; one extra zero row
+    # (the all-NaN case's source: no masked fill over the pool)
+    raw_ext = torch.zeros((n + 1,) + tuple(pool.shape[1:]), dtype=torch.float32, device=dev)
+    raw = raw_ext[:n]
     # precalculated negatives (the reference's hosted f16 sets): large 2/3, medium 1/3
     g = torch.Generator(device=dev).manual_seed(seed + 4)
     n_neg = 200_000
@@ -638,7 +641,8 @@ def setup_e2e(args, dev, rank, world, seed):
         frames = mel_frames(x, mplan, N_FRAMES)
         if evs:
             evs[2].record(stream)
-        replace_nan_rows_device(embed_clips(frames, eplan, out=raw), out=pool)  # no host sync
+        embed_clips(frames, eplan, out=raw)
+        replace_nan_rows_device(raw_ext, out=pool)  # no host sync
         if evs:
             evs[3].record(stream)
         sample()
@@ -710,7 +714,8 @@ def setup_e2e(args, dev, rank, world, seed):
                         eplan.clips_front(frames[a1:], K, mids[b])
                     front_done[b].record(fs)
                 else:
-                    replace_nan_rows_device(embed_clips(frames, eplan, out=raw), out=pools[b])
+                    embed_clips(frames, eplan, out=raw)
+                    replace_nan_rows_device(raw_ext, out=pools[b])
                     feat_done[b].record(fs)
                 if part is not None:
                     part.append(("featurize", e0, mark("featurize", fs)))
@@ -724,7 +729,7 @@ def setup_e2e(args, dev, rank, world, seed):
                     eplan.clips_back(mids1[b], a1, K - 1, raw[:a1])
                 if a1 < n:
                     eplan.clips_back(mids[b], n - a1, K, raw[a1:])
-                replace_nan_rows_device(raw, out=pools[b])
+                replace_nan_rows_device(raw_ext, out=pools[b])
                 feat_done[b].record(ts)
 
         def step(evs):  # noqa: F811

@@ -288,14 +288,25 @@ def replace_nan_rows_device(emb: torch.Tensor, out: torch.Tensor,
     clip (device RNG in place of np.random.choice), all zeros when every clip
     is NaN; the result is gathered into out (same shape, not emb). The
     reference's warning needs the count on the host and is not emitted here
-    (_replace_nan_rows is the logging form)."""
-    n = emb.shape[0]
-    bad = torch.isnan(emb.reshape(n, -1)).any(dim=1)
+    (_replace_nan_rows is the logging form). emb may carry one extra all-zero
+    row (n + 1 rows for out's n): the all-NaN case then gathers it instead of a
+    masked fill over the whole output (one pass less)."""
+    n = out.shape[0]
+    ext = emb.shape[0] == n + 1
+    if not ext and emb.shape[0] != n:
+        raise ValueError("emb must have out's rows (or one extra zero row)")
+    rows = emb.reshape(emb.shape[0], -1)
+    bad = rows[:n].amax(dim=1).isnan()  # amax propagates NaN: one reduction pass, no bool plane
     order = torch.argsort(bad.to(torch.uint8), stable=True)  # NaN-free clips first
     n_good = n - bad.sum()
     r = (torch.rand(n, device=emb.device, generator=generator) * n_good).long().clamp_(max=n - 1)
-    src = torch.where(bad, order[r], torch.arange(n, device=emb.device))
-    torch.index_select(emb.reshape(n, -1), 0, src, out=out.view(n, -1))
+    pick = order[r]
+    if ext:
+        pick = torch.where(n_good > 0, pick, torch.full_like(pick, n))
+    src = torch.where(bad, pick, torch.arange(n, device=emb.device))
+    torch.index_select(rows, 0, src, out=out.view(n, -1))
+    if ext:
+        return out
     return out.masked_fill_((n_good == 0).reshape([1] * out.dim()), 0.0)
 
 

@@ -52,6 +52,19 @@ def test_replace_nan_rows_device_cpu_semantics():
         assert any(torch.equal(out[i], e[j]) for j in clean)
     allnan = torch.full((3, 16, 96), float("nan"))
     assert (replace_nan_rows_device(allnan, torch.empty_like(allnan)) == 0).all()
+    # with an extra zero row: the same result, the all-NaN case gathers the zero row
+    ext = torch.cat([e, torch.zeros(1, 16, 96)])
+    out2 = torch.empty_like(e)
+    replace_nan_rows_device(ext, out2, generator=torch.Generator().manual_seed(1))
+    assert torch.equal(out2, out)
+    allnan_ext = torch.cat([allnan, torch.zeros(1, 16, 96)])
+    assert (replace_nan_rows_device(allnan_ext, torch.empty_like(allnan)) == 0).all()
+    # +-inf without NaN is not a NaN row
+    inf_row = e.clone()
+    inf_row[4, 0, 0], inf_row[4, 0, 1] = float("inf"), -float("inf")
+    out3 = torch.empty_like(e)
+    replace_nan_rows_device(inf_row, out3, generator=torch.Generator().manual_seed(1))
+    assert torch.equal(out3[4], inf_row[4])
 
 
 @pytest.mark.gpu
