@@ -1162,15 +1162,15 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8
     if (rms_g != rms_g) continue;  // uniform per block: colored_noise_kernel's clip
     const float* gb = a.gbuf + grp * kN1;
     const float* x = a.x + clip * a.x_stride;
-    float xr[kPer];
+    // two passes over x (the second from the cache): nothing is held across the block sum,
+    // so the kernel fits 64 VGPRs without spills; ex in colored_noise_kernel's order
     float ex = 0.f, en = 0.f;
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
       const int s = tid + u * kThreads;
-      xr[u] = 0.f;
-      if (s < kT) {  // 32-bit byte offsets on uniform bases (few VGPRs: two blocks per CU)
-        xr[u] = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(x) + (static_cast<uint32_t>(s) << 2));
-        ex += xr[u] * xr[u];
+      if (s < kT) {  // 32-bit byte offsets on uniform bases
+        const float v = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(x) + (static_cast<uint32_t>(s) << 2));
+        ex += v * v;
       }
     }
     block_sum2(ex, en, red);
@@ -1182,10 +1182,10 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8
       const int s = tid + u * kThreads;
       if (s < kT) {
         const int sn = s < kN1 ? s : s - kN1;
+        const float xv = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(x) + (static_cast<uint32_t>(s) << 2));
         const float nv =
             *reinterpret_cast<const float*>(reinterpret_cast<const char*>(gb) + (static_cast<uint32_t>(sn) << 2));
-        *reinterpret_cast<float*>(reinterpret_cast<char*>(out) + (static_cast<uint32_t>(s) << 2)) =
-            fmaf(scale, nv, xr[u]);
+        *reinterpret_cast<float*>(reinterpret_cast<char*>(out) + (static_cast<uint32_t>(s) << 2)) = fmaf(scale, nv, xv);
       }
     }
     __syncthreads();  // red is reused by the next clip
