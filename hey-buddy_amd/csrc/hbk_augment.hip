@@ -1220,7 +1220,10 @@ __device__ __forceinline__ unsigned abs_bits(float v, int s) {
 
 __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8)))
 tanh_distortion_kernel(TanhArgs a) {
-  __shared__ unsigned hist[256];
+  // radix-select digits over |x|'s bits 30..0 (bit 31 is 0): 12 + 10 + 9 bits. The first
+  // digit spans the exponent and 4 mantissa bits, so a clip's values spread over ~200 bins
+  // instead of crowding the ~9 of an 8-bit top digit (LDS atomics to one address serialise)
+  __shared__ unsigned hist[4096];
   __shared__ float red[32];
   __shared__ unsigned pick[2];  // selected digit, rank left within it
   constexpr int kPer = (kT + kThreads - 1) / kThreads;
@@ -1253,40 +1256,36 @@ tanh_distortion_kernel(TanhArgs a) {
     const double frac = pos - lo;
     unsigned prefix = 0, mask = 0, rank = static_cast<unsigned>(lo);
 #pragma unroll 1
-    for (int shift = 24; shift >= 0; shift -= 8) {
-      if (tid < 256) hist[tid] = 0;
+    for (int p = 0; p < 3; ++p) {
+      const int shift = p == 0 ? 19 : (p == 1 ? 9 : 0), bins = p == 0 ? 4096 : (p == 1 ? 1024 : 512);
+      const int per_lane = bins >> 6;  // bins per lane of wave 0's scan
+      for (int i = tid; i < bins; i += kThreads) hist[i] = 0;
       __syncthreads();
       const int t = opaque_tid();
 #pragma unroll
       for (int u = 0; u < kPer; ++u) {
         const unsigned b = abs_bits(xr[u], t + u * kThreads);
-        if ((b & mask) == prefix && b != 0xFFFFFFFFu) atomicAdd(&hist[(b >> shift) & 255], 1u);
+        if ((b & mask) == prefix && b != 0xFFFFFFFFu) atomicAdd(&hist[(b >> shift) & (bins - 1)], 1u);
       }
       __syncthreads();
-      if (tid < 64) {  // wave 0: 4 bins per lane, inclusive scan over lanes, first lane past rank
-        const unsigned h0 = hist[4 * tid], h1 = hist[4 * tid + 1], h2 = hist[4 * tid + 2], h3 = hist[4 * tid + 3];
-        unsigned inc = h0 + h1 + h2 + h3;
+      if (tid < 64) {  // wave 0: per_lane bins per lane, inclusive scan over lanes, first lane past rank
+        unsigned own = 0;
+        for (int i = 0; i < per_lane; ++i) own += hist[per_lane * tid + i];
+        unsigned inc = own;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
           const unsigned v = __shfl_up(inc, d, 64);
           if (tid >= d) inc += v;
         }
-        const unsigned excl = inc - (h0 + h1 + h2 + h3);
         const unsigned long long hit = __ballot(inc > rank);
         const int l = __ffsll(static_cast<long long>(hit)) - 1;
         if (tid == l) {
-          unsigned r = rank - excl, dsel = 4 * l;
-          if (r >= h0) {
-            r -= h0;
+          unsigned r = rank - (inc - own), dsel = per_lane * l;
+          for (int i = 0; i < per_lane - 1; ++i) {
+            const unsigned h = hist[dsel];
+            if (r < h) break;
+            r -= h;
             ++dsel;
-            if (r >= h1) {
-              r -= h1;
-              ++dsel;
-              if (r >= h2) {
-                r -= h2;
-                ++dsel;
-              }
-            }
           }
           pick[0] = dsel;
           pick[1] = r;
@@ -1294,7 +1293,7 @@ tanh_distortion_kernel(TanhArgs a) {
       }
       __syncthreads();
       prefix |= pick[0] << shift;
-      mask |= 255u << shift;
+      mask |= static_cast<unsigned>(bins - 1) << shift;
       rank = pick[1];
     }
     // successor: v_lo again if more than lo + 1 values are <= v_lo, else min{|x| > v_lo}
