@@ -15,7 +15,8 @@ for r in csv.DictReader(open(f)):
     name = r["Kernel_Name"]
     if "ps_" not in name:
         continue
-    base = name.split("(anonymous namespace)::")[-1].split("(")[0]
+    parts = name.split("(anonymous namespace)::")
+    base = (parts[1] if len(parts) > 1 else name).split("(")[0]
     acc[base][r["Counter_Name"]] += float(r["Counter_Value"])
 for k, c in acc.items():
     print(k, " ".join("%s=%.3g" % (n, v) for n, v in sorted(c.items())))
