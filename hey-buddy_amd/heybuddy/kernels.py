@@ -895,8 +895,8 @@ class ReverbPlan:
 
         # clips_per_noise > 1: each group's coloured second is made once (hbk_colored_noise_ws)
         ws_bytes = int(lib().hbk_colored_noise_workspace_size(n, int(clips_per_noise)))
-        if os.environ.get("HBK_COLORED_NO_GROUP"):  # A/B: every clip colours its own second
-            ws_bytes = 0
+        if os.environ.get("HBK_COLORED_NO_GROUP") or ws_bytes > (1 << 30):
+            ws_bytes = 0  # A/B switch; and tiny groups over huge n are not worth 64 KB per group
         ws = None
         if ws_bytes > 0:
             ws = self._cn_ws
