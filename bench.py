@@ -432,7 +432,7 @@ def setup_train(args, dev, rank, world, seed):
 
     def roofline(name, ms, pmc):
         return roof("k1a/k1b + k2_rows + k3_wgrad + k4_update (fused train step, %d steps over 3 stages)" % n_steps,
-                    "mfma", flops_per_sample * units / world, ms, "TFLOP/s",
+                    "latency", flops_per_sample * units / world, ms, "TFLOP/s",
                     load_traffic(pmc, ("k1b_kernel", "k2_rows", "k3_wgrad", "k4_update")),
                     algorithmic_flops_per_sample=flops_per_sample, params=P_, steps=n_steps,
                     us_per_train_step=round(ms * 1e3 / n_steps, 2))
@@ -643,7 +643,7 @@ def setup_e2e(args, dev, rank, world, seed):
         if evs:
             evs[2].record(stream)
         embed_clips(frames, eplan, out=raw)
-        replace_nan_rows_device(raw_ext, out=pool)  # no host sync
+        replace_nan_rows_device(raw_ext, out=pool, zero_row=True)  # no host sync
         if evs:
             evs[3].record(stream)
         sample()
@@ -716,7 +716,7 @@ def setup_e2e(args, dev, rank, world, seed):
                     front_done[b].record(fs)
                 else:
                     embed_clips(frames, eplan, out=raw)
-                    replace_nan_rows_device(raw_ext, out=pools[b])
+                    replace_nan_rows_device(raw_ext, out=pools[b], zero_row=True)
                     feat_done[b].record(fs)
                 if part is not None:
                     part.append(("featurize", e0, mark("featurize", fs)))
@@ -730,7 +730,7 @@ def setup_e2e(args, dev, rank, world, seed):
                     eplan.clips_back(mids1[b], a1, K - 1, raw[:a1])
                 if a1 < n:
                     eplan.clips_back(mids[b], n - a1, K, raw[a1:])
-                replace_nan_rows_device(raw_ext, out=pools[b])
+                replace_nan_rows_device(raw_ext, out=pools[b], zero_row=True)
                 feat_done[b].record(ts)
 
         def step(evs):  # noqa: F811
@@ -798,8 +798,9 @@ def setup_e2e(args, dev, rank, world, seed):
                              ("tanh_distortion",), "x read + y written"),
                     "bandstop": (AUG_T * 4 * 2, "band_stop_kernel (+ sums / spectrum, the batches whose coin came up)",
                                  ("band_stop",), "x read + y written"),
-                    "colored": (AUG_T * 4 * 2, "colored_noise_kernel (the batches whose coin came up)",
-                                ("colored_noise",), "x read + y written")}
+                    "colored": (AUG_T * 4 * 2, "colored_group_kernel + colored_mix_kernel (+ colored_noise_kernel for "
+                                "clips outside a group; the batches whose coin came up)",
+                                ("colored_noise", "colored_mix", "colored_group"), "x read + y written")}
         for name, (bpc, kname, subs, basis) in per_clip.items():
             if sub_ms.get(name):
                 m = cnt.get(name, n)
@@ -815,7 +816,7 @@ def setup_e2e(args, dev, rank, world, seed):
                         "colored_noise_kernel + augment_kernel (placement, 7-band EQ, tanh, pitch shift, band-stop, "
                         "colored noise, gain + noise mix + 23040-pt FFT reverb)", "hbm",
                         n * AUG_T * 4 * 2, ms, "GB/s", load_traffic(pmc, ("place_kernel", "augment_kernel", "eq_kernel",
-                                                                          "band_stop", "colored_noise", "ps_",
+                                                                          "band_stop", "colored_", "ps_",
                                                                           "tanh_distortion")),
                         algorithmic_bytes_per_clip=AUG_T * 4 * 2, summary=True,
                         bytes_basis="placed clip written + augmented clip written in place (92,160 B each); "
@@ -833,10 +834,12 @@ def setup_e2e(args, dev, rank, world, seed):
                         peak_basis="f16 dense MFMA peak / 3 (hi*hi + hi*lo + lo*hi per f32-accurate MAC)",
                         algorithmic_flops_per_clip=2.0 * eplan.macs_per_clip)
         return roof("k1a + k1b + k2_rows + k3_wgrad + k4_update (fused train step, %d steps of B=%d)" % (S, B),
-                    "mfma", flops_step * S, ms, "TFLOP/s",
+                    "latency", flops_step * S, ms, "TFLOP/s",
                     load_traffic(pmc, ("k1a_kernel", "k1b_kernel", "k2_rows", "k3_wgrad", "k4_update")),
                     algorithmic_flops_per_sample=2.0 * 559_296, steps=S, batch=B,
-                    us_per_train_step=round(ms * 1e3 / S, 2))
+                    us_per_train_step=round(ms * 1e3 / S, 2),
+                    bound_note="a chain of dependent small GEMMs at B = 1,100 (PMC: MFMA busy a few %): latency-"
+                               "bound; frac is against the f32 MFMA peak (157.3 TF/s)")
 
     def cpu_baseline(sample_n):
         """The same pipeline on the host CPU (oracle/): placement, the
@@ -847,30 +850,36 @@ def setup_e2e(args, dev, rank, world, seed):
         round(p * batches) of each), featurize at the reference's cost
         structure, then the train steps of exactly those clips (50 positives +
         50 adversarials of the sample per step + 1,000 negatives, numpy fp32
-        forward / backward / Adam at B = 1,100)."""
-        from oracle.augment import augment_chain
-        from oracle.featurizer import cpu_featurize
+        forward / backward / Adam at B = 1,100). Featurization runs on a pool
+        of single-threaded worker processes, one 128-clip batch per job
+        (oracle.pipeline_cpu; the reference's feature generation also runs in
+        worker processes); the 1-thread figure is the same work timed as the
+        workers' summed busy time plus the train steps on one BLAS thread."""
+        from oracle.pipeline_cpu import featurize_pool
         from oracle import mlp as omlp
         from threadpoolctl import threadpool_limits
         gr = default_graph()
         nb_cpu = [v.numpy() for v in noise_bank(64, seed=seed + 2)]
         ir_cpu = [v.numpy() for v in impulse_responses(32, seed=seed + 3)]
-        res = {}
-        for th, m in ((host_threads(), sample_n or 512), (1, 128)):
-            # half positives, half adversarials, as the step's clips
-            rows = np.concatenate([np.arange(m // 2), half + np.arange(m - m // 2)])
-            xs, ls = src[rows].cpu().numpy(), lens[rows]
-            rng = np.random.default_rng(0)
-            with threadpool_limits(limits=th):
-                torch.set_num_threads(th)
-                cpu_featurize(xs[:4, :AUG_T], gr, threads=th)
-                t0 = time.perf_counter()
-                xa, counts = augment_chain(xs, ls, rng, nb_cpu, ir_cpu, stratify=True, fast_pitch=True)
-                emb = cpu_featurize(xa, gr, threads=th)
+        th = host_threads()
+        m = sample_n or 1024  # 8 batches of 128 (32 jobs of 32 clips): ~40 s of single-thread work
+        # half positives, half adversarials, as the step's clips
+        rows = np.concatenate([np.arange(m // 2), half + np.arange(m - m // 2)])
+        order = np.random.default_rng(0).permutation(m)  # batches mix both halves, as the device sampler's
+        rows = rows[order]
+        xs, ls = src[rows].cpu().numpy(), lens[rows]
+        emb, wall, busy, counts = featurize_pool(xs, ls, nb_cpu, ir_cpu, gr, th, seed=seed)
+        emb = emb[np.argsort(order)]  # back to [positives | adversarials]
+        steps = max(1, (m // 2) // P)
+        yy = np.concatenate([np.ones(P), np.zeros(B - P)]).astype(np.int64)
+        train_s = {}
+        for tth in (th, 1):
+            rng = np.random.default_rng(1)
+            with threadpool_limits(limits=tth):
+                torch.set_num_threads(tth)
                 params = omlp.init_params(seed=0)
                 opt = omlp.Adam(params)
-                steps = max(1, (m // 2) // P)
-                yy = np.concatenate([np.ones(P), np.zeros(B - P)]).astype(np.int64)
+                t0 = time.perf_counter()
                 for s_ in range(steps):
                     pos_ = emb[s_ * P:(s_ + 1) * P]
                     adv_ = emb[m // 2 + s_ * A:m // 2 + (s_ + 1) * A]
@@ -880,22 +889,22 @@ def setup_e2e(args, dev, rank, world, seed):
                     loss, nsel, dz = omlp.step_loss_and_dz(prob, yy)
                     grads = omlp.backward(params, cache, dz, dtype=np.float32)
                     params = opt.step(params, grads, 1e-3)
-                el = time.perf_counter() - t0
-            res[th] = (m / el, m, el, steps, counts)
-        torch.set_num_threads(host_threads())
-        th = host_threads()
-        v, m, el, steps, counts = res[th]
-        return {"value": round(v, 2), "unit": "clips/s", "cores": th, "kind": "port",
+                train_s[tth] = time.perf_counter() - t0
+        torch.set_num_threads(th)
+        el, el1 = wall + train_s[th], busy + train_s[1]
+        return {"value": round(m / el, 2), "unit": "clips/s", "cores": th, "kind": "port",
                 "cpu_model": cpu_model(),
-                "sample": f"{m} of the step's clips through oracle/: placement + the full augmentation chain "
-                          f"(7-band EQ, tanh, pitch shift [float32 torch.stft/istft + phase vocoder + sinc "
+                "sample": f"{m} of the step's clips through oracle/ on {th} single-threaded worker processes "
+                          f"(jobs of 32 clips of a 128-clip batch, oracle/pipeline_cpu.py): placement + the full augmentation "
+                          f"chain (7-band EQ, tanh, pitch shift [float32 torch.stft/istft + phase vocoder + sinc "
                           f"resample], band-stop, colored noise, gain, background noise, reverb; applied: "
                           f"{counts}) + featurize at the reference's cost structure (4 x 105 mel frames, "
-                          f"16 windows per clip, batch 64) + {steps} train steps of B={B} on those clips' "
-                          f"embeddings incl. Adam, {el:.1f} s",
-                "value_1thread": round(res[1][0], 2),
-                "sample_1thread": f"{res[1][1]} clips (same chain, {res[1][4]}) + {res[1][3]} train steps, "
-                                  f"{res[1][2]:.1f} s"}
+                          f"16 windows per clip, batch 64) in {wall:.1f} s wall, then {steps} train steps of B={B} "
+                          f"on those clips' embeddings incl. Adam ({th} BLAS threads) in {train_s[th]:.1f} s",
+                "value_1thread": round(m / el1, 2),
+                "sample_1thread": f"the same {m} clips and {steps} train steps on one thread: featurize = the "
+                                  f"workers' summed busy time {busy:.1f} s, train {train_s[1]:.1f} s",
+                "speedup_vs_1thread": round(el1 / el, 2)}
 
     def extra_rooflines():
         """Untimed, after the measurement: the embedding on the generic

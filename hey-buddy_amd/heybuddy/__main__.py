@@ -310,8 +310,11 @@ def extract(name: str, repo_id: str, directory: Optional[str], config: Optional[
         if tokenizer is not None:
             from transformers import AutoTokenizer
             t = AutoTokenizer.from_pretrained(tokenizer, local_files_only=True)
-            tok = lambda text: t(text, padding="max_length", truncation=True,  # noqa: E731
-                                 max_length=tokenizer_max_length)["input_ids"]
+            # BERTTokenizer(length=L) (tokens.py:53-66): ids without [CLS] / [SEP]
+            # (encode(text).ids[1:-1]), cut to L, padded with 0
+            def tok(text):
+                ids = list(t(text, add_special_tokens=False)["input_ids"])[:tokenizer_max_length]
+                return ids + [0] * (tokenizer_max_length - len(ids))
         gen = pc.PrecalculatedLabeledTrainingDatasetGenerator(repo_id, transcript_key=transcript_key,
                                                               tokenizer_max_length=tokenizer_max_length,
                                                               tokenizer=tok, **kw)

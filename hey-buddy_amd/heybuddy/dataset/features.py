@@ -90,12 +90,24 @@ def _sharded(fn, n: int) -> np.ndarray:
     if world == 1:
         return fn(n).cpu().numpy()
     lo, hi = hd.clip_range(n, rank, world)
+    # every global stream the share draws from (numpy's for placement and the
+    # coins, torch's CPU generator for the augmentation parameters, python's)
+    # is offset by the rank for the share and restored afterwards: how many
+    # draws a rank makes depends on its shard, and whatever runs next (the
+    # trainer's parameter init) must see the same state on every rank
     state = np.random.get_state()
-    np.random.seed((int(state[1][0]) + 7919 * (rank + 1)) % (2 ** 32))
+    t_state = torch.random.get_rng_state()
+    p_state = random.getstate()
+    salt = (int(state[1][0]) + 7919 * (rank + 1)) % (2 ** 32)
+    np.random.seed(salt)
+    torch.random.default_generator.manual_seed(salt)  # CPU only: device generators untouched
+    random.seed(salt)
     try:
         local = fn(hi - lo)
     finally:
         np.random.set_state(state)
+        torch.random.set_rng_state(t_state)
+        random.setstate(p_state)
     return _gather_rows(local, n).cpu().numpy()
 
 

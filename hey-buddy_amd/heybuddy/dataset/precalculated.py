@@ -100,9 +100,12 @@ class PrecalculatedDatasetIterator:
             np.random.shuffle(self.indexes)
         return self
 
-    def take(self, n: int) -> np.ndarray:
+    def take(self, n: int, _depth: int = 0) -> np.ndarray:
         """The next n rows of the (shuffled) order; at the end the order is
-        reshuffled and the batch continues from its start (precalculated.py:501-536)."""
+        reshuffled and the batch continues from its start (precalculated.py:501-536).
+        Rows whose token row holds an excluded token are dropped and refilled
+        from the following rows, as the reference does (:520-533); a set whose
+        every row is excluded raises instead of recursing without end."""
         batch = self.precalculated[self.indexes[self.index:self.index + n]]
         if batch.shape[0] < n:
             self.index = n - batch.shape[0]
@@ -117,7 +120,9 @@ class PrecalculatedDatasetIterator:
                 batch = batch[keep]
             batch = batch[:, :-1]
             if batch.shape[0] < n:  # refill what the exclusion removed
-                batch = np.concatenate([batch, self.take(n - batch.shape[0])])
+                if batch.shape[0] == 0 and _depth > len(self) // max(n, 1) + 1:
+                    raise ValueError(f"{self.name}: every row contains an excluded token")
+                batch = np.concatenate([batch, self.take(n - batch.shape[0], _depth + 1)])
         self.total_taken += n
         return batch
 
@@ -161,7 +166,8 @@ def _phrase_tokens(phrase: str) -> Optional[set]:
     if path:
         from transformers import AutoTokenizer
         tok = AutoTokenizer.from_pretrained(path, local_files_only=True)
-        return set(int(t) for t in tok(text)["input_ids"])
+        # the reference's BERTTokenizer drops [CLS] / [SEP] (tokens.py:57: ids[1:-1])
+        return set(int(t) for t in tok(text, add_special_tokens=False)["input_ids"])
     logger.warning(f"no local tokenizer (HEYBUDDY_EXCLUDE_TOKENIZER): rows containing {phrase!r} are not excluded")
     return None
 

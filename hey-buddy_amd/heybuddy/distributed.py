@@ -64,3 +64,17 @@ def reduce_bucket(bucket: torch.Tensor, group: Optional[dist.ProcessGroup] = Non
     if dist.is_available() and dist.is_initialized() and (dist.get_world_size(group) > 1 or force_reduce()):
         dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=group)
     return bucket
+
+
+def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
+    """Overwrite t with rank src's copy on every rank (in place; a device tensor
+    goes through the host on gloo). No-op without a process group."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return t
+    if dist.get_backend() == "gloo" and t.device.type != "cpu":
+        h = t.detach().cpu()
+        dist.broadcast(h, src)
+        t.copy_(h)
+    else:
+        dist.broadcast(t, src)
+    return t

@@ -281,20 +281,21 @@ def _replace_nan_rows(emb: torch.Tensor) -> torch.Tensor:
 
 
 def replace_nan_rows_device(emb: torch.Tensor, out: torch.Tensor,
-                            generator: Optional[torch.Generator] = None) -> torch.Tensor:
+                            generator: Optional[torch.Generator] = None, zero_row: bool = False) -> torch.Tensor:
     """The NaN replacement of embeddings.py:213-227 with no host
     synchronisation, for pipelined featurization: every clip (row of emb
     [n, ...]) holding a NaN takes the embeddings of a uniformly drawn NaN-free
     clip (device RNG in place of np.random.choice), all zeros when every clip
     is NaN; the result is gathered into out (same shape, not emb). The
     reference's warning needs the count on the host and is not emitted here
-    (_replace_nan_rows is the logging form). emb may carry one extra all-zero
-    row (n + 1 rows for out's n): the all-NaN case then gathers it instead of a
-    masked fill over the whole output (one pass less)."""
+    (_replace_nan_rows is the logging form). zero_row=True: emb carries one
+    extra row (n + 1 rows for out's n) that the CALLER keeps all zero; the
+    all-NaN case then gathers it instead of a masked fill over the whole output
+    (one pass less)."""
     n = out.shape[0]
-    ext = emb.shape[0] == n + 1
-    if not ext and emb.shape[0] != n:
-        raise ValueError("emb must have out's rows (or one extra zero row)")
+    ext = bool(zero_row)
+    if emb.shape[0] != n + (1 if ext else 0):
+        raise ValueError("emb must have out's rows (plus the zero row when zero_row=True)")
     rows = emb.reshape(emb.shape[0], -1)
     bad = rows[:n].amax(dim=1).isnan()  # amax propagates NaN: one reduction pass, no bool plane
     order = torch.argsort(bad.to(torch.uint8), stable=True)  # NaN-free clips first

@@ -766,6 +766,9 @@ class ReverbPlan:
     background-noise mix + IR reverb for clips of 23,040 samples."""
 
     T = 23040
+    # colored noise: the group path (one coloured second per group, 64 KB of
+    # workspace each) only for groups of at least this many clips
+    COLORED_GROUP_MIN = 8
 
     def __init__(self, device: torch.device | int | None = None) -> None:
         self.device = _native.require_device(device)
@@ -895,8 +898,9 @@ class ReverbPlan:
 
         # clips_per_noise > 1: each group's coloured second is made once (hbk_colored_noise_ws)
         ws_bytes = int(lib().hbk_colored_noise_workspace_size(n, int(clips_per_noise)))
-        if os.environ.get("HBK_COLORED_NO_GROUP") or ws_bytes > (1 << 30):
-            ws_bytes = 0  # A/B switch; and tiny groups over huge n are not worth 64 KB per group
+        if (os.environ.get("HBK_COLORED_NO_GROUP") or ws_bytes > (1 << 30)
+                or int(clips_per_noise) < self.COLORED_GROUP_MIN):
+            ws_bytes = 0  # A/B switch; small groups are not worth 64 KB of resident workspace each
         ws = None
         if ws_bytes > 0:
             ws = self._cn_ws

@@ -27,6 +27,7 @@ placement in time changes. How the two streams share the CUs is a policy:
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 from typing import List, Optional, Tuple
 
@@ -69,19 +70,59 @@ class _MaskedStream:
         self.cus = list(cus)
         self.device = device
         _MASKS[handle.value] = self.cus
+        _LIVE[id(self)] = self
+        _register_teardown()
+
+    def destroy(self) -> None:
+        """Synchronise and destroy the stream (idempotent). Called by __del__
+        while the interpreter runs, and for every live stream by the atexit hook
+        (_teardown), i.e. while the HIP runtime is still up: a hipStreamDestroy
+        left to module teardown ran after the runtime (and rocprofv3's tool
+        library) had begun shutting down and crashed in __cxa_finalize."""
+        h, self.handle = self.handle, None
+        _LIVE.pop(id(self), None)
+        if not h or not h.value or _SHUTDOWN[0]:
+            return
+        _MASKS.pop(h.value, None)
+        self.stream.synchronize()  # this stream only: no device-wide stall
+        self._lib.hbk_stream_destroy(h)
 
     def __del__(self):
         try:
-            if self.handle:
-                _MASKS.pop(self.handle.value, None)
-                self.stream.synchronize()  # this stream only: no device-wide stall
-                self._lib.hbk_stream_destroy(self.handle)
+            self.destroy()
         except Exception:
             pass
 
 
 _MASKS: dict = {}  # raw stream handle -> its CU set (the live _MaskedStreams)
 _CAPTURE: dict = {}  # (device, CU set) -> the one masked capture stream kept for it
+_LIVE: dict = {}  # id -> every _MaskedStream not yet destroyed
+_SHUTDOWN = [False]
+_REGISTERED = [False]
+
+
+def _teardown() -> None:
+    """atexit: drain the device, then destroy every live masked stream while the
+    HIP runtime is alive; later __del__ calls (module teardown) do nothing."""
+    try:
+        if _LIVE:
+            torch.cuda.synchronize()
+        _CAPTURE.clear()
+        for ms in list(_LIVE.values()):
+            try:
+                ms.destroy()
+            except Exception:
+                pass
+    finally:
+        _SHUTDOWN[0] = True
+
+
+def _register_teardown() -> None:
+    # registered at the first masked stream, i.e. after torch's own atexit
+    # hooks, so it runs before them (atexit is LIFO)
+    if not _REGISTERED[0]:
+        _REGISTERED[0] = True
+        atexit.register(_teardown)
 
 
 def masked_stream(device: torch.device, cus) -> "_MaskedStream":

@@ -70,6 +70,10 @@ class Trainer(nn.Module):
         self.learning_rate = learning_rate
         self.optimizer = torch.optim.Adam(self.model.parameters(), lr=learning_rate)
         self._init_state()
+        # data-parallel: every rank starts from rank 0's initial weights (the
+        # identical all-reduced Adam updates then keep them identical)
+        with torch.no_grad():
+            distributed.broadcast_(self.model.flat_parameters)
 
     def create_model(self, **kwargs: Any) -> nn.Module:
         raise NotImplementedError()

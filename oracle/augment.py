@@ -478,14 +478,33 @@ def place(clip, length: int, T: int, rng) -> np.ndarray:
     return out
 
 
+COIN_KINDS = ("pitch", "bandstop", "colored", "gain", "noise", "reverb")
+
+
+def stratified_coins(rng, nb: int, p_pitch=0.25, p_bandstop=0.25, p_colored=0.25, p_gain=1.0, p_noise=0.75,
+                     p_reverb=0.75):
+    """augment_chain's per-batch coins for nb batches, each kind on exactly
+    round(p * nb) batches (a random subset)."""
+    out = {}
+    for k, p in zip(COIN_KINDS, (p_pitch, p_bandstop, p_colored, p_gain, p_noise, p_reverb)):
+        on = np.zeros(nb, bool)
+        on[rng.permutation(nb)[:int(round(p * nb))]] = True
+        out[k] = on
+    return out
+
+
 def augment_chain(src, lengths, rng, noise_bank, irs, T: int = 23040, batch: int = 128,
                   p_eq=0.25, p_tanh=0.25, p_pitch=0.25, p_bandstop=0.25, p_colored=0.25, p_gain=1.0,
-                  p_noise=0.75, p_reverb=0.75, stratify: bool = False, fast_pitch: bool = False):
+                  p_noise=0.75, p_reverb=0.75, stratify: bool = False, fast_pitch: bool = False,
+                  coins_given=None, batch0: int = 0):
     """src [n, >= T] utterances with valid lengths -> augmented [n, T] float32.
     Per-batch coins from ``rng``; stratify=True turns each per-batch coin into
     exactly round(p * n_batches) batches (a random subset), so a small sample
     carries the chain's expected cost; fast_pitch: the float32 torch pitch
     shift (the reference's own cost) instead of the float64 restatement.
+    coins_given: {"pitch", "bandstop", "colored", "gain", "noise", "reverb"} ->
+    per-batch booleans decided by the caller (a worker's share of a larger
+    sample, whose first batch is global batch ``batch0``; stratified_coins).
     Returns (y, counts of applied stages)."""
     n = len(src)
     x = np.stack([place(src[i], int(lengths[i]), T, rng) for i in range(n)])
@@ -508,10 +527,13 @@ def augment_chain(src, lengths, rng, noise_bank, irs, T: int = 23040, batch: int
             return on
         return rng.random(nb) < p
 
-    c_pitch, c_bs, c_col, c_gain, c_noise, c_rev = (coins(p) for p in (p_pitch, p_bandstop, p_colored, p_gain,
-                                                                       p_noise, p_reverb))
+    if coins_given is not None:
+        c_pitch, c_bs, c_col, c_gain, c_noise, c_rev = (np.asarray(coins_given[k], bool)[:nb] for k in COIN_KINDS)
+    else:
+        c_pitch, c_bs, c_col, c_gain, c_noise, c_rev = (coins(p) for p in (p_pitch, p_bandstop, p_colored, p_gain,
+                                                                           p_noise, p_reverb))
     ring = np.concatenate([np.asarray(v, np.float32) for v in noise_bank])
-    ring_pos = 0
+    ring_pos = (batch0 * batch * T) % ring.size
     shifts = ((125, 128), (128, 125))
     for b in range(nb):
         sl = slice(b * batch, min(n, (b + 1) * batch))
@@ -535,7 +557,7 @@ def augment_chain(src, lengths, rng, noise_bank, irs, T: int = 23040, batch: int
             ring_pos = (ring_pos + m * T) % ring.size
             snr = rng.uniform(-10, 15, m)
         if c_rev[b]:
-            ir = np.asarray(irs[b % len(irs)], np.float64)
+            ir = np.asarray(irs[(batch0 + b) % len(irs)], np.float64)
         x[sl] = augment_batch(y, noise, snr, ir, gain=gain).astype(np.float32)
     for k, v in (("pitch", c_pitch), ("bandstop", c_bs), ("colored", c_col), ("gain", c_gain),
                  ("noise", c_noise), ("reverb", c_rev)):

@@ -323,6 +323,7 @@ def test_colored_noise_parity():
     # group path (hbk_colored_noise_ws): f_decay shared within each group -> one coloured second per
     # group, bit-identical to colouring each clip's own copy of its group's noise
     xt = torch.from_numpy(x).float().cuda()
+    plan.COLORED_GROUP_MIN = 1  # the product takes the group path from 8 clips per group
     fd_g = torch.tensor([0.5, 0.5, 1.3, 1.3, -1.0])
     out3 = plan.colored_noise(xt, fd_g, torch.from_numpy(snr), white=torch.from_numpy(w[:3]).cuda(),
                               clips_per_noise=2)

@@ -83,3 +83,52 @@ def test_dp_bucket_allreduce_equals_full_batch():
     # stratified shards and a complete clip partition
     assert res[0][3] + res[1][3] == 150 and res[0][4] == res[1][4] == 25
     assert res[0][2] == (0, 501) and res[1][2] == (501, 1003)
+
+
+def _init_worker(rank, world, port, q, tmp):
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "hey-buddy_amd")]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(1234)
+    np.random.seed(1234)
+    from heybuddy.dataset.features import _sharded
+    from heybuddy.trainer import WakeWordTrainer
+
+    def fn(m):  # a shard's draws: how many depends on the shard (and the rank)
+        torch.rand(1000 * (rank + 1) + m)
+        np.random.rand(37 * (rank + 1))
+        return torch.zeros((m, 16, 96))
+
+    feats = _sharded(fn, 11)
+    after = (torch.rand(4).tolist(), float(np.random.rand()))
+    tr = WakeWordTrainer(checkpoint_dir=os.path.join(tmp, f"ck{rank}"), device="cpu")
+    flat_shared = tr.model.flat_parameters.clone()
+    # a rank whose generator differs on its own: the broadcast from rank 0 still aligns the weights
+    torch.manual_seed(99 + rank)
+    tr2 = WakeWordTrainer(checkpoint_dir=os.path.join(tmp, f"ck{rank}b"), device="cpu")
+    q.put((rank, feats.shape, after, flat_shared.numpy(), tr2.model.flat_parameters.clone().numpy()))
+    dist.destroy_process_group()
+
+
+def test_dp_ranks_start_from_the_same_weights(tmp_path):
+    """the sharded feature generation restores every global
+    RNG stream (numpy, torch CPU, python) it offset per rank, and the trainer
+    broadcasts rank 0's initial parameters, so data-parallel ranks start from
+    identical weights."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_init_worker, args=(r, 2, port, q, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in procs], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][1] == res[1][1] == (11, 16, 96)
+    assert res[0][2] == res[1][2]  # the callers' RNG streams are the same after the sharded call
+    np.testing.assert_array_equal(res[0][3], res[1][3])
+    np.testing.assert_array_equal(res[0][4], res[1][4])
+    assert np.abs(res[0][4]).sum() > 0

@@ -85,3 +85,28 @@ def test_load_to_device_hbm(tmp_path):
     t = load_to_device(p, torch.device("cuda", 0), dtype=torch.float32, chunk_rows=512)
     assert t.is_cuda and t.dtype == torch.float32
     np.testing.assert_array_equal(t.cpu().numpy(), x.astype(np.float32))
+
+
+def test_labeled_take_excludes_phrase_tokens(tmp_path):
+    """PrecalculatedDatasetIterator.take on a labeled [N, 17, 96] set (ref
+    precalculated.py:520-533): rows whose token row holds an excluded id are
+    dropped and refilled from the following rows; the token row is cut off;
+    a set whose every row is excluded raises instead of recursing."""
+    from heybuddy.dataset.precalculated import PrecalculatedDatasetIterator
+    np.random.seed(0)
+    n = 40
+    arr = np.zeros((n, 17, 96), np.float32)
+    arr[:, :16] = np.arange(n, dtype=np.float32)[:, None, None]  # row id in the features
+    arr[:, 16, :3] = [[7592, 2088 if i % 3 == 0 else 3000, 0] for i in range(n)]
+    np.save(tmp_path / "lab.npy", arr)
+    it = PrecalculatedDatasetIterator("lab", directory=str(tmp_path), labeled=True, exclude_tokens=[2088])
+    got = np.concatenate([it.take(8) for _ in range(10)])
+    assert got.shape == (80, 16, 96)
+    ids = got[:, 0, 0].astype(int)
+    assert not np.any(ids % 3 == 0) and set(ids) == {i for i in range(n) if i % 3}
+    it2 = PrecalculatedDatasetIterator("lab", directory=str(tmp_path), labeled=True, exclude_tokens=[7592])
+    with pytest.raises(ValueError):
+        it2.take(8)
+    # the phrase tokens drop [CLS] / [SEP] (ref tokens.py:57), so a token row with them is not excluded
+    dev = it.to_device("cpu")
+    assert dev.shape == (n - len(range(0, n, 3)), 16, 96)

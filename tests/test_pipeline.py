@@ -55,10 +55,12 @@ def test_replace_nan_rows_device_cpu_semantics():
     # with an extra zero row: the same result, the all-NaN case gathers the zero row
     ext = torch.cat([e, torch.zeros(1, 16, 96)])
     out2 = torch.empty_like(e)
-    replace_nan_rows_device(ext, out2, generator=torch.Generator().manual_seed(1))
+    replace_nan_rows_device(ext, out2, generator=torch.Generator().manual_seed(1), zero_row=True)
     assert torch.equal(out2, out)
     allnan_ext = torch.cat([allnan, torch.zeros(1, 16, 96)])
-    assert (replace_nan_rows_device(allnan_ext, torch.empty_like(allnan)) == 0).all()
+    assert (replace_nan_rows_device(allnan_ext, torch.empty_like(allnan), zero_row=True) == 0).all()
+    with pytest.raises(ValueError):  # an extra row is only taken when declared
+        replace_nan_rows_device(ext, torch.empty_like(e))
     # +-inf without NaN is not a NaN row
     inf_row = e.clone()
     inf_row[4, 0, 0], inf_row[4, 0, 1] = float("inf"), -float("inf")
