@@ -92,6 +92,10 @@ def parse():
                     help="with --embed-split K: this fraction of each chunk's clips is split after K - 1 "
                          "chains instead (a finer balance of the two streams; default 3 / 0.4: p2s of 60 %% "
                          "of the clips on the featurize stream, measured 900-904 k vs 883 k clips/s at 2 / 0)")
+    ap.add_argument("--validation-steps", type=int, default=250,
+                    help="config 5: the reference's validation + testing passes every this many stage steps "
+                         "(DEFAULT_VALIDATION_STEPS, trainer.py:496-566; 0 = off): 500 batches of 50 + 1,000 "
+                         "validation rows and 500 of 50 + 50 testing rows, dynamic negative weight on the device")
     ap.add_argument("--stage-steps", type=int, default=2,
                     help="overlapped runs: sequential (untimed) steps that time the stages for the rooflines")
     ap.add_argument("--pmc", default=None,
@@ -595,9 +599,40 @@ def setup_e2e(args, dev, rank, world, seed):
     tr = WakeWordTrainer(checkpoint_dir="/tmp/hb_bench_ck", device=dev)
     tr.model.train()  # dropout 0.1 stays on, as in the reference
     steps_total = 5000  # stage-1 LR schedule (warmup 1000, hold 1666, cosine)
-    lr = tr.get_learning_rate(np.arange(S) + 1000, warmup_steps=1000, hold_steps=1666, total_steps=steps_total)
+    STEP0 = 1000  # a chunk's steps are stage steps STEP0 .. STEP0 + S - 1
+    lr = tr.get_learning_rate(np.arange(S) + STEP0, warmup_steps=1000, hold_steps=1666, total_steps=steps_total)
     sched = torch.from_numpy(np.stack([lr, np.ones(S)], 1).astype(np.float32)).to(dev)
     hist = torch.zeros((S, 8), dtype=torch.float32, device=dev)
+    # the reference validates (and tests) after every stage step g > 0 with g % validation_steps == 0
+    # (trainer.py:496): local steps s of the chunk with (STEP0 + s) % V == 0
+    V = args.validation_steps
+    val_after = [s_ for s_ in range(S) if V > 0 and (STEP0 + s_) > 0 and (STEP0 + s_) % V == 0]
+    ev = None
+    if val_after:
+        from heybuddy.kernels import place_clips
+        from heybuddy.trainer import EvalPasses
+        n_eval = 25_000  # DEFAULT_VALIDATION_SAMPLES / DEFAULT_TESTING_*_SAMPLES (constants.py:107-109)
+
+        def featurize_pool(x):
+            out = torch.empty((x.shape[0], len(WINDOW_STARTS), 96), dtype=torch.float32, device=dev)
+            ext = torch.zeros((x.shape[0] + 1, len(WINDOW_STARTS), 96), dtype=torch.float32, device=dev)
+            embed_clips(mel_frames(x, mplan, N_FRAMES), eplan, out=ext[:x.shape[0]])
+            replace_nan_rows_device(ext, out=out, zero_row=True)
+            return out
+
+        # validation positives: un-augmented, centre-padded wake-phrase clips (get_validation_features,
+        # features.py:413-427); validation negatives: the hosted validation set's stand-in (f16)
+        vsrc, vlen = speech_clips("hello world", n_eval, seed=seed + 5, device=dev)
+        vpre = np.maximum((AUG_T - np.asarray(vlen)) // 2, 0).astype(np.int32)
+        vpos = featurize_pool(place_clips(vsrc, np.asarray(vlen, np.int32), vpre, AUG_T))
+        del vsrc
+        gv = torch.Generator(device=dev).manual_seed(seed + 6)
+        vneg = torch.randn((n_eval, 16, 96), generator=gv, device=dev).half()
+        # testing: augmented positive / adversarial features (TrainingFeaturesGenerator, testing=True)
+        tpos = featurize_pool(aug.augment_device(src[:n_eval], lens[:n_eval]))
+        tadv = featurize_pool(aug.augment_device(src[half:half + n_eval], lens[half:half + n_eval]))
+        ev = EvalPasses(tr, vpos, vneg, tpos, tadv, seed=seed + 7)
+        torch.cuda.synchronize(dev)
     stream = torch.cuda.current_stream(dev)
     stages = ["augment", "mel", "embed", "train"]
     neg_pos = [0]
@@ -616,6 +651,36 @@ def setup_e2e(args, dev, rank, world, seed):
         k = torch.arange(S * NM, device=dev, dtype=torch.int64)
         idx[:, P + A + NL:] = (-1 - n_large - ((o + k) % (n_neg - n_large))).to(torch.int32).view(S, NM)
         neg_pos[0] = (o + S * NL) % n_large
+
+    eval_events = []  # per staged step: (start, end) events of its evaluation passes
+
+    def train_chunk(pool_b, evs=None):
+        """The chunk's S stage steps on pool_b, with the evaluation passes after
+        the validation steps (all on the current stream, no host sync)."""
+        stream_ = torch.cuda.current_stream(dev)
+        sample()
+        tr._reset_accumulation()
+        if not val_after:
+            tr.train_indexed(idx, y, sched, pool32=pool_b, pool16=neg, history=hist, steps_per_graph=50)
+            return
+        # the dynamic negative weight carries over from the previous chunk's last validation
+        sched[:, 1].copy_(sched[S - 1:S, 1].expand(S))
+        done = 0
+        for v_ in val_after:
+            tr.train_indexed(idx, y, sched, pool32=pool_b, pool16=neg, history=hist, steps_per_graph=50,
+                             n_steps=v_ + 1 - done, continued=done > 0)
+            done = v_ + 1
+            if evs is not None:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record(stream_)
+            ev.run(sched, next_step=done)
+            if evs is not None:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record(stream_)
+                evs.append((e0, e1))
+        if done < S:
+            tr.train_indexed(idx, y, sched, pool32=pool_b, pool16=neg, history=hist, steps_per_graph=50,
+                             n_steps=S - done, continued=True)
 
     sub_events = []   # per staged step: (sub-stage, start, end) events of the augment chain
     plan_counts = []  # per staged step: clips each augmentation was applied to
@@ -646,9 +711,8 @@ def setup_e2e(args, dev, rank, world, seed):
         replace_nan_rows_device(raw_ext, out=pool, zero_row=True)  # no host sync
         if evs:
             evs[3].record(stream)
-        sample()
-        tr._reset_accumulation()
-        tr.train_indexed(idx, y, sched, pool32=pool, pool16=neg, history=hist, steps_per_graph=50)
+        eval_events.append([])
+        train_chunk(pool, eval_events[-1] if evs else None)
         if evs:
             evs[4].record(stream)
 
@@ -750,9 +814,7 @@ def setup_e2e(args, dev, rank, world, seed):
             with torch.cuda.stream(ts):
                 ts.wait_event(feat_done[b])
                 e0 = mark("train", ts)
-                sample()
-                tr._reset_accumulation()
-                tr.train_indexed(idx, y, sched, pool32=pools[b], pool16=neg, history=hist, steps_per_graph=50)
+                train_chunk(pools[b])
                 train_done[b].record(ts)
             if K:
                 featurize_back(c + 1)
@@ -806,8 +868,20 @@ def setup_e2e(args, dev, rank, world, seed):
                 m = cnt.get(name, n)
                 out.append(roof(kname, "hbm", bpc * m, sub_ms[name], "GB/s", load_traffic(pmc, subs),
                                 algorithmic_bytes_per_clip=bpc, bytes_basis=basis, clips=round(m)))
+        ev_ms = 0.0
+        staged_ev = [e for e in eval_events if e]
+        if staged_ev:
+            ev_ms = sum(a.elapsed_time(b) for evl in staged_ev for a, b in evl) / len(staged_ev)
+            rows = ev.rows_per_pass * len(val_after)
+            out.append(roof("kv_gemm_kernel + k2_rows_kernel<false> (+ kv_prep / kv_finish): the validation and "
+                            "testing passes, %d per chunk of %d rows each (dropout on)" % (len(val_after),
+                                                                                           ev.rows_per_pass),
+                            "mfma", 2.0 * 251_968 * rows, ev_ms, "TFLOP/s",
+                            load_traffic(pmc, ("kv_gemm", "kv_prep", "kv_finish")), peak=SPLIT_PEAK_TFLOPS,
+                            peak_basis="f16 dense MFMA peak / 3 (split-f16 products; f16 pool rows need 2)",
+                            algorithmic_flops_per_row=2.0 * 251_968, rows=rows))
         for name in ("augment", "mel", "embed", "train"):
-            out.append(roofline(name, stage_ms[name], pmc))
+            out.append(roofline(name, stage_ms[name] - (ev_ms if name == "train" else 0.0), pmc))
         return out
 
     def roofline(name, ms, pmc):
@@ -871,6 +945,7 @@ def setup_e2e(args, dev, rank, world, seed):
         emb, wall, busy, counts = featurize_pool(xs, ls, nb_cpu, ir_cpu, gr, th, seed=seed)
         emb = emb[np.argsort(order)]  # back to [positives | adversarials]
         steps = max(1, (m // 2) // P)
+        eval_rows = int(round(ev.rows_per_pass * steps / V)) if ev is not None else 0
         yy = np.concatenate([np.ones(P), np.zeros(B - P)]).astype(np.int64)
         train_s = {}
         for tth in (th, 1):
@@ -889,6 +964,12 @@ def setup_e2e(args, dev, rank, world, seed):
                     loss, nsel, dz = omlp.step_loss_and_dz(prob, yy)
                     grads = omlp.backward(params, cache, dz, dtype=np.float32)
                     params = opt.step(params, grads, 1e-3)
+                # the evaluation passes' share of these steps: rows_per_pass x steps / validation_steps
+                # forward rows (dropout on, the reference's validation loop without .eval())
+                for r0_ in range(0, eval_rows, 4096):
+                    xr = rng.standard_normal((min(4096, eval_rows - r0_), 16, 96)).astype(np.float32)
+                    xr *= (rng.random(xr.shape) >= 0.1) / np.float32(0.9)
+                    omlp.forward(params, xr, dtype=np.float32)
                 train_s[tth] = time.perf_counter() - t0
         torch.set_num_threads(th)
         el, el1 = wall + train_s[th], busy + train_s[1]
@@ -900,7 +981,8 @@ def setup_e2e(args, dev, rank, world, seed):
                           f"resample], band-stop, colored noise, gain, background noise, reverb; applied: "
                           f"{counts}) + featurize at the reference's cost structure (4 x 105 mel frames, "
                           f"16 windows per clip, batch 64) in {wall:.1f} s wall, then {steps} train steps of B={B} "
-                          f"on those clips' embeddings incl. Adam ({th} BLAS threads) in {train_s[th]:.1f} s",
+                          f"on those clips' embeddings incl. Adam and the evaluation passes' share ({eval_rows} "
+                          f"forward rows) ({th} BLAS threads) in {train_s[th]:.1f} s",
                 "value_1thread": round(m / el1, 2),
                 "sample_1thread": f"the same {m} clips and {steps} train steps on one thread: featurize = the "
                                   f"workers' summed busy time {busy:.1f} s, train {train_s[1]:.1f} s",
@@ -954,6 +1036,13 @@ def setup_e2e(args, dev, rank, world, seed):
                                         args.train_batch == "global" and world > 1 else
                                         "per-rank: 1,100 per rank (global batch 1,100 x N)"),
                    "negative_pool": f"{n_neg} x [16,96] f16",
+                   "validation": ("off" if not val_after else
+                                  f"every {V} stage steps (stage steps {STEP0}..{STEP0 + S - 1}: after local steps "
+                                  f"{val_after}): validation = 500 batches of 50 positives (25,000 un-augmented "
+                                  f"features) + 1,000 negatives (25,000 f16), testing = 500 batches of 50 positives "
+                                  f"+ 50 adversarial (25,000 each, augmented); dropout on; counts, false positives "
+                                  f"per hour and the dynamic negative weight (x2 above 1.5 / h, /2 floor 1) on the "
+                                  f"device; {ev.rows_per_pass} rows per pass"),
                    "parallelism": f"dp{world} (clip shards; 1 all-reduce of the 1,025,700-B bucket per train step)",
                    "schedule": ("sequential: featurize(s) then train(s)" if args.overlap == "off" else
                                 f"pipelined (heybuddy.pipeline {args.overlap}): featurize(s + 1) on one stream while "

@@ -691,7 +691,7 @@ int hbk_mlp_step_fwd_bwd(const hbk_mlp_plan* p, const float* params, const float
   if (ws_bytes < mlp_fused_ws_floats(*p, batch) * int64_t(sizeof(float))) return arg_error("workspace too small");
   if (n32 < 0 || n16 < 0) return arg_error("negative pool size");
   if (!idx && n32 < batch) return arg_error("idx NULL: pool32 must hold the batch rows");
-  if (flags & ~(HBK_STEP_XHAT_READY | HBK_STEP_PREFETCH_NEXT | HBK_STEP_WEIGHTS_READY))
+  if (flags & ~(HBK_STEP_XHAT_READY | HBK_STEP_PREFETCH_NEXT | HBK_STEP_WEIGHTS_READY | HBK_STEP_DEFER_PARTIALS))
     return arg_error("unknown flags");
   if (!pool32 && !pool16) return arg_error("no embedding pool");
   return mlp_fused_run(*p, params, pool32, n32, pool16, n16, idx, idx_step_stride, idx_steps, y, y_step_stride,
@@ -715,6 +715,60 @@ int hbk_mlp_step_update(const hbk_mlp_plan* p, float* params, float* bucket, flo
   return mlp_fused_update(*p, params, bucket, m, v, state, parity, sched,
                           static_cast<int>(std::min<int64_t>(sched_len, 1 << 30)), lr, beta1, beta2, eps, history,
                           history ? history_cap : 0, static_cast<float*>(workspace), as_stream(stream));
+}
+
+int hbk_mlp_eval_workspace_size(const hbk_mlp_plan* p, int64_t rows, int64_t* bytes) {
+  using namespace hbk;
+  if (!p || !bytes) return arg_error("NULL");
+  if (!mlp_fused_supported(*p)) {
+    set_error("hbk: the evaluation pass covers the fused plans (d_in 1536, layer 96, hidden 64, <= 4 layers)");
+    return HBK_ERR_UNSUPPORTED;
+  }
+  *bytes = mlp_eval_ws_floats(*p, std::max<int64_t>(rows, 1)) * int64_t(sizeof(float));
+  return HBK_OK;
+}
+
+int hbk_mlp_eval_prepare(const hbk_mlp_plan* p, const float* params, void* workspace, int64_t ws_bytes,
+                         void* stream) {
+  using namespace hbk;
+  if (!p || !params || !workspace) return arg_error("NULL pointer");
+  if (!mlp_fused_supported(*p)) {
+    set_error("hbk: the evaluation pass covers the fused plans");
+    return HBK_ERR_UNSUPPORTED;
+  }
+  if (ws_bytes < mlp_eval_ws_floats(*p, 1) * int64_t(sizeof(float))) return arg_error("workspace too small");
+  return mlp_eval_prepare(*p, params, static_cast<float*>(workspace), as_stream(stream));
+}
+
+int hbk_mlp_eval_count(const hbk_mlp_plan* p, const float* params, const void* pool, int32_t pool_is_f16,
+                       int64_t n_pool, const int32_t* idx, int64_t rows, int64_t row_offset, int32_t label,
+                       float activation_threshold, float dropout_p, uint64_t seed, float* counts, float* prob,
+                       void* workspace, int64_t ws_bytes, void* stream) {
+  using namespace hbk;
+  if (!p || !params || !workspace || !counts) return arg_error("NULL pointer");
+  if (!mlp_fused_supported(*p)) {
+    set_error("hbk: the evaluation pass covers the fused plans");
+    return HBK_ERR_UNSUPPORTED;
+  }
+  if (rows < 0 || row_offset < 0 || rows + row_offset > (int64_t(1) << 31) / 768) return arg_error("rows out of range");
+  if (rows == 0) return HBK_OK;
+  if (!pool || n_pool <= 0) return arg_error("empty pool");
+  if (label != 0 && label != 1) return arg_error("label must be 0 or 1");
+  if (dropout_p < 0.f || dropout_p >= 1.f) return arg_error("dropout_p must be in [0, 1)");
+  if (ws_bytes < mlp_eval_ws_floats(*p, rows) * int64_t(sizeof(float))) return arg_error("workspace too small");
+  return mlp_eval_count(*p, params, pool, pool_is_f16 != 0, n_pool, idx, rows, row_offset, label,
+                        activation_threshold, dropout_p, seed, counts, prob, static_cast<float*>(workspace),
+                        as_stream(stream));
+}
+
+int hbk_mlp_eval_finish(const float* counts_val, const float* counts_test, const double* sizes,
+                        float target_false_positives_per_hour, float adjust_ratio, float* sched, int64_t sched_len,
+                        int64_t next_step, float* out, void* stream) {
+  using namespace hbk;
+  if (!sizes) return arg_error("sizes is NULL");
+  if (sched && (sched_len <= 0 || next_step < 0)) return arg_error("schedule range");
+  return mlp_eval_finish(counts_val, counts_test, sizes, target_false_positives_per_hour, adjust_ratio, sched,
+                         sched_len, next_step, out, as_stream(stream));
 }
 
 }  // extern "C"

@@ -624,6 +624,10 @@ struct K2Args {
   // weight cache (WSplit): hi planes of W_o_k / W_hg_k as stored and transposed
   const _Float16* wc;
   int64_t c_o[kMaxG], c_hg[kMaxG], c_oT[kMaxG], c_hgT[kMaxG];
+  // inference only (evaluation passes): counts[2 label] += #(p >= act_thr),
+  // counts[2 label + 1] += #(p > act_thr) over the live rows (float counters)
+  float* counts;
+  int count_label;
 };
 
 #ifdef HBK_TRACE
@@ -899,6 +903,20 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
       }
     }
     dzS[r] = dz;
+    if (!kTrain && a.counts) {  // evaluation pass: predictions at the activation threshold
+      float pge = 0.f, pgt = 0.f;
+      if (r < nrow) {
+        const float p = sigm(zS[r]);
+        pge = p >= a.act_thr ? 1.f : 0.f;
+        pgt = p > a.act_thr ? 1.f : 0.f;
+      }
+      pge = rsum16(pge);
+      pgt = rsum16(pgt);
+      if (tid == 0) {
+        if (pge != 0.f) atomicAdd(a.counts + 2 * a.count_label, pge);
+        if (pgt != 0.f) atomicAdd(a.counts + 2 * a.count_label + 1, pgt);
+      }
+    }
     if (kTrain) {
 #pragma unroll
       for (int s = 0; s < kStats; ++s) {
@@ -1067,9 +1085,25 @@ constexpr int kK3StepsNarrow = 4, kK3NarrowCUs = 96;
 struct WJob {
   const float* X;  // [M][Bp]
   const float* Y;  // [N][Bp]
-  float* C;        // [M][ldc]
+  int64_t c_off;   // the gradient [M][ldc] at this offset of the parameter layout
   int ldc, M, N, tn;
 };
+// The covered parameter ranges (k3's weight gradients, norm_in's gamma / beta):
+// k3 writes them as one partial slab per batch split, part[split][n_params],
+// with plain stores (float atomics run at the memory side, ~1 TB/s chip-wide,
+// and were most of k3's time); k4 adds the slabs while it reads the bucket
+// (or k3_fold_kernel adds them into the bucket first, for the all-reduce).
+constexpr int kMaxRng = 2 + 2 * kMaxG;
+struct Ranges {
+  int n;
+  int64_t lo[kMaxRng], hi[kMaxRng];
+};
+__device__ __forceinline__ bool in_ranges(const Ranges& r, int64_t i) {
+  bool c = false;
+#pragma unroll
+  for (int k = 0; k < kMaxRng; ++k) c |= k < r.n && i >= r.lo[k] && i < r.hi[k];
+  return c;
+}
 struct K3Args {
   WJob job[kMaxJobs];
   int start[kMaxJobs + 1];
@@ -1079,8 +1113,9 @@ struct K3Args {
   const float* g_in;
   const float* b_in;
   const float* W0;
-  float* dg_in;
-  float* db_in;
+  int64_t g_off, b_off;  // norm_in gamma / beta in the parameter layout
+  float* part;           // [KS][pstride] partial slabs
+  int64_t pstride;
 };
 
 // STEPS: batch rows per split / 32 (the grid's split count follows); the launch
@@ -1101,6 +1136,7 @@ __global__ void __launch_bounds__(256) k3_wgrad_kernel(K3Args a) {
   const WJob jb = a.job[j];
   const int local = blk - a.start[j];
   const int split = local % a.KS, tile = local / a.KS;
+  float* const C = a.part + split * a.pstride + jb.c_off;
   const int tm = tile / jb.tn, tn = tile - tm * jb.tn;
   HBK_MT(2, 1);
   const int rb0 = split * kK3Rows;
@@ -1199,8 +1235,8 @@ __global__ void __launch_bounds__(256) k3_wgrad_kernel(K3Args a) {
       for (int e = 0; e < 4; ++e) {
         const int row = mrow + 16 * t + 4 * kq + e;
         if (row < jb.M) {
-          if (nok0) atomicAdd(jb.C + static_cast<int64_t>(row) * jb.ldc + n0 + m, acc[t][0][e]);
-          if (nok1) atomicAdd(jb.C + static_cast<int64_t>(row) * jb.ldc + n0 + 16 + m, acc[t][1][e]);
+          if (nok0) C[static_cast<int64_t>(row) * jb.ldc + n0 + m] = acc[t][0][e];
+          if (nok1) C[static_cast<int64_t>(row) * jb.ldc + n0 + 16 + m] = acc[t][1][e];
         }
       }
     return;
@@ -1238,12 +1274,12 @@ __global__ void __launch_bounds__(256) k3_wgrad_kernel(K3Args a) {
       if (row >= jb.M) continue;
       const float sj = sS[32 * wave + 16 * t + 4 * kq + e];
       if (nok0) {
-        atomicAdd(jb.C + static_cast<int64_t>(row) * jb.ldc + c0, g0 * acc[t][0][e] + be0 * sj);
+        C[static_cast<int64_t>(row) * jb.ldc + c0] = g0 * acc[t][0][e] + be0 * sj;
         dg0 += w0[t][e] * acc[t][0][e];
         dbt0 += w0[t][e] * sj;
       }
       if (nok1) {
-        atomicAdd(jb.C + static_cast<int64_t>(row) * jb.ldc + c1, g1 * acc[t][1][e] + be1 * sj);
+        C[static_cast<int64_t>(row) * jb.ldc + c1] = g1 * acc[t][1][e] + be1 * sj;
         dg1 += w1[t][e] * acc[t][1][e];
         dbt1 += w1[t][e] * sj;
       }
@@ -1266,9 +1302,22 @@ __global__ void __launch_bounds__(256) k3_wgrad_kernel(K3Args a) {
   if (tid < kTN) {
     const int c = n0 + tid;
     if (c < jb.N) {
-      atomicAdd(a.dg_in + c, red[0][0][tid] + red[0][1][tid] + red[0][2][tid] + red[0][3][tid]);
-      atomicAdd(a.db_in + c, red[1][0][tid] + red[1][1][tid] + red[1][2][tid] + red[1][3][tid]);
+      float* P = a.part + split * a.pstride;
+      P[a.g_off + c] = red[0][0][tid] + red[0][1][tid] + red[0][2][tid] + red[0][3][tid];
+      P[a.b_off + c] = red[1][0][tid] + red[1][1][tid] + red[1][2][tid] + red[1][3][tid];
     }
+  }
+}
+
+// Steps whose update does not get the workspace (or is preceded by the
+// data-parallel all-reduce): the slabs added into the bucket's covered ranges
+__global__ void __launch_bounds__(256) k3_fold_kernel(Ranges rg, const float* __restrict__ part, int64_t pstride,
+                                                      int ns, float* __restrict__ G, int64_t n) {
+  for (int64_t i = blockIdx.x * int64_t(256) + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
+    if (!in_ranges(rg, i)) continue;
+    float g = G[i];
+    for (int sp = 0; sp < ns; ++sp) g += part[sp * pstride + i];
+    G[i] = g;
   }
 }
 
@@ -1294,6 +1343,11 @@ struct K4Args {
   // transposed planes from LDS as 16-B column runs; the rest do everything else
   int n_tiles;
   int tile_seg[kMaxTiles], tile_r0[kMaxTiles];
+  // k3's partial slabs left for this update (ns of them; 0: none)
+  const float* part;
+  int64_t pstride;
+  int ns;
+  Ranges rg;
 };
 
 // The accumulation gate (trainer.py:443-465), computed identically by every
@@ -1346,23 +1400,43 @@ __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
   }
   float lr = a.lr;
   if (a.sched) lr = a.sched[2 * min(step, a.sched_len - 1)];
-  const float bc1 = 1.f - powf(a.b1, t), bc2s = sqrtf(1.f - powf(a.b2, t));
-  const float step_size = lr / bc1;
-  const bool on = fire != 0.f;
-  // float4 body (the bucket, params and moments are 16-B aligned torch buffers), scalar tail
   const int64_t n4 = a.n >> 2;
   f4* G4 = reinterpret_cast<f4*>(a.G);
   f4* P4 = reinterpret_cast<f4*>(a.P);
   f4* M4 = reinterpret_cast<f4*>(a.m);
   f4* V4 = reinterpret_cast<f4*>(a.v);
   const f4 z4 = {0.f, 0.f, 0.f, 0.f};
+  const int ns = a.part ? a.ns : 0;
+  const f4* PT4 = reinterpret_cast<const f4*>(a.part);
+  const int64_t ps4 = a.pstride >> 2;
+  // the step's gradient of float4 i: the bucket (k2's atomics) and zero it, or, in a range
+  // covered by k3's deferred slabs (where the bucket holds zeros), the slabs' sum
+  auto grad4 = [&](int64_t i, bool covered, bool zero) -> f4 {
+    if (!covered) {
+      const f4 g = G4[i];
+      if (zero) G4[i] = z4;
+      return g;
+    }
+    f4 q[4] = {z4, z4, z4, z4};
+    int sp = 0;
+    for (; sp + 4 <= ns; sp += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) q[u] += PT4[(sp + u) * ps4 + i];
+    }
+    for (; sp < ns; ++sp) q[0] += PT4[sp * ps4 + i];
+    return (q[0] + q[1]) + (q[2] + q[3]);
+  };
+  const float bc1 = 1.f - powf(a.b1, t), bc2s = sqrtf(1.f - powf(a.b2, t));
+  const float step_size = lr / bc1;
+  const bool on = fire != 0.f;
+  // float4 body (the bucket, params and moments are 16-B aligned torch buffers), scalar tail
+
   // one float4: all four loads unconditional (issued together, no wait behind
   // the gate decision, which itself waits on the statistics); the parameters
   // after the step are returned
   auto adam4 = [&](int64_t i) -> f4 {
-    const f4 g = G4[i], m0 = M4[i], v0 = V4[i];
+    const f4 g = grad4(i, ns > 0 && in_ranges(a.rg, 4 * i), true), m0 = M4[i], v0 = V4[i];
     f4 p = P4[i];
-    G4[i] = z4;
     if (on) {
       const f4 gi = g * scale;
       const f4 mi = a.b1 * m0 + (1.f - a.b1) * gi;
@@ -1392,7 +1466,7 @@ __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
       const int q = min(static_cast<int>(threadIdx.x) + 256 * it, rows * C4 - 1);
       const int r = q / C4, c4 = q - r * C4;
       const int64_t i = (g.src + int64_t(r0 + r) * C + 4 * c4) >> 2;
-      lg_[it] = G4[i];
+      lg_[it] = grad4(i, ns > 0, false);  // the cached matrices are k3's (covered); zeroed by the owner below
       lm_[it] = M4[i];
       lv_[it] = V4[i];
       lp_[it] = P4[i];
@@ -1405,7 +1479,7 @@ __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
       const int64_t off = int64_t(r0 + r) * C + 4 * c4;
       const int64_t i = (g.src + off) >> 2;
       f4 p = lp_[it];
-      G4[i] = z4;
+      if (ns == 0) G4[i] = z4;  // (with slabs the bucket holds zeros here)
       if (on) {
         const f4 gi = lg_[it] * scale;
         const f4 mi = a.b1 * lm_[it] + (1.f - a.b1) * gi;
@@ -1453,7 +1527,9 @@ __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
     adam4(i);
   }
   for (int64_t i = 4 * n4 + b0 * 256 + threadIdx.x; i < a.n; i += nb * 256) {
-    const float g = a.G[i];
+    float g = a.G[i];
+    if (ns > 0 && in_ranges(a.rg, i))
+      for (int sp = 0; sp < ns; ++sp) g += a.part[sp * a.pstride + i];
     a.G[i] = 0.f;
     if (on) {
       const float gi = g * scale;
@@ -1466,9 +1542,287 @@ __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
   }
 }
 
+
+// ---------------------------------------------------------- evaluation ----
+// The validation / testing passes of train_epoch (trainer.py:496-566): a
+// forward with input dropout over hundreds of thousands of rows (the default
+// validation pass is 500 batches of 50 + 1,000 rows, the testing pass 500 of
+// 50 + 50), reduced to prediction counts. The input layer is a real GEMM here
+// ([rows, 1536] x [1536, 128]), so it gets a throughput kernel of its own,
+// kv_gemm: the LayerNorm is folded into the GEMM's epilogue,
+//   (LN(x) g + b) W^T = rs (x W'^T - mu c1) + c0,  W' = W o g (columns scaled),
+//   c1[n] = sum_k W'[n][k],  c0[n] = sum_k b[k] W[n][k],
+// so the product runs on the raw (dropped-out) rows: an f16 pool row is exact
+// in f16 (its hi part; no lo), two products per 32-deep block instead of
+// three. mu / rs come from the same loaded values (per-lane float sums of 8,
+// accumulated in double). W' (f16 hi / lo planes of 16 W') is staged through
+// LDS in 64-deep chunks, double-buffered, shared by 8 waves of 32 rows each;
+// the rows stream from HBM straight into MFMA A fragments, prefetched two
+// chunks ahead. The pre-bias HG0 rows go to a slab that k2_rows_kernel
+// <false> (the inference chain, with its counters) reads as its one K-split.
+constexpr int kKvRows = 256, kKvKC = 64, kKvLd = kKvKC + 8, kKvChunks = kD / kKvKC;
+struct KvArgs {
+  const void* pool;      // f32 or f16 rows of 1536
+  int64_t n_pool;
+  const int32_t* idx;    // row r -> pool row idx[r]; NULL: r0 + r modulo n_pool
+  int64_t rows, r0;      // this launch's rows; r0 = their first index in the pass (dropout counter)
+  const _Float16* wq;    // [2][128][1536] hi / lo planes of 16 W'
+  const float* c0;
+  const float* c1;
+  float drop_p;
+  uint64_t seed;
+  float* hg;             // [rows][128] pre-bias HG0
+};
+
+__global__ void __launch_bounds__(256) kv_prep_kernel(const float* __restrict__ P, int64_t w0, int64_t g_in,
+                                                      int64_t b_in, _Float16* __restrict__ wq, float* c0,
+                                                      float* c1) {
+  __shared__ double red[2][4];
+  const int n = blockIdx.x, tid = threadIdx.x;
+  const float* W = P + w0 + int64_t(n) * kD;
+  double s0 = 0.0, s1 = 0.0;
+  for (int k = 2 * tid; k < kD; k += 512) {
+    const float wa = W[k], wb = W[k + 1];
+    const float ga = wa * P[g_in + k], gb = wb * P[g_in + k + 1];
+    uint32_t hi, lo;
+    split_pair(16.f * ga, 16.f * gb, hi, lo);
+    *reinterpret_cast<uint32_t*>(wq + int64_t(n) * kD + k) = hi;
+    *reinterpret_cast<uint32_t*>(wq + int64_t(kH2) * kD + int64_t(n) * kD + k) = lo;
+    s1 += double(ga) + double(gb);
+    s0 += double(P[b_in + k]) * wa + double(P[b_in + k + 1]) * wb;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    s0 += __shfl_xor(s0, o, 64);
+    s1 += __shfl_xor(s1, o, 64);
+  }
+  if ((tid & 63) == 0) {
+    red[0][tid >> 6] = s0;
+    red[1][tid >> 6] = s1;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    c0[n] = static_cast<float>((red[0][0] + red[0][1]) + (red[0][2] + red[0][3]));
+    c1[n] = static_cast<float>((red[1][0] + red[1][1]) + (red[1][2] + red[1][3]));
+  }
+}
+
+// kF16: the rows are f16 (exact in hi); else f32 (split hi / lo)
+template <bool kF16>
+__global__ void __launch_bounds__(512) kv_gemm_kernel(KvArgs a) {
+  __shared__ __attribute__((aligned(16))) _Float16 wb[2][2][kH2][kKvLd];  // [buf][hi / lo][n][k]
+  __shared__ float stS[8][32][2];
+  constexpr int kDepth = 2;  // A chunks in flight (this one + kDepth - 1 ahead)
+  constexpr int kU = kF16 ? 1 : 2;      // 16-B loads per 8 elements
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = lane & 15, kq = lane >> 4;
+  const int64_t tile0 = int64_t(blockIdx.x) * kKvRows;
+  const char* rp[2];
+  uint32_t rid[2];
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt) {
+    const int64_t r = min(tile0 + 32 * wave + 16 * rt + m, a.rows - 1);
+    int64_t pr = a.idx ? static_cast<int64_t>(a.idx[r]) : (a.r0 + r) % a.n_pool;
+    pr = min(max(pr, int64_t(0)), a.n_pool - 1);
+    rp[rt] = static_cast<const char*>(a.pool) + pr * kD * (kF16 ? 2 : 4);
+    rid[rt] = static_cast<uint32_t>(a.r0 + r);
+  }
+  const uint64_t seed = a.seed;
+  const uint32_t s0 = static_cast<uint32_t>(seed), s1 = static_cast<uint32_t>(seed >> 32) * 0x27D4EB2Fu;
+  const uint32_t thr = static_cast<uint32_t>(a.drop_p * 65536.f + 0.5f);
+  const float keep = a.drop_p > 0.f ? 1.f / (1.f - a.drop_p) : 1.f;
+  // A ring: [slot][rt][kb][u]
+  uint4 ar[kDepth][2][2][kU];
+  auto load_a = [&](int c, int slot) {
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        const int k = kKvKC * c + 32 * kb + 8 * kq;
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+          ar[slot][rt][kb][u] = *reinterpret_cast<const uint4*>(rp[rt] + int64_t(k) * (kF16 ? 2 : 4) + 16 * u);
+      }
+  };
+  // W' chunk c: 2 planes x 128 n x 64 k = 4,096 16-B pieces, 8 per thread... (512 threads: 4)
+  uint4 wr[4];
+  auto load_w = [&](int c) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q = tid + 512 * j, pl = q >> 10, n = (q >> 3) & 127, kk = (q & 7) * 8;
+      wr[j] = *reinterpret_cast<const uint4*>(a.wq + int64_t(pl) * kH2 * kD + int64_t(n) * kD + kKvKC * c + kk);
+    }
+  };
+  auto store_w = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q = tid + 512 * j, pl = q >> 10, n = (q >> 3) & 127, kk = (q & 7) * 8;
+      *reinterpret_cast<uint4*>(&wb[buf][pl][n][kk]) = wr[j];
+    }
+  };
+#pragma unroll
+  for (int d = 0; d < kDepth; ++d) load_a(d, d);
+  load_w(0);
+  store_w(0);
+  __syncthreads();
+  f4 acc[2][8];
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+    for (int ct = 0; ct < 8; ++ct) acc[rt][ct] = f4{0.f, 0.f, 0.f, 0.f};
+  double sd1[2] = {0.0, 0.0}, sd2[2] = {0.0, 0.0};
+  static_assert(kKvChunks % kDepth == 0, "the A ring's slots must be compile-time");
+#pragma unroll 1
+  for (int cb = 0; cb < kKvChunks; cb += kDepth)
+#pragma unroll
+  for (int slot = 0; slot < kDepth; ++slot) {
+    const int c = cb + slot;
+    if (c + 1 < kKvChunks) load_w(c + 1);
+    // this chunk's A values (dropout mask, row sums, split), one 32-deep block at a time
+    const int buf = c & 1;
+    float t1[2] = {0.f, 0.f}, t2[2] = {0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      h8 ah[2], al[2];
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        float v[8];
+        if (kF16) {
+          const h8 hv = __builtin_bit_cast(h8, ar[slot][rt][kb][0]);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = static_cast<float>(hv[e]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = __builtin_bit_cast(float, (&ar[slot][rt][kb][e >> 2].x)[e & 3]);
+        }
+        if (a.drop_p > 0.f) {  // nn.Dropout's mask (the 1 / (1 - p) scale is applied after the GEMM)
+          const uint32_t base = rid[rt] * (kD / 2) + ((kKvKC * c + 32 * kb + 8 * kq) >> 1);
+#pragma unroll
+          for (int e = 0; e < 8; e += 2) {
+            const uint32_t hsh = drop_hash(s0, s1, base + (e >> 1));
+            v[e] = (hsh & 0xFFFFu) < thr ? 0.f : v[e];
+            v[e + 1] = (hsh >> 16) < thr ? 0.f : v[e + 1];
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          t1[rt] += v[e];
+          t2[rt] += v[e] * v[e];
+        }
+        if (kF16) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ah[rt][e] = static_cast<_Float16>(v[e]);  // exact
+        } else {
+          split8(f4{v[0], v[1], v[2], v[3]}, f4{v[4], v[5], v[6], v[7]}, ah[rt], al[rt]);
+        }
+      }
+#pragma unroll
+      for (int ct = 0; ct < 8; ++ct) {
+        const h8 bh = *reinterpret_cast<const h8*>(&wb[buf][0][16 * ct + m][32 * kb + 8 * kq]);
+        const h8 bl = *reinterpret_cast<const h8*>(&wb[buf][1][16 * ct + m][32 * kb + 8 * kq]);
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+          acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt], bh, acc[rt][ct], 0, 0, 0);
+          acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt], bl, acc[rt][ct], 0, 0, 0);
+          if (!kF16) acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[rt], bh, acc[rt][ct], 0, 0, 0);
+        }
+        if ((ct & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bound the B fragments in flight (registers)
+      }
+    }
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      sd1[rt] += double(t1[rt]);
+      sd2[rt] += double(t2[rt]);
+    }
+    if (c + kDepth < kKvChunks) load_a(c + kDepth, slot);
+    if (c + 1 < kKvChunks) {
+      store_w(buf ^ 1);  // its readers (chunk c - 1) passed the barrier below one iteration ago
+      __syncthreads();
+    }
+  }
+  // row statistics: the 4 lanes m + 16 kq hold a row's parts
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt) {
+#pragma unroll
+    for (int o = 16; o < 64; o <<= 1) {
+      sd1[rt] += __shfl_xor(sd1[rt], o, 64);
+      sd2[rt] += __shfl_xor(sd2[rt], o, 64);
+    }
+    if (kq == 0) {
+      const double mu = sd1[rt] * (1.0 / kD);
+      const double var = fmax(sd2[rt] * (1.0 / kD) - mu * mu, 0.0);
+      const double kp = double(keep);
+      stS[wave][16 * rt + m][0] = static_cast<float>(kp * mu);                              // mean of the dropped-out row
+      stS[wave][16 * rt + m][1] = static_cast<float>(1.0 / sqrt(kp * kp * var + double(kLnEps)));  // its 1 / std
+    }
+  }
+  __syncthreads();
+  const float ks = keep * (1.f / 16.f);
+  float cc0[8], cc1[8];
+#pragma unroll
+  for (int ct = 0; ct < 8; ++ct) {
+    cc0[ct] = a.c0[16 * ct + m];
+    cc1[ct] = a.c1[16 * ct + m];
+  }
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int lr = 16 * rt + 4 * kq + e;
+      const int64_t r = tile0 + 32 * wave + lr;
+      const float mu = stS[wave][lr][0], rs = stS[wave][lr][1];
+      if (r < a.rows) {
+        float* out = a.hg + r * kH2 + m;
+#pragma unroll
+        for (int ct = 0; ct < 8; ++ct) out[16 * ct] = rs * (acc[rt][ct][e] * ks - mu * cc1[ct]) + cc0[ct];
+      }
+    }
+}
+
+
+// After the passes (trainer.py:509-536, :549-566): the validation false
+// positives per hour (count / hours in float32, as torch divides an integer
+// count tensor by a Python float), recall, the testing rates, and the dynamic
+// negative weight (x ratio above the target rate, / ratio with a floor of 1
+// otherwise) written into the schedule rows of every later step.
+struct EvalFinish {
+  const float* cv;  // validation counts [4] (label 0: >=, >; label 1: >=, >)
+  const float* ct;  // testing counts [4] or NULL
+  float n_neg_v, n_pos_v, n_neg_t, n_pos_t;
+  float hours_v;    // n_neg_v * 1.44 / 3600, rounded to float32 on the host
+  float target, ratio;  // ratio <= 0: no dynamic adjustment
+  float* sched;
+  int64_t sched_len, next_step;
+  float* out;       // [8]
+};
+__global__ void __launch_bounds__(256) kv_finish_kernel(EvalFinish f) {
+  const float cur = f.sched ? f.sched[2 * max(int64_t(0), min(f.next_step - 1, f.sched_len - 1)) + 1] : 1.f;
+  float fph = 0.f, rec = 0.f, nw = cur;
+  if (f.cv) {
+    fph = f.cv[0] / f.hours_v;  // float32 division (x / 0 -> inf, 0 / 0 -> nan, as torch)
+    rec = f.n_pos_v > 0.f ? f.cv[3] / f.n_pos_v : 0.f;
+    if (f.ratio > 0.f) nw = fph > f.target ? cur * f.ratio : fmaxf(1.f, cur / f.ratio);
+  }
+  if (threadIdx.x == 0 && f.out) {
+    f.out[0] = fph;
+    f.out[1] = rec;
+    if (f.ct) {
+      f.out[2] = f.ct[0] / fmaxf(f.n_neg_t, 1.f);
+      f.out[3] = f.n_pos_t > 0.f ? f.ct[3] / f.n_pos_t : 0.f;
+      f.out[4] = (f.ct[3] + (f.n_neg_t - f.ct[1])) / fmaxf(f.n_neg_t + f.n_pos_t, 1.f);
+    } else {
+      f.out[2] = f.out[3] = f.out[4] = 0.f;
+    }
+    f.out[5] = nw;
+    f.out[6] = cur;
+    f.out[7] = 0.f;
+  }
+  if (f.cv && f.ratio > 0.f && f.sched)
+    for (int64_t s = f.next_step + threadIdx.x; s < f.sched_len; s += blockDim.x) f.sched[2 * s + 1] = nw;
+}
+
 // --------------------------------------------------------- workspace ------
 struct FusedWs {
-  int64_t wsplit, hg_part, xhat[2], U, Xn, dS, dHG, total;  // float offsets
+  int64_t wsplit, part, pstride, hg_part, xhat[2], U, Xn, dS, dHG, total;  // float offsets
 };
 // the weight cache's segments (WSplit) for plan p: W_o_k (k < NG - 1), then W_hg_k (k >= 1)
 WSplit make_wsplit(const hbk_mlp_plan& p) {
@@ -1497,12 +1851,22 @@ int k1_splits(int B) {  // (one round of three per CU on a 64-CU stream, KS 8, m
     if (k1_blocks(B) * ks >= 256) return ks;
   return 24;
 }
-FusedWs fused_layout(int64_t B, int NG) {
+// k3's batch splits: rows per split by the stream's width (see kK3Steps)
+int k3_rows(const void* stream) {
+  static const bool k3_wide = getenv("HBK_K3_WIDE") != nullptr;
+  const bool narrow = !k3_wide && persistent_blocks(1, stream) <= kK3NarrowCUs;
+  return 32 * (narrow ? kK3StepsNarrow : kK3Steps);
+}
+FusedWs fused_layout(int64_t B, int NG, int64_t n_params = 0) {
   FusedWs w;
   int64_t o = 0;
   auto take = [&](int64_t n) { const int64_t r = o; o += (n + 63) & ~int64_t(63); return r; };
   const int64_t Bp = (B + kR - 1) / kR * kR;
   w.wsplit = take(wsplit_halves(NG) / 2);  // first: its offset does not depend on B
+  // k3's partial slabs (the most splits either width takes), at a fixed offset too
+  w.pstride = (n_params + 63) & ~int64_t(63);
+  w.part = take(w.pstride * ((Bp + 32 * std::min(kK3StepsNarrow, kK3Steps) - 1) /
+                             (32 * std::min(kK3StepsNarrow, kK3Steps))));
   w.hg_part = take(int64_t(24) * B * kH2);
   w.xhat[0] = take(Bp * kD);
   w.xhat[1] = take(Bp * kD);
@@ -1529,6 +1893,55 @@ void fill_k2(const hbk_mlp_plan& p, K2Args& k) {
   }
 }
 
+// the weight cache's plane offsets as k2 reads them
+void set_k2_cache(const WSplit& wsp, int NG, const _Float16* wc, K2Args& k2) {
+  k2.wc = wc;
+  for (int k = 0; k < NG; ++k) k2.c_o[k] = k2.c_oT[k] = k2.c_hg[k] = k2.c_hgT[k] = 0;
+  for (int sg = 0; sg < wsp.n; ++sg) {
+    const WSeg& g = wsp.s[sg];
+    const int64_t rc = int64_t(g.rows) * g.cols;
+    const bool is_o = sg < NG - 1;
+    const int k = is_o ? sg : sg - (NG - 1) + 1;
+    (is_o ? k2.c_o : k2.c_hg)[k] = g.dst;
+    (is_o ? k2.c_oT : k2.c_hgT)[k] = g.dst + 2 * rc;
+  }
+}
+
+// k3's covered parameter ranges: norm_in gamma / beta, every W_hg and W_o
+Ranges make_ranges(const hbk_mlp_plan& p) {
+  Ranges r{};
+  auto add = [&](int64_t lo, int64_t n) {
+    r.lo[r.n] = lo;
+    r.hi[r.n++] = lo + n;
+  };
+  add(p.ln_in.g, p.ln_in.d);
+  add(p.ln_in.b, p.ln_in.d);
+  for (const Gmlp& g : p.g) {
+    add(g.w_hg, int64_t(2) * g.hid * g.in);
+    add(g.w_o, int64_t(g.out) * g.hid);
+  }
+  return r;
+}
+
+// evaluation workspace: the weight cache (as the fused layout's first region),
+// W' planes, c0, c1, then one chunk's HG0 slab
+constexpr int64_t kEvalChunk = 131072;
+struct EvalWs {
+  int64_t wsplit, wq, c0, c1, hg, total;  // float offsets
+};
+EvalWs eval_layout(int NG, int64_t rows) {
+  EvalWs w;
+  int64_t o = 0;
+  auto take = [&](int64_t n) { const int64_t r = o; o += (n + 63) & ~int64_t(63); return r; };
+  w.wsplit = take(wsplit_halves(NG) / 2);
+  w.wq = take(int64_t(kH2) * kD);  // 2 planes of halves
+  w.c0 = take(kH2);
+  w.c1 = take(kH2);
+  w.hg = take(std::min<int64_t>(std::max<int64_t>(rows, 1), kEvalChunk) * kH2);
+  w.total = o;
+  return w;
+}
+
 }  // namespace
 
 bool mlp_fused_supported(const hbk_mlp_plan& p) {
@@ -1537,7 +1950,7 @@ bool mlp_fused_supported(const hbk_mlp_plan& p) {
 }
 
 int64_t mlp_fused_ws_floats(const hbk_mlp_plan& p, int64_t B) {
-  return fused_layout(std::max<int64_t>(B, 1), static_cast<int>(p.g.size())).total;
+  return fused_layout(std::max<int64_t>(B, 1), static_cast<int>(p.g.size()), p.n_params).total;
 }
 
 // k1 + k2 (+ k3): the forward (inference) or forward/backward half of a step.
@@ -1547,7 +1960,7 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
                   int sched_len, float neg_weight, float thr, float act_thr, float drop_p, uint64_t seed,
                   float* bucket, float* prob, float* logit, float* ws, bool train, int flags, hipStream_t s) {
   const int NG = static_cast<int>(p.g.size());
-  const FusedWs w = fused_layout(B, NG);
+  const FusedWs w = fused_layout(B, NG, p.n_params);
   const int KS = k1_splits(B);
   const int64_t Bp = (B + kR - 1) / kR * kR;
   const int rt = (B + kR - 1) / kR;
@@ -1622,6 +2035,8 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
   k2.act_thr = act_thr;
   k2.prob = prob;
   k2.logit = logit;
+  k2.counts = nullptr;
+  k2.count_label = 0;
   k2.G = bucket;
   k2.stats = bucket ? bucket + p.n_params : nullptr;
   k2.U = ws + w.U;
@@ -1632,16 +2047,7 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
   k2.n_rt = rt;
   k2.prefetch = train && idx && (flags & HBK_STEP_PREFETCH_NEXT);
   k2.pre = ka;
-  k2.wc = wc;
-  for (int k = 0; k < NG; ++k) k2.c_o[k] = k2.c_oT[k] = k2.c_hg[k] = k2.c_hgT[k] = 0;
-  for (int sg = 0; sg < wsp.n; ++sg) {
-    const WSeg& g = wsp.s[sg];
-    const int64_t rc = int64_t(g.rows) * g.cols;
-    const bool is_o = sg < NG - 1;
-    const int k = is_o ? sg : sg - (NG - 1) + 1;
-    (is_o ? k2.c_o : k2.c_hg)[k] = g.dst;
-    (is_o ? k2.c_oT : k2.c_hgT)[k] = g.dst + 2 * rc;
-  }
+  set_k2_cache(wsp, NG, wc, k2);
   {
     const int grid = k2.prefetch ? rt + (rt + kPreTiles - 1) / kPreTiles : rt;
     auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, k2); };
@@ -1661,16 +2067,15 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
   K3Args k3;
   int nj = 0, blocks = 0;
   // HBK_K3_WIDE=1: the 288-row splits on narrow streams too (4 instead of 9
-  // splits at B = 1100: fewer partial-sum atomics, more time on a small partition)
-  static const bool k3_wide = getenv("HBK_K3_WIDE") != nullptr;
-  const bool narrow = !k3_wide && persistent_blocks(1, s) <= kK3NarrowCUs;
-  const int rows3 = 32 * (narrow ? kK3StepsNarrow : kK3Steps);
+  // splits at B = 1100: fewer partial slabs, more time on a small partition)
+  const int rows3 = k3_rows(s);
+  const bool narrow = rows3 == 32 * kK3StepsNarrow;
   const int KS3 = static_cast<int>((Bp + rows3 - 1) / rows3);
-  auto add = [&](const float* X, const float* Y, float* C, int ldc, int M, int N) {
+  auto add = [&](const float* X, const float* Y, int64_t c_off, int ldc, int M, int N) {
     WJob& j = k3.job[nj];
     j.X = X;
     j.Y = Y;
-    j.C = C;
+    j.c_off = c_off;
     j.ldc = ldc;
     j.M = M;
     j.N = N;
@@ -1679,12 +2084,11 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
     blocks += ((M + kTM - 1) / kTM) * j.tn * KS3;
     ++nj;
   };
-  float* G = bucket;
-  add(ws + w.dHG, xhat, G + p.g[0].w_hg, kD, kH2, kD);
+  add(ws + w.dHG, xhat, p.g[0].w_hg, kD, kH2, kD);
   for (int k = 1; k < NG; ++k)
-    add(ws + w.dHG + int64_t(k) * kH2 * Bp, ws + w.Xn + int64_t(k) * kL * Bp, G + p.g[k].w_hg, kL, kH2, kL);
+    add(ws + w.dHG + int64_t(k) * kH2 * Bp, ws + w.Xn + int64_t(k) * kL * Bp, p.g[k].w_hg, kL, kH2, kL);
   for (int k = 0; k < NG; ++k)
-    add(ws + w.dS + int64_t(k) * kL * Bp, ws + w.U + int64_t(k) * kH * Bp, G + p.g[k].w_o, kH, p.g[k].out, kH);
+    add(ws + w.dS + int64_t(k) * kL * Bp, ws + w.U + int64_t(k) * kH * Bp, p.g[k].w_o, kH, p.g[k].out, kH);
   k3.start[nj] = blocks;
   k3.n_jobs = nj;
   k3.KS = KS3;
@@ -1692,22 +2096,44 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
   k3.g_in = params + p.ln_in.g;
   k3.b_in = params + p.ln_in.b;
   k3.W0 = params + p.g[0].w_hg;
-  k3.dg_in = G + p.ln_in.g;
-  k3.db_in = G + p.ln_in.b;
+  k3.g_off = p.ln_in.g;
+  k3.b_off = p.ln_in.b;
+  k3.part = ws + w.part;
+  k3.pstride = w.pstride;
   if (narrow)
     hipLaunchKernelGGL(k3_wgrad_kernel<kK3StepsNarrow>, dim3(blocks), dim3(256), 0, s, k3);
   else
     hipLaunchKernelGGL(k3_wgrad_kernel<kK3Steps>, dim3(blocks), dim3(256), 0, s, k3);
   HBK_LAUNCH_CHECK("k3_wgrad_kernel");
+  if (flags & HBK_STEP_DEFER_PARTIALS) {  // the update adds the slabs
+    p.deferred_ws = ws;
+    p.deferred_ks = KS3;
+  } else {
+    p.deferred_ws = nullptr;
+    hipLaunchKernelGGL(k3_fold_kernel, dim3(unsigned(std::min<int64_t>((p.n_params + 255) / 256, 1024))), dim3(256),
+                       0, s, make_ranges(p), ws + w.part, w.pstride, KS3, bucket, p.n_params);
+    HBK_LAUNCH_CHECK("k3_fold_kernel");
+  }
   return HBK_OK;
 }
 
 int mlp_fused_update(const hbk_mlp_plan& p, float* params, float* bucket, float* m, float* v, float* state,
                      int parity, const float* sched, int sched_len, float lr, float b1, float b2, float eps,
                      float* hist, int hist_cap, float* ws, hipStream_t s) {
+  if (p.deferred_ws && p.deferred_ws != ws) {
+    set_error("hbk: the previous hbk_mlp_step_fwd_bwd deferred its weight-gradient partials to its workspace: "
+              "pass that workspace to hbk_mlp_step_update");
+    return HBK_ERR_ARG;
+  }
   K4Args k;
   k.w = make_wsplit(p);
-  k.wc = ws ? reinterpret_cast<_Float16*>(ws + fused_layout(1, static_cast<int>(p.g.size())).wsplit) : nullptr;
+  const FusedWs fl = fused_layout(1, static_cast<int>(p.g.size()), p.n_params);
+  k.wc = ws ? reinterpret_cast<_Float16*>(ws + fl.wsplit) : nullptr;
+  k.part = p.deferred_ws ? ws + fl.part : nullptr;
+  k.pstride = fl.pstride;
+  k.ns = p.deferred_ws ? p.deferred_ks : 0;
+  k.rg = make_ranges(p);
+  p.deferred_ws = nullptr;
   k.n_tiles = 0;
   for (int sg = 0; sg < k.w.n; ++sg)
     for (int r0 = 0; r0 < k.w.s[sg].rows && k.n_tiles < kMaxTiles; r0 += kTileR) {
@@ -1732,6 +2158,93 @@ int mlp_fused_update(const hbk_mlp_plan& p, float* params, float* bucket, float*
   const int64_t blocks = (k.wc ? k.n_tiles : 0) + std::min<int64_t>((p.n_params / 4 + 255) / 256, 1024);
   hipLaunchKernelGGL(k4_update_kernel, dim3(unsigned(blocks)), dim3(256), 0, s, k);
   HBK_LAUNCH_CHECK("k4_update_kernel");
+  return HBK_OK;
+}
+
+int64_t mlp_eval_ws_floats(const hbk_mlp_plan& p, int64_t rows) {
+  return eval_layout(static_cast<int>(p.g.size()), rows).total;
+}
+
+int mlp_eval_prepare(const hbk_mlp_plan& p, const float* params, float* ws, hipStream_t s) {
+  const int NG = static_cast<int>(p.g.size());
+  const EvalWs w = eval_layout(NG, 1);
+  const WSplit wsp = make_wsplit(p);
+  const int64_t n4 = wsplit_halves(NG) / 16;
+  hipLaunchKernelGGL(k0_wsplit_kernel, dim3(unsigned(std::min<int64_t>((n4 + 255) / 256, 256))), dim3(256), 0, s,
+                     wsp, params, reinterpret_cast<_Float16*>(ws + w.wsplit), n4);
+  HBK_LAUNCH_CHECK("k0_wsplit_kernel");
+  hipLaunchKernelGGL(kv_prep_kernel, dim3(kH2), dim3(256), 0, s, params, p.g[0].w_hg, p.ln_in.g, p.ln_in.b,
+                     reinterpret_cast<_Float16*>(ws + w.wq), ws + w.c0, ws + w.c1);
+  HBK_LAUNCH_CHECK("kv_prep_kernel");
+  return HBK_OK;
+}
+
+int mlp_eval_count(const hbk_mlp_plan& p, const float* params, const void* pool, bool f16, int64_t n_pool,
+                   const int32_t* idx, int64_t rows, int64_t r0, int label, float act_thr, float drop_p,
+                   uint64_t seed, float* counts, float* prob, float* ws, hipStream_t s) {
+  const int NG = static_cast<int>(p.g.size());
+  const EvalWs w = eval_layout(NG, rows);
+  const WSplit wsp = make_wsplit(p);
+  for (int64_t c0 = 0; c0 < rows; c0 += kEvalChunk) {
+    const int64_t n = std::min(kEvalChunk, rows - c0);
+    KvArgs ka;
+    ka.pool = pool;
+    ka.n_pool = n_pool;
+    ka.idx = idx ? idx + c0 : nullptr;
+    ka.rows = n;
+    ka.r0 = r0 + c0;
+    ka.wq = reinterpret_cast<const _Float16*>(ws + w.wq);
+    ka.c0 = ws + w.c0;
+    ka.c1 = ws + w.c1;
+    ka.drop_p = drop_p;
+    ka.seed = seed;
+    ka.hg = ws + w.hg;
+    const dim3 grid(unsigned((n + kKvRows - 1) / kKvRows));
+    if (f16)
+      hipLaunchKernelGGL(kv_gemm_kernel<true>, grid, dim3(512), 0, s, ka);
+    else
+      hipLaunchKernelGGL(kv_gemm_kernel<false>, grid, dim3(512), 0, s, ka);
+    HBK_LAUNCH_CHECK("kv_gemm_kernel");
+    K2Args k2{};
+    k2.P = params;
+    k2.B = static_cast<int>(n);
+    k2.KS = 1;
+    fill_k2(p, k2);
+    k2.hg_part = ws + w.hg;
+    k2.act_thr = act_thr;
+    k2.prob = prob ? prob + c0 : nullptr;
+    k2.Bp = (n + kR - 1) / kR * kR;
+    k2.n_rt = static_cast<int>((n + kR - 1) / kR);
+    set_k2_cache(wsp, NG, reinterpret_cast<const _Float16*>(ws + w.wsplit), k2);
+    k2.counts = counts;
+    k2.count_label = label;
+    auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(unsigned(k2.n_rt)), dim3(256), 0, s, k2); };
+    if (NG == 2) launch(k2_rows_kernel<false, 2>);
+    else if (NG == 3) launch(k2_rows_kernel<false, 3>);
+    else launch(k2_rows_kernel<false, 4>);
+    HBK_LAUNCH_CHECK("k2_rows_kernel");
+  }
+  return HBK_OK;
+}
+
+int mlp_eval_finish(const float* cv, const float* ct, const double* sizes, float target, float ratio, float* sched,
+                    int64_t sched_len, int64_t next_step, float* out, hipStream_t s) {
+  EvalFinish f;
+  f.cv = cv;
+  f.ct = ct;
+  f.n_neg_v = static_cast<float>(sizes[0]);
+  f.n_pos_v = static_cast<float>(sizes[1]);
+  f.n_neg_t = static_cast<float>(sizes[2]);
+  f.n_pos_t = static_cast<float>(sizes[3]);
+  f.hours_v = static_cast<float>(sizes[0] * 1.44 / 3600.0);
+  f.target = target;
+  f.ratio = ratio;
+  f.sched = sched;
+  f.sched_len = sched_len;
+  f.next_step = next_step;
+  f.out = out;
+  hipLaunchKernelGGL(kv_finish_kernel, dim3(1), dim3(256), 0, s, f);
+  HBK_LAUNCH_CHECK("kv_finish_kernel");
   return HBK_OK;
 }
 

@@ -29,6 +29,10 @@ struct hbk_mlp_plan {
   // hbk_mlp_set_step_scalars: device [lr, neg_weight, seed] read by the train
   // kernels in place of their by-value arguments (graph-captured steps)
   const double* step_scalars = nullptr;
+  // hbk_mlp_step_fwd_bwd with HBK_STEP_DEFER_PARTIALS left its weight-gradient
+  // slabs (deferred_ks of them) in this workspace for the next hbk_mlp_step_update
+  mutable const void* deferred_ws = nullptr;
+  mutable int deferred_ks = 0;
 };
 
 namespace hbk {
@@ -53,4 +57,12 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
 int mlp_fused_update(const hbk_mlp_plan& p, float* params, float* bucket, float* m, float* v, float* state,
                      int parity, const float* sched, int sched_len, float lr, float b1, float b2, float eps,
                      float* hist, int hist_cap, float* ws, hipStream_t s);
+// Evaluation passes (validation / testing forwards reduced to prediction counts)
+int64_t mlp_eval_ws_floats(const hbk_mlp_plan& p, int64_t rows);
+int mlp_eval_prepare(const hbk_mlp_plan& p, const float* params, float* ws, hipStream_t s);
+int mlp_eval_count(const hbk_mlp_plan& p, const float* params, const void* pool, bool f16, int64_t n_pool,
+                   const int32_t* idx, int64_t rows, int64_t r0, int label, float act_thr, float drop_p,
+                   uint64_t seed, float* counts, float* prob, float* ws, hipStream_t s);
+int mlp_eval_finish(const float* cv, const float* ct, const double* sizes, float target, float ratio, float* sched,
+                    int64_t sched_len, int64_t next_step, float* out, hipStream_t s);
 }  // namespace hbk

@@ -58,10 +58,15 @@ def graph_capturable(world_size: int) -> bool:
     return dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl"
 
 
+def reduces(group: Optional[dist.ProcessGroup] = None) -> bool:
+    """Does reduce_bucket run a collective here?"""
+    return dist.is_available() and dist.is_initialized() and (dist.get_world_size(group) > 1 or force_reduce())
+
+
 def reduce_bucket(bucket: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
     """Sum the gradient + statistics bucket over the data-parallel ranks (one
     all-reduce of the 1,025,700-B bucket; capturable into a hipGraph on RCCL)."""
-    if dist.is_available() and dist.is_initialized() and (dist.get_world_size(group) > 1 or force_reduce()):
+    if reduces(group):
         dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=group)
     return bucket
 

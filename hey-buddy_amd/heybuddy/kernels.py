@@ -473,7 +473,7 @@ class MlpPlan:
                      dropout_p: float = 0.0, seed: int = 0, prob: torch.Tensor | None = None,
                      workspace: torch.Tensor | None = None, xhat_ready: bool = False,
                      prefetch_next: bool = False, idx_steps: int | None = None,
-                     weights_ready: bool = False) -> None:
+                     weights_ready: bool = False, defer_partials: bool = False) -> None:
         """Forward / filter / BCE / backward of one step into ``bucket``
         (hbk_mlp_step_fwd_bwd). Rows come from pool32 [n, 1536] f32 and pool16
         [n, 1536] f16 by ``idx`` (int32, >= 0 -> pool32, < 0 -> pool16 row -i-1;
@@ -482,7 +482,10 @@ class MlpPlan:
         step + 1 < idx_steps, default idx.numel() // idx_stride) during this
         step; ``xhat_ready``: the previous call on this workspace did that for
         this step; ``weights_ready``: the previous step_update got this
-        workspace, so its weight cache is current (else it is refreshed)."""
+        workspace, so its weight cache is current (else it is refreshed);
+        ``defer_partials``: the weight gradients' per-split slabs stay in the
+        workspace for the next step_update, which must get it (one process, no
+        all-reduce in between); else they are summed into ``bucket`` here."""
         dev = params.device
         if params.numel() != self.n_params or bucket.numel() != self.n_params + self.N_STATS:
             raise ValueError("params / bucket do not match the plan")
@@ -504,7 +507,7 @@ class MlpPlan:
         if idx_steps is None:
             idx_steps = idx.numel() // idx_stride if idx is not None and idx_stride > 0 else 1
         flags = (1 if xhat_ready else 0) | (2 if prefetch_next and idx is not None else 0) | (
-            4 if weights_ready else 0)
+            4 if weights_ready else 0) | (8 if defer_partials else 0)
         torch.ops.hbk.mlp_step_fwd_bwd(params, bucket, state, int(parity), y, int(batch), pool32, pool16, idx,
                                        int(idx_stride), int(y_stride), sched, float(neg_weight), float(threshold),
                                        float(activation_threshold), float(dropout_p), _u64_to_i64(seed), prob, ws,
@@ -519,6 +522,54 @@ class MlpPlan:
         step_fwd_bwd on it may pass weights_ready."""
         torch.ops.hbk.mlp_step_update(params, bucket, m, v, state, int(parity), sched, float(lr), float(beta1),
                                       float(beta2), float(eps), history, workspace, self.id)
+
+    # -- evaluation passes (hbk_mlp_eval_*) ---------------------------------
+    def eval_workspace_bytes(self, rows: int) -> int:
+        need = ctypes.c_int64()
+        check(lib().hbk_mlp_eval_workspace_size(self._handle, int(rows), ctypes.byref(need)),
+              "hbk_mlp_eval_workspace_size")
+        return need.value
+
+    def eval_prepare(self, params: torch.Tensor, ws: torch.Tensor) -> None:
+        """The pass's weight planes from ``params`` (hbk_mlp_eval_prepare): once per
+        pass, before any eval_count."""
+        torch.ops.hbk.mlp_eval_prepare_(params, ws, self.id)
+
+    def eval_count(self, params: torch.Tensor, pool: torch.Tensor, rows: int, label: int, counts: torch.Tensor,
+                   ws: torch.Tensor, idx: torch.Tensor | None = None, row_offset: int = 0,
+                   activation_threshold: float = 0.5, dropout_p: float = 0.0, seed: int = 0,
+                   prob: torch.Tensor | None = None) -> None:
+        """Forward ``rows`` rows of ONE pool ([n, 1536] f32 or f16; row r = pool
+        row idx[r], or (row_offset + r) % n without idx), all labelled ``label``,
+        into ``counts`` [4] f32 (hbk_mlp_eval_count): counts[2 label] +=
+        #(p >= threshold), counts[2 label + 1] += #(p > threshold)."""
+        dev = params.device
+        flat = pool.reshape(pool.shape[0], -1)
+        if flat.shape[1] != self.d_in or pool.dtype not in (torch.float32, torch.float16) or pool.device != dev \
+                or not pool.is_contiguous():
+            raise ValueError(f"pool must be a contiguous [n, {self.d_in}] f32 / f16 tensor on {dev}")
+        if idx is not None and (idx.dtype != torch.int32 or idx.device != dev or not idx.is_contiguous()
+                                or idx.numel() < rows):
+            raise ValueError("idx must be a contiguous int32 device tensor of >= rows entries")
+        if counts.dtype != torch.float32 or counts.numel() < 4 or counts.device != dev:
+            raise ValueError("counts must be a float32 [4] device tensor")
+        if prob is not None and (prob.dtype != torch.float32 or prob.numel() < rows or prob.device != dev):
+            raise ValueError("prob must be a float32 device tensor of >= rows entries")
+        torch.ops.hbk.mlp_eval_count_(params, pool, idx, int(rows), int(row_offset), int(label),
+                                      float(activation_threshold), float(dropout_p), _u64_to_i64(seed), counts, prob,
+                                      ws, self.id)
+
+    @staticmethod
+    def eval_finish(counts_val: torch.Tensor | None, counts_test: torch.Tensor | None, sizes, out: torch.Tensor,
+                    target: float = 1.5, ratio: float = 0.0, sched: torch.Tensor | None = None,
+                    next_step: int = 0) -> None:
+        """The reference's bookkeeping after the passes (hbk_mlp_eval_finish):
+        out [8] = (validation false positives / hour, validation recall, testing
+        false-positive rate, testing recall, testing accuracy, new negative weight,
+        weight before, 0); ratio > 0 writes the new negative weight into sched
+        rows next_step .. (the dynamic negative weight, trainer.py:531-536)."""
+        torch.ops.hbk.mlp_eval_finish_(counts_val, counts_test, [float(v) for v in sizes], float(target),
+                                       float(ratio), sched, int(next_step), out)
 
     def gate_adam(self, params, bucket, m, v, state, ctrl, history, lr, beta1=0.9, beta2=0.999,
                   eps=1e-8) -> None:
@@ -577,6 +628,36 @@ def _mlp_step_update_op(params: torch.Tensor, bucket: torch.Tensor, m: torch.Ten
         ptr(sched) if sched is not None else None, sched.shape[0] if sched is not None else 0, lr, beta1, beta2,
         eps, ptr(history) if history is not None else None, cap, ptr(ws) if ws is not None else None,
         ws.numel() if ws is not None else 0, stream_ptr(params.device)), "hbk_mlp_step_update")
+
+
+@torch.library.custom_op("hbk::mlp_eval_prepare_", mutates_args=("ws",))
+def _mlp_eval_prepare_op(params: torch.Tensor, ws: torch.Tensor, plan_id: int) -> None:
+    plan = _plans[plan_id]
+    check(lib().hbk_mlp_eval_prepare(plan._handle, ptr(params), ptr(ws), ws.numel(), stream_ptr(params.device)),
+          "hbk_mlp_eval_prepare")
+
+
+@torch.library.custom_op("hbk::mlp_eval_count_", mutates_args=("counts", "prob", "ws"))
+def _mlp_eval_count_op(params: torch.Tensor, pool: torch.Tensor, idx: torch.Tensor | None, rows: int,
+                       row_offset: int, label: int, activation_threshold: float, dropout_p: float, seed: int,
+                       counts: torch.Tensor, prob: torch.Tensor | None, ws: torch.Tensor, plan_id: int) -> None:
+    plan = _plans[plan_id]
+    check(lib().hbk_mlp_eval_count(
+        plan._handle, ptr(params), ptr(pool), 1 if pool.dtype == torch.float16 else 0, pool.shape[0],
+        ptr(idx) if idx is not None else None, rows, row_offset, label, activation_threshold, dropout_p,
+        seed & (2 ** 64 - 1), ptr(counts), ptr(prob) if prob is not None else None, ptr(ws), ws.numel(),
+        stream_ptr(params.device)), "hbk_mlp_eval_count")
+
+
+@torch.library.custom_op("hbk::mlp_eval_finish_", mutates_args=("sched", "out"))
+def _mlp_eval_finish_op(counts_val: torch.Tensor | None, counts_test: torch.Tensor | None, sizes: list[float],
+                        target: float, ratio: float, sched: torch.Tensor | None, next_step: int,
+                        out: torch.Tensor) -> None:
+    sz = (ctypes.c_double * 4)(*sizes[:4])
+    check(lib().hbk_mlp_eval_finish(
+        ptr(counts_val) if counts_val is not None else None, ptr(counts_test) if counts_test is not None else None,
+        sz, target, ratio, ptr(sched) if sched is not None else None, sched.shape[0] if sched is not None else 0,
+        next_step, ptr(out), stream_ptr(out.device)), "hbk_mlp_eval_finish")
 
 
 @torch.library.custom_op("hbk::place_clips", mutates_args=())

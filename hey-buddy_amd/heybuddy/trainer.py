@@ -48,7 +48,7 @@ from heybuddy.pipeline import capture_stream
 from heybuddy.util import logger
 from heybuddy.wakeword import WakeWordMLPModel
 
-__all__ = ["Trainer", "WakeWordTrainer"]
+__all__ = ["Trainer", "WakeWordTrainer", "EvalPasses"]
 
 BETAS = (0.9, 0.999)
 EPS = 1e-8
@@ -186,6 +186,91 @@ class Trainer(nn.Module):
 
     def __call__(self, training: Any, **kwargs: Any) -> None:
         raise NotImplementedError()
+
+
+class EvalPasses:
+    """The validation and testing passes of train_epoch on the device
+    (trainer.py:496-566), for HBM-resident embedding pools: every pass is the
+    reference's batch loop (validation: ``validation_batches`` batches of
+    (50 positives, 1,000 negatives), by default max(n_neg // 1000, n_pos // 50)
+    as WakeWordTrainingDatasetIterator.validation's max_samples, training.py:
+    693-701; testing: batches of (50 positives, 50 adversarial), max(n_pos // 50,
+    n_adv // 50), :621-630) as ONE forward over all of its rows per pool
+    (hbk_mlp_eval_count; the order of rows within a pass does not change its
+    counts), with the input dropout on as in the reference (it never calls
+    .eval()), then the bookkeeping of :509-536 / :549-561 and the dynamic
+    negative weight on the device (hbk_mlp_eval_finish): no host
+    synchronisation. Each pool is read in order with wrap-around, continuing
+    where the previous pass stopped (the datasets' take() stream; a pass that
+    covers whole laps of a pool reads every row equally often, as the
+    reference's permutations do).
+
+    ``run(sched, next_step)`` enqueues one validation (+ testing) pass on the
+    current stream; the metrics land in ``history[k]`` = (false positives per
+    hour, recall, testing false-positive rate, testing recall, testing
+    accuracy, negative weight after, before, 0)."""
+
+    def __init__(self, trainer: "WakeWordTrainer", validation_positive: torch.Tensor,
+                 validation_negative: torch.Tensor, testing_positive: Optional[torch.Tensor] = None,
+                 testing_adversarial: Optional[torch.Tensor] = None, validation_batch: Tuple[int, int] = (50, 1000),
+                 testing_batch: Tuple[int, int] = (50, 50), validation_batches: Optional[int] = None,
+                 testing_batches: Optional[int] = None,
+                 target_false_positive_rate: float = DEFAULT_TARGET_FALSE_POSITIVE_RATE,
+                 adjust_ratio: Optional[float] = DEFAULT_NEGATIVE_WEIGHT_ADJUST_RATIO,
+                 activation_threshold: float = DEFAULT_ACTIVATION_THRESHOLD, seed: int = 0,
+                 history_cap: int = 256) -> None:
+        self.trainer = trainer
+        dev = trainer.device
+        pv, nv = validation_batch
+        if validation_batches is None:
+            validation_batches = max(validation_negative.shape[0] // nv, validation_positive.shape[0] // pv)
+        # (pool, rows, label, counter set: 0 validation / 1 testing)
+        self.parts = [(validation_positive, validation_batches * pv, 1, 0),
+                      (validation_negative, validation_batches * nv, 0, 0)]
+        self.sizes = [float(validation_batches * nv), float(validation_batches * pv), 0.0, 0.0]
+        self.testing = testing_positive is not None and testing_adversarial is not None
+        if self.testing:
+            pt, at = testing_batch
+            if testing_batches is None:
+                testing_batches = max(testing_positive.shape[0] // pt, testing_adversarial.shape[0] // at)
+            self.parts += [(testing_positive, testing_batches * pt, 1, 1),
+                           (testing_adversarial, testing_batches * at, 0, 1)]
+            self.sizes[2:] = [float(testing_batches * at), float(testing_batches * pt)]
+        for pool, _, _, _ in self.parts:
+            if pool.device != dev or pool.dtype not in (torch.float32, torch.float16) or not pool.is_contiguous():
+                raise ValueError("evaluation pools must be contiguous f32 / f16 tensors on the trainer's device")
+        self.offsets = [0] * len(self.parts)
+        self.target = float(target_false_positive_rate)
+        self.ratio = float(adjust_ratio) if adjust_ratio else 0.0
+        self.act_thr = float(activation_threshold)
+        self.seed = int(seed)
+        plan = trainer.model.plan
+        self.ws = torch.empty(plan.eval_workspace_bytes(max(r for _, r, _, _ in self.parts)), dtype=torch.uint8,
+                              device=dev)
+        self.counts = torch.zeros((2, 4), dtype=torch.float32, device=dev)
+        self.history = torch.zeros((history_cap, 8), dtype=torch.float32, device=dev)
+        self.n = 0
+
+    @property
+    def rows_per_pass(self) -> int:
+        return sum(r for _, r, _, _ in self.parts)
+
+    def run(self, sched: Optional[torch.Tensor] = None, next_step: int = 0) -> None:
+        tr = self.trainer
+        plan = tr.model.plan
+        flat = tr.model.flat_parameters
+        p = tr.model.dropout.p if tr.model.training else 0.0
+        self.counts.zero_()
+        plan.eval_prepare(flat, self.ws)
+        for k, (pool, rows, label, which) in enumerate(self.parts):
+            plan.eval_count(flat, pool, rows, label, self.counts[which], self.ws, row_offset=self.offsets[k],
+                            activation_threshold=self.act_thr, dropout_p=p,
+                            seed=(self.seed + 0x9E3779B97F4A7C15 * (self.n * 8 + k + 1)) % (1 << 64))
+            self.offsets[k] = (self.offsets[k] + rows) % pool.shape[0]
+        plan.eval_finish(self.counts[0], self.counts[1] if self.testing else None, self.sizes,
+                         self.history[self.n % self.history.shape[0]], target=self.target, ratio=self.ratio,
+                         sched=sched, next_step=next_step)
+        self.n += 1
 
 
 def _recall(tp: float, n_pos: float) -> float:
@@ -340,7 +425,7 @@ class WakeWordTrainer(Trainer):
                       threshold: float = DEFAULT_HIGH_LOSS_THRESHOLD,
                       activation_threshold: float = DEFAULT_ACTIVATION_THRESHOLD,
                       history: Optional[torch.Tensor] = None, steps_per_graph: int = 16,
-                      graphs: bool = True) -> None:
+                      graphs: bool = True, n_steps: Optional[int] = None, continued: bool = False) -> None:
         """S fused optimisation steps whose batches are rows of HBM-resident
         embedding pools (the device-side sampler's output): step s trains on
         rows idx[s] (int32 [S, B]; >= 0 -> pool32 f32 [n, 16, 96], < 0 ->
@@ -348,14 +433,19 @@ class WakeWordTrainer(Trainer):
         step, or [S, B]) at sched[s] = (lr, neg_weight). The step index lives on
         the device, so a hipGraph of ``steps_per_graph`` steps replays the whole
         run; continues from the current state (call _reset_accumulation() to
-        start an epoch). Data-parallel: every rank passes its own rows; one
-        all-reduce of the bucket per step."""
+        start an epoch). ``n_steps``: run only this many of the steps (the rest
+        in later calls, e.g. around an evaluation pass); ``continued``: the
+        previous call ran the steps just before these on the same buffers, so
+        its last step already gathered this call's first rows and kept the
+        weight cache current. Data-parallel: every rank passes its own rows;
+        one all-reduce of the bucket per step."""
         if not self._fused:
             raise NotImplementedError("train_indexed needs the fused train step (default architecture)")
         dev = self.device
         plan = self.model.plan
         flat = self.model.flat_parameters
-        S, B = int(idx.shape[0]), int(idx.shape[1])
+        S_all, B = int(idx.shape[0]), int(idx.shape[1])
+        S = S_all if n_steps is None else int(n_steps)
         y_stride = B if y.dim() == 2 else 0
         p = self.model.dropout.p if self.model.training else 0.0
         p32 = None if pool32 is None else pool32.reshape(pool32.shape[0], -1)
@@ -365,21 +455,26 @@ class WakeWordTrainer(Trainer):
         need = plan.workspace_bytes(B)
         if ws is None or ws.numel() < need or ws.device != dev:
             ws = self._indexed_ws = torch.empty(need, dtype=torch.uint8, device=dev)
+            continued = False  # a new workspace holds no prefetched rows or weight cache
 
         # Each step also gathers + normalises the NEXT step's rows inside its own
         # launches (prefetch_next); only the first step of this call gathers its own.
+        # One process: the weight-gradient slabs go straight to the update (no all-reduce between).
+        defer = not distributed.reduces()
+
         def one(parity: int, ready: bool) -> None:
             plan.step_fwd_bwd(flat, self._bucket, self._fstate, parity, y, B, pool32=p32, pool16=p16, idx=idx,
                               idx_stride=B, y_stride=y_stride, sched=sched, threshold=threshold,
                               activation_threshold=activation_threshold, dropout_p=p, seed=self._seed_base,
-                              workspace=ws, xhat_ready=ready, prefetch_next=True, idx_steps=S, weights_ready=ready)
+                              workspace=ws, xhat_ready=ready, prefetch_next=True, idx_steps=S_all,
+                              weights_ready=ready, defer_partials=defer)
             distributed.reduce_bucket(self._bucket)
             plan.step_update(flat, self._bucket, self._m, self._v, self._fstate, parity, sched=sched,
                              beta1=BETAS[0], beta2=BETAS[1], eps=EPS, history=history, workspace=ws)
 
         done = 0
-        if S > 0:  # the first step gathers its own rows and prefetches the next
-            one(self._parity, False)
+        if S > 0:  # the first step gathers its own rows (unless continued) and prefetches the next
+            one(self._parity, bool(continued))
             self._parity ^= 1
             done = 1
         k = max(2, steps_per_graph - steps_per_graph % 2)

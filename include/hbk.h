@@ -269,10 +269,18 @@ int hbk_mlp_gate_adam(const hbk_mlp_plan* plan, float* params, const float* buck
  * (plain and transposed) from a cache at the start of the workspace:
  *   flags & HBK_STEP_WEIGHTS_READY: the previous hbk_mlp_step_update got the same
  *     workspace and left the cache current (it rewrites the cached matrices with
- *     every update); without it the step refreshes the cache from params first. */
+ *     every update); without it the step refreshes the cache from params first.
+ * The weight gradients are written per batch split as partial slabs in the
+ * workspace (plain stores; no float atomics) and summed once:
+ *   flags & HBK_STEP_DEFER_PARTIALS: by the next hbk_mlp_step_update, which must
+ *     get this workspace (it fails otherwise) and must follow with nothing that
+ *     reads the bucket in between (one process: no all-reduce);
+ *   without it: into the bucket at the end of this call (for the data-parallel
+ *     all-reduce, or an update without the workspace). */
 #define HBK_STEP_XHAT_READY 1
 #define HBK_STEP_PREFETCH_NEXT 2
 #define HBK_STEP_WEIGHTS_READY 4
+#define HBK_STEP_DEFER_PARTIALS 8
 int hbk_mlp_fused_supported(const hbk_mlp_plan* plan, int32_t* supported);
 int hbk_mlp_step_fwd_bwd(const hbk_mlp_plan* plan, const float* params, const float* pool32, int64_t n32,
                          const void* pool16, int64_t n16, const int32_t* idx, int64_t idx_step_stride,
@@ -292,6 +300,43 @@ int hbk_mlp_step_update(const hbk_mlp_plan* plan, float* params, float* bucket, 
  * neg_weight and seed arguments, so one captured hipGraph replays every step
  * of a stage with the schedule's values written before each replay. */
 int hbk_mlp_set_step_scalars(hbk_mlp_plan* plan, const double* dev_scalars);
+
+/* Evaluation passes: the validation and testing forwards of train_epoch
+ * (trainer.py:496-566; the default validation pass is 500 batches of 50
+ * positives + 1,000 negatives, the testing pass 500 of 50 + 50, every
+ * validation_steps = 250 steps, with dropout active as the reference never
+ * calls .eval()), reduced on the device to prediction counts, and the
+ * reference's bookkeeping after them (false positives per hour, recall,
+ * testing rates, the dynamic negative weight of :531-536). Fused plans only.
+ *
+ * hbk_mlp_eval_prepare: the pass's weight planes from params (once per pass:
+ *   params must not change between it and the counts).
+ * hbk_mlp_eval_count: rows r = 0 .. rows-1 of ONE pool (pool_is_f16: f16 [n_pool,
+ *   1536], else f32), row r = pool row idx[r] (idx != NULL) or (row_offset + r) %
+ *   n_pool, all labelled `label`; counts[2 label] += #(p >= activation_threshold),
+ *   counts[2 label + 1] += #(p > activation_threshold) (f32 counters, exact below
+ *   2^24: the caller zeroes them). The dropout mask of element i of row r is
+ *   f(seed, row_offset + r, i). prob (optional, [rows]) receives p.
+ *   Replaces the per-batch `self.model(x)[:, 0]` loops of trainer.py:503-510, 542-548.
+ * hbk_mlp_eval_finish: sizes (host) = {validation negatives, validation
+ *   positives, testing negatives, testing positives}; counts_test may be NULL.
+ *   out (device f32 [8]) = {validation false positives per hour (count / (n_neg
+ *   1.44 / 3600) in f32), validation recall, testing false-positive rate,
+ *   testing recall, testing accuracy, new negative weight, weight before, 0}.
+ *   adjust_ratio > 0: the negative weight of step next_step - 1 (sched row) is
+ *   multiplied by adjust_ratio when the rate exceeds the target, else divided
+ *   by it with a floor of 1, and written to sched rows next_step .. sched_len - 1
+ *   (trainer.py:531-536). */
+int hbk_mlp_eval_workspace_size(const hbk_mlp_plan* plan, int64_t rows, int64_t* bytes);
+int hbk_mlp_eval_prepare(const hbk_mlp_plan* plan, const float* params, void* workspace, int64_t workspace_bytes,
+                         void* stream);
+int hbk_mlp_eval_count(const hbk_mlp_plan* plan, const float* params, const void* pool, int32_t pool_is_f16,
+                       int64_t n_pool, const int32_t* idx, int64_t rows, int64_t row_offset, int32_t label,
+                       float activation_threshold, float dropout_p, uint64_t seed, float* counts, float* prob,
+                       void* workspace, int64_t workspace_bytes, void* stream);
+int hbk_mlp_eval_finish(const float* counts_val, const float* counts_test, const double* sizes,
+                        float target_false_positives_per_hour, float adjust_ratio, float* sched, int64_t sched_len,
+                        int64_t next_step, float* out, void* stream);
 
 /* ------------------------------------------------------------------------ *
  * Batch augmentation: background-noise mix + impulse-response reverb

@@ -282,3 +282,59 @@ def flat_bucket(params, x, y, neg_weight=1.0, threshold=1e-4, act_thr=0.5):
         stats[5] = ((~neg) & (ps > act_thr)).sum()
     grads = backward(params, cache, dz)
     return np.concatenate([g.reshape(-1) for g in grads.values()]), stats
+
+
+# ------------------------------------------------------------ evaluation ----
+def dropout_keep(seed: int, row_ids, d: int = 1536, p: float = 0.1) -> np.ndarray:
+    """The counter-based input-dropout mask of the HIP kernels (k1a_tile /
+    kv_gemm_kernel, hbk_mlp_fused.hip: drop_hash): element c of row r is dropped
+    iff a 16-bit uniform from hash(seed, r * d / 2 + c / 2) (low half for even c,
+    high half for odd c) is below round(p * 65536). [n, d] bool (True = kept).
+    The reference draws torch's Philox mask instead; only the rate matches."""
+    m32 = np.uint64(0xFFFFFFFF)
+    s0 = np.uint64(seed) & m32
+    s1 = ((np.uint64(seed) >> np.uint64(32)) * np.uint64(0x27D4EB2F)) & m32
+    r = np.asarray(row_ids, dtype=np.uint64)[:, None]
+    i = (r * np.uint64(d // 2) + np.arange(d // 2, dtype=np.uint64)[None, :]) & m32
+    h = (i * np.uint64(0x9E3779B1) + s0) & m32
+    h ^= s1
+    h ^= h >> np.uint64(16)
+    h = (h * np.uint64(0x85EBCA6B)) & m32
+    h ^= h >> np.uint64(13)
+    h = (h * np.uint64(0xC2B2AE35)) & m32
+    h ^= h >> np.uint64(16)
+    thr = np.uint64(int(p * 65536.0 + 0.5))
+    keep = np.empty((r.shape[0], d), dtype=bool)
+    keep[:, 0::2] = (h & np.uint64(0xFFFF)) >= thr
+    keep[:, 1::2] = (h >> np.uint64(16)) >= thr
+    return keep
+
+
+def eval_counts(prob, label: int, activation_threshold: float = 0.5) -> np.ndarray:
+    """counts [4] of one labelled set: [2 label] = #(p >= thr), [2 label + 1] = #(p > thr)."""
+    c = np.zeros(4)
+    c[2 * label] = float((prob >= activation_threshold).sum())
+    c[2 * label + 1] = float((prob > activation_threshold).sum())
+    return c
+
+
+def eval_finish(cv, ct, sizes, nw_before: float, target: float = 1.5, ratio: float = 2.0):
+    """trainer.py:511-536, :552-561 on the counts: validation false positives per
+    hour (an integer count tensor / a Python float -> float32), recall
+    (preds > threshold over the positives), the testing false-positive rate,
+    recall and accuracy, and the dynamic negative weight."""
+    n_neg_v, n_pos_v, n_neg_t, n_pos_t = sizes
+    hours = np.float32(n_neg_v * 1.44 / 3600)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        fph = np.float32(cv[0]) / hours
+    rec = cv[3] / n_pos_v if n_pos_v > 0 else 0.0
+    nw = nw_before
+    if ratio > 0:
+        nw = nw_before * ratio if fph > target else max(1.0, nw_before / ratio)
+    out = [float(fph), rec]
+    if ct is not None:
+        out += [ct[0] / max(n_neg_t, 1.0), ct[3] / n_pos_t if n_pos_t > 0 else 0.0,
+                (ct[3] + (n_neg_t - ct[1])) / max(n_neg_t + n_pos_t, 1.0)]
+    else:
+        out += [0.0, 0.0, 0.0]
+    return np.array(out + [nw, nw_before, 0.0])

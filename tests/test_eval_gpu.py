@@ -1,0 +1,121 @@
+"""The evaluation passes of train_epoch on the GPU (hbk_mlp_eval_*,
+kv_gemm_kernel + k2_rows_kernel<false> + kv_finish_kernel): the validation /
+testing forwards of trainer.py:496-566 reduced to prediction counts, and the
+post-validation bookkeeping (false positives per hour, recall, testing rates,
+dynamic negative weight, trainer.py:509-536).
+
+Oracle: oracle/mlp.py (float64 forward, the counter-based dropout mask
+restated, eval_counts / eval_finish). The classifier forward itself is pinned
+against the reference (tests/golden/classifier.npz, test_mlp_fused_gpu.py);
+here the input LayerNorm is folded into the GEMM's epilogue and the rows run
+through the throughput kernel. Tolerance: probabilities 2e-5 absolute (the
+split-f16 products are ~2^-22 relative; the fold adds ~|mean / std| of that);
+counts exact against the kernel's own probabilities, and against the oracle's
+away from the threshold.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import mlp as omlp
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(params):
+    from heybuddy.wakeword import WakeWordMLPModel
+    m = WakeWordMLPModel()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=True)
+    return m.cuda()
+
+
+def _pools(seed=0, n32=300, n16=500):
+    rng = np.random.default_rng(seed)
+    p32 = (rng.standard_normal((n32, 16, 96)) * 1.5 + 0.3).astype(np.float32)
+    p16 = (rng.standard_normal((n16, 16, 96)) - 0.2).astype(np.float16)
+    return p32, p16
+
+
+def _run(plan, flat, pool, rows, label, p=0.0, seed=0, row_offset=0, idx=None):
+    ws = torch.empty(plan.eval_workspace_bytes(rows), dtype=torch.uint8, device="cuda")
+    plan.eval_prepare(flat, ws)
+    counts = torch.zeros(4, device="cuda")
+    prob = torch.zeros(rows, device="cuda")
+    plan.eval_count(flat, pool, rows, label, counts, ws, idx=idx, row_offset=row_offset, dropout_p=p, seed=seed,
+                    prob=prob)
+    return counts.cpu().numpy(), prob.cpu().numpy()
+
+
+def test_eval_probabilities_and_counts_match_oracle():
+    params = omlp.init_params(seed=5)
+    m = _model(params)
+    p32, p16 = _pools()
+    # positives from an f32 pool, every row once
+    c, pr = _run(m.plan, m.flat_parameters, torch.from_numpy(p32).cuda(), 300, 1)
+    ref, _, _ = omlp.forward(params, p32)
+    np.testing.assert_allclose(pr, ref, atol=2e-5, rtol=0)
+    np.testing.assert_array_equal(c, omlp.eval_counts(pr, 1))
+    # negatives from an f16 pool, 1,000 rows wrapping around its 500 (row r = pool row r % 500)
+    c16, pr16 = _run(m.plan, m.flat_parameters, torch.from_numpy(p16).cuda(), 1000, 0)
+    ref16, _, _ = omlp.forward(params, p16.astype(np.float32))
+    np.testing.assert_allclose(pr16[:500], ref16, atol=2e-5, rtol=0)
+    np.testing.assert_allclose(pr16[500:], pr16[:500], atol=1e-6, rtol=0)  # no dropout: independent of r
+    np.testing.assert_array_equal(c16, omlp.eval_counts(pr16, 0))
+    # against the oracle's counts: exact but for predictions within the tolerance of the threshold
+    allref = np.concatenate([ref16, ref16])
+    near = int((np.abs(allref - 0.5) <= 2e-5).sum())
+    assert np.abs(c16 - omlp.eval_counts(allref, 0)).max() <= near
+    assert 0 < c16[0] < 1000  # the seeded weights put predictions on both sides
+
+
+def test_eval_dropout_mask_and_indexed_rows():
+    """Dropout p = 0.1 (the reference keeps it on in validation): the mask is
+    the counter hash of (seed, row_offset + r, element), restated in the
+    oracle; rows by an index array."""
+    params = omlp.init_params(seed=6)
+    m = _model(params)
+    p32, p16 = _pools(seed=1)
+    rng = np.random.default_rng(2)
+    idx = rng.integers(0, 500, 700).astype(np.int32)
+    seed, off = 0x1234_5678_9ABC, 4242
+    c, pr = _run(m.plan, m.flat_parameters, torch.from_numpy(p16).cuda(), 700, 0, p=0.1, seed=seed, row_offset=off,
+                 idx=torch.from_numpy(idx).cuda())
+    keep = omlp.dropout_keep(seed, off + np.arange(700), p=0.1)
+    x = p16[idx].astype(np.float32).reshape(700, -1) * keep / np.float32(0.9)
+    ref, _, _ = omlp.forward(params, x.reshape(700, 16, 96))
+    np.testing.assert_allclose(pr, ref, atol=2e-5, rtol=0)
+    np.testing.assert_array_equal(c, omlp.eval_counts(pr, 0))
+    # f32 rows with dropout
+    c, pr = _run(m.plan, m.flat_parameters, torch.from_numpy(p32).cuda(), 300, 1, p=0.1, seed=seed + 1)
+    keep = omlp.dropout_keep(seed + 1, np.arange(300), p=0.1)
+    ref, _, _ = omlp.forward(params, (p32.reshape(300, -1) * keep / np.float32(0.9)).reshape(300, 16, 96))
+    np.testing.assert_allclose(pr, ref, atol=2e-5, rtol=0)
+
+
+def test_eval_chunk_boundary_and_ragged_tiles():
+    """More rows than one launch chunk (131,072) and a ragged last tile."""
+    params = omlp.init_params(seed=7)
+    m = _model(params)
+    _, p16 = _pools(seed=3, n16=333)
+    rows = 131072 + 301
+    c, pr = _run(m.plan, m.flat_parameters, torch.from_numpy(p16).cuda(), rows, 0, row_offset=5)
+    ref, _, _ = omlp.forward(params, p16.astype(np.float32))
+    np.testing.assert_allclose(pr, ref[(5 + np.arange(rows)) % 333], atol=2e-5, rtol=0)
+    np.testing.assert_array_equal(c, omlp.eval_counts(pr, 0))
+
+
+def test_eval_finish_matches_reference_bookkeeping():
+    from heybuddy.kernels import MlpPlan
+    sizes = (500_000.0, 25_000.0, 25_000.0, 25_000.0)
+    cv = np.array([310.0, 309.0, 24_000.0, 23_990.0], np.float32)
+    ct = np.array([120.0, 118.0, 20_000.0, 19_876.0], np.float32)
+    for cv0, nw0 in ((310.0, 1.0), (100.0, 4.0), (10.0, 1.0), (0.0, 8.0)):
+        cv[0] = cv0
+        sched = torch.tensor([[1e-3, nw0]] * 10, device="cuda")
+        out = torch.zeros(8, device="cuda")
+        MlpPlan.eval_finish(torch.from_numpy(cv).cuda(), torch.from_numpy(ct).cuda(), sizes, out, target=1.5,
+                            ratio=2.0, sched=sched, next_step=4)
+        ref = omlp.eval_finish(cv, ct, sizes, nw0, 1.5, 2.0)
+        np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-6)
+        s = sched.cpu().numpy()
+        assert (s[:4, 1] == nw0).all() and (s[4:, 1] == np.float32(ref[5])).all()

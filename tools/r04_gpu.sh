@@ -1,0 +1,30 @@
+#!/bin/bash
+# Round-4 GPU session: GPU tests + smoke, the driver's bench command, the train-step CU probe.
+# STEPS selects parts (default "tests bench cus"); every GPU step has its own time limit and
+# the first failure ends the script.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(pwd)}"
+export TMPDIR=/tmp
+OUT=gpurun_out
+mkdir -p $OUT
+TAG=${TAG:-r04a}
+for S in ${STEPS:-tests bench cus}; do
+  case $S in
+    tests)
+      echo "=== tests"
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/${TAG}_tests_gpu.log 2>&1 || { tail -40 $OUT/${TAG}_tests_gpu.log; exit 1; }
+      tail -2 $OUT/${TAG}_tests_gpu.log
+      echo "=== smoke"
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/${TAG}_smoke.log 2>&1 || { tail -20 $OUT/${TAG}_smoke.log; exit 1; }
+      tail -1 $OUT/${TAG}_smoke.log ;;
+    bench)
+      echo "=== bench (driver settings) ${BENCH_ARGS:-}"
+      timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 ${BENCH_ARGS:-} > $OUT/${TAG}_bench_c5.json 2> $OUT/${TAG}_bench_c5.err || { tail -30 $OUT/${TAG}_bench_c5.err; exit 1; }
+      cut -c1-400 $OUT/${TAG}_bench_c5.json ;;
+    cus)
+      echo "=== train step per CU count"
+      timeout -k 10 500 bash tools/mlp_cus.sh > $OUT/${TAG}_mlp_cus.log 2>&1 || { tail -20 $OUT/${TAG}_mlp_cus.log; exit 1; }
+      cat $OUT/${TAG}_mlp_cus.log ;;
+  esac
+done
+echo "=== done"
