@@ -154,6 +154,30 @@ def roof(kernel, bound, work, ms, unit, traffic, peak=None, **extra):
     return d
 
 
+def mel_variant_roofline(x, mplan, n):
+    """Untimed, after the measurement: the mel stage with the split-f16 MFMA
+    filterbank (hbk_mel_set_variant 1, mel_frames_mfma_kernel) on the same clips,
+    beside the default sparse VALU filterbank (north_star names the MFMA form;
+    both are reported). HBM algorithmic bytes as the default's entry."""
+    from heybuddy.kernels import mel_frames
+    mplan.set_variant(1)
+    try:
+        mel_frames(x, mplan, N_FRAMES)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(3):
+            mel_frames(x, mplan, N_FRAMES)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / 3
+    finally:
+        mplan.set_variant(0)
+    return roof("mel_frames_mfma_kernel (variant: the 32-mel filterbank as a dense split-f16 "
+                "v_mfma_f32_16x16x32_f16 product, 24 MFMAs per 4 frames; %d clips, untimed)" % n, "hbm",
+                n * (MEL_READ_SAMPLES * 4 + N_FRAMES * 32 * 4), ms, "GB/s", None,
+                algorithmic_bytes_per_clip=MEL_READ_SAMPLES * 4 + N_FRAMES * 32 * 4, clips=n)
+
+
 def prof_mark(tag, dev):
     """hbk_profile_mark_kernel on the current stream, behind a device
     synchronize (outside the timed region): rocprofv3 traces and counter
@@ -364,8 +388,12 @@ def setup_featurize(args, dev, rank, world, seed):
         return {"value": round(sample / el, 2), "unit": "clips/s", "cores": threads, "kind": "port",
                 "sample": f"{sample} of the step's clips through oracle/ ({what}), {el:.1f} s"}
 
+    def extra_rooflines():
+        return [mel_variant_roofline(aug(clips, out=aug_out) if augment else clips, mplan, n)]
+
     return {
         "step": step, "stages": stages, "roofline": roofline, "cpu_baseline": cpu_baseline,
+        "extra_rooflines": extra_rooflines,
         "units_per_step": n, "scaling": "weak", "unit": "clips/s",
         "metric": "audio clips/sec featurized+trained, 1.5 s @16 kHz, 1/2/4/8 GPU",
         "data": "synthetic 1.5 s @16 kHz clips (seeded), SE20 stand-in embedding graph"
@@ -1018,6 +1046,7 @@ def setup_e2e(args, dev, rank, world, seed):
                       "kernel on every chain, as for a graph without SE20's chain shapes; %d clips, untimed)" % m,
                       "mfma", 2.0 * gplan.macs_per_clip * m, ms, "TFLOP/s", None, peak=SPLIT_PEAK_TFLOPS,
                       peak_basis="f16 dense MFMA peak / 3", clips=m)]
+        extra.append(mel_variant_roofline(aug.augment_device(src, lens), mplan, n))
         return extra
 
     return {

@@ -463,13 +463,259 @@ mel_frames_v2_kernel(Mel2Args a) {
   }
 }
 
+
+// ------------------------------------------------------------------ v3 ----
+// The MFMA filterbank variant (BASELINE north_star: "MFMA used only for the
+// mel-filterbank x power-spectrum ... contractions"): the transform of v2, then
+// the 32-mel filterbank as a dense [frames x 128 bins] x [128 x 32] product on
+// v_mfma_f32_16x16x32_f16 instead of the sparse per-lane dot products.
+//  - f32 accuracy from f16 operands: every frame's power row is scaled by a
+//    power of two into [0, 2^15) (|X|^2 reaches ~1e14) and split hi / lo, the
+//    weights (x 2^8) likewise; hi*hi + hi*lo + lo*hi, f32 accumulation: the
+//    products are ~2^-22 relative and the sums are of non-negative terms (no
+//    cancellation), far inside the 1e-4 output tolerance;
+//  - a wave holds 4 frames, an MFMA tile 16 rows: row 4 q + f holds frame f's
+//    bins of quarter q (32 bins, the 32-deep k-block q; zero elsewhere), so each
+//    lane fetches ONE k-block of one frame from the power row in LDS and the
+//    4 k-blocks x 2 mel tiles x 3 products = 24 MFMAs give the 4 quarters'
+//    partial sums in 4 rows each; a reduce-scatter over the quarters
+//    (v_permlane32_swap, v_permlane16_swap) leaves frame kq's two mels on lane
+//    (n, kq), i.e. the log of v2's 2 values per lane;
+//  - 6-wave blocks (2 per CU: the split weight planes take 17 KB of LDS).
+// The dense product multiplies ~4x the non-zero taps, on the matrix pipe.
+constexpr int kWaves3 = 6;
+constexpr int kThreads3 = 64 * kWaves3;
+constexpr int kFramesPerBlock3 = kFramesPerWave * kWaves3;
+constexpr int kBlocksPerCU3 = 2;
+constexpr int kWLd3 = kBins2 + 8;  // halves per mel row of a weight plane (bank spread)
+constexpr float kWScale3 = 256.f;
+typedef _Float16 h8m __attribute__((ext_vector_type(8)));
+typedef _Float16 h2m __attribute__((ext_vector_type(2)));
+typedef float f2m __attribute__((ext_vector_type(2)));
+typedef float f4m __attribute__((ext_vector_type(4)));
+
+struct Mel3Args {
+  const float* pcm;
+  float* out;
+  const float* window;  // [512], in_scale folded in
+  const float2* tw256;  // [256] W256^i
+  const float2* twsm;   // [128] -i W512^k
+  const float* fbt;     // [32][128] filterbank^T x 1/4 (the split's 1/2, squared)
+  int64_t n_clips;
+  int64_t clip_stride;
+  int64_t n_frames;
+  int hop;
+  float log_floor;
+  float out_scale;  // 10 / out_div
+  float out_add;
+};
+
+__device__ __forceinline__ void split8m(const float (&v)[8], h8m& hi, h8m& lo) {
+#pragma unroll
+  for (int e = 0; e < 8; e += 2) {
+    const h2m h = __builtin_convertvector(f2m{v[e], v[e + 1]}, h2m);
+    const f2m r = f2m{v[e], v[e + 1]} - __builtin_convertvector(h, f2m);
+    const h2m l = __builtin_convertvector(r, h2m);
+    hi[e] = h[0];
+    hi[e + 1] = h[1];
+    lo[e] = l[0];
+    lo[e + 1] = l[1];
+  }
+}
+// reduce-scatter across lane ^ 16 / lane ^ 32 (v_permlane*_swap; see hbk_augment.hip's pv_swap_add)
+template <bool kSwap16>
+__device__ __forceinline__ float mel_swap_add(float x, float y) {
+  if (kSwap16)
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(x), "+v"(y));
+  else
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(x), "+v"(y));
+  return x + y;
+}
+
+template <bool EDGE0, class C>
+__global__ void __launch_bounds__(kThreads3) __attribute__((amdgpu_waves_per_eu(3)))
+mel_frames_mfma_kernel(Mel3Args a) {
+  __shared__ __attribute__((aligned(16))) cf s_frame[kFramesPerBlock3 * kFrameC2];
+  __shared__ __attribute__((aligned(16))) cf s_c[kCWa * 16 + 16 * 16];  // tw (16), ws (8), window (16)
+  __shared__ __attribute__((aligned(16))) _Float16 s_w[2][kMaxMels][kWLd3];
+  __shared__ float s_inv[kWaves3][kFramesPerWave];
+  constexpr int kCWin3 = kCWa;  // window entries follow the twiddles here
+  const int tid = threadIdx.x;
+  for (int i = tid; i < (kCWin3 + 16) * 16; i += kThreads3) {
+    const int e = i >> 4, jj = i & 15;
+    cf c;
+    if (e < kCWs) {
+      const float2 t = a.tw256[(jj * e) & 255];
+      c = cf{t.x, t.y};
+    } else if (e < kCWa) {
+      const float2 t = a.twsm[jj + 16 * (e - kCWs)];
+      c = cf{t.x, t.y};
+    } else {
+      c = *reinterpret_cast<const cf*>(a.window + 2 * (16 * (e - kCWin3) + jj));
+    }
+    s_c[i] = c;
+  }
+  for (int i = tid; i < kMaxMels * kBins2 / 2; i += kThreads3) {
+    const int m = i / (kBins2 / 2), k = 2 * (i % (kBins2 / 2));
+    const float w0 = a.fbt[m * kBins2 + k] * kWScale3, w1 = a.fbt[m * kBins2 + k + 1] * kWScale3;
+    const h2m h = __builtin_convertvector(f2m{w0, w1}, h2m);
+    const h2m l = __builtin_convertvector(f2m{w0, w1} - __builtin_convertvector(h, f2m), h2m);
+    *reinterpret_cast<h2m*>(&s_w[0][m][k]) = h;
+    *reinterpret_cast<h2m*>(&s_w[1][m][k]) = l;
+  }
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int slot = wave * kFramesPerWave + (lane >> 4);
+  const int j = lane & 15;
+  const int kq = lane >> 4;  // MFMA lane group (== the frame slot of the transform)
+  const cf* cj = s_c + j;
+  __syncthreads();
+
+  const uint32_t total = static_cast<uint32_t>(a.n_clips * a.n_frames);
+  const uint32_t nf = static_cast<uint32_t>(a.n_frames);
+  const uint32_t groups = (total + kFramesPerBlock3 - 1) / kFramesPerBlock3;
+  cf* buf = s_frame + slot * kFrameC2;
+  float* pbuf = reinterpret_cast<float*>(buf) + (slot & 1) * 32;
+  // MFMA operand rows: row m = 4 q + f reads frame f's quarter q
+  const int mq = j >> 2, mf = j & 3;
+  const float* arow = reinterpret_cast<const float*>(s_frame + (wave * kFramesPerWave + mf) * kFrameC2) +
+                      (mf & 1) * 32 + 32 * mq + 8 * kq;
+  constexpr int n1lo = EDGE0 ? 1 : 0, n1hi = EDGE0 ? 15 : 16;
+
+  auto frame_src = [&](uint32_t grp) {
+    uint32_t g = min(grp, groups - 1) * kFramesPerBlock3 + slot;
+    g = g < total ? g : total - 1;
+    const uint32_t clip = g / nf;
+    const uint32_t f = g - clip * nf;
+    return a.pcm + static_cast<int64_t>(clip) * a.clip_stride + static_cast<int64_t>(f) * a.hop + 2 * j;
+  };
+  auto load = [&](const float* src, C (&x)[16]) {
+#pragma unroll
+    for (int n1 = n1lo; n1 < n1hi; ++n1) x[n1] = cpx<C>(*reinterpret_cast<const cf*>(src + 32 * n1));
+  };
+
+  auto process = [&](uint32_t grp, const C (&cur)[16], C (&nxt)[16]) {
+    C v[16];
+#pragma unroll
+    for (int n1 = n1lo; n1 < n1hi; ++n1) v[n1] = cpx<C>(cj[16 * (kCWin3 + n1)]);
+    C tw[16];
+#pragma unroll
+    for (int k1 = 1; k1 < 16; ++k1) tw[k1] = cpx<C>(cj[16 * (kCTw + k1)]);
+#pragma unroll
+    for (int n1 = 0; n1 < 16; ++n1) v[n1] = (n1 < n1lo || n1 >= n1hi) ? C{0.f, 0.f} : cur[n1] * v[n1];
+    load(frame_src(grp + gridDim.x), nxt);  // prefetch (clamped past the end)
+    fft16(v);
+#pragma unroll
+    for (int k1 = 1; k1 < 16; ++k1) v[k1] = cmul(v[k1], tw[k1]);
+#pragma unroll
+    for (int k1 = 0; k1 < 16; ++k1) buf[k1 * kRow2 + j] = cf{v[k1].x, v[k1].y};
+    wave_sync();
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float4 t = *reinterpret_cast<const float4*>(buf + j * kRow2 + 2 * q);
+      v[2 * q] = C{t.x, t.y};
+      v[2 * q + 1] = C{t.z, t.w};
+    }
+    C ws[8];
+#pragma unroll
+    for (int k2 = 0; k2 < 8; ++k2) ws[k2] = cpx<C>(cj[16 * (kCWs + k2)]);
+    fft16(v);
+    float p[8];
+    int mx[8], my[8];
+#pragma unroll
+    for (int k2 = 0; k2 < 8; ++k2) {
+      mx[k2] = mirror(v[15 - k2].x);
+      my[k2] = mirror(v[15 - k2].y);
+    }
+#pragma unroll
+    for (int k2 = 0; k2 < 8; ++k2) {
+      const C own = v[(16 - k2) & 15];
+      const C zr = C{shr1_or(mx[k2], own.x), shr1_or(my[k2], own.y)};
+      const C zc = C{zr.x, -zr.y};
+      const C s = v[k2] + zc;
+      const C d = v[k2] - zc;
+      const C X = s + cmul(d, ws[k2]);
+      p[k2] = fmaf(X.x, X.x, X.y * X.y);
+    }
+    // the frame's power-of-two scale: max over its 16 lanes' bins into [2^14, 2^15)
+    float pm = fmaxf(fmaxf(fmaxf(p[0], p[1]), fmaxf(p[2], p[3])), fmaxf(fmaxf(p[4], p[5]), fmaxf(p[6], p[7])));
+    pm = fmaxf(pm, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, pm), 0xB1, 0xF, 0xF, false)));
+    pm = fmaxf(pm, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, pm), 0x4E, 0xF, 0xF, false)));
+    pm = fmaxf(pm, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, pm), 0x141, 0xF, 0xF, false)));
+    pm = fmaxf(pm, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, pm), 0x140, 0xF, 0xF, false)));
+    const int ex = (__builtin_bit_cast(int, pm) >> 23) & 255;
+    const int pw = max(-100, min(100, 141 - ex));
+    const float sc = __builtin_bit_cast(float, (127 + pw) << 23);
+    wave_sync();
+#pragma unroll
+    for (int k2 = 0; k2 < 8; ++k2) pbuf[j + 16 * k2] = p[k2] * sc;
+    if (j == 0) s_inv[wave][kq] = __builtin_bit_cast(float, (127 - pw) << 23) * (1.f / kWScale3);
+    wave_sync();
+    // A: this lane's quarter of its frame (row 4 mq + mf), zero in the other k-blocks
+    float av[8];
+    {
+      const float4 t0 = *reinterpret_cast<const float4*>(arow), t1 = *reinterpret_cast<const float4*>(arow + 4);
+      av[0] = t0.x; av[1] = t0.y; av[2] = t0.z; av[3] = t0.w;
+      av[4] = t1.x; av[5] = t1.y; av[6] = t1.z; av[7] = t1.w;
+    }
+    h8m ah, al;
+    split8m(av, ah, al);
+    const h8m hz = {};
+    f4m acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const h8m aih = mq == i ? ah : hz, ail = mq == i ? al : hz;
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        const h8m bh = *reinterpret_cast<const h8m*>(&s_w[0][16 * ct + j][32 * i + 8 * kq]);
+        const h8m bl = *reinterpret_cast<const h8m*>(&s_w[1][16 * ct + j][32 * i + 8 * kq]);
+        acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aih, bh, acc[ct], 0, 0, 0);
+        acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aih, bl, acc[ct], 0, 0, 0);
+        acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ail, bh, acc[ct], 0, 0, 0);
+      }
+    }
+    // lane (n, kq) holds quarter kq of frames 0..3: reduce-scatter over the quarters -> frame kq
+    float y[2];
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      const float w0 = mel_swap_add<false>(acc[ct][0], acc[ct][2]);  // frames 0 / 2 (lane bit 5)
+      const float w1 = mel_swap_add<false>(acc[ct][1], acc[ct][3]);  // frames 1 / 3
+      y[ct] = mel_swap_add<true>(w0, w1);                            // frame 2 (kq >> 1) + (kq & 1) = kq
+    }
+    const float inv = s_inv[wave][kq];
+    const uint32_t g = grp * kFramesPerBlock3 + wave * kFramesPerWave + kq;
+    if (g < total) {
+      float* o = a.out + static_cast<int64_t>(g) * kMaxMels;
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        const float acc1 = y[ct] * inv;
+        const float c = acc1 < a.log_floor ? a.log_floor : acc1;  // keeps NaN
+        o[16 * ct + j] = log10f(c) * a.out_scale + a.out_add;
+      }
+    }
+    wave_sync();  // the next group's transpose overwrites the frame buffers
+  };
+
+  uint32_t grp = blockIdx.x;
+  C xa[16], xb[16];
+  if (grp < groups) load(frame_src(grp), xa);
+  while (grp < groups) {
+    process(grp, xa, xb);
+    grp += gridDim.x;
+    if (grp >= groups) break;
+    process(grp, xb, xa);
+    grp += gridDim.x;
+  }
+}
 }  // namespace
 }  // namespace hbk
 
 #ifdef HBK_MEL_PACKED
 #define HBK_MEL_V2(e) (hbk::mel_frames_v2_kernel<e, hbk::cf>)
+#define HBK_MEL_V3(e) (hbk::mel_frames_mfma_kernel<e, hbk::cf>)
 #else
 #define HBK_MEL_V2(e) (hbk::mel_frames_v2_kernel<e, hbk::sc>)
+#define HBK_MEL_V3(e) (hbk::mel_frames_mfma_kernel<e, hbk::sc>)
 #endif
 
 struct hbk_mel_plan {
@@ -485,6 +731,9 @@ struct hbk_mel_plan {
   float2* d_twsm = nullptr;
   int* d_lo2 = nullptr;
   float* d_w2 = nullptr;
+  // v3 (hbk_mel_set_variant 1): the dense filterbank^T [32][128] x 1/4 for the MFMA variant
+  int variant = 0;
+  float* d_fbt = nullptr;
 };
 
 extern "C" {
@@ -611,6 +860,13 @@ int hbk_mel_plan_create(const float* window, const float* fbank, int n_fft, int 
       return fail(e, "copy lo2");
     if ((e = hipMemcpy(p->d_w2, w2.data(), w2.size() * sizeof(float), hipMemcpyHostToDevice)) != hipSuccess)
       return fail(e, "copy w2");
+    std::vector<float> fbt(static_cast<size_t>(kMaxMels) * kBins2);
+    for (int m = 0; m < kMaxMels; ++m)
+      for (int k = 0; k < kBins2; ++k) fbt[m * kBins2 + k] = 0.25f * fbank[k * n_mels + m];
+    if ((e = hipMalloc(&p->d_fbt, fbt.size() * sizeof(float))) != hipSuccess) return fail(e, "hipMalloc fbt");
+    if ((e = hipMemcpy(p->d_fbt, fbt.data(), fbt.size() * sizeof(float), hipMemcpyHostToDevice)) != hipSuccess)
+      return fail(e, "copy fbt");
+    p->variant = getenv("HBK_MEL_MFMA") ? 1 : 0;
   }
   *plan = p;
   return HBK_OK;
@@ -626,7 +882,20 @@ int hbk_mel_plan_destroy(hbk_mel_plan* p) {
   (void)hipFree(p->d_twsm);
   (void)hipFree(p->d_lo2);
   (void)hipFree(p->d_w2);
+  (void)hipFree(p->d_fbt);
   delete p;
+  return HBK_OK;
+}
+
+int hbk_mel_set_variant(hbk_mel_plan* plan, int32_t variant) {
+  using namespace hbk;
+  if (!plan) return arg_error("plan is NULL");
+  if (variant != 0 && variant != 1) return arg_error("variant must be 0 (sparse VALU) or 1 (MFMA)");
+  if (variant == 1 && !plan->v2) {
+    set_error("hbk: the MFMA filterbank variant covers 32 mels on bins < 128");
+    return HBK_ERR_UNSUPPORTED;
+  }
+  plan->variant = variant;
   return HBK_OK;
 }
 
@@ -643,6 +912,32 @@ int hbk_mel_frames(const hbk_mel_plan* plan, const float* pcm, int64_t n_clips, 
   if (plan->hop * (n_frames - 1) + plan->n_fft > clip_stride) return arg_error("frames exceed clip_stride");
   const int64_t total = n_clips * n_frames;
   if (total >= (int64_t(1) << 31)) return arg_error("more than 2^31 frames in one call");
+  if (plan->v2 && plan->variant == 1) {
+    const int64_t groups3 = (total + kFramesPerBlock3 - 1) / kFramesPerBlock3;
+    Mel3Args a;
+    a.pcm = pcm;
+    a.out = out;
+    a.window = plan->d_window;
+    a.tw256 = plan->d_tw256;
+    a.twsm = plan->d_twsm;
+    a.fbt = plan->d_fbt;
+    a.n_clips = n_clips;
+    a.clip_stride = clip_stride;
+    a.n_frames = n_frames;
+    a.hop = plan->hop;
+    a.log_floor = plan->log_floor;
+    a.out_scale = 10.f / plan->out_div;
+    a.out_add = plan->out_add;
+    const int64_t blocks = std::min<int64_t>(groups3, persistent_blocks(kBlocksPerCU3, stream));
+    if (plan->edge0)
+      hipLaunchKernelGGL(HBK_MEL_V3(true), dim3(static_cast<unsigned>(blocks)), dim3(kThreads3), 0,
+                         as_stream(stream), a);
+    else
+      hipLaunchKernelGGL(HBK_MEL_V3(false), dim3(static_cast<unsigned>(blocks)), dim3(kThreads3), 0,
+                         as_stream(stream), a);
+    HBK_LAUNCH_CHECK("mel_frames_mfma_kernel");
+    return HBK_OK;
+  }
   if (plan->v2) {
     const int64_t groups2 = (total + kFramesPerBlock2 - 1) / kFramesPerBlock2;
     Mel2Args a;

@@ -53,6 +53,7 @@ _PROTOS = {
     "hbk_mel_plan_create": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int, _c_float, _c_float,
                                      _c_float, _c_float, ctypes.POINTER(_vp)]),
     "hbk_mel_plan_destroy": (_c_int, [_vp]),
+    "hbk_mel_set_variant": (_c_int, [_vp, ctypes.c_int32]),
     "hbk_mel_frames": (_c_int, [_vp, _vp, _c_int64, _c_int64, _c_int64, _vp, _vp]),
     "hbk_embed_plan_create": (_c_int, [_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _vp,
                                        ctypes.c_int32, ctypes.POINTER(_vp)]),

@@ -70,6 +70,12 @@ class MelPlan:
     def n_frames(self, n_samples: int) -> int:
         return 0 if n_samples < self.n_fft else (n_samples - self.n_fft) // self.hop + 1
 
+    def set_variant(self, variant: int) -> "MelPlan":
+        """The filterbank stage (hbk_mel_set_variant): 0 = sparse per-lane dot
+        products on the VALU (default), 1 = the dense split-f16 MFMA product."""
+        check(lib().hbk_mel_set_variant(self._handle, int(variant)), "hbk_mel_set_variant")
+        return self
+
     def __call__(self, pcm: torch.Tensor, n_frames: int | None = None) -> torch.Tensor:
         return mel_frames(pcm, self, n_frames)
 

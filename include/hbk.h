@@ -79,6 +79,11 @@ int hbk_mel_plan_create(const float* window, const float* fbank, int n_fft,
                         int hop, int n_mels, float in_scale, float log_floor,
                         float out_div, float out_add, hbk_mel_plan** plan);
 int hbk_mel_plan_destroy(hbk_mel_plan* plan);
+/* The filterbank stage of hbk_mel_frames: 0 = sparse per-lane dot products on
+ * the VALU (default), 1 = a dense split-f16 MFMA product (32 mels on bins < 128
+ * only; HBK_MEL_MFMA=1 in the environment selects it at plan creation).
+ * Same transform and outputs (within the 1e-4 tolerance). */
+int hbk_mel_set_variant(hbk_mel_plan* plan, int32_t variant);
 
 /* pcm: [n_clips, clip_stride] f32; frames f in [0, n_frames) of every clip
  *   (caller guarantees hop*(n_frames-1) + n_fft <= samples per clip);

@@ -72,9 +72,10 @@ def _clips(n=24, length=24000):
 
 
 @pytest.mark.gpu
-def test_mel_kernel_parity_realistic_clips():
+@pytest.mark.parametrize("variant", [0, 1])  # sparse VALU filterbank / split-f16 MFMA filterbank
+def test_mel_kernel_parity_realistic_clips(variant):
     from heybuddy.kernels import MelPlan
-    plan = MelPlan(omel.hann_window(), omel.mel_fbank())
+    plan = MelPlan(omel.hann_window(), omel.mel_fbank()).set_variant(variant)
     clips, _ = _clips()
     out = plan(clips.cuda(), 141).cpu().numpy()
     ref, _, _ = omel.mel_frames(clips.numpy(), 141)
@@ -84,9 +85,10 @@ def test_mel_kernel_parity_realistic_clips():
 
 
 @pytest.mark.gpu
-def test_mel_kernel_parity_edge_clips():
+@pytest.mark.parametrize("variant", [0, 1])
+def test_mel_kernel_parity_edge_clips(variant):
     from heybuddy.kernels import MelPlan
-    plan = MelPlan(omel.hann_window(), omel.mel_fbank())
+    plan = MelPlan(omel.hann_window(), omel.mel_fbank()).set_variant(variant)
     _, edges = _clips()
     out = plan(edges.cuda()).cpu().numpy()
     ref, mel_pow, energy = omel.mel_frames(edges.numpy())
@@ -99,11 +101,12 @@ def test_mel_kernel_parity_edge_clips():
 
 
 @pytest.mark.gpu
-def test_mel_kernel_ragged_and_strided():
+@pytest.mark.parametrize("variant", [0, 1])
+def test_mel_kernel_ragged_and_strided(variant):
     """Odd clip counts (partial last block), a frame count below the maximum,
     and a strided (row-sliced) input."""
     from heybuddy.kernels import MelPlan
-    plan = MelPlan(omel.hann_window(), omel.mel_fbank())
+    plan = MelPlan(omel.hann_window(), omel.mel_fbank()).set_variant(variant)
     clips, _ = _clips(n=7, length=23040)
     big = torch.zeros((7, 24000))
     big[:, :23040] = clips

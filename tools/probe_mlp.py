@@ -4,6 +4,10 @@
                                              steps of B = 1100 (bench composition)
   python tools/probe_mlp.py --trace          s_memtime stage timeline of block 0's
                                              waves in k1 / k2 / k3 (libhbk_trace.so)
+  options: --cus=N (a stream masked to N CUs), --batch=B (the stage-1 mix
+  scaled to B rows), --reduce (a one-rank RCCL group with
+  HBK_DP_REDUCE_ALWAYS=1: every step's bucket all-reduce captured into the
+  graph, as the data-parallel path runs it)
 """
 import ctypes
 import os
@@ -21,7 +25,13 @@ import torch  # noqa: E402
 from heybuddy.trainer import WakeWordTrainer  # noqa: E402
 
 
-def setup(S, B=1100, P=50, A=50):
+BATCH = next((int(a[8:]) for a in sys.argv[1:] if a.startswith("--batch=")), 1100)
+
+
+def setup(S, B=None, P=None, A=None):
+    B = BATCH if B is None else B
+    P = max(1, 50 * B // 1100) if P is None else P
+    A = max(1, 50 * B // 1100) if A is None else A
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
     pos = torch.randn((50_000, 16, 96), generator=g, device=dev) + 0.3
@@ -59,7 +69,8 @@ def timing(S, n_cus=0):
         tr.train_indexed(idx, y, sched, pool32=pos, pool16=neg, history=hist, steps_per_graph=50)
     e1.record()
     torch.cuda.synchronize()
-    print(f"{e0.elapsed_time(e1) * 1e3 / (3 * S):.2f} us per train step (B=1100, {S} steps x 3)")
+    print(f"{e0.elapsed_time(e1) * 1e3 / (3 * S):.2f} us per train step (B={BATCH}, {S} steps x 3"
+          f"{', captured 1-rank all-reduce' if '--reduce' in sys.argv else ''})")
 
 
 def trace():
@@ -92,6 +103,11 @@ def trace():
 
 
 if __name__ == "__main__":
+    if "--reduce" in sys.argv:
+        import torch.distributed as dist
+        os.environ.update(HBK_DP_REDUCE_ALWAYS="1", MASTER_ADDR="127.0.0.1", MASTER_PORT="29533",
+                          HSA_ENABLE_IPC_MODE_LEGACY="0")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     if TRACE:
         trace()
     else:

@@ -21,6 +21,26 @@ for S in ${STEPS:-tests bench cus}; do
       echo "=== bench (driver settings) ${BENCH_ARGS:-}"
       timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 ${BENCH_ARGS:-} > $OUT/${TAG}_bench_c5.json 2> $OUT/${TAG}_bench_c5.err || { tail -30 $OUT/${TAG}_bench_c5.err; exit 1; }
       cut -c1-400 $OUT/${TAG}_bench_c5.json ;;
+    configs)
+      for C in 1 2 3 4; do
+        echo "=== bench config $C"
+        timeout -k 10 600 python bench.py --config $C > $OUT/${TAG}_bench_c$C.json 2> $OUT/${TAG}_bench_c$C.err || { tail -30 $OUT/${TAG}_bench_c$C.err; exit 1; }
+        cut -c1-300 $OUT/${TAG}_bench_c$C.json
+      done ;;
+    prof23)
+      for C in 2 3; do
+        echo "=== profile config $C"
+        TAG=$TAG CONFIG=$C SKIP_BENCH=1 timeout -k 10 900 bash tools/profile_headline.sh > $OUT/${TAG}_prof_c$C.log 2>&1 || { tail -30 $OUT/${TAG}_prof_c$C.log; exit 1; }
+        tail -3 $OUT/${TAG}_prof_c$C.log
+      done ;;
+    prof5)
+      echo "=== profile config 5"
+      TAG=$TAG CONFIG=5 SKIP_BENCH=1 timeout -k 10 1100 bash tools/profile_headline.sh > $OUT/${TAG}_prof_c5.log 2>&1 || { tail -30 $OUT/${TAG}_prof_c5.log; exit 1; }
+      tail -3 $OUT/${TAG}_prof_c5.log ;;
+    dp)
+      echo "=== DP step latency"
+      timeout -k 10 900 bash tools/dp_probe.sh > $OUT/${TAG}_dp_probe.log 2>&1 || { tail -20 $OUT/${TAG}_dp_probe.log; exit 1; }
+      cat $OUT/${TAG}_dp_probe.log ;;
     cus)
       echo "=== train step per CU count"
       timeout -k 10 500 bash tools/mlp_cus.sh > $OUT/${TAG}_mlp_cus.log 2>&1 || { tail -20 $OUT/${TAG}_mlp_cus.log; exit 1; }
