@@ -48,8 +48,11 @@ def _run(plan, flat, pool, rows, label, p=0.0, seed=0, row_offset=0, idx=None):
 
 def test_eval_probabilities_and_counts_match_oracle():
     params = omlp.init_params(seed=5)
-    m = _model(params)
     p32, p16 = _pools()
+    # centre the output bias so that the f16 rows' predictions straddle the threshold
+    _, z, _ = omlp.forward(params, p16.astype(np.float32))
+    params["mlp_out.output.bias"] = (params["mlp_out.output.bias"] - np.median(z) + 1e-3).astype(np.float32)
+    m = _model(params)
     # positives from an f32 pool, every row once
     c, pr = _run(m.plan, m.flat_parameters, torch.from_numpy(p32).cuda(), 300, 1)
     ref, _, _ = omlp.forward(params, p32)
