@@ -468,12 +468,15 @@ mel_frames_v2_kernel(Mel2Args a) {
 // The MFMA filterbank variant (BASELINE north_star: "MFMA used only for the
 // mel-filterbank x power-spectrum ... contractions"): the transform of v2, then
 // the 32-mel filterbank as a dense [frames x 128 bins] x [128 x 32] product on
-// v_mfma_f32_16x16x32_f16 instead of the sparse per-lane dot products.
-//  - f32 accuracy from f16 operands: every frame's power row is scaled by a
-//    power of two into [0, 2^15) (|X|^2 reaches ~1e14) and split hi / lo, the
-//    weights (x 2^8) likewise; hi*hi + hi*lo + lo*hi, f32 accumulation: the
-//    products are ~2^-22 relative and the sums are of non-negative terms (no
-//    cancellation), far inside the 1e-4 output tolerance;
+// v_mfma_f32_16x16x32_bf16 instead of the sparse per-lane dot products.
+//  - f32-range operands: the power row and the weights are split into bf16
+//    hi / lo pairs (hi = bf16(x), lo = bf16(x - hi): 16 significant bits, f32's
+//    exponent range). A frame's bins span more than f16's range after any one
+//    scale (a DC clip: ~1e14 at bin 0 against ~1 in the upper filters, which
+//    an f16 split with a per-frame scale flushed to zero), bf16 keeps them.
+//    hi*hi + hi*lo + lo*hi, f32 accumulation: ~2^-16 relative per product, and
+//    the sums are of non-negative terms (no cancellation): ~1e-5 of log10,
+//    inside the 1e-4 output tolerance;
 //  - a wave holds 4 frames, an MFMA tile 16 rows: row 4 q + f holds frame f's
 //    bins of quarter q (32 bins, the 32-deep k-block q; zero elsewhere), so each
 //    lane fetches ONE k-block of one frame from the power row in LDS and the
@@ -487,10 +490,9 @@ constexpr int kWaves3 = 6;
 constexpr int kThreads3 = 64 * kWaves3;
 constexpr int kFramesPerBlock3 = kFramesPerWave * kWaves3;
 constexpr int kBlocksPerCU3 = 2;
-constexpr int kWLd3 = kBins2 + 8;  // halves per mel row of a weight plane (bank spread)
-constexpr float kWScale3 = 256.f;
-typedef _Float16 h8m __attribute__((ext_vector_type(8)));
-typedef _Float16 h2m __attribute__((ext_vector_type(2)));
+constexpr int kWLd3 = kBins2 + 8;  // bf16 per mel row of a weight plane (bank spread)
+typedef __bf16 h8m __attribute__((ext_vector_type(8)));
+typedef __bf16 h2m __attribute__((ext_vector_type(2)));
 typedef float f2m __attribute__((ext_vector_type(2)));
 typedef float f4m __attribute__((ext_vector_type(4)));
 
@@ -537,8 +539,7 @@ __global__ void __launch_bounds__(kThreads3) __attribute__((amdgpu_waves_per_eu(
 mel_frames_mfma_kernel(Mel3Args a) {
   __shared__ __attribute__((aligned(16))) cf s_frame[kFramesPerBlock3 * kFrameC2];
   __shared__ __attribute__((aligned(16))) cf s_c[kCWa * 16 + 16 * 16];  // tw (16), ws (8), window (16)
-  __shared__ __attribute__((aligned(16))) _Float16 s_w[2][kMaxMels][kWLd3];
-  __shared__ float s_inv[kWaves3][kFramesPerWave];
+  __shared__ __attribute__((aligned(16))) __bf16 s_w[2][kMaxMels][kWLd3];
   constexpr int kCWin3 = kCWa;  // window entries follow the twiddles here
   const int tid = threadIdx.x;
   for (int i = tid; i < (kCWin3 + 16) * 16; i += kThreads3) {
@@ -557,7 +558,7 @@ mel_frames_mfma_kernel(Mel3Args a) {
   }
   for (int i = tid; i < kMaxMels * kBins2 / 2; i += kThreads3) {
     const int m = i / (kBins2 / 2), k = 2 * (i % (kBins2 / 2));
-    const float w0 = a.fbt[m * kBins2 + k] * kWScale3, w1 = a.fbt[m * kBins2 + k + 1] * kWScale3;
+    const float w0 = a.fbt[m * kBins2 + k], w1 = a.fbt[m * kBins2 + k + 1];
     const h2m h = __builtin_convertvector(f2m{w0, w1}, h2m);
     const h2m l = __builtin_convertvector(f2m{w0, w1} - __builtin_convertvector(h, f2m), h2m);
     *reinterpret_cast<h2m*>(&s_w[0][m][k]) = h;
@@ -637,19 +638,9 @@ mel_frames_mfma_kernel(Mel3Args a) {
       const C X = s + cmul(d, ws[k2]);
       p[k2] = fmaf(X.x, X.x, X.y * X.y);
     }
-    // the frame's power-of-two scale: max over its 16 lanes' bins into [2^14, 2^15)
-    float pm = fmaxf(fmaxf(fmaxf(p[0], p[1]), fmaxf(p[2], p[3])), fmaxf(fmaxf(p[4], p[5]), fmaxf(p[6], p[7])));
-    pm = fmaxf(pm, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, pm), 0xB1, 0xF, 0xF, false)));
-    pm = fmaxf(pm, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, pm), 0x4E, 0xF, 0xF, false)));
-    pm = fmaxf(pm, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, pm), 0x141, 0xF, 0xF, false)));
-    pm = fmaxf(pm, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, pm), 0x140, 0xF, 0xF, false)));
-    const int ex = (__builtin_bit_cast(int, pm) >> 23) & 255;
-    const int pw = max(-100, min(100, 141 - ex));
-    const float sc = __builtin_bit_cast(float, (127 + pw) << 23);
     wave_sync();
 #pragma unroll
-    for (int k2 = 0; k2 < 8; ++k2) pbuf[j + 16 * k2] = p[k2] * sc;
-    if (j == 0) s_inv[wave][kq] = __builtin_bit_cast(float, (127 - pw) << 23) * (1.f / kWScale3);
+    for (int k2 = 0; k2 < 8; ++k2) pbuf[j + 16 * k2] = p[k2];
     wave_sync();
     // A: this lane's quarter of its frame (row 4 mq + mf), zero in the other k-blocks
     float av[8];
@@ -669,9 +660,9 @@ mel_frames_mfma_kernel(Mel3Args a) {
       for (int ct = 0; ct < 2; ++ct) {
         const h8m bh = *reinterpret_cast<const h8m*>(&s_w[0][16 * ct + j][32 * i + 8 * kq]);
         const h8m bl = *reinterpret_cast<const h8m*>(&s_w[1][16 * ct + j][32 * i + 8 * kq]);
-        acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aih, bh, acc[ct], 0, 0, 0);
-        acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aih, bl, acc[ct], 0, 0, 0);
-        acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ail, bh, acc[ct], 0, 0, 0);
+        acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aih, bh, acc[ct], 0, 0, 0);
+        acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aih, bl, acc[ct], 0, 0, 0);
+        acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ail, bh, acc[ct], 0, 0, 0);
       }
     }
     // lane (n, kq) holds quarter kq of frames 0..3: reduce-scatter over the quarters -> frame kq
@@ -682,13 +673,12 @@ mel_frames_mfma_kernel(Mel3Args a) {
       const float w1 = mel_swap_add<false>(acc[ct][1], acc[ct][3]);  // frames 1 / 3
       y[ct] = mel_swap_add<true>(w0, w1);                            // frame 2 (kq >> 1) + (kq & 1) = kq
     }
-    const float inv = s_inv[wave][kq];
     const uint32_t g = grp * kFramesPerBlock3 + wave * kFramesPerWave + kq;
     if (g < total) {
       float* o = a.out + static_cast<int64_t>(g) * kMaxMels;
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct) {
-        const float acc1 = y[ct] * inv;
+        const float acc1 = y[ct];
         const float c = acc1 < a.log_floor ? a.log_floor : acc1;  // keeps NaN
         o[16 * ct + j] = log10f(c) * a.out_scale + a.out_add;
       }

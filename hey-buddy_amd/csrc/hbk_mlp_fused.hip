@@ -1779,6 +1779,182 @@ __global__ void __launch_bounds__(512) kv_gemm_kernel(KvArgs a) {
 }
 
 
+// kv_net: the rest of the network for the evaluation passes, from the HG0 slab
+// to the prediction counts. k2_rows_kernel<false> does this one 16-row tile per
+// workgroup, reading its weight fragments from the global cache per tile; here
+// a 512-thread workgroup takes 128 rows (a 16-row tile per wave, every column
+// tile of a stage in that wave), stages each matrix's f16 hi / lo planes into
+// LDS once for the 8 waves (the next stage's planes prefetched into registers
+// during the current one), and keeps every activation in its wave's own LDS
+// tile: a wave never waits for another except at the weight swaps. LayerNorm
+// reductions run in the MFMA output layout (rows 4 kq + e of lane (n, kq): sum
+// over the lane's column tiles, then over the 16 lanes n by DPP).
+constexpr int kNetRows = 128, kNetWLd = 104;  // halves per weight row (K <= 96, bank spread)
+struct KvNetArgs {
+  const float* P;
+  const float* hg;  // [rows][128] pre-bias HG0
+  int64_t rows;
+  int64_t b_hg[kMaxG], b_o[kMaxG], w_o[kMaxG], ln_g[kMaxG], ln_b[kMaxG];
+  const _Float16* wc;  // weight cache: hi / lo planes of 16 W
+  int64_t c_o[kMaxG], c_hg[kMaxG];
+  float act_thr;
+  float* counts;
+  int label;
+  float* prob;
+};
+template <int NG>
+__global__ void __launch_bounds__(512) kv_net_kernel(KvNetArgs a) {
+  __shared__ __attribute__((aligned(16))) _Float16 wS[2][kH2][kNetWLd];
+  __shared__ __attribute__((aligned(16))) float actS[8][kR][kLd];
+  __shared__ float cntS[2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = lane & 15, kq = lane >> 4;
+  const int64_t r0 = int64_t(blockIdx.x) * kNetRows + kR * wave;
+  float* A = &actS[wave][0][0];
+  const float* P = a.P;
+  if (tid < 2) cntS[tid] = 0.f;
+  // stage plan: W_o_0, W_hg_1, W_o_1, ..., W_hg_{NG-1}: (cache offset, N, K)
+  constexpr int kStages = 2 * (NG - 1);
+  auto st_off = [&](int st) { return (st & 1) ? a.c_hg[st / 2 + 1] : a.c_o[st / 2]; };
+  auto st_n = [](int st) { return (st & 1) ? kH2 : kL; };
+  auto st_k = [](int st) { return (st & 1) ? kL : kH; };
+  uint4 wr[6];
+  auto load_w = [&](int st) {
+    const int N = st_n(st), K = st_k(st), pieces = N * K / 8;  // per plane
+    const _Float16* src = a.wc + st_off(st);
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int q = min(tid + 512 * j, 2 * pieces - 1), pl = q / pieces, e = q - pl * pieces;
+      wr[j] = *reinterpret_cast<const uint4*>(src + int64_t(pl) * N * K + 8 * e);
+    }
+  };
+  auto store_w = [&](int st) {
+    const int N = st_n(st), K = st_k(st), pieces = N * K / 8;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int q = tid + 512 * j;
+      if (q < 2 * pieces) {
+        const int pl = q / pieces, e = q - pl * pieces, n = (8 * e) / K, k = 8 * e - n * K;
+        *reinterpret_cast<uint4*>(&wS[pl][n][k]) = wr[j];
+      }
+    }
+  };
+  load_w(0);
+  // U0 = silu(HG0 + b) o (G0 + b): lane -> row lane / 4, columns 16 (lane & 3) ..
+  {
+    const int r = lane >> 2, c0 = 16 * (lane & 3);
+    const float* hr = a.hg + min(r0 + r, a.rows - 1) * kH2;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f4 h = *reinterpret_cast<const f4*>(hr + c0 + 4 * q);
+      const f4 g = *reinterpret_cast<const f4*>(hr + kH + c0 + 4 * q);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = c0 + 4 * q + e;
+        const float hh = h[e] + P[a.b_hg[0] + c], gg = g[e] + P[a.b_hg[0] + kH + c];
+        A[r * kLd + c] = hh * sigm(hh) * gg;
+      }
+    }
+  }
+  store_w(0);
+  __syncthreads();
+#pragma unroll
+  for (int st = 0; st < kStages; ++st) {
+    if (st + 1 < kStages) load_w(st + 1);
+    if ((st & 1) == 0) {
+      // S = U W_o^T + b_o (K 64, N 96: 6 column tiles), then LayerNorm k -> X (A, K 96)
+      const int k = st / 2;
+      const AFrag<kH> af = load_a<kH>(A, lane);
+      f4 c[6];
+#pragma unroll
+      for (int ct = 0; ct < 6; ++ct) {
+        c[ct] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < kH / 32; ++i) {
+          const h8 bh = *reinterpret_cast<const h8*>(&wS[0][16 * ct + m][32 * i + 8 * kq]);
+          const h8 bl = *reinterpret_cast<const h8*>(&wS[1][16 * ct + m][32 * i + 8 * kq]);
+          c[ct] = mma3(af.h[i], af.l[i], bh, bl, c[ct]);
+        }
+      }
+      float sm[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ct = 0; ct < 6; ++ct) {
+        const float bo = P[a.b_o[k] + 16 * ct + m];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          c[ct][e] = c[ct][e] * af.inv + bo;
+          sm[e] += c[ct][e];
+        }
+      }
+      float mu[4], sq[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) mu[e] = rsum16(sm[e]) * (1.f / kL);
+#pragma unroll
+      for (int ct = 0; ct < 6; ++ct)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sq[e] += (c[ct][e] - mu[e]) * (c[ct][e] - mu[e]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sq[e] = 1.f / sqrtf(rsum16(sq[e]) * (1.f / kL) + kLnEps);
+#pragma unroll
+      for (int ct = 0; ct < 6; ++ct) {
+        const int col = 16 * ct + m;
+        const float gm = P[a.ln_g[k] + col], bt = P[a.ln_b[k] + col];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) A[(4 * kq + e) * kLd + col] = (c[ct][e] - mu[e]) * sq[e] * gm + bt;
+      }
+    } else {
+      // HG = X W_hg^T + b (K 96, N 128), gate in the epilogue -> U (A, K 64)
+      const int k = st / 2 + 1;
+      const AFrag<kL> af = load_a<kL>(A, lane);
+      f4 c[8];
+#pragma unroll
+      for (int ct = 0; ct < 8; ++ct) {
+        c[ct] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < kL / 32; ++i) {
+          const h8 bh = *reinterpret_cast<const h8*>(&wS[0][16 * ct + m][32 * i + 8 * kq]);
+          const h8 bl = *reinterpret_cast<const h8*>(&wS[1][16 * ct + m][32 * i + 8 * kq]);
+          c[ct] = mma3(af.h[i], af.l[i], bh, bl, c[ct]);
+        }
+      }
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        const int col = 16 * ct + m;
+        const float bh = P[a.b_hg[k] + col], bg = P[a.b_hg[k] + kH + col];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float h = c[ct][e] * af.inv + bh, g = c[ct + 4][e] * af.inv + bg;
+          A[(4 * kq + e) * kLd + col] = h * sigm(h) * g;
+        }
+      }
+    }
+    if (st + 1 < kStages) {
+      __syncthreads();  // every wave is done with this stage's planes
+      store_w(st + 1);
+      __syncthreads();
+    }
+  }
+  // z = U w_out + b_out: lane -> row lane / 4, 16 columns
+  {
+    const int r = lane >> 2, c0 = 16 * (lane & 3);
+    float z = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) z = fmaf(A[r * kLd + c0 + q], P[a.w_o[NG - 1] + c0 + q], z);
+    z += dpp_f<0xB1>(z);  // quad_perm: lanes ^ 1, ^ 2 hold the row's other columns
+    z += dpp_f<0x4E>(z);
+    z += P[a.b_o[NG - 1]];
+    const bool live = r0 + r < a.rows && (lane & 3) == 0;
+    const float p = sigm(z);
+    if (live && a.prob) a.prob[r0 + r] = p;
+    const uint64_t ge = __ballot(live && p >= a.act_thr), gt = __ballot(live && p > a.act_thr);
+    if (lane == 0) {
+      if (ge) atomicAdd(&cntS[0], static_cast<float>(__popcll(ge)));
+      if (gt) atomicAdd(&cntS[1], static_cast<float>(__popcll(gt)));
+    }
+  }
+  __syncthreads();
+  if (tid < 2 && cntS[tid] != 0.f) atomicAdd(a.counts + 2 * a.label + tid, cntS[tid]);
+}
+
 // After the passes (trainer.py:509-536, :549-566): the validation false
 // positives per hour (count / hours in float32, as torch divides an integer
 // count tensor by a Python float), recall, the testing rates, and the dynamic
@@ -2205,24 +2381,56 @@ int mlp_eval_count(const hbk_mlp_plan& p, const float* params, const void* pool,
     else
       hipLaunchKernelGGL(kv_gemm_kernel<false>, grid, dim3(512), 0, s, ka);
     HBK_LAUNCH_CHECK("kv_gemm_kernel");
-    K2Args k2{};
-    k2.P = params;
-    k2.B = static_cast<int>(n);
-    k2.KS = 1;
-    fill_k2(p, k2);
-    k2.hg_part = ws + w.hg;
-    k2.act_thr = act_thr;
-    k2.prob = prob ? prob + c0 : nullptr;
-    k2.Bp = (n + kR - 1) / kR * kR;
-    k2.n_rt = static_cast<int>((n + kR - 1) / kR);
-    set_k2_cache(wsp, NG, reinterpret_cast<const _Float16*>(ws + w.wsplit), k2);
-    k2.counts = counts;
-    k2.count_label = label;
-    auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(unsigned(k2.n_rt)), dim3(256), 0, s, k2); };
-    if (NG == 2) launch(k2_rows_kernel<false, 2>);
-    else if (NG == 3) launch(k2_rows_kernel<false, 3>);
-    else launch(k2_rows_kernel<false, 4>);
-    HBK_LAUNCH_CHECK("k2_rows_kernel");
+    static const bool use_k2 = getenv("HBK_EVAL_K2") != nullptr;  // A/B: the per-tile inference chain
+    if (use_k2) {
+      K2Args k2{};
+      k2.P = params;
+      k2.B = static_cast<int>(n);
+      k2.KS = 1;
+      fill_k2(p, k2);
+      k2.hg_part = ws + w.hg;
+      k2.act_thr = act_thr;
+      k2.prob = prob ? prob + c0 : nullptr;
+      k2.Bp = (n + kR - 1) / kR * kR;
+      k2.n_rt = static_cast<int>((n + kR - 1) / kR);
+      set_k2_cache(wsp, NG, reinterpret_cast<const _Float16*>(ws + w.wsplit), k2);
+      k2.counts = counts;
+      k2.count_label = label;
+      auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(unsigned(k2.n_rt)), dim3(256), 0, s, k2); };
+      if (NG == 2) launch(k2_rows_kernel<false, 2>);
+      else if (NG == 3) launch(k2_rows_kernel<false, 3>);
+      else launch(k2_rows_kernel<false, 4>);
+      HBK_LAUNCH_CHECK("k2_rows_kernel");
+      continue;
+    }
+    K2Args kc{};  // the cache offsets as k2 reads them
+    set_k2_cache(wsp, NG, reinterpret_cast<const _Float16*>(ws + w.wsplit), kc);
+    KvNetArgs kn;
+    kn.P = params;
+    kn.hg = ws + w.hg;
+    kn.rows = n;
+    for (int i = 0; i < kMaxG; ++i) {
+      const int g = std::min(i, NG - 1);
+      kn.b_hg[i] = p.g[g].b_hg;
+      kn.b_o[i] = p.g[g].b_o;
+      kn.w_o[i] = p.g[g].w_o;
+      kn.ln_g[i] = i + 1 < NG ? p.ln[i].g : 0;
+      kn.ln_b[i] = i + 1 < NG ? p.ln[i].b : 0;
+      kn.c_o[i] = kc.c_o[i];
+      kn.c_hg[i] = kc.c_hg[i];
+    }
+    kn.wc = kc.wc;
+    kn.act_thr = act_thr;
+    kn.counts = counts;
+    kn.label = label;
+    kn.prob = prob ? prob + c0 : nullptr;
+    auto launch_net = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(unsigned((n + kNetRows - 1) / kNetRows)), dim3(512), 0, s, kn);
+    };
+    if (NG == 2) launch_net(kv_net_kernel<2>);
+    else if (NG == 3) launch_net(kv_net_kernel<3>);
+    else launch_net(kv_net_kernel<4>);
+    HBK_LAUNCH_CHECK("kv_net_kernel");
   }
   return HBK_OK;
 }
