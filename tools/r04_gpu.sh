@@ -41,6 +41,10 @@ for S in ${STEPS:-tests bench cus}; do
       echo "=== DP step latency"
       timeout -k 10 900 bash tools/dp_probe.sh > $OUT/${TAG}_dp_probe.log 2>&1 || { tail -20 $OUT/${TAG}_dp_probe.log; exit 1; }
       cat $OUT/${TAG}_dp_probe.log ;;
+    eval)
+      echo "=== evaluation passes"
+      timeout -k 10 500 bash tools/eval_probe.sh > $OUT/${TAG}_eval_probe.log 2>&1 || { tail -20 $OUT/${TAG}_eval_probe.log; exit 1; }
+      cat $OUT/${TAG}_eval_probe.log ;;
     cus)
       echo "=== train step per CU count"
       timeout -k 10 500 bash tools/mlp_cus.sh > $OUT/${TAG}_mlp_cus.log 2>&1 || { tail -20 $OUT/${TAG}_mlp_cus.log; exit 1; }
