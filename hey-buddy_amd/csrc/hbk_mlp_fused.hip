@@ -1560,7 +1560,7 @@ __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
 // the rows stream from HBM straight into MFMA A fragments, prefetched two
 // chunks ahead. The pre-bias HG0 rows go to a slab that k2_rows_kernel
 // <false> (the inference chain, with its counters) reads as its one K-split.
-constexpr int kKvRows = 256, kKvKC = 64, kKvLd = kKvKC + 8, kKvChunks = kD / kKvKC;
+constexpr int kKvKC = 64, kKvChunks = kD / kKvKC;
 struct KvArgs {
   const void* pool;      // f32 or f16 rows of 1536
   int64_t n_pool;
@@ -1607,20 +1607,53 @@ __global__ void __launch_bounds__(256) kv_prep_kernel(const float* __restrict__ 
   }
 }
 
-// kF16: the rows are f16 (exact in hi); else f32 (split hi / lo)
+// The streamed rows are read once: non-temporal loads (HBK_KV_NT, default on)
+// keep them from evicting W', which every tile re-reads, from the XCD's L2.
+#ifndef HBK_KV_NT
+#define HBK_KV_NT 1
+#endif
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 load_rows4(const uint4* p) {
+#if HBK_KV_NT
+  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  return uint4{v[0], v[1], v[2], v[3]};
+#else
+  return *p;
+#endif
+}
+
+// kF16: the rows are f16 (exact in hi); else f32 (split hi / lo).
+// W' chunks reach LDS by global->LDS DMA (global_load_lds_dwordx4: no register
+// staging, so no spills at 8 waves x ~240 VGPRs), issued two chunks ahead. The
+// DMA writes a wave's 64 x 16 B contiguously, so the image is unpadded
+// [plane][n][64 halves] rows with the 16-B pieces XOR-swizzled by (n >> 1) & 7
+// on the SOURCE address (the B-fragment reads of 16 lanes then hit 16
+// distinct 4-bank groups). The chunk's barrier waits with a counted vmcnt
+// (the DMA retired, the next rows' loads still in flight) and a raw s_barrier:
+// __syncthreads() would emit vmcnt(0) and drain the row prefetch.
+constexpr int kKvPiece = 8;  // 16-B pieces per 64-deep row of a chunk
+__device__ __forceinline__ int kv_swz(int n) { return (n >> 1) & 7; }
 template <bool kF16>
 __global__ void __launch_bounds__(512) kv_gemm_kernel(KvArgs a) {
-  __shared__ __attribute__((aligned(16))) _Float16 wb[2][2][kH2][kKvLd];  // [buf][hi / lo][n][k]
-  __shared__ float stS[8][32][2];
-  constexpr int kDepth = 2;  // A chunks in flight (this one + kDepth - 1 ahead)
-  constexpr int kU = kF16 ? 1 : 2;      // 16-B loads per 8 elements
+  // ONE __shared__ object: beside a second one hipcc drains the DMA (vmcnt(0))
+  // before every chunk's first LDS read. The row statistics reuse buffer 0.
+  constexpr int kWBuf = 3;  // W' ring: chunk c + 2's DMA is issued during chunk c (kWBuf - 1 == 2 assumed below)
+  __shared__ __attribute__((aligned(16))) _Float16 wb[kWBuf][2][kH2][kKvKC];  // [buf][hi / lo][n][k] (swizzled pieces)
+  float (*stS)[32][2] = reinterpret_cast<float (*)[32][2]>(&wb[0][0][0][0]);
+  static_assert(sizeof(float) * 8 * 32 * 2 <= sizeof(_Float16) * 2 * kH2 * kKvKC, "statistics fit in buffer 0");
+  constexpr int kDepth = 2;         // A chunks in flight (this one + 1 ahead)
+  constexpr int kU = kF16 ? 1 : 2;  // 16-B loads per 8 elements
+  constexpr int kRT = kF16 ? 2 : 1; // 16-row tiles per wave (f32 rows: one, for the registers of the split)
+  constexpr int kALoads = kRT * 2 * kU;  // per chunk
+  constexpr int kTile = 8 * 16 * kRT;
+  static_assert(kALoads + 4 < 16, "the counted waits use vmcnt's low field");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = lane & 15, kq = lane >> 4;
-  const int64_t tile0 = int64_t(blockIdx.x) * kKvRows;
-  const char* rp[2];
-  uint32_t rid[2];
+  const int64_t tile0 = int64_t(blockIdx.x) * kTile;
+  const char* rp[kRT];
+  uint32_t rid[kRT];
 #pragma unroll
-  for (int rt = 0; rt < 2; ++rt) {
-    const int64_t r = min(tile0 + 32 * wave + 16 * rt + m, a.rows - 1);
+  for (int rt = 0; rt < kRT; ++rt) {
+    const int64_t r = min(tile0 + 16 * kRT * wave + 16 * rt + m, a.rows - 1);
     int64_t pr = a.idx ? static_cast<int64_t>(a.idx[r]) : (a.r0 + r) % a.n_pool;
     pr = min(max(pr, int64_t(0)), a.n_pool - 1);
     rp[rt] = static_cast<const char*>(a.pool) + pr * kD * (kF16 ? 2 : 4);
@@ -1630,61 +1663,64 @@ __global__ void __launch_bounds__(512) kv_gemm_kernel(KvArgs a) {
   const uint32_t s0 = static_cast<uint32_t>(seed), s1 = static_cast<uint32_t>(seed >> 32) * 0x27D4EB2Fu;
   const uint32_t thr = static_cast<uint32_t>(a.drop_p * 65536.f + 0.5f);
   const float keep = a.drop_p > 0.f ? 1.f / (1.f - a.drop_p) : 1.f;
-  // A ring: [slot][rt][kb][u]
-  uint4 ar[kDepth][2][2][kU];
+  uint4 ar[kDepth][kRT][2][kU];
   auto load_a = [&](int c, int slot) {
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
+    for (int rt = 0; rt < kRT; ++rt)
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
         const int k = kKvKC * c + 32 * kb + 8 * kq;
 #pragma unroll
         for (int u = 0; u < kU; ++u)
-          ar[slot][rt][kb][u] = *reinterpret_cast<const uint4*>(rp[rt] + int64_t(k) * (kF16 ? 2 : 4) + 16 * u);
+          ar[slot][rt][kb][u] = load_rows4(reinterpret_cast<const uint4*>(rp[rt] + int64_t(k) * (kF16 ? 2 : 4) + 16 * u));
       }
   };
-  // W' chunk c: 2 planes x 128 n x 64 k = 4,096 16-B pieces, 8 per thread... (512 threads: 4)
-  uint4 wr[4];
-  auto load_w = [&](int c) {
+  // W' chunk c -> buffer buf: 2 planes x 128 rows x 8 pieces = 2,048 pieces, 4 DMA
+  // instructions per wave (8 rows each); lane l of instruction j writes piece
+  // (row 8 (4 wave + j) + l / 8, slot l % 8), reading the source piece slot ^ swz(row)
+  auto dma_w = [&](int c, int buf) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int q = tid + 512 * j, pl = q >> 10, n = (q >> 3) & 127, kk = (q & 7) * 8;
-      wr[j] = *reinterpret_cast<const uint4*>(a.wq + int64_t(pl) * kH2 * kD + int64_t(n) * kD + kKvKC * c + kk);
+      const int row8 = 4 * wave + j;                 // 0 .. 31: plane row8 / 16, rows 8 (row8 % 16) ..
+      const int pl = row8 >> 4, n = 8 * (row8 & 15) + (lane >> 3), pc = (lane & 7) ^ kv_swz(n);
+      const _Float16* src = a.wq + int64_t(pl) * kH2 * kD + int64_t(n) * kD + kKvKC * c + kKvPiece * pc;
+      __builtin_amdgcn_global_load_lds(src, &wb[buf][pl][8 * (row8 & 15)][0], 16, 0, 0);
     }
   };
-  auto store_w = [&](int buf) {
+  // prologue: chunks 0 and 1 (W' buffers 0, 1; A slots 0, 1); chunk 0 waited for here,
+  // chunk 1 at the end of chunk 0
+  dma_w(0, 0);
+  load_a(0, 0);
+  dma_w(1, 1);
+  load_a(1, 1);
+  __builtin_amdgcn_s_waitcnt((kALoads + 4) | (0x7 << 4) | (0xF << 8));  // vmcnt(4 + kALoads): chunk 0 in
+  __builtin_amdgcn_s_barrier();
+  f4 acc[kRT][8];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int q = tid + 512 * j, pl = q >> 10, n = (q >> 3) & 127, kk = (q & 7) * 8;
-      *reinterpret_cast<uint4*>(&wb[buf][pl][n][kk]) = wr[j];
-    }
-  };
-#pragma unroll
-  for (int d = 0; d < kDepth; ++d) load_a(d, d);
-  load_w(0);
-  store_w(0);
-  __syncthreads();
-  f4 acc[2][8];
-#pragma unroll
-  for (int rt = 0; rt < 2; ++rt)
+  for (int rt = 0; rt < kRT; ++rt)
 #pragma unroll
     for (int ct = 0; ct < 8; ++ct) acc[rt][ct] = f4{0.f, 0.f, 0.f, 0.f};
-  double sd1[2] = {0.0, 0.0}, sd2[2] = {0.0, 0.0};
+  double sd1[kRT], sd2[kRT];
+#pragma unroll
+  for (int rt = 0; rt < kRT; ++rt) sd1[rt] = sd2[rt] = 0.0;
   static_assert(kKvChunks % kDepth == 0, "the A ring's slots must be compile-time");
+  int buf = 0;  // W' buffer of chunk c (c % kWBuf; a run-time LDS offset, the A slot is unrolled)
 #pragma unroll 1
   for (int cb = 0; cb < kKvChunks; cb += kDepth)
 #pragma unroll
   for (int slot = 0; slot < kDepth; ++slot) {
     const int c = cb + slot;
-    if (c + 1 < kKvChunks) load_w(c + 1);
-    // this chunk's A values (dropout mask, row sums, split), one 32-deep block at a time
-    const int buf = c & 1;
-    float t1[2] = {0.f, 0.f}, t2[2] = {0.f, 0.f};
+    const int bnext = buf == 0 ? kWBuf - 1 : buf - 1;  // (c + 2) % kWBuf
+    // this chunk's A values (dropout mask, row sums, split) first: their loads are
+    // ordinary global loads, so no DMA may be outstanding when they are used
+    h8 ah[kRT][2], al[kRT][2];
+    float t1[kRT], t2[kRT];
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      h8 ah[2], al[2];
+    for (int rt = 0; rt < kRT; ++rt) t1[rt] = t2[rt] = 0.f;
 #pragma unroll
-      for (int rt = 0; rt < 2; ++rt) {
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int rt = 0; rt < kRT; ++rt) {
         float v[8];
         if (kF16) {
           const h8 hv = __builtin_bit_cast(h8, ar[slot][rt][kb][0]);
@@ -1710,38 +1746,51 @@ __global__ void __launch_bounds__(512) kv_gemm_kernel(KvArgs a) {
         }
         if (kF16) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) ah[rt][e] = static_cast<_Float16>(v[e]);  // exact
+          for (int e = 0; e < 8; ++e) ah[rt][kb][e] = static_cast<_Float16>(v[e]);  // exact
         } else {
-          split8(f4{v[0], v[1], v[2], v[3]}, f4{v[4], v[5], v[6], v[7]}, ah[rt], al[rt]);
+          split8(f4{v[0], v[1], v[2], v[3]}, f4{v[4], v[5], v[6], v[7]}, ah[rt][kb], al[rt][kb]);
         }
       }
 #pragma unroll
-      for (int ct = 0; ct < 8; ++ct) {
-        const h8 bh = *reinterpret_cast<const h8*>(&wb[buf][0][16 * ct + m][32 * kb + 8 * kq]);
-        const h8 bl = *reinterpret_cast<const h8*>(&wb[buf][1][16 * ct + m][32 * kb + 8 * kq]);
-#pragma unroll
-        for (int rt = 0; rt < 2; ++rt) {
-          acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt], bh, acc[rt][ct], 0, 0, 0);
-          acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt], bl, acc[rt][ct], 0, 0, 0);
-          if (!kF16) acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[rt], bh, acc[rt][ct], 0, 0, 0);
-        }
-        if ((ct & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bound the B fragments in flight (registers)
-      }
-    }
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
+    for (int rt = 0; rt < kRT; ++rt) {
       sd1[rt] += double(t1[rt]);
       sd2[rt] += double(t2[rt]);
     }
-    if (c + kDepth < kKvChunks) load_a(c + kDepth, slot);
-    if (c + 1 < kKvChunks) {
-      store_w(buf ^ 1);  // its readers (chunk c - 1) passed the barrier below one iteration ago
-      __syncthreads();
-    }
-  }
-  // row statistics: the 4 lanes m + 16 kq hold a row's parts
+    // unconditional (past the end: a clamped re-read) so that the loop has no
+    // branches and hipcc's counted waits stay exact across the back edge
+    dma_w(min(c + 2, kKvChunks - 1), bnext);  // its readers (chunk c - 1) passed the last barrier
+    load_a(min(c + kDepth, kKvChunks - 1), slot);
 #pragma unroll
-  for (int rt = 0; rt < 2; ++rt) {
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int ct = 0; ct < 8; ++ct) {
+        const int n = 16 * ct + m, pc = (4 * kb + kq) ^ kv_swz(n);
+        const h8 bh = *reinterpret_cast<const h8*>(&wb[buf][0][n][kKvPiece * pc]);
+        const h8 bl = *reinterpret_cast<const h8*>(&wb[buf][1][n][kKvPiece * pc]);
+#pragma unroll
+        for (int rt = 0; rt < kRT; ++rt) {
+          acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt][kb], bh, acc[rt][ct], 0, 0, 0);
+          acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt][kb], bl, acc[rt][ct], 0, 0, 0);
+          if (!kF16) acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[rt][kb], bh, acc[rt][ct], 0, 0, 0);
+        }
+        if ((ct & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bound the B fragments in flight (registers)
+      }
+    // chunk c + 1's DMA and rows retired (chunk c + 2's, issued above, may still fly), then the barrier.
+    // The sched_barriers keep the next chunk's conversions below the counted wait: hoisted
+    // above it, hipcc guards them with vmcnt(0) (DMA and row loads pending together)
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt((kALoads + 4) | (0x7 << 4) | (0xF << 8));  // vmcnt(4 + kALoads)
+    __builtin_amdgcn_s_waitcnt((0x3F & 0xF) | ((0x3F >> 4) << 14) | (0x7 << 4) | (0x0 << 8));  // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    buf = buf == kWBuf - 1 ? 0 : buf + 1;
+  }
+  __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xF << 8));  // vmcnt(0): the clamped re-reads (into buffers 0, 1) in
+  __builtin_amdgcn_s_barrier();
+  // row statistics: the 4 lanes m + 16 kq hold a row's parts
+  // (buffer 0's last readers, chunk kKvChunks - 2, passed that chunk's barrier)
+#pragma unroll
+  for (int rt = 0; rt < kRT; ++rt) {
 #pragma unroll
     for (int o = 16; o < 64; o <<= 1) {
       sd1[rt] += __shfl_xor(sd1[rt], o, 64);
@@ -1764,11 +1813,11 @@ __global__ void __launch_bounds__(512) kv_gemm_kernel(KvArgs a) {
     cc1[ct] = a.c1[16 * ct + m];
   }
 #pragma unroll
-  for (int rt = 0; rt < 2; ++rt)
+  for (int rt = 0; rt < kRT; ++rt)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int lr = 16 * rt + 4 * kq + e;
-      const int64_t r = tile0 + 32 * wave + lr;
+      const int64_t r = tile0 + 16 * kRT * wave + lr;
       const float mu = stS[wave][lr][0], rs = stS[wave][lr][1];
       if (r < a.rows) {
         float* out = a.hg + r * kH2 + m;
@@ -1845,8 +1894,8 @@ __global__ void __launch_bounds__(512) kv_net_kernel(KvNetArgs a) {
     const float* hr = a.hg + min(r0 + r, a.rows - 1) * kH2;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const f4 h = *reinterpret_cast<const f4*>(hr + c0 + 4 * q);
-      const f4 g = *reinterpret_cast<const f4*>(hr + kH + c0 + 4 * q);
+      const f4 h = __builtin_bit_cast(f4, load_rows4(reinterpret_cast<const uint4*>(hr + c0 + 4 * q)));
+      const f4 g = __builtin_bit_cast(f4, load_rows4(reinterpret_cast<const uint4*>(hr + kH + c0 + 4 * q)));
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int c = c0 + 4 * q + e;
@@ -2375,7 +2424,8 @@ int mlp_eval_count(const hbk_mlp_plan& p, const float* params, const void* pool,
     ka.drop_p = drop_p;
     ka.seed = seed;
     ka.hg = ws + w.hg;
-    const dim3 grid(unsigned((n + kKvRows - 1) / kKvRows));
+    const int tile = f16 ? 256 : 128;  // kv_gemm_kernel's rows per workgroup
+    const dim3 grid(unsigned((n + tile - 1) / tile));
     if (f16)
       hipLaunchKernelGGL(kv_gemm_kernel<true>, grid, dim3(512), 0, s, ka);
     else
