@@ -901,7 +901,8 @@ def setup_e2e(args, dev, rank, world, seed):
         if staged_ev:
             ev_ms = sum(a.elapsed_time(b) for evl in staged_ev for a, b in evl) / len(staged_ev)
             rows = ev.rows_per_pass * len(val_after)
-            out.append(roof("kv_gemm_kernel + k2_rows_kernel<false> (+ kv_prep / kv_finish): the validation and "
+            out.append(roof("kv_gemm_kernel (input GEMM + the rest of the network, one launch per pool; + kv_prep / "
+                            "kv_finish): the validation and "
                             "testing passes, %d per chunk of %d rows each (dropout on)" % (len(val_after),
                                                                                            ev.rows_per_pass),
                             "mfma", 2.0 * 251_968 * rows, ev_ms, "TFLOP/s",

@@ -1,5 +1,5 @@
 """The evaluation passes of train_epoch on the GPU (hbk_mlp_eval_*,
-kv_gemm_kernel + k2_rows_kernel<false> + kv_finish_kernel): the validation /
+kv_gemm_kernel (input GEMM + network) + kv_finish_kernel): the validation /
 testing forwards of trainer.py:496-566 reduced to prediction counts, and the
 post-validation bookkeeping (false positives per hour, recall, testing rates,
 dynamic negative weight, trainer.py:509-536).

@@ -108,8 +108,16 @@ if __name__ == "__main__":
         os.environ.update(HBK_DP_REDUCE_ALWAYS="1", MASTER_ADDR="127.0.0.1", MASTER_PORT="29533",
                           HSA_ENABLE_IPC_MODE_LEGACY="0")
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    cus = next((int(a[6:]) for a in sys.argv[1:] if a.startswith("--cus=")), 0)
     if TRACE:
-        trace()
+        if cus:
+            from heybuddy.pipeline import masked_stream, train_cu_set
+            ms = masked_stream(torch.device("cuda", 0),
+                               train_cu_set(torch.cuda.get_device_properties(0).multi_processor_count, cus))
+            with torch.cuda.stream(ms.stream):
+                trace()
+            print(f"  (above: stream masked to {cus} CUs)")
+        else:
+            trace()
     else:
-        cus = next((int(a[6:]) for a in sys.argv[1:] if a.startswith("--cus=")), 0)
         timing(int(next((a for a in sys.argv[1:] if a.isdigit()), 200)), cus)
