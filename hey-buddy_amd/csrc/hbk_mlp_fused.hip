@@ -105,6 +105,26 @@ __device__ __forceinline__ float wmax(float v) {
 }
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
 
+// Barrier of a loop with global->LDS DMA in flight (its waits counted by hand
+// before it): a fenced barrier would wait vmcnt(0), as the DMA writes LDS. The
+// empty asm statements keep the compiler from moving memory accesses across.
+__device__ __forceinline__ void dma_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+// Workgroup barrier for LDS traffic only: the release / acquire fences are
+// restricted to the local address space, so the barrier waits for the wave's
+// LDS operations (lgkmcnt) but not for its global loads in flight (a plain
+// __syncthreads() waits vmcnt(0) too: every register prefetch of the next
+// stage's operands would land before the barrier). None of these kernels
+// hands data between its own waves through global memory.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 #ifdef HBK_TRACE
 // Tracing build only (lib/libhbk_trace.so, tools/probe_mlp.py): lane 0 of every
 // wave of block 0 records (mark << 56 | s_memtime) at stage marks of k1 / k2 / k3.
@@ -269,7 +289,7 @@ __device__ __forceinline__ void k1a_tile(const K1aArgs& a, int rt, int step, flo
   }
 #pragma unroll
   for (int t = 0; t < 3; ++t) {
-    __syncthreads();  // the slab's previous readers are done
+    lds_barrier();  // the slab's previous readers are done
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       float* row = slab + (wave * 4 + i) * kSlabLd;
@@ -280,7 +300,7 @@ __device__ __forceinline__ void k1a_tile(const K1aArgs& a, int rt, int step, flo
         row[col] = xh[i][j];
       }
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int col = tid + 256 * h;
@@ -409,7 +429,7 @@ __global__ void __launch_bounds__(256) k1b_kernel(K1bArgs a) {
   for (int c = 0; c < 2; ++c)
 #pragma unroll
     for (int i = 0; i < kN32; ++i) split8(wr[c][i][0] * 16.f, wr[c][i][1] * 16.f, whi[c][i], wlo[c][i]);
-  __syncthreads();
+  lds_barrier();
   HBK_MT(3, 2);
   // wave w -> output columns [32 w, 32 w + 32) of all 64 rows: 4 row tiles x 2
   // column tiles, A = LN output = xhat g + b from LDS (k = 32 i + 8 kq ..)
@@ -685,7 +705,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
       for (int t = 0; t < kPreTiles; ++t) {
         const int rt = (blockIdx.x - a.n_rt) * kPreTiles + t;
         if (rt >= a.n_rt) break;
-        if (t) __syncthreads();  // the slab's previous readers are done
+        if (t) lds_barrier();  // the slab's previous readers are done
         k1a_tile<true>(a.pre, rt, step, a.pre.xhat[a.pre.parity ^ 1], hgRaw);
       }
     }
@@ -768,7 +788,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
       bU[r][j4 + q] = hh * sigm(hh) * gg;
     }
   }
-  __syncthreads();
+  lds_barrier();
   K2_MARK(2);
   // transposed activation stores: 4 consecutive rows of one column per float4
   auto st4 = [&](float* base, int width, int col, int row4, f4 v) {
@@ -806,7 +826,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
         for (int e = 0; e < 4; ++e) bS[4 * kq + e][n1] = c1[e] + bo1_;
       }
     }
-    __syncthreads();
+    lds_barrier();
     K2_MARK(10 + k);
     // LayerNorm k over 96 columns: 16 lanes per row (wave w -> rows 4w..4w+3,
     // lane -> row 4w + lane / 16, columns 6 (lane % 16) ..), both reductions of
@@ -831,7 +851,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
       }
       if ((lane & 15) == 0) rsS[k][r] = rs;
     }
-    __syncthreads();
+    lds_barrier();
     K2_MARK(20 + k);
     // HG_{k+1} = Xn W_hg^T + b, gate in the epilogue -> hgS[k+1], U_{k+1} -> bU
     if (kTrain) store_t(a.Xn + (k + 1) * kL * Bs, &bX[0][0], kL);
@@ -853,7 +873,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
       }
       if (kTrain) st4(a.U + (k + 1) * kH * Bs, kH, j, 4 * kq, uo);
     }
-    __syncthreads();
+    lds_barrier();
     K2_MARK(30 + k);
   }
   // backward weight fragments of the first two backward matrix stages (from
@@ -875,7 +895,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
       if (lane == 0) zS[r] = z;
     }
   }
-  __syncthreads();
+  lds_barrier();
   K2_MARK(40);
   // sigmoid, high-loss filter (trainer.py:407-424), weighted BCE (:301-312, torch
   // formulas incl. the log clamp at -100 and the 1e-12 in BCE's backward)
@@ -933,7 +953,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
     }
   }
   if constexpr (!kTrain) return;
-  __syncthreads();
+  lds_barrier();
   K2_MARK(41);
   if (tid < kStats && red[tid] != 0.f) atomicAdd(a.stats + tid, red[tid]);
   // ---------------------------------------------------------- backward ---
@@ -964,7 +984,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
     st4(a.dHG + k * kH2 * Bs, kH2, j, rg, dho);
     st4(a.dHG + k * kH2 * Bs, kH2, kH + j, rg, dgo);
   }
-  __syncthreads();
+  lds_barrier();
   K2_MARK(42);
 #pragma unroll
   for (int k = NG - 1; k >= 1; --k) {
@@ -987,7 +1007,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
         for (int e = 0; e < 4; ++e) bU[4 * kq + e][n1] = c1[e];
       }
     }
-    __syncthreads();
+    lds_barrier();
     K2_MARK(50 + k);
     // LayerNorm k-1 backward: gamma / beta column sums, dS_{k-1} per row -> bS
     {
@@ -1018,7 +1038,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
 #pragma unroll
       for (int e = 0; e < 6; ++e) bS[r][c0 + e] = rs * (t[e] - s1 - x[e] * s2);
     }
-    __syncthreads();
+    lds_barrier();
     K2_MARK(60 + k);
     // GMLP k-1: output bias gradient (column sums of dS), dU = dS W_o (NN: K 96 -> N 64,
     // fragments fy) with the gate backward in the epilogue -> dHG_{k-1} (bX)
@@ -1048,7 +1068,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
       st4(a.dHG + kk * kH2 * Bs, kH2, j, 4 * kq, dho);
       st4(a.dHG + kk * kH2 * Bs, kH2, kH + j, 4 * kq, dgo);
     }
-    __syncthreads();
+    lds_barrier();
     K2_MARK(70 + k);
   }
   // bias gradient of mlp_in's hidden + gate
@@ -1167,8 +1187,7 @@ __global__ void __launch_bounds__(512) k3_wgrad_kernel(K3Args a) {
       }
       HBK_MT(2, 10 + s);
       fetch(s + kK3Depth, slot);
-      __builtin_amdgcn_s_waitcnt((0x3F & 0xF) | ((0x3F >> 4) << 14) | (0x7 << 4) | (0x0 << 8));  // lgkmcnt(0)
-      __builtin_amdgcn_s_barrier();
+      lds_barrier();
       // the previous readers of buffer buf (step s - 2) passed this step's barrier's predecessor
       const float* xa = &xS[buf][16 * mt + m][8 * kq];
       const f4 v0 = *reinterpret_cast<const f4*>(xa), v1 = *reinterpret_cast<const f4*>(xa + 4);
@@ -1221,7 +1240,7 @@ __global__ void __launch_bounds__(512) k3_wgrad_kernel(K3Args a) {
   rsum += __shfl_xor(rsum, 16, 64);
   rsum += __shfl_xor(rsum, 32, 64);
   if (wave < 4 && kq == 0) sS[16 * mt + m] = rsum;
-  __syncthreads();
+  lds_barrier();
   float dg[2] = {0.f, 0.f}, db[2] = {0.f, 0.f};
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -1249,7 +1268,7 @@ __global__ void __launch_bounds__(512) k3_wgrad_kernel(K3Args a) {
       red[1][mt][16 * (nt0 + t) + m] = db[t];
     }
   }
-  __syncthreads();
+  lds_barrier();
   if (tid < kTN) {
     const int col = n0 + tid;
     if (col < jb.N) {  // the tile's 64 rows of j; the other M tile adds its own (2 addends onto zero)
@@ -1415,7 +1434,7 @@ __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
       }
     }
     if (!on) return;  // the gate is the same in every thread: parameters and cache unchanged
-    __syncthreads();
+    lds_barrier();
     for (int u = threadIdx.x; u < C * (kTileR / 8); u += 256) {
       const int c = u / (kTileR / 8), rb = 8 * (u % (kTileR / 8));
       if (rb >= rows) continue;
@@ -1623,7 +1642,7 @@ __global__ void __launch_bounds__(512) kv_gemm_kernel(KvArgs a) {
   dma_w(1, 1);
   load_rows(1, 1);
   __builtin_amdgcn_s_waitcnt((kALoads + 4) | (0x7 << 4) | (0xF << 8));  // vmcnt(4 + kALoads): chunk 0 in
-  __builtin_amdgcn_s_barrier();
+  dma_barrier();
   f4 acc[kRT][8];
 #pragma unroll
   for (int rt = 0; rt < kRT; ++rt)
@@ -1710,12 +1729,12 @@ __global__ void __launch_bounds__(512) kv_gemm_kernel(KvArgs a) {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_waitcnt((kALoads + 4) | (0x7 << 4) | (0xF << 8));  // vmcnt(4 + kALoads)
     __builtin_amdgcn_s_waitcnt((0x3F & 0xF) | ((0x3F >> 4) << 14) | (0x7 << 4) | (0x0 << 8));  // lgkmcnt(0)
-    __builtin_amdgcn_s_barrier();
+    dma_barrier();
     __builtin_amdgcn_sched_barrier(0);
     buf = buf == kWBuf - 1 ? 0 : buf + 1;
   }
   __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xF << 8));  // vmcnt(0): the clamped re-reads (into buffers 0, 1) in
-  __builtin_amdgcn_s_barrier();
+  dma_barrier();
   // row statistics: the 4 lanes m + 16 kq hold a row's parts
   // (buffer 0's last readers, chunk kKvChunks - 2, passed that chunk's barrier)
 #pragma unroll
@@ -1733,7 +1752,7 @@ __global__ void __launch_bounds__(512) kv_gemm_kernel(KvArgs a) {
       stS[wave][16 * rt + m][1] = static_cast<float>(1.0 / sqrt(kp * kp * var + double(kLnEps)));  // its 1 / std
     }
   }
-  __syncthreads();
+  dma_barrier();
   // ---- the rest of the network, per wave on its kRT row tiles ----
   // HG0 = rs (acc / 16 keep - mu c1) + c0 + b; U0 = silu(H) G into the wave's
   // activation tile (the lane holds hidden column j = 16 ct + m and gate column
@@ -1749,7 +1768,7 @@ __global__ void __launch_bounds__(512) kv_gemm_kernel(KvArgs a) {
         mu[rt][e] = stS[wave][16 * rt + 4 * kq + e][0];
         rs[rt][e] = stS[wave][16 * rt + 4 * kq + e][1];
       }
-    __syncthreads();  // every wave has its statistics: the activation tiles may overwrite them
+    lds_barrier();  // every wave has its statistics: the activation tiles may overwrite them
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) {
       const int j = 16 * ct + m;
@@ -1811,7 +1830,7 @@ __global__ void __launch_bounds__(512) kv_gemm_kernel(KvArgs a) {
   };
   load_w(0);
   store_w(0);
-  __syncthreads();
+  lds_barrier();
   const float* P = a.P;
 #pragma unroll
   for (int st = 0; st < kStages; ++st) {
@@ -1900,15 +1919,15 @@ __global__ void __launch_bounds__(512) kv_gemm_kernel(KvArgs a) {
       }
     }
     if (st + 1 < kStages) {
-      __syncthreads();  // every wave is done with this stage's planes
+      lds_barrier();  // every wave is done with this stage's planes
       store_w(st + 1);
-      __syncthreads();
+      lds_barrier();
     }
   }
   // z = U w_out + b_out: lane -> row lane / 4 of a tile, 16 columns; sigmoid, counts
   float* cntS = reinterpret_cast<float*>(smem + kWsBytes + kActBytes);
   if (tid < 2) cntS[tid] = 0.f;
-  __syncthreads();
+  lds_barrier();
   {
     const int r = lane >> 2, c0 = 16 * (lane & 3);
     float wo[16];
@@ -1936,7 +1955,7 @@ __global__ void __launch_bounds__(512) kv_gemm_kernel(KvArgs a) {
       if (gt) atomicAdd(&cntS[1], static_cast<float>(gt));
     }
   }
-  __syncthreads();
+  lds_barrier();
   if (tid < 2 && cntS[tid] != 0.f) atomicAdd(a.counts + 2 * a.label + tid, cntS[tid]);
 }
 
