@@ -59,7 +59,7 @@ def featurize_pool(src, lens, noise_bank, irs, graph, workers: int, batch: int =
     per job: the same cost; a pitch-shifted batch is ~7x the work of another,
     so whole batches would leave most workers idle behind it). The pool is
     started and warmed before the clock starts (a worker's interpreter start
-    is not pipeline work)."""
+    is not pipeline work); jobs are handed out longest first."""
     import multiprocessing as mp
     from oracle.augment import COIN_KINDS, stratified_coins
     m = len(src)
@@ -78,11 +78,18 @@ def featurize_pool(src, lens, noise_bank, irs, graph, workers: int, batch: int =
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
+    # longest first (a pitch-shifted batch is ~7x another's work): the pool's
+    # tail is then the cheap jobs, not one expensive job started last
+    cost = [7.0 if int(j[2]["pitch"][0]) else 1.0 for j in jobs]
+    order = sorted(range(len(jobs)), key=lambda i: -cost[i])
     try:
         pool.map(_warm, range(workers), chunksize=1)
         t0 = time.perf_counter()
-        res = pool.map(_batch, jobs, chunksize=1)
+        res_o = pool.map(_batch, [jobs[i] for i in order], chunksize=1)
         wall = time.perf_counter() - t0
+        res = [None] * len(jobs)
+        for i, r in zip(order, res_o):
+            res[i] = r
     finally:
         pool.close()
         pool.join()
