@@ -61,7 +61,6 @@ VARIANTS = {  # profiling builds (load with HBK_LIB=hey-buddy_amd/lib/<name>)
     "phase": ("libhbk_phase.so", ("-DHBK_PHASE_TIMING",)),  # s_memtime phase counters + ablation
     "ablate": ("libhbk_ablate.so", ("-DHBK_ABLATE",)),      # HBK_DEBUG_SKIP phase ablation only
     "trace": ("libhbk_trace.so", ("-DHBK_TRACE",)),         # per-wave s_memtime timeline
-    "k3d4": ("libhbk_k3d4.so", ("-DHBK_K3_DEPTH=4",)),       # k3 ring depth 4 (A/B)
     "pvc1": ("libhbk_pvc1.so", ("-DHBK_PV_CLIPS=1",)),       # pitch vocoder: 1 clip per workgroup (A/B)
     "pvr256": ("libhbk_pvr256.so", ("-DHBK_PV_RESTART=256",)),  # pitch vocoder: direct DFT every 256 frames
     "pvab1": ("libhbk_pvab1.so", ("-DHBK_PV_ABLATE=1",)),    # pitch vocoder ablation: no bin reduction

@@ -691,7 +691,7 @@ int hbk_mlp_step_fwd_bwd(const hbk_mlp_plan* p, const float* params, const float
   if (ws_bytes < mlp_fused_ws_floats(*p, batch) * int64_t(sizeof(float))) return arg_error("workspace too small");
   if (n32 < 0 || n16 < 0) return arg_error("negative pool size");
   if (!idx && n32 < batch) return arg_error("idx NULL: pool32 must hold the batch rows");
-  if (flags & ~(HBK_STEP_XHAT_READY | HBK_STEP_PREFETCH_NEXT | HBK_STEP_WEIGHTS_READY))
+  if (flags & ~(HBK_STEP_XHAT_READY | HBK_STEP_PREFETCH_NEXT | HBK_STEP_WEIGHTS_READY | HBK_STEP_DEFER_PARTIALS))
     return arg_error("unknown flags");
   if (!pool32 && !pool16) return arg_error("no embedding pool");
   return mlp_fused_run(*p, params, pool32, n32, pool16, n16, idx, idx_step_stride, idx_steps, y, y_step_stride,

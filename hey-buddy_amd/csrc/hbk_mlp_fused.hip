@@ -113,17 +113,18 @@ __device__ __forceinline__ void dma_barrier() {
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }
-// Workgroup barrier for LDS traffic only: the release / acquire fences are
-// restricted to the local address space, so the barrier waits for the wave's
-// LDS operations (lgkmcnt) but not for its global loads in flight (a plain
-// __syncthreads() waits vmcnt(0) too: every register prefetch of the next
-// stage's operands would land before the barrier). None of these kernels
-// hands data between its own waves through global memory.
+// Workgroup barrier for LDS traffic only (the evaluation network's stages):
+// the release / acquire fences are restricted to the local address space, so
+// the barrier waits for the wave's LDS operations (lgkmcnt) but not for the
+// next stage's weight loads in flight (a plain __syncthreads() waits vmcnt(0)
+// too). Its waves hand nothing to each other through global memory. (In the
+// train step's k2 the same change measured no difference: 36.89 vs 36.89 us.)
 __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
+
 
 #ifdef HBK_TRACE
 // Tracing build only (lib/libhbk_trace.so, tools/probe_mlp.py): lane 0 of every
@@ -148,18 +149,6 @@ __device__ int g_mlp_trace_n[4][4];
   } while (0)
 #endif
 
-// The activations handed between kernels (xhat for k1b / k3; U, Xn, dS, dHG
-// for k3) are stored TRANSPOSED and BLOCKED: [B_s / 32][width][32] floats
-// (B_s = B rounded up to 32), i.e. for each block of 32 batch rows a
-// [width][32] tile with the rows contiguous. A k3 step (32 batch rows x 64
-// columns) is then one contiguous 8 KB run and a k1b chunk a few KB runs, where
-// a plain [width][B] layout scatters them over as many 128-B pieces as columns.
-constexpr int kTB = 32;
-__host__ __device__ __forceinline__ int64_t t_rows(int64_t B) { return (B + kTB - 1) / kTB * kTB; }
-__device__ __forceinline__ int64_t tix(int64_t col, int64_t row, int64_t width) {
-  return (row >> 5) * (width << 5) + (col << 5) + (row & 31);
-}
-
 __device__ __forceinline__ int step_of(const float* state, int parity) {
   return state ? static_cast<int>(state[parity * 8 + 3]) : 0;
 }
@@ -177,7 +166,7 @@ struct K1aArgs {
   int B;
   float drop_p;
   uint64_t seed;
-  float* xhat[2];      // transposed, blocked (tix, width 1536; rows >= B zero), by step parity
+  float* xhat[2];      // TRANSPOSED [1536][Bp] (rows >= B zero), by step parity
   int64_t Bp;
 };
 
@@ -289,7 +278,7 @@ __device__ __forceinline__ void k1a_tile(const K1aArgs& a, int rt, int step, flo
   }
 #pragma unroll
   for (int t = 0; t < 3; ++t) {
-    lds_barrier();  // the slab's previous readers are done
+    __syncthreads();  // the slab's previous readers are done
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       float* row = slab + (wave * 4 + i) * kSlabLd;
@@ -300,11 +289,11 @@ __device__ __forceinline__ void k1a_tile(const K1aArgs& a, int rt, int step, flo
         row[col] = xh[i][j];
       }
     }
-    lds_barrier();
+    __syncthreads();
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int col = tid + 256 * h;
-      float* dst = xout + tix(512 * t + col, rt * kR, kD);
+      float* dst = xout + static_cast<int64_t>(512 * t + col) * a.Bp + rt * kR;
 #pragma unroll
       for (int q4 = 0; q4 < 4; ++q4)
         *reinterpret_cast<f4*>(dst + 4 * q4) =
@@ -391,7 +380,7 @@ __global__ void __launch_bounds__(256) k1b_kernel(K1bArgs a) {
   for (int h = 0; h < kXl; ++h) {
     const int e = tid + 256 * h, col = e >> 4;
     const int row = min(r0 + 4 * (e & 15), static_cast<int>(a.Bp) - 4);
-    xt[h] = *reinterpret_cast<const f4*>(a.xhat + tix(k0 + col, row, kD));
+    xt[h] = *reinterpret_cast<const f4*>(a.xhat + static_cast<int64_t>(k0 + col) * a.Bp + row);
   }
   float gv[2], bv[2];
 #pragma unroll
@@ -429,7 +418,7 @@ __global__ void __launch_bounds__(256) k1b_kernel(K1bArgs a) {
   for (int c = 0; c < 2; ++c)
 #pragma unroll
     for (int i = 0; i < kN32; ++i) split8(wr[c][i][0] * 16.f, wr[c][i][1] * 16.f, whi[c][i], wlo[c][i]);
-  lds_barrier();
+  __syncthreads();
   HBK_MT(3, 2);
   // wave w -> output columns [32 w, 32 w + 32) of all 64 rows: 4 row tiles x 2
   // column tiles, A = LN output = xhat g + b from LDS (k = 32 i + 8 kq ..)
@@ -643,8 +632,7 @@ struct K2Args {
   float* logit;  // [B] or NULL
   float* G;      // gradient bucket (params layout)
   float* stats;  // its statistics tail (8 floats)
-  // activations for k3, transposed and blocked (tix), [NG] x t_rows(B) x width (Bp = B rounded
-  // up to 16: rows in [B, Bp) are zero, rows past Bp are never written):
+  // activations for k3, TRANSPOSED [NG][width][Bp] (Bp = B rounded up to 16, pad rows zero):
   // U 64, Xn 96 (k >= 1), dS 96 (k = NG-1: row 0 = dz), dHG 128
   int64_t Bp;
   float* U;
@@ -705,7 +693,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
       for (int t = 0; t < kPreTiles; ++t) {
         const int rt = (blockIdx.x - a.n_rt) * kPreTiles + t;
         if (rt >= a.n_rt) break;
-        if (t) lds_barrier();  // the slab's previous readers are done
+        if (t) __syncthreads();  // the slab's previous readers are done
         k1a_tile<true>(a.pre, rt, step, a.pre.xhat[a.pre.parity ^ 1], hgRaw);
       }
     }
@@ -717,7 +705,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
   const int nrow = min(kR, a.B - r0);
   const float* P = a.P;
   const int64_t B = a.B;
-  const int64_t Bs = t_rows(a.B);  // rows of the blocked activation arrays
+  const int64_t Bp = a.Bp;
   K2_MARK(1);
   // step, label and negative weight of this workgroup's rows (used by the loss,
   // loaded now so their two dependent latencies hide under the forward pass)
@@ -755,59 +743,65 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
       if (tid < kH2) sBhg[k][tid] = vbhg[k];
     if (tid < kH) sWo[tid] = vwo;
   }
-  // HG0 = sum of k1b's KS partial slabs + bias; U0 = silu(H) G. Thread -> row
-  // tid / 16, hidden / gate columns 4 (tid % 16) .. + 3 (16-B loads); up to 8
-  // slabs' loads are issued together (unrolled, clamped: slabs past KS are
-  // re-reads weighted 0; rows past B read row B - 1, whose values are finite and
-  // whose every gradient is multiplied by dz = 0).
+  // HG0 = sum of k1b's KS partial slabs + bias; U0 = silu(H) G. Thread ->
+  // 4 (row, j) pairs; up to 12 slabs' loads are issued together (unrolled,
+  // clamped: slabs past KS are re-reads weighted 0; rows past B read row B - 1,
+  // whose values are finite and whose every gradient is multiplied by dz = 0).
   {
-    const int r = tid >> 4, j4 = 4 * (tid & 15);
-    const float* src0 = a.hg_part + (r0 + min(r, nrow - 1)) * kH2 + j4;
-    f4 h = {0.f, 0.f, 0.f, 0.f}, g = h;
-    for (int s0 = 0; s0 < a.KS; s0 += 8) {
-      f4 lh[8], lgv[8];
+    float h[4] = {0.f, 0.f, 0.f, 0.f}, g[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int s0 = 0; s0 < a.KS; s0 += 12) {
+      float lh[12][4], lg[12][4];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const float* src = src0 + static_cast<int64_t>(min(s0 + u, a.KS - 1)) * B * kH2;
-        lh[u] = *reinterpret_cast<const f4*>(src);
-        lgv[u] = *reinterpret_cast<const f4*>(src + kH);
+      for (int u = 0; u < 12; ++u) {
+        const int sl = min(s0 + u, a.KS - 1);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int e = tid + 256 * q, r = min(e >> 6, nrow - 1), j = e & 63;
+          const float* src = a.hg_part + (sl * B + r0 + r) * kH2;
+          lh[u][q] = src[j];
+          lg[u][q] = src[kH + j];
+        }
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < 12; ++u) {
         const float on = s0 + u < a.KS ? 1.f : 0.f;
-        h += on * lh[u];
-        g += on * lgv[u];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          h[q] += on * lh[u][q];
+          g[q] += on * lg[u][q];
+        }
       }
     }
-    const f4 bh = *reinterpret_cast<const f4*>(P + a.b_hg[0] + j4), bg = *reinterpret_cast<const f4*>(P + a.b_hg[0] + kH + j4);
+    const float bh = P[a.b_hg[0] + (tid & 63)], bg = P[a.b_hg[0] + kH + (tid & 63)];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float hh = h[q] + bh[q], gg = g[q] + bg[q];
-      hgS[0][r][j4 + q] = hh;
-      hgS[0][r][kH + j4 + q] = gg;
-      bU[r][j4 + q] = hh * sigm(hh) * gg;
+      const int e = tid + 256 * q, r = e >> 6, j = e & 63;
+      const float hh = h[q] + bh, gg = g[q] + bg;
+      hgS[0][r][j] = hh;
+      hgS[0][r][kH + j] = gg;
+      bU[r][j] = hh * sigm(hh) * gg;
     }
   }
-  lds_barrier();
+  __syncthreads();
   K2_MARK(2);
   // transposed activation stores: 4 consecutive rows of one column per float4
-  auto st4 = [&](float* base, int width, int col, int row4, f4 v) {
+  auto st4 = [&](float* base, int col, int row4, f4 v) {
 #pragma unroll
     for (int e = 0; e < 4; ++e)
       if (r0 + row4 + e >= a.B) v[e] = 0.f;
-    *reinterpret_cast<f4*>(base + tix(col, r0 + row4, width)) = v;
+    *reinterpret_cast<f4*>(base + col * Bp + r0 + row4) = v;
   };
-  // a [16][kLd] LDS tile's first ncols columns -> base^T (4 rows per float4; width ncols)
+  // a [16][kLd] LDS tile's first ncols columns -> base^T (4 rows per float4)
   auto store_t = [&](float* base, const float* src, int ncols) {
     for (int e = tid; e < 4 * ncols; e += 256) {
       const int col = e >> 2, r4 = 4 * (e & 3);
-      st4(base, ncols, col, r4,
+      st4(base, col, r4,
           f4{src[r4 * kLd + col], src[(r4 + 1) * kLd + col], src[(r4 + 2) * kLd + col], src[(r4 + 3) * kLd + col]});
     }
   };
   if (kTrain) {  // U_0 from bU: thread -> column tid & 63, rows 4 (tid >> 6) ..
     const int j = tid & 63, rg = 4 * (tid >> 6);
-    st4(a.U, kH, j, rg, f4{bU[rg][j], bU[rg + 1][j], bU[rg + 2][j], bU[rg + 3][j]});
+    st4(a.U, j, rg, f4{bU[rg][j], bU[rg + 1][j], bU[rg + 2][j], bU[rg + 3][j]});
   }
   // ---------------------------------------------------------- forward ----
 #pragma unroll
@@ -826,7 +820,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
         for (int e = 0; e < 4; ++e) bS[4 * kq + e][n1] = c1[e] + bo1_;
       }
     }
-    lds_barrier();
+    __syncthreads();
     K2_MARK(10 + k);
     // LayerNorm k over 96 columns: 16 lanes per row (wave w -> rows 4w..4w+3,
     // lane -> row 4w + lane / 16, columns 6 (lane % 16) ..), both reductions of
@@ -851,10 +845,10 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
       }
       if ((lane & 15) == 0) rsS[k][r] = rs;
     }
-    lds_barrier();
+    __syncthreads();
     K2_MARK(20 + k);
     // HG_{k+1} = Xn W_hg^T + b, gate in the epilogue -> hgS[k+1], U_{k+1} -> bU
-    if (kTrain) store_t(a.Xn + (k + 1) * kL * Bs, &bX[0][0], kL);
+    if (kTrain) store_t(a.Xn + (k + 1) * kL * Bp, &bX[0][0], kL);
     {
       f4 ch, cg;
       gemm2<kL>(wb, load_a<kL>(&bX[0][0], lane), ch, cg);
@@ -871,9 +865,9 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
         bU[r][j] = u;
         uo[e] = u;
       }
-      if (kTrain) st4(a.U + (k + 1) * kH * Bs, kH, j, 4 * kq, uo);
+      if (kTrain) st4(a.U + (k + 1) * kH * Bp, j, 4 * kq, uo);
     }
-    lds_barrier();
+    __syncthreads();
     K2_MARK(30 + k);
   }
   // backward weight fragments of the first two backward matrix stages (from
@@ -895,7 +889,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
       if (lane == 0) zS[r] = z;
     }
   }
-  lds_barrier();
+  __syncthreads();
   K2_MARK(40);
   // sigmoid, high-loss filter (trainer.py:407-424), weighted BCE (:301-312, torch
   // formulas incl. the log clamp at -100 and the 1e-12 in BCE's backward)
@@ -953,12 +947,12 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
     }
   }
   if constexpr (!kTrain) return;
-  lds_barrier();
+  __syncthreads();
   K2_MARK(41);
   if (tid < kStats && red[tid] != 0.f) atomicAdd(a.stats + tid, red[tid]);
   // ---------------------------------------------------------- backward ---
   float* G = a.G;
-  if (tid < 4) st4(a.dS + (NG - 1) * kL * Bs, kL, 0, 4 * tid, f4{dzS[4 * tid], dzS[4 * tid + 1], dzS[4 * tid + 2], dzS[4 * tid + 3]});
+  if (tid < 4) st4(a.dS + (NG - 1) * kL * Bp, 0, 4 * tid, f4{dzS[4 * tid], dzS[4 * tid + 1], dzS[4 * tid + 2], dzS[4 * tid + 3]});
   if (tid == 64) {  // output bias gradient = sum dz
     float s = 0.f;
     for (int r = 0; r < kR; ++r) s += dzS[r];
@@ -981,10 +975,10 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
       dho[e] = dh;
       dgo[e] = dg;
     }
-    st4(a.dHG + k * kH2 * Bs, kH2, j, rg, dho);
-    st4(a.dHG + k * kH2 * Bs, kH2, kH + j, rg, dgo);
+    st4(a.dHG + k * kH2 * Bp, j, rg, dho);
+    st4(a.dHG + k * kH2 * Bp, kH + j, rg, dgo);
   }
-  lds_barrier();
+  __syncthreads();
   K2_MARK(42);
 #pragma unroll
   for (int k = NG - 1; k >= 1; --k) {
@@ -1007,7 +1001,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
         for (int e = 0; e < 4; ++e) bU[4 * kq + e][n1] = c1[e];
       }
     }
-    lds_barrier();
+    __syncthreads();
     K2_MARK(50 + k);
     // LayerNorm k-1 backward: gamma / beta column sums, dS_{k-1} per row -> bS
     {
@@ -1038,13 +1032,13 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
 #pragma unroll
       for (int e = 0; e < 6; ++e) bS[r][c0 + e] = rs * (t[e] - s1 - x[e] * s2);
     }
-    lds_barrier();
+    __syncthreads();
     K2_MARK(60 + k);
     // GMLP k-1: output bias gradient (column sums of dS), dU = dS W_o (NN: K 96 -> N 64,
     // fragments fy) with the gate backward in the epilogue -> dHG_{k-1} (bX)
     {
       const int kk = k - 1;
-      store_t(a.dS + kk * kL * Bs, &bS[0][0], kL);
+      store_t(a.dS + kk * kL * Bp, &bS[0][0], kL);
       if (tid < kL) {
         float s = 0.f;
         for (int r = 0; r < kR; ++r) s += bS[r][tid];
@@ -1065,10 +1059,10 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
         dho[e] = dh;
         dgo[e] = dg;
       }
-      st4(a.dHG + kk * kH2 * Bs, kH2, j, 4 * kq, dho);
-      st4(a.dHG + kk * kH2 * Bs, kH2, kH + j, 4 * kq, dgo);
+      st4(a.dHG + kk * kH2 * Bp, j, 4 * kq, dho);
+      st4(a.dHG + kk * kH2 * Bp, kH + j, 4 * kq, dgo);
     }
-    lds_barrier();
+    __syncthreads();
     K2_MARK(70 + k);
   }
   // bias gradient of mlp_in's hidden + gate
@@ -1087,194 +1081,264 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
 }
 
 // ------------------------------------------------------------------ k3 ----
-// dW [M][N] = X^T Y over ALL batch rows, from k1a/k2's transposed, blocked
-// activations X (width M: a gradient, dHG or dS) and Y (width N: an
-// activation, xhat, Xn or U); rows in [B, Bp) zero. No batch split: every output
-// element has one owner, written with a plain store straight into the gradient
-// bucket (no partial slabs, no float atomics; the input layer's gamma / beta
-// gradients add two workgroups' column sums, exact in either order onto the
-// bucket's zero). Tile 64 x 64 per 512-thread workgroup: the batch is walked in
-// steps of 32 rows (one block of the layout); each step's X and Y tiles (8 KB
-// each, contiguous) are prefetched
-// kK3Depth steps ahead in registers (one float4 of each per thread), then
-// staged through double-buffered LDS (one barrier per step): X raw, Y split
-// into f16 hi / lo planes once for all waves. Wave w owns M rows 16 (w & 3) ..
-// and the two 16-column tiles 2 (w >> 2), 2 (w >> 2) + 1. Split-f16 products on
-// v_mfma_f32_16x16x32_f16 (hi*hi + hi*lo + lo*hi, f32 accumulation). Gradients
-// can be arbitrarily small, so each wave scales its A fragments by a power of
-// two that it lowers whenever a step's max |X| needs it (max |X| 2^e < 2^15),
-// rescaling its accumulators exactly; the sums are scaled back at the end.
-constexpr int kTM = 64, kTN = 64, kMaxJobs = 2 * kMaxG;
-#ifndef HBK_K3_DEPTH
-#define HBK_K3_DEPTH 8
+// dW [M][N] += X^T Y over a split of batch rows, from k1a/k2's TRANSPOSED
+// activations X^T [M][Bp] (a gradient: dHG or dS), Y^T [N][Bp] (an
+// activation: xhat, Xn or U); rows of b contiguous, pad rows zero. Split-f16
+// products on v_mfma_f32_16x16x32_f16 (hi*hi + hi*lo + lo*hi, f32
+// accumulation): lane (m, kq) of step u holds b = 32 u + 8 kq .. + 7, so A and B
+// are two float4 runs along b. Gradients can be arbitrarily small, so X is
+// scaled by a power of two per workgroup (its tile's max |X| into [2^14, 2^15):
+// no f16 overflow, lo parts in f16's normal range) and the sums are scaled
+// back exactly. Tile 128 x 32: wave w owns M rows 32 w .. 32 w + 31 (two MFMA
+// row tiles, X in registers, all loads in flight together) and both 16-column
+// halves; the split's Y^T tile (32 x 288) is loaded once per workgroup, split
+// into f16 hi / lo planes in LDS and shared by the four waves. Split-K partials
+// are added with float atomics into the bucket (zeroed by the previous k4).
+constexpr int kTM = 128, kTN = 32, kMaxJobs = 2 * kMaxG;
+// batch rows per split: measured 4 / 5 / 6 / 9 steps (124 / 152 / 180 / 248 VGPRs) at 60.2 / 60.3 /
+// 61.6 / 58.9 us per step on 256 CUs and 88.7 / 88.9 / 94.8 / 92.1 on a 64-CU stream
+#ifndef HBK_K3_STEPS
+#define HBK_K3_STEPS 9
 #endif
-constexpr int kK3Depth = HBK_K3_DEPTH;  // batch steps in flight
-constexpr int kXLd = 36, kYLdH = 40;  // LDS row strides: floats of X, halves of Y
+constexpr int kK3Steps = HBK_K3_STEPS, kK3Rows = 32 * kK3Steps;  // batch rows per split (B = 1100: 4 splits)
+constexpr int kYLdH = kK3Rows + 8;                    // LDS row stride (halves) of the Y planes
+constexpr int kK3StepsNarrow = 4, kK3NarrowCUs = 96;
 struct WJob {
-  const float* X;  // blocked [t_rows(B) / 32][xw][32] (xw >= M: the stored width)
-  const float* Y;  // blocked [t_rows(B) / 32][yw][32]
+  const float* X;  // [M][Bp]
+  const float* Y;  // [N][Bp]
   int64_t c_off;   // the gradient [M][ldc] at this offset of the parameter layout
-  int ldc, M, N, tn, xw, yw;
+  int ldc, M, N, tn;
 };
+// The covered parameter ranges (k3's weight gradients, norm_in's gamma / beta):
+// k3 writes them as one partial slab per batch split, part[split][n_params],
+// with plain stores (float atomics run at the memory side, ~1 TB/s chip-wide,
+// and were most of k3's time); k4 adds the slabs while it reads the bucket
+// (or k3_fold_kernel adds them into the bucket first, for the all-reduce).
+constexpr int kMaxRng = 2 + 2 * kMaxG;
+struct Ranges {
+  int n;
+  int64_t lo[kMaxRng], hi[kMaxRng];
+};
+__device__ __forceinline__ bool in_ranges(const Ranges& r, int64_t i) {
+  bool c = false;
+#pragma unroll
+  for (int k = 0; k < kMaxRng; ++k) c |= k < r.n && i >= r.lo[k] && i < r.hi[k];
+  return c;
+}
 struct K3Args {
   WJob job[kMaxJobs];
   int start[kMaxJobs + 1];
-  int n_jobs;
-  int64_t Bp;  // B rounded up to 16: rows past it are not written (read as zero)
-  float* G;  // gradient bucket
+  int n_jobs, KS;
+  int64_t Bp;
   // input-layer job (job 0): post-op with norm_in's affine and W_hg0
   const float* g_in;
   const float* b_in;
   const float* W0;
   int64_t g_off, b_off;  // norm_in gamma / beta in the parameter layout
+  float* part;           // [KS][pstride] partial slabs
+  int64_t pstride;
 };
 
-__global__ void __launch_bounds__(512) k3_wgrad_kernel(K3Args a) {
-  __shared__ __attribute__((aligned(16))) float xS[2][kTM][kXLd];
-  __shared__ __attribute__((aligned(16))) _Float16 yS[2][2][kTN][kYLdH];
+// STEPS: batch rows per split / 32 (the grid's split count follows); the launch
+// takes kK3Steps on a wide stream and kK3StepsNarrow on a CU-masked one of at
+// most kK3NarrowCUs CUs (fewer, longer workgroups: see kK3Steps' sweep)
+template <int STEPS>
+__global__ void __launch_bounds__(256) k3_wgrad_kernel(K3Args a) {
+  constexpr int kK3Steps = STEPS, kK3Rows = 32 * STEPS, kYLdH = kK3Rows + 8;
+  __shared__ __attribute__((aligned(16))) _Float16 yh[kTN * kYLdH];
+  __shared__ __attribute__((aligned(16))) _Float16 yl[kTN * kYLdH];
   __shared__ float sS[kTM];
   __shared__ float red[2][4][kTN];
+  __shared__ float smax[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int blk = blockIdx.x;
   int j = 0;
   while (j + 1 < a.n_jobs && blk >= a.start[j + 1]) ++j;
   const WJob jb = a.job[j];
   const int local = blk - a.start[j];
-  const int tm = local / jb.tn, tn = local - tm * jb.tn;
-  const int m0 = tm * kTM, n0 = tn * kTN;
-  const int Bp = static_cast<int>(a.Bp);
-  const int n_steps = (Bp + 31) / 32;
+  const int split = local % a.KS, tile = local / a.KS;
+  float* const C = a.part + split * a.pstride + jb.c_off;
+  const int tm = tile / jb.tn, tn = tile - tm * jb.tn;
   HBK_MT(2, 1);
-  // staging: thread -> row (tid >> 3) of the X and Y tiles, batch rows 4 (tid & 7) ..;
-  // rows past M / N read a clamped valid row (their outputs are never stored)
-  const int sr = tid >> 3, sq = 4 * (tid & 7);
-  const float* xp = jb.X + static_cast<int64_t>(min(m0 + sr, jb.M - 1)) * kTB + sq;
-  const float* yp = jb.Y + static_cast<int64_t>(min(n0 + sr, jb.N - 1)) * kTB + sq;
-  const int64_t xblk = int64_t(jb.xw) * kTB, yblk = int64_t(jb.yw) * kTB;
-  f4 xr[kK3Depth], yr[kK3Depth];
-  auto fetch = [&](int s, int slot) {  // step s; past the last step: the last one again
-    const int64_t b = min(s, n_steps - 1);
-    xr[slot] = *reinterpret_cast<const f4*>(xp + b * xblk);
-    yr[slot] = *reinterpret_cast<const f4*>(yp + b * yblk);
-  };
+  const int rb0 = split * kK3Rows;
+  const int Bp = static_cast<int>(a.Bp);
+  const int m = lane & 15, kq = lane >> 4;
+  const int mrow = tm * kTM + 32 * wave;  // first M row of this wave (two 16-row tiles)
+  const int n0 = tn * kTN;
+  // Y^T tile: 32 columns x 288 rows = 72 float4 per column; rows past Bp are
+  // zeroed (their loads read a clamped valid run). Columns past N read a
+  // clamped row: their products only reach outputs that are never stored.
+  constexpr int kYv = kTN * kK3Rows / 4 / 256;  // float4 per thread (9)
+  f4 yv[kYv];
+#pragma unroll
+  for (int h = 0; h < kYv; ++h) {
+    const int e = tid + 256 * h, col = e / (kK3Rows / 4), off = 4 * (e % (kK3Rows / 4));
+    const int b = min(rb0 + off, Bp - 4);
+    yv[h] = *reinterpret_cast<const f4*>(jb.Y + static_cast<int64_t>(min(n0 + col, jb.N - 1)) * Bp + b);
+  }
+  // X: rows past M read a clamped row (discarded outputs); this lane's 8 batch
+  // rows past Bp (8-row granularity: Bp is a multiple of 16) read the last 8
+  // rows and are zeroed
+  const float* X0 = jb.X + static_cast<int64_t>(min(mrow + m, jb.M - 1)) * Bp;
+  const float* X1 = jb.X + static_cast<int64_t>(min(mrow + 16 + m, jb.M - 1)) * Bp;
+  f4 rx[2][kK3Steps][2];
+#pragma unroll
+  for (int u = 0; u < kK3Steps; ++u) {
+    const int b = min(rb0 + 32 * u + 8 * kq, Bp - 8);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      rx[0][u][h] = *reinterpret_cast<const f4*>(X0 + b + 4 * h);
+      rx[1][u][h] = *reinterpret_cast<const f4*>(X1 + b + 4 * h);
+    }
+  }
   const f4 z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int d = 0; d < kK3Depth; ++d) {
-    fetch(d, d);
-    __builtin_amdgcn_sched_barrier(0);  // in slot order, as the loop issues them: hipcc's counted waits stay exact
+  for (int h = 0; h < kYv; ++h) {
+    const int e = tid + 256 * h, col = e / (kK3Rows / 4), off = 4 * (e % (kK3Rows / 4));
+    const f4 v = rb0 + off < Bp ? yv[h] : z;
+    uint32_t h0, l0, h1, l1;
+    split_pair(v[0], v[1], h0, l0);
+    split_pair(v[2], v[3], h1, l1);
+    *reinterpret_cast<uint2*>(&yh[col * kYLdH + off]) = uint2{h0, h1};
+    *reinterpret_cast<uint2*>(&yl[col * kYLdH + off]) = uint2{l0, l1};
   }
-  const int m = lane & 15, kq = lane >> 4, mt = wave & 3, nt0 = 2 * (wave >> 2);
-  f4 acc[2] = {z, z};
-  float rsum = 0.f;  // this lane's part of the row sum of X (input job)
-  int e_cur = 127;   // the A scale 2^e_cur (127: not set yet)
-  const int n_groups = (n_steps + kK3Depth - 1) / kK3Depth;
-#pragma unroll 1
-  for (int g = 0; g < n_groups; ++g)
+  // zero the dead batch rows of X, row sums (input job) and the tile's max |X|
+  f4 ssum[2] = {z, z};
+  float mx = 0.f;
 #pragma unroll
-    for (int slot = 0; slot < kK3Depth; ++slot) {
-      const int s = g * kK3Depth + slot, buf = slot & 1;
-      static_assert(kK3Depth % 2 == 0, "the LDS buffer of a slot must be compile-time");
-      // stage step s (zero past the batch: rows >= Bp, unwritten; steps >= n_steps)
-      {
-        const bool live = s < n_steps && 32 * s + sq < Bp;
-        const f4 xv = live ? xr[slot] : z, yv = live ? yr[slot] : z;
-        *reinterpret_cast<f4*>(&xS[buf][sr][sq]) = xv;
-        uint32_t h0, l0, h1, l1;
-        split_pair(yv[0], yv[1], h0, l0);
-        split_pair(yv[2], yv[3], h1, l1);
-        *reinterpret_cast<uint2*>(&yS[buf][0][sr][sq]) = uint2{h0, h1};
-        *reinterpret_cast<uint2*>(&yS[buf][1][sr][sq]) = uint2{l0, l1};
-      }
-      HBK_MT(2, 10 + s);
-      fetch(s + kK3Depth, slot);
-      lds_barrier();
-      // the previous readers of buffer buf (step s - 2) passed this step's barrier's predecessor
-      const float* xa = &xS[buf][16 * mt + m][8 * kq];
-      const f4 v0 = *reinterpret_cast<const f4*>(xa), v1 = *reinterpret_cast<const f4*>(xa + 4);
-      rsum += ((v0[0] + v0[1]) + (v0[2] + v0[3])) + ((v1[0] + v1[1]) + (v1[2] + v1[3]));
-      float mx = 0.f;
+  for (int u = 0; u < kK3Steps; ++u) {
+    const bool live = rb0 + 32 * u + 8 * kq < Bp;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) mx = fmaxf(mx, fmaxf(fabsf(v0[e]), fabsf(v1[e])));
-      mx = wmax(mx);
-      if (mx > 0.f) {  // wave-uniform
-        const int e_need = min(14 - ilogbf(mx), 100);
-        if (e_need < e_cur) {
-          if (e_cur != 127) {
-            const float f = ldexpf(1.f, e_need - e_cur);
-            acc[0] *= f;
-            acc[1] *= f;
-          }
-          e_cur = e_need;
-        }
-      }
-      const float sc = ldexpf(1.f, e_cur == 127 ? 0 : e_cur);
-      h8 ah, al;
-      split8(v0 * sc, v1 * sc, ah, al);
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int n = 16 * (nt0 + t) + m;
-        const h8 bh = *reinterpret_cast<const h8*>(&yS[buf][0][n][8 * kq]);
-        const h8 bl = *reinterpret_cast<const h8*>(&yS[buf][1][n][8 * kq]);
-        acc[t] = mma3(ah, al, bh, bl, acc[t]);
+      for (int h = 0; h < 2; ++h) {
+        rx[t][u][h] = live ? rx[t][u][h] : z;
+        ssum[t] += rx[t][u][h];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) mx = fmaxf(mx, fabsf(rx[t][u][h][e]));
       }
-    }
-  const float unscale = e_cur == 127 ? 0.f : ldexpf(1.f, -e_cur);
-  acc[0] *= unscale;
-  acc[1] *= unscale;
-  HBK_MT(2, 2);
-  float* C = a.G + jb.c_off;
-  if (j != 0) {
+  }
+  mx = wmax(mx);
+  if (lane == 0) smax[wave] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
+  // scale = 2^(14 - floor(log2 max)): max |X| * scale in [2^14, 2^15)
+  const int ex = mx > 0.f ? min(14 - ilogbf(mx), 126) : 0;
+  const float scale = ldexpf(1.f, ex), unscale = ldexpf(1.f, -ex);
+  f4 acc[2][2] = {{z, z}, {z, z}};
+  const _Float16* y0h = &yh[m * kYLdH + 8 * kq];
+  const _Float16* y0l = &yl[m * kYLdH + 8 * kq];
+  const _Float16* y1h = &yh[(16 + m) * kYLdH + 8 * kq];
+  const _Float16* y1l = &yl[(16 + m) * kYLdH + 8 * kq];
+#pragma unroll
+  for (int u = 0; u < kK3Steps; ++u) {
+    const h8 bh0 = *reinterpret_cast<const h8*>(y0h + 32 * u), bl0 = *reinterpret_cast<const h8*>(y0l + 32 * u);
+    const h8 bh1 = *reinterpret_cast<const h8*>(y1h + 32 * u), bl1 = *reinterpret_cast<const h8*>(y1l + 32 * u);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      const int col = n0 + 16 * (nt0 + t) + m;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = m0 + 16 * mt + 4 * kq + e;
-        if (row < jb.M && col < jb.N) C[static_cast<int64_t>(row) * jb.ldc + col] = acc[t][e];
-      }
+      h8 ah, al;
+      split8(rx[t][u][0] * scale, rx[t][u][1] * scale, ah, al);
+      acc[t][0] = mma3(ah, al, bh0, bl0, acc[t][0]);
+      acc[t][1] = mma3(ah, al, bh1, bl1, acc[t][1]);
     }
-    return;
   }
-  // input layer: dW0 = g o (dHG0^T xhat) + b (x) s, s_j = sum_b dHG0[b][j];
-  // dgamma[k] = sum_j W0[j][k] (dHG0^T xhat)[j][k], dbeta[k] = sum_j W0[j][k] s_j
-  rsum += __shfl_xor(rsum, 16, 64);
-  rsum += __shfl_xor(rsum, 32, 64);
-  if (wave < 4 && kq == 0) sS[16 * mt + m] = rsum;
-  lds_barrier();
-  float dg[2] = {0.f, 0.f}, db[2] = {0.f, 0.f};
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    const int col = n0 + 16 * (nt0 + t) + m, cc = min(col, jb.N - 1);
-    const float g = a.g_in[cc], be = a.b_in[cc];
-    float w[4];
+    acc[t][0] *= unscale;
+    acc[t][1] *= unscale;
+  }
+  const bool nok0 = n0 + m < jb.N, nok1 = n0 + 16 + m < jb.N;
+  HBK_MT(2, 2);
+  if (j != 0) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) w[e] = a.W0[static_cast<int64_t>(min(m0 + 16 * mt + 4 * kq + e, jb.M - 1)) * jb.ldc + cc];
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = mrow + 16 * t + 4 * kq + e;
+        if (row < jb.M) {
+          if (nok0) C[static_cast<int64_t>(row) * jb.ldc + n0 + m] = acc[t][0][e];
+          if (nok1) C[static_cast<int64_t>(row) * jb.ldc + n0 + 16 + m] = acc[t][1][e];
+        }
+      }
+    return;
+  }
+  // input layer: s_j = sum over the split's rows of dHG0[b][j] (lanes m + 16 q hold parts)
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    float sj_part = (ssum[t][0] + ssum[t][1]) + (ssum[t][2] + ssum[t][3]);
+    sj_part += __shfl_xor(sj_part, 16, 64);
+    sj_part += __shfl_xor(sj_part, 32, 64);
+    if (kq == 0) sS[32 * wave + 16 * t + m] = sj_part;
+  }
+  __syncthreads();
+  float dg0 = 0.f, dg1 = 0.f, dbt0 = 0.f, dbt1 = 0.f;
+  const int c0 = n0 + m, c1 = n0 + 16 + m;
+  // every epilogue load is issued up front at clamped (valid) addresses, so none
+  // sits behind an atomic in a predicated branch
+  const int c0c = min(c0, jb.N - 1), c1c = min(c1, jb.N - 1);
+  const float g0 = a.g_in[c0c], g1 = a.g_in[c1c];
+  const float be0 = a.b_in[c0c], be1 = a.b_in[c1c];
+  float w0[2][4], w1[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int lr = 16 * mt + 4 * kq + e, row = m0 + lr;
-      if (row < jb.M) {
-        const float sj = sS[lr];
-        if (col < jb.N) C[static_cast<int64_t>(row) * jb.ldc + col] = g * acc[t][e] + be * sj;
-        dg[t] += w[e] * acc[t][e];
-        db[t] += w[e] * sj;
+      const float* wr = a.W0 + static_cast<int64_t>(min(mrow + 16 * t + 4 * kq + e, jb.M - 1)) * jb.ldc;
+      w0[t][e] = wr[c0c];
+      w1[t][e] = wr[c1c];
+    }
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = mrow + 16 * t + 4 * kq + e;  // j
+      if (row >= jb.M) continue;
+      const float sj = sS[32 * wave + 16 * t + 4 * kq + e];
+      if (nok0) {
+        C[static_cast<int64_t>(row) * jb.ldc + c0] = g0 * acc[t][0][e] + be0 * sj;
+        dg0 += w0[t][e] * acc[t][0][e];
+        dbt0 += w0[t][e] * sj;
+      }
+      if (nok1) {
+        C[static_cast<int64_t>(row) * jb.ldc + c1] = g1 * acc[t][1][e] + be1 * sj;
+        dg1 += w1[t][e] * acc[t][1][e];
+        dbt1 += w1[t][e] * sj;
       }
     }
-    dg[t] += __shfl_xor(dg[t], 16, 64);
-    dg[t] += __shfl_xor(dg[t], 32, 64);
-    db[t] += __shfl_xor(db[t], 16, 64);
-    db[t] += __shfl_xor(db[t], 32, 64);
-    if (kq == 0) {
-      red[0][mt][16 * (nt0 + t) + m] = dg[t];
-      red[1][mt][16 * (nt0 + t) + m] = db[t];
+  // reduce over kq (lanes m + 16 q) then over waves
+#pragma unroll
+  for (int o = 16; o < 64; o <<= 1) {
+    dg0 += __shfl_xor(dg0, o, 64);
+    dg1 += __shfl_xor(dg1, o, 64);
+    dbt0 += __shfl_xor(dbt0, o, 64);
+    dbt1 += __shfl_xor(dbt1, o, 64);
+  }
+  if (kq == 0) {
+    red[0][wave][m] = dg0;
+    red[0][wave][16 + m] = dg1;
+    red[1][wave][m] = dbt0;
+    red[1][wave][16 + m] = dbt1;
+  }
+  __syncthreads();
+  if (tid < kTN) {
+    const int c = n0 + tid;
+    if (c < jb.N) {
+      float* P = a.part + split * a.pstride;
+      P[a.g_off + c] = red[0][0][tid] + red[0][1][tid] + red[0][2][tid] + red[0][3][tid];
+      P[a.b_off + c] = red[1][0][tid] + red[1][1][tid] + red[1][2][tid] + red[1][3][tid];
     }
   }
-  lds_barrier();
-  if (tid < kTN) {
-    const int col = n0 + tid;
-    if (col < jb.N) {  // the tile's 64 rows of j; the other M tile adds its own (2 addends onto zero)
-      atomicAdd(a.G + a.g_off + col, (red[0][0][tid] + red[0][1][tid]) + (red[0][2][tid] + red[0][3][tid]));
-      atomicAdd(a.G + a.b_off + col, (red[1][0][tid] + red[1][1][tid]) + (red[1][2][tid] + red[1][3][tid]));
-    }
+}
+
+// Steps whose update does not get the workspace (or is preceded by the
+// data-parallel all-reduce): the slabs added into the bucket's covered ranges
+__global__ void __launch_bounds__(256) k3_fold_kernel(Ranges rg, const float* __restrict__ part, int64_t pstride,
+                                                      int ns, float* __restrict__ G, int64_t n) {
+  for (int64_t i = blockIdx.x * int64_t(256) + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
+    if (!in_ranges(rg, i)) continue;
+    float g = G[i];
+    for (int sp = 0; sp < ns; ++sp) g += part[sp * pstride + i];
+    G[i] = g;
   }
 }
 
@@ -1300,6 +1364,11 @@ struct K4Args {
   // transposed planes from LDS as 16-B column runs; the rest do everything else
   int n_tiles;
   int tile_seg[kMaxTiles], tile_r0[kMaxTiles];
+  // k3's partial slabs left for this update (ns of them; 0: none)
+  const float* part;
+  int64_t pstride;
+  int ns;
+  Ranges rg;
 };
 
 // The accumulation gate (trainer.py:443-465), computed identically by every
@@ -1358,6 +1427,26 @@ __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
   f4* M4 = reinterpret_cast<f4*>(a.m);
   f4* V4 = reinterpret_cast<f4*>(a.v);
   const f4 z4 = {0.f, 0.f, 0.f, 0.f};
+  const int ns = a.part ? a.ns : 0;
+  const f4* PT4 = reinterpret_cast<const f4*>(a.part);
+  const int64_t ps4 = a.pstride >> 2;
+  // the step's gradient of float4 i: the bucket (k2's atomics) and zero it, or, in a range
+  // covered by k3's deferred slabs (where the bucket holds zeros), the slabs' sum
+  auto grad4 = [&](int64_t i, bool covered, bool zero) -> f4 {
+    if (!covered) {
+      const f4 g = G4[i];
+      if (zero) G4[i] = z4;
+      return g;
+    }
+    f4 q[4] = {z4, z4, z4, z4};
+    int sp = 0;
+    for (; sp + 4 <= ns; sp += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) q[u] += PT4[(sp + u) * ps4 + i];
+    }
+    for (; sp < ns; ++sp) q[0] += PT4[sp * ps4 + i];
+    return (q[0] + q[1]) + (q[2] + q[3]);
+  };
   const float bc1 = 1.f - powf(a.b1, t), bc2s = sqrtf(1.f - powf(a.b2, t));
   const float step_size = lr / bc1;
   const bool on = fire != 0.f;
@@ -1367,8 +1456,7 @@ __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
   // the gate decision, which itself waits on the statistics); the parameters
   // after the step are returned
   auto adam4 = [&](int64_t i) -> f4 {
-    const f4 g = G4[i], m0 = M4[i], v0 = V4[i];
-    G4[i] = z4;
+    const f4 g = grad4(i, ns > 0 && in_ranges(a.rg, 4 * i), true), m0 = M4[i], v0 = V4[i];
     f4 p = P4[i];
     if (on) {
       const f4 gi = g * scale;
@@ -1399,7 +1487,7 @@ __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
       const int q = min(static_cast<int>(threadIdx.x) + 256 * it, rows * C4 - 1);
       const int r = q / C4, c4 = q - r * C4;
       const int64_t i = (g.src + int64_t(r0 + r) * C + 4 * c4) >> 2;
-      lg_[it] = G4[i];  // zeroed by the owner below (the clamped duplicates only read)
+      lg_[it] = grad4(i, ns > 0, false);  // the cached matrices are k3's (covered); zeroed by the owner below
       lm_[it] = M4[i];
       lv_[it] = V4[i];
       lp_[it] = P4[i];
@@ -1412,7 +1500,7 @@ __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
       const int64_t off = int64_t(r0 + r) * C + 4 * c4;
       const int64_t i = (g.src + off) >> 2;
       f4 p = lp_[it];
-      G4[i] = z4;
+      if (ns == 0) G4[i] = z4;  // (with slabs the bucket holds zeros here)
       if (on) {
         const f4 gi = lg_[it] * scale;
         const f4 mi = a.b1 * lm_[it] + (1.f - a.b1) * gi;
@@ -1434,7 +1522,7 @@ __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
       }
     }
     if (!on) return;  // the gate is the same in every thread: parameters and cache unchanged
-    lds_barrier();
+    __syncthreads();
     for (int u = threadIdx.x; u < C * (kTileR / 8); u += 256) {
       const int c = u / (kTileR / 8), rb = 8 * (u % (kTileR / 8));
       if (rb >= rows) continue;
@@ -1460,7 +1548,9 @@ __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
     adam4(i);
   }
   for (int64_t i = 4 * n4 + b0 * 256 + threadIdx.x; i < a.n; i += nb * 256) {
-    const float g = a.G[i];
+    float g = a.G[i];
+    if (ns > 0 && in_ranges(a.rg, i))
+      for (int sp = 0; sp < ns; ++sp) g += a.part[sp * a.pstride + i];
     a.G[i] = 0.f;
     if (on) {
       const float gi = g * scale;
@@ -2003,7 +2093,7 @@ __global__ void __launch_bounds__(256) kv_finish_kernel(EvalFinish f) {
 
 // --------------------------------------------------------- workspace ------
 struct FusedWs {
-  int64_t wsplit, hg_part, xhat[2], U, Xn, dS, dHG, total;  // float offsets
+  int64_t wsplit, part, pstride, hg_part, xhat[2], U, Xn, dS, dHG, total;  // float offsets
 };
 // the weight cache's segments (WSplit) for plan p: W_o_k (k < NG - 1), then W_hg_k (k >= 1)
 WSplit make_wsplit(const hbk_mlp_plan& p) {
@@ -2032,19 +2122,29 @@ int k1_splits(int B) {  // (one round of three per CU on a 64-CU stream, KS 8, m
     if (k1_blocks(B) * ks >= 256) return ks;
   return 24;
 }
+// k3's batch splits: rows per split by the stream's width (see kK3Steps)
+int k3_rows(const void* stream) {
+  static const bool k3_wide = getenv("HBK_K3_WIDE") != nullptr;
+  const bool narrow = !k3_wide && persistent_blocks(1, stream) <= kK3NarrowCUs;
+  return 32 * (narrow ? kK3StepsNarrow : kK3Steps);
+}
 FusedWs fused_layout(int64_t B, int NG, int64_t n_params = 0) {
   FusedWs w;
   int64_t o = 0;
   auto take = [&](int64_t n) { const int64_t r = o; o += (n + 63) & ~int64_t(63); return r; };
-  const int64_t Bs = t_rows(B);
+  const int64_t Bp = (B + kR - 1) / kR * kR;
   w.wsplit = take(wsplit_halves(NG) / 2);  // first: its offset does not depend on B
+  // k3's partial slabs (the most splits either width takes), at a fixed offset too
+  w.pstride = (n_params + 63) & ~int64_t(63);
+  w.part = take(w.pstride * ((Bp + 32 * std::min(kK3StepsNarrow, kK3Steps) - 1) /
+                             (32 * std::min(kK3StepsNarrow, kK3Steps))));
   w.hg_part = take(int64_t(24) * B * kH2);
-  w.xhat[0] = take(Bs * kD);
-  w.xhat[1] = take(Bs * kD);
-  w.U = take(int64_t(NG) * Bs * kH);
-  w.Xn = take(int64_t(NG) * Bs * kL);
-  w.dS = take(int64_t(NG) * Bs * kL);
-  w.dHG = take(int64_t(NG) * Bs * kH2);
+  w.xhat[0] = take(Bp * kD);
+  w.xhat[1] = take(Bp * kD);
+  w.U = take(int64_t(NG) * Bp * kH);
+  w.Xn = take(int64_t(NG) * Bp * kL);
+  w.dS = take(int64_t(NG) * Bp * kL);
+  w.dHG = take(int64_t(NG) * Bp * kH2);
   w.total = o;
   return w;
 }
@@ -2078,6 +2178,21 @@ void set_k2_cache(const WSplit& wsp, int NG, const _Float16* wc, K2Args& k2) {
   }
 }
 
+// k3's covered parameter ranges: norm_in gamma / beta, every W_hg and W_o
+Ranges make_ranges(const hbk_mlp_plan& p) {
+  Ranges r{};
+  auto add = [&](int64_t lo, int64_t n) {
+    r.lo[r.n] = lo;
+    r.hi[r.n++] = lo + n;
+  };
+  add(p.ln_in.g, p.ln_in.d);
+  add(p.ln_in.b, p.ln_in.d);
+  for (const Gmlp& g : p.g) {
+    add(g.w_hg, int64_t(2) * g.hid * g.in);
+    add(g.w_o, int64_t(g.out) * g.hid);
+  }
+  return r;
+}
 
 // evaluation workspace: the weight cache (as the fused layout's first region),
 // W' planes, c0, c1
@@ -2220,48 +2335,74 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
   // k3: job 0 = input layer, then dW_hg of GMLPs 1.., then dW_o of every GMLP
   K3Args k3;
   int nj = 0, blocks = 0;
-  auto add = [&](const float* X, int xw, const float* Y, int yw, int64_t c_off, int ldc, int M, int N) {
+  // HBK_K3_WIDE=1: the 288-row splits on narrow streams too (4 instead of 9
+  // splits at B = 1100: fewer partial slabs, more time on a small partition)
+  const int rows3 = k3_rows(s);
+  const bool narrow = rows3 == 32 * kK3StepsNarrow;
+  const int KS3 = static_cast<int>((Bp + rows3 - 1) / rows3);
+  auto add = [&](const float* X, const float* Y, int64_t c_off, int ldc, int M, int N) {
     WJob& j = k3.job[nj];
     j.X = X;
     j.Y = Y;
-    j.xw = xw;
-    j.yw = yw;
     j.c_off = c_off;
     j.ldc = ldc;
     j.M = M;
     j.N = N;
     j.tn = (N + kTN - 1) / kTN;
     k3.start[nj] = blocks;
-    blocks += ((M + kTM - 1) / kTM) * j.tn;
+    blocks += ((M + kTM - 1) / kTM) * j.tn * KS3;
     ++nj;
   };
-  const int64_t Bs = t_rows(B);
-  add(ws + w.dHG, kH2, xhat, kD, p.g[0].w_hg, kD, kH2, kD);
+  add(ws + w.dHG, xhat, p.g[0].w_hg, kD, kH2, kD);
   for (int k = 1; k < NG; ++k)
-    add(ws + w.dHG + int64_t(k) * kH2 * Bs, kH2, ws + w.Xn + int64_t(k) * kL * Bs, kL, p.g[k].w_hg, kL, kH2, kL);
+    add(ws + w.dHG + int64_t(k) * kH2 * Bp, ws + w.Xn + int64_t(k) * kL * Bp, p.g[k].w_hg, kL, kH2, kL);
   for (int k = 0; k < NG; ++k)
-    add(ws + w.dS + int64_t(k) * kL * Bs, kL, ws + w.U + int64_t(k) * kH * Bs, kH, p.g[k].w_o, kH, p.g[k].out, kH);
+    add(ws + w.dS + int64_t(k) * kL * Bp, ws + w.U + int64_t(k) * kH * Bp, p.g[k].w_o, kH, p.g[k].out, kH);
   k3.start[nj] = blocks;
   k3.n_jobs = nj;
+  k3.KS = KS3;
   k3.Bp = Bp;
-  k3.G = bucket;
   k3.g_in = params + p.ln_in.g;
   k3.b_in = params + p.ln_in.b;
   k3.W0 = params + p.g[0].w_hg;
   k3.g_off = p.ln_in.g;
   k3.b_off = p.ln_in.b;
-  hipLaunchKernelGGL(k3_wgrad_kernel, dim3(blocks), dim3(512), 0, s, k3);
+  k3.part = ws + w.part;
+  k3.pstride = w.pstride;
+  if (narrow)
+    hipLaunchKernelGGL(k3_wgrad_kernel<kK3StepsNarrow>, dim3(blocks), dim3(256), 0, s, k3);
+  else
+    hipLaunchKernelGGL(k3_wgrad_kernel<kK3Steps>, dim3(blocks), dim3(256), 0, s, k3);
   HBK_LAUNCH_CHECK("k3_wgrad_kernel");
+  if (flags & HBK_STEP_DEFER_PARTIALS) {  // the update adds the slabs
+    p.deferred_ws = ws;
+    p.deferred_ks = KS3;
+  } else {
+    p.deferred_ws = nullptr;
+    hipLaunchKernelGGL(k3_fold_kernel, dim3(unsigned(std::min<int64_t>((p.n_params + 255) / 256, 1024))), dim3(256),
+                       0, s, make_ranges(p), ws + w.part, w.pstride, KS3, bucket, p.n_params);
+    HBK_LAUNCH_CHECK("k3_fold_kernel");
+  }
   return HBK_OK;
 }
 
 int mlp_fused_update(const hbk_mlp_plan& p, float* params, float* bucket, float* m, float* v, float* state,
                      int parity, const float* sched, int sched_len, float lr, float b1, float b2, float eps,
                      float* hist, int hist_cap, float* ws, hipStream_t s) {
+  if (p.deferred_ws && p.deferred_ws != ws) {
+    set_error("hbk: the previous hbk_mlp_step_fwd_bwd deferred its weight-gradient partials to its workspace: "
+              "pass that workspace to hbk_mlp_step_update");
+    return HBK_ERR_ARG;
+  }
   K4Args k;
   k.w = make_wsplit(p);
   const FusedWs fl = fused_layout(1, static_cast<int>(p.g.size()), p.n_params);
   k.wc = ws ? reinterpret_cast<_Float16*>(ws + fl.wsplit) : nullptr;
+  k.part = p.deferred_ws ? ws + fl.part : nullptr;
+  k.pstride = fl.pstride;
+  k.ns = p.deferred_ws ? p.deferred_ks : 0;
+  k.rg = make_ranges(p);
+  p.deferred_ws = nullptr;
   k.n_tiles = 0;
   for (int sg = 0; sg < k.w.n; ++sg)
     for (int r0 = 0; r0 < k.w.s[sg].rows && k.n_tiles < kMaxTiles; r0 += kTileR) {

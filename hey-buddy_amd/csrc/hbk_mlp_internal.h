@@ -29,6 +29,10 @@ struct hbk_mlp_plan {
   // hbk_mlp_set_step_scalars: device [lr, neg_weight, seed] read by the train
   // kernels in place of their by-value arguments (graph-captured steps)
   const double* step_scalars = nullptr;
+  // hbk_mlp_step_fwd_bwd with HBK_STEP_DEFER_PARTIALS left its weight-gradient
+  // slabs (deferred_ks of them) in this workspace for the next hbk_mlp_step_update
+  mutable const void* deferred_ws = nullptr;
+  mutable int deferred_ks = 0;
 };
 
 namespace hbk {

@@ -479,7 +479,7 @@ class MlpPlan:
                      dropout_p: float = 0.0, seed: int = 0, prob: torch.Tensor | None = None,
                      workspace: torch.Tensor | None = None, xhat_ready: bool = False,
                      prefetch_next: bool = False, idx_steps: int | None = None,
-                     weights_ready: bool = False) -> None:
+                     weights_ready: bool = False, defer_partials: bool = False) -> None:
         """Forward / filter / BCE / backward of one step into ``bucket``
         (hbk_mlp_step_fwd_bwd). Rows come from pool32 [n, 1536] f32 and pool16
         [n, 1536] f16 by ``idx`` (int32, >= 0 -> pool32, < 0 -> pool16 row -i-1;
@@ -488,9 +488,10 @@ class MlpPlan:
         step + 1 < idx_steps, default idx.numel() // idx_stride) during this
         step; ``xhat_ready``: the previous call on this workspace did that for
         this step; ``weights_ready``: the previous step_update got this
-        workspace, so its weight cache is current (else it is refreshed). The
-        weight gradients are complete in ``bucket`` when the step's work ends
-        (ready for an all-reduce before step_update)."""
+        workspace, so its weight cache is current (else it is refreshed);
+        ``defer_partials``: the weight gradients' per-split slabs stay in the
+        workspace for the next step_update, which must get it (one process, no
+        all-reduce in between); else they are summed into ``bucket`` here."""
         dev = params.device
         if params.numel() != self.n_params or bucket.numel() != self.n_params + self.N_STATS:
             raise ValueError("params / bucket do not match the plan")
@@ -512,7 +513,7 @@ class MlpPlan:
         if idx_steps is None:
             idx_steps = idx.numel() // idx_stride if idx is not None and idx_stride > 0 else 1
         flags = (1 if xhat_ready else 0) | (2 if prefetch_next and idx is not None else 0) | (
-            4 if weights_ready else 0)
+            4 if weights_ready else 0) | (8 if defer_partials else 0)
         torch.ops.hbk.mlp_step_fwd_bwd(params, bucket, state, int(parity), y, int(batch), pool32, pool16, idx,
                                        int(idx_stride), int(y_stride), sched, float(neg_weight), float(threshold),
                                        float(activation_threshold), float(dropout_p), _u64_to_i64(seed), prob, ws,

@@ -459,13 +459,15 @@ class WakeWordTrainer(Trainer):
 
         # Each step also gathers + normalises the NEXT step's rows inside its own
         # launches (prefetch_next); only the first step of this call gathers its own.
+        # One process: the weight-gradient slabs go straight to the update (no all-reduce between).
+        defer = not distributed.reduces()
 
         def one(parity: int, ready: bool) -> None:
             plan.step_fwd_bwd(flat, self._bucket, self._fstate, parity, y, B, pool32=p32, pool16=p16, idx=idx,
                               idx_stride=B, y_stride=y_stride, sched=sched, threshold=threshold,
                               activation_threshold=activation_threshold, dropout_p=p, seed=self._seed_base,
                               workspace=ws, xhat_ready=ready, prefetch_next=True, idx_steps=S_all,
-                              weights_ready=ready)
+                              weights_ready=ready, defer_partials=defer)
             distributed.reduce_bucket(self._bucket)
             plan.step_update(flat, self._bucket, self._m, self._v, self._fstate, parity, sched=sched,
                              beta1=BETAS[0], beta2=BETAS[1], eps=EPS, history=history, workspace=ws)

@@ -275,12 +275,17 @@ int hbk_mlp_gate_adam(const hbk_mlp_plan* plan, float* params, const float* buck
  *   flags & HBK_STEP_WEIGHTS_READY: the previous hbk_mlp_step_update got the same
  *     workspace and left the cache current (it rewrites the cached matrices with
  *     every update); without it the step refreshes the cache from params first.
- * The weight gradients land in the bucket complete when the call's work ends
- * (each element written once, over the whole batch): the bucket can be
- * all-reduced between this call and hbk_mlp_step_update. */
+ * The weight gradients are written per batch split as partial slabs in the
+ * workspace (plain stores; no float atomics) and summed once:
+ *   flags & HBK_STEP_DEFER_PARTIALS: by the next hbk_mlp_step_update, which must
+ *     get this workspace (it fails otherwise) and must follow with nothing that
+ *     reads the bucket in between (one process: no all-reduce);
+ *   without it: into the bucket at the end of this call (for the data-parallel
+ *     all-reduce, or an update without the workspace). */
 #define HBK_STEP_XHAT_READY 1
 #define HBK_STEP_PREFETCH_NEXT 2
 #define HBK_STEP_WEIGHTS_READY 4
+#define HBK_STEP_DEFER_PARTIALS 8
 int hbk_mlp_fused_supported(const hbk_mlp_plan* plan, int32_t* supported);
 int hbk_mlp_step_fwd_bwd(const hbk_mlp_plan* plan, const float* params, const float* pool32, int64_t n32,
                          const void* pool16, int64_t n16, const int32_t* idx, int64_t idx_step_stride,
