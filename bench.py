@@ -84,14 +84,16 @@ def parse():
                     help="config 5 at N > 1: the reference's batch of 1,100 per rank (weak: global batch "
                          "1,100 N, 1,000 steps per rank) or split over the ranks (global batch 1,100, "
                          "N x 1,000 steps per rank)")
-    ap.add_argument("--embed-split", type=int, default=3,
+    ap.add_argument("--embed-split", type=int, default=0,
                     help="config 5, pipelined: the embedding's first K fused chains run on the featurize stream, "
                          "the rest (and the NaN replacement) on the train stream after its steps "
-                         "(hbk_embed_clips_front / _back; 0: the whole embedding on the featurize stream)")
-    ap.add_argument("--embed-split-frac", type=float, default=0.4,
+                         "(hbk_embed_clips_front / _back; 0: the whole embedding on the featurize stream). "
+                         "With the validation + testing passes in the train chunk the train stream carries "
+                         "enough: r04g, one box, 0 (no split) 857 k clips/s, partitions featurize 114.5 / "
+                         "train 114.1 ms, against 3 / 0.4 776 k (111.1 / 127.2 ms), 3 / 0 785 k")
+    ap.add_argument("--embed-split-frac", type=float, default=0.0,
                     help="with --embed-split K: this fraction of each chunk's clips is split after K - 1 "
-                         "chains instead (a finer balance of the two streams; default 3 / 0.4: p2s of 60 %% "
-                         "of the clips on the featurize stream, measured 900-904 k vs 883 k clips/s at 2 / 0)")
+                         "chains instead (a finer balance of the two streams)")
     ap.add_argument("--validation-steps", type=int, default=250,
                     help="config 5: the reference's validation + testing passes every this many stage steps "
                          "(DEFAULT_VALIDATION_STEPS, trainer.py:496-566; 0 = off): 500 batches of 50 + 1,000 "
