@@ -1636,6 +1636,9 @@ __global__ void __launch_bounds__(256) kv_prep_kernel(const float* __restrict__ 
   }
 }
 
+#ifndef HBK_KV_ABLATE
+#define HBK_KV_ABLATE 0  // profiling builds: 1 skips the network phase, 2 the dropout mask
+#endif
 // The streamed rows are read once: non-temporal loads (HBK_KV_NT, default on)
 // keep them from evicting W', which every tile re-reads, from the XCD's L2.
 #ifndef HBK_KV_NT
@@ -1768,7 +1771,7 @@ __global__ void __launch_bounds__(512) kv_gemm_kernel(KvArgs a) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = __builtin_bit_cast(float, (&ar[slot][rt][kb][e >> 2].x)[e & 3]);
         }
-        if (a.drop_p > 0.f) {  // nn.Dropout's mask (the 1 / (1 - p) scale is applied after the GEMM)
+        if (!(HBK_KV_ABLATE & 2) && a.drop_p > 0.f) {  // nn.Dropout's mask (the 1 / (1 - p) scale is applied after the GEMM)
           const uint32_t base = rid[rt] * (kD / 2) + ((kKvKC * c + 32 * kb + 8 * kq) >> 1);
 #pragma unroll
           for (int e = 0; e < 8; e += 2) {
@@ -1843,6 +1846,9 @@ __global__ void __launch_bounds__(512) kv_gemm_kernel(KvArgs a) {
     }
   }
   dma_barrier();
+#if HBK_KV_ABLATE & 1  // profiling build: the input GEMM only (no network, no counts)
+  if (a.rows > 0) return;
+#endif
   // ---- the rest of the network, per wave on its kRT row tiles ----
   // HG0 = rs (acc / 16 keep - mu c1) + c0 + b; U0 = silu(H) G into the wave's
   // activation tile (the lane holds hidden column j = 16 ct + m and gate column

@@ -462,11 +462,14 @@ class WakeWordTrainer(Trainer):
         # One process: the weight-gradient slabs go straight to the update (no all-reduce between).
         defer = not distributed.reduces()
 
+        # HBK_NO_PREFETCH=1 (A/B): every step gathers its own rows in a k1a launch
+        pre = os.environ.get("HBK_NO_PREFETCH") is None
+
         def one(parity: int, ready: bool) -> None:
             plan.step_fwd_bwd(flat, self._bucket, self._fstate, parity, y, B, pool32=p32, pool16=p16, idx=idx,
                               idx_stride=B, y_stride=y_stride, sched=sched, threshold=threshold,
                               activation_threshold=activation_threshold, dropout_p=p, seed=self._seed_base,
-                              workspace=ws, xhat_ready=ready, prefetch_next=True, idx_steps=S_all,
+                              workspace=ws, xhat_ready=ready and pre, prefetch_next=pre, idx_steps=S_all,
                               weights_ready=ready, defer_partials=defer)
             distributed.reduce_bucket(self._bucket)
             plan.step_update(flat, self._bucket, self._m, self._v, self._fstate, parity, sched=sched,

@@ -14,7 +14,7 @@ for L in ${LIBS:-libhbk.so}; do
 import csv, glob, sys
 f = glob.glob(sys.argv[1] + "/**/*kernel_stats.csv", recursive=True)[0]
 for r in csv.DictReader(open(f)):
-    if any(s in r["Name"] for s in ("k1b", "k2_", "k3_", "k4_")):
+    if any(s in r["Name"] for s in ("k1a", "k1b", "k2_", "k3_", "k4_")):
         print("  %-40s calls %6s avg %7.2f us" % (r["Name"][:40], r["Calls"], float(r["AverageNs"]) / 1e3))
 PY
   rm -rf gpurun_out/ab_$L
