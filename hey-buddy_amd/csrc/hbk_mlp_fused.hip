@@ -1103,6 +1103,14 @@ constexpr int kTM = 128, kTN = 32, kMaxJobs = 2 * kMaxG;
 constexpr int kK3Steps = HBK_K3_STEPS, kK3Rows = 32 * kK3Steps;  // batch rows per split (B = 1100: 4 splits)
 constexpr int kYLdH = kK3Rows + 8;                    // LDS row stride (halves) of the Y planes
 constexpr int kK3StepsNarrow = 4, kK3NarrowCUs = 96;
+// narrow streams: one workgroup may walk this many consecutive 128-row splits
+// (one partial slab per group). Measured at 3 on a 64-CU stream: k3 23.8 ->
+// 38.9 us (256 VGPRs, two workgroups per CU, the splits' latencies in series)
+// and k4 unchanged at 11.7 us with 3 slabs instead of 9, so it stays 1.
+#ifndef HBK_K3_GROUP
+#define HBK_K3_GROUP 1
+#endif
+constexpr int kK3GroupNarrow = HBK_K3_GROUP;
 struct WJob {
   const float* X;  // [M][Bp]
   const float* Y;  // [N][Bp]
@@ -1142,7 +1150,7 @@ struct K3Args {
 // STEPS: batch rows per split / 32 (the grid's split count follows); the launch
 // takes kK3Steps on a wide stream and kK3StepsNarrow on a CU-masked one of at
 // most kK3NarrowCUs CUs (fewer, longer workgroups: see kK3Steps' sweep)
-template <int STEPS>
+template <int STEPS, int G>
 __global__ void __launch_bounds__(256) k3_wgrad_kernel(K3Args a) {
   constexpr int kK3Steps = STEPS, kK3Rows = 32 * STEPS, kYLdH = kK3Rows + 8;
   __shared__ __attribute__((aligned(16))) _Float16 yh[kTN * kYLdH];
@@ -1156,96 +1164,111 @@ __global__ void __launch_bounds__(256) k3_wgrad_kernel(K3Args a) {
   while (j + 1 < a.n_jobs && blk >= a.start[j + 1]) ++j;
   const WJob jb = a.job[j];
   const int local = blk - a.start[j];
-  const int split = local % a.KS, tile = local / a.KS;
+  const int split = local % a.KS, tile = local / a.KS;  // split: a group of G consecutive batch splits
   float* const C = a.part + split * a.pstride + jb.c_off;
   const int tm = tile / jb.tn, tn = tile - tm * jb.tn;
   HBK_MT(2, 1);
-  const int rb0 = split * kK3Rows;
   const int Bp = static_cast<int>(a.Bp);
   const int m = lane & 15, kq = lane >> 4;
   const int mrow = tm * kTM + 32 * wave;  // first M row of this wave (two 16-row tiles)
   const int n0 = tn * kTN;
-  // Y^T tile: 32 columns x 288 rows = 72 float4 per column; rows past Bp are
-  // zeroed (their loads read a clamped valid run). Columns past N read a
-  // clamped row: their products only reach outputs that are never stored.
-  constexpr int kYv = kTN * kK3Rows / 4 / 256;  // float4 per thread (9)
+  // Y^T tile of a split: 32 columns x kK3Rows rows; rows past Bp are zeroed
+  // (their loads read a clamped valid run). Columns past N read a clamped row:
+  // their products only reach outputs that are never stored.
+  constexpr int kYv = kTN * kK3Rows / 4 / 256;  // float4 per thread
   f4 yv[kYv];
+  auto load_y = [&](int rb0) {
 #pragma unroll
-  for (int h = 0; h < kYv; ++h) {
-    const int e = tid + 256 * h, col = e / (kK3Rows / 4), off = 4 * (e % (kK3Rows / 4));
-    const int b = min(rb0 + off, Bp - 4);
-    yv[h] = *reinterpret_cast<const f4*>(jb.Y + static_cast<int64_t>(min(n0 + col, jb.N - 1)) * Bp + b);
-  }
+    for (int h = 0; h < kYv; ++h) {
+      const int e = tid + 256 * h, col = e / (kK3Rows / 4), off = 4 * (e % (kK3Rows / 4));
+      const int b = min(rb0 + off, Bp - 4);
+      yv[h] = *reinterpret_cast<const f4*>(jb.Y + static_cast<int64_t>(min(n0 + col, jb.N - 1)) * Bp + b);
+    }
+  };
   // X: rows past M read a clamped row (discarded outputs); this lane's 8 batch
   // rows past Bp (8-row granularity: Bp is a multiple of 16) read the last 8
   // rows and are zeroed
   const float* X0 = jb.X + static_cast<int64_t>(min(mrow + m, jb.M - 1)) * Bp;
   const float* X1 = jb.X + static_cast<int64_t>(min(mrow + 16 + m, jb.M - 1)) * Bp;
   f4 rx[2][kK3Steps][2];
-#pragma unroll
-  for (int u = 0; u < kK3Steps; ++u) {
+  auto load_x = [&](int rb0, int u) {
     const int b = min(rb0 + 32 * u + 8 * kq, Bp - 8);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       rx[0][u][h] = *reinterpret_cast<const f4*>(X0 + b + 4 * h);
       rx[1][u][h] = *reinterpret_cast<const f4*>(X1 + b + 4 * h);
     }
-  }
+  };
+  const int rbase = split * G * kK3Rows;
+  load_y(rbase);
+#pragma unroll
+  for (int u = 0; u < kK3Steps; ++u) load_x(rbase, u);
   const f4 z = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int h = 0; h < kYv; ++h) {
-    const int e = tid + 256 * h, col = e / (kK3Rows / 4), off = 4 * (e % (kK3Rows / 4));
-    const f4 v = rb0 + off < Bp ? yv[h] : z;
-    uint32_t h0, l0, h1, l1;
-    split_pair(v[0], v[1], h0, l0);
-    split_pair(v[2], v[3], h1, l1);
-    *reinterpret_cast<uint2*>(&yh[col * kYLdH + off]) = uint2{h0, h1};
-    *reinterpret_cast<uint2*>(&yl[col * kYLdH + off]) = uint2{l0, l1};
-  }
-  // zero the dead batch rows of X, row sums (input job) and the tile's max |X|
   f4 ssum[2] = {z, z};
-  float mx = 0.f;
-#pragma unroll
-  for (int u = 0; u < kK3Steps; ++u) {
-    const bool live = rb0 + 32 * u + 8 * kq < Bp;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        rx[t][u][h] = live ? rx[t][u][h] : z;
-        ssum[t] += rx[t][u][h];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) mx = fmaxf(mx, fabsf(rx[t][u][h][e]));
-      }
-  }
-  mx = wmax(mx);
-  if (lane == 0) smax[wave] = mx;
-  __syncthreads();
-  mx = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
-  // scale = 2^(14 - floor(log2 max)): max |X| * scale in [2^14, 2^15)
-  const int ex = mx > 0.f ? min(14 - ilogbf(mx), 126) : 0;
-  const float scale = ldexpf(1.f, ex), unscale = ldexpf(1.f, -ex);
   f4 acc[2][2] = {{z, z}, {z, z}};
   const _Float16* y0h = &yh[m * kYLdH + 8 * kq];
   const _Float16* y0l = &yl[m * kYLdH + 8 * kq];
   const _Float16* y1h = &yh[(16 + m) * kYLdH + 8 * kq];
   const _Float16* y1l = &yl[(16 + m) * kYLdH + 8 * kq];
+  // the group's splits one after the other, each with its own power-of-two
+  // scale; the next split's Y loads are issued once this one's tile is in LDS,
+  // its X loads step by step as this one's products release the registers
 #pragma unroll
-  for (int u = 0; u < kK3Steps; ++u) {
-    const h8 bh0 = *reinterpret_cast<const h8*>(y0h + 32 * u), bl0 = *reinterpret_cast<const h8*>(y0l + 32 * u);
-    const h8 bh1 = *reinterpret_cast<const h8*>(y1h + 32 * u), bl1 = *reinterpret_cast<const h8*>(y1l + 32 * u);
+  for (int g = 0; g < G; ++g) {
+    const int rb0 = rbase + g * kK3Rows;
+    if (g) lds_barrier();  // the previous split's readers of yh / yl (and smax) are done
+#pragma unroll
+    for (int h = 0; h < kYv; ++h) {
+      const int e = tid + 256 * h, col = e / (kK3Rows / 4), off = 4 * (e % (kK3Rows / 4));
+      const f4 v = rb0 + off < Bp ? yv[h] : z;
+      uint32_t h0, l0, h1, l1;
+      split_pair(v[0], v[1], h0, l0);
+      split_pair(v[2], v[3], h1, l1);
+      *reinterpret_cast<uint2*>(&yh[col * kYLdH + off]) = uint2{h0, h1};
+      *reinterpret_cast<uint2*>(&yl[col * kYLdH + off]) = uint2{l0, l1};
+    }
+    // zero the dead batch rows of X, row sums (input job) and the split's max |X|
+    float mx = 0.f;
+#pragma unroll
+    for (int u = 0; u < kK3Steps; ++u) {
+      const bool live = rb0 + 32 * u + 8 * kq < Bp;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          rx[t][u][h] = live ? rx[t][u][h] : z;
+          ssum[t] += rx[t][u][h];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) mx = fmaxf(mx, fabsf(rx[t][u][h][e]));
+        }
+    }
+    mx = wmax(mx);
+    if (lane == 0) smax[wave] = mx;
+    lds_barrier();  // (LDS only: the next split's loads issued below stay in flight)
+    if (g + 1 < G) load_y(rb0 + kK3Rows);
+    mx = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
+    // scale = 2^(14 - floor(log2 max)): max |X| * scale in [2^14, 2^15)
+    const int ex = mx > 0.f ? min(14 - ilogbf(mx), 126) : 0;
+    const float scale = ldexpf(1.f, ex), unscale = ldexpf(1.f, -ex);
+    f4 as[2][2] = {{z, z}, {z, z}};
+#pragma unroll
+    for (int u = 0; u < kK3Steps; ++u) {
+      const h8 bh0 = *reinterpret_cast<const h8*>(y0h + 32 * u), bl0 = *reinterpret_cast<const h8*>(y0l + 32 * u);
+      const h8 bh1 = *reinterpret_cast<const h8*>(y1h + 32 * u), bl1 = *reinterpret_cast<const h8*>(y1l + 32 * u);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        h8 ah, al;
+        split8(rx[t][u][0] * scale, rx[t][u][1] * scale, ah, al);
+        as[t][0] = mma3(ah, al, bh0, bl0, as[t][0]);
+        as[t][1] = mma3(ah, al, bh1, bl1, as[t][1]);
+      }
+      if (g + 1 < G) load_x(rb0 + kK3Rows, u);
+    }
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      h8 ah, al;
-      split8(rx[t][u][0] * scale, rx[t][u][1] * scale, ah, al);
-      acc[t][0] = mma3(ah, al, bh0, bl0, acc[t][0]);
-      acc[t][1] = mma3(ah, al, bh1, bl1, acc[t][1]);
+      acc[t][0] += as[t][0] * unscale;
+      acc[t][1] += as[t][1] * unscale;
     }
-  }
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    acc[t][0] *= unscale;
-    acc[t][1] *= unscale;
   }
   const bool nok0 = n0 + m < jb.N, nok1 = n0 + 16 + m < jb.N;
   HBK_MT(2, 2);
@@ -2132,7 +2155,7 @@ int k1_splits(int B) {  // (one round of three per CU on a 64-CU stream, KS 8, m
 int k3_rows(const void* stream) {
   static const bool k3_wide = getenv("HBK_K3_WIDE") != nullptr;
   const bool narrow = !k3_wide && persistent_blocks(1, stream) <= kK3NarrowCUs;
-  return 32 * (narrow ? kK3StepsNarrow : kK3Steps);
+  return 32 * (narrow ? kK3StepsNarrow * kK3GroupNarrow : kK3Steps);
 }
 FusedWs fused_layout(int64_t B, int NG, int64_t n_params = 0) {
   FusedWs w;
@@ -2344,7 +2367,7 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
   // HBK_K3_WIDE=1: the 288-row splits on narrow streams too (4 instead of 9
   // splits at B = 1100: fewer partial slabs, more time on a small partition)
   const int rows3 = k3_rows(s);
-  const bool narrow = rows3 == 32 * kK3StepsNarrow;
+  const bool narrow = rows3 == 32 * kK3StepsNarrow * kK3GroupNarrow;
   const int KS3 = static_cast<int>((Bp + rows3 - 1) / rows3);
   auto add = [&](const float* X, const float* Y, int64_t c_off, int ldc, int M, int N) {
     WJob& j = k3.job[nj];
@@ -2376,9 +2399,9 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
   k3.part = ws + w.part;
   k3.pstride = w.pstride;
   if (narrow)
-    hipLaunchKernelGGL(k3_wgrad_kernel<kK3StepsNarrow>, dim3(blocks), dim3(256), 0, s, k3);
+    hipLaunchKernelGGL((k3_wgrad_kernel<kK3StepsNarrow, kK3GroupNarrow>), dim3(blocks), dim3(256), 0, s, k3);
   else
-    hipLaunchKernelGGL(k3_wgrad_kernel<kK3Steps>, dim3(blocks), dim3(256), 0, s, k3);
+    hipLaunchKernelGGL((k3_wgrad_kernel<kK3Steps, 1>), dim3(blocks), dim3(256), 0, s, k3);
   HBK_LAUNCH_CHECK("k3_wgrad_kernel");
   if (flags & HBK_STEP_DEFER_PARTIALS) {  // the update adds the slabs
     p.deferred_ws = ws;
