@@ -129,11 +129,11 @@ __device__ __forceinline__ void lds_barrier() {
 #ifdef HBK_TRACE
 // Tracing build only (lib/libhbk_trace.so, tools/probe_mlp.py): lane 0 of every
 // wave of block 0 records (mark << 56 | s_memtime) at stage marks of k1 / k2 / k3.
-__device__ unsigned long long g_mlp_trace[4][4][128];
-__device__ int g_mlp_trace_n[4][4];
-#define HBK_MT(kern, id)                                                                       \
+__device__ unsigned long long g_mlp_trace[6][4][128];
+__device__ int g_mlp_trace_n[6][4];
+#define HBK_MTB(kern, id, blk)                                                                       \
   do {                                                                                         \
-    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) {                                          \
+    if (blockIdx.x == (blk) && (threadIdx.x & 63) == 0) {                                          \
       const int w_ = threadIdx.x >> 6;                                                          \
       const int n_ = g_mlp_trace_n[kern][w_];                                                   \
       if (n_ < 128) {                                                                           \
@@ -143,9 +143,13 @@ __device__ int g_mlp_trace_n[4][4];
       }                                                                                         \
     }                                                                                           \
   } while (0)
+#define HBK_MT(kern, id) HBK_MTB(kern, id, 0)
 #else
 #define HBK_MT(kern, id) \
   do {                   \
+  } while (0)
+#define HBK_MTB(kern, id, blk) \
+  do {                         \
   } while (0)
 #endif
 
@@ -2555,10 +2559,10 @@ int mlp_eval_finish(const float* cv, const float* ct, const double* sizes, float
 
 #ifdef HBK_TRACE
 extern "C" int hbk_debug_mlp_trace(unsigned long long* out, int* counts) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hbk::g_mlp_trace), sizeof(unsigned long long) * 4 * 4 * 128) != hipSuccess)
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hbk::g_mlp_trace), sizeof(unsigned long long) * 6 * 4 * 128) != hipSuccess)
     return -2;
-  if (hipMemcpyFromSymbol(counts, HIP_SYMBOL(hbk::g_mlp_trace_n), sizeof(int) * 16) != hipSuccess) return -2;
-  int z[16] = {};
+  if (hipMemcpyFromSymbol(counts, HIP_SYMBOL(hbk::g_mlp_trace_n), sizeof(int) * 24) != hipSuccess) return -2;
+  int z[24] = {};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(hbk::g_mlp_trace_n), z, sizeof(z));
   return 0;
 }

@@ -78,8 +78,8 @@ def trace():
     tr, pos, neg, idx, y, sched = setup(4)
     fn = lib().hbk_debug_mlp_trace
     fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-    buf = (ctypes.c_ulonglong * (4 * 4 * 128))()
-    cnt = (ctypes.c_int * 16)()
+    buf = (ctypes.c_ulonglong * (6 * 4 * 128))()
+    cnt = (ctypes.c_int * 24)()
     tr._reset_accumulation()
     tr.train_indexed(idx[:2], y, sched, pool32=pos, pool16=neg, graphs=False)
     torch.cuda.synchronize()
@@ -87,7 +87,8 @@ def trace():
     tr.train_indexed(idx[2:3], y, sched, pool32=pos, pool16=neg, graphs=False)
     torch.cuda.synchronize()
     fn(buf, cnt)
-    for k, name in enumerate(("k1a (standalone only)", "k2_rows", "k3_wgrad", "k1b_gemm")):
+    for k, name in enumerate(("k1a (standalone only)", "k2_rows", "k3_wgrad", "k1b_gemm", "k4 tile block 0",
+                              "k4 first non-tile block")):
         evs = []
         for w in range(4):
             n = cnt[k * 4 + w]
