@@ -1693,28 +1693,32 @@ __device__ __forceinline__ uint4 load_rows4(const uint4* p) {
 constexpr int kKvPiece = 8;  // 16-B pieces per 64-deep row of a chunk
 __device__ __forceinline__ int kv_swz(int n) { return (n >> 1) & 7; }
 constexpr int kNetWLd = 104, kAld = 100;  // LDS row strides: weight halves (K <= 96), activation floats
-template <bool kF16, int NG>
-__global__ void __launch_bounds__(512) kv_gemm_kernel(KvArgs a) {
+// W: waves per workgroup, 8 (f16 rows: two 16-row tiles per wave) or 16 (one tile per wave:
+// twice the waves per CU to hide the stream's latency, at most 128 VGPRs each)
+template <bool kF16, int NG, int W>
+__global__ void __launch_bounds__(64 * W) kv_gemm_kernel(KvArgs a) {
   // ONE __shared__ object: beside a second one hipcc drains the DMA (vmcnt(0))
   // before every chunk's first LDS read. GEMM phase: the W' ring (the row
   // statistics reuse buffer 0 after it); network phase: a stage's weight planes
   // at 0, the waves' activation tiles after them, two counters last.
   constexpr int kWBuf = 3;  // W' ring: chunk c + 2's DMA is issued during chunk c (kWBuf - 1 == 2 assumed below)
-  constexpr int kRT = kF16 ? 2 : 1; // 16-row tiles per wave (f32 rows: one, for the registers of the split)
+  constexpr int kRT = (kF16 && W == 8) ? 2 : 1;  // 16-row tiles per wave (f32 rows: one, for the split's registers)
+  constexpr int kThr = 64 * W;
   constexpr int kGemmBytes = kWBuf * 2 * kH2 * kKvKC * 2;
   constexpr int kWsBytes = 2 * kH2 * kNetWLd * 2;
-  constexpr int kActBytes = 8 * 16 * kRT * kAld * 4;
+  constexpr int kActBytes = W * 16 * kRT * kAld * 4;
   constexpr int kLdsBytes = (kGemmBytes > kWsBytes + kActBytes ? kGemmBytes : kWsBytes + kActBytes) + 16;
   static_assert(kLdsBytes <= 160 * 1024, "one workgroup's LDS");
   __shared__ __attribute__((aligned(16))) unsigned char smem[kLdsBytes];
   auto wb = reinterpret_cast<_Float16 (*)[2][kH2][kKvKC]>(smem);  // [buf][hi / lo][n][k] (swizzled pieces)
-  float (*stS)[32][2] = reinterpret_cast<float (*)[32][2]>(smem);
-  static_assert(sizeof(float) * 8 * 32 * 2 <= kWsBytes, "statistics: below the activation tiles");
+  float (*stS)[16 * kRT][2] = reinterpret_cast<float (*)[16 * kRT][2]>(smem);
+  static_assert(sizeof(float) * W * 16 * kRT * 2 <= kWsBytes, "statistics: below the activation tiles");
   constexpr int kDepth = 2;         // A chunks in flight (this one + 1 ahead)
   constexpr int kU = kF16 ? 1 : 2;  // 16-B loads per 8 elements
   constexpr int kALoads = kRT * 2 * kU;  // per chunk
-  constexpr int kTile = 8 * 16 * kRT;
-  static_assert(kALoads + 4 < 16, "the counted waits use vmcnt's low field");
+  constexpr int kTile = W * 16 * kRT;
+  constexpr int kDma = 32 / W;  // W' DMA instructions per wave and chunk (2 planes x 128 rows of 128 B)
+  static_assert(kALoads + kDma < 16, "the counted waits use vmcnt's low field");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = lane & 15, kq = lane >> 4;
   const int64_t tile0 = int64_t(blockIdx.x) * kTile;
   const char* rp[kRT];
@@ -1748,8 +1752,8 @@ __global__ void __launch_bounds__(512) kv_gemm_kernel(KvArgs a) {
   // (row 8 (4 wave + j) + l / 8, slot l % 8), reading the source piece slot ^ swz(row)
   auto dma_w = [&](int c, int buf) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int row8 = 4 * wave + j;                 // 0 .. 31: plane row8 / 16, rows 8 (row8 % 16) ..
+    for (int j = 0; j < kDma; ++j) {
+      const int row8 = kDma * wave + j;              // 0 .. 31: plane row8 / 16, rows 8 (row8 % 16) ..
       const int pl = row8 >> 4, n = 8 * (row8 & 15) + (lane >> 3), pc = (lane & 7) ^ kv_swz(n);
       const _Float16* src = a.wq + int64_t(pl) * kH2 * kD + int64_t(n) * kD + kKvKC * c + kKvPiece * pc;
       __builtin_amdgcn_global_load_lds(src, &wb[buf][pl][8 * (row8 & 15)][0], 16, 0, 0);
@@ -1761,7 +1765,7 @@ __global__ void __launch_bounds__(512) kv_gemm_kernel(KvArgs a) {
   load_rows(0, 0);
   dma_w(1, 1);
   load_rows(1, 1);
-  __builtin_amdgcn_s_waitcnt((kALoads + 4) | (0x7 << 4) | (0xF << 8));  // vmcnt(4 + kALoads): chunk 0 in
+  __builtin_amdgcn_s_waitcnt((kALoads + kDma) | (0x7 << 4) | (0xF << 8));  // vmcnt(4 + kALoads): chunk 0 in
   dma_barrier();
   f4 acc[kRT][8];
 #pragma unroll
@@ -1847,7 +1851,7 @@ __global__ void __launch_bounds__(512) kv_gemm_kernel(KvArgs a) {
     // The sched_barriers keep the next chunk's conversions below the counted wait: hoisted
     // above it, hipcc guards them with vmcnt(0) (DMA and row loads pending together)
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_waitcnt((kALoads + 4) | (0x7 << 4) | (0xF << 8));  // vmcnt(4 + kALoads)
+    __builtin_amdgcn_s_waitcnt((kALoads + kDma) | (0x7 << 4) | (0xF << 8));  // vmcnt(4 + kALoads)
     __builtin_amdgcn_s_waitcnt((0x3F & 0xF) | ((0x3F >> 4) << 14) | (0x7 << 4) | (0x0 << 8));  // lgkmcnt(0)
     dma_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -1918,9 +1922,10 @@ __global__ void __launch_bounds__(512) kv_gemm_kernel(KvArgs a) {
   // (six named registers, not an array: an array here stays in scratch memory
   // beside the GEMM phase's register pressure)
   uint4 wr0, wr1, wr2, wr3, wr4, wr5;
+  constexpr int kWr = 3072 / kThr;  // staged 16-B pieces per thread (W_hg: 2 planes x 1,536)
   auto piece = [&](int st, int j, int& pl, int& n, int& k) {
     const int N = st_n(st), K = st_k(st), pieces = N * K / 8;  // per plane
-    const int q = min(tid + 512 * j, 2 * pieces - 1), e0 = q % pieces;
+    const int q = min(tid + kThr * j, 2 * pieces - 1), e0 = q % pieces;
     pl = q / pieces;
     n = (8 * e0) / K;
     k = 8 * e0 - n * K;
@@ -1939,17 +1944,21 @@ __global__ void __launch_bounds__(512) kv_gemm_kernel(KvArgs a) {
     load1(st, 0, wr0);
     load1(st, 1, wr1);
     load1(st, 2, wr2);
-    load1(st, 3, wr3);
-    load1(st, 4, wr4);
-    load1(st, 5, wr5);
+    if constexpr (kWr > 3) {
+      load1(st, 3, wr3);
+      load1(st, 4, wr4);
+      load1(st, 5, wr5);
+    }
   };
   auto store_w = [&](int st) {
     store1(st, 0, wr0);
     store1(st, 1, wr1);
     store1(st, 2, wr2);
-    store1(st, 3, wr3);
-    store1(st, 4, wr4);
-    store1(st, 5, wr5);
+    if constexpr (kWr > 3) {
+      store1(st, 3, wr3);
+      store1(st, 4, wr4);
+      store1(st, 5, wr5);
+    }
   };
   load_w(0);
   store_w(0);
@@ -2518,17 +2527,25 @@ int mlp_eval_count(const hbk_mlp_plan& p, const float* params, const void* pool,
   ka.counts = counts;
   ka.label = label;
   ka.prob = prob;
-  const int tile = f16 ? 256 : 128;  // kv_gemm_kernel's rows per workgroup
+  // f16 rows: 16 waves of one 16-row tile each (126 VGPRs); f32 rows (the split's registers
+  // spill at 128): 8 waves. HBK_KV_WAVES=8: 8 waves of two tiles for f16 rows too (A/B)
+  static const bool w8 = getenv("HBK_KV_WAVES") && atoi(getenv("HBK_KV_WAVES")) == 8;
+  const int waves = f16 && !w8 ? 16 : 8;
+  const int tile = (f16 ? 256 : 128);  // kv_gemm_kernel's rows per workgroup
   const dim3 grid(unsigned((rows + tile - 1) / tile));
-  auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(512), 0, s, ka); };
-  if (f16) {
-    if (NG == 2) launch(kv_gemm_kernel<true, 2>);
-    else if (NG == 3) launch(kv_gemm_kernel<true, 3>);
-    else launch(kv_gemm_kernel<true, 4>);
+  auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(64 * waves), 0, s, ka); };
+  if (waves == 16) {
+    if (NG == 2) launch(kv_gemm_kernel<true, 2, 16>);
+    else if (NG == 3) launch(kv_gemm_kernel<true, 3, 16>);
+    else launch(kv_gemm_kernel<true, 4, 16>);
+  } else if (f16) {
+    if (NG == 2) launch(kv_gemm_kernel<true, 2, 8>);
+    else if (NG == 3) launch(kv_gemm_kernel<true, 3, 8>);
+    else launch(kv_gemm_kernel<true, 4, 8>);
   } else {
-    if (NG == 2) launch(kv_gemm_kernel<false, 2>);
-    else if (NG == 3) launch(kv_gemm_kernel<false, 3>);
-    else launch(kv_gemm_kernel<false, 4>);
+    if (NG == 2) launch(kv_gemm_kernel<false, 2, 8>);
+    else if (NG == 3) launch(kv_gemm_kernel<false, 3, 8>);
+    else launch(kv_gemm_kernel<false, 4, 8>);
   }
   HBK_LAUNCH_CHECK("kv_gemm_kernel");
   return HBK_OK;
