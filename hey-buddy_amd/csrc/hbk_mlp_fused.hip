@@ -668,6 +668,9 @@ struct K2Args {
   } while (0)
 #endif
 
+#ifndef HBK_K2_ABLATE
+#define HBK_K2_ABLATE 0  // profiling builds (wrong results): 1 loads each matrix's fragments once, 2 sums one slab group
+#endif
 // NG (= n_layers + 2 gated MLPs) is a template argument: every stage below is
 // straight-line code, so the register prefetches and their waits are exact.
 template <bool kTrain, int NG>
@@ -757,7 +760,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
       float lh[12][4], lg[12][4];
 #pragma unroll
       for (int u = 0; u < 12; ++u) {
-        const int sl = min(s0 + u, a.KS - 1);
+        const int sl = (HBK_K2_ABLATE & 2) ? 0 : min(s0 + u, a.KS - 1);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int e = tid + 256 * q, r = min(e >> 6, nrow - 1), j = e & 63;
@@ -811,7 +814,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
 #pragma unroll
   for (int k = 0; k + 1 < NG; ++k) {
     // S_k = U_k W_o_k^T + b_o_k  -> bS   (weights in wa; prefetch HG_{k+1}'s into wb)
-    load_wf<kL, kH2, 2>(wb, a.wc + a.c_hg[k + 1], wave, lane);
+    if (!(HBK_K2_ABLATE & 1) || k == 0) load_wf<kL, kH2, 2>(wb, a.wc + a.c_hg[k + 1], wave, lane);
     {
       f4 c0, c1;
       gemm2<kH>(wa, load_a<kH>(&bU[0][0], lane), c0, c1);
@@ -830,7 +833,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
     // lane -> row 4w + lane / 16, columns 6 (lane % 16) ..), both reductions of
     // the four rows in parallel within 16-lane DPP rows (rsum16: no cross-row
     // steps); Xn^T goes to HBM from LDS in the next stage
-    if (k + 2 < NG) load_wf<kH, kL, 2>(wa, a.wc + a.c_o[k + 1], wave, lane);
+    if (!(HBK_K2_ABLATE & 1) && k + 2 < NG) load_wf<kH, kL, 2>(wa, a.wc + a.c_o[k + 1], wave, lane);
     {
       const int r = wave * 4 + (lane >> 4), c0 = 6 * (lane & 15);
       float v[6];
@@ -996,7 +999,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
     {
       f4 c0, c1;
       gemm2<kH2>(fx, load_a<kH2>(&bX[0][0], lane), c0, c1);
-      if (k - 1 >= 1) load_wf<kH2, kL, 2>(fx, a.wc + a.c_hgT[k - 1], wave, lane);
+      if (!(HBK_K2_ABLATE & 1) && k - 1 >= 1) load_wf<kH2, kL, 2>(fx, a.wc + a.c_hgT[k - 1], wave, lane);
       const int n0 = 16 * wave + m, n1 = 16 * (wave + 4) + m;
 #pragma unroll
       for (int e = 0; e < 4; ++e) bU[4 * kq + e][n0] = c0[e];
@@ -1049,7 +1052,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
         atomicAdd(G + a.b_o[kk] + tid, s);
       }
       const f4 du = gemm1<kL>(fy, load_a<kL>(&bS[0][0], lane));
-      if (k - 2 >= 0) load_wf<kL, kH, 1>(fy, a.wc + a.c_oT[k - 2], wave, lane);
+      if (!(HBK_K2_ABLATE & 1) && k - 2 >= 0) load_wf<kL, kH, 1>(fy, a.wc + a.c_oT[k - 2], wave, lane);
       const int j = 16 * wave + m;
       f4 dho, dgo;
 #pragma unroll
