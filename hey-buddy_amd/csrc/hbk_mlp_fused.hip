@@ -104,6 +104,13 @@ __device__ __forceinline__ float wmax(float v) {
                      __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 48))));
 }
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+// The evaluation kernel's network phase: the hardware exp2 and reciprocal (1 ulp
+// each) instead of expf's range reduction and the IEEE division sequence
+// (~20 VALU instructions per sigmoid); predictions move by ~1e-7 (the tests'
+// tolerance is 2e-5, and their counts allow predictions that near the threshold)
+__device__ __forceinline__ float sigm_fast(float x) {
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x));
+}
 
 // Barrier of a loop with global->LDS DMA in flight (its waits counted by hand
 // before it): a fenced barrier would wait vmcnt(0), as the DMA writes LDS. The
@@ -1910,7 +1917,7 @@ __global__ void __launch_bounds__(64 * W) kv_gemm_kernel(KvArgs a) {
         for (int e = 0; e < 4; ++e) {
           const float h = rs[rt][e] * (acc[rt][ct][e] * ks - mu[rt][e] * c1h) + c0h;
           const float g = rs[rt][e] * (acc[rt][ct + 4][e] * ks - mu[rt][e] * c1g) + c0g;
-          A[(16 * rt + 4 * kq + e) * kAld + j] = h * sigm(h) * g;
+          A[(16 * rt + 4 * kq + e) * kAld + j] = h * sigm_fast(h) * g;
         }
     }
   }
@@ -2014,7 +2021,7 @@ __global__ void __launch_bounds__(64 * W) kv_gemm_kernel(KvArgs a) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) sq[e] += (c[rt][ct][e] - mu[e]) * (c[rt][ct][e] - mu[e]);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) sq[e] = 1.f / sqrtf(rsum16(sq[e]) * (1.f / kL) + kLnEps);
+        for (int e = 0; e < 4; ++e) sq[e] = __builtin_amdgcn_rsqf(rsum16(sq[e]) * (1.f / kL) + kLnEps);
 #pragma unroll
         for (int ct = 0; ct < 6; ++ct)
 #pragma unroll
@@ -2049,7 +2056,7 @@ __global__ void __launch_bounds__(64 * W) kv_gemm_kernel(KvArgs a) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const float h = c[rt][ct][e] * af[rt].inv + bh, g = c[rt][ct + 4][e] * af[rt].inv + bg;
-            A[(16 * rt + 4 * kq + e) * kAld + col] = h * sigm(h) * g;
+            A[(16 * rt + 4 * kq + e) * kAld + col] = h * sigm_fast(h) * g;
           }
       }
     }
@@ -2080,7 +2087,7 @@ __global__ void __launch_bounds__(64 * W) kv_gemm_kernel(KvArgs a) {
       z += bz;
       const int64_t row = tile0 + 16 * kRT * wave + 16 * rt + r;
       const bool live = row < a.rows && (lane & 3) == 0;
-      const float p = sigm(z);
+      const float p = sigm_fast(z);
       if (live && a.prob) a.prob[row] = p;
       ge += __popcll(__ballot(live && p >= a.act_thr));
       gt += __popcll(__ballot(live && p > a.act_thr));
