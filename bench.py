@@ -785,12 +785,14 @@ def setup_e2e(args, dev, rank, world, seed):
         # train ~93 ms on 64 at split:64), so the embedding's last chains of chunk c + 1
         # run on the train stream after train(c): its front half writes mid[b] on the
         # feature stream, its back half reads it on the train stream
-        K = args.embed_split if 0 < args.embed_split < eplan.n_chains else 0
+        # (K = n_chains: only the --embed-split-frac clips are split, after K - 1 chains)
+        K = args.embed_split if 0 < args.embed_split <= eplan.n_chains else 0
+        whole = K == eplan.n_chains  # the rest of the clips: the whole embedding on the featurize stream
         # --embed-split-frac f: clips [0, a1) split after K - 1 chains, the rest after K
         a1 = int(round(n * args.embed_split_frac)) if K > 1 else 0
         a1 = min(max(a1, 0), n)
         mids = [torch.empty((n - a1, eplan.mid_floats(K)), dtype=torch.float32, device=dev)
-                for _ in range(2)] if K else []
+                for _ in range(2)] if K and not whole else []
         mids1 = [torch.empty((a1, eplan.mid_floats(K - 1)), dtype=torch.float32, device=dev)
                  for _ in range(2)] if a1 else []
         front_done = [torch.cuda.Event(), torch.cuda.Event()]
@@ -805,7 +807,9 @@ def setup_e2e(args, dev, rank, world, seed):
                 if K:
                     if a1:
                         eplan.clips_front(frames[:a1], K - 1, mids1[b])
-                    if a1 < n:
+                    if a1 < n and whole:
+                        embed_clips(frames[a1:], eplan, out=raw[a1:])
+                    elif a1 < n:
                         eplan.clips_front(frames[a1:], K, mids[b])
                     front_done[b].record(fs)
                 else:
@@ -822,7 +826,7 @@ def setup_e2e(args, dev, rank, world, seed):
                 ts.wait_event(front_done[b])
                 if a1:
                     eplan.clips_back(mids1[b], a1, K - 1, raw[:a1])
-                if a1 < n:
+                if a1 < n and not whole:
                     eplan.clips_back(mids[b], n - a1, K, raw[a1:])
                 replace_nan_rows_device(raw_ext, out=pools[b], zero_row=True)
                 feat_done[b].record(ts)
@@ -1080,9 +1084,12 @@ def setup_e2e(args, dev, rank, world, seed):
                                 f"pipelined (heybuddy.pipeline {args.overlap}): featurize(s + 1) on one stream while "
                                 f"train(s) runs on another"
                                 + (f", then the embedding's chains >= {args.embed_split} of chunk s + 1 on the train "
-                                   "stream (hbk_embed_clips_back)" if args.embed_split > 0 else "")
+                                   "stream (hbk_embed_clips_back)" if 0 < args.embed_split < eplan.n_chains else "")
                                 + (f" (chains >= {args.embed_split - 1} for {args.embed_split_frac:.0%} of the clips)"
-                                   if args.embed_split > 1 and args.embed_split_frac > 0 else "")
+                                   if 1 < args.embed_split < eplan.n_chains and args.embed_split_frac > 0 else "")
+                                + (f", then the embedding's chains >= {args.embed_split - 1} of {args.embed_split_frac:.0%}"
+                                   " of chunk s + 1's clips on the train stream (hbk_embed_clips_back)"
+                                   if args.embed_split == eplan.n_chains and args.embed_split_frac > 0 else "")
                                 + f"; per-stage ms from {args.stage_steps} sequential steps")},
     }
 

@@ -2221,6 +2221,237 @@ p2s_chain_kernel(P2sArgs a) {
   raise_range(a.range_flag, amax);
 }
 
+// ------------------------------------------------------------------ t3s ----
+// Streaming form of SE20's tail (chain 3 over the phase images of the tail
+// deduplication): the input pool 2x1 over p2s's 27 x 1 x 48 rows, then
+// 3x1 (48 -> 64), 1x1, 3x1, 1x1 (64), 2x1 (64 -> 96), four 1x1 (96; the last
+// without activation): 8 x 1 x 96 per phase image. The rows are one position
+// wide, so a tile packs IMAGES: 16 positions = 8 clips x 2 phase images
+// (position p = image img0 + p, image = 2 clip + phase). The weights are the A
+// operand in VGPRs (hi / lo f16), the activations the B operand from LDS rings
+// (hi / lo planes [position][channel]); the bias starts the accumulator. Waves
+// 0-3 run the four 64-channel stages for output block mb = wave, waves 4-9 the
+// five 96-channel stages for mb = wave - 4. Tick y (one barrier after it):
+// pooled row y is staged (waves 0-2, loaded a tick ahead), stage s computes its
+// row y - kT3Delay[s] (each stage reads only rows written in earlier ticks).
+constexpr int kT3Waves = 10, kT3Threads = 64 * kT3Waves, kT3Pos = 16;
+constexpr int kT3Hin = 27, kT3C0 = 48, kT3Hp = 13, kT3C1 = 64, kT3C2 = 96, kT3Hout = 8;
+constexpr int kT3Ticks = 22;
+constexpr int kT3CS0 = 56, kT3CS1 = 72, kT3CS2 = 104;  // f16 per position (odd 16-B groups)
+// ring slots (rows) and LDS offsets (f16): P (pooled, 4), A1 (2), A2 (4), A3 (2), A4 (4), A5..A8 (2 each)
+constexpr int kT3PlP = kT3Pos * kT3CS0, kT3Pl1 = kT3Pos * kT3CS1, kT3Pl2 = kT3Pos * kT3CS2;
+constexpr int kT3P = 0, kT3A1 = kT3P + 4 * 2 * kT3PlP, kT3A2 = kT3A1 + 2 * 2 * kT3Pl1,
+              kT3A3 = kT3A2 + 4 * 2 * kT3Pl1, kT3A4 = kT3A3 + 2 * 2 * kT3Pl1, kT3A5 = kT3A4 + 4 * 2 * kT3Pl1;
+constexpr int kT3Zero = kT3A5 + 4 * 2 * 2 * kT3Pl2;  // 16 zero halfs (stage 1's K padding)
+constexpr int kT3Halfs = kT3Zero + 16;
+constexpr int kT3BiasOff = kT3Halfs * 2;            // bytes: biases [4][64] then [5][96] f32
+constexpr int kT3Lds = kT3BiasOff + (4 * kT3C1 + 5 * kT3C2) * 4;
+// weights (f16, hi plane then lo plane per stage, [cout][K], K = tap * cin + ci)
+constexpr int kT3K[9] = {160, 64, 192, 64, 128, 96, 96, 96, 96};  // stage 1: 144 + 16 zero
+constexpr int kT3W[9] = {0,
+                         2 * 64 * 160,
+                         2 * 64 * (160 + 64),
+                         2 * 64 * (160 + 64 + 192),
+                         2 * 64 * (160 + 64 + 192 + 64),
+                         2 * 64 * 480 + 2 * 96 * 128,
+                         2 * 64 * 480 + 2 * 96 * (128 + 96),
+                         2 * 64 * 480 + 2 * 96 * (128 + 192),
+                         2 * 64 * 480 + 2 * 96 * (128 + 288)};
+constexpr int kT3WHalfs = 2 * 64 * 480 + 2 * 96 * 512;
+
+struct T3sArgs {
+  const float* in;      // [clip][27][48] f32 (p2s output)
+  float* out;           // [image][8][96] f32, image = 2 clip + phase
+  const _Float16* w;    // kT3WHalfs
+  const float* bias;    // [4][64] + [5][96]
+  int64_t n_img, src_clip_stride, out_img_stride;
+  float alpha;
+  int* range_flag;
+};
+
+// one output block (16 channels) of one row: KS K-steps of 32, B from the
+// ring rows `rows` (tap t -> rows[t]), channel group 8 cg of tap g / (CIN / 8)
+template <int KS, int CIN, int CS, int PL>
+__device__ __forceinline__ f4 t3_block(const h8 (&wh)[KS], const h8 (&wl)[KS], f4 acc, const _Float16* sm,
+                                       const int (&rowoff)[3], int pos, int kq, const _Float16* zero) {
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const int g = 4 * ks + kq, tap = g / (CIN / 8), cg = g - tap * (CIN / 8);
+    const bool pad = tap >= 3;  // stage 1's K padding (groups 18, 19)
+    const _Float16* src = pad ? zero : sm + rowoff[tap < 3 ? tap : 0] + pos * CS + 8 * cg;
+    const h8 bh = *reinterpret_cast<const h8*>(src), bl = *reinterpret_cast<const h8*>(pad ? zero : src + PL);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[ks], bh, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[ks], bl, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[ks], bh, acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+// activation, split and ring store of one block's tile (channels 16 mb + 4 kq + j of position pos)
+template <bool ACT, int CS, int PL>
+__device__ __forceinline__ void t3_store(f4 acc, _Float16* oh, int pos, int mb, int kq, float alpha, float& amax) {
+  float v[4] = {acc[0], acc[1], acc[2], acc[3]};
+  p0s_act2<ACT>(v[0], v[1], alpha);
+  p0s_act2<ACT>(v[2], v[3], alpha);
+  uint32_t h01, l01, h23, l23;
+  split2_mix(v[0], v[1], h01, l01, amax);
+  split2_mix(v[2], v[3], h23, l23, amax);
+  const int o = pos * CS + 16 * mb + 4 * kq;
+  *reinterpret_cast<uint2*>(oh + o) = uint2{h01, h23};
+  *reinterpret_cast<uint2*>(oh + PL + o) = uint2{l01, l23};
+}
+
+template <int KS, int K>
+__device__ __forceinline__ void t3_load_w(h8 (&wh)[KS], h8 (&wl)[KS], const _Float16* w, int cout, int n, int kq) {
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    wh[ks] = *reinterpret_cast<const h8*>(w + n * K + 32 * ks + 8 * kq);
+    wl[ks] = *reinterpret_cast<const h8*>(w + cout * K + n * K + 32 * ks + 8 * kq);
+  }
+}
+
+__device__ __forceinline__ f4 t3_bias(const float* b) {
+  const float4 v = *reinterpret_cast<const float4*>(b);
+  return f4{v.x, v.y, v.z, v.w};
+}
+
+template <bool LEAKY>
+__global__ void __launch_bounds__(kT3Threads) __attribute__((amdgpu_waves_per_eu(3)))
+t3s_chain_kernel(T3sArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char t3smem[];
+  _Float16* sm = reinterpret_cast<_Float16*>(t3smem);
+  float* sb = reinterpret_cast<float*>(t3smem + kT3BiasOff);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int pos = lane & 15, kq = lane >> 4;
+  for (int i = tid; i < 16; i += kT3Threads) sm[kT3Zero + i] = static_cast<_Float16>(0.f);
+  for (int i = tid; i < 4 * kT3C1 + 5 * kT3C2; i += kT3Threads) sb[i] = a.bias[i];
+  const _Float16* zero = sm + kT3Zero;
+  const int64_t n_groups = (a.n_img + kT3Pos - 1) / kT3Pos;
+  const float alpha = a.alpha;
+  float amax = 0.f;
+  // staging: threads 0..191 take 4 channels (c4) of position sp
+  const int sp = tid / 12, c4 = tid - 12 * sp;
+  const bool stager = tid < kT3Pos * 12;
+  float4 r0 = {0.f, 0.f, 0.f, 0.f}, r1 = r0;
+  auto load_row = [&](int64_t img0, int y) {  // pooled row y's two source rows, this thread's share
+    const int64_t img = min(img0 + sp, a.n_img - 1);
+    const int64_t clip = img >> 1;
+    const int row = static_cast<int>(img & 1) + 2 * min(y, kT3Hp - 1);
+    const float* src = a.in + clip * a.src_clip_stride + row * kT3C0 + 4 * c4;
+    r0 = *reinterpret_cast<const float4*>(src);
+    r1 = *reinterpret_cast<const float4*>(src + kT3C0);
+  };
+  auto stage_row = [&](int y) {
+    const float4 v = {nan_max(r0.x, r1.x), nan_max(r0.y, r1.y), nan_max(r0.z, r1.z), nan_max(r0.w, r1.w)};
+    uint32_t h01, l01, h23, l23;
+    split2_mix(v.x, v.y, h01, l01, amax);
+    split2_mix(v.z, v.w, h23, l23, amax);
+    _Float16* d = sm + kT3P + (y & 3) * 2 * kT3PlP + sp * kT3CS0 + 4 * c4;
+    *reinterpret_cast<uint2*>(d) = uint2{h01, h23};
+    *reinterpret_cast<uint2*>(d + kT3PlP) = uint2{l01, l23};
+  };
+  __syncthreads();
+
+  if (wave < 4) {  // ---------------- the 64-channel stages, block mb = wave
+    const int mb = wave, n = 16 * mb + pos;
+    h8 w1h[5], w1l[5], w2h[2], w2l[2], w3h[6], w3l[6], w4h[2], w4l[2];
+    t3_load_w<5, 160>(w1h, w1l, a.w + kT3W[0], kT3C1, n, kq);
+    t3_load_w<2, 64>(w2h, w2l, a.w + kT3W[1], kT3C1, n, kq);
+    t3_load_w<6, 192>(w3h, w3l, a.w + kT3W[2], kT3C1, n, kq);
+    t3_load_w<2, 64>(w4h, w4l, a.w + kT3W[3], kT3C1, n, kq);
+    const int bo = 16 * mb + 4 * kq;
+    for (int64_t gi = blockIdx.x; gi < n_groups; gi += gridDim.x) {
+      const int64_t img0 = gi * kT3Pos;
+      if (stager) load_row(img0, 0);
+      for (int y = 0; y < kT3Ticks; ++y) {
+        if (stager && y < kT3Hp) {
+          stage_row(y);
+          load_row(img0, y + 1);
+        }
+        if (y >= 3 && y < 3 + 11) {  // stage 1: row r from pooled rows r .. r + 2
+          const int r = y - 3;
+          const int ro[3] = {kT3P + (r & 3) * 2 * kT3PlP, kT3P + ((r + 1) & 3) * 2 * kT3PlP,
+                             kT3P + ((r + 2) & 3) * 2 * kT3PlP};
+          const f4 acc = t3_block<5, kT3C0, kT3CS0, kT3PlP>(w1h, w1l, t3_bias(sb + bo), sm, ro, pos, kq, zero);
+          t3_store<LEAKY, kT3CS1, kT3Pl1>(acc, sm + kT3A1 + (r & 1) * 2 * kT3Pl1, pos, mb, kq, alpha, amax);
+        }
+        if (y >= 4 && y < 4 + 11) {  // stage 2 (1x1)
+          const int r = y - 4;
+          const int ro[3] = {kT3A1 + (r & 1) * 2 * kT3Pl1, 0, 0};
+          const f4 acc = t3_block<2, kT3C1, kT3CS1, kT3Pl1>(w2h, w2l, t3_bias(sb + kT3C1 + bo), sm, ro, pos, kq, zero);
+          t3_store<LEAKY, kT3CS1, kT3Pl1>(acc, sm + kT3A2 + (r & 3) * 2 * kT3Pl1, pos, mb, kq, alpha, amax);
+        }
+        if (y >= 7 && y < 7 + 9) {  // stage 3 (3x1)
+          const int r = y - 7;
+          const int ro[3] = {kT3A2 + (r & 3) * 2 * kT3Pl1, kT3A2 + ((r + 1) & 3) * 2 * kT3Pl1,
+                             kT3A2 + ((r + 2) & 3) * 2 * kT3Pl1};
+          const f4 acc = t3_block<6, kT3C1, kT3CS1, kT3Pl1>(w3h, w3l, t3_bias(sb + 2 * kT3C1 + bo), sm, ro, pos, kq,
+                                                           zero);
+          t3_store<LEAKY, kT3CS1, kT3Pl1>(acc, sm + kT3A3 + (r & 1) * 2 * kT3Pl1, pos, mb, kq, alpha, amax);
+        }
+        if (y >= 8 && y < 8 + 9) {  // stage 4 (1x1)
+          const int r = y - 8;
+          const int ro[3] = {kT3A3 + (r & 1) * 2 * kT3Pl1, 0, 0};
+          const f4 acc = t3_block<2, kT3C1, kT3CS1, kT3Pl1>(w4h, w4l, t3_bias(sb + 3 * kT3C1 + bo), sm, ro, pos, kq,
+                                                           zero);
+          t3_store<LEAKY, kT3CS1, kT3Pl1>(acc, sm + kT3A4 + (r & 3) * 2 * kT3Pl1, pos, mb, kq, alpha, amax);
+        }
+        __syncthreads();
+      }
+    }
+  } else {  // ---------------- the 96-channel stages, block mb = wave - 4
+    const int mb = wave - 4, n = 16 * mb + pos;
+    h8 w5h[4], w5l[4], w6h[3], w6l[3], w7h[3], w7l[3], w8h[3], w8l[3], w9h[3], w9l[3];
+    t3_load_w<4, 128>(w5h, w5l, a.w + kT3W[4], kT3C2, n, kq);
+    t3_load_w<3, 96>(w6h, w6l, a.w + kT3W[5], kT3C2, n, kq);
+    t3_load_w<3, 96>(w7h, w7l, a.w + kT3W[6], kT3C2, n, kq);
+    t3_load_w<3, 96>(w8h, w8l, a.w + kT3W[7], kT3C2, n, kq);
+    t3_load_w<3, 96>(w9h, w9l, a.w + kT3W[8], kT3C2, n, kq);
+    const float* bb = sb + 4 * kT3C1 + 16 * mb + 4 * kq;
+    constexpr int A5 = kT3A5, A6 = A5 + 2 * 2 * kT3Pl2, A7 = A6 + 2 * 2 * kT3Pl2, A8 = A7 + 2 * 2 * kT3Pl2;
+    for (int64_t gi = blockIdx.x; gi < n_groups; gi += gridDim.x) {
+      const int64_t img0 = gi * kT3Pos;
+      for (int y = 0; y < kT3Ticks; ++y) {
+        if (y >= 10 && y < 10 + 8) {  // stage 5 (2x1, 64 -> 96) from rows r, r + 1 of A4
+          const int r = y - 10;
+          const int ro[3] = {kT3A4 + (r & 3) * 2 * kT3Pl1, kT3A4 + ((r + 1) & 3) * 2 * kT3Pl1, 0};
+          const f4 acc = t3_block<4, kT3C1, kT3CS1, kT3Pl1>(w5h, w5l, t3_bias(bb), sm, ro, pos, kq, zero);
+          t3_store<LEAKY, kT3CS2, kT3Pl2>(acc, sm + A5 + (r & 1) * 2 * kT3Pl2, pos, mb, kq, alpha, amax);
+        }
+        if (y >= 11 && y < 11 + 8) {  // stage 6
+          const int r = y - 11;
+          const int ro[3] = {A5 + (r & 1) * 2 * kT3Pl2, 0, 0};
+          const f4 acc = t3_block<3, kT3C2, kT3CS2, kT3Pl2>(w6h, w6l, t3_bias(bb + kT3C2), sm, ro, pos, kq, zero);
+          t3_store<LEAKY, kT3CS2, kT3Pl2>(acc, sm + A6 + (r & 1) * 2 * kT3Pl2, pos, mb, kq, alpha, amax);
+        }
+        if (y >= 12 && y < 12 + 8) {  // stage 7
+          const int r = y - 12;
+          const int ro[3] = {A6 + (r & 1) * 2 * kT3Pl2, 0, 0};
+          const f4 acc = t3_block<3, kT3C2, kT3CS2, kT3Pl2>(w7h, w7l, t3_bias(bb + 2 * kT3C2), sm, ro, pos, kq, zero);
+          t3_store<LEAKY, kT3CS2, kT3Pl2>(acc, sm + A7 + (r & 1) * 2 * kT3Pl2, pos, mb, kq, alpha, amax);
+        }
+        if (y >= 13 && y < 13 + 8) {  // stage 8
+          const int r = y - 13;
+          const int ro[3] = {A7 + (r & 1) * 2 * kT3Pl2, 0, 0};
+          const f4 acc = t3_block<3, kT3C2, kT3CS2, kT3Pl2>(w8h, w8l, t3_bias(bb + 3 * kT3C2), sm, ro, pos, kq, zero);
+          t3_store<LEAKY, kT3CS2, kT3Pl2>(acc, sm + A8 + (r & 1) * 2 * kT3Pl2, pos, mb, kq, alpha, amax);
+        }
+        if (y >= 14 && y < 14 + 8) {  // stage 9 (no activation) -> out
+          const int r = y - 14;
+          const int ro[3] = {A8 + (r & 1) * 2 * kT3Pl2, 0, 0};
+          const f4 acc = t3_block<3, kT3C2, kT3CS2, kT3Pl2>(w9h, w9l, t3_bias(bb + 4 * kT3C2), sm, ro, pos, kq, zero);
+          if (img0 + pos < a.n_img) {
+            float* o = a.out + (img0 + pos) * a.out_img_stride + r * kT3C2 + 16 * mb + 4 * kq;
+            *reinterpret_cast<float4*>(o) = float4{acc[0], acc[1], acc[2], acc[3]};
+          }
+        }
+        __syncthreads();
+      }
+    }
+  }
+  raise_range(a.range_flag, amax);
+}
+
 // ------------------------------------------------------------------ host ----
 
 struct OpInfo {
@@ -2259,6 +2490,8 @@ struct ChainPlan {
   P2sArgs p2{};
   void (*p1fn)(P1Args) = nullptr;  // p1 pattern (shares d_p0 / p0_lds / p0_blocks_per_cu)
   P1Args p1{};
+  void (*t3fn)(T3sArgs) = nullptr;  // t3s pattern (SE20's deduplicated tail; shares d_p0 / p0_lds / ...)
+  T3sArgs t3{};
   size_t p0_lds = 0;
   int p0_blocks_per_cu = 0;
   void* d_p0 = nullptr;
@@ -2937,6 +3170,83 @@ bool plan_p2s(const std::vector<OpInfo>& ops, const std::vector<int>& st, const 
   return true;
 }
 
+// The t3s pattern (SE20's tail over its two phase images per clip): an input
+// pool 2x1 of the 27 x 1 x 48 chain-2 rows, 3x1 (48 -> 64), 1x1, 3x1, 1x1 (64),
+// 2x1 (64 -> 96), four 1x1 (96), the last without activation. Weights hi / lo
+// [cout][K] per stage (K = tap * cin + ci; stage 1 zero-padded to 160), biases f32.
+bool plan_t3s(const std::vector<OpInfo>& ops, const std::vector<int>& st, const ChainArgs& a, Dims d, Dims od,
+              ChainPlan& cp) {
+  if (getenv("HBK_EMBED_NO_T3S")) return false;
+  if (st.size() != 9 || a.ipc != 2 || a.row_off[0] != 0 || a.row_off[1] != 1 || a.in_ph != 2 || a.in_pw != 1 ||
+      a.out_ph != 1 || a.out_pw != 1)
+    return false;
+  if (d.h != kT3Hp || d.w != 1 || d.c != kT3C0 || a.C_src != kT3C0 || a.src_row_stride != kT3C0 ||
+      a.src_clip_stride != int64_t(kT3Hin) * kT3C0)
+    return false;
+  if (od.h != kT3Hout || od.w != 1 || od.c != kT3C2 || cp.x.out_img_stride != int64_t(kT3Hout) * kT3C2) return false;
+  const int kh[9] = {3, 1, 3, 1, 2, 1, 1, 1, 1};
+  const int cin[9] = {kT3C0, kT3C1, kT3C1, kT3C1, kT3C1, kT3C2, kT3C2, kT3C2, kT3C2};
+  const bool leaky = ops[st[0]].act != 0;
+  for (int i = 0; i < 9; ++i) {
+    const OpInfo& o = ops[st[i]];
+    if (o.kh != kh[i] || o.kw != 1 || o.cin != cin[i] || o.cout != (i < 4 ? kT3C1 : kT3C2)) return false;
+    if ((o.act != 0) != (leaky && i < 8)) return false;
+    if (o.act != 0 && (o.alpha != ops[st[0]].alpha || !(o.alpha >= 0.f && o.alpha <= 1.f))) return false;
+  }
+  std::vector<_Float16> w(kT3WHalfs, static_cast<_Float16>(0.f));
+  std::vector<float> b(4 * kT3C1 + 5 * kT3C2, 0.f);
+  int boff = 0;
+  for (int i = 0; i < 9; ++i) {
+    const OpInfo& o = ops[st[i]];
+    const int K = o.kh * o.cin, Kp = kT3K[i];
+    for (int n = 0; n < o.cout; ++n) {
+      for (int k = 0; k < K; ++k) {
+        const float v = o.w[size_t(k) * o.cout + n];  // HWIO: (tap cin + ci) cout + n
+        uint32_t bits;
+        memcpy(&bits, &v, 4);
+        bits &= 0xFFFFE000u;
+        float hv;
+        memcpy(&hv, &bits, 4);
+        w[kT3W[i] + size_t(n) * Kp + k] = static_cast<_Float16>(hv);
+        w[kT3W[i] + size_t(o.cout) * Kp + size_t(n) * Kp + k] = static_cast<_Float16>(v - hv);
+      }
+      b[boff + n] = o.b[n];
+    }
+    boff += o.cout;
+  }
+  const size_t wbytes = (w.size() * 2 + 15) & ~size_t(15);
+  hipError_t e = hipMalloc(&cp.d_p0, wbytes + b.size() * 4);
+  if (e == hipSuccess) e = hipMemcpy(cp.d_p0, w.data(), w.size() * 2, hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = hipMemcpy(static_cast<unsigned char*>(cp.d_p0) + wbytes, b.data(), b.size() * 4, hipMemcpyHostToDevice);
+  cp.t3fn = leaky ? t3s_chain_kernel<true> : t3s_chain_kernel<false>;
+  cp.p0_lds = kT3Lds;
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(cp.t3fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            int(cp.p0_lds));
+  int per_cu = 0;
+  if (e == hipSuccess)
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(cp.t3fn), kT3Threads,
+                                                     cp.p0_lds);
+  if (e != hipSuccess || per_cu < 1) {
+    (void)hipGetLastError();
+    if (cp.d_p0) (void)hipFree(cp.d_p0);
+    cp.d_p0 = nullptr;
+    cp.t3fn = nullptr;
+    return false;
+  }
+  cp.p0_blocks_per_cu = per_cu;
+  T3sArgs& p = cp.t3;
+  p.w = static_cast<const _Float16*>(cp.d_p0);
+  p.bias = reinterpret_cast<const float*>(static_cast<unsigned char*>(cp.d_p0) + wbytes);
+  p.out_img_stride = cp.x.out_img_stride;
+  p.alpha = leaky ? ops[st[0]].alpha : 0.f;
+  if (getenv("HBK_DEBUG_EMBED"))
+    fprintf(stderr, "hbk t3s chain: %dx%dx%d (pool 2x1) -> %dx%dx%d, %d images per workgroup, LDS %zu B, %d blocks/CU\n",
+            d.h, d.w, d.c, od.h, od.w, od.c, kT3Pos, cp.p0_lds, per_cu);
+  return true;
+}
+
 bool plan_p1(const std::vector<OpInfo>& ops, const std::vector<int>& st, const ChainArgs& a, Dims d, Dims od,
              ChainPlan& cp) {
   if (getenv("HBK_EMBED_NO_P1")) return false;
@@ -3056,8 +3366,9 @@ int build_segment(const std::vector<OpInfo>& ops, int o0, int o1, Dims in, int i
       Dims od;
       const int rc = layout_split(ops, stage_ops, d, a, cp, od);
       if (rc) return rc;
-      if (!plan_p0(ops, stage_ops, a, d, od, cp) && !plan_p1(ops, stage_ops, a, d, od, cp))
-        plan_p2s(ops, stage_ops, a, d, od, cp);
+      if (!plan_p0(ops, stage_ops, a, d, od, cp) && !plan_p1(ops, stage_ops, a, d, od, cp) &&
+          !plan_p2s(ops, stage_ops, a, d, od, cp))
+        plan_t3s(ops, stage_ops, a, d, od, cp);
       cp.x.dbg_slot = static_cast<int>(prog.chains.size() % 4);
       if (const char* e = getenv("HBK_DEBUG_SKIP")) cp.x.dbg_skip = atoi(e);
       cp.src_buf = src_buf;
@@ -3308,6 +3619,24 @@ int run_program(const Program& prog, const float* in, int64_t n_units, int64_t i
           if (blocks <= 0) continue;
           hipLaunchKernelGGL(c.p2fn, dim3(unsigned(blocks)), dim3(kP2sThreads), c.p0_lds, stream, pa);
           HBK_LAUNCH_CHECK("p2s_chain_kernel");
+          continue;
+        }
+      }
+      if (c.t3fn) {
+        T3sArgs pa = c.t3;
+        pa.range_flag = range_flag;
+        pa.in = c.src_buf < 0 ? in + u0 * in_unit_stride : bufs[c.src_buf];
+        pa.src_clip_stride = c.src_buf < 0 ? in_unit_stride : c.x.src_clip_stride;
+        pa.out = c.dst_buf < 0 ? out + u0 * out_unit_floats : bufs[c.dst_buf];
+        pa.n_img = nu * imgs_per_unit[k];
+        const bool aligned = !(reinterpret_cast<uintptr_t>(pa.in) & 15) && !(pa.src_clip_stride & 3) &&
+                             !(reinterpret_cast<uintptr_t>(pa.out) & 15) && !(pa.out_img_stride & 3);
+        if (aligned && pa.src_clip_stride >= int64_t(kT3Hin) * kT3C0) {
+          const int64_t groups = (pa.n_img + kT3Pos - 1) / kT3Pos;
+          const int64_t blocks = std::min<int64_t>(groups, persistent_blocks(c.p0_blocks_per_cu, stream));
+          if (blocks <= 0) continue;
+          hipLaunchKernelGGL(c.t3fn, dim3(unsigned(blocks)), dim3(kT3Threads), c.p0_lds, stream, pa);
+          HBK_LAUNCH_CHECK("t3s_chain_kernel");
           continue;
         }
       }

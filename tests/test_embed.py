@@ -122,7 +122,8 @@ def test_embed_pattern_kernels_match_generic_path(monkeypatch, capfd):
     """The plan picks the streaming p0s kernel (one wave per clip) for SE20's
     chain 0, the two-wave p1s pipeline for chain 1, the 16-clip p2s pipeline for
     chain 2 and the phase-deduplicated tail (2 phase images per clip instead of
-    16 windows); HBK_EMBED_NO_P0S /
+    16 windows) on the 16-image t3s pipeline; HBK_EMBED_NO_T3S runs that tail on
+    the generic split-f16 kernel, HBK_EMBED_NO_P0S /
     NO_P1S fall back to the banded p0 / p1 kernels, HBK_EMBED_NO_DEDUP to the
     per-window tail, and with every pattern disabled the generic split-f16
     kernel runs every chain. All paths match the oracle and each other."""
@@ -134,13 +135,16 @@ def test_embed_pattern_kernels_match_generic_path(monkeypatch, capfd):
     monkeypatch.setenv("HBK_DEBUG_EMBED", "1")
     capfd.readouterr()
     outs = {}
-    for name, env, want in (("p0s", {}, ("hbk p0s chain", "hbk p1s chain", "hbk p2s chain", "hbk tail dedup")),
+    for name, env, want in (("p0s", {}, ("hbk p0s chain", "hbk p1s chain", "hbk p2s chain", "hbk tail dedup",
+                                          "hbk t3s chain")),
+                            ("not3s", {"HBK_EMBED_NO_T3S": "1"}, ("hbk p2s chain", "hbk tail dedup")),
                             ("p0", {"HBK_EMBED_NO_P0S": "1", "HBK_EMBED_NO_P1S": "1"},
                              ("hbk p0 chain", "hbk p1 chain", "hbk tail dedup")),
                             ("nodedup", {"HBK_EMBED_NO_DEDUP": "1"}, ("hbk p0s chain", "hbk p1s chain")),
-                            ("generic", {"HBK_EMBED_NO_P0": "1", "HBK_EMBED_NO_P1": "1", "HBK_EMBED_NO_P2S": "1"}, ())):
+                            ("generic", {"HBK_EMBED_NO_P0": "1", "HBK_EMBED_NO_P1": "1", "HBK_EMBED_NO_P2S": "1",
+                                         "HBK_EMBED_NO_T3S": "1"}, ())):
         for k in ("HBK_EMBED_NO_P0S", "HBK_EMBED_NO_P1S", "HBK_EMBED_NO_P0", "HBK_EMBED_NO_P1", "HBK_EMBED_NO_P2S",
-                  "HBK_EMBED_NO_DEDUP"):
+                  "HBK_EMBED_NO_DEDUP", "HBK_EMBED_NO_T3S"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
@@ -149,14 +153,16 @@ def test_embed_pattern_kernels_match_generic_path(monkeypatch, capfd):
         for w in want:
             assert w + ":" in err, (name, err)
         if not want:
-            assert "hbk p0" not in err and "hbk p1" not in err and "hbk p2" not in err, err
+            assert "hbk p0" not in err and "hbk p1" not in err and "hbk p2" not in err and "hbk t3" not in err, err
+        if name in ("nodedup", "not3s"):
+            assert "hbk t3s chain" not in err, err
         if name == "nodedup":
             assert "hbk tail dedup" not in err, err
         outs[name] = plan.clips(torch.from_numpy(mel).cuda()).cpu().numpy()
     for name, out in outs.items():
         ok, worst = _close(out, ref)
         assert ok, f"{name}: max |diff| {worst}"
-    for name in ("p0", "nodedup", "generic"):
+    for name in ("p0", "not3s", "nodedup", "generic"):
         assert np.abs(outs["p0s"] - outs[name]).max() <= 1e-5 * (1.0 + np.abs(ref).max()), name
 
 
