@@ -112,10 +112,11 @@ def parse():
 
 
 # the split-f16 embedding path's kernels (SE20): streaming chain 0, two-wave chain 1,
-# the generic kernel on chain 2 and on the phase-deduplicated tail, the window gather
-EMBED_KERNELS = ("p0s_chain_kernel + p1s_chain_kernel + conv_chain_x3_kernel x2 (chain 2; tail on 2 phase images "
-                 "per clip) + embed_gather_kernel")
-EMBED_KERNEL_SUBSTR = ("conv_chain", "p0_chain", "p1_chain", "p0s_chain", "p1s_chain", "embed_gather")
+# the 16-clip chain 2, the 16-image tail pipeline on the phase-deduplicated tail, the window gather
+EMBED_KERNELS = ("p0s_chain_kernel + p1s_chain_kernel + p2s_chain_kernel + t3s_chain_kernel (tail on 2 phase "
+                 "images per clip) + embed_gather_kernel")
+EMBED_KERNEL_SUBSTR = ("conv_chain", "p0_chain", "p1_chain", "p0s_chain", "p1s_chain", "p2s_chain", "t3s_chain",
+                       "embed_gather")
 TRAFFIC_SOURCE = [None]
 CURRENT_CONFIG = [None]
 
@@ -1030,8 +1031,10 @@ def setup_e2e(args, dev, rank, world, seed):
         from heybuddy.kernels import EmbedPlan
         m = min(n, 16384)
         frames = mel_frames(aug.augment_device(src[:m], lens[:m]), mplan, N_FRAMES)
-        saved = {k: os.environ.get(k) for k in ("HBK_EMBED_NO_P0", "HBK_EMBED_NO_P1")}
-        os.environ.update({"HBK_EMBED_NO_P0": "1", "HBK_EMBED_NO_P1": "1"})
+        saved = {k: os.environ.get(k) for k in ("HBK_EMBED_NO_P0", "HBK_EMBED_NO_P1", "HBK_EMBED_NO_P2S",
+                                                "HBK_EMBED_NO_T3S")}
+        os.environ.update({"HBK_EMBED_NO_P0": "1", "HBK_EMBED_NO_P1": "1", "HBK_EMBED_NO_P2S": "1",
+                           "HBK_EMBED_NO_T3S": "1"})
         try:
             gplan = EmbedPlan(default_graph(), starts=WINDOW_STARTS, device=dev, precision=eplan.precision)
         finally:
@@ -1049,7 +1052,7 @@ def setup_e2e(args, dev, rank, world, seed):
         e1.record()
         torch.cuda.synchronize(dev)
         ms = e0.elapsed_time(e1) / 3
-        extra = [roof("conv_chain_x3_kernel only (HBK_EMBED_NO_P0=1 HBK_EMBED_NO_P1=1: the generic split-f16 chain "
+        extra = [roof("conv_chain_x3_kernel only (HBK_EMBED_NO_P0 / P1 / P2S / T3S: the generic split-f16 chain "
                       "kernel on every chain, as for a graph without SE20's chain shapes; %d clips, untimed)" % m,
                       "mfma", 2.0 * gplan.macs_per_clip * m, ms, "TFLOP/s", None, peak=SPLIT_PEAK_TFLOPS,
                       peak_basis="f16 dense MFMA peak / 3", clips=m)]
