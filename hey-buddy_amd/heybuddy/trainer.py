@@ -249,6 +249,8 @@ class EvalPasses:
                               device=dev)
         self.counts = torch.zeros((2, 4), dtype=torch.float32, device=dev)
         self.history = torch.zeros((history_cap, 8), dtype=torch.float32, device=dev)
+        self.side = os.environ.get("HBK_EVAL_SIDE", "0") == "1"  # the f32 pools on a side stream (run(); off)
+        self._side_keep = None
         self.n = 0
 
     @property
@@ -262,11 +264,31 @@ class EvalPasses:
         p = tr.model.dropout.p if tr.model.training else 0.0
         self.counts.zero_()
         plan.eval_prepare(flat, self.ws)
+        # on a CU-masked stream (the pipelined train partition) the f32 pools' launches
+        # (25 k rows each: a few rounds of workgroups, the last one partly empty) run on
+        # a side stream with the same CU set, concurrently with the large f16 pool's, so
+        # their workgroups fill each other's tails (64 CUs: 3.50 -> 3.43 ms per pass; on
+        # the whole GPU it measured slower, so unmasked streams keep one queue); the
+        # counts are atomics and the prepared weights are read-only here. Off by default
+        # (HBK_EVAL_SIDE=1 turns it on): in the pipelined headline the extra queue cost
+        # the featurize stream ~3 ms per 100 k-clip step (881 / 875 k against 857 / 853 k
+        # clips/s, same box, alternating)
+        cur = torch.cuda.current_stream(self.trainer.device)
+        side = None
+        if self.side and any(pool.dtype == torch.float32 for pool, _, _, _ in self.parts):
+            side, self._side_keep = capture_stream(self.trainer.device)
+            if self._side_keep is None:  # not a CU-masked stream
+                side = None
+            else:
+                side.wait_stream(cur)
         for k, (pool, rows, label, which) in enumerate(self.parts):
-            plan.eval_count(flat, pool, rows, label, self.counts[which], self.ws, row_offset=self.offsets[k],
-                            activation_threshold=self.act_thr, dropout_p=p,
-                            seed=(self.seed + 0x9E3779B97F4A7C15 * (self.n * 8 + k + 1)) % (1 << 64))
+            with torch.cuda.stream(side if side is not None and pool.dtype == torch.float32 else cur):
+                plan.eval_count(flat, pool, rows, label, self.counts[which], self.ws, row_offset=self.offsets[k],
+                                activation_threshold=self.act_thr, dropout_p=p,
+                                seed=(self.seed + 0x9E3779B97F4A7C15 * (self.n * 8 + k + 1)) % (1 << 64))
             self.offsets[k] = (self.offsets[k] + rows) % pool.shape[0]
+        if side is not None:
+            cur.wait_stream(side)
         plan.eval_finish(self.counts[0], self.counts[1] if self.testing else None, self.sizes,
                          self.history[self.n % self.history.shape[0]], target=self.target, ratio=self.ratio,
                          sched=sched, next_step=next_step)
