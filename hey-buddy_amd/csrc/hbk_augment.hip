@@ -2030,6 +2030,111 @@ __global__ void __launch_bounds__(128) ps_resample_kernel(PitchArgs a) {
   }
 }
 
+
+// The resampler as a GEMM on the matrix cores: out[f nw + ph] = sum_q taps[ph][q]
+// ypad[f orig - width + q] is [frames x 160] x [160 x nw] per clip (K = the taps,
+// zero-padded from kPsTapMax to 5 blocks of 32). v_mfma_f32_16x16x32_f16 in split
+// f16 (hi*hi + hi*lo + lo*hi, f32 accumulation: ~2^-22 relative per product, as
+// the f32 FMAs it replaces). A workgroup takes 64 frames of one clip: their
+// windows are staged once into LDS as f16 hi / lo planes (one row per frame, the
+// overlapping samples duplicated so every A fragment is one aligned 16-B read)
+// after a power-of-two scale that puts the block's largest |sample| in
+// [2^14, 2^15); the taps (x 2^10) are each wave's B fragments in VGPRs, two
+// 16-phase tiles per wave.
+constexpr int kRsFrames = 64, kRsK = 160, kRsLd = kRsK + 8;  // 336-B rows (odd 16-B count)
+static_assert(kPsTapMax <= kRsK && kPsPhaseMax <= 128, "the MFMA resampler's K padding and 8 phase tiles");
+typedef _Float16 rs_h8 __attribute__((ext_vector_type(8)));
+typedef float rs_f4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void rs_split(float v, _Float16& h, _Float16& l) {
+  h = static_cast<_Float16>(v);
+  l = static_cast<_Float16>(v - static_cast<float>(h));
+}
+__global__ void __launch_bounds__(256) ps_resample_mfma_kernel(PitchArgs a) {
+  __shared__ __attribute__((aligned(16))) _Float16 wh[kRsFrames][kRsLd];
+  __shared__ __attribute__((aligned(16))) _Float16 wl[kRsFrames][kRsLd];
+  __shared__ float red[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int e = blockIdx.y, f0 = blockIdx.x * kRsFrames;
+  const float* y = a.y + static_cast<int64_t>(e) * a.l1;
+  // staging: pair p = tid + 256 u of (frame p / 80, taps 2 (p % 80) and + 1)
+  constexpr int kPairs = kRsFrames * kRsK / 2, kPer = kPairs / 256;
+  float v0[kPer], v1[kPer];
+  float mx = 0.f;
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int p = tid + 256 * u, fr = p / (kRsK / 2), q = 2 * (p - fr * (kRsK / 2));
+    const int src = (f0 + fr) * a.orig - a.width + q;
+    const int s0 = min(max(src, 0), a.l1 - 1), s1 = min(max(src + 1, 0), a.l1 - 1);
+    const float x0 = y[s0], x1 = y[s1];
+    v0[u] = (src >= 0 && src < a.l1 && q < kPsTapMax) ? x0 : 0.f;
+    v1[u] = (src + 1 >= 0 && src + 1 < a.l1 && q + 1 < kPsTapMax) ? x1 : 0.f;
+    mx = fmaxf(mx, fmaxf(fabsf(v0[u]), fabsf(v1[u])));
+  }
+  // B fragments: phases 16 (2 wave + t) + (lane & 15), taps 32 ks + 8 (lane >> 4) ..
+  const int n = lane & 15, kq = lane >> 4;
+  rs_h8 bh[2][5], bl[2][5];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int ph = min(16 * (2 * wave + t) + n, a.nw - 1);
+    const float* tr = a.taps + ph * kPsTapMax;
+#pragma unroll
+    for (int ks = 0; ks < 5; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int q = 32 * ks + 8 * kq + j;
+        const float tv = tr[min(q, kPsTapMax - 1)];
+        _Float16 h, l;
+        rs_split(q < kPsTapMax ? tv * 1024.f : 0.f, h, l);
+        bh[t][ks][j] = h;
+        bl[t][ks][j] = l;
+      }
+  }
+  for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  if (lane == 0) red[wave] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const int ex = mx > 0.f ? min(14 - ilogbf(mx), 100) : 0;
+  const float scale = ldexpf(1.f, ex), unscale = ldexpf(1.f, -ex - 10);
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int p = tid + 256 * u, fr = p / (kRsK / 2), q = 2 * (p - fr * (kRsK / 2));
+    _Float16 h0, l0, h1, l1;
+    rs_split(v0[u] * scale, h0, l0);
+    rs_split(v1[u] * scale, h1, l1);
+    wh[fr][q] = h0;
+    wh[fr][q + 1] = h1;
+    wl[fr][q] = l0;
+    wl[fr][q + 1] = l1;
+  }
+  __syncthreads();
+  float* out = a.out + static_cast<int64_t>(a.idx[e]) * a.out_stride;
+#pragma unroll
+  for (int ft = 0; ft < kRsFrames / 16; ++ft) {
+    rs_f4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int ks = 0; ks < 5; ++ks) {
+      const rs_h8 ah = *reinterpret_cast<const rs_h8*>(&wh[16 * ft + n][32 * ks + 8 * kq]);
+      const rs_h8 al = *reinterpret_cast<const rs_h8*>(&wl[16 * ft + n][32 * ks + 8 * kq]);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[t][ks], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[t][ks], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[t][ks], acc[t], 0, 0, 0);
+      }
+    }
+    // lane (n, kq) holds frames 16 ft + 4 kq + j of phase 16 (2 wave + t) + n
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int ph = 16 * (2 * wave + t) + n;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int i = (f0 + 16 * ft + 4 * kq + j) * a.nw + ph;
+        if (ph < a.nw && i < a.L) out[i] = i < a.target ? acc[t][j] * unscale : 0.f;
+      }
+    }
+  }
+}
+
 }  // namespace
 }  // namespace hbk
 
@@ -2468,9 +2573,16 @@ int hbk_pitch_shift(const float* x, int64_t x_stride, int64_t n, const int32_t* 
                      sizeof(PvShared), st, a);
   HBK_LAUNCH_CHECK("ps_vocoder_kernel");
   const int res_frames = (a.L + a.nw - 1) / a.nw;
-  hipLaunchKernelGGL(ps_resample_kernel, dim3(unsigned((res_frames + kPsResFrames - 1) / kPsResFrames), unsigned(n)),
-                     dim3(128), 0, st, a);
-  HBK_LAUNCH_CHECK("ps_resample_kernel");
+  static const bool valu_rs = getenv("HBK_PS_RESAMPLE_VALU") != nullptr;  // the f32 VALU resampler (A/B)
+  if (valu_rs || a.nw > 128) {
+    hipLaunchKernelGGL(ps_resample_kernel, dim3(unsigned((res_frames + kPsResFrames - 1) / kPsResFrames), unsigned(n)),
+                       dim3(128), 0, st, a);
+    HBK_LAUNCH_CHECK("ps_resample_kernel");
+  } else {
+    hipLaunchKernelGGL(ps_resample_mfma_kernel, dim3(unsigned((res_frames + kRsFrames - 1) / kRsFrames), unsigned(n)),
+                       dim3(256), 0, st, a);
+    HBK_LAUNCH_CHECK("ps_resample_mfma_kernel");
+  }
   return HBK_OK;
 }
 
