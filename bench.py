@@ -879,7 +879,7 @@ def setup_e2e(args, dev, rank, world, seed):
         out = []
         if sub_ms.get("pitch"):
             m = cnt["pitch"]
-            out.append(roof("ps_vocoder_kernel + ps_resample_kernel (hbk_pitch_shift: %.0f clips shifted per step, "
+            out.append(roof("ps_vocoder_kernel + ps_resample_mfma_kernel (hbk_pitch_shift: %.0f clips shifted per step, "
                             "p = %g per batch of 128)" % (m, args.pitch_prob), "valu", PITCH_FLOP_PER_CLIP * m,
                             sub_ms["pitch"], "TFLOP/s", load_traffic(pmc, ("ps_vocoder", "ps_resample", "ps_taps")),
                             peak=157.3, peak_basis="f32 vector peak (MI355X_MICROARCH.md)",
