@@ -352,14 +352,14 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
   if (ctrl[0] == 0.f) return;
   if (step_sc) lr = static_cast<float>(step_sc[0]);
   const float scale = ctrl[1], bc1 = ctrl[2], bc2s = sqrtf(ctrl[3]);
-  const float step_size = lr / bc1;
+  const float step_size = lr / bc1, inv_bc2s = 1.f / bc2s;
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
     const float gi = g[i] * scale;
     const float mi = beta1 * m[i] + (1.f - beta1) * gi;
     const float vi = beta2 * v[i] + (1.f - beta2) * gi * gi;
     m[i] = mi;
     v[i] = vi;
-    p[i] -= step_size * mi / (sqrtf(vi) / bc2s + eps);
+    p[i] -= adam_step(mi, vi, step_size, inv_bc2s, eps);
   }
 }
 

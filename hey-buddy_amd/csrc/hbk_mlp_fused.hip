@@ -1487,7 +1487,7 @@ __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
     return (q[0] + q[1]) + (q[2] + q[3]);
   };
   const float bc1 = 1.f - powf(a.b1, t), bc2s = sqrtf(1.f - powf(a.b2, t));
-  const float step_size = lr / bc1;
+  const float step_size = lr / bc1, inv_bc2s = 1.f / bc2s;
   const bool on = fire != 0.f;
   // float4 body (the bucket, params and moments are 16-B aligned torch buffers), scalar tail
 
@@ -1504,7 +1504,7 @@ __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
       M4[i] = mi;
       V4[i] = vi;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) p[e] -= step_size * mi[e] / (sqrtf(vi[e]) / bc2s + a.eps);
+      for (int e = 0; e < 4; ++e) p[e] -= adam_step(mi[e], vi[e], step_size, inv_bc2s, a.eps);
       P4[i] = p;
     }
     return p;
@@ -1547,7 +1547,7 @@ __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
         M4[i] = mi;
         V4[i] = vi;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) p[e] -= step_size * mi[e] / (sqrtf(vi[e]) / bc2s + a.eps);
+        for (int e = 0; e < 4; ++e) p[e] -= adam_step(mi[e], vi[e], step_size, inv_bc2s, a.eps);
         P4[i] = p;
       }
       if (on) {
@@ -1597,7 +1597,7 @@ __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
       const float vi = a.b2 * a.v[i] + (1.f - a.b2) * gi * gi;
       a.m[i] = mi;
       a.v[i] = vi;
-      a.P[i] -= step_size * mi / (sqrtf(vi) / bc2s + a.eps);
+      a.P[i] -= adam_step(mi, vi, step_size, inv_bc2s, a.eps);
     }
   }
 }

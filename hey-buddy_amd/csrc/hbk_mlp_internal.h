@@ -46,6 +46,14 @@ __device__ __forceinline__ float uniform01(uint64_t seed, uint64_t i) {
   return static_cast<float>(z >> 40) * (1.f / 16777216.f);
 }
 
+// Adam's parameter step, torch's step_size * m / (sqrt(v) / bc2s + eps), on the
+// hardware v_sqrt_f32 / v_rcp_f32 (1 ulp each) instead of the IEEE square root
+// and two IEEE divisions; shared by k4 and the generic adam_kernel so that the
+// two update paths stay bit-identical (k4: 12.0 -> 10.9 us per step on 64 CUs)
+__device__ __forceinline__ float adam_step(float mi, float vi, float step_size, float inv_bc2s, float eps) {
+  return step_size * mi * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vi) * inv_bc2s + eps);
+}
+
 // True when the fused kernels of hbk_mlp_fused.hip cover this plan.
 bool mlp_fused_supported(const hbk_mlp_plan& p);
 int64_t mlp_fused_ws_floats(const hbk_mlp_plan& p, int64_t B);
