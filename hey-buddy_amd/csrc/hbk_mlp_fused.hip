@@ -1782,7 +1782,7 @@ __global__ void __launch_bounds__(64 * W) kv_gemm_kernel(KvArgs a) {
   dma_w(1, 1);
 #pragma unroll
   for (int d = 1; d < kDepth; ++d) load_rows(d, d);
-  __builtin_amdgcn_s_waitcnt((kALoads * (kDepth - 1) + kDma) | (0x7 << 4) | (0xF << 8));  // vmcnt(4 + kALoads): chunk 0 in
+  __builtin_amdgcn_s_waitcnt((kALoads * (kDepth - 1) + kDma) | (0x7 << 4) | (0xF << 8));  // chunk 0 in (the later chunks' DMA and rows may fly)
   dma_barrier();
   f4 acc[kRT][8];
 #pragma unroll
@@ -1868,7 +1868,7 @@ __global__ void __launch_bounds__(64 * W) kv_gemm_kernel(KvArgs a) {
     // The sched_barriers keep the next chunk's conversions below the counted wait: hoisted
     // above it, hipcc guards them with vmcnt(0) (DMA and row loads pending together)
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_waitcnt((kALoads * (kDepth - 1) + kDma) | (0x7 << 4) | (0xF << 8));  // vmcnt(4 + kALoads)
+    __builtin_amdgcn_s_waitcnt((kALoads * (kDepth - 1) + kDma) | (0x7 << 4) | (0xF << 8));  // chunk c + 1 in
     __builtin_amdgcn_s_waitcnt((0x3F & 0xF) | ((0x3F >> 4) << 14) | (0x7 << 4) | (0x0 << 8));  // lgkmcnt(0)
     dma_barrier();
     __builtin_amdgcn_sched_barrier(0);
