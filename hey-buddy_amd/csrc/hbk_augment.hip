@@ -1537,10 +1537,22 @@ constexpr int kPvClips = HBK_PV_CLIPS;                 // clips per workgroup (1
 constexpr int kPvGroup = 8;                            // output frames per istft step (lane 8u + .: frame u)
 constexpr int kPvRows = 64;                            // input frames of d rows held in LDS
 constexpr int kPvGh = 64;                              // ring of G(t, .) rows (>= 36 + kPvGroup)
+#ifndef HBK_PV_F32STATE
+#define HBK_PV_F32STATE 0  // 1: the sliding DFT's state in float32, restarted every 128 frames (variant pv32)
+#endif
 #ifndef HBK_PV_RESTART
+#if HBK_PV_F32STATE
+#define HBK_PV_RESTART 128
+#else
 #define HBK_PV_RESTART 1024  // measured L2 vs the float64 oracle: 3.8e-5 at 128, 5.6e-5 at 256, 6.5e-5 at 1024
 #endif
+#endif
 constexpr int kPvRestart = HBK_PV_RESTART;             // sliding-DFT frames between direct DFTs
+#if HBK_PV_F32STATE
+typedef float pv_t;   // sliding-DFT state
+#else
+typedef double pv_t;
+#endif
 
 struct PitchArgs {
   const float* x;
@@ -1693,7 +1705,7 @@ ps_vocoder_kernel(PitchArgs a) {
   const int k = min(lane, kPsBins - 1);
   // per-bin constants: w^-7 in float64 (w^j, j < 7, read from sh.wt per slide), the synthesis weight
   const int q7 = (7 * k) % kPsFft;
-  const double rr = sh.tw64[q7][0], ri = -sh.tw64[q7][1];
+  const pv_t rr = static_cast<pv_t>(sh.tw64[q7][0]), ri = static_cast<pv_t>(-sh.tw64[q7][1]);
   const float ck = lane < kPsBins ? ((lane == 0 || lane == kPsBins - 1) ? 1.f : 2.f) : 0.f;
   // synthesis weights c_k e^{2 pi i k s / 250} of the lane's registers (s = r ^ pv_g(lane & 7); s = 7: 0)
   const int gb = pv_g(lane & 7), w = lane >> 6, ou = (lane >> 3) & 7;
@@ -1720,19 +1732,24 @@ ps_vocoder_kernel(PitchArgs a) {
       q -= q >= kPsFft ? kPsFft : 0;
     }
   };
-  double xre, xim;
-  direct(xre, xim);
+  pv_t xre, xim;
+  {
+    double dre, dim;
+    direct(dre, dim);
+    xre = static_cast<pv_t>(dre);
+    xim = static_cast<pv_t>(dim);
+  }
   int cnt = __builtin_amdgcn_readfirstlane(C.cnt0);
-  if (cnt == 0) xre = xim = 0.0;
+  if (cnt == 0) xre = xim = pv_t(0);
   int sf = 0;  // last slid frame
   int anchor = 0;  // frame of the last direct DFT
   // the sliding DFT's next frame (sf + 1) from the current state, as a candidate
   // (xre, xim, cnt are committed by the caller): two partial sums per component
   // keep the float64 dependency chain short
-  auto slide_to = [&](double& nre, double& nim, int& ncnt) {
+  auto slide_to = [&](pv_t& nre, pv_t& nim, int& ncnt) {
     const int f = sf + 1;
     if (f >= a.f_in) {
-      nre = nim = 0.0;
+      nre = nim = pv_t(0);
       ncnt = cnt;
       return;
     }
@@ -1751,19 +1768,19 @@ ps_vocoder_kernel(PitchArgs a) {
     acc = __builtin_elementwise_fma(cf{db.y, db.y}, cf{w56.x, w56.y}, acc);
     acc = __builtin_elementwise_fma(cf{db.z, db.z}, cf{w56.z, w56.w}, acc);
     ncnt = __builtin_amdgcn_readfirstlane(cnt + static_cast<int>(db.w));  // a clip's count: wave-uniform
-    const double ar = xre + static_cast<double>(acc.x), ai = xim + static_cast<double>(acc.y);
+    const pv_t ar = xre + static_cast<pv_t>(acc.x), ai = xim + static_cast<pv_t>(acc.y);
     nre = ar * rr - ai * ri;
     nim = ar * ri + ai * rr;
-    if (ncnt == 0) nre = nim = 0.0;
+    if (ncnt == 0) nre = nim = pv_t(0);
   };
-  auto commit = [&](double nre, double nim, int ncnt) {
+  auto commit = [&](pv_t nre, pv_t nim, int ncnt) {
     xre = nre;
     xim = nim;
     cnt = ncnt;
     ++sf;
   };
   // unit vector and magnitude of a frame's bin (X = 0: u = 1, |X| = 0)
-  auto polar_of = [&](double re, double im, cf& u, float& mag) {
+  auto polar_of = [&](pv_t re, pv_t im, cf& u, float& mag) {
     const float fr = static_cast<float>(re), fi = static_cast<float>(im);
     const float n2 = fmaf(fr, fr, fi * fi);
     const float rs = __builtin_amdgcn_rsqf(n2);  // v_rsq_f32 (1 ulp)
@@ -1777,7 +1794,7 @@ ps_vocoder_kernel(PitchArgs a) {
   float cm, nm, pm;
   polar(ca, cm);
   {
-    double nre, nim;
+    pv_t nre, nim;
     int ncnt;
     slide_to(nre, nim, ncnt);
     commit(nre, nim, ncnt);
@@ -1821,8 +1838,11 @@ ps_vocoder_kernel(PitchArgs a) {
       __syncthreads();
       for (int q = lane; q < kPsFft; q += 128) C.xs[q] = ps_xp(xr, a.L, kPsHop * sf + q);
       __syncthreads();
-      direct(xre, xim);
-      if (cnt == 0) xre = xim = 0.0;
+      double dre, dim;
+      direct(dre, dim);
+      xre = static_cast<pv_t>(dre);
+      xim = static_cast<pv_t>(dim);
+      if (cnt == 0) xre = xim = pv_t(0);
       anchor = sf;
     }
     HBK_PVT(1);  // row refills, restarts
@@ -1861,7 +1881,7 @@ ps_vocoder_kernel(PitchArgs a) {
           na = pa;
           nm = pm;
           R = cmul(R, cmul_conj(ca, na));  // P_t = P_{t-1} u_{c+1} conj u_c = R u_{c+1}, and c + 2 becomes the frame
-          double nre, nim;
+          pv_t nre, nim;
           int ncnt;
           slide_to(nre, nim, ncnt);
           commit(nre, nim, ncnt);
@@ -1876,7 +1896,7 @@ ps_vocoder_kernel(PitchArgs a) {
         cm = step ? nm : cm;
         na = step ? pa : na;
         nm = step ? pm : nm;
-        double nre, nim;
+        pv_t nre, nim;
         int ncnt;
         slide_to(nre, nim, ncnt);  // candidate frame sf + 1 and its polar form, kept only when stepping
         cf qa;
