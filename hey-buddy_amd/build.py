@@ -62,6 +62,7 @@ VARIANTS = {  # profiling builds (load with HBK_LIB=hey-buddy_amd/lib/<name>)
     "ablate": ("libhbk_ablate.so", ("-DHBK_ABLATE",)),      # HBK_DEBUG_SKIP phase ablation only
     "trace": ("libhbk_trace.so", ("-DHBK_TRACE",)),         # per-wave s_memtime timeline
     "pv32": ("libhbk_pv32.so", ("-DHBK_PV_F32STATE=1",)),  # the vocoder's sliding-DFT state in float32
+    "pv32r": ("libhbk_pv32r.so", ("-DHBK_PV_F32STATE=1", "-DHBK_PV_RESTART=1024")),  # ... restarted every 1,024
     "k2ab1": ("libhbk_k2ab1.so", ("-DHBK_K2_ABLATE=1",)),   # k2 ablation (timing only): weights loaded once
     "k2ab2": ("libhbk_k2ab2.so", ("-DHBK_K2_ABLATE=2",)),   # k2 ablation (timing only): slab 0 read KS times
     "kvab1": ("libhbk_kvab1.so", ("-DHBK_KV_ABLATE=1",)),   # eval ablation: the input GEMM only
