@@ -63,8 +63,8 @@ AUG_T = 23040
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=5, choices=(1, 2, 3, 4, 5))
     ap.add_argument("--clips", type=int, default=100_000, help="clips per rank per step (configs 2, 3, 5)")
     ap.add_argument("--cpu-sample", type=int, default=None, help="units timed on the host CPU (~10-30 s)")
