@@ -100,12 +100,19 @@ def parse():
                          "validation rows and 500 of 50 + 50 testing rows, dynamic negative weight on the device")
     ap.add_argument("--stage-steps", type=int, default=2,
                     help="overlapped runs: sequential (untimed) steps that time the stages for the rooflines")
+    ap.add_argument("--other-configs", default=None,
+                    help="with --config 5: these configs (comma list of 1-4) are measured after the headline and "
+                         "reported in the same JSON line as configs_other (default 2,3,4,1; '' for none)")
+    ap.add_argument("--other-steps", type=int, default=5, help="timed steps of each configs_other measurement")
+    ap.add_argument("--other-warmup", type=int, default=2, help="warmup steps of each configs_other measurement")
     ap.add_argument("--pmc", default=None,
                     help="per-kernel HBM bytes per step from rocprofv3 --pmc passes (tools/prof_summary.py JSON; "
                          "default profiles/pmc_c<config>_latest.json)")
     args = ap.parse_args()
     if args.pmc is None:
         args.pmc = os.path.join(ROOT, "profiles", f"pmc_c{args.config}_latest.json")
+    if args.other_configs is None:
+        args.other_configs = "2,3,4,1"
     if args.overlap is None:  # r03j: split:64 652k clips/s vs split:32 617k with pitch shift on
         args.overlap = "split:64"
     return args
@@ -208,11 +215,95 @@ def launch_ranks(args) -> int:
     return subprocess.call(cmd, env=env)
 
 
+def sub_args(args, config, **over):
+    """A copy of the parsed arguments for another measurement in the same run
+    (configs_other, the faithful global-batch mode): its own --config, the
+    short step counts, its own PMC summary and no profiling markers."""
+    a = argparse.Namespace(**vars(args))
+    a.config = config
+    a.steps, a.warmup = args.other_steps, args.other_warmup
+    a.pmc = os.path.join(ROOT, "profiles", f"pmc_c{config}_latest.json")
+    a.clips = 100_000
+    a.cpu_sample = {2: 1500, 3: 1500, 4: 200}.get(config)
+    for k, v in over.items():
+        setattr(a, k, v)
+    return a
+
+
+def measure(args, dev, rank, world, marks=True) -> dict:
+    """One measurement of --config args.config (2-5) on every rank: setup,
+    W warmup steps, then K steps timed between barrier + synchronize on both
+    sides; the max over ranks. Returns the JSON line (complete on rank 0)."""
+    from heybuddy.synthetic import seed_for
+    CURRENT_CONFIG[0] = args.config
+    mark = prof_mark if marks else (lambda tag, dev: None)
+    setup = {2: setup_featurize, 3: setup_featurize, 4: setup_train, 5: setup_e2e}[args.config]
+    job = setup(args, dev, rank, world, seed_for(args.config, rank))
+
+    staged = job.get("staged_step")  # overlapped stages: timed per stage in separate sequential steps
+    n_ev = args.stage_steps if staged else args.steps
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(len(job["stages"]) + 1)] for _ in range(n_ev)]
+    if staged:  # before the pipelined warmup, which leaves the next chunk's features pending
+        staged(None)
+        mark(3, dev)
+        for k in range(n_ev):
+            staged(evs[k])
+        torch.cuda.synchronize(dev)
+        mark(4, dev)
+    for _ in range(args.warmup):
+        job["step"](None)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    mark(1, dev)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        job["step"](None if staged else evs[k])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    mark(2, dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    stage_ms = [sum(e[i].elapsed_time(e[i + 1]) for e in evs) / n_ev for i in range(len(job["stages"]))]
+    if "rooflines" in job:  # per kernel group (sub-stages timed on their own); the dominant one leads
+        roofs = job["rooflines"](dict(zip(job["stages"], stage_ms)), args.pmc)
+    else:
+        roofs = [job["roofline"](name, ms, args.pmc) for name, ms in zip(job["stages"], stage_ms)]
+    # the dominant kernel group by device time (a stage summary that only aggregates
+    # groups listed on their own is never the headline entry)
+    dom = max(range(len(roofs)), key=lambda i: (not roofs[i].get("summary"), roofs[i]["ms_per_step"]))
+
+    extra = job["extra_rooflines"]() if "extra_rooflines" in job and world == 1 else []
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = job["cpu_baseline"](args.cpu_sample)
+    units = job["units_per_step"] * (world if job["scaling"] == "weak" else 1)
+    line = {
+        "metric": job["metric"], "value": round(units * args.steps / elapsed, 1), "unit": job["unit"],
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": job["scaling"],
+        "vs_baseline": None, "dtype": "f32", "data": job["data"], "config": job["config"], "roofline": roofs[dom],
+        "roofline_other": [r for i, r in enumerate(roofs) if i != dom] + extra, "cpu_baseline": cpu,
+    }
+    del job, staged, evs  # the next measurement's buffers take their place
+    import gc
+    gc.collect()
+    torch.cuda.synchronize(dev)
+    torch.cuda.empty_cache()
+    return line
+
+
 def main():
     args = parse()
     CURRENT_CONFIG[0] = args.config
     if args.config == 1:
-        return cpu_mel_only(args)
+        print(json.dumps(cpu_mel_only(args)), flush=True)
+        return
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -233,64 +324,27 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=dev)
 
-    from heybuddy.synthetic import seed_for
-    setup = {2: setup_featurize, 3: setup_featurize, 4: setup_train, 5: setup_e2e}[args.config]
-    job = setup(args, dev, rank, world, seed_for(args.config, rank))
-    stream = torch.cuda.current_stream(dev)
-
-    staged = job.get("staged_step")  # overlapped stages: timed per stage in separate sequential steps
-    n_ev = args.stage_steps if staged else args.steps
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(len(job["stages"]) + 1)] for _ in range(n_ev)]
-    if staged:  # before the pipelined warmup, which leaves the next chunk's features pending
-        staged(None)
-        prof_mark(3, dev)
-        for k in range(n_ev):
-            staged(evs[k])
-        torch.cuda.synchronize(dev)
-        prof_mark(4, dev)
-    for _ in range(args.warmup):
-        job["step"](None)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    prof_mark(1, dev)
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        job["step"](None if staged else evs[k])
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    prof_mark(2, dev)
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
-    stage_ms = [sum(e[i].elapsed_time(e[i + 1]) for e in evs) / n_ev for i in range(len(job["stages"]))]
-    if "rooflines" in job:  # per kernel group (sub-stages timed on their own); the dominant one leads
-        roofs = job["rooflines"](dict(zip(job["stages"], stage_ms)), args.pmc)
-    else:
-        roofs = [job["roofline"](name, ms, args.pmc) for name, ms in zip(job["stages"], stage_ms)]
-    # the dominant kernel group by device time (a stage summary that only aggregates
-    # groups listed on their own is never the headline entry)
-    dom = max(range(len(roofs)), key=lambda i: (not roofs[i].get("summary"), roofs[i]["ms_per_step"]))
-
-    extra = job["extra_rooflines"]() if "extra_rooflines" in job and world == 1 else []
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = job["cpu_baseline"](args.cpu_sample)
-
+    line = measure(args, dev, rank, world)
+    if args.config == 5 and world > 1 and args.train_batch == "per-rank":
+        # the reference's optimisation on N GPUs: the global batch of 1,100 split over
+        # the ranks, N x 1,000 steps per chunk; measured beside the weak-scaling value and named
+        g = measure(sub_args(args, 5, train_batch="global"), dev, rank, world, marks=False)
+        line["faithful_global_batch"] = {
+            k: g[k] for k in ("value", "unit", "steps", "warmup", "ms_per_step", "config", "roofline")}
+        line["faithful_global_batch"]["note"] = (
+            "the reference's training on N GPUs: global batch 1,100 split over the ranks (SURVEY §8e-2), "
+            "N x 1,000 sequential train steps per chunk of N x 100 k clips; `value` above is the weak-scaling "
+            "mode (1,100 per rank, 1,000 steps per rank)")
+    others = [int(c) for c in args.other_configs.split(",") if c.strip()] if args.config == 5 else []
+    if others:
+        line["configs_other"] = []
+    for c in others:  # BASELINE configs[c - 1] in the same run, after the headline
+        if c == 1:
+            if rank == 0 and world == 1:
+                line["configs_other"].append(cpu_mel_only(sub_args(args, 1)))
+            continue
+        line["configs_other"].append(measure(sub_args(args, c), dev, rank, world, marks=False))
     if rank == 0:
-        units = job["units_per_step"] * (world if job["scaling"] == "weak" else 1)
-        value = units * args.steps / elapsed
-        line = {
-            "metric": job["metric"], "value": round(value, 1), "unit": job["unit"], "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": job["scaling"], "vs_baseline": None, "dtype": "f32",
-            "data": job["data"], "config": job["config"], "roofline": roofs[dom],
-            "roofline_other": [r for i, r in enumerate(roofs) if i != dom] + extra, "cpu_baseline": cpu,
-        }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -562,7 +616,7 @@ def cpu_mel_only(args):
                        "clips": int(nn), "threads": threads, "cpu_model": cpu_model()},
             "cpu_1thread": {"value": round(runs[1][0], 1), "unit": "clips/s", "cores": 1,
                             "sample": f"{runs[1][1]} clips, {runs[1][2]:.1f} s"}}
-    print(json.dumps(line), flush=True)
+    return line
 
 
 # --------------------------------------------------------------- config 5 ----

@@ -138,11 +138,17 @@ __device__ __forceinline__ void lds_barrier() {
 #ifdef HBK_TRACE
 // Tracing build only (lib/libhbk_trace.so, tools/probe_mlp.py): lane 0 of every
 // wave of block 0 records (mark << 56 | s_memtime) at stage marks of k1 / k2 / k3.
-__device__ unsigned long long g_mlp_trace[6][4][128];
-__device__ int g_mlp_trace_n[6][4];
+// Slots: kTraceKerns kernels x kTraceWaves waves. Every mark is bound-checked on
+// both (r04: the k4 marks at kernel slots 4 and 5 wrote past a [4]-kernel array --
+// the hipErrorIllegalAddress of gpurun_out/trace64.log -- until the array grew to 6).
+constexpr int kTraceKerns = 6, kTraceWaves = 4;
+static_assert(kTraceWaves * 64 >= 256, "every traced kernel runs <= 256 threads (4 waves)");
+__device__ unsigned long long g_mlp_trace[kTraceKerns][kTraceWaves][128];
+__device__ int g_mlp_trace_n[kTraceKerns][kTraceWaves];
 #define HBK_MTB(kern, id, blk)                                                                       \
   do {                                                                                         \
-    if (blockIdx.x == (blk) && (threadIdx.x & 63) == 0) {                                          \
+    static_assert((kern) >= 0 && (kern) < kTraceKerns, "trace kernel slot out of range");     \
+    if (blockIdx.x == (blk) && (threadIdx.x & 63) == 0 && (threadIdx.x >> 6) < kTraceWaves) {   \
       const int w_ = threadIdx.x >> 6;                                                          \
       const int n_ = g_mlp_trace_n[kern][w_];                                                   \
       if (n_ < 128) {                                                                           \
@@ -667,7 +673,7 @@ struct K2Args {
 #ifdef HBK_TRACE
 #define K2_MARK(id)                                                                \
   do {                                                                             \
-    if (blockIdx.x == 0 && lane == 0 && trn < 48)                                  \
+    if (blockIdx.x == 0 && lane == 0 && wave < kTraceWaves && trn < 48)            \
       trS[wave][trn++] = (static_cast<unsigned long long>(id) << 56) |             \
                          (__builtin_amdgcn_s_memtime() & 0xFFFFFFFFFFFFFFull);     \
   } while (0)
@@ -1089,7 +1095,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
   }
   K2_MARK(99);
 #ifdef HBK_TRACE
-  if (blockIdx.x == 0 && lane == 0) {
+  if (blockIdx.x == 0 && lane == 0 && wave < kTraceWaves) {
     for (int i = 0; i < trn; ++i) g_mlp_trace[1][wave][i] = trS[wave][i];
     g_mlp_trace_n[1][wave] = trn;
   }
@@ -2593,10 +2599,11 @@ int mlp_eval_finish(const float* cv, const float* ct, const double* sizes, float
 
 #ifdef HBK_TRACE
 extern "C" int hbk_debug_mlp_trace(unsigned long long* out, int* counts) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hbk::g_mlp_trace), sizeof(unsigned long long) * 6 * 4 * 128) != hipSuccess)
+  static_assert(sizeof(hbk::g_mlp_trace) == sizeof(unsigned long long) * 6 * 4 * 128, "probe_mlp.py's buffer");
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hbk::g_mlp_trace), sizeof(hbk::g_mlp_trace)) != hipSuccess) return -2;
+  if (hipMemcpyFromSymbol(counts, HIP_SYMBOL(hbk::g_mlp_trace_n), sizeof(hbk::g_mlp_trace_n)) != hipSuccess)
     return -2;
-  if (hipMemcpyFromSymbol(counts, HIP_SYMBOL(hbk::g_mlp_trace_n), sizeof(int) * 24) != hipSuccess) return -2;
-  int z[24] = {};
+  int z[hbk::kTraceKerns * hbk::kTraceWaves] = {};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(hbk::g_mlp_trace_n), z, sizeof(z));
   return 0;
 }

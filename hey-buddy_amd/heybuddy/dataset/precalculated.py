@@ -100,12 +100,9 @@ class PrecalculatedDatasetIterator:
             np.random.shuffle(self.indexes)
         return self
 
-    def take(self, n: int, _depth: int = 0) -> np.ndarray:
-        """The next n rows of the (shuffled) order; at the end the order is
-        reshuffled and the batch continues from its start (precalculated.py:501-536).
-        Rows whose token row holds an excluded token are dropped and refilled
-        from the following rows, as the reference does (:520-533); a set whose
-        every row is excluded raises instead of recursing without end."""
+    def _next_rows(self, n: int) -> np.ndarray:
+        """The next n rows of the (shuffled) order, reshuffling at the end and
+        continuing from its start (precalculated.py:508-517)."""
         batch = self.precalculated[self.indexes[self.index:self.index + n]]
         if batch.shape[0] < n:
             self.index = n - batch.shape[0]
@@ -113,18 +110,38 @@ class PrecalculatedDatasetIterator:
             batch = np.concatenate([batch, self.precalculated[self.indexes[:self.index]]])
         else:
             self.index += n
-        if self.labeled:
-            if self.exclude_tokens:
-                keep = np.array([self.exclude_tokens.isdisjoint(set(np.asarray(r[-1]).astype(np.int64).ravel()))
-                                 for r in batch], dtype=bool)
-                batch = batch[keep]
-            batch = batch[:, :-1]
-            if batch.shape[0] < n:  # refill what the exclusion removed
-                if batch.shape[0] == 0 and _depth > len(self) // max(n, 1) + 1:
-                    raise ValueError(f"{self.name}: every row contains an excluded token")
-                batch = np.concatenate([batch, self.take(n - batch.shape[0], _depth + 1)])
-        self.total_taken += n
         return batch
+
+    def take(self, n: int) -> np.ndarray:
+        """The next n rows of the (shuffled) order; at the end the order is
+        reshuffled and the batch continues from its start (precalculated.py:501-536).
+        Rows whose token row holds an excluded token are dropped and refilled
+        from the following rows, as the reference does (:520-533) -- there by
+        recursion, here by a loop (the same rows in the same order, and the
+        same total_taken: every refill counts its own request), so a set that
+        keeps only a few rows per lap fills any n without Python's recursion
+        limit. A full lap of the set that adds no row raises ValueError."""
+        parts = []
+        want = n
+        scanned_dry = 0  # rows read since a row was last kept
+        while True:
+            batch = self._next_rows(want)
+            if self.labeled:
+                if self.exclude_tokens:
+                    keep = np.array([self.exclude_tokens.isdisjoint(set(np.asarray(r[-1]).astype(np.int64).ravel()))
+                                     for r in batch], dtype=bool)
+                    batch = batch[keep]
+                batch = batch[:, :-1]
+            self.total_taken += want
+            parts.append(batch)
+            got = batch.shape[0]
+            if got >= want or not self.labeled:
+                break
+            scanned_dry = 0 if got else scanned_dry + want
+            if scanned_dry >= max(len(self), 1):
+                raise ValueError(f"{self.name}: every row contains an excluded token")
+            want -= got
+        return parts[0] if len(parts) == 1 else np.concatenate(parts)
 
     def iterate(self) -> Iterator[np.ndarray]:
         while True:

@@ -21,10 +21,11 @@ import torch
 import torch.distributed as dist
 
 
-def world() -> Tuple[int, int]:
-    """(rank, world size); (0, 1) when torch.distributed is not initialised."""
+def world(group: Optional[dist.ProcessGroup] = None) -> Tuple[int, int]:
+    """(rank, world size) in ``group`` (default the world); (0, 1) when
+    torch.distributed is not initialised."""
     if dist.is_available() and dist.is_initialized():
-        return dist.get_rank(), dist.get_world_size()
+        return dist.get_rank(group), dist.get_world_size(group)
     return 0, 1
 
 
@@ -71,15 +72,24 @@ def reduce_bucket(bucket: torch.Tensor, group: Optional[dist.ProcessGroup] = Non
     return bucket
 
 
-def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
-    """Overwrite t with rank src's copy on every rank (in place; a device tensor
-    goes through the host on gloo). No-op without a process group."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+def reduce_counts(counts: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
+    """Sum the evaluation passes' prediction counts over the ranks (in place;
+    float32 counts are exact below 2^24 rows). No-op on one rank."""
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
+    return counts
+
+
+def broadcast_(t: torch.Tensor, src: int = 0, group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
+    """Overwrite t with rank src's copy on every rank of ``group`` (in place; a
+    device tensor goes through the host on gloo). No-op without a process
+    group."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
         return t
-    if dist.get_backend() == "gloo" and t.device.type != "cpu":
+    if dist.get_backend(group) == "gloo" and t.device.type != "cpu":
         h = t.detach().cpu()
-        dist.broadcast(h, src)
+        dist.broadcast(h, src, group=group)
         t.copy_(h)
     else:
-        dist.broadcast(t, src)
+        dist.broadcast(t, src, group=group)
     return t

@@ -21,6 +21,7 @@ record with the reference's bookkeeping rules (trainer.py:443-494).
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 import random
@@ -70,10 +71,22 @@ class Trainer(nn.Module):
         self.learning_rate = learning_rate
         self.optimizer = torch.optim.Adam(self.model.parameters(), lr=learning_rate)
         self._init_state()
-        # data-parallel: every rank starts from rank 0's initial weights (the
-        # identical all-reduced Adam updates then keep them identical)
+        self._weights_synced = False
+
+    def sync_initial_weights(self, group: Optional["dist.ProcessGroup"] = None) -> None:
+        """Data-parallel: overwrite this rank's parameters with rank 0's, so that
+        every rank starts from the same weights (the identical all-reduced Adam
+        updates then keep them identical). A collective over ``group``: the
+        first data-parallel train call (train_epoch's steps, train_indexed)
+        runs it; constructing a trainer is rank-local (a rank-0-only export or
+        evaluation tool builds one without a partner)."""
         with torch.no_grad():
-            distributed.broadcast_(self.model.flat_parameters)
+            distributed.broadcast_(self.model.flat_parameters, group=group)
+        self._weights_synced = True
+
+    def _ensure_synced(self) -> None:
+        if not self._weights_synced and distributed.reduces():
+            self.sync_initial_weights()
 
     def create_model(self, **kwargs: Any) -> nn.Module:
         raise NotImplementedError()
@@ -205,6 +218,13 @@ class EvalPasses:
     covers whole laps of a pool reads every row equally often, as the
     reference's permutations do).
 
+    Data-parallel (``group``, default the world): every rank evaluates a
+    contiguous 1/W share of each pass's rows of its own pools, and the [2, 4]
+    counts are summed with one all-reduce before the bookkeeping, so the
+    false-positive rate, recall and the dynamic negative weight written into
+    ``sched`` are the same on every rank (one global weight, as in the
+    reference) and a pass costs each rank 1/W of its rows.
+
     ``run(sched, next_step)`` enqueues one validation (+ testing) pass on the
     current stream; the metrics land in ``history[k]`` = (false positives per
     hour, recall, testing false-positive rate, testing recall, testing
@@ -218,8 +238,9 @@ class EvalPasses:
                  target_false_positive_rate: float = DEFAULT_TARGET_FALSE_POSITIVE_RATE,
                  adjust_ratio: Optional[float] = DEFAULT_NEGATIVE_WEIGHT_ADJUST_RATIO,
                  activation_threshold: float = DEFAULT_ACTIVATION_THRESHOLD, seed: int = 0,
-                 history_cap: int = 256) -> None:
+                 history_cap: int = 256, group: Optional["dist.ProcessGroup"] = None) -> None:
         self.trainer = trainer
+        self.group = group
         dev = trainer.device
         pv, nv = validation_batch
         if validation_batches is None:
@@ -257,6 +278,16 @@ class EvalPasses:
     def rows_per_pass(self) -> int:
         return sum(r for _, r, _, _ in self.parts)
 
+    def run_metrics(self) -> List[float]:
+        """One pass (run() without a schedule), then its 8 metrics on the host:
+        the train_epoch form (one device -> host read per validation step)."""
+        saved, self.ratio = self.ratio, 0.0  # the caller applies the weight rule
+        try:
+            self.run()
+        finally:
+            self.ratio = saved
+        return [float(v) for v in self.history[(self.n - 1) % self.history.shape[0]].tolist()]
+
     def run(self, sched: Optional[torch.Tensor] = None, next_step: int = 0) -> None:
         tr = self.trainer
         plan = tr.model.plan
@@ -273,22 +304,34 @@ class EvalPasses:
         # (HBK_EVAL_SIDE=1 turns it on): in the pipelined headline the extra queue cost
         # the featurize stream ~3 ms per 100 k-clip step (881 / 875 k against 857 / 853 k
         # clips/s, same box, alternating)
-        cur = torch.cuda.current_stream(self.trainer.device)
+        cuda = self.trainer.device.type == "cuda"
+        cur = torch.cuda.current_stream(self.trainer.device) if cuda else None
         side = None
-        if self.side and any(pool.dtype == torch.float32 for pool, _, _, _ in self.parts):
+        if cuda and self.side and any(pool.dtype == torch.float32 for pool, _, _, _ in self.parts):
             side, self._side_keep = capture_stream(self.trainer.device)
             if self._side_keep is None:  # not a CU-masked stream
                 side = None
             else:
                 side.wait_stream(cur)
+        rank, world = distributed.world(self.group)
         for k, (pool, rows, label, which) in enumerate(self.parts):
-            with torch.cuda.stream(side if side is not None and pool.dtype == torch.float32 else cur):
-                plan.eval_count(flat, pool, rows, label, self.counts[which], self.ws, row_offset=self.offsets[k],
-                                activation_threshold=self.act_thr, dropout_p=p,
-                                seed=(self.seed + 0x9E3779B97F4A7C15 * (self.n * 8 + k + 1)) % (1 << 64))
+            # data-parallel: this rank's contiguous share of the pass's rows (the
+            # shares partition the pass); the per-rank dropout stream differs
+            lo, hi = distributed.clip_range(rows, rank, world)
+            if hi > lo:
+                with torch.cuda.stream(side if side is not None and pool.dtype == torch.float32 else cur) \
+                        if cuda else contextlib.nullcontext():
+                    plan.eval_count(flat, pool, hi - lo, label, self.counts[which], self.ws,
+                                    row_offset=(self.offsets[k] + lo) % pool.shape[0],
+                                    activation_threshold=self.act_thr, dropout_p=p,
+                                    seed=(self.seed + 0x9E3779B97F4A7C15 * (self.n * 8 + k + 1)
+                                          + 0xD1B54A32D192ED03 * rank) % (1 << 64))
             self.offsets[k] = (self.offsets[k] + rows) % pool.shape[0]
         if side is not None:
             cur.wait_stream(side)
+        # one all-reduce of the [2, 4] counts: every rank computes the same rates and
+        # the same next negative weight (the reference keeps one global weight)
+        distributed.reduce_counts(self.counts, self.group)
         plan.eval_finish(self.counts[0], self.counts[1] if self.testing else None, self.sizes,
                          self.history[self.n % self.history.shape[0]], target=self.target, ratio=self.ratio,
                          sched=sched, next_step=next_step)
@@ -339,6 +382,7 @@ class WakeWordTrainer(Trainer):
 
     def _step(self, x: torch.Tensor, y: torch.Tensor, lr: float, neg_weight: float, threshold: float,
               activation_threshold: float, history: Optional[torch.Tensor], seed: int) -> None:
+        self._ensure_synced()
         rank, world = self._world()
         x, y = distributed.shard_batch(x, y, rank, world)
         dev = self.device
@@ -463,6 +507,7 @@ class WakeWordTrainer(Trainer):
         one all-reduce of the bucket per step."""
         if not self._fused:
             raise NotImplementedError("train_indexed needs the fused train step (default architecture)")
+        self._ensure_synced()
         dev = self.device
         plan = self.model.plan
         flat = self.model.flat_parameters
@@ -509,7 +554,7 @@ class WakeWordTrainer(Trainer):
         def graph_of(n: int) -> "torch.cuda.CUDAGraph":
             """The captured graph of n (even) steps from the current parity."""
             key = ("indexed", n, self._parity, B, y_stride, float(threshold), float(activation_threshold), float(p),
-                   ptrs, torch.cuda.current_stream(dev).cuda_stream)
+                   defer, pre, ptrs, torch.cuda.current_stream(dev).cuda_stream)
             entry = self._graphs.get(key)
             if entry is not None:
                 return entry[0]
@@ -641,7 +686,12 @@ class WakeWordTrainer(Trainer):
                     last_validation_recall: float = 0.0, last_testing_accuracy: float = 0.0,
                     last_testing_recall: float = 0.0, last_testing_false_positive_rate: float = 0.0,
                     use_wandb: bool = False) -> Tuple[Optional[torch.Tensor], ...]:
-        """One epoch (trainer.py:314-608). Returns the reference's 11 histories."""
+        """One epoch (trainer.py:314-608). Returns the reference's 11 histories.
+
+        ``validation`` / ``testing``: iterables of (x, y) batches, evaluated by
+        the HIP forward batch by batch (_predict_all: the CLI's dataset
+        iterators), or ``validation`` an EvalPasses over HBM-resident pools
+        (validation and testing in one device pass each, ``testing`` None)."""
         if use_wandb:
             logger.warning("wandb logging is outside the MI355X hot path; ignored")
         self._reset_accumulation(salt=random.getrandbits(24))
@@ -679,7 +729,25 @@ class WakeWordTrainer(Trainer):
             batch_sizes.append(int(y.shape[0]))
             self._step(x, y, lr, nw, high_loss_threshold, activation_threshold, history, seed0 + step)
             if step > 0 and step % validation_steps == 0:
-                if validation is not None:
+                if isinstance(validation, EvalPasses):
+                    # HBM-resident pools: the passes on the device (hbk_mlp_eval_*), one
+                    # host read of the pass's 8 metrics; the weight rule stays on the host
+                    vals = validation.run_metrics()
+                    fph = vals[0]
+                    v_fp.append(fph)
+                    v_rec.append(vals[1])
+                    if validation.testing:
+                        t_fp.append(vals[2])
+                        t_rec.append(vals[3])
+                        t_acc.append(vals[4])
+                    if negative_weight_adjust_ratio is not None:
+                        assert isinstance(negative_weight_schedule, float), \
+                            "Negative weight schedule must be a float when using dynamic negative weight adjustment."
+                        if fph > target_false_positive_rate:
+                            negative_weight_schedule = negative_weight_schedule * negative_weight_adjust_ratio
+                        else:
+                            negative_weight_schedule = max(1.0, negative_weight_schedule / negative_weight_adjust_ratio)
+                elif validation is not None:
                     preds, labels = self._predict_all(validation)
                     n_neg = int((labels == 0).sum().item())
                     hours = n_neg * 1.44 / 3600
@@ -697,7 +765,7 @@ class WakeWordTrainer(Trainer):
                             negative_weight_schedule = negative_weight_schedule * negative_weight_adjust_ratio
                         else:
                             negative_weight_schedule = max(1.0, negative_weight_schedule / negative_weight_adjust_ratio)
-                if testing is not None:
+                if testing is not None and not isinstance(validation, EvalPasses):
                     preds, labels = self._predict_all(testing)
                     n_neg = max(int((labels == 0).sum().item()), 1)
                     t_fp.append(float(self.num_false_positives(preds, labels, activation_threshold).item()) / n_neg)
@@ -709,7 +777,7 @@ class WakeWordTrainer(Trainer):
                 if validation is not None:
                     v_fp.append(v_fp[-1])
                     v_rec.append(v_rec[-1])
-                if testing is not None:
+                if testing is not None or (isinstance(validation, EvalPasses) and validation.testing):
                     t_fp.append(t_fp[-1])
                     t_rec.append(t_rec[-1])
                     t_acc.append(t_acc[-1])
@@ -717,7 +785,7 @@ class WakeWordTrainer(Trainer):
                 if validation is not None:
                     v_fp.append(last_validation_false_positive_per_hour)
                     v_rec.append(last_validation_recall)
-                if testing is not None:
+                if testing is not None or (isinstance(validation, EvalPasses) and validation.testing):
                     t_fp.append(last_testing_false_positive_rate)
                     t_rec.append(last_testing_recall)
                     t_acc.append(last_testing_accuracy)

@@ -108,7 +108,10 @@ def _init_worker(rank, world, port, q, tmp):
     # a rank whose generator differs on its own: the broadcast from rank 0 still aligns the weights
     torch.manual_seed(99 + rank)
     tr2 = WakeWordTrainer(checkpoint_dir=os.path.join(tmp, f"ck{rank}b"), device="cpu")
-    q.put((rank, feats.shape, after, flat_shared.numpy(), tr2.model.flat_parameters.clone().numpy()))
+    own = tr2.model.flat_parameters.clone().numpy()  # construction is rank-local: no collective
+    tr2._ensure_synced()  # what the first data-parallel train call runs
+    assert tr2._weights_synced
+    q.put((rank, feats.shape, after, flat_shared.numpy(), tr2.model.flat_parameters.clone().numpy(), own))
     dist.destroy_process_group()
 
 
@@ -132,3 +135,114 @@ def test_dp_ranks_start_from_the_same_weights(tmp_path):
     np.testing.assert_array_equal(res[0][3], res[1][3])
     np.testing.assert_array_equal(res[0][4], res[1][4])
     assert np.abs(res[0][4]).sum() > 0
+    assert np.abs(res[0][5] - res[1][5]).max() > 0  # before the sync the ranks' weights differed
+    np.testing.assert_array_equal(res[1][4], res[0][5])  # ... and rank 0's won
+
+
+def _eval_worker(rank, world, port, q):
+    """EvalPasses.run on CPU with a stand-in plan whose eval_count is the
+    oracle forward (the kernels need a GPU): which rows each rank evaluates,
+    the reduced counts and the negative weight written into sched."""
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "hey-buddy_amd")]
+    if world > 1:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    from heybuddy.trainer import EvalPasses
+    q.put((rank, *_run_eval_passes(EvalPasses)))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+class _OraclePlan:
+    """eval_* of the HIP plan restated on the host (test infrastructure)."""
+
+    def __init__(self, params):
+        self.params = params
+        self.seen = []
+
+    def eval_workspace_bytes(self, rows):
+        return 0
+
+    def eval_prepare(self, flat, ws):
+        pass
+
+    def eval_count(self, flat, pool, rows, label, counts, ws, row_offset=0, activation_threshold=0.5,
+                   dropout_p=0.0, seed=0):
+        from oracle import mlp as omlp
+        n = pool.shape[0]
+        r = (row_offset + np.arange(rows)) % n
+        self.seen.append((id(pool), r))
+        prob, _, _ = omlp.forward(self.params, pool[r].float().numpy())
+        counts[2 * label] += float((prob >= activation_threshold).sum())
+        counts[2 * label + 1] += float((prob > activation_threshold).sum())
+
+    @staticmethod
+    def eval_finish(cv, ct, sizes, out, target=1.5, ratio=0.0, sched=None, next_step=0):
+        fph = float(cv[1]) / (sizes[0] * 1.44 / 3600)  # negatives predicted positive per hour
+        w0 = float(sched[next_step - 1, 1]) if next_step > 0 else 1.0
+        w = w0 * ratio if fph > target else max(1.0, w0 / ratio)
+        out[0], out[5], out[6] = fph, w, w0
+        sched[next_step:, 1] = w
+
+
+def _run_eval_passes(EvalPasses):
+    from oracle import mlp as omlp
+    params = omlp.init_params(seed=4)
+    rng = np.random.default_rng(3)
+    pools = [torch.from_numpy(rng.standard_normal((n, 16, 96)).astype(np.float32) + off)
+             for n, off in ((130, 0.3), (410, 0.0), (90, 0.2), (95, -0.1))]
+    pools[1] = pools[1].half()
+
+    class _Model:
+        training = False
+        dropout = type("D", (), {"p": 0.0})()
+        flat_parameters = torch.zeros(1)
+        plan = _OraclePlan(params)
+
+    class _Trainer:
+        device = torch.device("cpu")
+        model = _Model()
+
+    tr = _Trainer()
+    ev = EvalPasses(tr, pools[0], pools[1], pools[2], pools[3], validation_batch=(20, 100),
+                    testing_batch=(20, 20), adjust_ratio=2.0, target_false_positive_rate=1e9)
+    sched = torch.ones((12, 2))
+    ev.run(sched, next_step=4)
+    ev.run(sched, next_step=8)
+    seen = [(next(i for i, p in enumerate(pools) if id(p) == pid), r) for pid, r in tr.model.plan.seen]
+    return ev.counts.numpy().copy(), sched.numpy().copy(), ev.history[:2].numpy().copy(), seen
+
+
+def test_eval_passes_shard_rows_and_agree_on_the_weight():
+    """data-parallel evaluation passes. Every rank
+    evaluates a contiguous share of each pass's rows (the shares partition the
+    pass), the counts are all-reduced before the bookkeeping, so both ranks
+    hold the counts of the whole pass and write the same negative weight into
+    sched -- the same as one process evaluating every row."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_eval_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in procs], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "hey-buddy_amd")]
+    from heybuddy.trainer import EvalPasses
+    c1, s1, h1, seen1 = _run_eval_passes(EvalPasses)  # one process
+    for r in res:
+        np.testing.assert_array_equal(r[1], c1)
+        np.testing.assert_array_equal(r[2], s1)
+        np.testing.assert_array_equal(r[3], h1)
+    # the ranks' rows partition the single process's rows, call by call
+    assert len(res[0][4]) == len(res[1][4]) == len(seen1)
+    for (p0, r0), (p1, r1), (p, r) in zip(res[0][4], res[1][4], seen1):
+        assert p0 == p1 == p
+        np.testing.assert_array_equal(np.concatenate([r0, r1]), r)
+        assert abs(len(r0) - len(r1)) <= 1
+    assert s1[4:, 1].max() == 0.5 or s1[4:, 1].min() >= 1.0  # the weight was written from step 4 on

@@ -122,3 +122,43 @@ def test_eval_finish_matches_reference_bookkeeping():
         np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-6)
         s = sched.cpu().numpy()
         assert (s[:4, 1] == nw0).all() and (s[4:, 1] == np.float32(ref[5])).all()
+
+
+def test_train_epoch_with_device_eval_passes_matches_host_batches(tmp_path):
+    """train_epoch takes an EvalPasses over HBM pools as
+    its validation (the device passes, one host read per validation step)
+    and reports the same validation / testing histories and dynamic negative
+    weight as the same rows fed as host (x, y) batches through the HIP
+    forward (_predict_all). Dropout off; the pools are whole batches, so both
+    paths see exactly the same rows."""
+    from heybuddy.trainer import EvalPasses, WakeWordTrainer
+    rng = np.random.default_rng(21)
+    vpos = torch.from_numpy((rng.standard_normal((100, 16, 96)) + 0.4).astype(np.float32)).cuda()
+    vneg = torch.from_numpy(rng.standard_normal((400, 16, 96)).astype(np.float16)).cuda()
+    tpos = torch.from_numpy((rng.standard_normal((60, 16, 96)) + 0.4).astype(np.float32)).cuda()
+    tadv = torch.from_numpy((rng.standard_normal((60, 16, 96)) - 0.1).astype(np.float32)).cuda()
+    xb = [torch.from_numpy(rng.standard_normal((64, 16, 96)).astype(np.float32) + 0.1 * (i % 2)) for i in range(9)]
+    yb = [torch.cat([torch.ones(20), torch.zeros(44)]).long() for _ in range(9)]
+    training = list(zip(xb, yb))
+    # the same rows as host batches: validation 2 x (50 positives + 200 negatives), testing 3 x (20 + 20)
+    val = [(torch.cat([vpos[50 * i:50 * i + 50], vneg[200 * i:200 * i + 200].float()]).cpu(),
+            torch.cat([torch.ones(50), torch.zeros(200)]).long()) for i in range(2)]
+    tst = [(torch.cat([tpos[20 * i:20 * i + 20], tadv[20 * i:20 * i + 20]]).cpu(),
+            torch.cat([torch.ones(20), torch.zeros(20)]).long()) for i in range(3)]
+    out = {}
+    for mode in ("host", "device"):
+        torch.manual_seed(3)
+        tr = WakeWordTrainer(checkpoint_dir=str(tmp_path / mode), device="cuda")
+        tr.model.dropout.p = 0.0
+        kw = dict(num_steps=9, warmup_steps=2, hold_steps=2, validation_steps=4, negative_weight_schedule=2.0,
+                  negative_weight_adjust_ratio=2.0, target_false_positive_rate=1e6)
+        if mode == "host":
+            h = tr.train_epoch(training, validation=val, testing=tst, **kw)
+        else:
+            ev = EvalPasses(tr, vpos, vneg, tpos, tadv, validation_batch=(50, 200), testing_batch=(20, 20))
+            assert ev.rows_per_pass == 500 + 120
+            h = tr.train_epoch(training, validation=ev, **kw)
+        out[mode] = h
+    for i in (1, 6, 7, 8, 9, 10):  # nw, vfp, vrecall, tacc, trecall, tfp
+        np.testing.assert_allclose(out["device"][i].numpy(), out["host"][i].numpy(), rtol=1e-6, atol=1e-6)
+    assert out["device"][1][-1] < 2.0  # the weight halved at the validations (fph under the target)

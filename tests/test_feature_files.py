@@ -110,3 +110,21 @@ def test_labeled_take_excludes_phrase_tokens(tmp_path):
     # the phrase tokens drop [CLS] / [SEP] (ref tokens.py:57), so a token row with them is not excluded
     dev = it.to_device("cpu")
     assert dev.shape == (n - len(range(0, n, 3)), 16, 96)
+
+
+def test_labeled_take_mostly_excluded_fills_without_recursion(tmp_path):
+    """a set that keeps one row in 50 fills take(n) far past
+    Python's recursion limit (the refill is a loop), with the reference's row
+    order: the kept rows of the shuffled order, lap after lap."""
+    from heybuddy.dataset.precalculated import PrecalculatedDatasetIterator
+    np.random.seed(1)
+    n = 500
+    arr = np.zeros((n, 17, 96), np.float16)
+    arr[:, :16] = (np.arange(n) % 2048).astype(np.float16)[:, None, None]
+    arr[:, 16, 0] = [5 if i % 50 else 6 for i in range(n)]  # rows 0, 50, ... kept
+    np.save(tmp_path / "sparse.npy", arr)
+    it = PrecalculatedDatasetIterator("sparse", directory=str(tmp_path), labeled=True, exclude_tokens=[5])
+    got = it.take(3000)  # 300 laps of the set
+    assert got.shape == (3000, 16, 96)
+    assert set(got[:, 0, 0].astype(int)) == set(range(0, n, 50))
+    assert it.total_taken >= 3000

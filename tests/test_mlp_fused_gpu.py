@@ -156,6 +156,62 @@ def test_train_indexed_equals_eager_steps(tmp_path):
     torch.testing.assert_close(s1, s0)
 
 
+def test_train_indexed_split_with_eval_between_equals_one_call(tmp_path):
+    """the headline splits every train chunk around the
+    evaluation passes with train_indexed(n_steps=..., continued=True), whose
+    first step relies on the previous call's last step having gathered its rows
+    and refreshed the weight cache. S steps in one call against the same S
+    steps split at k (an odd and an even split, each with an EvalPasses.run in
+    between that does not touch sched: ratio 0), dropout on."""
+    from heybuddy.trainer import EvalPasses, WakeWordTrainer
+    params = gc.golden_inputs()[0]
+    rng = np.random.default_rng(11)
+    S, npos, nneg = 14, 24, 100
+    pos = torch.from_numpy(rng.standard_normal((300, 16, 96)).astype(np.float32) + 0.7).cuda()
+    neg = torch.from_numpy(rng.standard_normal((500, 16, 96)).astype(np.float32)).half().cuda()
+    ip = np.stack([rng.choice(300, npos, replace=False) for _ in range(S)])
+    ineg = np.stack([rng.choice(500, nneg, replace=False) for _ in range(S)])
+    idx = torch.from_numpy(np.concatenate([ip, -ineg - 1], axis=1).astype(np.int32)).cuda()
+    y = torch.from_numpy(np.concatenate([np.ones(npos), np.zeros(nneg)]).astype(np.float32)).cuda()
+    lr = np.linspace(1e-4, 1e-3, S).astype(np.float32)
+    sched0 = torch.from_numpy(np.stack([lr, np.full(S, 1.5, np.float32)], 1)).cuda()
+    runs = {}
+    for split in (None, (5,), (4, 9)):
+        tr = WakeWordTrainer(checkpoint_dir=str(tmp_path / str(split)), device="cuda")
+        tr.model.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=True)
+        tr.model.train()  # dropout 0.1 on: the prefetched rows carry the next step's mask
+        tr._seed_base_v = 12345
+        tr._reset_accumulation()
+        hist = torch.zeros((S, 8), device="cuda")
+        sched = sched0.clone()
+        if split is None:
+            tr.train_indexed(idx, y, sched, pool32=pos, pool16=neg, history=hist, steps_per_graph=4)
+        else:
+            ev = EvalPasses(tr, pos[:100], neg[:200], pos[100:150], pos[150:200], validation_batch=(10, 50),
+                            testing_batch=(10, 10), adjust_ratio=0.0)
+            done = 0
+            for k in split:
+                tr.train_indexed(idx, y, sched, pool32=pos, pool16=neg, history=hist, steps_per_graph=4,
+                                 n_steps=k - done, continued=done > 0)
+                done = k
+                ev.run(sched, next_step=done)
+            tr.train_indexed(idx, y, sched, pool32=pos, pool16=neg, history=hist, steps_per_graph=4,
+                             n_steps=S - done, continued=True)
+            torch.testing.assert_close(sched, sched0, rtol=0, atol=0)  # ratio 0: the passes leave sched alone
+        torch.cuda.synchronize()
+        runs[split] = (tr.model.flat_parameters.clone(), hist.clone(), tr._fstate.clone())
+    p0, h0, s0 = runs[None]
+    for split in ((5,), (4, 9)):
+        p1, h1, s1 = runs[split]
+        # as test_train_indexed_equals_eager_steps: counts / gate / selection, loss and parameters
+        # to the float-atomic summation order (a wrong first step after a split moves them all)
+        np.testing.assert_allclose(h1[:, [0, 2, 4, 5, 6, 7]].cpu().numpy(), h0[:, [0, 2, 4, 5, 6, 7]].cpu().numpy())
+        np.testing.assert_allclose(h1[:, 3].cpu().numpy(), h0[:, 3].cpu().numpy(), rtol=1e-4)
+        d = (p1 - p0).abs()
+        assert float((d > 1e-5).float().mean()) < 1e-3 and float(d.max()) <= 2e-2
+        torch.testing.assert_close(s1, s0)
+
+
 @pytest.mark.parametrize("B", [1, 100, 273, 500, 550, 1000, 1100, 2000, 5000])
 def test_fused_forward_matches_oracle(B):
     """Inference (hbk_mlp_forward: k1a + k1b + k2) against the oracle forward

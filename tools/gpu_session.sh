@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 GPU session: GPU tests + smoke, the driver's bench command, the train-step CU probe.
+# A GPU session: GPU tests + smoke, the driver's bench command (with configs_other), probes, profiles.
 # STEPS selects parts (default "tests bench cus"); every GPU step has its own time limit and
 # the first failure ends the script.
 set -o pipefail
@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 export TMPDIR=/tmp
 OUT=gpurun_out
 mkdir -p $OUT
-TAG=${TAG:-r04a}
+TAG=${TAG:-r05a}
 for S in ${STEPS:-tests bench cus}; do
   case $S in
     tests)
@@ -27,8 +27,8 @@ for S in ${STEPS:-tests bench cus}; do
         timeout -k 10 600 python bench.py --config $C > $OUT/${TAG}_bench_c$C.json 2> $OUT/${TAG}_bench_c$C.err || { tail -30 $OUT/${TAG}_bench_c$C.err; exit 1; }
         cut -c1-300 $OUT/${TAG}_bench_c$C.json
       done ;;
-    prof23)
-      for C in 2 3; do
+    prof234)
+      for C in 2 3 4; do
         echo "=== profile config $C"
         TAG=$TAG CONFIG=$C SKIP_BENCH=1 timeout -k 10 900 bash tools/profile_headline.sh > $OUT/${TAG}_prof_c$C.log 2>&1 || { tail -30 $OUT/${TAG}_prof_c$C.log; exit 1; }
         tail -3 $OUT/${TAG}_prof_c$C.log
@@ -45,6 +45,10 @@ for S in ${STEPS:-tests bench cus}; do
       echo "=== evaluation passes"
       timeout -k 10 500 bash tools/eval_probe.sh > $OUT/${TAG}_eval_probe.log 2>&1 || { tail -20 $OUT/${TAG}_eval_probe.log; exit 1; }
       cat $OUT/${TAG}_eval_probe.log ;;
+    trace64)
+      echo "=== train-step stage trace on a 64-CU stream (libhbk_trace.so)"
+      timeout -k 10 300 python tools/probe_mlp.py --trace --cus=64 > $OUT/${TAG}_trace64.log 2>&1 || { tail -20 $OUT/${TAG}_trace64.log; exit 1; }
+      tail -5 $OUT/${TAG}_trace64.log ;;
     cus)
       echo "=== train step per CU count"
       timeout -k 10 500 bash tools/mlp_cus.sh > $OUT/${TAG}_mlp_cus.log 2>&1 || { tail -20 $OUT/${TAG}_mlp_cus.log; exit 1; }

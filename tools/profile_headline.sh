@@ -14,7 +14,7 @@ OUT=gpurun_out
 mkdir -p $OUT
 TAG=${TAG:-r03a}
 C=${CONFIG:-5}
-BA="--config $C ${BENCH_ARGS:-}"
+BA="--config $C --other-configs= ${BENCH_ARGS:-}"
 SQ="SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE"
 
 if [ -z "$SKIP_BENCH" ]; then
