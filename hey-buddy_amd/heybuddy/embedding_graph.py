@@ -7,9 +7,15 @@ that is downloaded at run time and absent offline. Its topology and weights
 are therefore NOT known here. This module describes the network as a list of
 ops (Keras Conv2D 'valid' / LeakyReLU / MaxPool2D, NHWC) that libhbk.so
 executes generically; ``se20_graph()`` is a 20-conv stand-in with the same
-I/O signature and the same last node name, with seeded weights. A graph read
-from the real ONNX file (sha256 70d16429..., embeddings.py:30) can be passed in
-the same form once it is supplied out of band.
+I/O signature and the same last node name, with seeded weights.
+
+``from_onnx(path)`` reads the reference's own file (sha256 70d16429...,
+embeddings.py:29-30) -- or any graph in the Keras / tf2onnx layout: NHWC
+input ``input_1`` [n, 76, 32, 1], Transpose to NCHW, Conv (+ bias, or a bias
+Add), LeakyRelu / Relu, MaxPool, Transpose back, Reshape / Squeeze to
+``conv2d_19`` -- into this form, and raises on any op or attribute the HIP
+kernels do not implement. ``to_onnx(graph, path)`` writes a graph in that
+layout (so a graph trained or edited here deploys where the reference's does).
 """
 from __future__ import annotations
 
@@ -18,7 +24,7 @@ from typing import List, Optional, Sequence, Union
 
 import numpy as np
 
-__all__ = ["Conv", "MaxPool", "Graph", "se20_graph", "WINDOW_STARTS", "LEAKY_ALPHA"]
+__all__ = ["Conv", "MaxPool", "Graph", "se20_graph", "from_onnx", "to_onnx", "WINDOW_STARTS", "LEAKY_ALPHA"]
 
 LEAKY_ALPHA = 0.2
 
@@ -129,4 +135,151 @@ def se20_graph(seed: int = 1234) -> Graph:
         i_conv += 1
     g = Graph(ops, (76, 32, 1), name="se20")
     assert g.out_dim == 96
+    return g
+
+
+# -- ONNX (Keras / tf2onnx layout) ---------------------------------------------------
+_TO_NCHW = (0, 3, 1, 2)
+_TO_NHWC = (0, 2, 3, 1)
+
+
+def to_onnx(graph: Graph, path: str, input_name: str = "input_1", opset_version: int = 13) -> None:
+    """Write ``graph`` as tf2onnx writes a Keras Conv2D stack: NHWC input
+    [n, H, W, C] -> Transpose -> (Conv [Cout, Cin, kh, kw] + bias, LeakyRelu |
+    MaxPool)* -> Transpose -> output named after the last conv ([n, 1, 1, out])."""
+    from heybuddy.util.onnx_util import write_model
+    nodes, inits = [], {}
+    x = f"{input_name}__0"
+    nodes.append(("Transpose", "transpose_in", [input_name], [x], {"perm": list(_TO_NCHW)}))
+    last = max(i for i, op in enumerate(graph.ops) if isinstance(op, Conv))
+    n_pool = 0
+    for i, op in enumerate(graph.ops):
+        if isinstance(op, MaxPool):
+            name = op.name or f"max_pooling2d_{n_pool}"
+            n_pool += 1
+            y = f"{name}/MaxPool"
+            nodes.append(("MaxPool", y, [x], [y], {"kernel_shape": [op.ph, op.pw], "strides": [op.ph, op.pw]}))
+            x = y
+            continue
+        name = op.name or f"conv2d_{i}"
+        w, b = f"{name}/kernel", f"{name}/bias"
+        inits[w] = np.ascontiguousarray(op.weight.transpose(3, 2, 0, 1))  # HWIO -> OIHW
+        inits[b] = op.bias
+        y = f"{name}/BiasAdd"
+        nodes.append(("Conv", y, [x, w, b], [y], {"kernel_shape": [op.kh, op.kw], "strides": [1, 1],
+                                                  "dilations": [1, 1], "group": 1, "pads": [0, 0, 0, 0]}))
+        x = y
+        if op.act == "leaky_relu":
+            y = f"{name}/LeakyRelu"
+            nodes.append(("LeakyRelu", y, [x], [y], {"alpha": float(op.alpha)}))
+            x = y
+        if i == last:
+            out = name
+    h, w_, c = graph.shapes()[-1]
+    nodes.append(("Transpose", "transpose_out", [x], [out], {"perm": list(_TO_NHWC)}))
+    write_model(path, nodes, inits, [(input_name, ["unk__n", *graph.in_shape])], [(out, ["unk__n", h, w_, c])],
+                opset_version=opset_version, producer="tf2onnx-layout (heybuddy-amd)")
+
+
+def from_onnx(path: str, name: Optional[str] = None) -> Graph:
+    """The speech-embedding graph of an ONNX file as runtime data for the HIP
+    kernels (the reference's ``speech-embedding.onnx``, embeddings.py:23-42; I/O
+    ``input_1`` [n, 76, 32, 1] -> ``conv2d_19`` [n, 1, 1, 96],
+    speech-embedding.js:125-146). The graph must be one chain from the input:
+    layout Transposes (NHWC <-> NCHW), Conv (stride 1, dilation 1, group 1, no
+    padding) with its bias as the Conv's third input or a following Add of a
+    [C] / [1, C, 1, 1] constant, LeakyRelu / Relu after a conv, MaxPool (kernel
+    = stride, no padding), and trailing Reshape / Squeeze / Flatten / Identity
+    to the output. Anything else raises ValueError naming the node."""
+    from heybuddy.util.onnx_util import read_model
+    m = read_model(path)
+    if len(m.inputs) != 1 or len(m.outputs) != 1:
+        raise ValueError(f"{path}: expected one graph input and one output, got {m.inputs} / {m.outputs}")
+    (in_name, in_dims), (out_name, _) = m.inputs[0], m.outputs[0]
+    dims = tuple(in_dims[1:])
+    if len(dims) != 3 or any(d is None for d in dims):
+        raise ValueError(f"{path}: input {in_name!r} must be [n, H, W, C] (or [n, C, H, W]), got {in_dims}")
+    inits = m.initializers
+    ops: List[Op] = []
+    # the chain from the input; the layout of the tensor "x" (NHWC as Keras, or NCHW)
+    nchw = dims[0] == 1 and dims[2] != 1  # [n, 1, H, W]: a one-channel NCHW input
+    in_shape = (dims[1], dims[2], dims[0]) if nchw else dims
+    x = in_name
+    terminal = False
+
+    def const(name_: str) -> np.ndarray:
+        if name_ not in inits:
+            raise ValueError(f"{path}: {name_!r} must be a constant (initializer) for the HIP kernels")
+        return np.asarray(inits[name_], dtype=np.float32)
+
+    while x != out_name:
+        users = m.consumers(x)
+        if len(users) != 1:
+            raise ValueError(f"{path}: tensor {x!r} feeds {len(users)} nodes; only a single chain is supported")
+        node = users[0]
+        a = node.attrs
+        where = f"{path}: node {node.name!r} ({node.op})"
+        if terminal and node.op not in ("Reshape", "Squeeze", "Flatten", "Identity"):
+            raise ValueError(f"{where}: after a reshape only reshapes may follow")
+        if node.op == "Transpose":
+            perm = tuple(a.get("perm", ()))
+            if perm == _TO_NCHW and not nchw:
+                nchw = True
+            elif perm == _TO_NHWC and nchw:
+                nchw = False
+            else:
+                raise ValueError(f"{where}: unsupported permutation {perm}")
+        elif node.op == "Conv":
+            if not nchw:
+                raise ValueError(f"{where}: Conv on an NHWC tensor")
+            w = const(node.inputs[1])
+            if w.ndim != 4:
+                raise ValueError(f"{where}: only 2-D convolutions are supported")
+            co, ci, kh, kw = w.shape
+            if (tuple(a.get("strides", (1, 1))) != (1, 1) or tuple(a.get("dilations", (1, 1))) != (1, 1)
+                    or int(a.get("group", 1)) != 1 or any(a.get("pads", (0, 0, 0, 0)))
+                    or a.get("auto_pad", b"NOTSET") not in (b"NOTSET", b"VALID")):
+                raise ValueError(f"{where}: only stride-1, undilated, ungrouped 'valid' convolutions run on the "
+                                 f"HIP kernels (attributes {a})")
+            b = const(node.inputs[2]).reshape(-1) if len(node.inputs) > 2 and node.inputs[2] else np.zeros(co, np.float32)
+            ops.append(Conv(kh, kw, ci, co, w.transpose(2, 3, 1, 0), b, act=None,
+                            name=(node.name.split("/")[0] or f"conv2d_{len(ops)}")))
+        elif node.op == "Add":
+            prev = ops[-1] if ops else None
+            if not isinstance(prev, Conv) or prev.act is not None:
+                raise ValueError(f"{where}: an Add is supported only as a conv's bias")
+            other = node.inputs[1] if node.inputs[0] == x else node.inputs[0]
+            b = const(other)
+            ok = (b.size == prev.cout and (b.ndim == 1 or (nchw and b.shape[-3:] == (prev.cout, 1, 1))
+                                           or (not nchw and b.shape[-1] == prev.cout)))
+            if not ok:
+                raise ValueError(f"{where}: bias of shape {b.shape} does not broadcast over {prev.cout} channels")
+            prev.bias = np.ascontiguousarray(prev.bias + b.reshape(-1), dtype=np.float32)
+        elif node.op in ("LeakyRelu", "Relu"):
+            prev = ops[-1] if ops else None
+            if not isinstance(prev, Conv) or prev.act is not None:
+                raise ValueError(f"{where}: an activation is supported only right after a conv (+ bias)")
+            prev.act = "leaky_relu"
+            prev.alpha = float(np.float32(a.get("alpha", 0.01))) if node.op == "LeakyRelu" else 0.0
+        elif node.op == "MaxPool":
+            if not nchw:
+                raise ValueError(f"{where}: MaxPool on an NHWC tensor")
+            k = tuple(a.get("kernel_shape", ()))
+            s = tuple(a.get("strides", k))
+            if (len(k) != 2 or s != k or any(a.get("pads", (0, 0, 0, 0)))
+                    or a.get("auto_pad", b"NOTSET") not in (b"NOTSET", b"VALID")
+                    or int(a.get("ceil_mode", 0)) or tuple(a.get("dilations", (1, 1))) != (1, 1)):
+                raise ValueError(f"{where}: only non-overlapping unpadded max-pools are supported ({a})")
+            ops.append(MaxPool(k[0], k[1], name=node.name.split("/")[0]))
+        elif node.op in ("Reshape", "Squeeze", "Flatten", "Identity"):
+            terminal = node.op != "Identity" or terminal
+        else:
+            raise ValueError(f"{where}: op {node.op!r} is not supported by the HIP embedding kernels")
+        x = node.outputs[0]
+    if not any(isinstance(o, Conv) for o in ops):
+        raise ValueError(f"{path}: no convolution on the path from {in_name!r} to {out_name!r}")
+    g = Graph(ops, tuple(int(d) for d in in_shape), name=name or out_name)
+    h, w_, _ = g.shapes()[-1]  # also checks the channel chain
+    if (h, w_) != (1, 1):
+        raise ValueError(f"{path}: the graph ends at {g.shapes()[-1]}, not a [1, 1, C] embedding")
     return g

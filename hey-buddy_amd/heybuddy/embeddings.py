@@ -24,21 +24,28 @@ import numpy as np
 import torch
 
 from heybuddy import _native
-from heybuddy.embedding_graph import Graph, se20_graph
+from heybuddy.embedding_graph import Graph, from_onnx, se20_graph
 from heybuddy.kernels import EmbedPlan, default_embed_precision, embed_clips, embed_windows, mel_frames
-from heybuddy.spectrogram import HOP, MelSpectrogramModel, N_FFT, default_mel_plan
+from heybuddy.spectrogram import HOP, MelSpectrogramModel, N_FFT, default_mel_plan, find_pretrained
 from heybuddy.util import audio_to_bct_tensor, logger
 
-__all__ = ["SpeechEmbeddingModel", "SpeechEmbeddings", "get_speech_embeddings", "default_graph"]
+__all__ = ["SpeechEmbeddingModel", "SpeechEmbeddings", "get_speech_embeddings", "default_graph",
+           "set_default_graph", "REFERENCE_EMBED_SHA256"]
 
 _GRAPH: Optional[Graph] = None
 
 
+REFERENCE_EMBED_FILE = "speech-embedding.onnx"  # embeddings.py:29
+REFERENCE_EMBED_SHA256 = "70d164290c1d095d1d4ee149bc5e00543250a7316b59f31d056cff7bd3075c1f"  # embeddings.py:30
+
+
 def default_graph() -> Graph:
     """The speech-embedding graph. The reference downloads an ONNX file
-    (embeddings.py:29-30) that is not available offline; this build uses the
-    seeded SE20 stand-in (heybuddy.embedding_graph) unless a graph is
-    registered with ``set_default_graph``.
+    (embeddings.py:29-30); nothing is downloaded here. If that file -- the
+    reference's sha256 -- is in the pretrained directory
+    (``heybuddy.spectrogram.pretrained_dir()``), it is imported
+    (``embedding_graph.from_onnx``); a graph registered with
+    ``set_default_graph`` wins; otherwise the seeded SE20 stand-in.
 
     The stand-in has the reference graph's shapes and cost but seeded random
     weights: its embeddings are NOT those of the reference's speech-embedding
@@ -47,6 +54,11 @@ def default_graph() -> Graph:
     warning says so once per process."""
     global _GRAPH
     if _GRAPH is None:
+        path = find_pretrained(REFERENCE_EMBED_FILE, REFERENCE_EMBED_SHA256)
+        if path is not None:
+            _GRAPH = from_onnx(path)
+            logger.info(f"heybuddy: speech-embedding graph imported from {path}")
+            return _GRAPH
         seed = int(os.environ.get("HEYBUDDY_EMBEDDING_SEED", "1234"))
         _GRAPH = se20_graph(seed)
         logger.warning(
@@ -56,7 +68,9 @@ def default_graph() -> Graph:
     return _GRAPH
 
 
-def set_default_graph(graph: Graph) -> None:
+def set_default_graph(graph: Optional[Graph]) -> None:
+    """Use ``graph`` (e.g. ``embedding_graph.from_onnx(path)``) for every later
+    call; None: back to the default (the pretrained file or SE20)."""
     global _GRAPH
     _GRAPH = graph
     _EMBED_PLANS.clear()
