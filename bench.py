@@ -941,8 +941,11 @@ def setup_e2e(args, dev, rank, world, seed):
                             flops_basis="FFT-based count of the reference's algorithm per shifted clip: stft 3,292 x "
                                         "2.5 N log2 N (N = 250) + vocoder 3,372 x 126 x 16 + istft 3,372 x (2.5 N log2 N "
                                         "+ 250) + resample 23,044 x 2 x 142", clips=round(m)))
-        per_clip = {"mix_reverb": (AUG_T * 4 * 3, "augment_kernel (gain + noise mix + 23040-pt FFT reverb, every clip)",
-                                   ("augment_kernel",), "x + noise read, y written"),
+        per_clip = {"mix_reverb": (AUG_T * 4 * 3, "augment_kernel (colored-noise mix of the batches that drew it, folded "
+                                   "into its prologue (+ colored_group_kernel: one coloured second per such batch) + gain + "
+                                   "noise mix + 23040-pt FFT reverb, every clip)",
+                                   ("augment_kernel", "colored_group", "colored_noise"),
+                                   "x + noise read, y written (the coloured seconds are L2-resident, 64 KB per batch)"),
                     "eq": (AUG_T * 4 * 2, "eq_kernel (7-band EQ, the clips whose coin came up)", ("eq_kernel",),
                            "x read + y written"),
                     "tanh": (AUG_T * 4 * 2, "tanh_distortion_kernel (the clips whose coin came up)",

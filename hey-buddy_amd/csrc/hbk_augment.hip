@@ -38,6 +38,8 @@ namespace {
 constexpr int kT = 23040;        // clip length (1.44 s @ 16 kHz, augmented.py:31)
 constexpr int kM = kT / 2;       // complex FFT length
 constexpr int kThreads = 1024;   // 16 waves: one clip per CU (92 KB of LDS)
+constexpr int kN1 = 16000;       // colored noise: torch_audiomentations' noise length = sample_rate
+constexpr int kM1 = kN1 / 2;     // 8000
 
 // ---- small DFTs in registers (constant twiddles) --------------------------
 template <bool INV>
@@ -390,7 +392,31 @@ struct AugArgs {
   const float2* thi;        // W_M^(128 h), h < 90
   const float2* tlo;        // W_M^l, l < 128
   const float2* twn;        // W_N^k, k <= kM, at hslot(k)
+  // colored noise folded into the prologue (hbk_augment_colored; c_snr NULL: none). A clip
+  // with a non-NaN c_snr whose group's coloured second was made (c_grms[g] not NaN) and
+  // whose f_decay equals its group's first clip's is mixed here, exactly as
+  // colored_mix_kernel mixes it; any other coloured clip was written to out by
+  // colored_noise_kernel beforehand and is read from out instead of x.
+  const float* c_snr;
+  const float* c_fd;
+  int64_t c_group;
+  const float* c_gbuf;      // [groups][16000]: the coloured second x 8000
+  const float* c_grms;      // [groups], NULL: no group path
 };
+
+// 0: no colored noise, 1: mixed in augment_kernel's prologue, 2: coloured by
+// colored_noise_kernel into out (uniform per clip)
+__device__ __forceinline__ int colored_mode(const AugArgs& a, int64_t clip) {
+  if (!a.c_snr) return 0;
+  const float snr = a.c_snr[clip];
+  if (snr != snr) return 0;
+  if (a.c_grms) {
+    const int64_t g = clip / a.c_group;
+    const float r = a.c_grms[g];
+    if (r == r && a.c_fd[clip] == a.c_fd[g * a.c_group]) return 1;
+  }
+  return 2;
+}
 
 __global__ void __launch_bounds__(kThreads) augment_kernel(AugArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -412,11 +438,15 @@ __global__ void __launch_bounds__(kThreads) augment_kernel(AugArgs a) {
   // VGPRs through the FFT passes
   // (noff: the clip's noise offset, read well before, so that no branch waits
   // on a load queued behind these; vmcnt retires loads in order)
-  auto prefetch = [&](int64_t clip, int64_t noff) {
+  // (cmode: colored_mode of the clip, read ahead like noff; 2 = read the clip from out)
+  auto prefetch = [&](int64_t clip, int64_t noff, int cmode) {
     // uniform base + 32-bit per-lane offsets from an opaque thread id (keeps
     // the 46 per-load addresses from being hoisted out of the clip loop)
     const int t = opaque_tid();
-    const float* x = a.x + clip * a.x_stride;
+    // one uniform element offset from a.x. (The colored fold pushes this kernel's SGPRs over
+    // the limit: 2 x 8 B of VGPR spills, stored and reloaded once per clip, outside the passes.)
+    const int64_t row = cmode == 2 ? (a.out - a.x) + clip * a.out_stride : clip * a.x_stride;
+    const float* x = a.x + row;
     // 32-bit BYTE offsets from a uniform base: global_load's saddr form, one
     // VGPR per address (ring_len < 2^30, checked on the host)
     auto at = [](const float* base, uint32_t i) {
@@ -434,7 +464,7 @@ __global__ void __launch_bounds__(kThreads) augment_kernel(AugArgs a) {
       }
     }
   };
-  if (blockIdx.x < a.n_clips) prefetch(blockIdx.x, a.noise_off[blockIdx.x]);
+  if (blockIdx.x < a.n_clips) prefetch(blockIdx.x, a.noise_off[blockIdx.x], colored_mode(a, blockIdx.x));
   unsigned long long ph_t0 = 0;
 #ifdef HBK_PHASE_TIMING
   ph_t0 = __builtin_amdgcn_s_memtime();
@@ -448,7 +478,33 @@ __global__ void __launch_bounds__(kThreads) augment_kernel(AugArgs a) {
     const float gain = a.gain ? a.gain[clip] : 1.f;
     const bool next = clip + gridDim.x < a.n_clips;
     const int64_t noff_next = __builtin_amdgcn_readfirstlane(static_cast<int>(next ? a.noise_off[clip + gridDim.x] : -1));
+    const int cmode = __builtin_amdgcn_readfirstlane(colored_mode(a, clip));
+    const int cmode_next = __builtin_amdgcn_readfirstlane(next ? colored_mode(a, clip + gridDim.x) : 0);
     float ex = 0.f, aa = 0.f;
+    if (cmode == 1) {
+      // colored noise (the group path), in colored_mix_kernel's per-thread order and block
+      // sum: bit-identical to hbk_colored_noise_ws followed by hbk_augment
+      const int64_t g = clip / a.c_group;
+      const float* gb = a.c_gbuf + g * kN1;
+      const int t = opaque_tid();
+      float ec = 0.f, ez = 0.f;
+#pragma unroll
+      for (int u = 0; u < kPer; ++u)
+        if (t + u * kThreads < kT) ec += xr[u] * xr[u];
+      block_sum2(ec, ez, red);
+      const float rms_x = sqrtf(ec / kT);
+      const float scale = rms_x / powf(10.f, a.c_snr[clip] / 20.f) / (a.c_grms[g] + 1e-8f) * (1.f / kM1);
+      // the coloured second from L2 (64 KB per batch), loaded after the sum: held across it,
+      // its 23 registers spilled
+#pragma unroll
+      for (int u = 0; u < kPer; ++u) {
+        const int s = min(t + u * kThreads, kT - 1);
+        const int sn = s < kN1 ? s : s - kN1;
+        xr[u] = fmaf(scale,
+                     *reinterpret_cast<const float*>(reinterpret_cast<const char*>(gb) + (static_cast<uint32_t>(sn) << 2)),
+                     xr[u]);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
       xr[u] *= gain;
@@ -482,7 +538,7 @@ __global__ void __launch_bounds__(kThreads) augment_kernel(AugArgs a) {
     HBK_APH(3);
     float* out = a.out + clip * a.out_stride;
     if (sp < 0) {  // no reverb: each thread stores the samples it wrote
-      if (next) prefetch(clip + gridDim.x, noff_next);
+      if (next) prefetch(clip + gridDim.x, noff_next, cmode_next);
       for (int s = opaque_tid(); s < kT; s += kThreads) out[s] = zf[s];
       __syncthreads();
       continue;
@@ -553,7 +609,7 @@ __global__ void __launch_bounds__(kThreads) augment_kernel(AugArgs a) {
     HBK_APH(9);
     // 5) inverse FFT (permuted -> natural), 1/M
     transform<true>(z, thi, tlo, ph_t0, 10);
-    if (next) prefetch(clip + gridDim.x, noff_next);
+    if (next) prefetch(clip + gridDim.x, noff_next, cmode_next);
     float ay = 0.f;
     for (int s = opaque_tid(); s < kT; s += kThreads) ay += fabsf(zf[s]);
     const float a_out = block_sum(ay, red) / kT / kM;
@@ -878,6 +934,7 @@ struct ColoredArgs {
   float* gbuf;            // [n_groups][kN1]
   float* grms;            // [n_groups]: rms of the coloured second, NaN where not made
   int64_t n_groups;
+  int no_copy;            // hbk_augment_colored: clips this kernel does not colour are left alone
 };
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
@@ -924,8 +981,6 @@ __device__ __forceinline__ void copy_clip(const float* x, float* out, int tid) {
 // noise): DIF passes 16 x 5 x 5 x 5 x 4 in LDS, twiddles W_8000^e =
 // HI8[e / 100] LO8[e % 100]; frequency f = k1 + 16 k2 + 80 k3 + 400 k4 + 2000 k5
 // lands at 500 k1 + 100 k2 + 20 k3 + 4 k4 + k5.
-constexpr int kN1 = 16000;               // torch_audiomentations' noise length = sample_rate
-constexpr int kM1 = kN1 / 2;             // 8000
 constexpr int kTw8Lo = 100, kTw8Hi = kM1 / kTw8Lo;  // 100 x 80
 
 template <bool INV>
@@ -1066,7 +1121,7 @@ __global__ void __launch_bounds__(kThreads) colored_noise_kernel(ColoredArgs a) 
     const int tid = opaque_tid();
     const float snr = a.snr_db[clip];
     if (snr != snr) {  // NaN: this clip's batch drew no colored noise (uniform per block)
-      if (a.out != a.x || a.out_stride != a.x_stride)
+      if (!a.no_copy && (a.out != a.x || a.out_stride != a.x_stride))
         copy_clip(a.x + clip * a.x_stride, a.out + clip * a.out_stride, tid);
       continue;
     }
@@ -2272,19 +2327,18 @@ int hbk_reverb_spectrum(const hbk_reverb_plan* p, const float* kernels, int64_t 
   return HBK_OK;
 }
 
-int hbk_augment(const hbk_reverb_plan* p, const float* x, int64_t n_clips, int64_t x_stride,
-                const float* noise_ring, int64_t ring_len, const int64_t* noise_off, const float* snr_db,
-                const float* spectra, const int32_t* spec_idx, const float* gain, float* out,
-                int64_t out_stride, void* stream) {
+static int augment_args(const hbk_reverb_plan* p, const float* x, int64_t n_clips, int64_t x_stride,
+                        const float* noise_ring, int64_t ring_len, const int64_t* noise_off, const float* snr_db,
+                        const float* spectra, const int32_t* spec_idx, const float* gain, float* out,
+                        int64_t out_stride, hbk::AugArgs& a) {
   using namespace hbk;
   if (!p) return arg_error("plan is NULL");
   if (n_clips < 0) return arg_error("negative n_clips");
-  if (n_clips == 0) return HBK_OK;
   if (!x || !out || !noise_off || !snr_db || !spec_idx) return arg_error("NULL pointer");
   if (x_stride < kT || out_stride < kT) return arg_error("stride < 23040");
   if (!noise_ring && ring_len > 0) return arg_error("noise ring is NULL");
   if (ring_len >= (int64_t(1) << 30)) return arg_error("noise ring longer than 2^30 samples");
-  AugArgs a;
+  a = AugArgs{};
   a.x = x;
   a.x_stride = x_stride;
   a.out = out;
@@ -2300,8 +2354,26 @@ int hbk_augment(const hbk_reverb_plan* p, const float* x, int64_t n_clips, int64
   a.thi = p->thi;
   a.tlo = p->tlo;
   a.twn = p->twn;
-  const int64_t blocks = std::min<int64_t>(n_clips, persistent_blocks(1, stream));
+  return HBK_OK;
+}
+
+static void augment_launch(const hbk::AugArgs& a, void* stream) {
+  using namespace hbk;
+  const int64_t blocks = std::min<int64_t>(a.n_clips, persistent_blocks(1, stream));
   hipLaunchKernelGGL(augment_kernel, dim3(unsigned(blocks)), dim3(kThreads), kAugLds, as_stream(stream), a);
+}
+
+int hbk_augment(const hbk_reverb_plan* p, const float* x, int64_t n_clips, int64_t x_stride,
+                const float* noise_ring, int64_t ring_len, const int64_t* noise_off, const float* snr_db,
+                const float* spectra, const int32_t* spec_idx, const float* gain, float* out,
+                int64_t out_stride, void* stream) {
+  using namespace hbk;
+  if (n_clips == 0 && p) return HBK_OK;
+  AugArgs a;
+  const int st = augment_args(p, x, n_clips, x_stride, noise_ring, ring_len, noise_off, snr_db, spectra, spec_idx,
+                              gain, out, out_stride, a);
+  if (st != HBK_OK) return st;
+  augment_launch(a, stream);
   HBK_LAUNCH_CHECK("augment_kernel");
   return HBK_OK;
 }
@@ -2323,24 +2395,24 @@ int hbk_colored_noise(const hbk_reverb_plan* p, const float* x, int64_t n_clips,
                               sample_rate, idx, n_entries, out, out_stride, nullptr, 0, stream);
 }
 
-int hbk_colored_noise_ws(const hbk_reverb_plan* p, const float* x, int64_t n_clips, int64_t x_stride,
-                         const float* white, int64_t white_stride, uint64_t seed, int64_t clips_per_noise,
-                         const float* f_decay, const float* snr_db, float sample_rate, const int32_t* idx,
-                         int64_t n_entries, float* out, int64_t out_stride, void* workspace, int64_t workspace_bytes,
-                         void* stream) {
+static int colored_args(const hbk_reverb_plan* p, const float* x, int64_t n_clips, int64_t x_stride,
+                        const float* white, int64_t white_stride, uint64_t seed, int64_t clips_per_noise,
+                        const float* f_decay, const float* snr_db, float sample_rate, const int32_t* idx,
+                        int64_t n_entries, float* out, int64_t out_stride, void* workspace, int64_t workspace_bytes,
+                        hbk::ColoredArgs& a) {
   using namespace hbk;
   if (!p) return arg_error("plan is NULL");
   if (n_clips < 0) return arg_error("negative n_clips");
-  if (n_clips == 0) return HBK_OK;
   if (!x || !out || !f_decay || !snr_db) return arg_error("NULL pointer");
   if (x_stride < kT || out_stride < kT) return arg_error("stride < 23040");
   if (white && white_stride < kN1) return arg_error("white_stride < 16000");
   if (clips_per_noise < 1) return arg_error("clips_per_noise < 1");
+  if (idx && n_entries < 0) return arg_error("negative n_entries");
   if (sample_rate != float(kN1)) {
     set_error("hbk: colored noise is generated at 16 kHz (one second = 16000 samples), got %g", double(sample_rate));
     return HBK_ERR_UNSUPPORTED;
   }
-  ColoredArgs a;
+  a = ColoredArgs{};
   a.x = x;
   a.x_stride = x_stride;
   a.out = out;
@@ -2360,26 +2432,87 @@ int hbk_colored_noise_ws(const hbk_reverb_plan* p, const float* x, int64_t n_cli
   a.twn = p->twn16;
   a.gbuf = a.grms = nullptr;
   a.n_groups = 0;
-  if (a.n_entries <= 0) return n_entries < 0 ? arg_error("negative n_entries") : HBK_OK;
+  a.no_copy = 0;
   const int64_t need = hbk_colored_noise_workspace_size(n_clips, clips_per_noise);
   if (workspace && need > 0) {
     if (workspace_bytes < need) return arg_error("workspace too small (hbk_colored_noise_workspace_size)");
     a.n_groups = colored_groups(n_clips, clips_per_noise);
     a.gbuf = static_cast<float*>(workspace);
     a.grms = a.gbuf + a.n_groups * kN1;
-    const int64_t gblocks = std::min<int64_t>(a.n_groups, persistent_blocks(1, stream));
-    hipLaunchKernelGGL(colored_group_kernel, dim3(unsigned(gblocks)), dim3(kThreads), kColoredLds, as_stream(stream),
-                       a);
-    HBK_LAUNCH_CHECK("colored_group_kernel");
   }
+  return HBK_OK;
+}
+
+static void colored_group_launch(const hbk::ColoredArgs& a, void* stream) {
+  using namespace hbk;
+  const int64_t gblocks = std::min<int64_t>(a.n_groups, persistent_blocks(1, stream));
+  hipLaunchKernelGGL(colored_group_kernel, dim3(unsigned(gblocks)), dim3(kThreads), kColoredLds, as_stream(stream), a);
+}
+
+static void colored_clip_launch(const hbk::ColoredArgs& a, void* stream) {
+  using namespace hbk;
+  const int64_t blocks = std::min<int64_t>(a.n_entries, persistent_blocks(1, stream));
+  hipLaunchKernelGGL(colored_noise_kernel, dim3(unsigned(blocks)), dim3(kThreads), kColoredLds, as_stream(stream), a);
+}
+
+int hbk_colored_noise_ws(const hbk_reverb_plan* p, const float* x, int64_t n_clips, int64_t x_stride,
+                         const float* white, int64_t white_stride, uint64_t seed, int64_t clips_per_noise,
+                         const float* f_decay, const float* snr_db, float sample_rate, const int32_t* idx,
+                         int64_t n_entries, float* out, int64_t out_stride, void* workspace, int64_t workspace_bytes,
+                         void* stream) {
+  using namespace hbk;
+  if (n_clips == 0 && p) return HBK_OK;
+  ColoredArgs a;
+  const int st = colored_args(p, x, n_clips, x_stride, white, white_stride, seed, clips_per_noise, f_decay, snr_db,
+                              sample_rate, idx, n_entries, out, out_stride, workspace, workspace_bytes, a);
+  if (st != HBK_OK) return st;
+  if (a.n_entries <= 0) return HBK_OK;
   if (a.grms) {
+    colored_group_launch(a, stream);
+    HBK_LAUNCH_CHECK("colored_group_kernel");
     const int64_t mblocks = std::min<int64_t>(a.n_entries, persistent_blocks(2, stream));
     hipLaunchKernelGGL(colored_mix_kernel, dim3(unsigned(mblocks)), dim3(kThreads), 0, as_stream(stream), a);
     HBK_LAUNCH_CHECK("colored_mix_kernel");
   }
-  const int64_t blocks = std::min<int64_t>(a.n_entries, persistent_blocks(1, stream));
-  hipLaunchKernelGGL(colored_noise_kernel, dim3(unsigned(blocks)), dim3(kThreads), kColoredLds, as_stream(stream), a);
+  colored_clip_launch(a, stream);
   HBK_LAUNCH_CHECK("colored_noise_kernel");
+  return HBK_OK;
+}
+
+int hbk_augment_colored(const hbk_reverb_plan* p, const float* x, int64_t n_clips, int64_t x_stride,
+                        const float* noise_ring, int64_t ring_len, const int64_t* noise_off, const float* snr_db,
+                        const float* spectra, const int32_t* spec_idx, const float* gain, const float* white,
+                        int64_t white_stride, uint64_t seed, int64_t clips_per_noise, const float* c_f_decay,
+                        const float* c_snr_db, float sample_rate, const int32_t* c_idx, int64_t c_n_entries,
+                        float* out, int64_t out_stride, void* workspace, int64_t workspace_bytes, void* stream) {
+  using namespace hbk;
+  if (n_clips == 0 && p) return HBK_OK;
+  AugArgs a;
+  int st = augment_args(p, x, n_clips, x_stride, noise_ring, ring_len, noise_off, snr_db, spectra, spec_idx, gain,
+                        out, out_stride, a);
+  if (st != HBK_OK) return st;
+  ColoredArgs c;
+  st = colored_args(p, x, n_clips, x_stride, white, white_stride, seed, clips_per_noise, c_f_decay, c_snr_db,
+                    sample_rate, c_idx, c_n_entries, out, out_stride, workspace, workspace_bytes, c);
+  if (st != HBK_OK) return st;
+  if (out != x && out + n_clips * out_stride > x && x + n_clips * x_stride > out)
+    return arg_error("out overlaps x without being x");
+  c.no_copy = 1;
+  if (c.grms) {
+    colored_group_launch(c, stream);
+    HBK_LAUNCH_CHECK("colored_group_kernel");
+  }
+  if (c.n_entries > 0) {  // the clips the group path does not cover, coloured into out
+    colored_clip_launch(c, stream);
+    HBK_LAUNCH_CHECK("colored_noise_kernel");
+  }
+  a.c_snr = c_snr_db;
+  a.c_fd = c_f_decay;
+  a.c_group = clips_per_noise;
+  a.c_gbuf = c.gbuf;
+  a.c_grms = c.grms;
+  augment_launch(a, stream);
+  HBK_LAUNCH_CHECK("augment_kernel");
   return HBK_OK;
 }
 

@@ -697,6 +697,265 @@ mel_frames_mfma_kernel(Mel3Args a) {
     grp += gridDim.x;
   }
 }
+// ------------------------------------------------------------------ v4 ----
+// The v2 transform with every float op packed: a lane carries TWO columns of
+// one frame (8 lanes per frame, 8 frames per wave), as SoA pairs -- re of
+// both columns in one 64-bit register pair, im of both in another -- so each
+// v_pk_{add,mul,fma}_f32 does the work of two scalar ops of v2 with no
+// re / im swaps (v2's AoS packed form, HBK_MEL_PACKED, spent ~20 % of its
+// instructions on v_mov / v_xor to swap and negate halves; multiplying by -i
+// here is a renaming). v2 runs at ~82 % VALU issue (PMC r03): the instruction
+// count per frame is its bound.
+//  - stage A: lane jj holds columns jj and jj + 8 of z[16 n1 + n2]; FFT16 over
+//    n1, twiddles W256^(n2 k1) as (jj, jj + 8) pairs from the [entry][lane] table;
+//  - transpose through LDS as re / im planes, rows stored in the order
+//    0, 8, 1, 15, 2, 14, ... (row k1 beside row 16 - k1), so that in stage B
+//    lane kk reads its row pair (kk, 16 - kk) (kk = 0: rows 0, 8) with
+//    ds_read2_b32 at one base;
+//  - FFT16 over n2: lane kk holds Z[k1 + 16 k2] for k1 = kk and 16 - kk, so the
+//    real-FFT split's partner Z[256 - k] sits in the SAME lane's other half
+//    (kk = 0: rows 0 and 8 are their own partners): no cross-lane moves;
+//  - power to LDS, then 4 mel filters per lane (two of the <= 8-tap set, two
+//    of the <= 16-tap set: v2's slots jj and jj + 8) as packed dot products.
+// LDS per frame: one 280-dword buffer that carries the transpose one plane at a time
+// (re, then im: half the LDS of both planes at once, so 3 blocks fit a CU) and then
+// the power row. Transform row k1 sits at LDS row row5(k1) = the pair index p of
+// (p, 16 - p) (rows 0, 8: pair 0), its partner 16 - p at row p + 8, so stage B's lane
+// jj reads rows jj and jj + 8. Frame bases 280 = 24 mod 32 apart put the 4 frames of
+// a 32-lane LDS group on disjoint banks: the stage-A stores (bank 24 f + jj), the
+// stage-B reads (24 f + 17 jj + n2) and the power stores are conflict-free
+// (tools/lds_bank_sim.py; the first 577-dword layout ran the stores 4-way). The power
+// row sits at +24 (f & 1) + 8 (f >> 1 & 1) (8-B aligned pairs for the filter reads).
+constexpr int kWaves4 = 4;
+constexpr int kThreads4 = 64 * kWaves4;
+constexpr int kFramesPerWave4 = 8;
+constexpr int kFramesPerBlock4 = kFramesPerWave4 * kWaves4;
+constexpr int kLdt4 = 17, kFs4 = 280;
+constexpr int kBlocksPerCU4 = 3;  // 3 x (35 KB frames + 6.5 KB table) of LDS, <= 168 VGPRs
+// constant table [entry][8 lanes] of float4
+constexpr int kE4Win = 0;           // 16: (w[32 n1 + 2jj], w[.. + 16], w[.. + 1], w[.. + 17])
+constexpr int kE4Tw = 16;           // 16 (k1 = 0 unused): (Re W^(jj k1), Re W^((jj+8) k1), Im .., Im ..)
+constexpr int kE4Ws = 32;           // 8: -i W512^k for bins (ra + 16 k2, rb + 16 k2), re pair, im pair
+constexpr int kE4Mel = 40;          // 12: weights of A slots jj, jj + 8 (8 each), B slots jj, jj + 8 (16 each)
+constexpr int kE4N = 52;
+
+struct P2 {
+  cf r, i;
+};
+__device__ __forceinline__ P2 operator+(P2 a, P2 b) { return {a.r + b.r, a.i + b.i}; }
+__device__ __forceinline__ P2 operator-(P2 a, P2 b) { return {a.r - b.r, a.i - b.i}; }
+// a * (cr + i ci), per-half constants
+__device__ __forceinline__ P2 pmul(P2 a, cf cr, cf ci) {
+  return {__builtin_elementwise_fma(a.r, cr, -(a.i * ci)), __builtin_elementwise_fma(a.r, ci, a.i * cr)};
+}
+__device__ __forceinline__ cf bc(float v) { return cf{v, v}; }
+__device__ __forceinline__ void fft4p(P2& a0, P2& a1, P2& a2, P2& a3) {
+  const P2 t0 = a0 + a2, t1 = a0 - a2, t2 = a1 + a3, d = a1 - a3;
+  a0 = t0 + t2;
+  a2 = t0 - t2;
+  a1 = P2{t1.r + d.i, t1.i - d.r};  // t1 - i d
+  a3 = P2{t1.r - d.i, t1.i + d.r};  // t1 + i d
+}
+// a * W16^p for the products p = m2 l1 of fft16 (1, 2, 3, 4, 6, 9)
+template <int p>
+__device__ __forceinline__ P2 w16p(P2 a) {
+  constexpr float c1 = 0.92387953251128674f, s1 = 0.38268343236508978f, r = 0.70710678118654757f;
+  if constexpr (p == 4) return P2{a.i, -a.r};
+  if constexpr (p == 2) return P2{bc(r) * (a.r + a.i), bc(r) * (a.i - a.r)};
+  if constexpr (p == 6) return P2{bc(r) * (a.i - a.r), bc(-r) * (a.r + a.i)};
+  if constexpr (p == 1) return pmul(a, bc(c1), bc(-s1));
+  if constexpr (p == 3) return pmul(a, bc(s1), bc(-c1));
+  return pmul(a, bc(-c1), bc(s1));  // p = 9
+}
+__device__ __forceinline__ void fft16p(P2 (&v)[16]) {
+#pragma unroll
+  for (int m2 = 0; m2 < 4; ++m2) fft4p(v[m2], v[4 + m2], v[8 + m2], v[12 + m2]);
+  v[5] = w16p<1>(v[5]);
+  v[6] = w16p<2>(v[6]);
+  v[7] = w16p<3>(v[7]);
+  v[9] = w16p<2>(v[9]);
+  v[10] = w16p<4>(v[10]);
+  v[11] = w16p<6>(v[11]);
+  v[13] = w16p<3>(v[13]);
+  v[14] = w16p<6>(v[14]);
+  v[15] = w16p<9>(v[15]);
+#pragma unroll
+  for (int l1 = 0; l1 < 4; ++l1) fft4p(v[4 * l1 + 0], v[4 * l1 + 1], v[4 * l1 + 2], v[4 * l1 + 3]);
+  P2 t[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) t[k] = v[4 * (k & 3) + (k >> 2)];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] = t[k];
+}
+// LDS row of transform row k1: pair index p of rows (p, 16 - p), +8 for the second
+// of the pair (row 0 -> 0, row 8 -> 8)
+__device__ __forceinline__ constexpr int row5(int k1) {
+  return k1 == 0 ? 0 : k1 == 8 ? 8 : k1 < 8 ? k1 : 16 - k1 + 8;
+}
+
+struct Mel4Args {
+  const float* pcm;
+  float* out;
+  const float4* table;  // [kE4N][8]
+  const int* mel_lo2;   // v2's [32]
+  int64_t n_clips;
+  int64_t clip_stride;
+  int64_t n_frames;
+  int hop;
+  float log_floor;
+  float out_scale;  // 10 / out_div
+  float out_add;
+};
+
+template <bool EDGE0>
+__global__ void __launch_bounds__(kThreads4) __attribute__((amdgpu_waves_per_eu(3)))
+mel_frames_soa_kernel(Mel4Args a) {
+  __shared__ float s_fr[kFramesPerBlock4 * kFs4];
+  __shared__ __attribute__((aligned(16))) float4 s_t[kE4N * 8];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < kE4N * 8; i += kThreads4) s_t[i] = a.table[i];
+  const int wave = tid >> 6, lane = tid & 63;
+  const int f = lane >> 3, jj = lane & 7;
+  const int slot = wave * kFramesPerWave4 + f;
+  const float4* tj = s_t + jj;  // entry e: tj[8 e]
+  float* fr = s_fr + slot * kFs4;
+  float* pw = fr + 24 * (f & 1) + 8 * ((f >> 1) & 1);  // the power row (8-B aligned pairs)
+  const int ra = jj == 0 ? 0 : jj, rb = jj == 0 ? 8 : 16 - jj;  // stage-B rows of this lane
+  const float* rowsB = fr + jj * kLdt4;                           // LDS rows jj, jj + 8
+  const int loA0 = a.mel_lo2[jj], loA1 = a.mel_lo2[jj + 8];
+  const int loB0 = a.mel_lo2[16 + jj], loB1 = a.mel_lo2[16 + jj + 8];
+  __syncthreads();
+
+  const uint32_t total = static_cast<uint32_t>(a.n_clips * a.n_frames);
+  const uint32_t nf = static_cast<uint32_t>(a.n_frames);
+  const uint32_t groups = (total + kFramesPerBlock4 - 1) / kFramesPerBlock4;
+  constexpr int n1lo = EDGE0 ? 1 : 0, n1hi = EDGE0 ? 15 : 16;
+  auto frame_src = [&](uint32_t grp) {
+    uint32_t g = min(grp, groups - 1) * kFramesPerBlock4 + slot;
+    g = g < total ? g : total - 1;  // clamp: tail slots recompute a valid frame, store nothing
+    const uint32_t clip = g / nf;
+    const uint32_t fi = g - clip * nf;
+    return a.pcm + static_cast<int64_t>(clip) * a.clip_stride + static_cast<int64_t>(fi) * a.hop + 2 * jj;
+  };
+  // samples of columns jj (x[32 n1 + 2 jj], + 1) and jj + 8 (x[.. + 16], + 17), loaded
+  // straight into SoA pairs: xr = (x[2 jj], x[2 jj + 16]), xi = (x[2 jj + 1], x[2 jj + 17])
+  // (4-B loads: the pair's halves land in adjacent registers with no moves)
+  auto load = [&](const float* src, cf (&xr)[16], cf (&xi)[16]) {
+#pragma unroll
+    for (int n1 = n1lo; n1 < n1hi; ++n1) {
+      const float* s = src + 32 * n1;
+      xr[n1] = cf{s[0], s[16]};
+      xi[n1] = cf{s[1], s[17]};
+    }
+  };
+  auto to_log = [&](float acc) {
+    const float c = acc < a.log_floor ? a.log_floor : acc;  // keeps NaN
+    return __log10f(c) * a.out_scale + a.out_add;
+  };
+
+  // one group: transform the samples in (cr, ci), prefetching group grp + stride into (nr, ni)
+  auto process = [&](uint32_t grp, const cf (&xr)[16], const cf (&xi)[16], cf (&nr)[16], cf (&ni)[16]) {
+    P2 v[16];
+#pragma unroll
+    for (int n1 = 0; n1 < 16; ++n1) {
+      if (n1 < n1lo || n1 >= n1hi) {
+        v[n1] = P2{bc(0.f), bc(0.f)};
+      } else {
+        const float4 w = tj[8 * (kE4Win + n1)];
+        v[n1] = P2{xr[n1] * cf{w.x, w.y}, xi[n1] * cf{w.z, w.w}};
+      }
+    }
+    load(frame_src(grp + gridDim.x), nr, ni);  // prefetch (clamped past the end)
+    fft16p(v);  // v[k1] = A[k1][(jj, jj + 8)]
+#pragma unroll
+    for (int k1 = 1; k1 < 16; ++k1) {
+      const float4 t = tj[8 * (kE4Tw + k1)];
+      v[k1] = pmul(v[k1], cf{t.x, t.y}, cf{t.z, t.w});
+    }
+    // the transpose, re plane then im plane through the frame's one buffer (wavefront-scope
+    // fences: ordering only, the frame belongs to this wave)
+#pragma unroll
+    for (int k1 = 0; k1 < 16; ++k1) {
+      float* row = fr + row5(k1) * kLdt4 + jj;
+      row[0] = v[k1].r.x;
+      row[8] = v[k1].r.y;
+    }
+    wave_sync();
+    cf tr[16];
+#pragma unroll
+    for (int n2 = 0; n2 < 16; ++n2) tr[n2] = cf{rowsB[n2], rowsB[8 * kLdt4 + n2]};
+    wave_sync();
+#pragma unroll
+    for (int k1 = 0; k1 < 16; ++k1) {
+      float* row = fr + row5(k1) * kLdt4 + jj;
+      row[0] = v[k1].i.x;
+      row[8] = v[k1].i.y;
+    }
+    wave_sync();
+#pragma unroll
+    for (int n2 = 0; n2 < 16; ++n2) v[n2] = P2{tr[n2], cf{rowsB[n2], rowsB[8 * kLdt4 + n2]}};
+    fft16p(v);  // v[k2] = (Z[ra + 16 k2], Z[rb + 16 k2])
+    // 2 X[k] = (Z[k] + Z*[256-k]) + (-i W512^k) (Z[k] - Z*[256-k]) for the bins below 128
+    cf p[8];
+#pragma unroll
+    for (int k2 = 0; k2 < 8; ++k2) {
+      const P2 z = v[k2], z15 = v[15 - k2], z16 = v[(16 - k2) & 15];
+      // partner pair: (Z[256 - lo bin], Z[256 - hi bin]): the other half of v[15 - k2];
+      // lane 0 (rows 0, 8): (row 0 of v[16 - k2], row 8 of v[15 - k2])
+      const cf pr = jj ? cf{z15.r.y, z15.r.x} : cf{z16.r.x, z15.r.y};
+      const cf pi = jj ? cf{z15.i.y, z15.i.x} : cf{z16.i.x, z15.i.y};
+      const cf sr = z.r + pr, si = z.i - pi, dr = z.r - pr, di = z.i + pi;
+      const float4 w = tj[8 * (kE4Ws + k2)];
+      const cf wr = cf{w.x, w.y}, wi = cf{w.z, w.w};
+      const cf xr = __builtin_elementwise_fma(-di, wi, __builtin_elementwise_fma(dr, wr, sr));
+      const cf xi = __builtin_elementwise_fma(dr, wi, __builtin_elementwise_fma(di, wr, si));
+      p[k2] = __builtin_elementwise_fma(xr, xr, xi * xi);
+    }
+    wave_sync();  // every lane of the frame has read its rows: the power row may overwrite them
+#pragma unroll
+    for (int k2 = 0; k2 < 8; ++k2) {
+      pw[ra + 16 * k2] = p[k2].x;
+      pw[rb + 16 * k2] = p[k2].y;
+    }
+    wave_sync();
+    // 4 filters: A slots jj, jj + 8 (filters jj, jj + 8), B slots jj, jj + 8 (filters 31 - jj, 23 - jj);
+    // taps in pairs (even start bins), weights x 1/4 from the table
+    auto dot = [&](int lo, int e0, int T) {
+      cf acc = bc(0.f);
+#pragma unroll
+      for (int q = 0; q < T / 4; ++q) {
+        const float4 w = tj[8 * (e0 + q)];
+        acc = __builtin_elementwise_fma(*reinterpret_cast<const cf*>(pw + lo + 4 * q), cf{w.x, w.y}, acc);
+        acc = __builtin_elementwise_fma(*reinterpret_cast<const cf*>(pw + lo + 4 * q + 2), cf{w.z, w.w}, acc);
+      }
+      return acc.x + acc.y;
+    };
+    const float yA0 = dot(loA0, kE4Mel, kTapsA), yA1 = dot(loA1, kE4Mel + 2, kTapsA);
+    const float yB0 = dot(loB0, kE4Mel + 4, kTapsB), yB1 = dot(loB1, kE4Mel + 8, kTapsB);
+    const uint32_t g = grp * kFramesPerBlock4 + slot;
+    if (g < total) {
+      float* o = a.out + static_cast<int64_t>(g) * kMaxMels;
+      o[jj] = to_log(yA0);
+      o[jj + 8] = to_log(yA1);
+      o[31 - jj] = to_log(yB0);
+      o[23 - jj] = to_log(yB1);
+    }
+    wave_sync();  // the next group's transpose overwrites the power row
+  };
+
+  // two explicit prefetch buffers (no register copies on the loop back edge)
+  uint32_t grp = blockIdx.x;
+  cf ar[16], ai[16], br[16], bi[16];
+  if (grp < groups) load(frame_src(grp), ar, ai);
+  while (grp < groups) {
+    process(grp, ar, ai, br, bi);
+    grp += gridDim.x;
+    if (grp >= groups) break;
+    process(grp, br, bi, ar, ai);
+    grp += gridDim.x;
+  }
+}
+
 }  // namespace
 }  // namespace hbk
 
@@ -724,6 +983,9 @@ struct hbk_mel_plan {
   // v3 (hbk_mel_set_variant 1): the dense filterbank^T [32][128] x 1/4 for the MFMA variant
   int variant = 0;
   float* d_fbt = nullptr;
+  // v4 (the default for v2 plans; HBK_MEL_V2=1 keeps v2): its per-lane constant table
+  int v4 = 0;
+  float4* d_t4 = nullptr;
 };
 
 extern "C" {
@@ -857,6 +1119,39 @@ int hbk_mel_plan_create(const float* window, const float* fbank, int n_fft, int 
     if ((e = hipMemcpy(p->d_fbt, fbt.data(), fbt.size() * sizeof(float), hipMemcpyHostToDevice)) != hipSuccess)
       return fail(e, "copy fbt");
     p->variant = getenv("HBK_MEL_MFMA") ? 1 : 0;
+    // v4 table [entry][lane jj]: window, W256 twiddles, split twiddles, filter weights
+    std::vector<float4> t4(static_cast<size_t>(kE4N) * 8, make_float4(0.f, 0.f, 0.f, 0.f));
+    auto W = [](double num) {
+      const double ang = -2.0 * M_PI * num;
+      return std::pair<float, float>(static_cast<float>(cos(ang)), static_cast<float>(sin(ang)));
+    };
+    for (int jj = 0; jj < 8; ++jj) {
+      for (int n1 = 0; n1 < 16; ++n1) {
+        const int s = 32 * n1 + 2 * jj;
+        t4[(kE4Win + n1) * 8 + jj] = make_float4(win[s], win[s + 16], win[s + 1], win[s + 17]);
+      }
+      for (int k1 = 1; k1 < 16; ++k1) {
+        const auto a0 = W(double(jj * k1) / 256.0), a1 = W(double((jj + 8) * k1) / 256.0);
+        t4[(kE4Tw + k1) * 8 + jj] = make_float4(a0.first, a1.first, a0.second, a1.second);
+      }
+      const int ra = jj == 0 ? 0 : jj, rb = jj == 0 ? 8 : 16 - jj;
+      for (int k2 = 0; k2 < 8; ++k2) {
+        const float2 s0 = twsm[ra + 16 * k2], s1 = twsm[rb + 16 * k2];
+        t4[(kE4Ws + k2) * 8 + jj] = make_float4(s0.x, s1.x, s0.y, s1.y);
+      }
+      const float* wa0 = w2.data() + jj * kTapsA;
+      const float* wa1 = w2.data() + (jj + 8) * kTapsA;
+      const float* wb0 = w2.data() + 16 * kTapsA + jj * kTapsB;
+      const float* wb1 = w2.data() + 16 * kTapsA + (jj + 8) * kTapsB;
+      for (int q = 0; q < 2; ++q) t4[(kE4Mel + q) * 8 + jj] = make_float4(wa0[4 * q], wa0[4 * q + 1], wa0[4 * q + 2], wa0[4 * q + 3]);
+      for (int q = 0; q < 2; ++q) t4[(kE4Mel + 2 + q) * 8 + jj] = make_float4(wa1[4 * q], wa1[4 * q + 1], wa1[4 * q + 2], wa1[4 * q + 3]);
+      for (int q = 0; q < 4; ++q) t4[(kE4Mel + 4 + q) * 8 + jj] = make_float4(wb0[4 * q], wb0[4 * q + 1], wb0[4 * q + 2], wb0[4 * q + 3]);
+      for (int q = 0; q < 4; ++q) t4[(kE4Mel + 8 + q) * 8 + jj] = make_float4(wb1[4 * q], wb1[4 * q + 1], wb1[4 * q + 2], wb1[4 * q + 3]);
+    }
+    if ((e = hipMalloc(&p->d_t4, t4.size() * sizeof(float4))) != hipSuccess) return fail(e, "hipMalloc t4");
+    if ((e = hipMemcpy(p->d_t4, t4.data(), t4.size() * sizeof(float4), hipMemcpyHostToDevice)) != hipSuccess)
+      return fail(e, "copy t4");
+    p->v4 = getenv("HBK_MEL_V4") ? 1 : 0;  // opt-in until measured on the GPU
   }
   *plan = p;
   return HBK_OK;
@@ -873,6 +1168,7 @@ int hbk_mel_plan_destroy(hbk_mel_plan* p) {
   (void)hipFree(p->d_lo2);
   (void)hipFree(p->d_w2);
   (void)hipFree(p->d_fbt);
+  (void)hipFree(p->d_t4);
   delete p;
   return HBK_OK;
 }
@@ -926,6 +1222,30 @@ int hbk_mel_frames(const hbk_mel_plan* plan, const float* pcm, int64_t n_clips, 
       hipLaunchKernelGGL(HBK_MEL_V3(false), dim3(static_cast<unsigned>(blocks)), dim3(kThreads3), 0,
                          as_stream(stream), a);
     HBK_LAUNCH_CHECK("mel_frames_mfma_kernel");
+    return HBK_OK;
+  }
+  if (plan->v2 && plan->v4) {
+    const int64_t groups4 = (total + kFramesPerBlock4 - 1) / kFramesPerBlock4;
+    Mel4Args a;
+    a.pcm = pcm;
+    a.out = out;
+    a.table = plan->d_t4;
+    a.mel_lo2 = plan->d_lo2;
+    a.n_clips = n_clips;
+    a.clip_stride = clip_stride;
+    a.n_frames = n_frames;
+    a.hop = plan->hop;
+    a.log_floor = plan->log_floor;
+    a.out_scale = 10.f / plan->out_div;
+    a.out_add = plan->out_add;
+    const int64_t blocks = std::min<int64_t>(groups4, persistent_blocks(kBlocksPerCU4, stream));
+    if (plan->edge0)
+      hipLaunchKernelGGL(hbk::mel_frames_soa_kernel<true>, dim3(static_cast<unsigned>(blocks)), dim3(kThreads4), 0,
+                         as_stream(stream), a);
+    else
+      hipLaunchKernelGGL(hbk::mel_frames_soa_kernel<false>, dim3(static_cast<unsigned>(blocks)), dim3(kThreads4), 0,
+                         as_stream(stream), a);
+    HBK_LAUNCH_CHECK("mel_frames_soa_kernel");
     return HBK_OK;
   }
   if (plan->v2) {

@@ -79,6 +79,9 @@ _PROTOS = {
                              _vp, _c_int64, _vp]),
     "hbk_colored_noise": (_c_int, [_vp, _vp, _c_int64, _c_int64, _vp, _c_int64, ctypes.c_uint64, _c_int64, _vp,
                                    _vp, _c_float, _vp, _c_int64, _vp, _c_int64, _vp]),
+    "hbk_augment_colored": (_c_int, [_vp, _vp, _c_int64, _c_int64, _vp, _c_int64, _vp, _vp, _vp, _vp, _vp,
+                                     _vp, _c_int64, ctypes.c_uint64, _c_int64, _vp, _vp, _c_float, _vp, _c_int64,
+                                     _vp, _c_int64, _vp, _c_int64, _vp]),
     "hbk_colored_noise_workspace_size": (_c_int64, [_c_int64, _c_int64]),
     "hbk_colored_noise_ws": (_c_int, [_vp, _vp, _c_int64, _c_int64, _vp, _c_int64, ctypes.c_uint64, _c_int64, _vp,
                                       _vp, _c_float, _vp, _c_int64, _vp, _c_int64, _vp, _c_int64, _vp]),

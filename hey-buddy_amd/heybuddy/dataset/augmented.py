@@ -49,6 +49,7 @@ from __future__ import annotations
 
 from typing import Any, Dict, Iterator, List, Optional, Sequence
 
+import os
 import numpy as np
 import torch
 
@@ -449,14 +450,18 @@ class BatchAugmenter:
                 out.copy_(x[:, :T])
             x = self.plan.band_stop(out, *pr["bandstop"], out=out)
             ev = self._tick("bandstop", ev)
+        colored = None
         if pr["colored"] is not None:  # colored noise precedes the gain (augmented.py:107-118)
             fd, csnr, seed = pr["colored"]
-            x = self.plan.colored_noise(x, fd, csnr, seed=seed, out=out, sample_rate=self.sample_rate,
-                                        clips_per_noise=self.batch_size)
-            out = x
-            ev = self._tick("colored", ev)
+            if self.sample_rate == 16000 and os.environ.get("HBK_AUG_COLORED_FOLD", "0") != "0":
+                colored = (fd, csnr, seed, self.batch_size)  # mixed in augment_kernel's pass
+            else:
+                x = self.plan.colored_noise(x, fd, csnr, seed=seed, out=out, sample_rate=self.sample_rate,
+                                            clips_per_noise=self.batch_size)
+                out = x
+                ev = self._tick("colored", ev)
         y = self.plan.augment(x, self.ring, pr["noise_off"], pr["snr"], self.spectra, pr["spec_idx"],
-                              out=out, gain=pr["gain"])
+                              out=out, gain=pr["gain"], colored=colored)
         self._tick("mix_reverb", ev)
         return y
 

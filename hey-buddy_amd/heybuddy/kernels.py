@@ -898,9 +898,13 @@ class ReverbPlan:
 
     def augment(self, x: torch.Tensor, ring: torch.Tensor | None, noise_off: torch.Tensor,
                 snr_db: torch.Tensor, spectra: torch.Tensor | None, spec_idx: torch.Tensor,
-                out: torch.Tensor | None = None, gain: torch.Tensor | None = None) -> torch.Tensor:
+                out: torch.Tensor | None = None, gain: torch.Tensor | None = None,
+                colored: tuple | None = None) -> torch.Tensor:
         """x [n, >= T] -> out [n, T]; per clip gain (linear factor, if given), then
-        noise (noise_off >= 0), then reverb (spec_idx >= 0)."""
+        noise (noise_off >= 0), then reverb (spec_idx >= 0). ``colored`` =
+        (f_decay, snr_db, seed, clips_per_noise) runs colored_noise() with the
+        generated white noise first, in the same pass (hbk_augment_colored:
+        bit-identical to the two calls, each clip read and written once)."""
         n = x.shape[0]
         if x.dim() != 2 or x.shape[1] < self.T or x.stride(1) != 1 or x.device != self.device:
             raise ValueError(f"x must be [n, >= {self.T}] f32 rows on {self.device}")
@@ -938,8 +942,46 @@ class ReverbPlan:
         noise_off, spec_idx, snr_db = to_dev(noise_off), to_dev(spec_idx), to_dev(snr_db)
         if gain is not None:
             gain = to_dev(gain)
-        torch.ops.hbk.augment_(x, ring, noise_off, snr_db, spectra, spec_idx, gain, out, self.id)
+        if colored is None:
+            torch.ops.hbk.augment_(x, ring, noise_off, snr_db, spectra, spec_idx, gain, out, self.id)
+            return out
+        f_decay, c_snr, seed, clips_per_noise = colored
+        f_decay, c_snr = per_clip(f_decay, torch.float32), per_clip(c_snr, torch.float32)
+        if clips_per_noise < 1:
+            raise ValueError("clips_per_noise must be >= 1")
+        if out.data_ptr() != x.data_ptr():
+            lo_o, hi_o = out.data_ptr(), out.data_ptr() + out.stride(0) * 4 * n
+            lo_x, hi_x = x.data_ptr(), x.data_ptr() + x.stride(0) * 4 * n
+            if lo_o < hi_x and lo_x < hi_o:
+                raise ValueError("out overlaps x without being x")
+        ws = self._colored_workspace(n, clips_per_noise)
+        # the clips the group path does not cover (a batch whose first clip drew no noise, or
+        # an f_decay other than its group's first clip's): coloured per clip before the pass
+        rows = None
+        if c_snr.device.type == "cpu" and f_decay.device.type == "cpu":
+            on = ~torch.isnan(c_snr)
+            if ws is not None:
+                first = (torch.arange(n) // clips_per_noise) * clips_per_noise
+                on &= torch.isnan(c_snr[first]) | (f_decay != f_decay[first])
+            rows = torch.nonzero(on).reshape(-1).to(torch.int32)
+            rows = rows.pin_memory().to(self.device, non_blocking=True) if rows.numel() else rows.to(self.device)
+        torch.ops.hbk.augment_colored_(x, ring, noise_off, snr_db, spectra, spec_idx, gain, to_dev(f_decay),
+                                       to_dev(c_snr), _u64_to_i64(seed), int(clips_per_noise), rows, out, ws,
+                                       self.id)
         return out
+
+    def _colored_workspace(self, n: int, clips_per_noise: int) -> torch.Tensor | None:
+        ws_bytes = int(lib().hbk_colored_noise_workspace_size(n, int(clips_per_noise)))
+        if (os.environ.get("HBK_COLORED_NO_GROUP") or ws_bytes > (1 << 30)
+                or int(clips_per_noise) < self.COLORED_GROUP_MIN):
+            return None  # A/B switch; small groups are not worth 64 KB of resident workspace each
+        if ws_bytes <= 0:
+            return None
+        ws = self._cn_ws
+        if ws is None or ws.numel() < ws_bytes:
+            ws = torch.empty(ws_bytes, dtype=torch.uint8, device=self.device)
+            self._cn_ws = ws
+        return ws
 
     def colored_noise(self, x: torch.Tensor, f_decay: torch.Tensor, snr_db: torch.Tensor,
                       white: torch.Tensor | None = None, seed: int = 0, out: torch.Tensor | None = None,
@@ -984,16 +1026,7 @@ class ReverbPlan:
             return t.pin_memory().to(self.device, non_blocking=True) if t.device.type == "cpu" else t.to(self.device)
 
         # clips_per_noise > 1: each group's coloured second is made once (hbk_colored_noise_ws)
-        ws_bytes = int(lib().hbk_colored_noise_workspace_size(n, int(clips_per_noise)))
-        if (os.environ.get("HBK_COLORED_NO_GROUP") or ws_bytes > (1 << 30)
-                or int(clips_per_noise) < self.COLORED_GROUP_MIN):
-            ws_bytes = 0  # A/B switch; small groups are not worth 64 KB of resident workspace each
-        ws = None
-        if ws_bytes > 0:
-            ws = self._cn_ws
-            if ws is None or ws.numel() < ws_bytes:
-                ws = torch.empty(ws_bytes, dtype=torch.uint8, device=self.device)
-                self._cn_ws = ws
+        ws = self._colored_workspace(n, clips_per_noise)
         torch.ops.hbk.colored_noise_(x, white, to_dev(f_decay), to_dev(snr_db), _u64_to_i64(seed),
                                      int(clips_per_noise), float(sample_rate), rows, out, ws, self.id)
         return out
@@ -1070,6 +1103,23 @@ def _augment_op(x: torch.Tensor, ring: torch.Tensor | None, noise_off: torch.Ten
     check(lib().hbk_augment(plan._handle, ptr(x), x.shape[0], x.stride(0), opt(ring),
                             0 if ring is None else ring.numel(), ptr(noise_off), ptr(snr_db), opt(spectra),
                             ptr(spec_idx), opt(gain), ptr(out), out.stride(0), stream_ptr(x.device)), "hbk_augment")
+
+
+@torch.library.custom_op("hbk::augment_colored_", mutates_args=("out", "workspace"))
+def _augment_colored_op(x: torch.Tensor, ring: torch.Tensor | None, noise_off: torch.Tensor, snr_db: torch.Tensor,
+                        spectra: torch.Tensor | None, spec_idx: torch.Tensor, gain: torch.Tensor | None,
+                        f_decay: torch.Tensor, c_snr: torch.Tensor, seed: int, clips_per_noise: int,
+                        rows: torch.Tensor | None, out: torch.Tensor, workspace: torch.Tensor | None,
+                        plan_id: int) -> None:
+    plan = _plans[plan_id]
+    opt = lambda t: ptr(t) if t is not None else None  # noqa: E731
+    check(lib().hbk_augment_colored(plan._handle, ptr(x), x.shape[0], x.stride(0), opt(ring),
+                                    0 if ring is None else ring.numel(), ptr(noise_off), ptr(snr_db), opt(spectra),
+                                    ptr(spec_idx), opt(gain), None, 0, seed & (2 ** 64 - 1), clips_per_noise,
+                                    ptr(f_decay), ptr(c_snr), 16000.0, opt(rows),
+                                    rows.numel() if rows is not None else 0, ptr(out), out.stride(0),
+                                    opt(workspace), workspace.numel() if workspace is not None else 0,
+                                    stream_ptr(x.device)), "hbk_augment_colored")
 
 
 @torch.library.custom_op("hbk::colored_noise_", mutates_args=("out", "workspace"))

@@ -414,6 +414,24 @@ int hbk_colored_noise_ws(const hbk_reverb_plan* plan, const float* x, int64_t n_
                          int64_t n_entries, float* out, int64_t out_stride, void* workspace, int64_t workspace_bytes,
                          void* stream);
 
+/* Colored noise followed by hbk_augment in one pass over the clips: out =
+ * hbk_augment(hbk_colored_noise_ws(x)), bit-identical to the two calls (the
+ * reference's batch chain runs AddColoredNoise right before the gain, noise and
+ * reverb, dataset/augmented.py:107-118). The group path's mix (the clips
+ * colored_mix_kernel would mix) happens in augment_kernel's prologue, so those
+ * clips are read and written once; the clips the group path does not cover
+ * (c_idx lists them; NULL = scan every clip) are coloured into out first and
+ * augment_kernel reads them from there. Arguments as in hbk_augment and
+ * hbk_colored_noise_ws (c_f_decay / c_snr_db per clip, NaN c_snr_db = no
+ * colored noise). out may equal x; otherwise it must not overlap it. */
+int hbk_augment_colored(const hbk_reverb_plan* plan, const float* x, int64_t n_clips, int64_t x_stride,
+                        const float* noise_ring, int64_t ring_len, const int64_t* noise_off,
+                        const float* snr_db, const float* spectra, const int32_t* spec_idx,
+                        const float* gain, const float* white, int64_t white_stride, uint64_t seed,
+                        int64_t clips_per_noise, const float* c_f_decay, const float* c_snr_db,
+                        float sample_rate, const int32_t* c_idx, int64_t c_n_entries, float* out,
+                        int64_t out_stride, void* workspace, int64_t workspace_bytes, void* stream);
+
 /* Band-stop: torch_audiomentations BandStopFilter, which the reference applies
  * in its batch chain with p 0.25 per batch, one parameter set per batch
  * (center mel-uniform in [200, 4000] Hz, bandwidth fraction U[0.5, 1.99];

@@ -367,6 +367,59 @@ def test_colored_noise_nan_snr_skips_and_generated_stream():
 
 
 @pytest.mark.gpu
+def test_augment_colored_fold_is_bit_identical():
+    """hbk_augment_colored (the colored mix folded into augment_kernel's prologue) equals
+    hbk_colored_noise_ws followed by hbk_augment bit for bit: group-path clips, a group
+    whose first clip drew no noise (its other clips take the per-clip path), a clip whose
+    f_decay differs from its group's first, NaN-snr clips; gain, noise, reverb; in place and
+    out of place."""
+    from heybuddy.kernels import ReverbPlan
+    plan = ReverbPlan()
+    plan.COLORED_GROUP_MIN = 1
+    n, g = 12, 4
+    x = torch.from_numpy(_clips(n, seed=41)).float().cuda()
+    noises, irs = _bank(seed=42)
+    ring = torch.from_numpy(np.concatenate(noises)).float().cuda()
+    rng = np.random.default_rng(43)
+    noise_off = torch.from_numpy(np.where(rng.random(n) < 0.7, rng.integers(0, ring.numel(), n), -1))
+    snr = torch.from_numpy(rng.uniform(0, 20, n)).float()
+    spec_idx = torch.from_numpy(np.where(rng.random(n) < 0.7, rng.integers(0, 2, n), -1)).int()
+    gain = torch.from_numpy(rng.uniform(0.5, 2.0, n)).float()
+    H = plan.spectra(torch.stack([ReverbPlan.rotated_kernel(torch.from_numpy(irs[i]), T) for i in range(2)]).cuda())
+    # groups of 4: {0-3} group path with clip 2's f_decay differing; {4-7} first clip NaN, the
+    # rest coloured per clip; {8-11} NaN (no colored noise)
+    fd = torch.tensor([0.5, 0.5, 1.5, 0.5, -1.0, 2.0, 2.0, 2.0, 0.0, 0.0, 0.0, 0.0])
+    c_snr = torch.tensor([12.0, 12.0, 12.0, 12.0, float("nan"), 20.0, 20.0, 20.0] + [float("nan")] * 4)
+    for seed in (5, 6):
+        ref = plan.colored_noise(x, fd, c_snr, seed=seed, clips_per_noise=g)
+        ref = plan.augment(ref, ring, noise_off, snr, H, spec_idx, gain=gain)
+        got = plan.augment(x, ring, noise_off, snr, H, spec_idx, gain=gain, colored=(fd, c_snr, seed, g))
+        assert torch.equal(got, ref)
+        y = x.clone()
+        got2 = plan.augment(y, ring, noise_off, snr, H, spec_idx, out=y, gain=gain, colored=(fd, c_snr, seed, g))
+        assert got2.data_ptr() == y.data_ptr() and torch.equal(y, ref)
+    assert not torch.equal(got[0], plan.augment(x, ring, noise_off, snr, H, spec_idx, gain=gain)[0])
+    # the batch driver with the fold (HBK_AUG_COLORED_FOLD=1) and without (=0): same output
+    import os
+    from heybuddy.dataset.augmented import BatchAugmenter
+    xb = torch.from_numpy(_clips(300, seed=44)).float().cuda()
+    outs = []
+    for fold in (True, False):
+        os.environ["HBK_AUG_COLORED_FOLD"] = "1" if fold else "0"
+        try:
+            np.random.seed(9)
+            torch.manual_seed(9)
+            aug = BatchAugmenter([torch.from_numpy(v).float() for v in noises],
+                                 [torch.from_numpy(v).float() for v in irs], device=0, batch_size=128,
+                                 colored_noise_prob=1.0, tanh_distortion_prob=0.0,
+                                 seven_band_prob=0.0, band_stop_prob=0.0, pitch_shift_prob=0.0)
+            outs.append(aug(xb))
+        finally:
+            os.environ.pop("HBK_AUG_COLORED_FOLD", None)
+    assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.gpu
 def test_batch_augmenter_colored_noise_is_per_batch():
     """mode="per_batch": one (snr, f_decay) AND one noise vector per batch of 128
     (torch_audiomentations runs the transform on the batch reshaped to
