@@ -487,10 +487,12 @@ __global__ void __launch_bounds__(kThreads) augment_kernel(AugArgs a) {
       const int64_t g = clip / a.c_group;
       const float* gb = a.c_gbuf + g * kN1;
       const int t = opaque_tid();
+      // explicit fmaf, as colored_mix_kernel: a plain `ec += x * x` here was SLP-vectorised
+      // into v_pk_mul + v_add (two roundings) and moved 1 in ~30 clips by an ulp
       float ec = 0.f, ez = 0.f;
 #pragma unroll
       for (int u = 0; u < kPer; ++u)
-        if (t + u * kThreads < kT) ec += xr[u] * xr[u];
+        if (t + u * kThreads < kT) ec = fmaf(xr[u], xr[u], ec);
       block_sum2(ec, ez, red);
       const float rms_x = sqrtf(ec / kT);
       const float scale = rms_x / powf(10.f, a.c_snr[clip] / 20.f) / (a.c_grms[g] + 1e-8f) * (1.f / kM1);
@@ -1140,7 +1142,7 @@ __global__ void __launch_bounds__(kThreads) colored_noise_kernel(ColoredArgs a) 
       xr[u] = 0.f;
       if (s < kT) {
         xr[u] = x[s];
-        ex += xr[u] * xr[u];
+        ex = fmaf(xr[u], xr[u], ex);
       }
       if (s < kN1) {
         const float nv = zf[s] * (1.f / kM1);
@@ -1225,7 +1227,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8
       const int s = tid + u * kThreads;
       if (s < kT) {  // 32-bit byte offsets on uniform bases
         const float v = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(x) + (static_cast<uint32_t>(s) << 2));
-        ex += v * v;
+        ex = fmaf(v, v, ex);
       }
     }
     block_sum2(ex, en, red);

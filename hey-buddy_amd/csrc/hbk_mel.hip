@@ -18,6 +18,7 @@
 // so no workgroup barrier is needed after the table load.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <vector>
 
 #include "hbk_common.h"
@@ -726,10 +727,7 @@ mel_frames_mfma_kernel(Mel3Args a) {
 // stage-B reads (24 f + 17 jj + n2) and the power stores are conflict-free
 // (tools/lds_bank_sim.py; the first 577-dword layout ran the stores 4-way). The power
 // row sits at +24 (f & 1) + 8 (f >> 1 & 1) (8-B aligned pairs for the filter reads).
-constexpr int kWaves4 = 4;
-constexpr int kThreads4 = 64 * kWaves4;
 constexpr int kFramesPerWave4 = 8;
-constexpr int kFramesPerBlock4 = kFramesPerWave4 * kWaves4;
 constexpr int kLdt4 = 17, kFs4 = 280;
 constexpr int kBlocksPerCU4 = 3;  // 3 x (35 KB frames + 6.5 KB table) of LDS, <= 168 VGPRs
 // constant table [entry][8 lanes] of float4
@@ -807,13 +805,17 @@ struct Mel4Args {
   float out_add;
 };
 
-template <bool EDGE0>
-__global__ void __launch_bounds__(kThreads4) __attribute__((amdgpu_waves_per_eu(3)))
+// W waves per block. W = 4: the next group's samples are prefetched into a second register
+// buffer (<= 168 VGPRs, 3 waves / SIMD, 3 blocks / CU); W = 8: no prefetch (<= 128 VGPRs,
+// 4 waves / SIMD: two 8-wave blocks share a CU's LDS)
+template <bool EDGE0, int W>
+__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W == 4 ? 3 : 4)))
 mel_frames_soa_kernel(Mel4Args a) {
-  __shared__ float s_fr[kFramesPerBlock4 * kFs4];
+  constexpr int kFPB = kFramesPerWave4 * W;
+  __shared__ float s_fr[kFPB * kFs4];
   __shared__ __attribute__((aligned(16))) float4 s_t[kE4N * 8];
   const int tid = threadIdx.x;
-  for (int i = tid; i < kE4N * 8; i += kThreads4) s_t[i] = a.table[i];
+  for (int i = tid; i < kE4N * 8; i += 64 * W) s_t[i] = a.table[i];
   const int wave = tid >> 6, lane = tid & 63;
   const int f = lane >> 3, jj = lane & 7;
   const int slot = wave * kFramesPerWave4 + f;
@@ -828,10 +830,10 @@ mel_frames_soa_kernel(Mel4Args a) {
 
   const uint32_t total = static_cast<uint32_t>(a.n_clips * a.n_frames);
   const uint32_t nf = static_cast<uint32_t>(a.n_frames);
-  const uint32_t groups = (total + kFramesPerBlock4 - 1) / kFramesPerBlock4;
+  const uint32_t groups = (total + kFPB - 1) / kFPB;
   constexpr int n1lo = EDGE0 ? 1 : 0, n1hi = EDGE0 ? 15 : 16;
   auto frame_src = [&](uint32_t grp) {
-    uint32_t g = min(grp, groups - 1) * kFramesPerBlock4 + slot;
+    uint32_t g = min(grp, groups - 1) * kFPB + slot;
     g = g < total ? g : total - 1;  // clamp: tail slots recompute a valid frame, store nothing
     const uint32_t clip = g / nf;
     const uint32_t fi = g - clip * nf;
@@ -854,7 +856,8 @@ mel_frames_soa_kernel(Mel4Args a) {
   };
 
   // one group: transform the samples in (cr, ci), prefetching group grp + stride into (nr, ni)
-  auto process = [&](uint32_t grp, const cf (&xr)[16], const cf (&xi)[16], cf (&nr)[16], cf (&ni)[16]) {
+  auto process = [&](uint32_t grp, cf (&xr)[16], cf (&xi)[16], cf (&nr)[16], cf (&ni)[16]) {
+    if constexpr (W != 4) load(frame_src(grp), xr, xi);
     P2 v[16];
 #pragma unroll
     for (int n1 = 0; n1 < 16; ++n1) {
@@ -865,7 +868,7 @@ mel_frames_soa_kernel(Mel4Args a) {
         v[n1] = P2{xr[n1] * cf{w.x, w.y}, xi[n1] * cf{w.z, w.w}};
       }
     }
-    load(frame_src(grp + gridDim.x), nr, ni);  // prefetch (clamped past the end)
+    if constexpr (W == 4) load(frame_src(grp + gridDim.x), nr, ni);  // prefetch (clamped past the end)
     fft16p(v);  // v[k1] = A[k1][(jj, jj + 8)]
 #pragma unroll
     for (int k1 = 1; k1 < 16; ++k1) {
@@ -932,7 +935,7 @@ mel_frames_soa_kernel(Mel4Args a) {
     };
     const float yA0 = dot(loA0, kE4Mel, kTapsA), yA1 = dot(loA1, kE4Mel + 2, kTapsA);
     const float yB0 = dot(loB0, kE4Mel + 4, kTapsB), yB1 = dot(loB1, kE4Mel + 8, kTapsB);
-    const uint32_t g = grp * kFramesPerBlock4 + slot;
+    const uint32_t g = grp * kFPB + slot;
     if (g < total) {
       float* o = a.out + static_cast<int64_t>(g) * kMaxMels;
       o[jj] = to_log(yA0);
@@ -946,7 +949,11 @@ mel_frames_soa_kernel(Mel4Args a) {
   // two explicit prefetch buffers (no register copies on the loop back edge)
   uint32_t grp = blockIdx.x;
   cf ar[16], ai[16], br[16], bi[16];
-  if (grp < groups) load(frame_src(grp), ar, ai);
+  if (W == 4 && grp < groups) load(frame_src(grp), ar, ai);
+  if constexpr (W != 4) {
+    for (; grp < groups; grp += gridDim.x) process(grp, ar, ai, ar, ai);
+    return;
+  }
   while (grp < groups) {
     process(grp, ar, ai, br, bi);
     grp += gridDim.x;
@@ -983,7 +990,7 @@ struct hbk_mel_plan {
   // v3 (hbk_mel_set_variant 1): the dense filterbank^T [32][128] x 1/4 for the MFMA variant
   int variant = 0;
   float* d_fbt = nullptr;
-  // v4 (the default for v2 plans; HBK_MEL_V2=1 keeps v2): its per-lane constant table
+  // v4 (HBK_MEL_V4): 4 or 8 waves per block, 0 = v2; its per-lane constant table
   int v4 = 0;
   float4* d_t4 = nullptr;
 };
@@ -1151,7 +1158,9 @@ int hbk_mel_plan_create(const float* window, const float* fbank, int n_fft, int 
     if ((e = hipMalloc(&p->d_t4, t4.size() * sizeof(float4))) != hipSuccess) return fail(e, "hipMalloc t4");
     if ((e = hipMemcpy(p->d_t4, t4.data(), t4.size() * sizeof(float4), hipMemcpyHostToDevice)) != hipSuccess)
       return fail(e, "copy t4");
-    p->v4 = getenv("HBK_MEL_V4") ? 1 : 0;  // opt-in until measured on the GPU
+    // opt-in until measured on the GPU: HBK_MEL_V4=1 (4-wave blocks, prefetch) or 8 (8-wave blocks)
+    const char* v4 = getenv("HBK_MEL_V4");
+    p->v4 = v4 ? (atoi(v4) == 8 ? 8 : 4) : 0;
   }
   *plan = p;
   return HBK_OK;
@@ -1225,7 +1234,9 @@ int hbk_mel_frames(const hbk_mel_plan* plan, const float* pcm, int64_t n_clips, 
     return HBK_OK;
   }
   if (plan->v2 && plan->v4) {
-    const int64_t groups4 = (total + kFramesPerBlock4 - 1) / kFramesPerBlock4;
+    const int W = plan->v4 == 8 ? 8 : 4;  // waves per block (hbk_mel_plan::v4)
+    const int64_t fpb = kFramesPerWave4 * W;
+    const int64_t groups4 = (total + fpb - 1) / fpb;
     Mel4Args a;
     a.pcm = pcm;
     a.out = out;
@@ -1238,13 +1249,19 @@ int hbk_mel_frames(const hbk_mel_plan* plan, const float* pcm, int64_t n_clips, 
     a.log_floor = plan->log_floor;
     a.out_scale = 10.f / plan->out_div;
     a.out_add = plan->out_add;
-    const int64_t blocks = std::min<int64_t>(groups4, persistent_blocks(kBlocksPerCU4, stream));
-    if (plan->edge0)
-      hipLaunchKernelGGL(hbk::mel_frames_soa_kernel<true>, dim3(static_cast<unsigned>(blocks)), dim3(kThreads4), 0,
-                         as_stream(stream), a);
-    else
-      hipLaunchKernelGGL(hbk::mel_frames_soa_kernel<false>, dim3(static_cast<unsigned>(blocks)), dim3(kThreads4), 0,
-                         as_stream(stream), a);
+    const int64_t blocks = std::min<int64_t>(groups4, persistent_blocks(W == 8 ? 2 : kBlocksPerCU4, stream));
+    const dim3 grid(static_cast<unsigned>(blocks)), block(64 * W);
+    if (W == 8) {
+      if (plan->edge0)
+        hipLaunchKernelGGL((hbk::mel_frames_soa_kernel<true, 8>), grid, block, 0, as_stream(stream), a);
+      else
+        hipLaunchKernelGGL((hbk::mel_frames_soa_kernel<false, 8>), grid, block, 0, as_stream(stream), a);
+    } else {
+      if (plan->edge0)
+        hipLaunchKernelGGL((hbk::mel_frames_soa_kernel<true, 4>), grid, block, 0, as_stream(stream), a);
+      else
+        hipLaunchKernelGGL((hbk::mel_frames_soa_kernel<false, 4>), grid, block, 0, as_stream(stream), a);
+    }
     HBK_LAUNCH_CHECK("mel_frames_soa_kernel");
     return HBK_OK;
   }

@@ -453,7 +453,7 @@ class BatchAugmenter:
         colored = None
         if pr["colored"] is not None:  # colored noise precedes the gain (augmented.py:107-118)
             fd, csnr, seed = pr["colored"]
-            if self.sample_rate == 16000 and os.environ.get("HBK_AUG_COLORED_FOLD", "0") != "0":
+            if self.sample_rate == 16000 and os.environ.get("HBK_AUG_COLORED_FOLD", "1") != "0":
                 colored = (fd, csnr, seed, self.batch_size)  # mixed in augment_kernel's pass
             else:
                 x = self.plan.colored_noise(x, fd, csnr, seed=seed, out=out, sample_rate=self.sample_rate,

@@ -964,10 +964,14 @@ class ReverbPlan:
                 first = (torch.arange(n) // clips_per_noise) * clips_per_noise
                 on &= torch.isnan(c_snr[first]) | (f_decay != f_decay[first])
             rows = torch.nonzero(on).reshape(-1).to(torch.int32)
-            rows = rows.pin_memory().to(self.device, non_blocking=True) if rows.numel() else rows.to(self.device)
+        n_rows = -1 if rows is None else rows.numel()  # -1: the kernel scans every clip
+        if n_rows == 0:
+            rows = torch.zeros(1, dtype=torch.int32)  # a valid pointer with no entries
+        if rows is not None:
+            rows = rows.pin_memory().to(self.device, non_blocking=True)
         torch.ops.hbk.augment_colored_(x, ring, noise_off, snr_db, spectra, spec_idx, gain, to_dev(f_decay),
-                                       to_dev(c_snr), _u64_to_i64(seed), int(clips_per_noise), rows, out, ws,
-                                       self.id)
+                                       to_dev(c_snr), _u64_to_i64(seed), int(clips_per_noise), rows, n_rows, out,
+                                       ws, self.id)
         return out
 
     def _colored_workspace(self, n: int, clips_per_noise: int) -> torch.Tensor | None:
@@ -1109,15 +1113,15 @@ def _augment_op(x: torch.Tensor, ring: torch.Tensor | None, noise_off: torch.Ten
 def _augment_colored_op(x: torch.Tensor, ring: torch.Tensor | None, noise_off: torch.Tensor, snr_db: torch.Tensor,
                         spectra: torch.Tensor | None, spec_idx: torch.Tensor, gain: torch.Tensor | None,
                         f_decay: torch.Tensor, c_snr: torch.Tensor, seed: int, clips_per_noise: int,
-                        rows: torch.Tensor | None, out: torch.Tensor, workspace: torch.Tensor | None,
+                        rows: torch.Tensor | None, n_rows: int, out: torch.Tensor, workspace: torch.Tensor | None,
                         plan_id: int) -> None:
     plan = _plans[plan_id]
     opt = lambda t: ptr(t) if t is not None else None  # noqa: E731
     check(lib().hbk_augment_colored(plan._handle, ptr(x), x.shape[0], x.stride(0), opt(ring),
                                     0 if ring is None else ring.numel(), ptr(noise_off), ptr(snr_db), opt(spectra),
                                     ptr(spec_idx), opt(gain), None, 0, seed & (2 ** 64 - 1), clips_per_noise,
-                                    ptr(f_decay), ptr(c_snr), 16000.0, opt(rows),
-                                    rows.numel() if rows is not None else 0, ptr(out), out.stride(0),
+                                    ptr(f_decay), ptr(c_snr), 16000.0, opt(rows) if n_rows >= 0 else None,
+                                    max(n_rows, 0), ptr(out), out.stride(0),
                                     opt(workspace), workspace.numel() if workspace is not None else 0,
                                     stream_ptr(x.device)), "hbk_augment_colored")
 
