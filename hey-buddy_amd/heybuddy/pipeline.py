@@ -36,11 +36,26 @@ import torch
 __all__ = ["train_cu_set", "cu_mask_words", "masked_stream", "make_streams"]
 
 
-def train_cu_set(n_cu: int, n_train: int, n_xcd: int = 8) -> List[int]:
-    """n_train CU ids spread evenly over the XCDs whether the mask's bit i maps
-    to XCD i // (n_cu / n_xcd) or to XCD i % n_xcd: XCD x takes the k = n_train
-    / n_xcd ids x * per + (floor(j per / k) + x) mod per (per = CUs per XCD)."""
+def train_cu_set(n_cu: int, n_train: int, n_xcd: int = 8, layout: Optional[str] = None) -> List[int]:
+    """The train partition's CU ids (mask bits). "spread" (default): n_train ids
+    spread evenly over the XCDs whether the mask's bit i maps to XCD
+    i // (n_cu / n_xcd) or to XCD i % n_xcd: XCD x takes the k = n_train / n_xcd
+    ids x * per + (floor(j per / k) + x) mod per (per = CUs per XCD).
+    "packed-rr" / "packed-contig": whole XCDs (n_train / per of them), for bit i
+    on XCD i % n_xcd / i // per (HBK_TRAIN_CU_LAYOUT; tools/xcd_probe.py maps the
+    bits on a device)."""
+    import os
+    layout = layout or os.environ.get("HBK_TRAIN_CU_LAYOUT", "spread")
     per = n_cu // n_xcd
+    if layout.startswith("xcds-rr:"):  # n_train CUs on the first X XCDs (bit i on XCD i % n_xcd), n_train / X each
+        nx = int(layout.split(":")[1])
+        if 0 < nx <= n_xcd and n_train % nx == 0 and n_train // nx <= per:
+            return sorted(x + n_xcd * j for x in range(nx) for j in range(n_train // nx))
+    if layout in ("packed-rr", "packed-contig") and n_train % per == 0:
+        xcds = range(n_train // per)
+        if layout == "packed-rr":
+            return sorted(x + n_xcd * j for x in xcds for j in range(per))
+        return sorted(x * per + j for x in xcds for j in range(per))
     k = max(1, min(per, n_train // n_xcd))
     return sorted(x * per + ((j * per // k + x) % per) for x in range(n_xcd) for j in range(k))
 
