@@ -47,6 +47,17 @@ def train_cu_set(n_cu: int, n_train: int, n_xcd: int = 8, layout: Optional[str] 
     import os
     layout = layout or os.environ.get("HBK_TRAIN_CU_LAYOUT", "spread")
     per = n_cu // n_xcd
+    if layout == "se-whole":  # whole shader engines: mask bit i = XCD i % 8, SE (i // 8) % 4, CU i // 32 (probed)
+        n_se = 4
+        per_se = n_cu // (n_xcd * n_se)
+        if n_train % (n_xcd * per_se) == 0:
+            ses = n_train // (n_xcd * per_se)
+            return sorted(i for i in range(n_cu) if (i // n_xcd) % n_se < ses)
+    if layout == "se-balanced" and n_train % n_xcd == 0:  # every XCD, and within it every quarter of its CUs
+        k = n_train // n_xcd                              # (bit i: XCD i % n_xcd, CU i // n_xcd)
+        if k % 4 == 0:
+            q = per // 4
+            return sorted(x + n_xcd * (s_ * q + j) for x in range(n_xcd) for s_ in range(4) for j in range(k // 4))
     if layout.startswith("xcds-rr:"):  # n_train CUs on the first X XCDs (bit i on XCD i % n_xcd), n_train / X each
         nx = int(layout.split(":")[1])
         if 0 < nx <= n_xcd and n_train % nx == 0 and n_train // nx <= per:

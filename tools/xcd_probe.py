@@ -1,7 +1,6 @@
-"""Which XCDs / CUs do the workgroups of a launch on a CU-masked stream run on? For each
-train-CU layout (heybuddy.pipeline.train_cu_set) and its complement, launch 1,024 one-wave
-blocks of a probe kernel that records the XCC_ID and HW_ID registers, and print the
-histogram of XCDs and the number of distinct CUs.
+"""Where do the workgroups of a launch on a CU-masked stream run? Launches 16,384 sleeping
+one-wave blocks of a probe kernel that records XCC_ID and HW_ID (SE / SH / CU fields) and
+prints, per mask, the distinct hardware CUs used per XCD and per (XCD, SE).
 usage: python tools/xcd_probe.py   (needs tools/libxcdprobe.so: hipcc -shared -fPIC
 --offload-arch=gfx950 tools/xcd_probe.hip -o tools/libxcdprobe.so)"""
 import collections
@@ -21,11 +20,11 @@ lib.xcd_probe.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_
 hbk = _native.lib()
 dev = torch.device("cuda:0")
 n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
-B = 1024
+B = 16384
 out = torch.zeros(2 * B, dtype=torch.int32, device=dev)
 
 
-def probe(cus, tag):
+def where(cus, tag):
     words = cu_mask_words(cus, n_cu)
     arr = (ctypes.c_uint32 * len(words))(*words)
     h = ctypes.c_void_p()
@@ -33,20 +32,28 @@ def probe(cus, tag):
     s = torch.cuda.ExternalStream(h.value, device=dev)
     out.zero_()
     torch.cuda.synchronize()
-    assert lib.xcd_probe(ctypes.c_void_p(out.data_ptr()), B, 200, ctypes.c_void_p(h.value)) == 0
+    assert lib.xcd_probe(ctypes.c_void_p(out.data_ptr()), B, 20, ctypes.c_void_p(h.value)) == 0
     s.synchronize()
-    v = out.cpu().view(-1, 2).tolist()
-    xh = collections.Counter(a & 0xF for a, _ in v)
-    cus_seen = {(a & 0xF, b & 0xFFFF) for a, b in v}
-    print(f"{tag:>26}: {len(cus)} mask bits -> XCD histogram {dict(sorted(xh.items()))}, "
-          f"{len(cus_seen)} distinct (XCD, HW_ID) slots", flush=True)
+    hw = set()
+    for a, b in out.cpu().view(-1, 2).tolist():
+        hw.add((a & 0xF, (b >> 13) & 7, (b >> 12) & 1, (b >> 8) & 0xF))  # (xcc, se, sh, cu)
+    per_xcd = collections.Counter(x for x, _, _, _ in hw)
+    per_se = collections.Counter((x, se, sh) for x, se, sh, _ in hw)
+    x0 = sorted((se, sh, cu) for x, se, sh, cu in hw if x == 0)
+    print(f"{tag:>24}: {len(cus):3d} bits -> {len(hw):3d} CUs; per XCD {dict(sorted(per_xcd.items()))}; "
+          f"XCD 0 per (SE, SH) {dict(sorted((k[1:], v) for k, v in per_se.items() if k[0] == 0))}; "
+          f"XCD 0 CUs {x0}", flush=True)
     hbk.hbk_stream_destroy(h)
 
 
-for layout in ("spread", "packed-rr", "packed-contig"):
+where(list(range(n_cu)), "all")
+for lo in (0, 8, 32, 64):
+    where(list(range(lo, lo + 32)), f"bits {lo}-{lo + 31}")
+where(list(range(0, 8)), "bits 0-7")
+for layout in ("spread", "se-balanced", "packed-contig"):
     t = train_cu_set(n_cu, 64, layout=layout)
-    probe(t, layout + " train")
-    probe(sorted(set(range(n_cu)) - set(t)), layout + " featurize")
-probe(list(range(n_cu)), "all")
-probe(list(range(32)), "bits 0-31")
-probe(list(range(0, n_cu, 8)), "bits 0, 8, 16, ...")
+    where(t, layout + " train")
+    where(sorted(set(range(n_cu)) - set(t)), layout + " feat")
+t = train_cu_set(n_cu, 64, layout="se-whole")
+where(t, "se-whole train")
+where(sorted(set(range(n_cu)) - set(t)), "se-whole feat")
