@@ -1,7 +1,8 @@
 """heybuddy.pipeline: CU partitions for featurizing beside training.
 
 CPU: the train CU set is spread evenly over the XCDs whether the mask's bit i
-maps to XCD i // 32 or to XCD i % 8, and the mask words hold exactly that set.
+maps to XCD i // 32 or to XCD i % 8, and over the shader engines of the probed
+mapping (XCD i % 8, SE (i // 8) % 4); the mask words hold exactly that set.
 GPU: on a CU-masked stream (persistent grids sized to the mask) the embedding
 chain gives the same bits as on the default stream, and the mel frames agree to
 the last bit or two (the persistent mel kernel's frame-group-to-workgroup
@@ -24,6 +25,27 @@ def test_train_cu_set_even_over_xcds(n_train):
     interleaved = np.bincount([c % 8 for c in cus], minlength=8)
     assert (contiguous == n_train // 8).all()
     assert (interleaved == n_train // 8).all()
+
+
+@pytest.mark.parametrize("n_train", [32, 64, 96, 128])
+@pytest.mark.parametrize("layout", ["spread", "se-whole"])
+def test_train_cu_set_balanced_over_xcds_and_shader_engines(n_train, layout):
+    """The probed MI355X mask mapping (profiles/r05h_cu_mask_layouts.log): bit i is XCD i % 8,
+    shader engine (i // 8) % 4, CU i // 32 of that SE. The dispatcher balances workgroups over
+    the XCDs and SEs, so both streams' CU sets must give every (XCD, SE) the same count (the
+    train set; its complement then too) — unbalanced sets measured 30-45 % slower, and sets
+    that leave an XCD empty are ignored by the runtime."""
+    cus = train_cu_set(256, n_train, layout=layout)
+    assert len(cus) == len(set(cus)) == n_train
+    for part in (cus, sorted(set(range(256)) - set(cus))):
+        per = np.zeros((8, 4), dtype=int)
+        for c in part:
+            per[c % 8, (c // 8) % 4] += 1
+        if layout == "se-whole" and n_train % 64 == 0:  # whole SEs (else the spread fallback)
+            assert (per.sum(1) == len(part) // 8).all()
+            assert set(per.ravel()) <= {0, 8}
+        else:
+            assert (per == len(part) // 32).all()
 
 
 def test_cu_mask_words():
