@@ -761,6 +761,37 @@ int hbk_mlp_eval_count(const hbk_mlp_plan* p, const float* params, const void* p
                         as_stream(stream));
 }
 
+int hbk_mlp_eval_count_multi(const hbk_mlp_plan* p, const float* params, int32_t n_pools,
+                             const void* const* pools, int32_t pools_are_f16, const int64_t* n_pool,
+                             const int64_t* rows, const int64_t* row_offsets, const int32_t* labels,
+                             const uint64_t* seeds, float* const* counts, float activation_threshold,
+                             float dropout_p, void* workspace, int64_t ws_bytes, void* stream) {
+  using namespace hbk;
+  if (!p || !params || !workspace) return arg_error("NULL pointer");
+  if (!mlp_fused_supported(*p)) {
+    set_error("hbk: the evaluation pass covers the fused plans");
+    return HBK_ERR_UNSUPPORTED;
+  }
+  if (n_pools < 0 || n_pools > kEvalMaxSeg) return arg_error("n_pools must be in [0, 4]");
+  if (n_pools == 0) return HBK_OK;
+  if (!pools || !n_pool || !rows || !row_offsets || !labels || !seeds || !counts) return arg_error("NULL array");
+  if (dropout_p < 0.f || dropout_p >= 1.f) return arg_error("dropout_p must be in [0, 1)");
+  EvalSeg seg[kEvalMaxSeg];
+  int64_t max_rows = 0;
+  for (int i = 0; i < n_pools; ++i) {
+    if (rows[i] < 0 || row_offsets[i] < 0 || rows[i] + row_offsets[i] > (int64_t(1) << 31) / 768)
+      return arg_error("rows out of range");
+    if (rows[i] > 0 && (!pools[i] || n_pool[i] <= 0)) return arg_error("empty pool");
+    if (labels[i] != 0 && labels[i] != 1) return arg_error("label must be 0 or 1");
+    if (rows[i] > 0 && !counts[i]) return arg_error("counts is NULL");
+    seg[i] = EvalSeg{pools[i], n_pool[i], rows[i], row_offsets[i], seeds[i], counts[i], labels[i]};
+    max_rows = std::max(max_rows, rows[i]);
+  }
+  if (ws_bytes < mlp_eval_ws_floats(*p, max_rows) * int64_t(sizeof(float))) return arg_error("workspace too small");
+  return mlp_eval_count_multi(*p, params, pools_are_f16 != 0, seg, n_pools, activation_threshold, dropout_p,
+                              static_cast<float*>(workspace), as_stream(stream));
+}
+
 int hbk_mlp_eval_finish(const float* counts_val, const float* counts_test, const double* sizes,
                         float target_false_positives_per_hour, float adjust_ratio, float* sched, int64_t sched_len,
                         int64_t next_step, float* out, void* stream) {

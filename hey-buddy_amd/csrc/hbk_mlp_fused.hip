@@ -1627,6 +1627,7 @@ __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
 // chunks ahead. The pre-bias HG0 rows go to a slab that k2_rows_kernel
 // <false> (the inference chain, with its counters) reads as its one K-split.
 constexpr int kKvKC = 64, kKvChunks = kD / kKvKC;
+constexpr int kKvMaxSeg = kEvalMaxSeg;
 struct KvArgs {
   const void* pool;      // f32 or f16 rows of 1536
   int64_t n_pool;
@@ -1646,6 +1647,15 @@ struct KvArgs {
   float* counts;  // [4]: counts[2 label] += #(p >= act_thr), counts[2 label + 1] += #(p > act_thr)
   int label;
   float* prob;    // [rows] or NULL
+  // several pools in one launch (hbk_mlp_eval_count_multi; nseg = 0: the fields above): workgroup
+  // b of segment s = the first segment with b < seg_tile0[s + 1] takes pool s's tile b - seg_tile0[s]
+  int nseg;
+  int seg_tile0[kKvMaxSeg + 1];
+  const void* seg_pool[kKvMaxSeg];
+  int64_t seg_npool[kKvMaxSeg], seg_rows[kKvMaxSeg], seg_r0[kKvMaxSeg];
+  uint64_t seg_seed[kKvMaxSeg];
+  float* seg_counts[kKvMaxSeg];
+  int seg_label[kKvMaxSeg];
 };
 
 __global__ void __launch_bounds__(256) kv_prep_kernel(const float* __restrict__ P, int64_t w0, int64_t g_in,
@@ -1714,7 +1724,25 @@ constexpr int kNetWLd = 104, kAld = 100;  // LDS row strides: weight halves (K <
 // W: waves per workgroup, 8 (f16 rows: two 16-row tiles per wave) or 16 (one tile per wave:
 // twice the waves per CU to hide the stream's latency, at most 128 VGPRs each)
 template <bool kF16, int NG, int W>
-__global__ void __launch_bounds__(64 * W) kv_gemm_kernel(KvArgs a) {
+__global__ void __launch_bounds__(64 * W) kv_gemm_kernel(KvArgs a0) {
+  // this workgroup's pool (segment): its fields replace the single-pool ones (uniform)
+  KvArgs a = a0;
+  int blk = static_cast<int>(blockIdx.x);
+  if (a0.nseg > 0) {
+    int sg = 0;
+#pragma unroll
+    for (int q = 1; q < kKvMaxSeg; ++q) sg += (q < a0.nseg && blk >= a0.seg_tile0[q]) ? 1 : 0;
+    blk -= a0.seg_tile0[sg];
+    a.pool = a0.seg_pool[sg];
+    a.n_pool = a0.seg_npool[sg];
+    a.idx = nullptr;
+    a.rows = a0.seg_rows[sg];
+    a.r0 = a0.seg_r0[sg];
+    a.seed = a0.seg_seed[sg];
+    a.counts = a0.seg_counts[sg];
+    a.label = a0.seg_label[sg];
+    a.prob = nullptr;
+  }
   // ONE __shared__ object: beside a second one hipcc drains the DMA (vmcnt(0))
   // before every chunk's first LDS read. GEMM phase: the W' ring (the row
   // statistics reuse buffer 0 after it); network phase: a stage's weight planes
@@ -1742,7 +1770,7 @@ __global__ void __launch_bounds__(64 * W) kv_gemm_kernel(KvArgs a) {
   constexpr int kDma = 32 / W;  // W' DMA instructions per wave and chunk (2 planes x 128 rows of 128 B)
   static_assert(kALoads * (kDepth - 1) + kDma < 16, "the counted waits use vmcnt's low field");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = lane & 15, kq = lane >> 4;
-  const int64_t tile0 = int64_t(blockIdx.x) * kTile;
+  const int64_t tile0 = int64_t(blk) * kTile;
   const char* rp[kRT];
   uint32_t rid[kRT];
 #pragma unroll
@@ -2514,26 +2542,26 @@ int mlp_eval_prepare(const hbk_mlp_plan& p, const float* params, float* ws, hipS
   return HBK_OK;
 }
 
-int mlp_eval_count(const hbk_mlp_plan& p, const float* params, const void* pool, bool f16, int64_t n_pool,
-                   const int32_t* idx, int64_t rows, int64_t r0, int label, float act_thr, float drop_p,
-                   uint64_t seed, float* counts, float* prob, float* ws, hipStream_t s) {
+// One kv_gemm_kernel launch over nseg pools of one dtype (nseg = 1: the single-pool fields,
+// which also allow idx / prob; nseg > 1: the segment table, workgroups in pool order).
+static int mlp_eval_launch(const hbk_mlp_plan& p, const float* params, bool f16, const EvalSeg* seg, int nseg,
+                           const int32_t* idx, float act_thr, float drop_p, float* prob, float* ws, hipStream_t s) {
   const int NG = static_cast<int>(p.g.size());
-  if (rows <= 0) return HBK_OK;
   const EvalWs w = eval_layout(NG);
   const WSplit wsp = make_wsplit(p);
   K2Args kc{};  // the weight cache's plane offsets as k2 reads them
   set_k2_cache(wsp, NG, reinterpret_cast<const _Float16*>(ws + w.wsplit), kc);
-  KvArgs ka;
-  ka.pool = pool;
-  ka.n_pool = n_pool;
+  KvArgs ka{};
+  ka.pool = seg[0].pool;
+  ka.n_pool = seg[0].n_pool;
   ka.idx = idx;
-  ka.rows = rows;
-  ka.r0 = r0;
+  ka.rows = seg[0].rows;
+  ka.r0 = seg[0].r0;
   ka.wq = reinterpret_cast<const _Float16*>(ws + w.wq);
   ka.c0 = ws + w.c0;
   ka.c1 = ws + w.c1;
   ka.drop_p = drop_p;
-  ka.seed = seed;
+  ka.seed = seg[0].seed;
   ka.P = params;
   for (int i = 0; i < kMaxG; ++i) {
     const int g = std::min(i, NG - 1);
@@ -2547,15 +2575,33 @@ int mlp_eval_count(const hbk_mlp_plan& p, const float* params, const void* pool,
   }
   ka.wc = kc.wc;
   ka.act_thr = act_thr;
-  ka.counts = counts;
-  ka.label = label;
+  ka.counts = seg[0].counts;
+  ka.label = seg[0].label;
   ka.prob = prob;
   // f16 rows: 16 waves of one 16-row tile each (126 VGPRs); f32 rows (the split's registers
   // spill at 128): 8 waves. HBK_KV_WAVES=8: 8 waves of two tiles for f16 rows too (A/B)
   static const bool w8 = getenv("HBK_KV_WAVES") && atoi(getenv("HBK_KV_WAVES")) == 8;
   const int waves = f16 && !w8 ? 16 : 8;
   const int tile = (f16 ? 256 : 128);  // kv_gemm_kernel's rows per workgroup
-  const dim3 grid(unsigned((rows + tile - 1) / tile));
+  int64_t tiles = (seg[0].rows + tile - 1) / tile;
+  ka.nseg = 0;
+  if (nseg > 1) {
+    ka.nseg = nseg;
+    tiles = 0;
+    for (int i = 0; i < nseg; ++i) {
+      ka.seg_tile0[i] = static_cast<int>(tiles);
+      ka.seg_pool[i] = seg[i].pool;
+      ka.seg_npool[i] = seg[i].n_pool;
+      ka.seg_rows[i] = seg[i].rows;
+      ka.seg_r0[i] = seg[i].r0;
+      ka.seg_seed[i] = seg[i].seed;
+      ka.seg_counts[i] = seg[i].counts;
+      ka.seg_label[i] = seg[i].label;
+      tiles += (seg[i].rows + tile - 1) / tile;
+    }
+    ka.seg_tile0[nseg] = static_cast<int>(tiles);
+  }
+  const dim3 grid(static_cast<unsigned>(tiles));
   auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(64 * waves), 0, s, ka); };
   if (waves == 16) {
     if (NG == 2) launch(kv_gemm_kernel<true, 2, 16>);
@@ -2572,6 +2618,24 @@ int mlp_eval_count(const hbk_mlp_plan& p, const float* params, const void* pool,
   }
   HBK_LAUNCH_CHECK("kv_gemm_kernel");
   return HBK_OK;
+}
+
+int mlp_eval_count(const hbk_mlp_plan& p, const float* params, const void* pool, bool f16, int64_t n_pool,
+                   const int32_t* idx, int64_t rows, int64_t r0, int label, float act_thr, float drop_p,
+                   uint64_t seed, float* counts, float* prob, float* ws, hipStream_t s) {
+  if (rows <= 0) return HBK_OK;
+  const EvalSeg seg{pool, n_pool, rows, r0, seed, counts, label};
+  return mlp_eval_launch(p, params, f16, &seg, 1, idx, act_thr, drop_p, prob, ws, s);
+}
+
+int mlp_eval_count_multi(const hbk_mlp_plan& p, const float* params, bool f16, const EvalSeg* seg, int nseg,
+                         float act_thr, float drop_p, float* ws, hipStream_t s) {
+  EvalSeg live[kKvMaxSeg];
+  int n = 0;
+  for (int i = 0; i < nseg; ++i)
+    if (seg[i].rows > 0) live[n++] = seg[i];
+  if (n == 0) return HBK_OK;
+  return mlp_eval_launch(p, params, f16, live, n, nullptr, act_thr, drop_p, nullptr, ws, s);
 }
 
 int mlp_eval_finish(const float* cv, const float* ct, const double* sizes, float target, float ratio, float* sched,

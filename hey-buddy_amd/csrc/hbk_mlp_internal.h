@@ -71,6 +71,17 @@ int mlp_eval_prepare(const hbk_mlp_plan& p, const float* params, float* ws, hipS
 int mlp_eval_count(const hbk_mlp_plan& p, const float* params, const void* pool, bool f16, int64_t n_pool,
                    const int32_t* idx, int64_t rows, int64_t r0, int label, float act_thr, float drop_p,
                    uint64_t seed, float* counts, float* prob, float* ws, hipStream_t s);
+// one pool of an evaluation launch (mlp_eval_count_multi: several pools of one dtype in one launch)
+struct EvalSeg {
+  const void* pool;
+  int64_t n_pool, rows, r0;
+  uint64_t seed;
+  float* counts;
+  int label;
+};
+constexpr int kEvalMaxSeg = 4;
+int mlp_eval_count_multi(const hbk_mlp_plan& p, const float* params, bool f16, const EvalSeg* seg, int nseg,
+                         float act_thr, float drop_p, float* ws, hipStream_t s);
 int mlp_eval_finish(const float* cv, const float* ct, const double* sizes, float target, float ratio, float* sched,
                     int64_t sched_len, int64_t next_step, float* out, hipStream_t s);
 }  // namespace hbk

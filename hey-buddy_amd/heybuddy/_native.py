@@ -115,6 +115,8 @@ _PROTOS = {
                                      _c_float, _c_float, _c_float, _vp, ctypes.c_int32, _vp, _c_int64, _vp]),
     "hbk_mlp_eval_workspace_size": (_c_int, [_vp, _c_int64, ctypes.POINTER(_c_int64)]),
     "hbk_mlp_eval_prepare": (_c_int, [_vp, _vp, _vp, _c_int64, _vp]),
+    "hbk_mlp_eval_count_multi": (_c_int, [_vp, _vp, ctypes.c_int32, _vp, ctypes.c_int32, _vp, _vp, _vp, _vp, _vp,
+                                          _vp, _c_float, _c_float, _vp, _c_int64, _vp]),
     "hbk_mlp_eval_count": (_c_int, [_vp, _vp, _vp, ctypes.c_int32, _c_int64, _vp, _c_int64, _c_int64,
                                     ctypes.c_int32, _c_float, _c_float, ctypes.c_uint64, _vp, _vp, _vp, _c_int64,
                                     _vp]),

@@ -565,6 +565,29 @@ class MlpPlan:
                                       float(activation_threshold), float(dropout_p), _u64_to_i64(seed), counts, prob,
                                       ws, self.id)
 
+    def eval_count_multi(self, params: torch.Tensor, parts, counts: torch.Tensor, ws: torch.Tensor,
+                         activation_threshold: float = 0.5, dropout_p: float = 0.0) -> None:
+        """eval_count for up to 4 pools of one dtype in ONE launch (hbk_mlp_eval_count_multi):
+        ``parts`` = [(pool, rows, row_offset, label, which, seed)], pool i counted into
+        counts[which] ([2, 4] f32), each exactly as its own eval_count (no idx, no prob)."""
+        dev = params.device
+        if not 0 < len(parts) <= 4:
+            raise ValueError("1 to 4 pools per launch")
+        dt = parts[0][0].dtype
+        for pool, rows, _, label, which, _ in parts:
+            if pool.dtype != dt or pool.dtype not in (torch.float32, torch.float16) or pool.device != dev \
+                    or not pool.is_contiguous() or pool.reshape(pool.shape[0], -1).shape[1] != self.d_in:
+                raise ValueError(f"pools must be contiguous [n, {self.d_in}] tensors of one dtype on {dev}")
+            if label not in (0, 1) or which not in (0, 1) or rows < 0:
+                raise ValueError("label / which must be 0 or 1, rows >= 0")
+        if counts.dtype != torch.float32 or counts.shape != (2, 4) or counts.device != dev \
+                or not counts.is_contiguous():
+            raise ValueError("counts must be a contiguous float32 [2, 4] device tensor")
+        torch.ops.hbk.mlp_eval_count_multi_(
+            params, [q[0] for q in parts], [int(q[1]) for q in parts], [int(q[2]) for q in parts],
+            [int(q[3]) for q in parts], [int(q[4]) for q in parts], [_u64_to_i64(q[5]) for q in parts],
+            float(activation_threshold), float(dropout_p), counts, ws, self.id)
+
     @staticmethod
     def eval_finish(counts_val: torch.Tensor | None, counts_test: torch.Tensor | None, sizes, out: torch.Tensor,
                     target: float = 1.5, ratio: float = 0.0, sched: torch.Tensor | None = None,
@@ -653,6 +676,23 @@ def _mlp_eval_count_op(params: torch.Tensor, pool: torch.Tensor, idx: torch.Tens
         ptr(idx) if idx is not None else None, rows, row_offset, label, activation_threshold, dropout_p,
         seed & (2 ** 64 - 1), ptr(counts), ptr(prob) if prob is not None else None, ptr(ws), ws.numel(),
         stream_ptr(params.device)), "hbk_mlp_eval_count")
+
+
+@torch.library.custom_op("hbk::mlp_eval_count_multi_", mutates_args=("counts", "ws"))
+def _mlp_eval_count_multi_op(params: torch.Tensor, pools: list[torch.Tensor], rows: list[int],
+                             row_offsets: list[int], labels: list[int], which: list[int], seeds: list[int],
+                             activation_threshold: float, dropout_p: float, counts: torch.Tensor, ws: torch.Tensor,
+                             plan_id: int) -> None:
+    plan = _plans[plan_id]
+    n = len(pools)
+    arr = lambda ct, vals: (ct * n)(*vals)  # noqa: E731
+    check(lib().hbk_mlp_eval_count_multi(
+        plan._handle, ptr(params), n, arr(ctypes.c_void_p, [ptr(q) for q in pools]),
+        1 if pools[0].dtype == torch.float16 else 0, arr(ctypes.c_int64, [q.shape[0] for q in pools]),
+        arr(ctypes.c_int64, rows), arr(ctypes.c_int64, row_offsets), arr(ctypes.c_int32, labels),
+        arr(ctypes.c_uint64, [v & (2 ** 64 - 1) for v in seeds]),
+        arr(ctypes.c_void_p, [counts.data_ptr() + 16 * w for w in which]), activation_threshold, dropout_p,
+        ptr(ws), ws.numel(), stream_ptr(params.device)), "hbk_mlp_eval_count_multi")
 
 
 @torch.library.custom_op("hbk::mlp_eval_finish_", mutates_args=("sched", "out"))

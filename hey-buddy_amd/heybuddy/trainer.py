@@ -314,19 +314,27 @@ class EvalPasses:
             else:
                 side.wait_stream(cur)
         rank, world = distributed.world(self.group)
+        # the f32 pools (validation positives, testing positives and adversarials: ~25 k rows
+        # each) in ONE launch (hbk_mlp_eval_count_multi): each alone is ~3 rounds of workgroups
+        # on a 64-CU stream run as 4; together their workgroups fill each other's last round
+        multi = [] if (side is None and cuda and os.environ.get("HBK_EVAL_MULTI", "1") != "0") else None
         for k, (pool, rows, label, which) in enumerate(self.parts):
             # data-parallel: this rank's contiguous share of the pass's rows (the
             # shares partition the pass); the per-rank dropout stream differs
             lo, hi = distributed.clip_range(rows, rank, world)
-            if hi > lo:
+            seed = (self.seed + 0x9E3779B97F4A7C15 * (self.n * 8 + k + 1) + 0xD1B54A32D192ED03 * rank) % (1 << 64)
+            if multi is not None and pool.dtype == torch.float32 and hi > lo:
+                multi.append((pool, hi - lo, (self.offsets[k] + lo) % pool.shape[0], label, which, seed))
+            elif hi > lo:
                 with torch.cuda.stream(side if side is not None and pool.dtype == torch.float32 else cur) \
                         if cuda else contextlib.nullcontext():
                     plan.eval_count(flat, pool, hi - lo, label, self.counts[which], self.ws,
                                     row_offset=(self.offsets[k] + lo) % pool.shape[0],
-                                    activation_threshold=self.act_thr, dropout_p=p,
-                                    seed=(self.seed + 0x9E3779B97F4A7C15 * (self.n * 8 + k + 1)
-                                          + 0xD1B54A32D192ED03 * rank) % (1 << 64))
+                                    activation_threshold=self.act_thr, dropout_p=p, seed=seed)
             self.offsets[k] = (self.offsets[k] + rows) % pool.shape[0]
+        if multi:
+            plan.eval_count_multi(flat, multi, self.counts, self.ws, activation_threshold=self.act_thr,
+                                  dropout_p=p)
         if side is not None:
             cur.wait_stream(side)
         # one all-reduce of the [2, 4] counts: every rank computes the same rates and

@@ -339,6 +339,16 @@ int hbk_mlp_eval_count(const hbk_mlp_plan* plan, const float* params, const void
                        int64_t n_pool, const int32_t* idx, int64_t rows, int64_t row_offset, int32_t label,
                        float activation_threshold, float dropout_p, uint64_t seed, float* counts, float* prob,
                        void* workspace, int64_t workspace_bytes, void* stream);
+/* hbk_mlp_eval_count for n_pools (<= 4) pools of one dtype in ONE launch: pool i's rows
+ * r = 0 .. rows[i]-1 are pool rows (row_offsets[i] + r) % n_pool[i], labelled labels[i], counted
+ * into counts[i] with dropout seed seeds[i], each exactly as its own hbk_mlp_eval_count (no idx, no
+ * prob); the workgroups of all pools share one grid, so small pools fill each other's last round.
+ * Host arrays of device pointers / values; workspace sized for the largest pool. */
+int hbk_mlp_eval_count_multi(const hbk_mlp_plan* plan, const float* params, int32_t n_pools,
+                             const void* const* pools, int32_t pools_are_f16, const int64_t* n_pool,
+                             const int64_t* rows, const int64_t* row_offsets, const int32_t* labels,
+                             const uint64_t* seeds, float* const* counts, float activation_threshold,
+                             float dropout_p, void* workspace, int64_t workspace_bytes, void* stream);
 int hbk_mlp_eval_finish(const float* counts_val, const float* counts_test, const double* sizes,
                         float target_false_positives_per_hour, float adjust_ratio, float* sched, int64_t sched_len,
                         int64_t next_step, float* out, void* stream);

@@ -107,6 +107,39 @@ def test_eval_chunk_boundary_and_ragged_tiles():
     np.testing.assert_array_equal(c, omlp.eval_counts(pr, 0))
 
 
+def test_eval_count_multi_equals_separate_launches():
+    """hbk_mlp_eval_count_multi: three f32 pools (ragged row counts, offsets, both labels, two
+    counter sets, dropout on) in one launch give exactly the counts of three hbk_mlp_eval_count
+    launches; the counts against the kernel's own probabilities (exact) and the oracle's."""
+    params = omlp.init_params(seed=8)
+    rng = np.random.default_rng(9)
+    host = [(rng.standard_normal((n, 16, 96)) * 1.3 + 0.2).astype(np.float32) for n in (301, 129, 77)]
+    # centre the output bias so that the predictions straddle the threshold (non-trivial counts)
+    _, z, _ = omlp.forward(params, np.concatenate(host))
+    params["mlp_out.output.bias"] = (params["mlp_out.output.bias"] - np.median(z) + 1e-3).astype(np.float32)
+    m = _model(params)
+    pools = [torch.from_numpy(h).cuda() for h in host]
+    parts = [(pools[0], 333, 7, 1, 0, 0x51), (pools[1], 129, 0, 1, 1, 0x52), (pools[2], 200, 40, 0, 1, 0x53)]
+    ws = torch.empty(m.plan.eval_workspace_bytes(400), dtype=torch.uint8, device="cuda")
+    m.plan.eval_prepare(m.flat_parameters, ws)
+    multi = torch.zeros((2, 4), device="cuda")
+    m.plan.eval_count_multi(m.flat_parameters, parts, multi, ws, dropout_p=0.1)
+    sep = torch.zeros((2, 4), device="cuda")
+    for pool, rows, off, label, which, seed in parts:
+        m.plan.eval_count(m.flat_parameters, pool, rows, label, sep[which], ws, row_offset=off, dropout_p=0.1,
+                          seed=seed)
+    torch.testing.assert_close(multi, sep, rtol=0, atol=0)
+    for pool, rows, off, label, which, seed in parts:  # each part's share against its own probabilities
+        c, pr = _run(m.plan, m.flat_parameters, pool, rows, label, p=0.1, seed=seed, row_offset=off)
+        n = pool.shape[0]
+        keep = omlp.dropout_keep(seed, off + np.arange(rows), p=0.1)
+        x = pool.cpu().numpy().reshape(n, -1)[(off + np.arange(rows)) % n] * keep / np.float32(0.9)
+        ref, _, _ = omlp.forward(params, x.reshape(rows, 16, 96))
+        np.testing.assert_allclose(pr, ref, atol=2e-5, rtol=0)
+        np.testing.assert_array_equal(c, omlp.eval_counts(pr, label))
+    assert 0 < multi[:, 0].sum() < 333 + 129 + 200  # both sides of the threshold
+
+
 def test_eval_finish_matches_reference_bookkeeping():
     from heybuddy.kernels import MlpPlan
     sizes = (500_000.0, 25_000.0, 25_000.0, 25_000.0)
