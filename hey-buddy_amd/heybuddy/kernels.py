@@ -710,10 +710,8 @@ def _mlp_eval_finish_op(counts_val: torch.Tensor | None, counts_test: torch.Tens
 def _place_clips_op(src: torch.Tensor, src_len: torch.Tensor, pre: torch.Tensor, T: int) -> torch.Tensor:
     n = src.shape[0]
     out = torch.empty((n, T), dtype=torch.float32, device=src.device)
-    for s in range(0, n, 65535):  # grid.y limit of one launch
-        m = min(65535, n - s)
-        check(lib().hbk_place_clips(ptr(src) + 4 * s * src.stride(0), m, src.stride(0),
-                                    ptr(src_len) + 4 * s, ptr(pre) + 4 * s, ptr(out) + 4 * s * T, T, T,
+    if n:
+        check(lib().hbk_place_clips(ptr(src), n, src.stride(0), ptr(src_len), ptr(pre), ptr(out), T, T,
                                     stream_ptr(src.device)), "hbk_place_clips")
     return out
 

@@ -521,7 +521,7 @@ int hbk_tanh_distortion(const float* x, int64_t n_clips, int64_t x_stride, const
  * The reference crops (pre = 0) when src_len >= T, else pads with
  * pre = np.random.randint(int(S/4), int(3S/4)) leading zeros, S = T - src_len
  * (pre = 0 when S == 1); the caller draws pre on the host with that rule.
- * T % 4 == 0, out rows 16-B aligned, n_clips <= 65535 per call. */
+ * T % 4 == 0, out rows 16-B aligned. One persistent launch (4,096-sample spans of the clips). */
 int hbk_place_clips(const float* src, int64_t n_clips, int64_t src_stride, const int32_t* src_len,
                     const int32_t* pre, float* out, int64_t out_stride, int64_t T, void* stream);
 
