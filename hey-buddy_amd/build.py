@@ -63,16 +63,10 @@ VARIANTS = {  # profiling builds (load with HBK_LIB=hey-buddy_amd/lib/<name>)
     "trace": ("libhbk_trace.so", ("-DHBK_TRACE",)),         # per-wave s_memtime timeline
     "pv32": ("libhbk_pv32.so", ("-DHBK_PV_F32STATE=1",)),  # the vocoder's sliding-DFT state in float32
     "pv32r": ("libhbk_pv32r.so", ("-DHBK_PV_F32STATE=1", "-DHBK_PV_RESTART=1024")),  # ... restarted every 1,024
-    "k2ab1": ("libhbk_k2ab1.so", ("-DHBK_K2_ABLATE=1",)),   # k2 ablation (timing only): weights loaded once
-    "k2ab2": ("libhbk_k2ab2.so", ("-DHBK_K2_ABLATE=2",)),   # k2 ablation (timing only): slab 0 read KS times
-    "kvab1": ("libhbk_kvab1.so", ("-DHBK_KV_ABLATE=1",)),   # eval ablation: the input GEMM only
-    "kvab2": ("libhbk_kvab2.so", ("-DHBK_KV_ABLATE=2",)),   # eval ablation: no dropout mask
-    "pvc1": ("libhbk_pvc1.so", ("-DHBK_PV_CLIPS=1",)),       # pitch vocoder: 1 clip per workgroup (A/B)
-    "pvr256": ("libhbk_pvr256.so", ("-DHBK_PV_RESTART=256",)),  # pitch vocoder: direct DFT every 256 frames
-    "pvab1": ("libhbk_pvab1.so", ("-DHBK_PV_ABLATE=1",)),    # pitch vocoder ablation: no bin reduction
-    "pvab2": ("libhbk_pvab2.so", ("-DHBK_PV_ABLATE=2",)),    # pitch vocoder ablation: no per-bin vocoder
-    "pvab3": ("libhbk_pvab3.so", ("-DHBK_PV_ABLATE=3",)),    # pitch vocoder ablation: neither
 }
+# Any other ablation / A/B build: --variant=NAME --define=MACRO[=VALUE] ... (e.g. --variant=kvab1
+# --define=HBK_KV_ABLATE=1 -> lib/libhbk_kvab1.so; the macros are documented where they are used:
+# HBK_K2_ABLATE, HBK_KV_ABLATE, HBK_PV_ABLATE, HBK_PV_CLIPS, HBK_PV_RESTART, HBK_X3_WAVES_PER_EU, HBK_X3_PF)
 
 
 def build(force: bool = False, variant: str | None = None) -> str:
@@ -97,4 +91,9 @@ def build(force: bool = False, variant: str | None = None) -> str:
 
 if __name__ == "__main__":
     var = next((a[len("--variant="):] for a in sys.argv if a.startswith("--variant=")), None)
+    defs = tuple("-D" + a[len("--define="):] for a in sys.argv if a.startswith("--define="))
+    if var and defs:
+        VARIANTS[var] = (f"libhbk_{var}.so", defs)
+    elif var and var not in VARIANTS:
+        sys.exit(f"unknown variant {var!r}: pass its macros with --define=MACRO[=VALUE]")
     print(build(force="--force" in sys.argv, variant=var))

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Evaluation-pass kernels: per-pass time on the whole GPU and on 64 CUs, with kernel stats.
-#   LIBS="libhbk.so libhbk_kvab1.so" CUS="64" bash tools/eval_probe.sh   (library A/B)
+#   LIBS="libhbk.so libhbk_kvab1.so" CUS="64" bash tools/eval_probe.sh   (library A/B; build the ablation with
+#   python hey-buddy_amd/build.py --variant=kvab1 --define=HBK_KV_ABLATE=1)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 export TMPDIR=/tmp
