@@ -35,7 +35,18 @@ constexpr int kMaxStages = 10;
 constexpr int kMaxWin = 32;
 constexpr int kLdsBudget = 78 * 1024;     // bytes per block: 2 blocks per CU
 constexpr int kLdsBudgetCU = 156 * 1024;  // one block per CU
-constexpr int kChunkClips = 16384;     // clips per workspace chunk
+constexpr int kChunkClips = 16384;     // clips per workspace chunk (default; HBK_EMBED_CHUNK overrides)
+// clips per workspace chunk: every chain kernel runs once per chunk (its last round of waves
+// partly filled); measured: 100 k clips in 16,384-clip chunks 24.30 ms, in 32,768-clip chunks
+// 24.43 ms, bit-identical (tools/embed_chunk_check.py), so the smaller workspace stays
+inline int64_t chunk_clips() {
+  static const int64_t c = [] {
+    const char* e = getenv("HBK_EMBED_CHUNK");
+    const long long v = e ? atoll(e) : 0;
+    return v >= 256 && v <= (int64_t(1) << 20) ? int64_t(v) : int64_t(kChunkClips);
+  }();
+  return c;
+}
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
@@ -3940,10 +3951,10 @@ int hbk_embed_workspace_size(const hbk_embed_plan* p, int64_t n, int64_t* bytes)
   using namespace hbk;
   if (!p || !bytes) return arg_error("plan/bytes is NULL");
   if (n < 0) return arg_error("negative n");
-  const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(n, kChunkClips));
+  const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(n, chunk_clips()));
   std::vector<int64_t> imgs, bc, bw;
   program_geometry(p->clip_prog, true, int(p->starts.size()), imgs, bc);
-  const int64_t chunk_w = std::max<int64_t>(1, std::min<int64_t>(n, kChunkClips));
+  const int64_t chunk_w = std::max<int64_t>(1, std::min<int64_t>(n, chunk_clips()));
   program_geometry(p->win_prog, false, 1, imgs, bw);
   const int64_t fc = chunk * (bc[0] + bc[1]);
   const int64_t fw = chunk_w * (bw[0] + bw[1]);
@@ -3964,7 +3975,7 @@ int hbk_embed_clips(const hbk_embed_plan* p, const float* mel, int64_t n_clips, 
   if (workspace_bytes < need) return arg_error("workspace too small");
   std::vector<int64_t> imgs, bufs;
   program_geometry(p->clip_prog, true, int(p->starts.size()), imgs, bufs);
-  const int64_t chunk = std::min<int64_t>(n_clips, kChunkClips);
+  const int64_t chunk = std::min<int64_t>(n_clips, chunk_clips());
   return run_program(p->clip_prog, mel, n_clips, mel_clip_stride, out,
                      int64_t(p->starts.size()) * p->out_dim, static_cast<float*>(workspace), chunk,
                      as_stream(stream), imgs, bufs, p->d_range);
@@ -3997,7 +4008,7 @@ int hbk_embed_clips_front(const hbk_embed_plan* p, const float* mel, int64_t n_c
   if (workspace_bytes < need) return arg_error("workspace too small");
   std::vector<int64_t> imgs, bufs;
   program_geometry(p->clip_prog, true, int(p->starts.size()), imgs, bufs);
-  const int64_t chunk = std::min<int64_t>(n_clips, kChunkClips);
+  const int64_t chunk = std::min<int64_t>(n_clips, chunk_clips());
   return run_program(p->clip_prog, mel, n_clips, mel_clip_stride, mid, mid_floats, static_cast<float*>(workspace),
                      chunk, as_stream(stream), imgs, bufs, p->d_range, 0, n_front);
 }
@@ -4016,7 +4027,7 @@ int hbk_embed_clips_back(const hbk_embed_plan* p, const float* mid, int64_t n_cl
   if (workspace_bytes < need) return arg_error("workspace too small");
   std::vector<int64_t> imgs, bufs;
   program_geometry(p->clip_prog, true, int(p->starts.size()), imgs, bufs);
-  const int64_t chunk = std::min<int64_t>(n_clips, kChunkClips);
+  const int64_t chunk = std::min<int64_t>(n_clips, chunk_clips());
   return run_program(p->clip_prog, mid, n_clips, mid_floats, out, int64_t(p->starts.size()) * p->out_dim,
                      static_cast<float*>(workspace), chunk, as_stream(stream), imgs, bufs, p->d_range, n_front, -1);
 }
@@ -4033,7 +4044,7 @@ int hbk_embed_windows(const hbk_embed_plan* p, const float* windows, int64_t n, 
   if (workspace_bytes < need) return arg_error("workspace too small");
   std::vector<int64_t> imgs, bufs;
   program_geometry(p->win_prog, false, 1, imgs, bufs);
-  const int64_t chunk = std::min<int64_t>(n, int64_t(kChunkClips));
+  const int64_t chunk = std::min<int64_t>(n, chunk_clips());
   return run_program(p->win_prog, windows, n, int64_t(p->in_h) * p->in_w, out, p->out_dim,
                      static_cast<float*>(workspace), chunk, as_stream(stream), imgs, bufs, p->d_range);
 }
