@@ -640,7 +640,9 @@ def setup_e2e(args, dev, rank, world, seed):
     import numpy as np
     from heybuddy.dataset.augmented import AugmentedAudioGenerator
     from heybuddy.embedding_graph import WINDOW_STARTS
+    from heybuddy._native import lib
     from heybuddy.embeddings import default_graph, embed_plan, replace_nan_rows_device
+    from heybuddy.kernels import nan_rows_fix
     from heybuddy.kernels import embed_clips, mel_frames
     from heybuddy.spectrogram import default_mel_plan
     from heybuddy.synthetic import impulse_responses, noise_bank, speech_clips
@@ -664,6 +666,21 @@ def setup_e2e(args, dev, rank, world, seed):
     # (the all-NaN case's source: no masked fill over the pool)
     raw_ext = torch.zeros((n + 1,) + tuple(pool.shape[1:]), dtype=torch.float32, device=dev)
     raw = raw_ext[:n]
+    # r05: the embedding writes the pool itself and hbk_nan_rows_fix patches its NaN rows in place
+    # (no gather copy of the pool, no torch reduction / sort; HBK_NAN_INPLACE=0: the gather form)
+    nan_inplace = os.environ.get("HBK_NAN_INPLACE", "1") != "0"
+    nan_ws = [torch.empty(int(lib().hbk_nan_rows_workspace_size(n)), dtype=torch.uint8, device=dev) for _ in range(2)]
+    nan_seed = [seed * 7919]
+
+    def emb_target(pool_t):
+        return pool_t if nan_inplace else raw
+
+    def finish_pool(pool_t, k=0):
+        nan_seed[0] += 1
+        if nan_inplace:
+            nan_rows_fix(pool_t, seed=nan_seed[0], ws=nan_ws[k])
+        else:
+            replace_nan_rows_device(raw_ext, out=pool_t, zero_row=True)  # no host sync
     # precalculated negatives (the reference's hosted f16 sets): large 2/3, medium 1/3
     g = torch.Generator(device=dev).manual_seed(seed + 4)
     n_neg = 200_000
@@ -792,8 +809,8 @@ def setup_e2e(args, dev, rank, world, seed):
         frames = mel_frames(x, mplan, N_FRAMES)
         if evs:
             evs[2].record(stream)
-        embed_clips(frames, eplan, out=raw)
-        replace_nan_rows_device(raw_ext, out=pool, zero_row=True)  # no host sync
+        embed_clips(frames, eplan, out=emb_target(pool))
+        finish_pool(pool)
         if evs:
             evs[3].record(stream)
         eval_events.append([])
@@ -863,13 +880,13 @@ def setup_e2e(args, dev, rank, world, seed):
                     if a1:
                         eplan.clips_front(frames[:a1], K - 1, mids1[b])
                     if a1 < n and whole:
-                        embed_clips(frames[a1:], eplan, out=raw[a1:])
+                        embed_clips(frames[a1:], eplan, out=emb_target(pools[b])[a1:])
                     elif a1 < n:
                         eplan.clips_front(frames[a1:], K, mids[b])
                     front_done[b].record(fs)
                 else:
-                    embed_clips(frames, eplan, out=raw)
-                    replace_nan_rows_device(raw_ext, out=pools[b], zero_row=True)
+                    embed_clips(frames, eplan, out=emb_target(pools[b]))
+                    finish_pool(pools[b], b)
                     feat_done[b].record(fs)
                 if part is not None:
                     part.append(("featurize", e0, mark("featurize", fs)))
@@ -880,10 +897,10 @@ def setup_e2e(args, dev, rank, world, seed):
             with torch.cuda.stream(ts):
                 ts.wait_event(front_done[b])
                 if a1:
-                    eplan.clips_back(mids1[b], a1, K - 1, raw[:a1])
+                    eplan.clips_back(mids1[b], a1, K - 1, emb_target(pools[b])[:a1])
                 if a1 < n and not whole:
-                    eplan.clips_back(mids[b], n - a1, K, raw[a1:])
-                replace_nan_rows_device(raw_ext, out=pools[b], zero_row=True)
+                    eplan.clips_back(mids[b], n - a1, K, emb_target(pools[b])[a1:])
+                finish_pool(pools[b], b)
                 feat_done[b].record(ts)
 
         def step(evs):  # noqa: F811

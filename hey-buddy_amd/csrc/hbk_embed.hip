@@ -3943,6 +3943,112 @@ void program_geometry(const Program& prog, bool clip_path, int n_win, std::vecto
 }
 
 }  // namespace
+
+// ---- NaN rows (embeddings.py:209-234): in place, no host synchronisation ----
+// Three grid-wide launches, each a no-op past one load when the batch has no NaN row:
+// nan_flags_kernel: block b owns the contiguous rows [b*per, (b+1)*per) (one wave per row,
+//   float4 loads): flags[r] = 1 for a NaN row, which is appended to bad[] (meta[0] counts
+//   them; the order is free, a row's draw depends on (seed, row) only), and blk_good[b] counts
+//   the block's NaN-free rows.
+// nan_list_kernel: block b lists its NaN-free rows in order at the offset sum(blk_good[< b])
+//   (ballot scans over 256-row slices), so good[] is every NaN-free row, ascending.
+// nan_patch_kernel: one wave per NaN row copies good[h % n_good], h a hash of (seed, row) — a
+//   uniformly drawn NaN-free clip, as the reference's np.random.choice — or writes zeros when
+//   every row is NaN.
+constexpr int kNanBlocks = 2048;  // flags / list blocks at most (blk_good's length)
+constexpr int kNanPatchBlocks = 512;
+
+__global__ void __launch_bounds__(256) nan_flags_kernel(const float* __restrict__ rows, int64_t n, int64_t row_len,
+                                                        int64_t per, int32_t* __restrict__ flags,
+                                                        int32_t* __restrict__ blk_good, int32_t* __restrict__ bad,
+                                                        int32_t* __restrict__ meta) {
+  __shared__ int32_t s_good;
+  if (threadIdx.x == 0) s_good = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t lo = static_cast<int64_t>(blockIdx.x) * per, hi = min<int64_t>(n, lo + per);
+  int32_t n_good = 0;
+  for (int64_t r = lo + wave; r < hi; r += 4) {
+    const float4* p = reinterpret_cast<const float4*>(rows + r * row_len);
+    bool nan = false;
+    for (int64_t j = lane; j < row_len / 4; j += 64) {
+      const float4 v = p[j];
+      nan |= (v.x != v.x) | (v.y != v.y) | (v.z != v.z) | (v.w != v.w);
+    }
+    const bool any = __ballot(nan) != 0;
+    if (lane == 0) {
+      flags[r] = any ? 1 : 0;
+      if (any)
+        bad[atomicAdd(meta, 1)] = static_cast<int32_t>(r);
+      else
+        ++n_good;
+    }
+  }
+  if (lane == 0) atomicAdd(&s_good, n_good);
+  __syncthreads();
+  if (threadIdx.x == 0) blk_good[blockIdx.x] = s_good;
+}
+
+__global__ void __launch_bounds__(256) nan_list_kernel(int64_t n, int64_t per, const int32_t* __restrict__ flags,
+                                                       const int32_t* __restrict__ blk_good,
+                                                       int32_t* __restrict__ good, const int32_t* __restrict__ meta) {
+  __shared__ int32_t s_w[4];
+  __shared__ int32_t s_off;
+  if (meta[0] == 0) return;  // uniform: the common case
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int32_t off = 0;  // NaN-free rows of the blocks before this one
+  for (int i = tid; i < static_cast<int>(blockIdx.x); i += 256) off += blk_good[i];
+  for (int o = 32; o > 0; o >>= 1) off += __shfl_xor(off, o, 64);
+  if (lane == 0) s_w[wave] = off;
+  __syncthreads();
+  if (tid == 0) s_off = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+  __syncthreads();
+  off = s_off;
+  const int64_t lo = static_cast<int64_t>(blockIdx.x) * per, hi = min<int64_t>(n, lo + per);
+  for (int64_t base = lo; base < hi; base += 256) {
+    const int64_t r = base + tid;
+    const bool keep = r < hi && flags[r] == 0;
+    const uint64_t m = __ballot(keep);
+    const int32_t below = __popcll(m & ((uint64_t(1) << lane) - 1));
+    __syncthreads();  // s_w of the previous slice has been read
+    if (lane == 0) s_w[wave] = __popcll(m);
+    __syncthreads();
+    int32_t pre = 0;
+    for (int w = 0; w < wave; ++w) pre += s_w[w];
+    if (keep) good[off + pre + below] = static_cast<int32_t>(r);
+    off += s_w[0] + s_w[1] + s_w[2] + s_w[3];
+  }
+}
+
+__device__ __forceinline__ uint64_t nan_hash(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ void __launch_bounds__(256) nan_patch_kernel(float* __restrict__ rows, int64_t n, int64_t row_len,
+                                                        const int32_t* __restrict__ bad,
+                                                        const int32_t* __restrict__ good,
+                                                        const int32_t* __restrict__ meta, uint64_t seed) {
+  const int64_t n_bad = meta[0];
+  if (n_bad == 0) return;
+  const int64_t n_good = n - n_bad;
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = static_cast<int64_t>(gridDim.x) * 4;
+  for (int64_t i = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) >> 6; i < n_bad; i += nw) {
+    const int64_t r = bad[i];
+    float4* dst = reinterpret_cast<float4*>(rows + r * row_len);
+    if (n_good == 0) {
+      for (int64_t j = lane; j < row_len / 4; j += 64) dst[j] = float4{0.f, 0.f, 0.f, 0.f};
+      continue;
+    }
+    const uint64_t h = nan_hash(seed ^ (0x9E3779B97F4A7C15ull * static_cast<uint64_t>(r + 1)));
+    const int64_t src = good[static_cast<int64_t>((static_cast<unsigned __int128>(h) * static_cast<uint64_t>(n_good)) >> 64)];
+    const float4* sp = reinterpret_cast<const float4*>(rows + src * row_len);
+    for (int64_t j = lane; j < row_len / 4; j += 64) dst[j] = sp[j];
+  }
+}
+
 }  // namespace hbk
 
 extern "C" {
@@ -4047,6 +4153,42 @@ int hbk_embed_windows(const hbk_embed_plan* p, const float* windows, int64_t n, 
   const int64_t chunk = std::min<int64_t>(n, chunk_clips());
   return run_program(p->win_prog, windows, n, int64_t(p->in_h) * p->in_w, out, p->out_dim,
                      static_cast<float*>(workspace), chunk, as_stream(stream), imgs, bufs, p->d_range);
+}
+
+int64_t hbk_nan_rows_workspace_size(int64_t n) {
+  return n < 0 ? 0 : (3 * n + hbk::kNanBlocks + 1) * int64_t(sizeof(int32_t));
+}
+
+int hbk_nan_rows_fix(float* rows, int64_t n, int64_t row_len, uint64_t seed, void* workspace,
+                     int64_t workspace_bytes, void* stream) {
+  using namespace hbk;
+  if (n < 0 || row_len <= 0 || row_len % 4) return arg_error("n >= 0, row_len a positive multiple of 4");
+  if (n == 0) return HBK_OK;
+  if (n >= (int64_t(1) << 31)) return arg_error("n >= 2^31 rows");
+  if (!rows || !workspace) return arg_error("NULL pointer");
+  if ((reinterpret_cast<uintptr_t>(rows) & 15)) return arg_error("rows must be 16-B aligned");
+  if (workspace_bytes < hbk_nan_rows_workspace_size(n)) return arg_error("workspace too small");
+  int32_t* flags = static_cast<int32_t*>(workspace);  // [n]
+  int32_t* good = flags + n;                          // [n]
+  int32_t* bad = good + n;                            // [n]
+  int32_t* blk_good = bad + n;                        // [kNanBlocks]
+  int32_t* meta = blk_good + kNanBlocks;              // [1]: NaN rows
+  hipStream_t st = as_stream(stream);
+  hipError_t e = hipMemsetAsync(meta, 0, sizeof(int32_t), st);
+  if (e != hipSuccess) return hip_error(e, "hbk_nan_rows_fix");
+  const int64_t blocks = std::min<int64_t>(kNanBlocks, (n + 3) / 4);
+  const int64_t per = (n + blocks - 1) / blocks;
+  const int64_t used = (n + per - 1) / per;  // every launched block owns at least one row
+  hipLaunchKernelGGL(nan_flags_kernel, dim3(unsigned(used)), dim3(256), 0, st, rows, n, row_len, per, flags,
+                     blk_good, bad, meta);
+  HBK_LAUNCH_CHECK("nan_flags_kernel");
+  hipLaunchKernelGGL(nan_list_kernel, dim3(unsigned(used)), dim3(256), 0, st, n, per, flags, blk_good, good, meta);
+  HBK_LAUNCH_CHECK("nan_list_kernel");
+  const int64_t pblocks = std::min<int64_t>(kNanPatchBlocks, (n + 3) / 4);
+  hipLaunchKernelGGL(nan_patch_kernel, dim3(unsigned(pblocks)), dim3(256), 0, st, rows, n, row_len, bad, good, meta,
+                     seed);
+  HBK_LAUNCH_CHECK("nan_patch_kernel");
+  return HBK_OK;
 }
 
 int hbk_embed_range_status(const hbk_embed_plan* p, int32_t* tripped, int32_t reset, void* stream) {

@@ -71,6 +71,8 @@ _PROTOS = {
     "hbk_embed_clips_front": (_c_int, [_vp, _vp, _c_int64, _c_int64, ctypes.c_int32, _vp, _vp, _c_int64, _vp]),
     "hbk_embed_clips_back": (_c_int, [_vp, _vp, _c_int64, ctypes.c_int32, _vp, _vp, _c_int64, _vp]),
     "hbk_embed_windows": (_c_int, [_vp, _vp, _c_int64, _vp, _vp, _c_int64, _vp]),
+    "hbk_nan_rows_workspace_size": (_c_int64, [_c_int64]),
+    "hbk_nan_rows_fix": (_c_int, [_vp, _c_int64, _c_int64, ctypes.c_uint64, _vp, _c_int64, _vp]),
     "hbk_embed_range_status": (_c_int, [_vp, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32, _vp]),
     "hbk_reverb_plan_create": (_c_int, [_c_int64, ctypes.POINTER(_vp)]),
     "hbk_reverb_plan_destroy": (_c_int, [_vp]),

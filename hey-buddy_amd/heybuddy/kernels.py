@@ -706,6 +706,31 @@ def _mlp_eval_finish_op(counts_val: torch.Tensor | None, counts_test: torch.Tens
         next_step, ptr(out), stream_ptr(out.device)), "hbk_mlp_eval_finish")
 
 
+@torch.library.custom_op("hbk::nan_rows_fix_", mutates_args=("rows", "ws"))
+def _nan_rows_fix_op(rows: torch.Tensor, seed: int, ws: torch.Tensor) -> None:
+    n = rows.shape[0]
+    check(lib().hbk_nan_rows_fix(ptr(rows), n, rows.numel() // max(n, 1), seed & (2 ** 64 - 1), ptr(ws), ws.numel(),
+                                 stream_ptr(rows.device)), "hbk_nan_rows_fix")
+
+
+def nan_rows_fix(rows: torch.Tensor, seed: int = 0, ws: torch.Tensor | None = None) -> torch.Tensor:
+    """In place (hbk_nan_rows_fix): every row of rows [n, ...] (f32, contiguous, a multiple of
+    4 elements per row) holding a NaN takes a uniformly drawn NaN-free row (a hash of (seed,
+    row)), or zeros when every row holds a NaN; no host synchronisation. ``ws``: a uint8
+    device tensor of >= hbk_nan_rows_workspace_size(n) bytes (allocated when None)."""
+    _native.require_device(rows.device)
+    n = rows.shape[0]
+    if rows.dtype != torch.float32 or not rows.is_contiguous() or (n and (rows.numel() // n) % 4):
+        raise ValueError("rows must be a contiguous float32 [n, ...] tensor with a multiple of 4 values per row")
+    if n == 0:
+        return rows
+    need = int(lib().hbk_nan_rows_workspace_size(n))
+    if ws is None or ws.numel() < need:
+        ws = torch.empty(need, dtype=torch.uint8, device=rows.device)
+    torch.ops.hbk.nan_rows_fix_(rows, _u64_to_i64(seed), ws)
+    return rows
+
+
 @torch.library.custom_op("hbk::place_clips", mutates_args=())
 def _place_clips_op(src: torch.Tensor, src_len: torch.Tensor, pre: torch.Tensor, T: int) -> torch.Tensor:
     n = src.shape[0]

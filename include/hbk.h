@@ -179,6 +179,16 @@ int hbk_embed_clips_back(const hbk_embed_plan* plan, const float* mid, int64_t n
 int hbk_embed_windows(const hbk_embed_plan* plan, const float* windows, int64_t n, float* out,
                       void* workspace, int64_t workspace_bytes, void* stream);
 
+/* NaN rows of an embedding batch, in place (embeddings.py:209-234): rows [n, row_len] f32
+ * (row_len % 4 == 0, 16-B aligned; one row = one clip's embeddings). Every row holding a NaN
+ * is replaced by a NaN-free row drawn uniformly (a counter-based hash of (seed, row) in place
+ * of np.random.choice), or by zeros when every row holds a NaN; NaN-free rows are unchanged.
+ * No host synchronisation (the reference's warning needs the count on the host and is not
+ * emitted). workspace: hbk_nan_rows_workspace_size(n) bytes. */
+int64_t hbk_nan_rows_workspace_size(int64_t n);
+int hbk_nan_rows_fix(float* rows, int64_t n, int64_t row_len, uint64_t seed, void* workspace,
+                     int64_t workspace_bytes, void* stream);
+
 /* Range guard of SPLIT_F16 plans (no reference counterpart: the ONNX graph runs
  * in f32). *tripped = 1 if any split kernel of this plan saw an activation with
  * |x| >= 65504 since the flag was last cleared (those outputs are not

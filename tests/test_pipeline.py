@@ -130,3 +130,61 @@ def test_replace_nan_rows_device_gpu():
     assert not torch.isnan(out).any()
     keep = [i for i in range(64) if i not in (5, 40)]
     assert torch.equal(out[keep], e[keep])
+
+
+@pytest.mark.gpu
+def test_nan_rows_fix_in_place():
+    """hbk_nan_rows_fix (embeddings.py:209-234 in place, no host sync): NaN-free rows keep their
+    bits, every NaN row becomes a copy of some NaN-free row, the draw depends on the seed and
+    covers several sources, an all-NaN batch becomes zeros, a clean batch is untouched."""
+    from heybuddy.kernels import nan_rows_fix
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(3)
+    for n in (1, 7, 3000):
+        e = torch.randn(n, 16, 96, device=dev, generator=g)
+        ref = e.clone()
+        bad = sorted({int(v) for v in torch.randint(0, n, (max(1, n // 5),), generator=g, device=dev).tolist()})
+        if n > 1:
+            bad = [b for b in bad if b != 0] or [n - 1]  # keep row 0 clean
+        for i, b in enumerate(bad):
+            e[b].view(-1)[(i * 37) % 1536] = float("nan")
+        if n == 1:
+            nan_rows_fix(e, seed=1)
+            assert torch.equal(e, torch.zeros_like(e))  # every row NaN: zeros
+            continue
+        good = [i for i in range(n) if i not in bad]
+        nan_rows_fix(e, seed=11)
+        assert not torch.isnan(e).any()
+        assert torch.equal(e[good], ref[good])
+        src = []
+        for b in bad:  # each patched row equals one NaN-free source row
+            d = (ref[good] - e[b]).abs().flatten(1).amax(1)
+            hit = torch.nonzero(d == 0).flatten()
+            assert hit.numel() >= 1, f"row {b} is not a copy of a NaN-free row"
+            src.append(good[int(hit[0])])
+        if len(bad) >= 20:
+            assert len(set(src)) > len(bad) // 4  # spread over many sources
+    # a clean batch is left exactly as it is; an all-NaN batch becomes zeros
+    e = torch.randn(257, 16, 96, device=dev, generator=g)
+    ref = e.clone()
+    nan_rows_fix(e, seed=2)
+    assert torch.equal(e, ref)
+    e.fill_(float("nan"))
+    nan_rows_fix(e, seed=2)
+    assert torch.equal(e, torch.zeros_like(e))
+    # many blocks (2048 row ranges) and few NaN-free rows: the ordered list spans the blocks;
+    # the same seed draws the same sources
+    n = 100_003
+    e = torch.full((n, 16, 96), float("nan"), device=dev)
+    keep = torch.tensor([5, 40_000, 99_999, 100_002], device=dev)
+    e[keep] = torch.randn(len(keep), 16, 96, device=dev, generator=g)
+    ref = e[keep].clone()
+    e2 = e.clone()
+    nan_rows_fix(e, seed=9)
+    nan_rows_fix(e2, seed=9)
+    assert torch.equal(e, e2)
+    assert torch.equal(e[keep], ref)
+    flat = e.flatten(1)
+    hits = torch.stack([(flat == ref[i].flatten()).all(1) for i in range(len(keep))])
+    assert bool(hits.any(0).all())  # every row is one of the 4 NaN-free rows
+    assert bool((hits.sum(1) > n // 8).all())  # each drawn about n / 4 times
