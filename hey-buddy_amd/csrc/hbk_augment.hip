@@ -1655,7 +1655,6 @@ struct PvClip {
 };
 struct PvShared {
   cf tw[256];                 // e^{+2 pi i q / 250}
-  float4 tw4[256];            // (x, y, -y, x) of tw[q]: complex products by tw[q] or its conjugate without negations
   double tw64[256][2];        // e^{-2 pi i q / 250}, float64
   float4 wt[3][128];          // w^j, w^{j+1} (j = 1, 3, 5) of bin lane, lane-major (one ds_read_b128 per wave)
   PvClip c[kPvClips];
@@ -1682,6 +1681,42 @@ __device__ __forceinline__ float pv_swap_add(float x, float y) {
   else
     asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(x), "+v"(y));
   return x + y;
+}
+
+// Complex products as two packed instructions with the operand swaps and the sign in the
+// VOP3P op_sel / neg modifiers (the compiler materialises a negated or swapped pair with
+// extra moves): a b = (a.x b.x - a.y b.y, a.x b.y + a.y b.x) and a conj(b)
+__device__ __forceinline__ cf pv_cmul(cf a, cf b) {
+  cf t, r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(b));  // (a.x b.x, a.x b.y)
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]" : "=v"(r) : "v"(a), "v"(b), "v"(t));
+  return r;
+}
+__device__ __forceinline__ cf pv_cmul_conj(cf a, cf b) {
+  cf t, r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1] neg_hi:[0,1]" : "=v"(t) : "v"(a), "v"(b));  // (a.x b.x, -a.x b.y)
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1]" : "=v"(r) : "v"(a), "v"(b), "v"(t));
+  return r;
+}
+
+typedef float pv_v4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const pv_v4 pv_lds_v4;  // an LDS float4 (32-bit address)
+__device__ __forceinline__ float4 pv_f4(pv_v4 v) { return float4{v.x, v.y, v.z, v.w}; }
+
+// sum_{j = 1..6} d_j w^j of a slide (d_j in da.yzw, db.xyz; w^j pairs in w12, w34, w56): one packed
+// product and five packed FMAs, each d_j broadcast by op_sel (no register copies)
+__device__ __forceinline__ cf pv_inc(float4 da, float4 db, float4 w12, float4 w34, float4 w56) {
+  const cf dxy = {da.x, da.y}, dzw = {da.z, da.w}, exy = {db.x, db.y}, ez = {db.z, db.w};
+  const cf w1 = {w12.x, w12.y}, w2 = {w12.z, w12.w}, w3 = {w34.x, w34.y}, w4 = {w34.z, w34.w};
+  const cf w5 = {w56.x, w56.y}, w6 = {w56.z, w56.w};
+  cf acc;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]" : "=v"(acc) : "v"(dxy), "v"(w1));
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,0,0] op_sel_hi:[0,1,1]" : "+v"(acc) : "v"(dzw), "v"(w2));
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "v"(dzw), "v"(w3));
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,0,0] op_sel_hi:[0,1,1]" : "+v"(acc) : "v"(exy), "v"(w4));
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "v"(exy), "v"(w5));
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,0,0] op_sel_hi:[0,1,1]" : "+v"(acc) : "v"(ez), "v"(w6));
+  return acc;
 }
 
 // padded sample p of clip row xr (reflect padding by n_fft / 2)
@@ -1711,7 +1746,7 @@ __device__ __forceinline__ void pv_load_rows(const PitchArgs& a, PvShared& sh, c
         delta += (vin != 0.f) - (vout != 0.f);
         if (j >= 4) dr[j] = vin - vout;
       }
-      dr[7] = static_cast<float>(delta);
+      dr[7] = __builtin_bit_cast(float, delta);  // the count change as int bits (read by SALU)
     }
   }
 }
@@ -1751,7 +1786,6 @@ ps_vocoder_kernel(PitchArgs a) {
     double sn, cs;
     sincospi(2.0 * q / kPsFft, &sn, &cs);
     sh.tw[q] = cf{static_cast<float>(cs), static_cast<float>(sn)};
-    sh.tw4[q] = float4{static_cast<float>(cs), static_cast<float>(sn), -static_cast<float>(sn), static_cast<float>(cs)};
     sh.tw64[q][0] = cs;
     sh.tw64[q][1] = -sn;
   }
@@ -1815,10 +1849,13 @@ ps_vocoder_kernel(PitchArgs a) {
   if (cnt == 0) xre = xim = pv_t(0);
   int sf = 0;  // last slid frame
   int anchor = 0;  // frame of the last direct DFT
+  static_assert(sizeof(sh.wt[0]) == 128 * sizeof(float4), "wt rows of 128 lanes");
+  uint32_t wt_addr = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((const pv_lds_v4*)&sh.wt[0][lane]));
   // the sliding DFT's next frame (sf + 1) from the current state, as a candidate
   // (xre, xim, cnt are committed by the caller): two partial sums per component
   // keep the float64 dependency chain short
-  auto slide_to = [&](pv_t& nre, pv_t& nim, int& ncnt) {
+  // drow: frame sf + 1's d row (C.d[sf + 1 - fb]; a FULL group passes its rows at constant offsets)
+  auto slide_to = [&](pv_t& nre, pv_t& nim, int& ncnt, const float* drow) {
     const int f = sf + 1;
     if (f >= a.f_in) {
       nre = nim = pv_t(0);
@@ -1827,19 +1864,16 @@ ps_vocoder_kernel(PitchArgs a) {
     }
     // the increment sum_j d_j w^j in float32 (packed; d_j rounded once to float32): its
     // rounding enters the float64 state as a random walk far below the state's level
-    const float4* drv = reinterpret_cast<const float4*>(C.d[f - fb]);
+    // the (loop-invariant) table reads stay in the loop, out of VGPRs: the lane's LDS address is
+    // made opaque in place (no copy, no address arithmetic per frame: ds_read_b128 wt_addr offset:..)
+    asm volatile("" : "+v"(wt_addr));
+    const pv_lds_v4* wtp = (const pv_lds_v4*)static_cast<uintptr_t>(wt_addr);
+    const float4 w12 = pv_f4(wtp[0]), w34 = pv_f4(wtp[128]), w56 = pv_f4(wtp[256]);
+    const float4* drv = reinterpret_cast<const float4*>(drow);
     const float4 da = drv[0], db = drv[1];
-    int wl = lane;
-    asm volatile("" : "+v"(wl));  // opaque: keeps the (loop-invariant) table reads in the loop, out of VGPRs
-    const float4 w12 = sh.wt[0][wl], w34 = sh.wt[1][wl], w56 = sh.wt[2][wl];
-    cf acc = {da.x, 0.f};  // w^0 = 1
-    acc = __builtin_elementwise_fma(cf{da.y, da.y}, cf{w12.x, w12.y}, acc);
-    acc = __builtin_elementwise_fma(cf{da.z, da.z}, cf{w12.z, w12.w}, acc);
-    acc = __builtin_elementwise_fma(cf{da.w, da.w}, cf{w34.x, w34.y}, acc);
-    acc = __builtin_elementwise_fma(cf{db.x, db.x}, cf{w34.z, w34.w}, acc);
-    acc = __builtin_elementwise_fma(cf{db.y, db.y}, cf{w56.x, w56.y}, acc);
-    acc = __builtin_elementwise_fma(cf{db.z, db.z}, cf{w56.z, w56.w}, acc);
-    ncnt = __builtin_amdgcn_readfirstlane(cnt + static_cast<int>(db.w));  // a clip's count: wave-uniform
+    cf acc = pv_inc(da, db, w12, w34, w56);
+    acc.x += da.x;  // w^0 = 1
+    ncnt = cnt + __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, db.w));  // a clip's count: wave-uniform
     const pv_t ar = xre + static_cast<pv_t>(acc.x), ai = xim + static_cast<pv_t>(acc.y);
     nre = ar * rr - ai * ri;
     nim = ar * ri + ai * rr;
@@ -1868,10 +1902,10 @@ ps_vocoder_kernel(PitchArgs a) {
   {
     pv_t nre, nim;
     int ncnt;
-    slide_to(nre, nim, ncnt);
+    slide_to(nre, nim, ncnt, C.d[sf + 1 - fb]);
     commit(nre, nim, ncnt);
     polar(na, nm);
-    slide_to(nre, nim, ncnt);
+    slide_to(nre, nim, ncnt, C.d[sf + 1 - fb]);
     commit(nre, nim, ncnt);
     polar(pa, pm);
   }
@@ -1887,8 +1921,7 @@ ps_vocoder_kernel(PitchArgs a) {
   const int dq = q7;
   // the istft rotation tw[qz] advances by e7 = tw[7k mod 250] per frame: rotated in registers
   // (tz and i tz), re-read from the table once per group (no drift, no scattered LDS read per frame)
-  const float4 e74 = sh.tw4[q7];
-  const cf e7 = {e74.x, e74.y}, e7r = {e74.z, e74.w};
+  const cf e7 = sh.tw[q7];
   const int jmax = (a.l1 + kPsPad - 1) / kPsHop;  // the frame of the last istft sample
   float* y = a.y + static_cast<int64_t>(e) * a.l1;
   HBK_PVT(0);  // init: tables, frame 0, the first rows
@@ -1919,20 +1952,19 @@ ps_vocoder_kernel(PitchArgs a) {
     }
     HBK_PVT(1);  // row refills, restarts
     R *= __builtin_amdgcn_rsqf(fmaf(R.x, R.x, R.y * R.y));
-    const float4 tz0 = sh.tw4[qz];
-    cf tz = {tz0.x, tz0.y}, tzr = {tz0.z, tz0.w};  // tw[qz] and i tw[qz]
+    cf tz = sh.tw[qz];  // tw[qz]; i tw[qz] = (-y, x) is read through the packed ops' neg / op_sel modifiers
+    const float* dg = C.d[0] + 8 * (sf + 1 - fb);  // FULL groups: frame u slides to row sf + 1 + u
     float gr[kPvGroup];  // frame u: G(t0 + u, pv_g(lane & 7)) over the lane's octet
     float al_lane = 0.f;  // full groups: the alpha of frame t0 + (lane & 7)
     // one output frame; FULL: t < f_out and i0(t) = c + 1 are known for the whole group
     auto frame = [&](int u, auto full) {
       constexpr bool FULL = decltype(full)::value;
       const int t = t0 + u;
-      const float4 tw = {tz.x, tz.y, tzr.x, tzr.y};  // e^{+2 pi i qz / 250} as (x, y, -y, x)
 #if HBK_PV_ABLATE & 2  // profiling build: the per-bin vocoder replaced by a stand-in
       if (t < a.f_out) {
         float al;
         ps_i0(a, t, al);
-        Q.x += al * tw.x;
+        Q.x += al * tz.x;
       }
       if (false) {
 #else
@@ -1955,7 +1987,7 @@ ps_vocoder_kernel(PitchArgs a) {
           R = cmul(R, cmul_conj(ca, na));  // P_t = P_{t-1} u_{c+1} conj u_c = R u_{c+1}, and c + 2 becomes the frame
           pv_t nre, nim;
           int ncnt;
-          slide_to(nre, nim, ncnt);
+          slide_to(nre, nim, ncnt, C.d[sf + 1 - fb]);
           commit(nre, nim, ncnt);
           polar(pa, pm);
         }
@@ -1970,14 +2002,16 @@ ps_vocoder_kernel(PitchArgs a) {
         nm = step ? pm : nm;
         pv_t nre, nim;
         int ncnt;
-        slide_to(nre, nim, ncnt);  // candidate frame sf + 1 and its polar form, kept only when stepping
+        // candidate frame sf + 1 and its polar form, kept only when stepping (FULL: frame u
+        // slides to the group's first row + u)
+        slide_to(nre, nim, ncnt, FULL ? dg + 8 * u : C.d[sf + 1 - fb]);
         cf qa;
         float qm;
         polar_of(nre, nim, qa, qm);
         const float m = fmaf(al, nm - cm, cm);
-        const cf P = cmul(R, ca);
+        const cf P = pv_cmul(R, ca);
         // Z_t = m P e^{-2 pi i qz / 250} = m (P.x (x, -y) + P.y (y, x))
-        const cf Z = __builtin_elementwise_fma(cf{P.y, P.y}, cf{tw.y, tw.x}, cf{P.x, P.x} * cf{tw.w, tw.z});
+        const cf Z = pv_cmul_conj(P, tz);
         Q = __builtin_elementwise_fma(cf{m, m}, Z, Q);
         xre = step ? nre : xre;
         xim = step ? nim : xim;
@@ -1988,7 +2022,7 @@ ps_vocoder_kernel(PitchArgs a) {
       }
       // G(t, .) over the wave's bins: 7 products, reduce-scatter over the lane octet,
       // all-reduce over the 8 octets
-      const cf vq = __builtin_elementwise_fma(cf{Q.y, Q.y}, cf{tw.z, tw.w}, cf{Q.x, Q.x} * cf{tw.x, tw.y});  // Q tw[qz]
+      const cf vq = pv_cmul(Q, tz);  // Q tw[qz]
 #if HBK_PV_ABLATE & 1  // profiling build: no bin reduction
       gr[u] = vq.x * esr[u & 3].x;
 #else
@@ -2006,10 +2040,7 @@ ps_vocoder_kernel(PitchArgs a) {
         for (int j = 0; j < kPvGroup; ++j) gr[j] = j == u ? gv : gr[j];
       }
 #endif
-      qz += dq;
-      qz -= qz >= kPsFft ? kPsFft : 0;
-      tz = __builtin_elementwise_fma(cf{tz.y, tz.y}, e7r, cf{tz.x, tz.x} * e7);
-      tzr = __builtin_elementwise_fma(cf{tzr.y, tzr.y}, e7r, cf{tzr.x, tzr.x} * e7);
+      tz = pv_cmul(tz, e7);
     };
     bool full = t0 + kPvGroup <= a.f_out;
     if (full) {  // per-frame advances are all >= 1 (rate > 1) or all <= 1 (rate < 1): a total of
@@ -2024,6 +2055,7 @@ ps_vocoder_kernel(PitchArgs a) {
 #pragma unroll 1
       for (int u = 0; u < kPvGroup; ++u) frame(u, std::false_type{});
     }
+    qz = (qz + kPvGroup * dq) % kPsFft;  // the next group's first frame
     // reduce-scatter over the octets: octet o keeps frame o (lane ^ 8, ^ 16, ^ 32)
     float h[4];
 #pragma unroll
