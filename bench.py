@@ -755,6 +755,7 @@ def setup_e2e(args, dev, rank, world, seed):
         neg_pos[0] = (o + S * NL) % n_large
 
     eval_events = []  # per staged step: (start, end) events of its evaluation passes
+    eval_stream = [None]  # HBK_EVAL_CUS: the evaluation passes' own stream (pipelined schedule only)
 
     def train_chunk(pool_b, evs=None):
         """The chunk's S stage steps on pool_b, with the evaluation passes after
@@ -775,7 +776,13 @@ def setup_e2e(args, dev, rank, world, seed):
             if evs is not None:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e0.record(stream_)
-            ev.run(sched, next_step=done)
+            if eval_stream[0] is not None:
+                eval_stream[0].wait_stream(stream_)
+                with torch.cuda.stream(eval_stream[0]):
+                    ev.run(sched, next_step=done)
+                stream_.wait_stream(eval_stream[0])
+            else:
+                ev.run(sched, next_step=done)
             if evs is not None:
                 e1 = torch.cuda.Event(enable_timing=True)
                 e1.record(stream_)
@@ -824,6 +831,18 @@ def setup_e2e(args, dev, rank, world, seed):
         # runs on the feature stream; two embedding pools
         from heybuddy.pipeline import make_streams
         fs, ts, keep = make_streams(dev, args.overlap)
+        # HBK_EVAL_CUS=N (A/B, off by default): the evaluation passes on their own stream masked to
+        # N CUs (N = all: unmasked), so their workgroups may also take featurize CUs' free slots
+        n_ecu = int(os.environ.get("HBK_EVAL_CUS", "0"))
+        if n_ecu and ev is not None:
+            from heybuddy.pipeline import masked_stream, train_cu_set
+            n_all = torch.cuda.get_device_properties(dev).multi_processor_count
+            if n_ecu >= n_all:
+                eval_stream[0] = torch.cuda.Stream(dev)
+            else:
+                es = masked_stream(dev, train_cu_set(n_all, n_ecu))
+                keep.append(es)
+                eval_stream[0] = es.stream
         pools = [pool, torch.empty_like(pool)]
         feat_done = [torch.cuda.Event(), torch.cuda.Event()]
         train_done = [torch.cuda.Event(), torch.cuda.Event()]
