@@ -669,7 +669,11 @@ def setup_e2e(args, dev, rank, world, seed):
     # r05: the embedding writes the pool itself and hbk_nan_rows_fix patches its NaN rows in place
     # (no gather copy of the pool, no torch reduction / sort; HBK_NAN_INPLACE=0: the gather form)
     nan_inplace = os.environ.get("HBK_NAN_INPLACE", "1") != "0"
-    nan_ws = [torch.empty(int(lib().hbk_nan_rows_workspace_size(n)), dtype=torch.uint8, device=dev) for _ in range(2)]
+    # pipelined schedule: embedding pools in flight (HBK_PIPE_BUFS, 2 or 3): featurize(c) waits for
+    # train(c - nbuf) to release pools[c % nbuf], so a third pool lets the feature stream run a step ahead
+    nbuf = max(2, int(os.environ.get("HBK_PIPE_BUFS", "2")))
+    nan_ws = [torch.empty(int(lib().hbk_nan_rows_workspace_size(n)), dtype=torch.uint8, device=dev)
+              for _ in range(nbuf)]
     nan_seed = [seed * 7919]
 
     def emb_target(pool_t):
@@ -843,9 +847,9 @@ def setup_e2e(args, dev, rank, world, seed):
                 es = masked_stream(dev, train_cu_set(n_all, n_ecu))
                 keep.append(es)
                 eval_stream[0] = es.stream
-        pools = [pool, torch.empty_like(pool)]
-        feat_done = [torch.cuda.Event(), torch.cuda.Event()]
-        train_done = [torch.cuda.Event(), torch.cuda.Event()]
+        pools = [pool] + [torch.empty_like(pool) for _ in range(nbuf - 1)]
+        feat_done = [torch.cuda.Event() for _ in range(nbuf)]
+        train_done = [torch.cuda.Event() for _ in range(nbuf)]
         count = [0]
         staged_step = step
 
@@ -883,15 +887,15 @@ def setup_e2e(args, dev, rank, world, seed):
         a1 = int(round(n * args.embed_split_frac)) if K > 1 else 0
         a1 = min(max(a1, 0), n)
         mids = [torch.empty((n - a1, eplan.mid_floats(K)), dtype=torch.float32, device=dev)
-                for _ in range(2)] if K and not whole else []
+                for _ in range(nbuf)] if K and not whole else []
         mids1 = [torch.empty((a1, eplan.mid_floats(K - 1)), dtype=torch.float32, device=dev)
-                 for _ in range(2)] if a1 else []
-        front_done = [torch.cuda.Event(), torch.cuda.Event()]
+                 for _ in range(nbuf)] if a1 else []
+        front_done = [torch.cuda.Event() for _ in range(nbuf)]
 
         def featurize(c):
-            b = c % 2
+            b = c % nbuf
             with torch.cuda.stream(fs):
-                fs.wait_event(train_done[b])  # train(c - 2) has finished reading pools[b] (and back(c - 2) mids[b])
+                fs.wait_event(train_done[b])  # train(c - nbuf) has finished reading pools[b] (and back(c - nbuf) mids[b])
                 e0 = mark("featurize", fs)
                 x = aug.augment_device(src, lens)
                 frames = mel_frames(x, mplan, N_FRAMES)
@@ -912,7 +916,7 @@ def setup_e2e(args, dev, rank, world, seed):
 
         def featurize_back(c):
             """Chunk c's embedding back half + NaN replacement on the train stream."""
-            b = c % 2
+            b = c % nbuf
             with torch.cuda.stream(ts):
                 ts.wait_event(front_done[b])
                 if a1:
@@ -935,7 +939,7 @@ def setup_e2e(args, dev, rank, world, seed):
             h0 = time.perf_counter()
             featurize(c + 1)
             h1 = time.perf_counter()
-            b = c % 2
+            b = c % nbuf
             with torch.cuda.stream(ts):
                 ts.wait_event(feat_done[b])
                 e0 = mark("train", ts)

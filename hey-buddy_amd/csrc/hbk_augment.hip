@@ -2083,7 +2083,9 @@ ps_vocoder_kernel(PitchArgs a) {
           g2 = C.gh[0][(t - 35) % kPvGh][r - 5] + C.gh[1][(t - 35) % kPvGh][r - 5];
         }
         const int lo = max(0, t - 35 + (r >= 5 ? 1 : 0)), hi = min(a.f_out - 1, t);
-        y[m] = (g1 - g2) / (static_cast<float>(kPsFft) * static_cast<float>(hi - lo + 1));
+        // / (250 env) as a product with v_rcp_f32 (1 ulp; the IEEE division's scale / fixup
+        // sequence is ~10 VALU per sample)
+        y[m] = (g1 - g2) * __builtin_amdgcn_rcpf(static_cast<float>(kPsFft) * static_cast<float>(hi - lo + 1));
       }
     }
     HBK_PVT(4);  // istft samples
