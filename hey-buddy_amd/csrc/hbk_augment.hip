@@ -1766,6 +1766,9 @@ __device__ __forceinline__ void pv_load_rows(const PitchArgs& a, PvShared& sh, c
   } while (0)
 #endif
 
+#ifndef HBK_PV_UNROLL_TAIL
+#define HBK_PV_UNROLL_TAIL 1  // 0: the non-FULL groups' frames in a loop (A/B)
+#endif
 #ifndef HBK_PV_WAVES
 #define HBK_PV_WAVES 4  // waves per SIMD the vocoder is register-limited to
 #endif
@@ -1889,10 +1892,11 @@ ps_vocoder_kernel(PitchArgs a) {
   auto polar_of = [&](pv_t re, pv_t im, cf& u, float& mag) {
     const float fr = static_cast<float>(re), fi = static_cast<float>(im);
     const float n2 = fmaf(fr, fr, fi * fi);
-    const float rs = __builtin_amdgcn_rsqf(n2);  // v_rsq_f32 (1 ulp)
-    const bool nz = n2 > 0.f;
-    u = nz ? cf{fr, fi} * rs : cf{1.f, 0.f};
-    mag = nz ? n2 * rs : 0.f;
+    // no selects: for X = 0, rs = rsq(2^-126) = 2^63 and (0 + 2^-63, 0) rs = (1, 0), n2 rs = 0; elsewhere
+    // (|X| > 2^-38) both offsets are below half an ulp, so rs and u are those of X itself
+    const float rs = __builtin_amdgcn_rsqf(n2 + 0x1p-126f);  // v_rsq_f32 (1 ulp)
+    u = cf{fr + 0x1p-63f, fi} * rs;
+    mag = n2 * rs;
   };
   auto polar = [&](cf& u, float& mag) { polar_of(xre, xim, u, mag); };
   // frames c, c + 1 in (ca, cm), (na, nm); frame c + 2 = sf ahead in (pa, pm)
@@ -1955,7 +1959,8 @@ ps_vocoder_kernel(PitchArgs a) {
     cf tz = sh.tw[qz];  // tw[qz]; i tw[qz] = (-y, x) is read through the packed ops' neg / op_sel modifiers
     const float* dg = C.d[0] + 8 * (sf + 1 - fb);  // FULL groups: frame u slides to row sf + 1 + u
     float gr[kPvGroup];  // frame u: G(t0 + u, pv_g(lane & 7)) over the lane's octet
-    float al_lane = 0.f;  // full groups: the alpha of frame t0 + (lane & 7)
+    float al_lane = 0.f;  // the source frame i0 and alpha of frame t0 + (lane & 7), read by frame u as lane u
+    int i0_lane = 0;
     // one output frame; FULL: t < f_out and i0(t) = c + 1 are known for the whole group
     auto frame = [&](int u, auto full) {
       constexpr bool FULL = decltype(full)::value;
@@ -1976,7 +1981,8 @@ ps_vocoder_kernel(PitchArgs a) {
           i0 = c + 1;
           al = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, al_lane), u));
         } else {
-          i0 = ps_i0(a, t, al);
+          i0 = __builtin_amdgcn_readlane(i0_lane, u);
+          al = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, al_lane), u));
         }
         if (!FULL && i0 > c + 1) {  // rate > 1: a second source frame this step (rare)
           ++c;
@@ -2047,12 +2053,16 @@ ps_vocoder_kernel(PitchArgs a) {
       float al;  // kPvGroup means every frame of the group steps exactly once
       full = ps_i0(a, t0 + kPvGroup - 1, al) - c == kPvGroup;
     }
+    i0_lane = ps_i0(a, t0 + (lane & 7), al_lane);
     if (full) {
-      ps_i0(a, t0 + (lane & 7), al_lane);
 #pragma unroll
       for (int u = 0; u < kPvGroup; ++u) frame(u, std::true_type{});
-    } else {  // tail or double-step group: not unrolled
+    } else {  // tail, repeat or double-step group (about a fifth of the groups at 125/128, 128/125)
+#if HBK_PV_UNROLL_TAIL  // unrolled too: the frame's result lands in gr[u] without a select chain
+#pragma unroll
+#else
 #pragma unroll 1
+#endif
       for (int u = 0; u < kPvGroup; ++u) frame(u, std::false_type{});
     }
     qz = (qz + kPvGroup * dq) % kPsFft;  // the next group's first frame
