@@ -835,9 +835,13 @@ def setup_e2e(args, dev, rank, world, seed):
         # runs on the feature stream; two embedding pools
         from heybuddy.pipeline import make_streams
         fs, ts, keep = make_streams(dev, args.overlap)
-        # HBK_EVAL_CUS=N (A/B, off by default): the evaluation passes on their own stream masked to
-        # N CUs (N = all: unmasked), so their workgroups may also take featurize CUs' free slots
-        n_ecu = int(os.environ.get("HBK_EVAL_CUS", "0"))
+        # the evaluation passes on their own stream, unmasked by default (HBK_EVAL_CUS=N: masked to N
+        # CUs; 0: on the train stream), so their workgroups also take the featurize CUs' free slots:
+        # 895.2 / 896.4 / 900.4 k against 889.7 / 890.8 / 888.8 k clips/s on the train stream
+        # (same box, alternating; profiles/r05l_ab_eval_cus2.log)
+        n_ecu = int(os.environ.get("HBK_EVAL_CUS", "-1"))
+        if n_ecu < 0:
+            n_ecu = torch.cuda.get_device_properties(dev).multi_processor_count
         if n_ecu and ev is not None:
             from heybuddy.pipeline import masked_stream, train_cu_set
             n_all = torch.cuda.get_device_properties(dev).multi_processor_count
@@ -1190,6 +1194,10 @@ def setup_e2e(args, dev, rank, world, seed):
                                 + (f", then the embedding's chains >= {args.embed_split - 1} of {args.embed_split_frac:.0%}"
                                    " of chunk s + 1's clips on the train stream (hbk_embed_clips_back)"
                                    if args.embed_split == eplan.n_chains and args.embed_split_frac > 0 else "")
+                                + (", the evaluation passes on a stream of their own over "
+                                   + ("all CUs" if eval_stream[0] is not None and not isinstance(
+                                       eval_stream[0], torch.cuda.ExternalStream) else "a CU-masked set")
+                                   if eval_stream[0] is not None else "")
                                 + f"; per-stage ms from {args.stage_steps} sequential steps")},
     }
 
