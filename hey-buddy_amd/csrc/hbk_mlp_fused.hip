@@ -1413,8 +1413,19 @@ struct K4Args {
   const float* part;
   int64_t pstride;
   int ns;
-  Ranges rg;
+  // 32-bit forms of the per-element tests (n < 2^31; fewer scalar registers than the int64
+  // WSplit / Ranges: those spilled 135 SGPRs): the cached matrices in float4 units [lo, hi),
+  // the tile workgroups' share; the slab-covered ranges in floats
+  int n_skip, n_cov;
+  int32_t skip_lo[kMaxSeg], skip_hi[kMaxSeg];
+  int32_t cov_lo[kMaxRng], cov_hi[kMaxRng];
 };
+__device__ __forceinline__ bool k4_covered(const K4Args& a, int32_t i) {
+  bool c = false;
+#pragma unroll
+  for (int k = 0; k < kMaxRng; ++k) c |= k < a.n_cov && i >= a.cov_lo[k] && i < a.cov_hi[k];
+  return c;
+}
 
 // The accumulation gate (trainer.py:443-465), computed identically by every
 // workgroup from the step's read-only state half; workgroup 0 writes the other
@@ -1501,7 +1512,7 @@ __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
   // the gate decision, which itself waits on the statistics); the parameters
   // after the step are returned
   auto adam4 = [&](int64_t i) -> f4 {
-    const f4 g = grad4(i, ns > 0 && in_ranges(a.rg, 4 * i), true), m0 = M4[i], v0 = V4[i];
+    const f4 g = grad4(i, ns > 0 && k4_covered(a, static_cast<int32_t>(4 * i)), true), m0 = M4[i], v0 = V4[i];
     f4 p = P4[i];
     if (on) {
       const f4 gi = g * scale;
@@ -1584,17 +1595,16 @@ __global__ void __launch_bounds__(256) k4_update_kernel(K4Args a) {
   for (int64_t i = b0 * 256 + threadIdx.x; i < n4; i += nb * 256) {
     if (t0) {  // cached matrices are the tile workgroups'
       bool cached = false;
+      const int32_t i32 = static_cast<int32_t>(i);
 #pragma unroll
-      for (int sg = 0; sg < kMaxSeg; ++sg)
-        cached |= sg < a.w.n && 4 * i >= a.w.s[sg].src &&
-                  4 * i < a.w.s[sg].src + int64_t(a.w.s[sg].rows) * a.w.s[sg].cols;
+      for (int sg = 0; sg < kMaxSeg; ++sg) cached |= sg < a.n_skip && i32 >= a.skip_lo[sg] && i32 < a.skip_hi[sg];
       if (cached) continue;
     }
     adam4(i);
   }
   for (int64_t i = 4 * n4 + b0 * 256 + threadIdx.x; i < a.n; i += nb * 256) {
     float g = a.G[i];
-    if (ns > 0 && in_ranges(a.rg, i))
+    if (ns > 0 && k4_covered(a, static_cast<int32_t>(i)))
       for (int sp = 0; sp < ns; ++sp) g += a.part[sp * a.pstride + i];
     a.G[i] = 0.f;
     if (on) {
@@ -2494,7 +2504,22 @@ int mlp_fused_update(const hbk_mlp_plan& p, float* params, float* bucket, float*
   k.part = p.deferred_ws ? ws + fl.part : nullptr;
   k.pstride = fl.pstride;
   k.ns = p.deferred_ws ? p.deferred_ks : 0;
-  k.rg = make_ranges(p);
+  if (p.n_params >= (int64_t(1) << 31) - 4) {
+    set_error("hbk: hbk_mlp_step_update: parameter count >= 2^31");
+    return HBK_ERR_ARG;
+  }
+  const Ranges rg = make_ranges(p);
+  k.n_cov = rg.n;
+  for (int i = 0; i < kMaxRng; ++i) {
+    k.cov_lo[i] = i < rg.n ? static_cast<int32_t>(rg.lo[i]) : 0;
+    k.cov_hi[i] = i < rg.n ? static_cast<int32_t>(rg.hi[i]) : 0;
+  }
+  k.n_skip = k.w.n;
+  for (int sg = 0; sg < kMaxSeg; ++sg) {  // 4 i in [src, src + rows cols) <=> i in [ceil(src / 4), ceil(end / 4))
+    const int64_t lo = sg < k.w.n ? k.w.s[sg].src : 0, hi = sg < k.w.n ? lo + int64_t(k.w.s[sg].rows) * k.w.s[sg].cols : 0;
+    k.skip_lo[sg] = static_cast<int32_t>((lo + 3) / 4);
+    k.skip_hi[sg] = static_cast<int32_t>((hi + 3) / 4);
+  }
   p.deferred_ws = nullptr;
   k.n_tiles = 0;
   for (int sg = 0; sg < k.w.n; ++sg)
