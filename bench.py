@@ -839,7 +839,9 @@ def setup_e2e(args, dev, rank, world, seed):
         # CUs; 0: on the train stream), so their workgroups also take the featurize CUs' free slots:
         # 895.2 / 896.4 / 900.4 k against 889.7 / 890.8 / 888.8 k clips/s on the train stream
         # (same box, alternating; profiles/r05l_ab_eval_cus2.log)
-        n_ecu = int(os.environ.get("HBK_EVAL_CUS", "-1"))
+        # (one process per GPU only: two ranks sharing cuda:0 in tools/rehearse_dp.sh stalled with the
+        # extra stream, so N > 1 keeps the passes on the train stream unless HBK_EVAL_CUS says otherwise)
+        n_ecu = int(os.environ.get("HBK_EVAL_CUS", "-1" if world == 1 else "0"))
         if n_ecu < 0:
             n_ecu = torch.cuda.get_device_properties(dev).multi_processor_count
         if n_ecu and ev is not None:
