@@ -36,14 +36,16 @@ constexpr int kMaxWin = 32;
 constexpr int kLdsBudget = 78 * 1024;     // bytes per block: 2 blocks per CU
 constexpr int kLdsBudgetCU = 156 * 1024;  // one block per CU
 constexpr int kChunkClips = 16384;     // clips per workspace chunk (default; HBK_EMBED_CHUNK overrides)
-// clips per workspace chunk: every chain kernel runs once per chunk (its last round of waves
+// clips per workspace chunk (HBK_EMBED_CHUNK: 256 .. 32,768): every chain kernel runs once per chunk (its last round of waves
 // partly filled); measured: 100 k clips in 16,384-clip chunks 24.30 ms, in 32,768-clip chunks
 // 24.43 ms, bit-identical (tools/embed_chunk_check.py), so the smaller workspace stays
 inline int64_t chunk_clips() {
   static const int64_t c = [] {
     const char* e = getenv("HBK_EMBED_CHUNK");
     const long long v = e ? atoll(e) : 0;
-    return v >= 256 && v <= (int64_t(1) << 20) ? int64_t(v) : int64_t(kChunkClips);
+    // (capped at 32,768, the size tools/embed_chunk_check.py validated: the chain kernels'
+    // task counts are 32-bit and assume at most that many clips x windows x bands)
+    return v >= 256 && v <= 32768 ? int64_t(v) : int64_t(kChunkClips);
   }();
   return c;
 }

@@ -1159,8 +1159,10 @@ int hbk_mel_plan_create(const float* window, const float* fbank, int n_fft, int 
     if ((e = hipMemcpy(p->d_t4, t4.data(), t4.size() * sizeof(float4), hipMemcpyHostToDevice)) != hipSuccess)
       return fail(e, "copy t4");
     // opt-in until measured on the GPU: HBK_MEL_V4=1 (4-wave blocks, prefetch) or 8 (8-wave blocks)
+    // (0 or unset: off, as the other HBK_* knobs read their values)
     const char* v4 = getenv("HBK_MEL_V4");
-    p->v4 = v4 ? (atoi(v4) == 8 ? 8 : 4) : 0;
+    const int v4n = v4 ? atoi(v4) : 0;
+    p->v4 = v4n == 0 ? 0 : (v4n == 8 ? 8 : 4);
   }
   *plan = p;
   return HBK_OK;

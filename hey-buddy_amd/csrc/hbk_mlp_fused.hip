@@ -47,6 +47,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <initializer_list>
+#include <utility>
 #include <cmath>
 
 #include "hbk_common.h"
@@ -168,6 +170,36 @@ __device__ int g_mlp_trace_n[kTraceKerns][kTraceWaves];
   } while (0)
 #endif
 
+#ifdef HBK_BOUNDS
+// Bounds-checked build (lib/libhbk_bounds.so, tools/probe_bounds.py): the step
+// kernels' global accesses go through BCK, which checks them against the ranges
+// the host registered for the call (workspace, parameters, pools, ...); the first
+// violation is recorded (source line, block, thread, address) and the access is
+// redirected to a scratch buffer, so a bad index shows up as a record instead of
+// a GPU memory fault.
+constexpr int kBMax = 16;
+__device__ unsigned long long g_brange[kBMax][2];
+__device__ int g_bn;
+__device__ unsigned long long g_berr[4];
+__device__ __attribute__((aligned(16))) char g_bsafe[1 << 16];
+template <typename T>
+__device__ __forceinline__ T* bck_(T* p, int nbytes, int line) {
+  const unsigned long long c = reinterpret_cast<unsigned long long>(p);
+  bool ok = false;
+  for (int i = 0; i < kBMax; ++i) ok |= i < g_bn && c >= g_brange[i][0] && c + nbytes <= g_brange[i][1];
+  if (ok) return p;
+  if (atomicCAS(&g_berr[0], 0ull, static_cast<unsigned long long>(line)) == 0ull) {
+    g_berr[1] = blockIdx.x;
+    g_berr[2] = threadIdx.x;
+    g_berr[3] = c;
+  }
+  return reinterpret_cast<T*>(g_bsafe);
+}
+#define BCK(p, n) bck_((p), (n), __LINE__)
+#else
+#define BCK(p, n) (p)
+#endif
+
 __device__ __forceinline__ int step_of(const float* state, int parity) {
   return state ? static_cast<int>(state[parity * 8 + 3]) : 0;
 }
@@ -185,8 +217,16 @@ struct K1aArgs {
   int B;
   float drop_p;
   uint64_t seed;
-  float* xhat[2];      // TRANSPOSED [1536][Bp] (rows >= B zero), by step parity
+  float* xhat[2];      // TRANSPOSED [1536][Bp] (rows >= B zero), by step parity (v1 step)
   int64_t Bp;
+  // v2 step (the default): per row of the step, by parity, its LayerNorm statistics
+  // and the row's address {mu, rs, addr lo, addr hi} (mu / rs as float bits; addr =
+  // the row's first byte in its pool with bit 0 set for an f16 row: consumers address
+  // rows without branches; a zero row points at a valid row of its pool) and its
+  // dropout mask (bit c of word c / 32 set = element c dropped; a zero row has every
+  // bit set, and mu = 0); no xhat^T
+  uint4* rinfo[2];     // [Bp]
+  uint32_t* mask[2];   // [Bp][48]
 };
 
 struct K1bArgs {
@@ -223,10 +263,14 @@ __device__ __forceinline__ uint32_t drop_hash(uint32_t s0, uint32_t s1, uint32_t
 // [512 t, 512 t + 512), so xhat^T is written in three 512-column slabs staged
 // through LDS (slab: [16][516] floats) as 64-B column runs.
 constexpr int kSlabLd = 516;
-constexpr int kPreTiles = 2;  // k1a row tiles per prefetch workgroup of k2
-template <bool kIdx>
+constexpr int kPreTiles = 2;    // k1a row tiles per prefetch workgroup of k2 (v1)
+constexpr int kPreTiles2 = 4;   // k1s (v2: statistics and mask only) row tiles per prefetch workgroup
+constexpr int kMaskW = kD / 32;  // mask words per row
+// kV2: the row statistics and dropout mask (rinfo, mask) instead of xhat^T; slab is then
+// >= 4 waves x 4 rows x 1536 bytes of LDS scratch (the mask's byte image)
+template <bool kIdx, bool kV2 = false>
 __device__ __forceinline__ void k1a_tile(const K1aArgs& a, int rt, int step, float* __restrict__ xout,
-                                         float* slab) {
+                                         float* slab, int dpar = 0) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t seed = a.seed + static_cast<uint64_t>(step) +
                         (a.state ? static_cast<uint64_t>(a.state[a.parity * 8 + 4]) << 24 : 0);
@@ -236,10 +280,11 @@ __device__ __forceinline__ void k1a_tile(const K1aArgs& a, int rt, int step, flo
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     ixs[i] = min(rt * kR + wave * 4 + i, a.B - 1);
-    if (kIdx) ixs[i] = a.idx[static_cast<int64_t>(step) * a.idx_stride + ixs[i]];
+    if (kIdx) ixs[i] = *BCK(&a.idx[static_cast<int64_t>(step) * a.idx_stride + ixs[i]], 4);
   }
   uint4 raw[4][6];
   bool is16[4], ok[4];
+  const char* rowptr[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int r = rt * kR + wave * 4 + i;
@@ -250,20 +295,23 @@ __device__ __forceinline__ void k1a_tile(const K1aArgs& a, int rt, int step, flo
     const char* bp = !ok[i] ? fallback
                      : is16[i] ? reinterpret_cast<const char*>(a.pool16 + row16 * kD)
                                : reinterpret_cast<const char*>(a.pool32 + static_cast<int64_t>(ix) * kD);
+    rowptr[i] = bp;
 #pragma unroll
     for (int u = 0; u < 6; ++u) {
       const int slot = is16[i] ? u % 3 : u;
-      raw[i][u] = *reinterpret_cast<const uint4*>(bp + 16 * (lane + 64 * slot));
+      raw[i][u] = *BCK(reinterpret_cast<const uint4*>(bp + 16 * (lane + 64 * slot)), 16);
     }
   }
   const float keep = a.drop_p > 0.f ? 1.f / (1.f - a.drop_p) : 1.f;
   const uint32_t thr = static_cast<uint32_t>(a.drop_p * 65536.f + 0.5f);
-  float xh[4][24];
+  float xh[4][kV2 ? 1 : 24];
+  unsigned char* mimg = reinterpret_cast<unsigned char*>(slab) + (wave * 4) * kD;  // v2: [4 rows][1536] flag bytes
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int r = rt * kR + wave * 4 + i;
     float v[24];
     int c[24];
+    bool dr[24];  // element dropped (v2's mask; a zero row drops everything)
 #pragma unroll
     for (int j = 0; j < 24; ++j) {
       const uint4 w16 = raw[i][j >> 3];
@@ -273,14 +321,18 @@ __device__ __forceinline__ void k1a_tile(const K1aArgs& a, int rt, int step, flo
       const float f = __builtin_bit_cast(float, (&w32.x)[j & 3]);
       v[j] = ok[i] ? (is16[i] ? static_cast<float>(h) : f) : 0.f;
       c[j] = is16[i] ? 8 * (lane + 64 * (j >> 3)) + (j & 7) : 4 * (lane + 64 * (j >> 2)) + (j & 3);
+      dr[j] = !ok[i];
     }
     if (a.drop_p > 0.f) {  // nn.Dropout on the input (wakeword.py:197, :338): one hash per element pair
       const uint32_t base = static_cast<uint32_t>(r) * (kD / 2);
 #pragma unroll
       for (int j = 0; j < 24; j += 2) {
         const uint32_t hsh = drop_hash(s0, s1, base + (c[j] >> 1));
-        v[j] = (hsh & 0xFFFFu) < thr ? 0.f : v[j] * keep;
-        v[j + 1] = (hsh >> 16) < thr ? 0.f : v[j + 1] * keep;
+        const bool d0 = (hsh & 0xFFFFu) < thr, d1 = (hsh >> 16) < thr;
+        v[j] = d0 ? 0.f : v[j] * keep;
+        v[j + 1] = d1 ? 0.f : v[j + 1] * keep;
+        dr[j] = dr[j] || d0;
+        dr[j + 1] = dr[j + 1] || d1;
       }
     }
     float sm = 0.f;
@@ -292,8 +344,47 @@ __device__ __forceinline__ void k1a_tile(const K1aArgs& a, int rt, int step, flo
     for (int j = 0; j < 24; ++j) sq += (v[j] - mu) * (v[j] - mu);
     const float rs = __builtin_amdgcn_rsqf(wsum(sq) * (1.f / kD) + kLnEps);
     const bool live = r < a.B;
+    if constexpr (kV2) {
+      // the flag bytes of this row: lane's elements are 4 (f32) / 8 (f16) consecutive per slot
+      unsigned char* row = mimg + i * kD;
 #pragma unroll
-    for (int j = 0; j < 24; ++j) xh[i][j] = live ? (v[j] - mu) * rs : 0.f;
+      for (int q = 0; q < 6; ++q) {
+        const uint32_t b4 = (dr[4 * q] ? 1u : 0u) | (dr[4 * q + 1] ? 0x100u : 0u) | (dr[4 * q + 2] ? 0x10000u : 0u) |
+                            (dr[4 * q + 3] ? 0x1000000u : 0u);
+        const int off = is16[i] ? 8 * lane + 512 * (q >> 1) + 4 * (q & 1) : 4 * lane + 256 * q;
+        *reinterpret_cast<uint32_t*>(row + off) = b4;
+      }
+      if (lane == 0) {
+        // a zero row's loads read its fallback row as that pool's dtype (in bounds either way)
+        const bool h = ok[i] ? is16[i] : a.pool32 == nullptr;
+        const uint64_t addr = reinterpret_cast<uint64_t>(rowptr[i]) | (h ? 1u : 0u);
+        *BCK(&a.rinfo[dpar][r], 16) =
+            uint4{__float_as_uint(live ? mu : 0.f), __float_as_uint(live ? rs : 0.f), static_cast<uint32_t>(addr),
+                  static_cast<uint32_t>(addr >> 32)};
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 24; ++j) xh[i][j] = live ? (v[j] - mu) * rs : 0.f;
+    }
+  }
+  if constexpr (kV2) {
+    // 32 flag bytes -> one mask word per lane (lanes 0..47), four rows
+    __syncthreads();
+    uint32_t* mdst = a.mask[dpar];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = rt * kR + wave * 4 + i;
+      if (lane < kMaskW) {
+        const uint4* src = reinterpret_cast<const uint4*>(mimg + i * kD + 32 * lane);
+        const uint4 b0 = src[0], b1 = src[1];
+        const uint32_t d[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+        uint32_t wd = 0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) wd |= ((d[e] * 0x01020408u) >> 24 & 0xFu) << (4 * e);  // 4 flag bytes -> 4 bits
+        *BCK(&mdst[static_cast<int64_t>(r) * kMaskW + lane], 4) = wd;
+      }
+    }
+    return;
   }
 #pragma unroll
   for (int t = 0; t < 3; ++t) {
@@ -331,6 +422,16 @@ __global__ void __launch_bounds__(256) k1a_kernel(K1aArgs a, int next) {
   HBK_MT(0, 1);
   k1a_tile<kIdx>(a, blockIdx.x, step, a.xhat[a.parity ^ next], slab);
   HBK_MT(0, 2);
+}
+// Standalone k1s (v2): the step's (next = 0) or its successor's (next = 1) row
+// statistics and dropout mask.
+static_assert(kR * kSlabLd * 4 >= 16 * kD, "k1s: the mask image fits the slab");
+template <bool kIdx>
+__global__ void __launch_bounds__(256) k1s_kernel(K1aArgs a, int next) {
+  __shared__ __attribute__((aligned(16))) float slab[kR * kSlabLd];
+  const int step = step_of(a.state, a.parity) + next;
+  if (kIdx && next && step >= a.idx_steps) return;
+  k1a_tile<kIdx, true>(a, blockIdx.x, step, nullptr, slab, a.parity ^ next);
 }
 
 // Split-f16 products on v_mfma_f32_16x16x32_f16: v = hi + lo with hi = f16(v)
@@ -469,6 +570,150 @@ __global__ void __launch_bounds__(256) k1b_kernel(K1bArgs a) {
       if (r < a.B) {
         out[static_cast<int64_t>(r) * kH2 + 32 * wave + m] = acc[t][0][e] * (1.f / 16.f);
         out[static_cast<int64_t>(r) * kH2 + 32 * wave + 16 + m] = acc[t][1][e] * (1.f / 16.f);
+      }
+    }
+  HBK_MT(3, 3);
+}
+
+// ------------------------------------------------------------ k1c (v2) ----
+// The input GEMM from the embedding pools themselves: no xhat^T round trip
+// through HBM (k1a wrote 6.8 MB per step at B = 1,100 and k1b and k3 read it
+// back). Workgroup = 16 RT rows x one KC-deep K chunk, 8 waves; grid = row blocks
+// x KS chunks, blockIdx = row block * KS + chunk, so the blocks of one chunk
+// share an XCD (when KS % 8 == 0) and its W slice is read from that XCD's L2.
+// Each thread stages 8-element runs of the block's rows: the raw pool values
+// (f16 or f32 row, by k1s's source), the dropout mask bits, xhat = (v - mu) rs
+// with k1s's statistics (the formula k1a used), then a = xhat g + b split into
+// f16 hi / lo planes in LDS ONCE (k1b split per wave and fragment); wave w then
+// multiplies every row tile by W's column tile w (16 W, pre-split in registers).
+struct K1cArgs {
+  const float* P;
+  int64_t g_in, b_in, w0;
+  int B, RT, KS;
+  const float* pool32;
+  const _Float16* pool16;
+  const uint4* rinfo;     // this step's rows (k1s)
+  const uint32_t* mask;   // [Bp][48]
+  float keep;             // 1 / (1 - p), or 1
+  float* hg_part;         // [KS][B][128]
+  float* stats;           // bucket tail, zeroed here (k2 accumulates into it); may be NULL
+};
+template <int KC>
+constexpr int k1c_rt_max() {
+  return 16 * (KC + 16) * 4 * 9 <= 150 * 1024 ? 9 : (150 * 1024) / (16 * (KC + 16) * 4);
+}
+// a row's first byte and dtype from k1s's row information (bit 0 of the address: f16)
+__device__ __forceinline__ const char* row_addr(const uint4& inf, bool& is16) {
+  const uint64_t ad = static_cast<uint64_t>(inf.z) | (static_cast<uint64_t>(inf.w) << 32);
+  is16 = (ad & 1u) != 0;
+  return reinterpret_cast<const char*>(ad & ~uint64_t(15));
+}
+template <int KC>
+__global__ void __launch_bounds__(512) k1c_kernel(K1cArgs a) {
+  constexpr int kNI = KC / 32, kLdA = KC + 16, kU8 = KC / 8;  // (KC + 16 halves: conflict-free b128 reads)
+  constexpr int kRTM = k1c_rt_max<KC>();
+  constexpr int kUPT = (kRTM * 16 * kU8 + 511) / 512;  // staging units per thread
+  static_assert(KC % 32 == 0 && kD % KC == 0 && KC <= 512, "K chunk");
+  __shared__ __attribute__((aligned(16))) _Float16 ahS[kRTM * 16 * kLdA];
+  __shared__ __attribute__((aligned(16))) _Float16 alS[kRTM * 16 * kLdA];
+  __shared__ __attribute__((aligned(16))) float gb[2][KC];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = lane & 15, kq = lane >> 4;
+  const int ks = blockIdx.x % a.KS, rb = blockIdx.x / a.KS;
+  const int RT = a.RT, rows = 16 * RT, r0 = rb * rows;
+  if (r0 >= a.B) return;
+  HBK_MT(3, 1);
+  const int k0 = ks * KC;
+  if (a.stats && rb == 0 && ks == 0 && tid < kStats) *BCK(&a.stats[tid], 4) = 0.f;
+  // every load issued up front: W's column tile, gamma / beta, the rows' statistics and mask words
+  f4 wr[kNI][2];
+  {
+    const float* wp = a.P + a.w0 + static_cast<int64_t>(16 * wave + m) * kD + k0 + 8 * kq;
+#pragma unroll
+    for (int i = 0; i < kNI; ++i) {
+      wr[i][0] = *BCK(reinterpret_cast<const f4*>(wp + 32 * i), 16);
+      wr[i][1] = *BCK(reinterpret_cast<const f4*>(wp + 32 * i + 4), 16);
+    }
+  }
+  const int cg = min(tid, KC - 1);
+  const float gv = *BCK(&a.P[a.g_in + k0 + cg], 4), bv = *BCK(&a.P[a.b_in + k0 + cg], 4);
+  // (the rows' information as uint4: clang miscompiles a bit_cast of an ext_vector element,
+  // __builtin_bit_cast(int, v[2]) / (int, v.z) read element 0 -- ROCm 7.2, gfx950)
+  uint4 info[kUPT];
+  uint32_t mw[kUPT];
+#pragma unroll
+  for (int j = 0; j < kUPT; ++j) {
+    const int q = tid + 512 * j, rr = min(q / kU8, rows - 1), c8 = q % kU8;
+    const int64_t r = min(r0 + rr, a.B - 1);
+    info[j] = *BCK(&a.rinfo[r], 16);
+    mw[j] = *BCK(&a.mask[r * kMaskW + (k0 + 8 * c8) / 32], 4);
+  }
+  uint4 lo[kUPT], hi[kUPT];
+#pragma unroll
+  for (int j = 0; j < kUPT; ++j) {
+    const int q = tid + 512 * j, c8 = q % kU8;
+    bool is16;
+    const char* base = row_addr(info[j], is16);
+    const char* p = base + (static_cast<int64_t>(k0 + 8 * c8) << (is16 ? 1 : 2));
+    lo[j] = *BCK(reinterpret_cast<const uint4*>(p), 16);
+    hi[j] = *BCK(reinterpret_cast<const uint4*>(p + (is16 ? 0 : 16)), 16);
+  }
+  if (tid < KC) {
+    gb[0][tid] = gv;
+    gb[1][tid] = bv;
+  }
+  __syncthreads();
+  // stage: a = ((v - mu) rs) g + b, split once into the hi / lo planes
+#pragma unroll
+  for (int j = 0; j < kUPT; ++j) {
+    const int q = tid + 512 * j;
+    if (q >= rows * kU8) break;
+    const int rr = q / kU8, c8 = q % kU8;
+    const bool is16 = (info[j].z & 1u) != 0;
+    const uint32_t bits = mw[j] >> (8 * (((k0 >> 3) + c8) & 3));
+    const float mu = __uint_as_float(info[j].x), rs = __uint_as_float(info[j].y);
+    const uint32_t hw[4] = {lo[j].x, lo[j].y, lo[j].z, lo[j].w};
+    const uint32_t fw[8] = {lo[j].x, lo[j].y, lo[j].z, lo[j].w, hi[j].x, hi[j].y, hi[j].z, hi[j].w};
+    float av[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float x = is16 ? static_cast<float>(__builtin_bit_cast(
+                                 _Float16, static_cast<uint16_t>((e & 1) ? hw[e >> 1] >> 16 : hw[e >> 1])))
+                           : __builtin_bit_cast(float, fw[e]);
+      const float v = (bits >> e) & 1u ? 0.f : x * a.keep;
+      const float xh = (v - mu) * rs;
+      av[e] = xh * gb[0][8 * c8 + e] + gb[1][8 * c8 + e];
+    }
+    h8 ahv, alv;
+    split8(f4{av[0], av[1], av[2], av[3]}, f4{av[4], av[5], av[6], av[7]}, ahv, alv);
+    *reinterpret_cast<h8*>(&ahS[rr * kLdA + 8 * c8]) = ahv;
+    *reinterpret_cast<h8*>(&alS[rr * kLdA + 8 * c8]) = alv;
+  }
+  h8 whi[kNI], wlo[kNI];
+#pragma unroll
+  for (int i = 0; i < kNI; ++i) split8(wr[i][0] * 16.f, wr[i][1] * 16.f, whi[i], wlo[i]);
+  __syncthreads();
+  HBK_MT(3, 2);
+  f4 acc[kRTM];
+#pragma unroll
+  for (int t = 0; t < kRTM; ++t) {
+    acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+    if (t < RT) {
+#pragma unroll
+      for (int i = 0; i < kNI; ++i) {
+        const h8 ah = *reinterpret_cast<const h8*>(&ahS[(16 * t + m) * kLdA + 32 * i + 8 * kq]);
+        const h8 al = *reinterpret_cast<const h8*>(&alS[(16 * t + m) * kLdA + 32 * i + 8 * kq]);
+        acc[t] = mma3(ah, al, whi[i], wlo[i], acc[t]);
+      }
+    }
+  }
+  float* out = a.hg_part + static_cast<int64_t>(ks) * a.B * kH2 + 16 * wave + m;
+#pragma unroll
+  for (int t = 0; t < kRTM; ++t)
+    if (t < RT) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int r = r0 + 16 * t + 4 * kq + e;
+        if (r < a.B) *BCK(&out[static_cast<int64_t>(r) * kH2], 4) = acc[t][e] * (1.f / 16.f);
       }
     }
   HBK_MT(3, 3);
@@ -668,6 +913,11 @@ struct K2Args {
   // counts[2 label + 1] += #(p > act_thr) over the live rows (float counters)
   float* counts;
   int count_label;
+  // v2: the prefetch workgroups run k1s (statistics + mask, kPreTiles2 tiles each),
+  // and every wave publishes the max |value| of the gradient tiles it stores
+  // (maxS[mat][row tile][wave], mat k = dHG_k, NG + k = dS_k: k3s's scales)
+  int v2;
+  float* maxS;
 };
 
 #ifdef HBK_TRACE
@@ -712,11 +962,20 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
     // the launch needs n_rt + n_rt / kPreTiles slots (two per CU)
     const int step = step_of(a.pre.state, a.pre.parity) + 1;
     if (step < a.pre.idx_steps) {
-      for (int t = 0; t < kPreTiles; ++t) {
-        const int rt = (blockIdx.x - a.n_rt) * kPreTiles + t;
-        if (rt >= a.n_rt) break;
-        if (t) __syncthreads();  // the slab's previous readers are done
-        k1a_tile<true>(a.pre, rt, step, a.pre.xhat[a.pre.parity ^ 1], hgRaw);
+      if (a.v2) {
+        for (int t = 0; t < kPreTiles2; ++t) {
+          const int rt = (blockIdx.x - a.n_rt) * kPreTiles2 + t;
+          if (rt >= a.n_rt) break;
+          if (t) __syncthreads();  // the mask image's previous readers are done
+          k1a_tile<true, true>(a.pre, rt, step, nullptr, hgRaw, a.pre.parity ^ 1);
+        }
+      } else {
+        for (int t = 0; t < kPreTiles; ++t) {
+          const int rt = (blockIdx.x - a.n_rt) * kPreTiles + t;
+          if (rt >= a.n_rt) break;
+          if (t) __syncthreads();  // the slab's previous readers are done
+          k1a_tile<true>(a.pre, rt, step, a.pre.xhat[a.pre.parity ^ 1], hgRaw);
+        }
       }
     }
     return;
@@ -734,8 +993,8 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
   const int step = step_of(a.state, a.parity);
   float y_pre = 0.f, nw_pre = a.neg_weight;
   if (kTrain) {
-    y_pre = a.y[static_cast<int64_t>(step) * a.y_stride + min(r0 + (tid & 15), a.B - 1)];
-    if (a.sched) nw_pre = a.sched[2 * min(step, a.sched_len - 1) + 1];
+    y_pre = *BCK(&a.y[static_cast<int64_t>(step) * a.y_stride + min(r0 + (tid & 15), a.B - 1)], 4);
+    if (a.sched) nw_pre = *BCK(&a.sched[2 * min(step, a.sched_len - 1) + 1], 4);
   }
   WFrag<kH, 2> wa;
   WFrag<kL, 2> wb;
@@ -780,8 +1039,8 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
         for (int q = 0; q < 4; ++q) {
           const int e = tid + 256 * q, r = min(e >> 6, nrow - 1), j = e & 63;
           const float* src = a.hg_part + (sl * B + r0 + r) * kH2;
-          lh[u][q] = src[j];
-          lg[u][q] = src[kH + j];
+          lh[u][q] = *BCK(&src[j], 4);
+          lg[u][q] = *BCK(&src[kH + j], 4);
         }
       }
 #pragma unroll
@@ -811,14 +1070,32 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
 #pragma unroll
     for (int e = 0; e < 4; ++e)
       if (r0 + row4 + e >= a.B) v[e] = 0.f;
-    *reinterpret_cast<f4*>(base + col * Bp + r0 + row4) = v;
+    *BCK(reinterpret_cast<f4*>(base + col * Bp + r0 + row4), 16) = v;
   };
-  // a [16][kLd] LDS tile's first ncols columns -> base^T (4 rows per float4)
+  // a [16][kLd] LDS tile's first ncols columns -> base^T (4 rows per float4);
+  // returns the max |value| stored (dead rows are stored as zeros)
+  auto amax4 = [&](f4 v, int row4) {
+    float x = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) x = fmaxf(x, r0 + row4 + e < a.B ? fabsf(v[e]) : 0.f);
+    return x;
+  };
   auto store_t = [&](float* base, const float* src, int ncols) {
+    float mx = 0.f;
     for (int e = tid; e < 4 * ncols; e += 256) {
       const int col = e >> 2, r4 = 4 * (e & 3);
-      st4(base, col, r4,
-          f4{src[r4 * kLd + col], src[(r4 + 1) * kLd + col], src[(r4 + 2) * kLd + col], src[(r4 + 3) * kLd + col]});
+      const f4 v = f4{src[r4 * kLd + col], src[(r4 + 1) * kLd + col], src[(r4 + 2) * kLd + col],
+                      src[(r4 + 3) * kLd + col]};
+      mx = fmaxf(mx, amax4(v, r4));
+      st4(base, col, r4, v);
+    }
+    return mx;
+  };
+  // v2: this wave's max |gradient| of matrix mat over this row tile
+  auto pub_max = [&](int mat, float mx) {
+    if (a.maxS) {
+      mx = wmax(mx);
+      if (lane == 0) *BCK(&a.maxS[(static_cast<int64_t>(mat) * a.n_rt + blockIdx.x) * 4 + wave], 4) = mx;
     }
   };
   if (kTrain) {  // U_0 from bU: thread -> column tid & 63, rows 4 (tid >> 6) ..
@@ -921,8 +1198,8 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
     float dz = 0.f;
     if (r < nrow) {
       const float z = zS[r], p = sigm(z);
-      if (a.prob) a.prob[r0 + r] = p;
-      if (a.logit) a.logit[r0 + r] = z;
+      if (a.prob) *BCK(&a.prob[r0 + r], 4) = p;
+      if (a.logit) *BCK(&a.logit[r0 + r], 4) = z;
       if (kTrain) {
         const float nw = nw_pre;
         const float yy = y_pre;
@@ -956,8 +1233,8 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
       pge = rsum16(pge);
       pgt = rsum16(pgt);
       if (tid == 0) {
-        if (pge != 0.f) atomicAdd(a.counts + 2 * a.count_label, pge);
-        if (pgt != 0.f) atomicAdd(a.counts + 2 * a.count_label + 1, pgt);
+        if (pge != 0.f) atomicAdd(BCK(a.counts + 2 * a.count_label, 4), pge);
+        if (pgt != 0.f) atomicAdd(BCK(a.counts + 2 * a.count_label + 1, 4), pgt);
       }
     }
     if (kTrain) {
@@ -971,14 +1248,18 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
   if constexpr (!kTrain) return;
   __syncthreads();
   K2_MARK(41);
-  if (tid < kStats && red[tid] != 0.f) atomicAdd(a.stats + tid, red[tid]);
+  if (tid < kStats && red[tid] != 0.f) atomicAdd(BCK(a.stats + tid, 4), red[tid]);
   // ---------------------------------------------------------- backward ---
   float* G = a.G;
-  if (tid < 4) st4(a.dS + (NG - 1) * kL * Bp, 0, 4 * tid, f4{dzS[4 * tid], dzS[4 * tid + 1], dzS[4 * tid + 2], dzS[4 * tid + 3]});
+  {
+    const f4 dz4 = f4{dzS[4 * (tid & 3)], dzS[4 * (tid & 3) + 1], dzS[4 * (tid & 3) + 2], dzS[4 * (tid & 3) + 3]};
+    if (tid < 4) st4(a.dS + (NG - 1) * kL * Bp, 0, 4 * tid, dz4);
+    pub_max(2 * NG - 1, tid < 4 ? amax4(dz4, 4 * tid) : 0.f);
+  }
   if (tid == 64) {  // output bias gradient = sum dz
     float s = 0.f;
     for (int r = 0; r < kR; ++r) s += dzS[r];
-    if (s != 0.f) atomicAdd(G + a.b_o[NG - 1], s);
+    if (s != 0.f) atomicAdd(BCK(G + a.b_o[NG - 1], 4), s);
   }
   // output unit: dU = dz w_o, gate backward -> dHG (bX)
   {
@@ -999,6 +1280,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
     }
     st4(a.dHG + k * kH2 * Bp, j, rg, dho);
     st4(a.dHG + k * kH2 * Bp, kH + j, rg, dgo);
+    pub_max(k, fmaxf(amax4(dho, rg), amax4(dgo, rg)));
   }
   __syncthreads();
   K2_MARK(42);
@@ -1008,7 +1290,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
     if (tid < kH2) {
       float s = 0.f;
       for (int r = 0; r < kR; ++r) s += bX[r][tid];
-      atomicAdd(G + a.b_hg[k] + tid, s);
+      atomicAdd(BCK(G + a.b_hg[k] + tid, 4), s);
     }
     // dXn = dHG_k W_hg_k (NN: K 128 -> N 96, fragments fx) -> bU; then W_hg_{k-1}'s
     {
@@ -1034,8 +1316,8 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
           sg += bU[r][tid] * xhS[l][r][tid];
           sb += bU[r][tid];
         }
-        atomicAdd(G + a.ln_g[l] + tid, sg);
-        atomicAdd(G + a.ln_b[l] + tid, sb);
+        atomicAdd(BCK(G + a.ln_g[l] + tid, 4), sg);
+        atomicAdd(BCK(G + a.ln_b[l] + tid, 4), sb);
       }
       // 16 lanes per row, as in the forward LayerNorm; dS^T goes to HBM from
       // LDS in the next stage
@@ -1060,11 +1342,11 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
     // fragments fy) with the gate backward in the epilogue -> dHG_{k-1} (bX)
     {
       const int kk = k - 1;
-      store_t(a.dS + kk * kL * Bp, &bS[0][0], kL);
+      pub_max(NG + kk, store_t(a.dS + kk * kL * Bp, &bS[0][0], kL));
       if (tid < kL) {
         float s = 0.f;
         for (int r = 0; r < kR; ++r) s += bS[r][tid];
-        atomicAdd(G + a.b_o[kk] + tid, s);
+        atomicAdd(BCK(G + a.b_o[kk] + tid, 4), s);
       }
       const f4 du = gemm1<kL>(fy, load_a<kL>(&bS[0][0], lane));
       if (!(HBK_K2_ABLATE & 1) && k - 2 >= 0) load_wf<kL, kH, 1>(fy, a.wc + a.c_oT[k - 2], wave, lane);
@@ -1083,6 +1365,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
       }
       st4(a.dHG + kk * kH2 * Bp, j, 4 * kq, dho);
       st4(a.dHG + kk * kH2 * Bp, kH + j, 4 * kq, dgo);
+      pub_max(kk, fmaxf(amax4(dho, 4 * kq), amax4(dgo, 4 * kq)));
     }
     __syncthreads();
     K2_MARK(70 + k);
@@ -1091,7 +1374,7 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
   if (tid < kH2) {
     float s = 0.f;
     for (int r = 0; r < kR; ++r) s += bX[r][tid];
-    atomicAdd(G + a.b_hg[0] + tid, s);
+    atomicAdd(BCK(G + a.b_hg[0] + tid, 4), s);
   }
   K2_MARK(99);
 #ifdef HBK_TRACE
@@ -1375,15 +1658,315 @@ __global__ void __launch_bounds__(256) k3_wgrad_kernel(K3Args a) {
   }
 }
 
+// ------------------------------------------------------------ k3s (v2) ---
+// The weight gradients dW [M][N] = dY^T X over S batch splits of R rows, with
+// wide N tiles: tile = 128 (M) x 16 NBT (N), 4 waves of 32 M rows each, so the
+// gradient operand dY^T is read from HBM / L2 once per N tile (the v1 kernel's
+// 32-column tiles re-read dHG0 48 times per split: 27 MB of its 47 MB per step at
+// B = 1,100). The batch streams through in 32-row steps: the activation chunk X
+// (16 NBT columns x 32 rows) is converted to f16 hi / lo planes in a double-
+// buffered LDS image (one barrier per step), the gradient chunk is loaded two steps
+// ahead into registers. The gradient's power-of-two scale comes from k2's per-tile
+// maxima (maxS), so the whole split accumulates in one scale. The input layer's X
+// is not stored anywhere: it is recomputed from the pool rows, k1s's statistics and
+// dropout mask (xhat = (v - mu) rs, the formula of k1a) as the chunk is staged.
+constexpr int kK3sMaxR = 512;  // rows per split
+struct K3sJob {
+  const float* X;  // the gradient dY^T [M][Bp]
+  const float* Y;  // the activation X^T [N][Bp]; NULL: the input layer's pool rows
+  int64_t c_off;
+  int ldc, M, N, tn, mat;
+};
+struct K3sArgs {
+  K3sJob job[kMaxJobs];
+  int start[kMaxJobs + 1];
+  int n_jobs, S, R, n_rt, B;
+  int64_t Bp;
+  const float* maxS;  // [2 NG][n_rt][4]
+  const float* pool32;
+  const _Float16* pool16;
+  const uint4* rinfo;
+  const uint32_t* mask;
+  float keep;
+  // input-layer post-op (job 0)
+  const float* g_in;
+  const float* b_in;
+  const float* W0;
+  int64_t g_off, b_off;
+  float* part;  // [S][pstride]
+  int64_t pstride;
+};
+template <int NBT>
+struct K3sShared {
+  static constexpr int NT = 16 * NBT, kLdY = 48;  // LDS column: 32 rows + 16 pad halves (conflict-free b128 reads)
+  _Float16 ys[2][2][NT * kLdY];                    // [buf][hi, lo][col][row]
+  float sS[128];
+  float red[2][4][NT];
+  uint4 rinfoS[kK3sMaxR];                          // input layer: the split's rows' {mu, rs, address}
+  uint32_t maskS[kK3sMaxR * (NT / 32)];            // ... and their mask words of this N tile
+};
+// one workgroup's tile; kRaw: the input layer (X from the pool rows). Straight-line steady
+// state: the prefetches are unconditional (clamped to the last step: a redundant reload at
+// the tail), so the counted vmcnt waits stay exact across the loop
+template <int NBT, bool kRaw>
+__device__ __forceinline__ void k3s_body(const K3sArgs& a, const K3sJob& jb, int split, int tm, int tnn,
+                                         K3sShared<NBT>& sh) {
+  constexpr int NT = 16 * NBT, kLdY = K3sShared<NBT>::kLdY;
+  constexpr int kYU = NT * 8 / 256;  // float4 units per thread and step (transposed X)
+  constexpr int kRPT = NT / 8;       // pool rows per thread and step (input layer)
+  static_assert(NT >= 64 && 256 % NT == 0, "a wave's lanes are 64 consecutive columns of one row group");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = lane & 15, kq = lane >> 4;
+  const int Bp = static_cast<int>(a.Bp);
+  const int rb0 = split * a.R;
+  const int nst = (min(a.R, Bp - rb0) + 31) / 32;  // 32-row steps of this split (>= 1)
+  const int n0 = tnn * NT;
+  const int nb = min(NBT, (jb.N - n0 + 15) / 16);  // live 16-column tiles (uniform)
+  const int mrow = tm * 128 + 32 * wave;
+  // the gradient's scale over the split's row tiles: max |dY| into [2^14, 2^15)
+  float sc, inv;
+  {
+    const int t0 = rb0 / 16, t1 = min(a.n_rt, (rb0 + 32 * nst) / 16);
+    float mx = 0.f;
+    for (int q = lane; q < 4 * (t1 - t0); q += 64)
+      mx = fmaxf(mx, *BCK(&a.maxS[(static_cast<int64_t>(jb.mat) * a.n_rt + t0) * 4 + q], 4));
+    pow2_scale(wmax(mx), sc, inv);
+  }
+  // gradient chunk of step u: two 16-row M tiles x 8 batch rows (b = 32 u + 8 kq ..)
+  const float* X0 = jb.X + static_cast<int64_t>(min(mrow + m, jb.M - 1)) * Bp;
+  const float* X1 = jb.X + static_cast<int64_t>(min(mrow + 16 + m, jb.M - 1)) * Bp;
+  auto load_g = [&](int u, f4 (&d)[2][2]) {
+    const int b = min(rb0 + 32 * u + 8 * kq, Bp - 8);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      d[0][h] = *BCK(reinterpret_cast<const f4*>(X0 + b + 4 * h), 16);
+      d[1][h] = *BCK(reinterpret_cast<const f4*>(X1 + b + 4 * h), 16);
+    }
+  };
+  const int rc = tid % NT, rg = __builtin_amdgcn_readfirstlane(tid / NT);  // input layer: column, row group
+  if constexpr (kRaw) {  // the split's row information and mask words (rows past B: row B - 1's, zeroed below)
+    // (unrolled, every load unconditional at a clamped row: all in flight together)
+    const int nr = 32 * nst;
+    constexpr int kRI = kK3sMaxR / 256, kMI = kK3sMaxR * (NT / 32) / 256;
+    uint4 ri[kRI];
+    uint32_t mi[kMI];
+#pragma unroll
+    for (int it = 0; it < kRI; ++it)
+      ri[it] = *BCK(&a.rinfo[min(rb0 + min(tid + 256 * it, nr - 1), a.B - 1)], 16);
+#pragma unroll
+    for (int it = 0; it < kMI; ++it) {
+      const int q = min(tid + 256 * it, nr * (NT / 32) - 1);
+      mi[it] = *BCK(&a.mask[static_cast<int64_t>(min(rb0 + q / (NT / 32), a.B - 1)) * kMaskW + n0 / 32 + q % (NT / 32)], 4);
+    }
+#pragma unroll
+    for (int it = 0; it < kRI; ++it)
+      if (tid + 256 * it < nr) sh.rinfoS[tid + 256 * it] = ri[it];
+#pragma unroll
+    for (int it = 0; it < kMI; ++it)
+      if (tid + 256 * it < nr * (NT / 32)) sh.maskS[tid + 256 * it] = mi[it];
+    __syncthreads();
+  }
+  HBK_MT(2, 3);
+  // activation chunk of step u into registers ...
+  f4 yv[kRaw ? 1 : kYU];
+  uint32_t yw[kRaw ? kRPT : 1];
+  auto load_y = [&](int u) {
+    if constexpr (kRaw) {
+      const int col = n0 + rc;
+#pragma unroll
+      for (int i = 0; i < kRPT; ++i) {
+        bool is16;
+        const char* base = row_addr(sh.rinfoS[32 * u + kRPT * rg + i], is16);
+        yw[i] = *BCK(reinterpret_cast<const uint32_t*>(base + ((static_cast<int64_t>(col) << (is16 ? 1 : 2)) & ~int64_t(3))), 4);
+      }
+    } else {
+#pragma unroll
+      for (int jj = 0; jj < kYU; ++jj) {
+        const int q = tid + 256 * jj, col = min(n0 + (q >> 3), jb.N - 1);
+        const int b = min(rb0 + 32 * u + 4 * (q & 7), Bp - 4);
+        yv[jj] = *BCK(reinterpret_cast<const f4*>(jb.Y + static_cast<int64_t>(col) * Bp + b), 16);
+      }
+    }
+  };
+  // ... converted into LDS buffer buf
+  auto write_y = [&](int u, int buf) {
+    _Float16* yh = &sh.ys[buf][0][0];
+    _Float16* yl = &sh.ys[buf][1][0];
+    if constexpr (kRaw) {
+      const int col = n0 + rc;
+      float xs[kRPT];
+#pragma unroll
+      for (int i = 0; i < kRPT; ++i) {
+        const int rl = 32 * u + kRPT * rg + i;
+        const uint4 inf = sh.rinfoS[rl];
+        const bool is16 = (inf.z & 1u) != 0;
+        const float x = is16 ? static_cast<float>(__builtin_bit_cast(
+                                   _Float16, static_cast<uint16_t>((col & 1) ? yw[i] >> 16 : yw[i])))
+                             : __builtin_bit_cast(float, yw[i]);
+        const uint32_t mwd = sh.maskS[rl * (NT / 32) + (rc >> 5)];
+        const float v = (mwd >> (col & 31)) & 1u ? 0.f : x * a.keep;
+        xs[i] = rb0 + rl < a.B ? (v - __uint_as_float(inf.x)) * __uint_as_float(inf.y) : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < kRPT; i += 8) {
+        h8 hv, lv;
+        split8(f4{xs[i], xs[i + 1], xs[i + 2], xs[i + 3]}, f4{xs[i + 4], xs[i + 5], xs[i + 6], xs[i + 7]}, hv, lv);
+        *reinterpret_cast<h8*>(yh + rc * kLdY + kRPT * rg + i) = hv;
+        *reinterpret_cast<h8*>(yl + rc * kLdY + kRPT * rg + i) = lv;
+      }
+    } else {
+#pragma unroll
+      for (int jj = 0; jj < kYU; ++jj) {
+        const int q = tid + 256 * jj, col = q >> 3, b4 = 4 * (q & 7);
+        const f4 v = rb0 + 32 * u + b4 < Bp ? yv[jj] : f4{0.f, 0.f, 0.f, 0.f};
+        uint32_t h0, l0, h1, l1;
+        split_pair(v[0], v[1], h0, l0);
+        split_pair(v[2], v[3], h1, l1);
+        *reinterpret_cast<uint2*>(yh + col * kLdY + b4) = uint2{h0, h1};
+        *reinterpret_cast<uint2*>(yl + col * kLdY + b4) = uint2{l0, l1};
+      }
+    }
+  };
+  const f4 z = {0.f, 0.f, 0.f, 0.f};
+  f4 acc[2][NBT];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int nt = 0; nt < NBT; ++nt) acc[t][nt] = z;
+  f4 ssum[2] = {z, z};
+  f4 ga[2][2][2];  // gradient ring: [slot][tile][half]
+  // prologue: step 0 staged, steps 0 / 1 of the gradient and step 1 of X in flight
+  const int last = nst - 1;
+  load_y(0);
+  load_g(0, ga[0]);
+  write_y(0, 0);
+  load_y(min(1, last));
+  load_g(min(1, last), ga[1]);
+  __syncthreads();
+  HBK_MT(2, 4);
+  auto step = [&](int u, f4 (&g)[2][2]) {
+    // this step's gradient: dead batch rows zeroed, row sums (input layer), scaled split
+    const bool live = rb0 + 32 * u + 8 * kq < Bp;
+    h8 ah[2], al[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const f4 g0 = live ? g[t][0] : z, g1 = live ? g[t][1] : z;
+      ssum[t] += g0 + g1;
+      split8(g0 * sc, g1 * sc, ah[t], al[t]);
+    }
+    const _Float16* yh = &sh.ys[u & 1][0][0];
+    const _Float16* yl = &sh.ys[u & 1][1][0];
+#pragma unroll
+    for (int nt = 0; nt < NBT; ++nt)
+      if (nt < nb) {
+        const h8 bh = *reinterpret_cast<const h8*>(yh + (16 * nt + m) * kLdY + 8 * kq);
+        const h8 bl = *reinterpret_cast<const h8*>(yl + (16 * nt + m) * kLdY + 8 * kq);
+        acc[0][nt] = mma3(ah[0], al[0], bh, bl, acc[0][nt]);
+        acc[1][nt] = mma3(ah[1], al[1], bh, bl, acc[1][nt]);
+      }
+    // step u + 1's X into the other buffer (read by nobody now: the barrier that ended step
+    // u - 1 passed), then step u + 2's loads (clamped: past the end they reload the last step)
+    write_y(min(u + 1, last), (u + 1) & 1);
+    load_y(min(u + 2, last));
+    load_g(min(u + 2, last), g);
+    lds_barrier();  // (LDS only: step u + 2's loads stay in flight)
+    HBK_MT(2, 16 + u);
+  };
+  for (int u = 0; u < nst; u += 2) {
+    step(u, ga[0]);
+    if (u + 1 < nst) step(u + 1, ga[1]);
+  }
+  HBK_MT(2, 2);
+  float* const C = a.part + split * a.pstride + jb.c_off;
+  if constexpr (!kRaw) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = mrow + 16 * t + 4 * kq + e;
+        if (row >= jb.M) continue;
+#pragma unroll
+        for (int nt = 0; nt < NBT; ++nt) {
+          const int c = n0 + 16 * nt + m;
+          if (nt < nb && c < jb.N) *BCK(&C[static_cast<int64_t>(row) * jb.ldc + c], 4) = acc[t][nt][e] * inv;
+        }
+      }
+    return;
+  } else {
+    // input layer: dW = g o (dHG0^T xhat) + s (x) b, dgamma = sum_j W o (dHG0^T xhat),
+    // dbeta = sum_j W s_j, with s_j = the split's sum of dHG0[b][j]
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      float sj = (ssum[t][0] + ssum[t][1]) + (ssum[t][2] + ssum[t][3]);
+      sj += __shfl_xor(sj, 16, 64);
+      sj += __shfl_xor(sj, 32, 64);
+      if (kq == 0) sh.sS[32 * wave + 16 * t + m] = sj;
+    }
+    __syncthreads();
+    float dg[NBT], db[NBT];
+#pragma unroll
+    for (int nt = 0; nt < NBT; ++nt) {
+      dg[nt] = db[nt] = 0.f;
+      const int c = min(n0 + 16 * nt + m, jb.N - 1);
+      const float gc = *BCK(&a.g_in[c], 4), bc = *BCK(&a.b_in[c], 4);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = mrow + 16 * t + 4 * kq + e;  // j (< 128 = M)
+          const float w = *BCK(&a.W0[static_cast<int64_t>(row) * jb.ldc + c], 4);
+          const float s = sh.sS[32 * wave + 16 * t + 4 * kq + e];
+          const float v = acc[t][nt][e] * inv;
+          if (nt < nb) *BCK(&C[static_cast<int64_t>(row) * jb.ldc + n0 + 16 * nt + m], 4) = gc * v + bc * s;
+          dg[nt] += w * v;
+          db[nt] += w * s;
+        }
+    }
+#pragma unroll
+    for (int nt = 0; nt < NBT; ++nt) {
+#pragma unroll
+      for (int o = 16; o < 64; o <<= 1) {
+        dg[nt] += __shfl_xor(dg[nt], o, 64);
+        db[nt] += __shfl_xor(db[nt], o, 64);
+      }
+      if (kq == 0) {
+        sh.red[0][wave][16 * nt + m] = dg[nt];
+        sh.red[1][wave][16 * nt + m] = db[nt];
+      }
+    }
+    __syncthreads();
+    if (tid < nb * 16) {
+      float* P = a.part + split * a.pstride;
+      *BCK(&P[a.g_off + n0 + tid], 4) = sh.red[0][0][tid] + sh.red[0][1][tid] + sh.red[0][2][tid] + sh.red[0][3][tid];
+      *BCK(&P[a.b_off + n0 + tid], 4) = sh.red[1][0][tid] + sh.red[1][1][tid] + sh.red[1][2][tid] + sh.red[1][3][tid];
+    }
+  }
+}
+template <int NBT>
+__global__ void __launch_bounds__(256) k3s_kernel(K3sArgs a) {
+  __shared__ __attribute__((aligned(16))) K3sShared<NBT> sh;
+  const int blk = blockIdx.x;
+  int j = 0;
+  while (j + 1 < a.n_jobs && blk >= a.start[j + 1]) ++j;
+  const K3sJob jb = a.job[j];
+  const int local = blk - a.start[j];
+  const int split = local % a.S, tile = local / a.S;
+  const int tm = tile / jb.tn, tnn = tile - tm * jb.tn;
+  HBK_MT(2, 1);
+  if (jb.Y == nullptr)
+    k3s_body<NBT, true>(a, jb, split, tm, tnn, sh);
+  else
+    k3s_body<NBT, false>(a, jb, split, tm, tnn, sh);
+}
+
 // Steps whose update does not get the workspace (or is preceded by the
 // data-parallel all-reduce): the slabs added into the bucket's covered ranges
 __global__ void __launch_bounds__(256) k3_fold_kernel(Ranges rg, const float* __restrict__ part, int64_t pstride,
                                                       int ns, float* __restrict__ G, int64_t n) {
   for (int64_t i = blockIdx.x * int64_t(256) + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
     if (!in_ranges(rg, i)) continue;
-    float g = G[i];
-    for (int sp = 0; sp < ns; ++sp) g += part[sp * pstride + i];
-    G[i] = g;
+    float g = *BCK(&G[i], 4);
+    for (int sp = 0; sp < ns; ++sp) g += *BCK(&part[sp * pstride + i], 4);
+    *BCK(&G[i], 4) = g;
   }
 }
 
@@ -2196,7 +2779,7 @@ __global__ void __launch_bounds__(256) kv_finish_kernel(EvalFinish f) {
 
 // --------------------------------------------------------- workspace ------
 struct FusedWs {
-  int64_t wsplit, part, pstride, hg_part, xhat[2], U, Xn, dS, dHG, total;  // float offsets
+  int64_t wsplit, part, pstride, hg_part, xhat[2], U, Xn, dS, dHG, rinfo[2], mask[2], maxS, total;  // float offsets
 };
 // the weight cache's segments (WSplit) for plan p: W_o_k (k < NG - 1), then W_hg_k (k >= 1)
 WSplit make_wsplit(const hbk_mlp_plan& p) {
@@ -2248,8 +2831,76 @@ FusedWs fused_layout(int64_t B, int NG, int64_t n_params = 0) {
   w.Xn = take(int64_t(NG) * Bp * kL);
   w.dS = take(int64_t(NG) * Bp * kL);
   w.dHG = take(int64_t(NG) * Bp * kH2);
+  w.rinfo[0] = take(Bp * 4);
+  w.rinfo[1] = take(Bp * 4);
+  w.mask[0] = take(Bp * kMaskW);
+  w.mask[1] = take(Bp * kMaskW);
+  w.maxS = take(int64_t(2) * NG * (Bp / kR) * 4);
   w.total = o;
   return w;
+}
+
+// HBK_STEP=2: the v2 step (k1s -> k1c / k3s from the pool rows); 1: the k1a -> xhat^T ->
+// k1b / k3 path. The default is kStepDefault (the faster one as measured, tools/ab_step.sh)
+constexpr int kStepDefault = 1;
+bool step_v2() {
+  static const bool v2 = (getenv("HBK_STEP") ? atoi(getenv("HBK_STEP")) : kStepDefault) == 2;
+  return v2;
+}
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+// k1c's geometry: K chunk KC (KS = 1536 / KC chunks) and row tiles RT per block, by a
+// per-CU byte model: the block's pool rows (~2.2 B per element at the training mix),
+// its W slice and its partial slab, times the rounds of blocks per CU, plus the KS
+// slabs each k2 row tile sums first (HBK_K1_KC / HBK_K1_RT override)
+struct K1cGeom {
+  int KC, RT, KS, blocks;
+};
+int k1c_rtmax(int KC) {
+  switch (KC) {
+    case 64: return k1c_rt_max<64>();
+    case 96: return k1c_rt_max<96>();
+    case 192: return k1c_rt_max<192>();
+    default: return k1c_rt_max<384>();
+  }
+}
+K1cGeom k1c_geom(int B, const void* stream) {
+  const int cus = static_cast<int>(std::max<int64_t>(1, persistent_blocks(1, stream)));
+  const int fkc = env_int("HBK_K1_KC", 0), frt = env_int("HBK_K1_RT", 0);
+  K1cGeom best{192, 9, 8, 0};
+  double best_cost = 1e30;
+  for (int KC : {64, 96, 192, 384}) {
+    if (fkc && KC != fkc) continue;
+    const int rtm = k1c_rtmax(KC);
+    const double lds = 16.0 * rtm * (KC + 16) * 4 + 8.0 * KC;
+    const int per_cu = std::max(1, std::min(2, static_cast<int>(160.0 * 1024 / lds)));
+    for (int RT = 1; RT <= rtm; ++RT) {
+      if (frt && RT != std::min(frt, rtm)) continue;
+      const int KS = kD / KC, nrb = (B + 16 * RT - 1) / (16 * RT), blocks = nrb * KS;
+      const int rounds = (blocks + cus * per_cu - 1) / (cus * per_cu);
+      const int on_cu = std::min(per_cu, (blocks + cus - 1) / cus);
+      const double rows = std::min(16 * RT, B);
+      const double per_wg = rows * KC * 2.2 + 128.0 * KC * 4 + rows * 128 * 4;
+      const double cost = per_wg * on_cu * rounds + KS * 16.0 * 128 * 4;
+      if (cost < best_cost) {
+        best_cost = cost;
+        best = K1cGeom{KC, RT, KS, blocks};
+      }
+    }
+  }
+  return best;
+}
+// k3s's batch split: about CUs / (the launch's tiles) splits, 128 .. 512 rows each (HBK_K3_R overrides)
+int k3s_rows(int64_t Bp, int tiles, const void* stream) {
+  const int cus = static_cast<int>(std::max<int64_t>(1, persistent_blocks(1, stream)));
+  int R = env_int("HBK_K3_R", 0);
+  if (R <= 0) {
+    const int S = std::max(1, cus / std::max(1, tiles));
+    R = static_cast<int>((Bp + S - 1) / S + 31) / 32 * 32;
+  }
+  return std::max(128, std::min(kK3sMaxR, R / 32 * 32));
 }
 
 void fill_k2(const hbk_mlp_plan& p, K2Args& k) {
@@ -2326,6 +2977,21 @@ int64_t mlp_fused_ws_floats(const hbk_mlp_plan& p, int64_t B) {
 }
 
 // k1 + k2 (+ k3): the forward (inference) or forward/backward half of a step.
+#ifdef HBK_BOUNDS
+void bounds_set(std::initializer_list<std::pair<const void*, int64_t>> rs) {
+  unsigned long long h[kBMax][2] = {};
+  int n = 0;
+  for (const auto& r : rs)
+    if (r.first && r.second > 0 && n < kBMax) {
+      h[n][0] = reinterpret_cast<unsigned long long>(r.first);
+      h[n][1] = h[n][0] + static_cast<unsigned long long>(r.second);
+      ++n;
+    }
+  (void)hipDeviceSynchronize();
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_brange), h, sizeof(h));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_bn), &n, sizeof(n));
+}
+#endif
 int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool32, int64_t n32,
                   const void* pool16, int64_t n16, const int32_t* idx, int64_t idx_stride, int64_t idx_steps,
                   const float* y, int64_t y_stride, int B, const float* state, int parity, const float* sched,
@@ -2333,7 +2999,20 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
                   float* bucket, float* prob, float* logit, float* ws, bool train, int flags, hipStream_t s) {
   const int NG = static_cast<int>(p.g.size());
   const FusedWs w = fused_layout(B, NG, p.n_params);
-  const int KS = k1_splits(B);
+#ifdef HBK_BOUNDS
+  bounds_set({{params, p.n_params * 4},
+              {pool32, n32 * kD * 4},
+              {pool16, n16 * kD * 2},
+              {idx, (std::max<int64_t>(idx_steps, 1) * idx_stride + B) * 4},
+              {y, (std::max<int64_t>(idx_steps, 1) * y_stride + B) * 4},
+              {state, 64},
+              {sched, int64_t(sched_len) * 8},
+              {bucket, (p.n_params + kStats) * 4},
+              {prob, int64_t(B) * 4},
+              {logit, int64_t(B) * 4},
+              {ws, w.total * 4}});
+#endif
+
   const int64_t Bp = (B + kR - 1) / kR * kR;
   const int rt = (B + kR - 1) / kR;
   K1aArgs ka;
@@ -2352,6 +3031,12 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
   ka.xhat[0] = ws + w.xhat[0];
   ka.xhat[1] = ws + w.xhat[1];
   ka.Bp = Bp;
+  for (int i = 0; i < 2; ++i) {
+    ka.rinfo[i] = reinterpret_cast<uint4*>(ws + w.rinfo[i]);
+    ka.mask[i] = reinterpret_cast<uint32_t*>(ws + w.mask[i]);
+  }
+  const bool v2 = step_v2();
+  const float keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
   const float* xhat = ws + w.xhat[parity];
   const WSplit wsp = make_wsplit(p);
   _Float16* wc = reinterpret_cast<_Float16*>(ws + w.wsplit);
@@ -2362,12 +3047,48 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
     HBK_LAUNCH_CHECK("k0_wsplit_kernel");
   }
   if (!(flags & HBK_STEP_XHAT_READY)) {  // this step's rows were not prefetched by the previous step
-    if (idx)
-      hipLaunchKernelGGL(k1a_kernel<true>, dim3(rt), dim3(256), 0, s, ka, 0);
-    else
-      hipLaunchKernelGGL(k1a_kernel<false>, dim3(rt), dim3(256), 0, s, ka, 0);
-    HBK_LAUNCH_CHECK("k1a_kernel");
+    if (v2) {
+      if (idx)
+        hipLaunchKernelGGL(k1s_kernel<true>, dim3(rt), dim3(256), 0, s, ka, 0);
+      else
+        hipLaunchKernelGGL(k1s_kernel<false>, dim3(rt), dim3(256), 0, s, ka, 0);
+      HBK_LAUNCH_CHECK("k1s_kernel");
+    } else {
+      if (idx)
+        hipLaunchKernelGGL(k1a_kernel<true>, dim3(rt), dim3(256), 0, s, ka, 0);
+      else
+        hipLaunchKernelGGL(k1a_kernel<false>, dim3(rt), dim3(256), 0, s, ka, 0);
+      HBK_LAUNCH_CHECK("k1a_kernel");
+    }
   }
+  int KS = k1_splits(B);
+  if (v2) {
+    const K1cGeom g1 = k1c_geom(B, s);
+    KS = g1.KS;
+    K1cArgs kc;
+    kc.P = params;
+    kc.g_in = p.ln_in.g;
+    kc.b_in = p.ln_in.b;
+    kc.w0 = p.g[0].w_hg;
+    kc.B = B;
+    kc.RT = g1.RT;
+    kc.KS = g1.KS;
+    kc.pool32 = pool32;
+    kc.pool16 = static_cast<const _Float16*>(pool16);
+    kc.rinfo = ka.rinfo[parity];
+    kc.mask = ka.mask[parity];
+    kc.keep = keep;
+    kc.hg_part = ws + w.hg_part;
+    kc.stats = train ? bucket + p.n_params : nullptr;
+    auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(g1.blocks), dim3(512), 0, s, kc); };
+    switch (g1.KC) {
+      case 64: launch(k1c_kernel<64>); break;
+      case 96: launch(k1c_kernel<96>); break;
+      case 192: launch(k1c_kernel<192>); break;
+      default: launch(k1c_kernel<384>);
+    }
+    HBK_LAUNCH_CHECK("k1c_kernel");
+  } else {
   K1bArgs kb;
   kb.P = params;
   kb.g_in = p.ln_in.g;
@@ -2389,6 +3110,7 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
       default: launch(k1b_kernel<24>);
     }
     HBK_LAUNCH_CHECK("k1b_kernel");
+  }
   }
   K2Args k2;
   k2.P = params;
@@ -2419,9 +3141,12 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
   k2.n_rt = rt;
   k2.prefetch = train && idx && (flags & HBK_STEP_PREFETCH_NEXT);
   k2.pre = ka;
+  k2.v2 = v2 ? 1 : 0;
+  k2.maxS = v2 && train ? ws + w.maxS : nullptr;
   set_k2_cache(wsp, NG, wc, k2);
   {
-    const int grid = k2.prefetch ? rt + (rt + kPreTiles - 1) / kPreTiles : rt;
+    const int pt = v2 ? kPreTiles2 : kPreTiles;
+    const int grid = k2.prefetch ? rt + (rt + pt - 1) / pt : rt;
     auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, k2); };
     if (train) {
       if (NG == 2) launch(k2_rows_kernel<true, 2>);
@@ -2435,6 +3160,65 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
     HBK_LAUNCH_CHECK("k2_rows_kernel");
   }
   if (!train) return HBK_OK;
+  if (v2) {  // k3s: job 0 = input layer (pool rows), then dW_hg of GMLPs 1.., then dW_o of every GMLP
+    constexpr int kNT = 128;
+    K3sArgs k3;
+    int nj = 0, tiles = 0;
+    auto add = [&](const float* X, const float* Y, int64_t c_off, int ldc, int M, int N, int mat) {
+      K3sJob& j = k3.job[nj];
+      j.X = X;
+      j.Y = Y;
+      j.c_off = c_off;
+      j.ldc = ldc;
+      j.M = M;
+      j.N = N;
+      j.tn = (N + kNT - 1) / kNT;
+      j.mat = mat;
+      k3.start[nj] = tiles;
+      tiles += ((M + 127) / 128) * j.tn;
+      ++nj;
+    };
+    add(ws + w.dHG, nullptr, p.g[0].w_hg, kD, kH2, kD, 0);
+    for (int k = 1; k < NG; ++k)
+      add(ws + w.dHG + int64_t(k) * kH2 * Bp, ws + w.Xn + int64_t(k) * kL * Bp, p.g[k].w_hg, kL, kH2, kL, k);
+    for (int k = 0; k < NG; ++k)
+      add(ws + w.dS + int64_t(k) * kL * Bp, ws + w.U + int64_t(k) * kH * Bp, p.g[k].w_o, kH, p.g[k].out, kH, NG + k);
+    const int R = k3s_rows(Bp, tiles, s);
+    const int S = static_cast<int>((Bp + R - 1) / R);
+    for (int i = 0; i < nj; ++i) k3.start[i] *= S;
+    k3.start[nj] = tiles * S;
+    k3.n_jobs = nj;
+    k3.S = S;
+    k3.R = R;
+    k3.n_rt = rt;
+    k3.B = B;
+    k3.Bp = Bp;
+    k3.maxS = ws + w.maxS;
+    k3.pool32 = pool32;
+    k3.pool16 = static_cast<const _Float16*>(pool16);
+    k3.rinfo = ka.rinfo[parity];
+    k3.mask = ka.mask[parity];
+    k3.keep = keep;
+    k3.g_in = params + p.ln_in.g;
+    k3.b_in = params + p.ln_in.b;
+    k3.W0 = params + p.g[0].w_hg;
+    k3.g_off = p.ln_in.g;
+    k3.b_off = p.ln_in.b;
+    k3.part = ws + w.part;
+    k3.pstride = w.pstride;
+    hipLaunchKernelGGL(k3s_kernel<kNT / 16>, dim3(tiles * S), dim3(256), 0, s, k3);
+    HBK_LAUNCH_CHECK("k3s_kernel");
+    if (flags & HBK_STEP_DEFER_PARTIALS) {
+      p.deferred_ws = ws;
+      p.deferred_ks = S;
+    } else {
+      p.deferred_ws = nullptr;
+      hipLaunchKernelGGL(k3_fold_kernel, dim3(unsigned(std::min<int64_t>((p.n_params + 255) / 256, 1024))), dim3(256),
+                         0, s, make_ranges(p), ws + w.part, w.pstride, S, bucket, p.n_params);
+      HBK_LAUNCH_CHECK("k3_fold_kernel");
+    }
+    return HBK_OK;
+  }
   // k3: job 0 = input layer, then dW_hg of GMLPs 1.., then dW_o of every GMLP
   K3Args k3;
   int nj = 0, blocks = 0;
@@ -2685,6 +3469,16 @@ int mlp_eval_finish(const float* cv, const float* ct, const double* sizes, float
 }
 
 }  // namespace hbk
+
+#ifdef HBK_BOUNDS
+extern "C" int hbk_debug_bounds(unsigned long long* out) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hbk::g_berr), 4 * sizeof(unsigned long long)) != hipSuccess) return -2;
+  unsigned long long z[4] = {};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(hbk::g_berr), z, sizeof(z));
+  return 0;
+}
+#endif
 
 #ifdef HBK_TRACE
 extern "C" int hbk_debug_mlp_trace(unsigned long long* out, int* counts) {

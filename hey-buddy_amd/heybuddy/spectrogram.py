@@ -107,7 +107,19 @@ def current_mel_params() -> MelParams:
     downloaded), else H0."""
     if _PARAMS[0] is None:
         path = find_pretrained(REFERENCE_MEL_FILE, REFERENCE_MEL_SHA256)
-        _PARAMS[0] = mel_params_from_onnx(path) if path is not None else MelParams(_hann_window(), _mel_fbank())
+        params = None
+        if path is not None:
+            # the importer's parity with the real graph is unpinned (the file is not in the
+            # reference tree): a graph it cannot map, or one with other frame geometry, falls
+            # back to H0 with a warning instead of failing every featurize call
+            try:
+                params = mel_params_from_onnx(path)
+                set_mel_parameters(params)
+            except ValueError as e:
+                logger.warning("%s could not be used (%s); using the H0 mel parameters", path, e)
+                params = None
+        if params is None:
+            _PARAMS[0] = MelParams(_hann_window(), _mel_fbank())
     return _PARAMS[0]
 
 

@@ -350,6 +350,93 @@ def _recall(tp: float, n_pos: float) -> float:
     return tp / n_pos if n_pos > 0 else 0.0
 
 
+def _device_pools(it: Any) -> Optional[List[Tuple[torch.Tensor, int, int]]]:
+    """[(rows [n, 1536] f32 / f16 on the device, per-batch count, label)] of a
+    device-pool TrainingDatasetIterator (positives first, as next_batch), or None."""
+    from heybuddy.dataset.training import DevicePool, TrainingDatasetIterator
+    if not isinstance(it, TrainingDatasetIterator):
+        return None
+    try:
+        it._pools()
+    except (TypeError, ValueError):
+        return None
+    out = []
+    for lst, lab in ((it.positive, 1), (it.negative, 0)):
+        for d, n in lst:
+            if not isinstance(d, DevicePool) or d.data.dtype not in (torch.float32, torch.float16):
+                return None
+            out.append((d, int(n), lab))
+    return out
+
+
+class _IndexedEpoch:
+    """train_epoch over a device-pool iterator (the CLI's WakeWordTrainingDatasetIterator):
+    the stage's batches drawn up front as pool indices (each dataset's take_indices(n x S):
+    the rows and order of S next_batch() calls), labels, and the lr / negative-weight
+    schedule on the device; the steps run as train_indexed segments (hipGraphs of 50
+    steps, rows gathered on the device) up to each validation / checkpoint point, and
+    validation / testing iterators become one EvalPasses over their pools. Same rows,
+    same kernels and dropout stream as the per-batch loop (_step); HBK_TRAIN_EAGER=1 keeps
+    the per-batch loop."""
+
+    @classmethod
+    def make(cls, tr: "WakeWordTrainer", training: Any, validation: Any, testing: Any, num_steps: int,
+             threshold: float, act_thr: float, history: torch.Tensor) -> Optional["_IndexedEpoch"]:
+        if not tr._fused or tr.device.type != "cuda" or os.environ.get("HBK_TRAIN_EAGER", "0") == "1":
+            return None
+        dsets = _device_pools(training)
+        if dsets is None:
+            return None
+        if validation is not None and not isinstance(validation, EvalPasses):
+            vd = _device_pools(validation)
+            if vd is None or {lab for _, _, lab in vd} != {0, 1} or validation.max_samples is None:
+                return None
+        if testing is not None:
+            td = _device_pools(testing)
+            if (td is None or {lab for _, _, lab in td} != {0, 1} or testing.max_samples is None
+                    or validation is None or isinstance(validation, EvalPasses)):
+                return None
+        return cls(tr, training, dsets, validation, testing, num_steps, threshold, act_thr, history)
+
+    def __init__(self, tr, training, dsets, validation, testing, num_steps, threshold, act_thr, history):
+        self.tr, self.threshold, self.act_thr, self.history = tr, threshold, act_thr, history
+        dev = tr.device
+        mx = training.max_samples
+        self.S = num_steps if mx is None else min(num_steps, int(mx))
+        p32, p16, off = tr._cat_pools([d.data for d, _, _ in dsets])
+        cols, ys = [], []
+        for d, n, lab in dsets:  # the S batches' rows, dataset by dataset (next_batch's column order)
+            ix = d.take_indices(n * self.S).view(self.S, n).to(torch.int64) + off[id(d.data)]
+            cols.append(ix if d.data.dtype == torch.float32 else -1 - ix)
+            ys.append(torch.full((n,), float(lab), device=dev))
+        training.total_yielded_samples += self.S
+        idx, y = torch.cat(cols, 1), torch.cat(ys)
+        self.batch = int(y.shape[0])
+        rank, world = tr._world()
+        if world > 1:  # distributed.shard_batch's class-stratified slice
+            idx, y = idx[:, rank::world], y[rank::world]
+        self.idx = idx.to(torch.int32).contiguous()
+        self.y = y.contiguous()
+        self.p32, self.p16 = p32, p16
+        self.sched = torch.zeros((max(self.S, 1), 2), dtype=torch.float32, device=dev)
+        self.done = 0
+        self.validation = validation
+        if validation is not None and not isinstance(validation, EvalPasses):
+            self.validation = tr._eval_from_iterators(validation, testing)
+
+    def run_to(self, end: int, lr_hist: List[float], nw_hist: List[float]) -> None:
+        """Steps done .. end - 1 (their lr / negative weights are in the host lists)."""
+        if end <= self.done:
+            return
+        sc = torch.tensor(np.stack([np.asarray(lr_hist[self.done:end], np.float32),
+                                    np.asarray(nw_hist[self.done:end], np.float32)], 1))
+        self.sched[self.done:end].copy_(sc, non_blocking=False)
+        self.tr.train_indexed(self.idx, self.y, self.sched, pool32=self.p32, pool16=self.p16,
+                              threshold=self.threshold, activation_threshold=self.act_thr, history=self.history,
+                              steps_per_graph=50, n_steps=end - self.done, continued=self.done > 0)
+        self.done = end
+
+
 class WakeWordTrainer(Trainer):
     """Trainer for the wake-word classifier (trainer.py:206-1007)."""
 
@@ -668,6 +755,58 @@ class WakeWordTrainer(Trainer):
         g["upd"].replay()
 
     @torch.no_grad()
+    def _cat_pools(self, tensors: List[torch.Tensor]):
+        """(pool32, pool16, {id(tensor): row offset}) for device datasets of both
+        dtypes: each dtype's distinct tensors as [n, 1536] rows, concatenated once and
+        cached (a single tensor of a dtype is used in place)."""
+        key = tuple((id(t), t.data_ptr(), t.shape[0], t.dtype) for t in tensors)
+        cache = getattr(self, "_pool_cache", None)
+        if cache is not None and cache[0] == key:
+            return cache[1]
+        out: List[Optional[torch.Tensor]] = []
+        off: Dict[int, int] = {}
+        for dt in (torch.float32, torch.float16):
+            uniq = list({id(t): t for t in tensors if t.dtype == dt}.values())
+            o = 0
+            for t in uniq:
+                off[id(t)] = o
+                o += int(t.shape[0])
+            rows = [t.reshape(t.shape[0], -1) for t in uniq]
+            out.append(None if not rows else rows[0].contiguous() if len(rows) == 1 else torch.cat(rows).contiguous())
+        res = (out[0], out[1], off)
+        self._pool_cache = (key, res)
+        return res
+
+    def _eval_from_iterators(self, validation: Any, testing: Any) -> "EvalPasses":
+        """EvalPasses over device-pool validation / testing iterators (batches of
+        their per-dataset counts, max_samples batches per pass; several datasets of a
+        side are concatenated once)."""
+        def side(it, label):
+            ds = [(d.data, n) for d, n, lab in _device_pools(it) if lab == label]
+            if not ds:
+                return None, 0
+            rows = [t.reshape(t.shape[0], -1) for t, _ in ds]
+            dt = torch.float16 if all(t.dtype == torch.float16 for t in rows) else torch.float32
+            pool = rows[0].contiguous() if len(rows) == 1 else torch.cat([r.to(dt) for r in rows]).contiguous()
+            return pool, sum(n for _, n in ds)
+        key = (id(validation), id(testing))
+        cache = getattr(self, "_eval_cache", None)
+        if cache is not None and cache[0] == key:
+            return cache[1]
+        vp, npv = side(validation, 1)
+        vn, nnv = side(validation, 0)
+        kw: Dict[str, Any] = {}
+        if testing is not None:
+            tp_, npt = side(testing, 1)
+            ta, nat = side(testing, 0)
+            if tp_ is not None and ta is not None:
+                kw = dict(testing_positive=tp_, testing_adversarial=ta, testing_batch=(npt, nat),
+                          testing_batches=testing.max_samples)
+        ev = EvalPasses(self, vp, vn, validation_batch=(npv, nnv), validation_batches=validation.max_samples,
+                        adjust_ratio=None, seed=random.getrandbits(31), **kw)
+        self._eval_cache = (key, ev)
+        return ev
+
     def _predict_all(self, data: Any) -> Tuple[torch.Tensor, torch.Tensor]:
         preds, labels = [], []
         for datum in data:
@@ -702,6 +841,9 @@ class WakeWordTrainer(Trainer):
         (validation and testing in one device pass each, ``testing`` None)."""
         if use_wandb:
             logger.warning("wandb logging is outside the MI355X hot path; ignored")
+        if isinstance(validation, EvalPasses) and testing is not None:
+            raise ValueError("train_epoch: with an EvalPasses validation the testing pass runs from its "
+                             "testing pools (EvalPasses(..., testing=...)); pass testing=None")
         self._reset_accumulation(salt=random.getrandbits(24))
         cap = getattr(self, "_history", None)
         if cap is None or cap.shape[0] < num_steps or cap.device != self.device:
@@ -718,10 +860,18 @@ class WakeWordTrainer(Trainer):
         t_rec: List[float] = []
         t_fp: List[float] = []
         seed0 = random.getrandbits(31)
-        for step, datum in enumerate(training):
+        # device-pool iterators (the CLI's): the stage as device-sampled indexed steps in
+        # hipGraph segments (train_indexed) between the validation / checkpoint points, the
+        # validation and testing iterators as device evaluation passes (EvalPasses)
+        fast = _IndexedEpoch.make(self, training, validation, testing, num_steps, high_loss_threshold,
+                                  activation_threshold, history)
+        if fast is not None:
+            validation, testing = fast.validation, None
+        for step, datum in enumerate(training) if fast is None else enumerate(range(fast.S)):
             if step >= num_steps:
                 break
-            x, y = datum[0], datum[1]
+            if fast is None:
+                x, y = datum[0], datum[1]
             lr = float(self.get_learning_rate(step, warmup_steps=warmup_steps, hold_steps=hold_steps,
                                               total_steps=num_steps, target_learning_rate=learning_rate))
             lr_hist.append(lr)
@@ -734,8 +884,14 @@ class WakeWordTrainer(Trainer):
             else:
                 nw = float(negative_weight_schedule[step])
             nw_hist.append(nw)
-            batch_sizes.append(int(y.shape[0]))
-            self._step(x, y, lr, nw, high_loss_threshold, activation_threshold, history, seed0 + step)
+            if fast is None:
+                batch_sizes.append(int(y.shape[0]))
+                self._step(x, y, lr, nw, high_loss_threshold, activation_threshold, history, seed0 + step)
+            else:
+                batch_sizes.append(fast.batch)
+                if step > 0 and ((validation is not None and step % validation_steps == 0)
+                                 or step % checkpoint_steps == 0):
+                    fast.run_to(step + 1, lr_hist, nw_hist)
             if step > 0 and step % validation_steps == 0:
                 if isinstance(validation, EvalPasses):
                     # HBM-resident pools: the passes on the device (hbk_mlp_eval_*), one
@@ -799,6 +955,8 @@ class WakeWordTrainer(Trainer):
                     t_acc.append(last_testing_accuracy)
             if step > 0 and step % checkpoint_steps == 0:
                 self.save_checkpoint(f"{name}_{step}")
+        if fast is not None:
+            fast.run_to(len(lr_hist), lr_hist, nw_hist)
         n_steps = len(lr_hist)
         h = history[:n_steps].cpu().numpy().astype(np.float64)
         loss_h, rec_h, fp_h, hlr_h = self._rebuild_histories(h, batch_sizes, last_loss, last_recall,

@@ -250,3 +250,57 @@ def test_narrow_stream_weight_gradients_match(B):
         a, b = gn[k].cpu().numpy(), gw[k].cpu().numpy()
         scale = np.abs(b).max() + 1e-12
         np.testing.assert_allclose(a / scale, b / scale, rtol=0, atol=1e-5, err_msg=k)
+
+
+def test_train_epoch_device_iterator_runs_indexed_and_equals_eager(tmp_path, monkeypatch):
+    """train_epoch over the CLI's device-pool iterators runs the
+    measured path (the stage's rows drawn up front as pool indices, train_indexed
+    hipGraph segments between the validation points, the validation / testing
+    iterators as one EvalPasses each) and gives what the per-batch loop gives
+    (HBK_TRAIN_EAGER=1: x gathered on the host side of the step, _predict_all over
+    the iterators). Dropout off; the validation / testing pools are whole numbers of
+    batches, so both evaluate the same rows. Tolerances as
+    test_train_indexed_equals_eager_steps (the f16 rows' LayerNorm sums run in
+    another order)."""
+    from heybuddy.dataset.training import WakeWordTrainingDatasetIterator
+    from heybuddy import trainer as trm
+    params = gc.golden_inputs()[0]
+    rng = np.random.default_rng(8)
+    dev = torch.device("cuda")
+    pos = torch.from_numpy(rng.standard_normal((300, 16, 96)).astype(np.float32) + 0.7).to(dev)
+    adv = torch.from_numpy(rng.standard_normal((300, 16, 96)).astype(np.float32) - 0.2).to(dev)
+    neg = torch.from_numpy(rng.standard_normal((2000, 16, 96)).astype(np.float32)).half().to(dev)
+    vpos = torch.from_numpy(rng.standard_normal((100, 16, 96)).astype(np.float32) + 0.4).to(dev)
+    vneg = torch.from_numpy(rng.standard_normal((400, 16, 96)).astype(np.float32)).half().to(dev)
+    tpos = torch.from_numpy(rng.standard_normal((60, 16, 96)).astype(np.float32) + 0.4).to(dev)
+    tadv = torch.from_numpy(rng.standard_normal((60, 16, 96)).astype(np.float32) - 0.1).to(dev)
+    runs = {}
+    for mode in ("fast", "eager"):
+        monkeypatch.setenv("HBK_TRAIN_EAGER", "1" if mode == "eager" else "0")
+        tr = trm.WakeWordTrainer(checkpoint_dir=str(tmp_path / mode), device="cuda")
+        tr.model.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=True)
+        tr.model.dropout.p = 0.0
+        training = WakeWordTrainingDatasetIterator(positive=[(pos, 20)], negative=[(adv, 20), (neg, 100)],
+                                                   device=dev, seed=5)
+        val = WakeWordTrainingDatasetIterator(positive=[(vpos, 50)], negative=[(vneg, 200)], device=dev, seed=6,
+                                              max_samples=2)
+        tst = WakeWordTrainingDatasetIterator(positive=[(tpos, 20)], negative=[(tadv, 20)], device=dev, seed=7,
+                                              max_samples=3)
+        called = []
+        orig = trm.WakeWordTrainer.train_indexed
+        monkeypatch.setattr(trm.WakeWordTrainer, "train_indexed",
+                            lambda self, *a, **k: (called.append(k.get("n_steps")), orig(self, *a, **k))[1])
+        h = tr.train_epoch(training, validation=val, testing=tst, num_steps=13, warmup_steps=3, hold_steps=3,
+                           validation_steps=5, checkpoint_steps=1000, negative_weight_schedule=2.0,
+                           negative_weight_adjust_ratio=2.0, target_false_positive_rate=1e6)
+        torch.cuda.synchronize()
+        runs[mode] = (h, tr.model.flat_parameters.clone(), called)
+    (hf, pf, cf), (he, pe, ce) = runs["fast"], runs["eager"]
+    assert cf == [6, 5, 2] and ce == []  # segments up to the validations after steps 5 and 10, then the rest
+    for i in (0, 1):  # lr, negative weight
+        np.testing.assert_allclose(hf[i].numpy(), he[i].numpy(), rtol=1e-6)
+    np.testing.assert_allclose(hf[2].numpy(), he[2].numpy(), rtol=2e-4)  # loss
+    for i in (6, 7, 8, 9, 10):  # validation fp/h, recall; testing accuracy, recall, fp rate
+        np.testing.assert_allclose(hf[i].numpy(), he[i].numpy(), rtol=1e-5, atol=1e-5)
+    d = (pf - pe).abs()
+    assert float((d > 1e-5).float().mean()) < 1e-3 and float(d.max()) <= 2e-2
