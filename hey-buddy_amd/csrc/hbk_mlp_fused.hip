@@ -602,6 +602,20 @@ template <int KC>
 constexpr int k1c_rt_max() {
   return 16 * (KC + 16) * 4 * 9 <= 150 * 1024 ? 9 : (150 * 1024) / (16 * (KC + 16) * 4);
 }
+// A load through a pointer the compiler cannot trace to a kernel argument (a row address
+// read from memory) is emitted as a FLAT load, which counts in both vmcnt and lgkmcnt and
+// is waited for with vmcnt(0) lgkmcnt(0) -- it serialised k3s's gathers. ldg: the same
+// load in the global address space.
+typedef uint32_t u4v_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ldg(const uint4* p) {
+  typedef const __attribute__((address_space(1))) u4v_t* gp_t;
+  const u4v_t v = *(gp_t)(uintptr_t)p;
+  return uint4{v.x, v.y, v.z, v.w};
+}
+__device__ __forceinline__ uint32_t ldg(const uint32_t* p) {
+  typedef const __attribute__((address_space(1))) uint32_t* gp_t;
+  return *(gp_t)(uintptr_t)p;
+}
 // a row's first byte and dtype from k1s's row information (bit 0 of the address: f16)
 __device__ __forceinline__ const char* row_addr(const uint4& inf, bool& is16) {
   const uint64_t ad = static_cast<uint64_t>(inf.z) | (static_cast<uint64_t>(inf.w) << 32);
@@ -654,8 +668,8 @@ __global__ void __launch_bounds__(512) k1c_kernel(K1cArgs a) {
     bool is16;
     const char* base = row_addr(info[j], is16);
     const char* p = base + (static_cast<int64_t>(k0 + 8 * c8) << (is16 ? 1 : 2));
-    lo[j] = *BCK(reinterpret_cast<const uint4*>(p), 16);
-    hi[j] = *BCK(reinterpret_cast<const uint4*>(p + (is16 ? 0 : 16)), 16);
+    lo[j] = ldg(BCK(reinterpret_cast<const uint4*>(p), 16));
+    hi[j] = ldg(BCK(reinterpret_cast<const uint4*>(p + (is16 ? 0 : 16)), 16));
   }
   if (tid < KC) {
     gb[0][tid] = gv;
@@ -1696,6 +1710,9 @@ struct K3sArgs {
   float* part;  // [S][pstride]
   int64_t pstride;
 };
+// XOR swizzle of the 16-B chunks of a 256-B row (the input layer's [32][128] images):
+// conflict-free ds_write_b128 of whole chunks and ds_read_b64_tr_b16 of the B operand
+__device__ __forceinline__ int k3s_swz(int row, int ch) { return ch ^ (((row & 3) << 2) | ((row >> 2) & 3)); }
 template <int NBT>
 struct K3sShared {
   static constexpr int NT = 16 * NBT, kLdY = 48;  // LDS column: 32 rows + 16 pad halves (conflict-free b128 reads)
@@ -1705,20 +1722,23 @@ struct K3sShared {
   uint4 rinfoS[kK3sMaxR];                          // input layer: the split's rows' {mu, rs, address}
   uint32_t maskS[kK3sMaxR * (NT / 32)];            // ... and their mask words of this N tile
 };
-// one workgroup's tile; kRaw: the input layer (X from the pool rows). Straight-line steady
-// state: the prefetches are unconditional (clamped to the last step: a redundant reload at
-// the tail), so the counted vmcnt waits stay exact across the loop
-template <int NBT, bool kRaw>
+// one workgroup's tile; kRaw: the input layer (X from the pool rows). NST steps of 32 rows,
+// fully unrolled, the prefetches unconditional (clamped to the last step: a redundant
+// reload at the tail): straight-line code, so the compiler's vmcnt waits are exact (a
+// rolled loop made it wait vmcnt(0) at the top of every step, i.e. for the loads issued
+// one step earlier: 8 k cycles per step). A split shorter than NST steps (the last)
+// computes zero rows in its tail steps.
+template <int NBT, bool kRaw, int NST>
 __device__ __forceinline__ void k3s_body(const K3sArgs& a, const K3sJob& jb, int split, int tm, int tnn,
                                          K3sShared<NBT>& sh) {
   constexpr int NT = 16 * NBT, kLdY = K3sShared<NBT>::kLdY;
   constexpr int kYU = NT * 8 / 256;  // float4 units per thread and step (transposed X)
-  constexpr int kRPT = NT / 8;       // pool rows per thread and step (input layer)
-  static_assert(NT >= 64 && 256 % NT == 0, "a wave's lanes are 64 consecutive columns of one row group");
+  static_assert(!kRaw || NT == 128, "the input layer's image is [32][128] halves (the swizzle's 256-B rows)");
+  static_assert(K3sShared<NBT>::kLdY * NT >= 32 * NT, "an input-layer image fits a buffer plane");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = lane & 15, kq = lane >> 4;
   const int Bp = static_cast<int>(a.Bp);
   const int rb0 = split * a.R;
-  const int nst = (min(a.R, Bp - rb0) + 31) / 32;  // 32-row steps of this split (>= 1)
+  constexpr int nst = NST;
   const int n0 = tnn * NT;
   const int nb = min(NBT, (jb.N - n0 + 15) / 16);  // live 16-column tiles (uniform)
   const int mrow = tm * 128 + 32 * wave;
@@ -1742,7 +1762,6 @@ __device__ __forceinline__ void k3s_body(const K3sArgs& a, const K3sJob& jb, int
       d[1][h] = *BCK(reinterpret_cast<const f4*>(X1 + b + 4 * h), 16);
     }
   };
-  const int rc = tid % NT, rg = __builtin_amdgcn_readfirstlane(tid / NT);  // input layer: column, row group
   if constexpr (kRaw) {  // the split's row information and mask words (rows past B: row B - 1's, zeroed below)
     // (unrolled, every load unconditional at a clamped row: all in flight together)
     const int nr = 32 * nst;
@@ -1767,23 +1786,30 @@ __device__ __forceinline__ void k3s_body(const K3sArgs& a, const K3sJob& jb, int
   }
   HBK_MT(2, 3);
   // activation chunk of step u into registers ...
-  f4 yv[kRaw ? 1 : kYU];
-  uint32_t yw[kRaw ? kRPT : 1];
+  // (input layer: thread -> 16-B chunks q = tid + 256 j of the step's [32 rows][NT] image, row
+  // q / (NT / 8), columns 8 (q % (NT / 8)) ..: the pool rows as they lie, 16 / 32 B per chunk)
+  constexpr int kCPR = NT / 8, kCPT = 32 * kCPR / 256;  // chunks per row, per thread
+  // two register sets: step v's loads are issued at step v - 3 and converted at step v - 1
+  f4 yv[2][kRaw ? 1 : kYU];
+  uint4 ylo[2][kRaw ? kCPT : 1], yhi[2][kRaw ? kCPT : 1];
   auto load_y = [&](int u) {
+    const int ys_ = u & 1;
     if constexpr (kRaw) {
-      const int col = n0 + rc;
 #pragma unroll
-      for (int i = 0; i < kRPT; ++i) {
+      for (int j = 0; j < kCPT; ++j) {
+        const int q = tid + 256 * j, row = q / kCPR, ch = q % kCPR;
         bool is16;
-        const char* base = row_addr(sh.rinfoS[32 * u + kRPT * rg + i], is16);
-        yw[i] = *BCK(reinterpret_cast<const uint32_t*>(base + ((static_cast<int64_t>(col) << (is16 ? 1 : 2)) & ~int64_t(3))), 4);
+        const char* base = row_addr(sh.rinfoS[32 * u + row], is16);
+        const char* p = base + (static_cast<int64_t>(n0 + 8 * ch) << (is16 ? 1 : 2));
+        ylo[ys_][j] = ldg(BCK(reinterpret_cast<const uint4*>(p), 16));
+        yhi[ys_][j] = ldg(BCK(reinterpret_cast<const uint4*>(p + (is16 ? 0 : 16)), 16));
       }
     } else {
 #pragma unroll
       for (int jj = 0; jj < kYU; ++jj) {
         const int q = tid + 256 * jj, col = min(n0 + (q >> 3), jb.N - 1);
         const int b = min(rb0 + 32 * u + 4 * (q & 7), Bp - 4);
-        yv[jj] = *BCK(reinterpret_cast<const f4*>(jb.Y + static_cast<int64_t>(col) * Bp + b), 16);
+        yv[ys_][jj] = *BCK(reinterpret_cast<const f4*>(jb.Y + static_cast<int64_t>(col) * Bp + b), 16);
       }
     }
   };
@@ -1791,33 +1817,40 @@ __device__ __forceinline__ void k3s_body(const K3sArgs& a, const K3sJob& jb, int
   auto write_y = [&](int u, int buf) {
     _Float16* yh = &sh.ys[buf][0][0];
     _Float16* yl = &sh.ys[buf][1][0];
+    const int ys_ = u & 1;
     if constexpr (kRaw) {
-      const int col = n0 + rc;
-      float xs[kRPT];
+      // xhat = (v - mu) rs of the chunk's 8 elements, split, into the row-major hi / lo images
+      // ([32][NT] halves, 16-B chunks XOR-swizzled: conflict-free b128 writes and tr reads)
 #pragma unroll
-      for (int i = 0; i < kRPT; ++i) {
-        const int rl = 32 * u + kRPT * rg + i;
+      for (int j = 0; j < kCPT; ++j) {
+        const int q = tid + 256 * j, row = q / kCPR, ch = q % kCPR, rl = 32 * u + row;
         const uint4 inf = sh.rinfoS[rl];
         const bool is16 = (inf.z & 1u) != 0;
-        const float x = is16 ? static_cast<float>(__builtin_bit_cast(
-                                   _Float16, static_cast<uint16_t>((col & 1) ? yw[i] >> 16 : yw[i])))
-                             : __builtin_bit_cast(float, yw[i]);
-        const uint32_t mwd = sh.maskS[rl * (NT / 32) + (rc >> 5)];
-        const float v = (mwd >> (col & 31)) & 1u ? 0.f : x * a.keep;
-        xs[i] = rb0 + rl < a.B ? (v - __uint_as_float(inf.x)) * __uint_as_float(inf.y) : 0.f;
-      }
+        const uint32_t bits = sh.maskS[rl * (NT / 32) + (ch >> 2)] >> (8 * (ch & 3));
+        const float mu = __uint_as_float(inf.x), rs = rb0 + rl < a.B ? __uint_as_float(inf.y) : 0.f;
+        const uint4 lo = ylo[ys_][j], hi = yhi[ys_][j];
+        const uint32_t hw[4] = {lo.x, lo.y, lo.z, lo.w};
+        const uint32_t fw[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        float xs[8];
 #pragma unroll
-      for (int i = 0; i < kRPT; i += 8) {
+        for (int e = 0; e < 8; ++e) {
+          const float x = is16 ? static_cast<float>(__builtin_bit_cast(
+                                     _Float16, static_cast<uint16_t>((e & 1) ? hw[e >> 1] >> 16 : hw[e >> 1])))
+                               : __builtin_bit_cast(float, fw[e]);
+          const float v = (bits >> e) & 1u ? 0.f : x * a.keep;
+          xs[e] = (v - mu) * rs;  // (rows past B: rs = 0 and a finite v -> 0)
+        }
         h8 hv, lv;
-        split8(f4{xs[i], xs[i + 1], xs[i + 2], xs[i + 3]}, f4{xs[i + 4], xs[i + 5], xs[i + 6], xs[i + 7]}, hv, lv);
-        *reinterpret_cast<h8*>(yh + rc * kLdY + kRPT * rg + i) = hv;
-        *reinterpret_cast<h8*>(yl + rc * kLdY + kRPT * rg + i) = lv;
+        split8(f4{xs[0], xs[1], xs[2], xs[3]}, f4{xs[4], xs[5], xs[6], xs[7]}, hv, lv);
+        const int off = row * NT + 8 * k3s_swz(row, ch);
+        *reinterpret_cast<h8*>(yh + off) = hv;
+        *reinterpret_cast<h8*>(yl + off) = lv;
       }
     } else {
 #pragma unroll
       for (int jj = 0; jj < kYU; ++jj) {
         const int q = tid + 256 * jj, col = q >> 3, b4 = 4 * (q & 7);
-        const f4 v = rb0 + 32 * u + b4 < Bp ? yv[jj] : f4{0.f, 0.f, 0.f, 0.f};
+        const f4 v = rb0 + 32 * u + b4 < Bp ? yv[ys_][jj] : f4{0.f, 0.f, 0.f, 0.f};
         uint32_t h0, l0, h1, l1;
         split_pair(v[0], v[1], h0, l0);
         split_pair(v[2], v[3], h1, l1);
@@ -1833,14 +1866,16 @@ __device__ __forceinline__ void k3s_body(const K3sArgs& a, const K3sJob& jb, int
 #pragma unroll
     for (int nt = 0; nt < NBT; ++nt) acc[t][nt] = z;
   f4 ssum[2] = {z, z};
-  f4 ga[2][2][2];  // gradient ring: [slot][tile][half]
-  // prologue: step 0 staged, steps 0 / 1 of the gradient and step 1 of X in flight
-  const int last = nst - 1;
+  f4 ga[3][2][2];  // gradient ring: [slot][tile][half], step v in slot v % 3
+  // prologue: step 0 staged; steps 1, 2 of X and 0, 1, 2 of the gradient in flight
+  constexpr int last = NST - 1;
   load_y(0);
   load_g(0, ga[0]);
   write_y(0, 0);
   load_y(min(1, last));
   load_g(min(1, last), ga[1]);
+  load_y(min(2, last));
+  load_g(min(2, last), ga[2]);
   __syncthreads();
   HBK_MT(2, 4);
   auto step = [&](int u, f4 (&g)[2][2]) {
@@ -1858,23 +1893,46 @@ __device__ __forceinline__ void k3s_body(const K3sArgs& a, const K3sJob& jb, int
 #pragma unroll
     for (int nt = 0; nt < NBT; ++nt)
       if (nt < nb) {
-        const h8 bh = *reinterpret_cast<const h8*>(yh + (16 * nt + m) * kLdY + 8 * kq);
-        const h8 bl = *reinterpret_cast<const h8*>(yl + (16 * nt + m) * kLdY + 8 * kq);
+        h8 bh, bl;
+        if constexpr (kRaw) {
+          // rows 8 kq .. 8 kq + 7 of column 16 nt + m, by two transposed reads (rows 8 kq + q
+          // and 8 kq + 4 + q supplied by lane 4 q + p of the 16-lane group, columns 16 nt + 4 p ..)
+          const int qq = (lane & 15) >> 2, pp = lane & 3;
+          const int r0 = 8 * kq + qq, r1 = r0 + 4, c2 = 2 * nt + (pp >> 1);
+          const int o0 = r0 * NT + 8 * k3s_swz(r0, c2) + 4 * (pp & 1);
+          const int o1 = r1 * NT + 8 * k3s_swz(r1, c2) + 4 * (pp & 1);
+          typedef __fp16 hv4 __attribute__((__vector_size__(4 * sizeof(__fp16))));
+          typedef __attribute__((address_space(3))) hv4* lp_t;
+          const hv4 h0 = __builtin_amdgcn_ds_read_tr16_b64_v4f16((lp_t)const_cast<_Float16*>(yh + o0));
+          const hv4 h1 = __builtin_amdgcn_ds_read_tr16_b64_v4f16((lp_t)const_cast<_Float16*>(yh + o1));
+          const hv4 l0 = __builtin_amdgcn_ds_read_tr16_b64_v4f16((lp_t)const_cast<_Float16*>(yl + o0));
+          const hv4 l1 = __builtin_amdgcn_ds_read_tr16_b64_v4f16((lp_t)const_cast<_Float16*>(yl + o1));
+          typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+          typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+          const u2v h0b = __builtin_bit_cast(u2v, h0), h1b = __builtin_bit_cast(u2v, h1);
+          const u2v l0b = __builtin_bit_cast(u2v, l0), l1b = __builtin_bit_cast(u2v, l1);
+          bh = __builtin_bit_cast(h8, u4v{h0b.x, h0b.y, h1b.x, h1b.y});
+          bl = __builtin_bit_cast(h8, u4v{l0b.x, l0b.y, l1b.x, l1b.y});
+        } else {
+          bh = *reinterpret_cast<const h8*>(yh + (16 * nt + m) * kLdY + 8 * kq);
+          bl = *reinterpret_cast<const h8*>(yl + (16 * nt + m) * kLdY + 8 * kq);
+        }
         acc[0][nt] = mma3(ah[0], al[0], bh, bl, acc[0][nt]);
         acc[1][nt] = mma3(ah[1], al[1], bh, bl, acc[1][nt]);
       }
     // step u + 1's X into the other buffer (read by nobody now: the barrier that ended step
     // u - 1 passed), then step u + 2's loads (clamped: past the end they reload the last step)
+    if (u < 4) HBK_MT(2, 40 + 3 * u);
     write_y(min(u + 1, last), (u + 1) & 1);
-    load_y(min(u + 2, last));
-    load_g(min(u + 2, last), g);
-    lds_barrier();  // (LDS only: step u + 2's loads stay in flight)
+    if (u < 4) HBK_MT(2, 41 + 3 * u);
+    load_y(min(u + 3, last));
+    load_g(min(u + 3, last), g);
+    if (u < 4) HBK_MT(2, 42 + 3 * u);
+    lds_barrier();  // (LDS only: step u + 2's and u + 3's loads stay in flight)
     HBK_MT(2, 16 + u);
   };
-  for (int u = 0; u < nst; u += 2) {
-    step(u, ga[0]);
-    if (u + 1 < nst) step(u + 1, ga[1]);
-  }
+#pragma unroll
+  for (int u = 0; u < NST; ++u) step(u, ga[u % 3]);
   HBK_MT(2, 2);
   float* const C = a.part + split * a.pstride + jb.c_off;
   if constexpr (!kRaw) {
@@ -1941,7 +1999,7 @@ __device__ __forceinline__ void k3s_body(const K3sArgs& a, const K3sJob& jb, int
     }
   }
 }
-template <int NBT>
+template <int NBT, int NST>
 __global__ void __launch_bounds__(256) k3s_kernel(K3sArgs a) {
   __shared__ __attribute__((aligned(16))) K3sShared<NBT> sh;
   const int blk = blockIdx.x;
@@ -1953,9 +2011,9 @@ __global__ void __launch_bounds__(256) k3s_kernel(K3sArgs a) {
   const int tm = tile / jb.tn, tnn = tile - tm * jb.tn;
   HBK_MT(2, 1);
   if (jb.Y == nullptr)
-    k3s_body<NBT, true>(a, jb, split, tm, tnn, sh);
+    k3s_body<NBT, true, NST>(a, jb, split, tm, tnn, sh);
   else
-    k3s_body<NBT, false>(a, jb, split, tm, tnn, sh);
+    k3s_body<NBT, false, NST>(a, jb, split, tm, tnn, sh);
 }
 
 // Steps whose update does not get the workspace (or is preceded by the
@@ -2892,15 +2950,17 @@ K1cGeom k1c_geom(int B, const void* stream) {
   }
   return best;
 }
-// k3s's batch split: about CUs / (the launch's tiles) splits, 128 .. 512 rows each (HBK_K3_R overrides)
-int k3s_rows(int64_t Bp, int tiles, const void* stream) {
+// k3s's batch split: about CUs / (the launch's tiles) splits, of 32 NST rows with NST one of
+// the compiled step counts 4, 8, 12, 16 (128 .. 512 rows; HBK_K3_R overrides the rows)
+int k3s_steps(int64_t Bp, int tiles, const void* stream) {
   const int cus = static_cast<int>(std::max<int64_t>(1, persistent_blocks(1, stream)));
   int R = env_int("HBK_K3_R", 0);
   if (R <= 0) {
     const int S = std::max(1, cus / std::max(1, tiles));
-    R = static_cast<int>((Bp + S - 1) / S + 31) / 32 * 32;
+    R = static_cast<int>((Bp + S - 1) / S);
   }
-  return std::max(128, std::min(kK3sMaxR, R / 32 * 32));
+  const int nst = (R + 31) / 32;
+  return nst <= 4 ? 4 : nst <= 8 ? 8 : nst <= 12 ? 12 : 16;
 }
 
 void fill_k2(const hbk_mlp_plan& p, K2Args& k) {
@@ -3183,7 +3243,7 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
       add(ws + w.dHG + int64_t(k) * kH2 * Bp, ws + w.Xn + int64_t(k) * kL * Bp, p.g[k].w_hg, kL, kH2, kL, k);
     for (int k = 0; k < NG; ++k)
       add(ws + w.dS + int64_t(k) * kL * Bp, ws + w.U + int64_t(k) * kH * Bp, p.g[k].w_o, kH, p.g[k].out, kH, NG + k);
-    const int R = k3s_rows(Bp, tiles, s);
+    const int NST = k3s_steps(Bp, tiles, s), R = 32 * NST;
     const int S = static_cast<int>((Bp + R - 1) / R);
     for (int i = 0; i < nj; ++i) k3.start[i] *= S;
     k3.start[nj] = tiles * S;
@@ -3206,7 +3266,13 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
     k3.b_off = p.ln_in.b;
     k3.part = ws + w.part;
     k3.pstride = w.pstride;
-    hipLaunchKernelGGL(k3s_kernel<kNT / 16>, dim3(tiles * S), dim3(256), 0, s, k3);
+    auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(tiles * S), dim3(256), 0, s, k3); };
+    switch (NST) {
+      case 4: launch(k3s_kernel<kNT / 16, 4>); break;
+      case 8: launch(k3s_kernel<kNT / 16, 8>); break;
+      case 12: launch(k3s_kernel<kNT / 16, 12>); break;
+      default: launch(k3s_kernel<kNT / 16, 16>);
+    }
     HBK_LAUNCH_CHECK("k3s_kernel");
     if (flags & HBK_STEP_DEFER_PARTIALS) {
       p.deferred_ws = ws;
