@@ -140,6 +140,9 @@ def se20_graph(seed: int = 1234) -> Graph:
 
 # -- ONNX (Keras / tf2onnx layout) ---------------------------------------------------
 _TO_NCHW = (0, 3, 1, 2)
+# integer shape arithmetic a Reshape's computed target may come from
+_SHAPE_OPS = ("Shape", "Gather", "Slice", "Unsqueeze", "Squeeze", "Concat", "Cast", "Mul", "Div", "Add", "Sub",
+              "ReduceProd", "Identity")
 _TO_NHWC = (0, 2, 3, 1)
 
 
@@ -188,9 +191,14 @@ def from_onnx(path: str, name: Optional[str] = None) -> Graph:
     speech-embedding.js:125-146). The graph must be one chain from the input:
     layout Transposes (NHWC <-> NCHW), Conv (stride 1, dilation 1, group 1, no
     padding) with its bias as the Conv's third input or a following Add of a
-    [C] / [1, C, 1, 1] constant, LeakyRelu / Relu after a conv, MaxPool (kernel
-    = stride, no padding), and trailing Reshape / Squeeze / Flatten / Identity
-    to the output. Anything else raises ValueError naming the node."""
+    [C] / [1, C, 1, 1] constant, per-channel Mul / Add (a BatchNorm folded by
+    the exporter) and BatchNormalization (inference form) after a conv --
+    folded into its weights and bias --, LeakyRelu / Relu after a conv, MaxPool
+    (kernel = stride, no padding), and trailing Reshape / Squeeze / Flatten /
+    Identity to the output. A Reshape's target shape may be computed (tf2onnx's
+    Shape -> Gather / Slice -> Unsqueeze -> Concat subgraphs): side consumers of
+    a chain tensor are allowed when they only feed such shape arithmetic ending
+    in a Reshape's shape input. Anything else raises ValueError naming the node."""
     from heybuddy.util.onnx_util import read_model
     m = read_model(path)
     if len(m.inputs) != 1 or len(m.outputs) != 1:
@@ -212,11 +220,44 @@ def from_onnx(path: str, name: Optional[str] = None) -> Graph:
             raise ValueError(f"{path}: {name_!r} must be a constant (initializer) for the HIP kernels")
         return np.asarray(inits[name_], dtype=np.float32)
 
+    def shape_only(node, seen=None) -> bool:
+        """node (a Shape of a chain tensor) and everything downstream only compute a
+        Reshape's target shape (integer shape arithmetic, no data)."""
+        seen = set() if seen is None else seen
+        if node.name in seen:
+            return True
+        seen.add(node.name)
+        if node.op not in _SHAPE_OPS:
+            return False
+        for t in node.outputs:
+            for u in m.consumers(t):
+                if u.op == "Reshape" and len(u.inputs) > 1 and u.inputs[1] == t and u.inputs[0] != t:
+                    continue
+                if not shape_only(u, seen):
+                    return False
+        return True
+
+    def channel_vec(b: np.ndarray, cout: int, where: str) -> np.ndarray:
+        """A per-channel constant of a conv's output ([C], [1, C, 1, 1] in NCHW,
+        [.., C] in NHWC, or a scalar) as [C]."""
+        ok = (b.size == 1 or (b.size == cout and (b.ndim == 1 or (nchw and b.shape[-3:] == (cout, 1, 1))
+                                                   or (not nchw and b.shape[-1] == cout))))
+        if not ok:
+            raise ValueError(f"{where}: constant of shape {b.shape} does not broadcast over {cout} channels")
+        return np.broadcast_to(b.reshape(-1), (cout,)).astype(np.float32)
+
+    def conv_before(where: str, what: str) -> "Conv":
+        prev = ops[-1] if ops else None
+        if not isinstance(prev, Conv) or prev.act is not None:
+            raise ValueError(f"{where}: {what} is supported only right after a conv (before its activation)")
+        return prev
+
     while x != out_name:
         users = m.consumers(x)
-        if len(users) != 1:
-            raise ValueError(f"{path}: tensor {x!r} feeds {len(users)} nodes; only a single chain is supported")
-        node = users[0]
+        data = [u for u in users if not (u.op == "Shape" and shape_only(u))]
+        if len(data) != 1:
+            raise ValueError(f"{path}: tensor {x!r} feeds {len(data)} nodes; only a single chain is supported")
+        node = data[0]
         a = node.attrs
         where = f"{path}: node {node.name!r} ({node.op})"
         if terminal and node.op not in ("Reshape", "Squeeze", "Flatten", "Identity"):
@@ -244,21 +285,29 @@ def from_onnx(path: str, name: Optional[str] = None) -> Graph:
             b = const(node.inputs[2]).reshape(-1) if len(node.inputs) > 2 and node.inputs[2] else np.zeros(co, np.float32)
             ops.append(Conv(kh, kw, ci, co, w.transpose(2, 3, 1, 0), b, act=None,
                             name=(node.name.split("/")[0] or f"conv2d_{len(ops)}")))
-        elif node.op == "Add":
-            prev = ops[-1] if ops else None
-            if not isinstance(prev, Conv) or prev.act is not None:
-                raise ValueError(f"{where}: an Add is supported only as a conv's bias")
+        elif node.op in ("Add", "Sub"):
+            prev = conv_before(where, f"an {node.op} of a per-channel constant")
+            if node.op == "Sub" and node.inputs[0] != x:
+                raise ValueError(f"{where}: only x - constant is supported")
             other = node.inputs[1] if node.inputs[0] == x else node.inputs[0]
-            b = const(other)
-            ok = (b.size == prev.cout and (b.ndim == 1 or (nchw and b.shape[-3:] == (prev.cout, 1, 1))
-                                           or (not nchw and b.shape[-1] == prev.cout)))
-            if not ok:
-                raise ValueError(f"{where}: bias of shape {b.shape} does not broadcast over {prev.cout} channels")
-            prev.bias = np.ascontiguousarray(prev.bias + b.reshape(-1), dtype=np.float32)
+            b = channel_vec(const(other), prev.cout, where)
+            prev.bias = np.ascontiguousarray(prev.bias + (b if node.op == "Add" else -b), dtype=np.float32)
+        elif node.op == "Mul":  # a per-channel scale (BatchNorm folded as Mul / Add): into W and b
+            prev = conv_before(where, "a Mul by a per-channel constant")
+            other = node.inputs[1] if node.inputs[0] == x else node.inputs[0]
+            sc = channel_vec(const(other), prev.cout, where)
+            prev.weight = np.ascontiguousarray(prev.weight * sc, dtype=np.float32)
+            prev.bias = np.ascontiguousarray(prev.bias * sc, dtype=np.float32)
+        elif node.op == "BatchNormalization":  # inference form: y = (x - mean) / sqrt(var + eps) * g + b
+            prev = conv_before(where, "a BatchNormalization")
+            if not nchw or len(node.outputs) > 1 and any(node.outputs[1:]) or int(a.get("training_mode", 0)):
+                raise ValueError(f"{where}: only the inference form over NCHW channels is supported")
+            g_, b_, mu, var = (channel_vec(const(t), prev.cout, where) for t in node.inputs[1:5])
+            sc = (g_.astype(np.float64) / np.sqrt(var.astype(np.float64) + float(a.get("epsilon", 1e-5))))
+            prev.weight = np.ascontiguousarray(prev.weight * sc, dtype=np.float32)
+            prev.bias = np.ascontiguousarray((prev.bias - mu) * sc + b_, dtype=np.float32)
         elif node.op in ("LeakyRelu", "Relu"):
-            prev = ops[-1] if ops else None
-            if not isinstance(prev, Conv) or prev.act is not None:
-                raise ValueError(f"{where}: an activation is supported only right after a conv (+ bias)")
+            prev = conv_before(where, "an activation")
             prev.act = "leaky_relu"
             prev.alpha = float(np.float32(a.get("alpha", 0.01))) if node.op == "LeakyRelu" else 0.0
         elif node.op == "MaxPool":

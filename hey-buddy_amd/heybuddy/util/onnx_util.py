@@ -353,7 +353,7 @@ def _node(op: str, name: str, ins: Sequence[str], outs: Sequence[str], attrs: Se
 
 
 def _initializer(name: str, arr: np.ndarray) -> bytes:
-    arr = np.ascontiguousarray(arr)
+    arr = np.asarray(arr, order="C")  # (not ascontiguousarray: it makes a 0-d scalar 1-d)
     body = b"".join(_f_varint(1, d) for d in arr.shape) + _f_varint(2, _NP2ONNX[arr.dtype])
     body += _f_str(8, name) + _f_bytes(9, arr.astype(arr.dtype.newbyteorder("<")).tobytes())
     return _f_bytes(5, body)

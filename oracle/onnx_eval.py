@@ -10,7 +10,8 @@ which is not installed here. Only tests/ import it; the product never does.
 Operators: Transpose, Conv (1-D / 2-D, pads, strides, group 1), LeakyRelu,
 Relu, MaxPool, Reshape, Squeeze, Unsqueeze, Flatten, Identity, Cast, Add, Sub,
 Mul, Div, Pow, Max, Min, Sqrt, Abs, Log, Exp, Neg, Clip, MatMul, ReduceSum,
-Concat, Slice, STFT.
+Concat, Slice, STFT, and the shape / normalisation ops of tf2onnx exports:
+Shape, Gather, ReduceProd, BatchNormalization (inference form).
 """
 from __future__ import annotations
 
@@ -152,6 +153,17 @@ def run(model, feeds: Dict[str, np.ndarray], outputs: Sequence[str] = ()) -> Dic
             y = _slice(node, vals, x)
         elif op == "STFT":
             y = _stft(node, vals)
+        elif op == "Shape":
+            shp = np.asarray(x.shape, np.int64)
+            y = shp[int(a.get("start", 0)):a.get("end", None)]
+        elif op == "Gather":
+            y = np.take(x, np.asarray(ins[1]).astype(np.int64), axis=int(a.get("axis", 0)))
+        elif op == "ReduceProd":
+            y = np.asarray(np.prod(x), dtype=x.dtype).reshape([1] * x.ndim if int(a.get("keepdims", 1)) else [])
+        elif op == "BatchNormalization":  # inference form over axis 1
+            c = (1, -1) + (1,) * (x.ndim - 2)
+            g_, b_, mu, var = (np.asarray(v, np.float64).reshape(c) for v in ins[1:5])
+            y = (x - mu) / np.sqrt(var + float(a.get("epsilon", 1e-5))) * g_ + b_
         else:
             raise NotImplementedError(f"onnx_eval: operator {op}")
         vals[node.outputs[0]] = y

@@ -134,6 +134,92 @@ def test_embedding_graph_keras_variants(tmp_path, relu):
     np.testing.assert_allclose(got, oembed.run_graph(h, x), rtol=1e-9, atol=1e-12)
 
 
+def _write_tf2onnx_variant(path, g, seed=0):
+    """SE20 as tf2onnx exports a Keras model with BatchNorm layers: conv weights
+    pre-scaled, each BatchNorm either folded by the exporter into a per-channel
+    Mul + Add ([1, C, 1, 1]) after a bias-less Conv or left as a
+    BatchNormalization node, and the final Reshape's target computed from the
+    tensor's own Shape (Shape -> Gather -> Unsqueeze -> Concat)."""
+    from heybuddy.embedding_graph import Conv
+    from heybuddy.util.onnx_util import write_model
+    rng = np.random.default_rng(seed)
+    nodes, inits = [("Transpose", "t_in", ["input_1"], ["x0"], {"perm": [0, 3, 1, 2]})], {}
+    x = "x0"
+    for i, op in enumerate(g.ops):
+        if not isinstance(op, Conv):
+            nodes.append(("MaxPool", f"pool{i}", [x], [f"p{i}"], {"kernel_shape": [op.ph, op.pw],
+                                                                  "strides": [op.ph, op.pw]}))
+            x = f"p{i}"
+            continue
+        inits[f"w{i}"] = np.ascontiguousarray(op.weight.transpose(3, 2, 0, 1))
+        c = op.cout
+        if i % 2 == 0:  # folded: Conv (no bias) -> Mul s -> Add t
+            nodes.append(("Conv", f"conv{i}", [x, f"w{i}"], [f"c{i}"], {"kernel_shape": [op.kh, op.kw]}))
+            inits[f"s{i}"] = rng.uniform(0.5, 1.5, (1, c, 1, 1)).astype(np.float32)
+            inits[f"t{i}"] = rng.standard_normal((1, c, 1, 1)).astype(np.float32) * 0.1
+            nodes.append(("Mul", f"bnmul{i}", [f"c{i}", f"s{i}"], [f"m{i}"], {}))
+            nodes.append(("Add", f"bnadd{i}", [f"m{i}", f"t{i}"], [f"n{i}"], {}))
+        else:  # Conv (+ bias) -> BatchNormalization
+            inits[f"b{i}"] = op.bias
+            nodes.append(("Conv", f"conv{i}", [x, f"w{i}", f"b{i}"], [f"c{i}"], {"kernel_shape": [op.kh, op.kw]}))
+            for k, v in (("g", rng.uniform(0.5, 1.5, c)), ("be", rng.standard_normal(c) * 0.1),
+                         ("mu", rng.standard_normal(c) * 0.1), ("var", rng.uniform(0.5, 2.0, c))):
+                inits[f"{k}{i}"] = v.astype(np.float32)
+            nodes.append(("BatchNormalization", f"bn{i}", [f"c{i}", f"g{i}", f"be{i}", f"mu{i}", f"var{i}"],
+                          [f"n{i}"], {"epsilon": 1e-3}))
+        x = f"n{i}"
+        if op.act == "leaky_relu":
+            nodes.append(("LeakyRelu", f"act{i}", [x], [f"a{i}"], {"alpha": float(op.alpha)}))
+            x = f"a{i}"
+    nodes.append(("Transpose", "t_out", [x], ["xo"], {"perm": [0, 2, 3, 1]}))
+    inits["i0"] = np.array(0, np.int64)
+    inits["ax0"] = np.array([0], np.int64)
+    inits["rest"] = np.array([-1], np.int64)
+    nodes += [("Shape", "shp", ["xo"], ["shp_o"], {}),
+              ("Gather", "gat", ["shp_o", "i0"], ["n_o"], {"axis": 0}),
+              ("Unsqueeze", "unsq", ["n_o", "ax0"], ["cnt1"], {}),
+              ("Concat", "cat", ["cnt1", "rest"], ["tgt"], {"axis": 0}),
+              ("Reshape", "flat", ["xo", "tgt"], ["emb"], {})]
+    write_model(path, nodes, inits, [("input_1", ["n", 76, 32, 1])], [("emb", ["n", 96])])
+
+
+def test_embedding_graph_tf2onnx_batchnorm_and_computed_reshape(tmp_path):
+    """BatchNorm (folded Mul / Add, or the op) is folded into the
+    conv it follows, and a Reshape whose shape is computed from the tensor's Shape
+    imports; the imported graph computes what the file computes."""
+    from heybuddy.embedding_graph import from_onnx
+    g = _se20()
+    p = str(tmp_path / "tf2onnx_bn.onnx")
+    _write_tf2onnx_variant(p, g)
+    h = from_onnx(p)
+    assert [type(o) for o in h.ops] == [type(o) for o in g.ops] and h.out_dim == 96
+    x = np.random.default_rng(2).standard_normal((3, 76, 32, 1))
+    got = onnx_eval.run(p, {"input_1": x})["emb"]
+    assert got.shape == (3, 96)
+    ref = oembed.run_graph(h, x)
+    # (the fold rounds the scaled weights to f32: relative 1e-6, not the 1e-9 of an exact import)
+    np.testing.assert_allclose(got, ref, rtol=2e-5, atol=2e-5 * np.abs(ref).max())
+
+
+def test_embedding_graph_rejects_a_shape_branch_that_feeds_data(tmp_path):
+    """A Shape side branch is allowed only when it ends in a Reshape's shape input."""
+    from heybuddy.embedding_graph import from_onnx
+    from heybuddy.util.onnx_util import read_model, write_model
+    p = str(tmp_path / "tf2onnx_bn.onnx")
+    _write_tf2onnx_variant(p, _se20())
+    m = read_model(p)
+    nodes = [(n.op, n.name, list(n.inputs), list(n.outputs), dict(n.attrs)) for n in m.nodes]
+    # the computed count also scales the data: Shape -> ... -> Cast -> Mul into the chain
+    k = next(i for i, n in enumerate(nodes) if n[0] == "Reshape")
+    nodes[k:k] = [("Cast", "cst", ["n_o"], ["n_f"], {"to": 1}), ("Mul", "scale", ["xo", "n_f"], ["xs"], {})]
+    nodes[-1] = ("Reshape", "flat", ["xs", "tgt"], ["emb"], {})
+    q = str(tmp_path / "bad.onnx")
+    write_model(q, nodes, dict(m.initializers), [(n, list(s)) for n, s in m.inputs],
+                [(n, list(s)) for n, s in m.outputs])
+    with pytest.raises(ValueError):
+        from_onnx(q)
+
+
 def _edit(tmp_path, mutate):
     """SE20's ONNX nodes through ``mutate(nodes, inits)``, rewritten."""
     from heybuddy.util.onnx_util import read_model, write_model
