@@ -50,6 +50,7 @@
 #include <initializer_list>
 #include <utility>
 #include <cmath>
+#include <cstdio>
 
 #include "hbk_common.h"
 #include "hbk_mlp_internal.h"
@@ -161,7 +162,17 @@ __device__ int g_mlp_trace_n[kTraceKerns][kTraceWaves];
     }                                                                                           \
   } while (0)
 #define HBK_MT(kern, id) HBK_MTB(kern, id, 0)
+// per-block spans of one kernel (k3s): {start, end} s_memrealtime (100 MHz, device-wide) and
+// the block's job / split
+__device__ unsigned long long g_span[1024][3];
+#define HBK_SPAN(slot, v)                                                               \
+  do {                                                                                  \
+    if (threadIdx.x == 0 && blockIdx.x < 1024) g_span[blockIdx.x][slot] = (v);           \
+  } while (0)
 #else
+#define HBK_SPAN(slot, v) \
+  do {                    \
+  } while (0)
 #define HBK_MT(kern, id) \
   do {                   \
   } while (0)
@@ -264,7 +275,7 @@ __device__ __forceinline__ uint32_t drop_hash(uint32_t s0, uint32_t s1, uint32_t
 // through LDS (slab: [16][516] floats) as 64-B column runs.
 constexpr int kSlabLd = 516;
 constexpr int kPreTiles = 2;    // k1a row tiles per prefetch workgroup of k2 (v1)
-constexpr int kPreTiles2 = 4;   // k1s (v2: statistics and mask only) row tiles per prefetch workgroup
+constexpr int kPreTiles2 = 3;   // k1s (v2: statistics and mask only) row tiles per prefetch workgroup (2: 84.0, 3: 83.6, 4: 86.0 us per step)
 constexpr int kMaskW = kD / 32;  // mask words per row
 // kV2: the row statistics and dropout mask (rinfo, mask) instead of xhat^T; slab is then
 // >= 4 waves x 4 rows x 1536 bytes of LDS scratch (the mask's byte image)
@@ -932,6 +943,7 @@ struct K2Args {
   // (maxS[mat][row tile][wave], mat k = dHG_k, NG + k = dS_k: k3s's scales)
   int v2;
   float* maxS;
+  int pre_tiles;  // v2: k1s row tiles per prefetch workgroup (kPreTiles2; HBK_PRE_TILES)
 };
 
 #ifdef HBK_TRACE
@@ -977,8 +989,8 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
     const int step = step_of(a.pre.state, a.pre.parity) + 1;
     if (step < a.pre.idx_steps) {
       if (a.v2) {
-        for (int t = 0; t < kPreTiles2; ++t) {
-          const int rt = (blockIdx.x - a.n_rt) * kPreTiles2 + t;
+        for (int t = 0; t < a.pre_tiles; ++t) {
+          const int rt = (blockIdx.x - a.n_rt) * a.pre_tiles + t;
           if (rt >= a.n_rt) break;
           if (t) __syncthreads();  // the mask image's previous readers are done
           k1a_tile<true, true>(a.pre, rt, step, nullptr, hgRaw, a.pre.parity ^ 1);
@@ -1674,7 +1686,7 @@ __global__ void __launch_bounds__(256) k3_wgrad_kernel(K3Args a) {
 
 // ------------------------------------------------------------ k3s (v2) ---
 // The weight gradients dW [M][N] = dY^T X over S batch splits of R rows, with
-// wide N tiles: tile = 128 (M) x 16 NBT (N), 4 waves of 32 M rows each, so the
+// wide N tiles: tile = 128 (M) x 16 NBT (N), kK3sWaves waves of 128 / kK3sWaves M rows, so the
 // gradient operand dY^T is read from HBM / L2 once per N tile (the v1 kernel's
 // 32-column tiles re-read dHG0 48 times per split: 27 MB of its 47 MB per step at
 // B = 1,100). The batch streams through in 32-row steps: the activation chunk X
@@ -1685,16 +1697,23 @@ __global__ void __launch_bounds__(256) k3_wgrad_kernel(K3Args a) {
 // is not stored anywhere: it is recomputed from the pool rows, k1s's statistics and
 // dropout mask (xhat = (v - mu) rs, the formula of k1a) as the chunk is staged.
 constexpr int kK3sMaxR = 512;  // rows per split
+// 8 waves of one 16-row M tile each: two waves per SIMD hide each other's latency (4 waves
+// of two M tiles ran one wave per SIMD at 256 VGPRs + AGPRs, 4.2 k cycles per 32-row step
+// against 1.9 k of issue). (4 M groups of two tiles x 2 column halves -- each B fragment read
+// from LDS feeding two M tiles, the gradient split twice -- measured slower: 24.2 vs 22.1 us)
+constexpr int kK3sWaves = 8, kK3sThr = 64 * kK3sWaves, kK3sMT = 1, kK3sMG = 8;
+static_assert(kK3sMG * kK3sMT * 16 == 128 && kK3sWaves == kK3sMG, "k3s wave layout");
 struct K3sJob {
   const float* X;  // the gradient dY^T [M][Bp]
   const float* Y;  // the activation X^T [N][Bp]; NULL: the input layer's pool rows
   int64_t c_off;
   int ldc, M, N, tn, mat;
+  int S, R;  // this job's batch splits, of R = 32 x (its compiled step count) rows
 };
 struct K3sArgs {
   K3sJob job[kMaxJobs];
   int start[kMaxJobs + 1];
-  int n_jobs, S, R, n_rt, B;
+  int n_jobs, S, n_rt, B;  // S: the slabs (the largest job split; a job with fewer zeroes the rest)
   int64_t Bp;
   const float* maxS;  // [2 NG][n_rt][4]
   const float* pool32;
@@ -1710,17 +1729,24 @@ struct K3sArgs {
   float* part;  // [S][pstride]
   int64_t pstride;
 };
-// XOR swizzle of the 16-B chunks of a 256-B row (the input layer's [32][128] images):
+// XOR swizzle of the 16-B chunks of a 256-B row (the input layer's [32][128] half images):
 // conflict-free ds_write_b128 of whole chunks and ds_read_b64_tr_b16 of the B operand
 __device__ __forceinline__ int k3s_swz(int row, int ch) { return ch ^ (((row & 3) << 2) | ((row >> 2) & 3)); }
-template <int NBT>
+// N tile widths: the input layer's 256 columns (each gradient chunk, loaded and split once,
+// feeds 16 column tiles: its 12x re-read of dHG0 per split became 6x, the split's VALU is
+// amortised over twice the MFMAs -- k3s is bound by the CU's load rate, not by MFMA), the
+// generic jobs' 128
+constexpr int kK3sNbtRaw = 16, kK3sNbtGen = 8;
+static_assert(kD % (16 * kK3sNbtRaw) == 0, "the input layer's tiles are all live");
 struct K3sShared {
-  static constexpr int NT = 16 * NBT, kLdY = 48;  // LDS column: 32 rows + 16 pad halves (conflict-free b128 reads)
-  _Float16 ys[2][2][NT * kLdY];                    // [buf][hi, lo][col][row]
+  static constexpr int kLdY = 48;  // generic: LDS column of 32 rows + 16 pad halves (conflict-free b128 reads)
+  static constexpr int kPlane = 32 * 16 * kK3sNbtRaw > 16 * kK3sNbtGen * kLdY ? 32 * 16 * kK3sNbtRaw
+                                                                             : 16 * kK3sNbtGen * kLdY;
+  _Float16 ys[2][2][kPlane];  // [buf][hi, lo]: generic [col][row]; input layer two [32][128] halves
   float sS[128];
-  float red[2][4][NT];
+  float red[2][kK3sWaves][16 * kK3sNbtRaw];
   uint4 rinfoS[kK3sMaxR];                          // input layer: the split's rows' {mu, rs, address}
-  uint32_t maskS[kK3sMaxR * (NT / 32)];            // ... and their mask words of this N tile
+  uint32_t maskS[kK3sMaxR * kK3sNbtRaw / 2];       // ... and their mask words of this N tile
 };
 // one workgroup's tile; kRaw: the input layer (X from the pool rows). NST steps of 32 rows,
 // fully unrolled, the prefetches unconditional (clamped to the last step: a redundant
@@ -1730,85 +1756,60 @@ struct K3sShared {
 // computes zero rows in its tail steps.
 template <int NBT, bool kRaw, int NST>
 __device__ __forceinline__ void k3s_body(const K3sArgs& a, const K3sJob& jb, int split, int tm, int tnn,
-                                         K3sShared<NBT>& sh) {
-  constexpr int NT = 16 * NBT, kLdY = K3sShared<NBT>::kLdY;
-  constexpr int kYU = NT * 8 / 256;  // float4 units per thread and step (transposed X)
-  static_assert(!kRaw || NT == 128, "the input layer's image is [32][128] halves (the swizzle's 256-B rows)");
-  static_assert(K3sShared<NBT>::kLdY * NT >= 32 * NT, "an input-layer image fits a buffer plane");
+                                         K3sShared& sh) {
+  constexpr int NT = 16 * NBT, kLdY = K3sShared::kLdY;
+  constexpr int kYU = NT * 8 / kK3sThr;  // float4 units per thread and step (transposed X)
+  constexpr int MT = kK3sMT, NBW = NBT;  // M tiles and column tiles per wave
+  static_assert(!kRaw || NT == 256, "the input layer's image is two [32][128] halves (the swizzle's 256-B rows)");
+  static_assert(kRaw || NT * kLdY <= K3sShared::kPlane, "a generic image fits a buffer plane");
+  static_assert(NT <= 16 * kK3sNbtRaw && NT / 32 <= kK3sNbtRaw / 2, "red / maskS sizes");
+  // input-layer image offset (halves) of row r, 16-B chunk c (0 .. NT / 8)
+  auto raw_off = [](int r, int c) { return (c >> 4) * (32 * 128) + r * 128 + 8 * k3s_swz(r, c & 15); };
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = lane & 15, kq = lane >> 4;
   const int Bp = static_cast<int>(a.Bp);
-  const int rb0 = split * a.R;
+  const int rb0 = split * jb.R;
   constexpr int nst = NST;
   const int n0 = tnn * NT;
-  const int nb = min(NBT, (jb.N - n0 + 15) / 16);  // live 16-column tiles (uniform)
-  const int mrow = tm * 128 + 32 * wave;
-  // the gradient's scale over the split's row tiles: max |dY| into [2^14, 2^15)
-  float sc, inv;
-  {
-    const int t0 = rb0 / 16, t1 = min(a.n_rt, (rb0 + 32 * nst) / 16);
-    float mx = 0.f;
-    for (int q = lane; q < 4 * (t1 - t0); q += 64)
-      mx = fmaxf(mx, *BCK(&a.maxS[(static_cast<int64_t>(jb.mat) * a.n_rt + t0) * 4 + q], 4));
-    pow2_scale(wmax(mx), sc, inv);
-  }
-  // gradient chunk of step u: two 16-row M tiles x 8 batch rows (b = 32 u + 8 kq ..)
-  const float* X0 = jb.X + static_cast<int64_t>(min(mrow + m, jb.M - 1)) * Bp;
-  const float* X1 = jb.X + static_cast<int64_t>(min(mrow + 16 + m, jb.M - 1)) * Bp;
-  auto load_g = [&](int u, f4 (&d)[2][2]) {
-    const int b = min(rb0 + 32 * u + 8 * kq, Bp - 8);
+  const int mg = wave, nt0 = 0;  // this wave's M group, first column tile
+  const int mrow = tm * 128 + 16 * MT * mg;
+  // gradient chunk of step u: MT 16-row M tiles x 8 batch rows (b = 32 u + 8 kq ..)
+  const float* Xt[MT];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      d[0][h] = *BCK(reinterpret_cast<const f4*>(X0 + b + 4 * h), 16);
-      d[1][h] = *BCK(reinterpret_cast<const f4*>(X1 + b + 4 * h), 16);
-    }
+  for (int t = 0; t < MT; ++t) Xt[t] = jb.X + static_cast<int64_t>(min(mrow + 16 * t + m, jb.M - 1)) * Bp;
+  // (unclamped: rows past Bp read the next row, or past the last row of the workspace array the
+  // arrays after it, <= R floats; they are zeroed at use. One base address per tile and
+  // immediate offsets per step: a clamp per step held a 64-bit address per unrolled step)
+  auto load_g = [&](int u, f4 (&d)[MT][2]) {
+    const int b = rb0 + 32 * u + 8 * kq;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int t = 0; t < MT; ++t) d[t][h] = *BCK(reinterpret_cast<const f4*>(Xt[t] + b + 4 * h), 16);
   };
-  if constexpr (kRaw) {  // the split's row information and mask words (rows past B: row B - 1's, zeroed below)
-    // (unrolled, every load unconditional at a clamped row: all in flight together)
-    const int nr = 32 * nst;
-    constexpr int kRI = kK3sMaxR / 256, kMI = kK3sMaxR * (NT / 32) / 256;
-    uint4 ri[kRI];
-    uint32_t mi[kMI];
-#pragma unroll
-    for (int it = 0; it < kRI; ++it)
-      ri[it] = *BCK(&a.rinfo[min(rb0 + min(tid + 256 * it, nr - 1), a.B - 1)], 16);
-#pragma unroll
-    for (int it = 0; it < kMI; ++it) {
-      const int q = min(tid + 256 * it, nr * (NT / 32) - 1);
-      mi[it] = *BCK(&a.mask[static_cast<int64_t>(min(rb0 + q / (NT / 32), a.B - 1)) * kMaskW + n0 / 32 + q % (NT / 32)], 4);
-    }
-#pragma unroll
-    for (int it = 0; it < kRI; ++it)
-      if (tid + 256 * it < nr) sh.rinfoS[tid + 256 * it] = ri[it];
-#pragma unroll
-    for (int it = 0; it < kMI; ++it)
-      if (tid + 256 * it < nr * (NT / 32)) sh.maskS[tid + 256 * it] = mi[it];
-    __syncthreads();
-  }
-  HBK_MT(2, 3);
   // activation chunk of step u into registers ...
-  // (input layer: thread -> 16-B chunks q = tid + 256 j of the step's [32 rows][NT] image, row
+  // (input layer: thread -> 16-B chunks q = tid + kK3sThr j of the step's [32 rows][NT] image, row
   // q / (NT / 8), columns 8 (q % (NT / 8)) ..: the pool rows as they lie, 16 / 32 B per chunk)
-  constexpr int kCPR = NT / 8, kCPT = 32 * kCPR / 256;  // chunks per row, per thread
+  constexpr int kCPR = NT / 8, kCPT = 32 * kCPR / kK3sThr;  // chunks per row, per thread
   // two register sets: step v's loads are issued at step v - 3 and converted at step v - 1
   f4 yv[2][kRaw ? 1 : kYU];
   uint4 ylo[2][kRaw ? kCPT : 1], yhi[2][kRaw ? kCPT : 1];
+  auto issue_raw = [&](int u, int j, const uint4& inf) {  // chunk j of step u, its row's info inf
+    bool is16;
+    const char* base = row_addr(inf, is16);
+    const char* p = base + (static_cast<int64_t>(n0 + 8 * ((tid + kK3sThr * j) % kCPR)) << (is16 ? 1 : 2));
+    ylo[u & 1][j] = ldg(BCK(reinterpret_cast<const uint4*>(p), 16));
+    yhi[u & 1][j] = ldg(BCK(reinterpret_cast<const uint4*>(p + (is16 ? 0 : 16)), 16));
+  };
   auto load_y = [&](int u) {
     const int ys_ = u & 1;
     if constexpr (kRaw) {
 #pragma unroll
-      for (int j = 0; j < kCPT; ++j) {
-        const int q = tid + 256 * j, row = q / kCPR, ch = q % kCPR;
-        bool is16;
-        const char* base = row_addr(sh.rinfoS[32 * u + row], is16);
-        const char* p = base + (static_cast<int64_t>(n0 + 8 * ch) << (is16 ? 1 : 2));
-        ylo[ys_][j] = ldg(BCK(reinterpret_cast<const uint4*>(p), 16));
-        yhi[ys_][j] = ldg(BCK(reinterpret_cast<const uint4*>(p + (is16 ? 0 : 16)), 16));
-      }
+      for (int j = 0; j < kCPT; ++j) issue_raw(u, j, sh.rinfoS[32 * u + (tid + kK3sThr * j) / kCPR]);
     } else {
 #pragma unroll
       for (int jj = 0; jj < kYU; ++jj) {
-        const int q = tid + 256 * jj, col = min(n0 + (q >> 3), jb.N - 1);
-        const int b = min(rb0 + 32 * u + 4 * (q & 7), Bp - 4);
+        const int q = tid + kK3sThr * jj, col = min(n0 + (q >> 3), jb.N - 1);
+        const int b = rb0 + 32 * u + 4 * (q & 7);  // (unclamped, as the gradient's)
         yv[ys_][jj] = *BCK(reinterpret_cast<const f4*>(jb.Y + static_cast<int64_t>(col) * Bp + b), 16);
       }
     }
@@ -1823,7 +1824,7 @@ __device__ __forceinline__ void k3s_body(const K3sArgs& a, const K3sJob& jb, int
       // ([32][NT] halves, 16-B chunks XOR-swizzled: conflict-free b128 writes and tr reads)
 #pragma unroll
       for (int j = 0; j < kCPT; ++j) {
-        const int q = tid + 256 * j, row = q / kCPR, ch = q % kCPR, rl = 32 * u + row;
+        const int q = tid + kK3sThr * j, row = q / kCPR, ch = q % kCPR, rl = 32 * u + row;
         const uint4 inf = sh.rinfoS[rl];
         const bool is16 = (inf.z & 1u) != 0;
         const uint32_t bits = sh.maskS[rl * (NT / 32) + (ch >> 2)] >> (8 * (ch & 3));
@@ -1842,14 +1843,14 @@ __device__ __forceinline__ void k3s_body(const K3sArgs& a, const K3sJob& jb, int
         }
         h8 hv, lv;
         split8(f4{xs[0], xs[1], xs[2], xs[3]}, f4{xs[4], xs[5], xs[6], xs[7]}, hv, lv);
-        const int off = row * NT + 8 * k3s_swz(row, ch);
+        const int off = raw_off(row, ch);
         *reinterpret_cast<h8*>(yh + off) = hv;
         *reinterpret_cast<h8*>(yl + off) = lv;
       }
     } else {
 #pragma unroll
       for (int jj = 0; jj < kYU; ++jj) {
-        const int q = tid + 256 * jj, col = q >> 3, b4 = 4 * (q & 7);
+        const int q = tid + kK3sThr * jj, col = q >> 3, b4 = 4 * (q & 7);
         const f4 v = rb0 + 32 * u + b4 < Bp ? yv[ys_][jj] : f4{0.f, 0.f, 0.f, 0.f};
         uint32_t h0, l0, h1, l1;
         split_pair(v[0], v[1], h0, l0);
@@ -1860,47 +1861,107 @@ __device__ __forceinline__ void k3s_body(const K3sArgs& a, const K3sJob& jb, int
     }
   };
   const f4 z = {0.f, 0.f, 0.f, 0.f};
-  f4 acc[2][NBT];
+  f4 acc[MT][NBW];
+  f4 ssum[MT];
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < MT; ++t) {
+    ssum[t] = z;
 #pragma unroll
-    for (int nt = 0; nt < NBT; ++nt) acc[t][nt] = z;
-  f4 ssum[2] = {z, z};
-  f4 ga[3][2][2];  // gradient ring: [slot][tile][half], step v in slot v % 3
-  // prologue: step 0 staged; steps 1, 2 of X and 0, 1, 2 of the gradient in flight
+    for (int i = 0; i < NBW; ++i) acc[t][i] = z;
+  }
+  f4 ga[3][MT][2];  // gradient ring: [slot][tile][half], step v in slot v % 3 (loaded 3 steps ahead)
   constexpr int last = NST - 1;
-  load_y(0);
+  // prologue, every independent load issued at once (the serial round trips were 4.6 us of a
+  // 12-step workgroup's 24): the gradient's per-tile maxima, the gradient of steps 0 .. 2,
+  // the input layer's row information and mask words (for LDS), and the activation of steps 0
+  // and 1 (the input layer's through row information loaded into registers here as well)
+  static_assert(kK3sMaxR / 16 * 4 <= 128, "maxS: two entries per lane");
+  float mxv[2];
+  {
+    const int t0 = rb0 / 16, n4 = 4 * (min(a.n_rt, (rb0 + 32 * nst) / 16) - t0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int q = lane + 64 * i;
+      const float v = *BCK(&a.maxS[(static_cast<int64_t>(jb.mat) * a.n_rt + t0) * 4 + min(q, n4 - 1)], 4);
+      mxv[i] = q < n4 ? v : 0.f;
+    }
+  }
   load_g(0, ga[0]);
-  write_y(0, 0);
-  load_y(min(1, last));
   load_g(min(1, last), ga[1]);
-  load_y(min(2, last));
   load_g(min(2, last), ga[2]);
+  float sc, inv;
+  if constexpr (kRaw) {  // the split's row information and mask words (rows past B: row B - 1's, zeroed below)
+    // (unrolled, every load unconditional at a clamped row: all in flight together)
+    const int nr = 32 * nst;
+    constexpr int kRI = kK3sMaxR / kK3sThr, kMI = kK3sMaxR * (NT / 32) / kK3sThr;
+    uint4 ri[kRI], r01[2][kCPT];
+    uint32_t mi[kMI];
+#pragma unroll
+    for (int it = 0; it < kRI; ++it)
+      ri[it] = *BCK(&a.rinfo[min(rb0 + min(tid + kK3sThr * it, nr - 1), a.B - 1)], 16);
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+#pragma unroll
+      for (int j = 0; j < kCPT; ++j)
+        r01[v][j] = *BCK(&a.rinfo[min(rb0 + 32 * min(v, last) + (tid + kK3sThr * j) / kCPR, a.B - 1)], 16);
+#pragma unroll
+    for (int it = 0; it < kMI; ++it) {
+      const int q = min(tid + kK3sThr * it, nr * (NT / 32) - 1);
+      mi[it] = *BCK(&a.mask[static_cast<int64_t>(min(rb0 + q / (NT / 32), a.B - 1)) * kMaskW + n0 / 32 + q % (NT / 32)], 4);
+    }
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+#pragma unroll
+      for (int j = 0; j < kCPT; ++j) issue_raw(min(v, last), j, r01[v][j]);
+    pow2_scale(wmax(fmaxf(mxv[0], mxv[1])), sc, inv);
+#pragma unroll
+    for (int it = 0; it < kRI; ++it)
+      if (tid + kK3sThr * it < nr) sh.rinfoS[tid + kK3sThr * it] = ri[it];
+#pragma unroll
+    for (int it = 0; it < kMI; ++it)
+      if (tid + kK3sThr * it < nr * (NT / 32)) sh.maskS[tid + kK3sThr * it] = mi[it];
+    __syncthreads();
+  } else {
+    load_y(0);
+    load_y(min(1, last));
+    pow2_scale(wmax(fmaxf(mxv[0], mxv[1])), sc, inv);
+  }
+  HBK_MT(2, 3);
+  // step 0 staged; steps 1, 2 of X and 0, 1, 2 of the gradient in flight
+  write_y(0, 0);
+  load_y(min(2, last));
   __syncthreads();
   HBK_MT(2, 4);
-  auto step = [&](int u, f4 (&g)[2][2]) {
+  auto step = [&](int u, f4 (&g)[MT][2]) {
     // this step's gradient: dead batch rows zeroed, row sums (input layer), scaled split
     const bool live = rb0 + 32 * u + 8 * kq < Bp;
-    h8 ah[2], al[2];
+    h8 ah[MT], al[MT];
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < MT; ++t) {
       const f4 g0 = live ? g[t][0] : z, g1 = live ? g[t][1] : z;
       ssum[t] += g0 + g1;
       split8(g0 * sc, g1 * sc, ah[t], al[t]);
     }
     const _Float16* yh = &sh.ys[u & 1][0][0];
     const _Float16* yl = &sh.ys[u & 1][1][0];
+    // every column tile, live or not (a generic job's dead tiles hold clamped columns: finite,
+    // never stored; a uniform branch per tile made each wait for its own LDS reads), in groups
+    // of kGrp tiles: group g + 1's B fragments are read while group g's MFMAs run (fenced:
+    // unfenced, all 16 tiles' reads were hoisted to the top, 128 VGPRs)
+    constexpr int kGrp = 4, nGrp = NBW / kGrp;
+    static_assert(NBW % kGrp == 0, "column-tile groups");
+    h8 fb[2][kGrp][2];  // [slot][tile][hi, lo]
+    auto read_grp = [&](int gi, h8 (&d)[kGrp][2]) {
 #pragma unroll
-    for (int nt = 0; nt < NBT; ++nt)
-      if (nt < nb) {
-        h8 bh, bl;
+      for (int i = 0; i < kGrp; ++i) {
+        const int nt = nt0 + gi * kGrp + i;
         if constexpr (kRaw) {
           // rows 8 kq .. 8 kq + 7 of column 16 nt + m, by two transposed reads (rows 8 kq + q
           // and 8 kq + 4 + q supplied by lane 4 q + p of the 16-lane group, columns 16 nt + 4 p ..)
           const int qq = (lane & 15) >> 2, pp = lane & 3;
           const int r0 = 8 * kq + qq, r1 = r0 + 4, c2 = 2 * nt + (pp >> 1);
-          const int o0 = r0 * NT + 8 * k3s_swz(r0, c2) + 4 * (pp & 1);
-          const int o1 = r1 * NT + 8 * k3s_swz(r1, c2) + 4 * (pp & 1);
+          const int o0 = raw_off(r0, c2) + 4 * (pp & 1);
+          const int o1 = raw_off(r1, c2) + 4 * (pp & 1);
           typedef __fp16 hv4 __attribute__((__vector_size__(4 * sizeof(__fp16))));
           typedef __attribute__((address_space(3))) hv4* lp_t;
           const hv4 h0 = __builtin_amdgcn_ds_read_tr16_b64_v4f16((lp_t)const_cast<_Float16*>(yh + o0));
@@ -1911,15 +1972,26 @@ __device__ __forceinline__ void k3s_body(const K3sArgs& a, const K3sJob& jb, int
           typedef uint32_t u4v __attribute__((ext_vector_type(4)));
           const u2v h0b = __builtin_bit_cast(u2v, h0), h1b = __builtin_bit_cast(u2v, h1);
           const u2v l0b = __builtin_bit_cast(u2v, l0), l1b = __builtin_bit_cast(u2v, l1);
-          bh = __builtin_bit_cast(h8, u4v{h0b.x, h0b.y, h1b.x, h1b.y});
-          bl = __builtin_bit_cast(h8, u4v{l0b.x, l0b.y, l1b.x, l1b.y});
+          d[i][0] = __builtin_bit_cast(h8, u4v{h0b.x, h0b.y, h1b.x, h1b.y});
+          d[i][1] = __builtin_bit_cast(h8, u4v{l0b.x, l0b.y, l1b.x, l1b.y});
         } else {
-          bh = *reinterpret_cast<const h8*>(yh + (16 * nt + m) * kLdY + 8 * kq);
-          bl = *reinterpret_cast<const h8*>(yl + (16 * nt + m) * kLdY + 8 * kq);
+          d[i][0] = *reinterpret_cast<const h8*>(yh + (16 * nt + m) * kLdY + 8 * kq);
+          d[i][1] = *reinterpret_cast<const h8*>(yl + (16 * nt + m) * kLdY + 8 * kq);
         }
-        acc[0][nt] = mma3(ah[0], al[0], bh, bl, acc[0][nt]);
-        acc[1][nt] = mma3(ah[1], al[1], bh, bl, acc[1][nt]);
       }
+    };
+    read_grp(0, fb[0]);
+#pragma unroll
+    for (int gi = 0; gi < nGrp; ++gi) {
+      if (gi + 1 < nGrp) read_grp(gi + 1, fb[(gi + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < kGrp; ++i)
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+          acc[t][gi * kGrp + i] = mma3(ah[t], al[t], fb[gi & 1][i][0], fb[gi & 1][i][1], acc[t][gi * kGrp + i]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     // step u + 1's X into the other buffer (read by nobody now: the barrier that ended step
     // u - 1 passed), then step u + 2's loads (clamped: past the end they reload the last step)
     if (u < 4) HBK_MT(2, 40 + 3 * u);
@@ -1928,24 +2000,33 @@ __device__ __forceinline__ void k3s_body(const K3sArgs& a, const K3sJob& jb, int
     load_y(min(u + 3, last));
     load_g(min(u + 3, last), g);
     if (u < 4) HBK_MT(2, 42 + 3 * u);
-    lds_barrier();  // (LDS only: step u + 2's and u + 3's loads stay in flight)
+    lds_barrier();  // (LDS only: the prefetched loads stay in flight)
     HBK_MT(2, 16 + u);
+    // a scheduling fence per step: unfenced, the scheduler hoisted every step's (address-
+    // independent) gradient loads to the top, ~11 VGPRs per unrolled step
+    __builtin_amdgcn_sched_barrier(0);
   };
 #pragma unroll
-  for (int u = 0; u < NST; ++u) step(u, ga[u % 3]);
+  for (int u = 0; u < NST; ++u) step(u, ga[u % 3]);  // (a runtime step bound, as a break or
+  // a guard per step, cost 35 us against 24: rolled loop / per-step branch joins)
   HBK_MT(2, 2);
   float* const C = a.part + split * a.pstride + jb.c_off;
   if constexpr (!kRaw) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < MT; ++t)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int row = mrow + 16 * t + 4 * kq + e;
         if (row >= jb.M) continue;
 #pragma unroll
-        for (int nt = 0; nt < NBT; ++nt) {
-          const int c = n0 + 16 * nt + m;
-          if (nt < nb && c < jb.N) *BCK(&C[static_cast<int64_t>(row) * jb.ldc + c], 4) = acc[t][nt][e] * inv;
+        for (int i = 0; i < NBW; ++i) {
+          const int c = n0 + 16 * (nt0 + i) + m;
+          if (c < jb.N) {
+            *BCK(&C[static_cast<int64_t>(row) * jb.ldc + c], 4) = acc[t][i][e] * inv;
+            // slabs past this job's splits (the launch's S is the largest job's): zeros
+            for (int z = split + jb.S; z < a.S; z += jb.S)
+              *BCK(&C[(z - split) * a.pstride + static_cast<int64_t>(row) * jb.ldc + c], 4) = 0.f;
+          }
         }
       }
     return;
@@ -1953,67 +2034,92 @@ __device__ __forceinline__ void k3s_body(const K3sArgs& a, const K3sJob& jb, int
     // input layer: dW = g o (dHG0^T xhat) + s (x) b, dgamma = sum_j W o (dHG0^T xhat),
     // dbeta = sum_j W s_j, with s_j = the split's sum of dHG0[b][j]
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < MT; ++t) {
       float sj = (ssum[t][0] + ssum[t][1]) + (ssum[t][2] + ssum[t][3]);
       sj += __shfl_xor(sj, 16, 64);
       sj += __shfl_xor(sj, 32, 64);
-      if (kq == 0) sh.sS[32 * wave + 16 * t + m] = sj;
+      if (kq == 0) sh.sS[16 * MT * mg + 16 * t + m] = sj;
+    }
+    // (the input layer's N is a multiple of the tile: every column live.) W0, gamma and beta
+    // are loaded before the first store (a store may alias them: interleaved, each load
+    // waited behind the one before)
+    float wv[NBW][MT][4], gcv[NBW], bcv[NBW];
+#pragma unroll
+    for (int i = 0; i < NBW; ++i) {
+      const int c = n0 + 16 * (nt0 + i) + m;
+      gcv[i] = *BCK(&a.g_in[c], 4);
+      bcv[i] = *BCK(&a.b_in[c], 4);
+#pragma unroll
+      for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          wv[i][t][e] = *BCK(&a.W0[static_cast<int64_t>(mrow + 16 * t + 4 * kq + e) * jb.ldc + c], 4);
     }
     __syncthreads();
-    float dg[NBT], db[NBT];
+    float dg[NBW], db[NBW];
 #pragma unroll
-    for (int nt = 0; nt < NBT; ++nt) {
-      dg[nt] = db[nt] = 0.f;
-      const int c = min(n0 + 16 * nt + m, jb.N - 1);
-      const float gc = *BCK(&a.g_in[c], 4), bc = *BCK(&a.b_in[c], 4);
+    for (int i = 0; i < NBW; ++i) {
+      dg[i] = db[i] = 0.f;
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < MT; ++t)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int row = mrow + 16 * t + 4 * kq + e;  // j (< 128 = M)
-          const float w = *BCK(&a.W0[static_cast<int64_t>(row) * jb.ldc + c], 4);
-          const float s = sh.sS[32 * wave + 16 * t + 4 * kq + e];
-          const float v = acc[t][nt][e] * inv;
-          if (nt < nb) *BCK(&C[static_cast<int64_t>(row) * jb.ldc + n0 + 16 * nt + m], 4) = gc * v + bc * s;
-          dg[nt] += w * v;
-          db[nt] += w * s;
+          const float s = sh.sS[16 * MT * mg + 16 * t + 4 * kq + e];
+          const float v = acc[t][i][e] * inv;
+          *BCK(&C[static_cast<int64_t>(row) * jb.ldc + n0 + 16 * (nt0 + i) + m], 4) = gcv[i] * v + bcv[i] * s;
+          dg[i] += wv[i][t][e] * v;
+          db[i] += wv[i][t][e] * s;
         }
     }
+    // per column, the M groups' partials: red[.][M group][column]
 #pragma unroll
-    for (int nt = 0; nt < NBT; ++nt) {
+    for (int i = 0; i < NBW; ++i) {
 #pragma unroll
       for (int o = 16; o < 64; o <<= 1) {
-        dg[nt] += __shfl_xor(dg[nt], o, 64);
-        db[nt] += __shfl_xor(db[nt], o, 64);
+        dg[i] += __shfl_xor(dg[i], o, 64);
+        db[i] += __shfl_xor(db[i], o, 64);
       }
       if (kq == 0) {
-        sh.red[0][wave][16 * nt + m] = dg[nt];
-        sh.red[1][wave][16 * nt + m] = db[nt];
+        sh.red[0][mg][16 * (nt0 + i) + m] = dg[i];
+        sh.red[1][mg][16 * (nt0 + i) + m] = db[i];
       }
     }
     __syncthreads();
-    if (tid < nb * 16) {
+    if (tid < NT) {
       float* P = a.part + split * a.pstride;
-      *BCK(&P[a.g_off + n0 + tid], 4) = sh.red[0][0][tid] + sh.red[0][1][tid] + sh.red[0][2][tid] + sh.red[0][3][tid];
-      *BCK(&P[a.b_off + n0 + tid], 4) = sh.red[1][0][tid] + sh.red[1][1][tid] + sh.red[1][2][tid] + sh.red[1][3][tid];
+      float rg = 0.f, rb = 0.f;
+#pragma unroll
+      for (int w = 0; w < kK3sMG; ++w) {
+        rg += sh.red[0][w][tid];
+        rb += sh.red[1][w][tid];
+      }
+      *BCK(&P[a.g_off + n0 + tid], 4) = rg;
+      *BCK(&P[a.b_off + n0 + tid], 4) = rb;
     }
   }
 }
-template <int NBT, int NST>
-__global__ void __launch_bounds__(256) k3s_kernel(K3sArgs a) {
-  __shared__ __attribute__((aligned(16))) K3sShared<NBT> sh;
+// NST0: the input layer's steps per split, NST1: the generic jobs'; kOcc waves per SIMD
+// (4: two workgroups per CU, <= 128 VGPRs -- the short-step pairs only: the unrolled steps'
+// registers grow with the step count)
+template <int NST0, int NST1, int kOcc>
+__global__ void __launch_bounds__(kK3sThr, kOcc) k3s_kernel(K3sArgs a) {
+  __shared__ __attribute__((aligned(16))) K3sShared sh;
   const int blk = blockIdx.x;
   int j = 0;
   while (j + 1 < a.n_jobs && blk >= a.start[j + 1]) ++j;
   const K3sJob jb = a.job[j];
   const int local = blk - a.start[j];
-  const int split = local % a.S, tile = local / a.S;
+  const int split = local % jb.S, tile = local / jb.S;
   const int tm = tile / jb.tn, tnn = tile - tm * jb.tn;
   HBK_MT(2, 1);
+  HBK_SPAN(0, __builtin_amdgcn_s_memrealtime());
   if (jb.Y == nullptr)
-    k3s_body<NBT, true, NST>(a, jb, split, tm, tnn, sh);
+    k3s_body<kK3sNbtRaw, true, NST0>(a, jb, split, tm, tnn, sh);
   else
-    k3s_body<NBT, false, NST>(a, jb, split, tm, tnn, sh);
+    k3s_body<kK3sNbtGen, false, NST1>(a, jb, split, tm, tnn, sh);
+  HBK_SPAN(1, __builtin_amdgcn_s_memrealtime());
+  HBK_SPAN(2, (static_cast<unsigned long long>(j) << 32) | split);
 }
 
 // Steps whose update does not get the workspace (or is preceded by the
@@ -2900,7 +3006,7 @@ FusedWs fused_layout(int64_t B, int NG, int64_t n_params = 0) {
 
 // HBK_STEP=2: the v2 step (k1s -> k1c / k3s from the pool rows); 1: the k1a -> xhat^T ->
 // k1b / k3 path. The default is kStepDefault (the faster one as measured, tools/ab_step.sh)
-constexpr int kStepDefault = 1;
+constexpr int kStepDefault = 2;
 bool step_v2() {
   static const bool v2 = (getenv("HBK_STEP") ? atoi(getenv("HBK_STEP")) : kStepDefault) == 2;
   return v2;
@@ -2950,17 +3056,53 @@ K1cGeom k1c_geom(int B, const void* stream) {
   }
   return best;
 }
-// k3s's batch split: about CUs / (the launch's tiles) splits, of 32 NST rows with NST one of
-// the compiled step counts 4, 8, 12, 16 (128 .. 512 rows; HBK_K3_R overrides the rows)
-int k3s_steps(int64_t Bp, int tiles, const void* stream) {
+// k3s's batch splits: the input layer's job (12 of the launch's tiles and the bulk of its
+// FLOPs) gets S0 splits of NST0 32-row steps, the small generic jobs S1 <= S0 of NST1, so
+// that the launch fits the CUs in one round and its longest workgroup (steps x the job's
+// relative step cost: the generic tiles have 4 or 6 of 8 column tiles live) is shortest.
+// The step counts are compile-time (fully unrolled steps), one of kK3sPairs; at most
+// ceil(Bp / 128) splits (the workspace's slabs). HBK_K3_R forces one pair by its rows.
+constexpr int kK3sPairs[][2] = {{1, 1}, {2, 2}, {3, 3}, {3, 5}, {4, 4}, {4, 9}, {4, 12}, {5, 12},
+                                {6, 14}, {7, 16}, {8, 8}, {9, 16}, {12, 12}, {16, 16}};
+constexpr int kK3sNPairs = sizeof(kK3sPairs) / sizeof(kK3sPairs[0]);
+constexpr int k3s_occ(int) { return 2; }  // (two workgroups per CU measured no faster: the
+                                          // CU's load rate binds, r06)
+struct K3sPlan {
+  int S0, S1, pair;
+};
+// per-workgroup time model (units of ~0.78 us, the generic jobs' 32-row step of r06, fitted
+// to the traced spans): the input layer's 3 + 1.6 x steps, a generic job's 2.5 + 0.65 x steps
+K3sPlan k3s_plan(int64_t Bp, int tiles0, int tiles1, const void* stream) {
   const int cus = static_cast<int>(std::max<int64_t>(1, persistent_blocks(1, stream)));
-  int R = env_int("HBK_K3_R", 0);
-  if (R <= 0) {
-    const int S = std::max(1, cus / std::max(1, tiles));
-    R = static_cast<int>((Bp + S - 1) / S);
+  const int64_t max_s = (Bp + 127) / 128;
+  const int fr = env_int("HBK_K3_R", 0), fq = env_int("HBK_K3_PAIR", -1);
+  auto splits = [&](int st) { return static_cast<int>((Bp + 32 * st - 1) / (32 * st)); };
+  K3sPlan best{splits(16), splits(16), kK3sNPairs - 1};
+  double best_cost = 1e30;
+  for (int q = 0; q < kK3sNPairs; ++q) {
+    const int st0 = kK3sPairs[q][0], st1 = kK3sPairs[q][1];
+    if (fr > 0 && 32 * st0 < fr) continue;
+    if (fq >= 0 && q != fq) continue;
+    const int s0 = splits(st0), s1 = splits(st1);
+    if (s0 > max_s && st0 < 16) continue;  // (the workspace's slabs)
+    const int wgs = tiles0 * s0 + tiles1 * s1, rounds = (wgs + cus - 1) / cus;
+    const double cost = rounds * std::max(3.0 + 1.6 * st0, 2.5 + 0.65 * st1) + 1e-3 * wgs;
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = K3sPlan{s0, s1, q};
+    }
+    if (fr > 0) break;
   }
-  const int nst = (R + 31) / 32;
-  return nst <= 4 ? 4 : nst <= 8 ? 8 : nst <= 12 ? 12 : 16;
+  return best;
+}
+template <int Q = 0>
+void launch_k3s(int q, dim3 grid, hipStream_t s, const K3sArgs& k3) {
+  if constexpr (Q < kK3sNPairs) {
+    if (q == Q)
+      hipLaunchKernelGGL((k3s_kernel<kK3sPairs[Q][0], kK3sPairs[Q][1], k3s_occ(Q)>), grid, dim3(kK3sThr), 0, s, k3);
+    else
+      launch_k3s<Q + 1>(q, grid, s, k3);
+  }
 }
 
 void fill_k2(const hbk_mlp_plan& p, K2Args& k) {
@@ -3205,7 +3347,8 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
   k2.maxS = v2 && train ? ws + w.maxS : nullptr;
   set_k2_cache(wsp, NG, wc, k2);
   {
-    const int pt = v2 ? kPreTiles2 : kPreTiles;
+    k2.pre_tiles = std::max(1, env_int("HBK_PRE_TILES", kPreTiles2));
+    const int pt = v2 ? k2.pre_tiles : kPreTiles;
     const int grid = k2.prefetch ? rt + (rt + pt - 1) / pt : rt;
     auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, k2); };
     if (train) {
@@ -3221,7 +3364,7 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
   }
   if (!train) return HBK_OK;
   if (v2) {  // k3s: job 0 = input layer (pool rows), then dW_hg of GMLPs 1.., then dW_o of every GMLP
-    constexpr int kNT = 128;
+    constexpr int kNtRaw = 16 * kK3sNbtRaw, kNtGen = 16 * kK3sNbtGen;
     K3sArgs k3;
     int nj = 0, tiles = 0;
     auto add = [&](const float* X, const float* Y, int64_t c_off, int ldc, int M, int N, int mat) {
@@ -3232,10 +3375,11 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
       j.ldc = ldc;
       j.M = M;
       j.N = N;
-      j.tn = (N + kNT - 1) / kNT;
+      const int nt = Y ? kNtGen : kNtRaw;
+      j.tn = (N + nt - 1) / nt;
       j.mat = mat;
-      k3.start[nj] = tiles;
-      tiles += ((M + 127) / 128) * j.tn;
+      k3.start[nj] = ((M + 127) / 128) * j.tn;  // (tiles; scaled by the job's splits below)
+      tiles += k3.start[nj];
       ++nj;
     };
     add(ws + w.dHG, nullptr, p.g[0].w_hg, kD, kH2, kD, 0);
@@ -3243,13 +3387,28 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
       add(ws + w.dHG + int64_t(k) * kH2 * Bp, ws + w.Xn + int64_t(k) * kL * Bp, p.g[k].w_hg, kL, kH2, kL, k);
     for (int k = 0; k < NG; ++k)
       add(ws + w.dS + int64_t(k) * kL * Bp, ws + w.U + int64_t(k) * kH * Bp, p.g[k].w_o, kH, p.g[k].out, kH, NG + k);
-    const int NST = k3s_steps(Bp, tiles, s), R = 32 * NST;
-    const int S = static_cast<int>((Bp + R - 1) / R);
-    for (int i = 0; i < nj; ++i) k3.start[i] *= S;
-    k3.start[nj] = tiles * S;
+    const K3sPlan pl = k3s_plan(Bp, k3.start[0], tiles - k3.start[0], s);
+    const int S = pl.S0;
+    if (getenv("HBK_PLAN_LOG")) {  // (tuning aid) the plan of each distinct batch, once
+      static int64_t logged = -1;
+      if (logged != Bp) {
+        logged = Bp;
+        fprintf(stderr, "hbk k3s plan: Bp %lld, CUs %lld, S0 %d x %d steps, S1 %d x %d steps\n",
+                static_cast<long long>(Bp), static_cast<long long>(persistent_blocks(1, s)), pl.S0,
+                kK3sPairs[pl.pair][0], pl.S1, kK3sPairs[pl.pair][1]);
+      }
+    }
+    int wgs = 0;
+    for (int i = 0; i < nj; ++i) {
+      k3.job[i].S = i == 0 ? pl.S0 : pl.S1;
+      k3.job[i].R = 32 * kK3sPairs[pl.pair][i == 0 ? 0 : 1];
+      const int t = k3.start[i];
+      k3.start[i] = wgs;
+      wgs += t * k3.job[i].S;
+    }
+    k3.start[nj] = wgs;
     k3.n_jobs = nj;
     k3.S = S;
-    k3.R = R;
     k3.n_rt = rt;
     k3.B = B;
     k3.Bp = Bp;
@@ -3266,13 +3425,7 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
     k3.b_off = p.ln_in.b;
     k3.part = ws + w.part;
     k3.pstride = w.pstride;
-    auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(tiles * S), dim3(256), 0, s, k3); };
-    switch (NST) {
-      case 4: launch(k3s_kernel<kNT / 16, 4>); break;
-      case 8: launch(k3s_kernel<kNT / 16, 8>); break;
-      case 12: launch(k3s_kernel<kNT / 16, 12>); break;
-      default: launch(k3s_kernel<kNT / 16, 16>);
-    }
+    launch_k3s(pl.pair, dim3(wgs), s, k3);
     HBK_LAUNCH_CHECK("k3s_kernel");
     if (flags & HBK_STEP_DEFER_PARTIALS) {
       p.deferred_ws = ws;
@@ -3555,5 +3708,9 @@ extern "C" int hbk_debug_mlp_trace(unsigned long long* out, int* counts) {
   int z[hbk::kTraceKerns * hbk::kTraceWaves] = {};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(hbk::g_mlp_trace_n), z, sizeof(z));
   return 0;
+}
+// k3s's per-block spans of the last launch: [1024][3] {start, end, job << 32 | split}
+extern "C" int hbk_debug_spans(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(hbk::g_span), sizeof(hbk::g_span)) == hipSuccess ? 0 : -2;
 }
 #endif

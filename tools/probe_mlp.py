@@ -101,6 +101,21 @@ def trace():
         print(f"--- {name} (block 0; cycles from the first mark)")
         for w, e in enumerate(evs):
             print(f"  wave {w}: " + " ".join(f"{m}@{t - t0}" for m, t in e))
+    if hasattr(lib(), "hbk_debug_spans"):  # k3s (v2 step): per-block spans, 100 MHz ticks
+        sp = (ctypes.c_ulonglong * (1024 * 3))()
+        lib().hbk_debug_spans(sp)
+        rows = [(sp[3 * b], sp[3 * b + 1], sp[3 * b + 2] >> 32, sp[3 * b + 2] & 0xFFFFFFFF) for b in range(1024)
+                if sp[3 * b] and sp[3 * b + 1] >= sp[3 * b]]
+        if rows:
+            t0 = min(r[0] for r in rows)
+            print("--- k3s block spans (us from the first start): job split start end")
+            by = {}
+            for r in rows:
+                by.setdefault(r[2], []).append(((r[0] - t0) / 100, (r[1] - t0) / 100, r[3]))
+            for jb, v in sorted(by.items()):
+                print(f"  job {jb}: {len(v)} blocks, start {min(x[0] for x in v):.2f}..{max(x[0] for x in v):.2f}, "
+                      f"end {min(x[1] for x in v):.2f}..{max(x[1] for x in v):.2f}, "
+                      f"mean dur {sum(x[1] - x[0] for x in v) / len(v):.2f}")
 
 
 if __name__ == "__main__":
