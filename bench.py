@@ -1104,9 +1104,13 @@ def setup_e2e(args, dev, rank, world, seed):
                         peak=SPLIT_PEAK_TFLOPS if split else FP32_MFMA_PEAK_TFLOPS,
                         peak_basis="f16 dense MFMA peak / 3 (hi*hi + hi*lo + lo*hi per f32-accurate MAC)",
                         algorithmic_flops_per_clip=2.0 * eplan.macs_per_clip)
-        return roof("k1a + k1b + k2_rows + k3_wgrad + k4_update (fused train step, %d steps of B=%d)" % (S, B),
+        # (the stage region runs on the whole GPU, where the library's step_v2 picks v1; the
+        # pipelined headline's 64-CU train partition runs v2 at B = 1,100)
+        step_kernels = "k1a + k1b + k2_rows + k3_wgrad + k4_update"
+        return roof("%s (fused train step, %d steps of B=%d)" % (step_kernels, S, B),
                     "latency", flops_step * S, ms, "TFLOP/s",
-                    load_traffic(pmc, ("k1a_kernel", "k1b_kernel", "k2_rows", "k3_wgrad", "k4_update")),
+                    load_traffic(pmc, ("k1a_kernel", "k1s_kernel", "k1b_kernel", "k1c_kernel", "k2_rows", "k3_wgrad",
+                                       "k3s_kernel", "k4_update")),
                     algorithmic_flops_per_sample=2.0 * 559_296, steps=S, batch=B,
                     us_per_train_step=round(ms * 1e3 / S, 2),
                     bound_note="a chain of dependent small GEMMs at B = 1,100 (PMC: MFMA busy a few %): latency-"

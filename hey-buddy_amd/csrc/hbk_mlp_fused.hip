@@ -3008,12 +3008,16 @@ FusedWs fused_layout(int64_t B, int NG, int64_t n_params = 0) {
 // k1b / k3 path. By default the faster one as measured for the batch (tools/ab_step.sh, 64
 // CUs, r06: B = 1,100 v2 83.2 / v1 87.3 us; 550 65.1 / 63.5; 273 59.8 / 56.7; 138 57.2 /
 // 51.4 -- k3s's fixed prologue and its 2 splits at ceil(Bp / 128) slabs cost it the small
-// batches): v2 from kStepV2MinB rows (HBK_STEP_V2_MIN_B)
-constexpr int kStepV2MinB = 800;
-bool step_v2(int64_t B) {
+// batches): v2 from kStepV2MinB rows (HBK_STEP_V2_MIN_B), on a stream of at most
+// kStepV2MaxCUs CUs -- on the whole GPU v1 is faster (B = 1,100: 59.1 against 66.1 us; its
+// 288-row splits and 32-column tiles spread over 256 CUs, where k3s's 256-column tiles and
+// fixed prologue do not)
+constexpr int kStepV2MinB = 800, kStepV2MaxCUs = 128;
+bool step_v2(int64_t B, const void* stream) {
   static const int forced = getenv("HBK_STEP") ? atoi(getenv("HBK_STEP")) : 0;
   static const int min_b = getenv("HBK_STEP_V2_MIN_B") ? atoi(getenv("HBK_STEP_V2_MIN_B")) : kStepV2MinB;
-  return forced ? forced == 2 : B >= min_b;
+  if (forced) return forced == 2;
+  return B >= min_b && persistent_blocks(1, stream) <= kStepV2MaxCUs;
 }
 int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
@@ -3241,7 +3245,7 @@ int mlp_fused_run(const hbk_mlp_plan& p, const float* params, const float* pool3
     ka.rinfo[i] = reinterpret_cast<uint4*>(ws + w.rinfo[i]);
     ka.mask[i] = reinterpret_cast<uint32_t*>(ws + w.mask[i]);
   }
-  const bool v2 = step_v2(B);
+  const bool v2 = step_v2(B, s);
   const float keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
   const float* xhat = ws + w.xhat[parity];
   const WSplit wsp = make_wsplit(p);
