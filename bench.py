@@ -84,14 +84,17 @@ def parse():
                     help="config 5 at N > 1: the reference's batch of 1,100 per rank (weak: global batch "
                          "1,100 N, 1,000 steps per rank) or split over the ranks (global batch 1,100, "
                          "N x 1,000 steps per rank)")
-    ap.add_argument("--embed-split", type=int, default=0,
+    ap.add_argument("--embed-split", type=int, default=-1,
                     help="config 5, pipelined: the embedding's first K fused chains run on the featurize stream, "
                          "the rest (and the NaN replacement) on the train stream after its steps "
                          "(hbk_embed_clips_front / _back; 0: the whole embedding on the featurize stream). "
                          "With the validation + testing passes in the train chunk the train stream carries "
                          "enough: r04g, one box, 0 (no split) 857 k clips/s, partitions featurize 114.5 / "
-                         "train 114.1 ms, against 3 / 0.4 776 k (111.1 / 127.2 ms), 3 / 0 785 k")
-    ap.add_argument("--embed-split-frac", type=float, default=0.0,
+                         "train 114.1 ms, against 3 / 0.4 776 k (111.1 / 127.2 ms), 3 / 0 785 k. Default (-1): "
+                         "the graph's chain count with --embed-split-frac 0.2 -- r06, with the train step at 83 us "
+                         "the partitions were featurize 109.2 / train 101.5 ms; at 0.2 105.6 / 103.6, headline "
+                         "936.5 k against 927.9 k clips/s (two same-box pairs, profiles/r06c_ab_embed_split.log)")
+    ap.add_argument("--embed-split-frac", type=float, default=None,
                     help="with --embed-split K: this fraction of each chunk's clips is split after K - 1 "
                          "chains instead (a finer balance of the two streams)")
     ap.add_argument("--validation-steps", type=int, default=250,
@@ -595,12 +598,17 @@ def setup_train(args, dev, rank, world, seed):
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ms = float(t.item()) * 1e3
+        c1 = time.perf_counter()  # the final checkpoint alone (a file write the indexed run does not do)
+        tr.save_checkpoint("bench_cli_ckpt_probe")
+        ck = (time.perf_counter() - c1) * 1e3
         return {"what": "WakeWordTrainer.__call__ (heybuddy train's loop) over device-pool iterators, 3 stages "
                         "(%d / %d / %d steps at 1,100 / 550 / 273), incl. the final checkpoint" % (
                             STEPS_1, 2 * STEPS_1, 4 * STEPS_1),
                 "ms": round(ms, 3), "us_per_train_step": round(ms * 1e3 / n_steps, 2),
                 "train_indexed_us_per_train_step": round(ms_indexed * 1e3 / n_steps, 2),
-                "ratio_to_train_indexed": round(ms / ms_indexed, 3)}
+                "ratio_to_train_indexed": round(ms / ms_indexed, 3),
+                "checkpoint_ms": round(ck, 3),
+                "ratio_to_train_indexed_excl_checkpoint": round((ms - ck) / ms_indexed, 3)}
 
     return {
         "step": step, "stages": ["train_3stage"], "roofline": roofline, "cpu_baseline": cpu_baseline,
@@ -945,6 +953,12 @@ def setup_e2e(args, dev, rank, world, seed):
         # run on the train stream after train(c): its front half writes mid[b] on the
         # feature stream, its back half reads it on the train stream
         # (K = n_chains: only the --embed-split-frac clips are split, after K - 1 chains)
+        if args.embed_split < 0:  # default: a fifth of the clips' last chains on the train stream
+            args.embed_split = eplan.n_chains
+            if args.embed_split_frac is None:
+                args.embed_split_frac = 0.2
+        if args.embed_split_frac is None:
+            args.embed_split_frac = 0.0
         K = args.embed_split if 0 < args.embed_split <= eplan.n_chains else 0
         whole = K == eplan.n_chains  # the rest of the clips: the whole embedding on the featurize stream
         # --embed-split-frac f: clips [0, a1) split after K - 1 chains, the rest after K

@@ -415,10 +415,24 @@ class _IndexedEpoch:
         rank, world = tr._world()
         if world > 1:  # distributed.shard_batch's class-stratified slice
             idx, y = idx[:, rank::world], y[rank::world]
-        self.idx = idx.to(torch.int32).contiguous()
-        self.y = y.contiguous()
+        # the stage's index / label / schedule buffers persist per shape on the trainer, so the
+        # next epoch's (and the next __call__'s) segments replay the hipGraphs captured now: the
+        # graphs bake in these addresses, and a capture per stage per call cost ~20 ms of the
+        # 3-stage bench run (bench.py's cli_path)
+        idx = idx.to(torch.int32).contiguous()
+        key = (tuple(idx.shape), str(dev))
+        cache = getattr(tr, "_epoch_bufs", None)
+        if cache is None:
+            cache = tr._epoch_bufs = {}
+        bufs = cache.get(key)
+        if bufs is None:
+            bufs = cache[key] = (torch.empty_like(idx), torch.empty_like(y),
+                                          torch.zeros((max(self.S, 1), 2), dtype=torch.float32, device=dev))
+        self.idx, self.y, self.sched = bufs
+        self.idx.copy_(idx)
+        self.y.copy_(y)
+        self.sched.zero_()
         self.p32, self.p16 = p32, p16
-        self.sched = torch.zeros((max(self.S, 1), 2), dtype=torch.float32, device=dev)
         self.done = 0
         self.validation = validation
         if validation is not None and not isinstance(validation, EvalPasses):
@@ -685,7 +699,7 @@ class WakeWordTrainer(Trainer):
             self._parity ^= 1
             done += 1
 
-    _MAX_GRAPHS = 8
+    _MAX_GRAPHS = 16  # (a 3-stage call: ~2 step graphs per stage and parity, kept across calls)
 
     def _state_ptrs(self) -> tuple:
         """Addresses a captured step bakes in besides its own buffers: the flat
@@ -865,15 +879,22 @@ class WakeWordTrainer(Trainer):
         # validation and testing iterators as device evaluation passes (EvalPasses)
         fast = _IndexedEpoch.make(self, training, validation, testing, num_steps, high_loss_threshold,
                                   activation_threshold, history)
+        lr_all = None
         if fast is not None:
             validation, testing = fast.validation, None
+            # the stage's schedule in one vectorised call (the same numpy ufuncs, bit-identical
+            # values; ~6.5 us of host time per step when evaluated step by step)
+            lr_all = self.get_learning_rate(np.arange(max(num_steps, 1)), warmup_steps=warmup_steps,
+                                            hold_steps=hold_steps, total_steps=num_steps,
+                                            target_learning_rate=learning_rate)
         for step, datum in enumerate(training) if fast is None else enumerate(range(fast.S)):
             if step >= num_steps:
                 break
             if fast is None:
                 x, y = datum[0], datum[1]
             lr = float(self.get_learning_rate(step, warmup_steps=warmup_steps, hold_steps=hold_steps,
-                                              total_steps=num_steps, target_learning_rate=learning_rate))
+                                              total_steps=num_steps, target_learning_rate=learning_rate)
+                       if lr_all is None else lr_all[step])
             lr_hist.append(lr)
             for g in self.optimizer.param_groups:
                 g["lr"] = lr
@@ -1033,6 +1054,16 @@ class WakeWordTrainer(Trainer):
             for d in (training, validation, testing):
                 if hasattr(d, hook):
                     getattr(d, hook)()
+        # the per-step history buffer sized once for the longest stage: train_indexed's hipGraphs
+        # bake in its address, so a buffer regrown by a later stage made every stage of the next
+        # call capture its graphs again (6 captures, ~28 ms of a 3-stage bench call)
+        n_max, n_ = num_steps, num_steps
+        for _ in range(num_stages - 1):
+            n_ = max(validation_steps, int(n_ * step_adjust_ratio))
+            n_max = max(n_max, n_)
+        cap = getattr(self, "_history", None)
+        if cap is None or cap.shape[0] < n_max or cap.device != self.device:
+            self._history = torch.zeros((max(n_max, 1), 8), dtype=torch.float32, device=self.device)
         for i in range(num_stages):
             if dynamic_negative_weight:
                 weights: Union[float, List[float]] = max_negative_weight
