@@ -476,7 +476,7 @@ def setup_train(args, dev, rank, world, seed):
     """configs[3]: the reference's 3-stage classifier schedule (trainer.py:848-926:
     stage s has 2^s x the steps at 1/2^s the batch and half the lr) on HBM-resident
     embedding pools, through the device-sampled fused train step (train_indexed:
-    k1c/k2/k3s/k4 per step, hipGraph-replayed). A bench step = one pass of
+    k1a/k1b/k2/k3/k4 per step on the whole GPU, hipGraph-replayed). A bench step = one pass of
     STEPS_1 stage-1 steps, 2 STEPS_1 stage-2 steps and 4 STEPS_1 stage-3 steps;
     units = embeddings trained (sum of the stages' batches)."""
     import numpy as np
@@ -537,9 +537,12 @@ def setup_train(args, dev, rank, world, seed):
     n_steps = sum(int(st[0].shape[0]) for st in stages)
 
     def roofline(name, ms, pmc):
-        return roof("k1s/k1c + k2_rows + k3s + k4_update (fused train step, %d steps over 3 stages)" % n_steps,
+        # (the whole GPU: the library's step_v2 picks the v1 kernels there; on a <= 128-CU stream at
+        # >= 800 rows it would run k1s / k1c / k3s)
+        return roof("k1a/k1b + k2_rows + k3_wgrad + k4_update (fused train step, %d steps over 3 stages)" % n_steps,
                     "latency", flops_per_sample * units / world, ms, "TFLOP/s",
-                    load_traffic(pmc, ("k1b_kernel", "k1c_kernel", "k2_rows", "k3_wgrad", "k3s_kernel", "k4_update")),
+                    load_traffic(pmc, ("k1a_kernel", "k1b_kernel", "k1s_kernel", "k1c_kernel", "k2_rows", "k3_wgrad",
+                                       "k3s_kernel", "k4_update")),
                     algorithmic_flops_per_sample=flops_per_sample, params=P_, steps=n_steps,
                     us_per_train_step=round(ms * 1e3 / n_steps, 2))
 
