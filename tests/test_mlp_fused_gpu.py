@@ -228,8 +228,10 @@ def test_fused_forward_matches_oracle(B):
 @pytest.mark.parametrize("B", [1100, 273])
 def test_narrow_stream_weight_gradients_match(B):
     """On a stream masked to <= 96 CUs (the pipelined schedule's train stream)
-    k3 runs with 128-row batch splits instead of 288; the gradients equal the
-    wide launch's up to the split-K summation order, and the generic path's."""
+    k3 runs with 128-row batch splits instead of 288, and from 800 rows the
+    library switches to the v2 kernels (k1s / k1c / k3s: the input rows
+    recomputed from the pool rows, no xhat^T); the gradients equal the wide
+    (v1) launch's up to the split-K summation order."""
     from heybuddy.pipeline import masked_stream, train_cu_set
     params = gc.golden_inputs()[0]
     m = _model(params)
@@ -250,6 +252,50 @@ def test_narrow_stream_weight_gradients_match(B):
         a, b = gn[k].cpu().numpy(), gw[k].cpu().numpy()
         scale = np.abs(b).max() + 1e-12
         np.testing.assert_allclose(a / scale, b / scale, rtol=0, atol=1e-5, err_msg=k)
+
+
+def test_v2_step_on_the_train_partition_equals_v1(tmp_path):
+    """The v2 step (k1s / k1c / k3s, picked for >= 800 rows on a <= 128-CU stream:
+    the pipelined headline's train partition) against v1 (the whole GPU) over 6
+    graph-replayed train_indexed steps of B = 1,100 rows gathered from an f32 and
+    an f16 pool, dropout on (k1s draws the same mask bits as k1a): counts, gate
+    and selection exact, loss 1e-4, parameters to the summation order."""
+    from heybuddy.pipeline import masked_stream, train_cu_set
+    from heybuddy.trainer import WakeWordTrainer
+    params = gc.golden_inputs()[0]
+    rng = np.random.default_rng(23)
+    S, npos, nneg = 6, 100, 1000
+    pos = torch.from_numpy(rng.standard_normal((2000, 16, 96)).astype(np.float32) + 0.6).cuda()
+    neg = torch.from_numpy(rng.standard_normal((4000, 16, 96)).astype(np.float32)).half().cuda()
+    ip = np.stack([rng.choice(2000, npos, replace=False) for _ in range(S)])
+    ineg = np.stack([rng.choice(4000, nneg, replace=False) for _ in range(S)])
+    idx = torch.from_numpy(np.concatenate([ip, -ineg - 1], axis=1).astype(np.int32)).cuda()
+    y = torch.from_numpy(np.concatenate([np.ones(npos), np.zeros(nneg)]).astype(np.float32)).cuda()
+    sched = torch.from_numpy(np.stack([np.linspace(2e-4, 1e-3, S), np.full(S, 1.5)], 1).astype(np.float32)).cuda()
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    ms = masked_stream(torch.device("cuda", 0), train_cu_set(n_cu, 64))
+    runs = {}
+    for mode in ("v1", "v2"):
+        tr = WakeWordTrainer(checkpoint_dir=str(tmp_path / mode), device="cuda")
+        tr.model.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=True)
+        tr.model.train()
+        tr._seed_base_v = 777
+        tr._reset_accumulation()
+        hist = torch.zeros((S, 8), device="cuda")
+        if mode == "v2":
+            ms.stream.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(ms.stream):
+                tr.train_indexed(idx, y, sched, pool32=pos, pool16=neg, history=hist, steps_per_graph=4)
+        else:
+            tr.train_indexed(idx, y, sched, pool32=pos, pool16=neg, history=hist, steps_per_graph=4)
+        torch.cuda.synchronize()
+        runs[mode] = (tr.model.flat_parameters.clone(), hist.clone(), tr._fstate.clone())
+    (p0, h0, s0), (p1, h1, s1) = runs["v1"], runs["v2"]
+    np.testing.assert_allclose(h1[:, [0, 2, 4, 5, 6, 7]].cpu().numpy(), h0[:, [0, 2, 4, 5, 6, 7]].cpu().numpy())
+    np.testing.assert_allclose(h1[:, 3].cpu().numpy(), h0[:, 3].cpu().numpy(), rtol=1e-4)
+    d = (p1 - p0).abs()
+    assert float((d > 1e-5).float().mean()) < 1e-3 and float(d.max()) <= 2e-2
+    torch.testing.assert_close(s1, s0)
 
 
 def test_train_epoch_device_iterator_runs_indexed_and_equals_eager(tmp_path, monkeypatch):
