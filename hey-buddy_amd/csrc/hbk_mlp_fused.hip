@@ -2969,6 +2969,8 @@ WSplit make_wsplit(const hbk_mlp_plan& p) {
 int64_t wsplit_halves(int NG) { return int64_t(NG - 1) * 4 * (kL * kH + kH2 * kL); }
 int k1_blocks(int B) { return ((B + kRB - 1) / kRB + 7) / 8 * 8; }  // row blocks, XCD-aware
 int k1_splits(int B) {  // (one round of three per CU on a 64-CU stream, KS 8, measured 92.1 vs 88.4 us per step)
+  static const int forced = getenv("HBK_K1_KS") ? atoi(getenv("HBK_K1_KS")) : 0;  // (A/B: 4 6 8 12 16 24)
+  if (forced == 4 || forced == 6 || forced == 8 || forced == 12 || forced == 16 || forced == 24) return forced;
   static const int ks_opts[] = {4, 6, 8, 12, 16, 24};
   for (int ks : ks_opts)
     if (k1_blocks(B) * ks >= 256) return ks;
