@@ -911,6 +911,10 @@ def setup_e2e(args, dev, rank, world, seed):
         # (27.6 against 24.6 s per rehearsal step: gpurun_out/rehearse0.log / rehearse.log)
         eval_default = "-1" if world == 1 or dist.get_backend() == "nccl" else "0"
         n_ecu = int(os.environ.get("HBK_EVAL_CUS", eval_default))
+        if n_ecu and world > 1 and dist.get_backend() != "nccl":
+            raise SystemExit("HBK_EVAL_CUS != 0 with %d gloo ranks: the evaluation passes' own stream needs a "
+                             "collective enqueued on it (RCCL); gloo's host-blocking count all-reduce would "
+                             "serialise it against the train stream (DESIGN.md §6)" % world)
         if n_ecu < 0:
             n_ecu = torch.cuda.get_device_properties(dev).multi_processor_count
         if n_ecu and ev is not None:
