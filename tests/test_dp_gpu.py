@@ -38,10 +38,11 @@ def _port():
     return str(p)
 
 
-def _run(mode, world, tmp_path):
+def _run(mode, world, tmp_path, **extra_env):
     port = _port()
-    outs = [str(tmp_path / f"{mode}_{r}.npz") for r in range(world)]
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    tag = "".join(f"_{k}{v}" for k, v in sorted(extra_env.items()))
+    outs = [str(tmp_path / f"{mode}{tag}_{r}.npz") for r in range(world)]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", **extra_env)
     procs = [subprocess.Popen([sys.executable, WORKER, mode, str(r), str(world), port, outs[r]], env=env,
                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(world)]
     logs = []
@@ -98,3 +99,20 @@ def test_rccl_allreduce_captured_in_train_graph(tmp_path):
     assert int(cap["reduce_calls"]) < dp_worker.S, int(cap["reduce_calls"])
     r0 = np.load(str(tmp_path / "gloo_0.npz")) if (tmp_path / "gloo_0.npz").exists() else None
     assert r0 is None or int(r0["reduce_calls"]) == dp_worker.S
+
+
+def test_rccl_allreduce_with_the_v2_step_on_the_train_partition(tmp_path):
+    """The DP per-rank mode's train step as the pipelined headline runs it at N > 1: B = 1,100
+    on a 64-CU stream (the v2 kernels), the weight-gradient slabs folded into the bucket
+    before the captured RCCL all-reduce -- against the single process on the whole GPU (v1,
+    slabs summed by the update)."""
+    sys.path[:0] = [os.path.join(ROOT, "tests")]
+    single = _run("single", 1, tmp_path, DP_BIG="1")[0]
+    cap = _run("nccl1", 1, tmp_path, DP_BIG="1", DP_MASK64="1")[0]
+    assert cap["flat"].shape == single["flat"].shape
+    S = single["hist"].shape[0]  # (lr sum from the worker's schedule)
+    lr_sum = float((1e-3 * (1.0 + np.arange(S) / S)).astype(np.float32).sum())
+    _close(cap["flat"], single["flat"], lr_sum)
+    cols = [0, 1, 2, 4, 5, 6, 7]
+    np.testing.assert_array_equal(cap["hist"][:, cols], single["hist"][:, cols])
+    assert int(cap["reduce_calls"]) < S
