@@ -90,7 +90,7 @@ def parse():
                          "(hbk_embed_clips_front / _back; 0: the whole embedding on the featurize stream). "
                          "With the validation + testing passes in the train chunk the train stream carries "
                          "enough: r04g, one box, 0 (no split) 857 k clips/s, partitions featurize 114.5 / "
-                         "train 114.1 ms, against 3 / 0.4 776 k (111.1 / 127.2 ms), 3 / 0 785 k. Default (-1): "
+                         "train 114.1 ms, against 3 / 0.4 776 k (111.1 / 127.2 ms), 3 / 0 785 k. Default (-1, N = 1): "
                          "the graph's chain count with --embed-split-frac 0.2 -- r06, with the train step at 83 us "
                          "the partitions were featurize 109.2 / train 101.5 ms; at 0.2 105.6 / 103.6, headline "
                          "936.5 k against 927.9 k clips/s (two same-box pairs, profiles/r06c_ab_embed_split.log)")
@@ -960,10 +960,13 @@ def setup_e2e(args, dev, rank, world, seed):
         # run on the train stream after train(c): its front half writes mid[b] on the
         # feature stream, its back half reads it on the train stream
         # (K = n_chains: only the --embed-split-frac clips are split, after K - 1 chains)
-        if args.embed_split < 0:  # default: a fifth of the clips' last chains on the train stream
+        if args.embed_split < 0:  # default: a fifth of the clips' last chains on the train stream at N = 1
             args.embed_split = eplan.n_chains
             if args.embed_split_frac is None:
-                args.embed_split_frac = 0.2
+                # N > 1: none -- the train stream then also folds the weight-gradient slabs and all-reduces
+                # the bucket every step (r06_dp_probe.log: +9 us per step before the collective itself), so
+                # the train partition is the longer one and the embedding stays on the featurize stream
+                args.embed_split_frac = 0.2 if world == 1 else 0.0
         if args.embed_split_frac is None:
             args.embed_split_frac = 0.0
         K = args.embed_split if 0 < args.embed_split <= eplan.n_chains else 0
