@@ -1056,29 +1056,37 @@ __global__ void __launch_bounds__(256) k2_rows_kernel(K2Args a) {
   // whose values are finite and whose every gradient is multiplied by dz = 0).
   {
     float h[4] = {0.f, 0.f, 0.f, 0.f}, g[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int s0 = 0; s0 < a.KS; s0 += 12) {
-      float lh[12][4], lg[12][4];
+    // rounds of U slabs (U = 12 for KS = 12 / 24, else 8: k1c's KS = 8 read 12 clamped slabs per round)
+    auto sum_slabs = [&](auto U_) {
+      constexpr int U = decltype(U_)::value;
+      for (int s0 = 0; s0 < a.KS; s0 += U) {
+        float lh[U][4], lg[U][4];
 #pragma unroll
-      for (int u = 0; u < 12; ++u) {
-        const int sl = (HBK_K2_ABLATE & 2) ? 0 : min(s0 + u, a.KS - 1);
+        for (int u = 0; u < U; ++u) {
+          const int sl = (HBK_K2_ABLATE & 2) ? 0 : min(s0 + u, a.KS - 1);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int e = tid + 256 * q, r = min(e >> 6, nrow - 1), j = e & 63;
-          const float* src = a.hg_part + (sl * B + r0 + r) * kH2;
-          lh[u][q] = *BCK(&src[j], 4);
-          lg[u][q] = *BCK(&src[kH + j], 4);
+          for (int q = 0; q < 4; ++q) {
+            const int e = tid + 256 * q, r = min(e >> 6, nrow - 1), j = e & 63;
+            const float* src = a.hg_part + (sl * B + r0 + r) * kH2;
+            lh[u][q] = *BCK(&src[j], 4);
+            lg[u][q] = *BCK(&src[kH + j], 4);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const float on = s0 + u < a.KS ? 1.f : 0.f;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            h[q] += on * lh[u][q];
+            g[q] += on * lg[u][q];
+          }
         }
       }
-#pragma unroll
-      for (int u = 0; u < 12; ++u) {
-        const float on = s0 + u < a.KS ? 1.f : 0.f;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          h[q] += on * lh[u][q];
-          g[q] += on * lg[u][q];
-        }
-      }
-    }
+    };
+    if (a.KS % 12 == 0)
+      sum_slabs(std::integral_constant<int, 12>{});
+    else
+      sum_slabs(std::integral_constant<int, 8>{});
     const float bh = P[a.b_hg[0] + (tid & 63)], bg = P[a.b_hg[0] + kH + (tid & 63)];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
