@@ -1699,7 +1699,7 @@ __global__ void __launch_bounds__(256) k3_wgrad_kernel(K3Args a) {
 // 32-column tiles re-read dHG0 48 times per split: 27 MB of its 47 MB per step at
 // B = 1,100). The batch streams through in 32-row steps: the activation chunk X
 // (16 NBT columns x 32 rows) is converted to f16 hi / lo planes in a double-
-// buffered LDS image (one barrier per step), the gradient chunk is loaded two steps
+// buffered LDS image (one barrier per step), the gradient chunk is loaded three steps
 // ahead into registers. The gradient's power-of-two scale comes from k2's per-tile
 // maxima (maxS), so the whole split accumulates in one scale. The input layer's X
 // is not stored anywhere: it is recomputed from the pool rows, k1s's statistics and
@@ -1742,8 +1742,10 @@ struct K3sArgs {
 __device__ __forceinline__ int k3s_swz(int row, int ch) { return ch ^ (((row & 3) << 2) | ((row >> 2) & 3)); }
 // N tile widths: the input layer's 256 columns (each gradient chunk, loaded and split once,
 // feeds 16 column tiles: its 12x re-read of dHG0 per split became 6x, the split's VALU is
-// amortised over twice the MFMAs -- k3s is bound by the CU's load rate, not by MFMA), the
-// generic jobs' 128
+// amortised over twice the MFMAs; 22.1 against 24.5 us), the generic jobs' 128. k3s is bound
+// per CU (two workgroups on one CU each ran 2.2x slower), not by a chip-wide resource, and
+// neither fewer VALU, half the LDS fragment traffic nor contiguous row loads moved it
+// (profiles/r06_ab_step.log)
 constexpr int kK3sNbtRaw = 16, kK3sNbtGen = 8;
 static_assert(kD % (16 * kK3sNbtRaw) == 0, "the input layer's tiles are all live");
 struct K3sShared {
